@@ -1,0 +1,322 @@
+"""Single schema source for the two pool kinds of group ``compute.my.domain/v1alpha1``.
+
+Everything that describes the API surface is derived from the dicts in this file:
+
+* ``config/crd/*.yaml`` (``make manifests`` -> ``scripts/gen_manifests.py``),
+* the apiserver-sim's OpenAPI validation / defaulting / pruning (it loads the CRDs),
+* ``native/include/gpupool/generated/schema_consts.h`` (group/version/plural/finalizer/
+  condition-type constants used by the C++ controller), so Python and C++ cannot drift.
+
+``AzureVmPool`` is wire-compatible with the reference guide's Go types
+(``/root/reference/README.md:92-151``): same field names and json tags, ``replicas`` with
+``+kubebuilder:validation:Minimum=0`` (README.md:94), a status subresource (README.md:131) and the
+Desired/Ready printer columns (README.md:132-133). Fields without ``omitempty`` in the reference
+are ``required`` here, exactly what controller-gen would emit.
+
+``Mi355xPool`` is the MI355X-native kind: the same declarative
+``spec.replicas``/``status.readyReplicas``/``conditions`` surface, reconciled against physical
+gfx950 devices on an on-prem node instead of Azure VMs.
+"""
+from __future__ import annotations
+
+import copy
+
+GROUP = "compute.my.domain"
+VERSION = "v1alpha1"
+API_VERSION = f"{GROUP}/{VERSION}"
+
+# Finalizer that guards device/VM release (reference roadmap README.md:309).
+FINALIZER = "compute.my.domain/device-release"
+
+# Well-known annotation/label keys shared by agent, manager and kubelet-fake.
+ANN_AGENT_ENDPOINT = "gpupool.amd.com/agent-endpoint"
+ANN_POD_DEVICES = "gpupool.amd.com/devices"
+LABEL_GFX = "amd.com/gpu.family"
+LABEL_POOL = "gpupool.amd.com/pool"
+DEFAULT_RESOURCE = "amd.com/gpu"
+
+# Condition types (metav1.Condition, README.md:126-127; roadmap README.md:310).
+COND_READY = "Ready"
+COND_PROGRESSING = "Progressing"
+COND_DEGRADED = "Degraded"
+COND_DELETING = "Deleting"
+COND_CREDENTIALS = "CredentialsValid"
+COND_XGMI = "XGMILinksHealthy"
+COND_ECC = "HBMECCHealthy"
+COND_THERMAL = "ThermalHealthy"
+COND_PROBE = "DeviceProbePassed"
+
+AZURE_CONDITIONS = [COND_READY, COND_PROGRESSING, COND_DEGRADED, COND_DELETING, COND_CREDENTIALS]
+MI355X_CONDITIONS = [COND_READY, COND_PROGRESSING, COND_DEGRADED, COND_DELETING,
+                     COND_XGMI, COND_ECC, COND_THERMAL, COND_PROBE]
+
+AZURE_CREDENTIAL_KEYS = ["AZURE_CLIENT_ID", "AZURE_CLIENT_SECRET", "AZURE_TENANT_ID",
+                         "AZURE_SUBSCRIPTION_ID"]  # README.md:108
+
+_S = {"type": "string"}
+_I32 = {"type": "integer", "format": "int32"}
+_I64 = {"type": "integer", "format": "int64"}
+_B = {"type": "boolean"}
+
+CONDITION_SCHEMA = {
+    "type": "object",
+    "required": ["type", "status", "lastTransitionTime", "reason", "message"],
+    "properties": {
+        "type": {"type": "string", "maxLength": 316,
+                 "pattern": r"^([a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*/)?(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])$"},
+        "status": {"type": "string", "enum": ["True", "False", "Unknown"]},
+        "observedGeneration": {"type": "integer", "format": "int64", "minimum": 0},
+        "lastTransitionTime": {"type": "string", "format": "date-time"},
+        "reason": {"type": "string", "maxLength": 1024, "minLength": 1,
+                   "pattern": r"^[A-Za-z]([A-Za-z0-9_,:]*[A-Za-z0-9_])?$"},
+        "message": {"type": "string", "maxLength": 32768},
+    },
+}
+
+CONDITIONS_FIELD = {
+    "type": "array",
+    "items": CONDITION_SCHEMA,
+    "x-kubernetes-list-type": "map",
+    "x-kubernetes-list-map-keys": ["type"],
+}
+
+# ---------------------------------------------------------------- AzureVmPool (README.md:92-128)
+AZURE_SPEC = {
+    "type": "object",
+    "description": "AzureVmPoolSpec defines the desired state of AzureVmPool (README.md:92-110).",
+    "required": ["replicas", "resourceGroupName", "location", "vmSize", "vnetName", "subnetName",
+                 "imageReference", "azureCredentialSecret"],
+    "properties": {
+        "replicas": {**_I32, "minimum": 0, "description": "Desired number of VM instances."},
+        "resourceGroupName": _S,
+        "location": _S,
+        "vmSize": {**_S, "description": "e.g. Standard_NC4as_T4_v3"},
+        "vnetName": _S,
+        "subnetName": _S,
+        "imageReference": {
+            "type": "object",
+            "required": ["publisher", "offer", "sku", "version"],
+            "properties": {"publisher": _S, "offer": _S, "sku": _S, "version": _S},
+        },
+        "azureCredentialSecret": {**_S, "description": "Secret with AZURE_CLIENT_ID, "
+                                  "AZURE_CLIENT_SECRET, AZURE_TENANT_ID, AZURE_SUBSCRIPTION_ID."},
+    },
+}
+
+AZURE_STATUS = {
+    "type": "object",
+    "properties": {
+        "observedGeneration": _I64,
+        "readyReplicas": _I32,
+        "replicas": _I32,
+        "vms": {"type": "array", "items": _S},
+        "conditions": CONDITIONS_FIELD,
+    },
+}
+
+# ---------------------------------------------------------------- Mi355xPool
+DEVICE_STATUS = {
+    "type": "object",
+    "required": ["uuid"],
+    "properties": {
+        "uuid": _S,
+        "hipUUID": _S,
+        "bdf": _S,
+        "index": _I32,
+        "node": _S,
+        "renderNode": _S,
+        "kfdNode": _I32,
+        "health": {"type": "string", "enum": ["Healthy", "Unhealthy", "Draining", "Probing"]},
+        "reasons": {"type": "array", "items": _S},
+        "advertised": _B,
+        "pods": {"type": "array", "items": _S},
+        "claimedAt": _S,
+        "probe": {
+            "type": "object",
+            "properties": {
+                "passed": _B,
+                "hbmGBps": {"type": "number"},
+                "mfmaTflops": {"type": "number"},
+                "ms": {"type": "number"},
+                "backend": _S,
+                "message": _S,
+            },
+        },
+    },
+}
+
+MI355X_SPEC = {
+    "type": "object",
+    "description": "Desired state of a pool of MI355X (gfx950) GPUs on one node.",
+    "required": ["replicas"],
+    "properties": {
+        "replicas": {**_I32, "minimum": 0, "maximum": 1024,
+                     "description": "Number of healthy GPUs to claim, probe and advertise."},
+        "nodeName": {**_S, "description": "Pin the pool to one node (else nodeSelector/any)."},
+        "nodeSelector": {"type": "object", "additionalProperties": _S},
+        "resourceName": {**_S, "default": DEFAULT_RESOURCE,
+                         "pattern": r"^[a-z0-9.-]+/[a-z0-9.-]+$",
+                         "description": "Extended resource the device plugin advertises "
+                                        "this pool's GPUs under."},
+        "topologyPolicy": {"type": "string", "enum": ["xgmi-packed", "any"],
+                           "default": "xgmi-packed"},
+        "partition": {
+            "type": "object",
+            "default": {},
+            "properties": {
+                "compute": {"type": "string", "enum": ["Any", "SPX", "DPX", "QPX", "CPX"],
+                            "default": "Any"},
+                "memory": {"type": "string", "enum": ["Any", "NPS1", "NPS2", "NPS4", "NPS8"],
+                           "default": "Any"},
+            },
+        },
+        "health": {
+            "type": "object",
+            "default": {},
+            "properties": {
+                "maxUncorrectableECC": {**_I64, "minimum": 0, "default": 0,
+                                        "description": "Uncorrectable ECC errors tolerated "
+                                                       "since claim (delta, not absolute)."},
+                "maxCorrectableECC": {**_I64, "minimum": 0, "default": 100000,
+                                      "description": "Correctable ECC errors tolerated "
+                                                     "since claim."},
+                "requireAllXGMILinks": {**_B, "default": True},
+                "minXGMILinksUp": {**_I32, "minimum": 0, "maximum": 8, "default": 7},
+                "thermal": {"type": "string", "default": "belowCritical",
+                            "enum": ["belowCritical", "belowEmergency", "ignore"]},
+                "thermalMarginC": {**_I32, "minimum": 0, "default": 0},
+            },
+        },
+        "drain": {
+            "type": "object",
+            "default": {},
+            "properties": {
+                "gracePeriodSeconds": {**_I64, "minimum": 0, "default": 30},
+                "evict": {**_B, "default": True},
+                "timeoutSeconds": {**_I64, "minimum": 0, "default": 300},
+            },
+        },
+        "probe": {
+            "type": "object",
+            "default": {},
+            "properties": {
+                "enabled": {**_B, "default": True},
+                "hbmBytes": {**_I64, "minimum": 1 << 20, "maximum": 64 << 30,
+                             "default": 1 << 30},
+                "mfma": {**_B, "default": True},
+            },
+        },
+        "replacePolicy": {"type": "string", "enum": ["Replace", "Keep"], "default": "Replace"},
+    },
+}
+
+MI355X_STATUS = {
+    "type": "object",
+    "properties": {
+        "observedGeneration": _I64,
+        "replicas": _I32,
+        "readyReplicas": _I32,
+        "nodeName": _S,
+        "selector": _S,
+        "devices": {"type": "array", "items": DEVICE_STATUS},
+        "conditions": CONDITIONS_FIELD,
+        "lastReconcileTime": _S,
+    },
+}
+
+KINDS = {
+    "AzureVmPool": {
+        "plural": "azurevmpools",
+        "singular": "azurevmpool",
+        "shortNames": ["avp"],
+        "spec": AZURE_SPEC,
+        "status": AZURE_STATUS,
+        "printerColumns": [
+            {"name": "Desired", "type": "integer", "jsonPath": ".spec.replicas"},
+            {"name": "Ready", "type": "integer", "jsonPath": ".status.readyReplicas"},
+            {"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"},
+        ],
+        "conditions": AZURE_CONDITIONS,
+    },
+    "Mi355xPool": {
+        "plural": "mi355xpools",
+        "singular": "mi355xpool",
+        "shortNames": ["mxp"],
+        "spec": MI355X_SPEC,
+        "status": MI355X_STATUS,
+        "printerColumns": [
+            {"name": "Desired", "type": "integer", "jsonPath": ".spec.replicas"},
+            {"name": "Ready", "type": "integer", "jsonPath": ".status.readyReplicas"},
+            {"name": "Node", "type": "string", "jsonPath": ".status.nodeName"},
+            {"name": "Status", "type": "string",
+             "jsonPath": ".status.conditions[?(@.type==\"Ready\")].reason"},
+            {"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"},
+        ],
+        "conditions": MI355X_CONDITIONS,
+    },
+}
+
+
+def crd(kind: str) -> dict:
+    """Return the apiextensions.k8s.io/v1 CustomResourceDefinition for ``kind``."""
+    k = KINDS[kind]
+    schema = {
+        "type": "object",
+        "description": f"{kind} is the Schema for the {k['plural']} API",
+        "properties": {
+            "apiVersion": _S,
+            "kind": _S,
+            "metadata": {"type": "object"},
+            "spec": copy.deepcopy(k["spec"]),
+            "status": copy.deepcopy(k["status"]),
+        },
+    }
+    return {
+        "apiVersion": "apiextensions.k8s.io/v1",
+        "kind": "CustomResourceDefinition",
+        "metadata": {"name": f"{k['plural']}.{GROUP}",
+                     "annotations": {"gpupool.amd.com/generated-by": "scripts/gen_manifests.py"}},
+        "spec": {
+            "group": GROUP,
+            "names": {"kind": kind, "listKind": f"{kind}List", "plural": k["plural"],
+                      "singular": k["singular"], "shortNames": list(k["shortNames"])},
+            "scope": "Namespaced",
+            "versions": [{
+                "name": VERSION,
+                "served": True,
+                "storage": True,
+                "schema": {"openAPIV3Schema": schema},
+                "subresources": {
+                    "status": {},
+                    "scale": {"specReplicasPath": ".spec.replicas",
+                              "statusReplicasPath": ".status.readyReplicas"},
+                },
+                "additionalPrinterColumns": copy.deepcopy(k["printerColumns"]),
+            }],
+        },
+    }
+
+
+def all_crds() -> list[dict]:
+    return [crd(k) for k in KINDS]
+
+
+def rbac_role() -> dict:
+    """ClusterRole the manager needs (the reference's missing 'step four', README.md:162->242)."""
+    rules = [
+        {"apiGroups": [GROUP], "resources": [k["plural"] for k in KINDS.values()],
+         "verbs": ["get", "list", "watch", "create", "update", "patch", "delete"]},
+        {"apiGroups": [GROUP], "resources": [k["plural"] + "/status" for k in KINDS.values()],
+         "verbs": ["get", "update", "patch"]},
+        {"apiGroups": [GROUP], "resources": [k["plural"] + "/finalizers" for k in KINDS.values()],
+         "verbs": ["update"]},
+        {"apiGroups": [""], "resources": ["secrets"], "verbs": ["get"]},
+        {"apiGroups": [""], "resources": ["events"], "verbs": ["create", "patch"]},
+        {"apiGroups": [""], "resources": ["pods"], "verbs": ["get", "list", "watch", "delete"]},
+        {"apiGroups": [""], "resources": ["pods/eviction"], "verbs": ["create"]},
+        {"apiGroups": [""], "resources": ["nodes"], "verbs": ["get", "list", "watch", "patch"]},
+        {"apiGroups": ["coordination.k8s.io"], "resources": ["leases"],
+         "verbs": ["get", "create", "update"]},
+    ]
+    return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+            "metadata": {"name": "gpupool-manager-role"}, "rules": rules}

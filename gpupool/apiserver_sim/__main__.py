@@ -1,0 +1,33 @@
+"""``python -m gpupool.apiserver_sim --port 0 --port-file /tmp/port --crd-dir config/crd``."""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+
+from .server import ApiServerSim, serve
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser(description="gpupool kube-apiserver simulator")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=6443)
+    ap.add_argument("--port-file", default=None, help="write the bound port here (for --port 0)")
+    ap.add_argument("--crd-dir", default=None, help="pre-install every CRD YAML in this dir")
+    ap.add_argument("--token", default=None, help="require 'Authorization: Bearer <token>'")
+    ap.add_argument("--bookmark-interval", type=float, default=5.0)
+    ap.add_argument("--window", type=int, default=50000, help="watch event-log window")
+    ap.add_argument("--unix", default=None, help="also listen on this unix socket")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    logging.basicConfig(level=logging.DEBUG if a.verbose else logging.WARNING,
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    sim = ApiServerSim(token=a.token, bookmark_interval=a.bookmark_interval, window=a.window)
+    try:
+        asyncio.run(serve(a.host, a.port, sim, a.port_file, a.crd_dir, a.unix))
+    except KeyboardInterrupt:
+        pass
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,460 @@
+"""aiohttp front-end of the apiserver simulator: the k8s REST shape over HTTP/1.1 JSON.
+
+Routes:
+  /api, /api/v1, /apis, /apis/{g}/{v}                         discovery
+  /api/v1/{plural}[/{name}[/{sub}]]                           cluster-scoped core
+  /api/v1/namespaces/{ns}/{plural}[/{name}[/{sub}]]           namespaced core
+  /apis/{g}/{v}/{plural}[/{name}[/{sub}]]                     cluster-scoped group
+  /apis/{g}/{v}/namespaces/{ns}/{plural}[/{name}[/{sub}]]     namespaced group
+  sub in {status, scale, eviction}
+  ?watch=1&resourceVersion=&allowWatchBookmarks=&timeoutSeconds=   chunked watch stream
+  Accept: application/json;as=Table                           server-side printing (kubectl get)
+  /healthz /readyz /livez /version /metrics
+"""
+from __future__ import annotations
+
+import asyncio
+import datetime as _dt
+import json
+import logging
+import re
+import time
+from typing import Any
+
+from aiohttp import web
+
+from .store import ApiError, ResourceType, Store, WatchEvent, get_path, parse_field_selector, \
+    parse_label_selector
+
+log = logging.getLogger("apiserver-sim")
+
+
+# ------------------------------------------------------------------ printing (Table)
+def _age(ts: str | None) -> str:
+    if not ts:
+        return "<unknown>"
+    try:
+        t = _dt.datetime.strptime(ts, "%Y-%m-%dT%H:%M:%SZ").replace(tzinfo=_dt.timezone.utc)
+    except ValueError:
+        return "<invalid>"
+    s = int((_dt.datetime.now(_dt.timezone.utc) - t).total_seconds())
+    if s < 120:
+        return f"{s}s"
+    if s < 7200:
+        return f"{s // 60}m"
+    if s < 172800:
+        return f"{s // 3600}h"
+    return f"{s // 86400}d"
+
+
+_FILTER = re.compile(r"^(.*?)\[\?\(@\.(\w+)==\"([^\"]*)\"\)\](.*)$")
+
+
+def jsonpath(obj: Any, path: str) -> Any:
+    """Subset of kubectl JSONPath: ``.a.b`` and ``.a[?(@.k=="v")].c``."""
+    m = _FILTER.match(path)
+    if m:
+        lst = get_path(obj, m.group(1)) or []
+        for x in lst:
+            if isinstance(x, dict) and str(x.get(m.group(2))) == m.group(3):
+                return get_path(x, m.group(4)) if m.group(4) else x
+        return None
+    return get_path(obj, path)
+
+
+def _cell(v: Any, typ: str) -> Any:
+    if typ == "date":
+        return _age(v)
+    if v is None:
+        return "" if typ == "string" else None
+    return v
+
+
+def builtin_columns(rt: ResourceType) -> list[tuple[str, str, Any]]:
+    if rt.kind == "Pod":
+        def ready(o):
+            cs = o.get("status", {}).get("containerStatuses") or []
+            return f"{sum(1 for c in cs if c.get('ready'))}/{len(o.get('spec', {}).get('containers', []))}"
+
+        def status(o):
+            if o["metadata"].get("deletionTimestamp"):
+                return "Terminating"
+            return o.get("status", {}).get("phase", "")
+        return [("Ready", "string", ready), ("Status", "string", status),
+                ("Node", "string", lambda o: o.get("spec", {}).get("nodeName", "")),
+                ("Age", "date", lambda o: o["metadata"].get("creationTimestamp"))]
+    if rt.kind == "Node":
+        def nstatus(o):
+            for c in o.get("status", {}).get("conditions") or []:
+                if c.get("type") == "Ready":
+                    return "Ready" if c.get("status") == "True" else "NotReady"
+            return "Unknown"
+
+        def gpus(o):
+            alloc = o.get("status", {}).get("allocatable") or {}
+            return ",".join(f"{k}={v}" for k, v in sorted(alloc.items()) if k.startswith("amd.com/"))
+        return [("Status", "string", nstatus), ("GPUs", "string", gpus),
+                ("Age", "date", lambda o: o["metadata"].get("creationTimestamp"))]
+    if rt.kind == "Event":
+        return [("Type", "string", lambda o: o.get("type", "")),
+                ("Reason", "string", lambda o: o.get("reason", "")),
+                ("Object", "string", lambda o: "{}/{}".format(
+                    (o.get("involvedObject") or {}).get("kind", "").lower(),
+                    (o.get("involvedObject") or {}).get("name", ""))),
+                ("Message", "string", lambda o: o.get("message", ""))]
+    return [("Age", "date", lambda o: o["metadata"].get("creationTimestamp"))]
+
+
+def to_table(rt: ResourceType, items: list[dict], rv: str) -> dict:
+    cols = [{"name": "Name", "type": "string", "format": "name"}]
+    getters = []
+    if rt.printer_columns:
+        for pc in rt.printer_columns:
+            cols.append({"name": pc["name"], "type": pc.get("type", "string")})
+            getters.append(lambda o, p=pc: _cell(jsonpath(o, p["jsonPath"]), p.get("type", "string")))
+    else:
+        for name, typ, fn in builtin_columns(rt):
+            cols.append({"name": name, "type": "string" if typ == "date" else typ})
+            getters.append(lambda o, f=fn, t=typ: _cell(f(o), t))
+    rows = [{"cells": [o["metadata"]["name"]] + [g(o) for g in getters],
+             "object": {"kind": "PartialObjectMetadata", "apiVersion": "meta.k8s.io/v1",
+                        "metadata": o["metadata"]}} for o in items]
+    return {"kind": "Table", "apiVersion": "meta.k8s.io/v1", "metadata": {"resourceVersion": rv},
+            "columnDefinitions": cols, "rows": rows}
+
+
+# ------------------------------------------------------------------ server
+class ApiServerSim:
+    def __init__(self, token: str | None = None, bookmark_interval: float = 5.0,
+                 window: int = 50000):
+        self.store = Store(window=window)
+        self.token = token
+        self.bookmark_interval = bookmark_interval
+        self.watchers: set[asyncio.Queue] = set()
+        self.store.listeners.append(self._fanout)
+        self.requests_total: dict[tuple[str, int], int] = {}
+        self.started = time.time()
+        self.app = web.Application(middlewares=[self._mw], client_max_size=64 << 20)
+        r = self.app.router
+        r.add_get("/healthz", self._ok)
+        r.add_get("/readyz", self._ok)
+        r.add_get("/livez", self._ok)
+        r.add_get("/version", self._version)
+        r.add_get("/metrics", self._metrics)
+        r.add_get("/api", self._api_versions)
+        r.add_get("/apis", self._api_groups)
+        r.add_get("/api/{version}", self._resource_list_core)
+        r.add_get("/apis/{group}/{version}", self._resource_list_group)
+        r.add_route("*", "/api/{version}/{rest:.*}", self._dispatch_core)
+        r.add_route("*", "/apis/{group}/{version}/{rest:.*}", self._dispatch_group)
+
+    # -------------------------------------------------------------- plumbing
+    @web.middleware
+    async def _mw(self, request: web.Request, handler):
+        if self.token and request.path not in ("/healthz", "/readyz", "/livez"):
+            if request.headers.get("Authorization") != f"Bearer {self.token}":
+                return self._err(ApiError(401, "Unauthorized", "Unauthorized"))
+        try:
+            resp = await handler(request)
+        except ApiError as e:
+            resp = self._err(e)
+        except web.HTTPException:
+            raise
+        except json.JSONDecodeError as e:
+            resp = self._err(ApiError(400, "BadRequest", f"invalid JSON body: {e}"))
+        except Exception as e:  # pragma: no cover - surfaced as 500
+            log.exception("internal error")
+            resp = self._err(ApiError(500, "InternalError", repr(e)))
+        key = (request.method, resp.status)
+        self.requests_total[key] = self.requests_total.get(key, 0) + 1
+        return resp
+
+    @staticmethod
+    def _err(e: ApiError) -> web.Response:
+        return web.json_response(e.status(), status=e.code)
+
+    async def _ok(self, request):
+        return web.Response(text="ok")
+
+    async def _version(self, request):
+        return web.json_response({"major": "1", "minor": "30", "gitVersion": "v1.30.0-gpupool-sim",
+                                  "platform": "linux/amd64"})
+
+    async def _metrics(self, request):
+        lines = ["# TYPE apiserver_request_total counter"]
+        for (m, c), n in sorted(self.requests_total.items()):
+            lines.append(f'apiserver_request_total{{verb="{m}",code="{c}"}} {n}')
+        lines.append("# TYPE apiserver_watchers gauge")
+        lines.append(f"apiserver_watchers {len(self.watchers)}")
+        lines.append("# TYPE etcd_resource_version gauge")
+        lines.append(f"etcd_resource_version {self.store.rv}")
+        return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
+
+    def _fanout(self, ev: WatchEvent) -> None:
+        for q in list(self.watchers):
+            q.put_nowait(ev)
+
+    # -------------------------------------------------------------- discovery
+    def _resources_for(self, group: str, version: str) -> list[dict]:
+        out = []
+        for rt in self.store.types.values():
+            if rt.group != group or rt.version != version:
+                continue
+            verbs = ["create", "delete", "deletecollection", "get", "list", "patch", "update",
+                     "watch"]
+            out.append({"name": rt.plural, "singularName": rt.singular, "namespaced": rt.namespaced,
+                        "kind": rt.kind, "verbs": verbs, "shortNames": rt.short_names})
+            if rt.status_sub:
+                out.append({"name": rt.plural + "/status", "namespaced": rt.namespaced,
+                            "kind": rt.kind, "verbs": ["get", "patch", "update"]})
+            if rt.scale_sub:
+                out.append({"name": rt.plural + "/scale", "namespaced": rt.namespaced,
+                            "kind": "Scale", "group": "autoscaling", "version": "v1",
+                            "verbs": ["get", "patch", "update"]})
+            if rt.kind == "Pod":
+                out.append({"name": "pods/eviction", "namespaced": True, "kind": "Eviction",
+                            "group": "policy", "version": "v1", "verbs": ["create"]})
+        return out
+
+    async def _api_versions(self, request):
+        return web.json_response({"kind": "APIVersions", "versions": ["v1"]})
+
+    async def _api_groups(self, request):
+        groups = {}
+        for rt in self.store.types.values():
+            if rt.group:
+                groups.setdefault(rt.group, set()).add(rt.version)
+        return web.json_response({"kind": "APIGroupList", "apiVersion": "v1", "groups": [
+            {"name": g, "versions": [{"groupVersion": f"{g}/{v}", "version": v} for v in sorted(vs)],
+             "preferredVersion": {"groupVersion": f"{g}/{sorted(vs)[-1]}",
+                                  "version": sorted(vs)[-1]}}
+            for g, vs in sorted(groups.items())]})
+
+    async def _resource_list_core(self, request):
+        return web.json_response({"kind": "APIResourceList", "groupVersion": "v1",
+                                  "resources": self._resources_for("", request.match_info["version"])})
+
+    async def _resource_list_group(self, request):
+        g, v = request.match_info["group"], request.match_info["version"]
+        res = self._resources_for(g, v)
+        if not res:
+            raise ApiError(404, "NotFound", f"the server could not find {g}/{v}")
+        return web.json_response({"kind": "APIResourceList", "groupVersion": f"{g}/{v}",
+                                  "resources": res})
+
+    # -------------------------------------------------------------- dispatch
+    async def _dispatch_core(self, request):
+        return await self._dispatch(request, "", request.match_info["version"],
+                                    request.match_info["rest"])
+
+    async def _dispatch_group(self, request):
+        return await self._dispatch(request, request.match_info["group"],
+                                    request.match_info["version"], request.match_info["rest"])
+
+    async def _dispatch(self, request: web.Request, group: str, version: str, rest: str):
+        parts = [p for p in rest.split("/") if p]
+        ns = None
+        # /namespaces/{ns}/{plural}/... vs /namespaces/{name}
+        if parts and parts[0] == "namespaces" and len(parts) >= 3:
+            ns, parts = parts[1], parts[2:]
+        if not parts:
+            raise ApiError(404, "NotFound", "not found")
+        rt = self.store.lookup(group, parts[0])
+        if rt.version != version:
+            raise ApiError(404, "NotFound", f"{group}/{version} {parts[0]} is not served")
+        name = parts[1] if len(parts) > 1 else None
+        sub = parts[2] if len(parts) > 2 else ""
+        if rt.namespaced and ns is None and name is not None:
+            raise ApiError(404, "NotFound", f"{rt.plural} is namespaced")
+        q = request.query
+        dry = q.get("dryRun") == "All"
+        m = request.method
+        if name is None:
+            if m == "GET":
+                if q.get("watch") in ("1", "true"):
+                    return await self._watch(request, rt, ns)
+                lst = self.store.list(rt, ns, q.get("labelSelector"), q.get("fieldSelector"),
+                                      int(q.get("limit", 0) or 0), q.get("continue"))
+                if "as=Table" in request.headers.get("Accept", ""):
+                    return web.json_response(to_table(rt, lst["items"],
+                                                      lst["metadata"]["resourceVersion"]))
+                return web.json_response(lst)
+            if m == "POST":
+                body = await request.json()
+                out = self.store.create(rt, ns, body, dry_run=dry)
+                return web.json_response(out, status=201)
+            if m == "DELETE":
+                lst = self.store.list(rt, ns, q.get("labelSelector"), q.get("fieldSelector"))
+                for o in lst["items"]:
+                    try:
+                        self.store.delete(rt, o["metadata"].get("namespace"), o["metadata"]["name"])
+                    except ApiError:
+                        pass
+                return web.json_response(lst)
+            raise ApiError(405, "MethodNotAllowed", f"{m} not allowed on collection")
+        if sub == "status":
+            return await self._object(request, rt, ns, name, "status", dry)
+        if sub == "scale":
+            if m == "GET":
+                return web.json_response(self.store.get_scale(rt, ns, name))
+            if m == "PUT":
+                return web.json_response(self.store.update_scale(rt, ns, name, await request.json()))
+            if m == "PATCH":
+                body = await request.json()
+                cur = self.store.get_scale(rt, ns, name)
+                cur["spec"]["replicas"] = body.get("spec", {}).get("replicas", cur["spec"]["replicas"])
+                cur["metadata"].pop("resourceVersion", None)
+                return web.json_response(self.store.update_scale(rt, ns, name, cur))
+            raise ApiError(405, "MethodNotAllowed", f"{m} not allowed on scale")
+        if sub == "eviction":
+            if rt.kind != "Pod" or m != "POST":
+                raise ApiError(405, "MethodNotAllowed", "eviction is POST on pods only")
+            body = await request.json() if request.can_read_body else {}
+            return web.json_response(self.store.evict(ns, name, body), status=201)
+        if sub:
+            raise ApiError(404, "NotFound", f"unknown subresource {sub}")
+        return await self._object(request, rt, ns, name, "", dry)
+
+    async def _object(self, request, rt, ns, name, sub, dry):
+        m = request.method
+        if m == "GET":
+            obj = self.store.get(rt, ns, name)
+            if "as=Table" in request.headers.get("Accept", ""):
+                return web.json_response(to_table(rt, [obj], obj["metadata"]["resourceVersion"]))
+            return web.json_response(obj)
+        if m == "PUT":
+            return web.json_response(self.store.update(rt, ns, name, await request.json(), sub, dry))
+        if m == "PATCH":
+            ctype = request.headers.get("Content-Type", "")
+            ptype = "json" if "json-patch" in ctype else "merge"
+            return web.json_response(self.store.patch(rt, ns, name, await request.json(), ptype,
+                                                      sub, dry))
+        if m == "DELETE" and not sub:
+            body = {}
+            if request.can_read_body:
+                try:
+                    body = await request.json()
+                except json.JSONDecodeError:
+                    body = {}
+            grace = request.query.get("gracePeriodSeconds", body.get("gracePeriodSeconds"))
+            out = self.store.delete(rt, ns, name, None if grace is None else int(grace),
+                                    body.get("preconditions"), dry)
+            return web.json_response(out)
+        raise ApiError(405, "MethodNotAllowed", f"{m} not allowed")
+
+    # -------------------------------------------------------------- watch
+    async def _watch(self, request: web.Request, rt: ResourceType, ns: str | None):
+        q = request.query
+        lm = parse_label_selector(q.get("labelSelector"))
+        fm = parse_field_selector(q.get("fieldSelector"))
+        bookmarks = q.get("allowWatchBookmarks") in ("1", "true")
+        timeout = float(q.get("timeoutSeconds") or 0) or None
+        rv_s = q.get("resourceVersion", "")
+
+        def match(ev_obj: dict) -> bool:
+            md = ev_obj["metadata"]
+            if rt.namespaced and ns and md.get("namespace") != ns:
+                return False
+            return lm(md.get("labels")) and fm(ev_obj)
+
+        queue: asyncio.Queue = asyncio.Queue()
+        # Register before computing the backlog so nothing falls between the two.
+        self.watchers.add(queue)
+        try:
+            initial: list[tuple[str, dict]] = []
+            if rv_s in ("", "0"):
+                start_rv = self.store.rv
+                for o in self.store.list(rt, ns)["items"]:
+                    if match(o):
+                        initial.append(("ADDED", o))
+            else:
+                start_rv = int(rv_s)
+                try:
+                    for ev in self.store.events_since(rt, start_rv):
+                        if match(ev.obj):
+                            initial.append((ev.type, ev.obj))
+                except ApiError as e:
+                    resp = web.StreamResponse(headers={"Content-Type": "application/json"})
+                    resp.enable_chunked_encoding()
+                    await resp.prepare(request)
+                    await resp.write((json.dumps({"type": "ERROR", "object": e.status()}) +
+                                      "\n").encode())
+                    await resp.write_eof()
+                    return resp
+            last_rv = max([start_rv] + [int(o["metadata"]["resourceVersion"]) for _, o in initial])
+            resp = web.StreamResponse(headers={"Content-Type": "application/json",
+                                               "Transfer-Encoding": "chunked"})
+            resp.enable_chunked_encoding()
+            await resp.prepare(request)
+            for etype, o in initial:
+                await resp.write((json.dumps({"type": etype, "object": o}) + "\n").encode())
+            deadline = time.monotonic() + timeout if timeout else None
+            next_bm = time.monotonic() + self.bookmark_interval
+            while True:
+                now = time.monotonic()
+                wait = next_bm - now
+                if deadline is not None:
+                    wait = min(wait, deadline - now)
+                    if wait <= 0:
+                        break
+                try:
+                    ev = await asyncio.wait_for(queue.get(), timeout=max(wait, 0.001))
+                except asyncio.TimeoutError:
+                    if bookmarks and time.monotonic() >= next_bm:
+                        bm = {"type": "BOOKMARK", "object": {
+                            "kind": rt.kind, "apiVersion": rt.api_version,
+                            "metadata": {"resourceVersion": str(self.store.rv)}}}
+                        await resp.write((json.dumps(bm) + "\n").encode())
+                    if time.monotonic() >= next_bm:
+                        next_bm = time.monotonic() + self.bookmark_interval
+                    continue
+                if ev.rtype != rt.key or ev.rv <= last_rv or not match(ev.obj):
+                    continue
+                last_rv = ev.rv
+                await resp.write((json.dumps({"type": ev.type, "object": ev.obj}) + "\n").encode())
+            await resp.write_eof()
+            return resp
+        except (ConnectionResetError, asyncio.CancelledError):
+            raise
+        finally:
+            self.watchers.discard(queue)
+
+
+async def serve(host: str, port: int, sim: ApiServerSim, port_file: str | None = None,
+                crd_dir: str | None = None, unix: str | None = None) -> None:
+    if crd_dir:
+        load_crd_dir(sim.store, crd_dir)
+    runner = web.AppRunner(sim.app, access_log=None)
+    await runner.setup()
+    site = web.TCPSite(runner, host, port, reuse_address=True)
+    await site.start()
+    bound = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+    if unix:
+        await web.UnixSite(runner, unix).start()
+    if port_file:
+        import os
+        tmp = port_file + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(str(bound))
+        os.replace(tmp, port_file)
+    log.info("apiserver-sim listening on %s:%d", host, bound)
+    print(f"apiserver-sim listening on http://{host}:{bound}", flush=True)
+    while True:
+        await asyncio.sleep(3600)
+
+
+def load_crd_dir(store: Store, crd_dir: str) -> None:
+    import glob
+    import os
+
+    import yaml
+    rt = store.types[("apiextensions.k8s.io", "customresourcedefinitions")]
+    for path in sorted(glob.glob(os.path.join(crd_dir, "*.yaml"))):
+        with open(path) as f:
+            for doc in yaml.safe_load_all(f):
+                if doc and doc.get("kind") == "CustomResourceDefinition":
+                    try:
+                        store.create(rt, None, doc)
+                    except ApiError as e:
+                        if e.code != 409:
+                            raise

@@ -1,0 +1,639 @@
+"""In-memory object store with kube-apiserver semantics (the envtest stand-in).
+
+Semantics implemented here (all exercised by tests/unit/test_apiserver_store.py):
+
+* one global, strictly increasing ``resourceVersion``; every write gets a fresh one;
+* optimistic concurrency: an update carrying a stale ``metadata.resourceVersion`` -> 409 Conflict;
+* ``metadata.generation`` starts at 1 and bumps only when the *spec* (anything outside
+  ``metadata``/``status``) changes, or when ``deletionTimestamp`` is first set;
+* status subresource isolation: main-resource writes ignore ``status``; ``/status`` writes
+  ignore everything except ``status`` (README.md:131 ``+kubebuilder:subresource:status``);
+* finalizers + ``deletionTimestamp`` two-phase delete; the object disappears (DELETED event)
+  when the last finalizer is removed; new finalizers may not be added once deleting;
+* graceful pod deletion: a bound pod gets ``deletionTimestamp`` and stays until the kubelet
+  deletes it with grace 0; eviction subresource = graceful delete;
+* CRD registration with structural-schema defaulting, pruning and validation;
+* ownerReference garbage collection (background propagation);
+* an event log with a compaction window: watching from a compacted RV -> 410 Gone.
+"""
+from __future__ import annotations
+
+import base64
+import collections
+import copy
+import datetime as _dt
+import re
+import uuid as _uuid
+from dataclasses import dataclass, field
+from typing import Any, Callable
+
+from ..api import openapi
+
+
+class ApiError(Exception):
+    def __init__(self, code: int, reason: str, message: str, details: dict | None = None):
+        super().__init__(message)
+        self.code = code
+        self.reason = reason
+        self.message = message
+        self.details = details or {}
+
+    def status(self) -> dict:
+        return {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Failure",
+                "message": self.message, "reason": self.reason, "details": self.details,
+                "code": self.code}
+
+
+def now_rfc3339() -> str:
+    return _dt.datetime.now(_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+_DNS1123_SUB = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*$")
+
+
+@dataclass
+class ResourceType:
+    group: str
+    version: str
+    plural: str
+    kind: str
+    namespaced: bool
+    singular: str = ""
+    short_names: list = field(default_factory=list)
+    schema: dict | None = None          # openAPIV3Schema for CRs
+    status_sub: bool = False
+    scale_sub: dict | None = None
+    printer_columns: list = field(default_factory=list)
+
+    @property
+    def api_version(self) -> str:
+        return f"{self.group}/{self.version}" if self.group else self.version
+
+    @property
+    def key(self) -> tuple[str, str]:
+        return (self.group, self.plural)
+
+
+BUILTINS = [
+    ResourceType("", "v1", "namespaces", "Namespace", False, "namespace", ["ns"]),
+    ResourceType("", "v1", "nodes", "Node", False, "node", ["no"], status_sub=True),
+    ResourceType("", "v1", "pods", "Pod", True, "pod", ["po"], status_sub=True),
+    ResourceType("", "v1", "events", "Event", True, "event", ["ev"]),
+    ResourceType("", "v1", "secrets", "Secret", True, "secret"),
+    ResourceType("", "v1", "configmaps", "ConfigMap", True, "configmap", ["cm"]),
+    ResourceType("coordination.k8s.io", "v1", "leases", "Lease", True, "lease"),
+    ResourceType("apiextensions.k8s.io", "v1", "customresourcedefinitions",
+                 "CustomResourceDefinition", False, "customresourcedefinition", ["crd", "crds"]),
+]
+
+
+@dataclass
+class WatchEvent:
+    rv: int
+    rtype: tuple[str, str]
+    type: str
+    obj: dict
+
+
+def _spec_part(obj: dict) -> dict:
+    return {k: v for k, v in obj.items() if k not in ("metadata", "status", "apiVersion", "kind")}
+
+
+# ------------------------------------------------------------------ selectors
+def parse_label_selector(sel: str | None) -> Callable[[dict], bool]:
+    if not sel:
+        return lambda labels: True
+    reqs = []
+    # split on commas not inside parentheses
+    parts, depth, cur = [], 0, ""
+    for ch in sel:
+        if ch == "(":
+            depth += 1
+        elif ch == ")":
+            depth -= 1
+        if ch == "," and depth == 0:
+            parts.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    parts.append(cur)
+    for p in (x.strip() for x in parts if x.strip()):
+        m = re.match(r"^([^\s!=]+)\s+(in|notin)\s+\((.*)\)$", p)
+        if m:
+            key, op, vals = m.group(1), m.group(2), {v.strip() for v in m.group(3).split(",")}
+            if op == "in":
+                reqs.append(lambda l, k=key, vs=vals: l.get(k) in vs)
+            else:
+                reqs.append(lambda l, k=key, vs=vals: l.get(k) not in vs)
+        elif "!=" in p:
+            k, v = p.split("!=", 1)
+            reqs.append(lambda l, k=k.strip(), v=v.strip(): l.get(k) != v)
+        elif "==" in p or "=" in p:
+            k, v = re.split(r"==?", p, maxsplit=1)
+            reqs.append(lambda l, k=k.strip(), v=v.strip(): l.get(k) == v)
+        elif p.startswith("!"):
+            reqs.append(lambda l, k=p[1:].strip(): k not in l)
+        else:
+            reqs.append(lambda l, k=p: k in l)
+    return lambda labels: all(r(labels or {}) for r in reqs)
+
+
+def get_path(obj: Any, dotted: str) -> Any:
+    cur = obj
+    for part in dotted.split("."):
+        if not part:
+            continue
+        if isinstance(cur, dict):
+            cur = cur.get(part)
+        else:
+            return None
+    return cur
+
+
+def parse_field_selector(sel: str | None) -> Callable[[dict], bool]:
+    if not sel:
+        return lambda obj: True
+    reqs = []
+    for p in (x.strip() for x in sel.split(",") if x.strip()):
+        if "!=" in p:
+            k, v = p.split("!=", 1)
+            reqs.append(lambda o, k=k.strip(), v=v.strip(): str(get_path(o, k) or "") != v)
+        else:
+            k, v = re.split(r"==?", p, maxsplit=1)
+            reqs.append(lambda o, k=k.strip(), v=v.strip(): str(get_path(o, k) or "") == v)
+    return lambda obj: all(r(obj) for r in reqs)
+
+
+# ------------------------------------------------------------------ patches
+def merge_patch(target: Any, patch: Any) -> Any:
+    """RFC 7386 JSON merge patch."""
+    if not isinstance(patch, dict):
+        return copy.deepcopy(patch)
+    out = copy.deepcopy(target) if isinstance(target, dict) else {}
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        else:
+            out[k] = merge_patch(out.get(k), v)
+    return out
+
+
+def _ptr_parts(path: str) -> list[str]:
+    if path == "":
+        return []
+    return [p.replace("~1", "/").replace("~0", "~") for p in path.lstrip("/").split("/")]
+
+
+def json_patch(target: Any, ops: list[dict]) -> Any:
+    """RFC 6902 JSON patch (add/remove/replace/test/copy/move)."""
+    doc = copy.deepcopy(target)
+
+    def resolve(parts):
+        cur = doc
+        for p in parts[:-1]:
+            cur = cur[int(p)] if isinstance(cur, list) else cur[p]
+        return cur, parts[-1]
+
+    for op in ops:
+        kind, parts = op.get("op"), _ptr_parts(op.get("path", ""))
+        try:
+            if kind == "test":
+                cur = doc
+                for p in parts:
+                    cur = cur[int(p)] if isinstance(cur, list) else cur[p]
+                if cur != op.get("value"):
+                    raise ApiError(422, "Invalid", f"test operation failed at {op['path']}")
+                continue
+            if kind in ("copy", "move"):
+                src = _ptr_parts(op["from"])
+                cur = doc
+                for p in src:
+                    cur = cur[int(p)] if isinstance(cur, list) else cur[p]
+                val = copy.deepcopy(cur)
+                if kind == "move":
+                    parent, last = resolve(src)
+                    if isinstance(parent, list):
+                        parent.pop(int(last))
+                    else:
+                        del parent[last]
+                kind, op = "add", {"value": val}
+            parent, last = resolve(parts)
+            if kind == "add":
+                if isinstance(parent, list):
+                    parent.insert(len(parent) if last == "-" else int(last), op["value"])
+                else:
+                    parent[last] = op["value"]
+            elif kind == "replace":
+                if isinstance(parent, list):
+                    parent[int(last)] = op["value"]
+                else:
+                    if last not in parent:
+                        raise KeyError(last)
+                    parent[last] = op["value"]
+            elif kind == "remove":
+                if isinstance(parent, list):
+                    parent.pop(int(last))
+                else:
+                    del parent[last]
+            else:
+                raise ApiError(422, "Invalid", f"unsupported patch op {kind!r}")
+        except (KeyError, IndexError, ValueError, TypeError) as e:
+            raise ApiError(422, "Invalid", f"json patch failed at {op.get('path')}: {e}") from e
+    return doc
+
+
+# ------------------------------------------------------------------ store
+class Store:
+    def __init__(self, window: int = 50000):
+        self.rv = 0
+        self.types: dict[tuple[str, str], ResourceType] = {}
+        self.objects: dict[tuple[str, str], dict[tuple[str, str], dict]] = {}
+        self.log: collections.deque[WatchEvent] = collections.deque(maxlen=window)
+        self.listeners: list[Callable[[WatchEvent], None]] = []
+        for rt in BUILTINS:
+            self.register(rt)
+        self._ensure_namespace("default")
+
+    # --------------------------------------------------------- registry
+    def register(self, rt: ResourceType) -> None:
+        self.types[rt.key] = rt
+        self.objects.setdefault(rt.key, {})
+
+    def unregister(self, key: tuple[str, str]) -> None:
+        self.types.pop(key, None)
+        self.objects.pop(key, None)
+
+    def lookup(self, group: str, plural: str) -> ResourceType:
+        rt = self.types.get((group, plural))
+        if rt is None:
+            raise ApiError(404, "NotFound", f"the server could not find the requested resource "
+                           f"({group or 'core'}/{plural})")
+        return rt
+
+    def resolve_name(self, name: str) -> ResourceType | None:
+        """kubectl-style resolution of plural/singular/kind/shortname (case-insensitive)."""
+        n = name.lower()
+        for rt in self.types.values():
+            if n in (rt.plural, rt.singular, rt.kind.lower()) or n in rt.short_names \
+                    or n == f"{rt.plural}.{rt.group}":
+                return rt
+        return None
+
+    @property
+    def compacted_rv(self) -> int:
+        if len(self.log) < (self.log.maxlen or 0):
+            return 0
+        return self.log[0].rv - 1
+
+    # --------------------------------------------------------- internals
+    def _next_rv(self) -> int:
+        self.rv += 1
+        return self.rv
+
+    def _emit(self, rt: ResourceType, etype: str, obj: dict) -> None:
+        ev = WatchEvent(int(obj["metadata"]["resourceVersion"]), rt.key, etype, copy.deepcopy(obj))
+        self.log.append(ev)
+        for fn in list(self.listeners):
+            fn(ev)
+
+    def _ensure_namespace(self, ns: str) -> None:
+        nss = self.objects[("", "namespaces")]
+        if ("", ns) in nss:
+            return
+        rt = self.types[("", "namespaces")]
+        obj = {"apiVersion": "v1", "kind": "Namespace",
+               "metadata": {"name": ns}, "spec": {"finalizers": ["kubernetes"]},
+               "status": {"phase": "Active"}}
+        self._stamp_new(obj)
+        nss[("", ns)] = obj
+        self._emit(rt, "ADDED", obj)
+
+    def _stamp_new(self, obj: dict) -> None:
+        md = obj["metadata"]
+        md["uid"] = str(_uuid.uuid4())
+        md["creationTimestamp"] = now_rfc3339()
+        md["resourceVersion"] = str(self._next_rv())
+        md["generation"] = 1
+        for k in ("deletionTimestamp", "deletionGracePeriodSeconds"):
+            md.pop(k, None)
+
+    def _admit_cr(self, rt: ResourceType, obj: dict) -> dict:
+        """Defaulting, pruning, validation for custom resources (+ secrets stringData)."""
+        if rt.kind == "Secret":
+            sd = obj.pop("stringData", None) or {}
+            data = obj.setdefault("data", {}) or {}
+            for k, v in sd.items():
+                data[k] = base64.b64encode(str(v).encode()).decode()
+            obj["data"] = data
+        if rt.schema is None:
+            return obj
+        obj = openapi.prune(obj, rt.schema)
+        obj = openapi.apply_defaults(obj, rt.schema)
+        errs = openapi.validate({k: v for k, v in obj.items() if k != "metadata"},
+                                {**rt.schema, "properties": {k: v for k, v in
+                                                             rt.schema.get("properties", {}).items()
+                                                             if k != "metadata"}})
+        if errs:
+            errs = [e.replace("<root>.", "") for e in errs]
+            name = obj.get("metadata", {}).get("name", "")
+            raise ApiError(422, "Invalid", f'{rt.kind}.{rt.group} "{name}" is invalid: '
+                           + ", ".join(errs),
+                           {"name": name, "kind": rt.plural,
+                            "causes": [{"message": e} for e in errs]})
+        return obj
+
+    def _check_ns(self, rt: ResourceType, ns: str | None) -> str:
+        if rt.namespaced:
+            if not ns:
+                raise ApiError(400, "BadRequest", "namespace is required")
+            return ns
+        return ""
+
+    # --------------------------------------------------------- reads
+    def get(self, rt: ResourceType, ns: str | None, name: str) -> dict:
+        ns = self._check_ns(rt, ns) if rt.namespaced else ""
+        obj = self.objects[rt.key].get((ns, name))
+        if obj is None:
+            raise ApiError(404, "NotFound", f'{rt.plural}{"." + rt.group if rt.group else ""} '
+                           f'"{name}" not found',
+                           {"name": name, "group": rt.group, "kind": rt.plural})
+        return copy.deepcopy(obj)
+
+    def list(self, rt: ResourceType, ns: str | None, label_selector: str | None = None,
+             field_selector: str | None = None, limit: int = 0, cont: str | None = None) -> dict:
+        lm = parse_label_selector(label_selector)
+        fm = parse_field_selector(field_selector)
+        items = [copy.deepcopy(o) for (ons, _), o in sorted(self.objects[rt.key].items())
+                 if (not rt.namespaced or not ns or ons == ns)
+                 and lm(o["metadata"].get("labels")) and fm(o)]
+        meta: dict[str, Any] = {"resourceVersion": str(self.rv)}
+        if limit:
+            start = int(cont or 0)
+            if start + limit < len(items):
+                meta["continue"] = str(start + limit)
+                meta["remainingItemCount"] = len(items) - start - limit
+            items = items[start:start + limit]
+        return {"kind": f"{rt.kind}List", "apiVersion": rt.api_version, "metadata": meta,
+                "items": items}
+
+    # --------------------------------------------------------- writes
+    def create(self, rt: ResourceType, ns: str | None, obj: dict, dry_run: bool = False) -> dict:
+        obj = copy.deepcopy(obj)
+        ns = self._check_ns(rt, ns or obj.get("metadata", {}).get("namespace"))
+        md = obj.setdefault("metadata", {})
+        if not md.get("name"):
+            gen = md.get("generateName")
+            if not gen:
+                raise ApiError(422, "Invalid", f"{rt.kind}: metadata.name: Required value")
+            md["name"] = gen + _uuid.uuid4().hex[:5]
+        name = md["name"]
+        if len(name) > 253 or not _DNS1123_SUB.match(name):
+            raise ApiError(422, "Invalid", f'{rt.kind} "{name}" is invalid: metadata.name: '
+                           "Invalid value: must be a lowercase RFC 1123 subdomain")
+        if md.get("namespace") and rt.namespaced and md["namespace"] != ns:
+            raise ApiError(400, "BadRequest", "the namespace of the provided object does not "
+                           "match the namespace sent on the request")
+        if rt.namespaced:
+            md["namespace"] = ns
+        else:
+            md.pop("namespace", None)
+        obj["apiVersion"], obj["kind"] = rt.api_version, rt.kind
+        if (ns, name) in self.objects[rt.key]:
+            raise ApiError(409, "AlreadyExists", f'{rt.plural}{"." + rt.group if rt.group else ""}'
+                           f' "{name}" already exists',
+                           {"name": name, "group": rt.group, "kind": rt.plural})
+        if rt.status_sub and rt.schema is not None:
+            obj.pop("status", None)  # CR status is not settable on create
+        obj = self._admit_cr(rt, obj)
+        if rt.kind == "Pod":
+            obj.setdefault("status", {}).setdefault("phase", "Pending")
+            obj["spec"].setdefault("terminationGracePeriodSeconds", 30)
+        if dry_run:
+            return obj
+        if rt.namespaced:
+            self._ensure_namespace(ns)
+        self._stamp_new(obj)
+        self.objects[rt.key][(ns, name)] = obj
+        if rt.kind == "CustomResourceDefinition":
+            self._register_crd(obj)
+        self._emit(rt, "ADDED", obj)
+        return copy.deepcopy(obj)
+
+    def update(self, rt: ResourceType, ns: str | None, name: str, obj: dict,
+               subresource: str = "", dry_run: bool = False) -> dict:
+        ns = self._check_ns(rt, ns) if rt.namespaced else ""
+        cur = self.objects[rt.key].get((ns, name))
+        if cur is None:
+            raise ApiError(404, "NotFound", f'{rt.plural} "{name}" not found',
+                           {"name": name, "kind": rt.plural})
+        new = copy.deepcopy(obj)
+        nmd = new.setdefault("metadata", {})
+        if nmd.get("name", name) != name:
+            raise ApiError(400, "BadRequest", "the name of the object does not match the URL")
+        rv = nmd.get("resourceVersion")
+        if rv and rv != cur["metadata"]["resourceVersion"]:
+            raise ApiError(409, "Conflict",
+                           f'Operation cannot be fulfilled on {rt.plural}'
+                           f'{"." + rt.group if rt.group else ""} "{name}": the object has been '
+                           "modified; please apply your changes to the latest version and try "
+                           "again", {"name": name, "group": rt.group, "kind": rt.plural})
+        cmd = cur["metadata"]
+        if subresource == "status":
+            merged = copy.deepcopy(cur)
+            if "status" in new:
+                merged["status"] = new["status"]
+            else:
+                merged.pop("status", None)
+            new = merged
+        else:
+            # immutable / server-owned metadata
+            for k in ("uid", "creationTimestamp", "deletionTimestamp",
+                      "deletionGracePeriodSeconds", "generation", "namespace"):
+                if k in cmd:
+                    nmd[k] = cmd[k]
+                else:
+                    nmd.pop(k, None)
+            nmd["name"] = name
+            if rt.status_sub:
+                if "status" in cur:
+                    new["status"] = copy.deepcopy(cur["status"])
+                else:
+                    new.pop("status", None)
+            if cmd.get("deletionTimestamp"):
+                added = set(nmd.get("finalizers") or []) - set(cmd.get("finalizers") or [])
+                if added:
+                    raise ApiError(422, "Forbidden", f"no new finalizers can be added if the "
+                                   f"object is being deleted, found new finalizers {sorted(added)}")
+        new["apiVersion"], new["kind"] = rt.api_version, rt.kind
+        new = self._admit_cr(rt, new)
+        new["metadata"]["resourceVersion"] = cmd["resourceVersion"]
+        if dry_run:
+            return new
+        if new == cur:  # no-op update: no new resourceVersion, no event (apiserver behaviour)
+            return copy.deepcopy(cur)
+        nmd = new["metadata"]
+        if _spec_part(new) != _spec_part(cur):
+            nmd["generation"] = int(cmd.get("generation", 1)) + 1
+        else:
+            nmd["generation"] = cmd.get("generation", 1)
+        nmd["resourceVersion"] = str(self._next_rv())
+        if nmd.get("deletionTimestamp") and not nmd.get("finalizers") and rt.kind != "Pod":
+            self._remove(rt, ns, name, new)
+            return copy.deepcopy(new)
+        self.objects[rt.key][(ns, name)] = new
+        if rt.kind == "CustomResourceDefinition":
+            self._register_crd(new)
+        self._emit(rt, "MODIFIED", new)
+        return copy.deepcopy(new)
+
+    def patch(self, rt: ResourceType, ns: str | None, name: str, patch: Any, ptype: str,
+              subresource: str = "", dry_run: bool = False) -> dict:
+        cur = self.get(rt, ns, name)
+        if ptype == "json":
+            new = json_patch(cur, patch)
+        else:  # merge / strategic (approximated as merge)
+            new = merge_patch(cur, patch)
+        if not (isinstance(patch, dict) and patch.get("metadata", {}).get("resourceVersion")):
+            new.setdefault("metadata", {})["resourceVersion"] = cur["metadata"]["resourceVersion"]
+        return self.update(rt, ns, name, new, subresource, dry_run)
+
+    def delete(self, rt: ResourceType, ns: str | None, name: str, grace: int | None = None,
+               preconditions: dict | None = None, dry_run: bool = False) -> dict:
+        ns = self._check_ns(rt, ns) if rt.namespaced else ""
+        cur = self.objects[rt.key].get((ns, name))
+        if cur is None:
+            raise ApiError(404, "NotFound", f'{rt.plural}{"." + rt.group if rt.group else ""} '
+                           f'"{name}" not found', {"name": name, "kind": rt.plural})
+        md = cur["metadata"]
+        pre = preconditions or {}
+        if pre.get("uid") and pre["uid"] != md["uid"]:
+            raise ApiError(409, "Conflict", "Precondition failed: UID in precondition: "
+                           f"{pre['uid']}, UID in object meta: {md['uid']}")
+        if pre.get("resourceVersion") and pre["resourceVersion"] != md["resourceVersion"]:
+            raise ApiError(409, "Conflict", "Precondition failed: resourceVersion mismatch")
+        if dry_run:
+            return copy.deepcopy(cur)
+        graceful = False
+        if rt.kind == "Pod" and cur.get("spec", {}).get("nodeName") \
+                and cur.get("status", {}).get("phase") not in ("Succeeded", "Failed"):
+            g = grace if grace is not None else cur["spec"].get("terminationGracePeriodSeconds", 30)
+            graceful = g > 0
+            if graceful:
+                md["deletionGracePeriodSeconds"] = int(g)
+        if graceful or md.get("finalizers"):
+            if not md.get("deletionTimestamp"):
+                md["deletionTimestamp"] = now_rfc3339()
+                md["generation"] = int(md.get("generation", 1)) + 1
+                md["resourceVersion"] = str(self._next_rv())
+                self._emit(rt, "MODIFIED", cur)
+            elif rt.kind == "Pod" and grace == 0 and not md.get("finalizers"):
+                self._remove(rt, ns, name, cur)
+            return copy.deepcopy(cur)
+        self._remove(rt, ns, name, cur)
+        return copy.deepcopy(cur)
+
+    def _remove(self, rt: ResourceType, ns: str, name: str, obj: dict) -> None:
+        self.objects[rt.key].pop((ns, name), None)
+        obj["metadata"]["resourceVersion"] = str(self._next_rv())
+        self._emit(rt, "DELETED", obj)
+        if rt.kind == "CustomResourceDefinition":
+            spec = obj["spec"]
+            key = (spec["group"], spec["names"]["plural"])
+            for (ons, oname), o in list(self.objects.get(key, {}).items()):
+                self.objects[key].pop((ons, oname), None)
+                o["metadata"]["resourceVersion"] = str(self._next_rv())
+                self._emit(self.types[key], "DELETED", o)
+            self.unregister(key)
+        if rt.kind == "Namespace":
+            for key, objs in list(self.objects.items()):
+                t = self.types.get(key)
+                if t and t.namespaced:
+                    for (ons, oname) in [k for k in objs if k[0] == name]:
+                        o = objs.pop((ons, oname))
+                        o["metadata"]["resourceVersion"] = str(self._next_rv())
+                        self._emit(t, "DELETED", o)
+        self._gc(obj["metadata"]["uid"])
+
+    def _gc(self, owner_uid: str) -> None:
+        """Background-propagation garbage collection of dependents."""
+        for key, objs in list(self.objects.items()):
+            rt = self.types.get(key)
+            if rt is None:
+                continue
+            for (ons, oname), o in list(objs.items()):
+                refs = o["metadata"].get("ownerReferences") or []
+                if any(r.get("uid") == owner_uid for r in refs):
+                    remaining = [r for r in refs if r.get("uid") != owner_uid]
+                    if remaining:
+                        o["metadata"]["ownerReferences"] = remaining
+                        o["metadata"]["resourceVersion"] = str(self._next_rv())
+                        self._emit(rt, "MODIFIED", o)
+                    else:
+                        try:
+                            self.delete(rt, ons or None, oname, grace=0)
+                        except ApiError:
+                            pass
+
+    def evict(self, ns: str, name: str, body: dict | None) -> dict:
+        rt = self.types[("", "pods")]
+        opts = (body or {}).get("deleteOptions") or {}
+        self.delete(rt, ns, name, grace=opts.get("gracePeriodSeconds"),
+                    preconditions=opts.get("preconditions"))
+        return {"kind": "Status", "apiVersion": "v1", "status": "Success", "code": 201,
+                "metadata": {}}
+
+    # --------------------------------------------------------- scale subresource
+    def get_scale(self, rt: ResourceType, ns: str, name: str) -> dict:
+        if not rt.scale_sub:
+            raise ApiError(404, "NotFound", f"{rt.plural} has no scale subresource")
+        obj = self.get(rt, ns, name)
+        spec_path = rt.scale_sub.get("specReplicasPath", ".spec.replicas")
+        st_path = rt.scale_sub.get("statusReplicasPath", ".status.replicas")
+        return {"kind": "Scale", "apiVersion": "autoscaling/v1",
+                "metadata": {"name": name, "namespace": ns, "uid": obj["metadata"]["uid"],
+                             "resourceVersion": obj["metadata"]["resourceVersion"],
+                             "creationTimestamp": obj["metadata"]["creationTimestamp"]},
+                "spec": {"replicas": get_path(obj, spec_path) or 0},
+                "status": {"replicas": get_path(obj, st_path) or 0}}
+
+    def update_scale(self, rt: ResourceType, ns: str, name: str, scale: dict) -> dict:
+        obj = self.get(rt, ns, name)
+        rv = scale.get("metadata", {}).get("resourceVersion")
+        if rv and rv != obj["metadata"]["resourceVersion"]:
+            raise ApiError(409, "Conflict", f'Operation cannot be fulfilled on {rt.plural} '
+                           f'"{name}": the object has been modified')
+        path = rt.scale_sub.get("specReplicasPath", ".spec.replicas").lstrip(".").split(".")
+        cur = obj
+        for p in path[:-1]:
+            cur = cur.setdefault(p, {})
+        cur[path[-1]] = int(scale.get("spec", {}).get("replicas", 0))
+        self.update(rt, ns, name, obj)
+        return self.get_scale(rt, ns, name)
+
+    # --------------------------------------------------------- CRDs
+    def _register_crd(self, crd: dict) -> None:
+        spec = crd["spec"]
+        ver = next((v for v in spec["versions"] if v.get("storage")), spec["versions"][0])
+        subs = ver.get("subresources") or {}
+        names = spec["names"]
+        self.register(ResourceType(
+            group=spec["group"], version=ver["name"], plural=names["plural"], kind=names["kind"],
+            namespaced=spec.get("scope", "Namespaced") == "Namespaced",
+            singular=names.get("singular", names["kind"].lower()),
+            short_names=list(names.get("shortNames") or []),
+            schema=(ver.get("schema") or {}).get("openAPIV3Schema"),
+            status_sub="status" in subs, scale_sub=subs.get("scale"),
+            printer_columns=list(ver.get("additionalPrinterColumns") or [])))
+        crd.setdefault("status", {})["conditions"] = [
+            {"type": "Established", "status": "True", "reason": "InitialNamesAccepted",
+             "message": "the initial names have been accepted",
+             "lastTransitionTime": now_rfc3339()}]
+        crd["status"]["acceptedNames"] = names
+
+    # --------------------------------------------------------- watch support
+    def events_since(self, rt: ResourceType, rv: int) -> list[WatchEvent]:
+        if rv < self.compacted_rv:
+            raise ApiError(410, "Expired", f"too old resource version: {rv} "
+                           f"({self.compacted_rv + 1})")
+        return [e for e in self.log if e.rtype == rt.key and e.rv > rv]
+

@@ -1,0 +1,300 @@
+"""Minimal, dependency-free Kubernetes REST client (stdlib ``http.client``).
+
+Used by gpuctl, the node agent, the fake kubelet, the bench and the tests. Thread-safe: each
+call opens its own connection unless a per-thread keep-alive connection is available.
+Speaks to the apiserver-sim (or any apiserver reachable without TLS client certs).
+"""
+from __future__ import annotations
+
+import http.client
+import json
+import os
+import socket
+import threading
+import time
+import urllib.parse
+from dataclasses import dataclass
+from typing import Any, Iterator
+
+from .api import schema
+
+
+class KubeError(Exception):
+    def __init__(self, code: int, body: Any):
+        self.code = code
+        self.body = body
+        msg = body.get("message") if isinstance(body, dict) else str(body)
+        self.reason = body.get("reason", "") if isinstance(body, dict) else ""
+        super().__init__(f"HTTP {code}: {msg}")
+
+
+@dataclass(frozen=True)
+class Res:
+    """A resource type: group ('' = core), version, plural, namespaced."""
+    group: str
+    version: str
+    plural: str
+    namespaced: bool = True
+
+    def path(self, ns: str | None = None, name: str | None = None, sub: str | None = None) -> str:
+        base = f"/apis/{self.group}/{self.version}" if self.group else f"/api/{self.version}"
+        if self.namespaced and ns:
+            base += f"/namespaces/{ns}"
+        base += f"/{self.plural}"
+        if name:
+            base += f"/{name}"
+        if sub:
+            base += f"/{sub}"
+        return base
+
+
+PODS = Res("", "v1", "pods")
+NODES = Res("", "v1", "nodes", namespaced=False)
+EVENTS = Res("", "v1", "events")
+SECRETS = Res("", "v1", "secrets")
+CONFIGMAPS = Res("", "v1", "configmaps")
+NAMESPACES = Res("", "v1", "namespaces", namespaced=False)
+LEASES = Res("coordination.k8s.io", "v1", "leases")
+CRDS = Res("apiextensions.k8s.io", "v1", "customresourcedefinitions", namespaced=False)
+MI355XPOOLS = Res(schema.GROUP, schema.VERSION, "mi355xpools")
+AZUREVMPOOLS = Res(schema.GROUP, schema.VERSION, "azurevmpools")
+
+BY_KIND = {
+    "Pod": PODS, "Node": NODES, "Event": EVENTS, "Secret": SECRETS, "ConfigMap": CONFIGMAPS,
+    "Namespace": NAMESPACES, "Lease": LEASES, "CustomResourceDefinition": CRDS,
+    "Mi355xPool": MI355XPOOLS, "AzureVmPool": AZUREVMPOOLS,
+}
+
+
+class Client:
+    def __init__(self, server: str, token: str | None = None, timeout: float = 30.0):
+        u = urllib.parse.urlparse(server if "://" in server else "http://" + server)
+        self.scheme = u.scheme
+        self.host = u.hostname or "127.0.0.1"
+        self.port = u.port or (443 if u.scheme == "https" else 80)
+        self.unix = u.path if u.scheme == "unix" else None
+        self.server = server
+        self.token = token
+        self.timeout = timeout
+        self._local = threading.local()
+
+    @classmethod
+    def from_env(cls) -> "Client":
+        return cls(os.environ.get("GPUPOOL_APISERVER", "http://127.0.0.1:6443"),
+                   os.environ.get("GPUPOOL_TOKEN") or None)
+
+    # ------------------------------------------------------------ transport
+    def _conn(self, timeout: float | None = None) -> http.client.HTTPConnection:
+        if self.unix:
+            return _UnixHTTPConnection(self.unix, timeout=timeout or self.timeout)
+        if self.scheme == "https":
+            return http.client.HTTPSConnection(self.host, self.port, timeout=timeout or self.timeout)
+        return http.client.HTTPConnection(self.host, self.port, timeout=timeout or self.timeout)
+
+    def _headers(self, ctype: str = "application/json", accept: str = "application/json") -> dict:
+        h = {"Content-Type": ctype, "Accept": accept}
+        if self.token:
+            h["Authorization"] = f"Bearer {self.token}"
+        return h
+
+    def request(self, method: str, path: str, body: Any = None, query: dict | None = None,
+                ctype: str = "application/json", accept: str = "application/json") -> Any:
+        if query:
+            q = {k: v for k, v in query.items() if v is not None}
+            if q:
+                path += "?" + urllib.parse.urlencode(q)
+        data = None if body is None else json.dumps(body).encode()
+        for attempt in range(2):
+            conn = getattr(self._local, "conn", None)
+            fresh = conn is None
+            if conn is None:
+                conn = self._local.conn = self._conn()
+            try:
+                conn.request(method, path, body=data, headers=self._headers(ctype, accept))
+                resp = conn.getresponse()
+                raw = resp.read()
+                break
+            except (http.client.HTTPException, ConnectionError, OSError):
+                self._local.conn = None
+                try:
+                    conn.close()
+                except Exception:
+                    pass
+                if fresh or attempt == 1:
+                    raise
+        try:
+            out = json.loads(raw) if raw else None
+        except json.JSONDecodeError:
+            out = raw.decode(errors="replace")
+        if resp.status >= 400:
+            raise KubeError(resp.status, out)
+        return out
+
+    # ------------------------------------------------------------ verbs
+    def get(self, res: Res, name: str, ns: str | None = None, sub: str | None = None) -> dict:
+        return self.request("GET", res.path(ns, name, sub))
+
+    def list(self, res: Res, ns: str | None = None, label_selector: str | None = None,
+             field_selector: str | None = None) -> dict:
+        return self.request("GET", res.path(ns), query={"labelSelector": label_selector,
+                                                        "fieldSelector": field_selector})
+
+    def table(self, res: Res, ns: str | None = None, name: str | None = None,
+              label_selector: str | None = None) -> dict:
+        return self.request("GET", res.path(ns, name), query={"labelSelector": label_selector},
+                            accept="application/json;as=Table;v=v1;g=meta.k8s.io")
+
+    def create(self, res: Res, obj: dict, ns: str | None = None, dry_run: bool = False) -> dict:
+        return self.request("POST", res.path(ns), obj, query={"dryRun": "All" if dry_run else None})
+
+    def update(self, res: Res, obj: dict, ns: str | None = None, sub: str | None = None,
+               dry_run: bool = False) -> dict:
+        return self.request("PUT", res.path(ns, obj["metadata"]["name"], sub), obj,
+                            query={"dryRun": "All" if dry_run else None})
+
+    def patch(self, res: Res, name: str, patch: Any, ns: str | None = None, sub: str | None = None,
+              ptype: str = "merge", dry_run: bool = False) -> dict:
+        ctype = {"merge": "application/merge-patch+json", "json": "application/json-patch+json",
+                 "strategic": "application/strategic-merge-patch+json"}[ptype]
+        return self.request("PATCH", res.path(ns, name, sub), patch, ctype=ctype,
+                            query={"dryRun": "All" if dry_run else None})
+
+    def delete(self, res: Res, name: str, ns: str | None = None, grace: int | None = None,
+               preconditions: dict | None = None) -> dict:
+        body: dict[str, Any] = {"kind": "DeleteOptions", "apiVersion": "v1"}
+        if grace is not None:
+            body["gracePeriodSeconds"] = grace
+        if preconditions:
+            body["preconditions"] = preconditions
+        return self.request("DELETE", res.path(ns, name), body)
+
+    def evict(self, ns: str, name: str, grace: int | None = None) -> dict:
+        body = {"apiVersion": "policy/v1", "kind": "Eviction",
+                "metadata": {"name": name, "namespace": ns}}
+        if grace is not None:
+            body["deleteOptions"] = {"gracePeriodSeconds": grace}
+        return self.request("POST", PODS.path(ns, name, "eviction"), body)
+
+    def apply(self, obj: dict, ns: str | None = None, dry_run: bool = False) -> tuple[str, dict]:
+        """kubectl-apply-like create-or-update (replace semantics; retries 409 on update)."""
+        res = res_for(obj)
+        ns = (obj.get("metadata", {}).get("namespace") or ns or "default") if res.namespaced else None
+        name = obj["metadata"]["name"]
+        for _ in range(10):
+            try:
+                cur = self.get(res, name, ns)
+            except KubeError as e:
+                if e.code != 404:
+                    raise
+                return "created", self.create(res, obj, ns, dry_run)
+            new = json.loads(json.dumps(obj))
+            md = new.setdefault("metadata", {})
+            md["resourceVersion"] = cur["metadata"]["resourceVersion"]
+            for k in ("finalizers", "labels", "annotations", "ownerReferences"):
+                if k not in md and k in cur["metadata"]:
+                    md[k] = cur["metadata"][k]
+            if "status" in cur:
+                new["status"] = cur["status"]
+            try:
+                out = self.update(res, new, ns, dry_run=dry_run)
+            except KubeError as e:
+                if e.code == 409:
+                    continue
+                raise
+            changed = out["metadata"]["resourceVersion"] != cur["metadata"]["resourceVersion"]
+            return ("configured" if changed else "unchanged"), out
+        raise KubeError(409, {"message": "apply: too many conflicts"})
+
+    # ------------------------------------------------------------ watch
+    def watch(self, res: Res, ns: str | None = None, resource_version: str | None = None,
+              label_selector: str | None = None, field_selector: str | None = None,
+              timeout_seconds: int | None = None, bookmarks: bool = True,
+              stop: threading.Event | None = None) -> Iterator[dict]:
+        """Yield watch events (dicts with ``type`` and ``object``) from one HTTP stream."""
+        q = {"watch": "1", "resourceVersion": resource_version, "labelSelector": label_selector,
+             "fieldSelector": field_selector, "allowWatchBookmarks": "true" if bookmarks else None,
+             "timeoutSeconds": timeout_seconds}
+        path = res.path(ns) + "?" + urllib.parse.urlencode({k: v for k, v in q.items() if v})
+        conn = self._conn(timeout=1.0 if stop is not None else (timeout_seconds or 3600) + 5)
+        conn.request("GET", path, headers=self._headers())
+        resp = conn.getresponse()
+        if resp.status >= 400:
+            raw = resp.read()
+            conn.close()
+            raise KubeError(resp.status, json.loads(raw) if raw else None)
+        buf = b""
+        try:
+            while True:
+                if stop is not None and stop.is_set():
+                    return
+                try:
+                    chunk = resp.read1(65536) if hasattr(resp, "read1") else resp.read(1)
+                except (socket.timeout, TimeoutError):
+                    continue
+                if not chunk:
+                    return
+                buf += chunk
+                while b"\n" in buf:
+                    line, buf = buf.split(b"\n", 1)
+                    if line.strip():
+                        yield json.loads(line)
+        finally:
+            conn.close()
+
+    def wait_for(self, res: Res, name: str, ns: str | None, pred, timeout: float = 30.0,
+                 poll: float | None = None) -> dict:
+        """Block until ``pred(obj)`` is true (watch-driven); returns the object."""
+        deadline = time.monotonic() + timeout
+        while True:
+            try:
+                obj = self.get(res, name, ns)
+                if pred(obj):
+                    return obj
+                rv = obj["metadata"]["resourceVersion"]
+            except KubeError as e:
+                if e.code != 404:
+                    raise
+                obj, rv = None, None
+                if pred(None):
+                    return None  # type: ignore[return-value]
+            remaining = deadline - time.monotonic()
+            if remaining <= 0:
+                raise TimeoutError(f"timed out waiting for {res.plural}/{name}: last={obj}")
+            if poll:
+                time.sleep(min(poll, remaining))
+                continue
+            try:
+                for ev in self.watch(res, ns, rv, field_selector=f"metadata.name={name}",
+                                     timeout_seconds=max(1, int(remaining) + 1)):
+                    if ev["type"] == "ERROR":
+                        break
+                    if ev["type"] == "BOOKMARK":
+                        continue
+                    o = None if ev["type"] == "DELETED" else ev["object"]
+                    if pred(o):
+                        return o  # type: ignore[return-value]
+                    if time.monotonic() > deadline:
+                        break
+            except (OSError, http.client.HTTPException):
+                time.sleep(0.05)
+
+
+class _UnixHTTPConnection(http.client.HTTPConnection):
+    def __init__(self, path: str, timeout: float = 30.0):
+        super().__init__("localhost", timeout=timeout)
+        self._path = path
+
+    def connect(self) -> None:
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.settimeout(self.timeout)
+        s.connect(self._path)
+        self.sock = s
+
+
+def res_for(obj: dict) -> Res:
+    kind = obj.get("kind")
+    if kind in BY_KIND:
+        return BY_KIND[kind]
+    api = obj.get("apiVersion", "v1")
+    g, v = api.split("/", 1) if "/" in api else ("", api)
+    return Res(g, v, kind.lower() + "s")

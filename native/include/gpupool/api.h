@@ -1,0 +1,79 @@
+// Typed views of the two pool kinds (schema source: gpupool/api/schema.py) plus metav1.Condition
+// semantics and validation that mirrors the CRD's OpenAPI checks (defence in depth: the manager
+// refuses to act on an object the apiserver should never have admitted).
+#pragma once
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "gpupool/json.h"
+
+namespace gpupool {
+
+struct ObjectMeta {
+  std::string ns, name, uid, resource_version, deletion_timestamp;
+  int64_t generation = 0;
+  std::vector<std::string> finalizers;
+  static ObjectMeta from(const Json& obj);
+  bool deleting() const { return !deletion_timestamp.empty(); }
+  bool has_finalizer(const std::string& f) const;
+  std::string key() const { return ns + "/" + name; }
+};
+
+// ---------------------------------------------------------------- AzureVmPool (README.md:92-118)
+struct ImageReference {
+  std::string publisher, offer, sku, version;
+};
+
+struct AzureVmPoolSpec {
+  int32_t replicas = 0;
+  std::string resource_group, location, vm_size, vnet, subnet, credential_secret;
+  ImageReference image;
+  static AzureVmPoolSpec from(const Json& spec);
+};
+
+// ---------------------------------------------------------------- Mi355xPool
+struct HealthPolicy {
+  int64_t max_uncorrectable_ecc = 0;
+  int64_t max_correctable_ecc = 100000;
+  bool require_all_xgmi = true;
+  int32_t min_xgmi_up = 7;
+  std::string thermal = "belowCritical";
+  int32_t thermal_margin_c = 0;
+  Json to_json() const;
+};
+
+struct Mi355xPoolSpec {
+  int32_t replicas = 0;
+  std::string node_name;
+  std::map<std::string, std::string> node_selector;
+  std::string resource_name = "amd.com/gpu";
+  std::string topology_policy = "xgmi-packed";
+  std::string partition_compute = "Any", partition_memory = "Any";
+  HealthPolicy health;
+  int64_t drain_grace_seconds = 30;
+  bool drain_evict = true;
+  int64_t drain_timeout_seconds = 300;
+  bool probe_enabled = true;
+  int64_t probe_hbm_bytes = 1LL << 30;
+  bool probe_mfma = true;
+  std::string replace_policy = "Replace";
+  static Mi355xPoolSpec from(const Json& spec);
+  Json policy_json() const;  // health + partition, as the agent/device library consume it
+};
+
+// Validation mirroring the CRD schema; returns "field: message" strings.
+std::vector<std::string> validate_azure(const Json& obj);
+std::vector<std::string> validate_mi355x(const Json& obj);
+
+// ---------------------------------------------------------------- conditions
+// meta.SetStatusCondition semantics: merge by type; lastTransitionTime moves only on a status
+// flip. Returns true if anything changed. ``conditions`` must be an array (or null).
+bool set_condition(Json& conditions, const std::string& type, const std::string& status,
+                   const std::string& reason, const std::string& message, int64_t generation,
+                   const std::string& now);
+const Json& find_condition(const Json& conditions, const std::string& type);
+bool condition_true(const Json& conditions, const std::string& type);
+
+}  // namespace gpupool

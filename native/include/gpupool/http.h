@@ -1,0 +1,121 @@
+// Blocking HTTP/1.1 client (TCP or unix socket, keep-alive pool, chunked decoding, line
+// streaming for k8s watches) and a tiny HTTP server for /metrics and /healthz.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <stdexcept>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+namespace gpupool {
+
+struct Url {
+  std::string scheme;     // http | unix
+  std::string host;       // tcp host
+  int port = 80;
+  std::string unix_path;  // for unix:///path/to.sock
+  static Url parse(const std::string& s);  // throws std::invalid_argument
+  std::string str() const;
+};
+
+struct HttpResponse {
+  int status = 0;
+  std::map<std::string, std::string> headers;  // lower-cased names
+  std::string body;
+};
+
+class HttpError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+// Incremental decoder for ``Transfer-Encoding: chunked`` bodies. Feed raw bytes; decoded payload
+// bytes are appended to ``out``. ``done()`` after the terminating zero-size chunk.
+class ChunkedDecoder {
+ public:
+  // Returns false on a protocol error (then the stream must be dropped).
+  bool feed(std::string_view in, std::string& out);
+  bool done() const { return state_ == State::Done; }
+
+ private:
+  enum class State { Size, SizeExt, SizeLF, Data, DataCR, DataLF, Trailer, TrailerLF, Done };
+  State state_ = State::Size;
+  uint64_t remaining_ = 0;
+  int size_digits_ = 0;
+  bool trailer_line_empty_ = true;
+};
+
+class HttpClient {
+ public:
+  explicit HttpClient(Url url, std::string bearer_token = "", int timeout_ms = 30000);
+  ~HttpClient();
+  HttpClient(const HttpClient&) = delete;
+  HttpClient& operator=(const HttpClient&) = delete;
+
+  HttpResponse request(const std::string& method, const std::string& path,
+                       const std::string& body = "",
+                       const std::string& content_type = "application/json",
+                       const std::string& accept = "application/json", int timeout_ms = -1);
+
+  // Streams a GET response line by line (k8s watch / agent long-poll). ``on_line`` returns false
+  // to stop. Returns the HTTP status; for status >= 400 ``err_body`` receives the body. Stops
+  // early when ``stop`` becomes true (checked at least every ``poll_ms``).
+  int stream_lines(const std::string& path, const std::function<bool(std::string_view)>& on_line,
+                   const std::atomic<bool>* stop, std::string* err_body = nullptr,
+                   int poll_ms = 200);
+
+  const Url& url() const { return url_; }
+
+ private:
+  struct Conn;
+  std::unique_ptr<Conn> connect_(int timeout_ms);
+  std::unique_ptr<Conn> take_();
+  void give_(std::unique_ptr<Conn> c);
+  bool send_request_(Conn& c, const std::string& method, const std::string& path,
+                     const std::string& body, const std::string& content_type,
+                     const std::string& accept);
+
+  Url url_;
+  std::string token_;
+  int timeout_ms_;
+  std::mutex mu_;
+  std::vector<std::unique_ptr<Conn>> idle_;
+};
+
+// Minimal threaded HTTP/1.1 server (Connection: close). For /metrics, /healthz, /readyz.
+class HttpServer {
+ public:
+  struct Reply {
+    int status = 200;
+    std::string content_type = "text/plain; charset=utf-8";
+    std::string body;
+  };
+  using Handler = std::function<Reply(const std::string& method, const std::string& path,
+                                      const std::string& body)>;
+
+  HttpServer() = default;
+  ~HttpServer();
+  void route(const std::string& path, Handler h);
+  // addr like ":8080", "127.0.0.1:0"; returns bound port. Throws on failure.
+  int listen(const std::string& addr);
+  void stop();
+
+ private:
+  void loop_();
+  void serve_(int fd);
+  std::map<std::string, Handler> routes_;
+  int lfd_ = -1;
+  std::atomic<bool> stop_{false};
+  std::thread th_;
+};
+
+std::string url_encode(std::string_view s);
+
+}  // namespace gpupool

@@ -1,0 +1,79 @@
+// Kubernetes REST client over HttpClient: typed errors, resource paths, CRUD, eviction, watch.
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <string>
+
+#include "gpupool/http.h"
+#include "gpupool/json.h"
+
+namespace gpupool {
+
+struct ResourceRef {
+  std::string group;  // "" = core
+  std::string version;
+  std::string plural;
+  bool namespaced = true;
+  std::string kind;
+
+  std::string path(const std::string& ns = "", const std::string& name = "",
+                   const std::string& sub = "") const;
+  std::string api_version() const { return group.empty() ? version : group + "/" + version; }
+};
+
+namespace res {
+ResourceRef pods();
+ResourceRef nodes();
+ResourceRef events();
+ResourceRef secrets();
+ResourceRef leases();
+ResourceRef mi355xpools();
+ResourceRef azurevmpools();
+}  // namespace res
+
+class KubeError : public std::runtime_error {
+ public:
+  KubeError(int code, std::string reason, const std::string& msg)
+      : std::runtime_error(msg), code(code), reason(std::move(reason)) {}
+  int code;
+  std::string reason;
+  bool not_found() const { return code == 404; }
+  bool conflict() const { return code == 409; }
+  bool gone() const { return code == 410; }
+};
+
+class KubeClient {
+ public:
+  KubeClient(const std::string& server, const std::string& token = "", int timeout_ms = 15000);
+
+  Json get(const ResourceRef& r, const std::string& ns, const std::string& name,
+           const std::string& sub = "");
+  Json list(const ResourceRef& r, const std::string& ns = "", const std::string& label_selector = "",
+            const std::string& field_selector = "");
+  Json create(const ResourceRef& r, const std::string& ns, const Json& obj);
+  Json update(const ResourceRef& r, const std::string& ns, const Json& obj,
+              const std::string& sub = "");
+  Json patch_merge(const ResourceRef& r, const std::string& ns, const std::string& name,
+                   const Json& patch, const std::string& sub = "");
+  Json del(const ResourceRef& r, const std::string& ns, const std::string& name, int grace = -1);
+  void evict(const std::string& ns, const std::string& name, int grace = -1);
+
+  // One watch stream from ``rv``; ``cb(type, object)`` returns false to stop. Throws KubeError
+  // (410 when ``rv`` was compacted, also for in-stream ERROR events). Returns the last RV seen.
+  std::string watch(const ResourceRef& r, const std::string& ns, const std::string& rv,
+                    const std::function<bool(const std::string&, const Json&)>& cb,
+                    const std::atomic<bool>* stop, int timeout_seconds = 300);
+
+  const std::string& server() const { return server_; }
+
+ private:
+  Json call_(const std::string& method, const std::string& path, const std::string& body,
+             const std::string& ctype = "application/json");
+  std::string server_;
+  std::string token_;
+  std::unique_ptr<HttpClient> http_;
+};
+
+}  // namespace gpupool

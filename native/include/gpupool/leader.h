@@ -1,0 +1,42 @@
+// Lease-based leader election (coordination.k8s.io/v1 Lease), the controller-runtime
+// ``--leader-elect`` analogue. Optimistic concurrency on the Lease's resourceVersion makes
+// two managers racing for an expired lease safe: exactly one update wins.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <string>
+
+#include "gpupool/kube.h"
+#include "gpupool/log.h"
+
+namespace gpupool {
+
+struct LeaderConfig {
+  std::string ns = "gpupool-system";
+  std::string name = "gpupool-manager-leader";
+  std::string identity;
+  std::chrono::milliseconds lease_duration{15000};
+  std::chrono::milliseconds renew_deadline{10000};
+  std::chrono::milliseconds retry_period{2000};
+};
+
+class LeaderElector {
+ public:
+  LeaderElector(KubeClient& client, LeaderConfig cfg);
+  // Blocks: acquires, calls on_started, renews until stop/loss, then calls on_stopped.
+  void run(const std::function<void()>& on_started, const std::function<void()>& on_stopped,
+           const std::atomic<bool>* stop);
+  // One acquire/renew attempt; returns true if we hold the lease afterwards.
+  bool try_acquire_or_renew();
+  bool is_leader() const { return leader_.load(); }
+
+ private:
+  KubeClient& client_;
+  LeaderConfig cfg_;
+  Logger log_;
+  std::atomic<bool> leader_{false};
+};
+
+}  // namespace gpupool

@@ -1,0 +1,172 @@
+// Provider layer (reference A5: getAzureVMClient/listManagedVMs/createVM/deleteVM,
+// README.md:179-221, contract README.md:238-240).
+//
+// Two provider families:
+//  * CloudProvider — the AzureVmPool contract (tag-scoped ownership, full cleanup of NIC + OS
+//    disk, idempotent create/delete). FakeCloudProvider implements it in-process (optionally
+//    persisted to a JSON file) because there is no Azure access here; provisioning is
+//    asynchronous (Creating -> Succeeded after a configurable delay) like ARM long-running ops.
+//  * DeviceProvider — the MI355X contract: enumerate physical GPUs per node, claim a delta
+//    all-or-nothing (gang-style), cordon/release, with per-device health verdicts.
+//    RocmProvider implements it by talking to each node's agent (HTTP over unix socket or TCP);
+//    the agent owns the claim ledger, libmi355x_dev and the HIP probe.
+#pragma once
+
+#include <chrono>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gpupool/api.h"
+#include "gpupool/http.h"
+#include "gpupool/json.h"
+
+namespace gpupool {
+
+class Informer;
+
+// ============================================================== cloud (AzureVmPool)
+struct Credentials {
+  std::map<std::string, std::string> values;
+};
+
+struct VmRecord {
+  std::string name, id, state;  // state: Creating | Succeeded | Deleting | Failed
+  std::string resource_group, location, vm_size, nic, os_disk, created_at, message;
+  std::map<std::string, std::string> tags;
+  Json to_json() const;
+};
+
+class ProviderError : public std::runtime_error {
+ public:
+  ProviderError(std::string code, const std::string& msg, bool transient = true)
+      : std::runtime_error(msg), code(std::move(code)), transient(transient) {}
+  std::string code;
+  bool transient;
+};
+
+class CloudProvider {
+ public:
+  virtual ~CloudProvider() = default;
+  // Tag-scoped listing: managed-by=azurevmpool-operator, owner=<ns>-<name> (README.md:238).
+  virtual std::vector<VmRecord> list(const Credentials& c, const std::string& rg, const std::string& owner) = 0;
+  // Starts an asynchronous create (idempotent on name). Returns the record in Creating state.
+  virtual VmRecord create(const Credentials& c, const AzureVmPoolSpec& spec, const std::string& owner,
+                          const std::string& name) = 0;
+  // Starts an asynchronous delete of VM + NIC + OS disk (README.md:216, :239). Idempotent.
+  virtual void destroy(const Credentials& c, const std::string& rg, const std::string& name) = 0;
+  // NICs / disks tagged for ``owner`` that no longer belong to a VM (must stay empty).
+  virtual std::vector<std::string> orphans(const std::string& rg, const std::string& owner) = 0;
+};
+
+struct FakeCloudOptions {
+  std::chrono::milliseconds provision{0};
+  std::chrono::milliseconds deprovision{0};
+  std::string state_file;     // persist the fake cloud across manager restarts
+  int quota_per_rg = 1000;    // create beyond this -> QuotaExceeded (transient)
+  std::string faults_file;    // {"failCreates": n, "failDeletes": n} consumed one by one
+};
+
+class FakeCloudProvider : public CloudProvider {
+ public:
+  explicit FakeCloudProvider(FakeCloudOptions opts);
+  std::vector<VmRecord> list(const Credentials& c, const std::string& rg, const std::string& owner) override;
+  VmRecord create(const Credentials& c, const AzureVmPoolSpec& spec, const std::string& owner,
+                  const std::string& name) override;
+  void destroy(const Credentials& c, const std::string& rg, const std::string& name) override;
+  std::vector<std::string> orphans(const std::string& rg, const std::string& owner) override;
+  Json dump();  // whole fake cloud (tests)
+
+ private:
+  struct Vm {
+    VmRecord rec;
+    std::chrono::steady_clock::time_point ready_at, gone_at;
+    bool deleting = false;
+  };
+  void advance_locked_();
+  void load_();
+  void save_locked_();
+  bool take_fault_(const char* key);
+  void check_creds_(const Credentials& c);
+  FakeCloudOptions opts_;
+  std::mutex mu_;
+  std::map<std::string, Vm> vms_;                       // key rg/name
+  std::map<std::string, std::map<std::string, std::string>> nics_, disks_;  // key rg/name -> tags
+  uint64_t seq_ = 0;
+};
+
+// ============================================================== devices (Mi355xPool)
+struct DeviceView {
+  std::string uuid, hip_uuid, bdf, render_node, node;
+  int64_t index = -1, kfd_node = -1;
+  std::string state;  // Free | Claimed | Draining | Quarantined | Probing
+  std::string pool_uid, pool;
+  bool healthy = false, advertised = false, probe_passed = false;
+  Json verdict, probe, pods;
+  std::string claimed_at, drain_started_at;
+  static DeviceView from(const Json& j);
+  Json status_json() const;
+};
+
+struct NodeView {
+  std::string name, endpoint, backend, error;
+  bool reachable = false;
+  bool advertise_required = true;
+  std::vector<DeviceView> devices;
+  int64_t gen = 0;
+};
+
+struct ClaimRequest {
+  std::string pool_uid, pool;  // pool = ns/name
+  int count = 0;
+  std::string topology_policy = "xgmi-packed";
+  std::string resource_name = "amd.com/gpu";
+  Json policy;  // {"health":{...},"partition":{...}}
+  Json probe;   // {"enabled","hbmBytes","mfma"}
+};
+
+struct ClaimResult {
+  bool ok = false;
+  std::string reason, message;
+  std::vector<DeviceView> devices;
+};
+
+class DeviceProvider {
+ public:
+  virtual ~DeviceProvider() = default;
+  virtual std::vector<std::string> node_names() = 0;
+  virtual Json node_labels(const std::string& node) = 0;
+  virtual NodeView observe(const std::string& node) = 0;
+  virtual ClaimResult claim(const std::string& node, const ClaimRequest& req) = 0;
+  virtual void cordon(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) = 0;
+  virtual void release(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) = 0;
+  virtual void update_policy(const std::string& node, const std::string& pool_uid, const Json& policy,
+                             const std::string& resource_name) = 0;
+};
+
+// Agents are discovered from Node objects annotated gpupool.amd.com/agent-endpoint.
+class RocmProvider : public DeviceProvider {
+ public:
+  RocmProvider(Informer& nodes, int timeout_ms = 30000);
+  std::vector<std::string> node_names() override;
+  Json node_labels(const std::string& node) override;
+  NodeView observe(const std::string& node) override;
+  ClaimResult claim(const std::string& node, const ClaimRequest& req) override;
+  void cordon(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) override;
+  void release(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) override;
+  void update_policy(const std::string& node, const std::string& pool_uid, const Json& policy,
+                     const std::string& resource_name) override;
+  std::string endpoint_of(const std::string& node);
+  HttpClient& client_for(const std::string& node);  // throws ProviderError if no agent
+
+ private:
+  Json post_(const std::string& node, const std::string& path, const Json& body);
+  Informer& nodes_;
+  int timeout_ms_;
+  std::mutex mu_;
+  std::map<std::string, std::pair<std::string, std::unique_ptr<HttpClient>>> clients_;
+};
+
+}  // namespace gpupool

@@ -1,0 +1,150 @@
+// Pool reconcilers — the MI355X-native re-design of AzureVmPoolReconciler.Reconcile
+// (README.md:170-235), fixing the reference's defects:
+//   A1 readyReplicas comes from a re-observation AFTER acting, counting only ready instances;
+//   A2 typed outcomes (RequeueAfter vs backoff) instead of RequeueAfter+err;
+//   A3 status written through the status subresource with conflict retry on a fresh GET;
+//   A4 deterministic scale-down victims with cordon + drain + eviction;
+//   A5 finalizer-guarded release; A6 full Conditions + status.devices/vms.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gpupool/api.h"
+#include "gpupool/events.h"
+#include "gpupool/informer.h"
+#include "gpupool/kube.h"
+#include "gpupool/log.h"
+#include "gpupool/metrics.h"
+#include "gpupool/provider.h"
+#include "gpupool/workqueue.h"
+
+namespace gpupool {
+
+// Typed reconcile outcome (SURVEY.md §5 failure-detection row).
+struct Outcome {
+  enum Kind { Done, RequeueAfter, Transient, Terminal } kind = Done;
+  std::chrono::milliseconds after{0};
+  std::string message;
+  static Outcome done(std::chrono::milliseconds resync) { return {Done, resync, ""}; }
+  static Outcome requeue(std::chrono::milliseconds d, std::string why = "") { return {RequeueAfter, d, std::move(why)}; }
+  static Outcome transient(std::string why) { return {Transient, std::chrono::milliseconds(0), std::move(why)}; }
+  static Outcome terminal(std::string why) { return {Terminal, std::chrono::milliseconds(0), std::move(why)}; }
+};
+
+struct ReconcilerOptions {
+  std::chrono::milliseconds resync{10000};        // steady-state health resync
+  std::chrono::milliseconds progress_poll{250};   // while scaling/draining
+  std::chrono::milliseconds credentials_retry{30000};  // README.md:184's 30 s, now effective
+  bool emit_events = true;
+};
+
+// Shared base: status writes with conflict retry, finalizer management, metrics.
+class PoolReconcilerBase {
+ public:
+  PoolReconcilerBase(KubeClient& client, Informer& pools, EventRecorder* events, ReconcilerOptions opts,
+                     std::string kind, ResourceRef res);
+  virtual ~PoolReconcilerBase() = default;
+  virtual Outcome reconcile(const std::string& ns, const std::string& name) = 0;
+  const std::string& kind() const { return kind_; }
+
+ protected:
+  // Writes ``status`` (unless semantically unchanged) with a fresh-GET retry on 409.
+  void write_status_(const Json& obj, const Json& status);
+  // Adds/removes the finalizer with RV precondition; returns the updated object.
+  Json ensure_finalizer_(const Json& obj);
+  Json remove_finalizer_(const Json& obj);
+  void event_(const Json& obj, const std::string& type, const std::string& reason, const std::string& msg);
+  void observe_ready_(const ObjectMeta& m, bool ready, int64_t desired);
+  void forget_(const std::string& uid);
+
+  KubeClient& client_;
+  Informer& pools_;
+  EventRecorder* events_;
+  ReconcilerOptions opts_;
+  std::string kind_;
+  ResourceRef res_;
+  Logger log_;
+  std::mutex mu_;
+  // reconcile-to-Ready tracking: uid -> (generation, first time that generation was seen)
+  std::map<std::string, std::pair<int64_t, std::chrono::steady_clock::time_point>> pending_;
+  std::map<std::string, int64_t> ready_gen_;
+};
+
+class Mi355xPoolReconciler : public PoolReconcilerBase {
+ public:
+  Mi355xPoolReconciler(KubeClient& client, Informer& pools, DeviceProvider& provider, EventRecorder* events,
+                       ReconcilerOptions opts = {});
+  Outcome reconcile(const std::string& ns, const std::string& name) override;
+  // Releases claims whose pool no longer exists (manager restart / force-deleted CR).
+  void sweep_orphans();
+
+ private:
+  struct Observed {
+    std::string node;
+    bool reachable = true;
+    std::string error;
+    std::vector<DeviceView> mine;
+    int64_t free_healthy = 0;
+  };
+  Observed observe_(const ObjectMeta& m, const Mi355xPoolSpec& spec, const Json& status);
+  std::string choose_node_(const Mi355xPoolSpec& spec, int need, const std::string& current);
+  Outcome finalize_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec);
+  // Evicts pods on draining devices and releases drained ones. Returns #devices still draining.
+  int drain_(const Json& obj, const std::string& node, const ObjectMeta& m, const Mi355xPoolSpec& spec,
+             std::vector<DeviceView>& mine);
+  Json build_status_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec, const Observed& o,
+                     const std::string& progress_reason, const std::string& progress_msg, bool insufficient,
+                     bool deleting);
+
+  DeviceProvider& provider_;
+  std::map<std::string, std::set<std::string>> evicted_;  // pool uid -> pod keys already evicted
+  std::map<std::string, int64_t> policy_gen_;             // pool uid -> generation pushed to agents
+};
+
+class AzureVmPoolReconciler : public PoolReconcilerBase {
+ public:
+  AzureVmPoolReconciler(KubeClient& client, Informer& pools, CloudProvider& cloud, EventRecorder* events,
+                        ReconcilerOptions opts = {});
+  Outcome reconcile(const std::string& ns, const std::string& name) override;
+
+ private:
+  bool credentials_(const ObjectMeta& m, const AzureVmPoolSpec& spec, Credentials* out, std::string* why);
+  CloudProvider& cloud_;
+  std::atomic<uint64_t> name_seq_{0};
+};
+
+// Controller: a shared work queue + N workers dispatching "Kind/ns/name" keys to reconcilers,
+// mapping Outcomes onto the queue (Done -> forget + resync; RequeueAfter -> forget + add_after;
+// Transient -> rate-limited backoff; Terminal -> forget, wait for the next spec change).
+class Controller {
+ public:
+  explicit Controller(int workers);
+  ~Controller();
+  void add_reconciler(PoolReconcilerBase* r);
+  void enqueue(const std::string& kind, const std::string& ns, const std::string& name);
+  void enqueue_after(const std::string& kind, const std::string& ns, const std::string& name,
+                     std::chrono::milliseconds d);
+  void start();
+  void stop();
+  WorkQueue& queue() { return q_; }
+  uint64_t reconciles() const { return reconciles_.load(); }
+
+ private:
+  void worker_();
+  int workers_;
+  WorkQueue q_;
+  std::map<std::string, PoolReconcilerBase*> by_kind_;
+  std::vector<std::thread> threads_;
+  std::atomic<uint64_t> reconciles_{0};
+  Logger log_{"controller"};
+};
+
+}  // namespace gpupool

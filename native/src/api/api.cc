@@ -1,0 +1,216 @@
+#include "gpupool/api.h"
+
+#include <algorithm>
+#include <regex>
+
+namespace gpupool {
+
+ObjectMeta ObjectMeta::from(const Json& obj) {
+  ObjectMeta m;
+  const Json& md = obj["metadata"];
+  m.ns = md["namespace"].as_string();
+  m.name = md["name"].as_string();
+  m.uid = md["uid"].as_string();
+  m.resource_version = md["resourceVersion"].as_string();
+  m.deletion_timestamp = md["deletionTimestamp"].as_string();
+  m.generation = md["generation"].as_int(0);
+  for (const auto& f : md["finalizers"].elements()) m.finalizers.push_back(f.as_string());
+  return m;
+}
+
+bool ObjectMeta::has_finalizer(const std::string& f) const {
+  return std::find(finalizers.begin(), finalizers.end(), f) != finalizers.end();
+}
+
+AzureVmPoolSpec AzureVmPoolSpec::from(const Json& s) {
+  AzureVmPoolSpec a;
+  a.replicas = static_cast<int32_t>(s["replicas"].as_int(0));
+  a.resource_group = s["resourceGroupName"].as_string();
+  a.location = s["location"].as_string();
+  a.vm_size = s["vmSize"].as_string();
+  a.vnet = s["vnetName"].as_string();
+  a.subnet = s["subnetName"].as_string();
+  a.credential_secret = s["azureCredentialSecret"].as_string();
+  const Json& img = s["imageReference"];
+  a.image = {img["publisher"].as_string(), img["offer"].as_string(), img["sku"].as_string(),
+             img["version"].as_string()};
+  return a;
+}
+
+Json HealthPolicy::to_json() const {
+  Json j = Json::object();
+  j["maxUncorrectableECC"] = max_uncorrectable_ecc;
+  j["maxCorrectableECC"] = max_correctable_ecc;
+  j["requireAllXGMILinks"] = require_all_xgmi;
+  j["minXGMILinksUp"] = min_xgmi_up;
+  j["thermal"] = thermal;
+  j["thermalMarginC"] = thermal_margin_c;
+  return j;
+}
+
+Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
+  Mi355xPoolSpec p;
+  p.replicas = static_cast<int32_t>(s["replicas"].as_int(0));
+  p.node_name = s["nodeName"].as_string();
+  for (const auto& kv : s["nodeSelector"].members()) p.node_selector[kv.first] = kv.second.as_string();
+  p.resource_name = s["resourceName"].str_or("amd.com/gpu");
+  p.topology_policy = s["topologyPolicy"].str_or("xgmi-packed");
+  p.partition_compute = s.path("partition.compute").str_or("Any");
+  p.partition_memory = s.path("partition.memory").str_or("Any");
+  const Json& h = s["health"];
+  p.health.max_uncorrectable_ecc = h["maxUncorrectableECC"].as_int(0);
+  p.health.max_correctable_ecc = h["maxCorrectableECC"].as_int(100000);
+  p.health.require_all_xgmi = h["requireAllXGMILinks"].as_bool(true);
+  p.health.min_xgmi_up = static_cast<int32_t>(h["minXGMILinksUp"].as_int(7));
+  p.health.thermal = h["thermal"].str_or("belowCritical");
+  p.health.thermal_margin_c = static_cast<int32_t>(h["thermalMarginC"].as_int(0));
+  const Json& d = s["drain"];
+  p.drain_grace_seconds = d["gracePeriodSeconds"].as_int(30);
+  p.drain_evict = d["evict"].as_bool(true);
+  p.drain_timeout_seconds = d["timeoutSeconds"].as_int(300);
+  const Json& pr = s["probe"];
+  p.probe_enabled = pr["enabled"].as_bool(true);
+  p.probe_hbm_bytes = pr["hbmBytes"].as_int(1LL << 30);
+  p.probe_mfma = pr["mfma"].as_bool(true);
+  p.replace_policy = s["replacePolicy"].str_or("Replace");
+  return p;
+}
+
+Json Mi355xPoolSpec::policy_json() const {
+  Json j = Json::object();
+  j["health"] = health.to_json();
+  j["partition"]["compute"] = partition_compute;
+  j["partition"]["memory"] = partition_memory;
+  return j;
+}
+
+namespace {
+
+void require_string(const Json& s, const char* field, std::vector<std::string>& errs) {
+  if (!s.contains(field)) {
+    errs.push_back(std::string("spec.") + field + ": Required value");
+  } else if (!s[field].is_string()) {
+    errs.push_back(std::string("spec.") + field + ": must be of type string");
+  }
+}
+
+bool in(const std::string& v, std::initializer_list<const char*> xs) {
+  for (const char* x : xs)
+    if (v == x) return true;
+  return false;
+}
+
+}  // namespace
+
+std::vector<std::string> validate_azure(const Json& obj) {
+  std::vector<std::string> errs;
+  const Json& s = obj["spec"];
+  if (!s.is_object()) return {"spec: Required value"};
+  if (!s["replicas"].is_int()) {
+    errs.push_back("spec.replicas: Required value (integer)");
+  } else if (s["replicas"].as_int() < 0) {
+    errs.push_back("spec.replicas: Invalid value: " + std::to_string(s["replicas"].as_int()) +
+                   ": should be greater than or equal to 0");
+  }
+  for (const char* f : {"resourceGroupName", "location", "vmSize", "vnetName", "subnetName", "azureCredentialSecret"})
+    require_string(s, f, errs);
+  const Json& img = s["imageReference"];
+  if (!img.is_object()) {
+    errs.push_back("spec.imageReference: Required value");
+  } else {
+    for (const char* f : {"publisher", "offer", "sku", "version"})
+      if (!img[f].is_string()) errs.push_back(std::string("spec.imageReference.") + f + ": Required value");
+  }
+  return errs;
+}
+
+std::vector<std::string> validate_mi355x(const Json& obj) {
+  std::vector<std::string> errs;
+  const Json& s = obj["spec"];
+  if (!s.is_object()) return {"spec: Required value"};
+  if (!s["replicas"].is_int()) {
+    errs.push_back("spec.replicas: Required value (integer)");
+  } else {
+    int64_t r = s["replicas"].as_int();
+    if (r < 0) errs.push_back("spec.replicas: Invalid value: " + std::to_string(r) + ": should be greater than or equal to 0");
+    if (r > 1024) errs.push_back("spec.replicas: Invalid value: " + std::to_string(r) + ": should be less than or equal to 1024");
+  }
+  if (s.contains("resourceName")) {
+    static const std::regex re("^[a-z0-9.-]+/[a-z0-9.-]+$");
+    if (!s["resourceName"].is_string() || !std::regex_match(s["resourceName"].as_string(), re))
+      errs.push_back("spec.resourceName: Invalid value: should match '^[a-z0-9.-]+/[a-z0-9.-]+$'");
+  }
+  if (s.contains("topologyPolicy") && !in(s["topologyPolicy"].as_string(), {"xgmi-packed", "any"}))
+    errs.push_back("spec.topologyPolicy: Unsupported value");
+  if (s.contains("replacePolicy") && !in(s["replacePolicy"].as_string(), {"Replace", "Keep"}))
+    errs.push_back("spec.replacePolicy: Unsupported value");
+  const Json& h = s["health"];
+  if (h.contains("thermal") && !in(h["thermal"].as_string(), {"belowCritical", "belowEmergency", "ignore"}))
+    errs.push_back("spec.health.thermal: Unsupported value");
+  if (h.contains("maxUncorrectableECC") && h["maxUncorrectableECC"].as_int(0) < 0)
+    errs.push_back("spec.health.maxUncorrectableECC: should be greater than or equal to 0");
+  if (h.contains("minXGMILinksUp")) {
+    int64_t v = h["minXGMILinksUp"].as_int(0);
+    if (v < 0 || v > 8) errs.push_back("spec.health.minXGMILinksUp: must be within [0, 8]");
+  }
+  const Json& pr = s["probe"];
+  if (pr.contains("hbmBytes")) {
+    int64_t b = pr["hbmBytes"].as_int(0);
+    if (b < (1LL << 20) || b > (64LL << 30)) errs.push_back("spec.probe.hbmBytes: must be within [1MiB, 64GiB]");
+  }
+  const Json& part = s["partition"];
+  if (part.contains("compute") && !in(part["compute"].as_string(), {"Any", "SPX", "DPX", "QPX", "CPX"}))
+    errs.push_back("spec.partition.compute: Unsupported value");
+  if (part.contains("memory") && !in(part["memory"].as_string(), {"Any", "NPS1", "NPS2", "NPS4", "NPS8"}))
+    errs.push_back("spec.partition.memory: Unsupported value");
+  return errs;
+}
+
+const Json& find_condition(const Json& conditions, const std::string& type) {
+  for (const auto& c : conditions.elements())
+    if (c["type"].as_string() == type) return c;
+  return Json::null_ref();
+}
+
+bool condition_true(const Json& conditions, const std::string& type) {
+  return find_condition(conditions, type)["status"].as_string() == "True";
+}
+
+bool set_condition(Json& conditions, const std::string& type, const std::string& status,
+                   const std::string& reason, const std::string& message, int64_t generation,
+                   const std::string& now) {
+  if (!conditions.is_array()) conditions = Json::array();
+  for (auto& c : conditions.elements()) {
+    if (c["type"].as_string() != type) continue;
+    bool changed = false;
+    if (c["status"].as_string() != status) {
+      c["status"] = status;
+      c["lastTransitionTime"] = now;
+      changed = true;
+    }
+    if (c["reason"].as_string() != reason) {
+      c["reason"] = reason;
+      changed = true;
+    }
+    if (c["message"].as_string() != message) {
+      c["message"] = message;
+      changed = true;
+    }
+    if (c["observedGeneration"].as_int(-1) != generation) {
+      c["observedGeneration"] = generation;
+      changed = true;
+    }
+    return changed;
+  }
+  Json c = Json::object();
+  c["type"] = type;
+  c["status"] = status;
+  c["observedGeneration"] = generation;
+  c["lastTransitionTime"] = now;
+  c["reason"] = reason;
+  c["message"] = message;
+  conditions.push_back(c);
+  return true;
+}
+
+}  // namespace gpupool

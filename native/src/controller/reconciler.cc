@@ -1,0 +1,867 @@
+#include "gpupool/reconciler.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <random>
+#include <sstream>
+
+#include "gpupool/generated/schema_consts.h"
+
+namespace gpupool {
+
+namespace {
+
+using clock_t_ = std::chrono::steady_clock;
+using ms = std::chrono::milliseconds;
+
+std::string join(const std::vector<std::string>& v, const char* sep) {
+  std::string out;
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (i) out += sep;
+    out += v[i];
+  }
+  return out;
+}
+
+std::string short_id(const DeviceView& d) {
+  std::string u = !d.hip_uuid.empty() ? d.hip_uuid : d.uuid;
+  return u + "(#" + std::to_string(d.index) + ")";
+}
+
+HistogramVec& reconcile_hist() {
+  static HistogramVec& h = Registry::global().histogram(
+      "gpupool_reconcile_duration_seconds", "Time spent in one reconcile pass.", exponential_buckets(0.0005, 2, 18));
+  return h;
+}
+HistogramVec& to_ready_hist() {
+  static HistogramVec& h = Registry::global().histogram(
+      "gpupool_reconcile_to_ready_seconds",
+      "From the first reconcile of a spec generation to the status write that reports it Ready.",
+      exponential_buckets(0.001, 2, 18));
+  return h;
+}
+CounterVec& reconcile_total() {
+  static CounterVec& c = Registry::global().counter("gpupool_reconcile_total", "Reconcile passes by kind and result.");
+  return c;
+}
+GaugeVec& ready_gauge() {
+  static GaugeVec& g = Registry::global().gauge("gpupool_ready_replicas", "status.readyReplicas per pool.");
+  return g;
+}
+GaugeVec& desired_gauge() {
+  static GaugeVec& g = Registry::global().gauge("gpupool_desired_replicas", "spec.replicas per pool.");
+  return g;
+}
+
+}  // namespace
+
+// ================================================================== base
+PoolReconcilerBase::PoolReconcilerBase(KubeClient& client, Informer& pools, EventRecorder* events,
+                                       ReconcilerOptions opts, std::string kind, ResourceRef res)
+    : client_(client), pools_(pools), events_(events), opts_(opts), kind_(std::move(kind)), res_(std::move(res)),
+      log_(Logger("reconciler").with("kind", kind_)) {}
+
+void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
+  Json cur = obj;
+  const std::string ns = obj.path("metadata.namespace").as_string();
+  const std::string name = obj.path("metadata.name").as_string();
+  if (cur["status"] == status) return;  // semantically unchanged: no write, no watch churn
+  for (int attempt = 0; attempt < 6; ++attempt) {
+    Json upd = cur;
+    upd["status"] = status;
+    try {
+      client_.update(res_, ns, upd, "status");
+      return;
+    } catch (const KubeError& e) {
+      if (!e.conflict()) throw;
+      cur = client_.get(res_, ns, name);  // fresh read, then re-apply our (re-derived) status
+      if (cur["status"] == status) return;
+    }
+  }
+  throw KubeError(409, "Conflict", "status update kept conflicting for " + ns + "/" + name);
+}
+
+Json PoolReconcilerBase::ensure_finalizer_(const Json& obj) {
+  ObjectMeta m = ObjectMeta::from(obj);
+  if (m.has_finalizer(gen::kFinalizer)) return obj;
+  Json fins = Json::array();
+  for (const auto& f : m.finalizers) fins.push_back(f);
+  fins.push_back(gen::kFinalizer);
+  Json patch = Json::object();
+  patch["metadata"]["finalizers"] = fins;
+  patch["metadata"]["resourceVersion"] = m.resource_version;  // optimistic concurrency
+  return client_.patch_merge(res_, m.ns, m.name, patch);
+}
+
+Json PoolReconcilerBase::remove_finalizer_(const Json& obj) {
+  ObjectMeta m = ObjectMeta::from(obj);
+  Json fins = Json::array();
+  for (const auto& f : m.finalizers)
+    if (f != gen::kFinalizer) fins.push_back(f);
+  Json patch = Json::object();
+  patch["metadata"]["finalizers"] = fins;
+  patch["metadata"]["resourceVersion"] = m.resource_version;
+  return client_.patch_merge(res_, m.ns, m.name, patch);
+}
+
+void PoolReconcilerBase::event_(const Json& obj, const std::string& type, const std::string& reason,
+                                const std::string& msg) {
+  if (events_ && opts_.emit_events) events_->record(obj, type, reason, msg);
+}
+
+void PoolReconcilerBase::observe_ready_(const ObjectMeta& m, bool ready, int64_t desired) {
+  Labels l{{"kind", kind_}, {"pool", m.key()}};
+  desired_gauge().set(l, static_cast<double>(desired));
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pending_.find(m.uid);
+  if (it == pending_.end() || it->second.first != m.generation) {
+    pending_[m.uid] = {m.generation, clock_t_::now()};
+    it = pending_.find(m.uid);
+  }
+  if (ready && ready_gen_[m.uid] != m.generation) {
+    ready_gen_[m.uid] = m.generation;
+    double s = std::chrono::duration<double>(clock_t_::now() - it->second.second).count();
+    to_ready_hist().observe({{"kind", kind_}}, s);
+    log_.info("pool ready", Json::object().set("pool", m.key()).set("generation", m.generation).set("reconcileToReadySeconds", s));
+  }
+}
+
+void PoolReconcilerBase::forget_(const std::string& uid) {
+  std::lock_guard<std::mutex> g(mu_);
+  pending_.erase(uid);
+  ready_gen_.erase(uid);
+}
+
+// ================================================================== Mi355xPool
+Mi355xPoolReconciler::Mi355xPoolReconciler(KubeClient& client, Informer& pools, DeviceProvider& provider,
+                                           EventRecorder* events, ReconcilerOptions opts)
+    : PoolReconcilerBase(client, pools, events, opts, "Mi355xPool", res::mi355xpools()), provider_(provider) {}
+
+Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& m, const Mi355xPoolSpec& spec,
+                                                              const Json& status) {
+  Observed o;
+  std::vector<std::string> nodes;
+  std::string hint = status["nodeName"].as_string();
+  if (!hint.empty()) nodes.push_back(hint);
+  if (!spec.node_name.empty() && spec.node_name != hint) nodes.push_back(spec.node_name);
+  if (nodes.empty()) nodes = provider_.node_names();
+  for (const auto& n : nodes) {
+    NodeView nv = provider_.observe(n);
+    if (!nv.reachable) {
+      if (n == hint || n == spec.node_name) {
+        o.reachable = false;
+        o.error = nv.error;
+        o.node = n;
+      }
+      continue;
+    }
+    std::vector<DeviceView> mine;
+    int64_t free_healthy = 0;
+    for (auto& d : nv.devices) {
+      if (d.pool_uid == m.uid) mine.push_back(d);
+      else if (d.state == "Free" && d.healthy) ++free_healthy;
+    }
+    if (!mine.empty() || n == hint || (o.node.empty() && n == spec.node_name)) {
+      o.node = n;
+      o.reachable = true;
+      o.error.clear();
+      o.mine = std::move(mine);
+      o.free_healthy = free_healthy;
+      if (!o.mine.empty()) break;
+    }
+  }
+  std::sort(o.mine.begin(), o.mine.end(), [](const DeviceView& a, const DeviceView& b) { return a.index < b.index; });
+  return o;
+}
+
+std::string Mi355xPoolReconciler::choose_node_(const Mi355xPoolSpec& spec, int need, const std::string& current) {
+  if (!spec.node_name.empty()) return spec.node_name;
+  if (!current.empty()) return current;
+  std::string best;
+  int64_t best_free = -1;
+  auto names = provider_.node_names();
+  std::sort(names.begin(), names.end());
+  for (const auto& n : names) {
+    Json labels = provider_.node_labels(n);
+    bool match = true;
+    for (const auto& kv : spec.node_selector)
+      if (labels[kv.first].as_string() != kv.second) match = false;
+    if (!match) continue;
+    NodeView nv = provider_.observe(n);
+    if (!nv.reachable) continue;
+    int64_t free = 0;
+    for (const auto& d : nv.devices)
+      if (d.state == "Free" && d.healthy) ++free;
+    // prefer the tightest node that fits (bin-packing keeps whole nodes free for big pools)
+    bool fits = free >= need, best_fits = best_free >= need;
+    if (best.empty() || (fits && !best_fits) || (fits && best_fits && free < best_free) ||
+        (!fits && !best_fits && free > best_free)) {
+      best = n;
+      best_free = free;
+    }
+  }
+  return best;
+}
+
+int Mi355xPoolReconciler::drain_(const Json& obj, const std::string& node, const ObjectMeta& m,
+                                 const Mi355xPoolSpec& spec, std::vector<DeviceView>& mine) {
+  int still = 0;
+  std::vector<std::string> release;
+  auto now = std::chrono::system_clock::now();
+  for (auto& d : mine) {
+    if (d.state != "Draining") continue;
+    if (d.pods.size() == 0) {
+      release.push_back(d.uuid);
+      continue;
+    }
+    ++still;
+    bool timed_out = false;
+    std::chrono::system_clock::time_point started;
+    if (parse_rfc3339(d.drain_started_at, &started))
+      timed_out = now - started > std::chrono::seconds(spec.drain_timeout_seconds);
+    for (const auto& p : d.pods.elements()) {
+      std::string pns = p["namespace"].as_string(), pname = p["name"].as_string();
+      if (p.is_string()) {
+        auto slash = p.as_string().find('/');
+        pns = p.as_string().substr(0, slash);
+        pname = p.as_string().substr(slash + 1);
+      }
+      std::string key = pns + "/" + pname;
+      try {
+        if (timed_out) {
+          client_.del(res::pods(), pns, pname, 0);
+          event_(obj, "Warning", "DrainTimeout", "force-deleted pod " + key + " on " + short_id(d) +
+                                                     " after " + std::to_string(spec.drain_timeout_seconds) + "s");
+        } else if (spec.drain_evict) {
+          bool first;
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            first = evicted_[m.uid].insert(key).second;
+          }
+          if (first) {
+            client_.evict(pns, pname, static_cast<int>(spec.drain_grace_seconds));
+            event_(obj, "Normal", "PodEvicted", "evicted pod " + key + " from " + short_id(d) + " (draining)");
+          }
+        }
+      } catch (const KubeError& e) {
+        if (!e.not_found()) log_.warn("drain action failed", Json::object().set("pod", key).set("error", e.what()));
+      }
+    }
+  }
+  if (!release.empty()) {
+    provider_.release(node, m.uid, release);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      evicted_[m.uid].clear();
+    }
+    event_(obj, "Normal", "GPUReleased", "released " + std::to_string(release.size()) + " GPU(s) on " + node + ": " + join(release, ","));
+  }
+  return still;
+}
+
+Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec,
+                                         const Observed& o, const std::string& progress_reason,
+                                         const std::string& progress_msg, bool insufficient, bool deleting) {
+  const std::string now = rfc3339_now();
+  Json st = Json::object();
+  st["observedGeneration"] = m.generation;
+  int64_t claimed = 0, ready = 0, probing = 0;
+  std::vector<std::string> xgmi_bad, ecc_bad, thermal_bad, probe_bad, unhealthy;
+  double min_gbps = 1e30, min_tf = 1e30;
+  Json devices = Json::array();
+  for (const auto& d : o.mine) {
+    devices.push_back(d.status_json());
+    if (d.state == "Draining") continue;
+    ++claimed;
+    if (d.state == "Probing") {
+      ++probing;
+      continue;
+    }
+    auto reasons = [&](const char* prefix) {
+      std::vector<std::string> rs;
+      for (const auto& r : d.verdict["reasons"].elements())
+        if (r.as_string().rfind(prefix, 0) == 0) rs.push_back(r.as_string());
+      return short_id(d) + ": " + join(rs, "; ");
+    };
+    if (!d.verdict["xgmiOk"].as_bool(true)) xgmi_bad.push_back(reasons("XGMI"));
+    if (!d.verdict["eccOk"].as_bool(true)) ecc_bad.push_back(reasons("HBM"));
+    if (!d.verdict["thermalOk"].as_bool(true)) thermal_bad.push_back(reasons("Thermal"));
+    if (!d.probe_passed) {
+      probe_bad.push_back(short_id(d) + ": " + d.probe["error"].str_or(d.probe.is_object() ? "probe failed" : "not probed"));
+    } else {
+      min_gbps = std::min(min_gbps, d.probe.path("hbm.GBps").as_double(1e30));
+      min_tf = std::min(min_tf, d.probe.path("mfma.tflops").as_double(1e30));
+    }
+    if (!d.healthy || !d.probe_passed) unhealthy.push_back(short_id(d));
+    if (d.state == "Claimed" && d.healthy && d.probe_passed && d.advertised) ++ready;
+  }
+  st["replicas"] = claimed;
+  st["readyReplicas"] = ready;
+  if (!o.node.empty()) st["nodeName"] = o.node;
+  st["devices"] = devices;
+  Json conds = obj.path("status.conditions").is_array() ? obj.path("status.conditions") : Json::array();
+  const int64_t gen = m.generation;
+  auto health_cond = [&](const char* type, const std::vector<std::string>& bad, const char* bad_reason,
+                         const char* ok_reason, const char* ok_msg) {
+    if (!bad.empty()) set_condition(conds, type, "False", bad_reason, join(bad, " | "), gen, now);
+    else set_condition(conds, type, "True", claimed ? ok_reason : "NoDevices",
+                       claimed ? std::to_string(claimed) + " GPU(s): " + ok_msg : "no GPUs claimed", gen, now);
+  };
+  health_cond(gen::kCondXGMILinksHealthy, xgmi_bad, "XGMILinkDown", "AllLinksUp", "xGMI links up");
+  health_cond(gen::kCondHBMECCHealthy, ecc_bad, "HBMECCErrors", "NoNewECCErrors", "no new HBM ECC errors since claim");
+  health_cond(gen::kCondThermalHealthy, thermal_bad, "ThermalLimit", "WithinThermalLimits",
+              "temperatures below device limits");
+  if (probing) {
+    set_condition(conds, gen::kCondDeviceProbePassed, "Unknown", "Probing", std::to_string(probing) + " GPU(s) probing", gen, now);
+  } else if (!probe_bad.empty()) {
+    set_condition(conds, gen::kCondDeviceProbePassed, "False", "ProbeFailed", join(probe_bad, " | "), gen, now);
+  } else if (claimed) {
+    char msg[200];
+    std::snprintf(msg, sizeof msg, "%lld GPU(s) passed HBM+MFMA probe (min HBM %.0f GB/s, min MFMA %.0f TFLOP/s)",
+                  static_cast<long long>(claimed), min_gbps > 1e29 ? 0.0 : min_gbps, min_tf > 1e29 ? 0.0 : min_tf);
+    set_condition(conds, gen::kCondDeviceProbePassed, "True", "ProbePassed", msg, gen, now);
+  } else {
+    set_condition(conds, gen::kCondDeviceProbePassed, "True", "NoDevices", "no GPUs claimed", gen, now);
+  }
+  if (!o.reachable) {
+    set_condition(conds, gen::kCondDegraded, "True", "AgentUnreachable", o.error, gen, now);
+  } else if (!unhealthy.empty()) {
+    set_condition(conds, gen::kCondDegraded, "True", "DeviceUnhealthy", join(unhealthy, ", "), gen, now);
+  } else if (insufficient) {
+    set_condition(conds, gen::kCondDegraded, "True", "InsufficientDevices", progress_msg, gen, now);
+  } else {
+    set_condition(conds, gen::kCondDegraded, "False", "AsExpected", "all claimed GPUs healthy", gen, now);
+  }
+  if (insufficient) {
+    set_condition(conds, gen::kCondProgressing, "False", "InsufficientDevices", progress_msg, gen, now);
+  } else if (!progress_reason.empty()) {
+    set_condition(conds, gen::kCondProgressing, "True", progress_reason, progress_msg, gen, now);
+  } else {
+    set_condition(conds, gen::kCondProgressing, "False", "Stable",
+                  std::to_string(ready) + "/" + std::to_string(spec.replicas) + " GPUs ready", gen, now);
+  }
+  set_condition(conds, gen::kCondDeleting, deleting ? "True" : "False", deleting ? "Finalizing" : "NotDeleting",
+                deleting ? "draining and releasing GPUs before removing the finalizer" : "", gen, now);
+  bool is_ready = !deleting && o.reachable && ready == spec.replicas && claimed == spec.replicas;
+  std::string reason = is_ready ? "AllReplicasReady"
+                       : deleting ? "Deleting"
+                       : !o.reachable ? "AgentUnreachable"
+                       : insufficient ? "InsufficientDevices"
+                       : probing ? "Probing"
+                       : !progress_reason.empty() ? progress_reason
+                       : !unhealthy.empty() ? "DeviceUnhealthy"
+                       : "NotReady";
+  set_condition(conds, gen::kCondReady, is_ready ? "True" : "False", reason,
+                std::to_string(ready) + "/" + std::to_string(spec.replicas) + " GPUs ready" +
+                    (o.node.empty() ? "" : " on " + o.node),
+                gen, now);
+  st["conditions"] = conds;
+  return st;
+}
+
+Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec) {
+  Observed o = observe_(m, spec, obj["status"]);
+  if (!o.reachable && !o.node.empty()) {
+    write_status_(obj, build_status_(obj, m, spec, o, "Deleting", "agent unreachable", false, true));
+    return Outcome::transient("agent unreachable during finalization: " + o.error);
+  }
+  std::vector<std::string> cordon;
+  for (const auto& d : o.mine)
+    if (d.state != "Draining") cordon.push_back(d.uuid);
+  if (!cordon.empty()) {
+    provider_.cordon(o.node, m.uid, cordon);
+    event_(obj, "Normal", "DrainStarted", "pool deleting: draining " + std::to_string(cordon.size()) + " GPU(s)");
+    o = observe_(m, spec, obj["status"]);
+  }
+  int still = drain_(obj, o.node, m, spec, o.mine);
+  if (!o.mine.empty()) o = observe_(m, spec, obj["status"]);
+  if (still > 0 || !o.mine.empty()) {
+    write_status_(obj, build_status_(obj, m, spec, o, "Draining", std::to_string(still) + " GPU(s) still have pods",
+                                     false, true));
+    return Outcome::requeue(opts_.progress_poll, "draining");
+  }
+  if (m.has_finalizer(gen::kFinalizer)) {
+    remove_finalizer_(obj);
+    event_(obj, "Normal", "Finalized", "all GPUs released; finalizer removed");
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    evicted_.erase(m.uid);
+    policy_gen_.erase(m.uid);
+  }
+  forget_(m.uid);
+  ready_gauge().erase({{"kind", kind_}, {"pool", m.key()}});
+  desired_gauge().erase({{"kind", kind_}, {"pool", m.key()}});
+  return Outcome::done(ms(0));
+}
+
+Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string& name) {
+  auto cached = pools_.get(ns, name);
+  if (!cached) return Outcome::done(ms(0));  // gone (finalizer already removed)
+  Json obj = *cached;
+  ObjectMeta m = ObjectMeta::from(obj);
+  Logger log = log_.with("pool", m.key()).with("generation", m.generation);
+  auto errs = validate_mi355x(obj);
+  if (!errs.empty()) {
+    Json st = obj["status"].is_object() ? obj["status"] : Json::object();
+    Json conds = st["conditions"].is_array() ? st["conditions"] : Json::array();
+    set_condition(conds, gen::kCondReady, "False", "InvalidSpec", join(errs, "; "), m.generation, rfc3339_now());
+    st["conditions"] = conds;
+    st["observedGeneration"] = m.generation;
+    write_status_(obj, st);
+    return Outcome::terminal("invalid spec: " + join(errs, "; "));
+  }
+  Mi355xPoolSpec spec = Mi355xPoolSpec::from(obj["spec"]);
+  if (m.deleting()) return finalize_(obj, m, spec);
+  if (!m.has_finalizer(gen::kFinalizer)) {
+    obj = ensure_finalizer_(obj);
+    m = ObjectMeta::from(obj);
+  }
+
+  Observed o = observe_(m, spec, obj["status"]);
+  if (!o.reachable && !o.node.empty()) {
+    write_status_(obj, build_status_(obj, m, spec, o, "", "", false, false));
+    ready_gauge().set({{"kind", kind_}, {"pool", m.key()}}, 0);
+    return Outcome::transient("agent on " + o.node + " unreachable: " + o.error);
+  }
+  // Push the (possibly edited) health policy to the agent owning our GPUs.
+  if (!o.mine.empty()) {
+    bool push;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      push = policy_gen_[m.uid] != m.generation;
+    }
+    if (push) {
+      provider_.update_policy(o.node, m.uid, spec.policy_json(), spec.resource_name);
+      std::lock_guard<std::mutex> g(mu_);
+      policy_gen_[m.uid] = m.generation;
+    }
+  }
+
+  std::string progress_reason, progress_msg;
+  bool insufficient = false, acted = false;
+  std::vector<const DeviceView*> active;
+  for (const auto& d : o.mine)
+    if (d.state != "Draining") active.push_back(&d);
+
+  std::vector<std::string> cordon;
+  std::vector<const DeviceView*> keep;
+  for (const DeviceView* d : active) {
+    bool bad = d->state != "Probing" && (!d->healthy || !d->probe_passed);
+    if (bad && spec.replace_policy == "Replace") {
+      cordon.push_back(d->uuid);
+      std::string why = join([&] {
+        std::vector<std::string> r;
+        for (const auto& x : d->verdict["reasons"].elements()) r.push_back(x.as_string());
+        if (!d->probe_passed) r.push_back("ProbeFailed");
+        return r;
+      }(), "; ");
+      event_(obj, "Warning", "HealthDegraded", short_id(*d) + " unhealthy (" + why + "): replacing");
+      progress_reason = "ReplacingUnhealthy";
+      progress_msg = "replacing " + short_id(*d);
+    } else {
+      keep.push_back(d);
+    }
+  }
+  int64_t n_active = static_cast<int64_t>(keep.size());
+  if (n_active > spec.replicas) {
+    // Deterministic victims (fixes README.md:214's arbitrary existingVMs[:n]): unhealthy first,
+    // then GPUs without pods, then the highest index.
+    std::vector<const DeviceView*> order = keep;
+    std::sort(order.begin(), order.end(), [](const DeviceView* a, const DeviceView* b) {
+      bool ua = !a->healthy || !a->probe_passed, ub = !b->healthy || !b->probe_passed;
+      if (ua != ub) return ua;
+      bool pa = a->pods.size() > 0, pb = b->pods.size() > 0;
+      if (pa != pb) return !pa;
+      return a->index > b->index;
+    });
+    int64_t drop = n_active - spec.replicas;
+    std::vector<std::string> victims;
+    for (int64_t i = 0; i < drop; ++i) victims.push_back(order[static_cast<size_t>(i)]->uuid);
+    cordon.insert(cordon.end(), victims.begin(), victims.end());
+    progress_reason = "ScalingDown";
+    progress_msg = "draining " + std::to_string(drop) + " GPU(s): " + join(victims, ",");
+    event_(obj, "Normal", "DrainStarted", progress_msg);
+    n_active = spec.replicas;
+  }
+  if (!cordon.empty()) {
+    provider_.cordon(o.node, m.uid, cordon);
+    acted = true;
+  }
+  if (n_active < spec.replicas) {
+    int need = static_cast<int>(spec.replicas - n_active);
+    std::string node = o.mine.empty() ? choose_node_(spec, need, obj.path("status.nodeName").as_string()) : o.node;
+    if (node.empty()) {
+      insufficient = true;
+      progress_msg = "no eligible node with a gpupool agent";
+    } else {
+      ClaimRequest req;
+      req.pool_uid = m.uid;
+      req.pool = m.key();
+      req.count = need;
+      req.topology_policy = spec.topology_policy;
+      req.resource_name = spec.resource_name;
+      req.policy = spec.policy_json();
+      req.probe = Json::object();
+      req.probe["enabled"] = spec.probe_enabled;
+      req.probe["hbmBytes"] = spec.probe_hbm_bytes;
+      req.probe["mfma"] = spec.probe_mfma;
+      auto t = clock_t_::now();
+      ClaimResult cr = provider_.claim(node, req);
+      double claim_ms = std::chrono::duration<double, std::milli>(clock_t_::now() - t).count();
+      if (!cr.ok) {
+        insufficient = true;
+        progress_msg = cr.reason + ": " + cr.message;
+        event_(obj, "Warning", cr.reason.empty() ? "InsufficientDevices" : cr.reason, cr.message);
+      } else {
+        std::vector<std::string> ids;
+        for (const auto& d : cr.devices) ids.push_back(short_id(d));
+        if (progress_reason.empty()) progress_reason = "ScalingUp";
+        progress_msg = "claimed " + std::to_string(cr.devices.size()) + " GPU(s) on " + node;
+        event_(obj, "Normal", "GPUClaimed", progress_msg + ": " + join(ids, ", "));
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          policy_gen_[m.uid] = m.generation;
+        }
+        log.info("claimed", Json::object().set("node", node).set("count", need).set("claimMs", claim_ms));
+      }
+      acted = true;
+    }
+  }
+  if (acted) o = observe_(m, spec, obj["status"]);
+  int still = drain_(obj, o.node, m, spec, o.mine);
+  bool released = false;
+  for (const auto& d : o.mine)
+    if (d.state == "Draining" && d.pods.size() == 0) released = true;
+  if (released) o = observe_(m, spec, obj["status"]);  // A1: status from ground truth after acting
+  if (still > 0 && progress_reason.empty()) {
+    progress_reason = "Draining";
+    progress_msg = std::to_string(still) + " GPU(s) waiting for pods to terminate";
+  }
+  Json status = build_status_(obj, m, spec, o, progress_reason, progress_msg, insufficient, false);
+  write_status_(obj, status);
+  int64_t ready = status["readyReplicas"].as_int(0);
+  ready_gauge().set({{"kind", kind_}, {"pool", m.key()}}, static_cast<double>(ready));
+  bool is_ready = condition_true(status["conditions"], gen::kCondReady);
+  observe_ready_(m, is_ready, spec.replicas);
+  if (insufficient) return Outcome::requeue(ms(5000), "insufficient devices");
+  bool draining = false;
+  for (const auto& d : o.mine) draining = draining || d.state == "Draining" || d.state == "Probing";
+  if (draining || !is_ready) return Outcome::requeue(opts_.progress_poll, progress_reason);
+  return Outcome::done(opts_.resync);
+}
+
+void Mi355xPoolReconciler::sweep_orphans() {
+  std::set<std::string> live;
+  for (const auto& p : pools_.list()) live.insert(p.path("metadata.uid").as_string());
+  for (const auto& n : provider_.node_names()) {
+    NodeView nv = provider_.observe(n);
+    if (!nv.reachable) continue;
+    std::map<std::string, std::vector<std::string>> orphans;
+    for (const auto& d : nv.devices)
+      if (!d.pool_uid.empty() && !live.count(d.pool_uid) && d.pods.size() == 0) orphans[d.pool_uid].push_back(d.uuid);
+    for (const auto& kv : orphans) {
+      log_.warn("releasing orphaned claims", Json::object().set("node", n).set("poolUID", kv.first).set("count", static_cast<long long>(kv.second.size())));
+      try {
+        provider_.release(n, kv.first, kv.second);
+      } catch (const std::exception& e) {
+        log_.warn("orphan release failed", Json::object().set("error", e.what()));
+      }
+    }
+  }
+}
+
+// ================================================================== AzureVmPool
+AzureVmPoolReconciler::AzureVmPoolReconciler(KubeClient& client, Informer& pools, CloudProvider& cloud,
+                                             EventRecorder* events, ReconcilerOptions opts)
+    : PoolReconcilerBase(client, pools, events, opts, "AzureVmPool", res::azurevmpools()), cloud_(cloud) {}
+
+static std::string b64decode(const std::string& in) {
+  static const std::string tbl = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string out;
+  int val = 0, bits = -8;
+  for (unsigned char c : in) {
+    if (c == '=') break;
+    auto p = tbl.find(static_cast<char>(c));
+    if (p == std::string::npos) continue;
+    val = (val << 6) + static_cast<int>(p);
+    bits += 6;
+    if (bits >= 0) {
+      out.push_back(static_cast<char>((val >> bits) & 0xFF));
+      bits -= 8;
+    }
+  }
+  return out;
+}
+
+bool AzureVmPoolReconciler::credentials_(const ObjectMeta& m, const AzureVmPoolSpec& spec, Credentials* out,
+                                         std::string* why) {
+  // README.md:179-185: the client is built from the Secret named by spec.azureCredentialSecret.
+  Json secret;
+  try {
+    secret = client_.get(res::secrets(), m.ns, spec.credential_secret);
+  } catch (const KubeError& e) {
+    if (e.not_found()) {
+      *why = "Secret " + m.ns + "/" + spec.credential_secret + " not found";
+      return false;
+    }
+    throw;
+  }
+  std::vector<std::string> missing;
+  for (const char* k : gen::kAzureCredentialKeys) {
+    std::string v = b64decode(secret["data"][k].as_string());
+    if (v.empty()) missing.push_back(k);
+    else out->values[k] = v;
+  }
+  if (!missing.empty()) {
+    *why = "Secret " + m.ns + "/" + spec.credential_secret + " lacks keys: " + join(missing, ",");
+    return false;
+  }
+  return true;
+}
+
+Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::string& name) {
+  auto cached = pools_.get(ns, name);
+  if (!cached) return Outcome::done(ms(0));
+  Json obj = *cached;
+  ObjectMeta m = ObjectMeta::from(obj);
+  const std::string now = rfc3339_now();
+  Json conds = obj.path("status.conditions").is_array() ? obj.path("status.conditions") : Json::array();
+  Json st = Json::object();
+  st["observedGeneration"] = m.generation;
+  auto errs = validate_azure(obj);
+  if (!errs.empty()) {
+    set_condition(conds, gen::kCondReady, "False", "InvalidSpec", join(errs, "; "), m.generation, now);
+    st["conditions"] = conds;
+    write_status_(obj, st);
+    return Outcome::terminal("invalid spec");
+  }
+  AzureVmPoolSpec spec = AzureVmPoolSpec::from(obj["spec"]);
+  const std::string owner = m.ns + "-" + m.name;  // README.md:238 owner tag
+  Credentials creds;
+  std::string why;
+  bool have_creds = credentials_(m, spec, &creds, &why);
+  if (!have_creds) {
+    set_condition(conds, gen::kCondCredentialsValid, "False", "CredentialsMissing", why, m.generation, now);
+    set_condition(conds, gen::kCondReady, "False", "CredentialsMissing", why, m.generation, now);
+    set_condition(conds, gen::kCondDegraded, "True", "CredentialsMissing", why, m.generation, now);
+    set_condition(conds, gen::kCondDeleting, m.deleting() ? "True" : "False", m.deleting() ? "Finalizing" : "NotDeleting", "",
+                  m.generation, now);
+    st["readyReplicas"] = obj.path("status.readyReplicas").as_int(0);
+    st["replicas"] = obj.path("status.replicas").as_int(0);
+    if (obj.path("status.vms").is_array()) st["vms"] = obj.path("status.vms");
+    st["conditions"] = conds;
+    write_status_(obj, st);
+    event_(obj, "Warning", "CredentialsMissing", why);
+    // README.md:184 intended a 30 s requeue; typed outcome makes that delay real.
+    return Outcome::requeue(opts_.credentials_retry, why);
+  }
+  set_condition(conds, gen::kCondCredentialsValid, "True", "SecretResolved",
+                "Secret " + m.ns + "/" + spec.credential_secret + " has all four keys", m.generation, now);
+
+  std::vector<VmRecord> vms;
+  try {
+    vms = cloud_.list(creds, spec.resource_group, owner);
+  } catch (const ProviderError& e) {
+    set_condition(conds, gen::kCondDegraded, "True", e.code, e.what(), m.generation, now);
+    st["conditions"] = conds;
+    write_status_(obj, st);
+    return e.transient ? Outcome::transient(e.what()) : Outcome::terminal(e.what());
+  }
+
+  if (m.deleting()) {
+    for (const auto& vm : vms)
+      if (vm.state != "Deleting") cloud_.destroy(creds, spec.resource_group, vm.name);
+    vms = cloud_.list(creds, spec.resource_group, owner);
+    auto orphans = cloud_.orphans(spec.resource_group, owner);
+    if (!vms.empty() || !orphans.empty()) {
+      set_condition(conds, gen::kCondDeleting, "True", "DeletingVMs",
+                    std::to_string(vms.size()) + " VM(s) still deleting", m.generation, now);
+      set_condition(conds, gen::kCondReady, "False", "Deleting", "pool is being deleted", m.generation, now);
+      st["conditions"] = conds;
+      st["replicas"] = static_cast<long long>(vms.size());
+      st["readyReplicas"] = 0;
+      write_status_(obj, st);
+      return Outcome::requeue(opts_.progress_poll, "deleting VMs");
+    }
+    if (m.has_finalizer(gen::kFinalizer)) remove_finalizer_(obj);
+    event_(obj, "Normal", "Finalized", "all VMs, NICs and OS disks deleted; finalizer removed");
+    forget_(m.uid);
+    return Outcome::done(ms(0));
+  }
+  if (!m.has_finalizer(gen::kFinalizer)) {
+    obj = ensure_finalizer_(obj);
+    m = ObjectMeta::from(obj);
+  }
+
+  std::vector<VmRecord> live;
+  for (const auto& vm : vms)
+    if (vm.state != "Deleting") live.push_back(vm);
+  std::string progress_reason, progress_msg, error_reason, error_msg;
+  int64_t desired = spec.replicas;
+  auto cur = static_cast<int64_t>(live.size());
+  try {
+    // replace failed VMs
+    for (const auto& vm : live) {
+      if (vm.state == "Failed") {
+        cloud_.destroy(creds, spec.resource_group, vm.name);
+        event_(obj, "Warning", "VMFailed", "VM " + vm.name + " failed provisioning: deleting");
+        --cur;
+      }
+    }
+    if (cur < desired) {
+      progress_reason = "ScalingUp";
+      for (int64_t i = cur; i < desired; ++i) {
+        char suffix[16];
+        uint64_t seq = name_seq_++;
+        std::snprintf(suffix, sizeof suffix, "%05llx",
+                      static_cast<unsigned long long>((std::random_device{}() ^ (seq * 2654435761ULL)) & 0xFFFFF));
+        std::string vname = m.name + "-" + suffix;  // README.md:204-205 unique name
+        cloud_.create(creds, spec, owner, vname);
+        event_(obj, "Normal", "VMCreating", "creating VM " + vname + " (" + spec.vm_size + ")");
+      }
+      progress_msg = "creating " + std::to_string(desired - cur) + " VM(s)";
+    } else if (cur > desired) {
+      std::vector<VmRecord> order;
+      for (const auto& vm : live)
+        if (vm.state != "Failed") order.push_back(vm);
+      std::sort(order.begin(), order.end(), [](const VmRecord& a, const VmRecord& b) {
+        bool ca = a.state == "Creating", cb = b.state == "Creating";
+        if (ca != cb) return ca;
+        if (a.created_at != b.created_at) return a.created_at > b.created_at;
+        return a.name > b.name;
+      });
+      int64_t drop = cur - desired;
+      for (int64_t i = 0; i < drop && i < static_cast<int64_t>(order.size()); ++i) {
+        cloud_.destroy(creds, spec.resource_group, order[static_cast<size_t>(i)].name);
+        event_(obj, "Normal", "VMDeleting", "deleting VM " + order[static_cast<size_t>(i)].name + " with its NIC and OS disk");
+      }
+      progress_reason = "ScalingDown";
+      progress_msg = "deleting " + std::to_string(drop) + " VM(s)";
+    }
+  } catch (const ProviderError& e) {
+    error_reason = e.code;
+    error_msg = e.what();
+    event_(obj, "Warning", e.code, e.what());
+  }
+  // Re-observe after acting (fixes README.md:225 which reported the pre-action count).
+  vms = cloud_.list(creds, spec.resource_group, owner);
+  int64_t ready = 0, total = 0;
+  bool inflight = false;
+  Json names = Json::array();
+  std::vector<std::string> sorted;
+  for (const auto& vm : vms) {
+    if (vm.state == "Deleting") {
+      inflight = true;
+      continue;
+    }
+    ++total;
+    if (vm.state == "Succeeded") ++ready;
+    else inflight = true;
+    sorted.push_back(vm.name);
+  }
+  std::sort(sorted.begin(), sorted.end());
+  for (const auto& n : sorted) names.push_back(n);
+  st["replicas"] = total;
+  st["readyReplicas"] = ready;
+  st["vms"] = names;
+  bool is_ready = ready == desired && total == desired;
+  if (!error_reason.empty()) {
+    set_condition(conds, gen::kCondDegraded, "True", error_reason, error_msg, m.generation, now);
+  } else {
+    set_condition(conds, gen::kCondDegraded, "False", "AsExpected", "", m.generation, now);
+  }
+  if (inflight || !progress_reason.empty()) {
+    set_condition(conds, gen::kCondProgressing, "True", progress_reason.empty() ? "Provisioning" : progress_reason,
+                  progress_msg.empty() ? "cloud operations in flight" : progress_msg, m.generation, now);
+  } else {
+    set_condition(conds, gen::kCondProgressing, "False", "Stable",
+                  std::to_string(ready) + "/" + std::to_string(desired) + " VMs ready", m.generation, now);
+  }
+  set_condition(conds, gen::kCondDeleting, "False", "NotDeleting", "", m.generation, now);
+  set_condition(conds, gen::kCondReady, is_ready ? "True" : "False",
+                is_ready ? "AllReplicasReady" : (!error_reason.empty() ? error_reason : "Provisioning"),
+                std::to_string(ready) + "/" + std::to_string(desired) + " VMs ready", m.generation, now);
+  st["conditions"] = conds;
+  write_status_(obj, st);
+  ready_gauge().set({{"kind", kind_}, {"pool", m.key()}}, static_cast<double>(ready));
+  observe_ready_(m, is_ready, desired);
+  if (!error_reason.empty()) return Outcome::transient(error_msg);
+  if (inflight || !is_ready) return Outcome::requeue(opts_.progress_poll, "cloud operations in flight");
+  return Outcome::done(opts_.resync);
+}
+
+// ================================================================== Controller
+Controller::Controller(int workers) : workers_(workers) {}
+
+Controller::~Controller() { stop(); }
+
+void Controller::add_reconciler(PoolReconcilerBase* r) { by_kind_[r->kind()] = r; }
+
+void Controller::enqueue(const std::string& kind, const std::string& ns, const std::string& name) {
+  q_.add(kind + "/" + ns + "/" + name);
+}
+
+void Controller::enqueue_after(const std::string& kind, const std::string& ns, const std::string& name, ms d) {
+  q_.add_after(kind + "/" + ns + "/" + name, d);
+}
+
+void Controller::start() {
+  for (int i = 0; i < workers_; ++i) threads_.emplace_back([this] { worker_(); });
+}
+
+void Controller::stop() {
+  q_.shutdown();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+}
+
+void Controller::worker_() {
+  std::string key;
+  while (q_.get(&key)) {
+    auto s1 = key.find('/');
+    auto s2 = key.find('/', s1 + 1);
+    std::string kind = key.substr(0, s1), ns = key.substr(s1 + 1, s2 - s1 - 1), name = key.substr(s2 + 1);
+    auto it = by_kind_.find(kind);
+    if (it == by_kind_.end()) {
+      q_.forget(key);
+      q_.done(key);
+      continue;
+    }
+    auto t0 = clock_t_::now();
+    Outcome out;
+    try {
+      out = it->second->reconcile(ns, name);
+    } catch (const std::exception& e) {
+      out = Outcome::transient(e.what());
+    }
+    double secs = std::chrono::duration<double>(clock_t_::now() - t0).count();
+    reconciles_++;
+    static const char* names[] = {"done", "requeue", "error", "terminal"};
+    reconcile_total().inc({{"kind", kind}, {"result", names[out.kind]}});
+    reconcile_hist().observe({{"kind", kind}}, secs);
+    switch (out.kind) {
+      case Outcome::Done:
+        q_.forget(key);
+        if (out.after.count() > 0) q_.add_after(key, out.after);
+        break;
+      case Outcome::RequeueAfter:
+        q_.forget(key);
+        q_.add_after(key, out.after);
+        break;
+      case Outcome::Transient:
+        log_.warn("reconcile failed; backing off",
+                  Json::object().set("key", key).set("error", out.message).set("requeues", q_.num_requeues(key)));
+        q_.add_rate_limited(key);
+        break;
+      case Outcome::Terminal:
+        log_.warn("reconcile terminal; waiting for a spec change", Json::object().set("key", key).set("reason", out.message));
+        q_.forget(key);
+        break;
+    }
+    q_.done(key);
+  }
+}
+
+}  // namespace gpupool

@@ -1,0 +1,625 @@
+// mi355x-probe: per-device readiness check for gfx950 (MI355X), the MI355X-native replacement for
+// the reference's GPU smoke test (`kubectl run ... nvidia-smi`, GPU调度平台搭建.md:134-138).
+//
+// A device passes only if
+//   1. HBM: two complementary pseudo-random patterns written over `hbmBytes` of HBM3E and read
+//      back bit-exactly (stuck-at / coupling faults in both polarities), with the achieved
+//      write+read bandwidth reported;
+//   2. MFMA: a bf16 GEMM on the matrix cores (`v_mfma_f32_32x32x16_bf16`) is bit-exact against
+//      (a) a full VALU fp32 reference on a 256^3 problem with an asymmetric B (catches fragment
+//      layout / row<->col faults) and (b) exact int64 ABFT row+column checksums on an N^3 problem
+//      whose operands are small integers (all partial sums exact in fp32), with TFLOP/s reported.
+//
+// Design for CDNA4: 64-wide waves; 16-byte vector loads/stores everywhere (Guideline 13);
+// HBM kernels grid-stride with ~8 workgroups per CU and 4 independent 16-B accesses in flight per
+// lane; the GEMM uses a 128x128x32 LDS tile, 4 waves (2x2) each owning 64x64 = 2x2 MFMA 32x32
+// tiles, register-staged double buffering and an XCD-aware bijective workgroup remap (T1) so
+// neighbouring tiles share an XCD's L2.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "mi355x/probe.h"
+
+#define PROBE_CHECK(expr)                                                                 \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      throw ProbeError(std::string(#expr) + " -> " + hipGetErrorString(e_));             \
+    }                                                                                     \
+  } while (0)
+
+namespace {
+
+struct ProbeError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+using bf16x8 = __attribute__((ext_vector_type(8))) short;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;  // native vector: 16-B global ops
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+// ------------------------------------------------------------------ HBM pattern test
+__device__ __forceinline__ uint32_t pattern_word(uint64_t idx, uint32_t seed) {
+  // Cheap invertible mix of the word index: distinct per address, dense in both bit values.
+  uint32_t x = static_cast<uint32_t>(idx) * 0x9E3779B1u ^ static_cast<uint32_t>(idx >> 32) * 0x85EBCA77u;
+  x ^= seed;
+  x ^= x >> 15;
+  x *= 0x2C1B3C6Du;
+  x ^= x >> 12;
+  return x;
+}
+
+__device__ __forceinline__ u32x4 pattern16(uint64_t i16, uint32_t seed, uint32_t flip) {
+  uint64_t w = i16 * 4;
+  u32x4 v;
+  v.x = pattern_word(w, seed) ^ flip;
+  v.y = pattern_word(w + 1, seed) ^ flip;
+  v.z = pattern_word(w + 2, seed) ^ flip;
+  v.w = pattern_word(w + 3, seed) ^ flip;
+  return v;
+}
+
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+constexpr int kHbmThreads = 256;
+constexpr int kHbmUnroll = 4;
+
+__global__ __launch_bounds__(kHbmThreads) void hbm_fill(u32x4* __restrict__ p, uint64_t n16,
+                                                        uint32_t seed, uint32_t flip) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kHbmThreads;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * kHbmThreads + threadIdx.x;
+  for (; i + (kHbmUnroll - 1) * stride < n16; i += kHbmUnroll * stride) {
+#pragma unroll
+    for (int u = 0; u < kHbmUnroll; ++u) {
+      uint64_t j = i + u * stride;
+      __builtin_nontemporal_store(pattern16(j, seed, flip), &p[j]);
+    }
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(pattern16(i, seed, flip), &p[i]);
+}
+
+__device__ __forceinline__ uint32_t mismatches16(u32x4 v, u32x4 e) {
+  return __builtin_popcount(v.x ^ e.x) + __builtin_popcount(v.y ^ e.y) +
+         __builtin_popcount(v.z ^ e.z) + __builtin_popcount(v.w ^ e.w);
+}
+
+// Counts flipped BITS; records the lowest faulting 16-byte index. One atomic per wave.
+__global__ __launch_bounds__(kHbmThreads) void hbm_verify(const u32x4* __restrict__ p, uint64_t n16,
+                                                          uint32_t seed, uint32_t flip,
+                                                          unsigned long long* __restrict__ bad_bits,
+                                                          unsigned long long* __restrict__ first_bad) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kHbmThreads;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * kHbmThreads + threadIdx.x;
+  uint32_t bad = 0;
+  uint64_t first = ~0ull;
+  for (; i + (kHbmUnroll - 1) * stride < n16; i += kHbmUnroll * stride) {
+    u32x4 v[kHbmUnroll];
+#pragma unroll
+    for (int u = 0; u < kHbmUnroll; ++u) v[u] = __builtin_nontemporal_load(&p[i + u * stride]);
+#pragma unroll
+    for (int u = 0; u < kHbmUnroll; ++u) {
+      uint32_t m = mismatches16(v[u], pattern16(i + u * stride, seed, flip));
+      if (m) {
+        bad += m;
+        first = umin64(first, i + u * stride);
+      }
+    }
+  }
+  for (; i < n16; i += stride) {
+    uint32_t m = mismatches16(__builtin_nontemporal_load(&p[i]), pattern16(i, seed, flip));
+    if (m) {
+      bad += m;
+      first = umin64(first, i);
+    }
+  }
+  // wave64 reduction
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    bad += __shfl_xor(bad, off, 64);
+    first = umin64(first, static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(first), off, 64)));
+  }
+  if ((threadIdx.x & 63) == 0 && bad) {
+    atomicAdd(bad_bits, static_cast<unsigned long long>(bad));
+    atomicMin(first_bad, static_cast<unsigned long long>(first));
+  }
+}
+
+// ------------------------------------------------------------------ operand generation
+__device__ __forceinline__ short small_int_bf16(uint32_t h, int span) {
+  // Integer in [-span, span] encoded as bf16 (exact).
+  float v = static_cast<float>(static_cast<int>(h % static_cast<uint32_t>(2 * span + 1)) - span);
+  return static_cast<short>(__float_as_uint(v) >> 16);
+}
+
+__global__ void gen_operand(short* __restrict__ out, uint64_t n, uint32_t seed, int span) {
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i < n; i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    out[i] = small_int_bf16(pattern_word(i, seed), span);
+}
+
+__device__ __forceinline__ float bf16_to_f32(short s) {
+  return __uint_as_float(static_cast<uint32_t>(static_cast<uint16_t>(s)) << 16);
+}
+
+// ------------------------------------------------------------------ MFMA GEMM  C = A * Bt^T
+// A: [M][K] bf16 row-major, Bt: [N][K] bf16 row-major (the "NT" layout: both operands are read
+// along K, so every MFMA fragment is one contiguous 16-byte LDS read), C: [M][N] fp32.
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int LDS_STRIDE = BK + 8;  // +16 B pad per row: 80-B rows spread ds_read_b128 lane groups
+constexpr int kGemmThreads = 256;
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  // Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+  // consecutive logical tiles land on the same XCD (shared L2) under round-robin dispatch.
+  int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_mfma_nt(const short* __restrict__ A,
+                                                                      const short* __restrict__ Bt,
+                                                                      float* __restrict__ C, int M,
+                                                                      int N, int K) {
+  __shared__ __attribute__((aligned(16))) short smem[2 * (BM + BN) * LDS_STRIDE];
+  short* As = smem;
+  short* Bs = smem + BM * LDS_STRIDE;
+
+  const int tiles_n = N / BN;
+  const int nwg = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int tile_m = wg / tiles_n, tile_n = wg % tiles_n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;  // 2x2 waves, each 64x64
+
+  // global->register staging: 128 rows x 32 bf16 = 512 x 16 B per operand, 2 per thread
+  const int ld_row = tid >> 2, ld_col = (tid & 3) * 8;
+  const short* a_src = A + static_cast<int64_t>(tile_m * BM + ld_row) * K + ld_col;
+  const short* b_src = Bt + static_cast<int64_t>(tile_n * BN + ld_row) * K + ld_col;
+  const int64_t row64 = static_cast<int64_t>(64) * K;
+
+  bf16x8 ra0, ra1, rb0, rb1;
+  auto gload = [&](int k0) {
+    ra0 = *reinterpret_cast<const bf16x8*>(a_src + k0);
+    ra1 = *reinterpret_cast<const bf16x8*>(a_src + row64 + k0);
+    rb0 = *reinterpret_cast<const bf16x8*>(b_src + k0);
+    rb1 = *reinterpret_cast<const bf16x8*>(b_src + row64 + k0);
+  };
+  auto swrite = [&](int buf) {
+    short* as = As + buf * (BM + BN) * LDS_STRIDE;
+    short* bs = as + BM * LDS_STRIDE;
+    *reinterpret_cast<bf16x8*>(as + ld_row * LDS_STRIDE + ld_col) = ra0;
+    *reinterpret_cast<bf16x8*>(as + (ld_row + 64) * LDS_STRIDE + ld_col) = ra1;
+    *reinterpret_cast<bf16x8*>(bs + ld_row * LDS_STRIDE + ld_col) = rb0;
+    *reinterpret_cast<bf16x8*>(bs + (ld_row + 64) * LDS_STRIDE + ld_col) = rb1;
+  };
+  (void)Bs;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;  // fragment row/col and k-half
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int ksteps = K / BK;
+  for (int kt = 0; kt < ksteps; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ksteps) gload((kt + 1) * BK);  // next tile in flight under this tile's MFMAs
+    const short* as = As + buf * (BM + BN) * LDS_STRIDE;
+    const short* bs = as + BM * LDS_STRIDE;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(as + (wr * 64 + i * 32 + fr) * LDS_STRIDE + ks * 16 + fh * 8);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + (wc * 64 + j * 32 + fr) * LDS_STRIDE + ks * 16 + fh * 8);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < ksteps) swrite(buf ^ 1);  // other buffer: last read one iteration ago
+    __syncthreads();
+  }
+  // C/D layout of 32x32x16: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = tile_n * BN + wc * 64 + j * 32 + fr;
+      const int row0 = tile_m * BM + wr * 64 + i * 32 + 4 * fh;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = row0 + (r & 3) + 8 * (r >> 2);
+        C[static_cast<int64_t>(row) * N + col] = acc[i][j][r];
+      }
+    }
+}
+
+// Full VALU reference (independent of the matrix cores), fp32, k-ordered.
+__global__ void gemm_ref_valu(const short* __restrict__ A, const short* __restrict__ Bt,
+                              float* __restrict__ C, int M, int N, int K) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  int m = blockIdx.y;
+  if (n >= N || m >= M) return;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s = fmaf(bf16_to_f32(A[static_cast<int64_t>(m) * K + k]),
+                                       bf16_to_f32(Bt[static_cast<int64_t>(n) * K + k]), s);
+  C[static_cast<int64_t>(m) * N + n] = s;
+}
+
+__global__ void count_diff(const float* __restrict__ x, const float* __restrict__ y, uint64_t n,
+                           unsigned long long* __restrict__ bad) {
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint32_t b = 0;
+  for (; i < n; i += static_cast<uint64_t>(gridDim.x) * blockDim.x) b += x[i] != y[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) b += __shfl_xor(b, off, 64);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(bad, static_cast<unsigned long long>(b));
+}
+
+// ABFT (algorithm-based fault tolerance) checks, exact in int64 because every operand is a small
+// integer: with C = A * Bt^T,
+//   column checksum  sum_m C[m][n] == sum_k (sum_m A[m][k]) * Bt[n][k]
+//   row checksum     sum_n C[m][n] == sum_k A[m][k] * (sum_n Bt[n][k])
+// Two memory-bound primitives, both coalesced: column sums split over row-chunks (one int64 atomic
+// per column per chunk), and one-wave-per-row dot products with 16-byte loads.
+__device__ __forceinline__ long long to_i64(short v) { return static_cast<long long>(bf16_to_f32(v)); }
+__device__ __forceinline__ long long to_i64(float v) { return static_cast<long long>(v); }
+
+constexpr int kColChunk = 64;  // rows per block in colsum_partial
+
+template <class T>
+__global__ __launch_bounds__(256) void colsum_partial(const T* __restrict__ X, int rows, int cols,
+                                                      unsigned long long* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int r0 = blockIdx.y * kColChunk;
+  const int r1 = min(rows, r0 + kColChunk);
+  long long s = 0;
+  for (int r = r0; r < r1; ++r) s += to_i64(X[static_cast<int64_t>(r) * cols + c]);
+  atomicAdd(&out[c], static_cast<unsigned long long>(s));  // two's complement: signed sums wrap exactly
+}
+
+// out[r] = sum_k X[r][k] * (w ? w[k] : 1); one wave64 per row, 4 rows per 256-thread block.
+template <class T>
+__global__ __launch_bounds__(256) void rowdot(const T* __restrict__ X, int rows, int K,
+                                              const unsigned long long* __restrict__ w,
+                                              unsigned long long* __restrict__ out) {
+  constexpr int V = 16 / sizeof(T);  // elements per 16-byte load
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const T* x = X + static_cast<int64_t>(row) * K;
+  long long s = 0;
+  for (int k0 = lane * V; k0 < K; k0 += 64 * V) {
+    using vec = __attribute__((ext_vector_type(V))) T;
+    vec v = *reinterpret_cast<const vec*>(x + k0);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      long long xv = to_i64(static_cast<T>(v[j]));
+      s += w ? xv * static_cast<long long>(w[k0 + j]) : xv;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[row] = static_cast<unsigned long long>(s);
+}
+
+__global__ void count_ne_u64(const unsigned long long* __restrict__ a, const unsigned long long* __restrict__ b,
+                             int n, unsigned long long* __restrict__ bad) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t d = (i < n && a[i] != b[i]) ? 1u : 0u;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+  if ((threadIdx.x & 63) == 0 && d) atomicAdd(bad, static_cast<unsigned long long>(d));
+}
+
+// ------------------------------------------------------------------ host side
+struct DeviceCtx {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {};
+  hipDeviceProp_t prop{};
+  bool ready = false;
+};
+
+std::mutex g_mu;
+std::vector<DeviceCtx> g_ctx;
+int g_count = -1;
+
+std::string jnum(double v) {
+  char b[64];
+  std::snprintf(b, sizeof b, "%.6g", v);
+  return b;
+}
+
+std::string jstr(const std::string& s) {
+  std::string o = "\"";
+  for (char c : s) {
+    if (c == '"' || c == '\\') o.push_back('\\');
+    if (static_cast<unsigned char>(c) < 0x20) continue;
+    o.push_back(c);
+  }
+  return o + "\"";
+}
+
+long long opt_int(const char* json, const char* key, long long def) {
+  if (!json) return def;
+  std::string pat = std::string("\"") + key + "\"";
+  const char* p = std::strstr(json, pat.c_str());
+  if (!p) return def;
+  p = std::strchr(p + pat.size(), ':');
+  if (!p) return def;
+  ++p;
+  while (*p == ' ') ++p;
+  if (std::strncmp(p, "true", 4) == 0) return 1;
+  if (std::strncmp(p, "false", 5) == 0) return 0;
+  return std::strtoll(p, nullptr, 10);
+}
+
+char* dup(const std::string& s) {
+  char* p = static_cast<char*>(std::malloc(s.size() + 1));
+  std::memcpy(p, s.c_str(), s.size() + 1);
+  return p;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+std::string hip_uuid(int dev) {
+  hipUUID u{};
+  if (hipDeviceGetUuid(&u, dev) != hipSuccess) return "";
+  std::string s(u.bytes, u.bytes + 16);
+  // ROCm reports the ASIC serial as ASCII hex: "GPU-<serial>" is the ROCR_VISIBLE_DEVICES form.
+  bool ascii = true;
+  for (char c : s) ascii = ascii && ((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'));
+  if (ascii) return "GPU-" + s;
+  char buf[40];
+  std::string hex;
+  for (int i = 0; i < 16; ++i) {
+    std::snprintf(buf, sizeof buf, "%02x", static_cast<unsigned char>(u.bytes[i]));
+    hex += buf;
+  }
+  return "GPU-" + hex;
+}
+
+std::string run_probe(int dev, const char* opts) {
+  const uint64_t hbm_bytes = static_cast<uint64_t>(opt_int(opts, "hbmBytes", 1LL << 30));
+  const bool do_mfma = opt_int(opts, "mfma", 1) != 0;
+  int gemm_n = static_cast<int>(opt_int(opts, "gemmN", 4096));
+  gemm_n = std::max(256, (gemm_n / 256) * 256);
+  const int patterns = static_cast<int>(std::max(1LL, opt_int(opts, "patterns", 2)));
+  auto t0 = std::chrono::steady_clock::now();
+  PROBE_CHECK(hipSetDevice(dev));
+  DeviceCtx& ctx = g_ctx[static_cast<size_t>(dev)];
+  if (!ctx.ready) {
+    PROBE_CHECK(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
+    for (auto& e : ctx.ev) PROBE_CHECK(hipEventCreate(&e));
+    PROBE_CHECK(hipGetDeviceProperties(&ctx.prop, dev));
+    ctx.ready = true;
+  }
+  hipStream_t s = ctx.stream;
+  const hipDeviceProp_t& prop = ctx.prop;
+  const int cus = prop.multiProcessorCount;
+  auto ms_since = [](std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+  };
+  const double setup_ms = ms_since(t0);
+  auto t_hbm = std::chrono::steady_clock::now();
+
+  // ---------------- HBM
+  const uint64_t n16 = hbm_bytes / 16;
+  DevBuf buf, counters;
+  PROBE_CHECK(hipMalloc(&buf.p, n16 * 16));
+  PROBE_CHECK(hipMalloc(&counters.p, 4 * sizeof(unsigned long long)));
+  auto* cnt = static_cast<unsigned long long*>(counters.p);
+  const int hbm_grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(cus) * 8,
+                                                          (n16 + kHbmThreads - 1) / kHbmThreads));
+  unsigned long long bad_bits = 0, first_bad = ~0ull;
+  float write_ms = 0, read_ms = 0;
+  for (int pi = 0; pi < patterns; ++pi) {
+    unsigned long long init[2] = {0, ~0ull};
+    PROBE_CHECK(hipMemcpyAsync(cnt, init, sizeof init, hipMemcpyHostToDevice, s));
+    const uint32_t seed = 0xA5A50000u + static_cast<uint32_t>(dev);
+    const uint32_t flip = (pi & 1) ? 0xFFFFFFFFu : 0u;  // complementary polarity on odd passes
+    PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
+    hipLaunchKernelGGL(hbm_fill, dim3(hbm_grid), dim3(kHbmThreads), 0, s, static_cast<u32x4*>(buf.p), n16, seed, flip);
+    PROBE_CHECK(hipGetLastError());
+    PROBE_CHECK(hipEventRecord(ctx.ev[1], s));
+    hipLaunchKernelGGL(hbm_verify, dim3(hbm_grid), dim3(kHbmThreads), 0, s, static_cast<const u32x4*>(buf.p), n16,
+                       seed, flip, cnt, cnt + 1);
+    PROBE_CHECK(hipGetLastError());
+    PROBE_CHECK(hipEventRecord(ctx.ev[2], s));
+    unsigned long long res[2];
+    PROBE_CHECK(hipMemcpyAsync(res, cnt, sizeof res, hipMemcpyDeviceToHost, s));
+    PROBE_CHECK(hipStreamSynchronize(s));
+    float w, r;
+    PROBE_CHECK(hipEventElapsedTime(&w, ctx.ev[0], ctx.ev[1]));
+    PROBE_CHECK(hipEventElapsedTime(&r, ctx.ev[1], ctx.ev[2]));
+    write_ms += w;
+    read_ms += r;
+    bad_bits += res[0];
+    if (res[1] < first_bad) first_bad = res[1];
+  }
+  const double bytes_moved = static_cast<double>(n16) * 16.0 * patterns;
+  const double write_gbps = bytes_moved / (write_ms * 1e-3) / 1e9;
+  const double read_gbps = bytes_moved / (read_ms * 1e-3) / 1e9;
+  const double hbm_gbps = 2.0 * bytes_moved / ((write_ms + read_ms) * 1e-3) / 1e9;
+  (void)hipFree(buf.p);  // release the pattern buffer before the GEMM operands are allocated
+  buf.p = nullptr;
+  const bool hbm_ok = bad_bits == 0;
+  const double hbm_wall_ms = ms_since(t_hbm);
+  auto t_mfma = std::chrono::steady_clock::now();
+
+  // ---------------- MFMA
+  bool mfma_ok = true;
+  unsigned long long small_bad = 0, abft_bad = 0;
+  double tflops = 0, gemm_ms = 0;
+  if (do_mfma) {
+    // (a) 256^3 full-element check vs the VALU reference; asymmetric operands
+    const int n0 = 256;
+    DevBuf a0, b0, c0, r0;
+    PROBE_CHECK(hipMalloc(&a0.p, static_cast<size_t>(n0) * n0 * 2));
+    PROBE_CHECK(hipMalloc(&b0.p, static_cast<size_t>(n0) * n0 * 2));
+    PROBE_CHECK(hipMalloc(&c0.p, static_cast<size_t>(n0) * n0 * 4));
+    PROBE_CHECK(hipMalloc(&r0.p, static_cast<size_t>(n0) * n0 * 4));
+    hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, static_cast<short*>(a0.p), static_cast<uint64_t>(n0) * n0, 0x1234u, 3);
+    hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, static_cast<short*>(b0.p), static_cast<uint64_t>(n0) * n0, 0xBEEFu, 3);
+    hipLaunchKernelGGL(gemm_bf16_mfma_nt, dim3((n0 / BM) * (n0 / BN)), dim3(kGemmThreads), 0, s,
+                       static_cast<const short*>(a0.p), static_cast<const short*>(b0.p), static_cast<float*>(c0.p), n0, n0, n0);
+    hipLaunchKernelGGL(gemm_ref_valu, dim3(n0 / 256, n0), dim3(256), 0, s, static_cast<const short*>(a0.p),
+                       static_cast<const short*>(b0.p), static_cast<float*>(r0.p), n0, n0, n0);
+    PROBE_CHECK(hipMemsetAsync(cnt + 2, 0, 2 * sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(count_diff, dim3(64), dim3(256), 0, s, static_cast<const float*>(c0.p),
+                       static_cast<const float*>(r0.p), static_cast<uint64_t>(n0) * n0, cnt + 2);
+    PROBE_CHECK(hipGetLastError());
+
+    // (b) N^3 timed GEMM + exact ABFT checksums
+    const int n = gemm_n;
+    DevBuf a, b, c, acol;
+    PROBE_CHECK(hipMalloc(&a.p, static_cast<size_t>(n) * n * 2));
+    PROBE_CHECK(hipMalloc(&b.p, static_cast<size_t>(n) * n * 2));
+    PROBE_CHECK(hipMalloc(&c.p, static_cast<size_t>(n) * n * 4));
+    PROBE_CHECK(hipMalloc(&acol.p, static_cast<size_t>(6) * n * 8));
+    hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, static_cast<short*>(a.p), static_cast<uint64_t>(n) * n, 0x51u, 2);
+    hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, static_cast<short*>(b.p), static_cast<uint64_t>(n) * n, 0x77u, 2);
+    const int grid = (n / BM) * (n / BN);
+    // warm-up launch, then one timed launch
+    hipLaunchKernelGGL(gemm_bf16_mfma_nt, dim3(grid), dim3(kGemmThreads), 0, s, static_cast<const short*>(a.p),
+                       static_cast<const short*>(b.p), static_cast<float*>(c.p), n, n, n);
+    PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
+    const int reps = static_cast<int>(std::max(1LL, opt_int(opts, "gemmReps", 3)));
+    for (int rep = 0; rep < reps; ++rep)
+      hipLaunchKernelGGL(gemm_bf16_mfma_nt, dim3(grid), dim3(kGemmThreads), 0, s, static_cast<const short*>(a.p),
+                         static_cast<const short*>(b.p), static_cast<float*>(c.p), n, n, n);
+    PROBE_CHECK(hipEventRecord(ctx.ev[1], s));
+    PROBE_CHECK(hipGetLastError());
+    // ABFT checksums: 6 int64 vectors [acol | bcol | colsumC | expCol | rowsumC | expRow]
+    auto* v = static_cast<unsigned long long*>(acol.p);
+    unsigned long long *vacol = v, *vbcol = v + n, *vcolC = v + 2 * n, *vexpC = v + 3 * n, *vrowC = v + 4 * n,
+                       *vexpR = v + 5 * n;
+    PROBE_CHECK(hipMemsetAsync(v, 0, static_cast<size_t>(3) * n * 8, s));
+    const dim3 cgrid((n + 255) / 256, (n + kColChunk - 1) / kColChunk);
+    hipLaunchKernelGGL(colsum_partial<short>, cgrid, dim3(256), 0, s, static_cast<const short*>(a.p), n, n, vacol);
+    hipLaunchKernelGGL(colsum_partial<short>, cgrid, dim3(256), 0, s, static_cast<const short*>(b.p), n, n, vbcol);
+    hipLaunchKernelGGL(colsum_partial<float>, cgrid, dim3(256), 0, s, static_cast<const float*>(c.p), n, n, vcolC);
+    const dim3 rgrid((n + 3) / 4);
+    hipLaunchKernelGGL(rowdot<short>, rgrid, dim3(256), 0, s, static_cast<const short*>(b.p), n, n, vacol, vexpC);
+    hipLaunchKernelGGL(rowdot<float>, rgrid, dim3(256), 0, s, static_cast<const float*>(c.p), n, n,
+                       static_cast<const unsigned long long*>(nullptr), vrowC);
+    hipLaunchKernelGGL(rowdot<short>, rgrid, dim3(256), 0, s, static_cast<const short*>(a.p), n, n, vbcol, vexpR);
+    hipLaunchKernelGGL(count_ne_u64, dim3((n + 255) / 256), dim3(256), 0, s, vcolC, vexpC, n, cnt + 3);
+    hipLaunchKernelGGL(count_ne_u64, dim3((n + 255) / 256), dim3(256), 0, s, vrowC, vexpR, n, cnt + 3);
+    PROBE_CHECK(hipGetLastError());
+    unsigned long long res[2];
+    PROBE_CHECK(hipMemcpyAsync(res, cnt + 2, sizeof res, hipMemcpyDeviceToHost, s));
+    PROBE_CHECK(hipStreamSynchronize(s));
+    float ms;
+    PROBE_CHECK(hipEventElapsedTime(&ms, ctx.ev[0], ctx.ev[1]));
+    gemm_ms = ms / reps;
+    tflops = 2.0 * n * static_cast<double>(n) * n / (gemm_ms * 1e-3) / 1e12;
+    small_bad = res[0];
+    abft_bad = res[1];
+    mfma_ok = small_bad == 0 && abft_bad == 0;
+  }
+  double total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::string out = "{";
+  out += "\"device\":" + std::to_string(dev);
+  out += ",\"hipUUID\":" + jstr(hip_uuid(dev));
+  out += ",\"gcnArch\":" + jstr(prop.gcnArchName);
+  out += ",\"passed\":" + std::string(hbm_ok && mfma_ok ? "true" : "false");
+  out += ",\"hbm\":{\"ok\":" + std::string(hbm_ok ? "true" : "false") + ",\"bytes\":" + std::to_string(n16 * 16) +
+         ",\"patterns\":" + std::to_string(patterns) + ",\"badBits\":" + std::to_string(bad_bits) +
+         ",\"firstBadOffset\":" + (first_bad == ~0ull ? std::string("null") : std::to_string(first_bad * 16)) +
+         ",\"writeGBps\":" + jnum(write_gbps) + ",\"readGBps\":" + jnum(read_gbps) + ",\"GBps\":" + jnum(hbm_gbps) +
+         ",\"ms\":" + jnum(write_ms + read_ms) + "}";
+  out += ",\"mfma\":{\"ok\":" + std::string(mfma_ok ? "true" : "false") + ",\"enabled\":" + (do_mfma ? "true" : "false") +
+         ",\"n\":" + std::to_string(gemm_n) + ",\"elementMismatches\":" + std::to_string(small_bad) +
+         ",\"abftMismatches\":" + std::to_string(abft_bad) + ",\"tflops\":" + jnum(tflops) + ",\"ms\":" + jnum(gemm_ms) + "}";
+  out += ",\"ms\":" + jnum(total_ms);
+  out += ",\"phases\":{\"setupMs\":" + jnum(setup_ms) + ",\"hbmWallMs\":" + jnum(hbm_wall_ms) +
+         ",\"mfmaWallMs\":" + jnum(do_mfma ? ms_since(t_mfma) : 0.0) + "}";
+  out += "}";
+  return out;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mi355x_probe_init(char* err, size_t errlen) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_count >= 0) return g_count;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    if (err && errlen) std::snprintf(err, errlen, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    return -1;
+  }
+  g_ctx.resize(static_cast<size_t>(n));
+  // Warm every context now so a claim-time probe pays no runtime/context initialisation.
+  g_count = n;
+  for (int d = 0; d < n; ++d) {
+    if (hipSetDevice(d) != hipSuccess) continue;
+    (void)hipFree(nullptr);
+    try {
+      (void)run_probe(d, "{\"hbmBytes\":1048576,\"patterns\":1,\"gemmN\":256,\"gemmReps\":1}");
+    } catch (const std::exception&) {
+      // a broken device fails its real probe later with the actual error
+    }
+  }
+  return n;
+}
+
+int mi355x_probe_device_count(void) { return g_count; }
+
+char* mi355x_probe_identify(int dev) {
+  if (g_count < 0 || dev < 0 || dev >= g_count) return dup("{\"error\":\"bad device\"}");
+  hipDeviceProp_t prop{};
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return dup("{\"error\":\"hipGetDeviceProperties failed\"}");
+  char bdf[32];
+  std::snprintf(bdf, sizeof bdf, "%04x:%02x:%02x.0", prop.pciDomainID, prop.pciBusID, prop.pciDeviceID);
+  std::string out = "{\"device\":" + std::to_string(dev) + ",\"hipUUID\":" + jstr(hip_uuid(dev)) +
+                    ",\"name\":" + jstr(prop.name) + ",\"gcnArch\":" + jstr(prop.gcnArchName) +
+                    ",\"bdf\":" + jstr(bdf) + ",\"totalMem\":" + std::to_string(prop.totalGlobalMem) +
+                    ",\"computeUnits\":" + std::to_string(prop.multiProcessorCount) + "}";
+  return dup(out);
+}
+
+char* mi355x_probe_run(int dev, const char* opts_json) {
+  if (g_count < 0 || dev < 0 || dev >= g_count) return dup("{\"passed\":false,\"error\":\"bad device index\"}");
+  // Per-device serialisation: concurrent probes of DIFFERENT devices run in parallel.
+  static std::vector<std::mutex> dev_mu(64);
+  std::lock_guard<std::mutex> g(dev_mu[static_cast<size_t>(dev) % dev_mu.size()]);
+  try {
+    return dup(run_probe(dev, opts_json));
+  } catch (const std::exception& e) {
+    (void)hipGetLastError();
+    return dup(std::string("{\"device\":") + std::to_string(dev) + ",\"passed\":false,\"error\":" + jstr(e.what()) + "}");
+  }
+}
+
+void mi355x_probe_free(char* p) { std::free(p); }
+
+}  // extern "C"

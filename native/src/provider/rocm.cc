@@ -1,0 +1,191 @@
+// RocmProvider: the MI355X provider. Where the reference called the Azure Go SDK over HTTPS
+// (README.md:179-221), this talks to the node agent that owns the node's GPUs (claim ledger,
+// libmi355x_dev telemetry, HIP probe, device plugin) over HTTP/1.1 JSON — a unix socket on the
+// same host, or TCP across nodes. Agents are found through the Node object's
+// gpupool.amd.com/agent-endpoint annotation.
+#include "gpupool/generated/schema_consts.h"
+#include "gpupool/informer.h"
+#include "gpupool/provider.h"
+
+namespace gpupool {
+
+DeviceView DeviceView::from(const Json& j) {
+  DeviceView d;
+  d.uuid = j["uuid"].as_string();
+  d.hip_uuid = j["hipUUID"].as_string();
+  d.bdf = j["bdf"].as_string();
+  d.render_node = j["renderNode"].as_string();
+  d.node = j["node"].as_string();
+  d.index = j["index"].as_int(-1);
+  d.kfd_node = j["kfdNode"].as_int(-1);
+  d.state = j["state"].str_or("Free");
+  d.pool_uid = j["poolUID"].as_string();
+  d.pool = j["pool"].as_string();
+  d.healthy = j["healthy"].as_bool(false);
+  d.advertised = j["advertised"].as_bool(false);
+  d.probe_passed = j.path("probe.passed").as_bool(false);
+  d.verdict = j["verdict"];
+  d.probe = j["probe"];
+  d.pods = j["pods"].is_array() ? j["pods"] : Json::array();
+  d.claimed_at = j["claimedAt"].as_string();
+  d.drain_started_at = j["drainStartedAt"].as_string();
+  return d;
+}
+
+Json DeviceView::status_json() const {
+  Json s = Json::object();
+  s["uuid"] = uuid;
+  if (!hip_uuid.empty()) s["hipUUID"] = hip_uuid;
+  if (!bdf.empty()) s["bdf"] = bdf;
+  s["index"] = index;
+  s["node"] = node;
+  if (!render_node.empty()) s["renderNode"] = render_node;
+  if (kfd_node >= 0) s["kfdNode"] = kfd_node;
+  std::string h = state == "Draining" ? "Draining" : state == "Probing" ? "Probing" : healthy && probe_passed ? "Healthy" : "Unhealthy";
+  s["health"] = h;
+  Json reasons = Json::array();
+  for (const auto& r : verdict["reasons"].elements()) reasons.push_back(r);
+  if (probe.is_object() && !probe_passed && state != "Probing") {
+    std::string msg = probe["error"].str_or(probe["message"].str_or("probe failed"));
+    reasons.push_back("ProbeFailed: " + msg);
+  }
+  s["reasons"] = reasons;
+  s["advertised"] = advertised;
+  Json pods_out = Json::array();
+  for (const auto& p : pods.elements()) pods_out.push_back(p.is_string() ? p : Json(p["namespace"].as_string() + "/" + p["name"].as_string()));
+  s["pods"] = pods_out;
+  if (!claimed_at.empty()) s["claimedAt"] = claimed_at;
+  if (probe.is_object()) {
+    Json p = Json::object();
+    p["passed"] = probe_passed;
+    if (probe.path("hbm.GBps").is_number()) p["hbmGBps"] = probe.path("hbm.GBps");
+    if (probe.path("mfma.tflops").is_number()) p["mfmaTflops"] = probe.path("mfma.tflops");
+    if (probe["ms"].is_number()) p["ms"] = probe["ms"];
+    if (probe["backend"].is_string()) p["backend"] = probe["backend"];
+    if (probe["error"].is_string()) p["message"] = probe["error"];
+    s["probe"] = p;
+  }
+  return s;
+}
+
+RocmProvider::RocmProvider(Informer& nodes, int timeout_ms) : nodes_(nodes), timeout_ms_(timeout_ms) {}
+
+std::vector<std::string> RocmProvider::node_names() {
+  std::vector<std::string> out;
+  for (const auto& n : nodes_.list())
+    if (n.path("metadata.annotations")[gen::kAnnAgentEndpoint].is_string()) out.push_back(n.path("metadata.name").as_string());
+  return out;
+}
+
+Json RocmProvider::node_labels(const std::string& node) {
+  auto n = nodes_.get("", node);
+  if (!n) return Json::object();
+  return n->path("metadata.labels");
+}
+
+std::string RocmProvider::endpoint_of(const std::string& node) {
+  auto n = nodes_.get("", node);
+  if (!n) return "";
+  return n->path("metadata.annotations")[gen::kAnnAgentEndpoint].as_string();
+}
+
+HttpClient& RocmProvider::client_for(const std::string& node) {
+  std::string ep = endpoint_of(node);
+  if (ep.empty()) throw ProviderError("AgentNotFound", "no gpupool agent registered on node " + node);
+  std::lock_guard<std::mutex> g(mu_);
+  auto& slot = clients_[node];
+  if (!slot.second || slot.first != ep) {
+    slot.first = ep;
+    slot.second = std::make_unique<HttpClient>(Url::parse(ep), "", timeout_ms_);
+  }
+  return *slot.second;
+}
+
+Json RocmProvider::post_(const std::string& node, const std::string& path, const Json& body) {
+  HttpClient& c = client_for(node);
+  HttpResponse r;
+  try {
+    r = c.request("POST", path, body.dump());
+  } catch (const std::exception& e) {
+    throw ProviderError("AgentUnreachable", "agent on " + node + ": " + e.what());
+  }
+  auto j = Json::try_parse(r.body);
+  if (r.status >= 400) {
+    std::string msg = j ? (*j)["message"].str_or(r.body) : r.body;
+    std::string code = j ? (*j)["reason"].str_or("AgentError") : "AgentError";
+    throw ProviderError(code, "agent on " + node + " " + path + ": HTTP " + std::to_string(r.status) + ": " + msg,
+                        r.status >= 500);
+  }
+  return j ? *j : Json::object();
+}
+
+NodeView RocmProvider::observe(const std::string& node) {
+  NodeView nv;
+  nv.name = node;
+  nv.endpoint = endpoint_of(node);
+  try {
+    HttpClient& c = client_for(node);
+    HttpResponse r = c.request("GET", "/v1/node");
+    if (r.status >= 400) throw ProviderError("AgentError", "GET /v1/node: HTTP " + std::to_string(r.status));
+    Json j = Json::parse(r.body);
+    nv.reachable = true;
+    nv.backend = j["backend"].as_string();
+    nv.gen = j["gen"].as_int(0);
+    nv.advertise_required = j["advertiseRequired"].as_bool(true);
+    for (const auto& d : j["devices"].elements()) {
+      DeviceView v = DeviceView::from(d);
+      if (v.node.empty()) v.node = node;
+      nv.devices.push_back(std::move(v));
+    }
+  } catch (const std::exception& e) {
+    nv.reachable = false;
+    nv.error = e.what();
+  }
+  return nv;
+}
+
+ClaimResult RocmProvider::claim(const std::string& node, const ClaimRequest& req) {
+  Json body = Json::object();
+  body["poolUID"] = req.pool_uid;
+  body["pool"] = req.pool;
+  body["count"] = req.count;
+  body["topologyPolicy"] = req.topology_policy;
+  body["resourceName"] = req.resource_name;
+  body["policy"] = req.policy;
+  body["probe"] = req.probe;
+  Json r = post_(node, "/v1/claims", body);
+  ClaimResult out;
+  out.ok = r["ok"].as_bool(false);
+  out.reason = r["reason"].as_string();
+  out.message = r["message"].as_string();
+  for (const auto& d : r["devices"].elements()) out.devices.push_back(DeviceView::from(d));
+  return out;
+}
+
+static Json uuid_body(const std::string& pool_uid, const std::vector<std::string>& uuids) {
+  Json body = Json::object();
+  body["poolUID"] = pool_uid;
+  Json arr = Json::array();
+  for (const auto& u : uuids) arr.push_back(u);
+  body["uuids"] = arr;
+  return body;
+}
+
+void RocmProvider::cordon(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) {
+  post_(node, "/v1/cordon", uuid_body(pool_uid, uuids));
+}
+
+void RocmProvider::release(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) {
+  post_(node, "/v1/release", uuid_body(pool_uid, uuids));
+}
+
+void RocmProvider::update_policy(const std::string& node, const std::string& pool_uid, const Json& policy,
+                                 const std::string& resource_name) {
+  Json body = Json::object();
+  body["poolUID"] = pool_uid;
+  body["policy"] = policy;
+  body["resourceName"] = resource_name;
+  post_(node, "/v1/policy", body);
+}
+
+}  // namespace gpupool

@@ -1,0 +1,580 @@
+#include "gpupool/http.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <sstream>
+#include <stdexcept>
+
+namespace gpupool {
+
+// ------------------------------------------------------------------ Url
+Url Url::parse(const std::string& s) {
+  Url u;
+  auto p = s.find("://");
+  std::string rest;
+  if (p == std::string::npos) {
+    u.scheme = "http";
+    rest = s;
+  } else {
+    u.scheme = s.substr(0, p);
+    rest = s.substr(p + 3);
+  }
+  if (u.scheme == "unix") {
+    u.unix_path = rest.empty() || rest[0] == '/' ? rest : "/" + rest;
+    if (u.unix_path.empty()) throw std::invalid_argument("empty unix socket path");
+    return u;
+  }
+  if (u.scheme != "http") throw std::invalid_argument("unsupported scheme: " + u.scheme);
+  auto slash = rest.find('/');
+  if (slash != std::string::npos) rest = rest.substr(0, slash);
+  auto colon = rest.rfind(':');
+  if (colon != std::string::npos) {
+    u.host = rest.substr(0, colon);
+    u.port = std::stoi(rest.substr(colon + 1));
+  } else {
+    u.host = rest;
+    u.port = 80;
+  }
+  if (u.host.empty()) u.host = "127.0.0.1";
+  return u;
+}
+
+std::string Url::str() const {
+  if (scheme == "unix") return "unix://" + unix_path;
+  return scheme + "://" + host + ":" + std::to_string(port);
+}
+
+std::string url_encode(std::string_view s) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string out;
+  for (unsigned char c : s) {
+    if (isalnum(c) || c == '-' || c == '_' || c == '.' || c == '~') {
+      out.push_back(static_cast<char>(c));
+    } else {
+      out.push_back('%');
+      out.push_back(hex[c >> 4]);
+      out.push_back(hex[c & 15]);
+    }
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ chunked
+bool ChunkedDecoder::feed(std::string_view in, std::string& out) {
+  size_t i = 0;
+  while (i < in.size()) {
+    char c = in[i];
+    switch (state_) {
+      case State::Size: {
+        int v = -1;
+        if (c >= '0' && c <= '9') v = c - '0';
+        else if (c >= 'a' && c <= 'f') v = c - 'a' + 10;
+        else if (c >= 'A' && c <= 'F') v = c - 'A' + 10;
+        if (v >= 0) {
+          if (++size_digits_ > 15) return false;  // > 2^60: refuse
+          remaining_ = remaining_ * 16 + static_cast<uint64_t>(v);
+          ++i;
+        } else if (c == ';' || c == ' ' || c == '\t') {
+          if (size_digits_ == 0) return false;
+          state_ = State::SizeExt;
+          ++i;
+        } else if (c == '\r') {
+          if (size_digits_ == 0) return false;
+          state_ = State::SizeLF;
+          ++i;
+        } else {
+          return false;
+        }
+        break;
+      }
+      case State::SizeExt:
+        if (c == '\r') state_ = State::SizeLF;
+        ++i;
+        break;
+      case State::SizeLF:
+        if (c != '\n') return false;
+        ++i;
+        size_digits_ = 0;
+        if (remaining_ == 0) {
+          state_ = State::Trailer;
+          trailer_line_empty_ = true;
+        } else {
+          state_ = State::Data;
+        }
+        break;
+      case State::Data: {
+        size_t n = std::min<uint64_t>(remaining_, in.size() - i);
+        out.append(in.data() + i, n);
+        i += n;
+        remaining_ -= n;
+        if (remaining_ == 0) state_ = State::DataCR;
+        break;
+      }
+      case State::DataCR:
+        if (c != '\r') return false;
+        state_ = State::DataLF;
+        ++i;
+        break;
+      case State::DataLF:
+        if (c != '\n') return false;
+        state_ = State::Size;
+        ++i;
+        break;
+      case State::Trailer:
+        if (c == '\r') {
+          state_ = State::TrailerLF;
+        } else {
+          trailer_line_empty_ = false;
+        }
+        ++i;
+        break;
+      case State::TrailerLF:
+        if (c != '\n') return false;
+        ++i;
+        if (trailer_line_empty_) {
+          state_ = State::Done;
+        } else {
+          state_ = State::Trailer;
+          trailer_line_empty_ = true;
+        }
+        break;
+      case State::Done:
+        return true;  // ignore anything after the terminator
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ connection
+struct HttpClient::Conn {
+  int fd = -1;
+  std::string rbuf;
+  ~Conn() {
+    if (fd >= 0) ::close(fd);
+  }
+
+  // Wait for readability; returns 1 ready, 0 timeout, -1 error.
+  int wait_readable(int timeout_ms) const {
+    pollfd p{fd, POLLIN, 0};
+    int r;
+    do {
+      r = ::poll(&p, 1, timeout_ms);
+    } while (r < 0 && errno == EINTR);
+    if (r < 0) return -1;
+    return r == 0 ? 0 : 1;
+  }
+
+  // Read more bytes into rbuf. Returns bytes read, 0 on EOF, -1 on error, -2 on timeout.
+  ssize_t fill(int timeout_ms) {
+    int w = wait_readable(timeout_ms);
+    if (w == 0) return -2;
+    if (w < 0) return -1;
+    char buf[65536];
+    ssize_t n;
+    do {
+      n = ::recv(fd, buf, sizeof buf, 0);
+    } while (n < 0 && errno == EINTR);
+    if (n > 0) rbuf.append(buf, static_cast<size_t>(n));
+    return n;
+  }
+
+  bool send_all(const std::string& data) const {
+    size_t off = 0;
+    while (off < data.size()) {
+      ssize_t n = ::send(fd, data.data() + off, data.size() - off, MSG_NOSIGNAL);
+      if (n < 0) {
+        if (errno == EINTR) continue;
+        return false;
+      }
+      off += static_cast<size_t>(n);
+    }
+    return true;
+  }
+};
+
+HttpClient::HttpClient(Url url, std::string bearer_token, int timeout_ms)
+    : url_(std::move(url)), token_(std::move(bearer_token)), timeout_ms_(timeout_ms) {}
+
+HttpClient::~HttpClient() = default;
+
+std::unique_ptr<HttpClient::Conn> HttpClient::connect_(int timeout_ms) {
+  auto c = std::make_unique<Conn>();
+  if (url_.scheme == "unix") {
+    c->fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (c->fd < 0) throw HttpError("socket: " + std::string(strerror(errno)));
+    sockaddr_un sa{};
+    sa.sun_family = AF_UNIX;
+    if (url_.unix_path.size() >= sizeof sa.sun_path) throw HttpError("unix path too long");
+    std::memcpy(sa.sun_path, url_.unix_path.c_str(), url_.unix_path.size() + 1);
+    if (::connect(c->fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0)
+      throw HttpError("connect " + url_.str() + ": " + strerror(errno));
+    return c;
+  }
+  addrinfo hints{};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  addrinfo* res = nullptr;
+  std::string port = std::to_string(url_.port);
+  int rc = ::getaddrinfo(url_.host.c_str(), port.c_str(), &hints, &res);
+  if (rc != 0) throw HttpError("getaddrinfo " + url_.host + ": " + gai_strerror(rc));
+  std::string last_err = "no address";
+  for (addrinfo* ai = res; ai; ai = ai->ai_next) {
+    int fd = ::socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC, ai->ai_protocol);
+    if (fd < 0) continue;
+    // non-blocking connect with timeout
+    int flags = fcntl(fd, F_GETFL, 0);
+    fcntl(fd, F_SETFL, flags | O_NONBLOCK);
+    int r = ::connect(fd, ai->ai_addr, ai->ai_addrlen);
+    if (r != 0 && errno == EINPROGRESS) {
+      pollfd p{fd, POLLOUT, 0};
+      r = ::poll(&p, 1, timeout_ms);
+      int err = 0;
+      socklen_t len = sizeof err;
+      if (r == 1 && getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &len) == 0 && err == 0) {
+        r = 0;
+      } else {
+        last_err = r == 0 ? "connect timeout" : strerror(err ? err : errno);
+        r = -1;
+      }
+    } else if (r != 0) {
+      last_err = strerror(errno);
+    }
+    if (r == 0) {
+      fcntl(fd, F_SETFL, flags);
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      c->fd = fd;
+      break;
+    }
+    ::close(fd);
+  }
+  freeaddrinfo(res);
+  if (c->fd < 0) throw HttpError("connect " + url_.str() + ": " + last_err);
+  return c;
+}
+
+std::unique_ptr<HttpClient::Conn> HttpClient::take_() {
+  std::lock_guard<std::mutex> g(mu_);
+  if (idle_.empty()) return nullptr;
+  auto c = std::move(idle_.back());
+  idle_.pop_back();
+  return c;
+}
+
+void HttpClient::give_(std::unique_ptr<Conn> c) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (idle_.size() < 16) idle_.push_back(std::move(c));
+}
+
+bool HttpClient::send_request_(Conn& c, const std::string& method, const std::string& path,
+                               const std::string& body, const std::string& content_type,
+                               const std::string& accept) {
+  std::string req;
+  req.reserve(256 + body.size());
+  req += method + " " + path + " HTTP/1.1\r\n";
+  req += "Host: " + (url_.scheme == "unix" ? std::string("localhost") : url_.host) + "\r\n";
+  req += "User-Agent: gpupool-manager/0.1\r\n";
+  req += "Accept: " + accept + "\r\n";
+  if (!token_.empty()) req += "Authorization: Bearer " + token_ + "\r\n";
+  if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
+    req += "Content-Type: " + content_type + "\r\n";
+    req += "Content-Length: " + std::to_string(body.size()) + "\r\n";
+  }
+  req += "\r\n";
+  req += body;
+  return c.send_all(req);
+}
+
+namespace {
+
+std::string lower(std::string s) {
+  for (auto& ch : s) ch = static_cast<char>(tolower(static_cast<unsigned char>(ch)));
+  return s;
+}
+
+// Parse status line + headers from c.rbuf (reading more as needed). Returns false on failure.
+template <class ConnT>
+bool read_head(ConnT& c, HttpResponse& r, int timeout_ms, std::string* err) {
+  size_t end;
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while ((end = c.rbuf.find("\r\n\r\n")) == std::string::npos) {
+    if (c.rbuf.size() > (1 << 20)) {
+      *err = "header too large";
+      return false;
+    }
+    int left = static_cast<int>(std::chrono::duration_cast<std::chrono::milliseconds>(
+                                    deadline - std::chrono::steady_clock::now())
+                                    .count());
+    if (left <= 0) {
+      *err = "timeout reading response head";
+      return false;
+    }
+    ssize_t n = c.fill(left);
+    if (n == 0) {
+      *err = "connection closed";
+      return false;
+    }
+    if (n == -2) {
+      *err = "timeout reading response head";
+      return false;
+    }
+    if (n < 0) {
+      *err = std::string("recv: ") + strerror(errno);
+      return false;
+    }
+  }
+  std::string head = c.rbuf.substr(0, end);
+  c.rbuf.erase(0, end + 4);
+  std::istringstream is(head);
+  std::string line;
+  std::getline(is, line);
+  if (line.size() < 12 || line.compare(0, 5, "HTTP/") != 0) {
+    *err = "bad status line";
+    return false;
+  }
+  r.status = std::atoi(line.c_str() + 9);
+  while (std::getline(is, line)) {
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    auto colon = line.find(':');
+    if (colon == std::string::npos) continue;
+    std::string v = line.substr(colon + 1);
+    size_t a = v.find_first_not_of(" \t");
+    v = a == std::string::npos ? "" : v.substr(a);
+    r.headers[lower(line.substr(0, colon))] = v;
+  }
+  return true;
+}
+
+}  // namespace
+
+HttpResponse HttpClient::request(const std::string& method, const std::string& path,
+                                 const std::string& body, const std::string& content_type,
+                                 const std::string& accept, int timeout_ms) {
+  if (timeout_ms < 0) timeout_ms = timeout_ms_;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    std::unique_ptr<Conn> c = take_();
+    bool reused = c != nullptr;
+    if (!c) c = connect_(timeout_ms);
+    if (!send_request_(*c, method, path, body, content_type, accept)) {
+      if (reused) continue;
+      throw HttpError("send failed: " + std::string(strerror(errno)));
+    }
+    HttpResponse r;
+    std::string err;
+    if (!read_head(*c, r, timeout_ms, &err)) {
+      if (reused && (err == "connection closed" || err.rfind("recv", 0) == 0)) continue;
+      throw HttpError(method + " " + path + ": " + err);
+    }
+    bool keep = true;
+    auto conn_hdr = r.headers.find("connection");
+    if (conn_hdr != r.headers.end() && lower(conn_hdr->second) == "close") keep = false;
+    auto te = r.headers.find("transfer-encoding");
+    auto cl = r.headers.find("content-length");
+    if (te != r.headers.end() && lower(te->second).find("chunked") != std::string::npos) {
+      ChunkedDecoder dec;
+      std::string pending = std::move(c->rbuf);
+      c->rbuf.clear();
+      for (;;) {
+        if (!dec.feed(pending, r.body)) throw HttpError("bad chunked encoding");
+        pending.clear();
+        if (dec.done()) break;
+        ssize_t n = c->fill(timeout_ms);
+        if (n <= 0) throw HttpError("connection lost reading chunked body");
+        pending = std::move(c->rbuf);
+        c->rbuf.clear();
+      }
+    } else if (cl != r.headers.end()) {
+      size_t want = std::stoull(cl->second);
+      while (c->rbuf.size() < want) {
+        ssize_t n = c->fill(timeout_ms);
+        if (n <= 0) throw HttpError("connection lost reading body");
+      }
+      r.body = c->rbuf.substr(0, want);
+      c->rbuf.erase(0, want);
+    } else if (r.status != 204 && r.status != 304 && method != "HEAD") {
+      for (;;) {
+        ssize_t n = c->fill(timeout_ms);
+        if (n == 0) break;
+        if (n < 0) throw HttpError("connection lost reading body");
+      }
+      r.body = std::move(c->rbuf);
+      keep = false;
+    }
+    if (keep) give_(std::move(c));
+    return r;
+  }
+  throw HttpError(method + " " + path + ": retries exhausted");
+}
+
+int HttpClient::stream_lines(const std::string& path,
+                             const std::function<bool(std::string_view)>& on_line,
+                             const std::atomic<bool>* stop, std::string* err_body, int poll_ms) {
+  auto c = connect_(timeout_ms_);
+  if (!send_request_(*c, "GET", path, "", "application/json", "application/json"))
+    throw HttpError("send failed");
+  HttpResponse r;
+  std::string err;
+  if (!read_head(*c, r, timeout_ms_, &err)) throw HttpError("GET " + path + ": " + err);
+  bool chunked = false;
+  auto te = r.headers.find("transfer-encoding");
+  if (te != r.headers.end() && lower(te->second).find("chunked") != std::string::npos) chunked = true;
+  ChunkedDecoder dec;
+  std::string payload, pending = std::move(c->rbuf);
+  c->rbuf.clear();
+  if (r.status >= 400) {
+    // read the (short) error body fully
+    for (int i = 0; i < 100; ++i) {
+      if (chunked) {
+        if (!dec.feed(pending, payload)) break;
+        if (dec.done()) break;
+      } else {
+        payload += pending;
+      }
+      pending.clear();
+      auto cl = r.headers.find("content-length");
+      if (!chunked && cl != r.headers.end() && payload.size() >= std::stoull(cl->second)) break;
+      ssize_t n = c->fill(timeout_ms_);
+      if (n <= 0) break;
+      pending = std::move(c->rbuf);
+      c->rbuf.clear();
+    }
+    if (err_body) *err_body = payload;
+    return r.status;
+  }
+  for (;;) {
+    if (chunked) {
+      if (!dec.feed(pending, payload)) throw HttpError("bad chunked encoding in stream");
+    } else {
+      payload += pending;
+    }
+    pending.clear();
+    size_t nl;
+    while ((nl = payload.find('\n')) != std::string::npos) {
+      std::string_view line(payload.data(), nl);
+      if (!line.empty() && line.back() == '\r') line.remove_suffix(1);
+      bool cont = line.empty() ? true : on_line(line);
+      payload.erase(0, nl + 1);
+      if (!cont) return r.status;
+    }
+    if (chunked && dec.done()) return r.status;
+    for (;;) {
+      if (stop && stop->load()) return r.status;
+      ssize_t n = c->fill(poll_ms);
+      if (n == -2) continue;  // timeout: re-check stop
+      if (n <= 0) return r.status;  // EOF / error: caller re-watches
+      break;
+    }
+    pending = std::move(c->rbuf);
+    c->rbuf.clear();
+  }
+}
+
+// ------------------------------------------------------------------ server
+HttpServer::~HttpServer() { stop(); }
+
+void HttpServer::route(const std::string& path, Handler h) { routes_[path] = std::move(h); }
+
+int HttpServer::listen(const std::string& addr) {
+  std::string host = "0.0.0.0";
+  int port = 0;
+  auto colon = addr.rfind(':');
+  if (colon == std::string::npos) {
+    port = std::stoi(addr);
+  } else {
+    if (colon > 0) host = addr.substr(0, colon);
+    port = std::stoi(addr.substr(colon + 1));
+  }
+  lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (lfd_ < 0) throw HttpError("socket failed");
+  int one = 1;
+  setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons(static_cast<uint16_t>(port));
+  if (inet_pton(AF_INET, host.c_str(), &sa.sin_addr) != 1) throw HttpError("bad listen host " + host);
+  if (::bind(lfd_, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0)
+    throw HttpError("bind " + addr + ": " + strerror(errno));
+  if (::listen(lfd_, 64) != 0) throw HttpError("listen failed");
+  socklen_t len = sizeof sa;
+  getsockname(lfd_, reinterpret_cast<sockaddr*>(&sa), &len);
+  th_ = std::thread([this] { loop_(); });
+  return ntohs(sa.sin_port);
+}
+
+void HttpServer::stop() {
+  if (stop_.exchange(true)) return;
+  if (lfd_ >= 0) {
+    ::shutdown(lfd_, SHUT_RDWR);
+  }
+  if (th_.joinable()) th_.join();
+  if (lfd_ >= 0) ::close(lfd_);
+  lfd_ = -1;
+}
+
+void HttpServer::loop_() {
+  while (!stop_.load()) {
+    pollfd p{lfd_, POLLIN, 0};
+    int r = ::poll(&p, 1, 200);
+    if (r <= 0) continue;
+    int fd = ::accept4(lfd_, nullptr, nullptr, SOCK_CLOEXEC);
+    if (fd < 0) continue;
+    serve_(fd);  // handlers are fast (metrics/health); serve inline
+    ::close(fd);
+  }
+}
+
+void HttpServer::serve_(int fd) {
+  std::string buf;
+  char tmp[4096];
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+  size_t hend;
+  while ((hend = buf.find("\r\n\r\n")) == std::string::npos) {
+    if (std::chrono::steady_clock::now() > deadline || buf.size() > 65536) return;
+    pollfd p{fd, POLLIN, 0};
+    if (::poll(&p, 1, 200) <= 0) continue;
+    ssize_t n = ::recv(fd, tmp, sizeof tmp, 0);
+    if (n <= 0) return;
+    buf.append(tmp, static_cast<size_t>(n));
+  }
+  std::istringstream is(buf.substr(0, hend));
+  std::string method, target;
+  is >> method >> target;
+  std::string body = buf.substr(hend + 4);
+  auto q = target.find('?');
+  std::string path = q == std::string::npos ? target : target.substr(0, q);
+  Reply rep;
+  auto it = routes_.find(path);
+  if (it == routes_.end()) {
+    rep.status = 404;
+    rep.body = "not found\n";
+  } else {
+    try {
+      rep = it->second(method, target, body);
+    } catch (const std::exception& e) {
+      rep.status = 500;
+      rep.body = std::string("error: ") + e.what() + "\n";
+    }
+  }
+  std::string out = "HTTP/1.1 " + std::to_string(rep.status) + " X\r\nContent-Type: " + rep.content_type +
+                    "\r\nContent-Length: " + std::to_string(rep.body.size()) +
+                    "\r\nConnection: close\r\n\r\n" + rep.body;
+  size_t off = 0;
+  while (off < out.size()) {
+    ssize_t n = ::send(fd, out.data() + off, out.size() - off, MSG_NOSIGNAL);
+    if (n <= 0) return;
+    off += static_cast<size_t>(n);
+  }
+}
+
+}  // namespace gpupool

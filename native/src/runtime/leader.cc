@@ -1,0 +1,109 @@
+#include "gpupool/leader.h"
+
+#include <thread>
+
+namespace gpupool {
+
+LeaderElector::LeaderElector(KubeClient& client, LeaderConfig cfg)
+    : client_(client), cfg_(std::move(cfg)), log_(Logger("leader").with("identity", cfg_.identity)) {}
+
+bool LeaderElector::try_acquire_or_renew() {
+  auto now_tp = std::chrono::system_clock::now();
+  std::string now = microtime_now();
+  int dur_s = static_cast<int>(std::chrono::duration_cast<std::chrono::seconds>(cfg_.lease_duration).count());
+  Json lease;
+  try {
+    lease = client_.get(res::leases(), cfg_.ns, cfg_.name);
+  } catch (const KubeError& e) {
+    if (!e.not_found()) throw;
+    Json obj = Json::object();
+    obj["apiVersion"] = "coordination.k8s.io/v1";
+    obj["kind"] = "Lease";
+    obj["metadata"]["name"] = cfg_.name;
+    obj["metadata"]["namespace"] = cfg_.ns;
+    obj["spec"]["holderIdentity"] = cfg_.identity;
+    obj["spec"]["leaseDurationSeconds"] = dur_s;
+    obj["spec"]["acquireTime"] = now;
+    obj["spec"]["renewTime"] = now;
+    obj["spec"]["leaseTransitions"] = 0;
+    try {
+      client_.create(res::leases(), cfg_.ns, obj);
+      leader_ = true;
+      return true;
+    } catch (const KubeError& e2) {
+      if (e2.code == 409) return false;  // someone else created it first
+      throw;
+    }
+  }
+  const Json& spec = lease["spec"];
+  const std::string& holder = spec["holderIdentity"].as_string();
+  bool mine = holder == cfg_.identity;
+  if (!mine && !holder.empty()) {
+    std::chrono::system_clock::time_point renew;
+    if (parse_rfc3339(spec["renewTime"].as_string(), &renew)) {
+      auto expiry = renew + std::chrono::seconds(spec["leaseDurationSeconds"].as_int(dur_s));
+      if (expiry > now_tp) {
+        leader_ = false;
+        return false;  // held by a live leader
+      }
+    }
+  }
+  Json upd = lease;
+  upd["spec"]["holderIdentity"] = cfg_.identity;
+  upd["spec"]["leaseDurationSeconds"] = dur_s;
+  upd["spec"]["renewTime"] = now;
+  if (!mine) {
+    upd["spec"]["acquireTime"] = now;
+    upd["spec"]["leaseTransitions"] = spec["leaseTransitions"].as_int(0) + 1;
+  }
+  try {
+    client_.update(res::leases(), cfg_.ns, upd);
+  } catch (const KubeError& e) {
+    if (e.conflict()) {
+      leader_ = false;
+      return false;
+    }
+    throw;
+  }
+  leader_ = true;
+  return true;
+}
+
+void LeaderElector::run(const std::function<void()>& on_started,
+                        const std::function<void()>& on_stopped, const std::atomic<bool>* stop) {
+  using clock = std::chrono::steady_clock;
+  while (!stop->load()) {
+    bool ok = false;
+    try {
+      ok = try_acquire_or_renew();
+    } catch (const std::exception& e) {
+      log_.warn("lease acquire failed", Json::object().set("error", e.what()));
+    }
+    if (ok) break;
+    std::this_thread::sleep_for(cfg_.retry_period);
+  }
+  if (stop->load()) return;
+  log_.info("became leader", Json::object().set("lease", cfg_.ns + "/" + cfg_.name));
+  on_started();
+  auto last_renew = clock::now();
+  while (!stop->load()) {
+    std::this_thread::sleep_for(std::min(cfg_.retry_period, std::chrono::milliseconds(500)));
+    if (clock::now() - last_renew < cfg_.retry_period) continue;
+    bool ok = false;
+    try {
+      ok = try_acquire_or_renew();
+    } catch (const std::exception& e) {
+      log_.warn("lease renew failed", Json::object().set("error", e.what()));
+    }
+    if (ok) {
+      last_renew = clock::now();
+    } else if (clock::now() - last_renew > cfg_.renew_deadline) {
+      log_.error("lost leadership", Json());
+      leader_ = false;
+      break;
+    }
+  }
+  on_stopped();
+}
+
+}  // namespace gpupool

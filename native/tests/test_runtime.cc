@@ -1,0 +1,228 @@
+// Unit tests: JSON DOM/parser (incl. a randomized fuzz loop), chunked decoding, work queue
+// semantics, metrics, conditions, validation. Run under ASan/UBSan and TSan via `make SAN=...`.
+#include <atomic>
+#include <random>
+#include <set>
+#include <thread>
+
+#include "gpupool/api.h"
+#include "gpupool/http.h"
+#include "gpupool/json.h"
+#include "gpupool/log.h"
+#include "gpupool/metrics.h"
+#include "gpupool/workqueue.h"
+#include "testing.h"
+
+using namespace gpupool;
+
+TEST(json_roundtrip) {
+  const char* doc = R"({"a":1,"b":[true,false,null,-2.5e3,"x\"y\\z\n"],"c":{"d":{}, "e":[]},"u":"\u00e9\ud83d\ude00"})";
+  Json j = Json::parse(doc);
+  EXPECT_EQ(j["a"].as_int(), 1);
+  EXPECT_EQ(j["b"].size(), 5u);
+  EXPECT_EQ(j["b"][3].as_double(), -2500.0);
+  EXPECT_EQ(j["b"][4].as_string(), std::string("x\"y\\z\n"));
+  EXPECT_EQ(j["u"].as_string(), std::string("\xc3\xa9\xf0\x9f\x98\x80"));
+  Json k = Json::parse(j.dump());
+  EXPECT_TRUE(j == k);
+  Json p = Json::parse(j.dump(2));
+  EXPECT_TRUE(j == p);
+  EXPECT_TRUE(j.path("c.d").is_object());
+  EXPECT_TRUE(j.path("c.missing.deeper").is_null());
+}
+
+TEST(json_key_order_and_mutation) {
+  Json j = Json::object();
+  j["z"] = 1;
+  j["a"] = 2;
+  j["m"]["n"] = "x";
+  EXPECT_EQ(j.dump(), std::string(R"({"z":1,"a":2,"m":{"n":"x"}})"));
+  EXPECT_TRUE(j.erase("a"));
+  EXPECT_EQ(j.dump(), std::string(R"({"z":1,"m":{"n":"x"}})"));
+  Json arr;
+  arr.push_back(1);
+  arr.push_back("two");
+  EXPECT_EQ(arr.dump(), std::string(R"([1,"two"])"));
+  EXPECT_TRUE(Json(3) == Json(3.0));
+}
+
+TEST(json_rejects_malformed) {
+  const char* bad[] = {"", "{", "[1,]", "{\"a\" 1}", "tru", "\"\\x\"", "01", "1.", "-", "\"\x01\"",
+                       "{\"a\":1}}", "\"\\ud800\"", "[1 2]"};
+  for (const char* b : bad) EXPECT_TRUE(!Json::try_parse(b).has_value());
+  std::string deep(100000, '[');
+  EXPECT_TRUE(!Json::try_parse(deep).has_value());  // depth limit, no stack overflow
+}
+
+TEST(json_fuzz_no_crash) {
+  // Mutational fuzz: random byte flips of valid documents must never crash (ASan/UBSan build).
+  std::mt19937 rng(12345);
+  std::vector<std::string> seeds = {R"({"type":"ADDED","object":{"metadata":{"name":"p","resourceVersion":"12"}}})",
+                                    R"([1,2.5,-3e-2,"a\u0041",{"x":[null,true]}])"};
+  for (int it = 0; it < 20000; ++it) {
+    std::string s = seeds[static_cast<size_t>(it) % seeds.size()];
+    int flips = 1 + static_cast<int>(rng() % 4);
+    for (int f = 0; f < flips; ++f) s[rng() % s.size()] = static_cast<char>(rng() % 256);
+    if (rng() % 5 == 0) s = s.substr(0, rng() % s.size());
+    auto j = Json::try_parse(s);
+    if (j) (void)j->dump();
+  }
+}
+
+TEST(chunked_decoder_basic_and_split) {
+  std::string wire = "4\r\nWiki\r\n5;ext=1\r\npedia\r\nE\r\n in\r\n\r\nchunks.\r\n0\r\n\r\n";
+  for (size_t split = 0; split <= wire.size(); ++split) {
+    ChunkedDecoder d;
+    std::string out;
+    EXPECT_TRUE(d.feed(std::string_view(wire).substr(0, split), out));
+    EXPECT_TRUE(d.feed(std::string_view(wire).substr(split), out));
+    EXPECT_TRUE(d.done());
+    EXPECT_EQ(out, std::string("Wikipedia in\r\n\r\nchunks."));
+  }
+}
+
+TEST(chunked_decoder_rejects_garbage) {
+  const char* bad[] = {"zz\r\n", "4\r\nabcdX", "\r\n", "4\rX", "ffffffffffffffffff\r\n"};
+  for (const char* b : bad) {
+    ChunkedDecoder d;
+    std::string out;
+    EXPECT_TRUE(!d.feed(b, out));
+  }
+  std::mt19937 rng(7);
+  for (int it = 0; it < 5000; ++it) {  // fuzz: never crash / over-read
+    std::string s(1 + rng() % 64, '\0');
+    for (auto& c : s) c = "0123456789abcdef\r\n;x"[rng() % 21];
+    ChunkedDecoder d;
+    std::string out;
+    (void)d.feed(s, out);
+  }
+}
+
+TEST(url_parse) {
+  Url u = Url::parse("http://127.0.0.1:6443");
+  EXPECT_EQ(u.host, std::string("127.0.0.1"));
+  EXPECT_EQ(u.port, 6443);
+  Url x = Url::parse("unix:///tmp/agent.sock");
+  EXPECT_EQ(x.unix_path, std::string("/tmp/agent.sock"));
+  EXPECT_THROW(Url::parse("ftp://x"));
+}
+
+TEST(workqueue_dedup_and_processing) {
+  WorkQueue q;
+  q.add("a");
+  q.add("a");
+  q.add("b");
+  EXPECT_EQ(q.len(), 2u);
+  std::string k;
+  EXPECT_TRUE(q.get_for(&k, std::chrono::milliseconds(10)));
+  EXPECT_EQ(k, std::string("a"));
+  q.add("a");  // while processing: marked dirty, not queued twice
+  EXPECT_EQ(q.len(), 1u);
+  q.done("a");  // re-queued now
+  EXPECT_EQ(q.len(), 2u);
+}
+
+TEST(workqueue_delay_and_backoff) {
+  WorkQueue q(std::chrono::milliseconds(5), std::chrono::milliseconds(40));
+  q.add_after("x", std::chrono::milliseconds(30));
+  std::string k;
+  EXPECT_TRUE(!q.get_for(&k, std::chrono::milliseconds(5)));
+  EXPECT_TRUE(q.get_for(&k, std::chrono::milliseconds(200)));
+  EXPECT_EQ(k, std::string("x"));
+  q.done("x");
+  EXPECT_EQ(q.backoff_for("y").count(), 5);
+  q.add_rate_limited("y");
+  EXPECT_EQ(q.backoff_for("y").count(), 10);
+  q.add_rate_limited("y");
+  q.add_rate_limited("y");
+  q.add_rate_limited("y");
+  EXPECT_EQ(q.backoff_for("y").count(), 40);  // capped
+  EXPECT_EQ(q.num_requeues("y"), 4);
+  q.forget("y");
+  EXPECT_EQ(q.num_requeues("y"), 0);
+}
+
+TEST(workqueue_concurrent_exclusive) {
+  // Many producers, 4 workers: a key is never processed by two workers at once.
+  WorkQueue q;
+  std::atomic<int> inflight_a{0}, violations{0}, processed{0};
+  std::atomic<bool> stop{false};
+  std::vector<std::thread> workers;
+  for (int w = 0; w < 4; ++w) {
+    workers.emplace_back([&] {
+      std::string k;
+      while (q.get(&k)) {
+        if (k == "a" && inflight_a.fetch_add(1) != 0) violations++;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (k == "a") inflight_a--;
+        processed++;
+        q.done(k);
+      }
+    });
+  }
+  std::vector<std::thread> producers;
+  for (int p = 0; p < 4; ++p)
+    producers.emplace_back([&, p] {
+      for (int i = 0; i < 500; ++i) q.add(i % 3 == 0 ? "a" : "k" + std::to_string((i + p) % 17));
+    });
+  for (auto& t : producers) t.join();
+  std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  q.shutdown();
+  for (auto& t : workers) t.join();
+  EXPECT_EQ(violations.load(), 0);
+  EXPECT_TRUE(processed.load() > 0);
+}
+
+TEST(metrics_render_and_quantile) {
+  Registry& r = Registry::global();
+  auto& c = r.counter("test_total", "help");
+  c.inc({{"k", "v"}});
+  c.inc({{"k", "v"}}, 2);
+  EXPECT_EQ(c.get({{"k", "v"}}), 3.0);
+  auto& h = r.histogram("test_seconds", "help", {0.1, 0.2, 0.4});
+  for (int i = 0; i < 10; ++i) h.observe({}, 0.15);
+  EXPECT_EQ(h.count(), 10u);
+  double q = h.quantile({}, 0.5);
+  EXPECT_TRUE(q > 0.1 && q <= 0.2);
+  std::string txt = r.render();
+  EXPECT_TRUE(txt.find("test_total{k=\"v\"} 3") != std::string::npos);
+  EXPECT_TRUE(txt.find("test_seconds_bucket{le=\"+Inf\"} 10") != std::string::npos);
+}
+
+TEST(conditions_transition_time_only_on_flip) {
+  Json conds;
+  EXPECT_TRUE(set_condition(conds, "Ready", "False", "ScalingUp", "0/1", 1, "T1"));
+  EXPECT_TRUE(!set_condition(conds, "Ready", "False", "ScalingUp", "0/1", 1, "T2"));
+  EXPECT_EQ(find_condition(conds, "Ready")["lastTransitionTime"].as_string(), std::string("T1"));
+  EXPECT_TRUE(set_condition(conds, "Ready", "False", "Probing", "0/1", 1, "T3"));
+  EXPECT_EQ(find_condition(conds, "Ready")["lastTransitionTime"].as_string(), std::string("T1"));
+  EXPECT_TRUE(set_condition(conds, "Ready", "True", "AllReplicasReady", "1/1", 2, "T4"));
+  EXPECT_EQ(find_condition(conds, "Ready")["lastTransitionTime"].as_string(), std::string("T4"));
+  EXPECT_EQ(find_condition(conds, "Ready")["observedGeneration"].as_int(), 2);
+  EXPECT_TRUE(condition_true(conds, "Ready"));
+  EXPECT_EQ(conds.size(), 1u);
+}
+
+TEST(validation_matches_crd) {
+  Json ok = Json::parse(R"({"kind":"Mi355xPool","spec":{"replicas":2}})");
+  EXPECT_TRUE(validate_mi355x(ok).empty());
+  Json neg = Json::parse(R"({"kind":"Mi355xPool","spec":{"replicas":-1}})");
+  EXPECT_EQ(validate_mi355x(neg).size(), 1u);
+  Json badres = Json::parse(R"({"kind":"Mi355xPool","spec":{"replicas":1,"resourceName":"BAD"}})");
+  EXPECT_EQ(validate_mi355x(badres).size(), 1u);
+  Json az = Json::parse(R"({"kind":"AzureVmPool","spec":{"replicas":0,"resourceGroupName":"rg","location":"eastus",
+    "vmSize":"s","vnetName":"v","subnetName":"s","azureCredentialSecret":"c",
+    "imageReference":{"publisher":"p","offer":"o","sku":"s","version":"v"}}})");
+  EXPECT_TRUE(validate_azure(az).empty());
+  az["spec"].erase("location");
+  EXPECT_EQ(validate_azure(az).size(), 1u);
+}
+
+TEST(rfc3339_roundtrip) {
+  auto now = std::chrono::system_clock::now();
+  std::chrono::system_clock::time_point t;
+  EXPECT_TRUE(parse_rfc3339(rfc3339(now), &t));
+  EXPECT_TRUE(std::chrono::abs(std::chrono::duration_cast<std::chrono::seconds>(t - now)).count() <= 1);
+  EXPECT_TRUE(parse_rfc3339(microtime_now(), &t));
+  EXPECT_TRUE(!parse_rfc3339("garbage", &t));
+}
