@@ -1,0 +1,60 @@
+"""``python -m gpupool.agent --node mi355x-node-0 --backend amdsmi --socket /run/gpupool/agent.sock
+--apiserver http://127.0.0.1:6443 --plugin-dir /var/lib/kubelet/device-plugins``"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import socket
+
+from .agent import Agent, AgentConfig, serve
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser(description="gpupool node agent (MI355X)")
+    ap.add_argument("--node", default=os.environ.get("GPUPOOL_NODE", socket.gethostname()))
+    ap.add_argument("--backend", default=os.environ.get("GPUPOOL_BACKEND", "auto"),
+                    choices=["auto", "amdsmi", "cli", "fake"])
+    ap.add_argument("--fixture", default="", help="fake backend node snapshot JSON")
+    ap.add_argument("--faults", default=os.environ.get("GPUPOOL_FAULTS", ""),
+                    help="fault overlay JSON (hot-reloaded)")
+    ap.add_argument("--count", type=int, default=-1, help="fake backend: limit #devices")
+    ap.add_argument("--cli-dir", default="", help="cli backend: read captured amd-smi JSON")
+    ap.add_argument("--state-dir", default=os.environ.get("GPUPOOL_STATE_DIR", "/var/lib/gpupool"))
+    ap.add_argument("--socket", default="", help="unix socket for the manager RPC")
+    ap.add_argument("--listen", default="", help="host:port for the manager RPC (TCP)")
+    ap.add_argument("--endpoint", default="", help="endpoint written to the Node annotation")
+    ap.add_argument("--apiserver", default=os.environ.get("GPUPOOL_APISERVER", ""))
+    ap.add_argument("--token", default=os.environ.get("GPUPOOL_TOKEN", ""))
+    ap.add_argument("--plugin-dir", default="", help="kubelet device-plugin directory")
+    ap.add_argument("--pod-resources", default="", help="kubelet PodResources socket")
+    ap.add_argument("--probe", default="", choices=["", "inproc", "subprocess", "simulated", "off"])
+    ap.add_argument("--probe-sim-ms", type=float, default=20.0)
+    ap.add_argument("--probe-gemm-n", type=int, default=4096)
+    ap.add_argument("--sample-interval", type=float, default=2.0)
+    ap.add_argument("--quarantine", type=float, default=300.0)
+    ap.add_argument("--no-fsync", action="store_true")
+    ap.add_argument("--ready-file", default="")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    logging.basicConfig(level=logging.DEBUG if a.verbose else logging.INFO,
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    cfg = AgentConfig(node=a.node, backend=a.backend, fixture=a.fixture, faults=a.faults,
+                      count=a.count, cli_dir=a.cli_dir, state_dir=a.state_dir, socket=a.socket,
+                      listen=a.listen, endpoint=a.endpoint, apiserver=a.apiserver, token=a.token,
+                      plugin_dir=a.plugin_dir, pod_resources=a.pod_resources, probe_mode=a.probe,
+                      probe_sim_ms=a.probe_sim_ms, probe_gemm_n=a.probe_gemm_n,
+                      sample_interval=a.sample_interval, quarantine_s=a.quarantine,
+                      fsync=not a.no_fsync)
+    agent = Agent(cfg)
+    try:
+        asyncio.run(serve(agent, a.ready_file or None))
+    except KeyboardInterrupt:
+        pass
+    finally:
+        agent.stop()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,660 @@
+"""gpupool node agent: owns one node's MI355X GPUs.
+
+Responsibilities (SURVEY.md §7.1 architecture):
+  * discovery + telemetry through libmi355x_dev (amdsmi | cli | fake backend, fault overlay);
+  * the claim ledger (all-or-nothing, topology-aware claims; cordon; release; quarantine);
+  * claim-time HIP probes (warm, in-process by default) — the B4 readiness check;
+  * health sampling against each owning pool's policy (verdicts from libmi355x_dev);
+  * the ROCm device plugin endpoints (one per extended resource) + PodResources lookups;
+  * Node registration (labels, agent endpoint annotation, GPUPoolAgentReady condition);
+  * an HTTP/JSON RPC surface for the manager (unix socket and/or TCP) with a long-poll event feed.
+
+Replaces what the reference's controller did through the Azure SDK (README.md:179-221) with a
+node-local owner of physical devices.
+"""
+from __future__ import annotations
+
+import asyncio
+import datetime as _dt
+import json
+import logging
+import os
+import socket
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any
+
+from aiohttp import web
+
+from ..api import schema
+from ..ops import devlib
+from .ledger import Ledger
+from .prober import Prober, default_mode
+
+log = logging.getLogger("gpupool.agent")
+
+
+def now_rfc3339() -> str:
+    return _dt.datetime.now(_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+@dataclass
+class AgentConfig:
+    node: str = field(default_factory=socket.gethostname)
+    backend: str = "auto"
+    fixture: str = ""
+    faults: str = ""
+    count: int = -1
+    cli_dir: str = ""
+    state_dir: str = "/var/lib/gpupool"
+    socket: str = ""                 # unix socket for the RPC server
+    listen: str = ""                 # optional host:port
+    endpoint: str = ""               # what the Node annotation advertises (default: socket)
+    apiserver: str = ""              # empty: no Node registration
+    token: str = ""
+    plugin_dir: str = ""             # kubelet device-plugin dir; empty: device plugin disabled
+    pod_resources: str = ""          # kubelet PodResources socket
+    probe_mode: str = ""             # inproc | subprocess | simulated | off (default by backend)
+    probe_sim_ms: float = 20.0
+    probe_gemm_n: int = 4096
+    sample_interval: float = 2.0
+    quarantine_s: float = 300.0
+    advertise_wait_s: float = 2.0
+    fsync: bool = True
+
+
+class Agent:
+    def __init__(self, cfg: AgentConfig):
+        self.cfg = cfg
+        self.lock = threading.RLock()
+        dev_cfg: dict[str, Any] = {"node": cfg.node}
+        if cfg.fixture:
+            dev_cfg["fixture"] = cfg.fixture
+        if cfg.faults:
+            dev_cfg["faults"] = cfg.faults
+        if cfg.count >= 0:
+            dev_cfg["count"] = cfg.count
+        if cfg.cli_dir:
+            dev_cfg["cliDir"] = cfg.cli_dir
+        self.dev = devlib.DeviceLib(cfg.backend, **dev_cfg)
+        self.ledger = Ledger(cfg.state_dir, fsync=cfg.fsync)
+        self.records: dict[str, dict] = self.ledger.load()
+        self.snap = self.dev.snapshot()
+        self.backend = self.snap.get("backend", cfg.backend)
+        self.by_uuid = {d["uuid"]: d for d in self.snap["devices"]}
+        self.verdicts: dict[str, dict] = {}
+        self.gen = 0
+        self.changes: list[tuple[int, set[str]]] = []
+        self.waiters: list[tuple[asyncio.AbstractEventLoop, asyncio.Future]] = []
+        self.advertised: dict[str, set[str]] = {}
+        self._adv_event = threading.Event()
+        self.plugins: dict = {}
+        self.probe_mode = cfg.probe_mode or default_mode(self.backend)
+        self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n)
+        self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0,
+                      "probe_ms_sum": 0.0, "samples": 0}
+        self._pods_cache: tuple[float, dict[str, list[dict]]] = (0.0, {})
+        self._stop = threading.Event()
+        self._threads: list[threading.Thread] = []
+        self._evaluate_all()
+        log.info("agent %s: backend=%s devices=%d probe=%s (init %.0f ms) ledger=%d claims",
+                 cfg.node, self.backend, len(self.by_uuid), self.probe_mode, self.prober.init_ms,
+                 len(self.records))
+
+    # ================================================================ health
+    def _policy_for(self, uuid: str) -> dict:
+        rec = self.records.get(uuid)
+        return (rec or {}).get("policy") or {}
+
+    def _evaluate_all(self) -> set[str]:
+        """Re-evaluate every device; returns pool UIDs whose devices changed verdict."""
+        changed: set[str] = set()
+        for uuid, d in self.by_uuid.items():
+            rec = self.records.get(uuid)
+            baseline = (rec or {}).get("baseline") or d
+            v = devlib.evaluate(d, baseline, self._policy_for(uuid))
+            old = self.verdicts.get(uuid)
+            if old is None or old.get("healthy") != v.get("healthy") or \
+                    old.get("reasons") != v.get("reasons"):
+                if rec:
+                    changed.add(rec["poolUID"])
+                else:
+                    changed.add("*free*")
+            self.verdicts[uuid] = v
+        # claimed devices that vanished from enumeration
+        for uuid, rec in self.records.items():
+            if uuid not in self.by_uuid:
+                v = {"healthy": False, "present": False, "xgmiOk": True, "eccOk": True,
+                     "thermalOk": True, "partitionOk": True,
+                     "reasons": ["DeviceMissing: device no longer enumerated"]}
+                if self.verdicts.get(uuid, {}).get("present", True):
+                    changed.add(rec["poolUID"])
+                self.verdicts[uuid] = v
+        return changed
+
+    def sample(self) -> set[str]:
+        snap = self.dev.snapshot()
+        with self.lock:
+            self.snap = snap
+            self.by_uuid = {d["uuid"]: d for d in snap["devices"]}
+            changed = self._evaluate_all()
+            self.stats["samples"] += 1
+        if changed:
+            self._bump(changed)
+            self._notify_plugins()
+        return changed
+
+    def _sampler(self) -> None:
+        while not self._stop.wait(self.cfg.sample_interval):
+            try:
+                self.sample()
+            except Exception:
+                log.exception("health sample failed")
+
+    # ================================================================ events
+    def _bump(self, pools: set[str]) -> None:
+        with self.lock:
+            self.gen += 1
+            self.changes.append((self.gen, set(pools)))
+            self.changes = self.changes[-256:]
+            waiters, self.waiters = self.waiters, []
+        for loop, fut in waiters:
+            loop.call_soon_threadsafe(lambda f=fut: f.done() or f.set_result(None))
+
+    def changed_since(self, since: int) -> tuple[int, list[str]]:
+        with self.lock:
+            pools: set[str] = set()
+            for g, ps in self.changes:
+                if g > since:
+                    pools |= ps
+            if self.changes and self.changes[0][0] > since + 1 and since >= 0:
+                pools.add("*")  # history truncated: tell the manager to resync everything
+            return self.gen, sorted(p for p in pools if p != "*free*") + \
+                (["*"] if "*free*" in pools else [])
+
+    # ================================================================ views
+    def _pods_by_device(self) -> dict[str, list[dict]]:
+        if not self.cfg.pod_resources:
+            return {}
+        ts, cache = self._pods_cache
+        if time.monotonic() - ts < 0.05:
+            return cache
+        from .podresources import list_pod_devices
+        try:
+            cache = list_pod_devices(self.cfg.pod_resources)
+        except Exception as e:  # kubelet down: keep last known view
+            log.debug("podresources list failed: %s", e)
+        self._pods_cache = (time.monotonic(), cache)
+        return cache
+
+    def _advertisable(self, uuid: str) -> bool:
+        rec = self.records.get(uuid)
+        if not rec or rec.get("state") != "Claimed":
+            return False
+        v = self.verdicts.get(uuid, {})
+        return bool(v.get("healthy")) and bool((rec.get("probe") or {}).get("passed"))
+
+    def device_view(self, uuid: str, pods: dict[str, list[dict]]) -> dict:
+        d = self.by_uuid.get(uuid, {"uuid": uuid, "index": -1})
+        rec = self.records.get(uuid)
+        v = self.verdicts.get(uuid, {})
+        out = {
+            "uuid": uuid, "hipUUID": d.get("hipUUID", ""), "bdf": d.get("bdf", ""),
+            "index": d.get("index", -1), "node": self.cfg.node,
+            "renderNode": d.get("renderNode", ""), "kfdNode": d.get("kfdNode", -1),
+            "numa": d.get("numa"), "healthy": bool(v.get("healthy")), "verdict": v,
+            "present": d.get("present", uuid in self.by_uuid),
+            "pods": pods.get(uuid, []),
+        }
+        if rec:
+            res = rec.get("resourceName", schema.DEFAULT_RESOURCE)
+            out.update({"state": rec.get("state", "Claimed"), "poolUID": rec["poolUID"],
+                        "pool": rec.get("pool", ""), "resourceName": res,
+                        "claimedAt": rec.get("claimedAt", ""),
+                        "drainStartedAt": rec.get("drainStartedAt", ""),
+                        "probe": rec.get("probe")})
+            if self.plugins or self.cfg.plugin_dir:
+                out["advertised"] = uuid in self.advertised.get(res, set()) and \
+                    self._advertisable(uuid)
+            else:
+                out["advertised"] = self._advertisable(uuid)
+        else:
+            q = self.ledger.quarantined().get(uuid) if self.ledger else None
+            out["state"] = "Quarantined" if q else "Free"
+            if q:
+                out["quarantine"] = q
+        return out
+
+    def node_view(self) -> dict:
+        pods = self._pods_by_device()
+        with self.lock:
+            uuids = list(self.by_uuid) + [u for u in self.records if u not in self.by_uuid]
+            devices = [self.device_view(u, pods) for u in uuids]
+            return {"node": self.cfg.node, "backend": self.backend, "gen": self.gen,
+                    "probeMode": self.probe_mode,
+                    "advertiseRequired": bool(self.cfg.plugin_dir),
+                    "devices": devices, "topology": self.snap.get("topology", {})}
+
+    # ================================================================ claims
+    def claim(self, req: dict) -> dict:
+        pool_uid, count = req["poolUID"], int(req["count"])
+        policy = req.get("policy") or {}
+        resource = req.get("resourceName") or schema.DEFAULT_RESOURCE
+        probe_opts = req.get("probe") or {}
+        with self.lock:
+            quarantined = self.ledger.quarantined()
+            free = []
+            for uuid, d in self.by_uuid.items():
+                if uuid in self.records or uuid in quarantined or not d.get("present", True):
+                    continue
+                # claimability under the requesting pool's policy (baseline = now)
+                if devlib.evaluate(d, d, policy).get("healthy"):
+                    free.append(d["index"])
+            owned = [self.by_uuid[u]["index"] for u, r in self.records.items()
+                     if r["poolUID"] == pool_uid and u in self.by_uuid]
+            topo = self.snap.get("topology") or {}
+            n = len(self.snap["devices"])
+            weights = topo.get("weights") or [[0 if i == j else 15 for j in range(n)]
+                                              for i in range(n)]
+            numa = [d.get("numa", 0) for d in sorted(self.snap["devices"], key=lambda x: x["index"])]
+            sel = devlib.select(count, free, owned, req.get("topologyPolicy", "xgmi-packed"),
+                                weights, numa)
+            if len(sel) < count:
+                return {"ok": False, "reason": "InsufficientDevices",
+                        "message": f"need {count} free healthy GPU(s) on {self.cfg.node}, "
+                                   f"{len(free)} available (all-or-nothing)", "devices": []}
+            by_index = {d["index"]: d for d in self.snap["devices"]}
+            chosen = [by_index[i] for i in sel]
+            ts = now_rfc3339()
+            for d in chosen:
+                rec = {"uuid": d["uuid"], "poolUID": pool_uid, "pool": req.get("pool", ""),
+                       "resourceName": resource, "policy": policy,
+                       "baseline": {"ecc": d.get("ecc", {})}, "claimedAt": ts,
+                       "state": "Probing", "probe": None}
+                self.records[d["uuid"]] = rec
+                self.ledger.put(rec)
+            self.stats["claims"] += len(chosen)
+        # probes run outside the lock, concurrently across GPUs
+        t0 = time.perf_counter()
+        results = self.prober.probe_many(chosen, {**probe_opts, "enabled":
+                                                  probe_opts.get("enabled", True)})
+        probe_wall = (time.perf_counter() - t0) * 1e3
+        with self.lock:
+            for d, res in zip(chosen, results):
+                rec = self.records.get(d["uuid"])
+                if rec is None or rec["poolUID"] != pool_uid:
+                    continue  # released concurrently
+                rec["probe"] = res
+                rec["state"] = "Claimed"
+                self.ledger.put(rec)
+                self.stats["probes"] += 1
+                self.stats["probe_ms_sum"] += float(res.get("ms", 0.0))
+                if not res.get("passed"):
+                    self.stats["probe_failures"] += 1
+            self._evaluate_all()
+        self._ensure_plugin(resource)
+        self._notify_plugins()
+        self._wait_advertised(resource, [d["uuid"] for d in chosen])
+        pods = self._pods_by_device()
+        with self.lock:
+            views = [self.device_view(d["uuid"], pods) for d in chosen]
+        log.info("claimed %d GPU(s) for %s: %s (probe wall %.1f ms)", len(chosen),
+                 req.get("pool"), [d["index"] for d in chosen], probe_wall)
+        return {"ok": True, "devices": views, "probeWallMs": probe_wall}
+
+    def cordon(self, pool_uid: str, uuids: list[str]) -> dict:
+        with self.lock:
+            n = 0
+            for u in uuids:
+                rec = self.records.get(u)
+                if rec and rec["poolUID"] == pool_uid and rec.get("state") != "Draining":
+                    rec["state"] = "Draining"
+                    rec["drainStartedAt"] = now_rfc3339()
+                    self.ledger.put(rec)
+                    n += 1
+        self._notify_plugins()
+        return {"ok": True, "cordoned": n}
+
+    def release(self, pool_uid: str, uuids: list[str]) -> dict:
+        pods = self._pods_by_device()
+        released, refused = [], []
+        with self.lock:
+            for u in uuids:
+                rec = self.records.get(u)
+                if not rec or rec["poolUID"] != pool_uid:
+                    continue
+                if pods.get(u):
+                    refused.append(u)  # never release a GPU that still runs a pod
+                    continue
+                probe_ok = (rec.get("probe") or {}).get("passed", True)
+                healthy = self.verdicts.get(u, {}).get("healthy", True)
+                if not probe_ok or not healthy:
+                    why = "probe failed" if not probe_ok else "; ".join(
+                        self.verdicts.get(u, {}).get("reasons", []))
+                    self.ledger.quarantine(u, self.cfg.quarantine_s, why)
+                del self.records[u]
+                self.ledger.delete(u)
+                released.append(u)
+            self.stats["releases"] += len(released)
+            self._evaluate_all()
+        self._notify_plugins()
+        if refused:
+            return {"ok": False, "reason": "PodsRunning", "released": released,
+                    "message": f"GPUs still hold pods: {refused}"}
+        return {"ok": True, "released": released}
+
+    def update_policy(self, pool_uid: str, policy: dict, resource: str | None) -> dict:
+        changed = set()
+        with self.lock:
+            for u, rec in self.records.items():
+                if rec["poolUID"] != pool_uid:
+                    continue
+                rec["policy"] = policy
+                if resource and rec.get("resourceName") != resource:
+                    rec["resourceName"] = resource
+                changed.add(u)
+                self.ledger.put(rec)
+            self._evaluate_all()
+        if resource:
+            self._ensure_plugin(resource)
+        self._notify_plugins()
+        return {"ok": True, "updated": len(changed)}
+
+    # ================================================================ device plugin glue
+    def plugin_devices(self, resource: str) -> list[dict]:
+        with self.lock:
+            out = []
+            for u, rec in sorted(self.records.items(),
+                                 key=lambda kv: self.by_uuid.get(kv[0], {}).get("index", 99)):
+                if rec.get("resourceName", schema.DEFAULT_RESOURCE) != resource:
+                    continue
+                out.append({"uuid": u, "advertisable": self._advertisable(u),
+                            "numa": self.by_uuid.get(u, {}).get("numa")})
+            return out
+
+    def mark_advertised(self, resource: str, healthy: set[str] | None) -> None:
+        with self.lock:
+            plugin = self.plugins.get(resource)
+            if healthy is None:
+                if plugin is None or plugin.streams <= 0:
+                    self.advertised[resource] = set()
+            else:
+                self.advertised[resource] = set(healthy)
+        self._adv_event.set()
+
+    def _wait_advertised(self, resource: str, uuids: list[str]) -> None:
+        if not self.cfg.plugin_dir:
+            return
+        deadline = time.monotonic() + self.cfg.advertise_wait_s
+        while time.monotonic() < deadline:
+            with self.lock:
+                want = [u for u in uuids if self._advertisable(u)]
+                if all(u in self.advertised.get(resource, set()) for u in want):
+                    return
+                plugin = self.plugins.get(resource)
+                if plugin is None or plugin.streams <= 0:
+                    return  # no kubelet stream connected: do not block the claim
+            self._adv_event.wait(0.05)
+            self._adv_event.clear()
+
+    def _ensure_plugin(self, resource: str) -> None:
+        if not self.cfg.plugin_dir:
+            return
+        with self.lock:
+            if resource in self.plugins:
+                return
+            from .deviceplugin.server import DevicePluginServer
+            p = DevicePluginServer(self, resource, self.cfg.plugin_dir)
+            self.plugins[resource] = p
+        p.start()
+        p.register()
+
+    def _notify_plugins(self) -> None:
+        for p in list(self.plugins.values()):
+            p.notify()
+
+    def preferred(self, resource: str, available: list[str], must: list[str], size: int) -> list[str]:
+        with self.lock:
+            idx = {u: self.by_uuid[u]["index"] for u in available + must if u in self.by_uuid}
+            inv = {v: k for k, v in idx.items()}
+            topo = self.snap.get("topology") or {}
+            n = len(self.snap["devices"])
+            weights = topo.get("weights") or [[0 if i == j else 15 for j in range(n)]
+                                              for i in range(n)]
+            numa = [d.get("numa", 0) for d in sorted(self.snap["devices"], key=lambda x: x["index"])]
+        need = size - len(must)
+        cand = [idx[u] for u in available if u not in must and u in idx]
+        sel = devlib.select(need, cand, [idx[u] for u in must if u in idx], "xgmi-packed",
+                            weights, numa) if need > 0 else []
+        return list(must) + [inv[i] for i in sel]
+
+    def allocate_spec(self, resource: str, ids: list[str]) -> dict:
+        with self.lock:
+            hip, render = [], []
+            for u in ids:
+                rec = self.records.get(u)
+                if not rec or rec.get("resourceName", schema.DEFAULT_RESOURCE) != resource:
+                    raise ValueError(f"device {u} is not in any pool advertised as {resource}")
+                if not self._advertisable(u):
+                    raise ValueError(f"device {u} is not healthy/allocatable (state "
+                                     f"{rec.get('state')})")
+                d = self.by_uuid[u]
+                hip.append(d.get("hipUUID") or str(d["index"]))
+                if d.get("renderNode"):
+                    render.append(d["renderNode"])
+            envs = {"ROCR_VISIBLE_DEVICES": ",".join(hip),
+                    "GPUPOOL_DEVICE_UUIDS": ",".join(ids),
+                    "GPUPOOL_NODE": self.cfg.node}
+            return {"envs": envs, "devices": ["/dev/kfd"] + render,
+                    "annotations": {schema.ANN_POD_DEVICES: ",".join(ids)}}
+
+    # ================================================================ node registration
+    def register_node(self) -> None:
+        if not self.cfg.apiserver:
+            return
+        from ..kube import NODES, Client, KubeError
+        c = Client(self.cfg.apiserver, self.cfg.token or None)
+        devs = self.snap["devices"]
+        gfx = sorted({(d.get("asic") or {}).get("gfx", "") for d in devs} - {""})
+        labels = {schema.LABEL_GFX: gfx[0] if gfx else "unknown",
+                  "amd.com/gpu.count": str(len(devs)),
+                  "amd.com/gpu.product": "MI355X",
+                  "gpupool.amd.com/backend": self.backend,
+                  "kubernetes.io/hostname": self.cfg.node}
+        parts = sorted({(d.get("partition") or {}).get("compute", "") for d in devs} - {""})
+        if parts:
+            labels["amd.com/compute-partition"] = parts[0]
+        ann = {schema.ANN_AGENT_ENDPOINT: self.endpoint()}
+        try:
+            c.create(NODES, {"apiVersion": "v1", "kind": "Node",
+                             "metadata": {"name": self.cfg.node, "labels": labels,
+                                          "annotations": ann}})
+        except KubeError as e:
+            if e.code != 409:
+                raise
+            c.patch(NODES, self.cfg.node, {"metadata": {"labels": labels, "annotations": ann}})
+        self._heartbeat(c)
+
+    def _heartbeat(self, c) -> None:
+        from ..kube import NODES
+        ready = {"type": "GPUPoolAgentReady", "status": "True", "reason": "AgentRunning",
+                 "message": f"{len(self.by_uuid)} GPU(s) via {self.backend}; probe "
+                            f"{self.probe_mode}",
+                 "lastHeartbeatTime": now_rfc3339(), "lastTransitionTime": now_rfc3339()}
+        try:
+            node = c.get(NODES, self.cfg.node)
+            conds = [x for x in node.get("status", {}).get("conditions", [])
+                     if x.get("type") != "GPUPoolAgentReady"]
+            old = [x for x in node.get("status", {}).get("conditions", [])
+                   if x.get("type") == "GPUPoolAgentReady"]
+            if old and old[0].get("status") == "True":
+                ready["lastTransitionTime"] = old[0].get("lastTransitionTime", ready[
+                    "lastTransitionTime"])
+            st = node.get("status", {})
+            st["conditions"] = conds + [ready]
+            if not any(x.get("type") == "Ready" for x in conds):
+                st["conditions"].append({"type": "Ready", "status": "True",
+                                         "reason": "KubeletReady" if self.cfg.plugin_dir
+                                         else "AgentReady", "message": "",
+                                         "lastHeartbeatTime": now_rfc3339(),
+                                         "lastTransitionTime": now_rfc3339()})
+            c.patch(NODES, self.cfg.node, {"status": st}, sub="status")
+        except Exception as e:
+            log.warning("node heartbeat failed: %s", e)
+
+    def _heartbeater(self) -> None:
+        from ..kube import Client
+        c = Client(self.cfg.apiserver, self.cfg.token or None)
+        while not self._stop.wait(10.0):
+            self._heartbeat(c)
+
+    def endpoint(self) -> str:
+        if self.cfg.endpoint:
+            return self.cfg.endpoint
+        if self.cfg.socket:
+            return "unix://" + os.path.abspath(self.cfg.socket)
+        return f"http://{self.cfg.listen}"
+
+    # ================================================================ metrics
+    def metrics_text(self) -> str:
+        lines = []
+        with self.lock:
+            lines.append("# TYPE gpupool_device_healthy gauge")
+            for u, d in self.by_uuid.items():
+                lab = f'uuid="{u}",index="{d.get("index")}",node="{self.cfg.node}"'
+                v = self.verdicts.get(u, {})
+                lines.append(f"gpupool_device_healthy{{{lab}}} {1 if v.get('healthy') else 0}")
+                lines.append(f"gpupool_device_claimed{{{lab}}} {1 if u in self.records else 0}")
+                lines.append(f"gpupool_device_xgmi_links_up{{{lab}}} "
+                             f"{(d.get('xgmi') or {}).get('up', 0)}")
+                for t in ("correctable", "uncorrectable"):
+                    lines.append(f'gpupool_device_ecc_errors_total{{{lab},type="{t}"}} '
+                                 f"{(d.get('ecc') or {}).get(t, 0)}")
+                for s, t in (d.get("temps") or {}).items():
+                    if isinstance(t, dict) and t.get("current") is not None:
+                        lines.append(f'gpupool_device_temperature_celsius{{{lab},sensor="{s}"}} '
+                                     f"{t['current']}")
+            for k, v in self.stats.items():
+                lines.append(f"gpupool_agent_{k} {v}")
+            lines.append(f"gpupool_agent_gen {self.gen}")
+        return "\n".join(lines) + "\n"
+
+    # ================================================================ lifecycle
+    def start_background(self) -> None:
+        for res in {r.get("resourceName", schema.DEFAULT_RESOURCE) for r in self.records.values()}:
+            self._ensure_plugin(res)
+        t = threading.Thread(target=self._sampler, daemon=True, name="sampler")
+        t.start()
+        self._threads.append(t)
+        if self.cfg.apiserver:
+            self.register_node()
+            t = threading.Thread(target=self._heartbeater, daemon=True, name="heartbeat")
+            t.start()
+            self._threads.append(t)
+
+    def stop(self) -> None:
+        self._stop.set()
+        for p in list(self.plugins.values()):
+            p.stop()
+        self.prober.close()
+
+
+# ==================================================================== RPC server
+def build_app(agent: Agent) -> web.Application:
+    app = web.Application()
+    loop_holder: dict[str, Any] = {}
+
+    async def run_blocking(fn, *a):
+        return await asyncio.get_running_loop().run_in_executor(None, fn, *a)
+
+    async def node(request):
+        return web.json_response(await run_blocking(agent.node_view))
+
+    async def claims(request):
+        body = await request.json()
+        if not body.get("poolUID") or int(body.get("count", 0)) <= 0:
+            return web.json_response({"reason": "BadRequest", "message": "poolUID and count>0 "
+                                      "required"}, status=400)
+        return web.json_response(await run_blocking(agent.claim, body))
+
+    async def cordon(request):
+        b = await request.json()
+        return web.json_response(await run_blocking(agent.cordon, b["poolUID"], b.get("uuids", [])))
+
+    async def release(request):
+        b = await request.json()
+        out = await run_blocking(agent.release, b["poolUID"], b.get("uuids", []))
+        return web.json_response(out, status=200 if out.get("ok") else 409)
+
+    async def policy(request):
+        b = await request.json()
+        return web.json_response(await run_blocking(agent.update_policy, b["poolUID"],
+                                                    b.get("policy") or {}, b.get("resourceName")))
+
+    async def events(request):
+        since = int(request.query.get("since", "-1"))
+        timeout = float(request.query.get("timeoutSeconds", "30"))
+        gen, pools = agent.changed_since(since)
+        if gen == since:
+            loop = asyncio.get_running_loop()
+            fut = loop.create_future()
+            with agent.lock:
+                if agent.gen == since:
+                    agent.waiters.append((loop, fut))
+                else:
+                    fut.set_result(None)
+            try:
+                await asyncio.wait_for(fut, timeout)
+            except asyncio.TimeoutError:
+                pass
+            gen, pools = agent.changed_since(since)
+        return web.Response(text=json.dumps({"gen": gen, "pools": pools}) + "\n",
+                            content_type="application/json")
+
+    async def sample(request):
+        changed = await run_blocking(agent.sample)
+        return web.json_response({"changed": sorted(changed), "gen": agent.gen})
+
+    async def healthz(request):
+        return web.Response(text="ok\n")
+
+    async def metrics(request):
+        return web.Response(text=await run_blocking(agent.metrics_text), content_type="text/plain")
+
+    app.router.add_get("/v1/node", node)
+    app.router.add_post("/v1/claims", claims)
+    app.router.add_post("/v1/cordon", cordon)
+    app.router.add_post("/v1/release", release)
+    app.router.add_post("/v1/policy", policy)
+    app.router.add_get("/v1/events", events)
+    app.router.add_post("/v1/sample", sample)
+    app.router.add_get("/healthz", healthz)
+    app.router.add_get("/metrics", metrics)
+    app["loop_holder"] = loop_holder
+    return app
+
+
+async def serve(agent: Agent, ready_file: str | None = None) -> None:
+    app = build_app(agent)
+    runner = web.AppRunner(app, access_log=None)
+    await runner.setup()
+    if agent.cfg.socket:
+        try:
+            os.unlink(agent.cfg.socket)
+        except FileNotFoundError:
+            pass
+        os.makedirs(os.path.dirname(os.path.abspath(agent.cfg.socket)), exist_ok=True)
+        await web.UnixSite(runner, agent.cfg.socket).start()
+    if agent.cfg.listen:
+        host, port = agent.cfg.listen.rsplit(":", 1)
+        await web.TCPSite(runner, host or "0.0.0.0", int(port)).start()
+    agent.start_background()
+    if ready_file:
+        with open(ready_file + ".tmp", "w") as f:
+            json.dump({"node": agent.cfg.node, "endpoint": agent.endpoint(),
+                       "devices": len(agent.by_uuid), "probe": agent.probe_mode}, f)
+        os.replace(ready_file + ".tmp", ready_file)
+    print(f"gpupool-agent {agent.cfg.node} serving on {agent.endpoint()}", flush=True)
+    while True:
+        await asyncio.sleep(3600)

@@ -1,0 +1,184 @@
+"""ROCm device plugin (kubelet DevicePlugin v1beta1) — SURVEY B3.
+
+The reference installs NVIDIA's plugin and requests ``nvidia.com/gpu`` (GPU调度平台搭建.md:128-132,
+:665-667). Here each extended resource used by a pool (default ``amd.com/gpu``) gets one plugin
+endpoint ``<plugin_dir>/gpupool-<resource>.sock`` registered with the kubelet:
+
+* ListAndWatch streams the pool-claimed GPUs for that resource: Healthy iff claimed, not draining,
+  healthy under the owning pool's policy and probe-passed; a cordoned (draining) GPU turns
+  Unhealthy so the kubelet places no new pods on it. Every send records which devices were
+  advertised Healthy — the agent's ``advertised`` bit that readyReplicas requires.
+* Allocate returns /dev/kfd + /dev/dri/renderD<N> DeviceSpecs and ``ROCR_VISIBLE_DEVICES`` set to
+  the GPUs' ROCr UUIDs (``GPU-<serial>``), so a container sees exactly its GPUs.
+* GetPreferredAllocation picks xGMI/NUMA-close sets with libmi355x_dev's selector.
+* The kubelet socket is watched; a kubelet restart (new socket inode) triggers re-registration.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import logging
+import os
+import threading
+import time
+from typing import TYPE_CHECKING
+
+import grpc
+
+from .proto import API_VERSION, DP, KUBELET_SOCKET, Stub, service_handler, unix_target
+
+if TYPE_CHECKING:  # pragma: no cover
+    from ..agent import Agent
+
+log = logging.getLogger("gpupool.agent.deviceplugin")
+
+
+def socket_name(resource: str) -> str:
+    return "gpupool-" + resource.replace("/", "_").replace(".", "-") + ".sock"
+
+
+class DevicePluginServer:
+    def __init__(self, agent: "Agent", resource: str, plugin_dir: str):
+        self.agent = agent
+        self.resource = resource
+        self.plugin_dir = plugin_dir
+        self.sock = os.path.join(plugin_dir, socket_name(resource))
+        self.server: grpc.Server | None = None
+        self.version = 0
+        self.cv = threading.Condition()
+        self.stopped = False
+        self.streams = 0
+        self.registered = False
+        self._kubelet_ino = None
+        self._mon: threading.Thread | None = None
+
+    # ------------------------------------------------------------ lifecycle
+    def start(self) -> None:
+        try:
+            os.unlink(self.sock)
+        except FileNotFoundError:
+            pass
+        self.server = grpc.server(cf.ThreadPoolExecutor(max_workers=16,
+                                                        thread_name_prefix=f"dp-{self.resource}"))
+        self.server.add_generic_rpc_handlers((service_handler("v1beta1.DevicePlugin", {
+            "GetDevicePluginOptions": self.GetDevicePluginOptions,
+            "ListAndWatch": self.ListAndWatch,
+            "GetPreferredAllocation": self.GetPreferredAllocation,
+            "Allocate": self.Allocate,
+            "PreStartContainer": self.PreStartContainer,
+        }),))
+        self.server.add_insecure_port(unix_target(self.sock))
+        self.server.start()
+        self._mon = threading.Thread(target=self._monitor_kubelet, daemon=True,
+                                     name=f"dp-mon-{self.resource}")
+        self._mon.start()
+
+    def stop(self) -> None:
+        self.stopped = True
+        with self.cv:
+            self.cv.notify_all()
+        if self.server:
+            self.server.stop(grace=0.5)
+        try:
+            os.unlink(self.sock)
+        except FileNotFoundError:
+            pass
+
+    def register(self) -> bool:
+        ksock = os.path.join(self.plugin_dir, KUBELET_SOCKET)
+        if not os.path.exists(ksock):
+            return False
+        try:
+            with grpc.insecure_channel(unix_target(ksock)) as ch:
+                opts = DP.DevicePluginOptions(pre_start_required=False,
+                                              get_preferred_allocation_available=True)
+                Stub(ch, "v1beta1.Registration").Register(
+                    DP.RegisterRequest(version=API_VERSION, endpoint=os.path.basename(self.sock),
+                                       resource_name=self.resource, options=opts), timeout=5)
+            self.registered = True
+            self._kubelet_ino = os.stat(ksock).st_ino
+            log.info("registered %s with kubelet at %s", self.resource, ksock)
+            return True
+        except (grpc.RpcError, OSError) as e:
+            log.warning("register %s failed: %s", self.resource, e)
+            return False
+
+    def _monitor_kubelet(self) -> None:
+        ksock = os.path.join(self.plugin_dir, KUBELET_SOCKET)
+        while not self.stopped:
+            try:
+                ino = os.stat(ksock).st_ino
+            except FileNotFoundError:
+                ino = None
+            if ino is not None and ino != self._kubelet_ino:
+                self.register()
+            time.sleep(0.2 if not self.registered else 1.0)
+
+    def notify(self) -> None:
+        with self.cv:
+            self.version += 1
+            self.cv.notify_all()
+
+    # ------------------------------------------------------------ API
+    def GetDevicePluginOptions(self, request, context):
+        return DP.DevicePluginOptions(pre_start_required=False,
+                                      get_preferred_allocation_available=True)
+
+    def _devices_msg(self) -> tuple[DP.ListAndWatchResponse, set[str]]:
+        resp = DP.ListAndWatchResponse()
+        healthy = set()
+        for d in self.agent.plugin_devices(self.resource):
+            dev = resp.devices.add()
+            dev.ID = d["uuid"]
+            dev.health = "Healthy" if d["advertisable"] else "Unhealthy"
+            if d.get("numa") is not None:
+                dev.topology.nodes.add().ID = int(d["numa"])
+            if d["advertisable"]:
+                healthy.add(d["uuid"])
+        return resp, healthy
+
+    def ListAndWatch(self, request, context):
+        with self.cv:
+            self.streams += 1
+        try:
+            seen = -1
+            while not self.stopped and context.is_active():
+                with self.cv:
+                    if seen == self.version:
+                        self.cv.wait(timeout=1.0)
+                    if seen == self.version:
+                        continue
+                    seen = self.version
+                resp, healthy = self._devices_msg()
+                yield resp
+                self.agent.mark_advertised(self.resource, healthy)
+        finally:
+            with self.cv:
+                self.streams -= 1
+            self.agent.mark_advertised(self.resource, None)
+
+    def GetPreferredAllocation(self, request, context):
+        out = DP.PreferredAllocationResponse()
+        for creq in request.container_requests:
+            ids = self.agent.preferred(self.resource, list(creq.available_deviceIDs),
+                                       list(creq.must_include_deviceIDs), creq.allocation_size)
+            out.container_responses.add().deviceIDs.extend(ids)
+        return out
+
+    def Allocate(self, request, context):
+        out = DP.AllocateResponse()
+        for creq in request.container_requests:
+            try:
+                spec = self.agent.allocate_spec(self.resource, list(creq.devices_ids))
+            except ValueError as e:
+                context.abort(grpc.StatusCode.FAILED_PRECONDITION, str(e))
+            c = out.container_responses.add()
+            for k, v in spec["envs"].items():
+                c.envs[k] = v
+            for k, v in spec["annotations"].items():
+                c.annotations[k] = v
+            for dspec in spec["devices"]:
+                c.devices.add(container_path=dspec, host_path=dspec, permissions="rw")
+        return out
+
+    def PreStartContainer(self, request, context):
+        return DP.PreStartContainerResponse()

@@ -1,0 +1,111 @@
+"""Claim-time readiness probes (the MI355X replacement of `nvidia-smi` in a pod).
+
+Modes:
+  inproc     — libmi355x_probe.so loaded once in the agent; HIP contexts warmed at start so a
+               claim pays only the kernels (HBM pattern fill/verify + bf16 MFMA GEMM checks);
+               GPUs are probed concurrently (ctypes drops the GIL).
+  subprocess — `mi355x-probe --device N` per GPU: process isolation (a faulting probe cannot take
+               the agent down) at the cost of HIP initialisation per probe.
+  simulated  — for the fake backend on CPU-only hosts: a fixed latency and a result that fails
+               only when the fault overlay sets ``probeFail``. Never used with real GPUs.
+  off        — no probe (result passes with backend "off").
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import json
+import logging
+import os
+import subprocess
+import time
+
+from ..ops import native_path
+
+log = logging.getLogger("gpupool.agent.prober")
+
+
+class Prober:
+    def __init__(self, mode: str = "inproc", sim_ms: float = 20.0, gemm_n: int = 4096,
+                 max_workers: int = 16):
+        self.mode = mode
+        self.sim_ms = sim_ms
+        self.gemm_n = gemm_n
+        self.pool = cf.ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix="probe")
+        self.ordinals: dict[str, int] = {}
+        self.init_ms = 0.0
+        t0 = time.perf_counter()
+        if mode == "inproc":
+            from ..ops import probe as hip_probe
+            self._hip = hip_probe
+            n = hip_probe.init()
+            self.ordinals = hip_probe.hip_uuid_map()
+            log.info("HIP probe initialised: %d device(s) %s", n, sorted(self.ordinals))
+        elif mode == "subprocess":
+            out = subprocess.run([native_path("mi355x-probe"), "--list"], capture_output=True,
+                                 text=True, timeout=120)
+            for line in out.stdout.splitlines():
+                info = json.loads(line)
+                if info.get("hipUUID"):
+                    self.ordinals[info["hipUUID"].lower()] = int(info["device"])
+        elif mode not in ("simulated", "off"):
+            raise ValueError(f"unknown probe mode {mode!r}")
+        self.init_ms = (time.perf_counter() - t0) * 1e3
+
+    def _one(self, dev: dict, opts: dict) -> dict:
+        t0 = time.perf_counter()
+        hbm = int(opts.get("hbmBytes", 1 << 30))
+        mfma = bool(opts.get("mfma", True))
+        if self.mode == "off" or not opts.get("enabled", True):
+            return {"passed": True, "backend": "off", "ms": 0.0}
+        if self.mode == "simulated":
+            time.sleep(self.sim_ms / 1e3)
+            fail = bool((dev.get("faults") or {}).get("probeFail")) or bool(dev.get("probeFail"))
+            res = {"passed": not fail, "backend": "simulated",
+                   "hbm": {"ok": not fail, "GBps": 5400.0, "bytes": hbm},
+                   "mfma": {"ok": not fail, "tflops": 750.0, "enabled": mfma}}
+            if fail:
+                res["error"] = "injected probe failure (fault overlay)"
+            res["ms"] = (time.perf_counter() - t0) * 1e3
+            return res
+        ordinal = self.ordinals.get(str(dev.get("hipUUID", "")).lower())
+        if ordinal is None:
+            return {"passed": False, "backend": self.mode,
+                    "error": f"device {dev.get('hipUUID')} not visible to HIP in this process",
+                    "ms": 0.0}
+        if self.mode == "inproc":
+            res = self._hip.run(ordinal, hbm_bytes=hbm, mfma=mfma, gemm_n=self.gemm_n)
+        else:
+            cmd = [native_path("mi355x-probe"), "--device", str(ordinal), "--hbm-bytes", str(hbm),
+                   "--gemm-n", str(self.gemm_n)] + ([] if mfma else ["--no-mfma"])
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            try:
+                res = json.loads(p.stdout.strip().splitlines()[-1])
+            except (ValueError, IndexError):
+                res = {"passed": False, "error": f"probe exited {p.returncode}: {p.stderr[-300:]}"}
+        fault = (dev.get("faults") or {}).get("probeFail") or dev.get("probeFail")
+        if fault:  # fault overlay also applies on top of real hardware
+            res["passed"] = False
+            res["error"] = "injected probe failure (fault overlay)"
+        res["backend"] = self.mode
+        res.setdefault("ms", (time.perf_counter() - t0) * 1e3)
+        return res
+
+    def probe_many(self, devs: list[dict], opts: dict) -> list[dict]:
+        futs = [self.pool.submit(self._one, d, opts) for d in devs]
+        out = []
+        for f in futs:
+            try:
+                out.append(f.result())
+            except Exception as e:  # a probe must never take the agent down
+                out.append({"passed": False, "backend": self.mode, "error": repr(e), "ms": 0.0})
+        return out
+
+    def close(self) -> None:
+        self.pool.shutdown(wait=False)
+
+
+def default_mode(backend: str) -> str:
+    env = os.environ.get("GPUPOOL_PROBE_MODE")
+    if env:
+        return env
+    return "simulated" if backend == "fake" else "inproc"

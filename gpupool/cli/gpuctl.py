@@ -1,0 +1,448 @@
+"""gpuctl — the kubectl stand-in for the gpupool operator.
+
+  gpuctl apply -f FILE [--dry-run]        create-or-update every document (kubectl apply, README.md:288-290)
+  gpuctl get KIND [NAME] [-o wide|yaml|json] [-l SEL] [-A]   server-side printing (printer columns)
+  gpuctl describe KIND NAME               spec/status, conditions table, devices, events
+  gpuctl delete KIND NAME | -f FILE [--wait]
+  gpuctl scale KIND NAME --replicas N     via the scale subresource
+  gpuctl wait KIND NAME --for condition=Ready|delete|jsonpath=.status.readyReplicas=N [--timeout 60]
+  gpuctl logs POD                         fake-kubelet container log
+  gpuctl events [-n NS]
+  gpuctl devices NODE                     the node agent's live device view
+  gpuctl install [--crd-dir config/crd]   install CRDs (make install)
+  gpuctl render job -f TEMPLATE           GoHai train-job template -> Pod requesting amd.com/gpu
+  gpuctl config view | set-context NAME --server URL [--namespace NS] [--token T] | use-context NAME
+
+Connection: --server/--token/-n flags, else GPUPOOL_APISERVER/GPUPOOL_TOKEN, else the current
+context of ~/.config/gpupool/config.yaml (the GoHai CLI context schema, GPU调度平台搭建.md:461-472).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+from typing import Any
+
+import yaml
+
+from ..api import schema
+from ..kube import EVENTS, NODES, PODS, Client, KubeError, Res, res_for
+
+CONFIG_PATH = os.path.expanduser(os.environ.get("GPUPOOL_CONFIG", "~/.config/gpupool/config.yaml"))
+
+
+# ------------------------------------------------------------------ config / contexts
+def load_config() -> dict:
+    if os.path.exists(CONFIG_PATH):
+        with open(CONFIG_PATH) as f:
+            return yaml.safe_load(f) or {}
+    return {}
+
+
+def save_config(cfg: dict) -> None:
+    os.makedirs(os.path.dirname(CONFIG_PATH), exist_ok=True)
+    with open(CONFIG_PATH, "w") as f:
+        yaml.safe_dump(cfg, f, sort_keys=False)
+
+
+def connection(args) -> tuple[str, str | None, str]:
+    cfg = load_config()
+    ctx = (cfg.get("contexts") or {}).get(cfg.get("current-context", ""), {})
+    server = args.server or os.environ.get("GPUPOOL_APISERVER") or ctx.get("server") or \
+        "http://127.0.0.1:6443"
+    token = args.token or os.environ.get("GPUPOOL_TOKEN") or ctx.get("token")
+    ns = args.namespace or ctx.get("namespace") or "default"
+    return server, token, ns
+
+
+# ------------------------------------------------------------------ discovery
+def resolve(c: Client, name: str) -> Res:
+    n = name.lower()
+    for path in ["/api/v1"] + [f"/apis/{g['name']}/{g['preferredVersion']['version']}"
+                               for g in c.request("GET", "/apis").get("groups", [])]:
+        lst = c.request("GET", path)
+        gv = lst["groupVersion"]
+        g, v = gv.split("/", 1) if "/" in gv else ("", gv)
+        for r in lst["resources"]:
+            if "/" in r["name"]:
+                continue
+            names = {r["name"], r.get("singularName", ""), r["kind"].lower(),
+                     *r.get("shortNames", [])}
+            if n in names or n == f"{r['name']}.{g}":
+                return Res(g, v, r["name"], r["namespaced"])
+    raise SystemExit(f"error: the server doesn't have a resource type \"{name}\"")
+
+
+def load_docs(path: str) -> list[dict]:
+    paths = sorted(glob.glob(os.path.join(path, "*.y*ml"))) if os.path.isdir(path) else [path]
+    docs = []
+    for p in paths:
+        with (sys.stdin if p == "-" else open(p)) as f:
+            docs += [d for d in yaml.safe_load_all(f) if d]
+    return docs
+
+
+# ------------------------------------------------------------------ printing
+def print_table(tbl: dict, wide: bool = False, with_ns: bool = False) -> None:
+    cols = [cd["name"].upper() for cd in tbl["columnDefinitions"]]
+    rows = []
+    for r in tbl["rows"]:
+        cells = ["" if x is None else str(x) for x in r["cells"]]
+        if with_ns:
+            cells = [r["object"]["metadata"].get("namespace", "")] + cells
+        rows.append(cells)
+    if with_ns:
+        cols = ["NAMESPACE"] + cols
+    if not rows:
+        print("No resources found.")
+        return
+    widths = [max(len(cols[i]), *(len(r[i]) for r in rows)) for i in range(len(cols))]
+    print("   ".join(c.ljust(w) for c, w in zip(cols, widths)).rstrip())
+    for r in rows:
+        print("   ".join(c.ljust(w) for c, w in zip(r, widths)).rstrip())
+
+
+def dump(obj: Any, fmt: str) -> None:
+    if fmt == "json":
+        print(json.dumps(obj, indent=2))
+    else:
+        print(yaml.safe_dump(obj, sort_keys=False).rstrip())
+
+
+# ------------------------------------------------------------------ commands
+def cmd_apply(c: Client, ns: str, args) -> int:
+    rc = 0
+    for doc in load_docs(args.filename):
+        try:
+            action, out = c.apply(doc, ns, dry_run=args.dry_run)
+            suffix = " (dry run)" if args.dry_run else ""
+            print(f"{doc['kind'].lower()}.{res_for(doc).group or 'core'}/{doc['metadata']['name']} "
+                  f"{action}{suffix}")
+            if args.dry_run and args.output:
+                dump(out, args.output)
+        except KubeError as e:
+            print(f"error: {e}", file=sys.stderr)
+            rc = 1
+    return rc
+
+
+def cmd_get(c: Client, ns: str, args) -> int:
+    res = resolve(c, args.kind)
+    target_ns = None if (args.all_namespaces or not res.namespaced) else ns
+    if args.output in ("yaml", "json"):
+        out = c.get(res, args.name, target_ns) if args.name else \
+            c.list(res, target_ns, label_selector=args.selector)
+        dump(out, args.output)
+        return 0
+    tbl = c.table(res, target_ns, args.name, label_selector=args.selector)
+    print_table(tbl, wide=args.output == "wide", with_ns=args.all_namespaces and res.namespaced)
+    return 0
+
+
+def _events_for(c: Client, ns: str, uid: str) -> list[dict]:
+    evs = [e for e in c.list(EVENTS, ns)["items"] if e.get("involvedObject", {}).get("uid") == uid]
+    return sorted(evs, key=lambda e: e.get("lastTimestamp", ""))
+
+
+def cmd_describe(c: Client, ns: str, args) -> int:
+    res = resolve(c, args.kind)
+    obj = c.get(res, args.name, ns if res.namespaced else None)
+    md = obj["metadata"]
+    print(f"Name:         {md['name']}")
+    if res.namespaced:
+        print(f"Namespace:    {md.get('namespace')}")
+    print(f"Kind:         {obj['kind']}")
+    print(f"UID:          {md.get('uid')}")
+    print(f"Generation:   {md.get('generation')}")
+    if md.get("finalizers"):
+        print(f"Finalizers:   {', '.join(md['finalizers'])}")
+    if md.get("deletionTimestamp"):
+        print(f"Deleting:     since {md['deletionTimestamp']}")
+    for k in ("labels", "annotations"):
+        if md.get(k):
+            print(f"{k.capitalize()}:")
+            for kk, vv in md[k].items():
+                print(f"  {kk}={vv}")
+    if "spec" in obj:
+        print("Spec:")
+        print("  " + yaml.safe_dump(obj["spec"], sort_keys=False).rstrip().replace("\n", "\n  "))
+    st = dict(obj.get("status") or {})
+    conds = st.pop("conditions", [])
+    devs = st.pop("devices", None)
+    if st:
+        print("Status:")
+        print("  " + yaml.safe_dump(st, sort_keys=False).rstrip().replace("\n", "\n  "))
+    if devs:
+        print("Devices:")
+        print(f"  {'INDEX':<6}{'UUID':<42}{'HEALTH':<11}{'ADV':<5}{'PROBE':<28}PODS")
+        for d in devs:
+            p = d.get("probe") or {}
+            probe = (f"{'ok' if p.get('passed') else 'FAIL'} {p.get('hbmGBps', 0):.0f}GB/s "
+                     f"{p.get('mfmaTflops', 0):.0f}TF") if p else "-"
+            print(f"  {d.get('index', ''):<6}{d.get('hipUUID') or d['uuid']:<42}"
+                  f"{d.get('health', ''):<11}{'yes' if d.get('advertised') else 'no':<5}"
+                  f"{probe:<28}{','.join(d.get('pods', [])) or '-'}")
+            for r in d.get("reasons") or []:
+                print(f"        ! {r}")
+    if conds:
+        print("Conditions:")
+        print(f"  {'TYPE':<20}{'STATUS':<9}{'REASON':<24}MESSAGE")
+        for cd in conds:
+            print(f"  {cd['type']:<20}{cd['status']:<9}{cd.get('reason', ''):<24}{cd.get('message', '')}")
+    if res.namespaced:
+        evs = _events_for(c, md.get("namespace"), md.get("uid"))
+        print("Events:" + ("" if evs else "  <none>"))
+        for e in evs[-20:]:
+            print(f"  {e.get('type', ''):<8}{e.get('reason', ''):<20}x{e.get('count', 1):<4}"
+                  f"{e.get('message', '')}")
+    return 0
+
+
+def cmd_delete(c: Client, ns: str, args) -> int:
+    targets = []
+    if args.filename:
+        for d in load_docs(args.filename):
+            r = res_for(d)
+            targets.append((r, d["metadata"]["name"], d["metadata"].get("namespace") or ns))
+    else:
+        r = resolve(c, args.kind)
+        targets.append((r, args.name, ns))
+    for r, name, tns in targets:
+        try:
+            c.delete(r, name, tns if r.namespaced else None)
+            print(f"{r.plural}/{name} deleted")
+        except KubeError as e:
+            print(f"error: {e}", file=sys.stderr)
+            continue
+        if args.wait:
+            c.wait_for(r, name, tns if r.namespaced else None, lambda o: o is None,
+                       timeout=args.timeout)
+    return 0
+
+
+def cmd_scale(c: Client, ns: str, args) -> int:
+    res = resolve(c, args.kind)
+    cur = c.get(res, args.name, ns, sub="scale")
+    cur["spec"]["replicas"] = args.replicas
+    c.request("PUT", res.path(ns, args.name, "scale"), cur)
+    print(f"{res.plural}/{args.name} scaled")
+    return 0
+
+
+def parse_for(cond: str):
+    if cond == "delete":
+        return lambda o: o is None
+    if cond.startswith("condition="):
+        spec = cond.split("=", 1)[1]
+        ctype, _, want = spec.partition("=")
+        want = want or "True"
+        return lambda o: bool(o) and any(
+            x["type"] == ctype and x["status"] == want and
+            x.get("observedGeneration", o["metadata"].get("generation")) ==
+            o["metadata"].get("generation")
+            for x in (o.get("status") or {}).get("conditions", []))
+    if cond.startswith("jsonpath="):
+        path, _, want = cond.split("=", 1)[1].partition("=")
+
+        def pred(o):
+            cur: Any = o
+            for p in path.strip(".").split("."):
+                cur = cur.get(p) if isinstance(cur, dict) else None
+            return o is not None and str(cur) == want
+        return pred
+    raise SystemExit(f"error: unsupported --for {cond}")
+
+
+def cmd_wait(c: Client, ns: str, args) -> int:
+    res = resolve(c, args.kind)
+    t0 = time.monotonic()
+    try:
+        c.wait_for(res, args.name, ns if res.namespaced else None, parse_for(args.for_),
+                   timeout=args.timeout)
+    except TimeoutError:
+        print(f"error: timed out waiting for the condition on {res.plural}/{args.name}",
+              file=sys.stderr)
+        return 1
+    print(f"{res.plural}/{args.name} condition met ({time.monotonic() - t0:.3f}s)")
+    return 0
+
+
+def cmd_logs(c: Client, ns: str, args) -> int:
+    pod = c.get(PODS, args.pod, ns)
+    path = (pod["metadata"].get("annotations") or {}).get("gpupool.amd.com/log-path")
+    if not path or not os.path.exists(path):
+        print("error: no log available for this pod (fake kubelet log path unknown)", file=sys.stderr)
+        return 1
+    sys.stdout.write(open(path).read())
+    return 0
+
+
+def cmd_events(c: Client, ns: str, args) -> int:
+    print_table(c.table(EVENTS, None if args.all_namespaces else ns), with_ns=args.all_namespaces)
+    return 0
+
+
+def cmd_devices(c: Client, ns: str, args) -> int:
+    node = c.get(NODES, args.node)
+    ep = (node["metadata"].get("annotations") or {}).get(schema.ANN_AGENT_ENDPOINT)
+    if not ep:
+        print(f"error: node {args.node} has no gpupool agent", file=sys.stderr)
+        return 1
+    view = Client(ep).request("GET", "/v1/node")
+    if args.output in ("json", "yaml"):
+        dump(view, args.output)
+        return 0
+    print(f"node {view['node']}  backend {view['backend']}  probe {view.get('probeMode')}")
+    print(f"{'IDX':<4}{'HIP UUID':<24}{'BDF':<15}{'STATE':<12}{'HEALTHY':<8}{'POOL':<28}REASONS")
+    for d in sorted(view["devices"], key=lambda x: x.get("index", 0)):
+        print(f"{d.get('index', ''):<4}{d.get('hipUUID', ''):<24}{d.get('bdf', ''):<15}"
+              f"{d.get('state', ''):<12}{'yes' if d.get('healthy') else 'NO':<8}"
+              f"{d.get('pool', '') or '-':<28}{'; '.join((d.get('verdict') or {}).get('reasons', []))}")
+    return 0
+
+
+def cmd_install(c: Client, ns: str, args) -> int:
+    from ..kube import CRDS
+    for doc in load_docs(args.crd_dir):
+        action, _ = c.apply(doc)
+        print(f"customresourcedefinition.apiextensions.k8s.io/{doc['metadata']['name']} {action}")
+        c.wait_for(CRDS, doc["metadata"]["name"], None, lambda o: bool(o) and any(
+            x["type"] == "Established" and x["status"] == "True"
+            for x in (o.get("status") or {}).get("conditions", [])), timeout=30)
+    return 0
+
+
+def render_job(tpl: dict) -> dict:
+    """GoHai train-job template (GPU调度平台搭建.md:512-535) -> Pod requesting amd.com/gpu."""
+    spec = tpl.get("spec") or {}
+    inst = str(spec.get("singleInstanceType", "gpu-1x"))
+    gpus = 1
+    for part in inst.split("-"):
+        if part.endswith("gpu") and part[:-3].isdigit():
+            gpus = int(part[:-3])
+    env = [{"name": k, "value": str(v)} for k, v in (tpl.get("env") or {}).items()] \
+        if isinstance(tpl.get("env"), dict) else list(tpl.get("env") or [])
+    cmd = tpl.get("command") or "python train.py"
+    name = str(tpl.get("title", "trainjob")).lower().replace(" ", "-").replace("_", "-")
+    return {"apiVersion": "v1", "kind": "Pod",
+            "metadata": {"generateName": name + "-",
+                         "annotations": {"gpupool.amd.com/description": str(tpl.get("description", "")),
+                                         "gpupool.amd.com/mode": str(tpl.get("mode", "single")).lower()}},
+            "spec": {"restartPolicy": "OnFailure",
+                     "containers": [{"name": "train", "image": tpl.get("image", "rocm/pytorch:latest"),
+                                     "command": ["bash", "-lc", cmd], "env": env,
+                                     "resources": {"limits": {schema.DEFAULT_RESOURCE: gpus}}}]}}
+
+
+def cmd_render(c, ns, args) -> int:
+    for d in load_docs(args.filename):
+        dump(render_job(d), args.output or "yaml")
+    return 0
+
+
+def cmd_config(args) -> int:
+    cfg = load_config()
+    cfg.setdefault("contexts", {})
+    if args.config_cmd == "view":
+        print(yaml.safe_dump(cfg, sort_keys=False).rstrip() or "{}")
+    elif args.config_cmd == "set-context":
+        ctx = cfg["contexts"].setdefault(args.name, {})
+        for k in ("server", "namespace", "token"):
+            v = getattr(args, k)
+            if v:
+                ctx[k] = v
+        cfg.setdefault("current-context", args.name)
+        save_config(cfg)
+        print(f"context {args.name} set")
+    elif args.config_cmd == "use-context":
+        if args.name not in cfg["contexts"]:
+            print(f"error: no context {args.name}", file=sys.stderr)
+            return 1
+        cfg["current-context"] = args.name
+        save_config(cfg)
+        print(f"switched to context {args.name}")
+    return 0
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="gpuctl", description="kubectl-like CLI for gpupool")
+    ap.add_argument("--server", default=None)
+    ap.add_argument("--token", default=None)
+    ap.add_argument("-n", "--namespace", default=None)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    p = sub.add_parser("apply")
+    p.add_argument("-f", "--filename", required=True)
+    p.add_argument("--dry-run", action="store_true")
+    p.add_argument("-o", "--output", default=None)
+    p = sub.add_parser("get")
+    p.add_argument("kind")
+    p.add_argument("name", nargs="?")
+    p.add_argument("-o", "--output", default="")
+    p.add_argument("-l", "--selector", default=None)
+    p.add_argument("-A", "--all-namespaces", action="store_true")
+    p = sub.add_parser("describe")
+    p.add_argument("kind")
+    p.add_argument("name")
+    p = sub.add_parser("delete")
+    p.add_argument("kind", nargs="?")
+    p.add_argument("name", nargs="?")
+    p.add_argument("-f", "--filename", default=None)
+    p.add_argument("--wait", action="store_true")
+    p.add_argument("--timeout", type=float, default=120)
+    p = sub.add_parser("scale")
+    p.add_argument("kind")
+    p.add_argument("name")
+    p.add_argument("--replicas", type=int, required=True)
+    p = sub.add_parser("wait")
+    p.add_argument("kind")
+    p.add_argument("name")
+    p.add_argument("--for", dest="for_", required=True)
+    p.add_argument("--timeout", type=float, default=60)
+    p = sub.add_parser("logs")
+    p.add_argument("pod")
+    p = sub.add_parser("events")
+    p.add_argument("-A", "--all-namespaces", action="store_true")
+    p = sub.add_parser("devices")
+    p.add_argument("node")
+    p.add_argument("-o", "--output", default="")
+    p = sub.add_parser("install")
+    p.add_argument("--crd-dir", default=os.path.join(os.path.dirname(os.path.dirname(
+        os.path.dirname(os.path.abspath(__file__)))), "config", "crd"))
+    p = sub.add_parser("render")
+    p.add_argument("what", choices=["job"])
+    p.add_argument("-f", "--filename", required=True)
+    p.add_argument("-o", "--output", default=None)
+    p = sub.add_parser("config")
+    csub = p.add_subparsers(dest="config_cmd", required=True)
+    csub.add_parser("view")
+    sc = csub.add_parser("set-context")
+    sc.add_argument("name")
+    sc.add_argument("--server", dest="server", default=None)
+    sc.add_argument("--namespace", dest="namespace", default=None)
+    sc.add_argument("--token", dest="token", default=None)
+    uc = csub.add_parser("use-context")
+    uc.add_argument("name")
+    return ap
+
+
+def main(argv: list[str] | None = None) -> int:
+    args = build_parser().parse_args(argv)
+    if args.cmd == "config":
+        return cmd_config(args)
+    server, token, ns = connection(args)
+    c = Client(server, token)
+    fn = {"apply": cmd_apply, "get": cmd_get, "describe": cmd_describe, "delete": cmd_delete,
+          "scale": cmd_scale, "wait": cmd_wait, "logs": cmd_logs, "events": cmd_events,
+          "devices": cmd_devices, "install": cmd_install, "render": cmd_render}[args.cmd]
+    try:
+        return fn(c, ns, args)
+    except KubeError as e:
+        print(f"Error from server ({e.reason or e.code}): {e}", file=sys.stderr)
+        return 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,42 @@
+"""``python -m gpupool.kubelet_fake --node n0 --apiserver URL --root /tmp/kubelet``"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import signal
+import threading
+
+from .kubelet import FakeKubelet
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser(description="fake kubelet (device plugins + pod runtime)")
+    ap.add_argument("--node", required=True)
+    ap.add_argument("--apiserver", required=True)
+    ap.add_argument("--token", default=None)
+    ap.add_argument("--root", required=True, help="kubelet root dir (device-plugins/, pod-resources/)")
+    ap.add_argument("--workdir", default=os.getcwd(), help="cwd for pod processes")
+    ap.add_argument("--no-schedule", action="store_true")
+    ap.add_argument("--ready-file", default="")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    logging.basicConfig(level=logging.DEBUG if a.verbose else logging.INFO,
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    k = FakeKubelet(a.node, a.apiserver, os.path.join(a.root, "device-plugins"),
+                    os.path.join(a.root, "pod-resources", "kubelet.sock"), workdir=a.workdir,
+                    log_dir=os.path.join(a.root, "pod-logs"), token=a.token,
+                    schedule=not a.no_schedule)
+    k.start()
+    if a.ready_file:
+        with open(a.ready_file, "w") as f:
+            f.write("ok")
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    signal.signal(signal.SIGINT, lambda *_: stop.set())
+    stop.wait()
+    k.stop()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,470 @@
+"""Fake kubelet: the kubelet side of the device-plugin contract plus a minimal pod runtime.
+
+There is no kubelet/kind/docker in this environment, so device-plugin conformance
+and drain semantics are exercised against this process:
+
+* Registration gRPC server on ``<plugin_dir>/kubelet.sock``; on Register it dials the plugin's
+  endpoint and consumes ListAndWatch, keeping per-resource device health;
+* Node status: ``capacity``/``allocatable`` for every registered extended resource;
+* pod admission for pods bound to this node: picks device IDs (GetPreferredAllocation when the
+  plugin offers it), calls Allocate, then runs ``containers[0].command`` as a host process with the
+  returned env (ROCR_VISIBLE_DEVICES …) — i.e. the reference's `--gpus=1` smoke pod and the
+  training job (GPU调度平台搭建.md:134-138, :638-675) run for real on the allotted MI355X;
+* graceful termination: a pod with ``deletionTimestamp`` (delete or eviction) gets SIGTERM, then
+  SIGKILL after its grace period, its devices are freed, and the pod object is deleted;
+* PodResources v1 ``List`` / ``GetAllocatableResources`` for the node agent;
+* an optional scheduler loop binding unscheduled pods that fit this node's allocatable.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import datetime as _dt
+import logging
+import os
+import shlex
+import signal
+import subprocess
+import threading
+import time
+from dataclasses import dataclass, field
+
+import grpc
+
+from ..agent.deviceplugin.proto import (API_VERSION, DP, KUBELET_SOCKET, PR, Stub,
+                                        service_handler, unix_target)
+from ..api import schema
+from ..kube import NODES, PODS, Client, KubeError
+
+log = logging.getLogger("gpupool.kubelet")
+
+
+def now_rfc3339() -> str:
+    return _dt.datetime.now(_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+@dataclass
+class PluginConn:
+    resource: str
+    endpoint: str
+    options: object
+    devices: dict[str, str] = field(default_factory=dict)  # ID -> health
+    numa: dict[str, int] = field(default_factory=dict)
+    channel: grpc.Channel | None = None
+    stub: Stub | None = None
+    updates: int = 0
+
+
+@dataclass
+class RunningPod:
+    ns: str
+    name: str
+    uid: str
+    devices: dict[str, list[str]]  # resource -> device IDs
+    container: str
+    proc: subprocess.Popen | None = None
+    log_path: str = ""
+    restarts: int = 0
+    terminating: bool = False
+
+
+class FakeKubelet:
+    def __init__(self, node: str, apiserver: str, plugin_dir: str, pod_resources_socket: str,
+                 workdir: str | None = None, log_dir: str | None = None, token: str | None = None,
+                 schedule: bool = True, extra_env: dict | None = None):
+        self.node = node
+        self.client = Client(apiserver, token)
+        self.apiserver = apiserver
+        self.plugin_dir = plugin_dir
+        self.pr_socket = pod_resources_socket
+        self.workdir = workdir or os.getcwd()
+        self.log_dir = log_dir or os.path.join(plugin_dir, "..", "pod-logs")
+        self.schedule = schedule
+        self.extra_env = extra_env or {}
+        self.plugins: dict[str, PluginConn] = {}
+        self.pods: dict[str, RunningPod] = {}          # pod uid -> running pod
+        self.assigned: dict[str, str] = {}             # device ID -> pod uid
+        self.lock = threading.RLock()
+        self.stop_ev = threading.Event()
+        self.threads: list[threading.Thread] = []
+        self.reg_server: grpc.Server | None = None
+        self.pr_server: grpc.Server | None = None
+        os.makedirs(plugin_dir, exist_ok=True)
+        os.makedirs(os.path.dirname(os.path.abspath(pod_resources_socket)), exist_ok=True)
+        os.makedirs(self.log_dir, exist_ok=True)
+
+    # ============================================================ gRPC servers
+    def start(self) -> None:
+        ksock = os.path.join(self.plugin_dir, KUBELET_SOCKET)
+        for p in (ksock, self.pr_socket):
+            try:
+                os.unlink(p)
+            except FileNotFoundError:
+                pass
+        self.reg_server = grpc.server(cf.ThreadPoolExecutor(max_workers=8))
+        self.reg_server.add_generic_rpc_handlers((service_handler("v1beta1.Registration",
+                                                                  {"Register": self.Register}),))
+        self.reg_server.add_insecure_port(unix_target(ksock))
+        self.reg_server.start()
+        self.pr_server = grpc.server(cf.ThreadPoolExecutor(max_workers=8))
+        self.pr_server.add_generic_rpc_handlers((service_handler("v1.PodResourcesLister", {
+            "List": self.List, "GetAllocatableResources": self.GetAllocatableResources}),))
+        self.pr_server.add_insecure_port(unix_target(self.pr_socket))
+        self.pr_server.start()
+        self._ensure_node()
+        for fn, name in ((self._pod_loop, "pods"), (self._reaper, "reaper")):
+            t = threading.Thread(target=fn, daemon=True, name=name)
+            t.start()
+            self.threads.append(t)
+        if self.schedule:
+            t = threading.Thread(target=self._scheduler_loop, daemon=True, name="scheduler")
+            t.start()
+            self.threads.append(t)
+        log.info("fake kubelet %s up (plugins %s, podresources %s)", self.node, self.plugin_dir,
+                 self.pr_socket)
+
+    def stop(self) -> None:
+        self.stop_ev.set()
+        with self.lock:
+            for rp in self.pods.values():
+                self._kill(rp, 0)
+        if self.reg_server:
+            self.reg_server.stop(0.2)
+        if self.pr_server:
+            self.pr_server.stop(0.2)
+
+    def Register(self, request, context):
+        if request.version != API_VERSION:
+            context.abort(grpc.StatusCode.INVALID_ARGUMENT,
+                          f"unsupported device plugin API version {request.version}")
+        conn = PluginConn(resource=request.resource_name, endpoint=request.endpoint,
+                          options=request.options)
+        conn.channel = grpc.insecure_channel(unix_target(os.path.join(self.plugin_dir,
+                                                                      request.endpoint)))
+        conn.stub = Stub(conn.channel, "v1beta1.DevicePlugin")
+        with self.lock:
+            old = self.plugins.get(request.resource_name)
+            self.plugins[request.resource_name] = conn
+        if old and old.channel:
+            old.channel.close()
+        t = threading.Thread(target=self._list_and_watch, args=(conn,), daemon=True,
+                             name=f"lw-{request.resource_name}")
+        t.start()
+        log.info("plugin registered: %s at %s", request.resource_name, request.endpoint)
+        return DP.Empty()
+
+    def _list_and_watch(self, conn: PluginConn) -> None:
+        backoff = 0.05
+        while not self.stop_ev.is_set():
+            with self.lock:
+                if self.plugins.get(conn.resource) is not conn:
+                    return  # superseded by a re-registration
+            try:
+                for resp in conn.stub.ListAndWatch(DP.Empty()):
+                    with self.lock:
+                        conn.devices = {d.ID: d.health for d in resp.devices}
+                        conn.numa = {d.ID: (d.topology.nodes[0].ID if d.topology.nodes else 0)
+                                     for d in resp.devices}
+                        conn.updates += 1
+                    self._update_node_status()
+                    backoff = 0.05
+                    if self.stop_ev.is_set():
+                        return
+            except grpc.RpcError as e:
+                log.debug("ListAndWatch %s ended: %s", conn.resource, e.code())
+            time.sleep(backoff)
+            backoff = min(backoff * 2, 2.0)
+
+    def List(self, request, context):
+        resp = PR.ListPodResourcesResponse()
+        with self.lock:
+            for rp in self.pods.values():
+                pr = resp.pod_resources.add(name=rp.name, namespace=rp.ns)
+                c = pr.containers.add(name=rp.container)
+                for res, ids in rp.devices.items():
+                    c.devices.add(resource_name=res, device_ids=ids)
+        return resp
+
+    def GetAllocatableResources(self, request, context):
+        resp = PR.AllocatableResourcesResponse()
+        with self.lock:
+            for res, conn in self.plugins.items():
+                ids = [i for i, h in conn.devices.items() if h == "Healthy"]
+                resp.devices.add(resource_name=res, device_ids=ids)
+        return resp
+
+    # ============================================================ node
+    def _ensure_node(self) -> None:
+        try:
+            self.client.create(NODES, {"apiVersion": "v1", "kind": "Node",
+                                       "metadata": {"name": self.node,
+                                                    "labels": {"kubernetes.io/hostname": self.node}}})
+        except KubeError as e:
+            if e.code != 409:
+                raise
+        self._update_node_status()
+
+    def _update_node_status(self) -> None:
+        with self.lock:
+            cap = {r: str(len(c.devices)) for r, c in self.plugins.items()}
+            alloc = {r: str(sum(1 for h in c.devices.values() if h == "Healthy"))
+                     for r, c in self.plugins.items()}
+        try:
+            self.client.patch(NODES, self.node, {"status": {
+                "capacity": {"cpu": "64", "memory": "1Ti", "pods": "110", **cap},
+                "allocatable": {"cpu": "64", "memory": "1Ti", "pods": "110", **alloc}}},
+                sub="status")
+        except KubeError as e:
+            log.warning("node status patch failed: %s", e)
+
+    def allocatable(self) -> dict[str, list[str]]:
+        with self.lock:
+            return {r: [i for i, h in c.devices.items() if h == "Healthy" and i not in self.assigned]
+                    for r, c in self.plugins.items()}
+
+    # ============================================================ pods
+    def _pod_loop(self) -> None:
+        rv = None
+        while not self.stop_ev.is_set():
+            try:
+                if rv is None:
+                    lst = self.client.list(PODS, field_selector=f"spec.nodeName={self.node}")
+                    for p in lst["items"]:
+                        self._handle_pod(p)
+                    rv = lst["metadata"]["resourceVersion"]
+                for ev in self.client.watch(PODS, resource_version=rv,
+                                            field_selector=f"spec.nodeName={self.node}",
+                                            stop=self.stop_ev, timeout_seconds=60):
+                    if ev["type"] == "ERROR":
+                        rv = None
+                        break
+                    rv = ev["object"]["metadata"].get("resourceVersion", rv)
+                    if ev["type"] == "BOOKMARK":
+                        continue
+                    if ev["type"] == "DELETED":
+                        self._forget(ev["object"]["metadata"]["uid"])
+                    else:
+                        self._handle_pod(ev["object"])
+            except Exception as e:
+                if not self.stop_ev.is_set():
+                    log.warning("pod watch error: %s", e)
+                time.sleep(0.2)
+                rv = None
+
+    def _requests(self, pod: dict) -> dict[str, int]:
+        req: dict[str, int] = {}
+        for c in pod["spec"].get("containers", []):
+            lim = (c.get("resources") or {}).get("limits") or {}
+            for k, v in lim.items():
+                if "/" in k:
+                    req[k] = req.get(k, 0) + int(v)
+        return req
+
+    def _handle_pod(self, pod: dict) -> None:
+        md = pod["metadata"]
+        uid = md["uid"]
+        if md.get("deletionTimestamp"):
+            with self.lock:
+                rp = self.pods.get(uid)
+            if rp is None:
+                self._delete_pod(md["namespace"], md["name"], uid)
+                return
+            if not rp.terminating:
+                rp.terminating = True
+                grace = int(md.get("deletionGracePeriodSeconds",
+                                   pod["spec"].get("terminationGracePeriodSeconds", 30)))
+                threading.Thread(target=self._terminate, args=(rp, grace), daemon=True).start()
+            return
+        phase = pod.get("status", {}).get("phase", "Pending")
+        with self.lock:
+            known = uid in self.pods
+        if known or phase in ("Succeeded", "Failed"):
+            return
+        self._admit(pod)
+
+    def _admit(self, pod: dict) -> None:
+        md = pod["metadata"]
+        ns, name, uid = md["namespace"], md["name"], md["uid"]
+        reqs = self._requests(pod)
+        devices: dict[str, list[str]] = {}
+        envs: dict[str, str] = {}
+        with self.lock:
+            for res, n in reqs.items():
+                conn = self.plugins.get(res)
+                avail = [i for i, h in (conn.devices.items() if conn else []) if h == "Healthy"
+                         and i not in self.assigned]
+                if conn is None or len(avail) < n:
+                    self._fail(pod, f"OutOf{res}", f"Node didn't have enough resource: {res}, "
+                               f"requested: {n}, available: {len(avail)}")
+                    return
+                ids = avail[:n]
+                if conn.options.get_preferred_allocation_available:
+                    try:
+                        pref = conn.stub.GetPreferredAllocation(DP.PreferredAllocationRequest(
+                            container_requests=[{"available_deviceIDs": avail,
+                                                 "allocation_size": n}]), timeout=5)
+                        got = list(pref.container_responses[0].deviceIDs)
+                        if len(got) == n and all(g in avail for g in got):
+                            ids = got
+                    except grpc.RpcError as e:
+                        log.warning("GetPreferredAllocation failed: %s", e)
+                try:
+                    resp = conn.stub.Allocate(DP.AllocateRequest(
+                        container_requests=[{"devices_ids": ids}]), timeout=10)
+                except grpc.RpcError as e:
+                    self._fail(pod, "UnexpectedAdmissionError", f"Allocate failed: {e.details()}")
+                    return
+                cr = resp.container_responses[0]
+                envs.update(dict(cr.envs))
+                for i in ids:
+                    self.assigned[i] = uid
+                devices[res] = ids
+            container = (pod["spec"].get("containers") or [{"name": "main"}])[0]
+            rp = RunningPod(ns, name, uid, devices, container.get("name", "main"))
+            self.pods[uid] = rp
+        self._start_process(rp, pod, envs)
+
+    def _start_process(self, rp: RunningPod, pod: dict, envs: dict[str, str]) -> None:
+        container = (pod["spec"].get("containers") or [{}])[0]
+        cmd = list(container.get("command") or []) + list(container.get("args") or [])
+        if not cmd:
+            cmd = ["sleep", "infinity"]  # a "pause" container: holds its GPUs until deleted
+        env = dict(os.environ)
+        env.update(self.extra_env)
+        for e in container.get("env") or []:
+            if "value" in e:
+                env[e["name"]] = str(e["value"])
+        env.update(envs)
+        env["POD_NAME"], env["POD_NAMESPACE"] = rp.name, rp.ns
+        rp.log_path = os.path.join(self.log_dir, f"{rp.ns}_{rp.name}.log")
+        logf = open(rp.log_path, "ab")
+        try:
+            rp.proc = subprocess.Popen(cmd, cwd=self.workdir, env=env, stdout=logf,
+                                       stderr=subprocess.STDOUT, start_new_session=True)
+        except OSError as e:
+            logf.close()
+            self._fail(pod, "RunContainerError", str(e))
+            with self.lock:
+                self._free(rp)
+            return
+        logf.close()
+        log.info("started pod %s/%s pid %d devices %s", rp.ns, rp.name, rp.proc.pid, rp.devices)
+        try:  # `gpuctl logs` finds the container log through this annotation
+            self.client.patch(PODS, rp.name, {"metadata": {"annotations": {
+                "gpupool.amd.com/log-path": rp.log_path,
+                schema.ANN_POD_DEVICES: ",".join(i for ids in rp.devices.values() for i in ids)}}},
+                ns=rp.ns)
+        except KubeError:
+            pass
+        self._set_status(rp.ns, rp.name, "Running", ready=True, extra={
+            "podIP": "127.0.0.1", "hostIP": "127.0.0.1", "startTime": now_rfc3339()})
+
+    def _reaper(self) -> None:
+        while not self.stop_ev.wait(0.1):
+            with self.lock:
+                pods = list(self.pods.values())
+            for rp in pods:
+                if rp.proc is None or rp.terminating:
+                    continue
+                rc = rp.proc.poll()
+                if rc is None:
+                    continue
+                phase = "Succeeded" if rc == 0 else "Failed"
+                with self.lock:
+                    self._free(rp)
+                    self.pods.pop(rp.uid, None)
+                self._set_status(rp.ns, rp.name, phase, ready=False, exit_code=rc)
+                log.info("pod %s/%s exited %d", rp.ns, rp.name, rc)
+
+    def _terminate(self, rp: RunningPod, grace: int) -> None:
+        self._kill(rp, grace)
+        with self.lock:
+            self._free(rp)
+            self.pods.pop(rp.uid, None)
+        self._delete_pod(rp.ns, rp.name, rp.uid)
+
+    def _kill(self, rp: RunningPod, grace: int) -> None:
+        if rp.proc is None or rp.proc.poll() is not None:
+            return
+        try:
+            os.killpg(rp.proc.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            return
+        try:
+            rp.proc.wait(timeout=max(grace, 0.05))
+        except subprocess.TimeoutExpired:
+            try:
+                os.killpg(rp.proc.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            rp.proc.wait(timeout=10)
+
+    def _free(self, rp: RunningPod) -> None:
+        for ids in rp.devices.values():
+            for i in ids:
+                if self.assigned.get(i) == rp.uid:
+                    del self.assigned[i]
+
+    def _forget(self, uid: str) -> None:
+        with self.lock:
+            rp = self.pods.pop(uid, None)
+            if rp:
+                self._kill(rp, 0)
+                self._free(rp)
+
+    def _delete_pod(self, ns: str, name: str, uid: str) -> None:
+        try:
+            self.client.delete(PODS, name, ns, grace=0, preconditions={"uid": uid})
+        except KubeError as e:
+            if e.code not in (404, 409):
+                log.warning("final pod delete failed: %s", e)
+
+    def _fail(self, pod: dict, reason: str, msg: str) -> None:
+        md = pod["metadata"]
+        log.warning("pod %s/%s rejected: %s", md["namespace"], md["name"], msg)
+        self._set_status(md["namespace"], md["name"], "Failed", ready=False,
+                         extra={"reason": reason, "message": msg})
+
+    def _set_status(self, ns: str, name: str, phase: str, ready: bool, exit_code: int | None = None,
+                    extra: dict | None = None) -> None:
+        st: dict = {"phase": phase, "conditions": [
+            {"type": "Ready", "status": "True" if ready else "False",
+             "lastTransitionTime": now_rfc3339()}]}
+        cs = {"name": "main", "ready": ready, "restartCount": 0}
+        if exit_code is not None:
+            cs["state"] = {"terminated": {"exitCode": exit_code, "finishedAt": now_rfc3339()}}
+        else:
+            cs["state"] = {"running": {"startedAt": now_rfc3339()}}
+        st["containerStatuses"] = [cs]
+        st.update(extra or {})
+        try:
+            self.client.patch(PODS, name, {"status": st}, ns=ns, sub="status")
+        except KubeError as e:
+            if e.code != 404:
+                log.warning("pod status patch failed: %s", e)
+
+    # ============================================================ scheduler
+    def _scheduler_loop(self) -> None:
+        while not self.stop_ev.wait(0.05):
+            try:
+                pending = self.client.list(PODS, field_selector="spec.nodeName=")["items"]
+            except Exception:
+                continue
+            for pod in pending:
+                if pod["metadata"].get("deletionTimestamp"):
+                    continue
+                if pod.get("status", {}).get("phase", "Pending") != "Pending":
+                    continue
+                sel = pod["spec"].get("nodeSelector") or {}
+                if sel.get("kubernetes.io/hostname", self.node) != self.node:
+                    continue
+                free = self.allocatable()
+                if all(len(free.get(r, [])) >= n for r, n in self._requests(pod).items()):
+                    pod["spec"]["nodeName"] = self.node
+                    try:
+                        self.client.update(PODS, pod, pod["metadata"]["namespace"])
+                    except KubeError:
+                        pass  # another kubelet bound it first (409) or it is gone
+
+
+def pod_command(cmdline: str) -> list[str]:
+    return shlex.split(cmdline)

@@ -1,0 +1,78 @@
+"""ctypes binding for libmi355x_probe.so — the gfx950 HIP readiness probe (probe.hip).
+
+``init()`` warms every HIP context once (done by the long-lived node agent at start-up), so a
+claim-time ``run()`` pays only its kernels. ``run()`` releases the GIL (ctypes does), so probes of
+different GPUs run concurrently from a thread pool.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import threading
+
+from . import native_path
+
+_lib = None
+_lock = threading.Lock()
+_count: int | None = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    with _lock:
+        if _lib is None:
+            l = ctypes.CDLL(native_path("libmi355x_probe.so"))
+            l.mi355x_probe_init.restype = ctypes.c_int
+            l.mi355x_probe_init.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+            l.mi355x_probe_device_count.restype = ctypes.c_int
+            l.mi355x_probe_identify.restype = ctypes.c_void_p
+            l.mi355x_probe_identify.argtypes = [ctypes.c_int]
+            l.mi355x_probe_run.restype = ctypes.c_void_p
+            l.mi355x_probe_run.argtypes = [ctypes.c_int, ctypes.c_char_p]
+            l.mi355x_probe_free.argtypes = [ctypes.c_void_p]
+            _lib = l
+    return _lib
+
+
+def _take(p) -> dict:
+    if not p:
+        raise RuntimeError("libmi355x_probe returned NULL")
+    try:
+        return json.loads(ctypes.string_at(p).decode())
+    finally:
+        lib().mi355x_probe_free(p)
+
+
+def init() -> int:
+    """Initialise HIP + warm all visible devices. Returns the HIP device count."""
+    global _count
+    if _count is not None:
+        return _count
+    err = ctypes.create_string_buffer(512)
+    n = lib().mi355x_probe_init(err, len(err))
+    if n < 0:
+        raise RuntimeError(f"HIP probe init failed: {err.value.decode()}")
+    _count = n
+    return n
+
+
+def identify(dev: int) -> dict:
+    return _take(lib().mi355x_probe_identify(dev))
+
+
+def run(dev: int, hbm_bytes: int = 1 << 30, mfma: bool = True, gemm_n: int = 4096,
+        patterns: int = 2, gemm_reps: int = 3) -> dict:
+    opts = json.dumps({"hbmBytes": int(hbm_bytes), "mfma": bool(mfma), "gemmN": int(gemm_n),
+                       "patterns": int(patterns), "gemmReps": int(gemm_reps)})
+    return _take(lib().mi355x_probe_run(dev, opts.encode()))
+
+
+def hip_uuid_map() -> dict[str, int]:
+    """hipUUID ("GPU-<serial>") -> HIP ordinal for every visible device."""
+    n = init()
+    out = {}
+    for d in range(n):
+        info = identify(d)
+        if info.get("hipUUID"):
+            out[info["hipUUID"].lower()] = d
+    return out

@@ -1,0 +1,226 @@
+"""Local control plane launcher: apiserver-sim + gpupool-manager + N node agents (+ fake kubelets).
+
+The envtest/kind stand-in used by the integration tests, ``bench.py`` and ``make run``. Every
+component runs as its own process (own session, so teardown kills whole process groups); logs go
+to ``<workdir>/*.log``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+from dataclasses import dataclass, field
+
+from ..kube import Client
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+FIXTURE = os.path.join(ROOT, "tests", "fixtures", "node_8x_mi355x.json")
+
+
+def native_bin(name: str) -> str:
+    d = os.environ.get("GPUPOOL_NATIVE_DIR") or os.path.join(ROOT, "build", "native")
+    p = os.path.join(d, name)
+    if not os.path.exists(p):
+        raise FileNotFoundError(f"{p} missing: run `make native`")
+    return p
+
+
+def _wait_file(path: str, timeout: float, proc: subprocess.Popen | None = None,
+               logpath: str | None = None) -> str:
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if os.path.exists(path):
+            with open(path) as f:
+                data = f.read()
+            if data:
+                return data
+        if proc is not None and proc.poll() is not None:
+            tail = open(logpath).read()[-3000:] if logpath and os.path.exists(logpath) else ""
+            raise RuntimeError(f"process exited ({proc.returncode}) before {path}:\n{tail}")
+        time.sleep(0.02)
+    tail = open(logpath).read()[-3000:] if logpath and os.path.exists(logpath) else ""
+    raise TimeoutError(f"timed out waiting for {path}\n{tail}")
+
+
+@dataclass
+class NodeSpec:
+    name: str
+    backend: str = "fake"
+    fixture: str = FIXTURE
+    count: int = -1
+    probe: str = ""               # "" -> agent default (simulated for fake, inproc for real)
+    kubelet: bool = True
+    extra_args: list[str] = field(default_factory=list)
+
+
+class Cluster:
+    def __init__(self, workdir: str, nodes: list[NodeSpec] | None = None,
+                 manager_args: list[str] | None = None, manager: bool = True,
+                 python: str = sys.executable, env: dict | None = None,
+                 sample_interval: float = 0.5, kinds: str = "mi355x,azure"):
+        self.workdir = os.path.abspath(workdir)
+        os.makedirs(self.workdir, exist_ok=True)
+        # unix socket paths are limited to 107 bytes: keep every socket under a short /tmp dir
+        import tempfile
+        self.sockdir = tempfile.mkdtemp(prefix="gp", dir="/tmp")
+        self.nodes = nodes if nodes is not None else [NodeSpec("mi355x-node-0")]
+        self.manager_args = manager_args or []
+        self.want_manager = manager
+        self.python = python
+        self.env = dict(os.environ)
+        self.env.setdefault("PYTHONPATH", ROOT)
+        self.env["PYTHONPATH"] = ROOT + os.pathsep + self.env.get("PYTHONPATH", "")
+        self.env.update(env or {})
+        self.sample_interval = sample_interval
+        self.kinds = kinds
+        self.procs: dict[str, subprocess.Popen] = {}
+        self.url = ""
+        self.client: Client | None = None
+
+    # ------------------------------------------------------------ process helpers
+    def _spawn(self, key: str, argv: list[str]) -> subprocess.Popen:
+        logpath = os.path.join(self.workdir, f"{key}.log")
+        logf = open(logpath, "ab")
+        p = subprocess.Popen(argv, cwd=ROOT, env=self.env, stdout=logf, stderr=subprocess.STDOUT,
+                             start_new_session=True)
+        logf.close()
+        self.procs[key] = p
+        return p
+
+    def _kill(self, key: str, sig=signal.SIGTERM, timeout: float = 10.0) -> None:
+        p = self.procs.pop(key, None)
+        if p is None or p.poll() is not None:
+            return
+        try:
+            os.killpg(p.pid, sig)
+        except ProcessLookupError:
+            return
+        try:
+            p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait(timeout=5)
+
+    def log(self, key: str) -> str:
+        p = os.path.join(self.workdir, f"{key}.log")
+        return open(p).read() if os.path.exists(p) else ""
+
+    # ------------------------------------------------------------ components
+    def start_apiserver(self) -> None:
+        pf = os.path.join(self.workdir, "apiserver.port")
+        if os.path.exists(pf):
+            os.remove(pf)
+        p = self._spawn("apiserver", [self.python, "-m", "gpupool.apiserver_sim", "--port", "0",
+                                      "--port-file", pf, "--crd-dir",
+                                      os.path.join(ROOT, "config", "crd"),
+                                      "--bookmark-interval", "2"])
+        port = int(_wait_file(pf, 60, p, os.path.join(self.workdir, "apiserver.log")))
+        self.url = f"http://127.0.0.1:{port}"
+        self.client = Client(self.url)
+
+    def kubelet_root(self, node: NodeSpec) -> str:
+        return os.path.join(self.sockdir, f"k-{node.name}")
+
+    def start_kubelet(self, node: NodeSpec) -> None:
+        root = self.kubelet_root(node)
+        rf = os.path.join(self.workdir, f"kubelet-{node.name}.ready")
+        if os.path.exists(rf):
+            os.remove(rf)
+        p = self._spawn(f"kubelet-{node.name}", [self.python, "-m", "gpupool.kubelet_fake",
+                                                 "--node", node.name, "--apiserver", self.url,
+                                                 "--root", root, "--workdir", ROOT,
+                                                 "--ready-file", rf])
+        _wait_file(rf, 60, p, os.path.join(self.workdir, f"kubelet-{node.name}.log"))
+
+    def faults_path(self, node: str) -> str:
+        return os.path.join(self.workdir, f"faults-{node}.json")
+
+    def agent_socket(self, node: str) -> str:
+        return os.path.join(self.sockdir, f"a-{node}.sock")
+
+    def start_agent(self, node: NodeSpec) -> None:
+        rf = os.path.join(self.workdir, f"agent-{node.name}.ready")
+        if os.path.exists(rf):
+            os.remove(rf)
+        argv = [self.python, "-m", "gpupool.agent", "--node", node.name, "--backend", node.backend,
+                "--state-dir", os.path.join(self.workdir, f"state-{node.name}"),
+                "--socket", self.agent_socket(node.name), "--apiserver", self.url,
+                "--faults", self.faults_path(node.name), "--ready-file", rf,
+                "--sample-interval", str(self.sample_interval), "--no-fsync"]
+        if node.backend == "fake":
+            argv += ["--fixture", node.fixture]
+        if node.count >= 0:
+            argv += ["--count", str(node.count)]
+        if node.probe:
+            argv += ["--probe", node.probe]
+        if node.kubelet:
+            root = self.kubelet_root(node)
+            argv += ["--plugin-dir", os.path.join(root, "device-plugins"),
+                     "--pod-resources", os.path.join(root, "pod-resources", "kubelet.sock")]
+        argv += node.extra_args
+        wrap = os.environ.get("GPUPOOL_AGENT_WRAP", "")  # e.g. "rocprofv3 --kernel-trace --stats -d D --"
+        if wrap:
+            import shlex
+            argv = shlex.split(wrap) + argv
+        p = self._spawn(f"agent-{node.name}", argv)
+        _wait_file(rf, 300, p, os.path.join(self.workdir, f"agent-{node.name}.log"))
+
+    def start_manager(self) -> None:
+        pf = os.path.join(self.workdir, "manager.port")
+        if os.path.exists(pf):
+            os.remove(pf)
+        argv = [native_bin("gpupool-manager"), "--apiserver", self.url, "--port-file", pf,
+                "--kinds", self.kinds, "--progress-poll", "100ms"] + self.manager_args
+        p = self._spawn("manager", argv)
+        self.metrics_port = int(_wait_file(pf, 60, p, os.path.join(self.workdir, "manager.log")))
+
+    def start(self) -> "Cluster":
+        self.start_apiserver()
+        for n in self.nodes:
+            if n.kubelet:
+                self.start_kubelet(n)
+            self.start_agent(n)
+        if self.want_manager:
+            self.start_manager()
+        return self
+
+    def stop(self) -> None:
+        for key in [k for k in self.procs if k == "manager"] + \
+                   [k for k in self.procs if k.startswith("agent")] + \
+                   [k for k in self.procs if k.startswith("kubelet")] + list(self.procs):
+            self._kill(key)
+        import shutil
+        shutil.rmtree(self.sockdir, ignore_errors=True)
+
+    def __enter__(self) -> "Cluster":
+        return self.start()
+
+    def __exit__(self, *exc) -> None:
+        self.stop()
+
+    # ------------------------------------------------------------ fault injection
+    def set_faults(self, node: str, faults: dict, sample: bool = True) -> None:
+        path = self.faults_path(node)
+        with open(path + ".tmp", "w") as f:
+            json.dump(faults, f)
+        os.replace(path + ".tmp", path)
+        # make sure the mtime changes even within one filesystem tick
+        st = os.stat(path)
+        os.utime(path, ns=(st.st_atime_ns, st.st_mtime_ns + 1000))
+        if sample:
+            self.agent_request(node, "POST", "/v1/sample", {})
+
+    def agent_request(self, node: str, method: str, path: str, body: dict | None = None) -> dict:
+        c = Client("unix://" + self.agent_socket(node))
+        return c.request(method, path, body)
+
+    def manager_metrics(self) -> str:
+        import urllib.request
+        with urllib.request.urlopen(f"http://127.0.0.1:{self.metrics_port}/metrics", timeout=5) as r:
+            return r.read().decode()

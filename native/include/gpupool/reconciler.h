@@ -62,6 +62,7 @@ class PoolReconcilerBase {
   Json ensure_finalizer_(const Json& obj);
   Json remove_finalizer_(const Json& obj);
   void event_(const Json& obj, const std::string& type, const std::string& reason, const std::string& msg);
+  void note_generation_(const ObjectMeta& m);  // starts the reconcile-to-Ready clock
   void observe_ready_(const ObjectMeta& m, bool ready, int64_t desired);
   void forget_(const std::string& uid);
 

@@ -109,15 +109,18 @@ void PoolReconcilerBase::event_(const Json& obj, const std::string& type, const 
   if (events_ && opts_.emit_events) events_->record(obj, type, reason, msg);
 }
 
+void PoolReconcilerBase::note_generation_(const ObjectMeta& m) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pending_.find(m.uid);
+  if (it == pending_.end() || it->second.first != m.generation) pending_[m.uid] = {m.generation, clock_t_::now()};
+}
+
 void PoolReconcilerBase::observe_ready_(const ObjectMeta& m, bool ready, int64_t desired) {
   Labels l{{"kind", kind_}, {"pool", m.key()}};
   desired_gauge().set(l, static_cast<double>(desired));
+  note_generation_(m);
   std::lock_guard<std::mutex> g(mu_);
   auto it = pending_.find(m.uid);
-  if (it == pending_.end() || it->second.first != m.generation) {
-    pending_[m.uid] = {m.generation, clock_t_::now()};
-    it = pending_.find(m.uid);
-  }
   if (ready && ready_gen_[m.uid] != m.generation) {
     ready_gen_[m.uid] = m.generation;
     double s = std::chrono::duration<double>(clock_t_::now() - it->second.second).count();
@@ -412,6 +415,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     return Outcome::terminal("invalid spec: " + join(errs, "; "));
   }
   Mi355xPoolSpec spec = Mi355xPoolSpec::from(obj["spec"]);
+  note_generation_(m);
   if (m.deleting()) return finalize_(obj, m, spec);
   if (!m.has_finalizer(gen::kFinalizer)) {
     obj = ensure_finalizer_(obj);
@@ -538,6 +542,18 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     progress_reason = "Draining";
     progress_msg = std::to_string(still) + " GPU(s) waiting for pods to terminate";
   }
+  {
+    // Converged within this pass (claimed, probed, advertised, nothing draining): report Stable now
+    // instead of leaving Progressing=True until the next resync.
+    int64_t ready_now = 0, active_now = 0;
+    bool inflight = false;
+    for (const auto& d : o.mine) {
+      if (d.state == "Draining" || d.state == "Probing") inflight = true;
+      else ++active_now;
+      if (d.state == "Claimed" && d.healthy && d.probe_passed && d.advertised) ++ready_now;
+    }
+    if (!inflight && !insufficient && ready_now == spec.replicas && active_now == spec.replicas) progress_reason.clear();
+  }
   Json status = build_status_(obj, m, spec, o, progress_reason, progress_msg, insufficient, false);
   write_status_(obj, status);
   int64_t ready = status["readyReplicas"].as_int(0);
@@ -637,6 +653,7 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
     return Outcome::terminal("invalid spec");
   }
   AzureVmPoolSpec spec = AzureVmPoolSpec::from(obj["spec"]);
+  note_generation_(m);
   const std::string owner = m.ns + "-" + m.name;  // README.md:238 owner tag
   Credentials creds;
   std::string why;

@@ -1,0 +1,49 @@
+"""Shared pytest setup.
+
+Markers:
+  gpu   — needs a real MI355X (run by the driver on the GPU box with ``-m gpu``);
+  slow  — multi-second integration/property runs (still part of the default CPU suite).
+The native artefacts (build/native) are built once per session with ``make -C native``.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: requires a real MI355X GPU (gfx950)")
+    config.addinivalue_line("markers", "slow: multi-second integration test")
+
+
+@pytest.fixture(scope="session")
+def native_built():
+    """Build the native targets (host-only unless hipcc is present) once per session."""
+    target = "all" if os.path.exists("/opt/rocm/bin/hipcc") else "host"
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "native"), target, "-j8"],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.fail("native build failed:\n" + r.stdout[-4000:] + r.stderr[-4000:])
+    return os.path.join(ROOT, "build", "native")
+
+
+@pytest.fixture
+def cluster_factory(tmp_path, native_built):
+    """Start local control planes; all are stopped at test teardown."""
+    from gpupool.testing.cluster import Cluster
+    made = []
+
+    def make(**kw):
+        c = Cluster(str(tmp_path / f"cluster{len(made)}"), **kw)
+        made.append(c)
+        c.start()
+        return c
+    yield make
+    for c in made:
+        c.stop()

@@ -1,0 +1,215 @@
+"""apiserver-sim semantics (SURVEY.md §4.2 'Python unit' row; §7.3 hard part 1)."""
+from __future__ import annotations
+
+import copy
+import glob
+import os
+
+import pytest
+import yaml
+
+from gpupool.apiserver_sim.store import ApiError, Store, json_patch, merge_patch, \
+    parse_label_selector
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+@pytest.fixture
+def store():
+    s = Store(window=100)
+    crd_rt = s.types[("apiextensions.k8s.io", "customresourcedefinitions")]
+    for p in sorted(glob.glob(os.path.join(ROOT, "config", "crd", "*.yaml"))):
+        s.create(crd_rt, None, yaml.safe_load(open(p)))
+    return s
+
+
+def pool(name="p", replicas=1, **spec):
+    return {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xPool",
+            "metadata": {"name": name}, "spec": {"replicas": replicas, **spec}}
+
+
+def mi(s):
+    return s.lookup("compute.my.domain", "mi355xpools")
+
+
+def test_rv_strictly_increasing_and_generation(store):
+    rt = mi(store)
+    a = store.create(rt, "default", pool("a"))
+    b = store.create(rt, "default", pool("b"))
+    assert int(b["metadata"]["resourceVersion"]) > int(a["metadata"]["resourceVersion"])
+    assert a["metadata"]["generation"] == 1
+    a["spec"]["replicas"] = 3
+    a2 = store.update(rt, "default", "a", a)
+    assert a2["metadata"]["generation"] == 2
+    # metadata-only change: no generation bump
+    a2["metadata"]["labels"] = {"x": "y"}
+    a3 = store.update(rt, "default", "a", a2)
+    assert a3["metadata"]["generation"] == 2
+    assert int(a3["metadata"]["resourceVersion"]) > int(a2["metadata"]["resourceVersion"])
+
+
+def test_stale_update_conflicts(store):
+    rt = mi(store)
+    a = store.create(rt, "default", pool("a"))
+    fresh = copy.deepcopy(a)
+    fresh["spec"]["replicas"] = 2
+    store.update(rt, "default", "a", fresh)
+    a["spec"]["replicas"] = 5
+    with pytest.raises(ApiError) as e:
+        store.update(rt, "default", "a", a)
+    assert e.value.code == 409
+
+
+def test_noop_update_keeps_rv(store):
+    rt = mi(store)
+    a = store.create(rt, "default", pool("a"))
+    b = store.update(rt, "default", "a", copy.deepcopy(a))
+    assert b["metadata"]["resourceVersion"] == a["metadata"]["resourceVersion"]
+
+
+def test_status_subresource_isolation(store):
+    rt = mi(store)
+    a = store.create(rt, "default", {**pool("a"), "status": {"readyReplicas": 9}})
+    assert "status" not in a  # status not settable on create
+    a["status"] = {"readyReplicas": 1}
+    a["spec"]["replicas"] = 7
+    b = store.update(rt, "default", "a", a, subresource="status")
+    assert b["status"]["readyReplicas"] == 1
+    assert b["spec"]["replicas"] == 1  # spec change via /status ignored
+    assert b["metadata"]["generation"] == 1
+    b["status"] = {"readyReplicas": 42}
+    c = store.update(rt, "default", "a", b)  # status change via main resource ignored
+    assert c["status"]["readyReplicas"] == 1
+
+
+def test_validation_and_defaulting(store):
+    rt = mi(store)
+    with pytest.raises(ApiError) as e:
+        store.create(rt, "default", pool("neg", replicas=-1))
+    assert e.value.code == 422 and "spec.replicas" in e.value.message
+    with pytest.raises(ApiError):
+        store.create(rt, "default", pool("bad", resourceName="NOT VALID"))
+    a = store.create(rt, "default", pool("d", unknownField=1))
+    assert "unknownField" not in a["spec"]  # pruned
+    assert a["spec"]["resourceName"] == "amd.com/gpu"
+    assert a["spec"]["probe"]["hbmBytes"] == 1 << 30
+    assert a["spec"]["health"]["maxUncorrectableECC"] == 0
+
+
+def test_azure_required_fields(store):
+    rt = store.lookup("compute.my.domain", "azurevmpools")
+    doc = yaml.safe_load(open(os.path.join(ROOT, "config", "samples",
+                                           "compute_v1alpha1_azurevmpool.yaml")))
+    store.create(rt, "default", doc)
+    del doc["spec"]["vmSize"]
+    doc["metadata"]["name"] = "x"
+    with pytest.raises(ApiError) as e:
+        store.create(rt, "default", doc)
+    assert "vmSize" in e.value.message
+
+
+def test_finalizer_two_phase_delete(store):
+    rt = mi(store)
+    a = store.create(rt, "default", {**pool("a"), "metadata": {"name": "a",
+                                                              "finalizers": ["x/y"]}})
+    d = store.delete(rt, "default", "a")
+    assert d["metadata"]["deletionTimestamp"]
+    assert d["metadata"]["generation"] == 2
+    cur = store.get(rt, "default", "a")
+    cur["metadata"]["finalizers"] = ["x/y", "new/one"]
+    with pytest.raises(ApiError):
+        store.update(rt, "default", "a", cur)  # no new finalizers while deleting
+    cur["metadata"]["finalizers"] = []
+    store.update(rt, "default", "a", cur)
+    with pytest.raises(ApiError) as e:
+        store.get(rt, "default", "a")
+    assert e.value.code == 404
+    assert a["metadata"]["uid"]
+
+
+def test_pod_graceful_delete_and_eviction(store):
+    pods = store.types[("", "pods")]
+    store.create(pods, "default", {"metadata": {"name": "p"}, "spec": {
+        "nodeName": "n0", "containers": [{"name": "c"}]}})
+    store.evict("default", "p", {"deleteOptions": {"gracePeriodSeconds": 5}})
+    p = store.get(pods, "default", "p")
+    assert p["metadata"]["deletionTimestamp"] and p["metadata"]["deletionGracePeriodSeconds"] == 5
+    store.delete(pods, "default", "p", grace=0)
+    with pytest.raises(ApiError):
+        store.get(pods, "default", "p")
+    # unbound pods go away immediately
+    store.create(pods, "default", {"metadata": {"name": "q"}, "spec": {"containers": [{}]}})
+    store.delete(pods, "default", "q")
+    with pytest.raises(ApiError):
+        store.get(pods, "default", "q")
+
+
+def test_watch_window_compaction(store):
+    rt = mi(store)
+    store.create(rt, "default", pool("a"))
+    first = store.rv
+    for i in range(150):
+        store.create(rt, "default", pool(f"x{i}"))
+    with pytest.raises(ApiError) as e:
+        store.events_since(rt, first - 1)
+    assert e.value.code == 410
+    evs = store.events_since(rt, store.rv - 3)
+    assert len(evs) == 3
+
+
+def test_scale_subresource(store):
+    rt = mi(store)
+    store.create(rt, "default", pool("a", replicas=1))
+    sc = store.get_scale(rt, "default", "a")
+    assert sc["spec"]["replicas"] == 1
+    sc["spec"]["replicas"] = 4
+    out = store.update_scale(rt, "default", "a", sc)
+    assert out["spec"]["replicas"] == 4
+    assert store.get(rt, "default", "a")["metadata"]["generation"] == 2
+
+
+def test_owner_gc_and_namespace_cascade(store):
+    rt = mi(store)
+    ev = store.types[("", "events")]
+    a = store.create(rt, "team", pool("a"))
+    store.create(ev, "team", {"metadata": {"name": "e1", "ownerReferences": [
+        {"uid": a["metadata"]["uid"], "kind": "Mi355xPool", "name": "a"}]}})
+    store.delete(rt, "team", "a")
+    with pytest.raises(ApiError):
+        store.get(ev, "team", "e1")
+    store.create(ev, "team", {"metadata": {"name": "e2"}})
+    store.delete(store.types[("", "namespaces")], None, "team")
+    assert store.list(ev, "team")["items"] == []
+
+
+def test_secret_string_data_and_selectors(store):
+    sec = store.types[("", "secrets")]
+    s = store.create(sec, "default", {"metadata": {"name": "s", "labels": {"a": "1"}},
+                                      "stringData": {"K": "v"}})
+    assert s["data"]["K"] == "dg=="
+    assert parse_label_selector("a=1,b!=2")({"a": "1"})
+    assert not parse_label_selector("a in (2,3)")({"a": "1"})
+    assert parse_label_selector("!c,a")({"a": "x"})
+    assert len(store.list(sec, "default", label_selector="a=1")["items"]) == 1
+    assert store.list(sec, "default", field_selector="metadata.name=zz")["items"] == []
+
+
+def test_patches():
+    assert merge_patch({"a": {"b": 1, "c": 2}}, {"a": {"b": None, "d": 3}}) == {"a": {"c": 2, "d": 3}}
+    doc = {"a": [1, 2], "b": {"c": 1}}
+    out = json_patch(doc, [{"op": "add", "path": "/a/-", "value": 3},
+                           {"op": "replace", "path": "/b/c", "value": 5},
+                           {"op": "test", "path": "/b/c", "value": 5},
+                           {"op": "move", "from": "/b/c", "path": "/z"}])
+    assert out == {"a": [1, 2, 3], "b": {}, "z": 5}
+    with pytest.raises(ApiError):
+        json_patch(doc, [{"op": "test", "path": "/a/0", "value": 9}])
+
+
+def test_crd_deletion_removes_instances(store):
+    rt = mi(store)
+    store.create(rt, "default", pool("a"))
+    crd_rt = store.types[("apiextensions.k8s.io", "customresourcedefinitions")]
+    store.delete(crd_rt, None, "mi355xpools.compute.my.domain")
+    with pytest.raises(ApiError):
+        store.lookup("compute.my.domain", "mi355xpools")
