@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""FashionMNIST CNN training job (ROCm version of the reference's train.py,
+GPU调度平台搭建.md:557-636): same model, SGD lr 0.01, CrossEntropy, argparse flags
+(--epochs --batch_size --lr --data_dir --mode), auto mode from PET_NNODES / WORLD_SIZE /
+device count, checkpoint to --output.
+
+Differences by design: the distributed mode is real DDP over RCCL (the reference's is a stub);
+without FashionMNIST idx files (no network here) it trains on synthetic FMNIST-shaped data;
+``--steps`` caps iterations for smoke runs. Run inside a pool pod: the device plugin sets
+ROCR_VISIBLE_DEVICES so ``cuda:0`` is the allotted MI355X.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+from torch import nn  # noqa: E402
+
+from gpupool.models.fmnist import get_model, load_fmnist, synthetic_fmnist  # noqa: E402
+from gpupool.parallel import ddp  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=5)
+    ap.add_argument("--batch_size", type=int, default=128)
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--data_dir", default="/dataset")
+    ap.add_argument("--mode", default="auto", choices=["auto", "single", "distributed"])
+    ap.add_argument("--output", default=os.environ.get("GPUPOOL_OUTPUT", "/tmp/fmnist_out"))
+    ap.add_argument("--synthetic", action="store_true", help="force synthetic data")
+    ap.add_argument("--samples", type=int, default=8192, help="synthetic dataset size")
+    ap.add_argument("--steps", type=int, default=0, help="stop after N steps (0 = full epochs)")
+    ap.add_argument("--cpu", action="store_true")
+    a = ap.parse_args()
+
+    mode = a.mode
+    if mode == "auto":  # GPU调度平台搭建.md:623-630
+        nnodes = int(os.environ.get("PET_NNODES", "1"))
+        mode = "distributed" if nnodes > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1 else "single"
+    env = ddp.init_from_env(prefer_gpu=not a.cpu) if mode == "distributed" else \
+        ddp.DistEnv(0, 1, 0, torch.device("cuda:0" if torch.cuda.is_available() and not a.cpu
+                                           else "cpu"), "none")
+    ds = None if a.synthetic else load_fmnist(a.data_dir, train=True)
+    data_kind = "fashion-mnist" if ds is not None else "synthetic"
+    if ds is None:
+        ds = synthetic_fmnist(a.samples)
+    smp = ddp.sampler(ds, env)
+    loader = torch.utils.data.DataLoader(ds, batch_size=a.batch_size, shuffle=smp is None,
+                                         sampler=smp, drop_last=True)
+    model = ddp.wrap(get_model(), env)
+    opt = torch.optim.SGD(model.parameters(), lr=a.lr)
+    loss_fn = nn.CrossEntropyLoss()
+    info = {"rank": env.rank, "world": env.world, "device": str(env.device), "mode": mode,
+            "data": data_kind, "rocr_visible": os.environ.get("ROCR_VISIBLE_DEVICES", "")}
+    if env.device.type == "cuda":
+        p = torch.cuda.get_device_properties(env.device)
+        info.update({"gpu": p.name, "arch": getattr(p, "gcnArchName", "")})
+    print(json.dumps({"event": "start", **info}), flush=True)
+    step, t0, first_loss, loss_v = 0, time.time(), None, float("nan")
+    for epoch in range(a.epochs):
+        if smp is not None:
+            smp.set_epoch(epoch)
+        model.train()
+        for x, y in loader:
+            x, y = x.to(env.device, non_blocking=True), y.to(env.device, non_blocking=True)
+            opt.zero_grad(set_to_none=True)
+            loss = loss_fn(model(x), y)
+            loss.backward()
+            opt.step()
+            step += 1
+            if step % 20 == 0 or step == 1:
+                loss_v = ddp.all_reduce_mean(float(loss.item()), env)
+                first_loss = loss_v if first_loss is None else first_loss
+                if env.is_main:
+                    print(json.dumps({"event": "step", "epoch": epoch, "step": step,
+                                      "loss": round(loss_v, 4)}), flush=True)
+            if a.steps and step >= a.steps:
+                break
+        if a.steps and step >= a.steps:
+            break
+    loss_v = ddp.all_reduce_mean(float(loss.item()), env)
+    if env.device.type == "cuda":
+        torch.cuda.synchronize()
+    if env.is_main:
+        os.makedirs(a.output, exist_ok=True)
+        state = (model.module if hasattr(model, "module") else model).state_dict()
+        torch.save(state, os.path.join(a.output, "fashion_mnist_cnn.pth"))  # GPU调度平台搭建.md:603
+        print(json.dumps({"event": "done", "steps": step, "first_loss": first_loss,
+                          "final_loss": round(loss_v, 4), "seconds": round(time.time() - t0, 3),
+                          **info}), flush=True)
+    ddp.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -61,9 +61,12 @@ def identify(dev: int) -> dict:
 
 
 def run(dev: int, hbm_bytes: int = 1 << 30, mfma: bool = True, gemm_n: int = 4096,
-        patterns: int = 2, gemm_reps: int = 3) -> dict:
+        patterns: int = 2, gemm_reps: int = 3, **test_hooks: int) -> dict:
+    """Probe HIP device ``dev``. ``test_hooks``: injectBitFlips=N / injectGemmFault=1 corrupt the
+    device buffers between compute and check so tests can prove the checkers catch faults."""
     opts = json.dumps({"hbmBytes": int(hbm_bytes), "mfma": bool(mfma), "gemmN": int(gemm_n),
-                       "patterns": int(patterns), "gemmReps": int(gemm_reps)})
+                       "patterns": int(patterns), "gemmReps": int(gemm_reps),
+                       **{k: int(v) for k, v in test_hooks.items()}})
     return _take(lib().mi355x_probe_run(dev, opts.encode()))
 
 

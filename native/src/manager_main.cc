@@ -60,6 +60,9 @@ struct Flags {
   int fakecloud_provision_ms = 0;
   int fakecloud_deprovision_ms = 0;
   int orphan_sweep_ms = 30000;
+  int lease_duration_ms = 15000;
+  int renew_deadline_ms = 10000;
+  int retry_period_ms = 2000;
   std::string log_level = "info";
   std::string validate;
 };
@@ -113,6 +116,9 @@ Flags parse(int argc, char** argv) {
     else if (is("--fakecloud-provision-ms")) f.fakecloud_provision_ms = std::stoi(val());
     else if (is("--fakecloud-deprovision-ms")) f.fakecloud_deprovision_ms = std::stoi(val());
     else if (is("--orphan-sweep")) f.orphan_sweep_ms = parse_duration_ms(val());
+    else if (is("--lease-duration")) f.lease_duration_ms = parse_duration_ms(val());
+    else if (is("--renew-deadline")) f.renew_deadline_ms = parse_duration_ms(val());
+    else if (is("--retry-period")) f.retry_period_ms = parse_duration_ms(val());
     else if (is("--log-level")) f.log_level = val();
     else if (is("--validate")) f.validate = val();
     else if (a == "-h" || a == "--help") {
@@ -386,6 +392,9 @@ int main(int argc, char** argv) {
       LeaderConfig lc;
       lc.ns = f.lease_ns;
       lc.identity = f.identity;
+      lc.lease_duration = std::chrono::milliseconds(f.lease_duration_ms);
+      lc.renew_deadline = std::chrono::milliseconds(f.renew_deadline_ms);
+      lc.retry_period = std::chrono::milliseconds(f.retry_period_ms);
       LeaderElector le(client, lc);
       le.run([&] { leading = true; },
              [&] {

@@ -323,6 +323,15 @@ __global__ __launch_bounds__(256) void rowdot(const T* __restrict__ X, int rows,
   if (lane == 0) out[row] = static_cast<unsigned long long>(s);
 }
 
+// ---- fault injection (test hooks: prove the checkers catch corruption on real hardware)
+// Flips bit (i % 32) of word i*stride for i < count: distinct words, so exactly ``count`` bits.
+__global__ void inject_bit_flips(unsigned int* __restrict__ p, uint64_t nwords, int count) {
+  const uint64_t stride = nwords / static_cast<uint64_t>(count + 1);
+  for (int i = threadIdx.x; i < count; i += blockDim.x) p[static_cast<uint64_t>(i + 1) * stride] ^= 1u << (i % 32);
+}
+
+__global__ void inject_gemm_fault(float* __restrict__ c, int64_t idx) { c[idx] += 1.0f; }
+
 __global__ void count_ne_u64(const unsigned long long* __restrict__ a, const unsigned long long* __restrict__ b,
                              int n, unsigned long long* __restrict__ bad) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -410,6 +419,8 @@ std::string run_probe(int dev, const char* opts) {
   int gemm_n = static_cast<int>(opt_int(opts, "gemmN", 4096));
   gemm_n = std::max(256, (gemm_n / 256) * 256);
   const int patterns = static_cast<int>(std::max(1LL, opt_int(opts, "patterns", 2)));
+  const int inject_flips = static_cast<int>(std::min(4096LL, std::max(0LL, opt_int(opts, "injectBitFlips", 0))));
+  const bool inject_gemm = opt_int(opts, "injectGemmFault", 0) != 0;
   auto t0 = std::chrono::steady_clock::now();
   PROBE_CHECK(hipSetDevice(dev));
   DeviceCtx& ctx = g_ctx[static_cast<size_t>(dev)];
@@ -447,6 +458,9 @@ std::string run_probe(int dev, const char* opts) {
     hipLaunchKernelGGL(hbm_fill, dim3(hbm_grid), dim3(kHbmThreads), 0, s, static_cast<u32x4*>(buf.p), n16, seed, flip);
     PROBE_CHECK(hipGetLastError());
     PROBE_CHECK(hipEventRecord(ctx.ev[1], s));
+    if (pi == 0 && inject_flips > 0)
+      hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, static_cast<unsigned int*>(buf.p), n16 * 4,
+                         inject_flips);
     hipLaunchKernelGGL(hbm_verify, dim3(hbm_grid), dim3(kHbmThreads), 0, s, static_cast<const u32x4*>(buf.p), n16,
                        seed, flip, cnt, cnt + 1);
     PROBE_CHECK(hipGetLastError());
@@ -515,6 +529,9 @@ std::string run_probe(int dev, const char* opts) {
                          static_cast<const short*>(b.p), static_cast<float*>(c.p), n, n, n);
     PROBE_CHECK(hipEventRecord(ctx.ev[1], s));
     PROBE_CHECK(hipGetLastError());
+    if (inject_gemm)
+      hipLaunchKernelGGL(inject_gemm_fault, dim3(1), dim3(1), 0, s, static_cast<float*>(c.p),
+                         static_cast<int64_t>(n / 3) * n + n / 5);
     // ABFT checksums: 6 int64 vectors [acol | bcol | colsumC | expCol | rowsumC | expRow]
     auto* v = static_cast<unsigned long long*>(acol.p);
     unsigned long long *vacol = v, *vbcol = v + n, *vcolC = v + 2 * n, *vexpC = v + 3 * n, *vrowC = v + 4 * n,

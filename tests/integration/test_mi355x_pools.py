@@ -1,0 +1,241 @@
+"""Mi355xPool end-to-end on the 8x MI355X fake node (BASELINE configs 3, 4, 5 and the failure
+paths): apiserver-sim + C++ manager + node agent + ROCm device plugin + fake kubelet."""
+from __future__ import annotations
+
+import time
+
+import pytest
+
+from gpupool.kube import EVENTS, MI355XPOOLS, NODES, PODS, KubeError
+from gpupool.testing.cluster import NodeSpec
+
+from .helpers import cond_is, conds, mi_pool, pause_pod, ready_at, wait_ready
+
+pytestmark = pytest.mark.slow
+
+
+@pytest.fixture
+def node8(cluster_factory):
+    return cluster_factory()
+
+
+def agent_view(c, node="mi355x-node-0"):
+    return c.agent_request(node, "GET", "/v1/node")
+
+
+def test_config3_scale_up_1_to_8(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 1), "default")
+    wait_ready(k, "p", 1)
+    seen = set()
+    for r in (2, 4, 8):
+        t0 = time.perf_counter()
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": r}}, "default")
+        o = wait_ready(k, "p", r)
+        assert time.perf_counter() - t0 < 30
+        uuids = [d["uuid"] for d in o["status"]["devices"]]
+        assert len(set(uuids)) == r and seen <= set(uuids)  # scale-up keeps existing GPUs
+        seen = set(uuids)
+        node = k.get(NODES, "mi355x-node-0")
+        assert node["status"]["allocatable"]["amd.com/gpu"] == str(r)
+    view = agent_view(node8)
+    assert sum(1 for d in view["devices"] if d.get("poolUID")) == 8
+    assert conds(o)["Progressing"]["reason"] == "Stable"
+
+
+def test_all_or_nothing_insufficient(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("big", 9), "default")
+    o = k.wait_for(MI355XPOOLS, "big", "default",
+                   cond_is("Progressing", "False", "InsufficientDevices"), timeout=20)
+    assert o["status"]["readyReplicas"] == 0
+    assert all(not d.get("poolUID") for d in agent_view(node8)["devices"])  # nothing claimed
+    k.patch(MI355XPOOLS, "big", {"spec": {"replicas": 8}}, "default")
+    wait_ready(k, "big", 8)
+
+
+def test_config4_scale_down_8_to_4_with_drain(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 8, drain={"gracePeriodSeconds": 1}), "default")
+    o = wait_ready(k, "p", 8)
+    for i in range(8):
+        k.create(PODS, pause_pod(f"w{i}"), "default")
+    for i in range(8):
+        k.wait_for(PODS, f"w{i}", "default", lambda o: o and o["status"].get("phase") == "Running",
+                   timeout=30)
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 4}}, "default")
+    o = wait_ready(k, "p", 4, timeout=60)
+    kept = {d["uuid"] for d in o["status"]["devices"]}
+    assert [d["index"] for d in o["status"]["devices"]] == [0, 1, 2, 3]  # highest indices drained
+    pods = k.list(PODS, "default")["items"]
+    assert len(pods) == 4  # exactly the pods on released GPUs were evicted
+    for p in pods:
+        assert p["metadata"]["annotations"]["gpupool.amd.com/devices"] in kept
+    view = agent_view(node8)
+    for d in view["devices"]:
+        if d["uuid"] not in kept:
+            assert d["state"] == "Free" and not d["pods"]  # no pod left on a released GPU
+    reasons = {e["reason"] for e in k.list(EVENTS, "default")["items"]}
+    assert {"DrainStarted", "PodEvicted", "GPUReleased"} <= reasons
+    # finalizer-guarded delete: pods evicted, GPUs released, then the CR disappears
+    k.delete(MI355XPOOLS, "p", "default")
+    k.wait_for(MI355XPOOLS, "p", "default", lambda o: o is None, timeout=60)
+    assert k.list(PODS, "default")["items"] == []
+    assert all(d["state"] == "Free" for d in agent_view(node8)["devices"])
+
+
+def test_config5_two_pools_with_health_conditions(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("team-a", 4, resourceName="amd.com/gpu-team-a",
+                                  replacePolicy="Keep"), "default")
+    k.create(MI355XPOOLS, mi_pool("team-b", 4, resourceName="amd.com/gpu-team-b"), "default")
+    a = wait_ready(k, "team-a", 4)
+    b = wait_ready(k, "team-b", 4)
+    ua = {d["uuid"] for d in a["status"]["devices"]}
+    ub = {d["uuid"] for d in b["status"]["devices"]}
+    assert not ua & ub  # no cross-pool claims
+    alloc = k.get(NODES, "mi355x-node-0")["status"]["allocatable"]
+    assert alloc["amd.com/gpu-team-a"] == "4" and alloc["amd.com/gpu-team-b"] == "4"
+    victim = sorted(a["status"]["devices"], key=lambda d: d["index"])[0]["uuid"]
+    # xGMI link down on one team-a GPU
+    node8.set_faults("mi355x-node-0", {"devices": {victim: {"xgmi": {
+        "links": ["X", "U", "D", "U", "U", "U", "U", "U"]}}}})
+    a = k.wait_for(MI355XPOOLS, "team-a", "default", cond_is("XGMILinksHealthy", "False",
+                                                            "XGMILinkDown"), timeout=20)
+    assert conds(a)["Degraded"]["status"] == "True" and a["status"]["readyReplicas"] == 3
+    assert conds(k.get(MI355XPOOLS, "team-b", "default"))["XGMILinksHealthy"]["status"] == "True"
+    # HBM ECC + thermal on the same GPU
+    node8.set_faults("mi355x-node-0", {"devices": {victim: {
+        "ecc": {"uncorrectable": 2}, "temps": {"hotspot": {"current": 104}}}}})
+    a = k.wait_for(MI355XPOOLS, "team-a", "default",
+                   lambda o: cond_is("HBMECCHealthy", "False")(o) and
+                   cond_is("ThermalHealthy", "False")(o) and
+                   cond_is("XGMILinksHealthy", "True")(o), timeout=20)
+    dev = next(d for d in a["status"]["devices"] if d["uuid"] == victim)
+    assert dev["health"] == "Unhealthy" and any("HBMUncorrectableECC" in r for r in dev["reasons"])
+    node8.set_faults("mi355x-node-0", {})
+    wait_ready(k, "team-a", 4)
+    # device plugin: the unhealthy GPU was advertised Unhealthy while faulted -> now healthy again
+    assert k.get(NODES, "mi355x-node-0")["status"]["allocatable"]["amd.com/gpu-team-a"] == "4"
+
+
+def test_replace_on_failure(cluster_factory):
+    c = cluster_factory(nodes=[NodeSpec("mi355x-node-0")])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    o = wait_ready(k, "p", 2)
+    bad = o["status"]["devices"][0]["uuid"]
+    c.set_faults("mi355x-node-0", {"devices": {bad: {"ecc": {"uncorrectable": 5}}}})
+
+    def replaced(o):
+        u = {d["uuid"] for d in (o or {}).get("status", {}).get("devices", [])}
+        return ready_at(2)(o) and bad not in u
+    k.wait_for(MI355XPOOLS, "p", "default", replaced, timeout=30)
+    view = c.agent_request("mi355x-node-0", "GET", "/v1/node")
+    assert next(d for d in view["devices"] if d["uuid"] == bad)["state"] == "Quarantined"
+
+
+def test_probe_failure_replaced(cluster_factory):
+    c = cluster_factory(nodes=[NodeSpec("mi355x-node-0")])
+    k = c.client
+    # the first two GPUs (NUMA-packed choice) fail their probe
+    c.set_faults("mi355x-node-0", {"devices": {"0": {"probeFail": True}, "1": {"probeFail": True}}})
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    o = wait_ready(k, "p", 2, timeout=30)
+    assert {d["index"] for d in o["status"]["devices"]}.isdisjoint({0, 1})
+    reasons = {e["reason"] for e in k.list(EVENTS, "default")["items"]}
+    assert "HealthDegraded" in reasons
+
+
+def test_manager_restart_readopts_claims(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 3), "default")
+    before = wait_ready(k, "p", 3)
+    node8._kill("manager")
+    node8.start_manager()
+    time.sleep(0.5)
+    after = wait_ready(k, "p", 3)
+    assert [d["uuid"] for d in after["status"]["devices"]] == \
+        [d["uuid"] for d in before["status"]["devices"]]
+
+
+def test_agent_restart_keeps_ledger(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    before = wait_ready(k, "p", 2)
+    node8._kill("agent-mi355x-node-0")
+    node8.start_agent(node8.nodes[0])
+    after = wait_ready(k, "p", 2, timeout=30)
+    assert {d["uuid"] for d in after["status"]["devices"]} == \
+        {d["uuid"] for d in before["status"]["devices"]}
+
+
+def test_orphan_sweep_releases_claims_of_deleted_pool(cluster_factory):
+    c = cluster_factory(manager_args=["--orphan-sweep", "500ms"])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    wait_ready(k, "p", 2)
+    c._kill("manager")
+    # force-delete the CR behind the operator's back (finalizer stripped)
+    k.patch(MI355XPOOLS, "p", {"metadata": {"finalizers": []}}, "default")
+    k.delete(MI355XPOOLS, "p", "default")
+    c.start_manager()
+    deadline = time.time() + 20
+    while time.time() < deadline:
+        if all(not d.get("poolUID") for d in c.agent_request("mi355x-node-0", "GET",
+                                                             "/v1/node")["devices"]):
+            break
+        time.sleep(0.1)
+    else:
+        pytest.fail("orphaned claims were not released")
+
+
+def test_leader_election_failover(cluster_factory):
+    lease = ["--leader-elect", "--lease-duration", "2s", "--renew-deadline", "1500ms",
+             "--retry-period", "200ms"]
+    c = cluster_factory(manager_args=lease)
+    k = c.client
+    from gpupool.kube import LEASES
+    first = k.get(LEASES, "gpupool-manager-leader", "gpupool-system")["spec"]["holderIdentity"]
+    # a second manager stands by
+    standby = c._spawn("manager2", [c.procs["manager"].args[0], "--apiserver", c.url,
+                                    "--identity", "standby", "--progress-poll", "100ms"] + lease)
+    time.sleep(0.5)
+    assert k.get(LEASES, "gpupool-manager-leader", "gpupool-system")["spec"]["holderIdentity"] == first
+    c._kill("manager")
+    k.wait_for(LEASES, "gpupool-manager-leader", "gpupool-system",
+               lambda o: o and o["spec"]["holderIdentity"] == "standby", timeout=15, poll=0.1)
+    k.create(MI355XPOOLS, mi_pool("p", 1), "default")
+    wait_ready(k, "p", 1)  # the new leader reconciles
+    assert standby.poll() is None
+
+
+def test_multinode_placement(cluster_factory):
+    c = cluster_factory(nodes=[NodeSpec("node-a", count=4), NodeSpec("node-b", count=8)])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("pinned", 2, nodeName="node-a"), "default")
+    o = wait_ready(k, "pinned", 2)
+    assert o["status"]["nodeName"] == "node-a"
+    k.create(MI355XPOOLS, mi_pool("big", 6), "default")  # only node-b fits 6
+    o = wait_ready(k, "big", 6)
+    assert o["status"]["nodeName"] == "node-b"
+    k.create(MI355XPOOLS, mi_pool("sel", 1, nodeSelector={"kubernetes.io/hostname": "node-a"}),
+             "default")
+    assert wait_ready(k, "sel", 1)["status"]["nodeName"] == "node-a"
+
+
+def test_metrics_and_events_exposed(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    wait_ready(k, "p", 2)
+    m = node8.manager_metrics()
+    assert "gpupool_reconcile_total" in m and "gpupool_reconcile_to_ready_seconds_bucket" in m
+    assert 'gpupool_ready_replicas{kind="Mi355xPool",pool="default/p"} 2' in m
+    am = node8.agent_request.__self__  # cluster
+    txt = am.agent_request("mi355x-node-0", "GET", "/v1/node")
+    assert txt["backend"] == "fake"
+
+
+def test_invalid_spec_is_rejected(node8):
+    with pytest.raises(KubeError):
+        node8.client.create(MI355XPOOLS, mi_pool("neg", -1), "default")
