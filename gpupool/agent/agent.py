@@ -376,12 +376,17 @@ class Agent:
     def mark_advertised(self, resource: str, healthy: set[str] | None) -> None:
         with self.lock:
             plugin = self.plugins.get(resource)
+            before = set(self.advertised.get(resource, set()))
             if healthy is None:
                 if plugin is None or plugin.streams <= 0:
                     self.advertised[resource] = set()
             else:
                 self.advertised[resource] = set(healthy)
+            flipped = before ^ self.advertised.get(resource, set())
+            pools = {self.records[u]["poolUID"] for u in flipped if u in self.records}
         self._adv_event.set()
+        if pools:  # readiness depends on the advertised bit: tell the manager
+            self._bump(pools)
 
     def _wait_advertised(self, resource: str, uuids: list[str]) -> None:
         if not self.cfg.plugin_dir:
@@ -393,8 +398,8 @@ class Agent:
                 if all(u in self.advertised.get(resource, set()) for u in want):
                     return
                 plugin = self.plugins.get(resource)
-                if plugin is None or plugin.streams <= 0:
-                    return  # no kubelet stream connected: do not block the claim
+                if plugin is None or not plugin.registered:
+                    return  # no kubelet: do not block the claim (readiness follows via events)
             self._adv_event.wait(0.05)
             self._adv_event.clear()
 
@@ -408,7 +413,6 @@ class Agent:
             p = DevicePluginServer(self, resource, self.cfg.plugin_dir)
             self.plugins[resource] = p
         p.start()
-        p.register()
 
     def _notify_plugins(self) -> None:
         for p in list(self.plugins.values()):

@@ -68,6 +68,7 @@ class DevicePluginServer:
         }),))
         self.server.add_insecure_port(unix_target(self.sock))
         self.server.start()
+        self.register()  # synchronous first registration; the monitor handles kubelet restarts
         self._mon = threading.Thread(target=self._monitor_kubelet, daemon=True,
                                      name=f"dp-mon-{self.resource}")
         self._mon.start()
@@ -95,7 +96,7 @@ class DevicePluginServer:
                     DP.RegisterRequest(version=API_VERSION, endpoint=os.path.basename(self.sock),
                                        resource_name=self.resource, options=opts), timeout=5)
             self.registered = True
-            self._kubelet_ino = os.stat(ksock).st_ino
+            self._kubelet_ino = self._sock_identity(ksock)
             log.info("registered %s with kubelet at %s", self.resource, ksock)
             return True
         except (grpc.RpcError, OSError) as e:
@@ -105,13 +106,21 @@ class DevicePluginServer:
     def _monitor_kubelet(self) -> None:
         ksock = os.path.join(self.plugin_dir, KUBELET_SOCKET)
         while not self.stopped:
-            try:
-                ino = os.stat(ksock).st_ino
-            except FileNotFoundError:
-                ino = None
-            if ino is not None and ino != self._kubelet_ino:
+            ident = self._sock_identity(ksock)
+            if ident is None:
+                self.registered = False  # kubelet gone: register again when it comes back
+            elif ident != self._kubelet_ino:
                 self.register()
-            time.sleep(0.2 if not self.registered else 1.0)
+            time.sleep(0.2)
+
+    @staticmethod
+    def _sock_identity(path: str):
+        # (inode, ctime) — a recreated socket may reuse the inode number on tmpfs
+        try:
+            st = os.stat(path)
+        except FileNotFoundError:
+            return None
+        return (st.st_ino, st.st_ctime_ns)
 
     def notify(self) -> None:
         with self.cv:

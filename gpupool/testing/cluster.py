@@ -60,7 +60,8 @@ class Cluster:
     def __init__(self, workdir: str, nodes: list[NodeSpec] | None = None,
                  manager_args: list[str] | None = None, manager: bool = True,
                  python: str = sys.executable, env: dict | None = None,
-                 sample_interval: float = 0.5, kinds: str = "mi355x,azure"):
+                 sample_interval: float = 0.5, kinds: str = "mi355x,azure",
+                 manager_bin: str | None = None):
         self.workdir = os.path.abspath(workdir)
         os.makedirs(self.workdir, exist_ok=True)
         # unix socket paths are limited to 107 bytes: keep every socket under a short /tmp dir
@@ -76,6 +77,7 @@ class Cluster:
         self.env.update(env or {})
         self.sample_interval = sample_interval
         self.kinds = kinds
+        self.manager_bin = manager_bin
         self.procs: dict[str, subprocess.Popen] = {}
         self.url = ""
         self.client: Client | None = None
@@ -175,7 +177,7 @@ class Cluster:
         pf = os.path.join(self.workdir, "manager.port")
         if os.path.exists(pf):
             os.remove(pf)
-        argv = [native_bin("gpupool-manager"), "--apiserver", self.url, "--port-file", pf,
+        argv = [self.manager_bin or native_bin("gpupool-manager"), "--apiserver", self.url, "--port-file", pf,
                 "--kinds", self.kinds, "--progress-poll", "100ms"] + self.manager_args
         p = self._spawn("manager", argv)
         self.metrics_port = int(_wait_file(pf, 60, p, os.path.join(self.workdir, "manager.log")))

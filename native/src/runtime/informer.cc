@@ -34,7 +34,8 @@ void Informer::stop() {
 
 bool Informer::wait_synced(std::chrono::milliseconds timeout) {
   std::unique_lock<std::mutex> lk(mu_);
-  return synced_cv_.wait_for(lk, timeout, [this] { return synced_.load(); });
+  // system_clock deadline: see WorkQueue::get_for (TSan-visible pthread_cond_timedwait)
+  return synced_cv_.wait_until(lk, std::chrono::system_clock::now() + timeout, [this] { return synced_.load(); });
 }
 
 std::optional<Json> Informer::get(const std::string& ns, const std::string& name) const {

@@ -102,7 +102,9 @@ bool WorkQueue::get_for(std::string* key, Duration timeout) {
     auto wake = deadline;
     if (!delayed_.empty()) wake = std::min(wake, delayed_.top().at);
     if (Clock::now() >= deadline) return false;
-    cv_.wait_until(lk, wake);
+    // system_clock deadline -> pthread_cond_timedwait (steady_clock waits use
+    // pthread_cond_clockwait, which gcc-11's TSan does not intercept: false "double lock").
+    cv_.wait_until(lk, std::chrono::system_clock::now() + (wake - Clock::now()));
   }
 }
 

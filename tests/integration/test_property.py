@@ -1,0 +1,89 @@
+"""Property test (SURVEY.md §4.2 'Property' row): random sequences of replicas edits and device
+faults on two pools sharing one 8-GPU node. After faults clear and the system settles:
+  * readyReplicas == spec.replicas for both pools (when the total fits the node);
+  * the pools' device sets are disjoint (never claims a device owned by another pool);
+  * the agent's claims are exactly the union of the pools' status.devices;
+  * the kubelet's allocatable per resource equals each pool's readyReplicas.
+"""
+from __future__ import annotations
+
+import time
+
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from gpupool.kube import MI355XPOOLS, NODES
+from gpupool.testing.cluster import Cluster, NodeSpec
+
+from .helpers import mi_pool, ready_at
+
+pytestmark = pytest.mark.slow
+
+op = st.one_of(
+    st.tuples(st.just("scale"), st.sampled_from(["pa", "pb"]), st.integers(0, 6)),
+    st.tuples(st.just("fault"), st.integers(0, 7), st.sampled_from(["ecc", "xgmi", "thermal"])),
+    st.tuples(st.just("clear"), st.just(0), st.just(0)),
+)
+
+
+@pytest.fixture(scope="module")
+def shared(tmp_path_factory, native_built):
+    c = Cluster(str(tmp_path_factory.mktemp("prop")),
+                nodes=[NodeSpec("mi355x-node-0", extra_args=["--quarantine", "0.3"])],
+                sample_interval=0.2)
+    c.start()
+    yield c
+    c.stop()
+
+
+FAULTS = {"ecc": {"ecc": {"uncorrectable": 1}},
+          "xgmi": {"xgmi": {"links": ["X", "U", "D", "U", "U", "U", "U", "U"]}},
+          "thermal": {"temps": {"hotspot": {"current": 110}}}}
+
+
+@settings(max_examples=8, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
+                                                                 HealthCheck.too_slow])
+@given(ops=st.lists(op, min_size=1, max_size=6), final=st.tuples(st.integers(0, 4),
+                                                                  st.integers(0, 4)))
+def test_random_edits_and_faults_converge(shared, ops, final):
+    c = shared
+    k = c.client
+    ns = f"p{int(time.time() * 1e6) % 10**9}"
+    k.create(MI355XPOOLS, mi_pool("pa", 1, resourceName="amd.com/gpu-a"), ns)
+    k.create(MI355XPOOLS, mi_pool("pb", 1, resourceName="amd.com/gpu-b"), ns)
+    faults: dict = {}
+    for kind, a, b in ops:
+        if kind == "scale":
+            k.patch(MI355XPOOLS, a, {"spec": {"replicas": b}}, ns)
+        elif kind == "fault":
+            faults[str(a)] = FAULTS[b]
+            c.set_faults("mi355x-node-0", {"devices": faults})
+        else:
+            faults = {}
+            c.set_faults("mi355x-node-0", {})
+        time.sleep(0.05)
+    c.set_faults("mi355x-node-0", {})
+    ra, rb = final
+    k.patch(MI355XPOOLS, "pa", {"spec": {"replicas": ra}}, ns)
+    k.patch(MI355XPOOLS, "pb", {"spec": {"replicas": rb}}, ns)
+    a = k.wait_for(MI355XPOOLS, "pa", ns, ready_at(ra), timeout=45)
+    b = k.wait_for(MI355XPOOLS, "pb", ns, ready_at(rb), timeout=45)
+    ua = {d["uuid"] for d in a["status"]["devices"]}
+    ub = {d["uuid"] for d in b["status"]["devices"]}
+    assert not ua & ub
+    view = c.agent_request("mi355x-node-0", "GET", "/v1/node")
+    claimed = {d["uuid"] for d in view["devices"] if d.get("poolUID") in
+               (a["metadata"]["uid"], b["metadata"]["uid"])}
+    assert claimed == ua | ub
+    deadline = time.time() + 10
+    while True:  # kubelet's view converges through ListAndWatch
+        alloc = k.get(NODES, "mi355x-node-0")["status"].get("allocatable", {})
+        if alloc.get("amd.com/gpu-a", "0") == str(ra) and alloc.get("amd.com/gpu-b", "0") == str(rb):
+            break
+        assert time.time() < deadline, alloc
+        time.sleep(0.05)
+    for name in ("pa", "pb"):
+        k.delete(MI355XPOOLS, name, ns)
+    for name in ("pa", "pb"):
+        k.wait_for(MI355XPOOLS, name, ns, lambda o: o is None, timeout=30)

@@ -1,0 +1,46 @@
+"""The real multithreaded manager (informers, work-queue workers, agent long-poll watchers, event
+recorder, metrics server) under ThreadSanitizer and ASan+UBSan through a scale/drain/fault/delete
+scenario ('TSan covers the informer/workqueue/worker threads')."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import pytest
+
+from gpupool.kube import MI355XPOOLS, PODS
+
+from .helpers import mi_pool, pause_pod, wait_ready
+
+pytestmark = pytest.mark.slow
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+@pytest.mark.parametrize("san", ["tsan", "asan"])
+def test_manager_scenario_under_sanitizer(san, cluster_factory):
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "native"), f"SAN={san}", "host", "-j8"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    os.environ["TSAN_OPTIONS"] = "halt_on_error=0:report_signal_unsafe=0"
+    os.environ["ASAN_OPTIONS"] = "detect_leaks=0"
+    c = cluster_factory(manager_bin=os.path.join(ROOT, "build", f"native-{san}", "gpupool-manager"),
+                        manager_args=["--workers", "4", "--orphan-sweep", "300ms"])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("a", 4, drain={"gracePeriodSeconds": 1}), "default")
+    k.create(MI355XPOOLS, mi_pool("b", 2, resourceName="amd.com/gpu-b"), "default")
+    wait_ready(k, "a", 4, timeout=60)
+    wait_ready(k, "b", 2, timeout=60)
+    k.create(PODS, pause_pod("w"), "default")
+    k.wait_for(PODS, "w", "default", lambda o: o and o["status"].get("phase") == "Running", 30)
+    c.set_faults("mi355x-node-0", {"devices": {"0": {"ecc": {"uncorrectable": 3}}}})
+    k.patch(MI355XPOOLS, "a", {"spec": {"replicas": 1}}, "default")
+    wait_ready(k, "a", 1, timeout=60)
+    c.set_faults("mi355x-node-0", {})
+    for name in ("a", "b"):
+        k.delete(MI355XPOOLS, name, "default")
+    for name in ("a", "b"):
+        k.wait_for(MI355XPOOLS, name, "default", lambda o: o is None, timeout=60)
+    c._kill("manager")
+    log = c.log("manager")
+    assert "WARNING: ThreadSanitizer" not in log, log[-8000:]
+    assert "ERROR: AddressSanitizer" not in log and "runtime error:" not in log, log[-8000:]

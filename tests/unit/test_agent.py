@@ -1,0 +1,206 @@
+"""Node agent + ROCm device plugin conformance against the fake kubelet, all in-process
+(SURVEY.md §4.2 'Device plugin' row): Registration, ListAndWatch health transitions, Allocate
+contents, GetPreferredAllocation, PodResources, kubelet restart -> re-registration, ledger
+persistence, quarantine, all-or-nothing + topology-aware claims."""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+
+import grpc
+import pytest
+
+from gpupool.agent.agent import Agent, AgentConfig
+from gpupool.agent.deviceplugin.proto import DP, PR, Stub, unix_target
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+FIXTURE = os.path.join(ROOT, "tests", "fixtures", "node_8x_mi355x.json")
+
+
+@pytest.fixture
+def sockdir():
+    import shutil
+    import tempfile
+    d = tempfile.mkdtemp(prefix="gpa", dir="/tmp")
+    yield d
+    shutil.rmtree(d, ignore_errors=True)
+
+
+def make_agent(tmp_path, sockdir, plugin=True, faults=None, **kw):
+    cfg = AgentConfig(node="n0", backend="fake", fixture=FIXTURE, state_dir=str(tmp_path / "state"),
+                      plugin_dir=os.path.join(sockdir, "dp") if plugin else "",
+                      pod_resources=os.path.join(sockdir, "pr", "kubelet.sock") if plugin else "",
+                      probe_mode="simulated", probe_sim_ms=1, fsync=False,
+                      faults=faults or "", **kw)
+    return Agent(cfg)
+
+
+def claim(agent, uid="pool-1", count=2, resource="amd.com/gpu", policy=None):
+    return agent.claim({"poolUID": uid, "pool": "default/p", "count": count,
+                        "resourceName": resource, "policy": policy or {},
+                        "topologyPolicy": "xgmi-packed", "probe": {"enabled": True}})
+
+
+def test_claim_all_or_nothing_and_topology(tmp_path, sockdir, native_built):
+    a = make_agent(tmp_path, sockdir, plugin=False)
+    r = claim(a, count=3)
+    assert r["ok"] and sorted(d["index"] for d in r["devices"]) == [0, 1, 2]  # NUMA-0 packed
+    r2 = claim(a, uid="pool-2", count=6)
+    assert not r2["ok"] and r2["reason"] == "InsufficientDevices"
+    assert sum(1 for d in a.node_view()["devices"] if d.get("poolUID")) == 3  # nothing partial
+    r3 = claim(a, uid="pool-1", count=1)  # grows next to its NUMA-0 devices
+    assert r3["devices"][0]["index"] == 3
+
+
+def test_ledger_survives_restart_and_quarantine(tmp_path, sockdir, native_built):
+    faults = str(tmp_path / "faults.json")
+    json.dump({"devices": {"0": {"probeFail": True}}}, open(faults, "w"))
+    a = make_agent(tmp_path, sockdir, plugin=False, faults=faults)
+    r = claim(a, count=2)
+    bad = [d for d in r["devices"] if not d["probe"]["passed"]]
+    assert len(bad) == 1 and bad[0]["index"] == 0
+    b = make_agent(tmp_path, sockdir, plugin=False, faults=faults)  # "restart": reload ledger
+    assert {u for u, rec in b.records.items()} == {d["uuid"] for d in r["devices"]}
+    out = b.release("pool-1", [bad[0]["uuid"]])
+    assert out["ok"]
+    view = {d["uuid"]: d for d in b.node_view()["devices"]}
+    assert view[bad[0]["uuid"]]["state"] == "Quarantined"
+    r2 = claim(b, uid="pool-2", count=6)  # 8 - 1 claimed - 1 quarantined = 6 free
+    assert r2["ok"] and bad[0]["uuid"] not in {d["uuid"] for d in r2["devices"]}
+    assert not claim(b, uid="pool-3", count=1)["ok"]
+
+
+def test_release_refuses_gpu_with_pods(tmp_path, sockdir, native_built, monkeypatch):
+    a = make_agent(tmp_path, sockdir, plugin=False)
+    r = claim(a, count=1)
+    u = r["devices"][0]["uuid"]
+    monkeypatch.setattr(a, "_pods_by_device", lambda: {u: [{"namespace": "d", "name": "p"}]})
+    out = a.release("pool-1", [u])
+    assert not out["ok"] and out["reason"] == "PodsRunning"
+    assert u in a.records
+
+
+def test_health_sampling_follows_fault_overlay(tmp_path, sockdir, native_built):
+    faults = str(tmp_path / "faults.json")
+    a = make_agent(tmp_path, sockdir, plugin=False, faults=faults)
+    r = claim(a, count=1)
+    u = r["devices"][0]["uuid"]
+    json.dump({"devices": {u: {"temps": {"hotspot": {"current": 101}}}}}, open(faults, "w"))
+    changed = a.sample()
+    assert "pool-1" in changed
+    v = {d["uuid"]: d for d in a.node_view()["devices"]}[u]
+    assert not v["healthy"] and not v["verdict"]["thermalOk"]
+    gen, pools = a.changed_since(0)
+    assert gen >= 1 and "pool-1" in pools
+    os.remove(faults)
+    a.sample()
+    assert {d["uuid"]: d for d in a.node_view()["devices"]}[u]["healthy"]
+
+
+class MiniKubelet:
+    """Just the kubelet's Registration service + a ListAndWatch consumer."""
+
+    def __init__(self, plugin_dir):
+        import concurrent.futures as cf
+        from gpupool.agent.deviceplugin.proto import service_handler
+        self.dir = plugin_dir
+        self.registrations = []
+        self.server = grpc.server(cf.ThreadPoolExecutor(4))
+        self.server.add_generic_rpc_handlers((service_handler("v1beta1.Registration",
+                                                              {"Register": self.Register}),))
+        os.makedirs(plugin_dir, exist_ok=True)
+        self.server.add_insecure_port(unix_target(os.path.join(plugin_dir, "kubelet.sock")))
+        self.server.start()
+
+    def Register(self, req, ctx):
+        self.registrations.append((req.version, req.endpoint, req.resource_name,
+                                   req.options.get_preferred_allocation_available))
+        return DP.Empty()
+
+    def stop(self):
+        self.server.stop(0)
+        try:
+            os.unlink(os.path.join(self.dir, "kubelet.sock"))
+        except FileNotFoundError:
+            pass
+
+
+def test_device_plugin_conformance(tmp_path, sockdir, native_built):
+    dp_dir = os.path.join(sockdir, "dp")
+    kubelet = MiniKubelet(dp_dir)
+    a = make_agent(tmp_path, sockdir)
+    try:
+        r = claim(a, count=2)
+        assert kubelet.registrations == [("v1beta1", "gpupool-amd-com_gpu.sock", "amd.com/gpu", True)]
+        ch = grpc.insecure_channel(unix_target(os.path.join(dp_dir, "gpupool-amd-com_gpu.sock")))
+        stub = Stub(ch, "v1beta1.DevicePlugin")
+        assert stub.GetDevicePluginOptions(DP.Empty()).get_preferred_allocation_available
+        stream = stub.ListAndWatch(DP.Empty())
+        first = next(stream)
+        ids = {d.ID: d.health for d in first.devices}
+        assert set(ids) == {d["uuid"] for d in r["devices"]} and set(ids.values()) == {"Healthy"}
+        assert all(d.topology.nodes[0].ID == 0 for d in first.devices)
+        # advertised bit set once the stream delivered them
+        deadline = time.time() + 5
+        while time.time() < deadline and not all(d["advertised"] for d in a.node_view()["devices"]
+                                                   if d.get("poolUID")):
+            time.sleep(0.02)
+        assert all(d["advertised"] for d in a.node_view()["devices"] if d.get("poolUID"))
+        # Allocate: ROCR_VISIBLE_DEVICES + /dev/kfd + render nodes
+        u0 = r["devices"][0]["uuid"]
+        resp = stub.Allocate(DP.AllocateRequest(container_requests=[{"devices_ids": [u0]}]))
+        cr = resp.container_responses[0]
+        assert cr.envs["ROCR_VISIBLE_DEVICES"] == r["devices"][0]["hipUUID"]
+        assert [d.host_path for d in cr.devices] == ["/dev/kfd", r["devices"][0]["renderNode"]]
+        assert all(d.permissions == "rw" for d in cr.devices)
+        # Allocate of a non-pool device is refused
+        free = next(d["uuid"] for d in a.node_view()["devices"] if not d.get("poolUID"))
+        with pytest.raises(grpc.RpcError) as e:
+            stub.Allocate(DP.AllocateRequest(container_requests=[{"devices_ids": [free]}]))
+        assert e.value.code() == grpc.StatusCode.FAILED_PRECONDITION
+        # cordon -> the device turns Unhealthy on the stream
+        a.cordon("pool-1", [u0])
+        upd = next(stream)
+        assert {d.ID: d.health for d in upd.devices}[u0] == "Unhealthy"
+        pref = stub.GetPreferredAllocation(DP.PreferredAllocationRequest(container_requests=[
+            {"available_deviceIDs": [d["uuid"] for d in r["devices"]], "allocation_size": 1}]))
+        assert len(pref.container_responses[0].deviceIDs) == 1
+        # kubelet restart -> plugin re-registers by itself
+        kubelet.stop()
+        kubelet = MiniKubelet(dp_dir)
+        deadline = time.time() + 5
+        while time.time() < deadline and not kubelet.registrations:
+            time.sleep(0.05)
+        assert kubelet.registrations and kubelet.registrations[0][2] == "amd.com/gpu"
+        stream.cancel()
+        ch.close()
+    finally:
+        a.stop()
+        kubelet.stop()
+
+
+def test_podresources_roundtrip(tmp_path, sockdir):
+    """The fake kubelet's PodResources server and the agent's client agree on the wire format."""
+    import concurrent.futures as cf
+
+    from gpupool.agent.deviceplugin.proto import service_handler
+    from gpupool.agent.podresources import list_pod_devices
+    sock = os.path.join(sockdir, "pr.sock")
+
+    def List(req, ctx):
+        resp = PR.ListPodResourcesResponse()
+        pr = resp.pod_resources.add(name="p", namespace="ns")
+        c = pr.containers.add(name="c")
+        c.devices.add(resource_name="amd.com/gpu", device_ids=["u1", "u2"])
+        return resp
+    s = grpc.server(cf.ThreadPoolExecutor(2))
+    s.add_generic_rpc_handlers((service_handler("v1.PodResourcesLister", {"List": List}),))
+    s.add_insecure_port(unix_target(sock))
+    s.start()
+    try:
+        out = list_pod_devices(sock)
+        assert set(out) == {"u1", "u2"} and out["u1"][0]["name"] == "p"
+    finally:
+        s.stop(0)
