@@ -106,9 +106,12 @@ def main() -> int:
         from gpupool.testing.cluster import FIXTURE, Cluster, NodeSpec
         from gpupool.bench import ground_truth as gt
         workdir = args.workdir or tempfile.mkdtemp(prefix="gpupool-bench-")
+        # fake mode: simulated probe latency calibrated to the measured real 1 GiB probe (2.6 ms,
+        # profiles/r1_probe_ctypes_real.txt)
         node = NodeSpec("mi355x-node-0", backend="amdsmi" if real else "fake",
                         probe="inproc" if real else "simulated",
-                        count=-1 if real else max(8, n))
+                        count=-1 if real else max(8, n),
+                        extra_args=[] if real else ["--probe-sim-ms", "2.6"])
         cluster = Cluster(workdir, nodes=[node], sample_interval=1.0)
         cluster.start()  # all child processes exist before this process touches the GPU
         c = cluster.client

@@ -98,6 +98,11 @@ class Agent:
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self._evaluate_all()
+        from .preflight import check as preflight_check
+        self.preflight = preflight_check(self.snap, fake=self.backend == "fake")
+        if not self.preflight["ready"]:
+            log.warning("preflight not ready: %s", {k: v["detail"] for k, v in
+                                                    self.preflight["checks"].items() if not v["ok"]})
         log.info("agent %s: backend=%s devices=%d probe=%s (init %.0f ms) ledger=%d claims",
                  cfg.node, self.backend, len(self.by_uuid), self.probe_mode, self.prober.init_ms,
                  len(self.records))
@@ -203,7 +208,8 @@ class Agent:
             "uuid": uuid, "hipUUID": d.get("hipUUID", ""), "bdf": d.get("bdf", ""),
             "index": d.get("index", -1), "node": self.cfg.node,
             "renderNode": d.get("renderNode", ""), "kfdNode": d.get("kfdNode", -1),
-            "numa": d.get("numa"), "healthy": bool(v.get("healthy")), "verdict": v,
+            "numa": d.get("numa"), "partition": d.get("partition") or {},
+            "healthy": bool(v.get("healthy")), "verdict": v,
             "present": d.get("present", uuid in self.by_uuid),
             "pods": pods.get(uuid, []),
         }
@@ -232,7 +238,7 @@ class Agent:
             uuids = list(self.by_uuid) + [u for u in self.records if u not in self.by_uuid]
             devices = [self.device_view(u, pods) for u in uuids]
             return {"node": self.cfg.node, "backend": self.backend, "gen": self.gen,
-                    "probeMode": self.probe_mode,
+                    "probeMode": self.probe_mode, "preflight": self.preflight,
                     "advertiseRequired": bool(self.cfg.plugin_dir),
                     "devices": devices, "topology": self.snap.get("topology", {})}
 
@@ -273,7 +279,7 @@ class Agent:
                        "baseline": {"ecc": d.get("ecc", {})}, "claimedAt": ts,
                        "state": "Probing", "probe": None}
                 self.records[d["uuid"]] = rec
-                self.ledger.put(rec)
+            self.ledger.commit(self.records)  # durable before probing: no double claim on crash
             self.stats["claims"] += len(chosen)
         # probes run outside the lock, concurrently across GPUs
         t0 = time.perf_counter()
@@ -287,11 +293,11 @@ class Agent:
                     continue  # released concurrently
                 rec["probe"] = res
                 rec["state"] = "Claimed"
-                self.ledger.put(rec)
                 self.stats["probes"] += 1
                 self.stats["probe_ms_sum"] += float(res.get("ms", 0.0))
                 if not res.get("passed"):
                     self.stats["probe_failures"] += 1
+            self.ledger.commit(self.records)
             self._evaluate_all()
         self._ensure_plugin(resource)
         self._notify_plugins()
@@ -311,8 +317,9 @@ class Agent:
                 if rec and rec["poolUID"] == pool_uid and rec.get("state") != "Draining":
                     rec["state"] = "Draining"
                     rec["drainStartedAt"] = now_rfc3339()
-                    self.ledger.put(rec)
                     n += 1
+            if n:
+                self.ledger.commit(self.records)
         self._notify_plugins()
         return {"ok": True, "cordoned": n}
 
@@ -334,8 +341,9 @@ class Agent:
                         self.verdicts.get(u, {}).get("reasons", []))
                     self.ledger.quarantine(u, self.cfg.quarantine_s, why)
                 del self.records[u]
-                self.ledger.delete(u)
                 released.append(u)
+            if released:
+                self.ledger.commit(self.records)
             self.stats["releases"] += len(released)
             self._evaluate_all()
         self._notify_plugins()
@@ -354,7 +362,8 @@ class Agent:
                 if resource and rec.get("resourceName") != resource:
                     rec["resourceName"] = resource
                 changed.add(u)
-                self.ledger.put(rec)
+            if changed:
+                self.ledger.commit(self.records)
             self._evaluate_all()
         if resource:
             self._ensure_plugin(resource)
@@ -447,8 +456,12 @@ class Agent:
                 hip.append(d.get("hipUUID") or str(d["index"]))
                 if d.get("renderNode"):
                     render.append(d["renderNode"])
+            # ROCR_VISIBLE_DEVICES pins the container to exactly its GPUs (HIP ordinals then
+            # start at 0); GPUPOOL_NUM_GPUS is the per-pod world-size hint for
+            # `torch.distributed.run --nproc-per-node $GPUPOOL_NUM_GPUS`.
             envs = {"ROCR_VISIBLE_DEVICES": ",".join(hip),
                     "GPUPOOL_DEVICE_UUIDS": ",".join(ids),
+                    "GPUPOOL_NUM_GPUS": str(len(ids)),
                     "GPUPOOL_NODE": self.cfg.node}
             return {"envs": envs, "devices": ["/dev/kfd"] + render,
                     "annotations": {schema.ANN_POD_DEVICES: ",".join(ids)}}
@@ -486,17 +499,23 @@ class Agent:
                  "message": f"{len(self.by_uuid)} GPU(s) via {self.backend}; probe "
                             f"{self.probe_mode}",
                  "lastHeartbeatTime": now_rfc3339(), "lastTransitionTime": now_rfc3339()}
+        failed = {k: v["detail"] for k, v in self.preflight["checks"].items() if not v["ok"]}
+        rocm = {"type": "ROCmReady", "status": "True" if self.preflight["ready"] else "False",
+                "reason": "PreflightPassed" if self.preflight["ready"] else "PreflightFailed",
+                "message": "; ".join(f"{k}: {v}" for k, v in failed.items()) or
+                "; ".join(v["detail"] for v in self.preflight["checks"].values()),
+                "lastHeartbeatTime": now_rfc3339(), "lastTransitionTime": now_rfc3339()}
         try:
             node = c.get(NODES, self.cfg.node)
             conds = [x for x in node.get("status", {}).get("conditions", [])
-                     if x.get("type") != "GPUPoolAgentReady"]
+                     if x.get("type") not in ("GPUPoolAgentReady", "ROCmReady")]
             old = [x for x in node.get("status", {}).get("conditions", [])
                    if x.get("type") == "GPUPoolAgentReady"]
             if old and old[0].get("status") == "True":
                 ready["lastTransitionTime"] = old[0].get("lastTransitionTime", ready[
                     "lastTransitionTime"])
             st = node.get("status", {})
-            st["conditions"] = conds + [ready]
+            st["conditions"] = conds + [ready, rocm]
             if not any(x.get("type") == "Ready" for x in conds):
                 st["conditions"].append({"type": "Ready", "status": "True",
                                          "reason": "KubeletReady" if self.cfg.plugin_dir

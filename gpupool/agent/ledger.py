@@ -1,10 +1,12 @@
 """Claim ledger: the node agent's durable record of which GPU belongs to which pool.
 
-One JSON file per claimed device (``<state>/claims/<uuid>.json``) written atomically
-(write temp -> fsync -> rename -> fsync dir), plus ``<state>/quarantine/<uuid>.json`` for GPUs that
-failed a probe. Together with ``status.devices`` on the pool and the device labels this is what
-makes the operator stateless across restarts (SURVEY.md §5 checkpoint/resume row): on start the
-agent reloads the ledger, and the manager's orphan sweep releases claims whose pool UID is gone.
+All claims live in one JSON document (``<state>/ledger.json``: ``{"version": 1, "claims": {uuid:
+record}}``) that is replaced atomically (write temp -> fsync -> rename -> fsync dir) once per
+agent operation, so a claim of 8 GPUs costs one fsync, not eight, and a crash can never leave a
+half-written batch. GPUs that failed a probe are recorded in ``<state>/quarantine/<uuid>.json``.
+Together with ``status.devices`` on the pool this makes the operator stateless across restarts
+(SURVEY.md §5 checkpoint/resume row): on start the agent reloads the ledger, and the manager's
+orphan sweep releases claims whose pool UID is gone.
 """
 from __future__ import annotations
 
@@ -13,16 +15,10 @@ import os
 import threading
 import time
 
+VERSION = 1
 
-def _atomic_write(path: str, data: dict) -> None:
-    d = os.path.dirname(path)
-    os.makedirs(d, exist_ok=True)
-    tmp = f"{path}.tmp.{os.getpid()}.{threading.get_ident()}"
-    with open(tmp, "w") as f:
-        json.dump(data, f, sort_keys=True)
-        f.flush()
-        os.fsync(f.fileno())
-    os.replace(tmp, path)
+
+def _fsync_dir(d: str) -> None:
     try:
         fd = os.open(d, os.O_RDONLY)
         try:
@@ -33,53 +29,72 @@ def _atomic_write(path: str, data: dict) -> None:
         pass
 
 
+def _atomic_write_text(path: str, text: str, fsync: bool = True) -> None:
+    d = os.path.dirname(path)
+    os.makedirs(d, exist_ok=True)
+    tmp = f"{path}.tmp.{os.getpid()}.{threading.get_ident()}"
+    with open(tmp, "w") as f:
+        f.write(text)
+        if fsync:
+            f.flush()
+            os.fsync(f.fileno())
+    os.replace(tmp, path)
+    if fsync:
+        _fsync_dir(d)
+
+
 def _safe(uuid: str) -> str:
     return "".join(c if c.isalnum() or c in "-_." else "_" for c in uuid)
+
+
+def read_claims(state_dir: str) -> dict[str, dict]:
+    """Parse a ledger directory without an agent (used by the bench's independent ground truth)."""
+    path = os.path.join(state_dir, "ledger.json")
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    return dict(doc.get("claims") or {})
 
 
 class Ledger:
     def __init__(self, state_dir: str, fsync: bool = True):
         self.dir = state_dir
-        self.claims_dir = os.path.join(state_dir, "claims")
+        self.path = os.path.join(state_dir, "ledger.json")
         self.quar_dir = os.path.join(state_dir, "quarantine")
-        os.makedirs(self.claims_dir, exist_ok=True)
         os.makedirs(self.quar_dir, exist_ok=True)
         self.fsync = fsync
+        self._mu = threading.Lock()
+        self.writes = 0
 
     # ---------------------------------------------------------------- claims
     def load(self) -> dict[str, dict]:
-        out = {}
-        for name in sorted(os.listdir(self.claims_dir)):
-            if not name.endswith(".json"):
-                continue
-            try:
-                with open(os.path.join(self.claims_dir, name)) as f:
-                    rec = json.load(f)
-                out[rec["uuid"]] = rec
-            except (OSError, ValueError, KeyError):
-                continue  # torn/partial files cannot exist (atomic rename); ignore stray junk
-        return out
+        claims = read_claims(self.dir)
+        legacy = os.path.join(self.dir, "claims")  # per-device files of earlier versions
+        if os.path.isdir(legacy):
+            for name in sorted(os.listdir(legacy)):
+                if name.endswith(".json"):
+                    try:
+                        with open(os.path.join(legacy, name)) as f:
+                            rec = json.load(f)
+                        claims.setdefault(rec["uuid"], rec)
+                    except (OSError, ValueError, KeyError):
+                        continue
+        return claims
 
-    def put(self, rec: dict) -> None:
-        path = os.path.join(self.claims_dir, _safe(rec["uuid"]) + ".json")
-        if self.fsync:
-            _atomic_write(path, rec)
-        else:
-            tmp = path + ".tmp"
-            with open(tmp, "w") as f:
-                json.dump(rec, f, sort_keys=True)
-            os.replace(tmp, path)
-
-    def delete(self, uuid: str) -> None:
-        try:
-            os.remove(os.path.join(self.claims_dir, _safe(uuid) + ".json"))
-        except FileNotFoundError:
-            pass
+    def commit(self, claims: dict[str, dict]) -> None:
+        """Persist the full claim map atomically (one write + one fsync per agent operation)."""
+        text = json.dumps({"version": VERSION, "claims": claims}, sort_keys=True)
+        with self._mu:
+            _atomic_write_text(self.path, text, self.fsync)
+            self.writes += 1
 
     # ---------------------------------------------------------------- quarantine
     def quarantine(self, uuid: str, seconds: float, reason: str) -> None:
-        _atomic_write(os.path.join(self.quar_dir, _safe(uuid) + ".json"),
-                      {"uuid": uuid, "until": time.time() + seconds, "reason": reason})
+        _atomic_write_text(os.path.join(self.quar_dir, _safe(uuid) + ".json"),
+                           json.dumps({"uuid": uuid, "until": time.time() + seconds,
+                                       "reason": reason}), self.fsync)
 
     def quarantined(self) -> dict[str, dict]:
         out, now = {}, time.time()

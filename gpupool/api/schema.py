@@ -131,6 +131,7 @@ DEVICE_STATUS = {
         "advertised": _B,
         "pods": {"type": "array", "items": _S},
         "claimedAt": _S,
+        "partition": {"type": "object", "properties": {"compute": _S, "memory": _S}},
         "probe": {
             "type": "object",
             "properties": {

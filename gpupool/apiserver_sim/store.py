@@ -81,7 +81,21 @@ BUILTINS = [
     ResourceType("", "v1", "events", "Event", True, "event", ["ev"]),
     ResourceType("", "v1", "secrets", "Secret", True, "secret"),
     ResourceType("", "v1", "configmaps", "ConfigMap", True, "configmap", ["cm"]),
+    ResourceType("", "v1", "resourcequotas", "ResourceQuota", True, "resourcequota", ["quota"],
+                 status_sub=True),
     ResourceType("coordination.k8s.io", "v1", "leases", "Lease", True, "lease"),
+    # stored-only kinds (no controllers behind them): lets `make deploy` manifests be applied
+    # and validated against the simulator
+    ResourceType("", "v1", "serviceaccounts", "ServiceAccount", True, "serviceaccount", ["sa"]),
+    ResourceType("", "v1", "services", "Service", True, "service", ["svc"], status_sub=True),
+    ResourceType("apps", "v1", "deployments", "Deployment", True, "deployment", ["deploy"],
+                 status_sub=True),
+    ResourceType("apps", "v1", "daemonsets", "DaemonSet", True, "daemonset", ["ds"],
+                 status_sub=True),
+    ResourceType("rbac.authorization.k8s.io", "v1", "clusterroles", "ClusterRole", False,
+                 "clusterrole"),
+    ResourceType("rbac.authorization.k8s.io", "v1", "clusterrolebindings", "ClusterRoleBinding",
+                 False, "clusterrolebinding"),
     ResourceType("apiextensions.k8s.io", "v1", "customresourcedefinitions",
                  "CustomResourceDefinition", False, "customresourcedefinition", ["crd", "crds"]),
 ]

@@ -10,7 +10,6 @@ truth = #{devices claimed by the pool (ledger) that are present+healthy (CLI) an
 """
 from __future__ import annotations
 
-import glob
 import json
 import os
 import subprocess
@@ -82,17 +81,12 @@ def healthy_uuids_fixture(fixture: str, faults: str | None, node: str) -> set[st
 
 
 def ledger_claims(state_dir: str, pool_uid: str) -> set[str]:
-    out = set()
-    for p in glob.glob(os.path.join(state_dir, "claims", "*.json")):
-        try:
-            with open(p) as f:
-                rec = json.load(f)
-        except (OSError, ValueError):
-            continue
-        if rec.get("poolUID") == pool_uid and rec.get("state") == "Claimed" and \
-                (rec.get("probe") or {}).get("passed"):
-            out.add(rec["uuid"])
-    return out
+    """Claims of ``pool_uid`` read straight from the agent's ledger file on disk."""
+    with open(os.path.join(state_dir, "ledger.json")) as f:
+        claims = (json.load(f) or {}).get("claims") or {}
+    return {u for u, rec in claims.items()
+            if rec.get("poolUID") == pool_uid and rec.get("state") == "Claimed"
+            and (rec.get("probe") or {}).get("passed")}
 
 
 def advertised_count(client: Client, node: str, resource: str) -> int:

@@ -63,6 +63,10 @@ BY_KIND = {
     "Pod": PODS, "Node": NODES, "Event": EVENTS, "Secret": SECRETS, "ConfigMap": CONFIGMAPS,
     "Namespace": NAMESPACES, "Lease": LEASES, "CustomResourceDefinition": CRDS,
     "Mi355xPool": MI355XPOOLS, "AzureVmPool": AZUREVMPOOLS,
+    "ClusterRole": Res("rbac.authorization.k8s.io", "v1", "clusterroles", namespaced=False),
+    "ClusterRoleBinding": Res("rbac.authorization.k8s.io", "v1", "clusterrolebindings",
+                              namespaced=False),
+    "ResourceQuota": Res("", "v1", "resourcequotas"),
 }
 
 

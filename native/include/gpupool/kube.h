@@ -29,6 +29,7 @@ ResourceRef nodes();
 ResourceRef events();
 ResourceRef secrets();
 ResourceRef leases();
+ResourceRef resourcequotas();
 ResourceRef mi355xpools();
 ResourceRef azurevmpools();
 }  // namespace res

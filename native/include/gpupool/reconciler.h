@@ -97,12 +97,13 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
   };
   Observed observe_(const ObjectMeta& m, const Mi355xPoolSpec& spec, const Json& status);
   std::string choose_node_(const Mi355xPoolSpec& spec, int need, const std::string& current);
+  bool quota_allows_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta, std::string* why);
   Outcome finalize_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec);
   // Evicts pods on draining devices and releases drained ones. Returns #devices still draining.
   int drain_(const Json& obj, const std::string& node, const ObjectMeta& m, const Mi355xPoolSpec& spec,
              std::vector<DeviceView>& mine);
   Json build_status_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec, const Observed& o,
-                     const std::string& progress_reason, const std::string& progress_msg, bool insufficient,
+                     const std::string& progress_reason, const std::string& progress_msg, const std::string& blocked,
                      bool deleting);
 
   DeviceProvider& provider_;

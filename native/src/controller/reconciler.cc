@@ -264,7 +264,7 @@ int Mi355xPoolReconciler::drain_(const Json& obj, const std::string& node, const
 
 Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec,
                                          const Observed& o, const std::string& progress_reason,
-                                         const std::string& progress_msg, bool insufficient, bool deleting) {
+                                         const std::string& progress_msg, const std::string& blocked, bool deleting) {
   const std::string now = rfc3339_now();
   Json st = Json::object();
   st["observedGeneration"] = m.generation;
@@ -330,13 +330,13 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
     set_condition(conds, gen::kCondDegraded, "True", "AgentUnreachable", o.error, gen, now);
   } else if (!unhealthy.empty()) {
     set_condition(conds, gen::kCondDegraded, "True", "DeviceUnhealthy", join(unhealthy, ", "), gen, now);
-  } else if (insufficient) {
-    set_condition(conds, gen::kCondDegraded, "True", "InsufficientDevices", progress_msg, gen, now);
+  } else if (!blocked.empty()) {
+    set_condition(conds, gen::kCondDegraded, "True", blocked, progress_msg, gen, now);
   } else {
     set_condition(conds, gen::kCondDegraded, "False", "AsExpected", "all claimed GPUs healthy", gen, now);
   }
-  if (insufficient) {
-    set_condition(conds, gen::kCondProgressing, "False", "InsufficientDevices", progress_msg, gen, now);
+  if (!blocked.empty()) {
+    set_condition(conds, gen::kCondProgressing, "False", blocked, progress_msg, gen, now);
   } else if (!progress_reason.empty()) {
     set_condition(conds, gen::kCondProgressing, "True", progress_reason, progress_msg, gen, now);
   } else {
@@ -349,7 +349,7 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
   std::string reason = is_ready ? "AllReplicasReady"
                        : deleting ? "Deleting"
                        : !o.reachable ? "AgentUnreachable"
-                       : insufficient ? "InsufficientDevices"
+                       : !blocked.empty() ? blocked
                        : probing ? "Probing"
                        : !progress_reason.empty() ? progress_reason
                        : !unhealthy.empty() ? "DeviceUnhealthy"
@@ -365,7 +365,7 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
 Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec) {
   Observed o = observe_(m, spec, obj["status"]);
   if (!o.reachable && !o.node.empty()) {
-    write_status_(obj, build_status_(obj, m, spec, o, "Deleting", "agent unreachable", false, true));
+    write_status_(obj, build_status_(obj, m, spec, o, "Deleting", "agent unreachable", "", true));
     return Outcome::transient("agent unreachable during finalization: " + o.error);
   }
   std::vector<std::string> cordon;
@@ -380,7 +380,7 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
   if (!o.mine.empty()) o = observe_(m, spec, obj["status"]);
   if (still > 0 || !o.mine.empty()) {
     write_status_(obj, build_status_(obj, m, spec, o, "Draining", std::to_string(still) + " GPU(s) still have pods",
-                                     false, true));
+                                     "", true));
     return Outcome::requeue(opts_.progress_poll, "draining");
   }
   if (m.has_finalizer(gen::kFinalizer)) {
@@ -424,7 +424,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
 
   Observed o = observe_(m, spec, obj["status"]);
   if (!o.reachable && !o.node.empty()) {
-    write_status_(obj, build_status_(obj, m, spec, o, "", "", false, false));
+    write_status_(obj, build_status_(obj, m, spec, o, "", "", "", false));
     ready_gauge().set({{"kind", kind_}, {"pool", m.key()}}, 0);
     return Outcome::transient("agent on " + o.node + " unreachable: " + o.error);
   }
@@ -443,7 +443,8 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
   }
 
   std::string progress_reason, progress_msg;
-  bool insufficient = false, acted = false;
+  std::string blocked;  // reason scale-up is blocked (InsufficientDevices | QuotaExceeded)
+  bool acted = false;
   std::vector<const DeviceView*> active;
   for (const auto& d : o.mine)
     if (d.state != "Draining") active.push_back(&d);
@@ -492,11 +493,18 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     provider_.cordon(o.node, m.uid, cordon);
     acted = true;
   }
-  if (n_active < spec.replicas) {
+  std::string quota_msg;
+  bool over_quota = n_active < spec.replicas &&
+                    !quota_allows_(m, spec, static_cast<int>(spec.replicas - n_active), &quota_msg);
+  if (over_quota) {
+    blocked = "QuotaExceeded";
+    progress_msg = quota_msg;
+    event_(obj, "Warning", "QuotaExceeded", quota_msg);
+  } else if (n_active < spec.replicas) {
     int need = static_cast<int>(spec.replicas - n_active);
     std::string node = o.mine.empty() ? choose_node_(spec, need, obj.path("status.nodeName").as_string()) : o.node;
     if (node.empty()) {
-      insufficient = true;
+      blocked = "InsufficientDevices";
       progress_msg = "no eligible node with a gpupool agent";
     } else {
       ClaimRequest req;
@@ -514,7 +522,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
       ClaimResult cr = provider_.claim(node, req);
       double claim_ms = std::chrono::duration<double, std::milli>(clock_t_::now() - t).count();
       if (!cr.ok) {
-        insufficient = true;
+        blocked = cr.reason.empty() ? "InsufficientDevices" : cr.reason;
         progress_msg = cr.reason + ": " + cr.message;
         event_(obj, "Warning", cr.reason.empty() ? "InsufficientDevices" : cr.reason, cr.message);
       } else {
@@ -552,19 +560,57 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
       else ++active_now;
       if (d.state == "Claimed" && d.healthy && d.probe_passed && d.advertised) ++ready_now;
     }
-    if (!inflight && !insufficient && ready_now == spec.replicas && active_now == spec.replicas) progress_reason.clear();
+    if (!inflight && blocked.empty() && ready_now == spec.replicas && active_now == spec.replicas) progress_reason.clear();
   }
-  Json status = build_status_(obj, m, spec, o, progress_reason, progress_msg, insufficient, false);
+  Json status = build_status_(obj, m, spec, o, progress_reason, progress_msg, blocked, false);
   write_status_(obj, status);
   int64_t ready = status["readyReplicas"].as_int(0);
   ready_gauge().set({{"kind", kind_}, {"pool", m.key()}}, static_cast<double>(ready));
   bool is_ready = condition_true(status["conditions"], gen::kCondReady);
   observe_ready_(m, is_ready, spec.replicas);
-  if (insufficient) return Outcome::requeue(ms(5000), "insufficient devices");
+  if (!blocked.empty()) return Outcome::requeue(ms(5000), blocked);
   bool draining = false;
   for (const auto& d : o.mine) draining = draining || d.state == "Draining" || d.state == "Probing";
   if (draining || !is_ready) return Outcome::requeue(opts_.progress_poll, progress_reason);
   return Outcome::done(opts_.resync);
+}
+
+// Per-namespace GPU quota (the reference's ResourceQuota practice,
+// GPU调度平台搭建.md:802): a ResourceQuota with spec.hard["<resourceName>"] or
+// spec.hard["requests.<resourceName>"] caps the GPUs all pools of that resource in the namespace
+// may claim. Usage = status.replicas of the other pools (informer cache) + our claimed + delta.
+bool Mi355xPoolReconciler::quota_allows_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta,
+                                         std::string* why) {
+  Json quotas;
+  try {
+    quotas = client_.list(res::resourcequotas(), m.ns);
+  } catch (const std::exception&) {
+    return true;  // quota API unavailable: do not block claims on an optional policy
+  }
+  int64_t hard = -1;
+  std::string qname;
+  for (const auto& q : quotas["items"].elements()) {
+    for (const std::string& key : {spec.resource_name, "requests." + spec.resource_name}) {
+      const Json& h = q.path("spec.hard")[key];
+      if (h.is_null()) continue;
+      int64_t v = h.is_number() ? h.as_int() : std::atoll(h.as_string().c_str());
+      if (hard < 0 || v < hard) {
+        hard = v;
+        qname = q.path("metadata.name").as_string();
+      }
+    }
+  }
+  if (hard < 0) return true;
+  int64_t used = 0;
+  for (const auto& p : pools_.list()) {
+    if (p.path("metadata.namespace").as_string() != m.ns) continue;
+    if (p.path("spec.resourceName").str_or(gen::kDefaultResource) != spec.resource_name) continue;
+    used += p.path("status.replicas").as_int(0);
+  }
+  if (used + delta <= hard) return true;
+  *why = "ResourceQuota " + m.ns + "/" + qname + " allows " + std::to_string(hard) + " " + spec.resource_name +
+         "; " + std::to_string(used) + " in use, " + std::to_string(delta) + " more requested";
+  return false;
 }
 
 void Mi355xPoolReconciler::sweep_orphans() {

@@ -28,6 +28,7 @@ DeviceView DeviceView::from(const Json& j) {
   d.probe = j["probe"];
   d.pods = j["pods"].is_array() ? j["pods"] : Json::array();
   d.claimed_at = j["claimedAt"].as_string();
+  d.partition = j["partition"];
   d.drain_started_at = j["drainStartedAt"].as_string();
   return d;
 }
@@ -55,6 +56,7 @@ Json DeviceView::status_json() const {
   for (const auto& p : pods.elements()) pods_out.push_back(p.is_string() ? p : Json(p["namespace"].as_string() + "/" + p["name"].as_string()));
   s["pods"] = pods_out;
   if (!claimed_at.empty()) s["claimedAt"] = claimed_at;
+  if (partition.is_object() && partition.size()) s["partition"] = partition;
   if (probe.is_object()) {
     Json p = Json::object();
     p["passed"] = probe_passed;

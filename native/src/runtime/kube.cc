@@ -20,6 +20,7 @@ ResourceRef nodes() { return {"", "v1", "nodes", false, "Node"}; }
 ResourceRef events() { return {"", "v1", "events", true, "Event"}; }
 ResourceRef secrets() { return {"", "v1", "secrets", true, "Secret"}; }
 ResourceRef leases() { return {"coordination.k8s.io", "v1", "leases", true, "Lease"}; }
+ResourceRef resourcequotas() { return {"", "v1", "resourcequotas", true, "ResourceQuota"}; }
 ResourceRef mi355xpools() { return {gen::kGroup, gen::kVersion, gen::kPluralMi355xPool, true, "Mi355xPool"}; }
 ResourceRef azurevmpools() { return {gen::kGroup, gen::kVersion, gen::kPluralAzureVmPool, true, "AzureVmPool"}; }
 }  // namespace res

@@ -236,6 +236,41 @@ def test_metrics_and_events_exposed(node8):
     assert txt["backend"] == "fake"
 
 
+def test_namespace_gpu_quota(node8):
+    """a ResourceQuota caps the GPUs pools in a namespace may claim."""
+    from gpupool.kube import Res
+    quotas = Res("", "v1", "resourcequotas")
+    k = node8.client
+    k.create(quotas, {"metadata": {"name": "gpu-quota"},
+                      "spec": {"hard": {"requests.amd.com/gpu": "3"}}}, "team")
+    k.create(MI355XPOOLS, mi_pool("a", 2), "team")
+    wait_ready(k, "a", 2, ns="team")
+    k.create(MI355XPOOLS, mi_pool("b", 2), "team")
+    o = k.wait_for(MI355XPOOLS, "b", "team", cond_is("Progressing", "False", "QuotaExceeded"),
+                   timeout=20)
+    assert o["status"].get("readyReplicas", 0) == 0 and "gpu-quota" in \
+        conds(o)["Progressing"]["message"]
+    k.patch(MI355XPOOLS, "b", {"spec": {"replicas": 1}}, "team")
+    wait_ready(k, "b", 1, ns="team")  # 2 + 1 fits the quota
+
+
+def test_node_preflight_and_partition_surface(node8):
+    k = node8.client
+    node = k.get(NODES, "mi355x-node-0")
+    c = {x["type"]: x for x in node["status"]["conditions"]}
+    assert c["ROCmReady"]["status"] == "True" and c["GPUPoolAgentReady"]["status"] == "True"
+    assert node["metadata"]["labels"]["amd.com/gpu.family"] == "gfx950"
+    assert node["metadata"]["labels"]["amd.com/compute-partition"] == "SPX"
+    k.create(MI355XPOOLS, mi_pool("p", 1, partition={"compute": "SPX", "memory": "NPS1"}),
+             "default")
+    o = wait_ready(k, "p", 1)
+    assert o["status"]["devices"][0]["partition"] == {"compute": "SPX", "memory": "NPS1"}
+    # a pool requiring CPX mode cannot use these SPX GPUs (observed, never changed)
+    k.create(MI355XPOOLS, mi_pool("cpx", 1, partition={"compute": "CPX"}), "default")
+    k.wait_for(MI355XPOOLS, "cpx", "default", cond_is("Progressing", "False",
+                                                      "InsufficientDevices"), timeout=20)
+
+
 def test_invalid_spec_is_rejected(node8):
     with pytest.raises(KubeError):
         node8.client.create(MI355XPOOLS, mi_pool("neg", -1), "default")
