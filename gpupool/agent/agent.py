@@ -471,7 +471,7 @@ class Agent:
         if not self.cfg.apiserver:
             return
         from ..kube import NODES, Client, KubeError
-        c = Client(self.cfg.apiserver, self.cfg.token or None)
+        c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
         devs = self.snap["devices"]
         gfx = sorted({(d.get("asic") or {}).get("gfx", "") for d in devs} - {""})
         labels = {schema.LABEL_GFX: gfx[0] if gfx else "unknown",
@@ -528,7 +528,7 @@ class Agent:
 
     def _heartbeater(self) -> None:
         from ..kube import Client
-        c = Client(self.cfg.apiserver, self.cfg.token or None)
+        c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
         while not self._stop.wait(10.0):
             self._heartbeat(c)
 

@@ -18,13 +18,17 @@ def main() -> None:
     ap.add_argument("--bookmark-interval", type=float, default=5.0)
     ap.add_argument("--window", type=int, default=50000, help="watch event-log window")
     ap.add_argument("--unix", default=None, help="also listen on this unix socket")
+    ap.add_argument("--tls-cert", default=None, help="serve HTTPS with this PEM certificate chain")
+    ap.add_argument("--tls-key", default=None, help="PEM private key for --tls-cert")
+    ap.add_argument("--client-ca", default=None, help="require client certs signed by this CA")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     logging.basicConfig(level=logging.DEBUG if a.verbose else logging.WARNING,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     sim = ApiServerSim(token=a.token, bookmark_interval=a.bookmark_interval, window=a.window)
     try:
-        asyncio.run(serve(a.host, a.port, sim, a.port_file, a.crd_dir, a.unix))
+        asyncio.run(serve(a.host, a.port, sim, a.port_file, a.crd_dir, a.unix,
+                          tls_cert=a.tls_cert, tls_key=a.tls_key, client_ca=a.client_ca))
     except KeyboardInterrupt:
         pass
 

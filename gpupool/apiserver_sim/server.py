@@ -421,12 +421,25 @@ class ApiServerSim:
 
 
 async def serve(host: str, port: int, sim: ApiServerSim, port_file: str | None = None,
-                crd_dir: str | None = None, unix: str | None = None) -> None:
+                crd_dir: str | None = None, unix: str | None = None,
+                tls_cert: str | None = None, tls_key: str | None = None,
+                client_ca: str | None = None) -> None:
+    """Serve the simulator. With ``tls_cert``/``tls_key`` the TCP listener is HTTPS (TLS >= 1.2);
+    with ``client_ca`` it additionally requires a client certificate signed by that CA."""
     if crd_dir:
         load_crd_dir(sim.store, crd_dir)
     runner = web.AppRunner(sim.app, access_log=None)
     await runner.setup()
-    site = web.TCPSite(runner, host, port, reuse_address=True)
+    ssl_ctx = None
+    if tls_cert:
+        import ssl
+        ssl_ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        ssl_ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+        ssl_ctx.load_cert_chain(tls_cert, tls_key)
+        if client_ca:
+            ssl_ctx.load_verify_locations(client_ca)
+            ssl_ctx.verify_mode = ssl.CERT_REQUIRED
+    site = web.TCPSite(runner, host, port, reuse_address=True, ssl_context=ssl_ctx)
     await site.start()
     bound = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
     if unix:
@@ -438,7 +451,7 @@ async def serve(host: str, port: int, sim: ApiServerSim, port_file: str | None =
             f.write(str(bound))
         os.replace(tmp, port_file)
     log.info("apiserver-sim listening on %s:%d", host, bound)
-    print(f"apiserver-sim listening on http://{host}:{bound}", flush=True)
+    print(f"apiserver-sim listening on {'https' if ssl_ctx else 'http'}://{host}:{bound}", flush=True)
     while True:
         await asyncio.sleep(3600)
 

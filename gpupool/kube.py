@@ -71,7 +71,9 @@ BY_KIND = {
 
 
 class Client:
-    def __init__(self, server: str, token: str | None = None, timeout: float = 30.0):
+    def __init__(self, server: str, token: str | None = None, timeout: float = 30.0,
+                 ca_file: str | None = None, insecure: bool = False,
+                 client_cert: str | None = None, client_key: str | None = None):
         u = urllib.parse.urlparse(server if "://" in server else "http://" + server)
         self.scheme = u.scheme
         self.host = u.hostname or "127.0.0.1"
@@ -81,18 +83,64 @@ class Client:
         self.token = token
         self.timeout = timeout
         self._local = threading.local()
+        self._ssl = None
+        if self.scheme == "https":
+            import ssl
+            ctx = ssl.create_default_context(cafile=ca_file or os.environ.get("GPUPOOL_CA_FILE") or None)
+            ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+            if insecure:
+                ctx.check_hostname = False
+                ctx.verify_mode = ssl.CERT_NONE
+            if client_cert:
+                ctx.load_cert_chain(client_cert, client_key)
+            self._ssl = ctx
+
+    SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
     @classmethod
     def from_env(cls) -> "Client":
-        return cls(os.environ.get("GPUPOOL_APISERVER", "http://127.0.0.1:6443"),
-                   os.environ.get("GPUPOOL_TOKEN") or None)
+        """``GPUPOOL_APISERVER``/``GPUPOOL_TOKEN``/``GPUPOOL_CA_FILE`` if set, else the in-cluster
+        ServiceAccount config, else the local simulator default."""
+        server = os.environ.get("GPUPOOL_APISERVER")
+        if not server or server == "in-cluster":
+            c = cls.in_cluster()
+            if c is not None:
+                return c
+        return cls(server or "http://127.0.0.1:6443", os.environ.get("GPUPOOL_TOKEN") or None,
+                   ca_file=os.environ.get("GPUPOOL_CA_FILE") or None)
+
+    @classmethod
+    def in_cluster(cls, sa_dir: str | None = None) -> "Client | None":
+        """ServiceAccount config: https://$KUBERNETES_SERVICE_HOST:$KUBERNETES_SERVICE_PORT with the
+        mounted token and CA. None when not running in a pod."""
+        sa_dir = sa_dir or cls.SA_DIR
+        host = os.environ.get("KUBERNETES_SERVICE_HOST")
+        if not host or not os.path.exists(os.path.join(sa_dir, "token")):
+            return None
+        if ":" in host:
+            host = f"[{host}]"
+        with open(os.path.join(sa_dir, "token")) as f:
+            token = f.read().strip()
+        return cls(f"https://{host}:{os.environ.get('KUBERNETES_SERVICE_PORT', '443')}", token,
+                   ca_file=os.path.join(sa_dir, "ca.crt"))
+
+    @classmethod
+    def connect(cls, server: str, token: str | None = None) -> "Client":
+        """``server == "in-cluster"`` selects the ServiceAccount config, anything else is a URL."""
+        if server == "in-cluster":
+            c = cls.in_cluster()
+            if c is None:
+                raise RuntimeError("--apiserver in-cluster but no ServiceAccount / KUBERNETES_SERVICE_HOST")
+            return c
+        return cls(server, token)
 
     # ------------------------------------------------------------ transport
     def _conn(self, timeout: float | None = None) -> http.client.HTTPConnection:
         if self.unix:
             return _UnixHTTPConnection(self.unix, timeout=timeout or self.timeout)
         if self.scheme == "https":
-            return http.client.HTTPSConnection(self.host, self.port, timeout=timeout or self.timeout)
+            return http.client.HTTPSConnection(self.host, self.port, timeout=timeout or self.timeout,
+                                               context=self._ssl)
         return http.client.HTTPConnection(self.host, self.port, timeout=timeout or self.timeout)
 
     def _headers(self, ctype: str = "application/json", accept: str = "application/json") -> dict:

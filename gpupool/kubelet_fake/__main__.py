@@ -14,7 +14,7 @@ def main() -> None:
     ap = argparse.ArgumentParser(description="fake kubelet (device plugins + pod runtime)")
     ap.add_argument("--node", required=True)
     ap.add_argument("--apiserver", required=True)
-    ap.add_argument("--token", default=None)
+    ap.add_argument("--token", default=os.environ.get("GPUPOOL_TOKEN") or None)
     ap.add_argument("--root", required=True, help="kubelet root dir (device-plugins/, pod-resources/)")
     ap.add_argument("--workdir", default=os.getcwd(), help="cwd for pod processes")
     ap.add_argument("--no-schedule", action="store_true")

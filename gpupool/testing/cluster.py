@@ -28,6 +28,26 @@ def native_bin(name: str) -> str:
     return p
 
 
+def make_test_pki(workdir: str, name: str = "apiserver") -> tuple[str, str, str]:
+    """Throw-away CA + server certificate (SAN IP:127.0.0.1, DNS:localhost) via the openssl CLI.
+    Returns (ca.crt, server.crt, server.key)."""
+    d = os.path.join(workdir, "pki")
+    os.makedirs(d, exist_ok=True)
+    ca_key, ca_crt = os.path.join(d, "ca.key"), os.path.join(d, "ca.crt")
+    key, csr, crt = (os.path.join(d, f"{name}.{ext}") for ext in ("key", "csr", "crt"))
+    ext = os.path.join(d, f"{name}.ext")
+    with open(ext, "w") as f:
+        f.write("subjectAltName=IP:127.0.0.1,DNS:localhost\nbasicConstraints=CA:FALSE\n"
+                "keyUsage=digitalSignature,keyEncipherment\nextendedKeyUsage=serverAuth,clientAuth\n")
+    run = lambda *a: subprocess.run(["openssl", *a], check=True, capture_output=True)  # noqa: E731
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", ca_key, "-out", ca_crt,
+        "-days", "2", "-subj", f"/CN=gpupool-test-ca-{os.urandom(4).hex()}")
+    run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", key, "-out", csr, "-subj", f"/CN={name}")
+    run("x509", "-req", "-in", csr, "-CA", ca_crt, "-CAkey", ca_key, "-CAcreateserial", "-out", crt,
+        "-days", "2", "-extfile", ext)
+    return ca_crt, crt, key
+
+
 def _wait_file(path: str, timeout: float, proc: subprocess.Popen | None = None,
                logpath: str | None = None) -> str:
     deadline = time.monotonic() + timeout
@@ -61,8 +81,10 @@ class Cluster:
                  manager_args: list[str] | None = None, manager: bool = True,
                  python: str = sys.executable, env: dict | None = None,
                  sample_interval: float = 0.5, kinds: str = "mi355x,azure",
-                 manager_bin: str | None = None):
+                 manager_bin: str | None = None, tls: bool = False, token: str | None = None):
         self.workdir = os.path.abspath(workdir)
+        self.tls = tls
+        self.token = token
         os.makedirs(self.workdir, exist_ok=True)
         # unix socket paths are limited to 107 bytes: keep every socket under a short /tmp dir
         import tempfile
@@ -118,13 +140,19 @@ class Cluster:
         pf = os.path.join(self.workdir, "apiserver.port")
         if os.path.exists(pf):
             os.remove(pf)
-        p = self._spawn("apiserver", [self.python, "-m", "gpupool.apiserver_sim", "--port", "0",
-                                      "--port-file", pf, "--crd-dir",
-                                      os.path.join(ROOT, "config", "crd"),
-                                      "--bookmark-interval", "2"])
+        argv = [self.python, "-m", "gpupool.apiserver_sim", "--port", "0", "--port-file", pf,
+                "--crd-dir", os.path.join(ROOT, "config", "crd"), "--bookmark-interval", "2"]
+        if self.token:
+            argv += ["--token", self.token]
+            self.env["GPUPOOL_TOKEN"] = self.token
+        if self.tls:
+            self.ca_file, cert, key = make_test_pki(self.workdir)
+            argv += ["--tls-cert", cert, "--tls-key", key]
+            self.env["GPUPOOL_CA_FILE"] = self.ca_file
+        p = self._spawn("apiserver", argv)
         port = int(_wait_file(pf, 60, p, os.path.join(self.workdir, "apiserver.log")))
-        self.url = f"http://127.0.0.1:{port}"
-        self.client = Client(self.url)
+        self.url = f"{'https' if self.tls else 'http'}://127.0.0.1:{port}"
+        self.client = Client(self.url, self.token, ca_file=self.ca_file if self.tls else None)
 
     def kubelet_root(self, node: NodeSpec) -> str:
         return os.path.join(self.sockdir, f"k-{node.name}")
@@ -178,7 +206,15 @@ class Cluster:
         if os.path.exists(pf):
             os.remove(pf)
         argv = [self.manager_bin or native_bin("gpupool-manager"), "--apiserver", self.url, "--port-file", pf,
-                "--kinds", self.kinds, "--progress-poll", "100ms"] + self.manager_args
+                "--kinds", self.kinds, "--progress-poll", "100ms"]
+        if self.tls:
+            argv += ["--ca-file", self.ca_file]
+        if self.token:
+            tf = os.path.join(self.workdir, "token")
+            with open(tf, "w") as f:
+                f.write(self.token + "\n")
+            argv += ["--token-file", tf]
+        argv += self.manager_args
         p = self._spawn("manager", argv)
         self.metrics_port = int(_wait_file(pf, 60, p, os.path.join(self.workdir, "manager.log")))
 

@@ -16,8 +16,16 @@
 
 namespace gpupool {
 
+// TLS settings for https:// URLs (OpenSSL). ca_file empty -> system trust store.
+struct TlsOptions {
+  std::string ca_file;
+  std::string cert_file;  // client certificate (kubeconfig client-certificate)
+  std::string key_file;
+  bool insecure = false;  // skip peer verification (tests / --insecure-skip-tls-verify)
+};
+
 struct Url {
-  std::string scheme;     // http | unix
+  std::string scheme;     // http | https | unix
   std::string host;       // tcp host
   int port = 80;
   std::string unix_path;  // for unix:///path/to.sock
@@ -54,7 +62,8 @@ class ChunkedDecoder {
 
 class HttpClient {
  public:
-  explicit HttpClient(Url url, std::string bearer_token = "", int timeout_ms = 30000);
+  explicit HttpClient(Url url, std::string bearer_token = "", int timeout_ms = 30000,
+                      TlsOptions tls = {});
   ~HttpClient();
   HttpClient(const HttpClient&) = delete;
   HttpClient& operator=(const HttpClient&) = delete;
@@ -85,6 +94,8 @@ class HttpClient {
   Url url_;
   std::string token_;
   int timeout_ms_;
+  TlsOptions tls_;
+  std::shared_ptr<void> ssl_ctx_;  // SSL_CTX*, shared by all connections of this client
   std::mutex mu_;
   std::vector<std::unique_ptr<Conn>> idle_;
 };

@@ -47,7 +47,12 @@ class KubeError : public std::runtime_error {
 
 class KubeClient {
  public:
-  KubeClient(const std::string& server, const std::string& token = "", int timeout_ms = 15000);
+  KubeClient(const std::string& server, const std::string& token = "", int timeout_ms = 15000,
+             TlsOptions tls = {});
+  // In-cluster configuration (ServiceAccount): https://$KUBERNETES_SERVICE_HOST:PORT, token and
+  // CA from /var/run/secrets/kubernetes.io/serviceaccount. Returns false if not in a pod.
+  static bool in_cluster(std::string* server, std::string* token, TlsOptions* tls,
+                         const std::string& sa_dir = "/var/run/secrets/kubernetes.io/serviceaccount");
 
   Json get(const ResourceRef& r, const std::string& ns, const std::string& name,
            const std::string& sub = "");
@@ -74,6 +79,7 @@ class KubeClient {
              const std::string& ctype = "application/json");
   std::string server_;
   std::string token_;
+  TlsOptions tls_;
   std::unique_ptr<HttpClient> http_;
 };
 

@@ -65,6 +65,10 @@ struct Flags {
   int retry_period_ms = 2000;
   std::string log_level = "info";
   std::string validate;
+  // TLS / auth for a real apiserver
+  std::string ca_file, client_cert, client_key, token_file;
+  bool insecure = false;
+  bool apiserver_set = false;
 };
 
 int parse_duration_ms(const std::string& s) {
@@ -96,7 +100,14 @@ Flags parse(int argc, char** argv) {
       return argv[++i];
     };
     auto is = [&](const char* name) { return a == name || a.rfind(std::string(name) + "=", 0) == 0; };
-    if (is("--apiserver")) f.apiserver = val();
+    if (is("--apiserver")) {
+      f.apiserver = val();
+      f.apiserver_set = true;
+    } else if (is("--ca-file")) f.ca_file = val();
+    else if (is("--client-cert")) f.client_cert = val();
+    else if (is("--client-key")) f.client_key = val();
+    else if (is("--token-file")) f.token_file = val();
+    else if (a == "--insecure-skip-tls-verify") f.insecure = true;
     else if (is("--token")) f.token = val();
     else if (is("--namespace")) f.ns = val();
     else if (is("--workers")) f.workers = std::stoi(val());
@@ -266,7 +277,28 @@ int main(int argc, char** argv) {
   bool want_mi = f.kinds.find("mi355x") != std::string::npos;
   bool want_az = f.kinds.find("azure") != std::string::npos;
 
-  KubeClient client(f.apiserver, f.token);
+  TlsOptions tls;
+  tls.ca_file = f.ca_file;
+  tls.cert_file = f.client_cert;
+  tls.key_file = f.client_key;
+  tls.insecure = f.insecure;
+  if (!f.token_file.empty()) {
+    std::ifstream tf(f.token_file);
+    std::stringstream ss;
+    ss << tf.rdbuf();
+    f.token = ss.str();
+    while (!f.token.empty() && (f.token.back() == '\n' || f.token.back() == '\r')) f.token.pop_back();
+  }
+  if (!f.apiserver_set && !getenv("GPUPOOL_APISERVER")) {
+    std::string server, token;
+    TlsOptions ic;
+    if (KubeClient::in_cluster(&server, &token, &ic)) {  // running in a pod: ServiceAccount config
+      f.apiserver = server;
+      if (f.token.empty()) f.token = token;
+      if (tls.ca_file.empty()) tls.ca_file = ic.ca_file;
+    }
+  }
+  KubeClient client(f.apiserver, f.token, 15000, tls);
   std::atomic<bool> healthy{true}, leading{!f.leader_elect};
 
   HttpServer metrics;
@@ -352,14 +384,27 @@ int main(int argc, char** argv) {
       azpools.add_handler(pool_handler("AzureVmPool"));
       azpools.start();
     }
+    // Workers start only on synced caches (controller-runtime WaitForCacheSync); the wait is sliced
+    // so SIGTERM during an unreachable/untrusted apiserver still exits promptly.
+    auto wait_cache = [&](Informer& inf, const char* what) {
+      auto warn_at = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+      while (!g_stop && !inf.wait_synced(std::chrono::milliseconds(100))) {
+        if (std::chrono::steady_clock::now() > warn_at) {
+          log.warn("waiting for informer cache sync", Json::object().set("resource", what));
+          warn_at = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+        }
+      }
+    };
     if (want_mi) {
-      nodes.wait_synced(std::chrono::seconds(30));
-      mipools.wait_synced(std::chrono::seconds(30));
-      watchers.sync(rocm.node_names());
+      wait_cache(nodes, "nodes");
+      wait_cache(mipools, "mi355xpools");
     }
-    if (want_az) azpools.wait_synced(std::chrono::seconds(30));
-    ctl.start();
-    log.info("controllers running", Json());
+    if (want_az) wait_cache(azpools, "azurevmpools");
+    if (!g_stop) {
+      if (want_mi) watchers.sync(rocm.node_names());
+      ctl.start();
+      log.info("controllers running", Json());
+    }
     auto last_sweep = std::chrono::steady_clock::now();
     GaugeVec& depth = Registry::global().gauge("gpupool_workqueue_depth", "Ready keys in the work queue.");
     while (!g_stop && leading) {

@@ -14,6 +14,10 @@
 #include <chrono>
 #include <cstring>
 #include <sstream>
+
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 #include <stdexcept>
 
 namespace gpupool {
@@ -35,16 +39,16 @@ Url Url::parse(const std::string& s) {
     if (u.unix_path.empty()) throw std::invalid_argument("empty unix socket path");
     return u;
   }
-  if (u.scheme != "http") throw std::invalid_argument("unsupported scheme: " + u.scheme);
+  if (u.scheme != "http" && u.scheme != "https") throw std::invalid_argument("unsupported scheme: " + u.scheme);
   auto slash = rest.find('/');
   if (slash != std::string::npos) rest = rest.substr(0, slash);
   auto colon = rest.rfind(':');
-  if (colon != std::string::npos) {
+  if (colon != std::string::npos && rest.find(']') == std::string::npos) {
     u.host = rest.substr(0, colon);
     u.port = std::stoi(rest.substr(colon + 1));
   } else {
     u.host = rest;
-    u.port = 80;
+    u.port = u.scheme == "https" ? 443 : 80;
   }
   if (u.host.empty()) u.host = "127.0.0.1";
   return u;
@@ -159,13 +163,19 @@ bool ChunkedDecoder::feed(std::string_view in, std::string& out) {
 // ------------------------------------------------------------------ connection
 struct HttpClient::Conn {
   int fd = -1;
+  SSL* ssl = nullptr;  // non-null for https
   std::string rbuf;
   ~Conn() {
+    if (ssl) {
+      SSL_shutdown(ssl);
+      SSL_free(ssl);
+    }
     if (fd >= 0) ::close(fd);
   }
 
   // Wait for readability; returns 1 ready, 0 timeout, -1 error.
   int wait_readable(int timeout_ms) const {
+    if (ssl && SSL_pending(ssl) > 0) return 1;  // decrypted bytes already buffered
     pollfd p{fd, POLLIN, 0};
     int r;
     do {
@@ -182,6 +192,22 @@ struct HttpClient::Conn {
     if (w < 0) return -1;
     char buf[65536];
     ssize_t n;
+    if (ssl) {
+      for (;;) {
+        int r = SSL_read(ssl, buf, sizeof buf);
+        if (r > 0) {
+          rbuf.append(buf, static_cast<size_t>(r));
+          return r;
+        }
+        int e = SSL_get_error(ssl, r);
+        if (e == SSL_ERROR_ZERO_RETURN) return 0;
+        if (e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) {
+          if (wait_readable(timeout_ms) <= 0) return -2;
+          continue;
+        }
+        return e == SSL_ERROR_SYSCALL && r == 0 ? 0 : -1;
+      }
+    }
     do {
       n = ::recv(fd, buf, sizeof buf, 0);
     } while (n < 0 && errno == EINTR);
@@ -190,6 +216,19 @@ struct HttpClient::Conn {
   }
 
   bool send_all(const std::string& data) const {
+    if (ssl) {
+      size_t off = 0;
+      while (off < data.size()) {
+        int r = SSL_write(ssl, data.data() + off, static_cast<int>(data.size() - off));
+        if (r <= 0) {
+          int e = SSL_get_error(ssl, r);
+          if (e == SSL_ERROR_WANT_WRITE || e == SSL_ERROR_WANT_READ) continue;
+          return false;
+        }
+        off += static_cast<size_t>(r);
+      }
+      return true;
+    }
     size_t off = 0;
     while (off < data.size()) {
       ssize_t n = ::send(fd, data.data() + off, data.size() - off, MSG_NOSIGNAL);
@@ -203,8 +242,42 @@ struct HttpClient::Conn {
   }
 };
 
-HttpClient::HttpClient(Url url, std::string bearer_token, int timeout_ms)
-    : url_(std::move(url)), token_(std::move(bearer_token)), timeout_ms_(timeout_ms) {}
+namespace {
+std::string ssl_errors() {
+  std::string out;
+  unsigned long e;
+  char buf[256];
+  while ((e = ERR_get_error()) != 0) {
+    ERR_error_string_n(e, buf, sizeof buf);
+    if (!out.empty()) out += "; ";
+    out += buf;
+  }
+  return out.empty() ? "unknown TLS error" : out;
+}
+}  // namespace
+
+HttpClient::HttpClient(Url url, std::string bearer_token, int timeout_ms, TlsOptions tls)
+    : url_(std::move(url)), token_(std::move(bearer_token)), timeout_ms_(timeout_ms), tls_(std::move(tls)) {
+  if (url_.scheme != "https") return;
+  SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+  if (!ctx) throw HttpError("SSL_CTX_new: " + ssl_errors());
+  ssl_ctx_ = std::shared_ptr<void>(ctx, [](void* p) { SSL_CTX_free(static_cast<SSL_CTX*>(p)); });
+  SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+  if (tls_.insecure) {
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_NONE, nullptr);
+  } else {
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+    int ok = tls_.ca_file.empty() ? SSL_CTX_set_default_verify_paths(ctx)
+                                  : SSL_CTX_load_verify_locations(ctx, tls_.ca_file.c_str(), nullptr);
+    if (ok != 1) throw HttpError("loading CA " + tls_.ca_file + ": " + ssl_errors());
+  }
+  if (!tls_.cert_file.empty()) {
+    if (SSL_CTX_use_certificate_chain_file(ctx, tls_.cert_file.c_str()) != 1 ||
+        SSL_CTX_use_PrivateKey_file(ctx, tls_.key_file.empty() ? tls_.cert_file.c_str() : tls_.key_file.c_str(),
+                                    SSL_FILETYPE_PEM) != 1)
+      throw HttpError("client certificate: " + ssl_errors());
+  }
+}
 
 HttpClient::~HttpClient() = default;
 
@@ -261,6 +334,32 @@ std::unique_ptr<HttpClient::Conn> HttpClient::connect_(int timeout_ms) {
   }
   freeaddrinfo(res);
   if (c->fd < 0) throw HttpError("connect " + url_.str() + ": " + last_err);
+  if (ssl_ctx_) {
+    c->ssl = SSL_new(static_cast<SSL_CTX*>(ssl_ctx_.get()));
+    if (!c->ssl) throw HttpError("SSL_new: " + ssl_errors());
+    SSL_set_fd(c->ssl, c->fd);
+    in6_addr a6{};
+    in_addr a4{};
+    bool is_ip = inet_pton(AF_INET, url_.host.c_str(), &a4) == 1 || inet_pton(AF_INET6, url_.host.c_str(), &a6) == 1;
+    if (!is_ip) SSL_set_tlsext_host_name(c->ssl, url_.host.c_str());  // SNI
+    if (!tls_.insecure) {
+      X509_VERIFY_PARAM* vp = SSL_get0_param(c->ssl);
+      if (is_ip) X509_VERIFY_PARAM_set1_ip_asc(vp, url_.host.c_str());
+      else X509_VERIFY_PARAM_set1_host(vp, url_.host.c_str(), 0);
+    }
+    // blocking handshake bounded by the socket timeout
+    timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
+    setsockopt(c->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    setsockopt(c->fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+    if (SSL_connect(c->ssl) != 1) {
+      long vr = SSL_get_verify_result(c->ssl);
+      std::string why = vr != X509_V_OK ? X509_verify_cert_error_string(vr) : ssl_errors();
+      throw HttpError("TLS handshake with " + url_.str() + ": " + why);
+    }
+    timeval zero{0, 0};
+    setsockopt(c->fd, SOL_SOCKET, SO_RCVTIMEO, &zero, sizeof zero);
+    setsockopt(c->fd, SOL_SOCKET, SO_SNDTIMEO, &zero, sizeof zero);
+  }
   return c;
 }
 

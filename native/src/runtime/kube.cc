@@ -1,5 +1,9 @@
 #include "gpupool/kube.h"
 
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+
 #include "gpupool/generated/schema_consts.h"
 
 namespace gpupool {
@@ -25,8 +29,26 @@ ResourceRef mi355xpools() { return {gen::kGroup, gen::kVersion, gen::kPluralMi35
 ResourceRef azurevmpools() { return {gen::kGroup, gen::kVersion, gen::kPluralAzureVmPool, true, "AzureVmPool"}; }
 }  // namespace res
 
-KubeClient::KubeClient(const std::string& server, const std::string& token, int timeout_ms)
-    : server_(server), token_(token), http_(std::make_unique<HttpClient>(Url::parse(server), token, timeout_ms)) {}
+KubeClient::KubeClient(const std::string& server, const std::string& token, int timeout_ms, TlsOptions tls)
+    : server_(server), token_(token), tls_(tls),
+      http_(std::make_unique<HttpClient>(Url::parse(server), token, timeout_ms, std::move(tls))) {}
+
+bool KubeClient::in_cluster(std::string* server, std::string* token, TlsOptions* tls, const std::string& sa_dir) {
+  const char* host = getenv("KUBERNETES_SERVICE_HOST");
+  const char* port = getenv("KUBERNETES_SERVICE_PORT");
+  if (!host || !*host) return false;
+  std::ifstream tf(sa_dir + "/token");
+  if (!tf) return false;
+  std::stringstream ss;
+  ss << tf.rdbuf();
+  *token = ss.str();
+  while (!token->empty() && (token->back() == '\n' || token->back() == '\r')) token->pop_back();
+  std::string h = host;
+  if (h.find(':') != std::string::npos) h = "[" + h + "]";  // IPv6 service IP
+  *server = "https://" + h + ":" + std::string(port && *port ? port : "443");
+  tls->ca_file = sa_dir + "/ca.crt";
+  return true;
+}
 
 static KubeError to_error(const HttpResponse& r, const std::string& what) {
   std::string reason, msg = what + ": HTTP " + std::to_string(r.status);
@@ -101,7 +123,7 @@ std::string KubeClient::watch(const ResourceRef& r, const std::string& ns, const
                   std::to_string(timeout_seconds);
   if (!rv.empty()) p += "&resourceVersion=" + url_encode(rv);
   // A dedicated client per stream: watches are long-lived and must not hold pooled sockets.
-  HttpClient stream(http_->url(), token_, 15000);
+  HttpClient stream(http_->url(), token_, 15000, tls_);
   std::string last = rv;
   std::string err_body;
   int status = stream.stream_lines(

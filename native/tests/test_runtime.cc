@@ -1,6 +1,11 @@
 // Unit tests: JSON DOM/parser (incl. a randomized fuzz loop), chunked decoding, work queue
 // semantics, metrics, conditions, validation. Run under ASan/UBSan and TSan via `make SAN=...`.
+#include <unistd.h>
+
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
 #include <random>
 #include <set>
 #include <thread>
@@ -8,6 +13,7 @@
 #include "gpupool/api.h"
 #include "gpupool/http.h"
 #include "gpupool/json.h"
+#include "gpupool/kube.h"
 #include "gpupool/log.h"
 #include "gpupool/metrics.h"
 #include "gpupool/workqueue.h"
@@ -105,6 +111,34 @@ TEST(url_parse) {
   Url x = Url::parse("unix:///tmp/agent.sock");
   EXPECT_EQ(x.unix_path, std::string("/tmp/agent.sock"));
   EXPECT_THROW(Url::parse("ftp://x"));
+  Url s = Url::parse("https://kubernetes.default.svc");
+  EXPECT_EQ(s.scheme, std::string("https"));
+  EXPECT_EQ(s.port, 443);
+}
+
+TEST(kube_in_cluster_config) {
+  char tmpl[] = "/tmp/gp-sa-XXXXXX";
+  std::string dir = mkdtemp(tmpl);
+  { std::ofstream(dir + "/token") << "abc.def\n"; }
+  { std::ofstream(dir + "/ca.crt") << "-----BEGIN CERTIFICATE-----\n"; }
+  std::string server, token;
+  TlsOptions tls;
+  unsetenv("KUBERNETES_SERVICE_HOST");
+  EXPECT_TRUE(!KubeClient::in_cluster(&server, &token, &tls, dir));
+  setenv("KUBERNETES_SERVICE_HOST", "10.96.0.1", 1);
+  setenv("KUBERNETES_SERVICE_PORT", "6443", 1);
+  EXPECT_TRUE(KubeClient::in_cluster(&server, &token, &tls, dir));
+  EXPECT_EQ(server, std::string("https://10.96.0.1:6443"));
+  EXPECT_EQ(token, std::string("abc.def"));
+  EXPECT_EQ(tls.ca_file, dir + "/ca.crt");
+  setenv("KUBERNETES_SERVICE_HOST", "fd00::1", 1);
+  EXPECT_TRUE(KubeClient::in_cluster(&server, &token, &tls, dir));
+  EXPECT_EQ(server, std::string("https://[fd00::1]:6443"));
+  unsetenv("KUBERNETES_SERVICE_HOST");
+  unsetenv("KUBERNETES_SERVICE_PORT");
+  std::remove((dir + "/token").c_str());
+  std::remove((dir + "/ca.crt").c_str());
+  rmdir(dir.c_str());
 }
 
 TEST(workqueue_dedup_and_processing) {
