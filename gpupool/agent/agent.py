@@ -248,6 +248,15 @@ class Agent:
         policy = req.get("policy") or {}
         resource = req.get("resourceName") or schema.DEFAULT_RESOURCE
         probe_opts = req.get("probe") or {}
+        timings: dict[str, float] = {}  # phase -> ms, returned to the manager as trace spans
+        t_phase = time.perf_counter()
+
+        def lap(name: str) -> None:
+            nonlocal t_phase
+            t = time.perf_counter()
+            timings[name] = round((t - t_phase) * 1e3, 3)
+            t_phase = t
+
         with self.lock:
             quarantined = self.ledger.quarantined()
             free = []
@@ -272,6 +281,7 @@ class Agent:
                                    f"{len(free)} available (all-or-nothing)", "devices": []}
             by_index = {d["index"]: d for d in self.snap["devices"]}
             chosen = [by_index[i] for i in sel]
+            lap("select")
             ts = now_rfc3339()
             for d in chosen:
                 rec = {"uuid": d["uuid"], "poolUID": pool_uid, "pool": req.get("pool", ""),
@@ -281,11 +291,13 @@ class Agent:
                 self.records[d["uuid"]] = rec
             self.ledger.commit(self.records)  # durable before probing: no double claim on crash
             self.stats["claims"] += len(chosen)
+        lap("commit")
         # probes run outside the lock, concurrently across GPUs
         t0 = time.perf_counter()
         results = self.prober.probe_many(chosen, {**probe_opts, "enabled":
                                                   probe_opts.get("enabled", True)})
         probe_wall = (time.perf_counter() - t0) * 1e3
+        lap("probe")
         with self.lock:
             for d, res in zip(chosen, results):
                 rec = self.records.get(d["uuid"])
@@ -299,15 +311,18 @@ class Agent:
                     self.stats["probe_failures"] += 1
             self.ledger.commit(self.records)
             self._evaluate_all()
+        lap("commit2")
         self._ensure_plugin(resource)
         self._notify_plugins()
         self._wait_advertised(resource, [d["uuid"] for d in chosen])
+        lap("advertise")
         pods = self._pods_by_device()
         with self.lock:
             views = [self.device_view(d["uuid"], pods) for d in chosen]
+        lap("view")
         log.info("claimed %d GPU(s) for %s: %s (probe wall %.1f ms)", len(chosen),
                  req.get("pool"), [d["index"] for d in chosen], probe_wall)
-        return {"ok": True, "devices": views, "probeWallMs": probe_wall}
+        return {"ok": True, "devices": views, "probeWallMs": probe_wall, "timingsMs": timings}
 
     def cordon(self, pool_uid: str, uuids: list[str]) -> dict:
         with self.lock:

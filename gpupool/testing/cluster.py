@@ -262,3 +262,12 @@ class Cluster:
         import urllib.request
         with urllib.request.urlopen(f"http://127.0.0.1:{self.metrics_port}/metrics", timeout=5) as r:
             return r.read().decode()
+
+    def manager_traces(self, key: str = "", n: int = 64) -> list:
+        """Recent reconcile traces from the manager's /debug/traces (newest first)."""
+        import urllib.parse
+        import urllib.request
+        q = urllib.parse.urlencode({"n": n, **({"key": key} if key else {})})
+        with urllib.request.urlopen(f"http://127.0.0.1:{self.metrics_port}/debug/traces?{q}",
+                                    timeout=5) as r:
+            return json.loads(r.read())

@@ -128,5 +128,6 @@ class HttpServer {
 };
 
 std::string url_encode(std::string_view s);
+std::string url_decode(std::string_view s);  // %XX and '+' (query strings)
 
 }  // namespace gpupool

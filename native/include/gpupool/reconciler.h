@@ -24,6 +24,7 @@
 #include "gpupool/log.h"
 #include "gpupool/metrics.h"
 #include "gpupool/provider.h"
+#include "gpupool/trace.h"
 #include "gpupool/workqueue.h"
 
 namespace gpupool {

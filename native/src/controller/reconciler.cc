@@ -62,6 +62,7 @@ PoolReconcilerBase::PoolReconcilerBase(KubeClient& client, Informer& pools, Even
       log_(Logger("reconciler").with("kind", kind_)) {}
 
 void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
+  trace::Span span("status");
   Json cur = obj;
   const std::string ns = obj.path("metadata.namespace").as_string();
   const std::string name = obj.path("metadata.name").as_string();
@@ -84,6 +85,7 @@ void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
 Json PoolReconcilerBase::ensure_finalizer_(const Json& obj) {
   ObjectMeta m = ObjectMeta::from(obj);
   if (m.has_finalizer(gen::kFinalizer)) return obj;
+  trace::Span span("finalizer");
   Json fins = Json::array();
   for (const auto& f : m.finalizers) fins.push_back(f);
   fins.push_back(gen::kFinalizer);
@@ -142,6 +144,7 @@ Mi355xPoolReconciler::Mi355xPoolReconciler(KubeClient& client, Informer& pools, 
 
 Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& m, const Mi355xPoolSpec& spec,
                                                               const Json& status) {
+  trace::Span span("observe");
   Observed o;
   std::vector<std::string> nodes;
   std::string hint = status["nodeName"].as_string();
@@ -208,6 +211,7 @@ std::string Mi355xPoolReconciler::choose_node_(const Mi355xPoolSpec& spec, int n
 
 int Mi355xPoolReconciler::drain_(const Json& obj, const std::string& node, const ObjectMeta& m,
                                  const Mi355xPoolSpec& spec, std::vector<DeviceView>& mine) {
+  trace::Span span("drain");
   int still = 0;
   std::vector<std::string> release;
   auto now = std::chrono::system_clock::now();
@@ -581,6 +585,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
 // may claim. Usage = status.replicas of the other pools (informer cache) + our claimed + delta.
 bool Mi355xPoolReconciler::quota_allows_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta,
                                          std::string* why) {
+  trace::Span span("quota");
   Json quotas;
   try {
     quotas = client_.list(res::resourcequotas(), m.ns);
@@ -894,14 +899,19 @@ void Controller::worker_() {
     }
     auto t0 = clock_t_::now();
     Outcome out;
-    try {
-      out = it->second->reconcile(ns, name);
-    } catch (const std::exception& e) {
-      out = Outcome::transient(e.what());
+    static const char* names[] = {"done", "requeue", "error", "terminal"};
+    {
+      trace::Trace tr(key);
+      try {
+        out = it->second->reconcile(ns, name);
+      } catch (const std::exception& e) {
+        out = Outcome::transient(e.what());
+      }
+      if (!out.message.empty()) tr.attr("reason", out.message);
+      tr.finish(names[out.kind]);
     }
     double secs = std::chrono::duration<double>(clock_t_::now() - t0).count();
     reconciles_++;
-    static const char* names[] = {"done", "requeue", "error", "terminal"};
     reconcile_total().inc({{"kind", kind}, {"result", names[out.kind]}});
     reconcile_hist().observe({{"kind", kind}}, secs);
     switch (out.kind) {

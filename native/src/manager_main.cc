@@ -11,6 +11,7 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstring>
 #include <fstream>
@@ -31,6 +32,7 @@
 #include "gpupool/metrics.h"
 #include "gpupool/provider.h"
 #include "gpupool/reconciler.h"
+#include "gpupool/trace.h"
 
 using namespace gpupool;
 
@@ -64,6 +66,7 @@ struct Flags {
   int renew_deadline_ms = 10000;
   int retry_period_ms = 2000;
   std::string log_level = "info";
+  int slow_reconcile_ms = 1000;
   std::string validate;
   // TLS / auth for a real apiserver
   std::string ca_file, client_cert, client_key, token_file;
@@ -79,6 +82,36 @@ int parse_duration_ms(const std::string& s) {
   if (s.back() == 'm') return static_cast<int>(v * 60000);
   return static_cast<int>(v);  // bare number = ms
 }
+
+const char* kUsage = R"(gpupool-manager: Mi355xPool / AzureVmPool operator
+
+connection (default: in-cluster ServiceAccount config, else http://127.0.0.1:6443):
+  --apiserver URL              http(s)://host:port or unix:///path   [$GPUPOOL_APISERVER]
+  --token T | --token-file F   bearer token                            [$GPUPOOL_TOKEN]
+  --ca-file F                  CA bundle to verify the apiserver certificate
+  --client-cert F --client-key F   client certificate authentication
+  --insecure-skip-tls-verify   do not verify the apiserver certificate (testing only)
+controllers:
+  --kinds mi355x,azure         reconcilers to run            --namespace NS   watch one namespace
+  --workers N (4)              reconcile worker threads      --resync D (10s) steady-state resync
+  --progress-poll D (250ms)    requeue while scaling/draining
+  --credentials-retry D (30s)  AzureVmPool retry after a credentials error
+  --agent-timeout D (60s)      node-agent RPC timeout (covers on-claim GPU probes)
+  --orphan-sweep D (30s)       release claims whose pool no longer exists
+leader election:
+  --leader-elect  --lease-namespace NS (gpupool-system)  --identity ID
+  --lease-duration D (15s)  --renew-deadline D (10s)  --retry-period D (2s)
+observability:
+  --metrics-addr H:P (127.0.0.1:0)  /metrics /healthz /readyz /debug/traces
+  --health-addr H:P                 separate /healthz listener
+  --port-file F                     write the bound metrics port here
+  --log-level debug|info|warn|error --slow-reconcile D (1s) log traces slower than D at info
+fake cloud (AzureVmPool):
+  --fakecloud-state F  --fakecloud-faults F  --fakecloud-provision-ms N  --fakecloud-deprovision-ms N
+tools:
+  --validate obj.json          print validation errors (JSON) for one object and exit
+durations: 250ms, 10s, 5m or bare milliseconds.
+)";
 
 Flags parse(int argc, char** argv) {
   Flags f;
@@ -131,9 +164,10 @@ Flags parse(int argc, char** argv) {
     else if (is("--renew-deadline")) f.renew_deadline_ms = parse_duration_ms(val());
     else if (is("--retry-period")) f.retry_period_ms = parse_duration_ms(val());
     else if (is("--log-level")) f.log_level = val();
+    else if (is("--slow-reconcile")) f.slow_reconcile_ms = parse_duration_ms(val());
     else if (is("--validate")) f.validate = val();
     else if (a == "-h" || a == "--help") {
-      std::cout << "see the header of native/src/manager_main.cc for flags\n";
+      std::cout << kUsage;
       std::exit(0);
     } else {
       std::cerr << "unknown flag " << a << "\n";
@@ -270,6 +304,7 @@ int main(int argc, char** argv) {
   Flags f = parse(argc, argv);
   if (!f.validate.empty()) return run_validate(f.validate);
   Logger::set_level(Logger::parse_level(f.log_level));
+  trace::set_slow_threshold(std::chrono::milliseconds(f.slow_reconcile_ms));
   signal(SIGINT, on_signal);
   signal(SIGTERM, on_signal);
   signal(SIGPIPE, SIG_IGN);
@@ -315,6 +350,32 @@ int main(int argc, char** argv) {
     return r;
   };
   metrics.route("/healthz", health);
+  // recent reconcile traces (newest first); ?n=N, ?key=substring filters by "Kind/ns/name"
+  metrics.route("/debug/traces", [](const std::string&, const std::string& target, const std::string&) {
+    size_t n = 64;
+    std::string key;
+    auto q = target.find('?');
+    if (q != std::string::npos) {
+      std::istringstream qs(target.substr(q + 1));
+      std::string kv;
+      while (std::getline(qs, kv, '&')) {
+        auto eq = kv.find('=');
+        if (eq == std::string::npos) continue;
+        if (kv.substr(0, eq) == "n") n = static_cast<size_t>(std::max(1, std::atoi(kv.c_str() + eq + 1)));
+        else if (kv.substr(0, eq) == "key") key = url_decode(kv.substr(eq + 1));
+      }
+    }
+    Json all = trace::recent(key.empty() ? n : 256);
+    Json out = Json::array();
+    for (const auto& t : all.elements()) {
+      if (out.size() >= n) break;
+      if (key.empty() || t["key"].as_string().find(key) != std::string::npos) out.push_back(t);
+    }
+    HttpServer::Reply r;
+    r.content_type = "application/json";
+    r.body = out.dump() + "\n";
+    return r;
+  });
   metrics.route("/readyz", [&](const std::string&, const std::string&, const std::string&) {
     HttpServer::Reply r;
     r.status = leading ? 200 : 503;

@@ -6,6 +6,7 @@
 #include "gpupool/generated/schema_consts.h"
 #include "gpupool/informer.h"
 #include "gpupool/provider.h"
+#include "gpupool/trace.h"
 
 namespace gpupool {
 
@@ -104,6 +105,7 @@ HttpClient& RocmProvider::client_for(const std::string& node) {
 }
 
 Json RocmProvider::post_(const std::string& node, const std::string& path, const Json& body) {
+  trace::Span span("agent:POST " + path);
   HttpClient& c = client_for(node);
   HttpResponse r;
   try {
@@ -125,6 +127,7 @@ NodeView RocmProvider::observe(const std::string& node) {
   NodeView nv;
   nv.name = node;
   nv.endpoint = endpoint_of(node);
+  trace::Span span("agent:GET /v1/node");
   try {
     HttpClient& c = client_for(node);
     HttpResponse r = c.request("GET", "/v1/node");
@@ -161,6 +164,8 @@ ClaimResult RocmProvider::claim(const std::string& node, const ClaimRequest& req
   out.reason = r["reason"].as_string();
   out.message = r["message"].as_string();
   for (const auto& d : r["devices"].elements()) out.devices.push_back(DeviceView::from(d));
+  // the agent's own phase timings (select/commit/probe/advertise) become child spans
+  for (const auto& kv : r["timingsMs"].members()) trace::add_span("agent.claim." + kv.first, kv.second.as_double(0));
   return out;
 }
 

@@ -74,6 +74,27 @@ std::string url_encode(std::string_view s) {
   return out;
 }
 
+std::string url_decode(std::string_view s) {
+  auto hexval = [](char c) -> int {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  };
+  std::string out;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && hexval(s[i + 1]) >= 0 && hexval(s[i + 2]) >= 0) {
+      out.push_back(static_cast<char>(hexval(s[i + 1]) * 16 + hexval(s[i + 2])));
+      i += 2;
+    } else if (s[i] == '+') {
+      out.push_back(' ');
+    } else {
+      out.push_back(s[i]);
+    }
+  }
+  return out;
+}
+
 // ------------------------------------------------------------------ chunked
 bool ChunkedDecoder::feed(std::string_view in, std::string& out) {
   size_t i = 0;

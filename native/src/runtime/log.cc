@@ -1,5 +1,7 @@
 #include "gpupool/log.h"
 
+#include "gpupool/trace.h"
+
 #include <cstdio>
 #include <ctime>
 
@@ -37,6 +39,8 @@ void Logger::log(LogLevel lvl, const std::string& msg, Json fields) const {
   rec["level"] = names[static_cast<int>(lvl)];
   rec["logger"] = name_;
   rec["msg"] = msg;
+  // every line logged inside a reconcile pass carries that pass's reconcileID
+  if (trace::Trace* t = trace::Trace::current()) rec["reconcileID"] = t->id();
   for (const auto& kv : ctx_.members()) rec[kv.first] = kv.second;
   for (const auto& kv : fields.members()) rec[kv.first] = kv.second;
   std::string line = rec.dump();

@@ -16,6 +16,7 @@
 #include "gpupool/kube.h"
 #include "gpupool/log.h"
 #include "gpupool/metrics.h"
+#include "gpupool/trace.h"
 #include "gpupool/workqueue.h"
 #include "testing.h"
 
@@ -114,6 +115,41 @@ TEST(url_parse) {
   Url s = Url::parse("https://kubernetes.default.svc");
   EXPECT_EQ(s.scheme, std::string("https"));
   EXPECT_EQ(s.port, 443);
+}
+
+TEST(trace_spans_ring_and_scoping) {
+  trace::reset();
+  trace::add_span("orphan", 1.0);  // no active trace: no-op
+  EXPECT_EQ(trace::current_id(), std::string());
+  std::string outer_id;
+  {
+    trace::Trace t("Mi355xPool/default/p");
+    outer_id = t.id();
+    EXPECT_EQ(trace::current_id(), outer_id);
+    { trace::Span s("observe"); }
+    trace::add_span("agent.claim.probe", 2.5);
+    {
+      trace::Trace inner("AzureVmPool/default/q");  // nested: restores the outer on close
+      EXPECT_TRUE(trace::current_id() != outer_id);
+    }
+    EXPECT_EQ(trace::current_id(), outer_id);
+    t.attr("reason", "ScalingUp");
+    t.finish("requeue");
+  }
+  EXPECT_EQ(trace::current_id(), std::string());
+  Json r = trace::recent(10);
+  EXPECT_EQ(r.size(), static_cast<size_t>(2));
+  const Json& last = r.elements()[0];  // newest first: the outer finished last
+  EXPECT_EQ(last["reconcileID"].as_string(), outer_id);
+  EXPECT_EQ(last["result"].as_string(), std::string("requeue"));
+  EXPECT_EQ(last["spans"].size(), static_cast<size_t>(2));
+  EXPECT_EQ(last["spans"].elements()[0]["name"].as_string(), std::string("observe"));
+  EXPECT_EQ(last["spans"].elements()[1]["ms"].as_double(), 2.5);
+  EXPECT_EQ(last.path("attrs.reason").as_string(), std::string("ScalingUp"));
+  for (int i = 0; i < 300; ++i) trace::Trace t("X/y/" + std::to_string(i));
+  EXPECT_EQ(trace::recent(1000).size(), static_cast<size_t>(256));
+  EXPECT_EQ(url_decode("Mi355xPool%2Fdefault%2Fa+b"), std::string("Mi355xPool/default/a b"));
+  trace::reset();
 }
 
 TEST(kube_in_cluster_config) {

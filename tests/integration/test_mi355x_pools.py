@@ -228,12 +228,39 @@ def test_metrics_and_events_exposed(node8):
     k = node8.client
     k.create(MI355XPOOLS, mi_pool("p", 2), "default")
     wait_ready(k, "p", 2)
-    m = node8.manager_metrics()
+    # the gauges are set right after the status write the watch just delivered: poll briefly
+    deadline = time.monotonic() + 5
+    while True:
+        m = node8.manager_metrics()
+        if 'gpupool_ready_replicas{kind="Mi355xPool",pool="default/p"} 2' in m or \
+                time.monotonic() > deadline:
+            break
+        time.sleep(0.05)
     assert "gpupool_reconcile_total" in m and "gpupool_reconcile_to_ready_seconds_bucket" in m
     assert 'gpupool_ready_replicas{kind="Mi355xPool",pool="default/p"} 2' in m
     am = node8.agent_request.__self__  # cluster
     txt = am.agent_request("mi355x-node-0", "GET", "/v1/node")
     assert txt["backend"] == "fake"
+
+
+def test_reconcile_traces(node8):
+    """SURVEY §5 tracing: each reconcile pass is a trace with per-phase spans (incl. the node
+    agent's own claim phases), served at /debug/traces and exported as a span histogram."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("tr", 2), "default")
+    wait_ready(k, "tr", 2)
+    traces = node8.manager_traces(key="Mi355xPool/default/tr", n=50)
+    assert traces and all(t["key"] == "Mi355xPool/default/tr" for t in traces)
+    claim = [t for t in traces if any(s["name"] == "agent:POST /v1/claims" for s in t["spans"])]
+    assert len(claim) == 1, traces
+    names = [s["name"] for s in claim[0]["spans"]]
+    for want in ("observe", "agent:GET /v1/node", "agent.claim.select", "agent.claim.probe",
+                 "agent.claim.advertise", "status"):
+        assert want in names, names
+    assert claim[0]["totalMs"] >= max(s["ms"] for s in claim[0]["spans"]) - 1e-6
+    assert len(claim[0]["reconcileID"]) == 16
+    m = node8.manager_metrics()
+    assert 'gpupool_reconcile_span_seconds_count{kind="Mi355xPool",span="observe"}' in m
 
 
 def test_namespace_gpu_quota(node8):
