@@ -63,12 +63,12 @@ docker-push:
 
 deploy: manifests
 	$(GPUCTL) apply -f config/crd
+	$(GPUCTL) apply -f config/manager   # creates the gpupool-system namespace first
 	$(GPUCTL) apply -f config/rbac
-	$(GPUCTL) apply -f config/manager
 	$(GPUCTL) apply -f config/agent
 
 undeploy:
-	$(GPUCTL) delete -f config/agent; $(GPUCTL) delete -f config/manager
+	$(GPUCTL) delete -f config/agent; $(GPUCTL) delete -f config/rbac; $(GPUCTL) delete -f config/manager
 
 clean:
 	rm -rf build

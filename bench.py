@@ -178,7 +178,23 @@ def main() -> int:
             metrics = cluster.manager_metrics()
         except Exception:
             metrics = ""
+        try:
+            traces = cluster.manager_traces(key=f"Mi355xPool/{ns}/{name}", n=256)
+        except Exception:
+            traces = []
         cluster.stop()
+        # latency breakdown of the scale-up passes (the reconcile that claims): median per span
+        claim_traces = [t for t in traces
+                        if any(s["name"] == "agent:POST /v1/claims" for s in t["spans"])][:args.steps]
+        span_ms: dict[str, list[float]] = {}
+        for t in claim_traces:
+            per: dict[str, float] = {}
+            for s in t["spans"]:
+                per[s["name"]] = per.get(s["name"], 0.0) + s["ms"]
+            per["total"] = t["totalMs"]
+            for k2, v in per.items():
+                span_ms.setdefault(k2, []).append(v)
+        span_p50 = {k2: round(statistics.median(v), 3) for k2, v in sorted(span_ms.items())}
         p50 = statistics.median(lat) if lat else float("nan")
         lat_sorted = sorted(lat)
         p90 = lat_sorted[min(len(lat_sorted) - 1, int(0.9 * len(lat_sorted)))] if lat else None
@@ -211,6 +227,7 @@ def main() -> int:
                 "max_s": round(max(lat), 4) if lat else None,
                 "readyReplicas_accuracy": accuracy,
                 "world_size": world,
+                "claim_pass_span_p50_ms": span_p50,
                 "steps_detail": details[:3],
             },
         }
@@ -221,6 +238,8 @@ def main() -> int:
             print(f"# workdir kept: {cluster.workdir}", file=sys.stderr)
             with open(os.path.join(cluster.workdir, "manager_metrics.txt"), "w") as f:
                 f.write(metrics)
+            with open(os.path.join(cluster.workdir, "traces.json"), "w") as f:
+                json.dump(traces, f, indent=1)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -318,6 +318,30 @@ def rbac_role() -> dict:
         {"apiGroups": [""], "resources": ["nodes"], "verbs": ["get", "list", "watch", "patch"]},
         {"apiGroups": ["coordination.k8s.io"], "resources": ["leases"],
          "verbs": ["get", "create", "update"]},
+        {"apiGroups": [""], "resources": ["resourcequotas"], "verbs": ["get", "list", "watch"]},
     ]
     return {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
             "metadata": {"name": "gpupool-manager-role"}, "rules": rules}
+
+
+AGENT_NAMESPACE = "gpupool-system"
+
+
+def agent_rbac() -> list[dict]:
+    """ServiceAccount + ClusterRole + binding for the node agent DaemonSet: it registers its Node
+    (labels, agent-endpoint annotation) and heartbeats the GPUPoolAgentReady/ROCmReady node
+    conditions; device/pod facts come from the kubelet's local sockets, not the API."""
+    sa = {"apiVersion": "v1", "kind": "ServiceAccount",
+          "metadata": {"name": "gpupool-agent", "namespace": AGENT_NAMESPACE}}
+    role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+            "metadata": {"name": "gpupool-agent-role"},
+            "rules": [{"apiGroups": [""], "resources": ["nodes"],
+                       "verbs": ["get", "create", "patch"]},
+                      {"apiGroups": [""], "resources": ["nodes/status"], "verbs": ["patch"]}]}
+    binding = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
+               "metadata": {"name": "gpupool-agent-rolebinding"},
+               "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",
+                           "name": "gpupool-agent-role"},
+               "subjects": [{"kind": "ServiceAccount", "name": "gpupool-agent",
+                             "namespace": AGENT_NAMESPACE}]}
+    return [sa, role, binding]

@@ -67,6 +67,10 @@ BY_KIND = {
     "ClusterRoleBinding": Res("rbac.authorization.k8s.io", "v1", "clusterrolebindings",
                               namespaced=False),
     "ResourceQuota": Res("", "v1", "resourcequotas"),
+    "ServiceAccount": Res("", "v1", "serviceaccounts"),
+    "Service": Res("", "v1", "services"),
+    "Deployment": Res("apps", "v1", "deployments"),
+    "DaemonSet": Res("apps", "v1", "daemonsets"),
 }
 
 

@@ -87,6 +87,8 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
   Outcome reconcile(const std::string& ns, const std::string& name) override;
   // Releases claims whose pool no longer exists (manager restart / force-deleted CR).
   void sweep_orphans();
+  // ResourceQuota cache; without one (or before it syncs) quota checks LIST from the API.
+  void set_quota_informer(Informer* q) { quotas_ = q; }
 
  private:
   struct Observed {
@@ -108,6 +110,7 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
                      bool deleting);
 
   DeviceProvider& provider_;
+  Informer* quotas_ = nullptr;
   std::map<std::string, std::set<std::string>> evicted_;  // pool uid -> pod keys already evicted
   std::map<std::string, int64_t> policy_gen_;             // pool uid -> generation pushed to agents
 };

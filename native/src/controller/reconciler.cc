@@ -449,6 +449,9 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
   std::string progress_reason, progress_msg;
   std::string blocked;  // reason scale-up is blocked (InsufficientDevices | QuotaExceeded)
   bool acted = false;
+  bool claimed_only = false;  // the only action was a successful claim
+  std::vector<DeviceView> claimed;
+  std::string claimed_node;
   std::vector<const DeviceView*> active;
   for (const auto& d : o.mine)
     if (d.state != "Draining") active.push_back(&d);
@@ -540,11 +543,25 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
           policy_gen_[m.uid] = m.generation;
         }
         log.info("claimed", Json::object().set("node", node).set("count", need).set("claimMs", claim_ms));
+        claimed_only = !acted;
+        claimed = std::move(cr.devices);
+        claimed_node = node;
       }
       acted = true;
     }
   }
-  if (acted) o = observe_(m, spec, obj["status"]);
+  if (claimed_only) {
+    // The claim RPC returns the agent's post-claim ground truth for the new GPUs (probed and,
+    // with a device plugin, already advertised); the rest of o.mine was observed this pass and
+    // nothing else changed, so merging replaces a second GET /v1/node (A1 still holds).
+    o.node = claimed_node;
+    o.reachable = true;
+    o.free_healthy = std::max<int64_t>(0, o.free_healthy - static_cast<int64_t>(claimed.size()));
+    for (auto& d : claimed) o.mine.push_back(std::move(d));
+    std::sort(o.mine.begin(), o.mine.end(), [](const DeviceView& a, const DeviceView& b) { return a.index < b.index; });
+  } else if (acted) {
+    o = observe_(m, spec, obj["status"]);
+  }
   int still = drain_(obj, o.node, m, spec, o.mine);
   bool released = false;
   for (const auto& d : o.mine)
@@ -586,15 +603,21 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
 bool Mi355xPoolReconciler::quota_allows_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta,
                                          std::string* why) {
   trace::Span span("quota");
-  Json quotas;
-  try {
-    quotas = client_.list(res::resourcequotas(), m.ns);
-  } catch (const std::exception&) {
-    return true;  // quota API unavailable: do not block claims on an optional policy
+  std::vector<Json> items;
+  if (quotas_ && quotas_->synced()) {
+    for (auto& q : quotas_->list())
+      if (q.path("metadata.namespace").as_string() == m.ns) items.push_back(std::move(q));
+  } else {
+    try {
+      Json quotas = client_.list(res::resourcequotas(), m.ns);
+      items = quotas["items"].elements();
+    } catch (const std::exception&) {
+      return true;  // quota API unavailable: do not block claims on an optional policy
+    }
   }
   int64_t hard = -1;
   std::string qname;
-  for (const auto& q : quotas["items"].elements()) {
+  for (const auto& q : items) {
     for (const std::string& key : {spec.resource_name, "requests." + spec.resource_name}) {
       const Json& h = q.path("spec.hard")[key];
       if (h.is_null()) continue;

@@ -409,6 +409,7 @@ int main(int argc, char** argv) {
     Informer nodes(client, res::nodes(), "", std::chrono::milliseconds(f.resync_ms));
     Informer mipools(client, res::mi355xpools(), f.ns, std::chrono::milliseconds(f.resync_ms));
     Informer azpools(client, res::azurevmpools(), f.ns, std::chrono::milliseconds(f.resync_ms));
+    Informer quotas(client, res::resourcequotas(), f.ns, std::chrono::milliseconds(f.resync_ms));
     RocmProvider rocm(nodes, f.agent_timeout_ms);
     FakeCloudOptions fco;
     fco.provision = std::chrono::milliseconds(f.fakecloud_provision_ms);
@@ -437,8 +438,20 @@ int main(int argc, char** argv) {
           if (!condition_true(p.path("status.conditions"), gen::kCondReady))
             ctl.enqueue("Mi355xPool", p.path("metadata.namespace").as_string(), p.path("metadata.name").as_string());
       });
+      // quota edits can unblock QuotaExceeded pools in that namespace; the cache is optional
+      // (not waited for): until it syncs, quota checks fall back to a LIST
+      mi.set_quota_informer(&quotas);
+      quotas.add_handler([&](const std::string& type, const Json& q) {
+        if (type == "RESYNC") return;
+        const std::string qns = q.path("metadata.namespace").as_string();
+        for (const auto& p : mipools.list())
+          if (p.path("metadata.namespace").as_string() == qns &&
+              !condition_true(p.path("status.conditions"), gen::kCondReady))
+            ctl.enqueue("Mi355xPool", qns, p.path("metadata.name").as_string());
+      });
       nodes.start();
       mipools.start();
+      quotas.start();
     }
     if (want_az) {
       ctl.add_reconciler(&az);
@@ -485,6 +498,7 @@ int main(int argc, char** argv) {
     watchers.stop_all();
     mipools.stop();
     azpools.stop();
+    quotas.stop();
     nodes.stop();
     events.flush(std::chrono::milliseconds(2000));
   };
