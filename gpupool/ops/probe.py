@@ -61,11 +61,14 @@ def identify(dev: int) -> dict:
 
 
 def run(dev: int, hbm_bytes: int = 1 << 30, mfma: bool = True, gemm_n: int = 4096,
-        patterns: int = 2, gemm_reps: int = 3, **test_hooks: int) -> dict:
-    """Probe HIP device ``dev``. ``test_hooks``: injectBitFlips=N / injectGemmFault=1 corrupt the
-    device buffers between compute and check so tests can prove the checkers catch faults."""
+        patterns: int = 2, gemm_reps: int = 1, gemm_tile: int = 256, **test_hooks: int) -> dict:
+    """Probe HIP device ``dev``. ``gemm_tile`` 256 (default, the glds 256x256 kernel) or 128 (the
+    older register-staged kernel, for A/B). ``test_hooks``: injectBitFlips=N / injectGemmFault=1
+    corrupt the device buffers between compute and check so tests can prove the checkers catch
+    faults."""
     opts = json.dumps({"hbmBytes": int(hbm_bytes), "mfma": bool(mfma), "gemmN": int(gemm_n),
                        "patterns": int(patterns), "gemmReps": int(gemm_reps),
+                       "gemmTile": int(gemm_tile),
                        **{k: int(v) for k, v in test_hooks.items()}})
     return _take(lib().mi355x_probe_run(dev, opts.encode()))
 

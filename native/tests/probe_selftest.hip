@@ -34,6 +34,50 @@ __global__ void one_tile(const short* A, const short* Bt, float* C) {
   }
 }
 
+// One wave computes C[16][16] = A[16][32] * B[32][16] with v_mfma_f32_16x16x32_bf16 (the probe's
+// main GEMM instruction): lane l holds A[l&15][8(l>>4)+j], Bt[l&15][8(l>>4)+j]; C/D col = l&15,
+// row = 4(l>>4) + reg.
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+__global__ void one_tile16(const short* A, const short* Bt, float* C) {
+  int lane = threadIdx.x, r = lane & 15, q = lane >> 4;
+  bf16x8 a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = A[r * 32 + 8 * q + j];
+    b[j] = Bt[r * 32 + 8 * q + j];
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  for (int i = 0; i < 4; ++i) C[(4 * q + i) * 16 + r] = acc[i];
+}
+
+static int check16() {
+  // A[16][32]: A[i][i] = 1, A[i][i+16] = 3 (both k-halves used); Bt asymmetric: Bt[n][k] = 4k + n%4.
+  std::vector<short> A(16 * 32, 0), Bt(16 * 32);
+  std::vector<float> ref(16 * 16, 0.f);
+  for (int i = 0; i < 16; ++i) {
+    A[i * 32 + i] = f2bf(1.f);
+    A[i * 32 + i + 16] = f2bf(3.f);
+  }
+  for (int n = 0; n < 16; ++n)
+    for (int k = 0; k < 32; ++k) Bt[n * 32 + k] = f2bf(static_cast<float>(4 * k + (n % 4)));
+  for (int m = 0; m < 16; ++m)
+    for (int n = 0; n < 16; ++n) ref[m * 16 + n] = 1.f * (4 * m + n % 4) + 3.f * (4 * (m + 16) + n % 4);
+  short *dA, *dB;
+  float* dC;
+  if (hipMalloc(&dA, A.size() * 2) || hipMalloc(&dB, Bt.size() * 2) || hipMalloc(&dC, 16 * 16 * 4)) return -1;
+  (void)hipMemcpy(dA, A.data(), A.size() * 2, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dB, Bt.data(), Bt.size() * 2, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(one_tile16, dim3(1), dim3(64), 0, 0, dA, dB, dC);
+  std::vector<float> C(16 * 16);
+  (void)hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost);
+  int bad = 0;
+  for (int i = 0; i < 16 * 16; ++i) bad += C[i] != ref[i];
+  (void)hipFree(dA);
+  (void)hipFree(dB);
+  (void)hipFree(dC);
+  return bad;
+}
+
 int main() {
   // A: 32x16 "identity" (A[i][i%16] = 1 for i<16, A[i][i-16]=2 for i>=16): rows pick rows of B.
   std::vector<short> A(32 * 16, 0), Bt(32 * 16);
@@ -57,16 +101,17 @@ int main() {
   short *dA, *dB;
   float* dC;
   if (hipMalloc(&dA, A.size() * 2) || hipMalloc(&dB, Bt.size() * 2) || hipMalloc(&dC, 32 * 32 * 4)) return 3;
-  hipMemcpy(dA, A.data(), A.size() * 2, hipMemcpyHostToDevice);
-  hipMemcpy(dB, Bt.data(), Bt.size() * 2, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dA, A.data(), A.size() * 2, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dB, Bt.data(), Bt.size() * 2, hipMemcpyHostToDevice);
   hipLaunchKernelGGL(one_tile, dim3(1), dim3(64), 0, 0, dA, dB, dC);
   std::vector<float> C(32 * 32);
-  hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost);
   int bad = 0;
   for (int i = 0; i < 32 * 32; ++i) bad += C[i] != ref[i];
-  std::printf("{\"mfma_layout_mismatches\": %d}\n", bad);
-  hipFree(dA);
-  hipFree(dB);
-  hipFree(dC);
-  return bad == 0 ? 0 : 1;
+  (void)hipFree(dA);
+  (void)hipFree(dB);
+  (void)hipFree(dC);
+  const int bad16 = check16();
+  std::printf("{\"mfma_layout_mismatches\": %d, \"mfma16_layout_mismatches\": %d}\n", bad, bad16);
+  return bad == 0 && bad16 == 0 ? 0 : 1;
 }

@@ -30,7 +30,8 @@ def test_mfma_fragment_layout_selftest(native_built):
     r = subprocess.run([os.path.join(NATIVE, "probe_selftest")], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert json.loads(r.stdout)["mfma_layout_mismatches"] == 0
+    out = json.loads(r.stdout)
+    assert out["mfma_layout_mismatches"] == 0 and out["mfma16_layout_mismatches"] == 0
 
 
 def test_identify_is_gfx950(hip):
