@@ -92,6 +92,7 @@ class Agent:
         self.plugins: dict = {}
         self.probe_mode = cfg.probe_mode or default_mode(self.backend)
         self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n)
+        self.last_probe: dict[str, dict] = {}
         self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0,
                       "probe_ms_sum": 0.0, "samples": 0}
         self._pods_cache: tuple[float, dict[str, list[dict]]] = (0.0, {})
@@ -305,6 +306,7 @@ class Agent:
                     continue  # released concurrently
                 rec["probe"] = res
                 rec["state"] = "Claimed"
+                self.last_probe[d["uuid"]] = res
                 self.stats["probes"] += 1
                 self.stats["probe_ms_sum"] += float(res.get("ms", 0.0))
                 if not res.get("passed"):
@@ -573,6 +575,13 @@ class Agent:
                     if isinstance(t, dict) and t.get("current") is not None:
                         lines.append(f'gpupool_device_temperature_celsius{{{lab},sensor="{s}"}} '
                                      f"{t['current']}")
+                pr = self.last_probe.get(u)
+                if pr:  # last claim-time probe of this GPU (performance trend across claims)
+                    lines.append(f"gpupool_device_probe_passed{{{lab}}} {1 if pr.get('passed') else 0}")
+                    lines.append(f"gpupool_device_probe_hbm_gbps{{{lab}}} "
+                                 f"{float((pr.get('hbm') or {}).get('GBps') or 0):.1f}")
+                    lines.append(f"gpupool_device_probe_mfma_tflops{{{lab}}} "
+                                 f"{float((pr.get('mfma') or {}).get('tflops') or 0):.1f}")
             for k, v in self.stats.items():
                 lines.append(f"gpupool_agent_{k} {v}")
             lines.append(f"gpupool_agent_gen {self.gen}")

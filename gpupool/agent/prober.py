@@ -60,9 +60,10 @@ class Prober:
         if self.mode == "simulated":
             time.sleep(self.sim_ms / 1e3)
             fail = bool((dev.get("faults") or {}).get("probeFail")) or bool(dev.get("probeFail"))
+            # nominal numbers = the measured MI355X probe (profiles/r1c_probe_gemm_ab_real.json)
             res = {"passed": not fail, "backend": "simulated",
-                   "hbm": {"ok": not fail, "GBps": 5400.0, "bytes": hbm},
-                   "mfma": {"ok": not fail, "tflops": 750.0, "enabled": mfma}}
+                   "hbm": {"ok": not fail, "GBps": 4900.0, "bytes": hbm},
+                   "mfma": {"ok": not fail, "tflops": 1200.0 if mfma else 0.0, "enabled": mfma}}
             if fail:
                 res["error"] = "injected probe failure (fault overlay)"
             res["ms"] = (time.perf_counter() - t0) * 1e3
@@ -90,12 +91,37 @@ class Prober:
         res.setdefault("ms", (time.perf_counter() - t0) * 1e3)
         return res
 
+    @staticmethod
+    def apply_floors(res: dict, dev: dict, opts: dict) -> dict:
+        """Performance floors (spec.probe.minHbmGBps / minMfmaTflops): a GPU that computes
+        correctly but slowly (throttled clocks, degraded HBM stack, bad cooling) fails the probe.
+        Fault overlay ``probeScale`` (0..1) scales the measured numbers to exercise this path."""
+        scale = (dev.get("faults") or {}).get("probeScale") or dev.get("probeScale")
+        hbm, mfma = res.get("hbm") or {}, res.get("mfma") or {}
+        if scale:
+            for part, key in ((hbm, "GBps"), (mfma, "tflops")):
+                if isinstance(part.get(key), (int, float)):
+                    part[key] = part[key] * float(scale)
+        if not res.get("passed"):
+            return res
+        why = []
+        floor_h = float(opts.get("minHbmGBps") or 0)
+        if floor_h > 0 and float(hbm.get("GBps") or 0) < floor_h:
+            why.append(f"HBM {float(hbm.get('GBps') or 0):.0f} GB/s < floor {floor_h:.0f}")
+        floor_m = float(opts.get("minMfmaTflops") or 0)
+        if floor_m > 0 and mfma.get("enabled", True) and float(mfma.get("tflops") or 0) < floor_m:
+            why.append(f"MFMA {float(mfma.get('tflops') or 0):.0f} TFLOP/s < floor {floor_m:.0f}")
+        if why:
+            res["passed"] = False
+            res["error"] = "PerformanceBelowFloor: " + "; ".join(why)
+        return res
+
     def probe_many(self, devs: list[dict], opts: dict) -> list[dict]:
         futs = [self.pool.submit(self._one, d, opts) for d in devs]
         out = []
-        for f in futs:
+        for d, f in zip(devs, futs):
             try:
-                out.append(f.result())
+                out.append(self.apply_floors(f.result(), d, opts))
             except Exception as e:  # a probe must never take the agent down
                 out.append({"passed": False, "backend": self.mode, "error": repr(e), "ms": 0.0})
         return out

@@ -205,6 +205,15 @@ MI355X_SPEC = {
                 "hbmBytes": {**_I64, "minimum": 1 << 20, "maximum": 64 << 30,
                              "default": 1 << 30},
                 "mfma": {**_B, "default": True},
+                "minHbmGBps": {"type": "number", "minimum": 0, "default": 0,
+                               "description": "Performance floor: a GPU whose probe measures "
+                                              "less HBM write+read bandwidth (GB/s) fails "
+                                              "DeviceProbePassed (0 = off; MI355X measures "
+                                              "~4900 with the default 1 GiB probe)."},
+                "minMfmaTflops": {"type": "number", "minimum": 0, "default": 0,
+                                  "description": "Performance floor for the probe's 4096^3 bf16 "
+                                                 "MFMA GEMM in TFLOP/s (0 = off; MI355X "
+                                                 "measures ~1200)."},
             },
         },
         "replacePolicy": {"type": "string", "enum": ["Replace", "Keep"], "default": "Replace"},

@@ -58,6 +58,8 @@ struct Mi355xPoolSpec {
   bool probe_enabled = true;
   int64_t probe_hbm_bytes = 1LL << 30;
   bool probe_mfma = true;
+  double probe_min_hbm_gbps = 0;     // performance floors (0 = off)
+  double probe_min_mfma_tflops = 0;
   std::string replace_policy = "Replace";
   static Mi355xPoolSpec from(const Json& spec);
   Json policy_json() const;  // health + partition, as the agent/device library consume it

@@ -72,6 +72,8 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.probe_enabled = pr["enabled"].as_bool(true);
   p.probe_hbm_bytes = pr["hbmBytes"].as_int(1LL << 30);
   p.probe_mfma = pr["mfma"].as_bool(true);
+  p.probe_min_hbm_gbps = pr["minHbmGBps"].as_double(0);
+  p.probe_min_mfma_tflops = pr["minMfmaTflops"].as_double(0);
   p.replace_policy = s["replacePolicy"].str_or("Replace");
   return p;
 }
@@ -158,6 +160,9 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
     int64_t b = pr["hbmBytes"].as_int(0);
     if (b < (1LL << 20) || b > (64LL << 30)) errs.push_back("spec.probe.hbmBytes: must be within [1MiB, 64GiB]");
   }
+  for (const char* k : {"minHbmGBps", "minMfmaTflops"})
+    if (pr.contains(k) && (!pr[k].is_number() || pr[k].as_double(0) < 0))
+      errs.push_back(std::string("spec.probe.") + k + ": should be greater than or equal to 0");
   const Json& part = s["partition"];
   if (part.contains("compute") && !in(part["compute"].as_string(), {"Any", "SPX", "DPX", "QPX", "CPX"}))
     errs.push_back("spec.partition.compute: Unsupported value");

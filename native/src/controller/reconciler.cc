@@ -465,7 +465,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
       std::string why = join([&] {
         std::vector<std::string> r;
         for (const auto& x : d->verdict["reasons"].elements()) r.push_back(x.as_string());
-        if (!d->probe_passed) r.push_back("ProbeFailed");
+        if (!d->probe_passed) r.push_back("ProbeFailed: " + d->probe["error"].str_or("probe failed"));
         return r;
       }(), "; ");
       event_(obj, "Warning", "HealthDegraded", short_id(*d) + " unhealthy (" + why + "): replacing");
@@ -525,6 +525,8 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
       req.probe["enabled"] = spec.probe_enabled;
       req.probe["hbmBytes"] = spec.probe_hbm_bytes;
       req.probe["mfma"] = spec.probe_mfma;
+      req.probe["minHbmGBps"] = spec.probe_min_hbm_gbps;
+      req.probe["minMfmaTflops"] = spec.probe_min_mfma_tflops;
       auto t = clock_t_::now();
       ClaimResult cr = provider_.claim(node, req);
       double claim_ms = std::chrono::duration<double, std::milli>(clock_t_::now() - t).count();

@@ -147,6 +147,21 @@ def test_probe_failure_replaced(cluster_factory):
     assert "HealthDegraded" in reasons
 
 
+def test_performance_floor_replaces_slow_gpu(cluster_factory):
+    """spec.probe.minMfmaTflops: a GPU that computes correctly but at half speed (fault overlay
+    probeScale, e.g. a throttled part) fails DeviceProbePassed and is replaced."""
+    c = cluster_factory(nodes=[NodeSpec("mi355x-node-0")])
+    k = c.client
+    c.set_faults("mi355x-node-0", {"devices": {"0": {"probeScale": 0.5}}})
+    k.create(MI355XPOOLS, mi_pool("p", 2, probe={"minMfmaTflops": 1000, "minHbmGBps": 3000}),
+             "default")
+    o = wait_ready(k, "p", 2, timeout=30)
+    assert 0 not in {d["index"] for d in o["status"]["devices"]}
+    assert all(d["probe"]["mfmaTflops"] >= 1000 for d in o["status"]["devices"])
+    msgs = " ".join(e.get("message", "") for e in k.list(EVENTS, "default")["items"])
+    assert "PerformanceBelowFloor" in msgs and "MFMA 600 TFLOP/s < floor 1000" in msgs
+
+
 def test_manager_restart_readopts_claims(node8):
     k = node8.client
     k.create(MI355XPOOLS, mi_pool("p", 3), "default")

@@ -204,3 +204,23 @@ def test_podresources_roundtrip(tmp_path, sockdir):
         assert set(out) == {"u1", "u2"} and out["u1"][0]["name"] == "p"
     finally:
         s.stop(0)
+
+
+def test_probe_performance_floors():
+    from gpupool.agent.prober import Prober
+    ok = {"passed": True, "hbm": {"GBps": 4900.0}, "mfma": {"tflops": 1200.0, "enabled": True}}
+    import copy
+    r = Prober.apply_floors(copy.deepcopy(ok), {}, {"minHbmGBps": 4000, "minMfmaTflops": 1000})
+    assert r["passed"]
+    r = Prober.apply_floors(copy.deepcopy(ok), {"probeScale": 0.5}, {"minMfmaTflops": 1000})
+    assert not r["passed"] and r["error"].startswith("PerformanceBelowFloor: MFMA 600")
+    r = Prober.apply_floors(copy.deepcopy(ok), {"faults": {"probeScale": 0.7}},
+                            {"minHbmGBps": 4000})
+    assert not r["passed"] and "HBM 3430 GB/s < floor 4000" in r["error"]
+    # floors off (0) and MFMA disabled: never fail on perf
+    r = Prober.apply_floors({"passed": True, "hbm": {"GBps": 1.0}, "mfma": {"enabled": False}},
+                            {}, {"minHbmGBps": 0, "minMfmaTflops": 500})
+    assert r["passed"]
+    # a failed probe keeps its own error
+    bad = {"passed": False, "error": "HBM mismatch", "hbm": {"GBps": 1.0}}
+    assert Prober.apply_floors(bad, {}, {"minHbmGBps": 4000})["error"] == "HBM mismatch"

@@ -46,6 +46,10 @@ CASES = [
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "health": {"thermal": "hot"}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "health": {"minXGMILinksUp": 9}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "probe": {"hbmBytes": 1024}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 1, "probe": {"minMfmaTflops": 1000.5,
+                                                             "minHbmGBps": 4000}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 1, "probe": {"minMfmaTflops": -1}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 1, "probe": {"minHbmGBps": "fast"}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "partition": {"compute": "CPX", "memory": "NPS4"}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "partition": {"compute": "XPX"}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "replacePolicy": "Never"}},
