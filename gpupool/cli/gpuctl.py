@@ -13,8 +13,10 @@
   gpuctl render job -f TEMPLATE           GoHai train-job template -> Pod requesting amd.com/gpu
   gpuctl config view | set-context NAME --server URL [--namespace NS] [--token T] | use-context NAME
 
-Connection: --server/--token/-n flags, else GPUPOOL_APISERVER/GPUPOOL_TOKEN, else the current
-context of ~/.config/gpupool/config.yaml (the GoHai CLI context schema, GPU调度平台搭建.md:461-472).
+Connection (first match wins): --server/--token/-n flags or GPUPOOL_APISERVER/GPUPOOL_TOKEN;
+--kubeconfig/--context or $KUBECONFIG (kubectl's file: token, tokenFile, client certificates,
+CA); the current context of ~/.config/gpupool/config.yaml (the GoHai CLI context schema,
+GPU调度平台搭建.md:461-472); ~/.kube/config.
 """
 from __future__ import annotations
 
@@ -48,14 +50,25 @@ def save_config(cfg: dict) -> None:
         yaml.safe_dump(cfg, f, sort_keys=False)
 
 
-def connection(args) -> tuple[str, str | None, str]:
+def connection(args) -> tuple[Client, str]:
+    """First match wins: --server / $GPUPOOL_APISERVER, --kubeconfig / $KUBECONFIG, the current
+    gpuctl context, ~/.kube/config, http://127.0.0.1:6443."""
     cfg = load_config()
     ctx = (cfg.get("contexts") or {}).get(cfg.get("current-context", ""), {})
-    server = args.server or os.environ.get("GPUPOOL_APISERVER") or ctx.get("server") or \
-        "http://127.0.0.1:6443"
+    server = args.server or os.environ.get("GPUPOOL_APISERVER")
+    kubeconfig = getattr(args, "kubeconfig", None) or os.environ.get("KUBECONFIG")
+    if not server and not ctx.get("server") and not kubeconfig and \
+            os.path.exists(os.path.expanduser("~/.kube/config")):
+        kubeconfig = os.path.expanduser("~/.kube/config")
+    if not server and kubeconfig:
+        c = Client.from_kubeconfig(kubeconfig, getattr(args, "context", None))
+        if args.token:
+            c.token = args.token
+        return c, args.namespace or c.namespace or "default"
+    server = server or ctx.get("server") or "http://127.0.0.1:6443"
     token = args.token or os.environ.get("GPUPOOL_TOKEN") or ctx.get("token")
     ns = args.namespace or ctx.get("namespace") or "default"
-    return server, token, ns
+    return Client(server, token), ns
 
 
 # ------------------------------------------------------------------ discovery
@@ -371,6 +384,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="gpuctl", description="kubectl-like CLI for gpupool")
     ap.add_argument("--server", default=None)
     ap.add_argument("--token", default=None)
+    ap.add_argument("--kubeconfig", default=None, help="kubeconfig file (default $KUBECONFIG)")
+    ap.add_argument("--context", default=None, help="kubeconfig context (default current)")
     ap.add_argument("-n", "--namespace", default=None)
     sub = ap.add_subparsers(dest="cmd", required=True)
     p = sub.add_parser("apply")
@@ -432,8 +447,7 @@ def main(argv: list[str] | None = None) -> int:
     args = build_parser().parse_args(argv)
     if args.cmd == "config":
         return cmd_config(args)
-    server, token, ns = connection(args)
-    c = Client(server, token)
+    c, ns = connection(args)
     fn = {"apply": cmd_apply, "get": cmd_get, "describe": cmd_describe, "delete": cmd_delete,
           "scale": cmd_scale, "wait": cmd_wait, "logs": cmd_logs, "events": cmd_events,
           "devices": cmd_devices, "install": cmd_install, "render": cmd_render}[args.cmd]

@@ -2,7 +2,8 @@
 
 Used by gpuctl, the node agent, the fake kubelet, the bench and the tests. Thread-safe: each
 call opens its own connection unless a per-thread keep-alive connection is available.
-Speaks to the apiserver-sim (or any apiserver reachable without TLS client certs).
+Transports: http, https (CA file or in-memory PEM, optional client certificate) and unix
+sockets; configuration from flags, the in-cluster ServiceAccount, or a kubeconfig.
 """
 from __future__ import annotations
 
@@ -74,6 +75,60 @@ BY_KIND = {
 }
 
 
+def load_kubeconfig(path: str | None = None, context: str | None = None) -> dict:
+    """Resolve a kubeconfig context (clientcmd semantics; same subset as the C++
+    ``load_kubeconfig``): path defaults to the first ``$KUBECONFIG`` entry, else ~/.kube/config;
+    context to ``current-context``. Returns {server, token, namespace, context, ca_file, ca_data,
+    cert_file, key_file, cert_data, key_data, insecure} (``*_data`` already base64-decoded)."""
+    import base64
+
+    import yaml
+    if not path:
+        env = os.environ.get("KUBECONFIG", "")
+        path = env.split(os.pathsep)[0] if env else os.path.expanduser("~/.kube/config")
+    with open(path) as f:
+        cfg = yaml.safe_load(f) or {}
+    base = os.path.dirname(os.path.abspath(path))
+
+    def named(kind: str, name: str) -> dict:
+        for e in cfg.get(kind) or []:
+            if e.get("name") == name:
+                return e
+        raise ValueError(f"kubeconfig {path}: no {kind[:-1]} named {name!r}")
+
+    def rel(p: str | None) -> str | None:
+        return p if not p or os.path.isabs(p) else os.path.join(base, p)
+
+    def b64(v: str | None) -> str | None:
+        return base64.b64decode(v).decode() if v else None
+
+    ctx_name = context or cfg.get("current-context")
+    if not ctx_name:
+        raise ValueError(f"kubeconfig {path}: no current-context")
+    ctx = named("contexts", ctx_name).get("context") or {}
+    cl = named("clusters", ctx.get("cluster", "")).get("cluster") or {}
+    out = {"server": cl.get("server"), "context": ctx_name, "namespace": ctx.get("namespace"),
+           "insecure": bool(cl.get("insecure-skip-tls-verify")),
+           "ca_file": rel(cl.get("certificate-authority")),
+           "ca_data": b64(cl.get("certificate-authority-data")), "token": None,
+           "cert_file": None, "key_file": None, "cert_data": None, "key_data": None}
+    if ctx.get("user"):
+        u = named("users", ctx["user"]).get("user") or {}
+        if "exec" in u or "auth-provider" in u:
+            raise ValueError(f"kubeconfig {path}: user {ctx['user']!r} uses an exec/auth-provider "
+                             "plugin; use a token or client certificate")
+        out["token"] = u.get("token")
+        if not out["token"] and u.get("tokenFile"):
+            with open(rel(u["tokenFile"])) as f:
+                out["token"] = f.read().strip()
+        out["cert_file"], out["key_file"] = rel(u.get("client-certificate")), rel(u.get("client-key"))
+        out["cert_data"], out["key_data"] = b64(u.get("client-certificate-data")), \
+            b64(u.get("client-key-data"))
+    if not out["server"]:
+        raise ValueError(f"kubeconfig {path}: cluster has no server")
+    return out
+
+
 class Client:
     def __init__(self, server: str, token: str | None = None, timeout: float = 30.0,
                  ca_file: str | None = None, insecure: bool = False,
@@ -86,11 +141,16 @@ class Client:
         self.server = server
         self.token = token
         self.timeout = timeout
+        self.namespace: str | None = None  # kubeconfig context namespace, if any
         self._local = threading.local()
         self._ssl = None
         if self.scheme == "https":
             import ssl
-            ctx = ssl.create_default_context(cafile=ca_file or os.environ.get("GPUPOOL_CA_FILE") or None)
+            ca_data = None
+            if ca_file and ca_file.startswith("-----BEGIN"):  # in-memory PEM (kubeconfig *-data)
+                ca_data, ca_file = ca_file, None
+            ctx = ssl.create_default_context(cafile=ca_file or os.environ.get("GPUPOOL_CA_FILE") or None,
+                                             cadata=ca_data)
             ctx.minimum_version = ssl.TLSVersion.TLSv1_2
             if insecure:
                 ctx.check_hostname = False
@@ -127,6 +187,24 @@ class Client:
             token = f.read().strip()
         return cls(f"https://{host}:{os.environ.get('KUBERNETES_SERVICE_PORT', '443')}", token,
                    ca_file=os.path.join(sa_dir, "ca.crt"))
+
+    @classmethod
+    def from_kubeconfig(cls, path: str | None = None, context: str | None = None,
+                        timeout: float = 30.0) -> "Client":
+        kc = load_kubeconfig(path, context)
+        cert, key = kc["cert_file"], kc["key_file"]
+        if kc["cert_data"]:  # ssl.load_cert_chain needs files: a private temp dir
+            import tempfile
+            d = tempfile.mkdtemp(prefix="gpuctl-kc-")
+            cert, key = os.path.join(d, "client.crt"), os.path.join(d, "client.key")
+            for pth, data in ((cert, kc["cert_data"]), (key, kc["key_data"] or kc["cert_data"])):
+                fd = os.open(pth, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+                with os.fdopen(fd, "w") as f:
+                    f.write(data)
+        c = cls(kc["server"], kc["token"], timeout=timeout, ca_file=kc["ca_data"] or kc["ca_file"],
+                insecure=kc["insecure"], client_cert=cert, client_key=key)
+        c.namespace = kc["namespace"]
+        return c
 
     @classmethod
     def connect(cls, server: str, token: str | None = None) -> "Client":

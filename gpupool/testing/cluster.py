@@ -48,6 +48,22 @@ def make_test_pki(workdir: str, name: str = "apiserver") -> tuple[str, str, str]
     return ca_crt, crt, key
 
 
+def issue_client_cert(workdir: str, cn: str = "gpupool-admin") -> tuple[str, str]:
+    """Client certificate (CN=user) signed by the CA ``make_test_pki(workdir)`` created.
+    Returns (client.crt, client.key)."""
+    d = os.path.join(workdir, "pki")
+    key, csr, crt = (os.path.join(d, f"client-{cn}.{ext}") for ext in ("key", "csr", "crt"))
+    ext = os.path.join(d, "client.ext")
+    with open(ext, "w") as f:
+        f.write("basicConstraints=CA:FALSE\nkeyUsage=digitalSignature,keyEncipherment\n"
+                "extendedKeyUsage=clientAuth\n")
+    run = lambda *a: subprocess.run(["openssl", *a], check=True, capture_output=True)  # noqa: E731
+    run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", key, "-out", csr, "-subj", f"/CN={cn}")
+    run("x509", "-req", "-in", csr, "-CA", os.path.join(d, "ca.crt"), "-CAkey",
+        os.path.join(d, "ca.key"), "-CAcreateserial", "-out", crt, "-days", "2", "-extfile", ext)
+    return crt, key
+
+
 def _wait_file(path: str, timeout: float, proc: subprocess.Popen | None = None,
                logpath: str | None = None) -> str:
     deadline = time.monotonic() + timeout

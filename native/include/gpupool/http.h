@@ -21,6 +21,8 @@ struct TlsOptions {
   std::string ca_file;
   std::string cert_file;  // client certificate (kubeconfig client-certificate)
   std::string key_file;
+  // in-memory PEM alternatives (kubeconfig *-data fields, already base64-decoded)
+  std::string ca_pem, cert_pem, key_pem;
   bool insecure = false;  // skip peer verification (tests / --insecure-skip-tls-verify)
 };
 
@@ -129,5 +131,7 @@ class HttpServer {
 
 std::string url_encode(std::string_view s);
 std::string url_decode(std::string_view s);  // %XX and '+' (query strings)
+// RFC 4648 base64 (padding optional; whitespace and other non-alphabet bytes are skipped).
+std::string base64_decode(std::string_view in);
 
 }  // namespace gpupool

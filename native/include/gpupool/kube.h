@@ -45,6 +45,19 @@ class KubeError : public std::runtime_error {
   bool gone() const { return code == 410; }
 };
 
+// A resolved kubeconfig context (clientcmd semantics, the subset a controller needs).
+struct KubeConfig {
+  std::string server, token, ns, context;
+  TlsOptions tls;
+};
+// Loads ``path`` ("" = first entry of $KUBECONFIG, else ~/.kube/config) and resolves ``context``
+// ("" = current-context): cluster server, certificate-authority(-data),
+// insecure-skip-tls-verify, user token / tokenFile, client-certificate(-data) /
+// client-key(-data), context namespace. Relative file paths are resolved against the
+// kubeconfig's directory. exec / auth-provider / basic-auth users are rejected with a clear
+// error. Throws std::runtime_error.
+KubeConfig load_kubeconfig(const std::string& path = "", const std::string& context = "");
+
 class KubeClient {
  public:
   KubeClient(const std::string& server, const std::string& token = "", int timeout_ms = 15000,

@@ -668,24 +668,6 @@ AzureVmPoolReconciler::AzureVmPoolReconciler(KubeClient& client, Informer& pools
                                              EventRecorder* events, ReconcilerOptions opts)
     : PoolReconcilerBase(client, pools, events, opts, "AzureVmPool", res::azurevmpools()), cloud_(cloud) {}
 
-static std::string b64decode(const std::string& in) {
-  static const std::string tbl = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
-  std::string out;
-  int val = 0, bits = -8;
-  for (unsigned char c : in) {
-    if (c == '=') break;
-    auto p = tbl.find(static_cast<char>(c));
-    if (p == std::string::npos) continue;
-    val = (val << 6) + static_cast<int>(p);
-    bits += 6;
-    if (bits >= 0) {
-      out.push_back(static_cast<char>((val >> bits) & 0xFF));
-      bits -= 8;
-    }
-  }
-  return out;
-}
-
 bool AzureVmPoolReconciler::credentials_(const ObjectMeta& m, const AzureVmPoolSpec& spec, Credentials* out,
                                          std::string* why) {
   // README.md:179-185: the client is built from the Secret named by spec.azureCredentialSecret.
@@ -701,7 +683,7 @@ bool AzureVmPoolReconciler::credentials_(const ObjectMeta& m, const AzureVmPoolS
   }
   std::vector<std::string> missing;
   for (const char* k : gen::kAzureCredentialKeys) {
-    std::string v = b64decode(secret["data"][k].as_string());
+    std::string v = base64_decode(secret["data"][k].as_string());
     if (v.empty()) missing.push_back(k);
     else out->values[k] = v;
   }

@@ -70,6 +70,7 @@ struct Flags {
   std::string validate;
   // TLS / auth for a real apiserver
   std::string ca_file, client_cert, client_key, token_file;
+  std::string kubeconfig, kube_context;
   bool insecure = false;
   bool apiserver_set = false;
 };
@@ -85,8 +86,10 @@ int parse_duration_ms(const std::string& s) {
 
 const char* kUsage = R"(gpupool-manager: Mi355xPool / AzureVmPool operator
 
-connection (default: in-cluster ServiceAccount config, else http://127.0.0.1:6443):
+connection, first match wins: --apiserver/$GPUPOOL_APISERVER, --kubeconfig/$KUBECONFIG,
+in-cluster ServiceAccount, ~/.kube/config, http://127.0.0.1:6443:
   --apiserver URL              http(s)://host:port or unix:///path   [$GPUPOOL_APISERVER]
+  --kubeconfig F [--context C] kubeconfig file and context (default: current-context)
   --token T | --token-file F   bearer token                            [$GPUPOOL_TOKEN]
   --ca-file F                  CA bundle to verify the apiserver certificate
   --client-cert F --client-key F   client certificate authentication
@@ -140,6 +143,8 @@ Flags parse(int argc, char** argv) {
     else if (is("--client-cert")) f.client_cert = val();
     else if (is("--client-key")) f.client_key = val();
     else if (is("--token-file")) f.token_file = val();
+    else if (is("--kubeconfig")) f.kubeconfig = val();
+    else if (is("--context")) f.kube_context = val();
     else if (a == "--insecure-skip-tls-verify") f.insecure = true;
     else if (is("--token")) f.token = val();
     else if (is("--namespace")) f.ns = val();
@@ -325,12 +330,37 @@ int main(int argc, char** argv) {
     while (!f.token.empty() && (f.token.back() == '\n' || f.token.back() == '\r')) f.token.pop_back();
   }
   if (!f.apiserver_set && !getenv("GPUPOOL_APISERVER")) {
-    std::string server, token;
+    std::string server, token, home_cfg;
     TlsOptions ic;
-    if (KubeClient::in_cluster(&server, &token, &ic)) {  // running in a pod: ServiceAccount config
+    if (const char* home = getenv("HOME")) home_cfg = std::string(home) + "/.kube/config";
+    const char* env_kc = getenv("KUBECONFIG");
+    bool use_kc = !f.kubeconfig.empty() || (env_kc && *env_kc);
+    if (!use_kc && KubeClient::in_cluster(&server, &token, &ic)) {  // running in a pod
       f.apiserver = server;
       if (f.token.empty()) f.token = token;
       if (tls.ca_file.empty()) tls.ca_file = ic.ca_file;
+    } else if (use_kc || (!home_cfg.empty() && std::ifstream(home_cfg).good())) {
+      KubeConfig kc;
+      try {
+        kc = load_kubeconfig(f.kubeconfig, f.kube_context);
+      } catch (const std::exception& e) {
+        log.error("kubeconfig", Json::object().set("error", e.what()));
+        return 2;
+      }
+      f.apiserver = kc.server;
+      if (f.token.empty()) f.token = kc.token;  // explicit flags win over the kubeconfig
+      if (tls.ca_file.empty() && tls.ca_pem.empty()) {
+        tls.ca_file = kc.tls.ca_file;
+        tls.ca_pem = kc.tls.ca_pem;
+      }
+      if (tls.cert_file.empty()) {
+        tls.cert_file = kc.tls.cert_file;
+        tls.key_file = kc.tls.key_file;
+        tls.cert_pem = kc.tls.cert_pem;
+        tls.key_pem = kc.tls.key_pem;
+      }
+      tls.insecure = tls.insecure || kc.tls.insecure;
+      log.info("using kubeconfig", Json::object().set("context", kc.context).set("server", kc.server));
     }
   }
   KubeClient client(f.apiserver, f.token, 15000, tls);

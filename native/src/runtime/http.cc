@@ -16,6 +16,7 @@
 #include <sstream>
 
 #include <openssl/err.h>
+#include <openssl/pem.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <stdexcept>
@@ -69,6 +70,33 @@ std::string url_encode(std::string_view s) {
       out.push_back('%');
       out.push_back(hex[c >> 4]);
       out.push_back(hex[c & 15]);
+    }
+  }
+  return out;
+}
+
+std::string base64_decode(std::string_view in) {
+  auto val = [](unsigned char c) -> int {
+    if (c >= 'A' && c <= 'Z') return c - 'A';
+    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+    if (c >= '0' && c <= '9') return c - '0' + 52;
+    if (c == '+' || c == '-') return 62;  // '-' '_': the URL-safe alphabet
+    if (c == '/' || c == '_') return 63;
+    return -1;
+  };
+  std::string out;
+  out.reserve(in.size() * 3 / 4);
+  uint32_t acc = 0;
+  int bits = 0;
+  for (unsigned char c : in) {
+    if (c == '=') break;
+    int v = val(c);
+    if (v < 0) continue;
+    acc = ((acc << 6) | static_cast<uint32_t>(v)) & 0xFFFFFFu;  // never more than 24 live bits
+    bits += 6;
+    if (bits >= 8) {
+      bits -= 8;
+      out.push_back(static_cast<char>((acc >> bits) & 0xFFu));
     }
   }
   return out;
@@ -288,11 +316,35 @@ HttpClient::HttpClient(Url url, std::string bearer_token, int timeout_ms, TlsOpt
     SSL_CTX_set_verify(ctx, SSL_VERIFY_NONE, nullptr);
   } else {
     SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
-    int ok = tls_.ca_file.empty() ? SSL_CTX_set_default_verify_paths(ctx)
-                                  : SSL_CTX_load_verify_locations(ctx, tls_.ca_file.c_str(), nullptr);
-    if (ok != 1) throw HttpError("loading CA " + tls_.ca_file + ": " + ssl_errors());
+    if (!tls_.ca_pem.empty()) {
+      // every certificate in the PEM bundle becomes a trust anchor
+      std::unique_ptr<BIO, decltype(&BIO_free)> bio(BIO_new_mem_buf(tls_.ca_pem.data(), static_cast<int>(tls_.ca_pem.size())),
+                                                    BIO_free);
+      X509_STORE* store = SSL_CTX_get_cert_store(ctx);
+      int added = 0;
+      while (X509* x = PEM_read_bio_X509(bio.get(), nullptr, nullptr, nullptr)) {
+        added += X509_STORE_add_cert(store, x) == 1;
+        X509_free(x);
+      }
+      ERR_clear_error();  // PEM_read_bio_X509 leaves "no start line" at end of input
+      if (added == 0) throw HttpError("certificate-authority-data: no usable certificate");
+    } else {
+      int ok = tls_.ca_file.empty() ? SSL_CTX_set_default_verify_paths(ctx)
+                                    : SSL_CTX_load_verify_locations(ctx, tls_.ca_file.c_str(), nullptr);
+      if (ok != 1) throw HttpError("loading CA " + tls_.ca_file + ": " + ssl_errors());
+    }
   }
-  if (!tls_.cert_file.empty()) {
+  if (!tls_.cert_pem.empty()) {
+    std::unique_ptr<BIO, decltype(&BIO_free)> cb(BIO_new_mem_buf(tls_.cert_pem.data(), static_cast<int>(tls_.cert_pem.size())),
+                                                 BIO_free);
+    std::unique_ptr<X509, decltype(&X509_free)> cert(PEM_read_bio_X509(cb.get(), nullptr, nullptr, nullptr), X509_free);
+    const std::string& kp = tls_.key_pem.empty() ? tls_.cert_pem : tls_.key_pem;
+    std::unique_ptr<BIO, decltype(&BIO_free)> kb(BIO_new_mem_buf(kp.data(), static_cast<int>(kp.size())), BIO_free);
+    std::unique_ptr<EVP_PKEY, decltype(&EVP_PKEY_free)> key(PEM_read_bio_PrivateKey(kb.get(), nullptr, nullptr, nullptr),
+                                                            EVP_PKEY_free);
+    if (!cert || !key || SSL_CTX_use_certificate(ctx, cert.get()) != 1 || SSL_CTX_use_PrivateKey(ctx, key.get()) != 1)
+      throw HttpError("client-certificate-data: " + ssl_errors());
+  } else if (!tls_.cert_file.empty()) {
     if (SSL_CTX_use_certificate_chain_file(ctx, tls_.cert_file.c_str()) != 1 ||
         SSL_CTX_use_PrivateKey_file(ctx, tls_.key_file.empty() ? tls_.cert_file.c_str() : tls_.key_file.c_str(),
                                     SSL_FILETYPE_PEM) != 1)

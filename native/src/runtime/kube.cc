@@ -5,6 +5,7 @@
 #include <sstream>
 
 #include "gpupool/generated/schema_consts.h"
+#include "gpupool/yaml.h"
 
 namespace gpupool {
 
@@ -48,6 +49,78 @@ bool KubeClient::in_cluster(std::string* server, std::string* token, TlsOptions*
   *server = "https://" + h + ":" + std::string(port && *port ? port : "443");
   tls->ca_file = sa_dir + "/ca.crt";
   return true;
+}
+
+static std::string read_file(const std::string& p) {
+  std::ifstream f(p, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot read " + p);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+static const Json& named(const Json& list, const std::string& name, const char* what, const std::string& path) {
+  for (const auto& e : list.elements())
+    if (e["name"].as_string() == name) return e;
+  throw std::runtime_error(std::string("kubeconfig ") + path + ": no " + what + " named '" + name + "'");
+}
+
+KubeConfig load_kubeconfig(const std::string& path_in, const std::string& context) {
+  std::string path = path_in;
+  if (path.empty()) {
+    if (const char* kc = getenv("KUBECONFIG"); kc && *kc) {
+      path = kc;
+      path = path.substr(0, path.find(':'));  // first file of the list
+    } else if (const char* home = getenv("HOME"); home && *home) {
+      path = std::string(home) + "/.kube/config";
+    }
+  }
+  if (path.empty()) throw std::runtime_error("no kubeconfig: set --kubeconfig or $KUBECONFIG");
+  Json cfg;
+  try {
+    cfg = yaml_parse(read_file(path));
+  } catch (const YamlError& e) {
+    throw std::runtime_error("kubeconfig " + path + ": " + e.what());
+  }
+  const std::string dir = path.find('/') == std::string::npos ? "." : path.substr(0, path.rfind('/'));
+  auto resolve = [&](const std::string& p) { return p.empty() || p[0] == '/' ? p : dir + "/" + p; };
+
+  KubeConfig out;
+  out.context = context.empty() ? cfg["current-context"].as_string() : context;
+  if (out.context.empty()) throw std::runtime_error("kubeconfig " + path + ": no current-context");
+  const Json& ctx = named(cfg["contexts"], out.context, "context", path)["context"];
+  const Json& cluster = named(cfg["clusters"], ctx["cluster"].as_string(), "cluster", path)["cluster"];
+  out.ns = ctx["namespace"].as_string();
+  out.server = cluster["server"].as_string();
+  if (out.server.empty()) throw std::runtime_error("kubeconfig " + path + ": cluster has no server");
+  out.tls.insecure = cluster["insecure-skip-tls-verify"].as_bool(false);
+  if (cluster["certificate-authority-data"].is_string())
+    out.tls.ca_pem = base64_decode(cluster["certificate-authority-data"].as_string());
+  else
+    out.tls.ca_file = resolve(cluster["certificate-authority"].as_string());
+  const std::string user_name = ctx["user"].as_string();
+  if (!user_name.empty()) {
+    const Json& user = named(cfg["users"], user_name, "user", path)["user"];
+    if (user.contains("exec") || user.contains("auth-provider"))
+      throw std::runtime_error("kubeconfig " + path + ": user '" + user_name +
+                               "' uses an exec/auth-provider plugin; use a token or client certificate");
+    if (user.contains("username") || user.contains("password"))
+      throw std::runtime_error("kubeconfig " + path + ": basic auth is not supported");
+    out.token = user["token"].as_string();
+    if (out.token.empty() && user["tokenFile"].is_string()) {
+      out.token = read_file(resolve(user["tokenFile"].as_string()));
+      while (!out.token.empty() && (out.token.back() == '\n' || out.token.back() == '\r')) out.token.pop_back();
+    }
+    if (user["client-certificate-data"].is_string())
+      out.tls.cert_pem = base64_decode(user["client-certificate-data"].as_string());
+    else
+      out.tls.cert_file = resolve(user["client-certificate"].as_string());
+    if (user["client-key-data"].is_string())
+      out.tls.key_pem = base64_decode(user["client-key-data"].as_string());
+    else
+      out.tls.key_file = resolve(user["client-key"].as_string());
+  }
+  return out;
 }
 
 static KubeError to_error(const HttpResponse& r, const std::string& what) {

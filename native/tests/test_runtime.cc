@@ -2,6 +2,7 @@
 // semantics, metrics, conditions, validation. Run under ASan/UBSan and TSan via `make SAN=...`.
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -18,6 +19,7 @@
 #include "gpupool/metrics.h"
 #include "gpupool/trace.h"
 #include "gpupool/workqueue.h"
+#include "gpupool/yaml.h"
 #include "testing.h"
 
 using namespace gpupool;
@@ -150,6 +152,147 @@ TEST(trace_spans_ring_and_scoping) {
   EXPECT_EQ(trace::recent(1000).size(), static_cast<size_t>(256));
   EXPECT_EQ(url_decode("Mi355xPool%2Fdefault%2Fa+b"), std::string("Mi355xPool/default/a b"));
   trace::reset();
+}
+
+TEST(base64_decode_long_and_urlsafe) {
+  EXPECT_EQ(base64_decode("aGVsbG8gd29ybGQ="), std::string("hello world"));
+  EXPECT_EQ(base64_decode("aGVs\nbG8=\n"), std::string("hello"));
+  std::string big(3000, '\0');
+  for (size_t i = 0; i < big.size(); ++i) big[i] = static_cast<char>(i * 7);
+  static const char* tbl = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string enc;
+  for (size_t i = 0; i < big.size(); i += 3) {
+    uint32_t v = (static_cast<uint8_t>(big[i]) << 16) | (static_cast<uint8_t>(big[i + 1]) << 8) | static_cast<uint8_t>(big[i + 2]);
+    for (int s = 18; s >= 0; s -= 6) enc.push_back(tbl[(v >> s) & 63]);
+  }
+  EXPECT_TRUE(base64_decode(enc) == big);  // no overflow on long inputs (UBSan build)
+  EXPECT_EQ(base64_decode("-_8="), base64_decode("+/8="));
+}
+
+TEST(yaml_subset) {
+  const char* doc = R"(# kubeconfig-like
+apiVersion: v1
+clusters:
+- cluster:
+    server: https://10.0.0.1:6443   # trailing comment
+    insecure-skip-tls-verify: true
+  name: "c1"
+contexts:
+- context: {cluster: c1, user: u1, namespace: team-a}
+  name: ctx1
+list:
+  - 1
+  - -2.5
+  - 'it''s'
+  - "a\tb \u00e9"
+  - [x, "y, z", {k: v}]
+  - ~
+nested:
+  - - a
+    - b
+empty_map: {}
+seq_at_parent_indent:
+- k: v
+  k2: null
+block: |
+  line one
+    indented
+tail: end
+---
+ignored: second document
+)";
+  Json j = yaml_parse(doc);
+  EXPECT_EQ(j["apiVersion"].as_string(), std::string("v1"));
+  EXPECT_EQ(j["clusters"][0]["name"].as_string(), std::string("c1"));
+  EXPECT_EQ(j["clusters"][0]["cluster"]["server"].as_string(), std::string("https://10.0.0.1:6443"));
+  EXPECT_TRUE(j["clusters"][0]["cluster"]["insecure-skip-tls-verify"].as_bool(false));
+  EXPECT_EQ(j["contexts"][0]["context"]["namespace"].as_string(), std::string("team-a"));
+  EXPECT_EQ(j["list"][0].as_int(), 1);
+  EXPECT_EQ(j["list"][1].as_double(), -2.5);
+  EXPECT_EQ(j["list"][2].as_string(), std::string("it's"));
+  EXPECT_EQ(j["list"][3].as_string(), std::string("a\tb \xc3\xa9"));
+  EXPECT_EQ(j["list"][4][1].as_string(), std::string("y, z"));
+  EXPECT_EQ(j["list"][4][2]["k"].as_string(), std::string("v"));
+  EXPECT_TRUE(j["list"][5].is_null());
+  EXPECT_EQ(j["nested"][0][1].as_string(), std::string("b"));
+  EXPECT_TRUE(j["empty_map"].is_object());
+  EXPECT_EQ(j["seq_at_parent_indent"][0]["k"].as_string(), std::string("v"));
+  EXPECT_EQ(j["block"].as_string(), std::string("line one\n  indented\n"));
+  EXPECT_EQ(j["tail"].as_string(), std::string("end"));
+  EXPECT_TRUE(!j.contains("ignored"));
+  EXPECT_THROW(yaml_parse("a: [1, 2"));
+  EXPECT_THROW(yaml_parse("a:\n\t- 1"));
+  EXPECT_THROW(yaml_parse("a: &x 1"));
+  std::mt19937 rng(99);  // fuzz: malformed input must throw or parse, never crash (ASan build)
+  std::string seed = doc;
+  for (int it = 0; it < 3000; ++it) {
+    std::string s = seed.substr(0, rng() % seed.size());
+    if (s.empty()) continue;
+    for (int f = 0; f < 3; ++f) s[rng() % s.size()] = "-: \n'\"[{#|"[rng() % 11];
+    try {
+      (void)yaml_parse(s);
+    } catch (const YamlError&) {
+    }
+  }
+}
+
+TEST(kubeconfig_resolution) {
+  char tmpl[] = "/tmp/gp-kc-XXXXXX";
+  std::string dir = mkdtemp(tmpl);
+  { std::ofstream(dir + "/ca.pem") << "PEM"; }
+  { std::ofstream(dir + "/tok") << "file-token\n"; }
+  {
+    std::ofstream(dir + "/config") << R"(apiVersion: v1
+kind: Config
+current-context: dev
+clusters:
+- name: prod
+  cluster:
+    server: https://prod:6443
+    certificate-authority-data: UEVNLURBVEE=
+- name: dev
+  cluster:
+    server: https://127.0.0.1:7443
+    certificate-authority: ca.pem
+contexts:
+- name: dev
+  context: {cluster: dev, user: dev-user, namespace: ns1}
+- name: prod
+  context:
+    cluster: prod
+    user: prod-user
+- name: broken
+  context: {cluster: dev, user: exec-user}
+users:
+- name: dev-user
+  user:
+    tokenFile: tok
+- name: prod-user
+  user:
+    token: abc
+    client-certificate-data: Q0VSVA==
+    client-key-data: S0VZ
+- name: exec-user
+  user:
+    exec: {command: aws}
+)";
+  }
+  KubeConfig d = load_kubeconfig(dir + "/config");
+  EXPECT_EQ(d.context, std::string("dev"));
+  EXPECT_EQ(d.server, std::string("https://127.0.0.1:7443"));
+  EXPECT_EQ(d.tls.ca_file, dir + "/ca.pem");
+  EXPECT_EQ(d.token, std::string("file-token"));
+  EXPECT_EQ(d.ns, std::string("ns1"));
+  KubeConfig p = load_kubeconfig(dir + "/config", "prod");
+  EXPECT_EQ(p.tls.ca_pem, std::string("PEM-DATA"));
+  EXPECT_EQ(p.tls.cert_pem, std::string("CERT"));
+  EXPECT_EQ(p.tls.key_pem, std::string("KEY"));
+  EXPECT_EQ(p.token, std::string("abc"));
+  EXPECT_THROW(load_kubeconfig(dir + "/config", "broken"));
+  EXPECT_THROW(load_kubeconfig(dir + "/config", "missing"));
+  EXPECT_THROW(load_kubeconfig(dir + "/nope"));
+  for (const char* f : {"/config", "/ca.pem", "/tok"}) std::remove((dir + f).c_str());
+  rmdir(dir.c_str());
 }
 
 TEST(kube_in_cluster_config) {

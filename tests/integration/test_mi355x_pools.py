@@ -211,7 +211,10 @@ def test_leader_election_failover(cluster_factory):
     c = cluster_factory(manager_args=lease)
     k = c.client
     from gpupool.kube import LEASES
-    first = k.get(LEASES, "gpupool-manager-leader", "gpupool-system")["spec"]["holderIdentity"]
+    # the port file appears before the first acquire: wait for the Lease itself
+    first = k.wait_for(LEASES, "gpupool-manager-leader", "gpupool-system",
+                       lambda o: bool(o) and bool(o["spec"].get("holderIdentity")), timeout=15,
+                       poll=0.05)["spec"]["holderIdentity"]
     # a second manager stands by
     standby = c._spawn("manager2", [c.procs["manager"].args[0], "--apiserver", c.url,
                                     "--identity", "standby", "--progress-poll", "100ms"] + lease)
