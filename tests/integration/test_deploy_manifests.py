@@ -81,3 +81,16 @@ def test_agent_rbac_covers_agent_api_calls():
             granted = _granted(o["rules"])
     missing = sorted(u for u in used if u not in granted)
     assert used and not missing, (used, missing)
+
+
+def test_kustomization_lists_every_deploy_manifest():
+    import glob
+
+    import yaml
+    kz = yaml.safe_load(open(os.path.join(ROOT, "config", "default", "kustomization.yaml")))
+    listed = {os.path.normpath(os.path.join(ROOT, "config", "default", r)) for r in kz["resources"]}
+    shipped = {os.path.normpath(p) for d in ("crd", "manager", "rbac", "agent")
+               for p in glob.glob(os.path.join(ROOT, "config", d, "*.yaml"))}
+    assert listed == shipped
+    mon = list(yaml.safe_load_all(open(os.path.join(ROOT, "config", "prometheus", "monitor.yaml"))))
+    assert {m["kind"] for m in mon} == {"Service", "ServiceMonitor"}
