@@ -360,14 +360,20 @@ __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const sho
 }
 
 // Full VALU reference (independent of the matrix cores), fp32, k-ordered.
+// One thread per output; both operand rows read with 16-byte loads (K % 8 == 0).
 __global__ void gemm_ref_valu(const short* __restrict__ A, const short* __restrict__ Bt,
                               float* __restrict__ C, int M, int N, int K) {
   int n = blockIdx.x * blockDim.x + threadIdx.x;
   int m = blockIdx.y;
   if (n >= N || m >= M) return;
+  const bf16x8* a = reinterpret_cast<const bf16x8*>(A + static_cast<int64_t>(m) * K);
+  const bf16x8* b = reinterpret_cast<const bf16x8*>(Bt + static_cast<int64_t>(n) * K);
   float s = 0.f;
-  for (int k = 0; k < K; ++k) s = fmaf(bf16_to_f32(A[static_cast<int64_t>(m) * K + k]),
-                                       bf16_to_f32(Bt[static_cast<int64_t>(n) * K + k]), s);
+  for (int k8 = 0; k8 < K / 8; ++k8) {
+    const bf16x8 av = a[k8], bv = b[k8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s = fmaf(bf16_to_f32(av[j]), bf16_to_f32(bv[j]), s);
+  }
   C[static_cast<int64_t>(m) * N + n] = s;
 }
 
@@ -577,18 +583,26 @@ std::string run_probe(int dev, const char* opts) {
   for (int pi = 0; pi < patterns; ++pi)
     PROBE_CHECK(hipMemsetAsync(cnt + 2 * pi + 1, 0xFF, sizeof(unsigned long long), s));
   auto* hbm = reinterpret_cast<u32x4*>(base);
-  const int hbm_grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(cus) * 8,
-                                                          (n16 + kHbmThreads - 1) / kHbmThreads));
+  // Grid per HBM kernel (workgroups per CU). Measured on MI355X (scripts/probe_hbm_sweep.py):
+  // the streaming store kernel is fastest with few long-running waves per CU, the verify kernel
+  // with a few more loads in flight; the old 8/CU for both was among the slowest settings.
+  auto hbm_grid_for = [&](const char* key, long long def) {
+    const uint64_t per_cu = static_cast<uint64_t>(std::max(1LL, opt_int(opts, key, def)));
+    return static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(cus) * per_cu,
+                                               (n16 + kHbmThreads - 1) / kHbmThreads));
+  };
+  const int fill_grid = hbm_grid_for("hbmFillBlocksPerCU", opt_int(opts, "hbmBlocksPerCU", 1));
+  const int verify_grid = hbm_grid_for("hbmVerifyBlocksPerCU", opt_int(opts, "hbmBlocksPerCU", 3));
   const uint32_t seed = 0xA5A50000u + static_cast<uint32_t>(dev);
   PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
   for (int pi = 0; pi < patterns; ++pi) {
     const uint32_t flip = (pi & 1) ? 0xFFFFFFFFu : 0u;  // complementary polarity on odd passes
-    hipLaunchKernelGGL(hbm_fill, dim3(hbm_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip);
+    hipLaunchKernelGGL(hbm_fill, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip);
     PROBE_CHECK(hipEventRecord(ctx.ev[1 + 2 * pi], s));
     if (pi == 0 && inject_flips > 0)
       hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(hbm), n16 * 4,
                          inject_flips);
-    hipLaunchKernelGGL(hbm_verify, dim3(hbm_grid), dim3(kHbmThreads), 0, s, static_cast<const u32x4*>(hbm), n16, seed,
+    hipLaunchKernelGGL(hbm_verify, dim3(verify_grid), dim3(kHbmThreads), 0, s, static_cast<const u32x4*>(hbm), n16, seed,
                        flip, cnt + 2 * pi, cnt + 2 * pi + 1);
     PROBE_CHECK(hipEventRecord(ctx.ev[2 + 2 * pi], s));
   }
