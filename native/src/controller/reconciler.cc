@@ -2,6 +2,9 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iterator>
 #include <random>
 #include <sstream>
 
@@ -668,8 +671,35 @@ AzureVmPoolReconciler::AzureVmPoolReconciler(KubeClient& client, Informer& pools
                                              EventRecorder* events, ReconcilerOptions opts)
     : PoolReconcilerBase(client, pools, events, opts, "AzureVmPool", res::azurevmpools()), cloud_(cloud) {}
 
+static const char* const kWorkloadIdentity = "workload-identity";
+
 bool AzureVmPoolReconciler::credentials_(const ObjectMeta& m, const AzureVmPoolSpec& spec, Credentials* out,
                                          std::string* why) {
+  // Workload Identity (README.md:311, the reference's production recommendation): with
+  // spec.azureCredentialSecret == "workload-identity" the manager uses ITS OWN federated identity:
+  // AZURE_CLIENT_ID / AZURE_TENANT_ID / AZURE_SUBSCRIPTION_ID and the projected ServiceAccount
+  // token at AZURE_FEDERATED_TOKEN_FILE (what the AKS webhook injects) - no static secret.
+  if (spec.credential_secret == kWorkloadIdentity) {
+    std::vector<std::string> missing;
+    for (const char* k : {"AZURE_CLIENT_ID", "AZURE_TENANT_ID", "AZURE_SUBSCRIPTION_ID", "AZURE_FEDERATED_TOKEN_FILE"}) {
+      const char* v = getenv(k);
+      if (!v || !*v) missing.push_back(k);
+      else out->values[k] = v;
+    }
+    if (!missing.empty()) {
+      *why = "workload identity: manager environment lacks " + join(missing, ",");
+      return false;
+    }
+    std::ifstream tf(out->values["AZURE_FEDERATED_TOKEN_FILE"]);
+    std::string token((std::istreambuf_iterator<char>(tf)), std::istreambuf_iterator<char>());
+    if (token.find_first_not_of(" \r\n\t") == std::string::npos) {
+      *why = "workload identity: federated token file " + out->values["AZURE_FEDERATED_TOKEN_FILE"] + " is empty or unreadable";
+      return false;
+    }
+    out->values["AZURE_CLIENT_SECRET"] = "";  // a client assertion (the token) replaces the secret
+    out->values["AZURE_FEDERATED_TOKEN"] = token;
+    return true;
+  }
   // README.md:179-185: the client is built from the Secret named by spec.azureCredentialSecret.
   Json secret;
   try {
@@ -731,8 +761,12 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
     // README.md:184 intended a 30 s requeue; typed outcome makes that delay real.
     return Outcome::requeue(opts_.credentials_retry, why);
   }
-  set_condition(conds, gen::kCondCredentialsValid, "True", "SecretResolved",
-                "Secret " + m.ns + "/" + spec.credential_secret + " has all four keys", m.generation, now);
+  if (spec.credential_secret == kWorkloadIdentity)
+    set_condition(conds, gen::kCondCredentialsValid, "True", "WorkloadIdentity",
+                  "federated token for client " + creds.values["AZURE_CLIENT_ID"], m.generation, now);
+  else
+    set_condition(conds, gen::kCondCredentialsValid, "True", "SecretResolved",
+                  "Secret " + m.ns + "/" + spec.credential_secret + " has all four keys", m.generation, now);
 
   std::vector<VmRecord> vms;
   try {

@@ -30,7 +30,11 @@ Json VmRecord::to_json() const {
 FakeCloudProvider::FakeCloudProvider(FakeCloudOptions opts) : opts_(std::move(opts)) { load_(); }
 
 void FakeCloudProvider::check_creds_(const Credentials& c) {
+  // ARM accepts either a client secret or a federated client assertion (workload identity)
+  auto fed = c.values.find("AZURE_FEDERATED_TOKEN");
+  const bool federated = fed != c.values.end() && !fed->second.empty();
   for (const char* k : gen::kAzureCredentialKeys) {
+    if (federated && std::string(k) == "AZURE_CLIENT_SECRET") continue;
     auto it = c.values.find(k);
     if (it == c.values.end() || it->second.empty())
       throw ProviderError("CredentialsMissing", std::string("credential key ") + k + " missing", false);

@@ -110,3 +110,29 @@ def test_invalid_spec_rejected_at_admission(azure):
     with pytest.raises(KubeError) as e:
         azure.client.create(AZUREVMPOOLS, doc, "default")
     assert e.value.code == 422 and "spec.replicas" in str(e.value)
+
+
+def test_workload_identity_credentials(cluster_factory, tmp_path):
+    """README.md:311 roadmap: Workload Identity instead of a static Secret. The manager's own
+    federated identity (env + projected token file) is used when the pool names the
+    'workload-identity' credential source."""
+    token = tmp_path / "azure-identity-token"
+    token.write_text("eyJhbGciOiJSUzI1NiJ9.fake.jwt\n")
+    env = {"AZURE_CLIENT_ID": "11111111-2222-3333-4444-555555555555",
+           "AZURE_TENANT_ID": "tenant", "AZURE_SUBSCRIPTION_ID": "sub",
+           "AZURE_FEDERATED_TOKEN_FILE": str(token)}
+    c = cluster_factory(nodes=[], kinds="azure", env=env,
+                        manager_args=["--fakecloud-state", str(tmp_path / "cloud.json"),
+                                      "--credentials-retry", "300ms"])
+    k = c.client
+    pool = sample("wi-pool", 1)
+    pool["spec"]["azureCredentialSecret"] = "workload-identity"
+    k.create(AZUREVMPOOLS, pool, "default")  # note: no Secret exists
+    o = k.wait_for(AZUREVMPOOLS, "wi-pool", "default", az_ready(1), timeout=20)
+    assert conds(o)["CredentialsValid"]["reason"] == "WorkloadIdentity"
+    # an empty projected token makes the credentials invalid (and the pool says why)
+    token.write_text("")
+    k.patch(AZUREVMPOOLS, "wi-pool", {"spec": {"replicas": 2}}, "default")
+    o = k.wait_for(AZUREVMPOOLS, "wi-pool", "default",
+                   cond_is("CredentialsValid", "False", "CredentialsMissing"), timeout=20)
+    assert "federated token file" in conds(o)["CredentialsValid"]["message"]
