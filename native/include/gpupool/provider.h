@@ -159,14 +159,16 @@ class RocmProvider : public DeviceProvider {
   void update_policy(const std::string& node, const std::string& pool_uid, const Json& policy,
                      const std::string& resource_name) override;
   std::string endpoint_of(const std::string& node);
-  HttpClient& client_for(const std::string& node);  // throws ProviderError if no agent
+  // Shared so an in-flight RPC keeps its client alive when the node's endpoint changes (agent
+  // restarted elsewhere) and another thread swaps the cached client. Throws ProviderError.
+  std::shared_ptr<HttpClient> client_for(const std::string& node);
 
  private:
   Json post_(const std::string& node, const std::string& path, const Json& body);
   Informer& nodes_;
   int timeout_ms_;
   std::mutex mu_;
-  std::map<std::string, std::pair<std::string, std::unique_ptr<HttpClient>>> clients_;
+  std::map<std::string, std::pair<std::string, std::shared_ptr<HttpClient>>> clients_;
 };
 
 }  // namespace gpupool

@@ -92,24 +92,24 @@ std::string RocmProvider::endpoint_of(const std::string& node) {
   return n->path("metadata.annotations")[gen::kAnnAgentEndpoint].as_string();
 }
 
-HttpClient& RocmProvider::client_for(const std::string& node) {
+std::shared_ptr<HttpClient> RocmProvider::client_for(const std::string& node) {
   std::string ep = endpoint_of(node);
   if (ep.empty()) throw ProviderError("AgentNotFound", "no gpupool agent registered on node " + node);
   std::lock_guard<std::mutex> g(mu_);
   auto& slot = clients_[node];
   if (!slot.second || slot.first != ep) {
     slot.first = ep;
-    slot.second = std::make_unique<HttpClient>(Url::parse(ep), "", timeout_ms_);
+    slot.second = std::make_shared<HttpClient>(Url::parse(ep), "", timeout_ms_);
   }
-  return *slot.second;
+  return slot.second;
 }
 
 Json RocmProvider::post_(const std::string& node, const std::string& path, const Json& body) {
   trace::Span span("agent:POST " + path);
-  HttpClient& c = client_for(node);
+  std::shared_ptr<HttpClient> c = client_for(node);
   HttpResponse r;
   try {
-    r = c.request("POST", path, body.dump());
+    r = c->request("POST", path, body.dump());
   } catch (const std::exception& e) {
     throw ProviderError("AgentUnreachable", "agent on " + node + ": " + e.what());
   }
@@ -129,8 +129,8 @@ NodeView RocmProvider::observe(const std::string& node) {
   nv.endpoint = endpoint_of(node);
   trace::Span span("agent:GET /v1/node");
   try {
-    HttpClient& c = client_for(node);
-    HttpResponse r = c.request("GET", "/v1/node");
+    std::shared_ptr<HttpClient> c = client_for(node);
+    HttpResponse r = c->request("GET", "/v1/node");
     if (r.status >= 400) throw ProviderError("AgentError", "GET /v1/node: HTTP " + std::to_string(r.status));
     Json j = Json::parse(r.body);
     nv.reachable = true;
