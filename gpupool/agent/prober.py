@@ -74,7 +74,11 @@ class Prober:
                     "error": f"device {dev.get('hipUUID')} not visible to HIP in this process",
                     "ms": 0.0}
         if self.mode == "inproc":
-            res = self._hip.run(ordinal, hbm_bytes=hbm, mfma=mfma, gemm_n=self.gemm_n)
+            # The HBM test and the MFMA phase normally overlap on two streams (~13 % shorter
+            # probe). With performance floors the pool wants clean numbers: run them serially.
+            floors = float(opts.get("minHbmGBps") or 0) > 0 or float(opts.get("minMfmaTflops") or 0) > 0
+            res = self._hip.run(ordinal, hbm_bytes=hbm, mfma=mfma, gemm_n=self.gemm_n,
+                                overlap=0 if floors else 1)
         else:
             cmd = [native_path("mi355x-probe"), "--device", str(ordinal), "--hbm-bytes", str(hbm),
                    "--gemm-n", str(self.gemm_n)] + ([] if mfma else ["--no-mfma"])

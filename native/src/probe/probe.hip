@@ -459,8 +459,10 @@ constexpr long long kMaxPatterns = 4;
 constexpr int kSlotSmall = 2 * kMaxPatterns, kSlotAbft = kSlotSmall + 1, kResSlots = kSlotAbft + 1;
 
 struct DeviceCtx {
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // HBM pattern test
+  hipStream_t stream2 = nullptr;  // MFMA checks, overlapped with the bandwidth-bound HBM test
   hipEvent_t ev[1 + 2 * kMaxPatterns] = {};
+  hipEvent_t gev[3] = {};         // GEMM timing + "counters zeroed" hand-off between the streams
   hipDeviceProp_t prop{};
   unsigned long long* host_res = nullptr;
   bool ready = false;
@@ -530,6 +532,79 @@ std::string hip_uuid(int dev) {
   return "GPU-" + hex;
 }
 
+// Enqueues the whole MFMA phase on stream s (no host sync): (a) a 256^3 GEMM checked element by
+// element against the VALU reference with asymmetric operands, (b) the timed N^3 GEMM (events
+// ctx.gev[0..1]) with exact int64 ABFT row/column checksums, then copies the two mismatch
+// counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``.
+void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, bool inject_gemm, unsigned long long* cnt,
+                       unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
+  const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
+  auto align = [](size_t x) { return (x + 4095) & ~static_cast<size_t>(4095); };
+  char* p = gbase;
+  auto carve = [&](size_t bytes) {
+    char* q = p;
+    p += align(bytes);
+    return q;
+  };
+  auto* a0 = reinterpret_cast<short*>(carve(n0 * n0 * 2));
+  auto* b0 = reinterpret_cast<short*>(carve(n0 * n0 * 2));
+  auto* c0 = reinterpret_cast<float*>(carve(n0 * n0 * 4));
+  auto* r0 = reinterpret_cast<float*>(carve(n0 * n0 * 4));
+  auto* a = reinterpret_cast<short*>(carve(n * n * 2));
+  auto* b = reinterpret_cast<short*>(carve(n * n * 2));
+  auto* c = reinterpret_cast<float*>(carve(n * n * 4));
+  auto* v = reinterpret_cast<unsigned long long*>(carve(6 * n * 8));
+  auto gemm = [&](const short* a_, const short* b_, float* c_, int nn) {
+    if (tile256)
+      hipLaunchKernelGGL(gemm_bf16_mfma_256, dim3((nn / G2_BM) * (nn / G2_BN)), dim3(kGemm2Threads), 0, s, a_, b_, c_, nn,
+                         nn, nn);
+    else
+      hipLaunchKernelGGL(gemm_bf16_mfma_nt, dim3((nn / BM) * (nn / BN)), dim3(kGemmThreads), 0, s, a_, b_, c_, nn, nn, nn);
+  };
+  // (a) 256^3 full-element check vs the VALU reference; asymmetric operands
+  const uint64_t e0 = static_cast<uint64_t>(n0) * n0;
+  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, a0, e0, 0x1234u, 3);
+  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, b0, e0, 0xBEEFu, 3);
+  gemm(a0, b0, c0, static_cast<int>(n0));
+  hipLaunchKernelGGL(gemm_ref_valu, dim3(n0 / 256, n0), dim3(256), 0, s, a0, b0, r0, static_cast<int>(n0),
+                     static_cast<int>(n0), static_cast<int>(n0));
+  hipLaunchKernelGGL(count_diff, dim3(64), dim3(256), 0, s, static_cast<const float*>(c0), static_cast<const float*>(r0),
+                     e0, cnt + kSlotSmall);
+  PROBE_CHECK(hipGetLastError());
+
+  // (b) N^3 timed GEMM + exact ABFT checksums
+  const uint64_t e = static_cast<uint64_t>(n) * n;
+  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, a, e, 0x51u, 2);
+  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, b, e, 0x77u, 2);
+  // the 256^3 check above already ran this kernel's code object: time the first launch
+  PROBE_CHECK(hipEventRecord(ctx.gev[0], s));
+  for (int rep = 0; rep < reps; ++rep) gemm(a, b, c, gemm_n);
+  PROBE_CHECK(hipEventRecord(ctx.gev[1], s));
+  PROBE_CHECK(hipGetLastError());
+  if (inject_gemm)
+    hipLaunchKernelGGL(inject_gemm_fault, dim3(1), dim3(1), 0, s, c, static_cast<int64_t>(gemm_n / 3) * gemm_n + gemm_n / 5);
+  // ABFT checksums: 6 int64 vectors [acol | bcol | colsumC | expCol | rowsumC | expRow]
+  unsigned long long *vacol = v, *vbcol = v + n, *vcolC = v + 2 * n, *vexpC = v + 3 * n, *vrowC = v + 4 * n,
+                     *vexpR = v + 5 * n;
+  PROBE_CHECK(hipMemsetAsync(v, 0, 3 * n * 8, s));
+  const dim3 cgrid((gemm_n + 255) / 256, (gemm_n + kColChunk - 1) / kColChunk);
+  hipLaunchKernelGGL(colsum_partial<short>, cgrid, dim3(256), 0, s, static_cast<const short*>(a), gemm_n, gemm_n, vacol);
+  hipLaunchKernelGGL(colsum_partial<short>, cgrid, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n, vbcol);
+  hipLaunchKernelGGL(colsum_partial<float>, cgrid, dim3(256), 0, s, static_cast<const float*>(c), gemm_n, gemm_n, vcolC);
+  const dim3 rgrid((gemm_n + 3) / 4);
+  hipLaunchKernelGGL(rowdot<short>, rgrid, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n,
+                     static_cast<const unsigned long long*>(vacol), vexpC);
+  hipLaunchKernelGGL(rowdot<float>, rgrid, dim3(256), 0, s, static_cast<const float*>(c), gemm_n, gemm_n,
+                     static_cast<const unsigned long long*>(nullptr), vrowC);
+  hipLaunchKernelGGL(rowdot<short>, rgrid, dim3(256), 0, s, static_cast<const short*>(a), gemm_n, gemm_n,
+                     static_cast<const unsigned long long*>(vbcol), vexpR);
+  hipLaunchKernelGGL(count_ne_u64, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vcolC, vexpC, gemm_n, cnt + kSlotAbft);
+  hipLaunchKernelGGL(count_ne_u64, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vrowC, vexpR, gemm_n, cnt + kSlotAbft);
+  PROBE_CHECK(hipGetLastError());
+  PROBE_CHECK(hipMemcpyAsync(hres + kSlotSmall, cnt + kSlotSmall, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             s));
+}
+
 std::string run_probe(int dev, const char* opts) {
   const uint64_t hbm_bytes = static_cast<uint64_t>(opt_int(opts, "hbmBytes", 1LL << 30));
   const bool do_mfma = opt_int(opts, "mfma", 1) != 0;
@@ -539,12 +614,17 @@ std::string run_probe(int dev, const char* opts) {
   const int inject_flips = static_cast<int>(std::min(4096LL, std::max(0LL, opt_int(opts, "injectBitFlips", 0))));
   const bool inject_gemm = opt_int(opts, "injectGemmFault", 0) != 0;
   const bool tile256 = opt_int(opts, "gemmTile", 256) != 128;  // 128 = the older 128x128 kernel (A/B)
+  // The HBM test is bandwidth-bound with few waves per CU; the MFMA phase is compute-bound and
+  // touches ~130 MiB: run them concurrently on two streams (overlap=0: one stream, serial).
+  const bool overlap = opt_int(opts, "overlap", 1) != 0;
   auto t0 = std::chrono::steady_clock::now();
   PROBE_CHECK(hipSetDevice(dev));
   DeviceCtx& ctx = g_ctx[static_cast<size_t>(dev)];
   if (!ctx.ready) {
     PROBE_CHECK(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
+    PROBE_CHECK(hipStreamCreateWithFlags(&ctx.stream2, hipStreamNonBlocking));
     for (auto& e : ctx.ev) PROBE_CHECK(hipEventCreate(&e));
+    for (auto& e : ctx.gev) PROBE_CHECK(hipEventCreate(&e));
     PROBE_CHECK(hipGetDeviceProperties(&ctx.prop, dev));
     // pinned result slots: device->host copies of the counters are truly async (one sync per phase)
     PROBE_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ctx.host_res), kResSlots * sizeof(unsigned long long)));
@@ -558,9 +638,8 @@ std::string run_probe(int dev, const char* opts) {
   };
   const double setup_ms = ms_since(t0);
 
-  // ---------------- one arena for the whole probe. The HBM pattern region is reused for the GEMM
-  // operands once its verify kernels have run (stream order), so a probe costs one hipMalloc/hipFree
-  // instead of a dozen, and the allocation is sized for the larger of the two phases.
+  // ---------------- one arena for the whole probe: [HBM pattern region | GEMM operands | counters],
+  // so a probe costs one hipMalloc/hipFree instead of a dozen.
   auto t_alloc = std::chrono::steady_clock::now();
   const uint64_t n16 = hbm_bytes / 16;
   const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
@@ -568,20 +647,35 @@ std::string run_probe(int dev, const char* opts) {
   const size_t sz_a0 = align(n0 * n0 * 2), sz_c0 = align(n0 * n0 * 4), sz_a = align(n * n * 2), sz_c = align(n * n * 4),
                sz_v = align(6 * n * 8);
   const size_t gemm_bytes = do_mfma ? 2 * sz_a0 + 2 * sz_c0 + 2 * sz_a + sz_c + sz_v : 0;
-  const size_t region = std::max(align(n16 * 16), gemm_bytes);
+  const size_t hbm_region = align(n16 * 16);
+  const size_t region = hbm_region + gemm_bytes;
   DevBuf arena;
   PROBE_CHECK(hipMalloc(&arena.p, region + align(kResSlots * sizeof(unsigned long long))));
   char* base = static_cast<char*>(arena.p);
   auto* cnt = reinterpret_cast<unsigned long long*>(base + region);
   unsigned long long* hres = ctx.host_res;
   const double alloc_ms = ms_since(t_alloc);
-  auto t_hbm = std::chrono::steady_clock::now();
+  auto t_run = std::chrono::steady_clock::now();
 
-  // ---------------- HBM: all patterns back to back, per-pattern counters, one sync
-  // counters: [2p] = flipped bits, [2p+1] = first bad 16-B index (init all-ones) of pattern p
+  // counters: [2p] = flipped bits, [2p+1] = first bad 16-B index (init all-ones) of pattern p,
+  // then the two GEMM check counters. Zeroed on s; s2 waits for that before its first kernel.
   PROBE_CHECK(hipMemsetAsync(cnt, 0, kResSlots * sizeof(unsigned long long), s));
   for (int pi = 0; pi < patterns; ++pi)
     PROBE_CHECK(hipMemsetAsync(cnt + 2 * pi + 1, 0xFF, sizeof(unsigned long long), s));
+  hipStream_t s2 = overlap ? ctx.stream2 : s;
+  if (overlap) {
+    PROBE_CHECK(hipEventRecord(ctx.gev[2], s));
+    PROBE_CHECK(hipStreamWaitEvent(s2, ctx.gev[2], 0));
+  }
+
+  // ---------------- MFMA phase (launched first so it starts beside the HBM fill)
+  bool mfma_ok = true;
+  unsigned long long small_bad = 0, abft_bad = 0;
+  double tflops = 0, gemm_ms = 0;
+  const int reps = static_cast<int>(std::max(1LL, opt_int(opts, "gemmReps", 1)));
+  if (do_mfma) launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, cnt, hres, ctx, s2);
+
+  // ---------------- HBM: all patterns back to back, per-pattern counters
   auto* hbm = reinterpret_cast<u32x4*>(base);
   // Grid per HBM kernel (workgroups per CU). Measured on MI355X (scripts/probe_hbm_sweep.py):
   // the streaming store kernel is fastest with few long-running waves per CU, the verify kernel
@@ -609,6 +703,18 @@ std::string run_probe(int dev, const char* opts) {
   PROBE_CHECK(hipGetLastError());
   PROBE_CHECK(hipMemcpyAsync(hres, cnt, 2 * patterns * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   PROBE_CHECK(hipStreamSynchronize(s));
+  const double hbm_wall_ms = ms_since(t_run);
+  if (do_mfma) {
+    PROBE_CHECK(hipStreamSynchronize(s2));
+    float ms;
+    PROBE_CHECK(hipEventElapsedTime(&ms, ctx.gev[0], ctx.gev[1]));
+    gemm_ms = ms / reps;
+    tflops = 2.0 * gemm_n * static_cast<double>(gemm_n) * gemm_n / (gemm_ms * 1e-3) / 1e12;
+    small_bad = hres[kSlotSmall];
+    abft_bad = hres[kSlotAbft];
+    mfma_ok = small_bad == 0 && abft_bad == 0;
+  }
+  const double mfma_wall_ms = do_mfma ? ms_since(t_run) : 0.0;
   unsigned long long bad_bits = 0, first_bad = ~0ull;
   float write_ms = 0, read_ms = 0;
   for (int pi = 0; pi < patterns; ++pi) {
@@ -625,89 +731,6 @@ std::string run_probe(int dev, const char* opts) {
   const double read_gbps = bytes_moved / (read_ms * 1e-3) / 1e9;
   const double hbm_gbps = 2.0 * bytes_moved / ((write_ms + read_ms) * 1e-3) / 1e9;
   const bool hbm_ok = bad_bits == 0;
-  const double hbm_wall_ms = ms_since(t_hbm);
-  auto t_mfma = std::chrono::steady_clock::now();
-
-  // ---------------- MFMA
-  bool mfma_ok = true;
-  unsigned long long small_bad = 0, abft_bad = 0;
-  double tflops = 0, gemm_ms = 0;
-  if (do_mfma) {
-    char* p = base;
-    auto carve = [&](size_t bytes) {
-      char* q = p;
-      p += bytes;
-      return q;
-    };
-    auto* a0 = reinterpret_cast<short*>(carve(sz_a0));
-    auto* b0 = reinterpret_cast<short*>(carve(sz_a0));
-    auto* c0 = reinterpret_cast<float*>(carve(sz_c0));
-    auto* r0 = reinterpret_cast<float*>(carve(sz_c0));
-    auto* a = reinterpret_cast<short*>(carve(sz_a));
-    auto* b = reinterpret_cast<short*>(carve(sz_a));
-    auto* c = reinterpret_cast<float*>(carve(sz_c));
-    auto* v = reinterpret_cast<unsigned long long*>(carve(sz_v));
-    auto gemm = [&](const short* a_, const short* b_, float* c_, int nn) {
-      if (tile256)
-        hipLaunchKernelGGL(gemm_bf16_mfma_256, dim3((nn / G2_BM) * (nn / G2_BN)), dim3(kGemm2Threads), 0, s, a_, b_, c_,
-                           nn, nn, nn);
-      else
-        hipLaunchKernelGGL(gemm_bf16_mfma_nt, dim3((nn / BM) * (nn / BN)), dim3(kGemmThreads), 0, s, a_, b_, c_, nn, nn,
-                           nn);
-    };
-    // (a) 256^3 full-element check vs the VALU reference; asymmetric operands
-    const uint64_t e0 = static_cast<uint64_t>(n0) * n0;
-    hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, a0, e0, 0x1234u, 3);
-    hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, b0, e0, 0xBEEFu, 3);
-    gemm(a0, b0, c0, static_cast<int>(n0));
-    hipLaunchKernelGGL(gemm_ref_valu, dim3(n0 / 256, n0), dim3(256), 0, s, a0, b0, r0, static_cast<int>(n0),
-                       static_cast<int>(n0), static_cast<int>(n0));
-    hipLaunchKernelGGL(count_diff, dim3(64), dim3(256), 0, s, static_cast<const float*>(c0),
-                       static_cast<const float*>(r0), e0, cnt + kSlotSmall);
-    PROBE_CHECK(hipGetLastError());
-
-    // (b) N^3 timed GEMM + exact ABFT checksums
-    const uint64_t e = static_cast<uint64_t>(n) * n;
-    hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, a, e, 0x51u, 2);
-    hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, b, e, 0x77u, 2);
-    // the 256^3 check above already ran this kernel's code object: time the first launch
-    PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
-    const int reps = static_cast<int>(std::max(1LL, opt_int(opts, "gemmReps", 1)));
-    for (int rep = 0; rep < reps; ++rep) gemm(a, b, c, gemm_n);
-    PROBE_CHECK(hipEventRecord(ctx.ev[1], s));
-    PROBE_CHECK(hipGetLastError());
-    if (inject_gemm)
-      hipLaunchKernelGGL(inject_gemm_fault, dim3(1), dim3(1), 0, s, c, static_cast<int64_t>(gemm_n / 3) * gemm_n + gemm_n / 5);
-    // ABFT checksums: 6 int64 vectors [acol | bcol | colsumC | expCol | rowsumC | expRow]
-    unsigned long long *vacol = v, *vbcol = v + n, *vcolC = v + 2 * n, *vexpC = v + 3 * n, *vrowC = v + 4 * n,
-                       *vexpR = v + 5 * n;
-    PROBE_CHECK(hipMemsetAsync(v, 0, 3 * n * 8, s));
-    const dim3 cgrid((gemm_n + 255) / 256, (gemm_n + kColChunk - 1) / kColChunk);
-    hipLaunchKernelGGL(colsum_partial<short>, cgrid, dim3(256), 0, s, static_cast<const short*>(a), gemm_n, gemm_n, vacol);
-    hipLaunchKernelGGL(colsum_partial<short>, cgrid, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n, vbcol);
-    hipLaunchKernelGGL(colsum_partial<float>, cgrid, dim3(256), 0, s, static_cast<const float*>(c), gemm_n, gemm_n, vcolC);
-    const dim3 rgrid((gemm_n + 3) / 4);
-    hipLaunchKernelGGL(rowdot<short>, rgrid, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n,
-                       static_cast<const unsigned long long*>(vacol), vexpC);
-    hipLaunchKernelGGL(rowdot<float>, rgrid, dim3(256), 0, s, static_cast<const float*>(c), gemm_n, gemm_n,
-                       static_cast<const unsigned long long*>(nullptr), vrowC);
-    hipLaunchKernelGGL(rowdot<short>, rgrid, dim3(256), 0, s, static_cast<const short*>(a), gemm_n, gemm_n,
-                       static_cast<const unsigned long long*>(vbcol), vexpR);
-    hipLaunchKernelGGL(count_ne_u64, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vcolC, vexpC, gemm_n, cnt + kSlotAbft);
-    hipLaunchKernelGGL(count_ne_u64, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vrowC, vexpR, gemm_n, cnt + kSlotAbft);
-    PROBE_CHECK(hipGetLastError());
-    PROBE_CHECK(hipMemcpyAsync(hres + kSlotSmall, cnt + kSlotSmall, 2 * sizeof(unsigned long long),
-                               hipMemcpyDeviceToHost, s));
-    PROBE_CHECK(hipStreamSynchronize(s));
-    float ms;
-    PROBE_CHECK(hipEventElapsedTime(&ms, ctx.ev[0], ctx.ev[1]));
-    gemm_ms = ms / reps;
-    tflops = 2.0 * gemm_n * static_cast<double>(gemm_n) * gemm_n / (gemm_ms * 1e-3) / 1e12;
-    small_bad = hres[kSlotSmall];
-    abft_bad = hres[kSlotAbft];
-    mfma_ok = small_bad == 0 && abft_bad == 0;
-  }
-  const double mfma_wall_ms = do_mfma ? ms_since(t_mfma) : 0.0;
   auto t_free = std::chrono::steady_clock::now();
   (void)hipFree(arena.p);
   arena.p = nullptr;

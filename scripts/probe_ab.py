@@ -37,8 +37,10 @@ def main() -> int:
                 if not res.get("passed"):
                     failures.append(res)
                 runs.setdefault(f"tile{tile}_n{n}", []).append(res)
-        # the agent's default probe (1 GiB HBM, N=4096, 256 tile): wall-time phases
+        # the agent's default probe (1 GiB HBM, N=4096, 256 tile, HBM test and MFMA phase
+        # overlapped on two streams) vs the same work serialised on one stream
         runs.setdefault("default_1GiB", []).append(probe.run(a.device))
+        runs.setdefault("serial_1GiB", []).append(probe.run(a.device, overlap=0))
     summary = {}
     for key, rs in runs.items():
         tf = [x["mfma"]["tflops"] for x in rs]
@@ -47,7 +49,7 @@ def main() -> int:
                             x["mfma"]["ms"] for x in rs), 4),
                         "probe_ms_median": round(statistics.median(x["ms"] for x in rs), 3),
                         "passed": all(x.get("passed") for x in rs)}
-        if key == "default_1GiB":
+        if key in ("default_1GiB", "serial_1GiB"):
             for ph in rs[0].get("phases", {}):
                 summary[key][ph + "_median"] = round(statistics.median(x["phases"][ph] for x in rs), 4)
             summary[key]["hbm_GBps_median"] = round(statistics.median(x["hbm"]["GBps"] for x in rs), 1)
