@@ -84,6 +84,8 @@ BUILTINS = [
     ResourceType("", "v1", "resourcequotas", "ResourceQuota", True, "resourcequota", ["quota"],
                  status_sub=True),
     ResourceType("coordination.k8s.io", "v1", "leases", "Lease", True, "lease"),
+    ResourceType("policy", "v1", "poddisruptionbudgets", "PodDisruptionBudget", True,
+                 "poddisruptionbudget", ["pdb"], status_sub=True),
     # stored-only kinds (no controllers behind them): lets `make deploy` manifests be applied
     # and validated against the simulator
     ResourceType("", "v1", "serviceaccounts", "ServiceAccount", True, "serviceaccount", ["sa"]),
@@ -588,8 +590,48 @@ class Store:
                         except ApiError:
                             pass
 
+    def _pdb_blocks(self, pod: dict) -> str | None:
+        """Eviction API semantics: refuse (429) when evicting ``pod`` would take a matching
+        PodDisruptionBudget below minAvailable / above maxUnavailable. Returns the PDB name."""
+        ns = pod["metadata"].get("namespace")
+        labels = pod["metadata"].get("labels") or {}
+        pods_rt = self.types[("", "pods")]
+        pdb_rt = self.types.get(("policy", "poddisruptionbudgets"))
+        if pdb_rt is None:
+            return None
+        for pdb in self.list(pdb_rt, ns)["items"]:
+            sel = ((pdb.get("spec") or {}).get("selector") or {}).get("matchLabels") or {}
+            if not sel or any(labels.get(k) != v for k, v in sel.items()):
+                continue
+            matching = [p for p in self.list(pods_rt, ns)["items"]
+                        if all((p["metadata"].get("labels") or {}).get(k) == v for k, v in sel.items())
+                        and not p["metadata"].get("deletionTimestamp")]
+            healthy = sum(1 for p in matching if (p.get("status") or {}).get("phase") == "Running")
+            expected = len(matching)
+
+            def resolve(v):
+                if isinstance(v, str) and v.endswith("%"):
+                    import math
+                    return math.ceil(expected * int(v[:-1]) / 100)
+                return int(v)
+            spec = pdb.get("spec") or {}
+            if "minAvailable" in spec and healthy - 1 < resolve(spec["minAvailable"]):
+                return pdb["metadata"]["name"]
+            if "maxUnavailable" in spec and expected - (healthy - 1) > resolve(spec["maxUnavailable"]):
+                return pdb["metadata"]["name"]
+        return None
+
     def evict(self, ns: str, name: str, body: dict | None) -> dict:
         rt = self.types[("", "pods")]
+        pod = self.get(rt, ns, name)
+        if not pod["metadata"].get("deletionTimestamp"):
+            blocker = self._pdb_blocks(pod)
+            if blocker:
+                raise ApiError(429, "TooManyRequests",
+                               "Cannot evict pod as it would violate the pod's disruption budget.",
+                               details={"causes": [{"reason": "DisruptionBudget",
+                                                    "message": f"The disruption budget {blocker} "
+                                                               "needs more healthy pods"}]})
         opts = (body or {}).get("deleteOptions") or {}
         self.delete(rt, ns, name, grace=opts.get("gracePeriodSeconds"),
                     preconditions=opts.get("preconditions"))

@@ -72,6 +72,7 @@ BY_KIND = {
     "Service": Res("", "v1", "services"),
     "Deployment": Res("apps", "v1", "deployments"),
     "DaemonSet": Res("apps", "v1", "daemonsets"),
+    "PodDisruptionBudget": Res("policy", "v1", "poddisruptionbudgets"),
 }
 
 

@@ -112,6 +112,7 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
   DeviceProvider& provider_;
   Informer* quotas_ = nullptr;
   std::map<std::string, std::set<std::string>> evicted_;  // pool uid -> pod keys already evicted
+  std::map<std::string, std::set<std::string>> eviction_blocked_;  // pool uid -> pods refused by a PDB (evented)
   std::map<std::string, int64_t> policy_gen_;             // pool uid -> generation pushed to agents
 };
 

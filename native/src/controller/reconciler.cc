@@ -243,18 +243,37 @@ int Mi355xPoolReconciler::drain_(const Json& obj, const std::string& node, const
           event_(obj, "Warning", "DrainTimeout", "force-deleted pod " + key + " on " + short_id(d) +
                                                      " after " + std::to_string(spec.drain_timeout_seconds) + "s");
         } else if (spec.drain_evict) {
-          bool first;
+          bool done;
           {
             std::lock_guard<std::mutex> g(mu_);
-            first = evicted_[m.uid].insert(key).second;
+            done = evicted_[m.uid].count(key) > 0;
           }
-          if (first) {
+          if (!done) {
+            // marked evicted only once the API accepted it: a PodDisruptionBudget refusal (429)
+            // is retried on the next pass until drain.timeoutSeconds forces the delete
             client_.evict(pns, pname, static_cast<int>(spec.drain_grace_seconds));
+            {
+              std::lock_guard<std::mutex> g(mu_);
+              evicted_[m.uid].insert(key);
+              eviction_blocked_[m.uid].erase(key);
+            }
             event_(obj, "Normal", "PodEvicted", "evicted pod " + key + " from " + short_id(d) + " (draining)");
           }
         }
       } catch (const KubeError& e) {
-        if (!e.not_found()) log_.warn("drain action failed", Json::object().set("pod", key).set("error", e.what()));
+        if (e.code == 429) {
+          bool first;
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            first = eviction_blocked_[m.uid].insert(key).second;
+          }
+          if (first)
+            event_(obj, "Warning", "EvictionBlocked", "pod " + key + " on " + short_id(d) + ": " + e.what() +
+                                                          " (retrying; forced after " +
+                                                          std::to_string(spec.drain_timeout_seconds) + "s)");
+        } else if (!e.not_found()) {
+          log_.warn("drain action failed", Json::object().set("pod", key).set("error", e.what()));
+        }
       }
     }
   }
@@ -263,6 +282,7 @@ int Mi355xPoolReconciler::drain_(const Json& obj, const std::string& node, const
     {
       std::lock_guard<std::mutex> g(mu_);
       evicted_[m.uid].clear();
+      eviction_blocked_[m.uid].clear();
     }
     event_(obj, "Normal", "GPUReleased", "released " + std::to_string(release.size()) + " GPU(s) on " + node + ": " + join(release, ","));
   }
@@ -397,6 +417,7 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
   {
     std::lock_guard<std::mutex> g(mu_);
     evicted_.erase(m.uid);
+    eviction_blocked_.erase(m.uid);
     policy_gen_.erase(m.uid);
   }
   forget_(m.uid);

@@ -319,3 +319,39 @@ def test_node_preflight_and_partition_surface(node8):
 def test_invalid_spec_is_rejected(node8):
     with pytest.raises(KubeError):
         node8.client.create(MI355XPOOLS, mi_pool("neg", -1), "default")
+
+
+def test_drain_respects_pod_disruption_budget(node8):
+    """Scale-down drains through the Eviction API: a PodDisruptionBudget refusal (429) leaves the
+    GPU draining (EvictionBlocked event, retried every pass) until the budget allows it."""
+    from gpupool.kube import BY_KIND
+    PDBS = BY_KIND["PodDisruptionBudget"]
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 2, drain={"gracePeriodSeconds": 1, "timeoutSeconds": 300}),
+             "default")
+    wait_ready(k, "p", 2)
+    for i in range(2):
+        pod = pause_pod(f"trainer-{i}")
+        pod["metadata"]["labels"] = {"app": "trainer"}
+        k.create(PODS, pod, "default")
+    for i in range(2):
+        k.wait_for(PODS, f"trainer-{i}", "default",
+                   lambda o: o and o["status"].get("phase") == "Running", timeout=30)
+    k.create(PDBS, {"apiVersion": "policy/v1", "kind": "PodDisruptionBudget",
+                    "metadata": {"name": "trainers"},
+                    "spec": {"minAvailable": 2, "selector": {"matchLabels": {"app": "trainer"}}}},
+             "default")
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 1}}, "default")
+
+    def blocked(_o):
+        return any(e["reason"] == "EvictionBlocked" for e in k.list(EVENTS, "default")["items"])
+    k.wait_for(MI355XPOOLS, "p", "default", blocked, timeout=20)
+    time.sleep(0.5)
+    o = k.get(MI355XPOOLS, "p", "default")
+    assert len(k.list(PODS, "default")["items"]) == 2  # nobody evicted
+    assert conds(o)["Progressing"]["reason"] == "ScalingDown" or \
+        conds(o)["Progressing"]["reason"] == "Draining"
+    # relax the budget: the next pass evicts and releases
+    k.delete(PDBS, "trainers", "default")
+    wait_ready(k, "p", 1, timeout=30)
+    assert len(k.list(PODS, "default")["items"]) == 1
