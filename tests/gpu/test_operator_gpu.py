@@ -106,3 +106,20 @@ def test_fault_overlay_on_real_hardware(cluster_factory):
     k.wait_for(MI355XPOOLS, "p", "default", degraded, timeout=30)
     c.set_faults("gpu-node", {})
     k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=30)
+
+
+def test_performance_floor_on_real_gpu(cluster_factory):
+    """spec.probe.minMfmaTflops above what any MI355X reaches: the (correct) GPU fails
+    DeviceProbePassed with PerformanceBelowFloor and the pool does not report Ready."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    k = c.client
+    k.create(MI355XPOOLS, pool("slow", 1, probe={"minMfmaTflops": 100000}, replacePolicy="Keep"),
+             "default")
+
+    def probe_failed(o):
+        return any(x["type"] == "DeviceProbePassed" and x["status"] == "False"
+                   for x in ((o or {}).get("status") or {}).get("conditions", []))
+    o = k.wait_for(MI355XPOOLS, "slow", "default", probe_failed, timeout=60)
+    msg = next(x["message"] for x in o["status"]["conditions"] if x["type"] == "DeviceProbePassed")
+    assert "PerformanceBelowFloor" in msg and "TFLOP/s" in msg
+    assert o["status"].get("readyReplicas", 0) == 0

@@ -72,3 +72,26 @@ def test_probe_cli(native_built):
     assert r.returncode == 0, r.stderr
     for line in r.stdout.strip().splitlines():
         assert json.loads(line)["passed"]
+
+
+@pytest.mark.parametrize("n", [256, 512, 1280, 2048])
+@pytest.mark.parametrize("tile", [128, 256])
+def test_gemm_kernels_exact_at_sizes(hip, n, tile):
+    """Both GEMM kernels (256x256 glds and 128x128 register-staged) are bit-exact (ABFT) at
+    several N, including one that is not a power of two (1280 = 5 x 256)."""
+    r = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemm_tile=tile)
+    assert r["passed"], r
+    assert r["mfma"]["tile"] == tile and r["mfma"]["n"] == n
+    assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
+
+
+def test_overlapped_and_serial_probe_agree(hip):
+    """The two-stream probe (HBM test beside the MFMA phase) finds the same injected faults as
+    the serial one and both pass clean runs."""
+    for overlap in (0, 1):
+        clean = hip.run(0, hbm_bytes=256 << 20, overlap=overlap)
+        assert clean["passed"], clean
+        bad = hip.run(0, hbm_bytes=256 << 20, gemm_n=1024, overlap=overlap, injectBitFlips=5,
+                      injectGemmFault=1)
+        assert not bad["passed"]
+        assert bad["hbm"]["badBits"] == 5 and bad["mfma"]["abftMismatches"] == 2
