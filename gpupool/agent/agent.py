@@ -93,7 +93,9 @@ class Agent:
         self.probe_mode = cfg.probe_mode or default_mode(self.backend)
         self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n)
         self.last_probe: dict[str, dict] = {}
-        self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0,
+        self._probe_mono: dict[str, float] = {}  # uuid -> monotonic time of its last probe
+        self._rechecking: set[str] = set()
+        self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0, "rechecks": 0,
                       "probe_ms_sum": 0.0, "samples": 0}
         self._pods_cache: tuple[float, dict[str, list[dict]]] = (0.0, {})
         self._stop = threading.Event()
@@ -157,6 +159,61 @@ class Agent:
                 self.sample()
             except Exception:
                 log.exception("health sample failed")
+            try:
+                self.recheck_probes()
+            except Exception:
+                log.exception("probe recheck failed")
+
+    def recheck_probes(self, force: bool = False) -> list[str]:
+        """Periodic functional re-probe (spec.probe.recheckSeconds) of claimed GPUs that run no
+        pod: silent degradation between claims (a GPU that now fails its pattern test, GEMM
+        checks or performance floor) surfaces as DeviceProbePassed=False and is replaced like
+        any other health fault. Probes run on the prober's threads; returns the uuids started."""
+        now = time.monotonic()
+        pods = self._pods_by_device()
+        due: list[tuple[str, dict, dict, str]] = []
+        with self.lock:
+            for u, rec in self.records.items():
+                opts = (rec.get("policy") or {}).get("probe") or {}
+                every = float(opts.get("recheckSeconds") or 0)
+                if (every <= 0 and not force) or rec.get("state") != "Claimed" or pods.get(u) or \
+                        u in self._rechecking or u not in self.by_uuid:
+                    continue
+                if force or now - self._probe_mono.get(u, now) >= every:
+                    self._rechecking.add(u)
+                    due.append((u, dict(self.by_uuid[u]), opts, rec["poolUID"]))
+        for u, dev, opts, pool_uid in due:
+            self.prober.pool.submit(self._recheck_one, u, dev, opts, pool_uid)
+        return [u for u, *_ in due]
+
+    def _recheck_one(self, uuid: str, dev: dict, opts: dict, pool_uid: str) -> None:
+        try:
+            res = self.prober.probe_many([dev], {**opts, "enabled": opts.get("enabled", True)})[0]
+            res["recheck"] = True
+            with self.lock:
+                rec = self.records.get(uuid)
+                if rec is None or rec["poolUID"] != pool_uid or rec.get("state") != "Claimed":
+                    return  # released / re-claimed meanwhile
+                was = bool((rec.get("probe") or {}).get("passed"))
+                rec["probe"] = res
+                self.last_probe[uuid] = res
+                self._probe_mono[uuid] = time.monotonic()
+                self.stats["rechecks"] = self.stats.get("rechecks", 0) + 1
+                if not res.get("passed"):
+                    self.stats["probe_failures"] += 1
+                if was != bool(res.get("passed")):
+                    self.ledger.commit(self.records)
+                    log.warning("recheck of %s: probe %s (%s)", uuid,
+                                "passed" if res.get("passed") else "FAILED", res.get("error", ""))
+                    flipped = True
+                else:
+                    flipped = False
+            if flipped:
+                self._bump({pool_uid})
+                self._notify_plugins()
+        finally:
+            with self.lock:
+                self._rechecking.discard(uuid)
 
     # ================================================================ events
     def _bump(self, pools: set[str]) -> None:
@@ -307,6 +364,7 @@ class Agent:
                 rec["probe"] = res
                 rec["state"] = "Claimed"
                 self.last_probe[d["uuid"]] = res
+                self._probe_mono[d["uuid"]] = time.monotonic()
                 self.stats["probes"] += 1
                 self.stats["probe_ms_sum"] += float(res.get("ms", 0.0))
                 if not res.get("passed"):

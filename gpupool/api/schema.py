@@ -210,6 +210,11 @@ MI355X_SPEC = {
                                               "less HBM write+read bandwidth (GB/s) fails "
                                               "DeviceProbePassed (0 = off; MI355X measures "
                                               "~4900 with the default 1 GiB probe)."},
+                "recheckSeconds": {**_I32, "minimum": 0, "default": 0,
+                                   "description": "Re-run the probe on claimed GPUs that have "
+                                                  "no pod every this many seconds (0 = only at "
+                                                  "claim time); a failure is handled like any "
+                                                  "health fault (DeviceProbePassed, replace)."},
                 "minMfmaTflops": {"type": "number", "minimum": 0, "default": 0,
                                   "description": "Performance floor for the probe's 4096^3 bf16 "
                                                  "MFMA GEMM in TFLOP/s (0 = off; MI355X "

@@ -60,6 +60,8 @@ struct Mi355xPoolSpec {
   bool probe_mfma = true;
   double probe_min_hbm_gbps = 0;     // performance floors (0 = off)
   double probe_min_mfma_tflops = 0;
+  int64_t probe_recheck_seconds = 0;  // periodic re-probe of idle claimed GPUs (0 = off)
+  Json probe_json() const;            // the probe options sent with claims and policy updates
   std::string replace_policy = "Replace";
   static Mi355xPoolSpec from(const Json& spec);
   Json policy_json() const;  // health + partition, as the agent/device library consume it

@@ -74,8 +74,20 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.probe_mfma = pr["mfma"].as_bool(true);
   p.probe_min_hbm_gbps = pr["minHbmGBps"].as_double(0);
   p.probe_min_mfma_tflops = pr["minMfmaTflops"].as_double(0);
+  p.probe_recheck_seconds = pr["recheckSeconds"].as_int(0);
   p.replace_policy = s["replacePolicy"].str_or("Replace");
   return p;
+}
+
+Json Mi355xPoolSpec::probe_json() const {
+  Json j = Json::object();
+  j["enabled"] = probe_enabled;
+  j["hbmBytes"] = probe_hbm_bytes;
+  j["mfma"] = probe_mfma;
+  j["minHbmGBps"] = probe_min_hbm_gbps;
+  j["minMfmaTflops"] = probe_min_mfma_tflops;
+  j["recheckSeconds"] = probe_recheck_seconds;
+  return j;
 }
 
 Json Mi355xPoolSpec::policy_json() const {
@@ -83,6 +95,7 @@ Json Mi355xPoolSpec::policy_json() const {
   j["health"] = health.to_json();
   j["partition"]["compute"] = partition_compute;
   j["partition"]["memory"] = partition_memory;
+  j["probe"] = probe_json();  // re-probe settings live with the claim (agent-side recheck)
   return j;
 }
 
@@ -160,6 +173,8 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
     int64_t b = pr["hbmBytes"].as_int(0);
     if (b < (1LL << 20) || b > (64LL << 30)) errs.push_back("spec.probe.hbmBytes: must be within [1MiB, 64GiB]");
   }
+  if (pr.contains("recheckSeconds") && (!pr["recheckSeconds"].is_int() || pr["recheckSeconds"].as_int(0) < 0))
+    errs.push_back("spec.probe.recheckSeconds: should be greater than or equal to 0");
   for (const char* k : {"minHbmGBps", "minMfmaTflops"})
     if (pr.contains(k) && (!pr[k].is_number() || pr[k].as_double(0) < 0))
       errs.push_back(std::string("spec.probe.") + k + ": should be greater than or equal to 0");

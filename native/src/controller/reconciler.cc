@@ -545,12 +545,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
       req.topology_policy = spec.topology_policy;
       req.resource_name = spec.resource_name;
       req.policy = spec.policy_json();
-      req.probe = Json::object();
-      req.probe["enabled"] = spec.probe_enabled;
-      req.probe["hbmBytes"] = spec.probe_hbm_bytes;
-      req.probe["mfma"] = spec.probe_mfma;
-      req.probe["minHbmGBps"] = spec.probe_min_hbm_gbps;
-      req.probe["minMfmaTflops"] = spec.probe_min_mfma_tflops;
+      req.probe = spec.probe_json();
       auto t = clock_t_::now();
       ClaimResult cr = provider_.claim(node, req);
       double claim_ms = std::chrono::duration<double, std::milli>(clock_t_::now() - t).count();

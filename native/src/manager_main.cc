@@ -263,7 +263,8 @@ class AgentWatchers {
     int backoff = 100;
     while (!w->stop && !g_stop) {
       try {
-        HttpClient c(Url::parse(w->endpoint), "", 5000);
+        // the agent holds the answer up to timeoutSeconds: allow that plus slack before timing out
+        HttpClient c(Url::parse(w->endpoint), "", 10000);
         std::string path = "/v1/events?timeoutSeconds=5&since=" + std::to_string(since);
         int status = c.stream_lines(
             path,

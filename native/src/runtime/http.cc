@@ -1,5 +1,6 @@
 #include "gpupool/http.h"
 
+#include <algorithm>
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -477,10 +478,15 @@ std::string lower(std::string s) {
 
 // Parse status line + headers from c.rbuf (reading more as needed). Returns false on failure.
 template <class ConnT>
-bool read_head(ConnT& c, HttpResponse& r, int timeout_ms, std::string* err) {
+bool read_head(ConnT& c, HttpResponse& r, int timeout_ms, std::string* err,
+               const std::atomic<bool>* stop = nullptr, int poll_ms = 200) {
   size_t end;
   auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
   while ((end = c.rbuf.find("\r\n\r\n")) == std::string::npos) {
+    if (stop && stop->load()) {
+      *err = "stopped";
+      return false;
+    }
     if (c.rbuf.size() > (1 << 20)) {
       *err = "header too large";
       return false;
@@ -492,12 +498,15 @@ bool read_head(ConnT& c, HttpResponse& r, int timeout_ms, std::string* err) {
       *err = "timeout reading response head";
       return false;
     }
-    ssize_t n = c.fill(left);
+    // with a stop flag, wait in poll_ms slices so a long-poll whose answer is still pending
+    // (the server holds the head until something changes) can be abandoned promptly
+    ssize_t n = c.fill(stop ? std::min(left, poll_ms) : left);
     if (n == 0) {
       *err = "connection closed";
       return false;
     }
     if (n == -2) {
+      if (stop) continue;  // slice elapsed: re-check stop and the overall deadline
       *err = "timeout reading response head";
       return false;
     }
@@ -597,7 +606,10 @@ int HttpClient::stream_lines(const std::string& path,
     throw HttpError("send failed");
   HttpResponse r;
   std::string err;
-  if (!read_head(*c, r, timeout_ms_, &err)) throw HttpError("GET " + path + ": " + err);
+  if (!read_head(*c, r, timeout_ms_, &err, stop, poll_ms)) {
+    if (stop && stop->load()) return 0;  // abandoned on request: not an error
+    throw HttpError("GET " + path + ": " + err);
+  }
   bool chunked = false;
   auto te = r.headers.find("transfer-encoding");
   if (te != r.headers.end() && lower(te->second).find("chunked") != std::string::npos) chunked = true;
@@ -624,11 +636,19 @@ int HttpClient::stream_lines(const std::string& path,
     if (err_body) *err_body = payload;
     return r.status;
   }
+  // A non-chunked body (long-poll answers) ends at Content-Length: the server keeps the
+  // connection alive, so waiting for EOF would stall until its keep-alive timeout.
+  int64_t remaining = -1;
+  if (!chunked) {
+    auto cl = r.headers.find("content-length");
+    if (cl != r.headers.end()) remaining = static_cast<int64_t>(std::stoull(cl->second));
+  }
   for (;;) {
     if (chunked) {
       if (!dec.feed(pending, payload)) throw HttpError("bad chunked encoding in stream");
     } else {
       payload += pending;
+      if (remaining >= 0) remaining -= static_cast<int64_t>(pending.size());
     }
     pending.clear();
     size_t nl;
@@ -640,6 +660,10 @@ int HttpClient::stream_lines(const std::string& path,
       if (!cont) return r.status;
     }
     if (chunked && dec.done()) return r.status;
+    if (remaining == 0) {
+      if (!payload.empty()) on_line(payload);  // last line without a trailing newline
+      return r.status;
+    }
     for (;;) {
       if (stop && stop->load()) return r.status;
       ssize_t n = c->fill(poll_ms);
