@@ -90,6 +90,8 @@ def main() -> int:
     ap.add_argument("--workdir", default="")
     ap.add_argument("--keep", action="store_true", help="keep the workdir (logs)")
     ap.add_argument("--timeout", type=float, default=120.0, help="per-transition timeout (s)")
+    ap.add_argument("--health-steps", type=int, default=5,
+                    help="fault->condition measurements after the timed steps (0 = skip)")
     args = ap.parse_args()
 
     rank, world = _dist_init()
@@ -173,6 +175,34 @@ def main() -> int:
     _barrier(world)
     elapsed = _gather_max(world, time.perf_counter() - t_start)
 
+    health = {}
+    if rank == 0 and args.health_steps > 0:
+        # Secondary measurement, outside the timed region (BASELINE config 5): fault overlay on
+        # one claimed GPU (uncorrectable ECC) -> HBMECCHealthy=False + Degraded=True on the pool,
+        # and back after the fault clears. Event-driven: agent sample -> long-poll -> reconcile.
+        c.patch(MI355XPOOLS, name, {"spec": {"replicas": 1, "replacePolicy": "Keep"}}, ns)
+        obj = c.wait_for(MI355XPOOLS, name, ns, ready_at(1), timeout=args.timeout)
+        victim = obj["status"]["devices"][0]["uuid"]
+
+        def cond(o, t):
+            return next((x for x in ((o or {}).get("status") or {}).get("conditions", [])
+                         if x["type"] == t), {}).get("status")
+        react, recover = [], []
+        for _ in range(args.health_steps):
+            t0 = time.perf_counter()
+            cluster.set_faults(node.name, {"devices": {victim: {"ecc": {"uncorrectable": 1}}}})
+            c.wait_for(MI355XPOOLS, name, ns, lambda o: cond(o, "HBMECCHealthy") == "False" and
+                       cond(o, "Degraded") == "True", timeout=args.timeout)
+            react.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            cluster.set_faults(node.name, {})
+            c.wait_for(MI355XPOOLS, name, ns, lambda o: cond(o, "HBMECCHealthy") == "True" and
+                       ready_at(1)(o), timeout=args.timeout)
+            recover.append(time.perf_counter() - t0)
+        health = {"fault_to_condition_p50_s": round(statistics.median(react), 4),
+                  "fault_cleared_to_ready_p50_s": round(statistics.median(recover), 4),
+                  "steps": args.health_steps}
+
     if rank == 0:
         try:
             metrics = cluster.manager_metrics()
@@ -228,6 +258,7 @@ def main() -> int:
                 "readyReplicas_accuracy": accuracy,
                 "world_size": world,
                 "claim_pass_span_p50_ms": span_p50,
+                "health_condition_latency": health,
                 "steps_detail": details[:3],
             },
         }
