@@ -532,11 +532,14 @@ class Agent:
                 if d.get("renderNode"):
                     render.append(d["renderNode"])
             # ROCR_VISIBLE_DEVICES pins the container to exactly its GPUs (HIP ordinals then
-            # start at 0); GPUPOOL_NUM_GPUS is the per-pod world-size hint for
-            # `torch.distributed.run --nproc-per-node $GPUPOOL_NUM_GPUS`.
+            # start at 0); GPUPOOL_NUM_GPUS is the per-pod world-size hint and PET_NPROC_PER_NODE
+            # the torchrun default for --nproc-per-node (torch.distributed.run reads PET_* env),
+            # so a plain `torchrun train.py` in the pod starts one rank per allotted GPU over
+            # RCCL (the reference's Kubeflow operator sets PET_*, GPU调度平台搭建.md:623).
             envs = {"ROCR_VISIBLE_DEVICES": ",".join(hip),
                     "GPUPOOL_DEVICE_UUIDS": ",".join(ids),
                     "GPUPOOL_NUM_GPUS": str(len(ids)),
+                    "PET_NPROC_PER_NODE": str(len(ids)),
                     "GPUPOOL_NODE": self.cfg.node}
             return {"envs": envs, "devices": ["/dev/kfd"] + render,
                     "annotations": {schema.ANN_POD_DEVICES: ",".join(ids)}}

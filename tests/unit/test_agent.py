@@ -153,6 +153,7 @@ def test_device_plugin_conformance(tmp_path, sockdir, native_built):
         resp = stub.Allocate(DP.AllocateRequest(container_requests=[{"devices_ids": [u0]}]))
         cr = resp.container_responses[0]
         assert cr.envs["ROCR_VISIBLE_DEVICES"] == r["devices"][0]["hipUUID"]
+        assert cr.envs["GPUPOOL_NUM_GPUS"] == cr.envs["PET_NPROC_PER_NODE"] == "1"
         assert [d.host_path for d in cr.devices] == ["/dev/kfd", r["devices"][0]["renderNode"]]
         assert all(d.permissions == "rw" for d in cr.devices)
         # Allocate of a non-pool device is refused
