@@ -356,6 +356,9 @@ class Agent:
                                                   probe_opts.get("enabled", True)})
         probe_wall = (time.perf_counter() - t0) * 1e3
         lap("probe")
+        if probe_opts.get("xgmiPeerCheck"):
+            self._xgmi_check(pool_uid, chosen, results, probe_opts)
+            lap("xgmi")
         with self.lock:
             for d, res in zip(chosen, results):
                 rec = self.records.get(d["uuid"])
@@ -383,6 +386,34 @@ class Agent:
         log.info("claimed %d GPU(s) for %s: %s (probe wall %.1f ms)", len(chosen),
                  req.get("pool"), [d["index"] for d in chosen], probe_wall)
         return {"ok": True, "devices": views, "probeWallMs": probe_wall, "timingsMs": timings}
+
+    def _xgmi_check(self, pool_uid: str, chosen: list[dict], results: list[dict],
+                    opts: dict) -> None:
+        """spec.probe.xgmiPeerCheck: ring peer copies across all of the pool's GPUs on this node
+        (already-owned + newly chosen, index order). Each newly chosen GPU's probe result gets
+        its outgoing link's {peer, GBps, passed}; a corrupted copy, an inaccessible peer or a
+        copy slower than minXgmiGBps fails its probe (-> DeviceProbePassed=False, replace)."""
+        with self.lock:
+            owned = [self.by_uuid[u] for u, r in self.records.items()
+                     if r["poolUID"] == pool_uid and u in self.by_uuid]
+        ring = sorted({d["uuid"]: d for d in owned + chosen}.values(), key=lambda d: d["index"])
+        links = self.prober.peer_ring(ring, opts)
+        floor = float(opts.get("minXgmiGBps") or 0)
+        for d, res in zip(chosen, results):
+            link = links.get(d["uuid"])
+            if link is None:
+                continue
+            res["xgmi"] = link
+            if not res.get("passed"):
+                continue
+            if not link.get("passed"):
+                res["passed"] = False
+                res["error"] = f"XGMIPeerCheckFailed: -> {link.get('peer')}: " \
+                               f"{link.get('error') or str(link.get('badBits')) + ' bad bits'}"
+            elif floor > 0 and float(link.get("GBps") or 0) < floor:
+                res["passed"] = False
+                res["error"] = f"XGMIPeerCheckFailed: -> {link.get('peer')}: " \
+                               f"{float(link.get('GBps') or 0):.0f} GB/s < floor {floor:.0f}"
 
     def cordon(self, pool_uid: str, uuids: list[str]) -> dict:
         with self.lock:

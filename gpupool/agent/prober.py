@@ -130,6 +130,42 @@ class Prober:
                 out.append({"passed": False, "backend": self.mode, "error": repr(e), "ms": 0.0})
         return out
 
+    def peer_ring(self, devs: list[dict], opts: dict) -> dict[str, dict]:
+        """xGMI peer check in ring order (dev i -> dev i+1): for each sender uuid, the copy
+        result {peer, GBps, passed[, error]}. Pairs run concurrently; the library serialises
+        pairs that share a device. Empty when fewer than 2 GPUs or the mode cannot do it."""
+        n = len(devs)
+        if n < 2 or self.mode not in ("inproc", "simulated"):
+            return {}
+        nbytes = int(opts.get("xgmiBytes") or (64 << 20))
+
+        def one(i: int) -> tuple[str, dict]:
+            src, dst = devs[i], devs[(i + 1) % n]
+            faults = {**(src.get("faults") or {}), **src}
+            if self.mode == "simulated" or faults.get("xgmiPeerFail"):
+                ok = not faults.get("xgmiPeerFail")
+                r = {"passed": ok, "GBps": 64.0 * float(faults.get("probeScale") or 1.0),
+                     "badBits": 0 if ok else 1}
+                if not ok:
+                    r["error"] = "injected xGMI peer failure (fault overlay)"
+            else:
+                a = self.ordinals.get(str(src.get("hipUUID", "")).lower())
+                b = self.ordinals.get(str(dst.get("hipUUID", "")).lower())
+                if a is None or b is None:
+                    r = {"passed": False, "error": "peer device not visible to HIP"}
+                else:
+                    r = self._hip.peer(a, b, nbytes)
+            r["peer"] = dst["uuid"]
+            return src["uuid"], r
+        out = {}
+        for fut in [self.pool.submit(one, i) for i in range(n)]:
+            try:
+                u, r = fut.result()
+                out[u] = r
+            except Exception as e:  # never take the agent down
+                log.warning("xGMI peer check failed: %r", e)
+        return out
+
     def close(self) -> None:
         self.pool.shutdown(wait=False)
 

@@ -138,6 +138,7 @@ DEVICE_STATUS = {
                 "passed": _B,
                 "hbmGBps": {"type": "number"},
                 "mfmaTflops": {"type": "number"},
+                "xgmiGBps": {"type": "number"},
                 "ms": {"type": "number"},
                 "backend": _S,
                 "message": _S,
@@ -210,6 +211,15 @@ MI355X_SPEC = {
                                               "less HBM write+read bandwidth (GB/s) fails "
                                               "DeviceProbePassed (0 = off; MI355X measures "
                                               "~4900 with the default 1 GiB probe)."},
+                "xgmiPeerCheck": {**_B, "default": False,
+                                  "description": "For pools of 2+ GPUs: each GPU copies a "
+                                                 "pattern to the next one over xGMI "
+                                                 "(hipMemcpyPeer, ring order) and the receiver "
+                                                 "verifies every bit; adds link GB/s to the "
+                                                 "probe result."},
+                "minXgmiGBps": {"type": "number", "minimum": 0, "default": 0,
+                                "description": "Floor for the peer-copy bandwidth of the "
+                                               "xGMI check (0 = off)."},
                 "recheckSeconds": {**_I32, "minimum": 0, "default": 0,
                                    "description": "Re-run the probe on claimed GPUs that have "
                                                   "no pod every this many seconds (0 = only at "

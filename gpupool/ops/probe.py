@@ -30,6 +30,8 @@ def lib() -> ctypes.CDLL:
             l.mi355x_probe_run.restype = ctypes.c_void_p
             l.mi355x_probe_run.argtypes = [ctypes.c_int, ctypes.c_char_p]
             l.mi355x_probe_free.argtypes = [ctypes.c_void_p]
+            l.mi355x_probe_peer.restype = ctypes.c_void_p
+            l.mi355x_probe_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
             _lib = l
     return _lib
 
@@ -71,6 +73,13 @@ def run(dev: int, hbm_bytes: int = 1 << 30, mfma: bool = True, gemm_n: int = 409
                        "gemmTile": int(gemm_tile),
                        **{k: int(v) for k, v in test_hooks.items()}})
     return _take(lib().mi355x_probe_run(dev, opts.encode()))
+
+
+def peer(src: int, dst: int, nbytes: int = 64 << 20) -> dict:
+    """xGMI peer check src -> dst: pattern written on src, hipMemcpyPeer over the link, every bit
+    verified on dst; reports GB/s. ``src == dst`` exercises the same path as a local copy."""
+    opts = json.dumps({"bytes": int(nbytes)})
+    return _take(lib().mi355x_probe_peer(src, dst, opts.encode()))
 
 
 def hip_uuid_map() -> dict[str, int]:

@@ -61,6 +61,8 @@ struct Mi355xPoolSpec {
   double probe_min_hbm_gbps = 0;     // performance floors (0 = off)
   double probe_min_mfma_tflops = 0;
   int64_t probe_recheck_seconds = 0;  // periodic re-probe of idle claimed GPUs (0 = off)
+  bool probe_xgmi_peer_check = false;   // ring peer-copy check across the pool's GPUs
+  double probe_min_xgmi_gbps = 0;
   Json probe_json() const;            // the probe options sent with claims and policy updates
   std::string replace_policy = "Replace";
   static Mi355xPoolSpec from(const Json& spec);

@@ -22,6 +22,11 @@ char* mi355x_probe_identify(int device);
 /* opts: {"hbmBytes":1073741824,"patterns":2,"mfma":true,"gemmN":4096,"gemmReps":3}
  * -> {"passed":bool,"hbm":{...,"GBps"},"mfma":{...,"tflops"},"ms":...} */
 char* mi355x_probe_run(int device, const char* opts_json);
+/* xGMI peer check: src writes a pattern, copies it to dst over the peer link
+ * (hipMemcpyPeerAsync after hipDeviceEnablePeerAccess), dst verifies every bit.
+ * opts: {"bytes":268435456}. src == dst runs the same path as a local device copy.
+ * -> {"src","dst","canAccessPeer":bool,"passed":bool,"badBits","GBps","ms"} */
+char* mi355x_probe_peer(int src, int dst, const char* opts_json);
 void mi355x_probe_free(char* p);
 
 #ifdef __cplusplus

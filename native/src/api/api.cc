@@ -75,6 +75,8 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.probe_min_hbm_gbps = pr["minHbmGBps"].as_double(0);
   p.probe_min_mfma_tflops = pr["minMfmaTflops"].as_double(0);
   p.probe_recheck_seconds = pr["recheckSeconds"].as_int(0);
+  p.probe_xgmi_peer_check = pr["xgmiPeerCheck"].as_bool(false);
+  p.probe_min_xgmi_gbps = pr["minXgmiGBps"].as_double(0);
   p.replace_policy = s["replacePolicy"].str_or("Replace");
   return p;
 }
@@ -87,6 +89,8 @@ Json Mi355xPoolSpec::probe_json() const {
   j["minHbmGBps"] = probe_min_hbm_gbps;
   j["minMfmaTflops"] = probe_min_mfma_tflops;
   j["recheckSeconds"] = probe_recheck_seconds;
+  j["xgmiPeerCheck"] = probe_xgmi_peer_check;
+  j["minXgmiGBps"] = probe_min_xgmi_gbps;
   return j;
 }
 
@@ -175,7 +179,9 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
   }
   if (pr.contains("recheckSeconds") && (!pr["recheckSeconds"].is_int() || pr["recheckSeconds"].as_int(0) < 0))
     errs.push_back("spec.probe.recheckSeconds: should be greater than or equal to 0");
-  for (const char* k : {"minHbmGBps", "minMfmaTflops"})
+  if (pr.contains("xgmiPeerCheck") && !pr["xgmiPeerCheck"].is_bool())
+    errs.push_back("spec.probe.xgmiPeerCheck: must be of type boolean");
+  for (const char* k : {"minHbmGBps", "minMfmaTflops", "minXgmiGBps"})
     if (pr.contains(k) && (!pr[k].is_number() || pr[k].as_double(0) < 0))
       errs.push_back(std::string("spec.probe.") + k + ": should be greater than or equal to 0");
   const Json& part = s["partition"];

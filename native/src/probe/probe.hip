@@ -472,6 +472,11 @@ std::mutex g_mu;
 std::vector<DeviceCtx> g_ctx;
 int g_count = -1;
 
+std::mutex& device_mutex(int dev) {
+  static std::vector<std::mutex> mu(64);
+  return mu[static_cast<size_t>(dev) % mu.size()];
+}
+
 std::string jnum(double v) {
   char b[64];
   std::snprintf(b, sizeof b, "%.6g", v);
@@ -758,6 +763,65 @@ std::string run_probe(int dev, const char* opts) {
   return out;
 }
 
+// One direction of the xGMI peer check (see mi355x_probe_peer in probe.h). Serialised against
+// probes of either device by the caller.
+std::string run_peer(int src, int dst, const char* opts) {
+  const uint64_t bytes = static_cast<uint64_t>(std::max(1LL << 20, opt_int(opts, "bytes", 256LL << 20)));
+  const uint64_t n16 = bytes / 16;
+  for (int d : {src, dst}) {
+    DeviceCtx& c = g_ctx[static_cast<size_t>(d)];
+    if (!c.ready) (void)run_probe(d, "{\"hbmBytes\":1048576,\"patterns\":1,\"mfma\":false}");  // create streams/events
+  }
+  int can = src == dst ? 1 : 0;
+  if (src != dst) PROBE_CHECK(hipDeviceCanAccessPeer(&can, src, dst));
+  if (!can)
+    return "{\"src\":" + std::to_string(src) + ",\"dst\":" + std::to_string(dst) +
+           ",\"canAccessPeer\":false,\"passed\":false,\"error\":\"hipDeviceCanAccessPeer=0\"}";
+  DeviceCtx& cs = g_ctx[static_cast<size_t>(src)];
+  DeviceCtx& cd = g_ctx[static_cast<size_t>(dst)];
+  if (src != dst) {
+    PROBE_CHECK(hipSetDevice(src));
+    hipError_t e = hipDeviceEnablePeerAccess(dst, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) PROBE_CHECK(e);
+    (void)hipGetLastError();  // clear a sticky "already enabled"
+  }
+  DevBuf sbuf, dbuf, cnt_buf;
+  PROBE_CHECK(hipSetDevice(src));
+  PROBE_CHECK(hipMalloc(&sbuf.p, n16 * 16));
+  PROBE_CHECK(hipSetDevice(dst));
+  PROBE_CHECK(hipMalloc(&dbuf.p, n16 * 16));
+  PROBE_CHECK(hipMalloc(&cnt_buf.p, 2 * sizeof(unsigned long long)));
+  auto* cnt = static_cast<unsigned long long*>(cnt_buf.p);
+  const uint32_t seed = 0x5EED0000u + static_cast<uint32_t>(src * 16 + dst);
+  // src: write the pattern
+  PROBE_CHECK(hipSetDevice(src));
+  const int sgrid = std::min<int>(cs.prop.multiProcessorCount, static_cast<int>((n16 + kHbmThreads - 1) / kHbmThreads));
+  hipLaunchKernelGGL(hbm_fill, dim3(sgrid), dim3(kHbmThreads), 0, cs.stream, static_cast<u32x4*>(sbuf.p), n16, seed, 0u);
+  PROBE_CHECK(hipGetLastError());
+  // the copy over the peer link, timed on src's stream
+  PROBE_CHECK(hipEventRecord(cs.gev[0], cs.stream));
+  PROBE_CHECK(hipMemcpyPeerAsync(dbuf.p, dst, sbuf.p, src, n16 * 16, cs.stream));
+  PROBE_CHECK(hipEventRecord(cs.gev[1], cs.stream));
+  PROBE_CHECK(hipStreamSynchronize(cs.stream));
+  float ms = 0;
+  PROBE_CHECK(hipEventElapsedTime(&ms, cs.gev[0], cs.gev[1]));
+  // dst: verify every bit that arrived
+  PROBE_CHECK(hipSetDevice(dst));
+  PROBE_CHECK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), cd.stream));
+  PROBE_CHECK(hipMemsetAsync(cnt + 1, 0xFF, sizeof(unsigned long long), cd.stream));
+  const int dgrid = std::min<int>(3 * cd.prop.multiProcessorCount, static_cast<int>((n16 + kHbmThreads - 1) / kHbmThreads));
+  hipLaunchKernelGGL(hbm_verify, dim3(dgrid), dim3(kHbmThreads), 0, cd.stream, static_cast<const u32x4*>(dbuf.p), n16,
+                     seed, 0u, cnt, cnt + 1);
+  PROBE_CHECK(hipGetLastError());
+  PROBE_CHECK(hipMemcpyAsync(cd.host_res, cnt, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, cd.stream));
+  PROBE_CHECK(hipStreamSynchronize(cd.stream));
+  const unsigned long long bad = cd.host_res[0];
+  const double gbps = ms > 0 ? static_cast<double>(n16 * 16) / (ms * 1e-3) / 1e9 : 0.0;
+  return "{\"src\":" + std::to_string(src) + ",\"dst\":" + std::to_string(dst) + ",\"canAccessPeer\":true" +
+         ",\"passed\":" + (bad == 0 ? "true" : "false") + ",\"badBits\":" + std::to_string(bad) +
+         ",\"bytes\":" + std::to_string(n16 * 16) + ",\"GBps\":" + jnum(gbps) + ",\"ms\":" + jnum(ms) + "}";
+}
+
 }  // namespace
 
 extern "C" {
@@ -804,13 +868,28 @@ char* mi355x_probe_identify(int dev) {
 char* mi355x_probe_run(int dev, const char* opts_json) {
   if (g_count < 0 || dev < 0 || dev >= g_count) return dup("{\"passed\":false,\"error\":\"bad device index\"}");
   // Per-device serialisation: concurrent probes of DIFFERENT devices run in parallel.
-  static std::vector<std::mutex> dev_mu(64);
-  std::lock_guard<std::mutex> g(dev_mu[static_cast<size_t>(dev) % dev_mu.size()]);
+  std::lock_guard<std::mutex> g(device_mutex(dev));
   try {
     return dup(run_probe(dev, opts_json));
   } catch (const std::exception& e) {
     (void)hipGetLastError();
     return dup(std::string("{\"device\":") + std::to_string(dev) + ",\"passed\":false,\"error\":" + jstr(e.what()) + "}");
+  }
+}
+
+char* mi355x_probe_peer(int src, int dst, const char* opts_json) {
+  if (g_count < 0 || src < 0 || dst < 0 || src >= g_count || dst >= g_count)
+    return dup("{\"passed\":false,\"error\":\"bad device index\"}");
+  // both devices' probe locks, in index order (no deadlock against a concurrent pair)
+  std::lock_guard<std::mutex> a(device_mutex(std::min(src, dst)));
+  std::unique_lock<std::mutex> b;
+  if (src != dst) b = std::unique_lock<std::mutex>(device_mutex(std::max(src, dst)));
+  try {
+    return dup(run_peer(src, dst, opts_json));
+  } catch (const std::exception& e) {
+    (void)hipGetLastError();
+    return dup(std::string("{\"src\":") + std::to_string(src) + ",\"dst\":" + std::to_string(dst) +
+               ",\"passed\":false,\"error\":" + jstr(e.what()) + "}");
   }
 }
 

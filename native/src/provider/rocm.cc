@@ -63,6 +63,7 @@ Json DeviceView::status_json() const {
     p["passed"] = probe_passed;
     if (probe.path("hbm.GBps").is_number()) p["hbmGBps"] = probe.path("hbm.GBps");
     if (probe.path("mfma.tflops").is_number()) p["mfmaTflops"] = probe.path("mfma.tflops");
+    if (probe.path("xgmi.GBps").is_number()) p["xgmiGBps"] = probe.path("xgmi.GBps");
     if (probe["ms"].is_number()) p["ms"] = probe["ms"];
     if (probe["backend"].is_string()) p["backend"] = probe["backend"];
     if (probe["error"].is_string()) p["message"] = probe["error"];

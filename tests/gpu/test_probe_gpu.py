@@ -95,3 +95,16 @@ def test_overlapped_and_serial_probe_agree(hip):
                       injectGemmFault=1)
         assert not bad["passed"]
         assert bad["hbm"]["badBits"] == 5 and bad["mfma"]["abftMismatches"] == 2
+
+
+def test_peer_copy_path(hip):
+    """The xGMI peer check's copy + bit-exact verify path. On a 1-GPU box src == dst exercises
+    it as a local device copy; with more GPUs visible, 0 -> 1 goes over an xGMI link."""
+    n = hip.init()
+    r = hip.peer(0, 0, 64 << 20)
+    assert r["passed"] and r["canAccessPeer"] and r["badBits"] == 0, r
+    assert r["GBps"] > 100, r
+    if n > 1:
+        x = hip.peer(0, 1, 64 << 20)
+        assert x["passed"] and x["badBits"] == 0, x
+        assert x["GBps"] > 10, x

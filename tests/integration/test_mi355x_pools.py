@@ -385,3 +385,20 @@ def test_periodic_recheck_replaces_degraded_gpu(cluster_factory):
     assert time.monotonic() - t0 < 6.0
     view = c.agent_request("mi355x-node-0", "GET", "/v1/node")
     assert next(d for d in view["devices"] if d["uuid"] == first["uuid"])["state"] == "Quarantined"
+
+
+def test_xgmi_peer_check(cluster_factory):
+    """spec.probe.xgmiPeerCheck: ring peer copies across the pool's GPUs; link bandwidth lands in
+    status.devices[].probe.xgmiGBps and a failing link (fault overlay xgmiPeerFail) makes its
+    sender fail the probe and get replaced."""
+    c = cluster_factory(nodes=[NodeSpec("mi355x-node-0")])
+    k = c.client
+    c.set_faults("mi355x-node-0", {"devices": {"1": {"xgmiPeerFail": True}}})
+    k.create(MI355XPOOLS, mi_pool("ring", 4, probe={"xgmiPeerCheck": True, "minXgmiGBps": 10}),
+             "default")
+    o = wait_ready(k, "ring", 4, timeout=30)
+    devs = o["status"]["devices"]
+    assert 1 not in {d["index"] for d in devs}
+    assert all(d["probe"]["xgmiGBps"] > 10 for d in devs)
+    msgs = " ".join(e.get("message", "") for e in k.list(EVENTS, "default")["items"])
+    assert "XGMIPeerCheckFailed" in msgs

@@ -49,6 +49,11 @@ CASES = [
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "probe": {"minMfmaTflops": 1000.5,
                                                              "minHbmGBps": 4000}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "probe": {"minMfmaTflops": -1}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 2, "probe": {"xgmiPeerCheck": True,
+                                                             "minXgmiGBps": 40,
+                                                             "recheckSeconds": 300}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 2, "probe": {"xgmiPeerCheck": "yes"}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 2, "probe": {"recheckSeconds": -5}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "probe": {"minHbmGBps": "fast"}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "partition": {"compute": "CPX", "memory": "NPS4"}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "partition": {"compute": "XPX"}}},
