@@ -94,6 +94,11 @@ class Agent:
         self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n)
         self.last_probe: dict[str, dict] = {}
         self._probe_mono: dict[str, float] = {}  # uuid -> monotonic time of its last probe
+        # admin maintenance (gpuctl gpu cordon): uuid -> reason; persisted as a quarantine entry
+        # without expiry so it survives agent restarts
+        self.maintenance: dict[str, str] = {
+            u: q.get("reason", "") for u, q in (self.ledger.quarantined().items() if self.ledger else [])
+            if q.get("maintenance")}
         self._rechecking: set[str] = set()
         self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0, "rechecks": 0,
                       "probe_ms_sum": 0.0, "samples": 0}
@@ -122,6 +127,10 @@ class Agent:
             rec = self.records.get(uuid)
             baseline = (rec or {}).get("baseline") or d
             v = devlib.evaluate(d, baseline, self._policy_for(uuid))
+            if uuid in self.maintenance:  # admin-cordoned: unhealthy for pools, never claimed
+                v = {**v, "healthy": False,
+                     "reasons": list(v.get("reasons") or []) +
+                     [f"AdminMaintenance: {self.maintenance[uuid] or 'cordoned by an administrator'}"]}
             old = self.verdicts.get(uuid)
             if old is None or old.get("healthy") != v.get("healthy") or \
                     old.get("reasons") != v.get("reasons"):
@@ -285,7 +294,7 @@ class Agent:
                 out["advertised"] = self._advertisable(uuid)
         else:
             q = self.ledger.quarantined().get(uuid) if self.ledger else None
-            out["state"] = "Quarantined" if q else "Free"
+            out["state"] = ("Maintenance" if q.get("maintenance") else "Quarantined") if q else "Free"
             if q:
                 out["quarantine"] = q
         return out
@@ -415,6 +424,27 @@ class Agent:
                 res["error"] = f"XGMIPeerCheckFailed: -> {link.get('peer')}: " \
                                f"{float(link.get('GBps') or 0):.0f} GB/s < floor {floor:.0f}"
 
+    def set_maintenance(self, ref: str, on: bool, reason: str = "") -> dict:
+        """Admin GPU cordon / uncordon (``gpuctl gpu cordon NODE GPU``). A cordoned GPU is never
+        claimed; if a pool holds it, it turns unhealthy (AdminMaintenance) and the pool replaces
+        it through the normal drain -> release path. Uncordon clears it (and any quarantine)."""
+        with self.lock:
+            uuid = next((u for u, d in self.by_uuid.items()
+                         if ref in (u, d.get("hipUUID"), str(d.get("index")))), None)
+            if uuid is None:
+                return {"ok": False, "reason": "NotFound", "message": f"no GPU {ref!r} on {self.cfg.node}"}
+            if on:
+                self.maintenance[uuid] = reason
+                self.ledger.quarantine(uuid, 1e12, f"AdminMaintenance: {reason}", maintenance=True)
+            else:
+                self.maintenance.pop(uuid, None)
+                self.ledger.clear_quarantine(uuid)
+            changed = self._evaluate_all()
+            pool = (self.records.get(uuid) or {}).get("poolUID")
+        self._bump(changed | ({pool} if pool else {"*free*"}))
+        self._notify_plugins()
+        return {"ok": True, "uuid": uuid, "maintenance": on, "claimedBy": pool}
+
     def cordon(self, pool_uid: str, uuids: list[str]) -> dict:
         with self.lock:
             n = 0
@@ -442,7 +472,9 @@ class Agent:
                     continue
                 probe_ok = (rec.get("probe") or {}).get("passed", True)
                 healthy = self.verdicts.get(u, {}).get("healthy", True)
-                if not probe_ok or not healthy:
+                if u in self.maintenance:
+                    pass  # stays cordoned (its non-expiring maintenance entry is already there)
+                elif not probe_ok or not healthy:
                     why = "probe failed" if not probe_ok else "; ".join(
                         self.verdicts.get(u, {}).get("reasons", []))
                     self.ledger.quarantine(u, self.cfg.quarantine_s, why)
@@ -726,6 +758,12 @@ def build_app(agent: Agent) -> web.Application:
         out = await run_blocking(agent.release, b["poolUID"], b.get("uuids", []))
         return web.json_response(out, status=200 if out.get("ok") else 409)
 
+    async def maintenance(request):
+        b = await request.json()
+        out = await run_blocking(agent.set_maintenance, str(b.get("gpu", "")), bool(b.get("on", True)),
+                                 str(b.get("reason", "")))
+        return web.json_response(out, status=200 if out.get("ok") else 404)
+
     async def policy(request):
         b = await request.json()
         return web.json_response(await run_blocking(agent.update_policy, b["poolUID"],
@@ -766,6 +804,7 @@ def build_app(agent: Agent) -> web.Application:
     app.router.add_post("/v1/cordon", cordon)
     app.router.add_post("/v1/release", release)
     app.router.add_post("/v1/policy", policy)
+    app.router.add_post("/v1/maintenance", maintenance)
     app.router.add_get("/v1/events", events)
     app.router.add_post("/v1/sample", sample)
     app.router.add_get("/healthz", healthz)

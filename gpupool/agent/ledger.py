@@ -91,10 +91,10 @@ class Ledger:
             self.writes += 1
 
     # ---------------------------------------------------------------- quarantine
-    def quarantine(self, uuid: str, seconds: float, reason: str) -> None:
+    def quarantine(self, uuid: str, seconds: float, reason: str, maintenance: bool = False) -> None:
         _atomic_write_text(os.path.join(self.quar_dir, _safe(uuid) + ".json"),
                            json.dumps({"uuid": uuid, "until": time.time() + seconds,
-                                       "reason": reason}), self.fsync)
+                                       "reason": reason, "maintenance": maintenance}), self.fsync)
 
     def quarantined(self) -> dict[str, dict]:
         out, now = {}, time.time()

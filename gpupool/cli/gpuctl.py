@@ -9,6 +9,7 @@
   gpuctl logs POD                         fake-kubelet container log
   gpuctl events [-n NS]
   gpuctl devices NODE                     the node agent's live device view
+  gpuctl gpu cordon|uncordon NODE GPU     per-GPU maintenance (replace it in its pool, never claim)
   gpuctl install [--crd-dir config/crd]   install CRDs (make install)
   gpuctl render job -f TEMPLATE           GoHai train-job template -> Pod requesting amd.com/gpu
   gpuctl config view | set-context NAME --server URL [--namespace NS] [--token T] | use-context NAME
@@ -317,6 +318,34 @@ def cmd_devices(c: Client, ns: str, args) -> int:
     return 0
 
 
+def _agent(c: Client, node: str) -> Client | None:
+    n = c.get(NODES, node)
+    ep = (n["metadata"].get("annotations") or {}).get(schema.ANN_AGENT_ENDPOINT)
+    if not ep:
+        print(f"error: node {node} has no gpupool agent", file=sys.stderr)
+        return None
+    return Client(ep)
+
+
+def cmd_gpu(c: Client, ns: str, args) -> int:
+    """gpuctl gpu cordon|uncordon NODE GPU [--reason R]: per-GPU maintenance (the per-device
+    analogue of `kubectl cordon`): never claimed while cordoned; a pool holding it replaces it."""
+    agent = _agent(c, args.node)
+    if agent is None:
+        return 1
+    try:
+        out = agent.request("POST", "/v1/maintenance", {"gpu": args.gpu, "on": args.action == "cordon",
+                                                        "reason": args.reason or ""})
+    except KubeError as e:
+        print(f"error: {e}", file=sys.stderr)
+        return 1
+    what = "cordoned" if out["maintenance"] else "uncordoned"
+    held = f" (held by pool {out['claimedBy']}: it will be replaced)" if out.get("claimedBy") and \
+        out["maintenance"] else ""
+    print(f"gpu/{out['uuid']} on {args.node} {what}{held}")
+    return 0
+
+
 def cmd_install(c: Client, ns: str, args) -> int:
     from ..kube import CRDS
     for doc in load_docs(args.crd_dir):
@@ -423,6 +452,11 @@ def build_parser() -> argparse.ArgumentParser:
     p = sub.add_parser("devices")
     p.add_argument("node")
     p.add_argument("-o", "--output", default="")
+    p = sub.add_parser("gpu", help="per-GPU maintenance: cordon | uncordon")
+    p.add_argument("action", choices=["cordon", "uncordon"])
+    p.add_argument("node")
+    p.add_argument("gpu", help="uuid, hipUUID or index on the node")
+    p.add_argument("--reason", default="")
     p = sub.add_parser("install")
     p.add_argument("--crd-dir", default=os.path.join(os.path.dirname(os.path.dirname(
         os.path.dirname(os.path.abspath(__file__)))), "config", "crd"))
@@ -450,7 +484,8 @@ def main(argv: list[str] | None = None) -> int:
     c, ns = connection(args)
     fn = {"apply": cmd_apply, "get": cmd_get, "describe": cmd_describe, "delete": cmd_delete,
           "scale": cmd_scale, "wait": cmd_wait, "logs": cmd_logs, "events": cmd_events,
-          "devices": cmd_devices, "install": cmd_install, "render": cmd_render}[args.cmd]
+          "devices": cmd_devices, "install": cmd_install, "render": cmd_render,
+          "gpu": cmd_gpu}[args.cmd]
     try:
         return fn(c, ns, args)
     except KubeError as e:

@@ -402,3 +402,39 @@ def test_xgmi_peer_check(cluster_factory):
     assert all(d["probe"]["xgmiGBps"] > 10 for d in devs)
     msgs = " ".join(e.get("message", "") for e in k.list(EVENTS, "default")["items"])
     assert "XGMIPeerCheckFailed" in msgs
+
+
+def test_gpu_maintenance_cordon(node8):
+    """`gpuctl gpu cordon NODE GPU`: the pool holding the GPU replaces it (event-driven), the GPU is
+    never claimed while cordoned (survives release), and `uncordon` returns it to the free set."""
+    import os
+    import subprocess
+    import sys
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    o = wait_ready(k, "p", 2)
+    victim = o["status"]["devices"][0]
+    env = dict(os.environ, PYTHONPATH=node8.env["PYTHONPATH"], GPUPOOL_APISERVER=node8.url)
+
+    def gpuctl(*a):
+        r = subprocess.run([sys.executable, "-m", "gpupool.cli", *a], env=env, capture_output=True,
+                           text=True, timeout=60)
+        assert r.returncode == 0, r.stdout + r.stderr
+        return r.stdout
+    out = gpuctl("gpu", "cordon", "mi355x-node-0", str(victim["index"]), "--reason", "fw update")
+    assert "cordoned" in out and "replaced" in out
+
+    def replaced(o):
+        u = {d["uuid"] for d in (o or {}).get("status", {}).get("devices", [])}
+        return ready_at(2)(o) and victim["uuid"] not in u
+    k.wait_for(MI355XPOOLS, "p", "default", replaced, timeout=15)
+    dev = next(d for d in agent_view(node8)["devices"] if d["uuid"] == victim["uuid"])
+    assert dev["state"] == "Maintenance" and "fw update" in dev["quarantine"]["reason"]
+    # a scale-up never picks the cordoned GPU
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 7}}, "default")
+    o = wait_ready(k, "p", 7)
+    assert victim["uuid"] not in {d["uuid"] for d in o["status"]["devices"]}
+    gpuctl("gpu", "uncordon", "mi355x-node-0", victim["uuid"])
+    assert next(d for d in agent_view(node8)["devices"] if d["uuid"] == victim["uuid"])["state"] == "Free"
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 8}}, "default")
+    wait_ready(k, "p", 8)
