@@ -242,8 +242,9 @@ class Agent:
                     pools |= ps
             if self.changes and self.changes[0][0] > since + 1 and since >= 0:
                 pools.add("*")  # history truncated: tell the manager to resync everything
-            return self.gen, sorted(p for p in pools if p != "*free*") + \
-                (["*"] if "*free*" in pools else [])
+            # "*free*": free-GPU capacity or health changed -> the manager wakes pools that are
+            # waiting for devices; "*": resync everything
+            return self.gen, sorted(pools)
 
     # ================================================================ views
     def _pods_by_device(self) -> dict[str, list[dict]]:
@@ -484,6 +485,8 @@ class Agent:
                 self.ledger.commit(self.records)
             self.stats["releases"] += len(released)
             self._evaluate_all()
+        if released:
+            self._bump({pool_uid, "*free*"})  # capacity freed: wake pools waiting for GPUs
         self._notify_plugins()
         if refused:
             return {"ok": False, "reason": "PodsRunning", "released": released,

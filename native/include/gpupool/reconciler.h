@@ -99,7 +99,8 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
     int64_t free_healthy = 0;
   };
   Observed observe_(const ObjectMeta& m, const Mi355xPoolSpec& spec, const Json& status);
-  std::string choose_node_(const Mi355xPoolSpec& spec, int need, const std::string& current);
+  // Nodes (reachable, selector-matching) with >= need free healthy GPUs, tightest fit first.
+  std::vector<std::string> choose_nodes_(const Mi355xPoolSpec& spec, int need);
   bool quota_allows_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta, std::string* why);
   Outcome finalize_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec);
   // Evicts pods on draining devices and releases drained ones. Returns #devices still draining.

@@ -183,14 +183,14 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
   return o;
 }
 
-std::string Mi355xPoolReconciler::choose_node_(const Mi355xPoolSpec& spec, int need, const std::string& current) {
-  if (!spec.node_name.empty()) return spec.node_name;
-  if (!current.empty()) return current;
-  std::string best;
-  int64_t best_free = -1;
-  auto names = provider_.node_names();
-  std::sort(names.begin(), names.end());
-  for (const auto& n : names) {
+std::vector<std::string> Mi355xPoolReconciler::choose_nodes_(const Mi355xPoolSpec& spec, int need) {
+  if (!spec.node_name.empty()) return {spec.node_name};
+  struct Cand {
+    std::string name;
+    int64_t free;
+  };
+  std::vector<Cand> fit;
+  for (const auto& n : provider_.node_names()) {
     Json labels = provider_.node_labels(n);
     bool match = true;
     for (const auto& kv : spec.node_selector)
@@ -201,15 +201,16 @@ std::string Mi355xPoolReconciler::choose_node_(const Mi355xPoolSpec& spec, int n
     int64_t free = 0;
     for (const auto& d : nv.devices)
       if (d.state == "Free" && d.healthy) ++free;
-    // prefer the tightest node that fits (bin-packing keeps whole nodes free for big pools)
-    bool fits = free >= need, best_fits = best_free >= need;
-    if (best.empty() || (fits && !best_fits) || (fits && best_fits && free < best_free) ||
-        (!fits && !best_fits && free > best_free)) {
-      best = n;
-      best_free = free;
-    }
+    if (free >= need) fit.push_back({n, free});
   }
-  return best;
+  // Tightest fit first (bin-packing keeps whole nodes free for big pools); the caller falls
+  // through the list when a concurrent claim took the capacity meanwhile.
+  std::sort(fit.begin(), fit.end(), [](const Cand& a, const Cand& b) {
+    return a.free != b.free ? a.free < b.free : a.name < b.name;
+  });
+  std::vector<std::string> out;
+  for (const auto& c : fit) out.push_back(c.name);
+  return out;
 }
 
 int Mi355xPoolReconciler::drain_(const Json& obj, const std::string& node, const ObjectMeta& m,
@@ -533,11 +534,15 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     event_(obj, "Warning", "QuotaExceeded", quota_msg);
   } else if (n_active < spec.replicas) {
     int need = static_cast<int>(spec.replicas - n_active);
-    std::string node = o.mine.empty() ? choose_node_(spec, need, obj.path("status.nodeName").as_string()) : o.node;
-    if (node.empty()) {
+    // A pool lives on one node: extend where it already is, else try the fitting nodes in order.
+    std::vector<std::string> candidates = o.mine.empty() ? choose_nodes_(spec, need) : std::vector<std::string>{o.node};
+    if (candidates.empty()) {
       blocked = "InsufficientDevices";
-      progress_msg = "no eligible node with a gpupool agent";
-    } else {
+      progress_msg = "no eligible node has " + std::to_string(need) + " free healthy GPU(s)";
+      event_(obj, "Warning", "InsufficientDevices", progress_msg);
+    }
+    for (size_t ci = 0; ci < candidates.size(); ++ci) {
+      const std::string& node = candidates[ci];
       ClaimRequest req;
       req.pool_uid = m.uid;
       req.pool = m.key();
@@ -550,9 +555,14 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
       ClaimResult cr = provider_.claim(node, req);
       double claim_ms = std::chrono::duration<double, std::milli>(clock_t_::now() - t).count();
       if (!cr.ok) {
-        blocked = cr.reason.empty() ? "InsufficientDevices" : cr.reason;
-        progress_msg = cr.reason + ": " + cr.message;
-        event_(obj, "Warning", cr.reason.empty() ? "InsufficientDevices" : cr.reason, cr.message);
+        const std::string reason = cr.reason.empty() ? "InsufficientDevices" : cr.reason;
+        // raced with another pool for this node's capacity: try the next candidate
+        if (reason == "InsufficientDevices" && ci + 1 < candidates.size()) continue;
+        blocked = reason;
+        progress_msg = reason + ": " + cr.message;
+        event_(obj, "Warning", reason, cr.message);
+        acted = true;
+        break;
       } else {
         std::vector<std::string> ids;
         for (const auto& d : cr.devices) ids.push_back(short_id(d));
@@ -567,8 +577,9 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
         claimed_only = !acted;
         claimed = std::move(cr.devices);
         claimed_node = node;
+        acted = true;
+        break;
       }
-      acted = true;
     }
   }
   if (claimed_only) {

@@ -291,8 +291,11 @@ class AgentWatchers {
     std::set<std::string> uids;
     for (const auto& u : pools.elements()) uids.insert(u.as_string());
     for (const auto& p : pools_.list()) {
+      // pools on that node, pools named in the event, and pools still waiting for capacity
+      // (a release or an un-cordon anywhere may unblock them: no need to sit out the requeue)
       bool hit = uids.count(p.path("metadata.uid").as_string()) > 0 ||
-                 p.path("status.nodeName").as_string() == node || uids.count("*") > 0;
+                 p.path("status.nodeName").as_string() == node || uids.count("*") > 0 ||
+                 (uids.count("*free*") > 0 && !condition_true(p.path("status.conditions"), gen::kCondReady));
       if (hit) ctl_.enqueue("Mi355xPool", p.path("metadata.namespace").as_string(), p.path("metadata.name").as_string());
     }
   }

@@ -438,3 +438,30 @@ def test_gpu_maintenance_cordon(node8):
     assert next(d for d in agent_view(node8)["devices"] if d["uuid"] == victim["uuid"])["state"] == "Free"
     k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 8}}, "default")
     wait_ready(k, "p", 8)
+
+
+def test_many_pools_fill_every_gpu_across_nodes(cluster_factory):
+    """32 one-GPU pools on 4 nodes x 8 GPUs: concurrent workers race for the tightest node; a
+    pool that loses the race falls through to the next fitting node in the same pass, so every
+    GPU ends up claimed exactly once."""
+    c = cluster_factory(nodes=[NodeSpec(f"n{i}") for i in range(4)])
+    k = c.client
+    t0 = time.monotonic()
+    for i in range(32):
+        k.create(MI355XPOOLS, mi_pool(f"p{i}", 1), "default")
+    deadline = time.monotonic() + 30
+    while time.monotonic() < deadline:
+        items = k.list(MI355XPOOLS, "default")["items"]
+        if sum(1 for o in items if ready_at(1)(o)) == 32:
+            break
+        time.sleep(0.1)
+    items = k.list(MI355XPOOLS, "default")["items"]
+    assert sum(1 for o in items if ready_at(1)(o)) == 32, time.monotonic() - t0
+    uuids = [o["status"]["devices"][0]["uuid"] for o in items]
+    assert len(set(uuids)) == 32
+    k.create(MI355XPOOLS, mi_pool("extra", 1), "default")
+    k.wait_for(MI355XPOOLS, "extra", "default",
+               cond_is("Progressing", "False", "InsufficientDevices"), timeout=15)
+    # freeing one GPU wakes the waiting pool without waiting for its requeue
+    k.patch(MI355XPOOLS, "p0", {"spec": {"replicas": 0}}, "default")
+    wait_ready(k, "extra", 1, timeout=15)
