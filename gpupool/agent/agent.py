@@ -247,17 +247,26 @@ class Agent:
             return self.gen, sorted(pools)
 
     # ================================================================ views
-    def _pods_by_device(self) -> dict[str, list[dict]]:
+    def _pods_by_device(self, fresh: bool = False) -> dict[str, list[dict]]:
+        """device ID -> pods holding it, from the kubelet's PodResources API.
+
+        Views (``fresh=False``) may use a 50 ms cache and keep the last known answer while the
+        kubelet is unreachable. Release decisions pass ``fresh=True``: they always ask the kubelet
+        and raise if it cannot answer, so a stale or failed lookup can never free a GPU that a pod
+        still holds."""
         if not self.cfg.pod_resources:
             return {}
         ts, cache = self._pods_cache
-        if time.monotonic() - ts < 0.05:
+        if not fresh and time.monotonic() - ts < 0.05:
             return cache
         from .podresources import list_pod_devices
         try:
             cache = list_pod_devices(self.cfg.pod_resources)
         except Exception as e:  # kubelet down: keep last known view
             log.debug("podresources list failed: %s", e)
+            if fresh:
+                raise
+            return cache
         self._pods_cache = (time.monotonic(), cache)
         return cache
 
@@ -461,7 +470,11 @@ class Agent:
         return {"ok": True, "cordoned": n}
 
     def release(self, pool_uid: str, uuids: list[str]) -> dict:
-        pods = self._pods_by_device()
+        try:
+            pods = self._pods_by_device(fresh=True)
+        except Exception as e:
+            return {"ok": False, "reason": "PodResourcesUnavailable", "released": [],
+                    "message": f"cannot confirm the GPUs are pod-free: {e}"}
         released, refused = [], []
         with self.lock:
             for u in uuids:

@@ -35,6 +35,13 @@ LABEL_GFX = "amd.com/gpu.family"
 LABEL_POOL = "gpupool.amd.com/pool"
 DEFAULT_RESOURCE = "amd.com/gpu"
 
+# Mi355xJob: finalizer that deletes the job's pods before the job goes away, and the labels every
+# job pod carries (the controller lists pods by them and checks the owner UID).
+JOB_FINALIZER = "compute.my.domain/job-cleanup"
+LABEL_JOB = "gpupool.amd.com/job-name"
+LABEL_JOB_INDEX = "gpupool.amd.com/replica-index"
+LABEL_JOB_ATTEMPT = "gpupool.amd.com/attempt"
+
 # Condition types (metav1.Condition, README.md:126-127; roadmap README.md:310).
 COND_READY = "Ready"
 COND_PROGRESSING = "Progressing"
@@ -49,6 +56,15 @@ COND_PROBE = "DeviceProbePassed"
 AZURE_CONDITIONS = [COND_READY, COND_PROGRESSING, COND_DEGRADED, COND_DELETING, COND_CREDENTIALS]
 MI355X_CONDITIONS = [COND_READY, COND_PROGRESSING, COND_DEGRADED, COND_DELETING,
                      COND_XGMI, COND_ECC, COND_THERMAL, COND_PROBE]
+
+# Mi355xJob condition types (Kubeflow JobCreated/JobRunning/JobRestarting/JobSucceeded/JobFailed,
+# plus the Volcano-style gang placement as Scheduled).
+COND_SCHEDULED = "Scheduled"
+COND_RUNNING = "Running"
+COND_RESTARTING = "Restarting"
+COND_SUCCEEDED = "Succeeded"
+COND_FAILED = "Failed"
+JOB_CONDITIONS = [COND_SCHEDULED, COND_RUNNING, COND_RESTARTING, COND_SUCCEEDED, COND_FAILED]
 
 AZURE_CREDENTIAL_KEYS = ["AZURE_CLIENT_ID", "AZURE_CLIENT_SECRET", "AZURE_TENANT_ID",
                          "AZURE_SUBSCRIPTION_ID"]  # README.md:108
@@ -249,6 +265,77 @@ MI355X_STATUS = {
     },
 }
 
+# ---------------------------------------------------------------- Mi355xJob
+# The GoHai platform's training-job path (reference GPU调度平台搭建.md:638-675 Volcano Job with
+# `minAvailable`/`queue`/`restartPolicy: OnFailure`, :300-306 Kubeflow Training Operator whose
+# `PET_*` env the workload reads at :623) as one MI355X-native kind: a gang of pods, each asking
+# for `gpusPerReplica` pool GPUs, placed all-or-nothing and wired for torchrun / RCCL.
+MI355X_JOB_SPEC = {
+    "type": "object",
+    "description": "A gang-scheduled distributed training job on pool-advertised MI355X GPUs.",
+    "required": ["replicas", "template"],
+    "properties": {
+        "replicas": {**_I32, "minimum": 1, "maximum": 1024,
+                     "description": "Worker pods (torchrun nnodes); placed all-or-nothing."},
+        "gpusPerReplica": {**_I32, "minimum": 0, "maximum": 64, "default": 1,
+                           "description": "GPUs per pod (torchrun nproc-per-node)."},
+        "resourceName": {**_S, "pattern": r"^[a-z0-9.-]+/[a-z0-9.-]+$",
+                         "description": "Extended resource to request (default: the poolRef's, "
+                                        "else amd.com/gpu)."},
+        "poolRef": {**_S, "description": "Mi355xPool in this namespace whose GPUs the job "
+                                         "uses: its resourceName and node."},
+        "nodeSelector": {"type": "object", "additionalProperties": _S},
+        "queue": {**_S, "default": "default",
+                  "description": "Jobs of one queue are placed strictly in (priority desc, "
+                                 "creation) order, so a large gang cannot be starved."},
+        "priority": {**_I32, "default": 0},
+        "restartPolicy": {"type": "string", "enum": ["OnFailure", "Never"],
+                          "default": "OnFailure",
+                          "description": "OnFailure: a failed or lost pod restarts the whole "
+                                         "gang (DDP ranks cannot rejoin alone)."},
+        "backoffLimit": {**_I32, "minimum": 0, "default": 3},
+        "activeDeadlineSeconds": {**_I64, "minimum": 0, "default": 0,
+                                  "description": "0 = no deadline."},
+        "ttlSecondsAfterFinished": {**_I64, "minimum": -1, "default": -1,
+                                    "description": "Delete the job this long after it "
+                                                   "finished (-1 = keep)."},
+        "cleanPodPolicy": {"type": "string", "enum": ["Running", "All", "None"],
+                           "default": "Running",
+                           "description": "Pods deleted when the job finishes."},
+        "successPolicy": {"type": "string", "enum": ["AllWorkers", "Rank0"],
+                          "default": "AllWorkers"},
+        "masterPort": {**_I32, "minimum": 1, "maximum": 65535, "default": 29500},
+        "template": {"type": "object", "x-kubernetes-preserve-unknown-fields": True,
+                     "description": "Pod template (metadata + spec) of every worker."},
+    },
+}
+
+MI355X_JOB_STATUS = {
+    "type": "object",
+    "properties": {
+        "observedGeneration": _I64,
+        "phase": {"type": "string",
+                  "enum": ["Pending", "Running", "Restarting", "Succeeded", "Failed"]},
+        "replicas": _I32,
+        "active": _I32,
+        "succeeded": _I32,
+        "failed": _I32,
+        "restarts": _I32,
+        "attempt": _I32,
+        "masterAddr": _S,
+        "startTime": _S,
+        "completionTime": _S,
+        "placement": {"type": "array", "items": {
+            "type": "object",
+            "properties": {"index": _I32, "node": _S}}},
+        "replicaStatuses": {"type": "array", "items": {
+            "type": "object",
+            "properties": {"index": _I32, "pod": _S, "node": _S, "phase": _S, "podIP": _S,
+                           "exitCode": _I32, "devices": _S, "message": _S}}},
+        "conditions": CONDITIONS_FIELD,
+    },
+}
+
 KINDS = {
     "AzureVmPool": {
         "plural": "azurevmpools",
@@ -278,6 +365,23 @@ KINDS = {
             {"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"},
         ],
         "conditions": MI355X_CONDITIONS,
+    },
+    "Mi355xJob": {
+        "plural": "mi355xjobs",
+        "singular": "mi355xjob",
+        "shortNames": ["mxj"],
+        "spec": MI355X_JOB_SPEC,
+        "status": MI355X_JOB_STATUS,
+        "printerColumns": [
+            {"name": "Replicas", "type": "integer", "jsonPath": ".spec.replicas"},
+            {"name": "GPUs", "type": "integer", "jsonPath": ".spec.gpusPerReplica"},
+            {"name": "Active", "type": "integer", "jsonPath": ".status.active"},
+            {"name": "Phase", "type": "string", "jsonPath": ".status.phase"},
+            {"name": "Restarts", "type": "integer", "jsonPath": ".status.restarts"},
+            {"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"},
+        ],
+        "conditions": JOB_CONDITIONS,
+        "scale": False,
     },
 }
 
@@ -311,11 +415,10 @@ def crd(kind: str) -> dict:
                 "served": True,
                 "storage": True,
                 "schema": {"openAPIV3Schema": schema},
-                "subresources": {
-                    "status": {},
+                "subresources": {"status": {}, **({
                     "scale": {"specReplicasPath": ".spec.replicas",
-                              "statusReplicasPath": ".status.readyReplicas"},
-                },
+                              "statusReplicasPath": ".status.readyReplicas"}}
+                    if k.get("scale", True) else {})},
                 "additionalPrinterColumns": copy.deepcopy(k["printerColumns"]),
             }],
         },
@@ -337,7 +440,8 @@ def rbac_role() -> dict:
          "verbs": ["update"]},
         {"apiGroups": [""], "resources": ["secrets"], "verbs": ["get"]},
         {"apiGroups": [""], "resources": ["events"], "verbs": ["create", "patch"]},
-        {"apiGroups": [""], "resources": ["pods"], "verbs": ["get", "list", "watch", "delete"]},
+        {"apiGroups": [""], "resources": ["pods"],
+         "verbs": ["get", "list", "watch", "create", "delete"]},
         {"apiGroups": [""], "resources": ["pods/eviction"], "verbs": ["create"]},
         {"apiGroups": [""], "resources": ["nodes"], "verbs": ["get", "list", "watch", "patch"]},
         {"apiGroups": ["coordination.k8s.io"], "resources": ["leases"],

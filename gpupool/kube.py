@@ -59,11 +59,12 @@ LEASES = Res("coordination.k8s.io", "v1", "leases")
 CRDS = Res("apiextensions.k8s.io", "v1", "customresourcedefinitions", namespaced=False)
 MI355XPOOLS = Res(schema.GROUP, schema.VERSION, "mi355xpools")
 AZUREVMPOOLS = Res(schema.GROUP, schema.VERSION, "azurevmpools")
+MI355XJOBS = Res(schema.GROUP, schema.VERSION, "mi355xjobs")
 
 BY_KIND = {
     "Pod": PODS, "Node": NODES, "Event": EVENTS, "Secret": SECRETS, "ConfigMap": CONFIGMAPS,
     "Namespace": NAMESPACES, "Lease": LEASES, "CustomResourceDefinition": CRDS,
-    "Mi355xPool": MI355XPOOLS, "AzureVmPool": AZUREVMPOOLS,
+    "Mi355xPool": MI355XPOOLS, "AzureVmPool": AZUREVMPOOLS, "Mi355xJob": MI355XJOBS,
     "ClusterRole": Res("rbac.authorization.k8s.io", "v1", "clusterroles", namespaced=False),
     "ClusterRoleBinding": Res("rbac.authorization.k8s.io", "v1", "clusterrolebindings",
                               namespaced=False),

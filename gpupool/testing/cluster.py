@@ -96,7 +96,7 @@ class Cluster:
     def __init__(self, workdir: str, nodes: list[NodeSpec] | None = None,
                  manager_args: list[str] | None = None, manager: bool = True,
                  python: str = sys.executable, env: dict | None = None,
-                 sample_interval: float = 0.5, kinds: str = "mi355x,azure",
+                 sample_interval: float = 0.5, kinds: str = "mi355x,azure,job",
                  manager_bin: str | None = None, tls: bool = False, token: str | None = None):
         self.workdir = os.path.abspath(workdir)
         self.tls = tls

@@ -69,9 +69,31 @@ struct Mi355xPoolSpec {
   Json policy_json() const;  // health + partition, as the agent/device library consume it
 };
 
+// ---------------------------------------------------------------- Mi355xJob
+// Gang-scheduled distributed training job (schema: gpupool/api/schema.py MI355X_JOB_SPEC).
+struct Mi355xJobSpec {
+  int32_t replicas = 1;
+  int32_t gpus_per_replica = 1;
+  std::string resource_name;  // "" = the poolRef's, else amd.com/gpu
+  std::string pool_ref;
+  std::map<std::string, std::string> node_selector;
+  std::string queue = "default";
+  int32_t priority = 0;
+  std::string restart_policy = "OnFailure";
+  int32_t backoff_limit = 3;
+  int64_t active_deadline_seconds = 0;
+  int64_t ttl_seconds_after_finished = -1;
+  std::string clean_pod_policy = "Running";
+  std::string success_policy = "AllWorkers";
+  int32_t master_port = 29500;
+  Json tmpl;  // PodTemplateSpec
+  static Mi355xJobSpec from(const Json& spec);
+};
+
 // Validation mirroring the CRD schema; returns "field: message" strings.
 std::vector<std::string> validate_azure(const Json& obj);
 std::vector<std::string> validate_mi355x(const Json& obj);
+std::vector<std::string> validate_job(const Json& obj);
 
 // ---------------------------------------------------------------- conditions
 // meta.SetStatusCondition semantics: merge by type; lastTransitionTime moves only on a status

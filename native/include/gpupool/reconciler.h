@@ -73,6 +73,7 @@ class PoolReconcilerBase {
   ReconcilerOptions opts_;
   std::string kind_;
   ResourceRef res_;
+  std::string finalizer_;  // gen::kFinalizer for pools
   Logger log_;
   std::mutex mu_;
   // reconcile-to-Ready tracking: uid -> (generation, first time that generation was seen)
@@ -127,6 +128,56 @@ class AzureVmPoolReconciler : public PoolReconcilerBase {
   bool credentials_(const ObjectMeta& m, const AzureVmPoolSpec& spec, Credentials* out, std::string* why);
   CloudProvider& cloud_;
   std::atomic<uint64_t> name_seq_{0};
+};
+
+// Mi355xJob: the GoHai platform's training-job path (reference GPU调度平台搭建.md:638-675 Volcano Job
+// with minAvailable/queue/restartPolicy, :300-306 Kubeflow PyTorchJob, PET_* env read at :623)
+// as one kind. A job is a gang of `replicas` pods, each requesting `gpusPerReplica` GPUs of a
+// pool's extended resource:
+//   * placement is all-or-nothing (every pod bound to a node up front, or none), per-queue strict
+//     (priority desc, creation) order so a big gang is not starved by smaller ones, packed onto
+//     the fewest nodes (tightest single node when the gang fits on one);
+//   * the rank-0 pod is created first; the others get MASTER_ADDR = its pod IP (+ MASTER_PORT,
+//     WORLD_SIZE/RANK for one-GPU workers, PET_NNODES/PET_NPROC_PER_NODE/PET_NODE_RANK for
+//     torchrun), so RCCL/gloo rendezvous needs no Service or DNS;
+//   * a failed or lost pod restarts the whole gang (restartPolicy OnFailure, backoffLimit), since
+//     DDP ranks cannot rejoin alone; activeDeadlineSeconds, successPolicy, cleanPodPolicy and
+//     ttlSecondsAfterFinished follow the batch/v1 Job and Kubeflow meanings.
+// Reservations of placed-but-not-yet-created pods live in status.placement, and every placement
+// decision runs under one mutex against fresh LISTs, so two gangs never share a GPU.
+class Mi355xJobReconciler : public PoolReconcilerBase {
+ public:
+  Mi355xJobReconciler(KubeClient& client, Informer& jobs, Informer& nodes, EventRecorder* events,
+                      ReconcilerOptions opts = {});
+  Outcome reconcile(const std::string& ns, const std::string& name) override;
+  // Jobs still waiting for a gang placement (re-enqueued when capacity may have freed up).
+  std::vector<std::pair<std::string, std::string>> pending() const;
+
+  struct Slot {
+    int index = 0;
+    std::string node;
+  };
+  // Pure placement: free GPUs per node (already ordered candidates) -> one node per replica, or
+  // empty when the gang does not fit. Exposed for unit tests.
+  static std::vector<Slot> place(const std::vector<std::pair<std::string, int64_t>>& free, int replicas,
+                                 int64_t gpus_per_replica);
+
+ private:
+  Outcome finish_(const Json& obj, const ObjectMeta& m, const Mi355xJobSpec& spec, Json st, const std::string& phase,
+                  const std::string& reason, const std::string& msg, const std::vector<Json>& pods);
+  Outcome cleanup_finished_(const Json& obj, const ObjectMeta& m, const Mi355xJobSpec& spec,
+                            const std::vector<Json>& pods);
+  std::vector<Json> list_pods_(const ObjectMeta& m);
+  // Tries to place the gang (under sched_mu_). Returns the placement, or empty with *why set.
+  std::vector<Slot> schedule_(const ObjectMeta& m, const Mi355xJobSpec& spec, const std::string& resource,
+                              const std::string& pool_node, std::string* reason, std::string* why);
+  Json build_pod_(const Json& job, const ObjectMeta& m, const Mi355xJobSpec& spec, const std::string& resource,
+                  int attempt, const Slot& slot, const std::string& master_addr);
+  bool resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec& spec, std::string* resource, std::string* node,
+                     std::string* why);
+
+  Informer& nodes_;
+  std::mutex sched_mu_;
 };
 
 // Controller: a shared work queue + N workers dispatching "Kind/ns/name" keys to reconcilers,

@@ -143,6 +143,65 @@ std::vector<std::string> validate_azure(const Json& obj) {
   return errs;
 }
 
+Mi355xJobSpec Mi355xJobSpec::from(const Json& s) {
+  Mi355xJobSpec j;
+  j.replicas = static_cast<int32_t>(s["replicas"].as_int(1));
+  j.gpus_per_replica = static_cast<int32_t>(s["gpusPerReplica"].as_int(1));
+  j.resource_name = s["resourceName"].as_string();
+  j.pool_ref = s["poolRef"].as_string();
+  for (const auto& kv : s["nodeSelector"].members()) j.node_selector[kv.first] = kv.second.as_string();
+  j.queue = s["queue"].str_or("default");
+  j.priority = static_cast<int32_t>(s["priority"].as_int(0));
+  j.restart_policy = s["restartPolicy"].str_or("OnFailure");
+  j.backoff_limit = static_cast<int32_t>(s["backoffLimit"].as_int(3));
+  j.active_deadline_seconds = s["activeDeadlineSeconds"].as_int(0);
+  j.ttl_seconds_after_finished = s["ttlSecondsAfterFinished"].as_int(-1);
+  j.clean_pod_policy = s["cleanPodPolicy"].str_or("Running");
+  j.success_policy = s["successPolicy"].str_or("AllWorkers");
+  j.master_port = static_cast<int32_t>(s["masterPort"].as_int(29500));
+  j.tmpl = s["template"].is_object() ? s["template"] : Json::object();
+  return j;
+}
+
+std::vector<std::string> validate_job(const Json& obj) {
+  std::vector<std::string> errs;
+  const Json& s = obj["spec"];
+  if (!s.is_object()) return {"spec: Required value"};
+  auto int_range = [&](const char* k, int64_t lo, int64_t hi, bool required) {
+    if (!s.contains(k)) {
+      if (required) errs.push_back(std::string("spec.") + k + ": Required value (integer)");
+      return;
+    }
+    if (!s[k].is_int()) {
+      errs.push_back(std::string("spec.") + k + ": must be of type integer");
+      return;
+    }
+    int64_t v = s[k].as_int();
+    if (v < lo || v > hi)
+      errs.push_back(std::string("spec.") + k + ": Invalid value: " + std::to_string(v) + ": must be within [" +
+                     std::to_string(lo) + ", " + std::to_string(hi) + "]");
+  };
+  int_range("replicas", 1, 1024, true);
+  int_range("gpusPerReplica", 0, 64, false);
+  int_range("backoffLimit", 0, INT32_MAX, false);
+  int_range("activeDeadlineSeconds", 0, INT64_MAX, false);
+  int_range("ttlSecondsAfterFinished", -1, INT64_MAX, false);
+  int_range("masterPort", 1, 65535, false);
+  if (s.contains("resourceName")) {
+    static const std::regex re("^[a-z0-9.-]+/[a-z0-9.-]+$");
+    if (!s["resourceName"].is_string() || !std::regex_match(s["resourceName"].as_string(), re))
+      errs.push_back("spec.resourceName: Invalid value: should match '^[a-z0-9.-]+/[a-z0-9.-]+$'");
+  }
+  if (s.contains("restartPolicy") && !in(s["restartPolicy"].as_string(), {"OnFailure", "Never"}))
+    errs.push_back("spec.restartPolicy: Unsupported value");
+  if (s.contains("cleanPodPolicy") && !in(s["cleanPodPolicy"].as_string(), {"Running", "All", "None"}))
+    errs.push_back("spec.cleanPodPolicy: Unsupported value");
+  if (s.contains("successPolicy") && !in(s["successPolicy"].as_string(), {"AllWorkers", "Rank0"}))
+    errs.push_back("spec.successPolicy: Unsupported value");
+  if (!s["template"].is_object()) errs.push_back("spec.template: Required value");
+  return errs;
+}
+
 std::vector<std::string> validate_mi355x(const Json& obj) {
   std::vector<std::string> errs;
   const Json& s = obj["spec"];

@@ -1,0 +1,645 @@
+// Mi355xJobReconciler — gang-scheduled distributed training jobs on pool-advertised MI355X GPUs.
+//
+// Reference behaviour being replaced: a Volcano Job
+// (GPU调度平台搭建.md:643-672: `minAvailable`, `schedulerName: volcano`, `queue: default`,
+// `restartPolicy: OnFailure`, `nvidia.com/gpu: 1`) run through the Kubeflow Training Operator
+// (:300-306) whose PET_* env the workload inspects to pick single vs distributed mode (:623-630).
+// Here one controller does gang placement, rendezvous wiring and gang restarts; see the class
+// comment in reconciler.h for the contract.
+#include <algorithm>
+#include <cstdlib>
+#include <set>
+#include <tuple>
+
+#include "gpupool/generated/schema_consts.h"
+#include "gpupool/reconciler.h"
+
+namespace gpupool {
+
+namespace {
+
+using ms = std::chrono::milliseconds;
+
+CounterVec& job_events() {
+  static CounterVec& c = Registry::global().counter("gpupool_job_transitions_total",
+                                                    "Mi355xJob lifecycle transitions by kind.");
+  return c;
+}
+HistogramVec& gang_wait_hist() {
+  static HistogramVec& h = Registry::global().histogram(
+      "gpupool_job_gang_wait_seconds", "From job creation (or gang restart) to its gang placement.",
+      exponential_buckets(0.001, 2, 20));
+  return h;
+}
+
+int64_t qty(const Json& v) {
+  if (v.is_int()) return v.as_int();
+  if (v.is_number()) return static_cast<int64_t>(v.as_double());
+  const std::string& s = v.as_string();
+  return s.empty() ? 0 : std::atoll(s.c_str());
+}
+
+bool terminal(const std::string& phase) { return phase == "Succeeded" || phase == "Failed"; }
+
+std::string pod_phase(const Json& p) { return p.path("status.phase").str_or("Pending"); }
+
+int64_t pod_request(const Json& pod, const std::string& resource) {
+  int64_t n = 0;
+  for (const auto& c : pod.path("spec.containers").elements()) {
+    const Json& r = c["resources"];
+    int64_t lim = qty(r["limits"][resource]);
+    n += lim ? lim : qty(r["requests"][resource]);
+  }
+  return n;
+}
+
+std::string pod_name(const std::string& job, int index) { return job + "-worker-" + std::to_string(index); }
+
+int label_int(const Json& pod, const char* key, int def) {
+  const std::string& v = pod.path("metadata.labels")[key].as_string();
+  return v.empty() ? def : std::atoi(v.c_str());
+}
+
+bool selector_matches(const std::map<std::string, std::string>& sel, const Json& node) {
+  const Json& labels = node.path("metadata.labels");
+  for (const auto& kv : sel)
+    if (labels[kv.first].as_string() != kv.second) return false;
+  return true;
+}
+
+bool node_schedulable(const Json& node) {
+  if (node.path("spec.unschedulable").as_bool(false)) return false;
+  for (const auto& c : node.path("status.conditions").elements())
+    if (c["type"].as_string() == "Ready" && c["status"].as_string() == "False") return false;
+  return true;
+}
+
+}  // namespace
+
+Mi355xJobReconciler::Mi355xJobReconciler(KubeClient& client, Informer& jobs, Informer& nodes, EventRecorder* events,
+                                         ReconcilerOptions opts)
+    : PoolReconcilerBase(client, jobs, events, opts, "Mi355xJob",
+                         ResourceRef{gen::kGroup, gen::kVersion, gen::kPluralMi355xJob, true, "Mi355xJob"}),
+      nodes_(nodes) {
+  finalizer_ = gen::kJobFinalizer;
+}
+
+std::vector<std::pair<std::string, std::string>> Mi355xJobReconciler::pending() const {
+  std::vector<std::pair<std::string, std::string>> out;
+  for (const auto& j : pools_.list()) {
+    const std::string phase = j.path("status.phase").str_or("Pending");
+    if (phase == "Pending" || phase == "Restarting")
+      out.emplace_back(j.path("metadata.namespace").as_string(), j.path("metadata.name").as_string());
+  }
+  return out;
+}
+
+std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::place(
+    const std::vector<std::pair<std::string, int64_t>>& free, int replicas, int64_t gpus) {
+  std::vector<Slot> out;
+  if (free.empty() || replicas <= 0) return out;
+  if (gpus <= 0) {  // CPU-only workers: no capacity to account, keep them together on the first node
+    for (int i = 0; i < replicas; ++i) out.push_back({i, free.front().first});
+    return out;
+  }
+  const int64_t need = gpus * replicas;
+  // Whole gang on one node (xGMI between every pair of its GPUs): the tightest node that fits.
+  const std::pair<std::string, int64_t>* best = nullptr;
+  for (const auto& f : free)
+    if (f.second >= need && (!best || f.second < best->second)) best = &f;
+  if (best) {
+    for (int i = 0; i < replicas; ++i) out.push_back({i, best->first});
+    return out;
+  }
+  // Otherwise the fewest nodes: fill the roomiest first. Rank 0 lands on the first node.
+  std::vector<std::pair<std::string, int64_t>> order(free.begin(), free.end());
+  std::stable_sort(order.begin(), order.end(), [](const auto& a, const auto& b) { return a.second > b.second; });
+  int i = 0;
+  for (auto& f : order) {
+    while (i < replicas && f.second >= gpus) {
+      out.push_back({i++, f.first});
+      f.second -= gpus;
+    }
+    if (i == replicas) return out;
+  }
+  return {};
+}
+
+std::vector<Json> Mi355xJobReconciler::list_pods_(const ObjectMeta& m) {
+  std::vector<Json> out;
+  Json lst = client_.list(res::pods(), m.ns, std::string(gen::kLabelJob) + "=" + m.name);
+  for (const auto& p : lst["items"].elements()) {
+    bool owned = false;
+    for (const auto& o : p.path("metadata.ownerReferences").elements())
+      owned = owned || o["uid"].as_string() == m.uid;
+    if (owned) out.push_back(p);
+  }
+  return out;
+}
+
+bool Mi355xJobReconciler::resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec& spec, std::string* resource,
+                                        std::string* node, std::string* why) {
+  *resource = spec.resource_name.empty() ? gen::kDefaultResource : spec.resource_name;
+  if (spec.pool_ref.empty()) return true;
+  Json pool;
+  try {
+    pool = client_.get(res::mi355xpools(), m.ns, spec.pool_ref);
+  } catch (const KubeError& e) {
+    if (!e.not_found()) throw;
+    *why = "Mi355xPool " + m.ns + "/" + spec.pool_ref + " not found";
+    return false;
+  }
+  if (spec.resource_name.empty()) *resource = pool.path("spec.resourceName").str_or(gen::kDefaultResource);
+  *node = pool.path("status.nodeName").as_string();
+  if (node->empty()) {
+    *why = "Mi355xPool " + spec.pool_ref + " has no GPUs placed yet";
+    return false;
+  }
+  return true;
+}
+
+std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const ObjectMeta& m, const Mi355xJobSpec& spec,
+                                                                      const std::string& resource,
+                                                                      const std::string& pool_node,
+                                                                      std::string* reason, std::string* why) {
+  trace::Span span("schedule");
+  // 1. queue order: jobs of the same queue that still wait for a placement and sort ahead of us
+  //    (priority desc, creation asc) block us, unless they could never fit the whole cluster.
+  Json jobs = client_.list(res_, "");
+  Json nodes = client_.list(res::nodes());
+  int64_t cluster_total = 0;
+  for (const auto& n : nodes["items"].elements()) cluster_total += qty(n.path("status.allocatable")[resource]);
+  auto key_of = [](const Json& j) {
+    return std::make_tuple(-j.path("spec.priority").as_int(0), j.path("metadata.creationTimestamp").as_string(),
+                           j.path("metadata.namespace").as_string() + "/" + j.path("metadata.name").as_string());
+  };
+  Json self;
+  for (const auto& j : jobs["items"].elements())
+    if (j.path("metadata.uid").as_string() == m.uid) self = j;
+  if (self.is_null()) return {};
+  auto my_key = key_of(self);
+  for (const auto& j : jobs["items"].elements()) {
+    if (j.path("metadata.uid").as_string() == m.uid || !j.path("metadata.deletionTimestamp").as_string().empty()) continue;
+    if (j.path("spec.queue").str_or("default") != spec.queue) continue;
+    const std::string phase = j.path("status.phase").str_or("Pending");
+    if (phase != "Pending" && phase != "Restarting") continue;
+    if (!j.path("status.placement").elements().empty()) continue;  // already placed
+    const std::string jres = j.path("spec.resourceName").str_or(resource);
+    int64_t jneed = j.path("spec.replicas").as_int(1) * j.path("spec.gpusPerReplica").as_int(1);
+    if (jres == resource && jneed > cluster_total) continue;  // can never run: must not block the queue
+    if (key_of(j) < my_key) {
+      *reason = "QueuedBehind";
+      *why = "queue " + spec.queue + ": waiting behind " + j.path("metadata.namespace").as_string() + "/" +
+             j.path("metadata.name").as_string();
+      return {};
+    }
+  }
+  // 2. free GPUs per candidate node = allocatable - live pod requests - other jobs' reservations
+  std::map<std::string, int64_t> free;
+  std::vector<std::string> order;
+  for (const auto& n : nodes["items"].elements()) {
+    const std::string name = n.path("metadata.name").as_string();
+    if (!node_schedulable(n) || !selector_matches(spec.node_selector, n)) continue;
+    if (!pool_node.empty() && name != pool_node) continue;
+    free[name] = qty(n.path("status.allocatable")[resource]);
+    order.push_back(name);
+  }
+  if (spec.gpus_per_replica > 0) {
+    Json pods = client_.list(res::pods(), "");
+    for (const auto& p : pods["items"].elements()) {
+      const std::string node = p.path("spec.nodeName").as_string();
+      if (node.empty() || !free.count(node) || terminal(pod_phase(p))) continue;
+      free[node] -= pod_request(p, resource);
+    }
+    for (const auto& j : jobs["items"].elements()) {
+      if (j.path("metadata.uid").as_string() == m.uid || terminal(j.path("status.phase").as_string())) continue;
+      if (j.path("spec.resourceName").str_or(resource) != resource) continue;
+      int64_t g = j.path("spec.gpusPerReplica").as_int(1);
+      for (const auto& s : j.path("status.placement").elements())
+        if (!s["created"].as_bool(false) && free.count(s["node"].as_string())) free[s["node"].as_string()] -= g;
+    }
+  }
+  std::vector<std::pair<std::string, int64_t>> cands;
+  for (const auto& n : order) cands.emplace_back(n, std::max<int64_t>(0, free[n]));
+  auto slots = place(cands, spec.replicas, spec.gpus_per_replica);
+  if (slots.empty()) {
+    int64_t total_free = 0;
+    for (const auto& c : cands) total_free += c.second;
+    *reason = "Unschedulable";
+    *why = "gang of " + std::to_string(spec.replicas) + " x " + std::to_string(spec.gpus_per_replica) + " " +
+           resource + " does not fit: " + std::to_string(total_free) + " free on " + std::to_string(cands.size()) +
+           " candidate node(s)";
+  }
+  return slots;
+}
+
+Json Mi355xJobReconciler::build_pod_(const Json& job, const ObjectMeta& m, const Mi355xJobSpec& spec,
+                                     const std::string& resource, int attempt, const Slot& slot,
+                                     const std::string& master_addr) {
+  Json pod = Json::object();
+  pod["apiVersion"] = "v1";
+  pod["kind"] = "Pod";
+  Json md = spec.tmpl["metadata"].is_object() ? spec.tmpl["metadata"] : Json::object();
+  Json out_md = Json::object();
+  out_md["name"] = pod_name(m.name, slot.index);
+  out_md["namespace"] = m.ns;
+  Json labels = md["labels"].is_object() ? md["labels"] : Json::object();
+  labels[gen::kLabelJob] = m.name;
+  labels[gen::kLabelJobIndex] = std::to_string(slot.index);
+  labels[gen::kLabelJobAttempt] = std::to_string(attempt);
+  out_md["labels"] = labels;
+  if (md["annotations"].is_object()) out_md["annotations"] = md["annotations"];
+  Json owner = Json::object();
+  owner["apiVersion"] = job["apiVersion"].str_or(gen::kApiVersion);
+  owner["kind"] = "Mi355xJob";
+  owner["name"] = m.name;
+  owner["uid"] = m.uid;
+  owner["controller"] = true;
+  owner["blockOwnerDeletion"] = true;
+  out_md["ownerReferences"] = Json::array({owner});
+  pod["metadata"] = out_md;
+
+  Json ps = spec.tmpl["spec"].is_object() ? spec.tmpl["spec"] : Json::object();
+  ps["nodeName"] = slot.node;       // gang placement binds every pod up front
+  ps["restartPolicy"] = "Never";    // restarts are gang-wide, by this controller
+  if (!ps["containers"].is_array() || ps["containers"].size() == 0) {
+    Json c = Json::object();
+    c["name"] = "main";
+    ps["containers"] = Json::array({c});
+  }
+  const int nnodes = spec.replicas, nproc = std::max(1, spec.gpus_per_replica);
+  std::vector<std::pair<std::string, std::string>> env = {
+      {"MASTER_ADDR", master_addr},
+      {"MASTER_PORT", std::to_string(spec.master_port)},
+      {"PET_MASTER_ADDR", master_addr},
+      {"PET_MASTER_PORT", std::to_string(spec.master_port)},
+      {"PET_NNODES", std::to_string(nnodes)},
+      {"PET_NPROC_PER_NODE", std::to_string(nproc)},
+      {"PET_NODE_RANK", std::to_string(slot.index)},
+      {"NODE_RANK", std::to_string(slot.index)},
+      {"GPUPOOL_JOB_NAME", m.name},
+      {"GPUPOOL_JOB_ATTEMPT", std::to_string(attempt)},
+      {"GPUPOOL_REPLICA_INDEX", std::to_string(slot.index)},
+  };
+  if (nproc == 1) {  // one process per pod: the pod IS the rank (no torchrun needed)
+    env.push_back({"WORLD_SIZE", std::to_string(nnodes)});
+    env.push_back({"RANK", std::to_string(slot.index)});
+    env.push_back({"LOCAL_RANK", "0"});
+    env.push_back({"LOCAL_WORLD_SIZE", "1"});
+  }
+  Json containers = Json::array();
+  for (size_t ci = 0; ci < ps["containers"].size(); ++ci) {
+    Json c = static_cast<const Json&>(ps)["containers"][ci];
+    Json cenv = Json::array();
+    std::set<std::string> ours;
+    for (const auto& kv : env) ours.insert(kv.first);
+    for (const auto& e : c["env"].elements())
+      if (!ours.count(e["name"].as_string())) cenv.push_back(e);  // controller-owned names win
+    for (const auto& kv : env) cenv.push_back(Json::object().set("name", kv.first).set("value", kv.second));
+    c["env"] = cenv;
+    if (ci == 0 && spec.gpus_per_replica > 0) {  // the GPU request sits on the first container
+      c["resources"]["limits"][resource] = std::to_string(spec.gpus_per_replica);
+      c["resources"]["requests"][resource] = std::to_string(spec.gpus_per_replica);
+    }
+    containers.push_back(c);
+  }
+  ps["containers"] = containers;
+  pod["spec"] = ps;
+  return pod;
+}
+
+Outcome Mi355xJobReconciler::cleanup_finished_(const Json& obj, const ObjectMeta& m, const Mi355xJobSpec& spec,
+                                               const std::vector<Json>& pods) {
+  (void)obj;
+  (void)m;
+  if (spec.clean_pod_policy == "None") return Outcome::done(ms(0));
+  int left = 0;
+  for (const auto& p : pods) {
+    if (!p.path("metadata.deletionTimestamp").as_string().empty()) {
+      ++left;
+      continue;
+    }
+    if (spec.clean_pod_policy == "Running" && terminal(pod_phase(p))) continue;
+    try {
+      client_.del(res::pods(), m.ns, p.path("metadata.name").as_string());
+      ++left;
+    } catch (const KubeError& e) {
+      if (!e.not_found()) throw;
+    }
+  }
+  return left ? Outcome::requeue(opts_.progress_poll, "cleaning up pods") : Outcome::done(ms(0));
+}
+
+Outcome Mi355xJobReconciler::finish_(const Json& obj, const ObjectMeta& m, const Mi355xJobSpec& spec, Json st,
+                                     const std::string& phase, const std::string& reason, const std::string& msg,
+                                     const std::vector<Json>& pods) {
+  const std::string now = rfc3339_now();
+  const Json& cst = st;
+  Json conds = cst["conditions"].is_array() ? cst["conditions"] : Json::array();
+  st["phase"] = phase;
+  st["completionTime"] = now;
+  st["active"] = 0;
+  st["placement"] = Json::array();
+  set_condition(conds, gen::kCondRunning, "False", phase == "Succeeded" ? "JobSucceeded" : reason, msg, m.generation,
+                now);
+  set_condition(conds, gen::kCondRestarting, "False", "Finished", "", m.generation, now);
+  set_condition(conds, phase == "Succeeded" ? gen::kCondSucceeded : gen::kCondFailed, "True", reason, msg, m.generation,
+                now);
+  st["conditions"] = conds;
+  write_status_(obj, st);
+  event_(obj, phase == "Succeeded" ? "Normal" : "Warning", phase == "Succeeded" ? "JobSucceeded" : "JobFailed", msg);
+  job_events().inc({{"transition", phase}});
+  log_.info("job finished", Json::object().set("job", m.key()).set("phase", phase).set("reason", reason));
+  cleanup_finished_(obj, m, spec, pods);
+  return Outcome::requeue(opts_.progress_poll, "finished");
+}
+
+Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string& name) {
+  Json obj;
+  try {
+    obj = client_.get(res_, ns, name);  // fresh: the state machine keys off our own status writes
+  } catch (const KubeError& e) {
+    if (e.not_found()) return Outcome::done(ms(0));
+    throw;
+  }
+  ObjectMeta m = ObjectMeta::from(obj);
+  const std::string now = rfc3339_now();
+  auto now_tp = std::chrono::system_clock::now();
+  Json st = obj["status"].is_object() ? obj["status"] : Json::object();
+  const Json& cst = st;  // reads: a non-const operator[] would insert nulls the schema rejects
+  Json conds = cst["conditions"].is_array() ? cst["conditions"] : Json::array();
+  auto errs = validate_job(obj);
+  if (!errs.empty()) {
+    std::string msg;
+    for (const auto& e : errs) msg += (msg.empty() ? "" : "; ") + e;
+    st["phase"] = "Failed";
+    st["observedGeneration"] = m.generation;
+    set_condition(conds, gen::kCondFailed, "True", "InvalidSpec", msg, m.generation, now);
+    st["conditions"] = conds;
+    write_status_(obj, st);
+    return Outcome::terminal("invalid spec: " + msg);
+  }
+  Mi355xJobSpec spec = Mi355xJobSpec::from(obj["spec"]);
+  std::vector<Json> pods = list_pods_(m);
+
+  if (m.deleting()) {  // finalizer: no pod of a deleted job keeps a GPU
+    int left = 0;
+    for (const auto& p : pods) {
+      ++left;
+      if (!p.path("metadata.deletionTimestamp").as_string().empty()) continue;
+      try {
+        client_.del(res::pods(), m.ns, p.path("metadata.name").as_string());
+      } catch (const KubeError& e) {
+        if (!e.not_found()) throw;
+      }
+    }
+    if (left) return Outcome::requeue(opts_.progress_poll, "deleting job pods");
+    if (m.has_finalizer(finalizer_)) remove_finalizer_(obj);
+    return Outcome::done(ms(0));
+  }
+  if (!m.has_finalizer(finalizer_)) {
+    obj = ensure_finalizer_(obj);
+    m = ObjectMeta::from(obj);
+  }
+  st["observedGeneration"] = m.generation;
+  st["replicas"] = spec.replicas;
+  std::string phase = cst["phase"].str_or("Pending");
+
+  // ---- finished: pod cleanup and TTL
+  if (terminal(phase)) {
+    Outcome o = cleanup_finished_(obj, m, spec, pods);
+    if (spec.ttl_seconds_after_finished >= 0) {
+      std::chrono::system_clock::time_point done_at;
+      if (parse_rfc3339(cst["completionTime"].as_string(), &done_at)) {
+        auto expire = done_at + std::chrono::seconds(spec.ttl_seconds_after_finished);
+        if (now_tp >= expire) {
+          client_.del(res_, m.ns, m.name);
+          event_(obj, "Normal", "TTLExpired", "deleted " + std::to_string(spec.ttl_seconds_after_finished) +
+                                                  "s after it finished");
+          return Outcome::requeue(opts_.progress_poll, "ttl delete");
+        }
+        auto left = std::chrono::duration_cast<ms>(expire - now_tp) + ms(5);
+        if (o.kind == Outcome::Done || left < o.after) return Outcome::requeue(left, "ttl");
+      }
+    }
+    return o;
+  }
+
+  // ---- deadline
+  if (spec.active_deadline_seconds > 0) {
+    std::chrono::system_clock::time_point started;
+    if (parse_rfc3339(cst["startTime"].as_string(), &started) &&
+        now_tp - started > std::chrono::seconds(spec.active_deadline_seconds))
+      return finish_(obj, m, spec, st, "Failed", "DeadlineExceeded",
+                     "ran longer than activeDeadlineSeconds=" + std::to_string(spec.active_deadline_seconds), pods);
+  }
+
+  int attempt = static_cast<int>(cst["attempt"].as_int(0));
+  for (const auto& p : pods) attempt = std::max(attempt, label_int(p, gen::kLabelJobAttempt, 0));
+  st["attempt"] = attempt;
+  Json placement = cst["placement"].is_array() ? cst["placement"] : Json::array();
+
+  // ---- needs a (new) gang placement: first run, or a restart whose old pods are gone
+  if (attempt == 0 || phase == "Restarting" || placement.size() == 0) {
+    if (!pods.empty()) {  // previous attempt's pods still hold GPUs: delete and wait
+      for (const auto& p : pods)
+        if (p.path("metadata.deletionTimestamp").as_string().empty()) {
+          try {
+            client_.del(res::pods(), m.ns, p.path("metadata.name").as_string(), terminal(pod_phase(p)) ? 0 : -1);
+          } catch (const KubeError& e) {
+            if (!e.not_found()) throw;
+          }
+        }
+      st["active"] = 0;
+      write_status_(obj, st);
+      return Outcome::requeue(opts_.progress_poll, "waiting for previous pods to terminate");
+    }
+    std::string resource, pool_node, reason, why;
+    if (!resolve_pool_(m, spec, &resource, &pool_node, &why)) {
+      st["phase"] = phase == "Restarting" ? "Restarting" : "Pending";
+      set_condition(conds, gen::kCondScheduled, "False", "PoolNotReady", why, m.generation, now);
+      st["conditions"] = conds;
+      write_status_(obj, st);
+      return Outcome::requeue(opts_.resync, "pool not ready");
+    }
+    std::lock_guard<std::mutex> g(sched_mu_);
+    auto slots = schedule_(m, spec, resource, pool_node, &reason, &why);
+    if (slots.empty()) {
+      st["phase"] = phase == "Restarting" ? "Restarting" : "Pending";
+      const Json& prev = find_condition(conds, gen::kCondScheduled);
+      if (prev["reason"].as_string() != reason) event_(obj, "Warning", reason, why);
+      set_condition(conds, gen::kCondScheduled, "False", reason, why, m.generation, now);
+      st["conditions"] = conds;
+      write_status_(obj, st);
+      return Outcome::requeue(opts_.resync, reason);
+    }
+    // gang wait: from creation, or from the moment the restart began
+    const std::string since_s = attempt > 0 ? find_condition(conds, gen::kCondRestarting)["lastTransitionTime"].as_string()
+                                            : obj.path("metadata.creationTimestamp").as_string();
+    ++attempt;
+    placement = Json::array();
+    std::map<std::string, int> per_node;
+    for (const auto& s : slots) {
+      placement.push_back(Json::object().set("index", s.index).set("node", s.node).set("created", false));
+      per_node[s.node]++;
+    }
+    std::string where;
+    for (const auto& kv : per_node) where += (where.empty() ? "" : ", ") + kv.first + " x" + std::to_string(kv.second);
+    st["attempt"] = attempt;
+    st["placement"] = placement;
+    st["phase"] = "Pending";
+    st["masterAddr"] = "";
+    set_condition(conds, gen::kCondScheduled, "True", "GangScheduled",
+                  std::to_string(spec.replicas) + " pod(s) x " + std::to_string(spec.gpus_per_replica) + " " +
+                      resource + " placed: " + where,
+                  m.generation, now);
+    if (attempt > 1) set_condition(conds, gen::kCondRestarting, "False", "Restarted", "attempt " + std::to_string(attempt),
+                                   m.generation, now);
+    st["conditions"] = conds;
+    // The reservation (status.placement) is written before any pod exists and while sched_mu_ is
+    // held, so the next placement decision sees it.
+    write_status_(obj, st);
+    obj = client_.get(res_, m.ns, m.name);
+    std::chrono::system_clock::time_point since;
+    if (parse_rfc3339(since_s, &since))
+      gang_wait_hist().observe({}, std::chrono::duration<double>(now_tp - since).count());
+    event_(obj, "Normal", "GangScheduled", "attempt " + std::to_string(attempt) + ": " + where);
+    job_events().inc({{"transition", "Scheduled"}});
+    pods.clear();
+  }
+
+  // ---- create pods of this attempt: rank 0 first, the rest once rank 0 has a pod IP
+  std::string resource = spec.resource_name, pool_node, why;
+  if (resource.empty()) resolve_pool_(m, spec, &resource, &pool_node, &why);
+  if (resource.empty()) resource = gen::kDefaultResource;
+  std::map<int, Json> by_index;
+  for (const auto& p : pods)
+    if (label_int(p, gen::kLabelJobAttempt, 0) == attempt) by_index[label_int(p, gen::kLabelJobIndex, -1)] = p;
+  std::string master_ip = by_index.count(0) ? by_index[0].path("status.podIP").as_string() : "";
+  bool created_any = false, lost = false;
+  std::string lost_msg;
+  for (size_t i = 0; i < placement.size(); ++i) {
+    Json& s = placement.at(i);
+    int idx = static_cast<int>(s["index"].as_int(0));
+    if (by_index.count(idx)) {
+      s["created"] = true;
+      continue;
+    }
+    if (s["created"].as_bool(false)) {  // existed in this attempt, now gone (evicted / deleted)
+      lost = true;
+      lost_msg = "pod " + pod_name(m.name, idx) + " disappeared";
+      continue;
+    }
+    if (idx != 0 && master_ip.empty()) continue;
+    Slot slot{idx, s["node"].as_string()};
+    Json pod = build_pod_(obj, m, spec, resource, attempt, slot, idx == 0 ? "localhost" : master_ip);
+    try {
+      by_index[idx] = client_.create(res::pods(), m.ns, pod);
+      s["created"] = true;
+      created_any = true;
+    } catch (const KubeError& e) {
+      if (!e.conflict()) throw;  // 409 AlreadyExists: a pod of an older attempt is still terminating
+      return Outcome::requeue(opts_.progress_poll, "pod name still in use");
+    }
+  }
+  if (created_any) event_(obj, "Normal", "PodsCreated", "attempt " + std::to_string(attempt));
+  st["placement"] = placement;
+  if (!master_ip.empty()) st["masterAddr"] = master_ip;
+
+  // ---- observe pods
+  int active = 0, succeeded = 0, failed = 0, running = 0;
+  std::string fail_msg;
+  Json rs = Json::array();
+  for (const auto& kv : by_index) {
+    const Json& p = kv.second;
+    const std::string ph = pod_phase(p);
+    Json r = Json::object();
+    r["index"] = kv.first;
+    r["pod"] = p.path("metadata.name").as_string();
+    r["node"] = p.path("spec.nodeName").as_string();
+    r["phase"] = ph;
+    if (!p.path("status.podIP").as_string().empty()) r["podIP"] = p.path("status.podIP").as_string();
+    const Json& cs = p.path("status.containerStatuses");
+    if (cs.size() > 0 && cs[0].path("state.terminated").is_object())
+      r["exitCode"] = cs[0].path("state.terminated.exitCode").as_int(0);
+    const std::string devs = p.path("metadata.annotations")[gen::kAnnPodDevices].as_string();
+    if (!devs.empty()) r["devices"] = devs;
+    if (ph == "Failed") {
+      ++failed;
+      std::string why_pod = p.path("status.message").as_string();
+      if (why_pod.empty() && r.contains("exitCode")) why_pod = "exit code " + std::to_string(r["exitCode"].as_int());
+      r["message"] = why_pod;
+      if (fail_msg.empty()) fail_msg = "pod " + r["pod"].as_string() + " failed: " + why_pod;
+    } else if (ph == "Succeeded") {
+      ++succeeded;
+    } else if (p.path("metadata.deletionTimestamp").as_string().empty()) {
+      ++active;
+      if (ph == "Running") ++running;
+    }
+    rs.push_back(r);
+  }
+  st["replicaStatuses"] = rs;
+  st["active"] = active;
+  st["succeeded"] = succeeded;
+  st["failed"] = failed;
+  st["restarts"] = std::max(0, attempt - 1);
+
+  // ---- transitions
+  if (failed > 0 || lost) {
+    const std::string msg = !fail_msg.empty() ? fail_msg : lost_msg;
+    if (spec.restart_policy == "OnFailure" && attempt - 1 < spec.backoff_limit) {
+      for (const auto& kv : by_index)  // the whole gang restarts
+        if (kv.second.path("metadata.deletionTimestamp").as_string().empty()) {
+          try {
+            client_.del(res::pods(), m.ns, kv.second.path("metadata.name").as_string(),
+                        terminal(pod_phase(kv.second)) ? 0 : -1);
+          } catch (const KubeError& e) {
+            if (!e.not_found()) throw;
+          }
+        }
+      st["phase"] = "Restarting";
+      st["placement"] = Json::array();
+      st["active"] = 0;
+      set_condition(conds, gen::kCondRestarting, "True", lost ? "PodLost" : "PodFailed",
+                    msg + "; restarting the gang (restart " + std::to_string(attempt) + "/" +
+                        std::to_string(spec.backoff_limit) + ")",
+                    m.generation, now);
+      set_condition(conds, gen::kCondRunning, "False", "Restarting", msg, m.generation, now);
+      st["conditions"] = conds;
+      write_status_(obj, st);
+      event_(obj, "Warning", "GangRestarting", msg);
+      job_events().inc({{"transition", "Restarting"}});
+      return Outcome::requeue(opts_.progress_poll, "gang restart");
+    }
+    st["conditions"] = conds;
+    return finish_(obj, m, spec, st, "Failed",
+                   spec.restart_policy == "Never" ? "PodFailed" : "BackoffLimitExceeded", msg, pods);
+  }
+  const bool all_done = succeeded == spec.replicas;
+  const bool rank0_done = by_index.count(0) && pod_phase(by_index[0]) == "Succeeded";
+  if (all_done || (spec.success_policy == "Rank0" && rank0_done)) {
+    st["conditions"] = conds;
+    return finish_(obj, m, spec, st, "Succeeded", "JobSucceeded",
+                   std::to_string(succeeded) + "/" + std::to_string(spec.replicas) + " worker(s) succeeded", pods);
+  }
+  if (static_cast<int>(by_index.size()) == spec.replicas && running + succeeded == spec.replicas) {
+    if (phase != "Running") {
+      event_(obj, "Normal", "JobRunning", std::to_string(running) + " worker(s) running");
+      job_events().inc({{"transition", "Running"}});
+    }
+    st["phase"] = "Running";
+    if (cst["startTime"].as_string().empty()) st["startTime"] = now;
+    set_condition(conds, gen::kCondRunning, "True", "AllWorkersRunning",
+                  std::to_string(running) + "/" + std::to_string(spec.replicas) + " worker(s) running", m.generation,
+                  now);
+    st["conditions"] = conds;
+    write_status_(obj, st);
+    return Outcome::done(opts_.resync);
+  }
+  st["phase"] = phase == "Running" ? "Running" : "Pending";
+  st["conditions"] = conds;
+  write_status_(obj, st);
+  return Outcome::requeue(opts_.progress_poll, "starting workers");
+}
+
+}  // namespace gpupool

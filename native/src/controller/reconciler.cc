@@ -62,7 +62,7 @@ GaugeVec& desired_gauge() {
 PoolReconcilerBase::PoolReconcilerBase(KubeClient& client, Informer& pools, EventRecorder* events,
                                        ReconcilerOptions opts, std::string kind, ResourceRef res)
     : client_(client), pools_(pools), events_(events), opts_(opts), kind_(std::move(kind)), res_(std::move(res)),
-      log_(Logger("reconciler").with("kind", kind_)) {}
+      finalizer_(gen::kFinalizer), log_(Logger("reconciler").with("kind", kind_)) {}
 
 void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
   trace::Span span("status");
@@ -87,11 +87,11 @@ void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
 
 Json PoolReconcilerBase::ensure_finalizer_(const Json& obj) {
   ObjectMeta m = ObjectMeta::from(obj);
-  if (m.has_finalizer(gen::kFinalizer)) return obj;
+  if (m.has_finalizer(finalizer_)) return obj;
   trace::Span span("finalizer");
   Json fins = Json::array();
   for (const auto& f : m.finalizers) fins.push_back(f);
-  fins.push_back(gen::kFinalizer);
+  fins.push_back(finalizer_);
   Json patch = Json::object();
   patch["metadata"]["finalizers"] = fins;
   patch["metadata"]["resourceVersion"] = m.resource_version;  // optimistic concurrency
@@ -102,7 +102,7 @@ Json PoolReconcilerBase::remove_finalizer_(const Json& obj) {
   ObjectMeta m = ObjectMeta::from(obj);
   Json fins = Json::array();
   for (const auto& f : m.finalizers)
-    if (f != gen::kFinalizer) fins.push_back(f);
+    if (f != finalizer_) fins.push_back(f);
   Json patch = Json::object();
   patch["metadata"]["finalizers"] = fins;
   patch["metadata"]["resourceVersion"] = m.resource_version;

@@ -46,7 +46,7 @@ struct Flags {
   std::string token;
   std::string ns;
   int workers = 4;
-  std::string kinds = "mi355x,azure";
+  std::string kinds = "mi355x,azure,job";
   bool leader_elect = false;
   std::string lease_ns = "gpupool-system";
   std::string identity;
@@ -95,7 +95,7 @@ in-cluster ServiceAccount, ~/.kube/config, http://127.0.0.1:6443:
   --client-cert F --client-key F   client certificate authentication
   --insecure-skip-tls-verify   do not verify the apiserver certificate (testing only)
 controllers:
-  --kinds mi355x,azure         reconcilers to run            --namespace NS   watch one namespace
+  --kinds mi355x,azure,job     reconcilers to run            --namespace NS   watch one namespace
   --workers N (4)              reconcile worker threads      --resync D (10s) steady-state resync
   --progress-poll D (250ms)    requeue while scaling/draining
   --credentials-retry D (30s)  AzureVmPool retry after a credentials error
@@ -195,6 +195,7 @@ int run_validate(const std::string& path) {
   std::vector<std::string> errs;
   std::string kind = obj["kind"].as_string();
   if (kind == "Mi355xPool") errs = validate_mi355x(obj);
+  else if (kind == "Mi355xJob") errs = validate_job(obj);
   else if (kind == "AzureVmPool") errs = validate_azure(obj);
   else errs.push_back("kind: unsupported " + kind);
   Json out = Json::object();
@@ -320,6 +321,7 @@ int main(int argc, char** argv) {
   Logger log("manager");
   bool want_mi = f.kinds.find("mi355x") != std::string::npos;
   bool want_az = f.kinds.find("azure") != std::string::npos;
+  bool want_job = f.kinds.find("job") != std::string::npos;
 
   TlsOptions tls;
   tls.ca_file = f.ca_file;
@@ -451,7 +453,11 @@ int main(int argc, char** argv) {
     fco.state_file = f.fakecloud_state;
     fco.faults_file = f.fakecloud_faults;
     FakeCloudProvider cloud(fco);
+    Informer jobs(client, ResourceRef{gen::kGroup, gen::kVersion, gen::kPluralMi355xJob, true, "Mi355xJob"}, f.ns,
+                  std::chrono::milliseconds(f.resync_ms));
+    Informer pods(client, res::pods(), "", std::chrono::milliseconds(f.resync_ms));
     Mi355xPoolReconciler mi(client, mipools, rocm, &events, ropts);
+    Mi355xJobReconciler jr(client, jobs, nodes, &events, ropts);
     AzureVmPoolReconciler az(client, azpools, cloud, &events, ropts);
     AgentWatchers watchers(rocm, mipools, ctl);
 
@@ -487,6 +493,34 @@ int main(int argc, char** argv) {
       mipools.start();
       quotas.start();
     }
+    if (want_job) {
+      ctl.add_reconciler(&jr);
+      jobs.add_handler(pool_handler("Mi355xJob"));
+      auto wake_pending = [&]() {
+        for (const auto& j : jr.pending()) ctl.enqueue("Mi355xJob", j.first, j.second);
+      };
+      // job pods drive their job; a pod that ends or goes away frees capacity for waiting gangs
+      pods.add_handler([&, wake_pending](const std::string& type, const Json& p) {
+        if (type == "RESYNC") return;
+        const std::string job = p.path("metadata.labels")[gen::kLabelJob].as_string();
+        if (!job.empty()) ctl.enqueue("Mi355xJob", p.path("metadata.namespace").as_string(), job);
+        const std::string phase = p.path("status.phase").as_string();
+        if (type == "DELETED" || phase == "Succeeded" || phase == "Failed") wake_pending();
+      });
+      nodes.add_handler([wake_pending](const std::string& type, const Json&) {
+        if (type != "RESYNC") wake_pending();
+      });
+      // pool changes (GPUs advertised or released) change capacity too
+      mipools.add_handler([wake_pending](const std::string& type, const Json&) {
+        if (type != "RESYNC") wake_pending();
+      });
+      if (!want_mi) {
+        nodes.start();
+        mipools.start();
+      }
+      jobs.start();
+      pods.start();
+    }
     if (want_az) {
       ctl.add_reconciler(&az);
       azpools.add_handler(pool_handler("AzureVmPool"));
@@ -508,6 +542,10 @@ int main(int argc, char** argv) {
       wait_cache(mipools, "mi355xpools");
     }
     if (want_az) wait_cache(azpools, "azurevmpools");
+    if (want_job) {
+      wait_cache(jobs, "mi355xjobs");
+      wait_cache(pods, "pods");
+    }
     if (!g_stop) {
       if (want_mi) watchers.sync(rocm.node_names());
       ctl.start();
@@ -530,6 +568,8 @@ int main(int argc, char** argv) {
     log.info("stopping controllers", Json());
     ctl.stop();
     watchers.stop_all();
+    jobs.stop();
+    pods.stop();
     mipools.stop();
     azpools.stop();
     quotas.stop();

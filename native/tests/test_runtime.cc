@@ -17,6 +17,7 @@
 #include "gpupool/kube.h"
 #include "gpupool/log.h"
 #include "gpupool/metrics.h"
+#include "gpupool/reconciler.h"
 #include "gpupool/trace.h"
 #include "gpupool/workqueue.h"
 #include "gpupool/yaml.h"
@@ -438,4 +439,36 @@ TEST(rfc3339_roundtrip) {
   EXPECT_TRUE(std::chrono::abs(std::chrono::duration_cast<std::chrono::seconds>(t - now)).count() <= 1);
   EXPECT_TRUE(parse_rfc3339(microtime_now(), &t));
   EXPECT_TRUE(!parse_rfc3339("garbage", &t));
+}
+
+// ---------------------------------------------------------------- Mi355xJob gang placement
+TEST(job_gang_placement) {
+  using gpupool::Mi355xJobReconciler;
+  using F = std::vector<std::pair<std::string, int64_t>>;
+  // whole gang fits one node: the tightest such node (keeps the roomy node for bigger gangs)
+  auto s = Mi355xJobReconciler::place(F{{"a", 8}, {"b", 4}, {"c", 2}}, 2, 2);
+  EXPECT_EQ(s.size(), 2u);
+  EXPECT_TRUE(s[0].node == "b" && s[1].node == "b" && s[0].index == 0 && s[1].index == 1);
+  // spans nodes: fewest nodes, roomiest first, rank 0 on the first
+  s = Mi355xJobReconciler::place(F{{"a", 2}, {"b", 5}, {"c", 3}}, 4, 2);
+  EXPECT_EQ(s.size(), 4u);
+  EXPECT_TRUE(s[0].node == "b" && s[1].node == "b" && s[2].node == "c" && s[3].node == "a");
+  // all-or-nothing: 3 x 2 GPUs do not fit 5 free GPUs split 3+1+1
+  EXPECT_TRUE(Mi355xJobReconciler::place(F{{"a", 3}, {"b", 1}, {"c", 1}}, 3, 2).empty());
+  EXPECT_TRUE(Mi355xJobReconciler::place(F{}, 1, 1).empty());
+  // CPU-only workers go together on the first candidate
+  s = Mi355xJobReconciler::place(F{{"x", 0}, {"y", 0}}, 3, 0);
+  EXPECT_TRUE(s.size() == 3 && s[2].node == "x");
+}
+
+TEST(job_validation) {
+  using gpupool::Json;
+  Json ok = Json::parse(R"({"spec":{"replicas":2,"template":{"spec":{}}}})");
+  EXPECT_TRUE(gpupool::validate_job(ok).empty());
+  Json bad = Json::parse(
+      R"({"spec":{"replicas":0,"gpusPerReplica":-1,"restartPolicy":"Always","masterPort":70000}})");
+  auto errs = gpupool::validate_job(bad);
+  EXPECT_EQ(errs.size(), 5u);  // replicas, gpusPerReplica, masterPort, restartPolicy, template
+  auto spec = gpupool::Mi355xJobSpec::from(ok["spec"]);
+  EXPECT_TRUE(spec.gpus_per_replica == 1 && spec.restart_policy == "OnFailure" && spec.master_port == 29500);
 }

@@ -1,0 +1,224 @@
+"""Mi355xJob end-to-end on the fake 8x MI355X node: gang placement over pool-advertised GPUs,
+torchrun/PET rendezvous env, gang restarts, queue order, deadline/TTL/cleanup, and the GoHai-style
+``gpuctl trainjob`` verbs (reference GPU调度平台搭建.md:503-550 CLI, :638-675 Volcano Job,
+:300-306 + :623 Kubeflow PET env)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+import yaml
+
+from gpupool.kube import EVENTS, MI355XJOBS, MI355XPOOLS, PODS, KubeError
+
+from .helpers import conds, mi_pool, wait_ready
+
+pytestmark = pytest.mark.slow
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+_port = [29600]
+
+
+def job(name: str, replicas: int, command: list[str], gpus: int = 1, **spec) -> dict:
+    _port[0] += 1
+    return {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xJob",
+            "metadata": {"name": name},
+            "spec": {"replicas": replicas, "gpusPerReplica": gpus, "masterPort": _port[0],
+                     "template": {"spec": {"terminationGracePeriodSeconds": 1,
+                                           "containers": [{"name": "main", "command": command}]}},
+                     **spec}}
+
+
+def phase_is(*phases):
+    return lambda o: bool(o) and (o.get("status") or {}).get("phase") in phases
+
+
+def job_pods(k, name, ns="default"):
+    return k.list(PODS, ns, label_selector=f"gpupool.amd.com/job-name={name}")["items"]
+
+
+def env_of(pod) -> dict:
+    return {e["name"]: e.get("value") for e in pod["spec"]["containers"][0].get("env", [])}
+
+
+@pytest.fixture
+def node8(cluster_factory):
+    return cluster_factory()
+
+
+def test_ddp_job_gang_runs_to_success(node8, tmp_path):
+    """Two workers x 1 GPU of a pool run real DDP (gloo on CPU here) through the job's env."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 2), "default")
+    wait_ready(k, "pool", 2)
+    cmd = [sys.executable, os.path.join(ROOT, "examples", "fmnist_train.py"), "--synthetic",
+           "--cpu", "--samples", "256", "--batch_size", "32", "--steps", "3", "--epochs", "1",
+           "--output", str(tmp_path / "out")]
+    k.create(MI355XJOBS, job("ddp", 2, cmd, poolRef="pool"), "default")
+    o = k.wait_for(MI355XJOBS, "ddp", "default", phase_is("Succeeded", "Failed"), timeout=120)
+    assert o["status"]["phase"] == "Succeeded", o["status"]
+    st = o["status"]
+    assert st["succeeded"] == 2 and st["restarts"] == 0 and st["attempt"] == 1
+    c = conds(o)
+    assert c["Scheduled"]["status"] == "True" and c["Succeeded"]["status"] == "True"
+    devs = [r["devices"] for r in st["replicaStatuses"]]
+    assert len(devs) == 2 and len(set(devs)) == 2  # distinct pool GPUs
+    # completed pods are kept (cleanPodPolicy Running); rank 1 rendezvoused at rank 0's pod IP
+    pods = {p["metadata"]["labels"]["gpupool.amd.com/replica-index"]: p for p in job_pods(k, "ddp")}
+    e0, e1 = env_of(pods["0"]), env_of(pods["1"])
+    assert e0["RANK"] == "0" and e1["RANK"] == "1" and e1["WORLD_SIZE"] == "2"
+    assert e1["MASTER_ADDR"] == "127.0.0.1" and e0["PET_NNODES"] == "2"
+    assert pods["1"]["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "1"
+    log = open(pods["0"]["metadata"]["annotations"]["gpupool.amd.com/log-path"]).read()
+    assert '"world": 2' in log or "'world': 2" in log, log[-2000:]
+    reasons = [e["reason"] for e in k.list(EVENTS, "default")["items"]]
+    assert "GangScheduled" in reasons and "JobSucceeded" in reasons
+
+
+def test_gang_is_all_or_nothing_and_queue_is_ordered(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 3), "default")
+    wait_ready(k, "pool", 3)
+    # can never fit (4 > 3 GPUs in the cluster): stays Unschedulable, creates nothing, blocks nobody
+    k.create(MI355XJOBS, job("huge", 4, ["sleep", "30"]), "default")
+    o = k.wait_for(MI355XJOBS, "huge", "default",
+                   lambda o: conds(o).get("Scheduled", {}).get("reason") == "Unschedulable", timeout=20)
+    assert o["status"]["phase"] == "Pending" and not job_pods(k, "huge")
+    k.create(MI355XJOBS, job("a", 2, ["sleep", "2"]), "default")
+    k.wait_for(MI355XJOBS, "a", "default", phase_is("Running"), timeout=30)
+    # b needs 2 (1 free): waits; c needs 1 and would fit, but is queued behind b
+    k.create(MI355XJOBS, job("b", 2, ["sleep", "1"]), "default")
+    time.sleep(0.05)
+    k.create(MI355XJOBS, job("c", 1, ["sleep", "1"]), "default")
+    k.wait_for(MI355XJOBS, "c", "default",
+               lambda o: conds(o).get("Scheduled", {}).get("reason") == "QueuedBehind", timeout=20)
+    assert not job_pods(k, "c") and not job_pods(k, "b")
+    for n in ("a", "b", "c"):
+        o = k.wait_for(MI355XJOBS, n, "default", phase_is("Succeeded", "Failed"), timeout=60)
+        assert o["status"]["phase"] == "Succeeded", (n, o["status"])
+    start = {n: k.get(MI355XJOBS, n, "default")["status"]["startTime"] for n in ("a", "b", "c")}
+    assert start["a"] <= start["b"] <= start["c"]
+    # a higher priority jumps the queue
+    k.create(MI355XJOBS, job("hold", 3, ["sleep", "2"]), "default")
+    k.wait_for(MI355XJOBS, "hold", "default", phase_is("Running"), timeout=30)
+    k.create(MI355XJOBS, job("low", 1, ["sleep", "1"]), "default")
+    time.sleep(0.05)
+    k.create(MI355XJOBS, job("high", 3, ["sleep", "1"], priority=10), "default")
+    k.wait_for(MI355XJOBS, "low", "default",
+               lambda o: "high" in conds(o).get("Scheduled", {}).get("message", ""), timeout=20)
+    for n in ("hold", "high", "low"):
+        k.wait_for(MI355XJOBS, n, "default", phase_is("Succeeded"), timeout=60)
+    assert k.get(MI355XJOBS, "high", "default")["status"]["startTime"] <= \
+        k.get(MI355XJOBS, "low", "default")["status"]["startTime"]
+    assert k.get(MI355XJOBS, "huge", "default")["status"]["phase"] == "Pending"
+
+
+def test_gang_restart_then_backoff_limit(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 2), "default")
+    wait_ready(k, "pool", 2)
+    # rank 1 fails on the first attempt only -> the whole gang restarts once, then succeeds
+    flaky = ["bash", "-c", 'if [ "$GPUPOOL_JOB_ATTEMPT" = 1 ] && [ "$RANK" = 1 ]; then exit 3; fi; sleep 0.5']
+    k.create(MI355XJOBS, job("flaky", 2, flaky), "default")
+    o = k.wait_for(MI355XJOBS, "flaky", "default", phase_is("Succeeded", "Failed"), timeout=60)
+    assert o["status"]["phase"] == "Succeeded" and o["status"]["restarts"] == 1, o["status"]
+    reasons = [e["reason"] for e in k.list(EVENTS, "default")["items"]
+               if e["involvedObject"]["name"] == "flaky"]
+    assert "GangRestarting" in reasons
+    # always failing with backoffLimit 1: two attempts, then Failed/BackoffLimitExceeded
+    k.create(MI355XJOBS, job("bad", 2, ["bash", "-c", "exit 7"], backoffLimit=1), "default")
+    o = k.wait_for(MI355XJOBS, "bad", "default", phase_is("Succeeded", "Failed"), timeout=60)
+    c = conds(o)
+    assert o["status"]["phase"] == "Failed" and c["Failed"]["reason"] == "BackoffLimitExceeded"
+    assert o["status"]["attempt"] == 2 and "exit code 7" in c["Failed"]["message"]
+    # restartPolicy Never: the first failure is final
+    k.create(MI355XJOBS, job("never", 1, ["false"], restartPolicy="Never"), "default")
+    o = k.wait_for(MI355XJOBS, "never", "default", phase_is("Failed"), timeout=30)
+    assert conds(o)["Failed"]["reason"] == "PodFailed" and o["status"]["attempt"] == 1
+
+
+def test_deadline_ttl_and_delete_cleanup(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 2), "default")
+    wait_ready(k, "pool", 2)
+    k.create(MI355XJOBS, job("slow", 2, ["sleep", "60"], activeDeadlineSeconds=1), "default")
+    o = k.wait_for(MI355XJOBS, "slow", "default", phase_is("Failed"), timeout=30)
+    assert conds(o)["Failed"]["reason"] == "DeadlineExceeded"
+    k.wait_for(PODS, "slow-worker-0", "default", lambda p: p is None, timeout=30)  # cleanPodPolicy
+    # ttlSecondsAfterFinished: the job object goes away after it finished
+    k.create(MI355XJOBS, job("ttl", 1, ["true"], ttlSecondsAfterFinished=0), "default")
+    k.wait_for(MI355XJOBS, "ttl", "default", lambda o: o is None, timeout=30)
+    # deleting a running job deletes its pods first (finalizer), freeing the GPUs
+    k.create(MI355XJOBS, job("run", 2, ["sleep", "600"]), "default")
+    k.wait_for(MI355XJOBS, "run", "default", phase_is("Running"), timeout=30)
+    k.delete(MI355XJOBS, "run", "default")
+    k.wait_for(MI355XJOBS, "run", "default", lambda o: o is None, timeout=30)
+    assert not job_pods(k, "run")
+    k.create(MI355XJOBS, job("after", 2, ["true"]), "default")  # both GPUs are free again
+    k.wait_for(MI355XJOBS, "after", "default", phase_is("Succeeded"), timeout=30)
+
+
+def test_pool_scale_down_evicts_worker_and_gang_waits(node8):
+    """Elastic interplay: scaling the pool down drains a GPU under a running gang; the lost pod
+    restarts the gang, which then waits (Unschedulable) until the pool grows back."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 2, drain={"gracePeriodSeconds": 1}), "default")
+    wait_ready(k, "pool", 2)
+    k.create(MI355XJOBS, job("train", 2, ["sleep", "600"], poolRef="pool"), "default")
+    k.wait_for(MI355XJOBS, "train", "default", phase_is("Running"), timeout=30)
+    k.patch(MI355XPOOLS, "pool", {"spec": {"replicas": 1}}, "default")
+    o = k.wait_for(MI355XJOBS, "train", "default",
+                   lambda o: conds(o).get("Scheduled", {}).get("reason") == "Unschedulable"
+                   and o["status"].get("restarts", 0) >= 0 and o["status"]["phase"] == "Restarting",
+                   timeout=60)
+    assert conds(o)["Restarting"]["status"] == "True"
+    wait_ready(k, "pool", 1)
+    k.patch(MI355XPOOLS, "pool", {"spec": {"replicas": 2}}, "default")
+    o = k.wait_for(MI355XJOBS, "train", "default", phase_is("Running"), timeout=60)
+    assert o["status"]["attempt"] == 2 and o["status"]["restarts"] == 1
+
+
+def test_invalid_job_is_rejected(node8):
+    k = node8.client
+    with pytest.raises(KubeError):
+        k.create(MI355XJOBS, job("zero", 0, ["true"]), "default")
+    with pytest.raises(KubeError):
+        k.create(MI355XJOBS, job("pol", 1, ["true"], restartPolicy="Always"), "default")
+
+
+def test_gpuctl_trainjob_verbs(node8, tmp_path):
+    """GoHai CLI flow (GPU调度平台搭建.md:503-550): template -> create --dry-run -> create ->
+    list -> logs -> template -s (export) -> create --bare -> delete."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 1), "default")
+    wait_ready(k, "pool", 1)
+
+    def gpuctl(*args, check=True):
+        r = subprocess.run([os.path.join(ROOT, "bin", "gpuctl"), "--server",
+                            node8.url, *args], capture_output=True, text=True, timeout=60)
+        if check:
+            assert r.returncode == 0, r.stderr
+        return r.stdout
+    tpl = yaml.safe_load(gpuctl("trainjob", "template"))
+    assert tpl["mode"] == "single" and tpl["spec"]["singleInstanceType"].endswith("1gpu")
+    tpl.update({"title": "CLI Demo_1", "command": "echo hello-from-$RANK", "mode": "Single"})
+    f = tmp_path / "train_job_template.yaml"
+    f.write_text(yaml.safe_dump(tpl))
+    dry = yaml.safe_load(gpuctl("trainjob", "create", "-f", str(f), "--dry-run"))
+    assert dry["kind"] == "Mi355xJob" and dry["metadata"]["name"] == "cli-demo-1"
+    assert dry["spec"]["replicas"] == 1 and dry["spec"]["gpusPerReplica"] == 1
+    assert "created" in gpuctl("trainjob", "create", "-f", str(f))
+    k.wait_for(MI355XJOBS, "cli-demo-1", "default", phase_is("Succeeded"), timeout=30)
+    assert "cli-demo-1" in gpuctl("trainjob", "list") and "Succeeded" in gpuctl("trainjob", "list")
+    assert "hello-from-0" in gpuctl("trainjob", "logs", "cli-demo-1")
+    exported = yaml.safe_load(gpuctl("trainjob", "template", "-s", "cli-demo-1"))
+    assert exported["command"] == "echo hello-from-$RANK" and exported["title"] == "CLI Demo_1"
+    bare = tmp_path / "job_full.yaml"
+    bare.write_text(yaml.safe_dump(job("bare", 1, ["true"])))
+    assert "created" in gpuctl("trainjob", "create", "-f", str(bare), "--bare")
+    k.wait_for(MI355XJOBS, "bare", "default", phase_is("Succeeded"), timeout=30)
+    gpuctl("trainjob", "delete", "bare")
+    k.wait_for(MI355XJOBS, "bare", "default", lambda o: o is None, timeout=30)

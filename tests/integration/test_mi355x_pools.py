@@ -94,8 +94,11 @@ def test_config5_two_pools_with_health_conditions(node8):
     ua = {d["uuid"] for d in a["status"]["devices"]}
     ub = {d["uuid"] for d in b["status"]["devices"]}
     assert not ua & ub  # no cross-pool claims
-    alloc = k.get(NODES, "mi355x-node-0")["status"]["allocatable"]
-    assert alloc["amd.com/gpu-team-a"] == "4" and alloc["amd.com/gpu-team-b"] == "4"
+    # the kubelet publishes node allocatable asynchronously after ListAndWatch (as a real kubelet's
+    # node-status sync does), so wait for it rather than racing it under load
+    k.wait_for(NODES, "mi355x-node-0", None, lambda n: (
+        (n["status"].get("allocatable") or {}).get("amd.com/gpu-team-a") == "4"
+        and n["status"]["allocatable"].get("amd.com/gpu-team-b") == "4"), timeout=20)
     victim = sorted(a["status"]["devices"], key=lambda d: d["index"])[0]["uuid"]
     # xGMI link down on one team-a GPU
     node8.set_faults("mi355x-node-0", {"devices": {victim: {"xgmi": {

@@ -76,7 +76,7 @@ def test_release_refuses_gpu_with_pods(tmp_path, sockdir, native_built, monkeypa
     a = make_agent(tmp_path, sockdir, plugin=False)
     r = claim(a, count=1)
     u = r["devices"][0]["uuid"]
-    monkeypatch.setattr(a, "_pods_by_device", lambda: {u: [{"namespace": "d", "name": "p"}]})
+    monkeypatch.setattr(a, "_pods_by_device", lambda **_: {u: [{"namespace": "d", "name": "p"}]})
     out = a.release("pool-1", [u])
     assert not out["ok"] and out["reason"] == "PodsRunning"
     assert u in a.records

@@ -70,6 +70,19 @@ CASES = [
                                      "imageReference": {"publisher": "p", "offer": "o", "sku": "s",
                                                         "version": "v"}}},
     {"kind": "AzureVmPool", "spec": {"replicas": 1, "resourceGroupName": "rg"}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 2, "template": {"spec": {}}}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 4, "gpusPerReplica": 8, "poolRef": "p",
+                                   "restartPolicy": "Never", "cleanPodPolicy": "All",
+                                   "successPolicy": "Rank0", "ttlSecondsAfterFinished": 0,
+                                   "template": {"spec": {"containers": [{"name": "m"}]}}}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 0, "template": {}}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 1}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 1, "gpusPerReplica": 65, "template": {}}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 1, "restartPolicy": "Always", "template": {}}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 1, "masterPort": 0, "template": {}}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 1, "ttlSecondsAfterFinished": -2, "template": {}}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 1, "resourceName": "Bad", "template": {}}},
+    {"kind": "Mi355xJob", "spec": {"replicas": 1, "cleanPodPolicy": "Some", "template": {}}},
 ]
 
 
@@ -83,7 +96,8 @@ def test_validation_parity_cpp_vs_crd(case, tmp_path, native_built):
     crd_rt = store.types[("apiextensions.k8s.io", "customresourcedefinitions")]
     for p in glob.glob(os.path.join(ROOT, "config", "crd", "*.yaml")):
         store.create(crd_rt, None, yaml.safe_load(open(p)))
-    plural = {"Mi355xPool": "mi355xpools", "AzureVmPool": "azurevmpools"}[case["kind"]]
+    plural = {"Mi355xPool": "mi355xpools", "AzureVmPool": "azurevmpools",
+              "Mi355xJob": "mi355xjobs"}[case["kind"]]
     obj = {"apiVersion": "compute.my.domain/v1alpha1", "kind": case["kind"],
            "metadata": {"name": "x"}, "spec": case["spec"]}
     try:
