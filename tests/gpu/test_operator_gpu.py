@@ -123,3 +123,41 @@ def test_performance_floor_on_real_gpu(cluster_factory):
     msg = next(x["message"] for x in o["status"]["conditions"] if x["type"] == "DeviceProbePassed")
     assert "PerformanceBelowFloor" in msg and "TFLOP/s" in msg
     assert o["status"].get("readyReplicas", 0) == 0
+
+
+def test_mi355xjob_torchrun_worker_on_pool_gpu(cluster_factory, tmp_path):
+    """Mi355xJob on real hardware: the gang is placed on the pool's GPU, the pod gets the job's
+    rendezvous env, and torchrun (driven by PET_*/MASTER_*) starts a distributed-mode worker on
+    exactly the allotted GPU (GPU调度平台搭建.md:300-306, :623-635, :638-675). One GPU per box here,
+    so world size is 1; multi-rank rendezvous is covered by the CPU job tests."""
+    from gpupool.kube import MI355XJOBS
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    k = c.client
+    k.create(MI355XPOOLS, pool("p", 1), "default")
+    obj = k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=60)
+    hip_uuid = obj["status"]["devices"][0]["hipUUID"]
+    script = ("exec python -m torch.distributed.run --nnodes $PET_NNODES "
+              "--nproc-per-node $PET_NPROC_PER_NODE --node-rank $PET_NODE_RANK "
+              "--master-addr $MASTER_ADDR --master-port $MASTER_PORT "
+              f"examples/fmnist_train.py --mode distributed --synthetic --epochs 1 --steps 40 "
+              f"--output {tmp_path}")
+    k.create(MI355XJOBS, {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xJob",
+                          "metadata": {"name": "ddp"},
+                          "spec": {"replicas": 1, "gpusPerReplica": 1, "poolRef": "p",
+                                   "masterPort": 29731, "backoffLimit": 0,
+                                   "template": {"spec": {"containers": [{
+                                       "name": "main", "command": ["bash", "-c", script]}]}}}},
+             "default")
+    done = k.wait_for(MI355XJOBS, "ddp", "default",
+                      lambda o: ((o or {}).get("status") or {}).get("phase") in ("Succeeded", "Failed"),
+                      timeout=240)
+    pod = k.list(PODS, "default", label_selector="gpupool.amd.com/job-name=ddp")["items"][0]
+    log = open(pod["metadata"]["annotations"]["gpupool.amd.com/log-path"]).read()
+    assert done["status"]["phase"] == "Succeeded", (done["status"], log[-3000:])
+    events = [json.loads(x) for x in log.splitlines() if x.startswith("{")]
+    start = next(e for e in events if e["event"] == "start")
+    assert start["mode"] == "distributed" and start["world"] == 1
+    assert start["device"] == "cuda:0" and start["arch"].startswith("gfx950")
+    assert start["rocr_visible"] == hip_uuid
+    assert done["status"]["replicaStatuses"][0]["devices"]
+    assert os.path.exists(tmp_path / "fashion_mnist_cnn.pth")
