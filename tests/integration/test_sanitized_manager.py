@@ -8,7 +8,7 @@ import subprocess
 
 import pytest
 
-from gpupool.kube import MI355XPOOLS, PODS
+from gpupool.kube import MI355XJOBS, MI355XPOOLS, PODS
 
 from .helpers import mi_pool, pause_pod, wait_ready
 
@@ -36,6 +36,20 @@ def test_manager_scenario_under_sanitizer(san, cluster_factory):
     k.patch(MI355XPOOLS, "a", {"spec": {"replicas": 1}}, "default")
     wait_ready(k, "a", 1, timeout=60)
     c.set_faults("mi355x-node-0", {})
+    # Mi355xJob gang on pool b's GPUs: placement under the scheduling mutex, pod-informer driven
+    # status, one gang restart (the first attempt fails), then success and TTL deletion
+    k.create(MI355XJOBS, {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xJob",
+                          "metadata": {"name": "j"},
+                          "spec": {"replicas": 2, "poolRef": "b", "backoffLimit": 2,
+                                   "ttlSecondsAfterFinished": 1, "template": {"spec": {
+                                       "terminationGracePeriodSeconds": 1, "containers": [{
+                                           "name": "m", "command": ["bash", "-c",
+                                                                    '[ "$GPUPOOL_JOB_ATTEMPT" != 1 ]'
+                                                                    ]}]}}}}, "default")
+    o = k.wait_for(MI355XJOBS, "j", "default", lambda o: o and (o.get("status") or {}).get(
+        "phase") in ("Succeeded", "Failed"), timeout=60)
+    assert o["status"]["phase"] == "Succeeded" and o["status"]["restarts"] == 1, o["status"]
+    k.wait_for(MI355XJOBS, "j", "default", lambda o: o is None, timeout=60)
     for name in ("a", "b"):
         k.delete(MI355XPOOLS, name, "default")
     for name in ("a", "b"):
