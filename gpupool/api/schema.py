@@ -41,6 +41,9 @@ JOB_FINALIZER = "compute.my.domain/job-cleanup"
 LABEL_JOB = "gpupool.amd.com/job-name"
 LABEL_JOB_INDEX = "gpupool.amd.com/replica-index"
 LABEL_JOB_ATTEMPT = "gpupool.amd.com/attempt"
+# Set on a running Mi355xJob by a higher-priority job that needs its GPUs ("<ns>/<name>/<uid>");
+# the victim's own reconciler then stops its gang (single status writer per job).
+ANN_JOB_PREEMPTED_BY = "gpupool.amd.com/preempted-by"
 
 # Condition types (metav1.Condition, README.md:126-127; roadmap README.md:310).
 COND_READY = "Ready"
@@ -64,7 +67,9 @@ COND_RUNNING = "Running"
 COND_RESTARTING = "Restarting"
 COND_SUCCEEDED = "Succeeded"
 COND_FAILED = "Failed"
-JOB_CONDITIONS = [COND_SCHEDULED, COND_RUNNING, COND_RESTARTING, COND_SUCCEEDED, COND_FAILED]
+COND_SUSPENDED = "Suspended"
+JOB_CONDITIONS = [COND_SCHEDULED, COND_RUNNING, COND_RESTARTING, COND_SUCCEEDED, COND_FAILED,
+                  COND_SUSPENDED]
 
 AZURE_CREDENTIAL_KEYS = ["AZURE_CLIENT_ID", "AZURE_CLIENT_SECRET", "AZURE_TENANT_ID",
                          "AZURE_SUBSCRIPTION_ID"]  # README.md:108
@@ -289,6 +294,15 @@ MI355X_JOB_SPEC = {
                   "description": "Jobs of one queue are placed strictly in (priority desc, "
                                  "creation) order, so a large gang cannot be starved."},
         "priority": {**_I32, "default": 0},
+        "preemptionPolicy": {"type": "string", "enum": ["Never", "PreemptLowerPriority"],
+                             "default": "Never",
+                             "description": "PreemptLowerPriority: when the gang does not fit, "
+                                            "stop running jobs of strictly lower priority (same "
+                                            "resource) until it does; victims go back to the queue "
+                                            "without using their backoffLimit."},
+        "suspend": {**_B, "default": False,
+                    "description": "true stops the gang and frees its GPUs (phase Suspended); "
+                                   "false resumes it through the queue. Not a restart."},
         "restartPolicy": {"type": "string", "enum": ["OnFailure", "Never"],
                           "default": "OnFailure",
                           "description": "OnFailure: a failed or lost pod restarts the whole "
@@ -315,23 +329,68 @@ MI355X_JOB_STATUS = {
     "properties": {
         "observedGeneration": _I64,
         "phase": {"type": "string",
-                  "enum": ["Pending", "Running", "Restarting", "Succeeded", "Failed"]},
+                  "enum": ["Pending", "Running", "Restarting", "Suspended", "Succeeded",
+                           "Failed"]},
         "replicas": _I32,
         "active": _I32,
         "succeeded": _I32,
         "failed": _I32,
         "restarts": _I32,
+        "preemptions": _I32,
+        "lastPreemption": {**_S, "description": "preempted-by annotation value last acted on"},
+        "preempting": {"type": "array", "items": _S,
+                       "description": "jobs this one preempted; its pods wait for their GPUs"},
         "attempt": _I32,
         "masterAddr": _S,
+        "resourceName": {**_S, "description": "extended resource the pods request (resolved "
+                                             "from poolRef at placement)"},
         "startTime": _S,
         "completionTime": _S,
         "placement": {"type": "array", "items": {
             "type": "object",
-            "properties": {"index": _I32, "node": _S}}},
+            "properties": {"index": _I32, "node": _S,
+                           "created": {**_B, "description": "pod exists; until then the slot "
+                                                            "is a reservation"}}}},
         "replicaStatuses": {"type": "array", "items": {
             "type": "object",
             "properties": {"index": _I32, "pod": _S, "node": _S, "phase": _S, "podIP": _S,
                            "exitCode": _I32, "devices": _S, "message": _S}}},
+        "conditions": CONDITIONS_FIELD,
+    },
+}
+
+# ---------------------------------------------------------------- Mi355xQueue
+# Volcano's Queue (the `queue: default` a job names, reference GPU调度平台搭建.md:650; Volcano install
+# :275-287) as a cluster-scoped kind: a GPU capability per extended resource, an Open/Closed state
+# and whether other queues' higher-priority jobs may preempt its jobs. The queue named "default"
+# is implicit (unlimited, open) until an object of that name exists.
+MI355X_QUEUE_SPEC = {
+    "type": "object",
+    "description": "A job queue: GPU capability, admission state and reclaim policy.",
+    "properties": {
+        "capability": {"type": "object", "additionalProperties": {**_I64, "minimum": 0},
+                       "description": "Max GPUs per extended resource (e.g. amd.com/gpu: 16) "
+                                      "that this queue's placed jobs may hold together."},
+        "state": {"type": "string", "enum": ["Open", "Closed"], "default": "Open",
+                  "description": "Closed: no new gang placements; running jobs continue."},
+        "reclaimable": {**_B, "default": True,
+                        "description": "Jobs of this queue may be preempted by higher-priority "
+                                       "PreemptLowerPriority jobs of other queues."},
+    },
+}
+
+MI355X_QUEUE_STATUS = {
+    "type": "object",
+    "properties": {
+        "observedGeneration": _I64,
+        "state": _S,
+        "pending": _I32,
+        "running": _I32,
+        "suspended": _I32,
+        "completed": _I32,
+        "failed": _I32,
+        "allocated": {"type": "object", "additionalProperties": _I64,
+                      "description": "GPUs held by placed jobs, per extended resource"},
         "conditions": CONDITIONS_FIELD,
     },
 }
@@ -383,6 +442,23 @@ KINDS = {
         "conditions": JOB_CONDITIONS,
         "scale": False,
     },
+    "Mi355xQueue": {
+        "plural": "mi355xqueues",
+        "singular": "mi355xqueue",
+        "shortNames": ["mxq"],
+        "scope": "Cluster",
+        "spec": MI355X_QUEUE_SPEC,
+        "status": MI355X_QUEUE_STATUS,
+        "printerColumns": [
+            {"name": "State", "type": "string", "jsonPath": ".status.state"},
+            {"name": "Pending", "type": "integer", "jsonPath": ".status.pending"},
+            {"name": "Running", "type": "integer", "jsonPath": ".status.running"},
+            {"name": "Allocated", "type": "string", "jsonPath": ".status.allocated"},
+            {"name": "Age", "type": "date", "jsonPath": ".metadata.creationTimestamp"},
+        ],
+        "conditions": [],
+        "scale": False,
+    },
 }
 
 
@@ -409,7 +485,7 @@ def crd(kind: str) -> dict:
             "group": GROUP,
             "names": {"kind": kind, "listKind": f"{kind}List", "plural": k["plural"],
                       "singular": k["singular"], "shortNames": list(k["shortNames"])},
-            "scope": "Namespaced",
+            "scope": k.get("scope", "Namespaced"),
             "versions": [{
                 "name": VERSION,
                 "served": True,

@@ -481,6 +481,10 @@ def cmd_trainjob(c: Client, ns: str, args) -> int:
     if args.tj_cmd == "list":
         print_table(c.table(MI355XJOBS, ns))
         return 0
+    if args.tj_cmd in ("suspend", "resume"):
+        c.patch(MI355XJOBS, args.job, {"spec": {"suspend": args.tj_cmd == "suspend"}}, ns)
+        print(f"mi355xjob.{schema.GROUP}/{args.job} {args.tj_cmd}d")
+        return 0
     if args.tj_cmd == "delete":
         c.delete(MI355XJOBS, args.job, ns)
         print(f"mi355xjob.{schema.GROUP}/{args.job} deleted")
@@ -600,6 +604,9 @@ def build_parser() -> argparse.ArgumentParser:
     t.add_argument("--rank", type=int, default=None)
     t = tsub.add_parser("delete")
     t.add_argument("job")
+    for verb in ("suspend", "resume"):
+        t = tsub.add_parser(verb, help=f"{verb} a job (spec.suspend): GPUs freed / re-queued")
+        t.add_argument("job")
     p = sub.add_parser("render")
     p.add_argument("what", choices=["job"])
     p.add_argument("-f", "--filename", required=True)

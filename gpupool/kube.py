@@ -60,11 +60,13 @@ CRDS = Res("apiextensions.k8s.io", "v1", "customresourcedefinitions", namespaced
 MI355XPOOLS = Res(schema.GROUP, schema.VERSION, "mi355xpools")
 AZUREVMPOOLS = Res(schema.GROUP, schema.VERSION, "azurevmpools")
 MI355XJOBS = Res(schema.GROUP, schema.VERSION, "mi355xjobs")
+MI355XQUEUES = Res(schema.GROUP, schema.VERSION, "mi355xqueues", namespaced=False)
 
 BY_KIND = {
     "Pod": PODS, "Node": NODES, "Event": EVENTS, "Secret": SECRETS, "ConfigMap": CONFIGMAPS,
     "Namespace": NAMESPACES, "Lease": LEASES, "CustomResourceDefinition": CRDS,
     "Mi355xPool": MI355XPOOLS, "AzureVmPool": AZUREVMPOOLS, "Mi355xJob": MI355XJOBS,
+    "Mi355xQueue": MI355XQUEUES,
     "ClusterRole": Res("rbac.authorization.k8s.io", "v1", "clusterroles", namespaced=False),
     "ClusterRoleBinding": Res("rbac.authorization.k8s.io", "v1", "clusterrolebindings",
                               namespaced=False),

@@ -84,6 +84,9 @@ class FakeKubelet:
         self.pods: dict[str, RunningPod] = {}          # pod uid -> running pod
         self.assigned: dict[str, str] = {}             # device ID -> pod uid
         self.lock = threading.RLock()
+        # serialises node-status snapshots with their PATCH: two ListAndWatch streams updating at
+        # once must not land an older snapshot after a newer one
+        self.status_lock = threading.Lock()
         self.stop_ev = threading.Event()
         self.threads: list[threading.Thread] = []
         self.reg_server: grpc.Server | None = None
@@ -204,17 +207,18 @@ class FakeKubelet:
         self._update_node_status()
 
     def _update_node_status(self) -> None:
-        with self.lock:
-            cap = {r: str(len(c.devices)) for r, c in self.plugins.items()}
-            alloc = {r: str(sum(1 for h in c.devices.values() if h == "Healthy"))
-                     for r, c in self.plugins.items()}
-        try:
-            self.client.patch(NODES, self.node, {"status": {
-                "capacity": {"cpu": "64", "memory": "1Ti", "pods": "110", **cap},
-                "allocatable": {"cpu": "64", "memory": "1Ti", "pods": "110", **alloc}}},
-                sub="status")
-        except KubeError as e:
-            log.warning("node status patch failed: %s", e)
+        with self.status_lock:
+            with self.lock:
+                cap = {r: str(len(c.devices)) for r, c in self.plugins.items()}
+                alloc = {r: str(sum(1 for h in c.devices.values() if h == "Healthy"))
+                         for r, c in self.plugins.items()}
+            try:
+                self.client.patch(NODES, self.node, {"status": {
+                    "capacity": {"cpu": "64", "memory": "1Ti", "pods": "110", **cap},
+                    "allocatable": {"cpu": "64", "memory": "1Ti", "pods": "110", **alloc}}},
+                    sub="status")
+            except KubeError as e:
+                log.warning("node status patch failed: %s", e)
 
     def allocatable(self) -> dict[str, list[str]]:
         with self.lock:

@@ -79,6 +79,8 @@ struct Mi355xJobSpec {
   std::map<std::string, std::string> node_selector;
   std::string queue = "default";
   int32_t priority = 0;
+  std::string preemption_policy = "Never";  // | PreemptLowerPriority
+  bool suspend = false;
   std::string restart_policy = "OnFailure";
   int32_t backoff_limit = 3;
   int64_t active_deadline_seconds = 0;

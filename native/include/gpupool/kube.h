@@ -31,6 +31,8 @@ ResourceRef secrets();
 ResourceRef leases();
 ResourceRef resourcequotas();
 ResourceRef mi355xpools();
+ResourceRef mi355xjobs();
+ResourceRef mi355xqueues();  // cluster-scoped
 ResourceRef azurevmpools();
 }  // namespace res
 

@@ -141,8 +141,12 @@ class AzureVmPoolReconciler : public PoolReconcilerBase {
 //     WORLD_SIZE/RANK for one-GPU workers, PET_NNODES/PET_NPROC_PER_NODE/PET_NODE_RANK for
 //     torchrun), so RCCL/gloo rendezvous needs no Service or DNS;
 //   * a failed or lost pod restarts the whole gang (restartPolicy OnFailure, backoffLimit), since
-//     DDP ranks cannot rejoin alone; activeDeadlineSeconds, successPolicy, cleanPodPolicy and
-//     ttlSecondsAfterFinished follow the batch/v1 Job and Kubeflow meanings.
+//     DDP ranks cannot rejoin alone; activeDeadlineSeconds, successPolicy, cleanPodPolicy,
+//     ttlSecondsAfterFinished and suspend follow the batch/v1 Job and Kubeflow meanings;
+//   * preemptionPolicy PreemptLowerPriority (Volcano's preempt action, PriorityClass semantics):
+//     a gang that does not fit annotates the fewest lower-priority running jobs whose GPUs make it
+//     fit; each victim's own reconciler stops its gang and re-queues it (not a failure restart),
+//     while the preemptor holds its reservation and creates pods once the GPUs are really free.
 // Reservations of placed-but-not-yet-created pods live in status.placement, and every placement
 // decision runs under one mutex against fresh LISTs, so two gangs never share a GPU.
 class Mi355xJobReconciler : public PoolReconcilerBase {
@@ -168,9 +172,15 @@ class Mi355xJobReconciler : public PoolReconcilerBase {
   Outcome cleanup_finished_(const Json& obj, const ObjectMeta& m, const Mi355xJobSpec& spec,
                             const std::vector<Json>& pods);
   std::vector<Json> list_pods_(const ObjectMeta& m);
-  // Tries to place the gang (under sched_mu_). Returns the placement, or empty with *why set.
+  // Tries to place the gang (under sched_mu_). Returns the placement, or empty with *why set. With
+  // preemptionPolicy PreemptLowerPriority a placement may rely on GPUs of lower-priority running
+  // jobs, returned in *victims (the smallest set found, lowest priority and newest first).
   std::vector<Slot> schedule_(const ObjectMeta& m, const Mi355xJobSpec& spec, const std::string& resource,
-                              const std::string& pool_node, std::string* reason, std::string* why);
+                              const std::string& pool_node, std::string* reason, std::string* why,
+                              std::vector<Json>* victims);
+  // True when every not-yet-created slot's node has that many GPUs free right now (pods of
+  // preempted jobs may still be terminating on it).
+  bool capacity_free_(const Mi355xJobSpec& spec, const std::string& resource, const Json& placement);
   Json build_pod_(const Json& job, const ObjectMeta& m, const Mi355xJobSpec& spec, const std::string& resource,
                   int attempt, const Slot& slot, const std::string& master_addr);
   bool resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec& spec, std::string* resource, std::string* node,
@@ -178,6 +188,19 @@ class Mi355xJobReconciler : public PoolReconcilerBase {
 
   Informer& nodes_;
   std::mutex sched_mu_;
+};
+
+// Mi355xQueue status (Volcano queue status): job counts per phase and the GPUs its placed jobs
+// hold per extended resource. Admission (state, capability, reclaimable) is enforced by the job
+// reconciler's scheduling step; this one only reports.
+class Mi355xQueueReconciler : public PoolReconcilerBase {
+ public:
+  Mi355xQueueReconciler(KubeClient& client, Informer& queues, Informer& jobs, EventRecorder* events,
+                        ReconcilerOptions opts = {});
+  Outcome reconcile(const std::string& ns, const std::string& name) override;
+
+ private:
+  Informer& jobs_;
 };
 
 // Controller: a shared work queue + N workers dispatching "Kind/ns/name" keys to reconcilers,

@@ -152,6 +152,8 @@ Mi355xJobSpec Mi355xJobSpec::from(const Json& s) {
   for (const auto& kv : s["nodeSelector"].members()) j.node_selector[kv.first] = kv.second.as_string();
   j.queue = s["queue"].str_or("default");
   j.priority = static_cast<int32_t>(s["priority"].as_int(0));
+  j.preemption_policy = s["preemptionPolicy"].str_or("Never");
+  j.suspend = s["suspend"].as_bool(false);
   j.restart_policy = s["restartPolicy"].str_or("OnFailure");
   j.backoff_limit = static_cast<int32_t>(s["backoffLimit"].as_int(3));
   j.active_deadline_seconds = s["activeDeadlineSeconds"].as_int(0);
@@ -196,6 +198,9 @@ std::vector<std::string> validate_job(const Json& obj) {
     errs.push_back("spec.restartPolicy: Unsupported value");
   if (s.contains("cleanPodPolicy") && !in(s["cleanPodPolicy"].as_string(), {"Running", "All", "None"}))
     errs.push_back("spec.cleanPodPolicy: Unsupported value");
+  if (s.contains("preemptionPolicy") && !in(s["preemptionPolicy"].as_string(), {"Never", "PreemptLowerPriority"}))
+    errs.push_back("spec.preemptionPolicy: Unsupported value");
+  if (s.contains("suspend") && !s["suspend"].is_bool()) errs.push_back("spec.suspend: must be of type boolean");
   if (s.contains("successPolicy") && !in(s["successPolicy"].as_string(), {"AllWorkers", "Rank0"}))
     errs.push_back("spec.successPolicy: Unsupported value");
   if (!s["template"].is_object()) errs.push_back("spec.template: Required value");

@@ -67,6 +67,21 @@ bool selector_matches(const std::map<std::string, std::string>& sel, const Json&
   return true;
 }
 
+// The extended resource a job's pods request: resolved at placement time (a poolRef's resource)
+// and recorded in status.resourceName; before that, the spec's or the given default.
+std::string job_resource(const Json& j, const std::string& dflt) {
+  const std::string& st = j.path("status.resourceName").as_string();
+  if (!st.empty()) return st;
+  return j.path("spec.resourceName").str_or(dflt);
+}
+
+// GPUs a placed (or running) job holds: gpusPerReplica per placement slot.
+int64_t job_held(const Json& j) {
+  return j.path("spec.gpusPerReplica").as_int(1) * static_cast<int64_t>(j.path("status.placement").size());
+}
+
+std::string job_queue(const Json& j) { return j.path("spec.queue").str_or("default"); }
+
 bool node_schedulable(const Json& node) {
   if (node.path("spec.unschedulable").as_bool(false)) return false;
   for (const auto& c : node.path("status.conditions").elements())
@@ -161,7 +176,8 @@ bool Mi355xJobReconciler::resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec
 std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const ObjectMeta& m, const Mi355xJobSpec& spec,
                                                                       const std::string& resource,
                                                                       const std::string& pool_node,
-                                                                      std::string* reason, std::string* why) {
+                                                                      std::string* reason, std::string* why,
+                                                                      std::vector<Json>* victims) {
   trace::Span span("schedule");
   // 1. queue order: jobs of the same queue that still wait for a placement and sort ahead of us
   //    (priority desc, creation asc) block us, unless they could never fit the whole cluster.
@@ -178,15 +194,56 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     if (j.path("metadata.uid").as_string() == m.uid) self = j;
   if (self.is_null()) return {};
   auto my_key = key_of(self);
+  // 0. the job's Mi355xQueue: must exist (the "default" queue is implicit), be Open, and have
+  //    capability left for the whole gang
+  auto get_queue = [&](const std::string& qname) {
+    try {
+      return client_.get(res::mi355xqueues(), "", qname);
+    } catch (const KubeError& e) {
+      if (!e.not_found()) throw;
+      return Json();
+    }
+  };
+  const Json queue = get_queue(spec.queue);
+  const int64_t need_total = static_cast<int64_t>(spec.replicas) * spec.gpus_per_replica;
+  int64_t cap = -1;  // -1 = unlimited
+  if (queue.is_null() && spec.queue != "default") {
+    *reason = "QueueNotFound";
+    *why = "Mi355xQueue " + spec.queue + " does not exist";
+    return {};
+  }
+  if (!queue.is_null()) {
+    if (queue.path("spec.state").str_or("Open") == "Closed") {
+      *reason = "QueueClosed";
+      *why = "Mi355xQueue " + spec.queue + " is Closed";
+      return {};
+    }
+    const Json& c = queue.path("spec.capability")[resource];
+    if (!c.is_null()) cap = qty(c);
+  }
+  if (cap >= 0) {
+    int64_t used = 0;
+    for (const auto& j : jobs["items"].elements()) {
+      if (j.path("metadata.uid").as_string() == m.uid || terminal(j.path("status.phase").as_string())) continue;
+      if (job_queue(j) == spec.queue && job_resource(j, resource) == resource) used += job_held(j);
+    }
+    if (used + need_total > cap) {
+      *reason = "QueueOverCapacity";
+      *why = "queue " + spec.queue + ": " + std::to_string(used) + " " + resource + " held + " +
+             std::to_string(need_total) + " needed > capability " + std::to_string(cap);
+      return {};
+    }
+  }
   for (const auto& j : jobs["items"].elements()) {
     if (j.path("metadata.uid").as_string() == m.uid || !j.path("metadata.deletionTimestamp").as_string().empty()) continue;
     if (j.path("spec.queue").str_or("default") != spec.queue) continue;
     const std::string phase = j.path("status.phase").str_or("Pending");
     if (phase != "Pending" && phase != "Restarting") continue;
     if (!j.path("status.placement").elements().empty()) continue;  // already placed
-    const std::string jres = j.path("spec.resourceName").str_or(resource);
+    const std::string jres = job_resource(j, resource);
     int64_t jneed = j.path("spec.replicas").as_int(1) * j.path("spec.gpusPerReplica").as_int(1);
-    if (jres == resource && jneed > cluster_total) continue;  // can never run: must not block the queue
+    // can never run (bigger than the cluster or than the queue's capability): must not block it
+    if (jres == resource && (jneed > cluster_total || (cap >= 0 && jneed > cap))) continue;
     if (key_of(j) < my_key) {
       *reason = "QueuedBehind";
       *why = "queue " + spec.queue + ": waiting behind " + j.path("metadata.namespace").as_string() + "/" +
@@ -213,24 +270,101 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     }
     for (const auto& j : jobs["items"].elements()) {
       if (j.path("metadata.uid").as_string() == m.uid || terminal(j.path("status.phase").as_string())) continue;
-      if (j.path("spec.resourceName").str_or(resource) != resource) continue;
+      if (job_resource(j, resource) != resource) continue;
       int64_t g = j.path("spec.gpusPerReplica").as_int(1);
       for (const auto& s : j.path("status.placement").elements())
         if (!s["created"].as_bool(false) && free.count(s["node"].as_string())) free[s["node"].as_string()] -= g;
     }
   }
-  std::vector<std::pair<std::string, int64_t>> cands;
-  for (const auto& n : order) cands.emplace_back(n, std::max<int64_t>(0, free[n]));
-  auto slots = place(cands, spec.replicas, spec.gpus_per_replica);
+  auto fit = [&](const std::map<std::string, int64_t>& f) {
+    std::vector<std::pair<std::string, int64_t>> cands;
+    for (const auto& n : order) cands.emplace_back(n, std::max<int64_t>(0, f.at(n)));
+    return place(cands, spec.replicas, spec.gpus_per_replica);
+  };
+  auto slots = fit(free);
+  if (slots.empty() && spec.preemption_policy == "PreemptLowerPriority" && spec.gpus_per_replica > 0 && !order.empty()) {
+    // 3. preemption: running (placed) jobs of strictly lower priority on our candidate nodes, the
+    //    lowest priority and then the most recently started first; add their GPUs back until the
+    //    gang fits, then drop every victim the placement does not need.
+    struct Cand {
+      Json job;
+      std::map<std::string, int64_t> held;
+    };
+    std::vector<Cand> pool;
+    for (const auto& j : jobs["items"].elements()) {
+      if (j.path("metadata.uid").as_string() == m.uid || !j.path("metadata.deletionTimestamp").as_string().empty())
+        continue;
+      const std::string ph = j.path("status.phase").str_or("Pending");
+      if (terminal(ph) || ph == "Suspended" || j.path("spec.suspend").as_bool(false)) continue;
+      if (j.path("spec.priority").as_int(0) >= spec.priority) continue;
+      if (job_resource(j, resource) != resource) continue;
+      if (job_queue(j) != spec.queue) {  // cross-queue reclaim only from reclaimable queues
+        const Json q = get_queue(job_queue(j));
+        if (!q.is_null() && !q.path("spec.reclaimable").as_bool(true)) continue;
+      }
+      Cand c{j, {}};
+      const int64_t g = j.path("spec.gpusPerReplica").as_int(1);
+      for (const auto& sl : j.path("status.placement").elements())
+        if (free.count(sl["node"].as_string())) c.held[sl["node"].as_string()] += g;
+      if (!c.held.empty()) pool.push_back(std::move(c));
+    }
+    std::stable_sort(pool.begin(), pool.end(), [](const Cand& a, const Cand& b) {
+      const int64_t pa = a.job.path("spec.priority").as_int(0), pb = b.job.path("spec.priority").as_int(0);
+      if (pa != pb) return pa < pb;
+      return a.job.path("status.startTime").as_string() > b.job.path("status.startTime").as_string();
+    });
+    std::map<std::string, int64_t> f2 = free;
+    std::vector<size_t> chosen;
+    for (size_t i = 0; i < pool.size() && slots.empty(); ++i) {
+      for (const auto& kv : pool[i].held) f2[kv.first] += kv.second;
+      chosen.push_back(i);
+      slots = fit(f2);
+    }
+    if (!slots.empty()) {
+      // minimise: the cheapest victims were added first, so try to spare the later (costlier) ones
+      for (size_t k = chosen.size(); k-- > 0;) {
+        std::map<std::string, int64_t> f3 = f2;
+        for (const auto& kv : pool[chosen[k]].held) f3[kv.first] -= kv.second;
+        auto s3 = fit(f3);
+        if (!s3.empty()) {
+          f2 = std::move(f3);
+          slots = std::move(s3);
+          chosen.erase(chosen.begin() + static_cast<std::ptrdiff_t>(k));
+        }
+      }
+      for (size_t i : chosen) victims->push_back(pool[i].job);
+    }
+  }
   if (slots.empty()) {
     int64_t total_free = 0;
-    for (const auto& c : cands) total_free += c.second;
+    for (const auto& n : order) total_free += std::max<int64_t>(0, free[n]);
     *reason = "Unschedulable";
     *why = "gang of " + std::to_string(spec.replicas) + " x " + std::to_string(spec.gpus_per_replica) + " " +
-           resource + " does not fit: " + std::to_string(total_free) + " free on " + std::to_string(cands.size()) +
+           resource + " does not fit: " + std::to_string(total_free) + " free on " + std::to_string(order.size()) +
            " candidate node(s)";
   }
   return slots;
+}
+
+bool Mi355xJobReconciler::capacity_free_(const Mi355xJobSpec& spec, const std::string& resource,
+                                         const Json& placement) {
+  std::map<std::string, int64_t> need;
+  for (const auto& sl : placement.elements())
+    if (!sl["created"].as_bool(false)) need[sl["node"].as_string()] += spec.gpus_per_replica;
+  if (need.empty() || spec.gpus_per_replica <= 0) return true;
+  std::map<std::string, int64_t> free;
+  const Json nodes = client_.list(res::nodes()), pods = client_.list(res::pods(), "");
+  for (const auto& n : nodes["items"].elements()) {
+    const std::string name = n.path("metadata.name").as_string();
+    if (need.count(name)) free[name] = qty(n.path("status.allocatable")[resource]);
+  }
+  for (const auto& p : pods["items"].elements()) {
+    const std::string node = p.path("spec.nodeName").as_string();
+    if (free.count(node) && !terminal(pod_phase(p))) free[node] -= pod_request(p, resource);
+  }
+  for (const auto& kv : need)
+    if (free[kv.first] < kv.second) return false;
+  return true;
 }
 
 Json Mi355xJobReconciler::build_pod_(const Json& job, const ObjectMeta& m, const Mi355xJobSpec& spec,
@@ -425,6 +559,73 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
     return o;
   }
 
+  Json placement = cst["placement"].is_array() ? cst["placement"] : Json::array();
+  auto stop_pods = [&]() {
+    int left = 0;
+    for (const auto& p : pods) {
+      ++left;
+      if (!p.path("metadata.deletionTimestamp").as_string().empty()) continue;
+      try {
+        client_.del(res::pods(), m.ns, p.path("metadata.name").as_string(), terminal(pod_phase(p)) ? 0 : -1);
+      } catch (const KubeError& e) {
+        if (!e.not_found()) throw;
+      }
+    }
+    return left;
+  };
+
+  // ---- preempted by a higher-priority gang (annotation written by its reconciler): stop the gang
+  //      and go back to the queue; not a failure, so backoffLimit is untouched
+  const std::string preempted_by = obj.path("metadata.annotations")[gen::kAnnJobPreemptedBy].as_string();
+  if (!preempted_by.empty() && preempted_by != cst["lastPreemption"].as_string()) {
+    st["lastPreemption"] = preempted_by;
+    if (phase != "Suspended" && (placement.size() > 0 || !pods.empty())) {
+      const std::string by = preempted_by.substr(0, preempted_by.find('@'));
+      stop_pods();
+      st["phase"] = "Restarting";
+      st["placement"] = Json::array();
+      st["active"] = 0;
+      st["preemptions"] = cst["preemptions"].as_int(0) + 1;
+      set_condition(conds, gen::kCondRestarting, "True", "Preempted",
+                    "preempted by higher-priority job " + by + "; waiting in the queue", m.generation, now);
+      set_condition(conds, gen::kCondRunning, "False", "Preempted", "preempted by " + by, m.generation, now);
+      st["conditions"] = conds;
+      write_status_(obj, st);
+      event_(obj, "Warning", "Preempted", "gang stopped for higher-priority job " + by);
+      job_events().inc({{"transition", "Preempted"}});
+      return Outcome::requeue(opts_.progress_poll, "preempted");
+    }
+  }
+
+  // ---- suspend / resume (batch/v1 Job semantics: pods deleted, GPUs freed, deadline clock reset)
+  if (spec.suspend) {
+    const int left = stop_pods();
+    if (phase != "Suspended") {
+      event_(obj, "Normal", "Suspended", "spec.suspend is true: stopping " + std::to_string(left) + " pod(s)");
+      job_events().inc({{"transition", "Suspended"}});
+    }
+    st["phase"] = "Suspended";
+    st["placement"] = Json::array();
+    st["preempting"] = Json::array();
+    st["active"] = 0;
+    st["masterAddr"] = "";
+    st.erase("startTime");
+    set_condition(conds, gen::kCondSuspended, "True", "JobSuspended",
+                  left ? std::to_string(left) + " pod(s) stopping" : "no pods; GPUs released", m.generation, now);
+    set_condition(conds, gen::kCondRunning, "False", "Suspended", "spec.suspend is true", m.generation, now);
+    st["conditions"] = conds;
+    write_status_(obj, st);
+    return left ? Outcome::requeue(opts_.progress_poll, "suspending") : Outcome::done(opts_.resync);
+  }
+  if (phase == "Suspended") {  // resumed: back through the queue for a fresh gang placement
+    phase = "Pending";
+    st["phase"] = "Pending";
+    placement = Json::array();
+    set_condition(conds, gen::kCondSuspended, "False", "Resumed", "spec.suspend is false", m.generation, now);
+    event_(obj, "Normal", "Resumed", "re-entering queue " + spec.queue);
+    job_events().inc({{"transition", "Resumed"}});
+  }
+
   // ---- deadline
   if (spec.active_deadline_seconds > 0) {
     std::chrono::system_clock::time_point started;
@@ -437,19 +638,13 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
   int attempt = static_cast<int>(cst["attempt"].as_int(0));
   for (const auto& p : pods) attempt = std::max(attempt, label_int(p, gen::kLabelJobAttempt, 0));
   st["attempt"] = attempt;
-  Json placement = cst["placement"].is_array() ? cst["placement"] : Json::array();
+  const int restarts = static_cast<int>(cst["restarts"].as_int(0));  // failure restarts only
+  st["restarts"] = restarts;
 
   // ---- needs a (new) gang placement: first run, or a restart whose old pods are gone
   if (attempt == 0 || phase == "Restarting" || placement.size() == 0) {
     if (!pods.empty()) {  // previous attempt's pods still hold GPUs: delete and wait
-      for (const auto& p : pods)
-        if (p.path("metadata.deletionTimestamp").as_string().empty()) {
-          try {
-            client_.del(res::pods(), m.ns, p.path("metadata.name").as_string(), terminal(pod_phase(p)) ? 0 : -1);
-          } catch (const KubeError& e) {
-            if (!e.not_found()) throw;
-          }
-        }
+      stop_pods();
       st["active"] = 0;
       write_status_(obj, st);
       return Outcome::requeue(opts_.progress_poll, "waiting for previous pods to terminate");
@@ -463,7 +658,8 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
       return Outcome::requeue(opts_.resync, "pool not ready");
     }
     std::lock_guard<std::mutex> g(sched_mu_);
-    auto slots = schedule_(m, spec, resource, pool_node, &reason, &why);
+    std::vector<Json> victims;
+    auto slots = schedule_(m, spec, resource, pool_node, &reason, &why, &victims);
     if (slots.empty()) {
       st["phase"] = phase == "Restarting" ? "Restarting" : "Pending";
       const Json& prev = find_condition(conds, gen::kCondScheduled);
@@ -485,6 +681,27 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
     }
     std::string where;
     for (const auto& kv : per_node) where += (where.empty() ? "" : ", ") + kv.first + " x" + std::to_string(kv.second);
+    // preemption: mark the victims (their reconcilers stop them); our pods wait for the GPUs
+    Json preempting = Json::array();
+    for (const auto& v : victims) {
+      const std::string vns = v.path("metadata.namespace").as_string(), vname = v.path("metadata.name").as_string();
+      Json patch = Json::object();
+      patch["metadata"]["annotations"][gen::kAnnJobPreemptedBy] = m.ns + "/" + m.name + "@" + now;
+      try {
+        client_.patch_merge(res_, vns, vname, patch);
+        preempting.push_back(vns + "/" + vname);
+      } catch (const KubeError& e) {
+        if (!e.not_found()) throw;
+      }
+    }
+    if (preempting.size() > 0) {
+      std::string names;
+      for (const auto& v : preempting.elements()) names += (names.empty() ? "" : ", ") + v.as_string();
+      where += "; preempting " + names;
+      event_(obj, "Normal", "Preempting", "lower-priority job(s) stopped for this gang: " + names);
+    }
+    st["preempting"] = preempting;
+    st["resourceName"] = resource;
     st["attempt"] = attempt;
     st["placement"] = placement;
     st["phase"] = "Pending";
@@ -512,6 +729,15 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
   std::string resource = spec.resource_name, pool_node, why;
   if (resource.empty()) resolve_pool_(m, spec, &resource, &pool_node, &why);
   if (resource.empty()) resource = gen::kDefaultResource;
+  if (cst["preempting"].size() > 0) {  // the preempted gangs' pods may still hold our GPUs
+    if (!capacity_free_(spec, resource, placement)) {
+      st["placement"] = placement;
+      st["conditions"] = conds;
+      write_status_(obj, st);
+      return Outcome::requeue(opts_.progress_poll, "waiting for preempted jobs to release GPUs");
+    }
+    st["preempting"] = Json::array();
+  }
   std::map<int, Json> by_index;
   for (const auto& p : pods)
     if (label_int(p, gen::kLabelJobAttempt, 0) == attempt) by_index[label_int(p, gen::kLabelJobIndex, -1)] = p;
@@ -582,26 +808,18 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
   st["active"] = active;
   st["succeeded"] = succeeded;
   st["failed"] = failed;
-  st["restarts"] = std::max(0, attempt - 1);
 
   // ---- transitions
   if (failed > 0 || lost) {
     const std::string msg = !fail_msg.empty() ? fail_msg : lost_msg;
-    if (spec.restart_policy == "OnFailure" && attempt - 1 < spec.backoff_limit) {
-      for (const auto& kv : by_index)  // the whole gang restarts
-        if (kv.second.path("metadata.deletionTimestamp").as_string().empty()) {
-          try {
-            client_.del(res::pods(), m.ns, kv.second.path("metadata.name").as_string(),
-                        terminal(pod_phase(kv.second)) ? 0 : -1);
-          } catch (const KubeError& e) {
-            if (!e.not_found()) throw;
-          }
-        }
+    if (spec.restart_policy == "OnFailure" && restarts < spec.backoff_limit) {
+      stop_pods();  // the whole gang restarts
       st["phase"] = "Restarting";
       st["placement"] = Json::array();
       st["active"] = 0;
+      st["restarts"] = restarts + 1;
       set_condition(conds, gen::kCondRestarting, "True", lost ? "PodLost" : "PodFailed",
-                    msg + "; restarting the gang (restart " + std::to_string(attempt) + "/" +
+                    msg + "; restarting the gang (restart " + std::to_string(restarts + 1) + "/" +
                         std::to_string(spec.backoff_limit) + ")",
                     m.generation, now);
       set_condition(conds, gen::kCondRunning, "False", "Restarting", msg, m.generation, now);
@@ -640,6 +858,48 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
   st["conditions"] = conds;
   write_status_(obj, st);
   return Outcome::requeue(opts_.progress_poll, "starting workers");
+}
+
+Mi355xQueueReconciler::Mi355xQueueReconciler(KubeClient& client, Informer& queues, Informer& jobs,
+                                             EventRecorder* events, ReconcilerOptions opts)
+    : PoolReconcilerBase(client, queues, events, opts, "Mi355xQueue", res::mi355xqueues()), jobs_(jobs) {}
+
+Outcome Mi355xQueueReconciler::reconcile(const std::string& ns, const std::string& name) {
+  (void)ns;
+  Json obj;
+  try {
+    obj = client_.get(res_, "", name);
+  } catch (const KubeError& e) {
+    if (e.not_found()) return Outcome::done(ms(0));
+    throw;
+  }
+  int pending = 0, running = 0, suspended = 0, completed = 0, failed = 0;
+  std::map<std::string, int64_t> alloc;
+  for (const auto& j : jobs_.list()) {
+    if (job_queue(j) != name) continue;
+    const std::string phase = j.path("status.phase").str_or("Pending");
+    if (phase == "Running") ++running;
+    else if (phase == "Suspended") ++suspended;
+    else if (phase == "Succeeded") ++completed;
+    else if (phase == "Failed") ++failed;
+    else ++pending;
+    if (!terminal(phase) && j.path("status.placement").size() > 0)
+      alloc[job_resource(j, gen::kDefaultResource)] += job_held(j);
+  }
+  const Json& cur = obj["status"];
+  Json st = cur.is_object() ? cur : Json::object();
+  st["observedGeneration"] = obj.path("metadata.generation").as_int(0);
+  st["state"] = obj.path("spec.state").str_or("Open");
+  st["pending"] = pending;
+  st["running"] = running;
+  st["suspended"] = suspended;
+  st["completed"] = completed;
+  st["failed"] = failed;
+  Json a = Json::object();
+  for (const auto& kv : alloc) a[kv.first] = kv.second;
+  st["allocated"] = a;
+  write_status_(obj, st);
+  return Outcome::done(opts_.resync);
 }
 
 }  // namespace gpupool

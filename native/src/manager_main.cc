@@ -456,8 +456,10 @@ int main(int argc, char** argv) {
     Informer jobs(client, ResourceRef{gen::kGroup, gen::kVersion, gen::kPluralMi355xJob, true, "Mi355xJob"}, f.ns,
                   std::chrono::milliseconds(f.resync_ms));
     Informer pods(client, res::pods(), "", std::chrono::milliseconds(f.resync_ms));
+    Informer queues(client, res::mi355xqueues(), "", std::chrono::milliseconds(f.resync_ms));
     Mi355xPoolReconciler mi(client, mipools, rocm, &events, ropts);
     Mi355xJobReconciler jr(client, jobs, nodes, &events, ropts);
+    Mi355xQueueReconciler qr(client, queues, jobs, &events, ropts);
     AzureVmPoolReconciler az(client, azpools, cloud, &events, ropts);
     AgentWatchers watchers(rocm, mipools, ctl);
 
@@ -495,7 +497,13 @@ int main(int argc, char** argv) {
     }
     if (want_job) {
       ctl.add_reconciler(&jr);
+      ctl.add_reconciler(&qr);
       jobs.add_handler(pool_handler("Mi355xJob"));
+      // a job's phase or placement changes its queue's status
+      jobs.add_handler([&ctl](const std::string& type, const Json& j) {
+        (void)type;
+        ctl.enqueue("Mi355xQueue", "", j.path("spec.queue").str_or("default"));
+      });
       auto wake_pending = [&]() {
         for (const auto& j : jr.pending()) ctl.enqueue("Mi355xJob", j.first, j.second);
       };
@@ -510,6 +518,11 @@ int main(int argc, char** argv) {
       nodes.add_handler([wake_pending](const std::string& type, const Json&) {
         if (type != "RESYNC") wake_pending();
       });
+      // queue edits (created, opened, capability raised) can admit waiting jobs
+      queues.add_handler([&ctl, wake_pending](const std::string& type, const Json& q) {
+        ctl.enqueue("Mi355xQueue", "", q.path("metadata.name").as_string());
+        if (type != "RESYNC") wake_pending();
+      });
       // pool changes (GPUs advertised or released) change capacity too
       mipools.add_handler([wake_pending](const std::string& type, const Json&) {
         if (type != "RESYNC") wake_pending();
@@ -520,6 +533,7 @@ int main(int argc, char** argv) {
       }
       jobs.start();
       pods.start();
+      queues.start();
     }
     if (want_az) {
       ctl.add_reconciler(&az);
@@ -545,6 +559,7 @@ int main(int argc, char** argv) {
     if (want_job) {
       wait_cache(jobs, "mi355xjobs");
       wait_cache(pods, "pods");
+      wait_cache(queues, "mi355xqueues");
     }
     if (!g_stop) {
       if (want_mi) watchers.sync(rocm.node_names());
@@ -570,6 +585,7 @@ int main(int argc, char** argv) {
     watchers.stop_all();
     jobs.stop();
     pods.stop();
+    queues.stop();
     mipools.stop();
     azpools.stop();
     quotas.stop();

@@ -27,6 +27,8 @@ ResourceRef secrets() { return {"", "v1", "secrets", true, "Secret"}; }
 ResourceRef leases() { return {"coordination.k8s.io", "v1", "leases", true, "Lease"}; }
 ResourceRef resourcequotas() { return {"", "v1", "resourcequotas", true, "ResourceQuota"}; }
 ResourceRef mi355xpools() { return {gen::kGroup, gen::kVersion, gen::kPluralMi355xPool, true, "Mi355xPool"}; }
+ResourceRef mi355xjobs() { return {gen::kGroup, gen::kVersion, gen::kPluralMi355xJob, true, "Mi355xJob"}; }
+ResourceRef mi355xqueues() { return {gen::kGroup, gen::kVersion, gen::kPluralMi355xQueue, false, "Mi355xQueue"}; }
 ResourceRef azurevmpools() { return {gen::kGroup, gen::kVersion, gen::kPluralAzureVmPool, true, "AzureVmPool"}; }
 }  // namespace res
 

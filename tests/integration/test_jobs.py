@@ -107,12 +107,13 @@ def test_gang_is_all_or_nothing_and_queue_is_ordered(node8):
     k.create(MI355XJOBS, job("low", 1, ["sleep", "1"]), "default")
     time.sleep(0.05)
     k.create(MI355XJOBS, job("high", 3, ["sleep", "1"], priority=10), "default")
-    k.wait_for(MI355XJOBS, "low", "default",
-               lambda o: "high" in conds(o).get("Scheduled", {}).get("message", ""), timeout=20)
     for n in ("hold", "high", "low"):
         k.wait_for(MI355XJOBS, n, "default", phase_is("Succeeded"), timeout=60)
-    assert k.get(MI355XJOBS, "high", "default")["status"]["startTime"] <= \
-        k.get(MI355XJOBS, "low", "default")["status"]["startTime"]
+    # placement order from the GangScheduled events (each written once: resourceVersion order)
+    evs = sorted(k.list(EVENTS, "default")["items"], key=lambda e: int(e["metadata"]["resourceVersion"]))
+    placed = [e["involvedObject"]["name"] for e in evs
+              if e["reason"] == "GangScheduled" and e["involvedObject"]["name"] in ("high", "low")]
+    assert placed.index("high") < placed.index("low"), placed
     assert k.get(MI355XJOBS, "huge", "default")["status"]["phase"] == "Pending"
 
 
@@ -222,3 +223,134 @@ def test_gpuctl_trainjob_verbs(node8, tmp_path):
     k.wait_for(MI355XJOBS, "bare", "default", phase_is("Succeeded"), timeout=30)
     gpuctl("trainjob", "delete", "bare")
     k.wait_for(MI355XJOBS, "bare", "default", lambda o: o is None, timeout=30)
+
+
+def test_priority_preemption_picks_fewest_lowest_victims(node8):
+    """Volcano preempt / PriorityClass semantics: a PreemptLowerPriority gang that does not fit
+    stops only the lowest-priority jobs it needs, holds its reservation until their pods are gone,
+    and the victims re-queue without spending their backoffLimit."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 4), "default")
+    wait_ready(k, "pool", 4)
+    k.create(MI355XJOBS, job("low", 2, ["sleep", "600"], priority=1), "default")
+    k.create(MI355XJOBS, job("mid", 2, ["sleep", "600"], priority=5), "default")
+    for n in ("low", "mid"):
+        k.wait_for(MI355XJOBS, n, "default", phase_is("Running"), timeout=30)
+    # Never (the default): a higher-priority gang just waits
+    k.create(MI355XJOBS, job("polite", 2, ["sleep", "1"], priority=9), "default")
+    o = k.wait_for(MI355XJOBS, "polite", "default",
+                   lambda o: conds(o).get("Scheduled", {}).get("reason") == "Unschedulable", timeout=20)
+    k.delete(MI355XJOBS, "polite", "default")
+    k.wait_for(MI355XJOBS, "polite", "default", lambda o: o is None, timeout=30)
+    # 2 GPUs needed: preempting "low" (priority 1) is enough, "mid" keeps running
+    k.create(MI355XJOBS, job("urgent", 2, ["sleep", "1"], priority=10,
+                             preemptionPolicy="PreemptLowerPriority"), "default")
+    o = k.wait_for(MI355XJOBS, "urgent", "default", phase_is("Running", "Succeeded"), timeout=30)
+    low = k.get(MI355XJOBS, "low", "default")
+    assert low["status"]["phase"] in ("Restarting", "Pending"), low["status"]
+    assert conds(low)["Restarting"]["reason"] == "Preempted"
+    assert low["status"]["preemptions"] == 1 and low["status"]["restarts"] == 0
+    mid = k.get(MI355XJOBS, "mid", "default")
+    assert mid["status"]["phase"] == "Running" and not mid["status"].get("preemptions")
+    reasons = {(e["involvedObject"]["name"], e["reason"]) for e in k.list(EVENTS, "default")["items"]}
+    assert ("urgent", "Preempting") in reasons and ("low", "Preempted") in reasons
+    # the preemptor never overlapped a victim's pod on a GPU
+    devs_u = {r.get("devices") for r in
+              k.wait_for(MI355XJOBS, "urgent", "default", phase_is("Succeeded"), timeout=30)
+              ["status"]["replicaStatuses"]}
+    assert len(devs_u) == 2
+    # once urgent is done the victim is placed again and runs (attempt 2, still 0 restarts)
+    low = k.wait_for(MI355XJOBS, "low", "default", phase_is("Running"), timeout=30)
+    assert low["status"]["attempt"] == 2 and low["status"]["restarts"] == 0
+    # equal priority is never preempted
+    k.create(MI355XJOBS, job("peer", 2, ["sleep", "1"], priority=5,
+                             preemptionPolicy="PreemptLowerPriority"), "default")
+    o = k.wait_for(MI355XJOBS, "peer", "default", phase_is("Running", "Succeeded"), timeout=30)
+    assert k.get(MI355XJOBS, "mid", "default")["status"]["phase"] == "Running"
+    assert k.get(MI355XJOBS, "low", "default")["status"]["preemptions"] == 2
+
+
+def test_suspend_frees_gpus_and_resume_requeues(node8):
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 2), "default")
+    wait_ready(k, "pool", 2)
+    k.create(MI355XJOBS, job("s", 2, ["sleep", "600"], activeDeadlineSeconds=3600), "default")
+    k.wait_for(MI355XJOBS, "s", "default", phase_is("Running"), timeout=30)
+    k.patch(MI355XJOBS, "s", {"spec": {"suspend": True}}, "default")
+    o = k.wait_for(MI355XJOBS, "s", "default", lambda o: phase_is("Suspended")(o) and not job_pods(k, "s"),
+                   timeout=30)
+    assert conds(o)["Suspended"]["status"] == "True" and not o["status"].get("startTime")
+    # its GPUs are usable by another gang meanwhile
+    k.create(MI355XJOBS, job("other", 2, ["true"]), "default")
+    k.wait_for(MI355XJOBS, "other", "default", phase_is("Succeeded"), timeout=30)
+    r = subprocess.run([os.path.join(ROOT, "bin", "gpuctl"), "--server", node8.url, "trainjob",
+                        "resume", "s"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "resumed" in r.stdout, r.stderr
+    o = k.wait_for(MI355XJOBS, "s", "default", phase_is("Running"), timeout=30)
+    assert conds(o)["Suspended"]["reason"] == "Resumed" and o["status"]["restarts"] == 0
+    assert o["status"]["attempt"] == 2
+
+
+def test_queue_admission_capability_state_and_status(node8):
+    """Volcano Queue semantics on Mi355xQueue: a named queue must exist, its capability bounds the
+    GPUs its placed jobs hold (even with free GPUs), Closed stops new placements, and the queue's
+    status reports job counts and allocated GPUs."""
+    from gpupool.kube import MI355XQUEUES
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 4), "default")
+    wait_ready(k, "pool", 4)
+    k.create(MI355XJOBS, job("orphan", 1, ["true"], queue="research"), "default")
+    k.wait_for(MI355XJOBS, "orphan", "default",
+               lambda o: conds(o).get("Scheduled", {}).get("reason") == "QueueNotFound", timeout=20)
+    k.create(MI355XQUEUES, {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xQueue",
+                            "metadata": {"name": "research"},
+                            "spec": {"capability": {"amd.com/gpu": 2}}}, None)
+    k.wait_for(MI355XJOBS, "orphan", "default", phase_is("Succeeded"), timeout=30)  # queue wakes it
+    for n in ("qa", "qb", "qc"):
+        k.create(MI355XJOBS, job(n, 1, ["sleep", "600"], queue="research"), "default")
+        time.sleep(0.05)
+    for n in ("qa", "qb"):
+        k.wait_for(MI355XJOBS, n, "default", phase_is("Running"), timeout=30)
+    o = k.wait_for(MI355XJOBS, "qc", "default",
+                   lambda o: conds(o).get("Scheduled", {}).get("reason") == "QueueOverCapacity",
+                   timeout=20)
+    assert "capability 2" in conds(o)["Scheduled"]["message"]
+    # other queues still use the two free GPUs
+    k.create(MI355XJOBS, job("dflt", 2, ["true"]), "default")
+    k.wait_for(MI355XJOBS, "dflt", "default", phase_is("Succeeded"), timeout=30)
+    q = k.wait_for(MI355XQUEUES, "research", None, lambda q: (q.get("status") or {}).get("running") == 2
+                   and q["status"].get("pending") == 1 and q["status"].get("completed") == 1,
+                   timeout=20)
+    assert q["status"]["allocated"] == {"amd.com/gpu": 2} and q["status"]["state"] == "Open"
+    r = subprocess.run([os.path.join(ROOT, "bin", "gpuctl"), "--server", node8.url, "get", "mxq"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "research" in r.stdout and "Open" in r.stdout, r.stdout + r.stderr
+    # Closed: freed capability is not used; reopening admits the waiting job
+    k.patch(MI355XQUEUES, "research", {"spec": {"state": "Closed"}}, None)
+    k.delete(MI355XJOBS, "qa", "default")
+    k.wait_for(MI355XJOBS, "qc", "default",
+               lambda o: conds(o).get("Scheduled", {}).get("reason") == "QueueClosed", timeout=20)
+    k.patch(MI355XQUEUES, "research", {"spec": {"state": "Open"}}, None)
+    k.wait_for(MI355XJOBS, "qc", "default", phase_is("Running"), timeout=30)
+    q = k.wait_for(MI355XQUEUES, "research", None,
+                   lambda q: (q.get("status") or {}).get("running") == 2, timeout=20)
+    assert q["status"]["pending"] == 0
+
+
+def test_cross_queue_preemption_respects_reclaimable(node8):
+    from gpupool.kube import MI355XQUEUES
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 2), "default")
+    wait_ready(k, "pool", 2)
+    k.create(MI355XQUEUES, {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xQueue",
+                            "metadata": {"name": "prod"}, "spec": {"reclaimable": False}}, None)
+    k.create(MI355XJOBS, job("svc", 2, ["sleep", "600"], queue="prod", priority=0), "default")
+    k.wait_for(MI355XJOBS, "svc", "default", phase_is("Running"), timeout=30)
+    k.create(MI355XJOBS, job("burst", 2, ["true"], priority=10,
+                             preemptionPolicy="PreemptLowerPriority"), "default")
+    k.wait_for(MI355XJOBS, "burst", "default",
+               lambda o: conds(o).get("Scheduled", {}).get("reason") == "Unschedulable", timeout=20)
+    assert k.get(MI355XJOBS, "svc", "default")["status"]["phase"] == "Running"
+    k.patch(MI355XQUEUES, "prod", {"spec": {"reclaimable": True}}, None)  # wakes waiting jobs
+    k.wait_for(MI355XJOBS, "burst", "default", phase_is("Succeeded"), timeout=30)
+    assert k.get(MI355XJOBS, "svc", "default")["status"]["preemptions"] == 1

@@ -50,6 +50,23 @@ def test_manager_scenario_under_sanitizer(san, cluster_factory):
         "phase") in ("Succeeded", "Failed"), timeout=60)
     assert o["status"]["phase"] == "Succeeded" and o["status"]["restarts"] == 1, o["status"]
     k.wait_for(MI355XJOBS, "j", "default", lambda o: o is None, timeout=60)
+    # priority preemption: "hi" stops "lo" (capacity check on the victims' pods), "lo" resumes
+    def gang(name, prio, cmd, **extra):
+        return {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xJob",
+                "metadata": {"name": name},
+                "spec": {"replicas": 2, "poolRef": "b", "priority": prio, **extra,
+                         "template": {"spec": {"terminationGracePeriodSeconds": 1,
+                                               "containers": [{"name": "m", "command": cmd}]}}}}
+    k.create(MI355XJOBS, gang("lo", 0, ["sleep", "600"]), "default")
+    k.wait_for(MI355XJOBS, "lo", "default", lambda o: (o.get("status") or {}).get("phase") == "Running",
+               timeout=60)
+    k.create(MI355XJOBS, gang("hi", 5, ["true"], preemptionPolicy="PreemptLowerPriority"), "default")
+    k.wait_for(MI355XJOBS, "hi", "default", lambda o: (o.get("status") or {}).get("phase") == "Succeeded",
+               timeout=60)
+    lo = k.wait_for(MI355XJOBS, "lo", "default", lambda o: (o.get("status") or {}).get("phase") == "Running"
+                    and o["status"].get("preemptions") == 1, timeout=60)
+    for name in ("lo", "hi"):
+        k.delete(MI355XJOBS, name, "default")
     for name in ("a", "b"):
         k.delete(MI355XPOOLS, name, "default")
     for name in ("a", "b"):
