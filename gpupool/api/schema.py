@@ -44,6 +44,9 @@ LABEL_JOB_ATTEMPT = "gpupool.amd.com/attempt"
 # Set on a running Mi355xJob by a higher-priority job that needs its GPUs ("<ns>/<name>/<uid>");
 # the victim's own reconciler then stops its gang (single status writer per job).
 ANN_JOB_PREEMPTED_BY = "gpupool.amd.com/preempted-by"
+# Written by the pool autoscaler: time of its last spec.replicas change and the demand it saw.
+ANN_AUTOSCALE_LAST = "gpupool.amd.com/autoscale-last-scale"
+ANN_AUTOSCALE_DEMAND = "gpupool.amd.com/autoscale-demand"
 
 # Condition types (metav1.Condition, README.md:126-127; roadmap README.md:310).
 COND_READY = "Ready"
@@ -253,6 +256,21 @@ MI355X_SPEC = {
             },
         },
         "replacePolicy": {"type": "string", "enum": ["Replace", "Keep"], "default": "Replace"},
+        "autoscale": {
+            "type": "object",
+            "description": "Demand-driven replicas (an HPA-style writer of spec.replicas through "
+                           "the scale subresource): demand = GPUs of this pool's resourceName "
+                           "requested by live pods + waiting or reserved Mi355xJob gangs, clamped "
+                           "to [minReplicas, maxReplicas]. Scale-up is immediate; scale-down waits "
+                           "until demand has stayed lower for scaleDownDelaySeconds, and only idle "
+                           "GPUs are released (drain picks pod-free GPUs first).",
+            "properties": {
+                "enabled": {**_B, "default": False},
+                "minReplicas": {**_I32, "minimum": 0, "maximum": 1024, "default": 0},
+                "maxReplicas": {**_I32, "minimum": 0, "maximum": 1024, "default": 8},
+                "scaleDownDelaySeconds": {**_I64, "minimum": 0, "default": 300},
+            },
+        },
     },
 }
 

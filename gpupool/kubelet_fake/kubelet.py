@@ -453,6 +453,23 @@ class FakeKubelet:
                 pending = self.client.list(PODS, field_selector="spec.nodeName=")["items"]
             except Exception:
                 continue
+            if not pending:
+                continue
+            # like kube-scheduler's assumed pods: GPUs of pods already bound here but not yet
+            # admitted (and of pods bound earlier in this pass) are not free
+            try:
+                bound = self.client.list(PODS, field_selector=f"spec.nodeName={self.node}")["items"]
+            except Exception:
+                continue
+            with self.lock:
+                admitted = set(self.pods)
+            assumed: dict[str, int] = {}
+            for b in bound:
+                if b["metadata"].get("uid") in admitted or \
+                        b.get("status", {}).get("phase") in ("Succeeded", "Failed"):
+                    continue
+                for r, n in self._requests(b).items():
+                    assumed[r] = assumed.get(r, 0) + n
             for pod in pending:
                 if pod["metadata"].get("deletionTimestamp"):
                     continue
@@ -462,10 +479,13 @@ class FakeKubelet:
                 if sel.get("kubernetes.io/hostname", self.node) != self.node:
                     continue
                 free = self.allocatable()
-                if all(len(free.get(r, [])) >= n for r, n in self._requests(pod).items()):
+                req = self._requests(pod)
+                if all(len(free.get(r, [])) - assumed.get(r, 0) >= n for r, n in req.items()):
                     pod["spec"]["nodeName"] = self.node
                     try:
                         self.client.update(PODS, pod, pod["metadata"]["namespace"])
+                        for r, n in req.items():
+                            assumed[r] = assumed.get(r, 0) + n
                     except KubeError:
                         pass  # another kubelet bound it first (409) or it is gone
 

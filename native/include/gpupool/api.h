@@ -65,6 +65,9 @@ struct Mi355xPoolSpec {
   double probe_min_xgmi_gbps = 0;
   Json probe_json() const;            // the probe options sent with claims and policy updates
   std::string replace_policy = "Replace";
+  bool autoscale = false;  // demand-driven spec.replicas (Mi355xPoolAutoscaler)
+  int32_t autoscale_min = 0, autoscale_max = 8;
+  int64_t scale_down_delay_seconds = 300;
   static Mi355xPoolSpec from(const Json& spec);
   Json policy_json() const;  // health + partition, as the agent/device library consume it
 };

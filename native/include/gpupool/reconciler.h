@@ -203,6 +203,33 @@ class Mi355xQueueReconciler : public PoolReconcilerBase {
   Informer& jobs_;
 };
 
+// Mi355xPoolAutoscaler: demand-driven spec.replicas for pools with spec.autoscale.enabled — the
+// on-prem counterpart of growing and shrinking the reference's AzureVmPool by hand
+// (README.md:292-296, roadmap :309-312) and of the cluster-autoscaler a GPU platform runs beside
+// Volcano (GPU调度平台搭建.md:275-287). Demand = GPUs of the pool's resourceName asked for by live
+// pods (bound or pending) + gangs of Mi355xJobs still waiting for a placement (their poolRef or
+// resource) + reserved-but-uncreated job slots, clamped to [minReplicas, maxReplicas]. Scale-up
+// is immediate; scale-down only after demand has stayed below spec.replicas for
+// scaleDownDelaySeconds, and the pool's drain then releases pod-free GPUs first. Writes are JSON
+// merge patches of spec.replicas + two annotations, so they never race the pool's status writes.
+class Mi355xPoolAutoscaler : public PoolReconcilerBase {
+ public:
+  Mi355xPoolAutoscaler(KubeClient& client, Informer& pools, Informer& jobs, Informer& pods, EventRecorder* events,
+                       ReconcilerOptions opts = {});
+  Outcome reconcile(const std::string& ns, const std::string& name) override;
+  // Pools with autoscale enabled (re-evaluated whenever pods or jobs change).
+  std::vector<std::pair<std::string, std::string>> autoscaled() const;
+  // Pure demand computation over cached pods and jobs; exposed for unit tests.
+  static int64_t demand(const std::vector<Json>& pods, const std::vector<Json>& jobs, const std::string& ns,
+                        const std::string& pool, const std::string& resource);
+
+ private:
+  Informer& jobs_;
+  Informer& pods_;
+  // pool uid -> last time demand was >= spec.replicas (the scale-down delay runs from there)
+  std::map<std::string, std::chrono::steady_clock::time_point> busy_since_;
+};
+
 // Controller: a shared work queue + N workers dispatching "Kind/ns/name" keys to reconcilers,
 // mapping Outcomes onto the queue (Done -> forget + resync; RequeueAfter -> forget + add_after;
 // Transient -> rate-limited backoff; Terminal -> forget, wait for the next spec change).

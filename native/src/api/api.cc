@@ -78,6 +78,11 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.probe_xgmi_peer_check = pr["xgmiPeerCheck"].as_bool(false);
   p.probe_min_xgmi_gbps = pr["minXgmiGBps"].as_double(0);
   p.replace_policy = s["replacePolicy"].str_or("Replace");
+  const Json& a = s["autoscale"];
+  p.autoscale = a["enabled"].as_bool(false);
+  p.autoscale_min = static_cast<int32_t>(a["minReplicas"].as_int(0));
+  p.autoscale_max = static_cast<int32_t>(a["maxReplicas"].as_int(8));
+  p.scale_down_delay_seconds = a["scaleDownDelaySeconds"].as_int(300);
   return p;
 }
 
@@ -253,6 +258,14 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
     errs.push_back("spec.partition.compute: Unsupported value");
   if (part.contains("memory") && !in(part["memory"].as_string(), {"Any", "NPS1", "NPS2", "NPS4", "NPS8"}))
     errs.push_back("spec.partition.memory: Unsupported value");
+  const Json& as = s["autoscale"];
+  if (as.contains("enabled") && !as["enabled"].is_bool()) errs.push_back("spec.autoscale.enabled: must be of type boolean");
+  for (const char* k : {"minReplicas", "maxReplicas"})
+    if (as.contains(k) && (!as[k].is_int() || as[k].as_int(0) < 0 || as[k].as_int(0) > 1024))
+      errs.push_back(std::string("spec.autoscale.") + k + ": must be within [0, 1024]");
+  if (as.contains("scaleDownDelaySeconds") &&
+      (!as["scaleDownDelaySeconds"].is_int() || as["scaleDownDelaySeconds"].as_int(0) < 0))
+    errs.push_back("spec.autoscale.scaleDownDelaySeconds: should be greater than or equal to 0");
   return errs;
 }
 

@@ -13,6 +13,7 @@
 
 #include "gpupool/generated/schema_consts.h"
 #include "gpupool/reconciler.h"
+#include "job_util.h"
 
 namespace gpupool {
 
@@ -32,26 +33,7 @@ HistogramVec& gang_wait_hist() {
   return h;
 }
 
-int64_t qty(const Json& v) {
-  if (v.is_int()) return v.as_int();
-  if (v.is_number()) return static_cast<int64_t>(v.as_double());
-  const std::string& s = v.as_string();
-  return s.empty() ? 0 : std::atoll(s.c_str());
-}
-
-bool terminal(const std::string& phase) { return phase == "Succeeded" || phase == "Failed"; }
-
-std::string pod_phase(const Json& p) { return p.path("status.phase").str_or("Pending"); }
-
-int64_t pod_request(const Json& pod, const std::string& resource) {
-  int64_t n = 0;
-  for (const auto& c : pod.path("spec.containers").elements()) {
-    const Json& r = c["resources"];
-    int64_t lim = qty(r["limits"][resource]);
-    n += lim ? lim : qty(r["requests"][resource]);
-  }
-  return n;
-}
+using namespace detail;
 
 std::string pod_name(const std::string& job, int index) { return job + "-worker-" + std::to_string(index); }
 
@@ -66,21 +48,6 @@ bool selector_matches(const std::map<std::string, std::string>& sel, const Json&
     if (labels[kv.first].as_string() != kv.second) return false;
   return true;
 }
-
-// The extended resource a job's pods request: resolved at placement time (a poolRef's resource)
-// and recorded in status.resourceName; before that, the spec's or the given default.
-std::string job_resource(const Json& j, const std::string& dflt) {
-  const std::string& st = j.path("status.resourceName").as_string();
-  if (!st.empty()) return st;
-  return j.path("spec.resourceName").str_or(dflt);
-}
-
-// GPUs a placed (or running) job holds: gpusPerReplica per placement slot.
-int64_t job_held(const Json& j) {
-  return j.path("spec.gpusPerReplica").as_int(1) * static_cast<int64_t>(j.path("status.placement").size());
-}
-
-std::string job_queue(const Json& j) { return j.path("spec.queue").str_or("default"); }
 
 bool node_schedulable(const Json& node) {
   if (node.path("spec.unschedulable").as_bool(false)) return false;

@@ -460,6 +460,7 @@ int main(int argc, char** argv) {
     Mi355xPoolReconciler mi(client, mipools, rocm, &events, ropts);
     Mi355xJobReconciler jr(client, jobs, nodes, &events, ropts);
     Mi355xQueueReconciler qr(client, queues, jobs, &events, ropts);
+    Mi355xPoolAutoscaler as(client, mipools, jobs, pods, &events, ropts);
     AzureVmPoolReconciler az(client, azpools, cloud, &events, ropts);
     AgentWatchers watchers(rocm, mipools, ctl);
 
@@ -527,6 +528,22 @@ int main(int argc, char** argv) {
       mipools.add_handler([wake_pending](const std::string& type, const Json&) {
         if (type != "RESYNC") wake_pending();
       });
+      // demand-driven pools: re-evaluated on their own edits and whenever pods or jobs change
+      if (want_mi) {
+        ctl.add_reconciler(&as);
+        mipools.add_handler([&ctl](const std::string& type, const Json& p) {
+          (void)type;
+          if (p.path("spec.autoscale.enabled").as_bool(false))
+            ctl.enqueue("Mi355xPoolAutoscale", p.path("metadata.namespace").as_string(),
+                        p.path("metadata.name").as_string());
+        });
+        auto wake_autoscaled = [&ctl, &as](const std::string& type, const Json&) {
+          if (type == "RESYNC") return;
+          for (const auto& p : as.autoscaled()) ctl.enqueue("Mi355xPoolAutoscale", p.first, p.second);
+        };
+        pods.add_handler(wake_autoscaled);
+        jobs.add_handler(wake_autoscaled);
+      }
       if (!want_mi) {
         nodes.start();
         mipools.start();

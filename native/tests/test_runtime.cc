@@ -461,6 +461,30 @@ TEST(job_gang_placement) {
   EXPECT_TRUE(s.size() == 3 && s[2].node == "x");
 }
 
+TEST(autoscale_demand) {
+  auto J = [](const char* s) { return gpupool::Json::parse(s); };
+  std::vector<gpupool::Json> pods = {
+      J(R"({"metadata":{},"spec":{"nodeName":"n","containers":[{"resources":{"limits":{"r/g":"2"}}}]},"status":{"phase":"Running"}})"),
+      J(R"({"metadata":{},"spec":{"containers":[{"resources":{"limits":{"r/g":1}}}]}})"),  // pending, unbound
+      J(R"({"metadata":{},"spec":{"containers":[{"resources":{"limits":{"r/g":1}}}]},"status":{"phase":"Succeeded"}})"),
+      J(R"({"metadata":{"deletionTimestamp":"x"},"spec":{"containers":[{"resources":{"limits":{"r/g":1}}}]}})"),
+      J(R"({"metadata":{},"spec":{"containers":[{"resources":{"limits":{"other/g":4}}}]}})"),
+  };
+  std::vector<gpupool::Json> jobs = {
+      // waiting gang on this pool: 2 x 2
+      J(R"({"metadata":{"namespace":"ns"},"spec":{"poolRef":"p","replicas":2,"gpusPerReplica":2}})"),
+      // held back by admission: adds nothing
+      J(R"({"metadata":{"namespace":"ns"},"spec":{"poolRef":"p","replicas":3},"status":{"conditions":[{"type":"Scheduled","status":"False","reason":"QueueClosed"}]}})"),
+      // placed, one slot not created yet (its created pod is already among the pods)
+      J(R"({"metadata":{"namespace":"ns"},"spec":{"resourceName":"r/g","replicas":2},"status":{"phase":"Pending","placement":[{"index":0,"node":"n","created":true},{"index":1,"node":"n","created":false}]}})"),
+      J(R"({"metadata":{"namespace":"ns"},"spec":{"poolRef":"p","replicas":4,"suspend":true}})"),
+      J(R"({"metadata":{"namespace":"ns"},"spec":{"poolRef":"p","replicas":4},"status":{"phase":"Succeeded"}})"),
+      J(R"({"metadata":{"namespace":"other"},"spec":{"poolRef":"p","replicas":4,"resourceName":"x/y"}})"),
+  };
+  EXPECT_EQ(gpupool::Mi355xPoolAutoscaler::demand(pods, jobs, "ns", "p", "r/g"), 8);  // 2 + 1 + 4 + 1
+  EXPECT_EQ(gpupool::Mi355xPoolAutoscaler::demand({}, {}, "ns", "p", "r/g"), 0);
+}
+
 TEST(job_validation) {
   using gpupool::Json;
   Json ok = Json::parse(R"({"spec":{"replicas":2,"template":{"spec":{}}}})");

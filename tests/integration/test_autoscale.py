@@ -1,0 +1,68 @@
+"""Demand-driven Mi355xPool (spec.autoscale, Mi355xPoolAutoscaler): pending pods and waiting
+Mi355xJob gangs grow the pool immediately, bounded by maxReplicas; when demand falls the pool
+shrinks after scaleDownDelaySeconds, releasing only idle GPUs (running pods keep theirs)."""
+from __future__ import annotations
+
+import time
+
+import pytest
+
+from gpupool.kube import EVENTS, MI355XJOBS, MI355XPOOLS, PODS
+
+from .helpers import mi_pool, pause_pod, wait_ready
+from .test_jobs import job, phase_is
+
+pytestmark = pytest.mark.slow
+RES = "amd.com/gpu-auto"
+
+
+def running(k, name):
+    return k.wait_for(PODS, name, "default", lambda o: o and o["status"].get("phase") == "Running",
+                      timeout=30)
+
+
+def test_pool_follows_pod_and_job_demand(cluster_factory):
+    k = cluster_factory().client
+    k.create(MI355XPOOLS, mi_pool("auto", 0, resourceName=RES, drain={"gracePeriodSeconds": 1},
+                                  autoscale={"enabled": True, "minReplicas": 0, "maxReplicas": 6,
+                                             "scaleDownDelaySeconds": 2}), "default")
+    wait_ready(k, "auto", 0)
+    # two pending pods on an empty pool: it grows to 2 and the pods bind and run
+    for n in ("w0", "w1"):
+        k.create(PODS, pause_pod(n, resource=RES), "default")
+    wait_ready(k, "auto", 2)
+    keep = {running(k, n)["metadata"]["annotations"]["gpupool.amd.com/devices"] for n in ("w0", "w1")}
+    # a 3 x 1 gang on the pool: 5 GPUs
+    k.create(MI355XJOBS, job("g", 3, ["sleep", "600"], poolRef="auto"), "default")
+    k.wait_for(MI355XJOBS, "g", "default", phase_is("Running"), timeout=30)
+    wait_ready(k, "auto", 5)
+    # demand 7 > maxReplicas 6: clamped
+    k.create(PODS, pause_pod("big", resource=RES, n=2), "default")
+    pool = wait_ready(k, "auto", 6)
+    assert pool["metadata"]["annotations"]["gpupool.amd.com/autoscale-demand"] == "7"
+    time.sleep(0.5)
+    assert k.get(MI355XPOOLS, "auto", "default")["spec"]["replicas"] == 6
+    # demand falls to 2: only after the delay, and w0/w1 keep their GPUs
+    k.delete(MI355XJOBS, "g", "default")
+    k.delete(PODS, "big", "default")
+    t0 = time.monotonic()
+    pool = wait_ready(k, "auto", 2, timeout=40)
+    assert time.monotonic() - t0 >= 1.5
+    still = {running(k, n)["metadata"]["annotations"]["gpupool.amd.com/devices"] for n in ("w0", "w1")}
+    assert still == keep and keep <= {d["uuid"] for d in pool["status"]["devices"]}
+    reasons = [e["reason"] for e in k.list(EVENTS, "default")["items"]
+               if e["involvedObject"]["name"] == "auto"]
+    assert "AutoscaledUp" in reasons and "AutoscaledDown" in reasons
+
+
+def test_min_replicas_floor_and_disable(cluster_factory):
+    k = cluster_factory().client
+    k.create(MI355XPOOLS, mi_pool("warm", 0, resourceName=RES,
+                                  autoscale={"enabled": True, "minReplicas": 2, "maxReplicas": 4,
+                                             "scaleDownDelaySeconds": 0}), "default")
+    wait_ready(k, "warm", 2)  # idle pool held at its floor
+    # disabling hands spec.replicas back to the user: no further changes
+    k.patch(MI355XPOOLS, "warm", {"spec": {"autoscale": {"enabled": False}, "replicas": 3}}, "default")
+    wait_ready(k, "warm", 3)
+    time.sleep(0.5)
+    assert k.get(MI355XPOOLS, "warm", "default")["spec"]["replicas"] == 3

@@ -58,6 +58,11 @@ CASES = [
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "partition": {"compute": "CPX", "memory": "NPS4"}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "partition": {"compute": "XPX"}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "replacePolicy": "Never"}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 0, "autoscale": {"enabled": True, "maxReplicas": 4,
+                                                                 "scaleDownDelaySeconds": 5}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 0, "autoscale": {"maxReplicas": 2000}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 0, "autoscale": {"minReplicas": -1}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 0, "autoscale": {"scaleDownDelaySeconds": -3}}},
     {"kind": "Mi355xPool", "spec": {}},
     {"kind": "AzureVmPool", "spec": {"replicas": 0, "resourceGroupName": "rg", "location": "e",
                                      "vmSize": "s", "vnetName": "v", "subnetName": "s",
