@@ -161,3 +161,27 @@ def test_mi355xjob_torchrun_worker_on_pool_gpu(cluster_factory, tmp_path):
     assert start["rocr_visible"] == hip_uuid
     assert done["status"]["replicaStatuses"][0]["devices"]
     assert os.path.exists(tmp_path / "fashion_mnist_cnn.pth")
+
+
+def test_autoscaled_pool_grows_for_pending_gpu_pod(cluster_factory, tmp_path):
+    """spec.autoscale on real hardware: an empty pool grows to 1 when a pod asks for its GPU,
+    the GPU is probed and advertised, the pod runs on it, and the pool shrinks back once the pod
+    has finished."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    k = c.client
+    k.create(MI355XPOOLS, pool("auto", 0, autoscale={"enabled": True, "maxReplicas": 1,
+                                                     "scaleDownDelaySeconds": 0}), "default")
+    k.wait_for(MI355XPOOLS, "auto", "default", ready_at(0), timeout=60)
+    k.create(PODS, {"metadata": {"name": "train"}, "spec": {"restartPolicy": "Never", "containers": [{
+        "name": "train", "command": ["python", "examples/fmnist_train.py", "--epochs", "1",
+                                     "--synthetic", "--steps", "20", "--output", str(tmp_path)],
+        "resources": {"limits": {"amd.com/gpu": 1}}}]}}, "default")
+    obj = k.wait_for(MI355XPOOLS, "auto", "default", ready_at(1), timeout=60)
+    assert obj["status"]["devices"][0]["probe"]["passed"]
+    done = k.wait_for(PODS, "train", "default",
+                      lambda o: o and o.get("status", {}).get("phase") in ("Succeeded", "Failed"),
+                      timeout=240)
+    log = open(done["metadata"]["annotations"]["gpupool.amd.com/log-path"]).read()
+    assert done["status"]["phase"] == "Succeeded", log[-3000:]
+    assert '"arch": "gfx950' in log
+    k.wait_for(MI355XPOOLS, "auto", "default", ready_at(0), timeout=60)

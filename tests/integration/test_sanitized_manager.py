@@ -67,6 +67,16 @@ def test_manager_scenario_under_sanitizer(san, cluster_factory):
                     and o["status"].get("preemptions") == 1, timeout=60)
     for name in ("lo", "hi"):
         k.delete(MI355XJOBS, name, "default")
+    # autoscaler: a pending pod grows an empty autoscaled pool, deleting it shrinks it again
+    k.create(MI355XPOOLS, mi_pool("auto", 0, resourceName="amd.com/gpu-auto",
+                                  drain={"gracePeriodSeconds": 1},
+                                  autoscale={"enabled": True, "maxReplicas": 2,
+                                             "scaleDownDelaySeconds": 0}), "default")
+    k.create(PODS, pause_pod("aw", resource="amd.com/gpu-auto"), "default")
+    wait_ready(k, "auto", 1, timeout=60)
+    k.delete(PODS, "aw", "default")
+    wait_ready(k, "auto", 0, timeout=60)
+    k.delete(MI355XPOOLS, "auto", "default")
     for name in ("a", "b"):
         k.delete(MI355XPOOLS, name, "default")
     for name in ("a", "b"):
