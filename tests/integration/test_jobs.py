@@ -354,3 +354,32 @@ def test_cross_queue_preemption_respects_reclaimable(node8):
     k.patch(MI355XQUEUES, "prod", {"spec": {"reclaimable": True}}, None)  # wakes waiting jobs
     k.wait_for(MI355XJOBS, "burst", "default", phase_is("Succeeded"), timeout=30)
     assert k.get(MI355XJOBS, "svc", "default")["status"]["preemptions"] == 1
+
+
+def test_gang_spans_nodes_with_torchrun_env(cluster_factory):
+    """A 2 x 4-GPU gang on two 4-GPU nodes: one pod per node, rank 0 on the first, PET_* env for
+    torchrun with nnodes 2 / nproc-per-node 4, and every worker pointed at rank 0's pod IP."""
+    from gpupool.testing.cluster import NodeSpec
+    c = cluster_factory(nodes=[NodeSpec("node-a", count=4), NodeSpec("node-b", count=4)])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("pa", 4, nodeName="node-a"), "default")
+    k.create(MI355XPOOLS, mi_pool("pb", 4, nodeName="node-b"), "default")
+    wait_ready(k, "pa", 4)
+    wait_ready(k, "pb", 4)
+    k.create(MI355XJOBS, job("wide", 2, ["sleep", "600"], gpus=4), "default")
+    o = k.wait_for(MI355XJOBS, "wide", "default", phase_is("Running"), timeout=30)
+    assert sorted(s["node"] for s in o["status"]["placement"]) == ["node-a", "node-b"]
+    pods = {p["metadata"]["labels"]["gpupool.amd.com/replica-index"]: p for p in job_pods(k, "wide")}
+    assert {pods["0"]["spec"]["nodeName"], pods["1"]["spec"]["nodeName"]} == {"node-a", "node-b"}
+    e0, e1 = env_of(pods["0"]), env_of(pods["1"])
+    assert e0["PET_NNODES"] == e1["PET_NNODES"] == "2"
+    assert e0["PET_NPROC_PER_NODE"] == "4" and e1["PET_NODE_RANK"] == "1"
+    assert e1["MASTER_ADDR"] == pods["0"]["status"]["podIP"]
+    for p in pods.values():
+        assert len(p["metadata"]["annotations"]["gpupool.amd.com/devices"].split(",")) == 4
+    # the cluster is full: a 1-GPU job waits, and gets a GPU once the gang is deleted
+    k.create(MI355XJOBS, job("small", 1, ["true"]), "default")
+    k.wait_for(MI355XJOBS, "small", "default",
+               lambda o: conds(o).get("Scheduled", {}).get("reason") == "Unschedulable", timeout=20)
+    k.delete(MI355XJOBS, "wide", "default")
+    k.wait_for(MI355XJOBS, "small", "default", phase_is("Succeeded"), timeout=30)
