@@ -17,6 +17,7 @@ import json
 import logging
 import os
 import subprocess
+import threading
 import time
 
 from ..ops import native_path
@@ -26,7 +27,7 @@ log = logging.getLogger("gpupool.agent.prober")
 
 class Prober:
     def __init__(self, mode: str = "inproc", sim_ms: float = 20.0, gemm_n: int = 4096,
-                 max_workers: int = 16):
+                 max_workers: int = 16, arena_idle_s: float = 10.0):
         self.mode = mode
         self.sim_ms = sim_ms
         self.gemm_n = gemm_n
@@ -40,6 +41,11 @@ class Prober:
             n = hip_probe.init()
             self.ordinals = hip_probe.hip_uuid_map()
             log.info("HIP probe initialised: %d device(s) %s", n, sorted(self.ordinals))
+            # probe arenas stay allocated between back-to-back claims (scale-up bursts) and are
+            # handed back to the GPU's workloads once idle for arena_idle_s
+            self._trim_stop = threading.Event()
+            self._trim_idle_ms = int(arena_idle_s * 1e3)
+            threading.Thread(target=self._trim_loop, daemon=True, name="probe-trim").start()
         elif mode == "subprocess":
             out = subprocess.run([native_path("mi355x-probe"), "--list"], capture_output=True,
                                  text=True, timeout=120)
@@ -166,7 +172,17 @@ class Prober:
                 log.warning("xGMI peer check failed: %r", e)
         return out
 
+    def _trim_loop(self) -> None:
+        period = max(0.05, min(1.0, self._trim_idle_ms / 4e3))
+        while not self._trim_stop.wait(period):
+            try:
+                self._hip.trim(self._trim_idle_ms)
+            except Exception as e:  # never let housekeeping kill the agent
+                log.warning("probe arena trim failed: %s", e)
+
     def close(self) -> None:
+        if self.mode == "inproc":
+            self._trim_stop.set()
         self.pool.shutdown(wait=False)
 
 

@@ -387,52 +387,92 @@ __global__ void count_diff(const float* __restrict__ x, const float* __restrict_
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(bad, static_cast<unsigned long long>(b));
 }
 
-// ABFT (algorithm-based fault tolerance) checks, exact in int64 because every operand is a small
-// integer: with C = A * Bt^T,
+// ABFT (algorithm-based fault tolerance) checks. Every operand is a small integer, so with
+// C = A * Bt^T these identities hold over the integers, and therefore modulo 2^32:
 //   column checksum  sum_m C[m][n] == sum_k (sum_m A[m][k]) * Bt[n][k]
 //   row checksum     sum_n C[m][n] == sum_k A[m][k] * (sum_n Bt[n][k])
-// Two memory-bound primitives, both coalesced: column sums split over row-chunks (one int64 atomic
-// per column per chunk), and one-wave-per-row dot products with 16-byte loads.
-__device__ __forceinline__ long long to_i64(short v) { return static_cast<long long>(bf16_to_f32(v)); }
-__device__ __forceinline__ long long to_i64(float v) { return static_cast<long long>(v); }
+// All arithmetic is unsigned 32-bit (wraps exactly; a corrupted element changes a sum by a
+// non-multiple of 2^32). Two memory-bound primitives with 16-byte loads per lane and four loads in
+// flight (profiles/r1q: the former 2-byte-load / int64 versions took ~0.5 ms per probe, 4-5x the
+// GEMM they check).
+__device__ __forceinline__ uint32_t to_u32(short v) { return static_cast<uint32_t>(static_cast<int>(bf16_to_f32(v))); }
+__device__ __forceinline__ uint32_t to_u32(float v) { return static_cast<uint32_t>(static_cast<int>(v)); }
 
-constexpr int kColChunk = 64;  // rows per block in colsum_partial
+constexpr int kColRows = 64;  // rows per colsum_partial block (4 waves x 16 interleaved rows)
+constexpr int kUnroll = 4;    // independent 16-byte loads in flight per lane
 
+// Column sums: a lane owns V = 16/sizeof(T) adjacent columns (one 16-byte load per row); the
+// block's 4 waves take interleaved rows of a kColRows chunk, combine through LDS, and add one
+// 32-bit atomic per column. cols % V == 0.
 template <class T>
 __global__ __launch_bounds__(256) void colsum_partial(const T* __restrict__ X, int rows, int cols,
-                                                      unsigned long long* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  const int r0 = blockIdx.y * kColChunk;
-  const int r1 = min(rows, r0 + kColChunk);
-  long long s = 0;
-  for (int r = r0; r < r1; ++r) s += to_i64(X[static_cast<int64_t>(r) * cols + c]);
-  atomicAdd(&out[c], static_cast<unsigned long long>(s));  // two's complement: signed sums wrap exactly
+                                                      uint32_t* __restrict__ out) {
+  constexpr int V = 16 / sizeof(T);
+  using vec = __attribute__((ext_vector_type(V))) T;
+  __shared__ uint32_t part[4][64 * V];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int cb = blockIdx.x * 64 * V;
+  const int c0 = cb + lane * V;
+  const int r0 = blockIdx.y * kColRows;
+  const int r1 = min(rows, r0 + kColRows);
+  uint32_t acc[V] = {};
+  if (c0 < cols) {
+    for (int r = r0 + wave; r < r1; r += 4 * kUnroll) {
+      vec v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+        if (r + 4 * u < r1) v[u] = *reinterpret_cast<const vec*>(X + static_cast<int64_t>(r + 4 * u) * cols + c0);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+        if (r + 4 * u < r1) {
+#pragma unroll
+          for (int j = 0; j < V; ++j) acc[j] += to_u32(static_cast<T>(v[u][j]));
+        }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) part[wave][lane * V + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * V && cb + i < cols; i += 256)
+    atomicAdd(&out[cb + i], part[0][i] + part[1][i] + part[2][i] + part[3][i]);
 }
 
-// out[r] = sum_k X[r][k] * (w ? w[k] : 1); one wave64 per row, 4 rows per 256-thread block.
+// out[r] = sum_k X[r][k] * w[k] mod 2^32 (w = nullptr: plain row sums); one wave64 per row, 4 rows
+// per block. The 32-bit weights (colsum_partial's output) are read with 16-byte loads and stay in
+// L1/L2 (K * 4 bytes). K % V == 0.
 template <class T>
-__global__ __launch_bounds__(256) void rowdot(const T* __restrict__ X, int rows, int K,
-                                              const unsigned long long* __restrict__ w,
-                                              unsigned long long* __restrict__ out) {
-  constexpr int V = 16 / sizeof(T);  // elements per 16-byte load
+__global__ __launch_bounds__(256) void rowdot(const T* __restrict__ X, int rows, int K, const uint32_t* __restrict__ w,
+                                              uint32_t* __restrict__ out) {
+  constexpr int V = 16 / sizeof(T);
+  using vec = __attribute__((ext_vector_type(V))) T;
+  using wvec = __attribute__((ext_vector_type(V))) uint32_t;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const T* x = X + static_cast<int64_t>(row) * K;
-  long long s = 0;
-  for (int k0 = lane * V; k0 < K; k0 += 64 * V) {
-    using vec = __attribute__((ext_vector_type(V))) T;
-    vec v = *reinterpret_cast<const vec*>(x + k0);
+  uint32_t s = 0;
+  for (int k0 = lane * V; k0 < K; k0 += 64 * V * kUnroll) {
+    vec v[kUnroll];
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      long long xv = to_i64(static_cast<T>(v[j]));
-      s += w ? xv * static_cast<long long>(w[k0 + j]) : xv;
+    for (int u = 0; u < kUnroll; ++u)
+      if (k0 + u * 64 * V < K) v[u] = *reinterpret_cast<const vec*>(x + k0 + u * 64 * V);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int k = k0 + u * 64 * V;
+      if (k >= K) break;
+      if (w) {
+        const wvec wv = *reinterpret_cast<const wvec*>(w + k);
+#pragma unroll
+        for (int j = 0; j < V; ++j) s += to_u32(static_cast<T>(v[u][j])) * wv[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) s += to_u32(static_cast<T>(v[u][j]));
+      }
     }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (lane == 0) out[row] = static_cast<unsigned long long>(s);
+  if (lane == 0) out[row] = s;
 }
 
 // ---- fault injection (test hooks: prove the checkers catch corruption on real hardware)
@@ -444,8 +484,8 @@ __global__ void inject_bit_flips(unsigned int* __restrict__ p, uint64_t nwords, 
 
 __global__ void inject_gemm_fault(float* __restrict__ c, int64_t idx) { c[idx] += 1.0f; }
 
-__global__ void count_ne_u64(const unsigned long long* __restrict__ a, const unsigned long long* __restrict__ b,
-                             int n, unsigned long long* __restrict__ bad) {
+__global__ void count_ne_u32(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, int n,
+                             unsigned long long* __restrict__ bad) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t d = (i < n && a[i] != b[i]) ? 1u : 0u;
 #pragma unroll
@@ -465,6 +505,11 @@ struct DeviceCtx {
   hipEvent_t gev[3] = {};         // GEMM timing + "counters zeroed" hand-off between the streams
   hipDeviceProp_t prop{};
   unsigned long long* host_res = nullptr;
+  // The probe arena is kept between probes (a hipMalloc of ~1.2 GiB costs ~0.25 ms, a fifth of a
+  // probe) and freed by mi355x_probe_trim once idle, so a pod on the GPU gets the memory back.
+  void* arena = nullptr;
+  size_t arena_bytes = 0;
+  std::chrono::steady_clock::time_point arena_used{};
   bool ready = false;
 };
 
@@ -588,23 +633,25 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, bool inj
   PROBE_CHECK(hipGetLastError());
   if (inject_gemm)
     hipLaunchKernelGGL(inject_gemm_fault, dim3(1), dim3(1), 0, s, c, static_cast<int64_t>(gemm_n / 3) * gemm_n + gemm_n / 5);
-  // ABFT checksums: 6 int64 vectors [acol | bcol | colsumC | expCol | rowsumC | expRow]
-  unsigned long long *vacol = v, *vbcol = v + n, *vcolC = v + 2 * n, *vexpC = v + 3 * n, *vrowC = v + 4 * n,
-                     *vexpR = v + 5 * n;
-  PROBE_CHECK(hipMemsetAsync(v, 0, 3 * n * 8, s));
-  const dim3 cgrid((gemm_n + 255) / 256, (gemm_n + kColChunk - 1) / kColChunk);
-  hipLaunchKernelGGL(colsum_partial<short>, cgrid, dim3(256), 0, s, static_cast<const short*>(a), gemm_n, gemm_n, vacol);
-  hipLaunchKernelGGL(colsum_partial<short>, cgrid, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n, vbcol);
-  hipLaunchKernelGGL(colsum_partial<float>, cgrid, dim3(256), 0, s, static_cast<const float*>(c), gemm_n, gemm_n, vcolC);
+  // ABFT checksums: 6 uint32 vectors [acol | bcol | colsumC | expCol | rowsumC | expRow]
+  uint32_t* v32 = reinterpret_cast<uint32_t*>(v);
+  uint32_t *vacol = v32, *vbcol = v32 + n, *vcolC = v32 + 2 * n, *vexpC = v32 + 3 * n, *vrowC = v32 + 4 * n,
+           *vexpR = v32 + 5 * n;
+  PROBE_CHECK(hipMemsetAsync(v32, 0, 3 * n * sizeof(uint32_t), s));
+  const int rows_y = (gemm_n + kColRows - 1) / kColRows;
+  const dim3 cgrid_h((gemm_n + 511) / 512, rows_y), cgrid_f((gemm_n + 255) / 256, rows_y);
+  hipLaunchKernelGGL(colsum_partial<short>, cgrid_h, dim3(256), 0, s, static_cast<const short*>(a), gemm_n, gemm_n, vacol);
+  hipLaunchKernelGGL(colsum_partial<short>, cgrid_h, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n, vbcol);
+  hipLaunchKernelGGL(colsum_partial<float>, cgrid_f, dim3(256), 0, s, static_cast<const float*>(c), gemm_n, gemm_n, vcolC);
   const dim3 rgrid((gemm_n + 3) / 4);
   hipLaunchKernelGGL(rowdot<short>, rgrid, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n,
-                     static_cast<const unsigned long long*>(vacol), vexpC);
+                     static_cast<const uint32_t*>(vacol), vexpC);
   hipLaunchKernelGGL(rowdot<float>, rgrid, dim3(256), 0, s, static_cast<const float*>(c), gemm_n, gemm_n,
-                     static_cast<const unsigned long long*>(nullptr), vrowC);
+                     static_cast<const uint32_t*>(nullptr), vrowC);
   hipLaunchKernelGGL(rowdot<short>, rgrid, dim3(256), 0, s, static_cast<const short*>(a), gemm_n, gemm_n,
-                     static_cast<const unsigned long long*>(vbcol), vexpR);
-  hipLaunchKernelGGL(count_ne_u64, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vcolC, vexpC, gemm_n, cnt + kSlotAbft);
-  hipLaunchKernelGGL(count_ne_u64, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vrowC, vexpR, gemm_n, cnt + kSlotAbft);
+                     static_cast<const uint32_t*>(vbcol), vexpR);
+  hipLaunchKernelGGL(count_ne_u32, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vcolC, vexpC, gemm_n, cnt + kSlotAbft);
+  hipLaunchKernelGGL(count_ne_u32, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vrowC, vexpR, gemm_n, cnt + kSlotAbft);
   PROBE_CHECK(hipGetLastError());
   PROBE_CHECK(hipMemcpyAsync(hres + kSlotSmall, cnt + kSlotSmall, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                              s));
@@ -654,9 +701,26 @@ std::string run_probe(int dev, const char* opts) {
   const size_t gemm_bytes = do_mfma ? 2 * sz_a0 + 2 * sz_c0 + 2 * sz_a + sz_c + sz_v : 0;
   const size_t hbm_region = align(n16 * 16);
   const size_t region = hbm_region + gemm_bytes;
-  DevBuf arena;
-  PROBE_CHECK(hipMalloc(&arena.p, region + align(kResSlots * sizeof(unsigned long long))));
-  char* base = static_cast<char*>(arena.p);
+  const size_t need = region + align(kResSlots * sizeof(unsigned long long));
+  const bool keep = opt_int(opts, "keepArena", 1) != 0;
+  if (ctx.arena && (ctx.arena_bytes < need || ctx.arena_bytes > 2 * need)) {
+    (void)hipFree(ctx.arena);
+    ctx.arena = nullptr;
+    ctx.arena_bytes = 0;
+  }
+  const bool reused = ctx.arena != nullptr;
+  if (!ctx.arena) {
+    PROBE_CHECK(hipMalloc(&ctx.arena, need));
+    ctx.arena_bytes = need;
+  }
+  ctx.arena_used = std::chrono::steady_clock::now();
+  DevBuf transient;  // owns the arena for this probe only when it is not kept
+  if (!keep) {
+    transient.p = ctx.arena;
+    ctx.arena = nullptr;
+    ctx.arena_bytes = 0;
+  }
+  char* base = static_cast<char*>(keep ? ctx.arena : transient.p);
   auto* cnt = reinterpret_cast<unsigned long long*>(base + region);
   unsigned long long* hres = ctx.host_res;
   const double alloc_ms = ms_since(t_alloc);
@@ -737,8 +801,10 @@ std::string run_probe(int dev, const char* opts) {
   const double hbm_gbps = 2.0 * bytes_moved / ((write_ms + read_ms) * 1e-3) / 1e9;
   const bool hbm_ok = bad_bits == 0;
   auto t_free = std::chrono::steady_clock::now();
-  (void)hipFree(arena.p);
-  arena.p = nullptr;
+  if (transient.p) {
+    (void)hipFree(transient.p);
+    transient.p = nullptr;
+  }
   const double free_ms = ms_since(t_free);
   double total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::string out = "{";
@@ -756,7 +822,8 @@ std::string run_probe(int dev, const char* opts) {
          ",\"elementMismatches\":" + std::to_string(small_bad) + ",\"abftMismatches\":" + std::to_string(abft_bad) +
          ",\"tflops\":" + jnum(tflops) + ",\"ms\":" + jnum(gemm_ms) + "}";
   out += ",\"ms\":" + jnum(total_ms);
-  out += ",\"phases\":{\"setupMs\":" + jnum(setup_ms) + ",\"allocMs\":" + jnum(alloc_ms) +
+  out += ",\"phases\":{\"arenaReused\":" + std::string(reused ? "true" : "false") +
+         ",\"setupMs\":" + jnum(setup_ms) + ",\"allocMs\":" + jnum(alloc_ms) +
          ",\"hbmWallMs\":" + jnum(hbm_wall_ms) + ",\"mfmaWallMs\":" + jnum(mfma_wall_ms) + ",\"freeMs\":" + jnum(free_ms) +
          "}";
   out += "}";
@@ -842,7 +909,7 @@ int mi355x_probe_init(char* err, size_t errlen) {
     if (hipSetDevice(d) != hipSuccess) continue;
     (void)hipFree(nullptr);
     try {
-      (void)run_probe(d, "{\"hbmBytes\":1048576,\"patterns\":1,\"gemmN\":256,\"gemmReps\":1}");
+      (void)run_probe(d, "{\"hbmBytes\":1048576,\"patterns\":1,\"gemmN\":256,\"gemmReps\":1,\"keepArena\":0}");
     } catch (const std::exception&) {
       // a broken device fails its real probe later with the actual error
     }
@@ -891,6 +958,24 @@ char* mi355x_probe_peer(int src, int dst, const char* opts_json) {
     return dup(std::string("{\"src\":") + std::to_string(src) + ",\"dst\":" + std::to_string(dst) +
                ",\"passed\":false,\"error\":" + jstr(e.what()) + "}");
   }
+}
+
+// Frees the probe arenas idle for at least ``idle_ms`` (0: all); returns how many were freed.
+int mi355x_probe_trim(int idle_ms) {
+  if (g_count <= 0) return 0;
+  int freed = 0;
+  const auto now = std::chrono::steady_clock::now();
+  for (int d = 0; d < g_count; ++d) {
+    std::lock_guard<std::mutex> g(device_mutex(d));
+    DeviceCtx& ctx = g_ctx[static_cast<size_t>(d)];
+    if (!ctx.arena || now - ctx.arena_used < std::chrono::milliseconds(idle_ms)) continue;
+    if (hipSetDevice(d) != hipSuccess) continue;
+    (void)hipFree(ctx.arena);
+    ctx.arena = nullptr;
+    ctx.arena_bytes = 0;
+    ++freed;
+  }
+  return freed;
 }
 
 void mi355x_probe_free(char* p) { std::free(p); }

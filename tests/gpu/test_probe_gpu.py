@@ -1,7 +1,7 @@
 """Real-MI355X tests of the gfx950 HIP probe kernels (run on the GPU box with ``-m gpu``).
 
 Numerics: the MFMA GEMM is checked bit-exactly against an fp32 VALU reference (256^3, asymmetric
-operands) and exact int64 ABFT checksums (N^3); the HBM test compares every bit. These tests also
+operands) and exact ABFT row/column checksums (N^3, modulo 2^32); the HBM test compares every bit. These tests also
 prove the checkers *detect* corruption by injecting faults between compute and check.
 """
 from __future__ import annotations
@@ -108,3 +108,18 @@ def test_peer_copy_path(hip):
         x = hip.peer(0, 1, 64 << 20)
         assert x["passed"] and x["badBits"] == 0, x
         assert x["GBps"] > 10, x
+
+
+def test_probe_arena_reused_then_trimmed(hip):
+    """The ~1.2 GiB probe arena is kept between back-to-back probes (no hipMalloc on the claim
+    path) and handed back by trim(); a probe after a trim allocates again and still passes."""
+    hip.trim(0)
+    a = hip.run(0, hbm_bytes=1 << 30)
+    b = hip.run(0, hbm_bytes=1 << 30)
+    assert a["passed"] and b["passed"]
+    assert a["phases"]["arenaReused"] is False and b["phases"]["arenaReused"] is True
+    assert b["phases"]["allocMs"] < a["phases"]["allocMs"]
+    assert hip.trim(0) == 1 and hip.trim(0) == 0
+    c = hip.run(0, hbm_bytes=1 << 30)
+    assert c["passed"] and c["phases"]["arenaReused"] is False
+    hip.trim(0)
