@@ -61,13 +61,15 @@ def test_gang_scheduler_invariants(shared, ops):
     names: list[str] = []
     suspended: set[str] = set()
     rejected: set[str] = set()
+    seq = 0
     for op in ops:
         if op[0] == "submit":
             _, replicas, gpus, prio, preempt = op
-            name = f"job{len(names)}"
+            name = f"job{seq}"
+            seq += 1
             names.append(name)
             spec = {"replicas": replicas, "gpusPerReplica": gpus, "priority": prio,
-                    "masterPort": 30000 + len(names),
+                    "masterPort": 30000 + seq,
                     "template": {"spec": {"terminationGracePeriodSeconds": 1, "containers": [{
                         "name": "m", "command": ["sleep", "0.4"]}]}}}
             if preempt:
