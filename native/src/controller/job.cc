@@ -26,6 +26,15 @@ CounterVec& job_events() {
                                                     "Mi355xJob lifecycle transitions by kind.");
   return c;
 }
+GaugeVec& queue_jobs_gauge() {
+  static GaugeVec& g = Registry::global().gauge("gpupool_queue_jobs", "Mi355xJobs per queue and phase.");
+  return g;
+}
+GaugeVec& queue_alloc_gauge() {
+  static GaugeVec& g = Registry::global().gauge("gpupool_queue_allocated_gpus",
+                                                "GPUs held by a queue's placed jobs, per extended resource.");
+  return g;
+}
 HistogramVec& gang_wait_hist() {
   static HistogramVec& h = Registry::global().histogram(
       "gpupool_job_gang_wait_seconds", "From job creation (or gang restart) to its gang placement.",
@@ -863,7 +872,15 @@ Outcome Mi355xQueueReconciler::reconcile(const std::string& ns, const std::strin
   st["completed"] = completed;
   st["failed"] = failed;
   Json a = Json::object();
-  for (const auto& kv : alloc) a[kv.first] = kv.second;
+  for (const auto& kv : alloc) {
+    a[kv.first] = kv.second;
+    queue_alloc_gauge().set({{"queue", name}, {"resource", kv.first}}, static_cast<double>(kv.second));
+  }
+  for (const auto& kv : cur["allocated"].members())  // resources no longer held go to zero
+    if (!alloc.count(kv.first)) queue_alloc_gauge().set({{"queue", name}, {"resource", kv.first}}, 0);
+  const std::pair<const char*, int> phases[] = {{"Pending", pending}, {"Running", running}, {"Suspended", suspended},
+                                                {"Succeeded", completed}, {"Failed", failed}};
+  for (const auto& ph : phases) queue_jobs_gauge().set({{"queue", name}, {"phase", ph.first}}, ph.second);
   st["allocated"] = a;
   write_status_(obj, st);
   return Outcome::done(opts_.resync);

@@ -322,6 +322,10 @@ def test_queue_admission_capability_state_and_status(node8):
                    and q["status"].get("pending") == 1 and q["status"].get("completed") == 1,
                    timeout=20)
     assert q["status"]["allocated"] == {"amd.com/gpu": 2} and q["status"]["state"] == "Open"
+    metrics = node8.manager_metrics()
+    assert 'gpupool_queue_jobs{phase="Running",queue="research"} 2' in metrics
+    assert 'gpupool_queue_allocated_gpus{queue="research",resource="amd.com/gpu"} 2' in metrics
+    assert "gpupool_job_gang_wait_seconds_bucket" in metrics
     r = subprocess.run([os.path.join(ROOT, "bin", "gpuctl"), "--server", node8.url, "get", "mxq"],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "research" in r.stdout and "Open" in r.stdout, r.stdout + r.stderr
