@@ -300,6 +300,12 @@ MI355X_JOB_SPEC = {
     "properties": {
         "replicas": {**_I32, "minimum": 1, "maximum": 1024,
                      "description": "Worker pods (torchrun nnodes); placed all-or-nothing."},
+        "minAvailable": {**_I32, "minimum": 1, "maximum": 1024,
+                         "description": "Elastic gang (Volcano minAvailable): start with as many "
+                                        "workers as fit, but at least this many (default: "
+                                        "replicas). The attempt's world size is then the number "
+                                        "placed (status.workers), handed to PET_NNODES / "
+                                        "WORLD_SIZE."},
         "gpusPerReplica": {**_I32, "minimum": 0, "maximum": 64, "default": 1,
                            "description": "GPUs per pod (torchrun nproc-per-node)."},
         "resourceName": {**_S, "pattern": r"^[a-z0-9.-]+/[a-z0-9.-]+$",
@@ -350,6 +356,7 @@ MI355X_JOB_STATUS = {
                   "enum": ["Pending", "Running", "Restarting", "Suspended", "Succeeded",
                            "Failed"]},
         "replicas": _I32,
+        "workers": {**_I32, "description": "workers placed for the current attempt"},
         "active": _I32,
         "succeeded": _I32,
         "failed": _I32,

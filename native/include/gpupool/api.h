@@ -76,6 +76,7 @@ struct Mi355xPoolSpec {
 // Gang-scheduled distributed training job (schema: gpupool/api/schema.py MI355X_JOB_SPEC).
 struct Mi355xJobSpec {
   int32_t replicas = 1;
+  int32_t min_available = 0;  // 0 = replicas (rigid gang)
   int32_t gpus_per_replica = 1;
   std::string resource_name;  // "" = the poolRef's, else amd.com/gpu
   std::string pool_ref;
@@ -92,6 +93,8 @@ struct Mi355xJobSpec {
   std::string success_policy = "AllWorkers";
   int32_t master_port = 29500;
   Json tmpl;  // PodTemplateSpec
+  // Smallest gang the job may start with (minAvailable clamped to [1, replicas]).
+  int32_t min_workers() const { return min_available > 0 && min_available < replicas ? min_available : replicas; }
   static Mi355xJobSpec from(const Json& spec);
 };
 

@@ -182,7 +182,7 @@ class Mi355xJobReconciler : public PoolReconcilerBase {
   // preempted jobs may still be terminating on it).
   bool capacity_free_(const Mi355xJobSpec& spec, const std::string& resource, const Json& placement);
   Json build_pod_(const Json& job, const ObjectMeta& m, const Mi355xJobSpec& spec, const std::string& resource,
-                  int attempt, const Slot& slot, const std::string& master_addr);
+                  int attempt, int world, const Slot& slot, const std::string& master_addr);
   bool resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec& spec, std::string* resource, std::string* node,
                      std::string* why);
 

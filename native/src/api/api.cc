@@ -151,6 +151,7 @@ std::vector<std::string> validate_azure(const Json& obj) {
 Mi355xJobSpec Mi355xJobSpec::from(const Json& s) {
   Mi355xJobSpec j;
   j.replicas = static_cast<int32_t>(s["replicas"].as_int(1));
+  j.min_available = static_cast<int32_t>(s["minAvailable"].as_int(0));
   j.gpus_per_replica = static_cast<int32_t>(s["gpusPerReplica"].as_int(1));
   j.resource_name = s["resourceName"].as_string();
   j.pool_ref = s["poolRef"].as_string();
@@ -190,6 +191,7 @@ std::vector<std::string> validate_job(const Json& obj) {
   };
   int_range("replicas", 1, 1024, true);
   int_range("gpusPerReplica", 0, 64, false);
+  int_range("minAvailable", 1, 1024, false);
   int_range("backoffLimit", 0, INT32_MAX, false);
   int_range("activeDeadlineSeconds", 0, INT64_MAX, false);
   int_range("ttlSecondsAfterFinished", -1, INT64_MAX, false);

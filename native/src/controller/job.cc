@@ -181,7 +181,10 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     }
   };
   const Json queue = get_queue(spec.queue);
-  const int64_t need_total = static_cast<int64_t>(spec.replicas) * spec.gpus_per_replica;
+  // elastic gangs (minAvailable): any size in [min_r, max_r] workers; max_r may shrink below
+  const int min_r = spec.min_workers();
+  int max_r = spec.replicas;
+  const int64_t need_total = static_cast<int64_t>(min_r) * spec.gpus_per_replica;
   int64_t cap = -1;  // -1 = unlimited
   if (queue.is_null() && spec.queue != "default") {
     *reason = "QueueNotFound";
@@ -209,6 +212,8 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
              std::to_string(need_total) + " needed > capability " + std::to_string(cap);
       return {};
     }
+    if (spec.gpus_per_replica > 0)
+      max_r = static_cast<int>(std::min<int64_t>(max_r, (cap - used) / spec.gpus_per_replica));
   }
   for (const auto& j : jobs["items"].elements()) {
     if (j.path("metadata.uid").as_string() == m.uid || !j.path("metadata.deletionTimestamp").as_string().empty()) continue;
@@ -217,7 +222,8 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     if (phase != "Pending" && phase != "Restarting") continue;
     if (!j.path("status.placement").elements().empty()) continue;  // already placed
     const std::string jres = job_resource(j, resource);
-    int64_t jneed = j.path("spec.replicas").as_int(1) * j.path("spec.gpusPerReplica").as_int(1);
+    const int64_t jrep = j.path("spec.replicas").as_int(1), jmin = j.path("spec.minAvailable").as_int(jrep);
+    int64_t jneed = std::min(jrep, std::max<int64_t>(1, jmin)) * j.path("spec.gpusPerReplica").as_int(1);
     // can never run (bigger than the cluster or than the queue's capability): must not block it
     if (jres == resource && (jneed > cluster_total || (cap >= 0 && jneed > cap))) continue;
     if (key_of(j) < my_key) {
@@ -252,10 +258,15 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
         if (!s["created"].as_bool(false) && free.count(s["node"].as_string())) free[s["node"].as_string()] -= g;
     }
   }
+  // the largest gang in [min_r, max_r] that fits ``f`` (a rigid gang has min_r == max_r)
   auto fit = [&](const std::map<std::string, int64_t>& f) {
     std::vector<std::pair<std::string, int64_t>> cands;
     for (const auto& n : order) cands.emplace_back(n, std::max<int64_t>(0, f.at(n)));
-    return place(cands, spec.replicas, spec.gpus_per_replica);
+    for (int r = max_r; r >= min_r; --r) {
+      auto s = place(cands, r, spec.gpus_per_replica);
+      if (!s.empty()) return s;
+    }
+    return std::vector<Slot>{};
   };
   auto slots = fit(free);
   if (slots.empty() && spec.preemption_policy == "PreemptLowerPriority" && spec.gpus_per_replica > 0 && !order.empty()) {
@@ -315,7 +326,8 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     int64_t total_free = 0;
     for (const auto& n : order) total_free += std::max<int64_t>(0, free[n]);
     *reason = "Unschedulable";
-    *why = "gang of " + std::to_string(spec.replicas) + " x " + std::to_string(spec.gpus_per_replica) + " " +
+    *why = "gang of " + (min_r < spec.replicas ? std::to_string(min_r) + ".." : std::string()) +
+           std::to_string(spec.replicas) + " x " + std::to_string(spec.gpus_per_replica) + " " +
            resource + " does not fit: " + std::to_string(total_free) + " free on " + std::to_string(order.size()) +
            " candidate node(s)";
   }
@@ -344,7 +356,7 @@ bool Mi355xJobReconciler::capacity_free_(const Mi355xJobSpec& spec, const std::s
 }
 
 Json Mi355xJobReconciler::build_pod_(const Json& job, const ObjectMeta& m, const Mi355xJobSpec& spec,
-                                     const std::string& resource, int attempt, const Slot& slot,
+                                     const std::string& resource, int attempt, int world, const Slot& slot,
                                      const std::string& master_addr) {
   Json pod = Json::object();
   pod["apiVersion"] = "v1";
@@ -377,7 +389,7 @@ Json Mi355xJobReconciler::build_pod_(const Json& job, const ObjectMeta& m, const
     c["name"] = "main";
     ps["containers"] = Json::array({c});
   }
-  const int nnodes = spec.replicas, nproc = std::max(1, spec.gpus_per_replica);
+  const int nnodes = world, nproc = std::max(1, spec.gpus_per_replica);
   std::vector<std::pair<std::string, std::string>> env = {
       {"MASTER_ADDR", master_addr},
       {"MASTER_PORT", std::to_string(spec.master_port)},
@@ -683,7 +695,7 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
     st["phase"] = "Pending";
     st["masterAddr"] = "";
     set_condition(conds, gen::kCondScheduled, "True", "GangScheduled",
-                  std::to_string(spec.replicas) + " pod(s) x " + std::to_string(spec.gpus_per_replica) + " " +
+                  std::to_string(slots.size()) + " pod(s) x " + std::to_string(spec.gpus_per_replica) + " " +
                       resource + " placed: " + where,
                   m.generation, now);
     if (attempt > 1) set_condition(conds, gen::kCondRestarting, "False", "Restarted", "attempt " + std::to_string(attempt),
@@ -734,7 +746,8 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
     }
     if (idx != 0 && master_ip.empty()) continue;
     Slot slot{idx, s["node"].as_string()};
-    Json pod = build_pod_(obj, m, spec, resource, attempt, slot, idx == 0 ? "localhost" : master_ip);
+    Json pod = build_pod_(obj, m, spec, resource, attempt, static_cast<int>(placement.size()), slot,
+                          idx == 0 ? "localhost" : master_ip);
     try {
       by_index[idx] = client_.create(res::pods(), m.ns, pod);
       s["created"] = true;
@@ -809,14 +822,16 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
     return finish_(obj, m, spec, st, "Failed",
                    spec.restart_policy == "Never" ? "PodFailed" : "BackoffLimitExceeded", msg, pods);
   }
-  const bool all_done = succeeded == spec.replicas;
+  const int world = static_cast<int>(placement.size());  // workers of this attempt
+  st["workers"] = world;
+  const bool all_done = world > 0 && succeeded == world;
   const bool rank0_done = by_index.count(0) && pod_phase(by_index[0]) == "Succeeded";
   if (all_done || (spec.success_policy == "Rank0" && rank0_done)) {
     st["conditions"] = conds;
     return finish_(obj, m, spec, st, "Succeeded", "JobSucceeded",
-                   std::to_string(succeeded) + "/" + std::to_string(spec.replicas) + " worker(s) succeeded", pods);
+                   std::to_string(succeeded) + "/" + std::to_string(world) + " worker(s) succeeded", pods);
   }
-  if (static_cast<int>(by_index.size()) == spec.replicas && running + succeeded == spec.replicas) {
+  if (world > 0 && static_cast<int>(by_index.size()) == world && running + succeeded == world) {
     if (phase != "Running") {
       event_(obj, "Normal", "JobRunning", std::to_string(running) + " worker(s) running");
       job_events().inc({{"transition", "Running"}});
@@ -824,7 +839,7 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
     st["phase"] = "Running";
     if (cst["startTime"].as_string().empty()) st["startTime"] = now;
     set_condition(conds, gen::kCondRunning, "True", "AllWorkersRunning",
-                  std::to_string(running) + "/" + std::to_string(spec.replicas) + " worker(s) running", m.generation,
+                  std::to_string(running) + "/" + std::to_string(world) + " worker(s) running", m.generation,
                   now);
     st["conditions"] = conds;
     write_status_(obj, st);

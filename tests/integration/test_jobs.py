@@ -387,3 +387,32 @@ def test_gang_spans_nodes_with_torchrun_env(cluster_factory):
                lambda o: conds(o).get("Scheduled", {}).get("reason") == "Unschedulable", timeout=20)
     k.delete(MI355XJOBS, "wide", "default")
     k.wait_for(MI355XJOBS, "small", "default", phase_is("Succeeded"), timeout=30)
+
+
+def test_elastic_gang_min_available(node8):
+    """Volcano minAvailable: a 4-replica job with minAvailable 2 starts with the 3 GPUs free, its
+    world size (status.workers, PET_NNODES, WORLD_SIZE) is 3, and it succeeds with 3 workers; with
+    fewer than minAvailable GPUs free it waits."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 3), "default")
+    wait_ready(k, "pool", 3)
+    k.create(MI355XJOBS, job("el", 4, ["sleep", "1"], minAvailable=2), "default")
+    o = k.wait_for(MI355XJOBS, "el", "default", phase_is("Running", "Succeeded"), timeout=30)
+    assert o["status"]["workers"] == 3 and len(o["status"]["placement"]) == 3
+    pods = job_pods(k, "el")
+    assert len(pods) == 3
+    for p in pods:
+        e = env_of(p)
+        assert e["WORLD_SIZE"] == "3" and e["PET_NNODES"] == "3"
+    o = k.wait_for(MI355XJOBS, "el", "default", phase_is("Succeeded"), timeout=30)
+    assert o["status"]["succeeded"] == 3
+    # 2 of 3 GPUs busy: a minAvailable-2 gang cannot start on the 1 left
+    k.create(MI355XJOBS, job("busy", 2, ["sleep", "600"]), "default")
+    k.wait_for(MI355XJOBS, "busy", "default", phase_is("Running"), timeout=30)
+    k.create(MI355XJOBS, job("el2", 4, ["true"], minAvailable=2), "default")
+    o = k.wait_for(MI355XJOBS, "el2", "default",
+                   lambda o: conds(o).get("Scheduled", {}).get("reason") == "Unschedulable", timeout=20)
+    assert "gang of 2..4" in conds(o)["Scheduled"]["message"]
+    k.delete(MI355XJOBS, "busy", "default")
+    o = k.wait_for(MI355XJOBS, "el2", "default", phase_is("Succeeded"), timeout=30)
+    assert o["status"]["workers"] == 3
