@@ -416,3 +416,25 @@ def test_elastic_gang_min_available(node8):
     k.delete(MI355XJOBS, "busy", "default")
     o = k.wait_for(MI355XJOBS, "el2", "default", phase_is("Succeeded"), timeout=30)
     assert o["status"]["workers"] == 3
+
+
+def test_gpu_fault_under_running_gang_restarts_it_on_healthy_gpus(node8):
+    """Failure handling end to end: an uncorrectable ECC error on a GPU under a running gang makes
+    the pool replace that GPU (drain evicts the worker), the job restarts the whole gang (PodLost)
+    and runs again on healthy GPUs only."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 2, drain={"gracePeriodSeconds": 1}), "default")
+    wait_ready(k, "pool", 2)
+    k.create(MI355XJOBS, job("tr", 2, ["sleep", "600"], poolRef="pool"), "default")
+    o = k.wait_for(MI355XJOBS, "tr", "default", phase_is("Running"), timeout=30)
+    victim = o["status"]["replicaStatuses"][0]["devices"]
+    node8.set_faults("mi355x-node-0", {"devices": {victim: {"ecc": {"uncorrectable": 2}}}})
+    o = k.wait_for(MI355XJOBS, "tr", "default",
+                   lambda o: phase_is("Running")(o) and o["status"]["attempt"] == 2, timeout=60)
+    assert o["status"]["restarts"] == 1
+    assert conds(o)["Restarting"]["reason"] == "Restarted"
+    assert any(e["reason"] == "GangRestarting" and e["involvedObject"]["name"] == "tr"
+               for e in k.list(EVENTS, "default")["items"])
+    devs = {r["devices"] for r in o["status"]["replicaStatuses"]}
+    assert victim not in devs and len(devs) == 2
+    node8.set_faults("mi355x-node-0", {})
