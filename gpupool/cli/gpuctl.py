@@ -154,6 +154,30 @@ def cmd_get(c: Client, ns: str, args) -> int:
         return 0
     tbl = c.table(res, target_ns, args.name, label_selector=args.selector)
     print_table(tbl, wide=args.output == "wide", with_ns=args.all_namespaces and res.namespaced)
+    if args.watch:  # `kubectl get -w` (GPU调度平台搭建.md:682): one row per change, no header
+        sys.stdout.flush()
+        rv = tbl.get("metadata", {}).get("resourceVersion")
+        deadline = time.monotonic() + args.watch_timeout if args.watch_timeout else None
+        for ev in c.watch(res, target_ns, resource_version=rv, label_selector=args.selector,
+                          field_selector=f"metadata.name={args.name}" if args.name else None,
+                          timeout_seconds=int(args.watch_timeout) if args.watch_timeout else None,
+                          bookmarks=False):
+            obj = ev.get("object") or {}
+            md = obj.get("metadata") or {}
+            if ev.get("type") == "DELETED":
+                print(f"{md.get('name', '')}   <deleted>", flush=True)
+            elif ev.get("type") in ("ADDED", "MODIFIED"):
+                try:
+                    row = c.table(res, md.get("namespace") if res.namespaced else None, md["name"])
+                except KubeError:
+                    continue  # gone between the event and the GET
+                for r in row["rows"]:
+                    cells = ["" if x is None else str(x) for x in r["cells"]]
+                    if args.all_namespaces and res.namespaced:
+                        cells = [md.get("namespace", "")] + cells
+                    print("   ".join(cells), flush=True)
+            if deadline and time.monotonic() > deadline:
+                break
     return 0
 
 
@@ -556,6 +580,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-o", "--output", default="")
     p.add_argument("-l", "--selector", default=None)
     p.add_argument("-A", "--all-namespaces", action="store_true")
+    p.add_argument("-w", "--watch", action="store_true", help="after the table, print a row per change")
+    p.add_argument("--watch-timeout", type=float, default=0, help="stop watching after N seconds")
     p = sub.add_parser("describe")
     p.add_argument("kind")
     p.add_argument("name")

@@ -438,3 +438,20 @@ def test_gpu_fault_under_running_gang_restarts_it_on_healthy_gpus(node8):
     devs = {r["devices"] for r in o["status"]["replicaStatuses"]}
     assert victim not in devs and len(devs) == 2
     node8.set_faults("mi355x-node-0", {})
+
+
+def test_gpuctl_get_watch_streams_rows(node8):
+    """`gpuctl get mxp NAME -w` (kubectl get -w, GPU调度平台搭建.md:682): the table, then a row per
+    change until the watch times out."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("wp", 1), "default")
+    wait_ready(k, "wp", 1)
+    proc = subprocess.Popen([os.path.join(ROOT, "bin", "gpuctl"), "--server", node8.url, "get", "mxp",
+                             "wp", "-w", "--watch-timeout", "4"], stdout=subprocess.PIPE, text=True)
+    time.sleep(1.0)
+    k.patch(MI355XPOOLS, "wp", {"spec": {"replicas": 3}}, "default")
+    wait_ready(k, "wp", 3)
+    out, _ = proc.communicate(timeout=30)
+    lines = [x for x in out.splitlines() if x.strip()]
+    assert lines[0].startswith("NAME") and "wp" in lines[1]
+    assert any(x.split()[:3] == ["wp", "3", "3"] for x in lines[2:]), out
