@@ -559,7 +559,53 @@ def cmd_config(args) -> int:
         cfg["current-context"] = args.name
         save_config(cfg)
         print(f"switched to context {args.name}")
+    elif args.config_cmd == "get-contexts":  # GoHai `context list` (GPU调度平台搭建.md:476-482)
+        cur = cfg.get("current-context")
+        print("CURRENT   NAME   SERVER   NAMESPACE")
+        for name, ctx in sorted(cfg["contexts"].items()):
+            print(f"{'*' if name == cur else ' '}   {name}   {ctx.get('server', '')}   "
+                  f"{ctx.get('namespace', 'default')}")
     return 0
+
+
+def cmd_login(args) -> int:
+    """GoHai `login` (GPU调度平台搭建.md:476): store a bearer token (e.g. an OIDC id-token from
+    the identity provider) in a context, creating or switching to it."""
+    cfg = load_config()
+    cfg.setdefault("contexts", {})
+    name = args.context_name or cfg.get("current-context") or "default"
+    ctx = cfg["contexts"].setdefault(name, {})
+    token = args.token_value if args.token_value is not None else sys.stdin.readline().strip()
+    if not token:
+        print("error: empty token", file=sys.stderr)
+        return 1
+    ctx["token"] = token
+    if args.server:
+        ctx["server"] = args.server
+    cfg["current-context"] = name
+    save_config(cfg)
+    print(f"logged in: context {name}")
+    return 0
+
+
+def cmd_whoami(c: Client, ns: str, args) -> int:
+    """GoHai `whoami` (GPU调度平台搭建.md:482): the context, apiserver, namespace and credential in
+    use, and whether the apiserver accepts it."""
+    cfg = load_config()
+    ok = True
+    try:
+        c.request("GET", "/version")
+    except KubeError as e:
+        ok = e.code not in (401, 403)
+    except OSError:
+        ok = False
+    auth = "bearer token" if c.token else "no bearer token (anonymous or client certificate)"
+    print(f"context:    {args.context or cfg.get('current-context') or '-'}")
+    print(f"server:     {c.server}")
+    print(f"namespace:  {ns}")
+    print(f"credential: {auth}")
+    print(f"reachable:  {'yes' if ok else 'no'}")
+    return 0 if ok else 1
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -647,6 +693,11 @@ def build_parser() -> argparse.ArgumentParser:
     sc.add_argument("--token", dest="token", default=None)
     uc = csub.add_parser("use-context")
     uc.add_argument("name")
+    csub.add_parser("get-contexts")
+    p = sub.add_parser("login", help="store a bearer token in a context (reads stdin without --token-value)")
+    p.add_argument("--token-value", default=None)
+    p.add_argument("--context-name", default=None)
+    sub.add_parser("whoami")
     return ap
 
 
@@ -654,11 +705,13 @@ def main(argv: list[str] | None = None) -> int:
     args = build_parser().parse_args(argv)
     if args.cmd == "config":
         return cmd_config(args)
+    if args.cmd == "login":
+        return cmd_login(args)
     c, ns = connection(args)
     fn = {"apply": cmd_apply, "get": cmd_get, "describe": cmd_describe, "delete": cmd_delete,
           "scale": cmd_scale, "wait": cmd_wait, "logs": cmd_logs, "events": cmd_events,
           "devices": cmd_devices, "install": cmd_install, "render": cmd_render,
-          "gpu": cmd_gpu, "trainjob": cmd_trainjob}[args.cmd]
+          "gpu": cmd_gpu, "trainjob": cmd_trainjob, "whoami": cmd_whoami}[args.cmd]
     try:
         return fn(c, ns, args)
     except KubeError as e:

@@ -455,3 +455,22 @@ def test_gpuctl_get_watch_streams_rows(node8):
     lines = [x for x in out.splitlines() if x.strip()]
     assert lines[0].startswith("NAME") and "wp" in lines[1]
     assert any(x.split()[:3] == ["wp", "3", "3"] for x in lines[2:]), out
+
+
+def test_gpuctl_login_contexts_whoami(node8, tmp_path):
+    """GoHai CLI identity verbs (GPU调度平台搭建.md:461-482): login stores a token in a context,
+    config get-contexts lists them, whoami reports the server/namespace/credential in use."""
+    env = {**os.environ, "GPUPOOL_CONFIG": str(tmp_path / "cfg.yaml")}
+
+    def gpuctl(*args, stdin=None):
+        r = subprocess.run([os.path.join(ROOT, "bin", "gpuctl"), *args], capture_output=True,
+                           text=True, timeout=60, env=env, input=stdin)
+        assert r.returncode == 0, r.stdout + r.stderr
+        return r.stdout
+    gpuctl("config", "set-context", "lab", "--server", node8.url, "--namespace", "team-a")
+    assert "logged in: context lab" in gpuctl("login", "--context-name", "lab", stdin="tok-123\n")
+    cfg = yaml.safe_load(open(tmp_path / "cfg.yaml"))
+    assert cfg["contexts"]["lab"]["token"] == "tok-123" and cfg["current-context"] == "lab"
+    assert "*   lab" in gpuctl("config", "get-contexts")
+    who = gpuctl("whoami")
+    assert node8.url in who and "team-a" in who and "bearer token" in who and "reachable:  yes" in who
