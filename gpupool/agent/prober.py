@@ -127,14 +127,15 @@ class Prober:
         return res
 
     def probe_many(self, devs: list[dict], opts: dict) -> list[dict]:
-        futs = [self.pool.submit(self._one, d, opts) for d in devs]
-        out = []
-        for d, f in zip(devs, futs):
+        def guarded(run):
             try:
-                out.append(self.apply_floors(f.result(), d, opts))
+                return run()
             except Exception as e:  # a probe must never take the agent down
-                out.append({"passed": False, "backend": self.mode, "error": repr(e), "ms": 0.0})
-        return out
+                return {"passed": False, "backend": self.mode, "error": repr(e), "ms": 0.0}
+        if len(devs) == 1:  # the caller is already off the event loop: no second thread hop
+            return [self.apply_floors(guarded(lambda: self._one(devs[0], opts)), devs[0], opts)]
+        futs = [self.pool.submit(self._one, d, opts) for d in devs]
+        return [self.apply_floors(guarded(f.result), d, opts) for d, f in zip(devs, futs)]
 
     def peer_ring(self, devs: list[dict], opts: dict) -> dict[str, dict]:
         """xGMI peer check in ring order (dev i -> dev i+1): for each sender uuid, the copy
