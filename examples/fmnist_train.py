@@ -39,6 +39,12 @@ def main() -> int:
     ap.add_argument("--samples", type=int, default=8192, help="synthetic dataset size")
     ap.add_argument("--steps", type=int, default=0, help="stop after N steps (0 = full epochs)")
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--checkpoint_dir", default=os.environ.get("GPUPOOL_CHECKPOINT_DIR", ""),
+                    help="save/resume {model, optimizer, step} here (Mi355xJob spec.checkpointDir)")
+    ap.add_argument("--checkpoint_every", type=int, default=10, help="steps between checkpoints")
+    ap.add_argument("--fail_at_step", type=int, default=0,
+                    help="test hook: exit 3 at this step on job attempt --fail_on_attempt")
+    ap.add_argument("--fail_on_attempt", default="1")
     a = ap.parse_args()
 
     mode = a.mode
@@ -65,7 +71,25 @@ def main() -> int:
         info.update({"gpu": p.name, "arch": getattr(p, "gcnArchName", "")})
     print(json.dumps({"event": "start", **info}), flush=True)
     step, t0, first_loss, loss_v = 0, time.time(), None, float("nan")
-    for epoch in range(a.epochs):
+    start_epoch = 0
+    ckpt = os.path.join(a.checkpoint_dir, "fmnist_ckpt.pt") if a.checkpoint_dir else ""
+    if ckpt and os.path.exists(ckpt):  # a restarted gang resumes instead of starting over
+        st = torch.load(ckpt, map_location=env.device, weights_only=True)
+        (model.module if hasattr(model, "module") else model).load_state_dict(st["model"])
+        opt.load_state_dict(st["opt"])
+        step, start_epoch = int(st["step"]), int(st["epoch"])
+        if env.is_main:
+            print(json.dumps({"event": "resume", "step": step, "epoch": start_epoch}), flush=True)
+
+    def save_checkpoint(epoch: int) -> None:
+        if not ckpt or not env.is_main:
+            return
+        os.makedirs(a.checkpoint_dir, exist_ok=True)
+        tmp = ckpt + ".tmp"
+        torch.save({"model": (model.module if hasattr(model, "module") else model).state_dict(),
+                    "opt": opt.state_dict(), "step": step, "epoch": epoch}, tmp)
+        os.replace(tmp, ckpt)  # atomic: a crash never leaves a torn checkpoint
+    for epoch in range(start_epoch, a.epochs):
         if smp is not None:
             smp.set_epoch(epoch)
         model.train()
@@ -76,6 +100,12 @@ def main() -> int:
             loss.backward()
             opt.step()
             step += 1
+            if ckpt and step % a.checkpoint_every == 0:
+                save_checkpoint(epoch)
+            if a.fail_at_step and step == a.fail_at_step and \
+                    os.environ.get("GPUPOOL_JOB_ATTEMPT", "1") == a.fail_on_attempt:
+                print(json.dumps({"event": "injected_failure", "step": step}), flush=True)
+                sys.exit(3)
             if step % 20 == 0 or step == 1:
                 loss_v = ddp.all_reduce_mean(float(loss.item()), env)
                 first_loss = loss_v if first_loss is None else first_loss

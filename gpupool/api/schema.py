@@ -343,6 +343,10 @@ MI355X_JOB_SPEC = {
         "successPolicy": {"type": "string", "enum": ["AllWorkers", "Rank0"],
                           "default": "AllWorkers"},
         "masterPort": {**_I32, "minimum": 1, "maximum": 65535, "default": 29500},
+        "checkpointDir": {**_S, "description": "Shared directory (e.g. the workspace PVC) passed to "
+                                               "every worker as GPUPOOL_CHECKPOINT_DIR: a gang "
+                                               "restarted after a failure or preemption resumes "
+                                               "from the last checkpoint instead of step 0."},
         "template": {"type": "object", "x-kubernetes-preserve-unknown-fields": True,
                      "description": "Pod template (metadata + spec) of every worker."},
     },

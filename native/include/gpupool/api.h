@@ -92,6 +92,7 @@ struct Mi355xJobSpec {
   std::string clean_pod_policy = "Running";
   std::string success_policy = "AllWorkers";
   int32_t master_port = 29500;
+  std::string checkpoint_dir;  // -> GPUPOOL_CHECKPOINT_DIR
   Json tmpl;  // PodTemplateSpec
   // Smallest gang the job may start with (minAvailable clamped to [1, replicas]).
   int32_t min_workers() const { return min_available > 0 && min_available < replicas ? min_available : replicas; }

@@ -167,6 +167,7 @@ Mi355xJobSpec Mi355xJobSpec::from(const Json& s) {
   j.clean_pod_policy = s["cleanPodPolicy"].str_or("Running");
   j.success_policy = s["successPolicy"].str_or("AllWorkers");
   j.master_port = static_cast<int32_t>(s["masterPort"].as_int(29500));
+  j.checkpoint_dir = s["checkpointDir"].as_string();
   j.tmpl = s["template"].is_object() ? s["template"] : Json::object();
   return j;
 }

@@ -403,6 +403,7 @@ Json Mi355xJobReconciler::build_pod_(const Json& job, const ObjectMeta& m, const
       {"GPUPOOL_JOB_ATTEMPT", std::to_string(attempt)},
       {"GPUPOOL_REPLICA_INDEX", std::to_string(slot.index)},
   };
+  if (!spec.checkpoint_dir.empty()) env.push_back({"GPUPOOL_CHECKPOINT_DIR", spec.checkpoint_dir});
   if (nproc == 1) {  // one process per pod: the pod IS the rank (no torchrun needed)
     env.push_back({"WORLD_SIZE", std::to_string(nnodes)});
     env.push_back({"RANK", std::to_string(slot.index)});

@@ -4,6 +4,7 @@ torchrun/PET rendezvous env, gang restarts, queue order, deadline/TTL/cleanup, a
 :300-306 + :623 Kubeflow PET env)."""
 from __future__ import annotations
 
+import json
 import os
 import subprocess
 import sys
@@ -474,3 +475,27 @@ def test_gpuctl_login_contexts_whoami(node8, tmp_path):
     assert "*   lab" in gpuctl("config", "get-contexts")
     who = gpuctl("whoami")
     assert node8.url in who and "team-a" in who and "bearer token" in who and "reachable:  yes" in who
+
+
+def test_restarted_gang_resumes_from_checkpoint(node8, tmp_path):
+    """Elastic recovery end to end: a 2-rank DDP job with spec.checkpointDir checkpoints every 5
+    steps; attempt 1 dies at step 12, the gang restarts and attempt 2 resumes at step 10 (the
+    last checkpoint), not at 0, and finishes the 20 steps."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 2), "default")
+    wait_ready(k, "pool", 2)
+    cmd = [sys.executable, os.path.join(ROOT, "examples", "fmnist_train.py"), "--synthetic",
+           "--cpu", "--samples", "2048", "--batch_size", "32", "--steps", "20", "--epochs", "1",
+           "--checkpoint_every", "5", "--fail_at_step", "12", "--output", str(tmp_path / "out")]
+    k.create(MI355XJOBS, job("ck", 2, cmd, poolRef="pool", checkpointDir=str(tmp_path / "ckpt")),
+             "default")
+    o = k.wait_for(MI355XJOBS, "ck", "default", phase_is("Succeeded", "Failed"), timeout=180)
+    assert o["status"]["phase"] == "Succeeded" and o["status"]["restarts"] == 1, o["status"]
+    pod0 = next(p for p in job_pods(k, "ck")
+                if p["metadata"]["labels"]["gpupool.amd.com/replica-index"] == "0")
+    assert env_of(pod0)["GPUPOOL_CHECKPOINT_DIR"] == str(tmp_path / "ckpt")
+    log = open(pod0["metadata"]["annotations"]["gpupool.amd.com/log-path"]).read()
+    events = [json.loads(x) for x in log.splitlines() if x.startswith("{")]
+    resume = next(e for e in events if e["event"] == "resume")
+    done = next(e for e in events if e["event"] == "done")
+    assert resume["step"] == 10 and done["steps"] == 20 and done["world"] == 2
