@@ -129,7 +129,8 @@ def test_mi355xjob_torchrun_worker_on_pool_gpu(cluster_factory, tmp_path):
     """Mi355xJob on real hardware: the gang is placed on the pool's GPU, the pod gets the job's
     rendezvous env, and torchrun (driven by PET_*/MASTER_*) starts a distributed-mode worker on
     exactly the allotted GPU (GPU调度平台搭建.md:300-306, :623-635, :638-675). One GPU per box here,
-    so world size is 1; multi-rank rendezvous is covered by the CPU job tests."""
+    so world size is 1; multi-rank rendezvous is covered by the CPU job tests. Attempt 1 fails on
+    purpose at step 25 and the restarted gang resumes from its checkpoint (spec.checkpointDir)."""
     from gpupool.kube import MI355XJOBS
     c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
     k = c.client
@@ -140,11 +141,12 @@ def test_mi355xjob_torchrun_worker_on_pool_gpu(cluster_factory, tmp_path):
               "--nproc-per-node $PET_NPROC_PER_NODE --node-rank $PET_NODE_RANK "
               "--master-addr $MASTER_ADDR --master-port $MASTER_PORT "
               f"examples/fmnist_train.py --mode distributed --synthetic --epochs 1 --steps 40 "
-              f"--output {tmp_path}")
+              f"--checkpoint_every 10 --fail_at_step 25 --output {tmp_path}")
     k.create(MI355XJOBS, {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xJob",
                           "metadata": {"name": "ddp"},
                           "spec": {"replicas": 1, "gpusPerReplica": 1, "poolRef": "p",
-                                   "masterPort": 29731, "backoffLimit": 0,
+                                   "masterPort": 29731, "backoffLimit": 1,
+                                   "checkpointDir": str(tmp_path / "ckpt"),
                                    "template": {"spec": {"containers": [{
                                        "name": "main", "command": ["bash", "-c", script]}]}}}},
              "default")
@@ -159,6 +161,11 @@ def test_mi355xjob_torchrun_worker_on_pool_gpu(cluster_factory, tmp_path):
     assert start["mode"] == "distributed" and start["world"] == 1
     assert start["device"] == "cuda:0" and start["arch"].startswith("gfx950")
     assert start["rocr_visible"] == hip_uuid
+    # attempt 1 died at step 25; the restarted gang resumed from the step-20 checkpoint on the GPU
+    assert done["status"]["restarts"] == 1
+    resume = next(e for e in events if e["event"] == "resume")
+    assert resume["step"] == 20
+    assert next(e for e in events if e["event"] == "done")["steps"] == 40
     assert done["status"]["replicaStatuses"][0]["devices"]
     assert os.path.exists(tmp_path / "fashion_mnist_cnn.pth")
 
