@@ -75,7 +75,12 @@ def test_ddp_job_gang_runs_to_success(node8, tmp_path):
     assert pods["1"]["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "1"
     log = open(pods["0"]["metadata"]["annotations"]["gpupool.amd.com/log-path"]).read()
     assert '"world": 2' in log or "'world': 2" in log, log[-2000:]
-    reasons = [e["reason"] for e in k.list(EVENTS, "default")["items"]]
+    deadline = time.time() + 10  # the manager's event recorder is asynchronous
+    while True:
+        reasons = [e["reason"] for e in k.list(EVENTS, "default")["items"]]
+        if "JobSucceeded" in reasons or time.time() > deadline:
+            break
+        time.sleep(0.05)
     assert "GangScheduled" in reasons and "JobSucceeded" in reasons
 
 
