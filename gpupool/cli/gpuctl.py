@@ -443,8 +443,9 @@ def render_trainjob(tpl: dict) -> dict:
                              "spec": {"containers": [{
                                  "name": "train", "image": tpl.get("image", "rocm/pytorch:latest"),
                                  "command": ["bash", "-lc", cmd], "env": env}]}}}
-    for k in ("poolRef", "queue", "priority", "backoffLimit", "activeDeadlineSeconds",
-              "ttlSecondsAfterFinished", "masterPort"):
+    for k in ("poolRef", "queue", "priority", "preemptionPolicy", "backoffLimit",
+              "activeDeadlineSeconds", "ttlSecondsAfterFinished", "masterPort", "minAvailable",
+              "checkpointDir"):
         if k in spec:
             job_spec[k] = spec[k]
     return {"apiVersion": schema.API_VERSION, "kind": "Mi355xJob",
