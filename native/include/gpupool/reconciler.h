@@ -226,8 +226,9 @@ class Mi355xPoolAutoscaler : public PoolReconcilerBase {
  private:
   Informer& jobs_;
   Informer& pods_;
-  // pool uid -> last time demand was >= spec.replicas (the scale-down delay runs from there)
-  std::map<std::string, std::chrono::steady_clock::time_point> busy_since_;
+  // pool uid -> first pass that saw demand below spec.replicas (the scale-down delay runs from
+  // there; a restarted manager starts it over, so it never shrinks early)
+  std::map<std::string, std::chrono::steady_clock::time_point> low_since_;
 };
 
 // Controller: a shared work queue + N workers dispatching "Kind/ns/name" keys to reconcilers,

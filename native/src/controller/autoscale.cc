@@ -82,7 +82,7 @@ Outcome Mi355xPoolAutoscaler::reconcile(const std::string& ns, const std::string
   Mi355xPoolSpec spec = Mi355xPoolSpec::from(obj["spec"]);
   if (m.deleting() || !spec.autoscale) {
     std::lock_guard<std::mutex> g(mu_);
-    busy_since_.erase(m.uid);
+    low_since_.erase(m.uid);
     return Outcome::done(ms(0));
   }
   const int64_t d = demand(pods_.list(), jobs_.list(), m.ns, m.name, spec.resource_name);
@@ -92,13 +92,13 @@ Outcome Mi355xPoolAutoscaler::reconcile(const std::string& ns, const std::string
   const auto now = std::chrono::steady_clock::now();
   ms wait{0};
   {
+    // The delay runs from the first pass that saw demand below spec.replicas (a long-idle steady
+    // state must not make a later drop shrink the pool at once); any pass at or above resets it.
     std::lock_guard<std::mutex> g(mu_);
-    auto it = busy_since_.find(m.uid);
-    if (target >= spec.replicas || it == busy_since_.end()) {
-      busy_since_[m.uid] = now;  // a fresh manager starts the delay over: never shrink early
-      it = busy_since_.find(m.uid);
-    }
-    if (target < spec.replicas) {
+    if (target >= spec.replicas) {
+      low_since_.erase(m.uid);
+    } else {
+      auto it = low_since_.emplace(m.uid, now).first;
       const auto due = it->second + std::chrono::seconds(spec.scale_down_delay_seconds);
       if (now < due) wait = std::chrono::duration_cast<ms>(due - now) + ms(20);
     }
@@ -120,7 +120,7 @@ Outcome Mi355xPoolAutoscaler::reconcile(const std::string& ns, const std::string
             Json::object().set("pool", m.key()).set("from", spec.replicas).set("to", target).set("demand", d));
   {
     std::lock_guard<std::mutex> g(mu_);
-    busy_since_[m.uid] = now;
+    low_since_.erase(m.uid);
   }
   return Outcome::done(opts_.resync);
 }

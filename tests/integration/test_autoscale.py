@@ -66,3 +66,23 @@ def test_min_replicas_floor_and_disable(cluster_factory):
     wait_ready(k, "warm", 3)
     time.sleep(0.5)
     assert k.get(MI355XPOOLS, "warm", "default")["spec"]["replicas"] == 3
+
+
+def test_scale_down_delay_counts_from_the_drop(cluster_factory):
+    """A long steady state must not shorten the delay: after demand has been constant for longer
+    than scaleDownDelaySeconds, a drop still waits the full delay before the pool shrinks."""
+    k = cluster_factory().client
+    k.create(MI355XPOOLS, mi_pool("steady", 0, resourceName=RES, drain={"gracePeriodSeconds": 1},
+                                  autoscale={"enabled": True, "maxReplicas": 4,
+                                             "scaleDownDelaySeconds": 3}), "default")
+    for n in ("s0", "s1"):
+        k.create(PODS, pause_pod(n, resource=RES), "default")
+    wait_ready(k, "steady", 2)
+    running(k, "s0")
+    time.sleep(4.0)  # steady for longer than the delay
+    k.delete(PODS, "s1", "default")
+    t0 = time.monotonic()
+    time.sleep(1.5)
+    assert k.get(MI355XPOOLS, "steady", "default")["spec"]["replicas"] == 2
+    wait_ready(k, "steady", 1, timeout=30)
+    assert time.monotonic() - t0 >= 2.5
