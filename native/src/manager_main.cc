@@ -552,6 +552,9 @@ int main(int argc, char** argv) {
       pods.start();
       queues.start();
     }
+    if (want_mi && !want_job)
+      log.warn("pool autoscaling (spec.autoscale) is off: it needs the job controller's pod and job caches",
+               Json::object().set("kinds", f.kinds).set("hint", "add 'job' to --kinds"));
     if (want_az) {
       ctl.add_reconciler(&az);
       azpools.add_handler(pool_handler("AzureVmPool"));
