@@ -3,9 +3,11 @@
 // a shared rate-limited work queue with N workers, the providers, an Event recorder, Lease leader
 // election, Prometheus /metrics and /healthz, and one long-poll per node agent so device health
 // changes trigger reconciles immediately (event-driven, no polling sleeps on the hot path).
+// With `job` in --kinds it also runs the Mi355xJob gang scheduler, the Mi355xQueue status
+// controller and the demand-driven pool autoscaler (pod + job informers).
 //
 //   gpupool-manager --apiserver http://127.0.0.1:6443 [--namespace NS] [--workers 4]
-//       [--kinds mi355x,azure] [--leader-elect] [--metrics-addr :8080] [--health-addr :8081]
+//       [--kinds mi355x,azure,job] [--leader-elect] [--metrics-addr :8080] [--health-addr :8081]
 //       [--resync 10s] [--fakecloud-state f.json] [--fakecloud-provision-ms N]
 //   gpupool-manager --validate obj.json     # validation parity check; prints JSON errors
 #include <signal.h>
