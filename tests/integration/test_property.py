@@ -67,8 +67,8 @@ def test_random_edits_and_faults_converge(shared, ops, final):
     ra, rb = final
     k.patch(MI355XPOOLS, "pa", {"spec": {"replicas": ra}}, ns)
     k.patch(MI355XPOOLS, "pb", {"spec": {"replicas": rb}}, ns)
-    a = k.wait_for(MI355XPOOLS, "pa", ns, ready_at(ra), timeout=45)
-    b = k.wait_for(MI355XPOOLS, "pb", ns, ready_at(rb), timeout=45)
+    a = k.wait_for(MI355XPOOLS, "pa", ns, ready_at(ra), timeout=90)
+    b = k.wait_for(MI355XPOOLS, "pb", ns, ready_at(rb), timeout=90)
     ua = {d["uuid"] for d in a["status"]["devices"]}
     ub = {d["uuid"] for d in b["status"]["devices"]}
     assert not ua & ub
