@@ -36,8 +36,8 @@ def test_config3_scale_up_1_to_8(node8):
         uuids = [d["uuid"] for d in o["status"]["devices"]]
         assert len(set(uuids)) == r and seen <= set(uuids)  # scale-up keeps existing GPUs
         seen = set(uuids)
-        node = k.get(NODES, "mi355x-node-0")
-        assert node["status"]["allocatable"]["amd.com/gpu"] == str(r)
+        k.wait_for(NODES, "mi355x-node-0", None, lambda n, r=r: (n["status"].get("allocatable") or {})
+                   .get("amd.com/gpu") == str(r), timeout=20)  # kubelet status is asynchronous
     view = agent_view(node8)
     assert sum(1 for d in view["devices"] if d.get("poolUID")) == 8
     assert conds(o)["Progressing"]["reason"] == "Stable"
@@ -119,7 +119,8 @@ def test_config5_two_pools_with_health_conditions(node8):
     node8.set_faults("mi355x-node-0", {})
     wait_ready(k, "team-a", 4)
     # device plugin: the unhealthy GPU was advertised Unhealthy while faulted -> now healthy again
-    assert k.get(NODES, "mi355x-node-0")["status"]["allocatable"]["amd.com/gpu-team-a"] == "4"
+    k.wait_for(NODES, "mi355x-node-0", None, lambda n: (n["status"].get("allocatable") or {}).get(
+        "amd.com/gpu-team-a") == "4", timeout=20)  # kubelet node status follows asynchronously
 
 
 def test_replace_on_failure(cluster_factory):
