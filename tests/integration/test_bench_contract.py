@@ -1,0 +1,61 @@
+"""bench.py output contract on the CPU (fake 8x MI355X backend): the driver's JSON line, the
+replicas sweep (per_n 1/2/4/8), config 4 scale-down, config 5 two pools and the health latencies."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+pytestmark = pytest.mark.slow
+
+
+def run_bench(*args: str, timeout: float = 600) -> dict:
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--backend", "fake", *args],
+                       capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
+    out = run_bench("--gpus", "8", "--steps", "1", "--warmup", "0", "--scale-down-steps", "1",
+                    "--pool-steps", "1", "--health-steps", "1")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out
+    assert out["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert out["n_gpus"] == 8 and out["higher_is_better"] is False and out["unit"] == "s"
+    assert "apiserver-sim" in out["data"] and "fake" in out["data"]
+    cfg = out["config"]
+    assert sorted(cfg["per_n"], key=int) == ["1", "2", "4", "8"]
+    for k, v in cfg["per_n"].items():
+        assert v["accuracy"] == 1.0 and 0 < v["p50_s"] < 30, (k, v)
+    assert out["value"] == cfg["per_n"]["8"]["p50_s"]
+    assert cfg["readyReplicas_accuracy"] == 1.0
+    # ground-truth time is reported apart from the operator's own time
+    assert cfg["operator_ms_per_step"] + cfg["ground_truth_ms_per_step"] == \
+        pytest.approx(out["ms_per_step"], abs=0.05)
+    sd = cfg["scale_down"]
+    assert sd["from"] == 8 and sd["to"] == 4 and sd["accuracy"] == 1.0
+    assert sd["evicted_per_step"] == [4] and sd["pods_left_on_released_gpus"] == 0
+    tp = cfg["two_pools"]
+    assert tp["pools"] == [4, 4] and tp["accuracy"] == 1.0 and tp["cross_pool_devices"] == 0
+    h = cfg["health_condition_latency"]
+    for k in ("fault_to_condition_p50_s", "forced_sample_to_condition_p50_s",
+              "fault_cleared_to_ready_p50_s"):
+        assert h[k] is not None and h[k] < 30
+
+
+def test_bench_gpus1_contract(native_built):
+    out = run_bench("--gpus", "1", "--steps", "2", "--warmup", "0", "--scale-down-steps", "1",
+                    "--pool-steps", "1", "--health-steps", "0")
+    cfg = out["config"]
+    assert list(cfg["per_n"]) == ["1"] and out["value"] == cfg["per_n"]["1"]["p50_s"]
+    assert cfg["scale_down"]["from"] == 1 and cfg["scale_down"]["to"] == 0
+    assert cfg["scale_down"]["accuracy"] == 1.0
+    assert "skipped" in cfg["two_pools"]
