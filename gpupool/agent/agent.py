@@ -103,6 +103,9 @@ class Agent:
         self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0, "rechecks": 0,
                       "probe_ms_sum": 0.0, "samples": 0}
         self._pods_cache: tuple[float, dict[str, list[dict]]] = (0.0, {})
+        self._pods_refreshing = False
+        from .podresources import PodResourcesClient
+        self._podres = PodResourcesClient(cfg.pod_resources) if cfg.pod_resources else None
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self._evaluate_all()
@@ -168,6 +171,11 @@ class Agent:
                 self.sample()
             except Exception:
                 log.exception("health sample failed")
+            if self._podres is not None:
+                try:
+                    self._refresh_pods()
+                except Exception as e:
+                    log.debug("podresources list failed: %s", e)
             try:
                 self.recheck_probes()
             except Exception:
@@ -250,25 +258,47 @@ class Agent:
     def _pods_by_device(self, fresh: bool = False) -> dict[str, list[dict]]:
         """device ID -> pods holding it, from the kubelet's PodResources API.
 
-        Views (``fresh=False``) may use a 50 ms cache and keep the last known answer while the
-        kubelet is unreachable. Release decisions pass ``fresh=True``: they always ask the kubelet
-        and raise if it cannot answer, so a stale or failed lookup can never free a GPU that a pod
-        still holds."""
+        Views (``fresh=False``) never wait for the kubelet: they return the last answer and, when
+        it is older than 50 ms, start one background refresh (single-flight). A refresh that
+        changes which pods hold a pool's GPUs bumps that pool, so a drain waiting for evicted pods
+        to end is woken by the change itself. The sampler also refreshes every period. Release
+        decisions pass ``fresh=True``: they always ask the kubelet synchronously and raise if it
+        cannot answer, so a stale or failed lookup can never free a GPU that a pod still holds."""
         if not self.cfg.pod_resources:
             return {}
+        if fresh:
+            return self._refresh_pods()
         ts, cache = self._pods_cache
-        if not fresh and time.monotonic() - ts < 0.05:
-            return cache
-        from .podresources import list_pod_devices
-        try:
-            cache = list_pod_devices(self.cfg.pod_resources)
-        except Exception as e:  # kubelet down: keep last known view
-            log.debug("podresources list failed: %s", e)
-            if fresh:
-                raise
-            return cache
-        self._pods_cache = (time.monotonic(), cache)
+        if time.monotonic() - ts >= 0.05:
+            self._refresh_pods_async()
         return cache
+
+    def _refresh_pods(self) -> dict[str, list[dict]]:
+        pods = self._podres.list_pod_devices()
+        with self.lock:
+            old = self._pods_cache[1]
+            self._pods_cache = (time.monotonic(), pods)
+            flipped = {u for u in set(old) | set(pods) if old.get(u) != pods.get(u)}
+            pools = {self.records[u]["poolUID"] for u in flipped if u in self.records}
+        if pools:
+            self._bump(pools)
+        return pods
+
+    def _refresh_pods_async(self) -> None:
+        with self.lock:
+            if self._pods_refreshing:
+                return
+            self._pods_refreshing = True
+
+        def run():
+            try:
+                self._refresh_pods()
+            except Exception as e:  # kubelet down: keep the last known view
+                log.debug("podresources list failed: %s", e)
+            finally:
+                with self.lock:
+                    self._pods_refreshing = False
+        threading.Thread(target=run, daemon=True, name="podres-refresh").start()
 
     def _advertisable(self, uuid: str) -> bool:
         rec = self.records.get(uuid)
@@ -729,6 +759,11 @@ class Agent:
 
     # ================================================================ lifecycle
     def start_background(self) -> None:
+        if self._podres is not None:
+            try:
+                self._refresh_pods()
+            except Exception as e:  # kubelet not up yet: the sampler retries every period
+                log.info("podresources not reachable yet: %s", e)
         for res in {r.get("resourceName", schema.DEFAULT_RESOURCE) for r in self.records.values()}:
             self._ensure_plugin(res)
         t = threading.Thread(target=self._sampler, daemon=True, name="sampler")
@@ -756,7 +791,9 @@ def build_app(agent: Agent) -> web.Application:
         return await asyncio.get_running_loop().run_in_executor(None, fn, *a)
 
     async def node(request):
-        return web.json_response(await run_blocking(agent.node_view))
+        # served on the event loop: node_view never blocks on I/O (cached pod map), and skipping
+        # the executor hop saves a thread wake-up on every reconcile's observe
+        return web.json_response(agent.node_view())
 
     async def claims(request):
         body = await request.json()

@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import json
 import os
+import time
 
 import pytest
 import yaml
@@ -78,7 +79,13 @@ def test_scale_up_down_and_cleanup(azure):
     k.wait_for(AZUREVMPOOLS, "gpu-pool-prod", "default", lambda o: o is None, timeout=20)
     st = cloud(azure)
     assert st["vms"] == []  # VM + NIC + OS disk all gone (README.md:216, :239)
-    reasons = {e["reason"] for e in k.list(EVENTS, "default")["items"]}
+    # the event recorder posts asynchronously (aggregated, off the reconcile path): wait for it
+    deadline = time.monotonic() + 10
+    while True:
+        reasons = {e["reason"] for e in k.list(EVENTS, "default")["items"]}
+        if {"VMCreating", "VMDeleting", "Finalized"} <= reasons or time.monotonic() > deadline:
+            break
+        time.sleep(0.05)
     assert {"VMCreating", "VMDeleting", "Finalized"} <= reasons
 
 
