@@ -34,6 +34,14 @@ def lib() -> ctypes.CDLL:
             l.mi355x_probe_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
             l.mi355x_probe_trim.restype = ctypes.c_int
             l.mi355x_probe_trim.argtypes = [ctypes.c_int]
+            l.mi355x_probe_hbm_sweep.restype = ctypes.c_void_p
+            l.mi355x_probe_hbm_sweep.argtypes = [ctypes.c_int, ctypes.c_char_p]
+            l.mi355x_probe_sweep_release.restype = ctypes.c_int
+            l.mi355x_probe_sweep_release.argtypes = [ctypes.c_int]
+            l.mi355x_probe_gemm_bf16.restype = ctypes.c_int
+            l.mi355x_probe_gemm_bf16.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int]
             _lib = l
     return _lib
 
@@ -99,3 +107,26 @@ def trim(idle_ms: int = 0) -> int:
     """Free the probe arenas (kept between probes to skip a ~1.2 GiB hipMalloc) that have been idle
     for at least ``idle_ms``; returns how many were freed."""
     return int(lib().mi355x_probe_trim(int(idle_ms)))
+
+
+def hbm_sweep(dev: int, offset: int, nbytes: int = 16 << 30, reserve: int = 4 << 30,
+              keep: bool = False, **test_hooks: int) -> dict:
+    """Pattern-test HBM window [offset, offset+nbytes) of a buffer spanning all free HBM minus
+    ``reserve`` (the rotating sweep that covers the whole 288 GB over successive calls). With
+    ``keep`` the big buffer stays allocated for the next window (free it with sweep_release)."""
+    opts = json.dumps({"offset": int(offset), "bytes": int(nbytes), "reserve": int(reserve),
+                       "keep": bool(keep), **{k: int(v) for k, v in test_hooks.items()}})
+    return _take(lib().mi355x_probe_hbm_sweep(dev, opts.encode()))
+
+
+def sweep_release(dev: int) -> int:
+    return int(lib().mi355x_probe_sweep_release(dev))
+
+
+def gemm_bf16(dev: int, a_ptr: int, bt_ptr: int, c_ptr: int, m: int, n: int, k: int) -> None:
+    """The probe's production MFMA GEMM on caller HOST buffers (C fp32 [m,n] = A bf16 [m,k] x
+    Bt bf16 [n,k]^T; e.g. CPU torch tensors' ``data_ptr()``), for independent numerics checks."""
+    rc = lib().mi355x_probe_gemm_bf16(dev, a_ptr, bt_ptr, c_ptr, m, n, k)
+    if rc != 0:
+        raise ValueError(f"mi355x_probe_gemm_bf16 failed (rc={rc}): m,n % 256 and k % 64 must be "
+                         f"0 and the device index valid")

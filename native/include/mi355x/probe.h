@@ -19,14 +19,31 @@ int mi355x_probe_init(char* err, size_t errlen);
 int mi355x_probe_device_count(void);
 /* {"device","hipUUID","name","gcnArch","bdf","totalMem","computeUnits"} */
 char* mi355x_probe_identify(int device);
-/* opts: {"hbmBytes":1073741824,"patterns":2,"mfma":true,"gemmN":4096,"gemmReps":3}
- * -> {"passed":bool,"hbm":{...,"GBps"},"mfma":{...,"tflops"},"ms":...} */
+/* opts: {"hbmBytes":1073741824,"patterns":2,"mfma":true,"gemmN":4096,"gemmReps":3,
+ *        "requireAllCUs":true}
+ * -> {"passed":bool,"hbm":{...,"GBps"},"mfma":{...,"tflops"},
+ *     "cus":{"expected","mfmaVerified","perXcd":[8],"gemmTiles","badWaves","ok"},"ms":...}
+ * cus: every CU's matrix cores are exercised by a census kernel (chained MFMAs checked exactly per
+ * wave, the CU identified by its XCC_ID/HW_ID registers); with requireAllCUs the probe fails
+ * unless mfmaVerified >= the runtime's CU count. gemmTiles = CUs that ran tiles of the timed GEMM. */
 char* mi355x_probe_run(int device, const char* opts_json);
 /* xGMI peer check: src writes a pattern, copies it to dst over the peer link
  * (hipMemcpyPeerAsync after hipDeviceEnablePeerAccess), dst verifies every bit.
  * opts: {"bytes":268435456}. src == dst runs the same path as a local device copy.
  * -> {"src","dst","canAccessPeer":bool,"passed":bool,"badBits","GBps","ms"} */
 char* mi355x_probe_peer(int src, int dst, const char* opts_json);
+/* One window of the rotating HBM sweep: a buffer of all free HBM minus "reserve" bytes is
+ * allocated (kept across calls while "keep" is true; released by mi355x_probe_sweep_release) and
+ * [offset, offset+bytes) of it is pattern-tested in both polarities.
+ * opts: {"offset":0,"bytes":17179869184,"reserve":4294967296,"keep":false,"injectBitFlips":0}
+ * -> {"passed","offset","bytes","span","badBits","firstBadOffset","GBps","ms","allocMs"} */
+char* mi355x_probe_hbm_sweep(int device, const char* opts_json);
+int mi355x_probe_sweep_release(int device);
+/* The probe's production GEMM (256x256x64 MFMA tile) on caller HOST buffers (copied in and out):
+ * C[m][n] (fp32) = A[m][k] (bf16, row-major) * Bt[n][k]^T (bf16, row-major). m, n multiples of
+ * 256, k of 64. For independent numerics checks against a CPU torch.matmul (torch bundles its own
+ * HIP runtime, so device pointers cannot be shared with it in one process). 0 = ok. */
+int mi355x_probe_gemm_bf16(int device, const void* A, const void* Bt, void* C, int m, int n, int k);
 void mi355x_probe_free(char* p);
 
 #ifdef __cplusplus

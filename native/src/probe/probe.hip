@@ -49,6 +49,7 @@ struct ProbeError : std::runtime_error {
 using bf16x8 = __attribute__((ext_vector_type(8))) short;
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;  // native vector: 16-B global ops
 using f32x16 = __attribute__((ext_vector_type(16))) float;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 // ------------------------------------------------------------------ HBM pattern test
 __device__ __forceinline__ uint32_t pattern_word(uint64_t idx, uint32_t seed) {
@@ -151,6 +152,63 @@ __global__ void gen_operand(short* __restrict__ out, uint64_t n, uint32_t seed, 
 
 __device__ __forceinline__ float bf16_to_f32(short s) {
   return __uint_as_float(static_cast<uint32_t>(static_cast<uint16_t>(s)) << 16);
+}
+
+// ------------------------------------------------------------------ CU identity + MFMA census
+// The hardware identity of the CU a wave runs on: XCC_ID (which XCD) and HW_ID's SE/SH/CU fields
+// (CDNA3/4 ISA "HW_ID": CU_ID [11:8], SH_ID [12], SE_ID [15:13]). Both are read-only hardware
+// registers (s_getreg), packed into an 11-bit key: xcc[10:8] se[7:5] sh[4] cu[3:0].
+constexpr int kCuKeys = 2048, kCuMapWords = kCuKeys / 64;
+
+__device__ __forceinline__ int cu_key() {
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  return static_cast<int>(((xcc & 7u) << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u));
+}
+
+__device__ __forceinline__ void mark_cu(unsigned long long* map) {
+  const int k = cu_key();
+  atomicOr(&map[k >> 6], 1ull << (k & 63));
+}
+
+// Every CU must prove its matrix cores: each wave chains ``iters`` v_mfma_f32_16x16x32_bf16 on
+// operands A[r][k] = fa(r), B[c][k] = gb(c) (small integers from the runtime seed, so nothing folds
+// at compile time) and checks every accumulator against iters * 32 * fa(r) * gb(c), exact in fp32.
+// A wave whose result is exact sets its CU's bit; a wrong result counts into ``bad``. The grid is
+// several waves per CU slot so the dispatcher places work on every CU of every XCD.
+constexpr int kCensusThreads = 256;
+__global__ __launch_bounds__(kCensusThreads) void cu_census(unsigned long long* __restrict__ map,
+                                                            unsigned long long* __restrict__ bad, int iters,
+                                                            uint32_t seed, int fault_xcc) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t h = seed ^ (blockIdx.x * 0x9E3779B1u);
+  const int fa = 1 + static_cast<int>((h + (lane & 15)) & 3);          // row value of this lane's A fragment
+  const int gb = 1 + static_cast<int>(((h >> 8) + (lane & 15)) & 3);   // col value of this lane's B fragment
+  const short a16 = static_cast<short>(__float_as_uint(static_cast<float>(fa)) >> 16);
+  const short b16 = static_cast<short>(__float_as_uint(static_cast<float>(gb)) >> 16);
+  bf16x8 av, bv;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    av[j] = a16;
+    bv[j] = b16;
+  }
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < iters; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+  if (fault_xcc >= 0 && (cu_key() >> 8) == fault_xcc) acc[0] += 1.0f;  // test hook: a "bad" XCD
+  // C/D layout of 16x16x32: col = lane&15, row = 4*(lane>>4) + j; fa of row r is held by lane r
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = 4 * (lane >> 4) + j;
+    const int far = 1 + static_cast<int>((h + r) & 3);
+    ok = ok && acc[j] == static_cast<float>(iters * 32 * far * gb);
+  }
+  const bool wave_ok = __all(ok);
+  if (lane == 0) {
+    if (wave_ok) mark_cu(map);
+    else atomicAdd(bad, 1ull);
+  }
 }
 
 // ------------------------------------------------------------------ MFMA GEMM  C = A * Bt^T
@@ -271,7 +329,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_mfma_nt(const short
 constexpr int G2_BM = 256, G2_BN = 256, G2_BK = 64;
 constexpr int kGemm2Threads = 512;
 constexpr int G2_STAGE_SHORTS = (G2_BM + G2_BN) * G2_BK;  // one stage: A then B, 64 KiB
-using f32x4 = __attribute__((ext_vector_type(4))) float;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 // byte offset, inside a [rows][64] bf16 tile (128-B rows), of logical 16-B chunk c of row r
@@ -280,8 +337,10 @@ __device__ __forceinline__ int g2_swz(int r, int c) { return r * 128 + ((c ^ ((r
 __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const short* __restrict__ A,
                                                                        const short* __restrict__ Bt,
                                                                        float* __restrict__ C, int M,
-                                                                       int N, int K) {
+                                                                       int N, int K,
+                                                                       unsigned long long* __restrict__ cu_map) {
   __shared__ __attribute__((aligned(16))) short smem[2 * G2_STAGE_SHORTS];  // 128 KiB, the only LDS object
+  if (cu_map && threadIdx.x == 0) mark_cu(cu_map);  // which CUs ran GEMM tiles (probe report)
   const int tiles_n = N / G2_BN;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_m = wg / tiles_n, tile_n = wg % tiles_n;
@@ -396,7 +455,10 @@ __global__ void count_diff(const float* __restrict__ x, const float* __restrict_
 // flight (profiles/r1q: the former 2-byte-load / int64 versions took ~0.5 ms per probe, 4-5x the
 // GEMM they check).
 __device__ __forceinline__ uint32_t to_u32(short v) { return static_cast<uint32_t>(static_cast<int>(bf16_to_f32(v))); }
-__device__ __forceinline__ uint32_t to_u32(float v) { return static_cast<uint32_t>(static_cast<int>(v)); }
+__device__ __forceinline__ uint32_t to_u32(float v) {
+  // clamp first: an out-of-range float-to-int conversion is undefined (colsum_partial flags it)
+  return static_cast<uint32_t>(static_cast<int>(fminf(fmaxf(v, -2.0e9f), 2.0e9f)));
+}
 
 constexpr int kColRows = 64;  // rows per colsum_partial block (4 waves x 16 interleaved rows)
 constexpr int kUnroll = 4;    // independent 16-byte loads in flight per lane
@@ -404,9 +466,13 @@ constexpr int kUnroll = 4;    // independent 16-byte loads in flight per lane
 // Column sums: a lane owns V = 16/sizeof(T) adjacent columns (one 16-byte load per row); the
 // block's 4 waves take interleaved rows of a kColRows chunk, combine through LDS, and add one
 // 32-bit atomic per column. cols % V == 0.
+// For the fp32 product C the same pass also flags any element that is not an exact integer, is
+// not finite, or exceeds ``bound`` (= K * span^2): a corrupted element that keeps its integer part
+// (a low-mantissa flip) or wraps the int cast would otherwise leave the mod-2^32 sums intact.
 template <class T>
 __global__ __launch_bounds__(256) void colsum_partial(const T* __restrict__ X, int rows, int cols,
-                                                      uint32_t* __restrict__ out) {
+                                                      uint32_t* __restrict__ out, float bound,
+                                                      unsigned long long* __restrict__ bad) {
   constexpr int V = 16 / sizeof(T);
   using vec = __attribute__((ext_vector_type(V))) T;
   __shared__ uint32_t part[4][64 * V];
@@ -416,6 +482,7 @@ __global__ __launch_bounds__(256) void colsum_partial(const T* __restrict__ X, i
   const int r0 = blockIdx.y * kColRows;
   const int r1 = min(rows, r0 + kColRows);
   uint32_t acc[V] = {};
+  uint32_t odd = 0;
   if (c0 < cols) {
     for (int r = r0 + wave; r < r1; r += 4 * kUnroll) {
       vec v[kUnroll];
@@ -426,9 +493,18 @@ __global__ __launch_bounds__(256) void colsum_partial(const T* __restrict__ X, i
       for (int u = 0; u < kUnroll; ++u)
         if (r + 4 * u < r1) {
 #pragma unroll
-          for (int j = 0; j < V; ++j) acc[j] += to_u32(static_cast<T>(v[u][j]));
+          for (int j = 0; j < V; ++j) {
+            const T x = static_cast<T>(v[u][j]);
+            if constexpr (sizeof(T) == 4) odd += !(x == rintf(x) && fabsf(x) <= bound);  // NaN fails both
+            acc[j] += to_u32(x);
+          }
         }
     }
+  }
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) odd += __shfl_xor(odd, off, 64);
+    if (lane == 0 && odd && bad) atomicAdd(bad, static_cast<unsigned long long>(odd));
   }
 #pragma unroll
   for (int j = 0; j < V; ++j) part[wave][lane * V + j] = acc[j];
@@ -482,7 +558,13 @@ __global__ void inject_bit_flips(unsigned int* __restrict__ p, uint64_t nwords, 
   for (int i = threadIdx.x; i < count; i += blockDim.x) p[static_cast<uint64_t>(i + 1) * stride] ^= 1u << (i % 32);
 }
 
-__global__ void inject_gemm_fault(float* __restrict__ c, int64_t idx) { c[idx] += 1.0f; }
+// mode 1: +1.0 (an integer error: caught by the mod-2^32 checksums); mode 2: +0.25 (the integer
+// part survives: caught only by the integrality check); mode 3: NaN.
+__global__ void inject_gemm_fault(float* __restrict__ c, int64_t idx, int mode) {
+  if (mode == 1) c[idx] += 1.0f;
+  else if (mode == 2) c[idx] += 0.25f;
+  else c[idx] = __int_as_float(0x7fc00000);
+}
 
 __global__ void count_ne_u32(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, int n,
                              unsigned long long* __restrict__ bad) {
@@ -496,7 +578,10 @@ __global__ void count_ne_u32(const uint32_t* __restrict__ a, const uint32_t* __r
 // ------------------------------------------------------------------ host side
 constexpr long long kMaxPatterns = 4;
 // device counter / pinned host result slots: 2 per HBM pattern, then the two GEMM check counters
-constexpr int kSlotSmall = 2 * kMaxPatterns, kSlotAbft = kSlotSmall + 1, kResSlots = kSlotAbft + 1;
+constexpr int kSlotSmall = 2 * kMaxPatterns, kSlotAbft = kSlotSmall + 1, kSlotCensusBad = kSlotAbft + 1,
+              kSlotCensusMap = kSlotCensusBad + 1, kSlotGemmMap = kSlotCensusMap + kCuMapWords,
+              kResSlots = kSlotGemmMap + kCuMapWords;
+constexpr int kCensusIters = 128;
 
 struct DeviceCtx {
   hipStream_t stream = nullptr;   // HBM pattern test
@@ -510,6 +595,10 @@ struct DeviceCtx {
   void* arena = nullptr;
   size_t arena_bytes = 0;
   std::chrono::steady_clock::time_point arena_used{};
+  // HBM sweep buffer (mi355x_probe_hbm_sweep): nearly all free HBM, held only for a scrub pass
+  void* sweep = nullptr;
+  size_t sweep_bytes = 0;
+  unsigned long long* sweep_cnt = nullptr;
   bool ready = false;
 };
 
@@ -586,8 +675,8 @@ std::string hip_uuid(int dev) {
 // element against the VALU reference with asymmetric operands, (b) the timed N^3 GEMM (events
 // ctx.gev[0..1]) with exact int64 ABFT row/column checksums, then copies the two mismatch
 // counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``.
-void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, bool inject_gemm, unsigned long long* cnt,
-                       unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
+void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inject_gemm, int census_fault_xcc,
+                       unsigned long long* cnt, unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
   const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
   auto align = [](size_t x) { return (x + 4095) & ~static_cast<size_t>(4095); };
   char* p = gbase;
@@ -604,10 +693,10 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, bool inj
   auto* b = reinterpret_cast<short*>(carve(n * n * 2));
   auto* c = reinterpret_cast<float*>(carve(n * n * 4));
   auto* v = reinterpret_cast<unsigned long long*>(carve(6 * n * 8));
-  auto gemm = [&](const short* a_, const short* b_, float* c_, int nn) {
+  auto gemm = [&](const short* a_, const short* b_, float* c_, int nn, unsigned long long* cu_map) {
     if (tile256)
       hipLaunchKernelGGL(gemm_bf16_mfma_256, dim3((nn / G2_BM) * (nn / G2_BN)), dim3(kGemm2Threads), 0, s, a_, b_, c_, nn,
-                         nn, nn);
+                         nn, nn, cu_map);
     else
       hipLaunchKernelGGL(gemm_bf16_mfma_nt, dim3((nn / BM) * (nn / BN)), dim3(kGemmThreads), 0, s, a_, b_, c_, nn, nn, nn);
   };
@@ -615,7 +704,7 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, bool inj
   const uint64_t e0 = static_cast<uint64_t>(n0) * n0;
   hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, a0, e0, 0x1234u, 3);
   hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, b0, e0, 0xBEEFu, 3);
-  gemm(a0, b0, c0, static_cast<int>(n0));
+  gemm(a0, b0, c0, static_cast<int>(n0), nullptr);
   hipLaunchKernelGGL(gemm_ref_valu, dim3(n0 / 256, n0), dim3(256), 0, s, a0, b0, r0, static_cast<int>(n0),
                      static_cast<int>(n0), static_cast<int>(n0));
   hipLaunchKernelGGL(count_diff, dim3(64), dim3(256), 0, s, static_cast<const float*>(c0), static_cast<const float*>(r0),
@@ -628,11 +717,12 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, bool inj
   hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, b, e, 0x77u, 2);
   // the 256^3 check above already ran this kernel's code object: time the first launch
   PROBE_CHECK(hipEventRecord(ctx.gev[0], s));
-  for (int rep = 0; rep < reps; ++rep) gemm(a, b, c, gemm_n);
+  for (int rep = 0; rep < reps; ++rep) gemm(a, b, c, gemm_n, cnt + kSlotGemmMap);
   PROBE_CHECK(hipEventRecord(ctx.gev[1], s));
   PROBE_CHECK(hipGetLastError());
   if (inject_gemm)
-    hipLaunchKernelGGL(inject_gemm_fault, dim3(1), dim3(1), 0, s, c, static_cast<int64_t>(gemm_n / 3) * gemm_n + gemm_n / 5);
+    hipLaunchKernelGGL(inject_gemm_fault, dim3(1), dim3(1), 0, s, c, static_cast<int64_t>(gemm_n / 3) * gemm_n + gemm_n / 5,
+                       inject_gemm);
   // ABFT checksums: 6 uint32 vectors [acol | bcol | colsumC | expCol | rowsumC | expRow]
   uint32_t* v32 = reinterpret_cast<uint32_t*>(v);
   uint32_t *vacol = v32, *vbcol = v32 + n, *vcolC = v32 + 2 * n, *vexpC = v32 + 3 * n, *vrowC = v32 + 4 * n,
@@ -640,9 +730,13 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, bool inj
   PROBE_CHECK(hipMemsetAsync(v32, 0, 3 * n * sizeof(uint32_t), s));
   const int rows_y = (gemm_n + kColRows - 1) / kColRows;
   const dim3 cgrid_h((gemm_n + 511) / 512, rows_y), cgrid_f((gemm_n + 255) / 256, rows_y);
-  hipLaunchKernelGGL(colsum_partial<short>, cgrid_h, dim3(256), 0, s, static_cast<const short*>(a), gemm_n, gemm_n, vacol);
-  hipLaunchKernelGGL(colsum_partial<short>, cgrid_h, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n, vbcol);
-  hipLaunchKernelGGL(colsum_partial<float>, cgrid_f, dim3(256), 0, s, static_cast<const float*>(c), gemm_n, gemm_n, vcolC);
+  const float bound = static_cast<float>(gemm_n) * 4.0f;  // |C| <= K * span^2, span 2
+  hipLaunchKernelGGL(colsum_partial<short>, cgrid_h, dim3(256), 0, s, static_cast<const short*>(a), gemm_n, gemm_n, vacol,
+                     0.f, static_cast<unsigned long long*>(nullptr));
+  hipLaunchKernelGGL(colsum_partial<short>, cgrid_h, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n, vbcol,
+                     0.f, static_cast<unsigned long long*>(nullptr));
+  hipLaunchKernelGGL(colsum_partial<float>, cgrid_f, dim3(256), 0, s, static_cast<const float*>(c), gemm_n, gemm_n, vcolC,
+                     bound, cnt + kSlotAbft);
   const dim3 rgrid((gemm_n + 3) / 4);
   hipLaunchKernelGGL(rowdot<short>, rgrid, dim3(256), 0, s, static_cast<const short*>(b), gemm_n, gemm_n,
                      static_cast<const uint32_t*>(vacol), vexpC);
@@ -652,9 +746,27 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, bool inj
                      static_cast<const uint32_t*>(vbcol), vexpR);
   hipLaunchKernelGGL(count_ne_u32, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vcolC, vexpC, gemm_n, cnt + kSlotAbft);
   hipLaunchKernelGGL(count_ne_u32, dim3((gemm_n + 255) / 256), dim3(256), 0, s, vrowC, vexpR, gemm_n, cnt + kSlotAbft);
+  // (c) every CU's matrix cores: the census (the GEMM above marked the CUs that ran its tiles)
+  hipLaunchKernelGGL(cu_census, dim3(8 * ctx.prop.multiProcessorCount), dim3(kCensusThreads), 0, s, cnt + kSlotCensusMap,
+                     cnt + kSlotCensusBad, kCensusIters, 0xC0FFEEu ^ static_cast<uint32_t>(gemm_n), census_fault_xcc);
   PROBE_CHECK(hipGetLastError());
-  PROBE_CHECK(hipMemcpyAsync(hres + kSlotSmall, cnt + kSlotSmall, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                             s));
+  PROBE_CHECK(hipMemcpyAsync(hres + kSlotSmall, cnt + kSlotSmall, (kResSlots - kSlotSmall) * sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, s));
+}
+
+struct CuCount {
+  int total = 0;
+  int per_xcc[8] = {};
+};
+
+CuCount count_cus(const unsigned long long* map) {
+  CuCount c;
+  for (int w = 0; w < kCuMapWords; ++w) {
+    const int n = __builtin_popcountll(map[w]);
+    c.total += n;
+    c.per_xcc[(w * 64) >> 8] += n;
+  }
+  return c;
 }
 
 std::string run_probe(int dev, const char* opts) {
@@ -664,7 +776,7 @@ std::string run_probe(int dev, const char* opts) {
   gemm_n = std::max(256, (gemm_n / 256) * 256);
   const int patterns = static_cast<int>(std::min(kMaxPatterns, std::max(1LL, opt_int(opts, "patterns", 2))));
   const int inject_flips = static_cast<int>(std::min(4096LL, std::max(0LL, opt_int(opts, "injectBitFlips", 0))));
-  const bool inject_gemm = opt_int(opts, "injectGemmFault", 0) != 0;
+  const int inject_gemm = static_cast<int>(opt_int(opts, "injectGemmFault", 0));
   const bool tile256 = opt_int(opts, "gemmTile", 256) != 128;  // 128 = the older 128x128 kernel (A/B)
   // The HBM test is bandwidth-bound with few waves per CU; the MFMA phase is compute-bound and
   // touches ~130 MiB: run them concurrently on two streams (overlap=0: one stream, serial).
@@ -739,10 +851,14 @@ std::string run_probe(int dev, const char* opts) {
 
   // ---------------- MFMA phase (launched first so it starts beside the HBM fill)
   bool mfma_ok = true;
-  unsigned long long small_bad = 0, abft_bad = 0;
+  unsigned long long small_bad = 0, abft_bad = 0, census_bad = 0;
+  CuCount census, gemm_cus;
+  const bool require_all_cus = opt_int(opts, "requireAllCUs", 1) != 0;
   double tflops = 0, gemm_ms = 0;
   const int reps = static_cast<int>(std::max(1LL, opt_int(opts, "gemmReps", 1)));
-  if (do_mfma) launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, cnt, hres, ctx, s2);
+  const int census_fault_xcc = static_cast<int>(opt_int(opts, "injectCensusFaultXcc", -1));
+  if (do_mfma)
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, cnt, hres, ctx, s2);
 
   // ---------------- HBM: all patterns back to back, per-pattern counters
   auto* hbm = reinterpret_cast<u32x4*>(base);
@@ -781,7 +897,12 @@ std::string run_probe(int dev, const char* opts) {
     tflops = 2.0 * gemm_n * static_cast<double>(gemm_n) * gemm_n / (gemm_ms * 1e-3) / 1e12;
     small_bad = hres[kSlotSmall];
     abft_bad = hres[kSlotAbft];
-    mfma_ok = small_bad == 0 && abft_bad == 0;
+    census_bad = hres[kSlotCensusBad];
+    census = count_cus(hres + kSlotCensusMap);
+    gemm_cus = count_cus(hres + kSlotGemmMap);
+    // every CU the runtime reports must have proven its matrix cores (requireAllCUs, default on)
+    const bool cus_ok = !require_all_cus || census.total >= cus;
+    mfma_ok = small_bad == 0 && abft_bad == 0 && census_bad == 0 && cus_ok;
   }
   const double mfma_wall_ms = do_mfma ? ms_since(t_run) : 0.0;
   unsigned long long bad_bits = 0, first_bad = ~0ull;
@@ -821,6 +942,14 @@ std::string run_probe(int dev, const char* opts) {
          ",\"n\":" + std::to_string(gemm_n) + ",\"tile\":" + (tile256 ? "256" : "128") +
          ",\"elementMismatches\":" + std::to_string(small_bad) + ",\"abftMismatches\":" + std::to_string(abft_bad) +
          ",\"tflops\":" + jnum(tflops) + ",\"ms\":" + jnum(gemm_ms) + "}";
+  if (do_mfma) {
+    std::string per = "[";
+    for (int x = 0; x < 8; ++x) per += (x ? "," : "") + std::to_string(census.per_xcc[x]);
+    out += ",\"cus\":{\"expected\":" + std::to_string(cus) + ",\"mfmaVerified\":" + std::to_string(census.total) +
+           ",\"perXcd\":" + per + "]" + ",\"gemmTiles\":" + std::to_string(gemm_cus.total) +
+           ",\"badWaves\":" + std::to_string(census_bad) + ",\"ok\":" +
+           (census_bad == 0 && census.total >= cus ? "true" : "false") + "}";
+  }
   out += ",\"ms\":" + jnum(total_ms);
   out += ",\"phases\":{\"arenaReused\":" + std::string(reused ? "true" : "false") +
          ",\"setupMs\":" + jnum(setup_ms) + ",\"allocMs\":" + jnum(alloc_ms) +
@@ -887,6 +1016,77 @@ std::string run_peer(int src, int dst, const char* opts) {
   return "{\"src\":" + std::to_string(src) + ",\"dst\":" + std::to_string(dst) + ",\"canAccessPeer\":true" +
          ",\"passed\":" + (bad == 0 ? "true" : "false") + ",\"badBits\":" + std::to_string(bad) +
          ",\"bytes\":" + std::to_string(n16 * 16) + ",\"GBps\":" + jnum(gbps) + ",\"ms\":" + jnum(ms) + "}";
+}
+
+// One window of the rotating HBM sweep (see mi355x_probe_hbm_sweep in probe.h). The claim-time
+// probe always tests the same ~1 GiB arena; this walks the rest of the 288 GB: a buffer of all free
+// HBM minus ``reserve`` is allocated once per scrub pass (kept while ``keep``), and each call
+// pattern-tests [offset, offset+bytes) of it with the same fill/verify kernels and both polarities.
+std::string run_sweep(int dev, const char* opts) {
+  const uint64_t want = static_cast<uint64_t>(std::max(1LL << 20, opt_int(opts, "bytes", 16LL << 30)));
+  const uint64_t reserve = static_cast<uint64_t>(std::max(0LL, opt_int(opts, "reserve", 4LL << 30)));
+  const uint64_t offset_in = static_cast<uint64_t>(std::max(0LL, opt_int(opts, "offset", 0)));
+  const bool keep = opt_int(opts, "keep", 0) != 0;
+  const int inject_flips = static_cast<int>(std::min(4096LL, std::max(0LL, opt_int(opts, "injectBitFlips", 0))));
+  DeviceCtx& ctx = g_ctx[static_cast<size_t>(dev)];
+  if (!ctx.ready) (void)run_probe(dev, "{\"hbmBytes\":1048576,\"patterns\":1,\"mfma\":false}");
+  PROBE_CHECK(hipSetDevice(dev));
+  auto t0 = std::chrono::steady_clock::now();
+  double alloc_ms = 0;
+  if (!ctx.sweep) {
+    size_t free_b = 0, total_b = 0;
+    PROBE_CHECK(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t gran = 2ull << 20;
+    if (free_b <= reserve + gran) throw ProbeError("not enough free HBM for a sweep window");
+    const uint64_t span = ((free_b - reserve) / gran) * gran;
+    PROBE_CHECK(hipMalloc(&ctx.sweep, span));
+    ctx.sweep_bytes = span;
+    alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  const uint64_t span = ctx.sweep_bytes;
+  const uint64_t offset = (offset_in % span) & ~static_cast<uint64_t>(15);
+  const uint64_t bytes = std::min<uint64_t>(want, span - offset) & ~static_cast<uint64_t>(15);
+  const uint64_t n16 = bytes / 16;
+  auto* win = reinterpret_cast<u32x4*>(static_cast<char*>(ctx.sweep) + offset);
+  if (!ctx.sweep_cnt) PROBE_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx.sweep_cnt), 4 * sizeof(unsigned long long)));
+  unsigned long long* cnt = ctx.sweep_cnt;
+  hipStream_t s = ctx.stream;
+  const int cus = ctx.prop.multiProcessorCount;
+  const int fill_grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(cus), (n16 + kHbmThreads - 1) / kHbmThreads));
+  const int verify_grid = static_cast<int>(std::min<uint64_t>(3ull * cus, (n16 + kHbmThreads - 1) / kHbmThreads));
+  const uint32_t seed = 0x5CAB0000u ^ static_cast<uint32_t>(offset >> 20);
+  PROBE_CHECK(hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned long long), s));
+  PROBE_CHECK(hipMemsetAsync(cnt + 1, 0xFF, sizeof(unsigned long long), s));
+  PROBE_CHECK(hipMemsetAsync(cnt + 3, 0xFF, sizeof(unsigned long long), s));
+  PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
+  for (int pi = 0; pi < 2; ++pi) {
+    const uint32_t flip = pi ? 0xFFFFFFFFu : 0u;
+    hipLaunchKernelGGL(hbm_fill, dim3(fill_grid), dim3(kHbmThreads), 0, s, win, n16, seed, flip);
+    if (pi == 0 && inject_flips > 0)
+      hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(win), n16 * 4,
+                         inject_flips);
+    hipLaunchKernelGGL(hbm_verify, dim3(verify_grid), dim3(kHbmThreads), 0, s, static_cast<const u32x4*>(win), n16, seed,
+                       flip, cnt + 2 * pi, cnt + 2 * pi + 1);
+  }
+  PROBE_CHECK(hipEventRecord(ctx.ev[1], s));
+  PROBE_CHECK(hipGetLastError());
+  PROBE_CHECK(hipMemcpyAsync(ctx.host_res, cnt, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  PROBE_CHECK(hipStreamSynchronize(s));
+  float ms = 0;
+  PROBE_CHECK(hipEventElapsedTime(&ms, ctx.ev[0], ctx.ev[1]));
+  const unsigned long long bad = ctx.host_res[0] + ctx.host_res[2];
+  const unsigned long long first = std::min(ctx.host_res[1], ctx.host_res[3]);
+  if (!keep) {
+    (void)hipFree(ctx.sweep);
+    ctx.sweep = nullptr;
+    ctx.sweep_bytes = 0;
+  }
+  const double gbps = ms > 0 ? 4.0 * static_cast<double>(bytes) / (ms * 1e-3) / 1e9 : 0.0;
+  return "{\"device\":" + std::to_string(dev) + ",\"passed\":" + (bad == 0 ? "true" : "false") +
+         ",\"offset\":" + std::to_string(offset) + ",\"bytes\":" + std::to_string(bytes) +
+         ",\"span\":" + std::to_string(span) + ",\"badBits\":" + std::to_string(bad) +
+         ",\"firstBadOffset\":" + (first == ~0ull ? std::string("null") : std::to_string(offset + first * 16)) +
+         ",\"GBps\":" + jnum(gbps) + ",\"ms\":" + jnum(ms) + ",\"allocMs\":" + jnum(alloc_ms) + "}";
 }
 
 }  // namespace
@@ -976,6 +1176,55 @@ int mi355x_probe_trim(int idle_ms) {
     ++freed;
   }
   return freed;
+}
+
+char* mi355x_probe_hbm_sweep(int dev, const char* opts_json) {
+  if (g_count < 0 || dev < 0 || dev >= g_count) return dup("{\"passed\":false,\"error\":\"bad device index\"}");
+  std::lock_guard<std::mutex> g(device_mutex(dev));
+  try {
+    return dup(run_sweep(dev, opts_json));
+  } catch (const std::exception& e) {
+    (void)hipGetLastError();
+    return dup(std::string("{\"device\":") + std::to_string(dev) + ",\"passed\":false,\"error\":" + jstr(e.what()) + "}");
+  }
+}
+
+int mi355x_probe_sweep_release(int dev) {
+  if (g_count < 0 || dev < 0 || dev >= g_count) return -1;
+  std::lock_guard<std::mutex> g(device_mutex(dev));
+  DeviceCtx& ctx = g_ctx[static_cast<size_t>(dev)];
+  if (!ctx.sweep) return 0;
+  if (hipSetDevice(dev) != hipSuccess) return -1;
+  (void)hipFree(ctx.sweep);
+  ctx.sweep = nullptr;
+  ctx.sweep_bytes = 0;
+  return 1;
+}
+
+int mi355x_probe_gemm_bf16(int dev, const void* A, const void* Bt, void* C, int m, int n, int k) {
+  if (g_count < 0 || dev < 0 || dev >= g_count) return -1;
+  if (m <= 0 || n <= 0 || k <= 0 || m % G2_BM || n % G2_BN || k % G2_BK || !A || !Bt || !C) return -2;
+  std::lock_guard<std::mutex> g(device_mutex(dev));
+  try {
+    PROBE_CHECK(hipSetDevice(dev));
+    const size_t sa = static_cast<size_t>(m) * k * 2, sb = static_cast<size_t>(n) * k * 2,
+                 sc = static_cast<size_t>(m) * n * 4;
+    DevBuf da, db, dc;
+    PROBE_CHECK(hipMalloc(&da.p, sa));
+    PROBE_CHECK(hipMalloc(&db.p, sb));
+    PROBE_CHECK(hipMalloc(&dc.p, sc));
+    PROBE_CHECK(hipMemcpy(da.p, A, sa, hipMemcpyHostToDevice));
+    PROBE_CHECK(hipMemcpy(db.p, Bt, sb, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(gemm_bf16_mfma_256, dim3((m / G2_BM) * (n / G2_BN)), dim3(kGemm2Threads), 0, nullptr,
+                       static_cast<const short*>(da.p), static_cast<const short*>(db.p), static_cast<float*>(dc.p), m, n,
+                       k, static_cast<unsigned long long*>(nullptr));
+    PROBE_CHECK(hipGetLastError());
+    PROBE_CHECK(hipMemcpy(C, dc.p, sc, hipMemcpyDeviceToHost));
+    return 0;
+  } catch (const std::exception&) {
+    (void)hipGetLastError();
+    return -4;
+  }
 }
 
 void mi355x_probe_free(char* p) { std::free(p); }

@@ -46,10 +46,15 @@ def test_probe_passes_and_is_fast(hip):
     assert r["passed"], r
     assert r["hbm"]["badBits"] == 0 and r["mfma"]["elementMismatches"] == 0
     assert r["mfma"]["abftMismatches"] == 0
-    # sanity floors well below what MI355X reaches (~5 TB/s, ~750 TF): catch a broken kernel
-    assert r["hbm"]["GBps"] > 2000, r["hbm"]
-    assert r["mfma"]["tflops"] > 300, r["mfma"]
-    assert r["ms"] < 1000
+    assert r["ms"] < 50
+    # performance floors at ~0.7x of what this MI355X measures with the phases run serially
+    # (profiles/r1g: ~6.0 TB/s write+read; r1c: ~1210 TFLOP/s for the 4096^3 bf16 GEMM), so a
+    # 1.5x regression fails here rather than passing a 3x-lower sanity bar
+    best = max((hip.run(0, hbm_bytes=1 << 30, gemm_reps=3, overlap=0) for _ in range(3)),
+               key=lambda x: x["mfma"]["tflops"])
+    assert best["passed"], best
+    assert best["hbm"]["GBps"] > 3900, best["hbm"]
+    assert best["mfma"]["tflops"] > 850, best["mfma"]
 
 
 def test_hbm_checker_counts_injected_bit_flips(hip):
@@ -64,6 +69,84 @@ def test_abft_detects_single_corrupted_element(hip):
     assert not r["passed"]
     assert r["mfma"]["abftMismatches"] == 2  # its row and its column checksum
     assert r["mfma"]["elementMismatches"] == 0
+
+
+@pytest.mark.parametrize("mode", [2, 3])
+def test_abft_flags_fractional_and_nan_elements(hip, mode):
+    """A corruption that keeps the integer part (+0.25) leaves the mod-2^32 checksums of the
+    truncated values intact for non-negative elements; NaN would make the int cast undefined.
+    The integrality/range check fused into the column-sum pass catches both."""
+    r = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=1024, injectGemmFault=mode)
+    assert not r["passed"], r
+    assert r["mfma"]["abftMismatches"] >= 1
+
+
+def test_cu_census_covers_every_cu(hip):
+    """Every one of the 256 CUs (8 XCDs x 32) proves its matrix cores with an exactly-checked
+    MFMA chain, identified by the XCC_ID / HW_ID hardware registers of the wave."""
+    r = hip.run(0, hbm_bytes=64 << 20)
+    assert r["passed"], r
+    cus = r["cus"]
+    assert cus["expected"] == 256 and cus["mfmaVerified"] == 256 and cus["badWaves"] == 0, cus
+    assert cus["perXcd"] == [32] * 8, cus
+    assert 0 < cus["gemmTiles"] <= 256  # CUs that ran tiles of the timed 4096^3 GEMM
+
+
+def test_cu_census_detects_a_bad_xcd(hip):
+    r = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=1024, injectCensusFaultXcc=3)
+    assert not r["passed"], r
+    cus = r["cus"]
+    assert cus["perXcd"][3] == 0 and cus["mfmaVerified"] == 224 and cus["badWaves"] > 0, cus
+    assert not cus["ok"]
+
+
+@pytest.mark.parametrize("mnk", [(1024, 768, 512), (2048, 2048, 2048), (512, 2048, 1024)])
+def test_probe_gemm_matches_torch_fp64_cpu(hip, mnk):
+    """Independent numerics oracle: the probe's production MFMA GEMM on random normal bf16
+    operands (non-integer: bf16 rounding and fp32 accumulation order are exercised) against a
+    float64 CPU torch.matmul of the same bf16 values (torch's own HIP runtime cannot share device
+    pointers with the probe library, so the oracle runs on the host). Tolerance: fp32
+    accumulation of K products, |err| <= 2e-6 * sqrt(K) * max|ref|."""
+    import torch
+    m, n, k = mnk
+    g = torch.Generator().manual_seed(m + n + k)
+    a = torch.randn(m, k, generator=g).to(torch.bfloat16).contiguous()
+    bt = torch.randn(n, k, generator=g).to(torch.bfloat16).contiguous()
+    c = torch.full((m, n), float("nan"), dtype=torch.float32)
+    hip.gemm_bf16(0, a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k)
+    ref = a.double() @ bt.double().T
+    err = (c.double() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert torch.isfinite(c).all()
+    assert err <= 2e-6 * (k ** 0.5) * scale, (err, scale)
+    with pytest.raises(ValueError):
+        hip.gemm_bf16(0, a.data_ptr(), bt.data_ptr(), c.data_ptr(), m + 1, n, k)
+
+
+def test_concurrent_probes_of_one_device_serialise(hip):
+    """Two probes of the same GPU from different threads (e.g. a claim racing a recheck) are
+    serialised by the per-device lock: both complete, both pass, neither corrupts the other."""
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(2) as ex:
+        futs = [ex.submit(hip.run, 0, 512 << 20) for _ in range(2)]
+        res = [f.result(timeout=60) for f in futs]
+    assert all(r["passed"] for r in res), res
+    assert all(r["hbm"]["badBits"] == 0 and r["mfma"]["abftMismatches"] == 0 for r in res)
+
+
+def test_hbm_sweep_windows_cover_free_hbm(hip):
+    """The rotating sweep: windows of a buffer spanning (nearly) all free HBM are pattern-tested,
+    an injected flip inside a window is found at the right offset, and the buffer is released."""
+    a = hip.hbm_sweep(0, 0, 4 << 30, keep=True)
+    assert a["passed"], a
+    assert a["span"] > 200e9, a  # ~288 GB MI355X minus the 4 GiB reserve and what is in use
+    far = a["span"] - (2 << 30)
+    b = hip.hbm_sweep(0, far, 4 << 30, keep=True)
+    assert b["passed"] and b["offset"] == far and b["bytes"] == 2 << 30, b
+    c = hip.hbm_sweep(0, 64 << 30, 1 << 30, keep=True, injectBitFlips=11)
+    assert not c["passed"] and c["badBits"] == 11 and c["firstBadOffset"] >= 64 << 30, c
+    assert a["GBps"] > 3000, a
+    assert hip.sweep_release(0) == 1 and hip.sweep_release(0) == 0
 
 
 def test_probe_cli(native_built):
