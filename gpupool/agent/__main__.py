@@ -35,6 +35,15 @@ def main() -> None:
     ap.add_argument("--sample-interval", type=float, default=2.0)
     ap.add_argument("--quarantine", type=float, default=300.0)
     ap.add_argument("--no-fsync", action="store_true")
+    ap.add_argument("--probe-arena-idle", type=float, default=10.0,
+                    help="seconds before the kept probe arena (~1.2 GiB/GPU) is freed")
+    ap.add_argument("--scrub-interval", type=float, default=60.0,
+                    help="HBM scrubber pass period over idle GPUs, seconds (0 = off)")
+    ap.add_argument("--scrub-window", type=int, default=4 << 30, help="bytes per scrub window")
+    ap.add_argument("--scrub-windows", type=int, default=8, help="windows per GPU per pass")
+    ap.add_argument("--scrub-reserve", type=int, default=4 << 30,
+                    help="HBM bytes the scrub buffer leaves free")
+    ap.add_argument("--scrub-start-delay", type=float, default=30.0)
     ap.add_argument("--ready-file", default="")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
@@ -46,7 +55,10 @@ def main() -> None:
                       plugin_dir=a.plugin_dir, pod_resources=a.pod_resources, probe_mode=a.probe,
                       probe_sim_ms=a.probe_sim_ms, probe_gemm_n=a.probe_gemm_n,
                       sample_interval=a.sample_interval, quarantine_s=a.quarantine,
-                      fsync=not a.no_fsync)
+                      fsync=not a.no_fsync, probe_arena_idle_s=a.probe_arena_idle,
+                      scrub_interval_s=a.scrub_interval, scrub_window_bytes=a.scrub_window,
+                      scrub_windows=a.scrub_windows, scrub_reserve_bytes=a.scrub_reserve,
+                      scrub_start_delay_s=a.scrub_start_delay)
     agent = Agent(cfg)
     try:
         asyncio.run(serve(agent, a.ready_file or None))

@@ -62,6 +62,12 @@ class AgentConfig:
     quarantine_s: float = 300.0
     advertise_wait_s: float = 2.0
     fsync: bool = True
+    probe_arena_idle_s: float = 10.0  # free the kept ~1.2 GiB probe arena after this idle time
+    scrub_interval_s: float = 60.0    # HBM scrubber pass period over idle GPUs (0 = off)
+    scrub_window_bytes: int = 4 << 30
+    scrub_windows: int = 8            # windows per device per pass
+    scrub_reserve_bytes: int = 4 << 30
+    scrub_start_delay_s: float = 30.0
 
 
 class Agent:
@@ -91,7 +97,8 @@ class Agent:
         self._adv_event = threading.Event()
         self.plugins: dict = {}
         self.probe_mode = cfg.probe_mode or default_mode(self.backend)
-        self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n)
+        self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n,
+                             arena_idle_s=cfg.probe_arena_idle_s)
         self.last_probe: dict[str, dict] = {}
         self._probe_mono: dict[str, float] = {}  # uuid -> monotonic time of its last probe
         # admin maintenance (gpuctl gpu cordon): uuid -> reason; persisted as a quarantine entry
@@ -108,6 +115,10 @@ class Agent:
         self._podres = PodResourcesClient(cfg.pod_resources) if cfg.pod_resources else None
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
+        from .scrubber import HbmScrubber
+        self.scrubber = HbmScrubber(self, cfg.scrub_interval_s, cfg.scrub_window_bytes,
+                                    cfg.scrub_windows, cfg.scrub_reserve_bytes,
+                                    cfg.scrub_start_delay_s)
         self._evaluate_all()
         from .preflight import check as preflight_check
         self.preflight = preflight_check(self.snap, fake=self.backend == "fake")
@@ -332,7 +343,10 @@ class Agent:
                     self._advertisable(uuid)
             else:
                 out["advertised"] = self._advertisable(uuid)
-        else:
+        cov = self.scrubber.coverage(uuid)
+        if cov:
+            out["hbmSweep"] = cov
+        if not rec:
             q = self.ledger.quarantined().get(uuid) if self.ledger else None
             out["state"] = ("Maintenance" if q.get("maintenance") else "Quarantined") if q else "Free"
             if q:
@@ -398,6 +412,8 @@ class Agent:
                 self.records[d["uuid"]] = rec
             self.ledger.commit(self.records)  # durable before probing: no double claim on crash
             self.stats["claims"] += len(chosen)
+        for d in chosen:  # an in-flight HBM scrub window finishes and hands its buffer back
+            self.scrubber.yield_device(d["uuid"])
         lap("commit")
         # probes run outside the lock, concurrently across GPUs
         t0 = time.perf_counter()
@@ -745,6 +761,10 @@ class Agent:
                     if isinstance(t, dict) and t.get("current") is not None:
                         lines.append(f'gpupool_device_temperature_celsius{{{lab},sensor="{s}"}} '
                                      f"{t['current']}")
+                cov = self.scrubber.coverage(u)
+                if cov:
+                    lines.append(f"gpupool_device_hbm_sweep_passes_total{{{lab}}} {cov.get('passes', 0)}")
+                    lines.append(f"gpupool_device_hbm_sweep_fraction{{{lab}}} {cov.get('fraction', 0)}")
                 pr = self.last_probe.get(u)
                 if pr:  # last claim-time probe of this GPU (performance trend across claims)
                     lines.append(f"gpupool_device_probe_passed{{{lab}}} {1 if pr.get('passed') else 0}")
@@ -754,6 +774,8 @@ class Agent:
                                  f"{float((pr.get('mfma') or {}).get('tflops') or 0):.1f}")
             for k, v in self.stats.items():
                 lines.append(f"gpupool_agent_{k} {v}")
+            for k, v in self.scrubber.stats.items():
+                lines.append(f"gpupool_agent_hbm_scrub_{k}_total {v}")
             lines.append(f"gpupool_agent_gen {self.gen}")
         return "\n".join(lines) + "\n"
 
@@ -769,6 +791,7 @@ class Agent:
         t = threading.Thread(target=self._sampler, daemon=True, name="sampler")
         t.start()
         self._threads.append(t)
+        self.scrubber.start()
         if self.cfg.apiserver:
             self.register_node()
             t = threading.Thread(target=self._heartbeater, daemon=True, name="heartbeat")
@@ -777,6 +800,7 @@ class Agent:
 
     def stop(self) -> None:
         self._stop.set()
+        self.scrubber.stop()
         for p in list(self.plugins.values()):
             p.stop()
         self.prober.close()
@@ -846,6 +870,19 @@ def build_app(agent: Agent) -> web.Application:
         changed = await run_blocking(agent.sample)
         return web.json_response({"changed": sorted(changed), "gen": agent.gen})
 
+    async def scrub(request):
+        """Synchronous HBM scrub of one free GPU (admin / tests): {"gpu": uuid|hipUUID|index,
+        "windows": n}."""
+        b = await request.json()
+        ref = str(b.get("gpu", ""))
+        uuid = next((u for u, d in agent.by_uuid.items()
+                     if ref in (u, d.get("hipUUID"), str(d.get("index")))), None)
+        if uuid is None:
+            return web.json_response({"ok": False, "reason": "NotFound"}, status=404)
+        rec = await run_blocking(agent.scrubber.scrub_device, uuid, int(b.get("windows") or 1))
+        return web.json_response({"ok": True, "uuid": uuid, "coverage": agent.scrubber.coverage(uuid),
+                                  "record": rec})
+
     async def healthz(request):
         return web.Response(text="ok\n")
 
@@ -860,6 +897,7 @@ def build_app(agent: Agent) -> web.Application:
     app.router.add_post("/v1/maintenance", maintenance)
     app.router.add_get("/v1/events", events)
     app.router.add_post("/v1/sample", sample)
+    app.router.add_post("/v1/scrub", scrub)
     app.router.add_get("/healthz", healthz)
     app.router.add_get("/metrics", metrics)
     app["loop_holder"] = loop_holder

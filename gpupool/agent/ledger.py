@@ -1,7 +1,7 @@
 """Claim ledger: the node agent's durable record of which GPU belongs to which pool.
 
 All claims live in one JSON document (``<state>/ledger.json``: ``{"version": 1, "claims": {uuid:
-record}}``) that is replaced atomically (write temp -> fsync -> rename -> fsync dir) once per
+record}, "hbmSweep": {uuid: scrubber cursor/coverage}}``) that is replaced atomically (write temp -> fsync -> rename -> fsync dir) once per
 agent operation, so a claim of 8 GPUs costs one fsync, not eight, and a crash can never leave a
 half-written batch. GPUs that failed a probe are recorded in ``<state>/quarantine/<uuid>.json``.
 Together with ``status.devices`` on the pool this makes the operator stateless across restarts
@@ -67,10 +67,20 @@ class Ledger:
         self.fsync = fsync
         self._mu = threading.Lock()
         self.writes = 0
+        # serialised sections: each is rendered by its writer's thread (the claim map under the
+        # agent lock), so a scrubber write never iterates a claim map another thread is editing
+        self._claims_text = "{}"
+        self._sweep: dict[str, dict] = {}
+        try:
+            with open(self.path) as f:
+                self._sweep = dict((json.load(f) or {}).get("hbmSweep") or {})
+        except (OSError, ValueError):
+            pass
 
     # ---------------------------------------------------------------- claims
     def load(self) -> dict[str, dict]:
         claims = read_claims(self.dir)
+        self._claims_text = json.dumps(claims, sort_keys=True)
         legacy = os.path.join(self.dir, "claims")  # per-device files of earlier versions
         if os.path.isdir(legacy):
             for name in sorted(os.listdir(legacy)):
@@ -85,10 +95,26 @@ class Ledger:
 
     def commit(self, claims: dict[str, dict]) -> None:
         """Persist the full claim map atomically (one write + one fsync per agent operation)."""
-        text = json.dumps({"version": VERSION, "claims": claims}, sort_keys=True)
+        text = json.dumps(claims, sort_keys=True)
         with self._mu:
-            _atomic_write_text(self.path, text, self.fsync)
-            self.writes += 1
+            self._claims_text = text
+            self._write_locked()
+
+    def commit_sweep(self, sweep: dict[str, dict]) -> None:
+        """Persist the HBM scrubber's per-device cursors/coverage (same document, same atomicity)."""
+        with self._mu:
+            self._sweep = {u: dict(r) for u, r in sweep.items()}
+            self._write_locked()
+
+    def sweep_state(self) -> dict[str, dict]:
+        with self._mu:
+            return {u: dict(r) for u, r in self._sweep.items()}
+
+    def _write_locked(self) -> None:
+        text = '{"version": %d, "claims": %s, "hbmSweep": %s}' % (
+            VERSION, self._claims_text, json.dumps(self._sweep, sort_keys=True))
+        _atomic_write_text(self.path, text, self.fsync)
+        self.writes += 1
 
     # ---------------------------------------------------------------- quarantine
     def quarantine(self, uuid: str, seconds: float, reason: str, maintenance: bool = False) -> None:

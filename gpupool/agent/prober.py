@@ -70,6 +70,13 @@ class Prober:
             res = {"passed": not fail, "backend": "simulated",
                    "hbm": {"ok": not fail, "GBps": 4900.0, "bytes": hbm},
                    "mfma": {"ok": not fail, "tflops": 1200.0 if mfma else 0.0, "enabled": mfma}}
+            if mfma:  # the CU census: every CU of this (partition of the) GPU proves its MFMA pipes
+                cus = int((dev.get("asic") or {}).get("computeUnits") or 256)
+                dead = int(dev.get("cuFault") or 0)
+                res["cus"] = {"expected": cus, "mfmaVerified": cus - dead, "badWaves": dead * 8,
+                              "ok": dead == 0}
+                if dead and not fail:
+                    res["passed"] = False
             if fail:
                 res["error"] = "injected probe failure (fault overlay)"
             res["ms"] = (time.perf_counter() - t0) * 1e3
@@ -126,6 +133,26 @@ class Prober:
             res["error"] = "PerformanceBelowFloor: " + "; ".join(why)
         return res
 
+    @staticmethod
+    def explain(res: dict) -> dict:
+        """A failed probe names what failed (HBM bits, GEMM element/ABFT mismatches, CU census)."""
+        if res.get("passed") or res.get("error"):
+            return res
+        why = []
+        hbm, mfma, cus = res.get("hbm") or {}, res.get("mfma") or {}, res.get("cus") or {}
+        if hbm.get("badBits"):
+            why.append(f"HBMPatternMismatch: {hbm['badBits']} flipped bit(s), first at offset "
+                       f"{hbm.get('firstBadOffset')}")
+        if mfma.get("elementMismatches") or mfma.get("abftMismatches"):
+            why.append(f"MFMAResultMismatch: {mfma.get('elementMismatches', 0)} element / "
+                       f"{mfma.get('abftMismatches', 0)} ABFT mismatch(es)")
+        if cus and not cus.get("ok", True):
+            why.append(f"CUCensusFailed: {cus.get('mfmaVerified')}/{cus.get('expected')} CUs "
+                       f"verified MFMA, per XCD {cus.get('perXcd')}, {cus.get('badWaves')} bad "
+                       f"wave(s)")
+        res["error"] = "; ".join(why) or "probe failed"
+        return res
+
     def probe_many(self, devs: list[dict], opts: dict) -> list[dict]:
         def guarded(run):
             try:
@@ -133,9 +160,11 @@ class Prober:
             except Exception as e:  # a probe must never take the agent down
                 return {"passed": False, "backend": self.mode, "error": repr(e), "ms": 0.0}
         if len(devs) == 1:  # the caller is already off the event loop: no second thread hop
-            return [self.apply_floors(guarded(lambda: self._one(devs[0], opts)), devs[0], opts)]
+            return [self.apply_floors(self.explain(guarded(lambda: self._one(devs[0], opts))),
+                                      devs[0], opts)]
         futs = [self.pool.submit(self._one, d, opts) for d in devs]
-        return [self.apply_floors(guarded(f.result), d, opts) for d, f in zip(devs, futs)]
+        return [self.apply_floors(self.explain(guarded(f.result)), d, opts)
+                for d, f in zip(devs, futs)]
 
     def peer_ring(self, devs: list[dict], opts: dict) -> dict[str, dict]:
         """xGMI peer check in ring order (dev i -> dev i+1): for each sender uuid, the copy

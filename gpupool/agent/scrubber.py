@@ -1,0 +1,215 @@
+"""HBM scrubber: walks the whole 288 GB of every idle MI355X in windows, between claims.
+
+The claim-time probe pattern-tests one ~1 GiB arena, which is the same physical memory on every
+claim. This thread covers the rest: for every GPU that is free (unclaimed, healthy, not
+quarantined, no pod), every ``interval_s`` it tests ``windows_per_pass`` windows of
+``window_bytes`` of a buffer spanning all free HBM minus ``reserve_bytes``
+(``probe.hbm_sweep``, the same fill/verify kernels, both polarities), advancing a per-device
+cursor that is persisted with the claim ledger. One full sweep of 288 GB costs ~0.2 s of HBM time
+(4 passes over the data at ~6 TB/s), spread over passes so a claim never waits on more than one
+window (~3 ms at 4 GiB). Coverage is reported per device (``hbmSweep`` in the agent's device view
+-> ``status.devices[].hbmCoverage``).
+
+Claims always win: ``yield_device`` (called by the claim path after the ledger commit) waits for an
+in-flight window and frees the big sweep buffer before the claim-time probe runs, and the scrubber
+re-checks eligibility under the same per-device lock before every window.
+
+A window with flipped bits quarantines a free GPU without expiry (``HBMSweepFailed``; cleared by
+``gpuctl gpu uncordon``), so it is never claimed. In ``simulated`` probe mode (fake backend) the
+windows are timed stand-ins and faults come from the overlay (``hbmBadOffset``: a byte offset).
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+
+log = logging.getLogger("gpupool.agent.scrubber")
+
+
+class HbmScrubber:
+    def __init__(self, agent, interval_s: float = 60.0, window_bytes: int = 4 << 30,
+                 windows_per_pass: int = 8, reserve_bytes: int = 4 << 30,
+                 start_delay_s: float = 30.0):
+        self.agent = agent
+        self.interval_s = interval_s
+        self.window_bytes = int(window_bytes)
+        self.windows_per_pass = int(windows_per_pass)
+        self.reserve_bytes = int(reserve_bytes)
+        self.start_delay_s = start_delay_s
+        self.state: dict[str, dict] = dict(agent.ledger.sweep_state())  # uuid -> coverage record
+        self._locks: dict[str, threading.Lock] = {}
+        self._mu = threading.Lock()
+        self._stop = threading.Event()
+        self._kick = threading.Event()
+        self._thread: threading.Thread | None = None
+        self.stats = {"windows": 0, "bytes": 0, "failures": 0}
+
+    # ------------------------------------------------------------------ coordination
+    def _lock_for(self, uuid: str) -> threading.Lock:
+        with self._mu:
+            return self._locks.setdefault(uuid, threading.Lock())
+
+    def yield_device(self, uuid: str) -> None:
+        """Called by the claim path (records already updated): wait for an in-flight window and
+        hand the sweep buffer back before the claim-time probe allocates its arena."""
+        with self._lock_for(uuid):
+            ordinal = self._ordinal(uuid)
+            if ordinal is not None and self.agent.prober.mode == "inproc":
+                self.agent.prober._hip.sweep_release(ordinal)
+
+    def _ordinal(self, uuid: str) -> int | None:
+        d = self.agent.by_uuid.get(uuid) or {}
+        return self.agent.prober.ordinals.get(str(d.get("hipUUID", "")).lower())
+
+    def _eligible(self, uuid: str) -> bool:
+        a = self.agent
+        if uuid in a.records or uuid in a.maintenance or uuid not in a.by_uuid:
+            return False
+        if not a.verdicts.get(uuid, {}).get("healthy"):
+            return False
+        if uuid in a.ledger.quarantined():
+            return False
+        return not a._pods_by_device().get(uuid)
+
+    # ------------------------------------------------------------------ one window
+    def _window(self, uuid: str, dev: dict, offset: int) -> dict:
+        p = self.agent.prober
+        if p.mode == "inproc":
+            ordinal = self._ordinal(uuid)
+            if ordinal is None:
+                return {"passed": False, "error": "device not visible to HIP"}
+            return p._hip.hbm_sweep(ordinal, offset, self.window_bytes, self.reserve_bytes,
+                                    keep=True)
+        # simulated: nominal window timing of the real kernels (~6 TB/s over 4 passes)
+        span = max(self.window_bytes, int(dev.get("memTotalBytes") or 288e9) - self.reserve_bytes)
+        off = offset % span
+        n = min(self.window_bytes, span - off)
+        time.sleep(min(0.05, 4 * n / 6e12))
+        bad_at = (dev.get("faults") or {}).get("hbmBadOffset", dev.get("hbmBadOffset"))
+        bad = 1 if bad_at is not None and off <= int(bad_at) < off + n else 0
+        return {"passed": not bad, "offset": off, "bytes": n, "span": span, "badBits": bad,
+                "firstBadOffset": int(bad_at) if bad else None, "GBps": 6000.0, "ms": 0.0}
+
+    def _release(self, uuid: str) -> None:
+        if self.agent.prober.mode == "inproc":
+            o = self._ordinal(uuid)
+            if o is not None:
+                self.agent.prober._hip.sweep_release(o)
+
+    def scrub_device(self, uuid: str, windows: int | None = None) -> dict:
+        """One pass over ``windows`` windows of one GPU; returns its coverage record."""
+        lock = self._lock_for(uuid)
+        with self._mu:
+            rec = dict(self.state.get(uuid) or {"cursor": 0, "span": 0, "coveredBytes": 0,
+                                                "passes": 0, "windows": 0, "lastBadBits": 0})
+        try:
+            for _ in range(windows or self.windows_per_pass):
+                if self._stop.is_set():
+                    break
+                with lock:
+                    with self.agent.lock:
+                        if not self._eligible(uuid):
+                            break
+                        dev = dict(self.agent.by_uuid[uuid])
+                    t0 = time.perf_counter()
+                    r = self._window(uuid, dev, int(rec["cursor"]))
+                if "error" in r and "span" not in r:
+                    log.warning("HBM sweep of %s failed to run: %s", uuid, r.get("error"))
+                    break
+                self.stats["windows"] += 1
+                self.stats["bytes"] += int(r.get("bytes") or 0)
+                span = int(r["span"])
+                if rec.get("span") and rec["span"] != span:  # free HBM changed: restart the sweep
+                    rec["cursor"], rec["coveredBytes"] = 0, 0
+                rec["span"] = span
+                end = int(r["offset"]) + int(r["bytes"])
+                rec["coveredBytes"] = min(span, int(rec["coveredBytes"]) + int(r["bytes"]))
+                rec["windows"] = int(rec["windows"]) + 1
+                rec["lastAt"] = time.time()
+                rec["lastGBps"] = round(float(r.get("GBps") or 0), 1)
+                rec["lastWindowMs"] = round((time.perf_counter() - t0) * 1e3, 3)
+                rec["lastBadBits"] = int(r.get("badBits") or 0)
+                if end >= span:
+                    rec["cursor"] = 0
+                    rec["passes"] = int(rec["passes"]) + 1
+                    rec["lastFullSweepAt"] = time.time()
+                    rec["coveredBytes"] = 0
+                else:
+                    rec["cursor"] = end
+                with self._mu:
+                    self.state[uuid] = dict(rec)
+                if not r.get("passed"):
+                    self.stats["failures"] += 1
+                    self._fail(uuid, r)
+                    break
+        finally:
+            with lock:
+                self._release(uuid)
+            with self._mu:
+                snap = {u: dict(r) for u, r in self.state.items()}
+            self.agent.ledger.commit_sweep(snap)
+        return rec
+
+    def _fail(self, uuid: str, r: dict) -> None:
+        why = (f"HBMSweepFailed: {r.get('badBits')} flipped bit(s) at HBM offset "
+               f"{r.get('firstBadOffset')} (window {r.get('offset')}+{r.get('bytes')})")
+        log.error("%s: %s", uuid, why)
+        a = self.agent
+        a.ledger.quarantine(uuid, 1e12, why)
+        with a.lock:
+            changed = a._evaluate_all()
+        a._bump(changed | {"*free*"})
+        a._notify_plugins()
+
+    # ------------------------------------------------------------------ loop
+    def coverage(self, uuid: str) -> dict | None:
+        with self._mu:
+            rec = self.state.get(uuid)
+            if not rec:
+                return None
+            out = dict(rec)
+        span = int(rec.get("span") or 0)
+        if span:
+            # fraction of the current sweep done (1.0 right after a full pass completes)
+            out["fraction"] = round(int(rec.get("coveredBytes") or 0) / span, 4) if \
+                int(rec.get("coveredBytes") or 0) else (1.0 if rec.get("passes") else 0.0)
+        return out
+
+    def run_once(self) -> int:
+        n = 0
+        with self.agent.lock:
+            uuids = sorted(self.agent.by_uuid)
+        for u in uuids:
+            if self._stop.is_set():
+                break
+            with self.agent.lock:
+                ok = self._eligible(u)
+            if ok:
+                self.scrub_device(u)
+                n += 1
+        return n
+
+    def _loop(self) -> None:
+        if self._stop.wait(self.start_delay_s):
+            return
+        while not self._stop.is_set():
+            try:
+                self.run_once()
+            except Exception:
+                log.exception("HBM scrub pass failed")
+            self._kick.wait(self.interval_s)
+            self._kick.clear()
+
+    def start(self) -> None:
+        if self.interval_s <= 0 or self.agent.prober.mode not in ("inproc", "simulated"):
+            return
+        self._thread = threading.Thread(target=self._loop, daemon=True, name="hbm-scrub")
+        self._thread.start()
+
+    def kick(self) -> None:
+        self._kick.set()
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._kick.set()

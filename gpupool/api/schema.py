@@ -163,10 +163,21 @@ DEVICE_STATUS = {
                 "hbmGBps": {"type": "number"},
                 "mfmaTflops": {"type": "number"},
                 "xgmiGBps": {"type": "number"},
+                "cusVerified": _I32,
+                "cusExpected": _I32,
                 "ms": {"type": "number"},
                 "backend": _S,
                 "message": _S,
             },
+        },
+        "hbmCoverage": {
+            "type": "object",
+            "description": "The agent's HBM scrubber on this GPU (rotating pattern-test windows "
+                           "over all free HBM while the GPU was idle): completed full sweeps, "
+                           "fraction of the current sweep, swept span in bytes.",
+            "properties": {"passes": _I64, "fraction": {"type": "number"}, "span": _I64,
+                           "cursor": _I64, "lastFullSweepAt": {"type": "number"},
+                           "lastBadBits": _I64},
         },
     },
 }
@@ -235,7 +246,7 @@ MI355X_SPEC = {
                                               "less HBM write+read bandwidth (GB/s) fails "
                                               "DeviceProbePassed (0 = off; MI355X measures "
                                               "~4900 with the default 1 GiB probe)."},
-                "xgmiPeerCheck": {**_B, "default": False,
+                "xgmiPeerCheck": {**_B, "default": True,
                                   "description": "For pools of 2+ GPUs: each GPU copies a "
                                                  "pattern to the next one over xGMI "
                                                  "(hipMemcpyPeer, ring order) and the receiver "

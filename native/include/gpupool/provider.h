@@ -104,7 +104,7 @@ struct DeviceView {
   std::string state;  // Free | Claimed | Draining | Quarantined | Probing
   std::string pool_uid, pool;
   bool healthy = false, advertised = false, probe_passed = false;
-  Json verdict, probe, pods, partition;
+  Json verdict, probe, pods, partition, hbm_sweep;
   std::string claimed_at, drain_started_at;
   static DeviceView from(const Json& j);
   Json status_json() const;

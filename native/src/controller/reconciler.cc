@@ -298,7 +298,7 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
   st["observedGeneration"] = m.generation;
   int64_t claimed = 0, ready = 0, probing = 0;
   std::vector<std::string> xgmi_bad, ecc_bad, thermal_bad, probe_bad, unhealthy;
-  double min_gbps = 1e30, min_tf = 1e30;
+  double min_gbps = 1e30, min_tf = 1e30, min_xgmi = 1e30;
   Json devices = Json::array();
   for (const auto& d : o.mine) {
     devices.push_back(d.status_json());
@@ -317,8 +317,12 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
     if (!d.verdict["xgmiOk"].as_bool(true)) xgmi_bad.push_back(reasons("XGMI"));
     if (!d.verdict["eccOk"].as_bool(true)) ecc_bad.push_back(reasons("HBM"));
     if (!d.verdict["thermalOk"].as_bool(true)) thermal_bad.push_back(reasons("Thermal"));
+    if (d.probe.path("xgmi.GBps").is_number()) min_xgmi = std::min(min_xgmi, d.probe.path("xgmi.GBps").as_double(1e30));
     if (!d.probe_passed) {
-      probe_bad.push_back(short_id(d) + ": " + d.probe["error"].str_or(d.probe.is_object() ? "probe failed" : "not probed"));
+      const std::string err = d.probe["error"].str_or(d.probe.is_object() ? "probe failed" : "not probed");
+      probe_bad.push_back(short_id(d) + ": " + err);
+      // the xGMI peer-copy check (spec.probe.xgmiPeerCheck) is link health too
+      if (err.rfind("XGMIPeerCheckFailed", 0) == 0) xgmi_bad.push_back(short_id(d) + ": " + err);
     } else {
       min_gbps = std::min(min_gbps, d.probe.path("hbm.GBps").as_double(1e30));
       min_tf = std::min(min_tf, d.probe.path("mfma.tflops").as_double(1e30));
@@ -338,7 +342,13 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
     else set_condition(conds, type, "True", claimed ? ok_reason : "NoDevices",
                        claimed ? std::to_string(claimed) + " GPU(s): " + ok_msg : "no GPUs claimed", gen, now);
   };
-  health_cond(gen::kCondXGMILinksHealthy, xgmi_bad, "XGMILinkDown", "AllLinksUp", "xGMI links up");
+  std::string xgmi_ok_msg = "xGMI links up";
+  if (min_xgmi < 1e29) {
+    char buf[96];
+    std::snprintf(buf, sizeof buf, "; peer-copy ring min %.0f GB/s", min_xgmi);
+    xgmi_ok_msg += buf;
+  }
+  health_cond(gen::kCondXGMILinksHealthy, xgmi_bad, "XGMILinkDown", "AllLinksUp", xgmi_ok_msg.c_str());
   health_cond(gen::kCondHBMECCHealthy, ecc_bad, "HBMECCErrors", "NoNewECCErrors", "no new HBM ECC errors since claim");
   health_cond(gen::kCondThermalHealthy, thermal_bad, "ThermalLimit", "WithinThermalLimits",
               "temperatures below device limits");

@@ -794,6 +794,11 @@ std::string run_probe(int dev, const char* opts) {
     PROBE_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ctx.host_res), kResSlots * sizeof(unsigned long long)));
     ctx.ready = true;
   }
+  if (ctx.sweep) {  // a claim-time probe always wins over the HBM scrubber's buffer
+    (void)hipFree(ctx.sweep);
+    ctx.sweep = nullptr;
+    ctx.sweep_bytes = 0;
+  }
   hipStream_t s = ctx.stream;
   const hipDeviceProp_t& prop = ctx.prop;
   const int cus = prop.multiProcessorCount;

@@ -31,6 +31,7 @@ DeviceView DeviceView::from(const Json& j) {
   d.claimed_at = j["claimedAt"].as_string();
   d.partition = j["partition"];
   d.drain_started_at = j["drainStartedAt"].as_string();
+  d.hbm_sweep = j["hbmSweep"];
   return d;
 }
 
@@ -67,7 +68,17 @@ Json DeviceView::status_json() const {
     if (probe["ms"].is_number()) p["ms"] = probe["ms"];
     if (probe["backend"].is_string()) p["backend"] = probe["backend"];
     if (probe["error"].is_string()) p["message"] = probe["error"];
+    if (probe.path("cus.mfmaVerified").is_number()) {
+      p["cusVerified"] = probe.path("cus.mfmaVerified");
+      p["cusExpected"] = probe.path("cus.expected");
+    }
     s["probe"] = p;
+  }
+  if (hbm_sweep.is_object()) {  // HBM scrubber coverage of this GPU (agent's rotating sweep)
+    Json c = Json::object();
+    for (const char* k : {"passes", "fraction", "span", "cursor", "lastFullSweepAt", "lastBadBits"})
+      if (!hbm_sweep[k].is_null()) c[k] = hbm_sweep[k];
+    s["hbmCoverage"] = c;
   }
   return s;
 }
