@@ -643,6 +643,9 @@ class Agent:
         return list(must) + [inv[i] for i in sel]
 
     def allocate_spec(self, resource: str, ids: list[str]) -> dict:
+        for u in ids:  # a pod never starts while the HBM scrubber still frees its buffer
+            if not self.scrubber.wait_released(u):
+                raise ValueError(f"device {u}: HBM scrub buffer still being released")
         with self.lock:
             hip, render = [], []
             for u in ids:

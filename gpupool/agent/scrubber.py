@@ -10,9 +10,11 @@ cursor that is persisted with the claim ledger. One full sweep of 288 GB costs ~
 window (~3 ms at 4 GiB). Coverage is reported per device (``hbmSweep`` in the agent's device view
 -> ``status.devices[].hbmCoverage``).
 
-Claims always win: ``yield_device`` (called by the claim path after the ledger commit) waits for an
-in-flight window and frees the big sweep buffer before the claim-time probe runs, and the scrubber
-re-checks eligibility under the same per-device lock before every window.
+Claims always win: the scrubber re-checks eligibility under a per-device lock before every window,
+and ``yield_device`` (called by the claim path after the ledger commit) only waits for an in-flight
+window. The big buffer is allocated and freed outside every lock a claim takes (~0.4 s / ~2.9 s for
+~282 GiB on MI355X, profiles/r2g): the claim-time probe runs in the reserve meanwhile, and the device
+plugin's Allocate waits for the free (``wait_released``) so a pod never starts beside it.
 
 A window with flipped bits quarantines a free GPU without expiry (``HBMSweepFailed``; cleared by
 ``gpuctl gpu uncordon``), so it is never claimed. In ``simulated`` probe mode (fake backend) the
@@ -40,6 +42,8 @@ class HbmScrubber:
         self.state: dict[str, dict] = dict(agent.ledger.sweep_state())  # uuid -> coverage record
         self._locks: dict[str, threading.Lock] = {}
         self._mu = threading.Lock()
+        self._cv = threading.Condition(self._mu)
+        self._held: set[str] = set()  # GPUs whose sweep buffer is allocated
         self._stop = threading.Event()
         self._kick = threading.Event()
         self._thread: threading.Thread | None = None
@@ -51,12 +55,24 @@ class HbmScrubber:
             return self._locks.setdefault(uuid, threading.Lock())
 
     def yield_device(self, uuid: str) -> None:
-        """Called by the claim path (records already updated): wait for an in-flight window and
-        hand the sweep buffer back before the claim-time probe allocates its arena."""
+        """Called by the claim path after the ledger commit (the GPU is no longer eligible): wait
+        for an in-flight window (one window, ~3 ms at 4 GiB). The scrubber then frees its buffer on
+        its own thread; the claim-time probe fits in the reserve meanwhile, and a pod's Allocate
+        waits for the free (``wait_released``)."""
         with self._lock_for(uuid):
-            ordinal = self._ordinal(uuid)
-            if ordinal is not None and self.agent.prober.mode == "inproc":
-                self.agent.prober._hip.sweep_release(ordinal)
+            pass
+
+    def wait_released(self, uuid: str, timeout: float = 30.0) -> bool:
+        """Block until no sweep buffer is held on ``uuid`` (the device plugin's Allocate calls this
+        so a pod never starts while the scrubber still holds the GPU's free HBM)."""
+        deadline = time.monotonic() + timeout
+        with self._cv:
+            while uuid in self._held:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    return False
+                self._cv.wait(left)
+        return True
 
     def _ordinal(self, uuid: str) -> int | None:
         d = self.agent.by_uuid.get(uuid) or {}
@@ -91,11 +107,28 @@ class HbmScrubber:
         return {"passed": not bad, "offset": off, "bytes": n, "span": span, "badBits": bad,
                 "firstBadOffset": int(bad_at) if bad else None, "GBps": 6000.0, "ms": 0.0}
 
-    def _release(self, uuid: str) -> None:
+    def _hold(self, uuid: str) -> bool:
+        """Allocate the sweep buffer (inproc: ~0.4 s for ~282 GiB) without any lock a claim takes."""
+        with self._cv:
+            self._held.add(uuid)
         if self.agent.prober.mode == "inproc":
             o = self._ordinal(uuid)
-            if o is not None:
-                self.agent.prober._hip.sweep_release(o)
+            if o is None or self.agent.prober._hip.sweep_alloc(o, self.reserve_bytes) < 0:
+                self._release(uuid)
+                return False
+        return True
+
+    def _release(self, uuid: str) -> None:
+        """Free the sweep buffer (inproc: ~2.9 s for ~282 GiB, the driver clears released VRAM)."""
+        try:
+            if self.agent.prober.mode == "inproc":
+                o = self._ordinal(uuid)
+                if o is not None:
+                    self.agent.prober._hip.sweep_release(o)
+        finally:
+            with self._cv:
+                self._held.discard(uuid)
+                self._cv.notify_all()
 
     def scrub_device(self, uuid: str, windows: int | None = None) -> dict:
         """One pass over ``windows`` windows of one GPU; returns its coverage record."""
@@ -103,6 +136,12 @@ class HbmScrubber:
         with self._mu:
             rec = dict(self.state.get(uuid) or {"cursor": 0, "span": 0, "coveredBytes": 0,
                                                 "passes": 0, "windows": 0, "lastBadBits": 0})
+        with self.agent.lock:
+            if not self._eligible(uuid):
+                return rec
+        if not self._hold(uuid):
+            log.warning("HBM sweep buffer allocation failed on %s", uuid)
+            return rec
         try:
             for _ in range(windows or self.windows_per_pass):
                 if self._stop.is_set():
@@ -144,8 +183,7 @@ class HbmScrubber:
                     self._fail(uuid, r)
                     break
         finally:
-            with lock:
-                self._release(uuid)
+            self._release(uuid)
             with self._mu:
                 snap = {u: dict(r) for u, r in self.state.items()}
             self.agent.ledger.commit_sweep(snap)

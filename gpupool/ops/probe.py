@@ -36,6 +36,8 @@ def lib() -> ctypes.CDLL:
             l.mi355x_probe_trim.argtypes = [ctypes.c_int]
             l.mi355x_probe_hbm_sweep.restype = ctypes.c_void_p
             l.mi355x_probe_hbm_sweep.argtypes = [ctypes.c_int, ctypes.c_char_p]
+            l.mi355x_probe_sweep_alloc.restype = ctypes.c_int
+            l.mi355x_probe_sweep_alloc.argtypes = [ctypes.c_int, ctypes.c_longlong]
             l.mi355x_probe_sweep_release.restype = ctypes.c_int
             l.mi355x_probe_sweep_release.argtypes = [ctypes.c_int]
             l.mi355x_probe_gemm_bf16.restype = ctypes.c_int
@@ -119,7 +121,13 @@ def hbm_sweep(dev: int, offset: int, nbytes: int = 16 << 30, reserve: int = 4 <<
     return _take(lib().mi355x_probe_hbm_sweep(dev, opts.encode()))
 
 
+def sweep_alloc(dev: int, reserve: int = 4 << 30) -> int:
+    """Allocate the sweep buffer (all free HBM minus ``reserve``) without blocking probes."""
+    return int(lib().mi355x_probe_sweep_alloc(dev, int(reserve)))
+
+
 def sweep_release(dev: int) -> int:
+    """Free the sweep buffer (seconds for ~280 GB; probes of the device are not blocked)."""
     return int(lib().mi355x_probe_sweep_release(dev))
 
 

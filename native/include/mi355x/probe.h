@@ -38,6 +38,10 @@ char* mi355x_probe_peer(int src, int dst, const char* opts_json);
  * opts: {"offset":0,"bytes":17179869184,"reserve":4294967296,"keep":false,"injectBitFlips":0}
  * -> {"passed","offset","bytes","span","badBits","firstBadOffset","GBps","ms","allocMs"} */
 char* mi355x_probe_hbm_sweep(int device, const char* opts_json);
+/* Allocate / free the sweep buffer without holding the device's probe lock (allocating ~282 GiB
+ * takes ~0.4 s and freeing it ~2.9 s on MI355X: a claim-time probe must never wait for either).
+ * alloc: 1 = allocated, 0 = already held, <0 = error. release: 1 = freed, 0 = none held. */
+int mi355x_probe_sweep_alloc(int device, long long reserve_bytes);
 int mi355x_probe_sweep_release(int device);
 /* The probe's production GEMM (256x256x64 MFMA tile) on caller HOST buffers (copied in and out):
  * C[m][n] (fp32) = A[m][k] (bf16, row-major) * Bt[n][k]^T (bf16, row-major). m, n multiples of

@@ -794,11 +794,6 @@ std::string run_probe(int dev, const char* opts) {
     PROBE_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ctx.host_res), kResSlots * sizeof(unsigned long long)));
     ctx.ready = true;
   }
-  if (ctx.sweep) {  // a claim-time probe always wins over the HBM scrubber's buffer
-    (void)hipFree(ctx.sweep);
-    ctx.sweep = nullptr;
-    ctx.sweep_bytes = 0;
-  }
   hipStream_t s = ctx.stream;
   const hipDeviceProp_t& prop = ctx.prop;
   const int cus = prop.multiProcessorCount;
@@ -1023,6 +1018,21 @@ std::string run_peer(int src, int dst, const char* opts) {
          ",\"bytes\":" + std::to_string(n16 * 16) + ",\"GBps\":" + jnum(gbps) + ",\"ms\":" + jnum(ms) + "}";
 }
 
+// All free HBM minus ``reserve``, 2 MiB granular. Measured on MI355X (profiles/r2g): ~0.4 s to
+// allocate ~282 GiB and ~2.9 s to free it (the driver clears released VRAM), so neither ever runs
+// under the device lock a claim-time probe takes.
+void* sweep_alloc_raw(uint64_t reserve, size_t* span_out) {
+  size_t free_b = 0, total_b = 0;
+  PROBE_CHECK(hipMemGetInfo(&free_b, &total_b));
+  const uint64_t gran = 2ull << 20;
+  if (free_b <= reserve + gran) throw ProbeError("not enough free HBM for a sweep window");
+  const uint64_t span = ((free_b - reserve) / gran) * gran;
+  void* p = nullptr;
+  PROBE_CHECK(hipMalloc(&p, span));
+  *span_out = span;
+  return p;
+}
+
 // One window of the rotating HBM sweep (see mi355x_probe_hbm_sweep in probe.h). The claim-time
 // probe always tests the same ~1 GiB arena; this walks the rest of the 288 GB: a buffer of all free
 // HBM minus ``reserve`` is allocated once per scrub pass (kept while ``keep``), and each call
@@ -1038,13 +1048,9 @@ std::string run_sweep(int dev, const char* opts) {
   PROBE_CHECK(hipSetDevice(dev));
   auto t0 = std::chrono::steady_clock::now();
   double alloc_ms = 0;
-  if (!ctx.sweep) {
-    size_t free_b = 0, total_b = 0;
-    PROBE_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const uint64_t gran = 2ull << 20;
-    if (free_b <= reserve + gran) throw ProbeError("not enough free HBM for a sweep window");
-    const uint64_t span = ((free_b - reserve) / gran) * gran;
-    PROBE_CHECK(hipMalloc(&ctx.sweep, span));
+  if (!ctx.sweep) {  // normally pre-allocated by mi355x_probe_sweep_alloc outside the device lock
+    size_t span = 0;
+    ctx.sweep = sweep_alloc_raw(reserve, &span);
     ctx.sweep_bytes = span;
     alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
@@ -1194,15 +1200,45 @@ char* mi355x_probe_hbm_sweep(int dev, const char* opts_json) {
   }
 }
 
-int mi355x_probe_sweep_release(int dev) {
+int mi355x_probe_sweep_alloc(int dev, long long reserve) {
   if (g_count < 0 || dev < 0 || dev >= g_count) return -1;
+  {
+    std::lock_guard<std::mutex> g(device_mutex(dev));
+    if (g_ctx[static_cast<size_t>(dev)].sweep) return 0;
+  }
+  void* p = nullptr;
+  size_t span = 0;
+  try {
+    if (hipSetDevice(dev) != hipSuccess) return -1;
+    p = sweep_alloc_raw(static_cast<uint64_t>(std::max(0LL, reserve)), &span);
+  } catch (const std::exception&) {
+    (void)hipGetLastError();
+    return -2;
+  }
   std::lock_guard<std::mutex> g(device_mutex(dev));
   DeviceCtx& ctx = g_ctx[static_cast<size_t>(dev)];
-  if (!ctx.sweep) return 0;
+  if (ctx.sweep) {  // lost a race with another allocator: keep theirs
+    (void)hipFree(p);
+    return 0;
+  }
+  ctx.sweep = p;
+  ctx.sweep_bytes = span;
+  return 1;
+}
+
+int mi355x_probe_sweep_release(int dev) {
+  if (g_count < 0 || dev < 0 || dev >= g_count) return -1;
+  void* p = nullptr;
+  {
+    std::lock_guard<std::mutex> g(device_mutex(dev));
+    DeviceCtx& ctx = g_ctx[static_cast<size_t>(dev)];
+    p = ctx.sweep;
+    ctx.sweep = nullptr;
+    ctx.sweep_bytes = 0;
+  }
+  if (!p) return 0;
   if (hipSetDevice(dev) != hipSuccess) return -1;
-  (void)hipFree(ctx.sweep);
-  ctx.sweep = nullptr;
-  ctx.sweep_bytes = 0;
+  (void)hipFree(p);  // seconds for ~280 GB: outside the device lock
   return 1;
 }
 

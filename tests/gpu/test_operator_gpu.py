@@ -192,3 +192,25 @@ def test_autoscaled_pool_grows_for_pending_gpu_pod(cluster_factory, tmp_path):
     assert done["status"]["phase"] == "Succeeded", log[-3000:]
     assert '"arch": "gfx950' in log
     k.wait_for(MI355XPOOLS, "auto", "default", ready_at(0), timeout=60)
+
+
+def test_hbm_scrub_on_real_gpu_and_claim_is_not_blocked(cluster_factory):
+    """The agent's HBM scrubber on the MI355X: two 16 GiB windows of the all-free-HBM buffer are
+    pattern-tested through the RPC, coverage lands in the agent view; a claim issued right after
+    (while the ~280 GB buffer is being freed, ~3 s) is Ready in well under a second, and the pod
+    Allocate path waits for the free. status.devices[] carries the CU census and coverage."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc", extra_args=[
+        "--scrub-interval", "0", "--scrub-window", str(16 << 30)])])
+    r = c.agent_request("gpu-node", "POST", "/v1/scrub", {"gpu": "0", "windows": 2})
+    assert r["ok"], r
+    cov = r["coverage"]
+    assert cov["windows"] == 2 and cov["cursor"] == 32 << 30 and cov["span"] > 200e9, cov
+    assert cov["lastBadBits"] == 0 and cov["lastGBps"] > 3000, cov
+    k = c.client
+    t0 = time.perf_counter()
+    k.create(MI355XPOOLS, pool("p", 1), "default")
+    obj = k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=60)
+    assert time.perf_counter() - t0 < 1.0
+    d = obj["status"]["devices"][0]
+    assert d["probe"]["cusVerified"] == d["probe"]["cusExpected"] == 256, d
+    assert d["hbmCoverage"]["span"] > 200e9, d
