@@ -86,6 +86,17 @@ class Agent:
         self.dev = devlib.DeviceLib(cfg.backend, **dev_cfg)
         self.ledger = Ledger(cfg.state_dir, fsync=cfg.fsync)
         self.records: dict[str, dict] = self.ledger.load()
+        # A claim commits 'Probing' before its probe runs; an agent that died mid-probe leaves such
+        # records behind. Nothing would ever finish them, so they become failed probes and take
+        # the normal replace path (drain -> release -> quarantine -> claim a healthy spare).
+        interrupted = [u for u, r in self.records.items() if r.get("state") == "Probing"]
+        for u in interrupted:
+            self.records[u]["state"] = "Claimed"
+            self.records[u]["probe"] = {"passed": False, "backend": "none", "ms": 0.0,
+                                        "error": "ProbeInterrupted: the agent restarted during "
+                                                 "the claim-time probe"}
+        if interrupted:
+            self.ledger.commit(self.records)
         self.snap = self.dev.snapshot()
         self.backend = self.snap.get("backend", cfg.backend)
         self.by_uuid = {d["uuid"]: d for d in self.snap["devices"]}

@@ -208,7 +208,8 @@ class Mi355xQueueReconciler : public PoolReconcilerBase {
 // (README.md:292-296, roadmap :309-312) and of the cluster-autoscaler a GPU platform runs beside
 // Volcano (GPU调度平台搭建.md:275-287). Demand = GPUs of the pool's resourceName asked for by live
 // pods (bound or pending) + gangs of Mi355xJobs still waiting for a placement (their poolRef or
-// resource) + reserved-but-uncreated job slots, clamped to [minReplicas, maxReplicas]. Scale-up
+// resource) + reserved-but-uncreated job slots, attributed across pools of the same resource
+// (pool_demand), clamped to [minReplicas, maxReplicas]. Scale-up
 // is immediate; scale-down only after demand has stayed below spec.replicas for
 // scaleDownDelaySeconds, and the pool's drain then releases pod-free GPUs first. Writes are JSON
 // merge patches of spec.replicas + two annotations, so they never race the pool's status writes.
@@ -222,6 +223,13 @@ class Mi355xPoolAutoscaler : public PoolReconcilerBase {
   // Pure demand computation over cached pods and jobs; exposed for unit tests.
   static int64_t demand(const std::vector<Json>& pods, const std::vector<Json>& jobs, const std::string& ns,
                         const std::string& pool, const std::string& resource);
+  // Demand attributed to one pool when several pools serve the same resource: gangs naming the
+  // pool (poolRef) are its own; pods and poolRef-less gangs are served first by fixed-size pools of
+  // the resource, the rest is split over autoscaled pools in (namespace, name) order up to their
+  // maxReplicas. A single pool gets exactly demand().
+  static int64_t pool_demand(const std::vector<Json>& pods, const std::vector<Json>& jobs,
+                             const std::vector<Json>& pools, const std::string& ns, const std::string& pool,
+                             const std::string& resource);
 
  private:
   Informer& jobs_;

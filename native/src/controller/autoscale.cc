@@ -60,8 +60,10 @@ int64_t Mi355xPoolAutoscaler::demand(const std::vector<Json>& pods, const std::v
     const std::string phase = j.path("status.phase").str_or("Pending");
     if (terminal(phase) || phase == "Suspended" || j.path("spec.suspend").as_bool(false)) continue;
     if (!j.path("metadata.deletionTimestamp").as_string().empty()) continue;
-    const bool mine = j.path("spec.poolRef").as_string() == pool && j.path("metadata.namespace").as_string() == ns;
-    if (!mine && job_resource(j, gen::kDefaultResource) != resource) continue;
+    const std::string ref = j.path("spec.poolRef").as_string();
+    const bool mine = ref == pool && j.path("metadata.namespace").as_string() == ns;
+    // a gang bound to another pool by poolRef is that pool's demand, never this one's
+    if (!mine && (!ref.empty() || job_resource(j, gen::kDefaultResource) != resource)) continue;
     const int64_t g = j.path("spec.gpusPerReplica").as_int(1);
     const Json& placement = j.path("status.placement");
     if (placement.size() == 0) {
@@ -72,6 +74,57 @@ int64_t Mi355xPoolAutoscaler::demand(const std::vector<Json>& pods, const std::v
     }
   }
   return total;
+}
+
+int64_t Mi355xPoolAutoscaler::pool_demand(const std::vector<Json>& pods, const std::vector<Json>& jobs,
+                                           const std::vector<Json>& pools, const std::string& ns,
+                                           const std::string& pool, const std::string& resource) {
+  // explicit(Q): gangs with poolRef == Q; shared: pods of the resource + gangs without a poolRef
+  auto is_job_of = [](const Json& j, const std::string& qns, const std::string& qname) {
+    return j.path("spec.poolRef").as_string() == qname && j.path("metadata.namespace").as_string() == qns;
+  };
+  auto explicit_of = [&](const std::string& qns, const std::string& qname) {
+    std::vector<Json> mine;
+    for (const auto& j : jobs)
+      if (is_job_of(j, qns, qname)) mine.push_back(j);
+    return demand({}, mine, qns, qname, resource);
+  };
+  std::vector<Json> unbound;
+  for (const auto& j : jobs)
+    if (j.path("spec.poolRef").as_string().empty()) unbound.push_back(j);
+  int64_t remaining = demand(pods, unbound, "", "", resource);
+  // fixed-size pools of the same resource serve shared demand first (whatever their own gangs
+  // leave free); what is left is split over the autoscaled pools in (namespace, name) order up to
+  // each one's maxReplicas, so two autoscaled pools never both grow for the same pods
+  struct Auto {
+    std::string ns, name;
+    int64_t cap, expl;
+  };
+  std::vector<Auto> autos;
+  for (const auto& q : pools) {
+    if (q.path("spec.resourceName").str_or(gen::kDefaultResource) != resource) continue;
+    if (!q.path("metadata.deletionTimestamp").as_string().empty()) continue;
+    const std::string qns = q.path("metadata.namespace").as_string(), qname = q.path("metadata.name").as_string();
+    const int64_t expl = explicit_of(qns, qname);
+    if (q.path("spec.autoscale.enabled").as_bool(false)) {
+      const int64_t hi = std::max(q.path("spec.autoscale.minReplicas").as_int(0), q.path("spec.autoscale.maxReplicas").as_int(0));
+      autos.push_back({qns, qname, std::max<int64_t>(0, hi - expl), expl});
+    } else {
+      remaining -= std::max<int64_t>(0, q.path("spec.replicas").as_int(0) - expl);
+    }
+  }
+  remaining = std::max<int64_t>(0, remaining);
+  std::sort(autos.begin(), autos.end(),
+            [](const Auto& a, const Auto& b) { return a.ns != b.ns ? a.ns < b.ns : a.name < b.name; });
+  for (size_t i = 0; i < autos.size(); ++i) {
+    const Auto& a = autos[i];
+    // the last pool in order takes all that is left (its own maxReplicas clamps it later), so a
+    // single pool's demand is exactly demand() and the overflow stays visible
+    const int64_t share = i + 1 == autos.size() ? remaining : std::min(remaining, a.cap);
+    remaining -= share;
+    if (a.ns == ns && a.name == pool) return a.expl + share;
+  }
+  return explicit_of(ns, pool);  // not (yet) in the pool list
 }
 
 Outcome Mi355xPoolAutoscaler::reconcile(const std::string& ns, const std::string& name) {
@@ -85,7 +138,7 @@ Outcome Mi355xPoolAutoscaler::reconcile(const std::string& ns, const std::string
     low_since_.erase(m.uid);
     return Outcome::done(ms(0));
   }
-  const int64_t d = demand(pods_.list(), jobs_.list(), m.ns, m.name, spec.resource_name);
+  const int64_t d = pool_demand(pods_.list(), jobs_.list(), pools_.list(), m.ns, m.name, spec.resource_name);
   const int64_t lo = spec.autoscale_min, hi = std::max(spec.autoscale_min, spec.autoscale_max);
   const int64_t target = std::clamp(d, lo, hi);
   demand_gauge().set({{"pool", m.key()}}, static_cast<double>(d));

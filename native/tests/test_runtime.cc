@@ -483,6 +483,41 @@ TEST(autoscale_demand) {
   };
   EXPECT_EQ(gpupool::Mi355xPoolAutoscaler::demand(pods, jobs, "ns", "p", "r/g"), 8);  // 2 + 1 + 4 + 1
   EXPECT_EQ(gpupool::Mi355xPoolAutoscaler::demand({}, {}, "ns", "p", "r/g"), 0);
+  // a gang naming another pool is not this pool's demand
+  std::vector<gpupool::Json> other = {J(R"({"metadata":{"namespace":"ns"},"spec":{"poolRef":"q","resourceName":"r/g","replicas":3}})")};
+  EXPECT_EQ(gpupool::Mi355xPoolAutoscaler::demand({}, other, "ns", "p", "r/g"), 0);
+}
+
+TEST(autoscale_pool_demand_attribution) {
+  auto J = [](const char* s) { return gpupool::Json::parse(s); };
+  auto pod = [&](int n) {
+    return J((std::string(R"({"metadata":{},"spec":{"containers":[{"resources":{"limits":{"r/g":)") +
+              std::to_string(n) + "}}}]}}").c_str());
+  };
+  auto P = [&](const char* name, bool autoscale, int replicas, int maxr) {
+    return J((std::string(R"({"metadata":{"namespace":"ns","name":")") + name + R"("},"spec":{"resourceName":"r/g","replicas":)" +
+              std::to_string(replicas) + R"(,"autoscale":{"enabled":)" + (autoscale ? "true" : "false") +
+              R"(,"minReplicas":0,"maxReplicas":)" + std::to_string(maxr) + "}}}")
+                 .c_str());
+  };
+  using A = gpupool::Mi355xPoolAutoscaler;
+  std::vector<gpupool::Json> pods = {pod(2), pod(2), pod(2)};  // 6 GPUs
+  // two autoscaled pools: split in name order up to maxReplicas (4 + 2), never 6 + 6
+  std::vector<gpupool::Json> pools = {P("b", true, 0, 4), P("a", true, 0, 4)};
+  EXPECT_EQ(A::pool_demand(pods, {}, pools, "ns", "a", "r/g"), 4);
+  EXPECT_EQ(A::pool_demand(pods, {}, pools, "ns", "b", "r/g"), 2);
+  pools = {P("b", true, 0, 4), P("a", true, 0, 2)};  // overflow goes to the last pool
+  EXPECT_EQ(A::pool_demand(pods, {}, pools, "ns", "a", "r/g"), 2);
+  EXPECT_EQ(A::pool_demand(pods, {}, pools, "ns", "b", "r/g"), 4);
+  // a fixed pool of 4 serves shared demand first: the autoscaled pool sees only 2
+  pools = {P("a", true, 0, 8), P("fixed", false, 4, 0)};
+  EXPECT_EQ(A::pool_demand(pods, {}, pools, "ns", "a", "r/g"), 2);
+  // its own gang counts for it regardless of the shared split
+  std::vector<gpupool::Json> jobs = {J(R"({"metadata":{"namespace":"ns"},"spec":{"poolRef":"a","replicas":3}})")};
+  EXPECT_EQ(A::pool_demand(pods, jobs, pools, "ns", "a", "r/g"), 5);
+  // a single pool gets exactly demand()
+  pools = {P("a", true, 0, 16)};
+  EXPECT_EQ(A::pool_demand(pods, jobs, pools, "ns", "a", "r/g"), A::demand(pods, jobs, "ns", "a", "r/g"));
 }
 
 TEST(job_validation) {

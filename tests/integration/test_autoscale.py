@@ -86,3 +86,24 @@ def test_scale_down_delay_counts_from_the_drop(cluster_factory):
     assert k.get(MI355XPOOLS, "steady", "default")["spec"]["replicas"] == 2
     wait_ready(k, "steady", 1, timeout=30)
     assert time.monotonic() - t0 >= 2.5
+
+
+def test_two_pools_same_resource_do_not_double_count(cluster_factory):
+    """A fixed pool of 4 and an autoscaled pool serve the same resource: 6 GPUs of pending pods
+    grow the autoscaled pool to 2 (the fixed pool serves 4), not to 6 (which would claim idle
+    GPUs for pods the other pool already serves)."""
+    k = cluster_factory().client
+    k.create(MI355XPOOLS, mi_pool("fixed", 4, resourceName=RES), "default")
+    wait_ready(k, "fixed", 4)
+    k.create(MI355XPOOLS, mi_pool("auto", 0, resourceName=RES,
+                                  autoscale={"enabled": True, "minReplicas": 0, "maxReplicas": 8,
+                                             "scaleDownDelaySeconds": 60}), "default")
+    wait_ready(k, "auto", 0)
+    for i in range(3):
+        k.create(PODS, pause_pod(f"p{i}", resource=RES, n=2), "default")
+    pool = wait_ready(k, "auto", 2)
+    assert pool["metadata"]["annotations"]["gpupool.amd.com/autoscale-demand"] == "2"
+    for i in range(3):
+        running(k, f"p{i}")
+    time.sleep(1.0)
+    assert k.get(MI355XPOOLS, "auto", "default")["spec"]["replicas"] == 2

@@ -189,6 +189,32 @@ def test_agent_restart_keeps_ledger(node8):
         {d["uuid"] for d in before["status"]["devices"]}
 
 
+def test_agent_crash_mid_probe_is_replaced(node8):
+    """A claim is committed as 'Probing' before the probe runs; an agent killed between the two
+    ledger commits must not leave the pool stuck Progressing=Probing forever: on restart the record
+    becomes a failed probe (ProbeInterrupted) and the pool replaces that GPU."""
+    import json
+    import os
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    before = wait_ready(k, "p", 2)
+    victim = before["status"]["devices"][1]["uuid"]
+    node8._kill("agent-mi355x-node-0")
+    path = os.path.join(node8.workdir, "state-mi355x-node-0", "ledger.json")
+    with open(path) as f:
+        doc = json.load(f)
+    doc["claims"][victim].update({"state": "Probing", "probe": None})
+    with open(path, "w") as f:
+        json.dump(doc, f)
+    node8.start_agent(node8.nodes[0])
+
+    def replaced(o):
+        return ready_at(2)(o) and victim not in {d["uuid"] for d in o["status"]["devices"]}
+    k.wait_for(MI355XPOOLS, "p", "default", replaced, timeout=30)
+    d = next(x for x in agent_view(node8)["devices"] if x["uuid"] == victim)
+    assert d["state"] == "Quarantined" and "probe failed" in d["quarantine"]["reason"]
+
+
 def test_orphan_sweep_releases_claims_of_deleted_pool(cluster_factory):
     c = cluster_factory(manager_args=["--orphan-sweep", "500ms"])
     k = c.client
