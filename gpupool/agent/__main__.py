@@ -27,6 +27,9 @@ def main() -> None:
     ap.add_argument("--endpoint", default="", help="endpoint written to the Node annotation")
     ap.add_argument("--apiserver", default=os.environ.get("GPUPOOL_APISERVER", ""))
     ap.add_argument("--token", default=os.environ.get("GPUPOOL_TOKEN", ""))
+    ap.add_argument("--auth-token-file", default=os.environ.get("GPUPOOL_AGENT_TOKEN_FILE", ""),
+                    help="shared secret required on the RPC (Authorization: Bearer); "
+                         "$GPUPOOL_AGENT_TOKEN also works")
     ap.add_argument("--plugin-dir", default="", help="kubelet device-plugin directory")
     ap.add_argument("--pod-resources", default="", help="kubelet PodResources socket")
     ap.add_argument("--probe", default="", choices=["", "inproc", "subprocess", "simulated", "off"])
@@ -49,7 +52,11 @@ def main() -> None:
     a = ap.parse_args()
     logging.basicConfig(level=logging.DEBUG if a.verbose else logging.INFO,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
-    cfg = AgentConfig(node=a.node, backend=a.backend, fixture=a.fixture, faults=a.faults,
+    auth = os.environ.get("GPUPOOL_AGENT_TOKEN", "")
+    if a.auth_token_file:
+        with open(a.auth_token_file) as f:
+            auth = f.read().strip()
+    cfg = AgentConfig(node=a.node, auth_token=auth, backend=a.backend, fixture=a.fixture, faults=a.faults,
                       count=a.count, cli_dir=a.cli_dir, state_dir=a.state_dir, socket=a.socket,
                       listen=a.listen, endpoint=a.endpoint, apiserver=a.apiserver, token=a.token,
                       plugin_dir=a.plugin_dir, pod_resources=a.pod_resources, probe_mode=a.probe,

@@ -94,6 +94,8 @@ BUILTINS = [
                  status_sub=True),
     ResourceType("apps", "v1", "daemonsets", "DaemonSet", True, "daemonset", ["ds"],
                  status_sub=True),
+    ResourceType("networking.k8s.io", "v1", "networkpolicies", "NetworkPolicy", True,
+                 "networkpolicy", ["netpol"]),
     ResourceType("rbac.authorization.k8s.io", "v1", "clusterroles", "ClusterRole", False,
                  "clusterrole"),
     ResourceType("rbac.authorization.k8s.io", "v1", "clusterrolebindings", "ClusterRoleBinding",

@@ -330,7 +330,7 @@ def cmd_devices(c: Client, ns: str, args) -> int:
     if not ep:
         print(f"error: node {args.node} has no gpupool agent", file=sys.stderr)
         return 1
-    view = Client(ep).request("GET", "/v1/node")
+    view = Client(ep, _agent_token()).request("GET", "/v1/node")
     if args.output in ("json", "yaml"):
         dump(view, args.output)
         return 0
@@ -349,7 +349,18 @@ def _agent(c: Client, node: str) -> Client | None:
     if not ep:
         print(f"error: node {node} has no gpupool agent", file=sys.stderr)
         return None
-    return Client(ep)
+    return Client(ep, _agent_token())
+
+
+def _agent_token() -> str | None:
+    """The node agents' shared RPC secret: $GPUPOOL_AGENT_TOKEN or the file named by
+    $GPUPOOL_AGENT_TOKEN_FILE (the gpupool-agent-token Secret in a cluster)."""
+    tok = os.environ.get("GPUPOOL_AGENT_TOKEN")
+    path = os.environ.get("GPUPOOL_AGENT_TOKEN_FILE")
+    if not tok and path and os.path.exists(path):
+        with open(path) as f:
+            tok = f.read().strip()
+    return tok or None
 
 
 def cmd_gpu(c: Client, ns: str, args) -> int:

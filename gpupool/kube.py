@@ -76,6 +76,7 @@ BY_KIND = {
     "Deployment": Res("apps", "v1", "deployments"),
     "DaemonSet": Res("apps", "v1", "daemonsets"),
     "PodDisruptionBudget": Res("policy", "v1", "poddisruptionbudgets"),
+    "NetworkPolicy": Res("networking.k8s.io", "v1", "networkpolicies"),
 }
 
 

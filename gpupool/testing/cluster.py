@@ -117,6 +117,13 @@ class Cluster:
         self.kinds = kinds
         self.manager_bin = manager_bin
         self.procs: dict[str, subprocess.Popen] = {}
+        # the agents' RPC requires a shared secret (as deployed: the gpupool-agent-token Secret)
+        self.agent_token = os.urandom(16).hex()
+        self.agent_token_file = os.path.join(self.workdir, "agent-token")
+        with open(self.agent_token_file, "w") as f:
+            f.write(self.agent_token + "\n")
+        os.chmod(self.agent_token_file, 0o600)
+        self.env["GPUPOOL_AGENT_TOKEN"] = self.agent_token
         self.url = ""
         self.client: Client | None = None
 
@@ -198,7 +205,8 @@ class Cluster:
                 "--state-dir", os.path.join(self.workdir, f"state-{node.name}"),
                 "--socket", self.agent_socket(node.name), "--apiserver", self.url,
                 "--faults", self.faults_path(node.name), "--ready-file", rf,
-                "--sample-interval", str(self.sample_interval), "--no-fsync"]
+                "--sample-interval", str(self.sample_interval), "--no-fsync",
+                "--auth-token-file", self.agent_token_file]
         if node.backend == "fake":
             argv += ["--fixture", node.fixture]
         if node.count >= 0:
@@ -222,7 +230,8 @@ class Cluster:
         if os.path.exists(pf):
             os.remove(pf)
         argv = [self.manager_bin or native_bin("gpupool-manager"), "--apiserver", self.url, "--port-file", pf,
-                "--kinds", self.kinds, "--progress-poll", "100ms"]
+                "--kinds", self.kinds, "--progress-poll", "100ms",
+                "--agent-token-file", self.agent_token_file]
         if self.tls:
             argv += ["--ca-file", self.ca_file]
         if self.token:
@@ -271,7 +280,7 @@ class Cluster:
             self.agent_request(node, "POST", "/v1/sample", {})
 
     def agent_request(self, node: str, method: str, path: str, body: dict | None = None) -> dict:
-        c = Client("unix://" + self.agent_socket(node))
+        c = Client("unix://" + self.agent_socket(node), self.agent_token)
         return c.request(method, path, body)
 
     def manager_metrics(self) -> str:

@@ -149,7 +149,9 @@ class DeviceProvider {
 // Agents are discovered from Node objects annotated gpupool.amd.com/agent-endpoint.
 class RocmProvider : public DeviceProvider {
  public:
-  RocmProvider(Informer& nodes, int timeout_ms = 30000);
+  RocmProvider(Informer& nodes, int timeout_ms = 30000, std::string agent_token = "");
+  // shared secret presented to the node agents (Authorization: Bearer)
+  const std::string& agent_token() const { return agent_token_; }
   std::vector<std::string> node_names() override;
   Json node_labels(const std::string& node) override;
   NodeView observe(const std::string& node) override;
@@ -167,6 +169,7 @@ class RocmProvider : public DeviceProvider {
   Json post_(const std::string& node, const std::string& path, const Json& body);
   Informer& nodes_;
   int timeout_ms_;
+  std::string agent_token_;
   std::mutex mu_;
   std::map<std::string, std::pair<std::string, std::shared_ptr<HttpClient>>> clients_;
 };

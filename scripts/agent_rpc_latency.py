@@ -17,7 +17,7 @@ node = NodeSpec("n0", backend="fake", probe="simulated", count=8)
 cl = Cluster(tempfile.mkdtemp(prefix="rpc-"), nodes=[node], manager=False)
 cl.start()
 try:
-    agent = Client("unix://" + cl.agent_socket("n0"))
+    agent = Client("unix://" + cl.agent_socket("n0"), cl.agent_token)
     prs = os.path.join(cl.kubelet_root(node), "pod-resources", "kubelet.sock")
     ops = {"agent_healthz": lambda: agent.request("GET", "/healthz"),
            "agent_node": lambda: agent.request("GET", "/v1/node"),

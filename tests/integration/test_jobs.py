@@ -20,7 +20,9 @@ from .helpers import conds, mi_pool, wait_ready
 pytestmark = pytest.mark.slow
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-_port = [29600]
+# per-process base: pytest-xdist workers each run their own copy of this module, so a fixed base
+# would hand two concurrently running DDP jobs the same rendezvous port
+_port = [29600 + 200 * (int(os.environ.get("PYTEST_XDIST_WORKER", "gw0")[2:] or 0) % 40)]
 
 
 def job(name: str, replicas: int, command: list[str], gpus: int = 1, **spec) -> dict:
@@ -421,7 +423,9 @@ def test_elastic_gang_min_available(node8):
     assert "gang of 2..4" in conds(o)["Scheduled"]["message"]
     k.delete(MI355XJOBS, "busy", "default")
     o = k.wait_for(MI355XJOBS, "el2", "default", phase_is("Succeeded"), timeout=30)
-    assert o["status"]["workers"] == 3
+    # the gang starts as soon as minAvailable GPUs are free: busy's two pods end one by one, so it
+    # sees 2 or (when both endings land in one pass) 3 — elastic, never below minAvailable
+    assert 2 <= o["status"]["workers"] <= 3 and o["status"]["succeeded"] == o["status"]["workers"]
 
 
 def test_gpu_fault_under_running_gang_restarts_it_on_healthy_gpus(node8):

@@ -66,6 +66,7 @@ def test_manager_and_gpuctl_via_kubeconfig_token(cluster_factory, tmp_path):
     # the manager gets NOTHING but the kubeconfig (no --apiserver / --token / --ca-file)
     mlog = open(tmp_path / "mgr.log", "wb")
     env = {k: v for k, v in os.environ.items() if k not in ("GPUPOOL_APISERVER", "GPUPOOL_TOKEN")}
+    env["GPUPOOL_AGENT_TOKEN"] = c.agent_token  # the agents' RPC secret (a mounted Secret in-cluster)
     m = subprocess.Popen([native_bin("gpupool-manager"), "--kubeconfig", kc, "--kinds", "mi355x",
                           "--progress-poll", "100ms"], stdout=mlog, stderr=subprocess.STDOUT,
                          start_new_session=True, env=env)

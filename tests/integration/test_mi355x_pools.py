@@ -444,7 +444,8 @@ def test_gpu_maintenance_cordon(node8):
     k.create(MI355XPOOLS, mi_pool("p", 2), "default")
     o = wait_ready(k, "p", 2)
     victim = o["status"]["devices"][0]
-    env = dict(os.environ, PYTHONPATH=node8.env["PYTHONPATH"], GPUPOOL_APISERVER=node8.url)
+    env = dict(os.environ, PYTHONPATH=node8.env["PYTHONPATH"], GPUPOOL_APISERVER=node8.url,
+               GPUPOOL_AGENT_TOKEN_FILE=node8.agent_token_file)  # the admin's copy of the Secret
 
     def gpuctl(*a):
         r = subprocess.run([sys.executable, "-m", "gpupool.cli", *a], env=env, capture_output=True,
@@ -495,3 +496,26 @@ def test_many_pools_fill_every_gpu_across_nodes(cluster_factory):
     # freeing one GPU wakes the waiting pool without waiting for its requeue
     k.patch(MI355XPOOLS, "p0", {"spec": {"replicas": 0}}, "default")
     wait_ready(k, "extra", 1, timeout=15)
+
+
+def test_agent_rpc_requires_the_shared_token(node8):
+    """The agent's RPC refuses callers without the manager's shared secret (any pod
+    could otherwise claim, cordon or release GPUs); /healthz and /metrics stay open."""
+    from gpupool.kube import Client
+    anon = Client("unix://" + node8.agent_socket("mi355x-node-0"))
+    for method, path, body in (("POST", "/v1/claims", {"poolUID": "x", "count": 1}),
+                               ("POST", "/v1/maintenance", {"gpu": "0", "on": True}),
+                               ("POST", "/v1/release", {"poolUID": "x", "uuids": []}),
+                               ("GET", "/v1/node", None)):
+        with pytest.raises(KubeError) as ei:
+            anon.request(method, path, body)
+        assert ei.value.code == 401
+    wrong = Client("unix://" + node8.agent_socket("mi355x-node-0"), "not-the-token")
+    with pytest.raises(KubeError) as ei:
+        wrong.request("POST", "/v1/claims", {"poolUID": "x", "count": 1})
+    assert ei.value.code == 401
+    assert "gpupool_device_healthy" in str(anon.request("GET", "/metrics"))
+    assert agent_view(node8)["devices"]  # the harness (and the manager) hold the token
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 1), "default")
+    wait_ready(k, "p", 1)
