@@ -7,6 +7,7 @@ import asyncio
 import logging
 import os
 import socket
+import sys
 
 from .agent import Agent, AgentConfig, serve
 
@@ -47,9 +48,17 @@ def main() -> None:
     ap.add_argument("--scrub-reserve", type=int, default=4 << 30,
                     help="HBM bytes the scrub buffer leaves free")
     ap.add_argument("--scrub-start-delay", type=float, default=30.0)
+    ap.add_argument("--gil-switch-interval", type=float,
+                    default=float(os.environ.get("GPUPOOL_GIL_SWITCH_INTERVAL", "0.0005")),
+                    help="sys.setswitchinterval for the agent (s): how long a thread that wants "
+                         "the GIL waits for the holder to yield (CPython default 0.005)")
     ap.add_argument("--ready-file", default="")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
+    if a.gil_switch_interval > 0:
+        # The agent's threads (RPC loop, claim executor, sampler, device-plugin gRPC) hand the GIL
+        # to each other on every claim; at the 5 ms default one hand-off can cost milliseconds.
+        sys.setswitchinterval(a.gil_switch_interval)
     logging.basicConfig(level=logging.DEBUG if a.verbose else logging.INFO,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     auth = os.environ.get("GPUPOOL_AGENT_TOKEN", "")

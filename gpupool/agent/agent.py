@@ -120,9 +120,14 @@ class Agent:
             if q.get("maintenance")}
         self._rechecking: set[str] = set()
         self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0, "rechecks": 0,
-                      "probe_ms_sum": 0.0, "samples": 0}
+                      "probe_ms_sum": 0.0, "samples": 0, "sample_ms_sum": 0.0,
+                      "device_events": 0, "fault_events": 0}
+        self.resetting: set[str] = set()       # GPUs between amdsmi GPUPreReset and GPUPostReset
+        self.recent_events: list[dict] = []   # last hardware/overlay events (node view, metrics)
+        self.events_supported: dict[str, Any] = {}
         self._pods_cache: tuple[float, dict[str, list[dict]]] = (0.0, {})
         self._pods_refreshing = False
+        self._pods_watch_until = 0.0
         from .podresources import PodResourcesClient
         self._podres = PodResourcesClient(cfg.pod_resources) if cfg.pod_resources else None
         self._stop = threading.Event()
@@ -146,13 +151,68 @@ class Agent:
         rec = self.records.get(uuid)
         return (rec or {}).get("policy") or {}
 
+    # Health categories that belong to the ASIC package, not to one partition: in CPX mode the 8
+    # logical GPUs of an MI355X share its HBM stacks (ECC, retired pages), xGMI links and sensors,
+    # so a fault seen through any partition is a fault of all of them. Probe results, partition
+    # mode and admin maintenance stay per logical GPU.
+    ASIC_SCOPED = ("xgmiOk", "eccOk", "thermalOk")
+
+    @staticmethod
+    def _asic_key(d: dict) -> str:
+        return str((d.get("asic") or {}).get("serial") or "") or f"bdf:{d.get('bdf', '')[:-1]}"
+
+    def _fan_out_asic(self, raw: dict[str, dict]) -> dict[str, dict]:
+        """Spread ASIC-scoped faults of one partition to its siblings (no-op in SPX mode)."""
+        groups: dict[str, list[str]] = {}
+        for u, d in self.by_uuid.items():
+            groups.setdefault(self._asic_key(d), []).append(u)
+        out = dict(raw)
+        for members in groups.values():
+            if len(members) < 2:
+                continue
+            for flag in self.ASIC_SCOPED:
+                bad = [m for m in members if raw.get(m, {}).get(flag) is False]
+                if not bad:
+                    continue
+                for s_ in members:
+                    if s_ in bad:
+                        continue
+                    src = bad[0]
+                    why = raw[src].get("reasons", [])
+                    v = dict(out[s_])
+                    v[flag] = False
+                    v["healthy"] = False
+                    v["reasons"] = list(v.get("reasons") or []) + [
+                        f"ASICFault: sibling partition {self.by_uuid[src].get('index')} of this "
+                        f"ASIC: {'; '.join(why) or flag}"]
+                    out[s_] = v
+        return out
+
+    def _asic_faulted(self) -> dict[str, set[str]]:
+        """ASIC key -> partitions whose own (pre-fan-out) ASIC-scoped health failed."""
+        bad: dict[str, set[str]] = {}
+        for u, v in self.verdicts.items():
+            d = self.by_uuid.get(u)
+            if d is not None and any(v.get(f) is False for f in self.ASIC_SCOPED) and \
+                    not any(str(r).startswith("ASICFault:") for r in v.get("reasons") or []):
+                bad.setdefault(self._asic_key(d), set()).add(u)
+        return bad
+
     def _evaluate_all(self) -> set[str]:
         """Re-evaluate every device; returns pool UIDs whose devices changed verdict."""
         changed: set[str] = set()
+        raw: dict[str, dict] = {}
         for uuid, d in self.by_uuid.items():
             rec = self.records.get(uuid)
             baseline = (rec or {}).get("baseline") or d
-            v = devlib.evaluate(d, baseline, self._policy_for(uuid))
+            raw[uuid] = devlib.evaluate(d, baseline, self._policy_for(uuid))
+        raw = self._fan_out_asic(raw)
+        for uuid, d in self.by_uuid.items():
+            rec = self.records.get(uuid)
+            v = raw[uuid]
+            if uuid in self.resetting:  # between amdsmi pre- and post-reset events
+                v = {**v, "healthy": False,
+                     "reasons": list(v.get("reasons") or []) + ["GPUReset: the GPU is being reset"]}
             if uuid in self.maintenance:  # admin-cordoned: unhealthy for pools, never claimed
                 v = {**v, "healthy": False,
                      "reasons": list(v.get("reasons") or []) +
@@ -177,12 +237,15 @@ class Agent:
         return changed
 
     def sample(self) -> set[str]:
+        t0 = time.perf_counter()
         snap = self.dev.snapshot()
+        dt = (time.perf_counter() - t0) * 1e3
         with self.lock:
             self.snap = snap
             self.by_uuid = {d["uuid"]: d for d in snap["devices"]}
             changed = self._evaluate_all()
             self.stats["samples"] += 1
+            self.stats["sample_ms_sum"] += dt
         if changed:
             self._bump(changed)
             self._notify_plugins()
@@ -203,6 +266,91 @@ class Agent:
                 self.recheck_probes()
             except Exception:
                 log.exception("probe recheck failed")
+
+    # ---- event-driven detection (the sampler is the fallback for what has no event)
+    def _note_event(self, ev: dict) -> None:
+        ev = {**ev, "at": now_rfc3339()}
+        with self.lock:
+            self.recent_events = (self.recent_events + [ev])[-32:]
+
+    def _device_event_watcher(self) -> None:
+        """amdsmi event notification (thermal throttle, GPU pre/post reset, VM fault): each event
+        triggers an immediate sample instead of waiting for the next period. A GPU between its
+        pre- and post-reset events is unhealthy (GPUReset); after the reset a claimed GPU is
+        re-probed, since the reset wiped whatever the claim-time probe verified."""
+        while not self._stop.is_set():
+            try:
+                r = self.dev.wait_events(500)
+            except Exception as e:
+                log.warning("device event wait failed: %s", e)
+                return
+            self.events_supported["device"] = r.get("supported", False)
+            if not r.get("supported"):
+                if r.get("error"):
+                    log.info("amdsmi event notification unavailable: %s", r["error"])
+                return
+            evs = r.get("events") or []
+            if not evs:
+                continue
+            recheck = []
+            with self.lock:
+                by_index = {d.get("index"): u for u, d in self.by_uuid.items()}
+                for ev in evs:
+                    u = by_index.get(ev.get("index"))
+                    self.stats["device_events"] += 1
+                    if ev.get("type") == "GPUPreReset" and u:
+                        self.resetting.add(u)
+                    elif ev.get("type") == "GPUPostReset" and u:
+                        self.resetting.discard(u)
+                        if (self.records.get(u) or {}).get("state") == "Claimed":
+                            recheck.append(u)
+            for ev in evs:
+                log.warning("device event on GPU %s: %s %s", ev.get("index"), ev.get("type"),
+                            ev.get("message", ""))
+                self._note_event({"source": "amdsmi", **ev})
+            self.sample()
+            for u in recheck:
+                self._recheck_after_reset(u)
+
+    def _recheck_after_reset(self, uuid: str) -> None:
+        with self.lock:
+            rec = self.records.get(uuid)
+            if not rec or uuid in self._rechecking or uuid not in self.by_uuid:
+                return
+            self._rechecking.add(uuid)
+            opts = (rec.get("policy") or {}).get("probe") or {}
+            job = (uuid, dict(self.by_uuid[uuid]), opts, rec["poolUID"])
+        self.prober.pool.submit(self._recheck_one, *job)
+
+    def _fault_watcher(self) -> None:
+        """The fault overlay file is itself an event source: a rewrite is applied at once (inotify)
+        unless the overlay sets ``"notify": false`` — then only the periodic sample sees it, which
+        is how a real ECC counter change (amdsmi has no ECC event) is detected."""
+        while not self._stop.is_set():
+            try:
+                r = self.dev.wait_faults(500)
+            except Exception as e:
+                log.warning("fault overlay watch failed: %s", e)
+                return
+            self.events_supported["faultOverlay"] = r.get("supported", False)
+            if not r.get("supported"):
+                return
+            if not r.get("changed"):
+                continue
+            try:
+                with open(self.cfg.faults) as f:
+                    overlay = json.load(f)
+            except (OSError, ValueError):
+                overlay = {}  # removed or mid-write: the change itself is the event
+            if isinstance(overlay, dict) and overlay.get("notify") is False:
+                continue
+            with self.lock:
+                self.stats["fault_events"] += 1
+            self._note_event({"source": "faultOverlay", "type": "FaultOverlayChanged"})
+            try:
+                self.sample()
+            except Exception:
+                log.exception("health sample failed")
 
     def recheck_probes(self, force: bool = False) -> list[str]:
         """Periodic functional re-probe (spec.probe.recheckSeconds) of claimed GPUs that run no
@@ -281,10 +429,13 @@ class Agent:
     def _pods_by_device(self, fresh: bool = False) -> dict[str, list[dict]]:
         """device ID -> pods holding it, from the kubelet's PodResources API.
 
-        Views (``fresh=False``) never wait for the kubelet: they return the last answer and, when
-        it is older than 50 ms, start one background refresh (single-flight). A refresh that
-        changes which pods hold a pool's GPUs bumps that pool, so a drain waiting for evicted pods
-        to end is woken by the change itself. The sampler also refreshes every period. Release
+        Views (``fresh=False``) never wait for the kubelet: they return the last answer. Only
+        while pod placement is expected to change (a GPU is draining, or a device-plugin Allocate
+        happened in the last 2 s) does a view older than 50 ms start one background refresh
+        (single-flight); otherwise the sampler refreshes every period. Spawning a refresh thread
+        on every view put a GIL hand-off on the claim path's ``GET /v1/node`` (profiles/
+        r2d_agent_rpc_latency_real.json). A refresh that changes which pods hold a pool's GPUs
+        bumps that pool, so a drain waiting for evicted pods to end is woken by the change itself. Release
         decisions pass ``fresh=True``: they always ask the kubelet synchronously and raise if it
         cannot answer, so a stale or failed lookup can never free a GPU that a pod still holds."""
         if not self.cfg.pod_resources:
@@ -292,9 +443,18 @@ class Agent:
         if fresh:
             return self._refresh_pods()
         ts, cache = self._pods_cache
-        if time.monotonic() - ts >= 0.05:
+        now = time.monotonic()
+        if now - ts >= 0.05 and (now < self._pods_watch_until or self._draining()):
             self._refresh_pods_async()
         return cache
+
+    def _draining(self) -> bool:
+        return any(r.get("state") == "Draining" for r in self.records.values())
+
+    def _watch_pods(self, seconds: float = 2.0) -> None:
+        """Pod placement is about to change (a device-plugin Allocate): views refresh the pod map
+        in the background for a while, so the new pod shows up without waiting for the sampler."""
+        self._pods_watch_until = max(self._pods_watch_until, time.monotonic() + seconds)
 
     def _refresh_pods(self) -> dict[str, list[dict]]:
         pods = self._podres.list_pod_devices()
@@ -358,12 +518,21 @@ class Agent:
         cov = self.scrubber.coverage(uuid)
         if cov:
             out["hbmSweep"] = cov
+        out["telemetry"] = self._telemetry(d)
         if not rec:
             q = self.ledger.quarantined().get(uuid) if self.ledger else None
             out["state"] = ("Maintenance" if q.get("maintenance") else "Quarantined") if q else "Free"
             if q:
                 out["quarantine"] = q
         return out
+
+    @staticmethod
+    def _telemetry(d: dict) -> dict:
+        """Utilisation as last sampled (amdsmi_get_gpu_activity / _power_info / _memory_usage)."""
+        act, pw = d.get("activity") or {}, d.get("power") or {}
+        return {"gfxActivity": act.get("gfx"), "umcActivity": act.get("umc"),
+                "powerW": pw.get("socketW"), "memUsedBytes": d.get("memUsedBytes"),
+                "memTotalBytes": d.get("memTotalBytes")}
 
     def node_view(self) -> dict:
         pods = self._pods_by_device()
@@ -373,6 +542,8 @@ class Agent:
             return {"node": self.cfg.node, "backend": self.backend, "gen": self.gen,
                     "probeMode": self.probe_mode, "preflight": self.preflight,
                     "advertiseRequired": bool(self.cfg.plugin_dir),
+                    "eventSources": dict(self.events_supported),
+                    "recentEvents": list(self.recent_events[-8:]),
                     "devices": devices, "topology": self.snap.get("topology", {})}
 
     # ================================================================ claims
@@ -393,11 +564,15 @@ class Agent:
         with self.lock:
             quarantined = self.ledger.quarantined()
             free = []
+            asic_bad = self._asic_faulted()
             for uuid, d in self.by_uuid.items():
                 if uuid in self.records or uuid in quarantined or not d.get("present", True):
                     continue
-                # claimability under the requesting pool's policy (baseline = now)
-                if devlib.evaluate(d, d, policy).get("healthy"):
+                # claimability under the requesting pool's policy (baseline = now: retired HBM
+                # pages and absolute limits count, deltas start at the claim), and no partition
+                # of the same ASIC carrying a package-level fault
+                if devlib.evaluate(d, d, policy).get("healthy") and \
+                        not asic_bad.get(self._asic_key(d), set()) - {uuid}:
                     free.append(d["index"])
             owned = [self.by_uuid[u]["index"] for u, r in self.records.items()
                      if r["poolUID"] == pool_uid and u in self.by_uuid]
@@ -419,7 +594,7 @@ class Agent:
             for d in chosen:
                 rec = {"uuid": d["uuid"], "poolUID": pool_uid, "pool": req.get("pool", ""),
                        "resourceName": resource, "policy": policy,
-                       "baseline": {"ecc": d.get("ecc", {})}, "claimedAt": ts,
+                       "baseline": {"ecc": dict(d.get("ecc") or {})}, "claimedAt": ts,
                        "state": "Probing", "probe": None}
                 self.records[d["uuid"]] = rec
             self.ledger.commit(self.records)  # durable before probing: no double claim on crash
@@ -658,6 +833,7 @@ class Agent:
         for u in ids:  # a pod never starts while the HBM scrubber still frees its buffer
             if not self.scrubber.wait_released(u):
                 raise ValueError(f"device {u}: HBM scrub buffer still being released")
+        self._watch_pods()
         with self.lock:
             hip, render = [], []
             for u in ids:
@@ -763,8 +939,25 @@ class Agent:
         with self.lock:
             lines.append("# TYPE gpupool_device_healthy gauge")
             for u, d in self.by_uuid.items():
-                lab = f'uuid="{u}",index="{d.get("index")}",node="{self.cfg.node}"'
+                rec = self.records.get(u) or {}
+                lab = f'uuid="{u}",index="{d.get("index")}",node="{self.cfg.node}",' \
+                      f'pool="{rec.get("pool", "")}"'
                 v = self.verdicts.get(u, {})
+                # utilisation (GPU调度平台搭建.md:800 "Prometheus + Grafana, GPU utilisation");
+                # the pool label lets dashboards aggregate per pool / tenant
+                tel = self._telemetry(d)
+                for name, key in (("gpupool_device_gfx_activity_percent", "gfxActivity"),
+                                  ("gpupool_device_umc_activity_percent", "umcActivity"),
+                                  ("gpupool_device_power_watts", "powerW"),
+                                  ("gpupool_device_vram_used_bytes", "memUsedBytes"),
+                                  ("gpupool_device_vram_total_bytes", "memTotalBytes")):
+                    if isinstance(tel.get(key), (int, float)):
+                        lines.append(f"{name}{{{lab}}} {tel[key]}")
+                ras = d.get("ras") or {}
+                if ras.get("badPagesSupported"):
+                    for t in ("retired", "pending", "unreservable"):
+                        lines.append(f'gpupool_device_hbm_bad_pages{{{lab},state="{t}"}} '
+                                     f"{ras.get(t + 'Pages', 0)}")
                 lines.append(f"gpupool_device_healthy{{{lab}}} {1 if v.get('healthy') else 0}")
                 lines.append(f"gpupool_device_claimed{{{lab}}} {1 if u in self.records else 0}")
                 lines.append(f"gpupool_device_xgmi_links_up{{{lab}}} "
@@ -789,6 +982,8 @@ class Agent:
                                  f"{float((pr.get('mfma') or {}).get('tflops') or 0):.1f}")
             for k, v in self.stats.items():
                 lines.append(f"gpupool_agent_{k} {v}")
+            for src, ok in self.events_supported.items():
+                lines.append(f'gpupool_agent_event_source_supported{{source="{src}"}} {1 if ok else 0}')
             for k, v in self.scrubber.stats.items():
                 lines.append(f"gpupool_agent_hbm_scrub_{k}_total {v}")
             lines.append(f"gpupool_agent_gen {self.gen}")
@@ -803,9 +998,11 @@ class Agent:
                 log.info("podresources not reachable yet: %s", e)
         for res in {r.get("resourceName", schema.DEFAULT_RESOURCE) for r in self.records.values()}:
             self._ensure_plugin(res)
-        t = threading.Thread(target=self._sampler, daemon=True, name="sampler")
-        t.start()
-        self._threads.append(t)
+        for fn, name in ((self._sampler, "sampler"), (self._device_event_watcher, "dev-events"),
+                         (self._fault_watcher, "fault-watch")):
+            t = threading.Thread(target=fn, daemon=True, name=name)
+            t.start()
+            self._threads.append(t)
         self.scrubber.start()
         if self.cfg.apiserver:
             self.register_node()

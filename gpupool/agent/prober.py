@@ -202,6 +202,12 @@ class Prober:
                 log.warning("xGMI peer check failed: %r", e)
         return out
 
+    def warm_arena(self, ordinal: int, hbm_bytes: int = 1 << 30) -> None:
+        """Run one default-sized probe so the device's probe arena is allocated and kept (the
+        library's trim skips it while an HBM sweep is held and for 30 s after its release)."""
+        if self.mode == "inproc":
+            self._hip.run(ordinal, hbm_bytes=hbm_bytes, gemm_n=self.gemm_n)
+
     def _trim_loop(self) -> None:
         period = max(0.05, min(1.0, self._trim_idle_ms / 4e3))
         while not self._trim_stop.wait(period):

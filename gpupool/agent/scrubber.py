@@ -12,9 +12,12 @@ window (~3 ms at 4 GiB). Coverage is reported per device (``hbmSweep`` in the ag
 
 Claims always win: the scrubber re-checks eligibility under a per-device lock before every window,
 and ``yield_device`` (called by the claim path after the ledger commit) only waits for an in-flight
-window. The big buffer is allocated and freed outside every lock a claim takes (~0.4 s / ~2.9 s for
-~282 GiB on MI355X, profiles/r2g): the claim-time probe runs in the reserve meanwhile, and the device
-plugin's Allocate waits for the free (``wait_released``) so a pod never starts beside it.
+window. The big buffer is allocated and freed outside every lock a claim takes (~282 GiB on
+MI355X: 0.2 s to allocate fresh, ~6 s once the driver has to clear previously used VRAM, ~2.5 s to
+free; profiles/r2h_sweep_claim_diag.txt). The claim-time probe arena is allocated first and kept
+while the sweep runs and for 30 s after its free, so a claim-time probe never allocates behind the
+driver's clear (a probe issued during the free or the allocation measured 1.1-1.3 ms); the device
+plugin's Allocate waits for the free (``wait_released``) so a pod never starts beside the buffer.
 
 A window with flipped bits quarantines a free GPU without expiry (``HBMSweepFailed``; cleared by
 ``gpuctl gpu uncordon``), so it is never claimed. In ``simulated`` probe mode (fake backend) the
@@ -113,6 +116,10 @@ class HbmScrubber:
             self._held.add(uuid)
         if self.agent.prober.mode == "inproc":
             o = self._ordinal(uuid)
+            # The claim-time probe arena comes first: a claim then never has to allocate while the
+            # sweep buffer is held or while the driver clears it after the free (seconds).
+            if o is not None:
+                self.agent.prober.warm_arena(o)
             if o is None or self.agent.prober._hip.sweep_alloc(o, self.reserve_bytes) < 0:
                 self._release(uuid)
                 return False

@@ -222,6 +222,20 @@ MI355X_SPEC = {
                 "thermal": {"type": "string", "default": "belowCritical",
                             "enum": ["belowCritical", "belowEmergency", "ignore"]},
                 "thermalMarginC": {**_I32, "minimum": 0, "default": 0},
+                "maxRetiredPages": {**_I64, "minimum": 0, "default": 64,
+                                    "description": "HBM pages the driver has retired after "
+                                                   "uncorrectable errors (absolute, "
+                                                   "amdsmi_get_gpu_bad_page_info). Above it the "
+                                                   "GPU is unhealthy and never claimed "
+                                                   "(HBMRetiredPages)."},
+                "maxPendingPages": {**_I64, "minimum": 0, "default": 0,
+                                    "description": "Bad HBM pages still awaiting retirement "
+                                                   "(HBMPendingRetirement)."},
+                "maxLifetimeUncorrectableECC": {**_I64, "minimum": 0,
+                                                "description": "Optional limit on the device's "
+                                                               "lifetime uncorrectable ECC count "
+                                                               "(absolute; unset = only the "
+                                                               "delta since claim counts)."},
             },
         },
         "drain": {

@@ -9,9 +9,10 @@
 * ``two_pools(n)``    config 5: pools A and B of n//2 GPUs each, created together, timed until
                       both are Ready; per-pool ground truth; no device in both;
 * ``health(pool)``    config 5 health Conditions: an uncorrectable-ECC fault on one claimed GPU
-                      -> HBMECCHealthy=False + Degraded=True, timed twice: as the agent detects
-                      it on its own (no forced sample: detection + reaction) and with a forced
-                      sample (reaction only), then cleared -> Ready again.
+                      -> HBMECCHealthy=False + Degraded=True, timed three ways: detected by the
+                      agent's periodic sample (polled, as a real ECC counter change is),
+                      delivered as an event (overlay rewrite -> inotify, like an amdsmi event),
+                      and with a forced sample (reaction only); then cleared -> Ready again.
 
 Every pool in a run owns its own extended resource so the kubelet's per-resource view is an
 independent ownership oracle (``ground_truth.pool_truth``).
@@ -246,13 +247,14 @@ class BenchRun:
             return conds(o).get(t, {}).get("status")
         faulted = (lambda o: cond(o, "HBMECCHealthy") == "False" and cond(o, "Degraded") == "True")
         cleared = (lambda o: cond(o, "HBMECCHealthy") == "True" and ready_at(1)(o))
-        out: dict[str, list[float]] = {"detect": [], "react": [], "recover": []}
+        out: dict[str, list[float]] = {"detect": [], "event": [], "react": [], "recover": []}
         for i in range(steps):
-            for key, forced in (("detect", False), ("react", True)):
+            for key, forced, notify in (("detect", False, False), ("event", False, True),
+                                        ("react", True, False)):
                 t0 = time.perf_counter()
                 self.cluster.set_faults(self.node.name,
                                         {"devices": {victim: {"ecc": {"uncorrectable": 1 + i}}}},
-                                        sample=forced)
+                                        sample=forced, notify=notify)
                 self.c.wait_for(MI355XPOOLS, name, self.ns, faulted, timeout=self.timeout)
                 out[key].append(time.perf_counter() - t0)
                 t0 = time.perf_counter()
@@ -263,10 +265,14 @@ class BenchRun:
                      self.ns)
         self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(0), timeout=self.timeout)
         return {
-            # detection included: the agent notices the fault on its own (health watcher /
-            # sampler), nothing forces a sample
+            # detection included, polled: the counter change is seen by the agent's periodic
+            # sample (amdsmi signals no ECC event), nothing forces or announces it
             "fault_to_condition_p50_s": summary(out["detect"])["p50_s"],
             "fault_to_condition_max_s": summary(out["detect"])["max_s"],
+            # detection included, event-driven: the fault arrives as an event (overlay rewrite
+            # via inotify, the same path an amdsmi thermal/reset event takes)
+            "event_to_condition_p50_s": summary(out["event"])["p50_s"],
+            "event_to_condition_max_s": summary(out["event"])["max_s"],
             # reaction only: a forced agent sample, then long-poll -> reconcile -> status
             "forced_sample_to_condition_p50_s": summary(out["react"])["p50_s"],
             "fault_cleared_to_ready_p50_s": summary(out["recover"])["p50_s"],

@@ -5,6 +5,7 @@ import argparse
 import logging
 import os
 import signal
+import sys
 import threading
 
 from .kubelet import FakeKubelet
@@ -21,6 +22,10 @@ def main() -> None:
     ap.add_argument("--ready-file", default="")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
+    # same GIL hand-off setting as the agent (ListAndWatch consumer, runtime and API threads)
+    sw = float(os.environ.get("GPUPOOL_GIL_SWITCH_INTERVAL", "0.0005"))
+    if sw > 0:
+        sys.setswitchinterval(sw)
     logging.basicConfig(level=logging.DEBUG if a.verbose else logging.INFO,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     k = FakeKubelet(a.node, a.apiserver, os.path.join(a.root, "device-plugins"),

@@ -24,6 +24,9 @@ def lib() -> ctypes.CDLL:
             for fn in ("mi355x_dev_snapshot",):
                 getattr(l, fn).restype = ctypes.c_void_p
                 getattr(l, fn).argtypes = [ctypes.c_void_p]
+            for fn in ("mi355x_dev_wait_events", "mi355x_dev_wait_faults"):
+                getattr(l, fn).restype = ctypes.c_void_p
+                getattr(l, fn).argtypes = [ctypes.c_void_p, ctypes.c_int]
             l.mi355x_dev_evaluate.restype = ctypes.c_void_p
             l.mi355x_dev_evaluate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
             l.mi355x_dev_select.restype = ctypes.c_void_p
@@ -60,6 +63,15 @@ class DeviceLib:
         if "error" in out:
             raise RuntimeError(out["error"])
         return out
+
+    def wait_events(self, timeout_ms: int = 500) -> dict:
+        """Block (GIL released) up to ``timeout_ms`` for amdsmi device events:
+        {"supported", "events": [{"index", "type", "message"}]}."""
+        return _take(lib().mi355x_dev_wait_events(self._h, int(timeout_ms)))
+
+    def wait_faults(self, timeout_ms: int = 500) -> dict:
+        """Block up to ``timeout_ms`` for the fault-overlay file to change: {"supported", "changed"}."""
+        return _take(lib().mi355x_dev_wait_faults(self._h, int(timeout_ms)))
 
     def close(self) -> None:
         if self._h:

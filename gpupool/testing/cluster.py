@@ -268,10 +268,13 @@ class Cluster:
         self.stop()
 
     # ------------------------------------------------------------ fault injection
-    def set_faults(self, node: str, faults: dict, sample: bool = True) -> None:
+    def set_faults(self, node: str, faults: dict, sample: bool = True, notify: bool = True) -> None:
+        """Write the node's fault overlay. ``sample`` forces an agent sample over the RPC;
+        ``notify=False`` marks the write as not-an-event, so only the agent's periodic sample sees
+        it (the detection path of a real ECC counter change, which amdsmi does not signal)."""
         path = self.faults_path(node)
         with open(path + ".tmp", "w") as f:
-            json.dump(faults, f)
+            json.dump(faults if notify else {**faults, "notify": False}, f)
         os.replace(path + ".tmp", path)
         # make sure the mtime changes even within one filesystem tick
         st = os.stat(path)

@@ -41,6 +41,9 @@ struct HealthPolicy {
   int32_t min_xgmi_up = 7;
   std::string thermal = "belowCritical";
   int32_t thermal_margin_c = 0;
+  int64_t max_retired_pages = 64;                 // HBM pages retired by the driver (absolute)
+  int64_t max_pending_pages = 0;                  // bad pages awaiting retirement
+  int64_t max_lifetime_uncorrectable_ecc = -1;    // -1: unset (only the delta since claim counts)
   Json to_json() const;
 };
 

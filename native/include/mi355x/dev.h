@@ -43,6 +43,15 @@ char* mi355x_dev_evaluate(const char* device_json, const char* baseline_json, co
  *       "weights":[[..]],"numa":[..]} -> {"selected":[idx..]} ("selected" empty if < k). */
 char* mi355x_dev_select(const char* request_json);
 
+/* Hardware event source (amdsmi event notification: ThermalThrottle, GPUPreReset, GPUPostReset,
+ * VMFault). Blocks up to timeout_ms: {"supported": bool, "events": [{"index","type","message"}]}.
+ * supported=false returns at once (fake/cli backends, or the driver refused the subscription). */
+char* mi355x_dev_wait_events(mi355x_dev* d, int timeout_ms);
+
+/* Fault-overlay watch (inotify): blocks up to timeout_ms for the overlay file to be rewritten,
+ * moved into place or deleted: {"supported": bool, "changed": bool}. */
+char* mi355x_dev_wait_faults(mi355x_dev* d, int timeout_ms);
+
 void mi355x_free(char* p);
 const char* mi355x_dev_version(void);
 

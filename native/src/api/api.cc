@@ -45,6 +45,9 @@ Json HealthPolicy::to_json() const {
   j["minXGMILinksUp"] = min_xgmi_up;
   j["thermal"] = thermal;
   j["thermalMarginC"] = thermal_margin_c;
+  j["maxRetiredPages"] = max_retired_pages;
+  j["maxPendingPages"] = max_pending_pages;
+  if (max_lifetime_uncorrectable_ecc >= 0) j["maxLifetimeUncorrectableECC"] = max_lifetime_uncorrectable_ecc;
   return j;
 }
 
@@ -64,6 +67,10 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.health.min_xgmi_up = static_cast<int32_t>(h["minXGMILinksUp"].as_int(7));
   p.health.thermal = h["thermal"].str_or("belowCritical");
   p.health.thermal_margin_c = static_cast<int32_t>(h["thermalMarginC"].as_int(0));
+  p.health.max_retired_pages = h["maxRetiredPages"].as_int(64);
+  p.health.max_pending_pages = h["maxPendingPages"].as_int(0);
+  p.health.max_lifetime_uncorrectable_ecc =
+      h.contains("maxLifetimeUncorrectableECC") ? h["maxLifetimeUncorrectableECC"].as_int(-1) : -1;
   const Json& d = s["drain"];
   p.drain_grace_seconds = d["gracePeriodSeconds"].as_int(30);
   p.drain_evict = d["evict"].as_bool(true);

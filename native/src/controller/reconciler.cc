@@ -56,6 +56,47 @@ GaugeVec& desired_gauge() {
   return g;
 }
 
+// Pool-level GPU utilisation (Prometheus + Grafana, GPU调度平台搭建.md:800), aggregated from the
+// agents' telemetry of the pool's claimed GPUs at every reconcile pass (steady-state resync).
+struct UtilGauges {
+  GaugeVec& gfx = Registry::global().gauge("gpupool_pool_gfx_activity_percent",
+                                           "Mean GFX (compute) activity of the pool's GPUs.");
+  GaugeVec& umc = Registry::global().gauge("gpupool_pool_umc_activity_percent",
+                                           "Mean memory-controller (HBM) activity of the pool's GPUs.");
+  GaugeVec& power = Registry::global().gauge("gpupool_pool_power_watts", "Summed socket power of the pool's GPUs.");
+  GaugeVec& vram_used = Registry::global().gauge("gpupool_pool_vram_used_bytes", "Summed VRAM in use on the pool's GPUs.");
+  GaugeVec& vram_total = Registry::global().gauge("gpupool_pool_vram_total_bytes", "Summed VRAM of the pool's GPUs.");
+};
+UtilGauges& util_gauges() {
+  static UtilGauges g;
+  return g;
+}
+
+void set_util_gauges(const Labels& l, const std::vector<DeviceView>& mine) {
+  double gfx = 0, umc = 0, power = 0, used = 0, total = 0;
+  int n = 0;
+  for (const auto& d : mine) {
+    if (!d.telemetry.is_object()) continue;
+    ++n;
+    gfx += d.telemetry["gfxActivity"].as_double(0);
+    umc += d.telemetry["umcActivity"].as_double(0);
+    power += d.telemetry["powerW"].as_double(0);
+    used += d.telemetry["memUsedBytes"].as_double(0);
+    total += d.telemetry["memTotalBytes"].as_double(0);
+  }
+  UtilGauges& g = util_gauges();
+  g.gfx.set(l, n ? gfx / n : 0);
+  g.umc.set(l, n ? umc / n : 0);
+  g.power.set(l, power);
+  g.vram_used.set(l, used);
+  g.vram_total.set(l, total);
+}
+
+void erase_util_gauges(const Labels& l) {
+  UtilGauges& g = util_gauges();
+  for (GaugeVec* v : {&g.gfx, &g.umc, &g.power, &g.vram_used, &g.vram_total}) v->erase(l);
+}
+
 }  // namespace
 
 // ================================================================== base
@@ -434,6 +475,7 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
   forget_(m.uid);
   ready_gauge().erase({{"kind", kind_}, {"pool", m.key()}});
   desired_gauge().erase({{"kind", kind_}, {"pool", m.key()}});
+  erase_util_gauges({{"kind", kind_}, {"pool", m.key()}});
   return Outcome::done(ms(0));
 }
 
@@ -629,6 +671,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
   write_status_(obj, status);
   int64_t ready = status["readyReplicas"].as_int(0);
   ready_gauge().set({{"kind", kind_}, {"pool", m.key()}}, static_cast<double>(ready));
+  set_util_gauges({{"kind", kind_}, {"pool", m.key()}}, o.mine);
   bool is_ready = condition_true(status["conditions"], gen::kCondReady);
   observe_ready_(m, is_ready, spec.replicas);
   if (!blocked.empty()) return Outcome::requeue(ms(5000), blocked);

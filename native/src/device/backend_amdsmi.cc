@@ -43,6 +43,13 @@ struct Api {
   AMDSMI_FN(amdsmi_get_temp_metric);
   AMDSMI_FN(amdsmi_get_gpu_activity);
   AMDSMI_FN(amdsmi_get_power_info);
+  // optional: bound when present, features degrade to "unsupported" otherwise
+  AMDSMI_FN(amdsmi_get_gpu_bad_page_info);
+  AMDSMI_FN(amdsmi_get_gpu_memory_usage);
+  AMDSMI_FN(amdsmi_init_gpu_event_notification);
+  AMDSMI_FN(amdsmi_set_gpu_event_notification_mask);
+  AMDSMI_FN(amdsmi_get_gpu_event_notification);
+  AMDSMI_FN(amdsmi_stop_gpu_event_notification);
 #undef AMDSMI_FN
 };
 
@@ -50,6 +57,21 @@ template <class F>
 void bind(void* lib, F& fn, const char* name) {
   fn = reinterpret_cast<F>(dlsym(lib, name));
   if (!fn) throw std::runtime_error(std::string("libamd_smi missing symbol ") + name);
+}
+
+template <class F>
+void bind_optional(void* lib, F& fn, const char* name) {
+  fn = reinterpret_cast<F>(dlsym(lib, name));
+}
+
+const char* event_name(amdsmi_evt_notification_type_t t) {
+  switch (t) {
+    case AMDSMI_EVT_NOTIF_VMFAULT: return "VMFault";
+    case AMDSMI_EVT_NOTIF_THERMAL_THROTTLE: return "ThermalThrottle";
+    case AMDSMI_EVT_NOTIF_GPU_PRE_RESET: return "GPUPreReset";
+    case AMDSMI_EVT_NOTIF_GPU_POST_RESET: return "GPUPostReset";
+    default: return "Other";
+  }
 }
 
 std::string bdf_str(const amdsmi_bdf_t& b) {
@@ -92,6 +114,12 @@ class AmdSmiBackend : public Backend {
     bind(api_.lib, api_.amdsmi_get_temp_metric, "amdsmi_get_temp_metric");
     bind(api_.lib, api_.amdsmi_get_gpu_activity, "amdsmi_get_gpu_activity");
     bind(api_.lib, api_.amdsmi_get_power_info, "amdsmi_get_power_info");
+    bind_optional(api_.lib, api_.amdsmi_get_gpu_bad_page_info, "amdsmi_get_gpu_bad_page_info");
+    bind_optional(api_.lib, api_.amdsmi_get_gpu_memory_usage, "amdsmi_get_gpu_memory_usage");
+    bind_optional(api_.lib, api_.amdsmi_init_gpu_event_notification, "amdsmi_init_gpu_event_notification");
+    bind_optional(api_.lib, api_.amdsmi_set_gpu_event_notification_mask, "amdsmi_set_gpu_event_notification_mask");
+    bind_optional(api_.lib, api_.amdsmi_get_gpu_event_notification, "amdsmi_get_gpu_event_notification");
+    bind_optional(api_.lib, api_.amdsmi_stop_gpu_event_notification, "amdsmi_stop_gpu_event_notification");
 
     amdsmi_status_t st = api_.amdsmi_init(AMDSMI_INIT_AMD_GPUS);
     if (st != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("amdsmi_init failed: status " + std::to_string(st));
@@ -115,9 +143,11 @@ class AmdSmiBackend : public Backend {
     if (handles_.empty()) throw std::runtime_error("amdsmi: no AMD GPUs found");
     node_ = cfg["node"].as_string();
     read_static_();
+    if (cfg["events"].as_bool(true)) init_events_();
   }
 
   ~AmdSmiBackend() override {
+    for (auto h : evt_handles_) api_.amdsmi_stop_gpu_event_notification(h);
     if (inited_) api_.amdsmi_shut_down();
     // libamd_smi is left loaded: unloading it while its threads wind down is not safe.
   }
@@ -180,6 +210,11 @@ class AmdSmiBackend : public Backend {
         d["activity"]["gfx"] = static_cast<long long>(eu.gfx_activity);
         d["activity"]["umc"] = static_cast<long long>(eu.umc_activity);
       }
+      uint64_t used = 0;
+      if (api_.amdsmi_get_gpu_memory_usage &&
+          api_.amdsmi_get_gpu_memory_usage(h, AMDSMI_MEM_TYPE_VRAM, &used) == AMDSMI_STATUS_SUCCESS)
+        d["memUsedBytes"] = static_cast<long long>(used);
+      d["ras"] = bad_pages_(h);
       char buf[64] = {0};
       if (api_.amdsmi_get_gpu_compute_partition(h, buf, sizeof buf) == AMDSMI_STATUS_SUCCESS) d["partition"]["compute"] = std::string(buf);
       char mbuf[64] = {0};
@@ -260,7 +295,93 @@ class AmdSmiBackend : public Backend {
     topology_["types"] = types;
   }
 
+  // amdsmi_get_gpu_bad_page_info: {badPagesSupported, retiredPages, pendingPages, unreservablePages}
+  Json bad_pages_(amdsmi_processor_handle h) {
+    Json r = Json::object();
+    uint32_t n = 0;
+    if (!api_.amdsmi_get_gpu_bad_page_info || api_.amdsmi_get_gpu_bad_page_info(h, &n, nullptr) != AMDSMI_STATUS_SUCCESS) {
+      r["badPagesSupported"] = false;
+      return r;
+    }
+    long long retired = 0, pending = 0, unres = 0;
+    if (n > 0) {
+      std::vector<amdsmi_retired_page_record_t> recs(n);
+      uint32_t m = n;
+      if (api_.amdsmi_get_gpu_bad_page_info(h, &m, recs.data()) == AMDSMI_STATUS_SUCCESS) {
+        for (uint32_t i = 0; i < m && i < n; ++i) {
+          if (recs[i].status == AMDSMI_MEM_PAGE_STATUS_RESERVED) ++retired;
+          else if (recs[i].status == AMDSMI_MEM_PAGE_STATUS_PENDING) ++pending;
+          else ++unres;
+        }
+      } else {
+        retired = n;
+      }
+    }
+    r["badPagesSupported"] = true;
+    r["retiredPages"] = retired;
+    r["pendingPages"] = pending;
+    r["unreservablePages"] = unres;
+    return r;
+  }
+
+  void init_events_() {
+    if (!api_.amdsmi_init_gpu_event_notification || !api_.amdsmi_set_gpu_event_notification_mask ||
+        !api_.amdsmi_get_gpu_event_notification || !api_.amdsmi_stop_gpu_event_notification)
+      return;
+    const uint64_t mask = AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_THERMAL_THROTTLE) |
+                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_PRE_RESET) |
+                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_POST_RESET) |
+                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_VMFAULT);
+    for (auto h : handles_) {
+      if (api_.amdsmi_init_gpu_event_notification(h) != AMDSMI_STATUS_SUCCESS) {
+        evt_error_ = "amdsmi_init_gpu_event_notification failed";
+        continue;
+      }
+      if (api_.amdsmi_set_gpu_event_notification_mask(h, mask) != AMDSMI_STATUS_SUCCESS) {
+        api_.amdsmi_stop_gpu_event_notification(h);
+        evt_error_ = "amdsmi_set_gpu_event_notification_mask failed";
+        continue;
+      }
+      evt_handles_.push_back(h);
+    }
+  }
+
+ public:
+  Json wait_events(int timeout_ms) override {
+    Json out = Json::object();
+    Json evs = Json::array();
+    out["supported"] = !evt_handles_.empty();
+    if (evt_handles_.empty()) {
+      if (!evt_error_.empty()) out["error"] = evt_error_;
+      out["events"] = evs;
+      return out;
+    }
+    amdsmi_evt_notification_data_t data[16];
+    uint32_t n = 16;
+    // not under mu_: this blocks for up to timeout_ms while snapshots continue
+    amdsmi_status_t st = api_.amdsmi_get_gpu_event_notification(timeout_ms, &n, data);
+    if (st == AMDSMI_STATUS_SUCCESS) {
+      for (uint32_t i = 0; i < n && i < 16; ++i) {
+        Json e = Json::object();
+        long long idx = -1;
+        for (size_t k = 0; k < handles_.size(); ++k)
+          if (handles_[k] == data[i].processor_handle) idx = static_cast<long long>(k);
+        e["index"] = idx;
+        e["type"] = event_name(data[i].event);
+        e["message"] = std::string(data[i].message);
+        evs.push_back(e);
+      }
+    } else if (st != AMDSMI_STATUS_NO_DATA && st != AMDSMI_STATUS_TIMEOUT) {
+      out["status"] = static_cast<long long>(st);
+    }
+    out["events"] = evs;
+    return out;
+  }
+
+ private:
   Api api_;
+  std::vector<amdsmi_processor_handle> evt_handles_;
+  std::string evt_error_;
   bool inited_ = false;
   std::vector<amdsmi_processor_handle> handles_;
   std::vector<Json> static_;

@@ -1,5 +1,8 @@
 // C ABI of libmi355x_dev (see native/include/mi355x/dev.h).
+#include <poll.h>
+#include <sys/inotify.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cstdlib>
@@ -19,8 +22,15 @@ struct mi355x_dev {
   Json faults;
   time_t faults_mtime = 0;
   long faults_mtime_ns = 0;
+  ino_t faults_ino = 0;
   std::string node;
   std::mutex mu;
+  // fault-overlay watch (mi355x_dev_wait_faults): inotify on the overlay's directory
+  std::mutex wmu;
+  int ino_fd = -1;
+  ~mi355x_dev() {
+    if (ino_fd >= 0) close(ino_fd);
+  }
 };
 
 namespace {
@@ -45,7 +55,9 @@ void reload_faults(mi355x_dev* d) {
     d->faults_mtime = 0;
     return;
   }
-  if (st.st_mtim.tv_sec == d->faults_mtime && st.st_mtim.tv_nsec == d->faults_mtime_ns) return;
+  // a replaced file (rename into place) is a new inode even within one mtime tick
+  if (st.st_mtim.tv_sec == d->faults_mtime && st.st_mtim.tv_nsec == d->faults_mtime_ns && st.st_ino == d->faults_ino)
+    return;
   std::ifstream f(d->faults_path);
   std::stringstream ss;
   ss << f.rdbuf();
@@ -54,6 +66,7 @@ void reload_faults(mi355x_dev* d) {
     d->faults = *j;
     d->faults_mtime = st.st_mtim.tv_sec;
     d->faults_mtime_ns = st.st_mtim.tv_nsec;
+    d->faults_ino = st.st_ino;
   }
 }
 
@@ -134,6 +147,57 @@ char* mi355x_dev_select(const char* request_json) {
     errj["selected"] = Json::array();
     return dup(errj.dump());
   }
+}
+
+char* mi355x_dev_wait_events(mi355x_dev* d, int timeout_ms) {
+  if (!d) return nullptr;
+  try {
+    return dup(d->backend->wait_events(timeout_ms).dump());
+  } catch (const std::exception& e) {
+    Json errj = Json::object();
+    errj["supported"] = false;
+    errj["events"] = Json::array();
+    errj["error"] = e.what();
+    return dup(errj.dump());
+  }
+}
+
+char* mi355x_dev_wait_faults(mi355x_dev* d, int timeout_ms) {
+  if (!d) return nullptr;
+  std::lock_guard<std::mutex> g(d->wmu);
+  Json out = Json::object();
+  out["supported"] = !d->faults_path.empty();
+  out["changed"] = false;
+  if (d->faults_path.empty()) return dup(out.dump());
+  std::string dir = ".", base = d->faults_path;
+  size_t slash = d->faults_path.rfind('/');
+  if (slash != std::string::npos) {
+    dir = slash ? d->faults_path.substr(0, slash) : "/";
+    base = d->faults_path.substr(slash + 1);
+  }
+  if (d->ino_fd < 0) {
+    d->ino_fd = inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
+    if (d->ino_fd < 0 || inotify_add_watch(d->ino_fd, dir.c_str(), IN_CLOSE_WRITE | IN_MOVED_TO | IN_DELETE) < 0) {
+      if (d->ino_fd >= 0) close(d->ino_fd);
+      d->ino_fd = -1;
+      out["supported"] = false;
+      out["error"] = "inotify on " + dir + " failed";
+      return dup(out.dump());
+    }
+  }
+  struct pollfd pfd {d->ino_fd, POLLIN, 0};
+  if (poll(&pfd, 1, timeout_ms) > 0 && (pfd.revents & POLLIN)) {
+    alignas(struct inotify_event) char buf[8192];
+    ssize_t n;
+    while ((n = read(d->ino_fd, buf, sizeof buf)) > 0) {
+      for (char* p = buf; p < buf + n;) {
+        auto* ev = reinterpret_cast<struct inotify_event*>(p);
+        if (ev->len && base == ev->name) out["changed"] = true;
+        p += sizeof(struct inotify_event) + ev->len;
+      }
+    }
+  }
+  return dup(out.dump());
 }
 
 void mi355x_free(char* p) { std::free(p); }

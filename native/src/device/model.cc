@@ -9,6 +9,13 @@
 
 namespace mi355x {
 
+Json Backend::wait_events(int /*timeout_ms*/) {
+  Json out = Json::object();
+  out["supported"] = false;
+  out["events"] = Json::array();
+  return out;
+}
+
 void deep_merge(Json& dst, const Json& src) {
   if (!src.is_object() || !dst.is_object()) {
     dst = src;
@@ -98,6 +105,37 @@ Json evaluate(const Json& dev, const Json& baseline, const Json& policy) {
     ecc_ok = false;
     reasons.push_back(fmt("HBMCorrectableECCExceeded: +%lld correctable since claim (max %lld)", d_cor,
                           health["maxCorrectableECC"].as_int(100000)));
+  }
+
+  // ---- HBM page retirement (amdsmi_get_gpu_bad_page_info): the driver's persistent record of HBM
+  // pages retired after uncorrectable errors. Absolute, not a delta: it is what makes a GPU with a
+  // failing HBM stack unclaimable even when no new error happens while it is claimed. Pending pages
+  // (marked bad, not yet retired) and pages the driver could not reserve are worse still.
+  const Json& ras = dev["ras"];
+  if (ras.is_object() && ras["badPagesSupported"].as_bool(true)) {
+    int64_t retired = ras["retiredPages"].as_int(0), pending = ras["pendingPages"].as_int(0),
+            unres = ras["unreservablePages"].as_int(0);
+    int64_t max_ret = health["maxRetiredPages"].as_int(64), max_pend = health["maxPendingPages"].as_int(0);
+    if (retired > max_ret) {
+      ecc_ok = false;
+      reasons.push_back(fmt("HBMRetiredPages: %lld HBM page(s) retired (max %lld)", retired, max_ret));
+    }
+    if (pending > max_pend) {
+      ecc_ok = false;
+      reasons.push_back(fmt("HBMPendingRetirement: %lld bad HBM page(s) awaiting retirement (max %lld)",
+                            pending, max_pend));
+    }
+    if (unres > 0) {
+      ecc_ok = false;
+      reasons.push_back(fmt("HBMUnreservablePages: %lld bad HBM page(s) could not be retired", unres));
+    }
+  }
+  // lifetime (absolute) uncorrectable count, when the pool sets a limit (unset: only the delta
+  // since claim counts, since retired pages already cover historic errors)
+  if (health.contains("maxLifetimeUncorrectableECC") && unc > health["maxLifetimeUncorrectableECC"].as_int(0)) {
+    ecc_ok = false;
+    reasons.push_back(fmt("HBMUncorrectableECCHistory: %lld uncorrectable error(s) over the device lifetime (max %lld)",
+                          unc, health["maxLifetimeUncorrectableECC"].as_int(0)));
   }
 
   // ---- thermals against the device's own limits (AMDSMI_TEMP_CRITICAL / _EMERGENCY)

@@ -17,6 +17,10 @@ class Backend {
   virtual std::string name() const = 0;
   // Node snapshot without fault overlay applied.
   virtual Json snapshot() = 0;
+  // Asynchronous device events (amdsmi event notification: thermal throttle, GPU pre/post reset,
+  // VM fault). Blocks up to timeout_ms; returns {"supported": bool, "events": [{index, type,
+  // message}]}. Backends without an event source report supported=false at once.
+  virtual Json wait_events(int timeout_ms);
 };
 
 std::unique_ptr<Backend> make_fake_backend(const Json& cfg);     // throws std::runtime_error

@@ -599,8 +599,15 @@ struct DeviceCtx {
   void* sweep = nullptr;
   size_t sweep_bytes = 0;
   unsigned long long* sweep_cnt = nullptr;
+  // Freed VRAM is cleared by the driver before it is handed out again (~6 s for ~282 GiB measured,
+  // profiles/r2h_sweep_claim_diag.txt): an arena hipMalloc issued in that window waits for it. The
+  // arena is therefore allocated before the sweep buffer and not trimmed while a sweep is held or
+  // for kSweepClearGrace after its release, so a claim-time probe never allocates behind a clear.
+  std::chrono::steady_clock::time_point sweep_released{};
   bool ready = false;
 };
+
+constexpr std::chrono::seconds kSweepClearGrace{30};
 
 std::mutex g_mu;
 std::vector<DeviceCtx> g_ctx;
@@ -1171,7 +1178,9 @@ char* mi355x_probe_peer(int src, int dst, const char* opts_json) {
   }
 }
 
-// Frees the probe arenas idle for at least ``idle_ms`` (0: all); returns how many were freed.
+// Frees the probe arenas idle for at least ``idle_ms`` (0: all, unconditionally); returns how many
+// were freed. With idle_ms > 0 an arena stays while its device holds an HBM sweep buffer or freed one
+// less than kSweepClearGrace ago.
 int mi355x_probe_trim(int idle_ms) {
   if (g_count <= 0) return 0;
   int freed = 0;
@@ -1180,6 +1189,7 @@ int mi355x_probe_trim(int idle_ms) {
     std::lock_guard<std::mutex> g(device_mutex(d));
     DeviceCtx& ctx = g_ctx[static_cast<size_t>(d)];
     if (!ctx.arena || now - ctx.arena_used < std::chrono::milliseconds(idle_ms)) continue;
+    if (idle_ms > 0 && (ctx.sweep || now - ctx.sweep_released < kSweepClearGrace)) continue;  // 0 = forced
     if (hipSetDevice(d) != hipSuccess) continue;
     (void)hipFree(ctx.arena);
     ctx.arena = nullptr;
@@ -1235,6 +1245,7 @@ int mi355x_probe_sweep_release(int dev) {
     p = ctx.sweep;
     ctx.sweep = nullptr;
     ctx.sweep_bytes = 0;
+    ctx.sweep_released = std::chrono::steady_clock::now();
   }
   if (!p) return 0;
   if (hipSetDevice(dev) != hipSuccess) return -1;

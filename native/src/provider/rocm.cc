@@ -32,6 +32,7 @@ DeviceView DeviceView::from(const Json& j) {
   d.partition = j["partition"];
   d.drain_started_at = j["drainStartedAt"].as_string();
   d.hbm_sweep = j["hbmSweep"];
+  d.telemetry = j["telemetry"];
   return d;
 }
 

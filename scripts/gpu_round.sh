@@ -5,7 +5,7 @@ set -u
 O=gpurun_out/${1:-round}
 mkdir -p $O
 export PYTHONPATH=$PWD
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.txt 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v ${PYTEST_ARGS:-} --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.txt 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1
 rc=$?; echo "smoke rc=$rc" >> $O/smoke.txt; [ $rc -eq 0 ] || exit $rc

@@ -130,9 +130,10 @@ def test_protobuf_descriptors_are_fresh():
 
 
 def test_fake_fixture_is_fresh(tmp_path):
-    """tests/fixtures/node_8x_mi355x.json matches its generator."""
-    fx = os.path.join(ROOT, "tests", "fixtures", "node_8x_mi355x.json")
-    before = open(fx).read()
+    """tests/fixtures/node_8x_mi355x{,_cpx}.json match their generator."""
+    fxs = [os.path.join(ROOT, "tests", "fixtures", n)
+           for n in ("node_8x_mi355x.json", "node_8x_mi355x_cpx.json")]
+    before = [open(fx).read() for fx in fxs]
     subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "gen_fake_fixture.py")],
                    check=True, capture_output=True)
-    assert open(fx).read() == before
+    assert [open(fx).read() for fx in fxs] == before
