@@ -214,3 +214,65 @@ def test_hbm_scrub_on_real_gpu_and_claim_is_not_blocked(cluster_factory):
     d = obj["status"]["devices"][0]
     assert d["probe"]["cusVerified"] == d["probe"]["cusExpected"] == 256, d
     assert d["hbmCoverage"]["span"] > 200e9, d
+
+
+def test_amdsmi_ras_event_source_and_utilisation_on_real_gpu(native_built):
+    """On the MI355X: the bad-page (RAS) read, VRAM in use and the amdsmi event subscription work
+    through libmi355x_dev, and GFX activity / VRAM used rise while a bf16 GEMM workload runs in
+    another process (what the agent exports as gpupool_device_* utilisation)."""
+    import subprocess
+    import sys
+    from gpupool.ops import devlib
+    lib = devlib.DeviceLib("amdsmi", node="t")
+    d0 = lib.snapshot()["devices"][0]
+    ras = d0["ras"]
+    assert isinstance(ras.get("badPagesSupported"), bool), ras
+    if ras["badPagesSupported"]:
+        assert min(ras["retiredPages"], ras["pendingPages"], ras["unreservablePages"]) >= 0
+    assert d0["memTotalBytes"] > 250e9 and d0.get("memUsedBytes", -1) >= 0
+    assert devlib.evaluate(d0, d0, {})["healthy"]  # the box's GPU passes the retirement rules
+    ev = lib.wait_events(50)
+    print("RAS", json.dumps(ras), "events", json.dumps(ev), "memUsed", d0.get("memUsedBytes"))
+    assert isinstance(ev.get("supported"), bool) and ev.get("events") == []
+    code = ("import torch,time,sys\n"
+            "a=torch.randn(8192,8192,device='cuda',dtype=torch.bfloat16)\n"
+            "(a@a).sum().item(); print('READY',flush=True); t=time.time()\n"
+            "while time.time()-t<4: (a@a).sum().item()\n")
+    p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+    peak_gfx, peak_used = 0, 0
+    try:
+        assert p.stdout.readline().strip() == "READY"
+        t0 = time.time()
+        while time.time() - t0 < 3.5:
+            s = lib.snapshot()["devices"][0]
+            peak_gfx = max(peak_gfx, int((s.get("activity") or {}).get("gfx") or 0))
+            peak_used = max(peak_used, int(s.get("memUsedBytes") or 0))
+            time.sleep(0.1)
+    finally:
+        p.wait(timeout=90)
+    print("peak gfx activity", peak_gfx, "peak VRAM used", peak_used)
+    assert p.returncode == 0
+    assert peak_gfx > 0 and peak_used > int(d0.get("memUsedBytes") or 0)
+
+
+def test_agent_exports_events_and_utilisation_on_real_gpu(cluster_factory):
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    k = c.client
+    k.create(MI355XPOOLS, pool("u", 1), "default")
+    k.wait_for(MI355XPOOLS, "u", "default", ready_at(1), timeout=60)
+    deadline = time.monotonic() + 10
+    view = c.agent_request("gpu-node", "GET", "/v1/node")
+    while "device" not in view["eventSources"] and time.monotonic() < deadline:
+        time.sleep(0.1)
+        view = c.agent_request("gpu-node", "GET", "/v1/node")
+    print("eventSources", view["eventSources"])
+    assert view["eventSources"].get("faultOverlay") is True and "device" in view["eventSources"]
+    d = next(x for x in view["devices"] if x.get("pool") == "default/u")
+    assert d["telemetry"]["memTotalBytes"] > 250e9 and d["telemetry"]["powerW"] > 0
+    text = c.agent_request("gpu-node", "GET", "/metrics")
+    assert 'gpupool_device_power_watts{' in text and 'pool="default/u"' in text
+    deadline = time.monotonic() + 20
+    while 'gpupool_pool_vram_total_bytes{kind="Mi355xPool",pool="default/u"}' not in \
+            c.manager_metrics() and time.monotonic() < deadline:
+        time.sleep(0.2)
+    assert 'gpupool_pool_vram_total_bytes{kind="Mi355xPool",pool="default/u"}' in c.manager_metrics()

@@ -206,3 +206,21 @@ def test_probe_arena_reused_then_trimmed(hip):
     c = hip.run(0, hbm_bytes=1 << 30)
     assert c["passed"] and c["phases"]["arenaReused"] is False
     hip.trim(0)
+
+
+def test_concurrent_probes_of_one_device_serialise(hip):
+    """Two probes of the same GPU at once (e.g. a claim and a periodic recheck): the per-device
+    lock serialises them (wall >= the sum of their own kernel walls) and neither corrupts the
+    other's arena (both pass, no flipped bits, no GEMM mismatches)."""
+    import concurrent.futures as cf
+    import time
+    hip.run(0, hbm_bytes=1 << 30)  # arena warm
+    with cf.ThreadPoolExecutor(2) as ex:
+        t0 = time.perf_counter()
+        futs = [ex.submit(hip.run, 0, 1 << 30) for _ in range(2)]
+        rs = [f.result() for f in futs]
+        wall_ms = (time.perf_counter() - t0) * 1e3
+    for r in rs:
+        assert r["passed"], r
+        assert r["hbm"]["badBits"] == 0 and not r["mfma"].get("elementMismatches")
+    assert wall_ms >= 0.9 * sum(r["ms"] for r in rs), (wall_ms, [r["ms"] for r in rs])

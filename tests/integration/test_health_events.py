@@ -199,3 +199,43 @@ def test_cpx_pool_moves_off_an_asic_with_an_ecc_fault(cluster_factory):
     # the SPX requirement is refused on a CPX node (partition mode is observed, never changed)
     k.create(MI355XPOOLS, mi_pool("spx", 1, partition={"compute": "SPX"}), "default")
     k.wait_for(MI355XPOOLS, "spx", "default", cond_is("Ready", "False"), timeout=30)
+
+
+@pytest.mark.slow
+def test_utilisation_metrics_agent_and_pool(cluster_factory):
+    """GPU utilisation export (GPU调度平台搭建.md:800): per-GPU gauges on the agent (with the pool
+    label) and pool-level aggregates on the manager, from the fake backend's telemetry."""
+    c = cluster_factory(nodes=[NodeSpec("mi355x-node-0")])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("util", 2), "default")
+    wait_ready(k, "util", 2)
+    view = c.agent_request("mi355x-node-0", "GET", "/v1/node")
+    tel = [d["telemetry"] for d in view["devices"] if d.get("pool") == "default/util"]
+    assert len(tel) == 2 and all(t["memTotalBytes"] == 309220868096 for t in tel)
+    text = c.agent_request("mi355x-node-0", "GET", "/metrics")  # text/plain on the RPC socket
+    for name in ("gpupool_device_gfx_activity_percent", "gpupool_device_umc_activity_percent",
+                 "gpupool_device_power_watts", "gpupool_device_vram_used_bytes",
+                 "gpupool_device_vram_total_bytes", "gpupool_device_hbm_bad_pages"):
+        assert name + "{" in text, name
+    assert 'pool="default/util"' in text
+    want = 2 * 309220868096
+
+    def pool_gauge(metrics: str, name: str) -> float | None:
+        for line in metrics.splitlines():
+            if line.startswith(name + "{") and 'pool="default/util"' in line:
+                return float(line.rsplit(" ", 1)[1])
+        return None
+    deadline = time.monotonic() + 20
+    while time.monotonic() < deadline:
+        m = c.manager_metrics()
+        if pool_gauge(m, "gpupool_pool_vram_total_bytes") == want:
+            break
+        time.sleep(0.1)
+    assert pool_gauge(m, "gpupool_pool_vram_total_bytes") == want
+    assert pool_gauge(m, "gpupool_pool_power_watts") == 2 * 262
+    assert pool_gauge(m, "gpupool_pool_gfx_activity_percent") == 0
+    dash = json.load(open(os.path.join(ROOT, "config", "prometheus", "grafana-dashboard.json")))
+    exprs = " ".join(t["expr"] for p in dash["panels"] for t in p.get("targets", []))
+    for name in ("gpupool_pool_gfx_activity_percent", "gpupool_device_vram_used_bytes",
+                 "gpupool_ready_replicas"):
+        assert name in exprs
