@@ -21,8 +21,9 @@ After the timed region (not part of ms_per_step):
     the pool is Ready at N//2 with the victims' pods evicted and the GPUs released);
   * config 5: ``--pool-steps`` x two pools of N//2 created together, timed until both are Ready,
     per-pool ground truth (needs N >= 2);
-  * health: fault -> condition latency with detection included (no forced sample) and reaction
-    only (forced sample).
+  * health: fault -> condition latency with detection included — by the agent's 100 ms health
+    poll (a silent ECC counter change) and as an event (overlay rewrite -> inotify, the path an
+    amdsmi event takes) — and reaction only (forced sample).
 
 ``value`` is the p50 reconcile-to-Ready latency at replicas = N (``--gpus``), the largest point of
 the sweep; ``per_n`` holds every point. With N GPUs visible (real MI355X) the agent uses the
@@ -132,7 +133,8 @@ def main() -> int:
                         probe="inproc" if real else "simulated",
                         count=-1 if real else max(8, n),
                         extra_args=[] if real else ["--probe-sim-ms", "1.0"])
-        cluster = Cluster(workdir, nodes=[node], sample_interval=args.sample_interval)
+        # production agent settings: ledger fsync on, 100 ms health poll, full sample every 1 s
+        cluster = Cluster(workdir, nodes=[node], sample_interval=args.sample_interval, fsync=True)
         cluster.start()  # all child processes exist before anything touches the GPU
         run = BenchRun(cluster, node, real, hbm_bytes=args.hbm_bytes, timeout=args.timeout)
         pool = run.make_pool("bench-pool", "amd.com/gpu", 0)
@@ -176,6 +178,10 @@ def main() -> int:
         elif args.pool_steps > 0:
             secondary["two_pools"] = {"skipped": "needs >= 2 GPUs (two pools of N//2)"}
         health = run.health(pool, args.health_steps) if args.health_steps > 0 else {}
+        try:
+            agent_stats = run.agent_stats()
+        except Exception as e:
+            agent_stats = {"error": repr(e)}
         try:
             metrics = cluster.manager_metrics()
         except Exception:
@@ -233,6 +239,8 @@ def main() -> int:
                 **secondary,
                 "health_condition_latency": health,
                 "sample_interval_s": args.sample_interval,
+                "health_poll_interval_s": 0.1,
+                "agent": agent_stats,
                 "world_size": world,
                 "claim_pass_span_p50_ms": span_p50,
                 "steps_detail": [{k2: (round(v, 4) if isinstance(v, float) else v)

@@ -36,7 +36,10 @@ def main() -> None:
     ap.add_argument("--probe", default="", choices=["", "inproc", "subprocess", "simulated", "off"])
     ap.add_argument("--probe-sim-ms", type=float, default=20.0)
     ap.add_argument("--probe-gemm-n", type=int, default=4096)
-    ap.add_argument("--sample-interval", type=float, default=2.0)
+    ap.add_argument("--sample-interval", type=float, default=2.0,
+                    help="full telemetry sample period (s): activity, power, VRAM, bad pages, pods")
+    ap.add_argument("--health-interval", type=float, default=0.1,
+                    help="health-only poll period (s): ECC, xGMI links, temperatures (0 = off)")
     ap.add_argument("--quarantine", type=float, default=300.0)
     ap.add_argument("--no-fsync", action="store_true")
     ap.add_argument("--probe-arena-idle", type=float, default=10.0,
@@ -70,7 +73,8 @@ def main() -> None:
                       listen=a.listen, endpoint=a.endpoint, apiserver=a.apiserver, token=a.token,
                       plugin_dir=a.plugin_dir, pod_resources=a.pod_resources, probe_mode=a.probe,
                       probe_sim_ms=a.probe_sim_ms, probe_gemm_n=a.probe_gemm_n,
-                      sample_interval=a.sample_interval, quarantine_s=a.quarantine,
+                      sample_interval=a.sample_interval, health_interval=a.health_interval,
+                      quarantine_s=a.quarantine,
                       fsync=not a.no_fsync, probe_arena_idle_s=a.probe_arena_idle,
                       scrub_interval_s=a.scrub_interval, scrub_window_bytes=a.scrub_window,
                       scrub_windows=a.scrub_windows, scrub_reserve_bytes=a.scrub_reserve,

@@ -60,6 +60,7 @@ class AgentConfig:
     probe_sim_ms: float = 20.0
     probe_gemm_n: int = 4096
     sample_interval: float = 2.0
+    health_interval: float = 0.1     # fast poll of the health-only fields (0 = off)
     quarantine_s: float = 300.0
     advertise_wait_s: float = 2.0
     fsync: bool = True
@@ -121,6 +122,7 @@ class Agent:
         self._rechecking: set[str] = set()
         self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0, "rechecks": 0,
                       "probe_ms_sum": 0.0, "samples": 0, "sample_ms_sum": 0.0,
+                      "health_polls": 0, "health_poll_ms_sum": 0.0,
                       "device_events": 0, "fault_events": 0}
         self.resetting: set[str] = set()       # GPUs between amdsmi GPUPreReset and GPUPostReset
         self.recent_events: list[dict] = []   # last hardware/overlay events (node view, metrics)
@@ -266,6 +268,42 @@ class Agent:
                 self.recheck_probes()
             except Exception:
                 log.exception("probe recheck failed")
+
+    def poll_health(self) -> set[str]:
+        """Fast poll of the fields verdicts depend on (ECC counts, xGMI links, temperatures):
+        amdsmi signals no ECC event, so this bounds the detection of an HBM error at
+        ``health_interval`` instead of the full-telemetry ``sample_interval``. Devices whose
+        health fields did not change are not re-evaluated."""
+        t0 = time.perf_counter()
+        h = self.dev.health_snapshot()
+        dt = (time.perf_counter() - t0) * 1e3
+        changed: set[str] = set()
+        with self.lock:
+            self.stats["health_polls"] += 1
+            self.stats["health_poll_ms_sum"] += dt
+            moved = False
+            by = dict(self.by_uuid)
+            for d in h.get("devices", []):
+                old = by.get(d.get("uuid"))
+                if old is None:
+                    continue  # enumeration changes are the full sample's job
+                if any(old.get(k) != v for k, v in d.items()):
+                    by[d["uuid"]] = {**old, **d}
+                    moved = True
+            if moved:
+                self.by_uuid = by
+                changed = self._evaluate_all()
+        if changed:
+            self._bump(changed)
+            self._notify_plugins()
+        return changed
+
+    def _health_poller(self) -> None:
+        while not self._stop.wait(self.cfg.health_interval):
+            try:
+                self.poll_health()
+            except Exception:
+                log.exception("health poll failed")
 
     # ---- event-driven detection (the sampler is the fallback for what has no event)
     def _note_event(self, ev: dict) -> None:
@@ -998,8 +1036,11 @@ class Agent:
                 log.info("podresources not reachable yet: %s", e)
         for res in {r.get("resourceName", schema.DEFAULT_RESOURCE) for r in self.records.values()}:
             self._ensure_plugin(res)
-        for fn, name in ((self._sampler, "sampler"), (self._device_event_watcher, "dev-events"),
-                         (self._fault_watcher, "fault-watch")):
+        loops = [(self._sampler, "sampler"), (self._device_event_watcher, "dev-events"),
+                 (self._fault_watcher, "fault-watch")]
+        if self.cfg.health_interval > 0:
+            loops.append((self._health_poller, "health-poll"))
+        for fn, name in loops:
             t = threading.Thread(target=fn, daemon=True, name=name)
             t.start()
             self._threads.append(t)

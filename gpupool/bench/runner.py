@@ -10,7 +10,7 @@
                       both are Ready; per-pool ground truth; no device in both;
 * ``health(pool)``    config 5 health Conditions: an uncorrectable-ECC fault on one claimed GPU
                       -> HBMECCHealthy=False + Degraded=True, timed three ways: detected by the
-                      agent's periodic sample (polled, as a real ECC counter change is),
+                      agent's 100 ms health poll (as a real ECC counter change is),
                       delivered as an event (overlay rewrite -> inotify, like an amdsmi event),
                       and with a forced sample (reaction only); then cleared -> Ready again.
 
@@ -235,6 +235,24 @@ class BenchRun:
         return {"pools": [half, half], "seconds": dt, "ok": ok, "crossPoolDevices": len(ua & ub),
                 "truth": {"a": ta, "b": tb}}
 
+    def agent_stats(self) -> dict:
+        """The agent's own counters (gpupool_agent_*): sample / health-poll cost, events."""
+        text = self.cluster.agent_request(self.node.name, "GET", "/metrics")
+        st = {}
+        for line in str(text).splitlines():
+            if line.startswith("gpupool_agent_") and "{" not in line:
+                k, v = line.split(" ", 1)
+                st[k[len("gpupool_agent_"):]] = float(v)
+        out = {"health_polls": int(st.get("health_polls", 0)),
+               "samples": int(st.get("samples", 0)),
+               "device_events": int(st.get("device_events", 0)),
+               "fault_events": int(st.get("fault_events", 0))}
+        if st.get("health_polls"):
+            out["health_poll_ms_avg"] = round(st["health_poll_ms_sum"] / st["health_polls"], 3)
+        if st.get("samples"):
+            out["sample_ms_avg"] = round(st["sample_ms_sum"] / st["samples"], 3)
+        return out
+
     def health(self, pool: dict, steps: int) -> dict:
         """Fault -> condition on one claimed GPU of ``pool`` (replacePolicy Keep, so the faulty
         GPU stays and the Conditions are what changes)."""
@@ -265,8 +283,8 @@ class BenchRun:
                      self.ns)
         self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(0), timeout=self.timeout)
         return {
-            # detection included, polled: the counter change is seen by the agent's periodic
-            # sample (amdsmi signals no ECC event), nothing forces or announces it
+            # detection included, polled: the counter change is seen by the agent's health-only
+            # poll (amdsmi signals no ECC event), nothing forces or announces it
             "fault_to_condition_p50_s": summary(out["detect"])["p50_s"],
             "fault_to_condition_max_s": summary(out["detect"])["max_s"],
             # detection included, event-driven: the fault arrives as an event (overlay rewrite

@@ -21,7 +21,7 @@ def lib() -> ctypes.CDLL:
             l.mi355x_dev_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                           ctypes.c_size_t]
             l.mi355x_dev_close.argtypes = [ctypes.c_void_p]
-            for fn in ("mi355x_dev_snapshot",):
+            for fn in ("mi355x_dev_snapshot", "mi355x_dev_health_snapshot"):
                 getattr(l, fn).restype = ctypes.c_void_p
                 getattr(l, fn).argtypes = [ctypes.c_void_p]
             for fn in ("mi355x_dev_wait_events", "mi355x_dev_wait_faults"):
@@ -60,6 +60,14 @@ class DeviceLib:
     def snapshot(self) -> dict:
         with self._mu:
             out = _take(lib().mi355x_dev_snapshot(self._h))
+        if "error" in out:
+            raise RuntimeError(out["error"])
+        return out
+
+    def health_snapshot(self) -> dict:
+        """ECC / xGMI / temperatures / presence only (the fields verdicts use), for a fast poll."""
+        with self._mu:
+            out = _take(lib().mi355x_dev_health_snapshot(self._h))
         if "error" in out:
             raise RuntimeError(out["error"])
         return out

@@ -97,7 +97,8 @@ class Cluster:
                  manager_args: list[str] | None = None, manager: bool = True,
                  python: str = sys.executable, env: dict | None = None,
                  sample_interval: float = 0.5, kinds: str = "mi355x,azure,job",
-                 manager_bin: str | None = None, tls: bool = False, token: str | None = None):
+                 manager_bin: str | None = None, tls: bool = False, token: str | None = None,
+                 fsync: bool = False):
         self.workdir = os.path.abspath(workdir)
         self.tls = tls
         self.token = token
@@ -114,6 +115,7 @@ class Cluster:
         self.env["PYTHONPATH"] = ROOT + os.pathsep + self.env.get("PYTHONPATH", "")
         self.env.update(env or {})
         self.sample_interval = sample_interval
+        self.fsync = fsync  # agents' ledger fsync (the production default; tests skip it for speed)
         self.kinds = kinds
         self.manager_bin = manager_bin
         self.procs: dict[str, subprocess.Popen] = {}
@@ -205,8 +207,8 @@ class Cluster:
                 "--state-dir", os.path.join(self.workdir, f"state-{node.name}"),
                 "--socket", self.agent_socket(node.name), "--apiserver", self.url,
                 "--faults", self.faults_path(node.name), "--ready-file", rf,
-                "--sample-interval", str(self.sample_interval), "--no-fsync",
-                "--auth-token-file", self.agent_token_file]
+                "--sample-interval", str(self.sample_interval),
+                "--auth-token-file", self.agent_token_file] + ([] if self.fsync else ["--no-fsync"])
         if node.backend == "fake":
             argv += ["--fixture", node.fixture]
         if node.count >= 0:

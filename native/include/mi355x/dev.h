@@ -34,6 +34,10 @@ void mi355x_dev_close(mi355x_dev* d);
 /* Node snapshot: {"backend","node","ts","devices":[...],"topology":{"weights":[[..]],"types":[[..]]}} */
 char* mi355x_dev_snapshot(mi355x_dev* d);
 
+/* Health-only snapshot: per device {index, uuid, ecc, xgmi, temps, present} (+ fault overlay),
+ * cheap enough for a ~10 Hz poll; same shape as the corresponding fields of the full snapshot. */
+char* mi355x_dev_health_snapshot(mi355x_dev* d);
+
 /* Health verdict for one device snapshot against a pool policy and the ECC baseline taken at
  * claim time: {"healthy","present","xgmiOk","eccOk","thermalOk","partitionOk","reasons":[...]} */
 char* mi355x_dev_evaluate(const char* device_json, const char* baseline_json, const char* policy_json);

