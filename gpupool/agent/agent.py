@@ -1034,7 +1034,11 @@ class Agent:
                 self._refresh_pods()
             except Exception as e:  # kubelet not up yet: the sampler retries every period
                 log.info("podresources not reachable yet: %s", e)
-        for res in {r.get("resourceName", schema.DEFAULT_RESOURCE) for r in self.records.values()}:
+        # Plugins for the default resource and every resource in the ledger register now (as a
+        # device plugin does at start-up), so a first claim never waits on plugin start, kubelet
+        # registration and the first ListAndWatch (seconds once on a busy box, profiles/r2l).
+        for res in {schema.DEFAULT_RESOURCE} | {r.get("resourceName", schema.DEFAULT_RESOURCE)
+                                                 for r in self.records.values()}:
             self._ensure_plugin(res)
         loops = [(self._sampler, "sampler"), (self._device_event_watcher, "dev-events"),
                  (self._fault_watcher, "fault-watch")]
