@@ -59,41 +59,50 @@ def main() -> int:
     if ds is None:
         ds = synthetic_fmnist(a.samples)
     smp = ddp.sampler(ds, env)
-    loader = torch.utils.data.DataLoader(ds, batch_size=a.batch_size, shuffle=smp is None,
-                                         sampler=smp, drop_last=True)
-    model = ddp.wrap(get_model(), env)
-    opt = torch.optim.SGD(model.parameters(), lr=a.lr)
+    loader = torch.utils.data.DataLoader(ds, batch_size=a.batch_size, sampler=smp, drop_last=True)
+    base = get_model().to(env.device)
+    opt = torch.optim.SGD(base.parameters(), lr=a.lr)
     loss_fn = nn.CrossEntropyLoss()
+    # Resume: rank 0 reads the checkpoint and broadcasts it, so every rank restarts at the same
+    # step/epoch/batch even when only rank 0's node holds GPUPOOL_CHECKPOINT_DIR (no shared volume);
+    # the weights are loaded BEFORE the DDP wrapper is built (DDP then starts from them).
+    step, start_epoch, skip = 0, 0, 0
+    ckpt = os.path.join(a.checkpoint_dir, "fmnist_ckpt.pt") if a.checkpoint_dir else ""
+    st = None
+    if ckpt and env.is_main and os.path.exists(ckpt):
+        st = torch.load(ckpt, map_location="cpu", weights_only=True)
+    if mode == "distributed":
+        st = ddp.broadcast_object(st, env)
+    if st is not None:
+        base.load_state_dict(st["model"])
+        opt.load_state_dict(st["opt"])
+        step, start_epoch, skip = int(st["step"]), int(st["epoch"]), int(st.get("batch", 0))
+        if env.is_main:
+            print(json.dumps({"event": "resume", "step": step, "epoch": start_epoch,
+                              "batch": skip}), flush=True)
+    model = ddp.wrap(base, env)
     info = {"rank": env.rank, "world": env.world, "device": str(env.device), "mode": mode,
             "data": data_kind, "rocr_visible": os.environ.get("ROCR_VISIBLE_DEVICES", "")}
     if env.device.type == "cuda":
         p = torch.cuda.get_device_properties(env.device)
         info.update({"gpu": p.name, "arch": getattr(p, "gcnArchName", "")})
     print(json.dumps({"event": "start", **info}), flush=True)
-    step, t0, first_loss, loss_v = 0, time.time(), None, float("nan")
-    start_epoch = 0
-    ckpt = os.path.join(a.checkpoint_dir, "fmnist_ckpt.pt") if a.checkpoint_dir else ""
-    if ckpt and os.path.exists(ckpt):  # a restarted gang resumes instead of starting over
-        st = torch.load(ckpt, map_location=env.device, weights_only=True)
-        (model.module if hasattr(model, "module") else model).load_state_dict(st["model"])
-        opt.load_state_dict(st["opt"])
-        step, start_epoch = int(st["step"]), int(st["epoch"])
-        if env.is_main:
-            print(json.dumps({"event": "resume", "step": step, "epoch": start_epoch}), flush=True)
+    t0, first_loss, loss_v = time.time(), None, float("nan")
 
-    def save_checkpoint(epoch: int) -> None:
+    def save_checkpoint(epoch: int, batch: int) -> None:
         if not ckpt or not env.is_main:
             return
         os.makedirs(a.checkpoint_dir, exist_ok=True)
         tmp = ckpt + ".tmp"
-        torch.save({"model": (model.module if hasattr(model, "module") else model).state_dict(),
-                    "opt": opt.state_dict(), "step": step, "epoch": epoch}, tmp)
+        torch.save({"model": base.state_dict(), "opt": opt.state_dict(), "step": step,
+                    "epoch": epoch, "batch": batch}, tmp)
         os.replace(tmp, ckpt)  # atomic: a crash never leaves a torn checkpoint
     for epoch in range(start_epoch, a.epochs):
-        if smp is not None:
-            smp.set_epoch(epoch)
+        smp.set_epoch(epoch)  # same order as before the restart: the skipped batches are exact
         model.train()
-        for x, y in loader:
+        for bi, (x, y) in enumerate(loader):
+            if epoch == start_epoch and bi < skip:
+                continue  # already trained on before the checkpoint (no replay)
             x, y = x.to(env.device, non_blocking=True), y.to(env.device, non_blocking=True)
             opt.zero_grad(set_to_none=True)
             loss = loss_fn(model(x), y)
@@ -101,7 +110,7 @@ def main() -> int:
             opt.step()
             step += 1
             if ckpt and step % a.checkpoint_every == 0:
-                save_checkpoint(epoch)
+                save_checkpoint(epoch, bi + 1)
             if a.fail_at_step and step == a.fail_at_step and \
                     os.environ.get("GPUPOOL_JOB_ATTEMPT", "1") == a.fail_on_attempt:
                 print(json.dumps({"event": "injected_failure", "step": step}), flush=True)
@@ -121,8 +130,7 @@ def main() -> int:
         torch.cuda.synchronize()
     if env.is_main:
         os.makedirs(a.output, exist_ok=True)
-        state = (model.module if hasattr(model, "module") else model).state_dict()
-        torch.save(state, os.path.join(a.output, "fashion_mnist_cnn.pth"))  # GPU调度平台搭建.md:603
+        torch.save(base.state_dict(), os.path.join(a.output, "fashion_mnist_cnn.pth"))  # GPU调度平台搭建.md:603
         print(json.dumps({"event": "done", "steps": step, "first_loss": first_loss,
                           "final_loss": round(loss_v, 4), "seconds": round(time.time() - t0, 3),
                           **info}), flush=True)

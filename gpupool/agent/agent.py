@@ -632,7 +632,8 @@ class Agent:
             for d in chosen:
                 rec = {"uuid": d["uuid"], "poolUID": pool_uid, "pool": req.get("pool", ""),
                        "resourceName": resource, "policy": policy,
-                       "baseline": {"ecc": dict(d.get("ecc") or {})}, "claimedAt": ts,
+                       "baseline": {"ecc": dict(d.get("ecc") or {}),
+                                    "eccUmc": dict(d.get("eccUmc") or {})}, "claimedAt": ts,
                        "state": "Probing", "probe": None}
                 self.records[d["uuid"]] = rec
             self.ledger.commit(self.records)  # durable before probing: no double claim on crash

@@ -57,10 +57,20 @@ def wrap(model: torch.nn.Module, env: DistEnv) -> torch.nn.Module:
 
 
 def sampler(dataset, env: DistEnv, shuffle: bool = True):
-    if env.world > 1:
-        return torch.utils.data.distributed.DistributedSampler(dataset, num_replicas=env.world,
-                                                               rank=env.rank, shuffle=shuffle)
-    return None
+    """Epoch-seeded order on every rank (also for a single process): a job resumed mid-epoch can
+    skip exactly the batches it already trained on."""
+    return torch.utils.data.distributed.DistributedSampler(dataset, num_replicas=env.world,
+                                                           rank=env.rank, shuffle=shuffle)
+
+
+def broadcast_object(obj, env: DistEnv, src: int = 0):
+    """Rank ``src``'s Python object on every rank (e.g. a checkpoint only rank 0 can read: ranks on
+    other nodes have no shared volume, and a per-rank load would desynchronise the collectives)."""
+    if env.world <= 1:
+        return obj
+    box = [obj if env.rank == src else None]
+    dist.broadcast_object_list(box, src=src, device=env.device if env.backend == "nccl" else None)
+    return box[0]
 
 
 def all_reduce_mean(x: float, env: DistEnv) -> float:

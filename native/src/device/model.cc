@@ -101,6 +101,18 @@ Json evaluate(const Json& dev, const Json& baseline, const Json& policy) {
     reasons.push_back(fmt("HBMUncorrectableECC: +%lld uncorrectable since claim (max %lld)", d_unc,
                           health["maxUncorrectableECC"].as_int(0)));
   }
+  // the UMC (HBM) block's own count, read by the fast health poll; checked as its own delta so a
+  // poll-only reading never mixes with the all-blocks total
+  const Json& umc = dev["eccUmc"];
+  if (ecc_ok && umc.is_object()) {
+    int64_t u = umc["uncorrectable"].as_int(0);
+    int64_t d_umc = u - baseline.path("eccUmc.uncorrectable").as_int(u);
+    if (d_umc > health["maxUncorrectableECC"].as_int(0)) {
+      ecc_ok = false;
+      reasons.push_back(fmt("HBMUncorrectableECC: +%lld uncorrectable in HBM (UMC) since claim (max %lld)", d_umc,
+                            health["maxUncorrectableECC"].as_int(0)));
+    }
+  }
   if (d_cor > health["maxCorrectableECC"].as_int(100000)) {
     ecc_ok = false;
     reasons.push_back(fmt("HBMCorrectableECCExceeded: +%lld correctable since claim (max %lld)", d_cor,

@@ -7,7 +7,7 @@
 //      write+read bandwidth reported;
 //   2. MFMA: a bf16 GEMM on the matrix cores (`v_mfma_f32_16x16x32_bf16`) is bit-exact against
 //      (a) a full VALU fp32 reference on a 256^3 problem with an asymmetric B (catches fragment
-//      layout / row<->col faults) and (b) exact int64 ABFT row+column checksums on an N^3 problem
+//      layout / row<->col faults) and (b) exact u32 (mod 2^32) ABFT row+column checksums on an N^3 problem
 //      whose operands are small integers (all partial sums exact in fp32), with TFLOP/s reported.
 //
 // Design for CDNA4: 64-wide waves; 16-byte vector loads/stores everywhere (Guideline 13);
@@ -680,7 +680,7 @@ std::string hip_uuid(int dev) {
 
 // Enqueues the whole MFMA phase on stream s (no host sync): (a) a 256^3 GEMM checked element by
 // element against the VALU reference with asymmetric operands, (b) the timed N^3 GEMM (events
-// ctx.gev[0..1]) with exact int64 ABFT row/column checksums, then copies the two mismatch
+// ctx.gev[0..1]) with exact u32 (mod 2^32) ABFT row/column checksums, then copies the two mismatch
 // counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``.
 void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inject_gemm, int census_fault_xcc,
                        unsigned long long* cnt, unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {

@@ -44,7 +44,15 @@ def main() -> None:
         "compute_partition": med_us(lambda: a.amdsmi_get_gpu_compute_partition(h)),
         "memory_partition": med_us(lambda: a.amdsmi_get_gpu_memory_partition(h)),
         "gpu_metrics_info": med_us(lambda: a.amdsmi_get_gpu_metrics_info(h)),
+        "ecc_count_umc": med_us(lambda: a.amdsmi_get_gpu_ecc_count(h, a.AmdSmiGpuBlock.UMC)),
+        "ecc_count_gfx": med_us(lambda: a.amdsmi_get_gpu_ecc_count(h, a.AmdSmiGpuBlock.GFX)),
+        "ecc_enabled": med_us(lambda: a.amdsmi_get_gpu_ecc_enabled(h)),
     }
+    try:
+        out["ecc_count_umc_value"] = a.amdsmi_get_gpu_ecc_count(h, a.AmdSmiGpuBlock.UMC)
+        out["ecc_enabled_value"] = a.amdsmi_get_gpu_ecc_enabled(h)
+    except Exception as e:
+        out["ecc_values_error"] = str(e)
     a.amdsmi_shut_down()
     from gpupool.ops import devlib
     d = devlib.DeviceLib("amdsmi", node="t", events=False)

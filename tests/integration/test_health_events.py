@@ -78,6 +78,12 @@ def test_evaluate_retired_pending_and_lifetime_rules(native_built):
     assert devlib.evaluate(hist, hist, {})["healthy"]
     v = devlib.evaluate(hist, hist, {"health": {"maxLifetimeUncorrectableECC": 0}})
     assert not v["healthy"] and any("HBMUncorrectableECCHistory" in r for r in v["reasons"])
+    # the health poll's UMC-only count is its own delta (never mixed with the all-blocks total)
+    base = {**dev, "eccUmc": {"correctable": 0, "uncorrectable": 0, "deferred": 0}}
+    now = {**base, "eccUmc": {"correctable": 0, "uncorrectable": 1, "deferred": 0}}
+    v = devlib.evaluate(now, base, {})
+    assert not v["eccOk"] and any("in HBM (UMC)" in r for r in v["reasons"]), v
+    assert devlib.evaluate(now, now, {})["healthy"]
 
 
 def test_retired_pages_make_a_gpu_unclaimable(workdir, native_built):

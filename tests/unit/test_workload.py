@@ -53,3 +53,37 @@ def test_ddp_two_ranks_gloo(tmp_path):
     sd = torch.load(out / "fashion_mnist_cnn.pth", weights_only=True)
     assert "0.weight" in sd  # plain (unwrapped) state_dict, loadable by get_model()
     get_model().load_state_dict(sd)
+
+
+def test_resume_on_two_ranks_without_a_shared_volume(tmp_path):
+    """only rank 0's node holds the checkpoint (no shared volume). Attempt 1 fails at
+    step 25 (checkpoint at step 20, batch 20 of epoch 0 with 2 ranks x 1024 samples / 32); on the
+    restart rank 0 loads and broadcasts it, BOTH ranks resume at step 20 / batch 20 (rank 1 has
+    an empty checkpoint dir), the collectives stay aligned and the job finishes at step 40."""
+    port = _free_port()
+    dirs = [tmp_path / "ckpt-rank0", tmp_path / "ckpt-rank1"]
+
+    def launch(attempt: str):
+        procs = []
+        for rank in range(2):
+            env = dict(os.environ, OMP_NUM_THREADS="2", RANK=str(rank), LOCAL_RANK="0",
+                       WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       GPUPOOL_JOB_ATTEMPT=attempt)
+            procs.append(subprocess.Popen(
+                [sys.executable, os.path.join(ROOT, "examples", "fmnist_train.py"), "--mode",
+                 "distributed", "--cpu", "--synthetic", "--samples", "2048", "--batch_size", "32",
+                 "--steps", "40", "--epochs", "3", "--checkpoint_dir", str(dirs[rank]),
+                 "--checkpoint_every", "10", "--fail_at_step", "25", "--output",
+                 str(tmp_path / f"out{rank}")], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                stderr=subprocess.STDOUT, text=True))
+        return [(p.communicate(timeout=300)[0], p.returncode) for p in procs]
+    first = launch("1")
+    assert all(rc == 3 for _, rc in first), first
+    assert (dirs[0] / "fmnist_ckpt.pt").exists() and not (dirs[1] / "fmnist_ckpt.pt").exists()
+    second = launch("2")
+    assert all(rc == 0 for _, rc in second), [o[-2000:] for o, _ in second]
+    out0 = [json.loads(x) for x in second[0][0].splitlines() if x.startswith("{")]
+    resume = next(e for e in out0 if e["event"] == "resume")
+    assert (resume["step"], resume["epoch"], resume["batch"]) == (20, 0, 20)
+    done = next(e for e in out0 if e["event"] == "done")
+    assert done["steps"] == 40 and done["world"] == 2
