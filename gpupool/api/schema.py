@@ -184,13 +184,19 @@ DEVICE_STATUS = {
 
 MI355X_SPEC = {
     "type": "object",
-    "description": "Desired state of a pool of MI355X (gfx950) GPUs on one node.",
+    "description": "Desired state of a pool of MI355X (gfx950) GPUs on one node (or up to "
+                   "spec.maxNodes nodes).",
     "required": ["replicas"],
     "properties": {
         "replicas": {**_I32, "minimum": 0, "maximum": 1024,
                      "description": "Number of healthy GPUs to claim, probe and advertise."},
         "nodeName": {**_S, "description": "Pin the pool to one node (else nodeSelector/any)."},
         "nodeSelector": {"type": "object", "additionalProperties": _S},
+        "maxNodes": {**_I32, "minimum": 1, "maximum": 64, "default": 1,
+                     "description": "How many nodes the pool may span (like the reference's pool "
+                                    "of N VMs). 1 keeps every GPU of the pool on one xGMI-connected "
+                                    "node; above 1 a scale-up that no single node fits is split "
+                                    "across nodes (fewest nodes first, all-or-nothing per pass)."},
         "resourceName": {**_S, "default": DEFAULT_RESOURCE,
                          "pattern": r"^[a-z0-9.-]+/[a-z0-9.-]+$",
                          "description": "Extended resource the device plugin advertises "
@@ -306,6 +312,8 @@ MI355X_STATUS = {
         "replicas": _I32,
         "readyReplicas": _I32,
         "nodeName": _S,
+        "nodes": {"type": "array", "items": _S,
+                  "description": "Every node holding GPUs of the pool (maxNodes > 1)."},
         "selector": _S,
         "devices": {"type": "array", "items": DEVICE_STATUS},
         "conditions": CONDITIONS_FIELD,

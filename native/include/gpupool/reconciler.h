@@ -93,15 +93,21 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
 
  private:
   struct Observed {
-    std::string node;
+    std::string node;                              // the pool's (primary) node
+    std::vector<std::string> nodes;                // every node holding GPUs of the pool
     bool reachable = true;
     std::string error;
     std::vector<DeviceView> mine;
     int64_t free_healthy = 0;
+    std::map<std::string, int64_t> free_by_node;   // free healthy GPUs per observed node
   };
   Observed observe_(const ObjectMeta& m, const Mi355xPoolSpec& spec, const Json& status);
   // Nodes (reachable, selector-matching) with >= need free healthy GPUs, tightest fit first.
   std::vector<std::string> choose_nodes_(const Mi355xPoolSpec& spec, int need);
+  // spec.maxNodes > 1: split a scale-up of ``need`` GPUs over the pool's nodes first, then the
+  // fewest new selector-matching nodes (most free first). Empty when it does not fit.
+  std::vector<std::pair<std::string, int>> plan_span_(const Mi355xPoolSpec& spec, int need, const Observed& o);
+  static bool spans_(const Mi355xPoolSpec& spec) { return spec.max_nodes > 1 && spec.node_name.empty(); }
   bool quota_allows_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta, std::string* why);
   Outcome finalize_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec);
   // Evicts pods on draining devices and releases drained ones. Returns #devices still draining.
@@ -116,6 +122,9 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
   std::map<std::string, std::set<std::string>> evicted_;  // pool uid -> pod keys already evicted
   std::map<std::string, std::set<std::string>> eviction_blocked_;  // pool uid -> pods refused by a PDB (evented)
   std::map<std::string, int64_t> policy_gen_;             // pool uid -> generation pushed to agents
+  // pool uid -> no spanning claim before this time: a rolled-back pass frees GPUs, whose capacity
+  // event would otherwise wake the same pool into the same failing claim at once
+  std::map<std::string, std::chrono::steady_clock::time_point> span_backoff_;
 };
 
 class AzureVmPoolReconciler : public PoolReconcilerBase {

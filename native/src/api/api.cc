@@ -85,6 +85,7 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.probe_xgmi_peer_check = pr["xgmiPeerCheck"].as_bool(false);
   p.probe_min_xgmi_gbps = pr["minXgmiGBps"].as_double(0);
   p.replace_policy = s["replacePolicy"].str_or("Replace");
+  p.max_nodes = static_cast<int32_t>(s["maxNodes"].as_int(1));
   const Json& a = s["autoscale"];
   p.autoscale = a["enabled"].as_bool(false);
   p.autoscale_min = static_cast<int32_t>(a["minReplicas"].as_int(0));
@@ -242,6 +243,10 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
     errs.push_back("spec.topologyPolicy: Unsupported value");
   if (s.contains("replacePolicy") && !in(s["replacePolicy"].as_string(), {"Replace", "Keep"}))
     errs.push_back("spec.replacePolicy: Unsupported value");
+  if (s.contains("maxNodes")) {
+    int64_t v = s["maxNodes"].as_int(0);
+    if (!s["maxNodes"].is_int() || v < 1 || v > 64) errs.push_back("spec.maxNodes: must be within [1, 64]");
+  }
   const Json& h = s["health"];
   if (h.contains("thermal") && !in(h["thermal"].as_string(), {"belowCritical", "belowEmergency", "ignore"}))
     errs.push_back("spec.health.thermal: Unsupported value");

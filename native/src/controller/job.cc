@@ -141,7 +141,14 @@ bool Mi355xJobReconciler::resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec
     return false;
   }
   if (spec.resource_name.empty()) *resource = pool.path("spec.resourceName").str_or(gen::kDefaultResource);
+  // a pool spanning nodes (spec.maxNodes > 1) lists them all: the gang may use any of them
   *node = pool.path("status.nodeName").as_string();
+  std::vector<std::string> span;
+  for (const auto& n : pool.path("status.nodes").elements()) span.push_back(n.as_string());
+  if (!span.empty()) {
+    node->clear();
+    for (const auto& n : span) *node += (node->empty() ? "" : ",") + n;
+  }
   if (node->empty()) {
     *why = "Mi355xPool " + spec.pool_ref + " has no GPUs placed yet";
     return false;
@@ -239,7 +246,7 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
   for (const auto& n : nodes["items"].elements()) {
     const std::string name = n.path("metadata.name").as_string();
     if (!node_schedulable(n) || !selector_matches(spec.node_selector, n)) continue;
-    if (!pool_node.empty() && name != pool_node) continue;
+    if (!pool_node.empty() && ("," + pool_node + ",").find("," + name + ",") == std::string::npos) continue;
     free[name] = qty(n.path("status.allocatable")[resource]);
     order.push_back(name);
   }

@@ -181,6 +181,37 @@ void PoolReconcilerBase::forget_(const std::string& uid) {
   ready_gen_.erase(uid);
 }
 
+namespace {
+// GPUs (by uuid) grouped by the node that holds them (spanning pools act per node).
+template <class Obs>
+std::map<std::string, std::vector<std::string>> by_node(const Obs& o, const std::vector<std::string>& uuids) {
+  std::map<std::string, std::vector<std::string>> out;
+  for (const auto& u : uuids)
+    for (const auto& d : o.mine)
+      if (d.uuid == u) out[d.node.empty() ? o.node : d.node].push_back(u);
+  return out;
+}
+
+// o.nodes = every node holding GPUs of the pool; for a spanning pool also the primary o.node (the
+// node holding most of it, ties by name) and its free count.
+template <class Obs>
+void index_nodes(Obs& o, bool primary) {
+  std::map<std::string, int> per_node;
+  for (const auto& d : o.mine) ++per_node[d.node.empty() ? o.node : d.node];
+  o.nodes.clear();
+  for (const auto& kv : per_node) o.nodes.push_back(kv.first);
+  if (!primary) return;
+  o.node.clear();
+  int best = 0;
+  for (const auto& kv : per_node)
+    if (kv.second > best) {
+      best = kv.second;
+      o.node = kv.first;
+    }
+  o.free_healthy = o.node.empty() || !o.free_by_node.count(o.node) ? 0 : o.free_by_node.at(o.node);
+}
+}  // namespace
+
 // ================================================================== Mi355xPool
 Mi355xPoolReconciler::Mi355xPoolReconciler(KubeClient& client, Informer& pools, DeviceProvider& provider,
                                            EventRecorder* events, ReconcilerOptions opts)
@@ -190,15 +221,23 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
                                                               const Json& status) {
   trace::Span span("observe");
   Observed o;
-  std::vector<std::string> nodes;
+  const bool span_nodes = spans_(spec);
+  std::set<std::string> hinted;
   std::string hint = status["nodeName"].as_string();
-  if (!hint.empty()) nodes.push_back(hint);
-  if (!spec.node_name.empty() && spec.node_name != hint) nodes.push_back(spec.node_name);
-  if (nodes.empty()) nodes = provider_.node_names();
+  if (!hint.empty()) hinted.insert(hint);
+  for (const auto& n : status["nodes"].elements()) hinted.insert(n.as_string());
+  std::vector<std::string> nodes;
+  if (span_nodes) {
+    nodes = provider_.node_names();  // a spanning pool may hold GPUs on any agent: see them all
+  } else {
+    if (!hint.empty()) nodes.push_back(hint);
+    if (!spec.node_name.empty() && spec.node_name != hint) nodes.push_back(spec.node_name);
+    if (nodes.empty()) nodes = provider_.node_names();
+  }
   for (const auto& n : nodes) {
     NodeView nv = provider_.observe(n);
     if (!nv.reachable) {
-      if (n == hint || n == spec.node_name) {
+      if (hinted.count(n) || n == spec.node_name) {
         o.reachable = false;
         o.error = nv.error;
         o.node = n;
@@ -211,6 +250,11 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
       if (d.pool_uid == m.uid) mine.push_back(d);
       else if (d.state == "Free" && d.healthy) ++free_healthy;
     }
+    o.free_by_node[n] = free_healthy;
+    if (span_nodes) {
+      for (auto& d : mine) o.mine.push_back(std::move(d));
+      continue;
+    }
     if (!mine.empty() || n == hint || (o.node.empty() && n == spec.node_name)) {
       o.node = n;
       o.reachable = true;
@@ -220,7 +264,10 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
       if (!o.mine.empty()) break;
     }
   }
-  std::sort(o.mine.begin(), o.mine.end(), [](const DeviceView& a, const DeviceView& b) { return a.index < b.index; });
+  std::sort(o.mine.begin(), o.mine.end(), [](const DeviceView& a, const DeviceView& b) {
+    return a.node != b.node ? a.node < b.node : a.index < b.index;
+  });
+  index_nodes(o, span_nodes && o.reachable);
   return o;
 }
 
@@ -254,16 +301,73 @@ std::vector<std::string> Mi355xPoolReconciler::choose_nodes_(const Mi355xPoolSpe
   return out;
 }
 
+std::vector<std::pair<std::string, int>> Mi355xPoolReconciler::plan_span_(const Mi355xPoolSpec& spec, int need,
+                                                                          const Observed& o) {
+  struct Cand {
+    std::string name;
+    int64_t free;
+    bool mine;
+  };
+  std::vector<Cand> cands;
+  for (const auto& kv : o.free_by_node) {
+    if (kv.second <= 0) continue;
+    bool mine = std::find(o.nodes.begin(), o.nodes.end(), kv.first) != o.nodes.end();
+    if (!mine) {
+      Json labels = provider_.node_labels(kv.first);
+      bool match = true;
+      for (const auto& sel : spec.node_selector)
+        if (labels[sel.first].as_string() != sel.second) match = false;
+      if (!match) continue;
+    }
+    cands.push_back({kv.first, kv.second, mine});
+  }
+  // nodes already holding the pool first (locality), then most free first (fewest nodes)
+  std::sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
+    if (a.mine != b.mine) return a.mine;
+    return a.free != b.free ? a.free > b.free : a.name < b.name;
+  });
+  const int allowed_new = spec.max_nodes - static_cast<int>(o.nodes.size());
+  std::vector<std::pair<std::string, int>> plan;
+  int left = need;
+  for (const auto& c : cands)  // 1. grow where the pool already is
+    if (c.mine && left > 0) {
+      int k = static_cast<int>(std::min<int64_t>(c.free, left));
+      plan.emplace_back(c.name, k);
+      left -= k;
+    }
+  if (left == 0) return plan;
+  if (allowed_new < 1) return {};
+  // 2. the rest on ONE new node if any fits it (the tightest such fit keeps big nodes whole)
+  const Cand* single = nullptr;
+  for (const auto& c : cands)
+    if (!c.mine && c.free >= left && (!single || c.free < single->free)) single = &c;
+  if (single) {
+    plan.emplace_back(single->name, left);
+    return plan;
+  }
+  // 3. else split over the fewest new nodes (most free first), within spec.maxNodes
+  int new_nodes = 0;
+  for (const auto& c : cands) {
+    if (c.mine || left <= 0 || new_nodes >= allowed_new) continue;
+    int k = static_cast<int>(std::min<int64_t>(c.free, left));
+    plan.emplace_back(c.name, k);
+    left -= k;
+    ++new_nodes;
+  }
+  if (left > 0) return {};
+  return plan;
+}
+
 int Mi355xPoolReconciler::drain_(const Json& obj, const std::string& node, const ObjectMeta& m,
                                  const Mi355xPoolSpec& spec, std::vector<DeviceView>& mine) {
   trace::Span span("drain");
   int still = 0;
-  std::vector<std::string> release;
+  std::map<std::string, std::vector<std::string>> release;  // node -> drained GPUs
   auto now = std::chrono::system_clock::now();
   for (auto& d : mine) {
     if (d.state != "Draining") continue;
     if (d.pods.size() == 0) {
-      release.push_back(d.uuid);
+      release[d.node.empty() ? node : d.node].push_back(d.uuid);
       continue;
     }
     ++still;
@@ -319,14 +423,15 @@ int Mi355xPoolReconciler::drain_(const Json& obj, const std::string& node, const
       }
     }
   }
-  if (!release.empty()) {
-    provider_.release(node, m.uid, release);
+  for (const auto& kv : release) {
+    provider_.release(kv.first, m.uid, kv.second);
     {
       std::lock_guard<std::mutex> g(mu_);
       evicted_[m.uid].clear();
       eviction_blocked_[m.uid].clear();
     }
-    event_(obj, "Normal", "GPUReleased", "released " + std::to_string(release.size()) + " GPU(s) on " + node + ": " + join(release, ","));
+    event_(obj, "Normal", "GPUReleased", "released " + std::to_string(kv.second.size()) + " GPU(s) on " + kv.first +
+                                             ": " + join(kv.second, ","));
   }
   return still;
 }
@@ -374,6 +479,11 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
   st["replicas"] = claimed;
   st["readyReplicas"] = ready;
   if (!o.node.empty()) st["nodeName"] = o.node;
+  if (o.nodes.size() > 1 || spans_(spec)) {
+    Json ns = Json::array();
+    for (const auto& n : o.nodes) ns.push_back(n);
+    st["nodes"] = ns;
+  }
   st["devices"] = devices;
   Json conds = obj.path("status.conditions").is_array() ? obj.path("status.conditions") : Json::array();
   const int64_t gen = m.generation;
@@ -435,7 +545,8 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
                        : "NotReady";
   set_condition(conds, gen::kCondReady, is_ready ? "True" : "False", reason,
                 std::to_string(ready) + "/" + std::to_string(spec.replicas) + " GPUs ready" +
-                    (o.node.empty() ? "" : " on " + o.node),
+                    (o.nodes.size() > 1 ? " on " + std::to_string(o.nodes.size()) + " nodes"
+                     : o.node.empty() ? "" : " on " + o.node),
                 gen, now);
   st["conditions"] = conds;
   return st;
@@ -451,7 +562,7 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
   for (const auto& d : o.mine)
     if (d.state != "Draining") cordon.push_back(d.uuid);
   if (!cordon.empty()) {
-    provider_.cordon(o.node, m.uid, cordon);
+    for (const auto& kv : by_node(o, cordon)) provider_.cordon(kv.first, m.uid, kv.second);
     event_(obj, "Normal", "DrainStarted", "pool deleting: draining " + std::to_string(cordon.size()) + " GPU(s)");
     o = observe_(m, spec, obj["status"]);
   }
@@ -471,6 +582,7 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
     evicted_.erase(m.uid);
     eviction_blocked_.erase(m.uid);
     policy_gen_.erase(m.uid);
+    span_backoff_.erase(m.uid);
   }
   forget_(m.uid);
   ready_gauge().erase({{"kind", kind_}, {"pool", m.key()}});
@@ -517,7 +629,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
       push = policy_gen_[m.uid] != m.generation;
     }
     if (push) {
-      provider_.update_policy(o.node, m.uid, spec.policy_json(), spec.resource_name);
+      for (const auto& n : o.nodes) provider_.update_policy(n, m.uid, spec.policy_json(), spec.resource_name);
       std::lock_guard<std::mutex> g(mu_);
       policy_gen_[m.uid] = m.generation;
     }
@@ -557,11 +669,15 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     // Deterministic victims (fixes README.md:214's arbitrary existingVMs[:n]): unhealthy first,
     // then GPUs without pods, then the highest index.
     std::vector<const DeviceView*> order = keep;
-    std::sort(order.begin(), order.end(), [](const DeviceView* a, const DeviceView* b) {
+    std::map<std::string, int> on_node;  // a spanning pool shrinks its smallest node first
+    for (const DeviceView* d : keep) ++on_node[d->node];
+    std::sort(order.begin(), order.end(), [&on_node](const DeviceView* a, const DeviceView* b) {
       bool ua = !a->healthy || !a->probe_passed, ub = !b->healthy || !b->probe_passed;
       if (ua != ub) return ua;
       bool pa = a->pods.size() > 0, pb = b->pods.size() > 0;
       if (pa != pb) return !pa;
+      if (on_node[a->node] != on_node[b->node]) return on_node[a->node] < on_node[b->node];
+      if (a->node != b->node) return a->node > b->node;
       return a->index > b->index;
     });
     int64_t drop = n_active - spec.replicas;
@@ -574,7 +690,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     n_active = spec.replicas;
   }
   if (!cordon.empty()) {
-    provider_.cordon(o.node, m.uid, cordon);
+    for (const auto& kv : by_node(o, cordon)) provider_.cordon(kv.first, m.uid, kv.second);
     acted = true;
   }
   std::string quota_msg;
@@ -584,6 +700,80 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     blocked = "QuotaExceeded";
     progress_msg = quota_msg;
     event_(obj, "Warning", "QuotaExceeded", quota_msg);
+  } else if (n_active < spec.replicas && spans_(spec)) {
+    // spec.maxNodes > 1: the delta may be split over nodes; all-or-nothing per pass (a claim that
+    // fails part-way hands back what this pass already claimed on the other nodes).
+    int need = static_cast<int>(spec.replicas - n_active);
+    bool backing_off;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      backing_off = span_backoff_.count(m.uid) && clock_t_::now() < span_backoff_[m.uid];
+    }
+    auto plan = backing_off ? std::vector<std::pair<std::string, int>>{} : plan_span_(spec, need, o);
+    if (backing_off) {
+      blocked = "InsufficientDevices";
+      progress_msg = "a spanning claim of " + std::to_string(need) + " GPU(s) was rolled back; retrying shortly";
+    } else if (plan.empty()) {
+      blocked = "InsufficientDevices";
+      progress_msg = "need " + std::to_string(need) + " free healthy GPU(s) on at most " +
+                     std::to_string(spec.max_nodes) + " node(s)";
+      event_(obj, "Warning", "InsufficientDevices", progress_msg);
+    } else {
+      std::vector<std::pair<std::string, std::vector<std::string>>> made;
+      std::vector<DeviceView> got;
+      std::string fail_reason, fail_msg;
+      for (const auto& step : plan) {
+        ClaimRequest req;
+        req.pool_uid = m.uid;
+        req.pool = m.key();
+        req.count = step.second;
+        req.topology_policy = spec.topology_policy;
+        req.resource_name = spec.resource_name;
+        req.policy = spec.policy_json();
+        req.probe = spec.probe_json();
+        ClaimResult cr = provider_.claim(step.first, req);
+        if (!cr.ok) {
+          fail_reason = cr.reason.empty() ? "InsufficientDevices" : cr.reason;
+          fail_msg = step.first + ": " + cr.message;
+          break;
+        }
+        std::vector<std::string> uuids;
+        for (auto& d : cr.devices) {
+          uuids.push_back(d.uuid);
+          got.push_back(std::move(d));
+        }
+        made.emplace_back(step.first, std::move(uuids));
+      }
+      acted = true;
+      if (!fail_reason.empty()) {
+        for (const auto& kv : made) provider_.release(kv.first, m.uid, kv.second);
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          span_backoff_[m.uid] = clock_t_::now() + ms(5000);
+        }
+        blocked = fail_reason;
+        progress_msg = fail_reason + ": " + fail_msg + (made.empty() ? "" : " (this pass's other claims released)");
+        event_(obj, "Warning", fail_reason, progress_msg);
+      } else {
+        if (progress_reason.empty()) progress_reason = "ScalingUp";
+        std::vector<std::string> where;
+        for (const auto& kv : made) where.push_back(std::to_string(kv.second.size()) + " on " + kv.first);
+        progress_msg = "claimed " + std::to_string(got.size()) + " GPU(s): " + join(where, ", ");
+        event_(obj, "Normal", "GPUClaimed", progress_msg);
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          policy_gen_[m.uid] = m.generation;
+        }
+        log.info("claimed", Json::object().set("nodes", static_cast<long long>(made.size())).set("count", need));
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          span_backoff_.erase(m.uid);
+        }
+        claimed_only = cordon.empty();
+        claimed = std::move(got);
+        claimed_node = made.front().first;
+      }
+    }
   } else if (n_active < spec.replicas) {
     int need = static_cast<int>(spec.replicas - n_active);
     // A pool lives on one node: extend where it already is, else try the fitting nodes in order.
@@ -638,11 +828,17 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     // The claim RPC returns the agent's post-claim ground truth for the new GPUs (probed and,
     // with a device plugin, already advertised); the rest of o.mine was observed this pass and
     // nothing else changed, so merging replaces a second GET /v1/node (A1 still holds).
-    o.node = claimed_node;
+    if (o.node.empty() || !spans_(spec)) o.node = claimed_node;
     o.reachable = true;
+    for (auto& d : claimed) {
+      if (o.free_by_node.count(d.node)) o.free_by_node[d.node] = std::max<int64_t>(0, o.free_by_node[d.node] - 1);
+      o.mine.push_back(std::move(d));
+    }
     o.free_healthy = std::max<int64_t>(0, o.free_healthy - static_cast<int64_t>(claimed.size()));
-    for (auto& d : claimed) o.mine.push_back(std::move(d));
-    std::sort(o.mine.begin(), o.mine.end(), [](const DeviceView& a, const DeviceView& b) { return a.index < b.index; });
+    std::sort(o.mine.begin(), o.mine.end(), [](const DeviceView& a, const DeviceView& b) {
+      return a.node != b.node ? a.node < b.node : a.index < b.index;
+    });
+    index_nodes(o, spans_(spec));
   } else if (acted) {
     o = observe_(m, spec, obj["status"]);
   }

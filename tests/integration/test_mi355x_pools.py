@@ -297,9 +297,15 @@ def test_reconcile_traces(node8):
     k = node8.client
     k.create(MI355XPOOLS, mi_pool("tr", 2), "default")
     wait_ready(k, "tr", 2)
-    traces = node8.manager_traces(key="Mi355xPool/default/tr", n=50)
+    # a pass's trace is committed after its status write, which the watch may deliver first
+    deadline = time.monotonic() + 10
+    while True:
+        traces = node8.manager_traces(key="Mi355xPool/default/tr", n=50)
+        claim = [t for t in traces if any(s["name"] == "agent:POST /v1/claims" for s in t["spans"])]
+        if claim or time.monotonic() > deadline:
+            break
+        time.sleep(0.05)
     assert traces and all(t["key"] == "Mi355xPool/default/tr" for t in traces)
-    claim = [t for t in traces if any(s["name"] == "agent:POST /v1/claims" for s in t["spans"])]
     assert len(claim) == 1, traces
     names = [s["name"] for s in claim[0]["spans"]]
     for want in ("observe", "agent:GET /v1/node", "agent.claim.select", "agent.claim.probe",
@@ -519,3 +525,72 @@ def test_agent_rpc_requires_the_shared_token(node8):
     k = node8.client
     k.create(MI355XPOOLS, mi_pool("p", 1), "default")
     wait_ready(k, "p", 1)
+
+
+def test_pool_spans_nodes(cluster_factory):
+    """spec.maxNodes (the reference's pool of N machines, README.md:23-31, :199-209): a pool of 12
+    on two 8-GPU nodes claims 8 + 4 (all-or-nothing per pass), is Ready with status.nodes listing
+    both and every device carrying its node; scaling to 4 drains the smaller node first and ends
+    on one node; maxNodes=1 pools still refuse what no single node fits; deletion releases the
+    GPUs on every node through the finalizer."""
+    c = cluster_factory(nodes=[NodeSpec("node-a"), NodeSpec("node-b")])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("one", 12), "default")  # maxNodes defaults to 1
+    k.wait_for(MI355XPOOLS, "one", "default", cond_is("Ready", "False", "InsufficientDevices"),
+               timeout=30)
+    k.delete(MI355XPOOLS, "one", "default")
+    k.wait_for(MI355XPOOLS, "one", "default", lambda o: o is None, timeout=30)
+    k.create(MI355XPOOLS, mi_pool("wide", 12, maxNodes=2), "default")
+    o = wait_ready(k, "wide", 12, timeout=60)
+    st = o["status"]
+    assert sorted(st["nodes"]) == ["node-a", "node-b"]
+    per = {}
+    for d in st["devices"]:
+        per[d["node"]] = per.get(d["node"], 0) + 1
+    assert sorted(per.values()) == [4, 8] and st["nodeName"] == max(per, key=per.get)
+    assert "on 2 nodes" in conds(o)["Ready"]["message"]
+    views = {n: agent_view(c, n) for n in ("node-a", "node-b")}
+    owned = {n: sum(1 for d in v["devices"] if d.get("pool") == "default/wide") for n, v in views.items()}
+    assert owned == per  # the agents agree with the status, node by node
+    small = min(per, key=per.get)
+    k.patch(MI355XPOOLS, "wide", {"spec": {"replicas": 4}}, "default")
+    o = wait_ready(k, "wide", 4, timeout=60)
+    assert {d["node"] for d in o["status"]["devices"]} == {max(per, key=per.get)}
+    assert sum(1 for d in agent_view(c, small)["devices"] if d.get("pool") == "default/wide") == 0
+    # grows back onto the node it is on first (8 there), then the other
+    k.patch(MI355XPOOLS, "wide", {"spec": {"replicas": 10}}, "default")
+    o = wait_ready(k, "wide", 10, timeout=60)
+    per = {}
+    for d in o["status"]["devices"]:
+        per[d["node"]] = per.get(d["node"], 0) + 1
+    assert sorted(per.values()) == [2, 8]
+    # maxNodes=3 cannot exceed what the cluster has: all-or-nothing, nothing partial
+    k.create(MI355XPOOLS, mi_pool("rest", 8, maxNodes=3), "default")
+    r = k.wait_for(MI355XPOOLS, "rest", "default", cond_is("Ready", "False", "InsufficientDevices"),
+                   timeout=30)
+    assert r["status"].get("replicas", 0) == 0
+    k.delete(MI355XPOOLS, "wide", "default")
+    k.wait_for(MI355XPOOLS, "wide", "default", lambda o: o is None, timeout=30)
+    for n in ("node-a", "node-b"):
+        assert not any(d.get("pool") == "default/wide" for d in agent_view(c, n)["devices"])
+    wait_ready(k, "rest", 8, timeout=60)  # the freed GPUs are claimed by the waiting pool
+
+
+def test_spanning_claim_is_all_or_nothing(cluster_factory):
+    """A spanning scale-up whose second node refuses its part (here: the pool's stricter
+    maxRetiredPages, which the node's free-GPU count does not know about) hands back the GPUs it
+    already claimed on the first node in the same pass: nothing partial is left held."""
+    c = cluster_factory(nodes=[NodeSpec("node-a"), NodeSpec("node-b", count=4)])
+    c.set_faults("node-b", {"devices": {str(i): {"ras": {"retiredPages": 10}} for i in range(4)}})
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("strict", 12, maxNodes=2, health={"maxRetiredPages": 5}),
+             "default")
+    o = k.wait_for(MI355XPOOLS, "strict", "default",
+                   cond_is("Ready", "False", "InsufficientDevices"), timeout=30)
+    time.sleep(0.5)
+    o = k.get(MI355XPOOLS, "strict", "default")
+    assert o["status"].get("replicas", 0) == 0
+    for n in ("node-a", "node-b"):
+        assert not any(d.get("pool") == "default/strict" for d in agent_view(c, n)["devices"])
+    msgs = " ".join(e.get("message", "") for e in k.list(EVENTS, "default")["items"])
+    assert "other claims released" in msgs

@@ -64,6 +64,9 @@ CASES = [
     {"kind": "Mi355xPool", "spec": {"replicas": 0, "autoscale": {"minReplicas": -1}}},
     {"kind": "Mi355xPool", "spec": {"replicas": 0, "autoscale": {"scaleDownDelaySeconds": -3}}},
     {"kind": "Mi355xPool", "spec": {}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 12, "maxNodes": 2}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 1, "maxNodes": 0}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 1, "maxNodes": 65}},
     {"kind": "AzureVmPool", "spec": {"replicas": 0, "resourceGroupName": "rg", "location": "e",
                                      "vmSize": "s", "vnetName": "v", "subnetName": "s",
                                      "azureCredentialSecret": "c",
