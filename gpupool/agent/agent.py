@@ -125,6 +125,7 @@ class Agent:
                       "health_polls": 0, "health_poll_ms_sum": 0.0,
                       "device_events": 0, "fault_events": 0}
         self.resetting: set[str] = set()       # GPUs between amdsmi GPUPreReset and GPUPostReset
+        self._claim_cache: dict[tuple[str, str], tuple[dict, bool]] = {}
         self.recent_events: list[dict] = []   # last hardware/overlay events (node view, metrics)
         self.events_supported: dict[str, Any] = {}
         self._pods_cache: tuple[float, dict[str, list[dict]]] = (0.0, {})
@@ -190,6 +191,31 @@ class Agent:
                     out[s_] = v
         return out
 
+    def _claimable(self, devs: list[dict], policy: dict, policy_key: str) -> list[bool]:
+        """Healthy under the requesting pool's policy with baseline = now, for each device. Cached
+        per (device snapshot, policy) — a snapshot dict is replaced, never mutated, when the device
+        changes — and the misses evaluated in one native call."""
+        out: list[bool | None] = []
+        miss = []
+        for d in devs:
+            hit = self._claim_cache.get((d["uuid"], policy_key))
+            if hit is not None and hit[0] is d:
+                out.append(hit[1])
+            else:
+                out.append(None)
+                miss.append(d)
+        if miss:
+            if len(self._claim_cache) > 4096:
+                self._claim_cache.clear()
+            vs = devlib.evaluate_batch([(d, d, policy) for d in miss])
+            it = iter(vs)
+            for i, d in enumerate(devs):
+                if out[i] is None:
+                    ok = bool(next(it).get("healthy"))
+                    self._claim_cache[(d["uuid"], policy_key)] = (d, ok)
+                    out[i] = ok
+        return out  # type: ignore[return-value]
+
     def _asic_faulted(self) -> dict[str, set[str]]:
         """ASIC key -> partitions whose own (pre-fan-out) ASIC-scoped health failed."""
         bad: dict[str, set[str]] = {}
@@ -203,11 +229,11 @@ class Agent:
     def _evaluate_all(self) -> set[str]:
         """Re-evaluate every device; returns pool UIDs whose devices changed verdict."""
         changed: set[str] = set()
-        raw: dict[str, dict] = {}
-        for uuid, d in self.by_uuid.items():
-            rec = self.records.get(uuid)
-            baseline = (rec or {}).get("baseline") or d
-            raw[uuid] = devlib.evaluate(d, baseline, self._policy_for(uuid))
+        uuids = list(self.by_uuid)
+        verdicts = devlib.evaluate_batch([
+            (self.by_uuid[u], (self.records.get(u) or {}).get("baseline") or self.by_uuid[u],
+             self._policy_for(u)) for u in uuids])
+        raw: dict[str, dict] = dict(zip(uuids, verdicts))
         raw = self._fan_out_asic(raw)
         for uuid, d in self.by_uuid.items():
             rec = self.records.get(uuid)
@@ -603,14 +629,15 @@ class Agent:
             quarantined = self.ledger.quarantined()
             free = []
             asic_bad = self._asic_faulted()
-            for uuid, d in self.by_uuid.items():
-                if uuid in self.records or uuid in quarantined or not d.get("present", True):
-                    continue
-                # claimability under the requesting pool's policy (baseline = now: retired HBM
-                # pages and absolute limits count, deltas start at the claim), and no partition
-                # of the same ASIC carrying a package-level fault
-                if devlib.evaluate(d, d, policy).get("healthy") and \
-                        not asic_bad.get(self._asic_key(d), set()) - {uuid}:
+            policy_key = json.dumps(policy, sort_keys=True)
+            cand = [d for uuid, d in self.by_uuid.items()
+                    if uuid not in self.records and uuid not in quarantined and d.get("present", True)
+                    and not asic_bad.get(self._asic_key(d), set()) - {uuid}]
+            # claimability under the requesting pool's policy (baseline = now: retired HBM pages
+            # and absolute limits count, deltas start at the claim); no partition of the same ASIC
+            # may carry a package-level fault (checked above)
+            for d, ok in zip(cand, self._claimable(cand, policy, policy_key)):
+                if ok:
                     free.append(d["index"])
             owned = [self.by_uuid[u]["index"] for u, r in self.records.items()
                      if r["poolUID"] == pool_uid and u in self.by_uuid]
@@ -636,7 +663,10 @@ class Agent:
                                     "eccUmc": dict(d.get("eccUmc") or {})}, "claimedAt": ts,
                        "state": "Probing", "probe": None}
                 self.records[d["uuid"]] = rec
-            self.ledger.commit(self.records)  # durable before probing: no double claim on crash
+            # The claim becomes durable while the probe runs (the ledger's writer fsyncs it
+            # concurrently); the RPC answers only after it is on disk, so no crash can ever make
+            # the manager believe it owns GPUs a restarted agent would hand out again.
+            claim_seq = self.ledger.commit(self.records, durable=False)
             self.stats["claims"] += len(chosen)
         for d in chosen:  # an in-flight HBM scrub window finishes and hands its buffer back
             self.scrubber.yield_device(d["uuid"])
@@ -663,8 +693,10 @@ class Agent:
                 self.stats["probe_ms_sum"] += float(res.get("ms", 0.0))
                 if not res.get("passed"):
                     self.stats["probe_failures"] += 1
-            self.ledger.commit(self.records)
+            # Probing -> Claimed may be lost by a crash (restart -> ProbeInterrupted -> replace)
+            self.ledger.commit(self.records, durable=False)
             self._evaluate_all()
+        self.ledger.flush(claim_seq)
         lap("commit2")
         self._ensure_plugin(resource)
         self._notify_plugins()

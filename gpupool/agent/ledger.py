@@ -1,9 +1,11 @@
 """Claim ledger: the node agent's durable record of which GPU belongs to which pool.
 
 All claims live in one JSON document (``<state>/ledger.json``: ``{"version": 1, "claims": {uuid:
-record}, "hbmSweep": {uuid: scrubber cursor/coverage}}``) that is replaced atomically (write temp -> fsync -> rename -> fsync dir) once per
-agent operation, so a claim of 8 GPUs costs one fsync, not eight, and a crash can never leave a
-half-written batch. GPUs that failed a probe are recorded in ``<state>/quarantine/<uuid>.json``.
+record}, "hbmSweep": {uuid: scrubber cursor/coverage}}``) that is replaced atomically (write temp
+-> fsync -> rename -> fsync dir), so a claim of 8 GPUs costs one fsync, not eight, and a crash can
+never leave a half-written batch. Commits that must be durable before the agent acts on them
+(claim, release) are flushed synchronously — the claim's while its probe runs; transitions a crash
+may safely lose (Probing -> Claimed) go through a coalescing background writer. GPUs that failed a probe are recorded in ``<state>/quarantine/<uuid>.json``.
 Together with ``status.devices`` on the pool this makes the operator stateless across restarts
 (SURVEY.md §5 checkpoint/resume row): on start the agent reloads the ledger, and the manager's
 orphan sweep releases claims whose pool UID is gone.
@@ -65,8 +67,23 @@ class Ledger:
         self.quar_dir = os.path.join(state_dir, "quarantine")
         os.makedirs(self.quar_dir, exist_ok=True)
         self.fsync = fsync
-        self._mu = threading.Lock()
+        self._mu = threading.Lock()      # guards the serialised sections + sequence numbers
+        self._wmu = threading.Lock()     # one writer at a time; the newest state wins
+        self._seq = 0                    # bumped by every commit
+        self._written = 0                # newest seq known to be on disk
+        self._lazy = threading.Event()
+        self._lazy_thread: threading.Thread | None = None
         self.writes = 0
+        # quarantine entries cached in memory (this process is the only writer): claims and node
+        # views consult them per GPU and must not rescan the directory each time
+        self._quar: dict[str, dict] = {}
+        for name in os.listdir(self.quar_dir):
+            try:
+                with open(os.path.join(self.quar_dir, name)) as f:
+                    rec = json.load(f)
+                self._quar[rec["uuid"]] = rec
+            except (OSError, ValueError, KeyError):
+                continue
         # serialised sections: each is rendered by its writer's thread (the claim map under the
         # agent lock), so a scrubber write never iterates a claim map another thread is editing
         self._claims_text = "{}"
@@ -93,54 +110,93 @@ class Ledger:
                         continue
         return claims
 
-    def commit(self, claims: dict[str, dict]) -> None:
-        """Persist the full claim map atomically (one write + one fsync per agent operation)."""
+    def commit(self, claims: dict[str, dict], durable: bool = True) -> int:
+        """Record the full claim map; returns its sequence number. ``durable``: written and
+        fsync'ed before returning (one write per agent operation, atomically replaced). Otherwise
+        the write is left to a background writer (coalesced) — for transitions a crash may lose
+        safely, e.g. Probing -> Claimed: a restarted agent turns a 'Probing' record into a failed
+        probe (ProbeInterrupted) and the pool replaces the GPU."""
         text = json.dumps(claims, sort_keys=True)
         with self._mu:
             self._claims_text = text
-            self._write_locked()
+            self._seq += 1
+            seq = self._seq
+        if durable:
+            self.flush(seq)
+        else:
+            self._kick_lazy()
+        return seq
+
+    def flush(self, upto: int | None = None) -> None:
+        """Make everything up to sequence ``upto`` (default: all) durable."""
+        with self._wmu:
+            with self._mu:
+                want = self._seq if upto is None else upto
+                if self._written >= want:
+                    return
+                seq = self._seq
+                text = '{"version": %d, "claims": %s, "hbmSweep": %s}' % (
+                    VERSION, self._claims_text, json.dumps(self._sweep, sort_keys=True))
+            _atomic_write_text(self.path, text, self.fsync)
+            self.writes += 1
+            with self._mu:
+                self._written = max(self._written, seq)
+
+    def _kick_lazy(self) -> None:
+        if self._lazy_thread is None:
+            self._lazy_thread = threading.Thread(target=self._lazy_loop, daemon=True,
+                                                 name="ledger-writer")
+            self._lazy_thread.start()
+        self._lazy.set()
+
+    def _lazy_loop(self) -> None:
+        while True:
+            self._lazy.wait()
+            self._lazy.clear()
+            try:
+                self.flush()
+            except OSError:
+                time.sleep(0.1)
+                self._lazy.set()
 
     def commit_sweep(self, sweep: dict[str, dict]) -> None:
         """Persist the HBM scrubber's per-device cursors/coverage (same document, same atomicity)."""
         with self._mu:
             self._sweep = {u: dict(r) for u, r in sweep.items()}
-            self._write_locked()
+            self._seq += 1
+            seq = self._seq
+        self.flush(seq)
 
     def sweep_state(self) -> dict[str, dict]:
         with self._mu:
             return {u: dict(r) for u, r in self._sweep.items()}
 
-    def _write_locked(self) -> None:
-        text = '{"version": %d, "claims": %s, "hbmSweep": %s}' % (
-            VERSION, self._claims_text, json.dumps(self._sweep, sort_keys=True))
-        _atomic_write_text(self.path, text, self.fsync)
-        self.writes += 1
-
     # ---------------------------------------------------------------- quarantine
     def quarantine(self, uuid: str, seconds: float, reason: str, maintenance: bool = False) -> None:
-        _atomic_write_text(os.path.join(self.quar_dir, _safe(uuid) + ".json"),
-                           json.dumps({"uuid": uuid, "until": time.time() + seconds,
-                                       "reason": reason, "maintenance": maintenance}), self.fsync)
+        rec = {"uuid": uuid, "until": time.time() + seconds, "reason": reason,
+               "maintenance": maintenance}
+        _atomic_write_text(os.path.join(self.quar_dir, _safe(uuid) + ".json"), json.dumps(rec),
+                           self.fsync)
+        with self._mu:
+            self._quar[uuid] = rec
 
     def quarantined(self) -> dict[str, dict]:
-        out, now = {}, time.time()
-        for name in os.listdir(self.quar_dir):
-            p = os.path.join(self.quar_dir, name)
+        now = time.time()
+        with self._mu:
+            expired = [u for u, r in self._quar.items() if r.get("until", 0) <= now]
+            for u in expired:
+                del self._quar[u]
+            out = dict(self._quar)
+        for u in expired:
             try:
-                with open(p) as f:
-                    rec = json.load(f)
-            except (OSError, ValueError):
-                continue
-            if rec.get("until", 0) > now:
-                out[rec["uuid"]] = rec
-            else:
-                try:
-                    os.remove(p)
-                except OSError:
-                    pass
+                os.remove(os.path.join(self.quar_dir, _safe(u) + ".json"))
+            except OSError:
+                pass
         return out
 
     def clear_quarantine(self, uuid: str) -> None:
+        with self._mu:
+            self._quar.pop(uuid, None)
         try:
             os.remove(os.path.join(self.quar_dir, _safe(uuid) + ".json"))
         except FileNotFoundError:

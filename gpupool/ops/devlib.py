@@ -29,6 +29,8 @@ def lib() -> ctypes.CDLL:
                 getattr(l, fn).argtypes = [ctypes.c_void_p, ctypes.c_int]
             l.mi355x_dev_evaluate.restype = ctypes.c_void_p
             l.mi355x_dev_evaluate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+            l.mi355x_dev_evaluate_batch.restype = ctypes.c_void_p
+            l.mi355x_dev_evaluate_batch.argtypes = [ctypes.c_char_p]
             l.mi355x_dev_select.restype = ctypes.c_void_p
             l.mi355x_dev_select.argtypes = [ctypes.c_char_p]
             l.mi355x_free.argtypes = [ctypes.c_void_p]
@@ -97,6 +99,17 @@ def evaluate(device: dict, baseline: dict | None, policy: dict | None) -> dict:
     return _take(lib().mi355x_dev_evaluate(json.dumps(device).encode(),
                                            json.dumps(baseline or {}).encode(),
                                            json.dumps(policy or {}).encode()))
+
+
+def evaluate_batch(items: list[tuple[dict, dict | None, dict | None]]) -> list[dict]:
+    """[(device, baseline or None, policy or None)] -> verdicts, in one native call."""
+    if not items:
+        return []
+    out = _take(lib().mi355x_dev_evaluate_batch(json.dumps(
+        [{"device": d, "baseline": b, "policy": p or {}} for d, b, p in items]).encode()))
+    if isinstance(out, dict) and "error" in out:
+        raise RuntimeError(out["error"])
+    return out
 
 
 def select(count: int, candidates: list[int], owned: list[int], policy: str,

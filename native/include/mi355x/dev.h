@@ -42,6 +42,10 @@ char* mi355x_dev_health_snapshot(mi355x_dev* d);
  * claim time: {"healthy","present","xgmiOk","eccOk","thermalOk","partitionOk","reasons":[...]} */
 char* mi355x_dev_evaluate(const char* device_json, const char* baseline_json, const char* policy_json);
 
+/* Many verdicts in one call: items [{"device", "baseline" (default: the device), "policy"}] ->
+ * [verdict, ...] in order (the agent evaluates every GPU on each health poll). */
+char* mi355x_dev_evaluate_batch(const char* items_json);
+
 /* Topology-aware all-or-nothing selection.
  * req: {"count":k,"candidates":[idx..],"owned":[idx..],"policy":"xgmi-packed"|"any",
  *       "weights":[[..]],"numa":[..]} -> {"selected":[idx..]} ("selected" empty if < k). */

@@ -149,6 +149,23 @@ char* mi355x_dev_evaluate(const char* device_json, const char* baseline_json, co
   }
 }
 
+char* mi355x_dev_evaluate_batch(const char* items_json) {
+  try {
+    Json items = Json::parse(items_json ? items_json : "[]");
+    Json out = Json::array();
+    const Json empty = Json::object();
+    for (const auto& it : items.elements()) {
+      const Json& base = it["baseline"].is_object() ? it["baseline"] : it["device"];
+      out.push_back(mi355x::evaluate(it["device"], base, it["policy"].is_object() ? it["policy"] : empty));
+    }
+    return dup(out.dump());
+  } catch (const std::exception& e) {
+    Json errj = Json::object();
+    errj["error"] = e.what();
+    return dup(errj.dump());
+  }
+}
+
 char* mi355x_dev_select(const char* request_json) {
   try {
     Json req = Json::parse(request_json ? request_json : "{}");
