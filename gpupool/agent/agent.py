@@ -668,9 +668,10 @@ class Agent:
             # the manager believe it owns GPUs a restarted agent would hand out again.
             claim_seq = self.ledger.commit(self.records, durable=False)
             self.stats["claims"] += len(chosen)
+        lap("commit")
         for d in chosen:  # an in-flight HBM scrub window finishes and hands its buffer back
             self.scrubber.yield_device(d["uuid"])
-        lap("commit")
+        lap("scrubYield")
         # probes run outside the lock, concurrently across GPUs
         t0 = time.perf_counter()
         results = self.prober.probe_many(chosen, {**probe_opts, "enabled":
@@ -706,8 +707,8 @@ class Agent:
         with self.lock:
             views = [self.device_view(d["uuid"], pods) for d in chosen]
         lap("view")
-        log.info("claimed %d GPU(s) for %s: %s (probe wall %.1f ms)", len(chosen),
-                 req.get("pool"), [d["index"] for d in chosen], probe_wall)
+        log.info("claimed %d GPU(s) for %s: %s (probe wall %.1f ms; phases %s)", len(chosen),
+                 req.get("pool"), [d["index"] for d in chosen], probe_wall, timings)
         return {"ok": True, "devices": views, "probeWallMs": probe_wall, "timingsMs": timings}
 
     def _xgmi_check(self, pool_uid: str, chosen: list[dict], results: list[dict],

@@ -14,8 +14,10 @@ Claims always win: the scrubber re-checks eligibility under a per-device lock be
 and ``yield_device`` (called by the claim path after the ledger commit) only waits for an in-flight
 window. The big buffer is allocated and freed outside every lock a claim takes (~282 GiB on
 MI355X: 0.2 s to allocate fresh, ~6 s once the driver has to clear previously used VRAM, ~2.5 s to
-free; profiles/r2h_sweep_claim_diag.txt). The claim-time probe arena is allocated first and kept
-while the sweep runs and for 30 s after its free, so a claim-time probe never allocates behind the
+free; profiles/r2h_sweep_claim_diag.txt), in 4 GiB chunks: one huge mapping's unmap held the
+process's address-space lock for ~2.5 s and stalled any claim thread that mapped memory meanwhile
+(profiles/r2o_scrub_claim_diag.txt). The claim-time probe arena is allocated first and kept while
+the sweep runs and for 30 s after its free, so a claim-time probe never allocates behind the
 driver's clear (a probe issued during the free or the allocation measured 1.1-1.3 ms); the device
 plugin's Allocate waits for the free (``wait_released``) so a pod never starts beside the buffer.
 
@@ -114,6 +116,7 @@ class HbmScrubber:
         """Allocate the sweep buffer (inproc: ~0.4 s for ~282 GiB) without any lock a claim takes."""
         with self._cv:
             self._held.add(uuid)
+        t0 = time.perf_counter()
         if self.agent.prober.mode == "inproc":
             o = self._ordinal(uuid)
             # The claim-time probe arena comes first: a claim then never has to allocate while the
@@ -123,16 +126,21 @@ class HbmScrubber:
             if o is None or self.agent.prober._hip.sweep_alloc(o, self.reserve_bytes) < 0:
                 self._release(uuid)
                 return False
+            log.info("HBM sweep buffer of %s allocated in %.1f ms", uuid,
+                     (time.perf_counter() - t0) * 1e3)
         return True
 
     def _release(self, uuid: str) -> None:
-        """Free the sweep buffer (inproc: ~2.9 s for ~282 GiB, the driver clears released VRAM)."""
+        """Free the sweep buffer (inproc: ~2.5 s for ~282 GiB, the driver clears released VRAM)."""
+        t0 = time.perf_counter()
         try:
             if self.agent.prober.mode == "inproc":
                 o = self._ordinal(uuid)
                 if o is not None:
                     self.agent.prober._hip.sweep_release(o)
         finally:
+            log.info("HBM sweep buffer of %s released in %.1f ms", uuid,
+                     (time.perf_counter() - t0) * 1e3)
             with self._cv:
                 self._held.discard(uuid)
                 self._cv.notify_all()

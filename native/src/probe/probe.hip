@@ -583,6 +583,19 @@ constexpr int kSlotSmall = 2 * kMaxPatterns, kSlotAbft = kSlotSmall + 1, kSlotCe
               kResSlots = kSlotGemmMap + kCuMapWords;
 constexpr int kCensusIters = 128;
 
+// The HBM sweep buffer is allocated as kSweepChunk pieces, not one ~282 GiB allocation: freeing
+// one huge mapping held the process's address-space lock for ~2.5 s, and every thread of the agent
+// that mapped memory meanwhile (a thread start, a large malloc) stalled behind it — a claim issued
+// right after a scrub waited 2.46 s (profiles/r2o_scrub_claim_diag.txt). Per chunk the stall is
+// bounded by one 4 GiB unmap.
+constexpr uint64_t kSweepChunk = 4ull << 30;
+
+struct SweepBuf {
+  std::vector<void*> chunks;  // kSweepChunk bytes each, the last one possibly shorter
+  uint64_t span = 0;
+  bool empty() const { return chunks.empty(); }
+};
+
 struct DeviceCtx {
   hipStream_t stream = nullptr;   // HBM pattern test
   hipStream_t stream2 = nullptr;  // MFMA checks, overlapped with the bandwidth-bound HBM test
@@ -596,8 +609,7 @@ struct DeviceCtx {
   size_t arena_bytes = 0;
   std::chrono::steady_clock::time_point arena_used{};
   // HBM sweep buffer (mi355x_probe_hbm_sweep): nearly all free HBM, held only for a scrub pass
-  void* sweep = nullptr;
-  size_t sweep_bytes = 0;
+  SweepBuf sweep;
   unsigned long long* sweep_cnt = nullptr;
   // Freed VRAM is cleared by the driver before it is handed out again (~6 s for ~282 GiB measured,
   // profiles/r2h_sweep_claim_diag.txt): an arena hipMalloc issued in that window waits for it. The
@@ -1025,19 +1037,34 @@ std::string run_peer(int src, int dst, const char* opts) {
          ",\"bytes\":" + std::to_string(n16 * 16) + ",\"GBps\":" + jnum(gbps) + ",\"ms\":" + jnum(ms) + "}";
 }
 
-// All free HBM minus ``reserve``, 2 MiB granular. Measured on MI355X (profiles/r2g): ~0.4 s to
-// allocate ~282 GiB and ~2.9 s to free it (the driver clears released VRAM), so neither ever runs
-// under the device lock a claim-time probe takes.
-void* sweep_alloc_raw(uint64_t reserve, size_t* span_out) {
+// All free HBM minus ``reserve``, 2 MiB granular, as kSweepChunk pieces. Measured on MI355X
+// (profiles/r2h_sweep_claim_diag.txt): ~0.2 s to allocate ~282 GiB of fresh VRAM, ~6 s once the
+// driver must clear previously used VRAM; neither runs under the device lock a probe takes.
+SweepBuf sweep_alloc_raw(uint64_t reserve) {
   size_t free_b = 0, total_b = 0;
   PROBE_CHECK(hipMemGetInfo(&free_b, &total_b));
   const uint64_t gran = 2ull << 20;
   if (free_b <= reserve + gran) throw ProbeError("not enough free HBM for a sweep window");
+  SweepBuf b;
   const uint64_t span = ((free_b - reserve) / gran) * gran;
-  void* p = nullptr;
-  PROBE_CHECK(hipMalloc(&p, span));
-  *span_out = span;
-  return p;
+  for (uint64_t at = 0; at < span; at += kSweepChunk) {
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, std::min<uint64_t>(kSweepChunk, span - at));
+    if (e != hipSuccess) {
+      for (void* q : b.chunks) (void)hipFree(q);
+      (void)hipGetLastError();
+      throw ProbeError(std::string("sweep chunk hipMalloc: ") + hipGetErrorString(e));
+    }
+    b.chunks.push_back(p);
+  }
+  b.span = span;
+  return b;
+}
+
+void sweep_free(SweepBuf& b) {
+  for (void* p : b.chunks) (void)hipFree(p);  // one bounded unmap per chunk
+  b.chunks.clear();
+  b.span = 0;
 }
 
 // One window of the rotating HBM sweep (see mi355x_probe_hbm_sweep in probe.h). The claim-time
@@ -1055,50 +1082,57 @@ std::string run_sweep(int dev, const char* opts) {
   PROBE_CHECK(hipSetDevice(dev));
   auto t0 = std::chrono::steady_clock::now();
   double alloc_ms = 0;
-  if (!ctx.sweep) {  // normally pre-allocated by mi355x_probe_sweep_alloc outside the device lock
-    size_t span = 0;
-    ctx.sweep = sweep_alloc_raw(reserve, &span);
-    ctx.sweep_bytes = span;
+  if (ctx.sweep.empty()) {  // normally pre-allocated by mi355x_probe_sweep_alloc outside the device lock
+    ctx.sweep = sweep_alloc_raw(reserve);
     alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
-  const uint64_t span = ctx.sweep_bytes;
+  const uint64_t span = ctx.sweep.span;
   const uint64_t offset = (offset_in % span) & ~static_cast<uint64_t>(15);
   const uint64_t bytes = std::min<uint64_t>(want, span - offset) & ~static_cast<uint64_t>(15);
-  const uint64_t n16 = bytes / 16;
-  auto* win = reinterpret_cast<u32x4*>(static_cast<char*>(ctx.sweep) + offset);
   if (!ctx.sweep_cnt) PROBE_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx.sweep_cnt), 4 * sizeof(unsigned long long)));
   unsigned long long* cnt = ctx.sweep_cnt;
   hipStream_t s = ctx.stream;
   const int cus = ctx.prop.multiProcessorCount;
-  const int fill_grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(cus), (n16 + kHbmThreads - 1) / kHbmThreads));
-  const int verify_grid = static_cast<int>(std::min<uint64_t>(3ull * cus, (n16 + kHbmThreads - 1) / kHbmThreads));
-  const uint32_t seed = 0x5CAB0000u ^ static_cast<uint32_t>(offset >> 20);
-  PROBE_CHECK(hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned long long), s));
-  PROBE_CHECK(hipMemsetAsync(cnt + 1, 0xFF, sizeof(unsigned long long), s));
-  PROBE_CHECK(hipMemsetAsync(cnt + 3, 0xFF, sizeof(unsigned long long), s));
-  PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
-  for (int pi = 0; pi < 2; ++pi) {
-    const uint32_t flip = pi ? 0xFFFFFFFFu : 0u;
-    hipLaunchKernelGGL(hbm_fill, dim3(fill_grid), dim3(kHbmThreads), 0, s, win, n16, seed, flip);
-    if (pi == 0 && inject_flips > 0)
-      hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(win), n16 * 4,
-                         inject_flips);
-    hipLaunchKernelGGL(hbm_verify, dim3(verify_grid), dim3(kHbmThreads), 0, s, static_cast<const u32x4*>(win), n16, seed,
-                       flip, cnt + 2 * pi, cnt + 2 * pi + 1);
-  }
-  PROBE_CHECK(hipEventRecord(ctx.ev[1], s));
-  PROBE_CHECK(hipGetLastError());
-  PROBE_CHECK(hipMemcpyAsync(ctx.host_res, cnt, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-  PROBE_CHECK(hipStreamSynchronize(s));
+  unsigned long long bad = 0, first = ~0ull;
   float ms = 0;
-  PROBE_CHECK(hipEventElapsedTime(&ms, ctx.ev[0], ctx.ev[1]));
-  const unsigned long long bad = ctx.host_res[0] + ctx.host_res[2];
-  const unsigned long long first = std::min(ctx.host_res[1], ctx.host_res[3]);
-  if (!keep) {
-    (void)hipFree(ctx.sweep);
-    ctx.sweep = nullptr;
-    ctx.sweep_bytes = 0;
+  // the window may straddle chunks: test it piece by piece (both polarities per piece)
+  for (uint64_t pos = offset; pos < offset + bytes;) {
+    const size_t ci = static_cast<size_t>(pos / kSweepChunk);
+    const uint64_t in = pos % kSweepChunk;
+    const uint64_t clen = std::min<uint64_t>(kSweepChunk, span - ci * kSweepChunk);
+    const uint64_t n = std::min<uint64_t>(offset + bytes - pos, clen - in) & ~static_cast<uint64_t>(15);
+    if (n == 0) break;
+    const uint64_t n16 = n / 16;
+    auto* win = reinterpret_cast<u32x4*>(static_cast<char*>(ctx.sweep.chunks[ci]) + in);
+    const int fill_grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(cus), (n16 + kHbmThreads - 1) / kHbmThreads));
+    const int verify_grid = static_cast<int>(std::min<uint64_t>(3ull * cus, (n16 + kHbmThreads - 1) / kHbmThreads));
+    const uint32_t seed = 0x5CAB0000u ^ static_cast<uint32_t>(pos >> 20);
+    PROBE_CHECK(hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned long long), s));
+    PROBE_CHECK(hipMemsetAsync(cnt + 1, 0xFF, sizeof(unsigned long long), s));
+    PROBE_CHECK(hipMemsetAsync(cnt + 3, 0xFF, sizeof(unsigned long long), s));
+    PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
+    for (int pi = 0; pi < 2; ++pi) {
+      const uint32_t flip = pi ? 0xFFFFFFFFu : 0u;
+      hipLaunchKernelGGL(hbm_fill, dim3(fill_grid), dim3(kHbmThreads), 0, s, win, n16, seed, flip);
+      if (pi == 0 && inject_flips > 0 && pos == offset)
+        hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(win), n16 * 4,
+                           inject_flips);
+      hipLaunchKernelGGL(hbm_verify, dim3(verify_grid), dim3(kHbmThreads), 0, s, static_cast<const u32x4*>(win), n16,
+                         seed, flip, cnt + 2 * pi, cnt + 2 * pi + 1);
+    }
+    PROBE_CHECK(hipEventRecord(ctx.ev[1], s));
+    PROBE_CHECK(hipGetLastError());
+    PROBE_CHECK(hipMemcpyAsync(ctx.host_res, cnt, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    PROBE_CHECK(hipStreamSynchronize(s));
+    float piece_ms = 0;
+    PROBE_CHECK(hipEventElapsedTime(&piece_ms, ctx.ev[0], ctx.ev[1]));
+    ms += piece_ms;
+    bad += ctx.host_res[0] + ctx.host_res[2];
+    const unsigned long long f = std::min(ctx.host_res[1], ctx.host_res[3]);
+    if (f != ~0ull) first = std::min(first, (pos - offset) / 16 + f);
+    pos += n;
   }
+  if (!keep) sweep_free(ctx.sweep);
   const double gbps = ms > 0 ? 4.0 * static_cast<double>(bytes) / (ms * 1e-3) / 1e9 : 0.0;
   return "{\"device\":" + std::to_string(dev) + ",\"passed\":" + (bad == 0 ? "true" : "false") +
          ",\"offset\":" + std::to_string(offset) + ",\"bytes\":" + std::to_string(bytes) +
@@ -1189,7 +1223,7 @@ int mi355x_probe_trim(int idle_ms) {
     std::lock_guard<std::mutex> g(device_mutex(d));
     DeviceCtx& ctx = g_ctx[static_cast<size_t>(d)];
     if (!ctx.arena || now - ctx.arena_used < std::chrono::milliseconds(idle_ms)) continue;
-    if (idle_ms > 0 && (ctx.sweep || now - ctx.sweep_released < kSweepClearGrace)) continue;  // 0 = forced
+    if (idle_ms > 0 && (!ctx.sweep.empty() || now - ctx.sweep_released < kSweepClearGrace)) continue;  // 0 = forced
     if (hipSetDevice(d) != hipSuccess) continue;
     (void)hipFree(ctx.arena);
     ctx.arena = nullptr;
@@ -1214,42 +1248,39 @@ int mi355x_probe_sweep_alloc(int dev, long long reserve) {
   if (g_count < 0 || dev < 0 || dev >= g_count) return -1;
   {
     std::lock_guard<std::mutex> g(device_mutex(dev));
-    if (g_ctx[static_cast<size_t>(dev)].sweep) return 0;
+    if (!g_ctx[static_cast<size_t>(dev)].sweep.empty()) return 0;
   }
-  void* p = nullptr;
-  size_t span = 0;
+  SweepBuf b;
   try {
     if (hipSetDevice(dev) != hipSuccess) return -1;
-    p = sweep_alloc_raw(static_cast<uint64_t>(std::max(0LL, reserve)), &span);
+    b = sweep_alloc_raw(static_cast<uint64_t>(std::max(0LL, reserve)));
   } catch (const std::exception&) {
     (void)hipGetLastError();
     return -2;
   }
   std::lock_guard<std::mutex> g(device_mutex(dev));
   DeviceCtx& ctx = g_ctx[static_cast<size_t>(dev)];
-  if (ctx.sweep) {  // lost a race with another allocator: keep theirs
-    (void)hipFree(p);
+  if (!ctx.sweep.empty()) {  // lost a race with another allocator: keep theirs
+    sweep_free(b);
     return 0;
   }
-  ctx.sweep = p;
-  ctx.sweep_bytes = span;
+  ctx.sweep = std::move(b);
   return 1;
 }
 
 int mi355x_probe_sweep_release(int dev) {
   if (g_count < 0 || dev < 0 || dev >= g_count) return -1;
-  void* p = nullptr;
+  SweepBuf b;
   {
     std::lock_guard<std::mutex> g(device_mutex(dev));
     DeviceCtx& ctx = g_ctx[static_cast<size_t>(dev)];
-    p = ctx.sweep;
-    ctx.sweep = nullptr;
-    ctx.sweep_bytes = 0;
+    b = std::move(ctx.sweep);
+    ctx.sweep = SweepBuf{};
     ctx.sweep_released = std::chrono::steady_clock::now();
   }
-  if (!p) return 0;
+  if (b.empty()) return 0;
   if (hipSetDevice(dev) != hipSuccess) return -1;
-  (void)hipFree(p);  // seconds for ~280 GB: outside the device lock
+  sweep_free(b);  // outside the device lock, chunk by chunk
   return 1;
 }
 
