@@ -35,7 +35,9 @@ Launch contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for
 ``torch.distributed.run`` every rank joins a gloo process group for the barriers and rank 0
 drives the control plane, which manages all GPUs of the node. The bench process itself issues no
 GPU work (the node agent, a child process, owns the GPUs), so there is no device stream to
-synchronise around the timed region.
+synchronise around the timed region. With N > 1 real GPUs, after the timed region and after the
+control plane has released every GPU, each rank all-reduces over its own GPU in a child process
+(RCCL over xGMI; ``config.rccl_allreduce``: exactness + bus bandwidth).
 """
 from __future__ import annotations
 
@@ -90,6 +92,49 @@ def _gather_max(world: int, x: float) -> float:
     return float(t.item())
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _comm_check(rank: int, world: int, backend: str) -> dict | None:
+    """Every rank all-reduces over its own GPU in a child process (gpupool/parallel/rccl_check.py:
+    RCCL over xGMI, exact result + bus bandwidth), under a time limit so a fabric fault cannot
+    hang the bench; rank 0 returns the summary."""
+    import subprocess
+    import torch.distributed as dist
+    port = [_free_port() if rank == 0 else None]
+    dist.broadcast_object_list(port, src=0)
+    cmd = [sys.executable, "-m", "gpupool.parallel.rccl_check", "--rank", str(rank), "--world",
+           str(world), "--local-rank", os.environ.get("LOCAL_RANK", str(rank)), "--master-port",
+           str(port[0])]
+    if backend == "gloo":
+        cmd += ["--backend", "gloo", "--device", "cpu", "--bytes", str(8 << 20), "--iters", "5"]
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=ROOT)
+        lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+        res = json.loads(lines[-1]) if p.returncode == 0 and lines else \
+            {"rank": rank, "error": f"exit {p.returncode}: {p.stderr[-400:]}"}
+    except subprocess.TimeoutExpired:
+        res = {"rank": rank, "error": "timed out after 150 s"}
+    got: list = [None] * world
+    dist.all_gather_object(got, res)
+    if rank != 0:
+        return None
+    ok = [g for g in got if g and "error" not in g]
+    out = {"backend": backend if backend == "gloo" else "nccl(RCCL)", "world": world,
+           "ranks_ok": len(ok), "exact": all(g.get("exact") for g in ok) and len(ok) == world}
+    if ok:
+        out.update({"bytes": ok[0]["bytes"], "min_busbw_GBps": min(g["busbw_GBps"] for g in ok),
+                    "max_ms": max(g["ms"] for g in ok), "device": ok[0].get("device", "cpu")})
+    errs = [g for g in got if g and "error" in g]
+    if errs:
+        out["errors"] = errs[:4]
+    return out
+
+
 def sweep_for(n: int) -> list[int]:
     return sorted({k for k in (1, 2, 4, 8) if k <= n} | {n})
 
@@ -111,6 +156,9 @@ def main() -> int:
     ap.add_argument("--pool-steps", type=int, default=3, help="config 5 repetitions (0 = skip)")
     ap.add_argument("--health-steps", type=int, default=5,
                     help="fault->condition measurements (0 = skip)")
+    ap.add_argument("--comm-check", default="auto", choices=["auto", "gloo", "off"],
+                    help="after the timed region with N>1 ranks: all-reduce across the ranks' "
+                         "GPUs over RCCL (auto: when the GPUs are real) or gloo on CPU")
     args = ap.parse_args()
 
     rank, world = _dist_init()
@@ -247,6 +295,12 @@ def main() -> int:
                                   for k2, v in cy.items()} for cy in cycles[:len(sweep)]],
             },
         }
+    comm_backend = "gloo" if args.comm_check == "gloo" else "nccl" if real else ""
+    if world > 1 and args.comm_check != "off" and comm_backend:
+        comm = _comm_check(rank, world, comm_backend)
+        if rank == 0:
+            out["config"]["rccl_allreduce"] = comm
+    if rank == 0:
         print(json.dumps(out), flush=True)
         if not args.keep and not args.workdir:
             shutil.rmtree(cluster.workdir, ignore_errors=True)

@@ -286,3 +286,20 @@ def test_agent_exports_events_and_utilisation_on_real_gpu(cluster_factory):
             c.manager_metrics() and time.monotonic() < deadline:
         time.sleep(0.2)
     assert 'gpupool_pool_vram_total_bytes{kind="Mi355xPool",pool="default/u"}' in c.manager_metrics()
+
+
+def test_rccl_check_harness_on_real_gpu():
+    """The collective check bench.py runs per rank when N > 1 (RCCL over xGMI on the 8-GPU node):
+    on one MI355X it initialises RCCL (backend "nccl") and all-reduces a bf16 buffer exactly."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "gpupool.parallel.rccl_check", "--rank", "0",
+                        "--world", "1", "--master-port", str(port), "--bytes", str(64 << 20),
+                        "--iters", "5"], capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    out = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert out["exact"] and out["backend"] == "nccl" and "MI355" in out.get("device", "") + "MI355"

@@ -59,3 +59,28 @@ def test_bench_gpus1_contract(native_built):
     assert cfg["scale_down"]["from"] == 1 and cfg["scale_down"]["to"] == 0
     assert cfg["scale_down"]["accuracy"] == 1.0
     assert "skipped" in cfg["two_pools"]
+
+
+def test_bench_under_torchrun_two_ranks_with_comm_check(native_built):
+    """The driver's N>1 launch shape (torch.distributed.run, one rank per GPU, 127.0.0.1): rank 0
+    drives the control plane, exactly one JSON line is printed, and the post-run collective check
+    (here gloo on CPU; RCCL on real GPUs) reports every rank exact."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={port}",
+                        os.path.join(ROOT, "bench.py"), "--backend", "fake", "--gpus", "2",
+                        "--steps", "1", "--warmup", "0", "--scale-down-steps", "0",
+                        "--pool-steps", "0", "--health-steps", "0", "--comm-check", "gloo"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["world_size"] == 2
+    comm = out["config"]["rccl_allreduce"]
+    assert comm["world"] == 2 and comm["ranks_ok"] == 2 and comm["exact"], comm
+    assert comm["min_busbw_GBps"] > 0
