@@ -598,12 +598,21 @@ class Agent:
                 "powerW": pw.get("socketW"), "memUsedBytes": d.get("memUsedBytes"),
                 "memTotalBytes": d.get("memTotalBytes")}
 
-    def node_view(self) -> dict:
+    def node_view(self, pool_uid: str = "") -> dict:
+        """The node's devices; with ``pool_uid`` only that pool's GPUs plus ``freeHealthy`` (the
+        count the manager needs to plan, without serialising every other GPU on every observe)."""
         pods = self._pods_by_device()
         with self.lock:
             uuids = list(self.by_uuid) + [u for u in self.records if u not in self.by_uuid]
+            extra = {}
+            if pool_uid:
+                quarantined = self.ledger.quarantined()
+                extra["freeHealthy"] = sum(
+                    1 for u in self.by_uuid if u not in self.records and u not in quarantined and
+                    self.verdicts.get(u, {}).get("healthy"))
+                uuids = [u for u in uuids if (self.records.get(u) or {}).get("poolUID") == pool_uid]
             devices = [self.device_view(u, pods) for u in uuids]
-            return {"node": self.cfg.node, "backend": self.backend, "gen": self.gen,
+            return {"node": self.cfg.node, "backend": self.backend, "gen": self.gen, **extra,
                     "probeMode": self.probe_mode, "preflight": self.preflight,
                     "advertiseRequired": bool(self.cfg.plugin_dir),
                     "eventSources": dict(self.events_supported),
@@ -1131,7 +1140,7 @@ def build_app(agent: Agent) -> web.Application:
     async def node(request):
         # served on the event loop: node_view never blocks on I/O (cached pod map), and skipping
         # the executor hop saves a thread wake-up on every reconcile's observe
-        return web.json_response(agent.node_view())
+        return web.json_response(agent.node_view(request.query.get("pool", "")))
 
     async def claims(request):
         body = await request.json()

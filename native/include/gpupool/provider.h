@@ -117,6 +117,7 @@ struct NodeView {
   bool advertise_required = true;
   std::vector<DeviceView> devices;
   int64_t gen = 0;
+  int64_t free_healthy = -1;  // pool-scoped views: the agent's count of free healthy GPUs
 };
 
 struct ClaimRequest {
@@ -140,6 +141,9 @@ class DeviceProvider {
   virtual std::vector<std::string> node_names() = 0;
   virtual Json node_labels(const std::string& node) = 0;
   virtual NodeView observe(const std::string& node) = 0;
+  // Only ``pool_uid``'s GPUs plus the node's free-healthy count (smaller, cheaper answer for the
+  // reconcile path). Default: the full view.
+  virtual NodeView observe_pool(const std::string& node, const std::string& /*pool_uid*/) { return observe(node); }
   virtual ClaimResult claim(const std::string& node, const ClaimRequest& req) = 0;
   virtual void cordon(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) = 0;
   virtual void release(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) = 0;
@@ -156,6 +160,7 @@ class RocmProvider : public DeviceProvider {
   std::vector<std::string> node_names() override;
   Json node_labels(const std::string& node) override;
   NodeView observe(const std::string& node) override;
+  NodeView observe_pool(const std::string& node, const std::string& pool_uid) override;
   ClaimResult claim(const std::string& node, const ClaimRequest& req) override;
   void cordon(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) override;
   void release(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) override;

@@ -235,7 +235,7 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
     if (nodes.empty()) nodes = provider_.node_names();
   }
   for (const auto& n : nodes) {
-    NodeView nv = provider_.observe(n);
+    NodeView nv = provider_.observe_pool(n, m.uid);
     if (!nv.reachable) {
       if (hinted.count(n) || n == spec.node_name) {
         o.reachable = false;
@@ -250,6 +250,7 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
       if (d.pool_uid == m.uid) mine.push_back(d);
       else if (d.state == "Free" && d.healthy) ++free_healthy;
     }
+    if (nv.free_healthy >= 0) free_healthy = nv.free_healthy;  // pool-scoped view
     o.free_by_node[n] = free_healthy;
     if (span_nodes) {
       for (auto& d : mine) o.mine.push_back(std::move(d));

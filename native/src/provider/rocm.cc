@@ -137,20 +137,23 @@ Json RocmProvider::post_(const std::string& node, const std::string& path, const
   return j ? *j : Json::object();
 }
 
-NodeView RocmProvider::observe(const std::string& node) {
+NodeView RocmProvider::observe(const std::string& node) { return observe_pool(node, ""); }
+
+NodeView RocmProvider::observe_pool(const std::string& node, const std::string& pool_uid) {
   NodeView nv;
   nv.name = node;
   nv.endpoint = endpoint_of(node);
   trace::Span span("agent:GET /v1/node");
   try {
     std::shared_ptr<HttpClient> c = client_for(node);
-    HttpResponse r = c->request("GET", "/v1/node");
+    HttpResponse r = c->request("GET", pool_uid.empty() ? "/v1/node" : "/v1/node?pool=" + pool_uid);
     if (r.status >= 400) throw ProviderError("AgentError", "GET /v1/node: HTTP " + std::to_string(r.status));
     Json j = Json::parse(r.body);
     nv.reachable = true;
     nv.backend = j["backend"].as_string();
     nv.gen = j["gen"].as_int(0);
     nv.advertise_required = j["advertiseRequired"].as_bool(true);
+    nv.free_healthy = j["freeHealthy"].as_int(-1);
     for (const auto& d : j["devices"].elements()) {
       DeviceView v = DeviceView::from(d);
       if (v.node.empty()) v.node = node;
