@@ -87,3 +87,70 @@ def test_random_edits_and_faults_converge(shared, ops, final):
         k.delete(MI355XPOOLS, name, ns)
     for name in ("pa", "pb"):
         k.wait_for(MI355XPOOLS, name, ns, lambda o: o is None, timeout=30)
+
+
+span_op = st.one_of(
+    st.tuples(st.just("scale"), st.sampled_from(["sa", "sb"]), st.integers(0, 6)),
+    st.tuples(st.just("fault"), st.sampled_from(["node-a", "node-b"]), st.integers(0, 3)),
+    st.tuples(st.just("clear"), st.just(""), st.just(0)),
+)
+
+
+@pytest.fixture(scope="module")
+def two_nodes(tmp_path_factory, native_built):
+    c = Cluster(str(tmp_path_factory.mktemp("prop2")),
+                nodes=[NodeSpec(n, count=4, extra_args=["--quarantine", "0.3"])
+                       for n in ("node-a", "node-b")],
+                sample_interval=0.2)
+    c.start()
+    yield c
+    c.stop()
+
+
+@settings(max_examples=6, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
+                                                                 HealthCheck.too_slow])
+@given(ops=st.lists(span_op, min_size=1, max_size=6),
+       final=st.tuples(st.integers(0, 5), st.integers(0, 3)))
+def test_spanning_pools_converge(two_nodes, ops, final):
+    """Two pools with spec.maxNodes=2 over two 4-GPU nodes under random edits and ECC faults:
+    once faults clear, both are Ready at their final size (sum <= 8), never share a GPU, hold GPUs
+    on at most 2 nodes, and the two agents' claims are exactly the union of the pools' devices."""
+    c = two_nodes
+    k = c.client
+    ns = f"s{int(time.time() * 1e6) % 10**9}"
+    k.create(MI355XPOOLS, mi_pool("sa", 1, maxNodes=2, resourceName="amd.com/gpu-sa"), ns)
+    k.create(MI355XPOOLS, mi_pool("sb", 1, maxNodes=2, resourceName="amd.com/gpu-sb"), ns)
+    faults: dict = {"node-a": {}, "node-b": {}}
+    for kind, a, b in ops:
+        if kind == "scale":
+            k.patch(MI355XPOOLS, a, {"spec": {"replicas": b}}, ns)
+        elif kind == "fault":
+            faults[a][str(b)] = FAULTS["ecc"]
+            c.set_faults(a, {"devices": faults[a]})
+        else:
+            faults = {"node-a": {}, "node-b": {}}
+            for n in faults:
+                c.set_faults(n, {})
+        time.sleep(0.05)
+    for n in ("node-a", "node-b"):
+        c.set_faults(n, {})
+    ra, rb = final
+    k.patch(MI355XPOOLS, "sa", {"spec": {"replicas": ra}}, ns)
+    k.patch(MI355XPOOLS, "sb", {"spec": {"replicas": rb}}, ns)
+    a = k.wait_for(MI355XPOOLS, "sa", ns, ready_at(ra), timeout=90)
+    b = k.wait_for(MI355XPOOLS, "sb", ns, ready_at(rb), timeout=90)
+    ua = {d["uuid"] for d in a["status"]["devices"]}
+    ub = {d["uuid"] for d in b["status"]["devices"]}
+    assert not ua & ub
+    for o in (a, b):
+        assert len({d["node"] for d in o["status"]["devices"]}) <= 2
+    claimed = set()
+    for n in ("node-a", "node-b"):
+        view = c.agent_request(n, "GET", "/v1/node")
+        claimed |= {d["uuid"] for d in view["devices"] if d.get("poolUID") in
+                    (a["metadata"]["uid"], b["metadata"]["uid"])}
+    assert claimed == ua | ub
+    for name in ("sa", "sb"):
+        k.delete(MI355XPOOLS, name, ns)
+    for name in ("sa", "sb"):
+        k.wait_for(MI355XPOOLS, name, ns, lambda o: o is None, timeout=30)
