@@ -334,12 +334,25 @@ def cmd_devices(c: Client, ns: str, args) -> int:
     if args.output in ("json", "yaml"):
         dump(view, args.output)
         return 0
-    print(f"node {view['node']}  backend {view['backend']}  probe {view.get('probeMode')}")
-    print(f"{'IDX':<4}{'HIP UUID':<24}{'BDF':<15}{'STATE':<12}{'HEALTHY':<8}{'POOL':<28}REASONS")
+    src = view.get("eventSources") or {}
+    print(f"node {view['node']}  backend {view['backend']}  probe {view.get('probeMode')}  "
+          f"events {','.join(k for k, v in sorted(src.items()) if v) or '-'}")
+    print(f"{'IDX':<4}{'HIP UUID':<24}{'BDF':<15}{'PART':<5}{'STATE':<12}{'HEALTHY':<8}{'GFX%':<5}"
+          f"{'VRAM(GiB)':<11}{'POWER':<7}{'POOL':<24}REASONS")
     for d in sorted(view["devices"], key=lambda x: x.get("index", 0)):
+        t = d.get("telemetry") or {}
+        used, total = t.get("memUsedBytes"), t.get("memTotalBytes")
+        vram = f"{used / 2**30:.0f}/{total / 2**30:.0f}" if used is not None and total else "-"
+        gfx = "-" if t.get("gfxActivity") is None else str(t["gfxActivity"])
+        power = "-" if t.get("powerW") is None else f"{t['powerW']}W"
         print(f"{d.get('index', ''):<4}{d.get('hipUUID', ''):<24}{d.get('bdf', ''):<15}"
-              f"{d.get('state', ''):<12}{'yes' if d.get('healthy') else 'NO':<8}"
-              f"{d.get('pool', '') or '-':<28}{'; '.join((d.get('verdict') or {}).get('reasons', []))}")
+              f"{(d.get('partition') or {}).get('compute', '-'):<5}"
+              f"{d.get('state', ''):<12}{'yes' if d.get('healthy') else 'NO':<8}{gfx:<5}{vram:<11}"
+              f"{power:<7}{d.get('pool', '') or '-':<24}"
+              f"{'; '.join((d.get('verdict') or {}).get('reasons', []))}")
+    for e in view.get("recentEvents") or []:
+        print(f"event {e.get('at', '')} {e.get('source', '')} {e.get('type', '')} "
+              f"gpu={e.get('index', '-')} {e.get('message', '')}".rstrip())
     return 0
 
 

@@ -263,6 +263,14 @@ def test_utilisation_metrics_agent_and_pool(cluster_factory):
     assert pool_gauge(m, "gpupool_pool_vram_total_bytes") == want
     assert pool_gauge(m, "gpupool_pool_power_watts") == 2 * 262
     assert pool_gauge(m, "gpupool_pool_gfx_activity_percent") == 0
+    # gpuctl devices: partition, utilisation, VRAM, power and the event sources per GPU
+    import subprocess
+    r = subprocess.run([os.path.join(ROOT, "bin", "gpuctl"), "--server", c.url, "devices",
+                        "mi355x-node-0"], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, GPUPOOL_AGENT_TOKEN=c.agent_token))
+    assert r.returncode == 0, r.stderr
+    assert "events faultOverlay" in r.stdout and "GFX%" in r.stdout
+    assert "0/288" in r.stdout and "262W" in r.stdout and "default/util" in r.stdout
     dash = json.load(open(os.path.join(ROOT, "config", "prometheus", "grafana-dashboard.json")))
     exprs = " ".join(t["expr"] for p in dash["panels"] for t in p.get("targets", []))
     for name in ("gpupool_pool_gfx_activity_percent", "gpupool_device_vram_used_bytes",
