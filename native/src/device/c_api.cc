@@ -218,18 +218,26 @@ char* mi355x_dev_wait_faults(mi355x_dev* d, int timeout_ms) {
       return dup(out.dump());
     }
   }
-  struct pollfd pfd {d->ino_fd, POLLIN, 0};
-  if (poll(&pfd, 1, timeout_ms) > 0 && (pfd.revents & POLLIN)) {
+  // other files of the directory (e.g. the writer's temp file) wake the poll too: keep waiting
+  // for the overlay itself until the deadline
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  bool changed = false;
+  while (!changed) {
+    const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
+    if (left.count() < 0) break;
+    struct pollfd pfd {d->ino_fd, POLLIN, 0};
+    if (poll(&pfd, 1, static_cast<int>(left.count())) <= 0 || !(pfd.revents & POLLIN)) break;
     alignas(struct inotify_event) char buf[8192];
     ssize_t n;
     while ((n = read(d->ino_fd, buf, sizeof buf)) > 0) {
       for (char* p = buf; p < buf + n;) {
         auto* ev = reinterpret_cast<struct inotify_event*>(p);
-        if (ev->len && base == ev->name) out["changed"] = true;
+        if (ev->len && base == ev->name) changed = true;
         p += sizeof(struct inotify_event) + ev->len;
       }
     }
   }
+  out["changed"] = changed;
   return dup(out.dump());
 }
 

@@ -1,7 +1,15 @@
 // Unit tests of the device model (health evaluation, topology-aware selection, fault overlay)
 // and the fake cloud provider.
+#include <unistd.h>
+
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <fstream>
+#include <thread>
+
+#include "mi355x/dev.h"
 
 #include "gpupool/provider.h"
 #include "model.h"
@@ -97,6 +105,88 @@ TEST(select_prefers_numa_locality_and_is_all_or_nothing) {
   EXPECT_TRUE(sel[0] >= 4 && sel[1] >= 4);
   req["count"] = 7;
   EXPECT_TRUE(mi355x::select_devices(req).empty());
+}
+
+TEST(evaluate_retired_pages_pending_and_umc_delta) {
+  Json d = healthy_dev();
+  d["ras"] = Json::parse(R"({"badPagesSupported":true,"retiredPages":65,"pendingPages":0,"unreservablePages":0})");
+  Json v = mi355x::evaluate(d, d, policy());
+  EXPECT_TRUE(!v["eccOk"].as_bool());
+  EXPECT_TRUE(v["reasons"][0].as_string().rfind("HBMRetiredPages: 65", 0) == 0);
+  EXPECT_TRUE(mi355x::evaluate(d, d, Json::parse(R"({"health":{"maxRetiredPages":100}})"))["healthy"].as_bool());
+  d["ras"]["pendingPages"] = 1;
+  v = mi355x::evaluate(d, d, Json::parse(R"({"health":{"maxRetiredPages":100}})"));
+  EXPECT_TRUE(!v["healthy"].as_bool());
+  EXPECT_TRUE(v["reasons"][0].as_string().rfind("HBMPendingRetirement", 0) == 0);
+  // the poll's UMC count is its own delta
+  Json base = healthy_dev();
+  base["eccUmc"] = Json::parse(R"({"uncorrectable":2})");
+  Json now = base;
+  now["eccUmc"]["uncorrectable"] = 3;
+  EXPECT_TRUE(!mi355x::evaluate(now, base, policy())["eccOk"].as_bool());
+  EXPECT_TRUE(mi355x::evaluate(base, base, policy())["eccOk"].as_bool());
+}
+
+TEST(c_api_evaluate_batch_and_fault_watch) {
+  // batched verdicts, in order, baseline defaulting to the device
+  Json items = Json::array();
+  Json a = Json::object();
+  a["device"] = healthy_dev();
+  items.push_back(a);
+  Json b = Json::object();
+  Json bad = healthy_dev();
+  bad["ras"] = Json::parse(R"({"retiredPages":1000})");
+  b["device"] = bad;
+  b["policy"] = policy();
+  items.push_back(b);
+  char* out = mi355x_dev_evaluate_batch(items.dump().c_str());
+  Json vs = Json::parse(out);
+  mi355x_free(out);
+  EXPECT_EQ(vs.size(), 2u);
+  EXPECT_TRUE(vs[0]["healthy"].as_bool());
+  EXPECT_TRUE(!vs[1]["healthy"].as_bool());
+  // fault-overlay watch: a rename into place wakes the waiter
+  char dir[] = "/tmp/gpdevXXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  const std::string faults = std::string(dir) + "/faults.json", fixture = std::string(dir) + "/node.json";
+  {
+    std::ofstream f(fixture);
+    f << R"({"devices":[{"index":0,"uuid":"u0","hipUUID":"GPU-0","present":true}]})";
+  }
+  Json cfg = Json::object();
+  cfg["fixture"] = fixture;
+  cfg["faults"] = faults;
+  char err[256] = {0};
+  mi355x_dev* dv = mi355x_dev_open("fake", cfg.dump().c_str(), err, sizeof err);
+  EXPECT_TRUE(dv != nullptr);
+  char* ev = mi355x_dev_wait_events(dv, 10);
+  EXPECT_TRUE(!Json::parse(ev)["supported"].as_bool(true));  // fake: no hardware event source
+  mi355x_free(ev);
+  char* w0 = mi355x_dev_wait_faults(dv, 20);  // arms the watch; nothing changed yet
+  EXPECT_TRUE(!Json::parse(w0)["changed"].as_bool(true));
+  mi355x_free(w0);
+  std::thread writer([&] {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    {
+      std::ofstream f(faults + ".tmp");
+      f << R"({"devices":{"0":{"ecc":{"uncorrectable":3}}}})";
+    }
+    std::rename((faults + ".tmp").c_str(), faults.c_str());
+  });
+  auto t0 = std::chrono::steady_clock::now();
+  char* w = mi355x_dev_wait_faults(dv, 2000);
+  double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  writer.join();
+  EXPECT_TRUE(Json::parse(w)["changed"].as_bool());
+  EXPECT_TRUE(ms < 1500);
+  mi355x_free(w);
+  char* snap = mi355x_dev_health_snapshot(dv);  // the overlay applies to the health poll too
+  EXPECT_EQ(Json::parse(snap)["devices"][0]["ecc"]["uncorrectable"].as_int(), 3);
+  mi355x_free(snap);
+  mi355x_dev_close(dv);
+  std::remove(faults.c_str());
+  std::remove(fixture.c_str());
+  rmdir(dir);
 }
 
 TEST(overlay_merges_by_uuid_and_index) {
