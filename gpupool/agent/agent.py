@@ -390,6 +390,7 @@ class Agent:
         """The fault overlay file is itself an event source: a rewrite is applied at once (inotify)
         unless the overlay sets ``"notify": false`` — then only the periodic sample sees it, which
         is how a real ECC counter change (amdsmi has no ECC event) is detected."""
+        self.events_supported["faultOverlay"] = bool(self.cfg.faults)
         while not self._stop.is_set():
             try:
                 r = self.dev.wait_faults(500)
