@@ -251,6 +251,22 @@ def main() -> int:
             for k2, v in per.items():
                 span_ms.setdefault(k2, []).append(v)
         span_p50 = {k2: round(statistics.median(v), 3) for k2, v in sorted(span_ms.items())}
+        # end-to-end accounting of each timed cycle (wall clocks of one host): PATCH -> the
+        # manager's claiming pass starts (apiserver write + watch + queue), the pass itself, and
+        # its status write -> the client's watch sees Ready
+        e2e: dict[str, list[float]] = {"patch_to_pass_ms": [], "pass_ms": [],
+                                       "status_to_client_ms": []}
+        for cy in cycles:
+            hit = [t for t in claim_traces if cy["patchAt"] <= t["start"] <= cy["readyAtWall"]]
+            if not hit:
+                continue
+            t = min(hit, key=lambda x: x["start"])
+            e2e["patch_to_pass_ms"].append((t["start"] - cy["patchAt"]) * 1e3)
+            e2e["pass_ms"].append(t["totalMs"])
+            e2e["status_to_client_ms"].append(
+                (cy["readyAtWall"] - t["start"]) * 1e3 - t["totalMs"])
+        e2e_p50 = {k2: round(statistics.median(v), 3) for k2, v in e2e.items() if v}
+        e2e_p50["cycles_matched"] = len(e2e["pass_ms"])
         head = per_n[str(n)]
         all_ok = sum(cy["ok"] for cy in cycles)
         src = ("real MI355X: amdsmi discovery + gfx950 HIP probe (HBM %d MiB + bf16 MFMA) + device "
@@ -291,8 +307,10 @@ def main() -> int:
                 "agent": agent_stats,
                 "world_size": world,
                 "claim_pass_span_p50_ms": span_p50,
+                "e2e_breakdown_p50_ms": e2e_p50,
                 "steps_detail": [{k2: (round(v, 4) if isinstance(v, float) else v)
-                                  for k2, v in cy.items()} for cy in cycles[:len(sweep)]],
+                                  for k2, v in cy.items() if k2 not in ("patchAt", "readyAtWall")}
+                                 for cy in cycles[:len(sweep)]],
             },
         }
     comm_backend = "gloo" if args.comm_check == "gloo" else "nccl" if real else ""

@@ -152,13 +152,16 @@ class BenchRun:
     # ------------------------------------------------------------ config 2/3
     def cycle(self, pool: dict, n: int) -> dict:
         name = pool["metadata"]["name"]
+        patch_at = time.time()  # wall clock, to place the manager's trace of this cycle
         t0 = time.perf_counter()
         obj = self.scale(name, n)
         t_ready = time.perf_counter() - t0
+        ready_at_wall = patch_at + t_ready
         truth = self.wait_truth(pool, n)
         ok = truth["ready"] == obj["status"]["readyReplicas"] == n and truth.get("ledgerAgrees", True)
         self.scale(name, 0)
         return {"n": n, "readySeconds": t_ready, "ok": ok, "truth": truth,
+                "patchAt": patch_at, "readyAtWall": ready_at_wall,
                 "probeMs": [round(d.get("probe", {}).get("ms", 0.0), 3)
                             for d in obj["status"]["devices"]]}
 
