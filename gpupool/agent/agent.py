@@ -337,6 +337,29 @@ class Agent:
         with self.lock:
             self.recent_events = (self.recent_events + [ev])[-32:]
 
+    def node_event(self, reason: str, message: str, etype: str = "Warning") -> None:
+        """A core/v1 Event on this Node (``gpuctl events``/``kubectl get events``) for hardware
+        happenings no pool owns: amdsmi thermal-throttle / reset / VM-fault events, HBM sweep
+        failures. Posted from a background thread; never blocks the caller."""
+        if not self.cfg.apiserver:
+            return
+
+        def post():
+            from ..kube import EVENTS, Client
+            try:
+                c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
+                ts = now_rfc3339()
+                c.create(EVENTS, {
+                    "apiVersion": "v1", "kind": "Event",
+                    "metadata": {"name": f"{self.cfg.node}.{os.urandom(6).hex()}"},
+                    "involvedObject": {"kind": "Node", "name": self.cfg.node, "apiVersion": "v1"},
+                    "reason": reason, "message": message, "type": etype, "count": 1,
+                    "firstTimestamp": ts, "lastTimestamp": ts,
+                    "source": {"component": "gpupool-agent", "host": self.cfg.node}}, "default")
+            except Exception as e:  # events are best effort
+                log.debug("node event %s not posted: %s", reason, e)
+        threading.Thread(target=post, daemon=True, name="node-event").start()
+
     def _device_event_watcher(self) -> None:
         """amdsmi event notification (thermal throttle, GPU pre/post reset, VM fault): each event
         triggers an immediate sample instead of waiting for the next period. A GPU between its
@@ -372,6 +395,9 @@ class Agent:
                 log.warning("device event on GPU %s: %s %s", ev.get("index"), ev.get("type"),
                             ev.get("message", ""))
                 self._note_event({"source": "amdsmi", **ev})
+                self.node_event(str(ev.get("type") or "DeviceEvent"),
+                                f"GPU {ev.get('index')}: {ev.get('message', '')}".strip(),
+                                "Normal" if ev.get("type") == "GPUPostReset" else "Warning")
             self.sample()
             for u in recheck:
                 self._recheck_after_reset(u)

@@ -210,6 +210,8 @@ class HbmScrubber:
         log.error("%s: %s", uuid, why)
         a = self.agent
         a.ledger.quarantine(uuid, 1e12, why)
+        a.node_event("HBMSweepFailed", f"GPU {(a.by_uuid.get(uuid) or {}).get('index')} "
+                     f"({uuid}) quarantined: {why}")
         with a.lock:
             changed = a._evaluate_all()
         a._bump(changed | {"*free*"})

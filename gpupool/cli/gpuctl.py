@@ -356,6 +356,46 @@ def cmd_devices(c: Client, ns: str, args) -> int:
     return 0
 
 
+def cmd_top(c: Client, ns: str, args) -> int:
+    """gpuctl top [pools|gpus]: live GPU utilisation (kubectl top for the pools; the reference's
+    "Prometheus + Grafana, GPU utilisation", GPU调度平台搭建.md:800) read from every node agent."""
+    rows = []
+    for n in c.list(NODES)["items"]:
+        ep = (n["metadata"].get("annotations") or {}).get(schema.ANN_AGENT_ENDPOINT)
+        if not ep:
+            continue
+        try:
+            view = Client(ep, _agent_token()).request("GET", "/v1/node")
+        except Exception as e:  # an unreachable agent is a row, not a failure
+            print(f"warning: node {n['metadata']['name']}: {e}", file=sys.stderr)
+            continue
+        for d in view["devices"]:
+            rows.append((view["node"], d))
+    num = lambda v: float(v) if isinstance(v, (int, float)) else 0.0  # noqa: E731
+    if args.what == "gpus":
+        print(f"{'NODE':<18}{'IDX':<5}{'POOL':<28}{'GFX%':<6}{'UMC%':<6}{'POWER(W)':<10}VRAM(GiB)")
+        for node, d in sorted(rows, key=lambda r: (r[0], r[1].get("index", 0))):
+            t = d.get("telemetry") or {}
+            print(f"{node:<18}{d.get('index', ''):<5}{d.get('pool', '') or '-':<28}"
+                  f"{num(t.get('gfxActivity')):<6.0f}{num(t.get('umcActivity')):<6.0f}"
+                  f"{num(t.get('powerW')):<10.0f}"
+                  f"{num(t.get('memUsedBytes')) / 2**30:.0f}/{num(t.get('memTotalBytes')) / 2**30:.0f}")
+        return 0
+    pools: dict[str, list[dict]] = {}
+    for _, d in rows:
+        if d.get("pool"):
+            pools.setdefault(d["pool"], []).append(d.get("telemetry") or {})
+    print(f"{'POOL':<32}{'GPUS':<6}{'GFX%':<6}{'UMC%':<6}{'POWER(W)':<10}VRAM(GiB)")
+    for p, ts in sorted(pools.items()):
+        k = len(ts)
+        print(f"{p:<32}{k:<6}{sum(num(t.get('gfxActivity')) for t in ts) / k:<6.0f}"
+              f"{sum(num(t.get('umcActivity')) for t in ts) / k:<6.0f}"
+              f"{sum(num(t.get('powerW')) for t in ts):<10.0f}"
+              f"{sum(num(t.get('memUsedBytes')) for t in ts) / 2**30:.0f}/"
+              f"{sum(num(t.get('memTotalBytes')) for t in ts) / 2**30:.0f}")
+    return 0
+
+
 def _agent(c: Client, node: str) -> Client | None:
     n = c.get(NODES, node)
     ep = (n["metadata"].get("annotations") or {}).get(schema.ANN_AGENT_ENDPOINT)
@@ -678,6 +718,8 @@ def build_parser() -> argparse.ArgumentParser:
     p = sub.add_parser("devices")
     p.add_argument("node")
     p.add_argument("-o", "--output", default="")
+    p = sub.add_parser("top", help="GPU utilisation per pool (or per GPU) from the node agents")
+    p.add_argument("what", nargs="?", default="pools", choices=["pools", "gpus"])
     p = sub.add_parser("gpu", help="per-GPU maintenance: cordon | uncordon")
     p.add_argument("action", choices=["cordon", "uncordon"])
     p.add_argument("node")
@@ -736,7 +778,7 @@ def main(argv: list[str] | None = None) -> int:
     fn = {"apply": cmd_apply, "get": cmd_get, "describe": cmd_describe, "delete": cmd_delete,
           "scale": cmd_scale, "wait": cmd_wait, "logs": cmd_logs, "events": cmd_events,
           "devices": cmd_devices, "install": cmd_install, "render": cmd_render,
-          "gpu": cmd_gpu, "trainjob": cmd_trainjob, "whoami": cmd_whoami}[args.cmd]
+          "gpu": cmd_gpu, "trainjob": cmd_trainjob, "whoami": cmd_whoami, "top": cmd_top}[args.cmd]
     try:
         return fn(c, ns, args)
     except KubeError as e:

@@ -9,7 +9,7 @@ import time
 
 import pytest
 
-from gpupool.kube import MI355XPOOLS
+from gpupool.kube import EVENTS, MI355XPOOLS
 from gpupool.testing.cluster import NodeSpec
 
 from .helpers import cond_is, mi_pool, wait_ready
@@ -60,6 +60,11 @@ def test_bad_hbm_window_quarantines_free_gpu(cluster_factory):
                            if x["uuid"] == victim and x["state"] == "Quarantined"), None))
     assert "HBMSweepFailed" in d["quarantine"]["reason"]
     k = cl.client
+    # the agent tells the cluster: a Warning Event on the Node
+    ev = wait(lambda: next((e for e in k.list(EVENTS, "default")["items"]
+                            if e.get("reason") == "HBMSweepFailed"), None))
+    assert ev["involvedObject"] == {"kind": "Node", "name": "mi355x-node-0", "apiVersion": "v1"}
+    assert ev["type"] == "Warning" and victim in ev["message"]
     k.create(MI355XPOOLS, mi_pool("all", 8), "default")
     o = k.wait_for(MI355XPOOLS, "all", "default",
                    cond_is("Progressing", "False", "InsufficientDevices"), timeout=20)

@@ -271,6 +271,12 @@ def test_utilisation_metrics_agent_and_pool(cluster_factory):
     assert r.returncode == 0, r.stderr
     assert "events faultOverlay" in r.stdout and "GFX%" in r.stdout
     assert "0/288" in r.stdout and "262W" in r.stdout and "default/util" in r.stdout
+    r = subprocess.run([os.path.join(ROOT, "bin", "gpuctl"), "--server", c.url, "top"],
+                       capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, GPUPOOL_AGENT_TOKEN=c.agent_token))
+    assert r.returncode == 0, r.stderr
+    row = next(ln for ln in r.stdout.splitlines() if ln.startswith("default/util"))
+    assert row.split()[1:] == ["2", "0", "0", "524", "1/576"], row
     dash = json.load(open(os.path.join(ROOT, "config", "prometheus", "grafana-dashboard.json")))
     exprs = " ".join(t["expr"] for p in dash["panels"] for t in p.get("targets", []))
     for name in ("gpupool_pool_gfx_activity_percent", "gpupool_device_vram_used_bytes",
