@@ -596,14 +596,16 @@ AGENT_NAMESPACE = "gpupool-system"
 def agent_rbac() -> list[dict]:
     """ServiceAccount + ClusterRole + binding for the node agent DaemonSet: it registers its Node
     (labels, agent-endpoint annotation) and heartbeats the GPUPoolAgentReady/ROCmReady node
-    conditions; device/pod facts come from the kubelet's local sockets, not the API."""
+    conditions and posts Events on its Node (amdsmi hardware events, HBM sweep failures);
+    device/pod facts come from the kubelet's local sockets, not the API."""
     sa = {"apiVersion": "v1", "kind": "ServiceAccount",
           "metadata": {"name": "gpupool-agent", "namespace": AGENT_NAMESPACE}}
     role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
             "metadata": {"name": "gpupool-agent-role"},
             "rules": [{"apiGroups": [""], "resources": ["nodes"],
                        "verbs": ["get", "create", "patch"]},
-                      {"apiGroups": [""], "resources": ["nodes/status"], "verbs": ["patch"]}]}
+                      {"apiGroups": [""], "resources": ["nodes/status"], "verbs": ["patch"]},
+                      {"apiGroups": [""], "resources": ["events"], "verbs": ["create"]}]}
     binding = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
                "metadata": {"name": "gpupool-agent-rolebinding"},
                "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",

@@ -12,6 +12,7 @@
 //    the agent owns the claim ledger, libmi355x_dev and the HIP probe.
 #pragma once
 
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <memory>
@@ -171,13 +172,35 @@ class RocmProvider : public DeviceProvider {
   // restarted elsewhere) and another thread swaps the cached client. Throws ProviderError.
   std::shared_ptr<HttpClient> client_for(const std::string& node);
 
+  // Informer-style cache of the agents' node views. The agent's event feed reports its state
+  // generation (note_gen); after a change the feed's thread prefetches the full view. A pool's
+  // observe is answered from the cache when it is at the newest generation the manager has heard
+  // of, younger than ``view_max_age`` (telemetry keeps moving without generation bumps) and no
+  // mutating RPC to that node started since it was fetched; otherwise it is an RPC as before.
+  void note_gen(const std::string& node, int64_t gen);
+  void prefetch(const std::string& node);
+  void set_view_max_age_ms(int ms) { view_max_age_ms_ = ms; }
+  uint64_t view_cache_hits() const { return cache_hits_.load(); }
+
  private:
   Json post_(const std::string& node, const std::string& path, const Json& body);
+  void invalidate_(const std::string& node);
   Informer& nodes_;
   int timeout_ms_;
   std::string agent_token_;
   std::mutex mu_;
   std::map<std::string, std::pair<std::string, std::shared_ptr<HttpClient>>> clients_;
+  struct CachedView {
+    bool valid = false;
+    std::chrono::steady_clock::time_point at;
+    NodeView view;
+  };
+  std::mutex cache_mu_;
+  std::map<std::string, CachedView> cache_;
+  std::map<std::string, int64_t> latest_gen_;  // newest agent generation heard of, per node
+  std::map<std::string, uint64_t> epoch_;      // bumped by every mutating RPC, per node
+  int view_max_age_ms_ = 5000;
+  std::atomic<uint64_t> cache_hits_{0};
 };
 
 }  // namespace gpupool

@@ -278,8 +278,13 @@ class AgentWatchers {
               auto j = Json::try_parse(line);
               if (!j) return true;
               int64_t gen = (*j)["gen"].as_int(since);
-              if (since >= 0 && gen != since) enqueue_pools(node, (*j)["pools"]);
+              prov_.note_gen(node, gen);
+              const bool changed = gen != since;
+              if (since >= 0 && changed) enqueue_pools(node, (*j)["pools"]);
               since = gen;
+              // after the pools are queued (latency first), refresh the view cache so the next
+              // reconcile of a pool on this node needs no observe RPC
+              if (changed) prov_.prefetch(node);
               return true;
             },
             &w->stop);

@@ -5,6 +5,7 @@
 // gpupool.amd.com/agent-endpoint annotation.
 #include "gpupool/generated/schema_consts.h"
 #include "gpupool/informer.h"
+#include "gpupool/metrics.h"
 #include "gpupool/provider.h"
 #include "gpupool/trace.h"
 
@@ -119,6 +120,7 @@ std::shared_ptr<HttpClient> RocmProvider::client_for(const std::string& node) {
 }
 
 Json RocmProvider::post_(const std::string& node, const std::string& path, const Json& body) {
+  invalidate_(node);  // every POST mutates the agent: the next observe must ask it
   trace::Span span("agent:POST " + path);
   std::shared_ptr<HttpClient> c = client_for(node);
   HttpResponse r;
@@ -139,7 +141,62 @@ Json RocmProvider::post_(const std::string& node, const std::string& path, const
 
 NodeView RocmProvider::observe(const std::string& node) { return observe_pool(node, ""); }
 
+void RocmProvider::note_gen(const std::string& node, int64_t gen) {
+  std::lock_guard<std::mutex> g(cache_mu_);
+  latest_gen_[node] = gen;
+}
+
+void RocmProvider::invalidate_(const std::string& node) {
+  std::lock_guard<std::mutex> g(cache_mu_);
+  cache_[node].valid = false;
+  ++epoch_[node];
+}
+
+void RocmProvider::prefetch(const std::string& node) {
+  uint64_t epoch;
+  {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    epoch = epoch_[node];
+  }
+  NodeView v = observe_pool(node, "");  // the full view (an RPC: the cache serves pools only)
+  if (!v.reachable) return;
+  std::lock_guard<std::mutex> g(cache_mu_);
+  auto lg = latest_gen_.find(node);
+  if (epoch_[node] != epoch || (lg != latest_gen_.end() && v.gen < lg->second)) return;  // raced
+  CachedView& c = cache_[node];
+  c.valid = true;
+  c.at = std::chrono::steady_clock::now();
+  c.view = std::move(v);
+}
+
 NodeView RocmProvider::observe_pool(const std::string& node, const std::string& pool_uid) {
+  if (!pool_uid.empty()) {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    auto it = cache_.find(node);
+    auto lg = latest_gen_.find(node);
+    if (it != cache_.end() && it->second.valid && lg != latest_gen_.end() && it->second.view.gen == lg->second &&
+        std::chrono::steady_clock::now() - it->second.at < std::chrono::milliseconds(view_max_age_ms_)) {
+      trace::Span span("agent:view-cache");
+      const NodeView& full = it->second.view;
+      NodeView nv;
+      nv.name = full.name;
+      nv.endpoint = full.endpoint;
+      nv.backend = full.backend;
+      nv.reachable = true;
+      nv.advertise_required = full.advertise_required;
+      nv.gen = full.gen;
+      nv.free_healthy = 0;
+      for (const auto& d : full.devices) {
+        if (d.pool_uid == pool_uid) nv.devices.push_back(d);
+        else if (d.state == "Free" && d.healthy) ++nv.free_healthy;
+      }
+      cache_hits_.fetch_add(1);
+      static CounterVec& hits = Registry::global().counter(
+          "gpupool_agent_view_cache_hits_total", "Pool observes answered from the agent view cache (no RPC).");
+      hits.inc({{"node", node}});
+      return nv;
+    }
+  }
   NodeView nv;
   nv.name = node;
   nv.endpoint = endpoint_of(node);

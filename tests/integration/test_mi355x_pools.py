@@ -317,6 +317,27 @@ def test_reconcile_traces(node8):
     assert 'gpupool_reconcile_span_seconds_count{kind="Mi355xPool",span="observe"}' in m
 
 
+def test_observe_served_from_the_agent_view_cache(node8):
+    """Informer-style cache of the agents' node views: after the agent's event feed announced a
+    change the manager prefetches the view, so the next reconcile observes without an RPC; a
+    mutating RPC invalidates it, so status after acting still comes from the agent."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("vc", 1), "default")
+    wait_ready(k, "vc", 1)
+    time.sleep(0.3)  # the claim's event -> prefetch
+    k.patch(MI355XPOOLS, "vc", {"spec": {"replicas": 3}}, "default")
+    o = wait_ready(k, "vc", 3)
+    hits = [ln for ln in node8.manager_metrics().splitlines()
+            if ln.startswith("gpupool_agent_view_cache_hits_total{")]
+    assert hits and float(hits[0].rsplit(" ", 1)[1]) >= 1, hits
+    # scale down: cordon + release are POSTs (cache invalidated) -> the status is ground truth
+    k.patch(MI355XPOOLS, "vc", {"spec": {"replicas": 1}}, "default")
+    o = wait_ready(k, "vc", 1)
+    view = agent_view(node8)
+    assert {d["uuid"] for d in view["devices"] if d.get("pool") == "default/vc"} == \
+        {d["uuid"] for d in o["status"]["devices"]}
+
+
 def test_namespace_gpu_quota(node8):
     """a ResourceQuota caps the GPUs pools in a namespace may claim."""
     from gpupool.kube import Res
