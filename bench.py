@@ -205,6 +205,10 @@ def main() -> int:
     if rank == 0:
         from gpupool.bench.runner import summary
         gt_s = run.gt_s
+        try:  # the timed cycles' traces, before the secondary scenarios push them out of the ring
+            traces = cluster.manager_traces(key="Mi355xPool/default/bench-pool", n=1024)
+        except Exception:
+            traces = []
         per_n = {}
         for k in sweep:
             cs = [cy for cy in cycles if cy["n"] == k]
@@ -234,10 +238,6 @@ def main() -> int:
             metrics = cluster.manager_metrics()
         except Exception:
             metrics = ""
-        try:
-            traces = cluster.manager_traces(key="Mi355xPool/default/bench-pool", n=512)
-        except Exception:
-            traces = []
         cluster.stop()
         # latency breakdown of the scale-up passes (the reconcile that claims): median per span
         claim_traces = [t for t in traces
