@@ -58,8 +58,9 @@ class CloudProvider {
                           const std::string& name) = 0;
   // Starts an asynchronous delete of VM + NIC + OS disk (README.md:216, :239). Idempotent.
   virtual void destroy(const Credentials& c, const std::string& rg, const std::string& name) = 0;
-  // NICs / disks tagged for ``owner`` that no longer belong to a VM (must stay empty).
-  virtual std::vector<std::string> orphans(const std::string& rg, const std::string& owner) = 0;
+  // NICs / disks of ``owner`` that no longer belong to a VM, as "nic/<name>" / "disk/<name>"
+  // (must end up empty; destroy() accepts these ids).
+  virtual std::vector<std::string> orphans(const Credentials& c, const std::string& rg, const std::string& owner) = 0;
 };
 
 struct FakeCloudOptions {
@@ -77,7 +78,7 @@ class FakeCloudProvider : public CloudProvider {
   VmRecord create(const Credentials& c, const AzureVmPoolSpec& spec, const std::string& owner,
                   const std::string& name) override;
   void destroy(const Credentials& c, const std::string& rg, const std::string& name) override;
-  std::vector<std::string> orphans(const std::string& rg, const std::string& owner) override;
+  std::vector<std::string> orphans(const Credentials& c, const std::string& rg, const std::string& owner) override;
   Json dump();  // whole fake cloud (tests)
 
  private:

@@ -998,6 +998,9 @@ bool AzureVmPoolReconciler::credentials_(const ObjectMeta& m, const AzureVmPoolS
     *why = "Secret " + m.ns + "/" + spec.credential_secret + " lacks keys: " + join(missing, ",");
     return false;
   }
+  // optional: the SSH key the VMs' admin account trusts (else the manager's --azure-ssh-public-key-file)
+  std::string ssh = base64_decode(secret["data"]["AZURE_SSH_PUBLIC_KEY"].as_string());
+  if (!ssh.empty()) out->values["AZURE_SSH_PUBLIC_KEY"] = ssh;
   return true;
 }
 
@@ -1049,20 +1052,42 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
   try {
     vms = cloud_.list(creds, spec.resource_group, owner);
   } catch (const ProviderError& e) {
+    const bool refused = e.code == "AuthenticationFailed" || e.code == "AuthorizationFailed";
+    if (refused) {  // the cloud refused the credentials: retried like missing ones (Secret may be fixed)
+      set_condition(conds, gen::kCondCredentialsValid, "False", e.code, e.what(), m.generation, now);
+      set_condition(conds, gen::kCondReady, "False", e.code, e.what(), m.generation, now);
+    }
     set_condition(conds, gen::kCondDegraded, "True", e.code, e.what(), m.generation, now);
     st["conditions"] = conds;
     write_status_(obj, st);
+    if (refused) {
+      event_(obj, "Warning", e.code, e.what());
+      return Outcome::requeue(opts_.credentials_retry, e.what());
+    }
     return e.transient ? Outcome::transient(e.what()) : Outcome::terminal(e.what());
   }
 
   if (m.deleting()) {
-    for (const auto& vm : vms)
-      if (vm.state != "Deleting") cloud_.destroy(creds, spec.resource_group, vm.name);
-    vms = cloud_.list(creds, spec.resource_group, owner);
-    auto orphans = cloud_.orphans(spec.resource_group, owner);
+    std::vector<std::string> orphans;
+    try {
+      for (const auto& vm : vms)
+        if (vm.state != "Deleting") cloud_.destroy(creds, spec.resource_group, vm.name);
+      vms = cloud_.list(creds, spec.resource_group, owner);
+      // NICs / OS disks left by an interrupted create: removed once their VMs are gone
+      orphans = cloud_.orphans(creds, spec.resource_group, owner);
+      if (vms.empty())
+        for (const auto& o : orphans) cloud_.destroy(creds, spec.resource_group, o);
+    } catch (const ProviderError& e) {
+      set_condition(conds, gen::kCondDegraded, "True", e.code, e.what(), m.generation, now);
+      st["conditions"] = conds;
+      write_status_(obj, st);
+      return Outcome::transient(e.what());
+    }
     if (!vms.empty() || !orphans.empty()) {
       set_condition(conds, gen::kCondDeleting, "True", "DeletingVMs",
-                    std::to_string(vms.size()) + " VM(s) still deleting", m.generation, now);
+                    std::to_string(vms.size()) + " VM(s), " + std::to_string(orphans.size()) +
+                        " leftover NIC/disk(s) still deleting",
+                    m.generation, now);
       set_condition(conds, gen::kCondReady, "False", "Deleting", "pool is being deleted", m.generation, now);
       st["conditions"] = conds;
       st["replicas"] = static_cast<long long>(vms.size());

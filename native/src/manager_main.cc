@@ -24,6 +24,7 @@
 #include <thread>
 
 #include "gpupool/api.h"
+#include "gpupool/azure_arm.h"
 #include "gpupool/events.h"
 #include "gpupool/generated/schema_consts.h"
 #include "gpupool/http.h"
@@ -63,6 +64,9 @@ struct Flags {
   std::string fakecloud_faults;
   int fakecloud_provision_ms = 0;
   int fakecloud_deprovision_ms = 0;
+  std::string cloud = "fake";  // fake | azure-arm
+  std::string azure_arm_endpoint, azure_authority_host, azure_ca_file, azure_ssh_key_file, azure_admin_user;
+  int azure_nic_wait_ms = 10000;
   int orphan_sweep_ms = 30000;
   int lease_duration_ms = 15000;
   int renew_deadline_ms = 10000;
@@ -112,8 +116,14 @@ observability:
   --health-addr H:P                 separate /healthz listener
   --port-file F                     write the bound metrics port here
   --log-level debug|info|warn|error --slow-reconcile D (1s) log traces slower than D at info
-fake cloud (AzureVmPool):
+AzureVmPool cloud:
+  --cloud fake|azure-arm (fake)  fake: in-process cloud; azure-arm: the Azure Resource Manager REST API
   --fakecloud-state F  --fakecloud-faults F  --fakecloud-provision-ms N  --fakecloud-deprovision-ms N
+  --azure-arm-endpoint URL (https://management.azure.com)
+  --azure-authority-host URL (https://login.microsoftonline.com)
+  --azure-ca-file F            CA bundle for both (private endpoints, tests)
+  --azure-ssh-public-key-file F  VM admin SSH key when the Secret has no AZURE_SSH_PUBLIC_KEY
+  --azure-admin-user U (azureuser)  --azure-nic-wait D (10s)
 tools:
   --validate obj.json          print validation errors (JSON) for one object and exit
 durations: 250ms, 10s, 5m or bare milliseconds.
@@ -169,6 +179,13 @@ Flags parse(int argc, char** argv) {
     else if (is("--fakecloud-faults")) f.fakecloud_faults = val();
     else if (is("--fakecloud-provision-ms")) f.fakecloud_provision_ms = std::stoi(val());
     else if (is("--fakecloud-deprovision-ms")) f.fakecloud_deprovision_ms = std::stoi(val());
+    else if (is("--cloud")) f.cloud = val();
+    else if (is("--azure-arm-endpoint")) f.azure_arm_endpoint = val();
+    else if (is("--azure-authority-host")) f.azure_authority_host = val();
+    else if (is("--azure-ca-file")) f.azure_ca_file = val();
+    else if (is("--azure-ssh-public-key-file")) f.azure_ssh_key_file = val();
+    else if (is("--azure-admin-user")) f.azure_admin_user = val();
+    else if (is("--azure-nic-wait")) f.azure_nic_wait_ms = parse_duration_ms(val());
     else if (is("--orphan-sweep")) f.orphan_sweep_ms = parse_duration_ms(val());
     else if (is("--lease-duration")) f.lease_duration_ms = parse_duration_ms(val());
     else if (is("--renew-deadline")) f.renew_deadline_ms = parse_duration_ms(val());
@@ -183,6 +200,10 @@ Flags parse(int argc, char** argv) {
       std::cerr << "unknown flag " << a << "\n";
       std::exit(2);
     }
+  }
+  if (f.cloud != "fake" && f.cloud != "azure-arm") {
+    std::cerr << "--cloud must be fake or azure-arm\n";
+    std::exit(2);
   }
   if (f.identity.empty()) {
     char host[256] = {0};
@@ -470,7 +491,25 @@ int main(int argc, char** argv) {
     fco.deprovision = std::chrono::milliseconds(f.fakecloud_deprovision_ms);
     fco.state_file = f.fakecloud_state;
     fco.faults_file = f.fakecloud_faults;
-    FakeCloudProvider cloud(fco);
+    std::unique_ptr<CloudProvider> cloud_impl;
+    if (f.cloud == "azure-arm") {
+      AzureArmOptions ao;
+      if (!f.azure_arm_endpoint.empty()) ao.arm_endpoint = f.azure_arm_endpoint;
+      if (!f.azure_authority_host.empty()) ao.authority_host = f.azure_authority_host;
+      if (!f.azure_admin_user.empty()) ao.admin_username = f.azure_admin_user;
+      ao.tls.ca_file = f.azure_ca_file;
+      ao.nic_wait_ms = f.azure_nic_wait_ms;
+      if (!f.azure_ssh_key_file.empty()) {
+        std::ifstream kf(f.azure_ssh_key_file);
+        std::string key((std::istreambuf_iterator<char>(kf)), std::istreambuf_iterator<char>());
+        while (!key.empty() && (key.back() == '\n' || key.back() == '\r' || key.back() == ' ')) key.pop_back();
+        ao.ssh_public_key = key;
+      }
+      cloud_impl = std::make_unique<AzureArmProvider>(ao);
+    } else {
+      cloud_impl = std::make_unique<FakeCloudProvider>(fco);
+    }
+    CloudProvider& cloud = *cloud_impl;
     Informer jobs(client, ResourceRef{gen::kGroup, gen::kVersion, gen::kPluralMi355xJob, true, "Mi355xJob"}, f.ns,
                   std::chrono::milliseconds(f.resync_ms));
     Informer pods(client, res::pods(), "", std::chrono::milliseconds(f.resync_ms));

@@ -130,6 +130,11 @@ void FakeCloudProvider::destroy(const Credentials& c, const std::string& rg, con
   check_creds_(c);
   std::lock_guard<std::mutex> g(mu_);
   advance_locked_();
+  if (name.rfind("nic/", 0) == 0 || name.rfind("disk/", 0) == 0) {  // a leftover from orphans()
+    const bool nic = name[0] == 'n';
+    (nic ? nics_ : disks_)[rg].erase(name.substr(nic ? 4 : 5));
+    return;
+  }
   auto it = vms_.find(rg + "/" + name);
   if (it == vms_.end() || it->second.deleting) return;  // idempotent
   if (take_fault_("failDeletes")) throw ProviderError("InternalServerError", "injected delete failure");
@@ -140,7 +145,9 @@ void FakeCloudProvider::destroy(const Credentials& c, const std::string& rg, con
   advance_locked_();
 }
 
-std::vector<std::string> FakeCloudProvider::orphans(const std::string& rg, const std::string& owner) {
+std::vector<std::string> FakeCloudProvider::orphans(const Credentials& c, const std::string& rg,
+                                                    const std::string& owner) {
+  check_creds_(c);
   std::lock_guard<std::mutex> g(mu_);
   advance_locked_();
   std::vector<std::string> out;

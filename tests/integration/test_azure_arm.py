@@ -1,0 +1,247 @@
+"""AzureVmPool against the Azure Resource Manager REST API (``--cloud azure-arm``).
+
+The reference's operator drove Azure through the Go SDK (README.md:179-221): client from the
+credentials Secret, tag-scoped listing, VM + NIC + OS disk create, delete that removes all three
+(README.md:238-240). Here the manager's AzureArmProvider speaks ARM's REST wire protocol over TLS
+to the in-repo ARM simulator (gpupool/testing/arm_sim.py; no Azure access exists in this
+environment — parity with live Azure is unpinned, the request/response shapes follow ARM's
+published API versions 2024-07-01 / 2024-05-01).
+"""
+from __future__ import annotations
+
+import base64
+import os
+import time
+
+import pytest
+import yaml
+
+from gpupool.kube import AZUREVMPOOLS, EVENTS, SECRETS
+from gpupool.testing.arm_sim import ArmSim
+from gpupool.testing.cluster import make_test_pki
+
+from .helpers import cond_is, conds
+
+pytestmark = pytest.mark.slow
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+SUB = "00000000-0000-0000-0000-000000000003"
+TENANT = "00000000-0000-0000-0000-000000000002"
+CLIENT = "00000000-0000-0000-0000-000000000001"
+RG = "MyGpuResourceGroup"
+SSH_KEY = "ssh-ed25519 AAAAC3NzaC1lZDI1NTE5AAAAIGpvb2wtdGVzdC1rZXk gpupool-test"
+
+
+def sample(name="gpu-pool-prod", replicas=2):
+    doc = yaml.safe_load(open(os.path.join(ROOT, "config", "samples",
+                                           "compute_v1alpha1_azurevmpool.yaml")))
+    doc["metadata"]["name"] = name
+    doc["spec"]["replicas"] = replicas
+    return doc
+
+
+def secret(client_secret="fake-secret", ssh_key=SSH_KEY):
+    doc = yaml.safe_load(open(os.path.join(ROOT, "config", "samples",
+                                           "azure-credentials-secret.yaml")))
+    doc["stringData"]["AZURE_CLIENT_SECRET"] = client_secret
+    if ssh_key:
+        doc["stringData"]["AZURE_SSH_PUBLIC_KEY"] = ssh_key
+    return doc
+
+
+def az_ready(r):
+    def pred(o):
+        st = (o or {}).get("status") or {}
+        return bool(o) and st.get("observedGeneration") == o["metadata"]["generation"] and \
+            st.get("readyReplicas") == r and len(st.get("vms", [])) == r and \
+            conds(o).get("Ready", {}).get("status") == "True"
+    return pred
+
+
+@pytest.fixture
+def arm(tmp_path):
+    ca, crt, key = make_test_pki(str(tmp_path), "arm")
+    sim = ArmSim(principals={CLIENT: {"tenant": TENANT, "secret": "fake-secret",
+                                      "subscriptions": [SUB]}},
+                 resource_groups={f"{SUB}/{RG}": {"location": "eastus",
+                                                  "vnets": {"MyVnet": ["default"]}}},
+                 vm_delay=0.3, delete_delay=0.3, certfile=crt, keyfile=key).start()
+    sim.ca = ca
+    yield sim
+    sim.stop()
+
+
+def arm_cluster(cluster_factory, sim, extra=(), env=None):
+    return cluster_factory(nodes=[], kinds="azure", env=env,
+                           manager_args=["--cloud", "azure-arm",
+                                         "--azure-arm-endpoint", sim.url,
+                                         "--azure-authority-host", sim.url,
+                                         "--azure-ca-file", sim.ca,
+                                         "--credentials-retry", "300ms", *extra])
+
+
+def wait_events(k, want: set, timeout=10.0) -> set:
+    deadline = time.monotonic() + timeout
+    while True:
+        reasons = {e["reason"] for e in k.list(EVENTS, "default")["items"]}
+        if want <= reasons or time.monotonic() > deadline:
+            return reasons
+        time.sleep(0.05)
+
+
+def test_arm_scale_up_down_and_full_cleanup(arm, cluster_factory):
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(), "default")
+    k.create(AZUREVMPOOLS, sample(replicas=2), "default")
+    o = k.wait_for(AZUREVMPOOLS, "gpu-pool-prod", "default", az_ready(2), timeout=30)
+    st = arm.state()
+    assert len(st["vms"]) == 2 and len(st["nics"]) == 2 and len(st["disks"]) == 2
+    assert sorted(o["status"]["vms"]) == sorted(v["name"] for v in st["vms"])
+    for vm in st["vms"]:
+        assert vm["tags"] == {"managed-by": "azurevmpool-operator",
+                              "owner": "default-gpu-pool-prod"}  # README.md:238
+        p = vm["properties"]
+        assert p["provisioningState"] == "Succeeded"
+        assert p["hardwareProfile"]["vmSize"] == "Standard_NC4as_T4_v3"
+        assert p["storageProfile"]["imageReference"]["offer"] == "0001-com-ubuntu-server-jammy"
+        assert p["storageProfile"]["osDisk"]["deleteOption"] == "Delete"
+        assert p["networkProfile"]["networkInterfaces"][0]["properties"]["deleteOption"] == "Delete"
+        lin = p["osProfile"]["linuxConfiguration"]
+        assert lin["disablePasswordAuthentication"] is True
+        assert lin["ssh"]["publicKeys"][0]["keyData"] == SSH_KEY
+    for nic in st["nics"]:
+        assert nic["properties"]["virtualMachine"]["id"].endswith(nic["name"][:-4])
+        assert nic["properties"]["ipConfigurations"][0]["properties"]["subnet"]["id"].endswith(
+            "/virtualNetworks/MyVnet/subnets/default")
+    assert all(d["managedBy"] for d in st["disks"])
+    # one token serves every call (cached until near expiry)
+    assert st["tokenRequests"] == 1
+
+    k.patch(AZUREVMPOOLS, "gpu-pool-prod", {"spec": {"replicas": 1}}, "default")
+    k.wait_for(AZUREVMPOOLS, "gpu-pool-prod", "default", az_ready(1), timeout=30)
+    deadline = time.monotonic() + 10
+    while len(arm.state()["nics"]) != 1 and time.monotonic() < deadline:
+        time.sleep(0.1)
+    st = arm.state()
+    assert len(st["vms"]) == 1 and len(st["nics"]) == 1 and len(st["disks"]) == 1
+
+    k.delete(AZUREVMPOOLS, "gpu-pool-prod", "default")
+    k.wait_for(AZUREVMPOOLS, "gpu-pool-prod", "default", lambda o: o is None, timeout=30)
+    st = arm.state()
+    assert st["vms"] == [] and st["nics"] == [] and st["disks"] == []  # README.md:216, :239
+    assert {"VMCreating", "VMDeleting", "Finalized"} <= wait_events(
+        k, {"VMCreating", "VMDeleting", "Finalized"})
+
+
+def test_arm_refused_secret_then_fixed(arm, cluster_factory):
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(client_secret="wrong"), "default")
+    k.create(AZUREVMPOOLS, sample("bad-secret", 1), "default")
+    o = k.wait_for(AZUREVMPOOLS, "bad-secret", "default",
+                   cond_is("CredentialsValid", "False", "AuthenticationFailed"), timeout=20)
+    assert "AADSTS7000215" in conds(o)["CredentialsValid"]["message"]
+    assert conds(o)["Ready"]["status"] == "False"
+    assert arm.state()["vms"] == []
+    fixed = base64.b64encode(b"fake-secret").decode()
+    k.patch(SECRETS, "azure-credentials", {"data": {"AZURE_CLIENT_SECRET": fixed}}, "default")
+    o = k.wait_for(AZUREVMPOOLS, "bad-secret", "default", az_ready(1), timeout=30)
+    assert conds(o)["CredentialsValid"]["status"] == "True"
+
+
+def test_arm_subscription_not_granted(arm, cluster_factory):
+    arm.principals[CLIENT]["subscriptions"] = ["another-subscription"]
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(), "default")
+    k.create(AZUREVMPOOLS, sample("no-rbac", 1), "default")
+    o = k.wait_for(AZUREVMPOOLS, "no-rbac", "default",
+                   cond_is("CredentialsValid", "False", "AuthorizationFailed"), timeout=20)
+    assert "has no access to subscription" in conds(o)["CredentialsValid"]["message"]
+
+
+def test_arm_workload_identity(arm, cluster_factory, tmp_path):
+    """README.md:311: a federated token (client assertion) instead of a client secret."""
+    arm.principals["wi-client"] = {"tenant": TENANT, "secret": None, "subscriptions": [SUB]}
+    token = tmp_path / "azure-identity-token"
+    token.write_text("eyJhbGciOiJSUzI1NiJ9.fake.jwt\n")
+    env = {"AZURE_CLIENT_ID": "wi-client", "AZURE_TENANT_ID": TENANT,
+           "AZURE_SUBSCRIPTION_ID": SUB, "AZURE_FEDERATED_TOKEN_FILE": str(token)}
+    key = tmp_path / "id_ed25519.pub"
+    key.write_text(SSH_KEY + "\n")
+    c = arm_cluster(cluster_factory, arm, env=env,
+                    extra=["--azure-ssh-public-key-file", str(key)])
+    k = c.client
+    pool = sample("wi-pool", 1)
+    pool["spec"]["azureCredentialSecret"] = "workload-identity"
+    k.create(AZUREVMPOOLS, pool, "default")  # no Secret at all
+    o = k.wait_for(AZUREVMPOOLS, "wi-pool", "default", az_ready(1), timeout=30)
+    assert conds(o)["CredentialsValid"]["reason"] == "WorkloadIdentity"
+    vm = arm.state()["vms"][0]
+    assert vm["properties"]["osProfile"]["linuxConfiguration"]["ssh"]["publicKeys"][0][
+        "keyData"] == SSH_KEY  # from the manager's key file
+
+
+def test_arm_throttling_token_revocation_paging_and_orphans(arm, cluster_factory):
+    arm.page_size = 1  # every list follows nextLink
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(), "default")
+    k.create(AZUREVMPOOLS, sample("busy", 3), "default")
+    k.wait_for(AZUREVMPOOLS, "busy", "default", az_ready(3), timeout=30)
+    # throttled calls are transient (backoff, no status flapping to a credentials error);
+    # a revoked token is refreshed once on the 401
+    arm.faults["throttle"] = 3
+    with arm.mu:
+        arm.tokens.clear()
+    before = arm.state()["tokenRequests"]
+    k.patch(AZUREVMPOOLS, "busy", {"spec": {"replicas": 4}}, "default")
+    o = k.wait_for(AZUREVMPOOLS, "busy", "default", az_ready(4), timeout=30)
+    assert arm.state()["tokenRequests"] == before + 1
+    assert conds(o)["CredentialsValid"]["status"] == "True"
+    # a NIC + OS disk left behind by an interrupted create are removed with the pool
+    arm.add_orphans(SUB, RG, "default-busy", "busy-0abcd")
+    arm.add_orphans(SUB, RG, "default-other", "other-0abcd")  # not ours: must survive
+    k.delete(AZUREVMPOOLS, "busy", "default")
+    k.wait_for(AZUREVMPOOLS, "busy", "default", lambda o: o is None, timeout=30)
+    st = arm.state()
+    assert st["vms"] == []
+    assert [n["name"] for n in st["nics"]] == ["other-0abcd-nic"]
+    assert [d["name"] for d in st["disks"]] == ["other-0abcd-osdisk"]
+
+
+def test_arm_failed_vm_put_leaves_no_nic(arm, cluster_factory):
+    arm.faults["failVmPut"] = 2
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(), "default")
+    k.create(AZUREVMPOOLS, sample("flaky", 2), "default")
+    k.wait_for(AZUREVMPOOLS, "flaky", "default", az_ready(2), timeout=30)
+    st = arm.state()
+    assert len(st["nics"]) == 2 and all(n["properties"].get("virtualMachine") for n in st["nics"])
+    assert "InternalServerError" in wait_events(k, {"InternalServerError"})
+
+
+def test_arm_missing_ssh_key_is_reported(arm, cluster_factory):
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(ssh_key=None), "default")
+    k.create(AZUREVMPOOLS, sample("nokey", 1), "default")
+    o = k.wait_for(AZUREVMPOOLS, "nokey", "default",
+                   cond_is("Degraded", "True", "SSHKeyMissing"), timeout=20)
+    assert "AZURE_SSH_PUBLIC_KEY" in conds(o)["Degraded"]["message"]
+    assert arm.state()["nics"] == []  # checked before anything is created
+
+
+def test_arm_bad_subnet_reference(arm, cluster_factory):
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(), "default")
+    pool = sample("badnet", 1)
+    pool["spec"]["subnetName"] = "missing"
+    k.create(AZUREVMPOOLS, pool, "default")
+    o = k.wait_for(AZUREVMPOOLS, "badnet", "default",
+                   cond_is("Degraded", "True", "InvalidResourceReference"), timeout=20)
+    assert "subnets/missing" in conds(o)["Degraded"]["message"]
+    k.patch(AZUREVMPOOLS, "badnet", {"spec": {"subnetName": "default"}}, "default")
+    k.wait_for(AZUREVMPOOLS, "badnet", "default", az_ready(1), timeout=30)
