@@ -61,6 +61,7 @@ class AgentConfig:
     probe_gemm_n: int = 4096
     sample_interval: float = 2.0
     health_interval: float = 0.1     # fast poll of the health-only fields (0 = off)
+    pod_watch_interval: float = 0.02  # PodResources poll while a GPU drains / after an Allocate
     quarantine_s: float = 300.0
     advertise_wait_s: float = 2.0
     fsync: bool = True
@@ -130,6 +131,7 @@ class Agent:
         self.events_supported: dict[str, Any] = {}
         self._pods_cache: tuple[float, dict[str, list[dict]]] = (0.0, {})
         self._pods_refreshing = False
+        self._pods_kick = threading.Event()
         self._pods_watch_until = 0.0
         from .podresources import PodResourcesClient
         self._podres = PodResourcesClient(cfg.pod_resources) if cfg.pod_resources else None
@@ -546,6 +548,27 @@ class Agent:
         """Pod placement is about to change (a device-plugin Allocate): views refresh the pod map
         in the background for a while, so the new pod shows up without waiting for the sampler."""
         self._pods_watch_until = max(self._pods_watch_until, time.monotonic() + seconds)
+        self._pods_kick.set()
+
+    def _pod_watcher(self) -> None:
+        """Polls the kubelet's PodResources (it has no watch) every ``pod_watch_interval`` while
+        pod placement is expected to change: a GPU is draining (its evicted pods' exit is what the
+        drain waits for) or a device-plugin Allocate just happened. A change bumps the owning
+        pool, so the manager's agent feed wakes the drain without the manager polling the agent
+        (its view cache answers observes without an RPC) or waiting for the sampler's period."""
+        while not self._stop.is_set():
+            self._pods_kick.wait(1.0)
+            self._pods_kick.clear()
+            while not self._stop.is_set():
+                with self.lock:
+                    active = time.monotonic() < self._pods_watch_until or self._draining()
+                if not active:
+                    break
+                try:
+                    self._refresh_pods()
+                except Exception as e:
+                    log.debug("podresources refresh failed: %s", e)
+                self._stop.wait(self.cfg.pod_watch_interval)
 
     def _refresh_pods(self) -> dict[str, list[dict]]:
         pods = self._podres.list_pod_devices()
@@ -572,6 +595,7 @@ class Agent:
             finally:
                 with self.lock:
                     self._pods_refreshing = False
+        self._pods_kick = threading.Event()
         threading.Thread(target=run, daemon=True, name="podres-refresh").start()
 
     def _advertisable(self, uuid: str) -> bool:
@@ -807,6 +831,8 @@ class Agent:
                     n += 1
             if n:
                 self.ledger.commit(self.records)
+        if n:
+            self._pods_kick.set()  # watch the evicted pods go
         self._notify_plugins()
         return {"ok": True, "cordoned": n}
 
@@ -1114,6 +1140,8 @@ class Agent:
                  (self._fault_watcher, "fault-watch")]
         if self.cfg.health_interval > 0:
             loops.append((self._health_poller, "health-poll"))
+        if self._podres is not None and self.cfg.pod_watch_interval > 0:
+            loops.append((self._pod_watcher, "pod-watch"))
         for fn, name in loops:
             t = threading.Thread(target=fn, daemon=True, name=name)
             t.start()

@@ -84,6 +84,27 @@ def test_config4_scale_down_8_to_4_with_drain(node8):
     assert all(d["state"] == "Free" for d in agent_view(node8)["devices"])
 
 
+def test_drain_wakes_on_pod_exit_not_the_sample_period(cluster_factory):
+    """A drain waits for the evicted pod to exit. The agent's pod watch (PodResources polled every
+    20 ms while a GPU drains) bumps the pool when the pod is gone, so the release follows within
+    tens of ms — not after the agent's sample period (5 s here) or the manager's 5 s view-cache
+    age, which a view-driven refresh alone would wait for (BENCH r2t: 0.96 s at a 1 s period)."""
+    c = cluster_factory(sample_interval=5.0)
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("p", 1, drain={"gracePeriodSeconds": 1}), "default")
+    wait_ready(k, "p", 1)
+    k.create(PODS, pause_pod("w0"), "default")
+    k.wait_for(PODS, "w0", "default", lambda o: o and o["status"].get("phase") == "Running",
+               timeout=30)
+    time.sleep(0.3)  # let the Allocate pod-watch window lapse into steady state
+    t0 = time.perf_counter()
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 0}}, "default")
+    wait_ready(k, "p", 0, timeout=20)
+    dt = time.perf_counter() - t0
+    assert k.list(PODS, "default")["items"] == []
+    assert dt < 1.5, f"scale-down with drain took {dt:.2f} s"
+
+
 def test_config5_two_pools_with_health_conditions(node8):
     k = node8.client
     k.create(MI355XPOOLS, mi_pool("team-a", 4, resourceName="amd.com/gpu-team-a",
