@@ -678,6 +678,8 @@ class Agent:
         probe_opts = req.get("probe") or {}
         timings: dict[str, float] = {}  # phase -> ms, returned to the manager as trace spans
         t_phase = time.perf_counter()
+        if "_t_in" in req:  # the RPC handler's hand-off to this executor thread
+            timings["executorIn"] = round((t_phase - req.pop("_t_in")) * 1e3, 3)
 
         def lap(name: str) -> None:
             nonlocal t_phase
@@ -769,7 +771,8 @@ class Agent:
         lap("view")
         log.info("claimed %d GPU(s) for %s: %s (probe wall %.1f ms; phases %s)", len(chosen),
                  req.get("pool"), [d["index"] for d in chosen], probe_wall, timings)
-        return {"ok": True, "devices": views, "probeWallMs": probe_wall, "timingsMs": timings}
+        return {"ok": True, "devices": views, "probeWallMs": probe_wall, "timingsMs": timings,
+                "_t_done": time.perf_counter()}
 
     def _xgmi_check(self, pool_uid: str, chosen: list[dict], results: list[dict],
                     opts: dict) -> None:
@@ -1202,7 +1205,14 @@ def build_app(agent: Agent) -> web.Application:
         if not body.get("poolUID") or int(body.get("count", 0)) <= 0:
             return web.json_response({"reason": "BadRequest", "message": "poolUID and count>0 "
                                       "required"}, status=400)
-        return web.json_response(await run_blocking(agent.claim, body))
+        t_in = time.perf_counter()
+        body["_t_in"] = t_in
+        out = await run_blocking(agent.claim, body)
+        t_back = time.perf_counter()
+        tm = out.get("timingsMs")
+        if tm is not None:  # the executor hop back to the event loop (GIL + loop wake-up)
+            tm["executorOut"] = round((t_back - out.pop("_t_done")) * 1e3, 3)
+        return web.Response(text=json.dumps(out), content_type="application/json")
 
     async def cordon(request):
         b = await request.json()

@@ -14,6 +14,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -179,7 +180,10 @@ class RocmProvider : public DeviceProvider {
   // of, younger than ``view_max_age`` (telemetry keeps moving without generation bumps) and no
   // mutating RPC to that node started since it was fetched; otherwise it is an RPC as before.
   void note_gen(const std::string& node, int64_t gen);
-  void prefetch(const std::string& node);
+  // Waits (up to ``max_wait_ms``) for the node's in-flight mutating RPCs to finish first: a
+  // claim bumps the agent's generation several times, and fetching the full view meanwhile only
+  // competes with the claim's reply on the agent's event loop for a view that is stale at once.
+  void prefetch(const std::string& node, int max_wait_ms = 30000);
   void set_view_max_age_ms(int ms) { view_max_age_ms_ = ms; }
   uint64_t view_cache_hits() const { return cache_hits_.load(); }
 
@@ -200,6 +204,8 @@ class RocmProvider : public DeviceProvider {
   std::map<std::string, CachedView> cache_;
   std::map<std::string, int64_t> latest_gen_;  // newest agent generation heard of, per node
   std::map<std::string, uint64_t> epoch_;      // bumped by every mutating RPC, per node
+  std::map<std::string, int> inflight_;        // mutating RPCs in progress, per node
+  std::condition_variable cache_cv_;           // signalled when a node's inflight_ drops to 0
   int view_max_age_ms_ = 5000;
   std::atomic<uint64_t> cache_hits_{0};
 };

@@ -120,6 +120,18 @@ std::shared_ptr<HttpClient> RocmProvider::client_for(const std::string& node) {
 }
 
 Json RocmProvider::post_(const std::string& node, const std::string& path, const Json& body) {
+  {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    ++inflight_[node];
+  }
+  struct Done {
+    RocmProvider* p;
+    const std::string& node;
+    ~Done() {
+      std::lock_guard<std::mutex> g(p->cache_mu_);
+      if (--p->inflight_[node] == 0) p->cache_cv_.notify_all();
+    }
+  } done{this, node};
   invalidate_(node);  // every POST mutates the agent: the next observe must ask it
   trace::Span span("agent:POST " + path);
   std::shared_ptr<HttpClient> c = client_for(node);
@@ -152,10 +164,11 @@ void RocmProvider::invalidate_(const std::string& node) {
   ++epoch_[node];
 }
 
-void RocmProvider::prefetch(const std::string& node) {
+void RocmProvider::prefetch(const std::string& node, int max_wait_ms) {
   uint64_t epoch;
   {
-    std::lock_guard<std::mutex> g(cache_mu_);
+    std::unique_lock<std::mutex> g(cache_mu_);
+    cache_cv_.wait_for(g, std::chrono::milliseconds(max_wait_ms), [&] { return inflight_[node] == 0; });
     epoch = epoch_[node];
   }
   NodeView v = observe_pool(node, "");  // the full view (an RPC: the cache serves pools only)
