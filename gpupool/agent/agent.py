@@ -672,6 +672,15 @@ class Agent:
 
     # ================================================================ claims
     def claim(self, req: dict) -> dict:
+        """Claim ``count`` GPUs for a pool, all or nothing: select (topology), commit to the
+        ledger, probe, commit, advertise through the device plugin, answer with device views."""
+        st = self._claim_start(req)
+        if not st.get("ok"):
+            return st
+        self._wait_advertised(st["_resource"], st["_uuids"])
+        return self._claim_finish(st)
+
+    def _claim_start(self, req: dict) -> dict:
         pool_uid, count = req["poolUID"], int(req["count"])
         policy = req.get("policy") or {}
         resource = req.get("resourceName") or schema.DEFAULT_RESOURCE
@@ -763,16 +772,22 @@ class Agent:
         lap("commit2")
         self._ensure_plugin(resource)
         self._notify_plugins()
-        self._wait_advertised(resource, [d["uuid"] for d in chosen])
-        lap("advertise")
+        return {"ok": True, "probeWallMs": probe_wall, "timingsMs": timings, "_t_phase": t_phase,
+                "_resource": resource, "_uuids": [d["uuid"] for d in chosen],
+                "_indices": [d["index"] for d in chosen], "_pool": req.get("pool")}
+
+    def _claim_finish(self, st: dict) -> dict:
+        timings = st["timingsMs"]
+        t = time.perf_counter()
+        timings["advertise"] = round((t - st["_t_phase"]) * 1e3, 3)
         pods = self._pods_by_device()
         with self.lock:
-            views = [self.device_view(d["uuid"], pods) for d in chosen]
-        lap("view")
-        log.info("claimed %d GPU(s) for %s: %s (probe wall %.1f ms; phases %s)", len(chosen),
-                 req.get("pool"), [d["index"] for d in chosen], probe_wall, timings)
-        return {"ok": True, "devices": views, "probeWallMs": probe_wall, "timingsMs": timings,
-                "_t_done": time.perf_counter()}
+            views = [self.device_view(u, pods) for u in st["_uuids"]]
+        timings["view"] = round((time.perf_counter() - t) * 1e3, 3)
+        log.info("claimed %d GPU(s) for %s: %s (probe wall %.1f ms; phases %s)", len(views),
+                 st["_pool"], st["_indices"], st["probeWallMs"], timings)
+        return {"ok": True, "devices": views, "probeWallMs": st["probeWallMs"],
+                "timingsMs": timings, "_t_done": time.perf_counter()}
 
     def _xgmi_check(self, pool_uid: str, chosen: list[dict], results: list[dict],
                     opts: dict) -> None:
@@ -921,20 +936,26 @@ class Agent:
         if pools:  # readiness depends on the advertised bit: tell the manager
             self._bump(pools)
 
+    def _advertise_done(self, resource: str, uuids: list[str]) -> bool:
+        """Every advertisable GPU of ``uuids`` reached the kubelet — or there is no registered
+        plugin to wait for (no kubelet: readiness follows via events, never block the claim)."""
+        with self.lock:
+            want = [u for u in uuids if self._advertisable(u)]
+            if all(u in self.advertised.get(resource, set()) for u in want):
+                return True
+            plugin = self.plugins.get(resource)
+            return plugin is None or not plugin.registered
+
     def _wait_advertised(self, resource: str, uuids: list[str]) -> None:
         if not self.cfg.plugin_dir:
             return
         deadline = time.monotonic() + self.cfg.advertise_wait_s
         while time.monotonic() < deadline:
-            with self.lock:
-                want = [u for u in uuids if self._advertisable(u)]
-                if all(u in self.advertised.get(resource, set()) for u in want):
-                    return
-                plugin = self.plugins.get(resource)
-                if plugin is None or not plugin.registered:
-                    return  # no kubelet: do not block the claim (readiness follows via events)
+            if self._advertise_done(resource, uuids):
+                return
             self._adv_event.wait(0.05)
             self._adv_event.clear()
+
 
     def _ensure_plugin(self, resource: str) -> None:
         if not self.cfg.plugin_dir:

@@ -32,15 +32,18 @@ def main() -> int:
     ap.add_argument("--n", type=int, default=50)
     ap.add_argument("--backend", default="fake")
     ap.add_argument("--out")
+    ap.add_argument("--agent-arg", action="append", default=[], help="extra agent flag (repeat)")
     a = ap.parse_args()
     wd = tempfile.mkdtemp(prefix="rpcov")
-    node = NodeSpec("n0", backend=a.backend, count=1 if a.backend != "fake" else -1)
+    node = NodeSpec("n0", backend=a.backend, count=1 if a.backend != "fake" else -1,
+                    extra_args=list(a.agent_arg))
     c = Cluster(wd, nodes=[node], manager=False, kinds="mi355x")
     c.start()
     try:
         from gpupool.kube import Client
         cl = Client("unix://" + c.agent_socket("n0"), c.agent_token)
         rt, inner, probe, ex_in, ex_out = [], [], [], [], []
+        phases: dict[str, list[float]] = {}
         health, view = [], []
         for i in range(a.n + 3):
             t0 = time.perf_counter()
@@ -62,6 +65,8 @@ def main() -> int:
             rt.append(dt)
             inner.append(sum(r["timingsMs"].values()))
             probe.append(r["timingsMs"].get("probe", 0.0))
+            for k, v in r["timingsMs"].items():
+                phases.setdefault(k, []).append(v)
             ex_in.append(r["timingsMs"].get("executorIn", 0.0))
             ex_out.append(r["timingsMs"].get("executorOut", 0.0))
             view.append(dv)
@@ -71,7 +76,8 @@ def main() -> int:
                "claim_phases_p50_ms": p50(inner), "probe_p50_ms": p50(probe),
                "rpc_overhead_p50_ms": p50([x - y for x, y in zip(rt, inner)]),
                "executor_in_p50_ms": p50(ex_in), "executor_out_p50_ms": p50(ex_out),
-               "pool_view_rtt_p50_ms": p50(view), "healthz_rtt_p50_ms": p50(health)}
+               "pool_view_rtt_p50_ms": p50(view), "healthz_rtt_p50_ms": p50(health),
+               "agent_args": a.agent_arg, "phases_p50_ms": {k: p50(v) for k, v in phases.items()}}
         print(json.dumps(out), flush=True)
         if a.out:
             with open(a.out, "w") as f:
