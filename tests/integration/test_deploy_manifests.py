@@ -94,3 +94,41 @@ def test_kustomization_lists_every_deploy_manifest():
     assert listed == shipped
     mon = list(yaml.safe_load_all(open(os.path.join(ROOT, "config", "prometheus", "monitor.yaml"))))
     assert {m["kind"] for m in mon} == {"Service", "ServiceMonitor"}
+
+
+def _json_patch_add(doc, path: str, value) -> None:
+    parts = [p.replace("~1", "/").replace("~0", "~") for p in path.lstrip("/").split("/")]
+    for p in parts[:-1]:
+        doc = doc[int(p)] if isinstance(doc, list) else doc[p]
+    last = parts[-1]
+    if isinstance(doc, list):
+        doc.append(value) if last == "-" else doc.insert(int(last), value)
+    else:
+        doc[last] = value
+
+
+def test_azure_overlay_flags_are_manager_flags(native_built):
+    """config/azure (kustomize overlay): the patched Deployment runs the ARM provider, and every
+    argument it passes is a flag the manager binary accepts."""
+    import yaml
+
+    from gpupool.testing.cluster import native_bin
+    kz = yaml.safe_load(open(os.path.join(ROOT, "config", "azure", "kustomization.yaml")))
+    assert kz["resources"] == ["../default"]
+    dep = next(d for d in yaml.safe_load_all(open(os.path.join(ROOT, "config", "manager",
+                                                               "manager.yaml")))
+               if d and d["kind"] == "Deployment")
+    for p in kz["patches"]:
+        assert p["target"]["name"] == dep["metadata"]["name"]
+        for op in yaml.safe_load(p["patch"]):
+            assert op["op"] == "add"
+            _json_patch_add(dep, op["path"], op["value"])
+    spec = dep["spec"]["template"]["spec"]
+    args = spec["containers"][0]["args"]
+    assert args[args.index("--cloud") + 1] == "azure-arm"
+    mounts = {m["name"] for m in spec["containers"][0]["volumeMounts"]}
+    assert mounts <= {v["name"] for v in spec["volumes"]}
+    assert dep["spec"]["template"]["metadata"]["labels"]["azure.workload.identity/use"] == "true"
+    r = subprocess.run([native_bin("gpupool-manager"), *args, "--help"], capture_output=True,
+                       text=True, timeout=30)
+    assert r.returncode == 0, r.stderr
