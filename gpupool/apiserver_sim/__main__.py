@@ -21,11 +21,14 @@ def main() -> None:
     ap.add_argument("--tls-cert", default=None, help="serve HTTPS with this PEM certificate chain")
     ap.add_argument("--tls-key", default=None, help="PEM private key for --tls-cert")
     ap.add_argument("--client-ca", default=None, help="require client certs signed by this CA")
+    ap.add_argument("--watch-delay", type=float, default=0.0,
+                    help="deliver every watch event this many seconds late (stale informers)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     logging.basicConfig(level=logging.DEBUG if a.verbose else logging.WARNING,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
-    sim = ApiServerSim(token=a.token, bookmark_interval=a.bookmark_interval, window=a.window)
+    sim = ApiServerSim(token=a.token, bookmark_interval=a.bookmark_interval, window=a.window,
+                       watch_delay=a.watch_delay)
     try:
         asyncio.run(serve(a.host, a.port, sim, a.port_file, a.crd_dir, a.unix,
                           tls_cert=a.tls_cert, tls_key=a.tls_key, client_ca=a.client_ca))

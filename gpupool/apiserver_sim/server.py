@@ -126,8 +126,11 @@ def to_table(rt: ResourceType, items: list[dict], rv: str) -> dict:
 # ------------------------------------------------------------------ server
 class ApiServerSim:
     def __init__(self, token: str | None = None, bookmark_interval: float = 5.0,
-                 window: int = 50000):
+                 window: int = 50000, watch_delay: float = 0.0):
         self.store = Store(window=window)
+        # a lagging watch cache (as a loaded kube-apiserver has): every watch event is delivered
+        # ``watch_delay`` seconds after the write, so informers see stale objects meanwhile
+        self.watch_delay = watch_delay
         self.token = token
         self.bookmark_interval = bookmark_interval
         self.watchers: set[asyncio.Queue] = set()
@@ -191,8 +194,9 @@ class ApiServerSim:
         return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
 
     def _fanout(self, ev: WatchEvent) -> None:
+        t = time.monotonic()
         for q in list(self.watchers):
-            q.put_nowait(ev)
+            q.put_nowait((t, ev))
 
     # -------------------------------------------------------------- discovery
     def _resources_for(self, group: str, version: str) -> list[dict]:
@@ -398,7 +402,7 @@ class ApiServerSim:
                     if wait <= 0:
                         break
                 try:
-                    ev = await asyncio.wait_for(queue.get(), timeout=max(wait, 0.001))
+                    t_ev, ev = await asyncio.wait_for(queue.get(), timeout=max(wait, 0.001))
                 except asyncio.TimeoutError:
                     if bookmarks and time.monotonic() >= next_bm:
                         bm = {"type": "BOOKMARK", "object": {
@@ -411,6 +415,10 @@ class ApiServerSim:
                 if ev.rtype != rt.key or ev.rv <= last_rv or not match(ev.obj):
                     continue
                 last_rv = ev.rv
+                if self.watch_delay > 0:
+                    lag = t_ev + self.watch_delay - time.monotonic()
+                    if lag > 0:
+                        await asyncio.sleep(lag)
                 await resp.write((json.dumps({"type": ev.type, "object": ev.obj}) + "\n").encode())
             await resp.write_eof()
             return resp

@@ -98,7 +98,7 @@ class Cluster:
                  python: str = sys.executable, env: dict | None = None,
                  sample_interval: float = 0.5, kinds: str = "mi355x,azure,job",
                  manager_bin: str | None = None, tls: bool = False, token: str | None = None,
-                 fsync: bool = False):
+                 fsync: bool = False, apiserver_args: list[str] | None = None):
         self.workdir = os.path.abspath(workdir)
         self.tls = tls
         self.token = token
@@ -108,6 +108,7 @@ class Cluster:
         self.sockdir = tempfile.mkdtemp(prefix="gp", dir="/tmp")
         self.nodes = nodes if nodes is not None else [NodeSpec("mi355x-node-0")]
         self.manager_args = manager_args or []
+        self.apiserver_args = apiserver_args or []
         self.want_manager = manager
         self.python = python
         self.env = dict(os.environ)
@@ -167,6 +168,7 @@ class Cluster:
             os.remove(pf)
         argv = [self.python, "-m", "gpupool.apiserver_sim", "--port", "0", "--port-file", pf,
                 "--crd-dir", os.path.join(ROOT, "config", "crd"), "--bookmark-interval", "2"]
+        argv += self.apiserver_args
         if self.token:
             argv += ["--token", self.token]
             self.env["GPUPOOL_TOKEN"] = self.token

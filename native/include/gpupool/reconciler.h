@@ -60,6 +60,7 @@ class PoolReconcilerBase {
   // Writes ``status`` (unless semantically unchanged) with a fresh-GET retry on 409.
   void write_status_(const Json& obj, const Json& status);
   // Adds/removes the finalizer with RV precondition; returns the updated object.
+  Json edit_finalizers_(const Json& obj, bool add);
   Json ensure_finalizer_(const Json& obj);
   Json remove_finalizer_(const Json& obj);
   void event_(const Json& obj, const std::string& type, const std::string& reason, const std::string& msg);

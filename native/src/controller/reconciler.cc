@@ -126,29 +126,39 @@ void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
   throw KubeError(409, "Conflict", "status update kept conflicting for " + ns + "/" + name);
 }
 
-Json PoolReconcilerBase::ensure_finalizer_(const Json& obj) {
-  ObjectMeta m = ObjectMeta::from(obj);
-  if (m.has_finalizer(finalizer_)) return obj;
-  trace::Span span("finalizer");
-  Json fins = Json::array();
-  for (const auto& f : m.finalizers) fins.push_back(f);
-  fins.push_back(finalizer_);
-  Json patch = Json::object();
-  patch["metadata"]["finalizers"] = fins;
-  patch["metadata"]["resourceVersion"] = m.resource_version;  // optimistic concurrency
-  return client_.patch_merge(res_, m.ns, m.name, patch);
+// Finalizer edits carry the object's resourceVersion (the list is replaced as a whole, so a
+// concurrent edit must not be lost). The informer cache can lag the apiserver — most often behind
+// this reconciler's own status write — and a stale version is a 409: then the object is read
+// fresh and the edit retried against it, instead of failing the pass into rate-limited backoff
+// until the watch catches up (seen as hundreds of 409s when 48 pools were created at once).
+Json PoolReconcilerBase::edit_finalizers_(const Json& obj, bool add) {
+  Json cur = obj;
+  for (int attempt = 0;; ++attempt) {
+    ObjectMeta m = ObjectMeta::from(cur);
+    if (m.has_finalizer(finalizer_) == add) return cur;
+    Json fins = Json::array();
+    for (const auto& f : m.finalizers)
+      if (f != finalizer_) fins.push_back(f);
+    if (add) fins.push_back(finalizer_);
+    Json patch = Json::object();
+    patch["metadata"]["finalizers"] = fins;
+    patch["metadata"]["resourceVersion"] = m.resource_version;  // optimistic concurrency
+    try {
+      return client_.patch_merge(res_, m.ns, m.name, patch);
+    } catch (const KubeError& e) {
+      if (!e.conflict() || attempt >= 3) throw;
+      cur = client_.get(res_, m.ns, m.name);
+    }
+  }
 }
 
-Json PoolReconcilerBase::remove_finalizer_(const Json& obj) {
-  ObjectMeta m = ObjectMeta::from(obj);
-  Json fins = Json::array();
-  for (const auto& f : m.finalizers)
-    if (f != finalizer_) fins.push_back(f);
-  Json patch = Json::object();
-  patch["metadata"]["finalizers"] = fins;
-  patch["metadata"]["resourceVersion"] = m.resource_version;
-  return client_.patch_merge(res_, m.ns, m.name, patch);
+Json PoolReconcilerBase::ensure_finalizer_(const Json& obj) {
+  if (ObjectMeta::from(obj).has_finalizer(finalizer_)) return obj;
+  trace::Span span("finalizer");
+  return edit_finalizers_(obj, true);
 }
+
+Json PoolReconcilerBase::remove_finalizer_(const Json& obj) { return edit_finalizers_(obj, false); }
 
 void PoolReconcilerBase::event_(const Json& obj, const std::string& type, const std::string& reason,
                                 const std::string& msg) {

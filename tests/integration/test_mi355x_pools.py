@@ -636,3 +636,24 @@ def test_spanning_claim_is_all_or_nothing(cluster_factory):
         assert not any(d.get("pool") == "default/strict" for d in agent_view(c, n)["devices"])
     msgs = " ".join(e.get("message", "") for e in k.list(EVENTS, "default")["items"])
     assert "other claims released" in msgs
+
+
+def test_lagging_watch_cache_does_not_fail_reconciles(cluster_factory):
+    """Informers can lag the apiserver (a loaded kube-apiserver's watch cache; here every watch
+    event arrives 300 ms late). Passes that act on a stale object — the finalizer patch and the
+    status write carry its resourceVersion — re-read it on 409 instead of failing into backoff, so
+    a pool still converges promptly and the manager logs no failed reconcile."""
+    c = cluster_factory(apiserver_args=["--watch-delay", "0.3"])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("p", 1), "default")
+    wait_ready(k, "p", 1, timeout=30)
+    t0 = time.perf_counter()
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 3}}, "default")
+    wait_ready(k, "p", 3, timeout=30)
+    assert time.perf_counter() - t0 < 3.0
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 0}}, "default")
+    wait_ready(k, "p", 0, timeout=30)
+    k.delete(MI355XPOOLS, "p", "default")
+    k.wait_for(MI355XPOOLS, "p", "default", lambda o: o is None, timeout=30)
+    failed = [ln for ln in c.log("manager").splitlines() if "reconcile failed" in ln]
+    assert not failed, failed[:3]
