@@ -514,6 +514,8 @@ class Agent:
                     pools |= ps
             if self.changes and self.changes[0][0] > since + 1 and since >= 0:
                 pools.add("*")  # history truncated: tell the manager to resync everything
+            if since > self.gen:
+                pools.add("*")  # a generation from before this agent restarted: resync
             # "*free*": free-GPU capacity or health changed -> the manager wakes pools that are
             # waiting for devices; "*": resync everything
             return self.gen, sorted(pools)

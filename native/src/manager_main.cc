@@ -301,7 +301,8 @@ class AgentWatchers {
               int64_t gen = (*j)["gen"].as_int(since);
               prov_.note_gen(node, gen);
               const bool changed = gen != since;
-              if (since >= 0 && changed) enqueue_pools(node, (*j)["pools"]);
+              // a generation going backwards is a restarted agent: everything on it may differ
+              if (since >= 0 && changed) enqueue_pools(node, (*j)["pools"], gen < since);
               since = gen;
               // after the pools are queued (latency first), refresh the view cache so the next
               // reconcile of a pool on this node needs no observe RPC
@@ -319,14 +320,22 @@ class AgentWatchers {
     }
   }
 
-  void enqueue_pools(const std::string& node, const Json& pools) {
+  void enqueue_pools(const std::string& node, const Json& pools, bool node_wide) {
     std::set<std::string> uids;
     for (const auto& u : pools.elements()) uids.insert(u.as_string());
+    const bool all = uids.count("*") > 0;
     for (const auto& p : pools_.list()) {
-      // pools on that node, pools named in the event, and pools still waiting for capacity
-      // (a release or an un-cordon anywhere may unblock them: no need to sit out the requeue)
-      bool hit = uids.count(p.path("metadata.uid").as_string()) > 0 ||
-                 p.path("status.nodeName").as_string() == node || uids.count("*") > 0 ||
+      // the pools the event names (the agent names every pool whose GPUs changed), every pool on
+      // the node after an agent restart or a truncated history ("*"), and pools still waiting for
+      // capacity ("*free*": a release or an un-cordon anywhere may unblock them). Waking every
+      // pool on the node for any event multiplied reconciles ~6x in a burst of claims.
+      bool on_node = false;
+      if (node_wide || all) {
+        on_node = p.path("status.nodeName").as_string() == node;
+        for (const auto& n : p.path("status.nodes").elements()) on_node = on_node || n.as_string() == node;
+      }
+      bool hit = uids.count(p.path("metadata.uid").as_string()) > 0 || on_node ||
+                 (all && p.path("status.nodeName").as_string().empty()) ||
                  (uids.count("*free*") > 0 && !condition_true(p.path("status.conditions"), gen::kCondReady));
       if (hit) ctl_.enqueue("Mi355xPool", p.path("metadata.namespace").as_string(), p.path("metadata.name").as_string());
     }

@@ -168,7 +168,10 @@ void RocmProvider::prefetch(const std::string& node, int max_wait_ms) {
   uint64_t epoch;
   {
     std::unique_lock<std::mutex> g(cache_mu_);
-    cache_cv_.wait_for(g, std::chrono::milliseconds(max_wait_ms), [&] { return inflight_[node] == 0; });
+    // system_clock deadline: libstdc++ then waits with pthread_cond_timedwait, which TSan
+    // intercepts (a steady_clock wait_for uses pthread_cond_clockwait, which GCC 11's TSan misses)
+    cache_cv_.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(max_wait_ms),
+                         [&] { return inflight_[node] == 0; });
     epoch = epoch_[node];
   }
   NodeView v = observe_pool(node, "");  // the full view (an RPC: the cache serves pools only)
