@@ -23,8 +23,16 @@ def main() -> None:
     ap.add_argument("--client-ca", default=None, help="require client certs signed by this CA")
     ap.add_argument("--watch-delay", type=float, default=0.0,
                     help="deliver every watch event this many seconds late (stale informers)")
+    ap.add_argument("--profile", default=None, help="write cProfile stats here on exit")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
+    prof = None
+    if a.profile:
+        import cProfile
+        import signal
+        prof = cProfile.Profile()
+        signal.signal(signal.SIGTERM, lambda *_: (_ for _ in ()).throw(KeyboardInterrupt()))
+        prof.enable()
     logging.basicConfig(level=logging.DEBUG if a.verbose else logging.WARNING,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     sim = ApiServerSim(token=a.token, bookmark_interval=a.bookmark_interval, window=a.window,
@@ -34,6 +42,10 @@ def main() -> None:
                           tls_cert=a.tls_cert, tls_key=a.tls_key, client_ca=a.client_ca))
     except KeyboardInterrupt:
         pass
+    finally:
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(a.profile)
 
 
 if __name__ == "__main__":

@@ -419,7 +419,7 @@ class ApiServerSim:
                     lag = t_ev + self.watch_delay - time.monotonic()
                     if lag > 0:
                         await asyncio.sleep(lag)
-                await resp.write((json.dumps({"type": ev.type, "object": ev.obj}) + "\n").encode())
+                await resp.write(ev.encoded())
             await resp.write_eof()
             return resp
         except (ConnectionResetError, asyncio.CancelledError):

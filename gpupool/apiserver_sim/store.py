@@ -20,14 +20,24 @@ from __future__ import annotations
 
 import base64
 import collections
-import copy
 import datetime as _dt
+import json
 import re
 import uuid as _uuid
 from dataclasses import dataclass, field
 from typing import Any, Callable
 
 from ..api import openapi
+
+
+def clone(o):
+    """Copy of a JSON-shaped value (dict / list / scalars): what the store hands out and keeps.
+    5x faster than copy.deepcopy (no memo table), which was the simulator's largest CPU cost."""
+    if isinstance(o, dict):
+        return {k: clone(v) for k, v in o.items()}
+    if isinstance(o, list):
+        return [clone(v) for v in o]
+    return o
 
 
 class ApiError(Exception):
@@ -111,6 +121,12 @@ class WatchEvent:
     rtype: tuple[str, str]
     type: str
     obj: dict
+    line: bytes | None = None  # the encoded watch line, built once and shared by every watcher
+
+    def encoded(self) -> bytes:
+        if self.line is None:
+            self.line = (json.dumps({"type": self.type, "object": self.obj}) + "\n").encode()
+        return self.line
 
 
 def _spec_part(obj: dict) -> dict:
@@ -186,8 +202,8 @@ def parse_field_selector(sel: str | None) -> Callable[[dict], bool]:
 def merge_patch(target: Any, patch: Any) -> Any:
     """RFC 7386 JSON merge patch."""
     if not isinstance(patch, dict):
-        return copy.deepcopy(patch)
-    out = copy.deepcopy(target) if isinstance(target, dict) else {}
+        return clone(patch)
+    out = clone(target) if isinstance(target, dict) else {}
     for k, v in patch.items():
         if v is None:
             out.pop(k, None)
@@ -204,7 +220,7 @@ def _ptr_parts(path: str) -> list[str]:
 
 def json_patch(target: Any, ops: list[dict]) -> Any:
     """RFC 6902 JSON patch (add/remove/replace/test/copy/move)."""
-    doc = copy.deepcopy(target)
+    doc = clone(target)
 
     def resolve(parts):
         cur = doc
@@ -227,7 +243,7 @@ def json_patch(target: Any, ops: list[dict]) -> Any:
                 cur = doc
                 for p in src:
                     cur = cur[int(p)] if isinstance(cur, list) else cur[p]
-                val = copy.deepcopy(cur)
+                val = clone(cur)
                 if kind == "move":
                     parent, last = resolve(src)
                     if isinstance(parent, list):
@@ -309,7 +325,7 @@ class Store:
         return self.rv
 
     def _emit(self, rt: ResourceType, etype: str, obj: dict) -> None:
-        ev = WatchEvent(int(obj["metadata"]["resourceVersion"]), rt.key, etype, copy.deepcopy(obj))
+        ev = WatchEvent(int(obj["metadata"]["resourceVersion"]), rt.key, etype, clone(obj))
         self.log.append(ev)
         for fn in list(self.listeners):
             fn(ev)
@@ -375,13 +391,13 @@ class Store:
             raise ApiError(404, "NotFound", f'{rt.plural}{"." + rt.group if rt.group else ""} '
                            f'"{name}" not found',
                            {"name": name, "group": rt.group, "kind": rt.plural})
-        return copy.deepcopy(obj)
+        return clone(obj)
 
     def list(self, rt: ResourceType, ns: str | None, label_selector: str | None = None,
              field_selector: str | None = None, limit: int = 0, cont: str | None = None) -> dict:
         lm = parse_label_selector(label_selector)
         fm = parse_field_selector(field_selector)
-        items = [copy.deepcopy(o) for (ons, _), o in sorted(self.objects[rt.key].items())
+        items = [clone(o) for (ons, _), o in sorted(self.objects[rt.key].items())
                  if (not rt.namespaced or not ns or ons == ns)
                  and lm(o["metadata"].get("labels")) and fm(o)]
         meta: dict[str, Any] = {"resourceVersion": str(self.rv)}
@@ -396,7 +412,7 @@ class Store:
 
     # --------------------------------------------------------- writes
     def create(self, rt: ResourceType, ns: str | None, obj: dict, dry_run: bool = False) -> dict:
-        obj = copy.deepcopy(obj)
+        obj = clone(obj)
         ns = self._check_ns(rt, ns or obj.get("metadata", {}).get("namespace"))
         md = obj.setdefault("metadata", {})
         if not md.get("name"):
@@ -435,7 +451,7 @@ class Store:
         if rt.kind == "CustomResourceDefinition":
             self._register_crd(obj)
         self._emit(rt, "ADDED", obj)
-        return copy.deepcopy(obj)
+        return clone(obj)
 
     def update(self, rt: ResourceType, ns: str | None, name: str, obj: dict,
                subresource: str = "", dry_run: bool = False) -> dict:
@@ -444,7 +460,7 @@ class Store:
         if cur is None:
             raise ApiError(404, "NotFound", f'{rt.plural} "{name}" not found',
                            {"name": name, "kind": rt.plural})
-        new = copy.deepcopy(obj)
+        new = clone(obj)
         nmd = new.setdefault("metadata", {})
         if nmd.get("name", name) != name:
             raise ApiError(400, "BadRequest", "the name of the object does not match the URL")
@@ -457,7 +473,7 @@ class Store:
                            "again", {"name": name, "group": rt.group, "kind": rt.plural})
         cmd = cur["metadata"]
         if subresource == "status":
-            merged = copy.deepcopy(cur)
+            merged = clone(cur)
             if "status" in new:
                 merged["status"] = new["status"]
             else:
@@ -474,7 +490,7 @@ class Store:
             nmd["name"] = name
             if rt.status_sub:
                 if "status" in cur:
-                    new["status"] = copy.deepcopy(cur["status"])
+                    new["status"] = clone(cur["status"])
                 else:
                     new.pop("status", None)
             if cmd.get("deletionTimestamp"):
@@ -488,7 +504,7 @@ class Store:
         if dry_run:
             return new
         if new == cur:  # no-op update: no new resourceVersion, no event (apiserver behaviour)
-            return copy.deepcopy(cur)
+            return clone(cur)
         nmd = new["metadata"]
         if _spec_part(new) != _spec_part(cur):
             nmd["generation"] = int(cmd.get("generation", 1)) + 1
@@ -497,12 +513,12 @@ class Store:
         nmd["resourceVersion"] = str(self._next_rv())
         if nmd.get("deletionTimestamp") and not nmd.get("finalizers") and rt.kind != "Pod":
             self._remove(rt, ns, name, new)
-            return copy.deepcopy(new)
+            return clone(new)
         self.objects[rt.key][(ns, name)] = new
         if rt.kind == "CustomResourceDefinition":
             self._register_crd(new)
         self._emit(rt, "MODIFIED", new)
-        return copy.deepcopy(new)
+        return clone(new)
 
     def patch(self, rt: ResourceType, ns: str | None, name: str, patch: Any, ptype: str,
               subresource: str = "", dry_run: bool = False) -> dict:
@@ -530,7 +546,7 @@ class Store:
         if pre.get("resourceVersion") and pre["resourceVersion"] != md["resourceVersion"]:
             raise ApiError(409, "Conflict", "Precondition failed: resourceVersion mismatch")
         if dry_run:
-            return copy.deepcopy(cur)
+            return clone(cur)
         graceful = False
         if rt.kind == "Pod" and cur.get("spec", {}).get("nodeName") \
                 and cur.get("status", {}).get("phase") not in ("Succeeded", "Failed"):
@@ -546,9 +562,9 @@ class Store:
                 self._emit(rt, "MODIFIED", cur)
             elif rt.kind == "Pod" and grace == 0 and not md.get("finalizers"):
                 self._remove(rt, ns, name, cur)
-            return copy.deepcopy(cur)
+            return clone(cur)
         self._remove(rt, ns, name, cur)
-        return copy.deepcopy(cur)
+        return clone(cur)
 
     def _remove(self, rt: ResourceType, ns: str, name: str, obj: dict) -> None:
         self.objects[rt.key].pop((ns, name), None)
