@@ -174,6 +174,10 @@ class Prober:
         if n < 2 or self.mode not in ("inproc", "simulated"):
             return {}
         nbytes = int(opts.get("xgmiBytes") or (64 << 20))
+        if self.mode == "inproc":
+            ring = self._ring_inproc(devs, nbytes)
+            if ring is not None:
+                return ring
 
         def one(i: int) -> tuple[str, dict]:
             src, dst = devs[i], devs[(i + 1) % n]
@@ -200,6 +204,31 @@ class Prober:
                 out[u] = r
             except Exception as e:  # never take the agent down
                 log.warning("xGMI peer check failed: %r", e)
+        return out
+
+    def _ring_inproc(self, devs: list[dict], nbytes: int) -> dict[str, dict] | None:
+        """All links of the ring in one library call, concurrently (each GPU pair of an MI355X node
+        has its own xGMI link): one copy time instead of n. None when a device is not visible to HIP
+        or an injected link fault must be honoured — the pairwise path handles those."""
+        if not hasattr(self._hip, "peer_ring"):
+            return None
+        ords = []
+        for d in devs:
+            o = self.ordinals.get(str(d.get("hipUUID", "")).lower())
+            if o is None or {**(d.get("faults") or {}), **d}.get("xgmiPeerFail"):
+                return None
+            ords.append(o)
+        r = self._hip.peer_ring(ords, nbytes)
+        links = r.get("links")
+        if not isinstance(links, list) or len(links) != len(devs):
+            err = r.get("error") or "xGMI ring check returned no links"
+            return {d["uuid"]: {"passed": False, "error": err, "peer": devs[(i + 1) % len(devs)]["uuid"]}
+                    for i, d in enumerate(devs)}
+        out = {}
+        for i, (d, link) in enumerate(zip(devs, links)):
+            link = dict(link)
+            link["peer"] = devs[(i + 1) % len(devs)]["uuid"]
+            out[d["uuid"]] = link
         return out
 
     def warm_arena(self, ordinal: int, hbm_bytes: int = 1 << 30) -> None:

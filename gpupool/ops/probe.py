@@ -32,6 +32,10 @@ def lib() -> ctypes.CDLL:
             l.mi355x_probe_free.argtypes = [ctypes.c_void_p]
             l.mi355x_probe_peer.restype = ctypes.c_void_p
             l.mi355x_probe_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
+            if hasattr(l, "mi355x_probe_peer_ring"):  # absent from a library built before it
+                l.mi355x_probe_peer_ring.restype = ctypes.c_void_p
+                l.mi355x_probe_peer_ring.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                                     ctypes.c_char_p]
             l.mi355x_probe_trim.restype = ctypes.c_int
             l.mi355x_probe_trim.argtypes = [ctypes.c_int]
             l.mi355x_probe_hbm_sweep.restype = ctypes.c_void_p
@@ -92,6 +96,19 @@ def peer(src: int, dst: int, nbytes: int = 64 << 20) -> dict:
     verified on dst; reports GB/s. ``src == dst`` exercises the same path as a local copy."""
     opts = json.dumps({"bytes": int(nbytes)})
     return _take(lib().mi355x_probe_peer(src, dst, opts.encode()))
+
+
+def peer_ring(ordinals: list[int], nbytes: int = 64 << 20) -> dict:
+    """The xGMI ring in one call: link i copies ordinals[i] -> ordinals[i+1] (wrapping), every link
+    concurrently, then each receiver verifies every bit. -> {"links": [...], "passed"}."""
+    n = len(ordinals)
+    if n < 2:
+        raise ValueError("a ring needs at least 2 entries")
+    if not hasattr(lib(), "mi355x_probe_peer_ring"):
+        raise RuntimeError("libmi355x_probe.so predates the ring check: rebuild it")
+    arr = (ctypes.c_int * n)(*[int(o) for o in ordinals])
+    opts = json.dumps({"bytes": int(nbytes)})
+    return _take(lib().mi355x_probe_peer_ring(arr, n, opts.encode()))
 
 
 def hip_uuid_map() -> dict[str, int]:

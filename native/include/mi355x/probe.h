@@ -32,6 +32,13 @@ char* mi355x_probe_run(int device, const char* opts_json);
  * opts: {"bytes":268435456}. src == dst runs the same path as a local device copy.
  * -> {"src","dst","canAccessPeer":bool,"passed":bool,"badBits","GBps","ms"} */
 char* mi355x_probe_peer(int src, int dst, const char* opts_json);
+/* The whole ring at once: link i copies devs[i] -> devs[(i+1) % n], all links concurrently (each
+ * GPU pair of an MI355X node has its own xGMI link), then every receiver verifies. Send / receive
+ * windows are kept between calls and freed with the idle arena. A device may repeat ([0, 0] on a
+ * 1-GPU box runs local copies through the same path). opts: {"bytes":67108864}
+ * -> {"bytes","links":[{"src","dst","canAccessPeer","passed","badBits","bytes","GBps","ms"}],
+ *     "passed":bool} */
+char* mi355x_probe_peer_ring(const int* devs, int n, const char* opts_json);
 /* One window of the rotating HBM sweep: a buffer of all free HBM minus "reserve" bytes is
  * allocated (kept across calls while "keep" is true; released by mi355x_probe_sweep_release) and
  * [offset, offset+bytes) of it is pattern-tested in both polarities.

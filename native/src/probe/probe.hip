@@ -616,6 +616,14 @@ struct DeviceCtx {
   // arena is therefore allocated before the sweep buffer and not trimmed while a sweep is held or
   // for kSweepClearGrace after its release, so a claim-time probe never allocates behind a clear.
   std::chrono::steady_clock::time_point sweep_released{};
+  // xGMI ring check (mi355x_probe_peer_ring): send / receive windows kept between claims like the
+  // arena (a 64 MiB hipMalloc + hipFree pair per link per claim cost more than the copy), freed by
+  // the same idle trim
+  void* peer_send = nullptr;
+  void* peer_recv = nullptr;
+  uint64_t peer_bytes = 0;
+  unsigned long long* peer_cnt = nullptr;
+  std::chrono::steady_clock::time_point peer_used{};
   bool ready = false;
 };
 
@@ -1037,6 +1045,138 @@ std::string run_peer(int src, int dst, const char* opts) {
          ",\"bytes\":" + std::to_string(n16 * 16) + ",\"GBps\":" + jnum(gbps) + ",\"ms\":" + jnum(ms) + "}";
 }
 
+// Cached peer windows of one device (caller holds its lock, device selected).
+void ensure_peer_bufs(DeviceCtx& c, uint64_t bytes) {
+  if (c.peer_bytes != bytes) {
+    if (c.peer_send) (void)hipFree(c.peer_send);
+    if (c.peer_recv) (void)hipFree(c.peer_recv);
+    c.peer_send = c.peer_recv = nullptr;
+    c.peer_bytes = 0;
+    PROBE_CHECK(hipMalloc(&c.peer_send, bytes));
+    PROBE_CHECK(hipMalloc(&c.peer_recv, bytes));
+    c.peer_bytes = bytes;
+  }
+  if (!c.peer_cnt) PROBE_CHECK(hipMalloc(&c.peer_cnt, 2 * sizeof(unsigned long long)));
+}
+
+void free_peer_bufs(DeviceCtx& c) {
+  if (c.peer_send) (void)hipFree(c.peer_send);
+  if (c.peer_recv) (void)hipFree(c.peer_recv);
+  c.peer_send = c.peer_recv = nullptr;
+  c.peer_bytes = 0;
+}
+
+// The whole xGMI ring at once (see mi355x_probe_peer_ring in probe.h): link i copies devs[i]'s send
+// window into devs[i+1]'s receive window. On an MI355X node every GPU pair has its own xGMI link, so
+// the n copies of a ring use n distinct links and run concurrently, one per source stream: the check
+// costs one copy time instead of n (a pair-at-a-time check also serialised pairs sharing a device).
+// Phases: every source fills its window (one pattern per source device), every link copies, the host
+// waits for all copies, every receiver verifies the bits that arrived. A device may appear more than
+// once (a 1-GPU box runs [0, 0]: local copies through the same code). Caller holds every device's lock.
+std::string run_peer_ring(const std::vector<int>& devs, const char* opts) {
+  const uint64_t bytes = static_cast<uint64_t>(std::max(1LL << 20, opt_int(opts, "bytes", 64LL << 20))) / 16 * 16;
+  const uint64_t n16 = bytes / 16;
+  const size_t n = devs.size();
+  std::vector<int> uniq(devs);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  for (int d : uniq) {
+    DeviceCtx& c = g_ctx[static_cast<size_t>(d)];
+    if (!c.ready) (void)run_probe(d, "{\"hbmBytes\":1048576,\"patterns\":1,\"mfma\":false}");  // streams/events
+    PROBE_CHECK(hipSetDevice(d));
+    ensure_peer_bufs(c, bytes);
+    c.peer_used = std::chrono::steady_clock::now();
+  }
+  std::vector<std::string> errs(n);
+  for (size_t i = 0; i < n; ++i) {  // peer access for every link (idempotent)
+    const int src = devs[i], dst = devs[(i + 1) % n];
+    if (src == dst) continue;
+    int can = 0;
+    PROBE_CHECK(hipDeviceCanAccessPeer(&can, src, dst));
+    if (!can) {
+      errs[i] = "hipDeviceCanAccessPeer=0";
+      continue;
+    }
+    PROBE_CHECK(hipSetDevice(src));
+    hipError_t e = hipDeviceEnablePeerAccess(dst, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) PROBE_CHECK(e);
+    (void)hipGetLastError();  // clear a sticky "already enabled"
+  }
+  auto seed_of = [](int dev) { return 0x5EED0000u + static_cast<uint32_t>(dev) * 0x9E37u; };
+  for (int d : uniq) {  // 1. each source device writes its pattern once
+    DeviceCtx& c = g_ctx[static_cast<size_t>(d)];
+    PROBE_CHECK(hipSetDevice(d));
+    const int grid = std::min<int>(c.prop.multiProcessorCount, static_cast<int>((n16 + kHbmThreads - 1) / kHbmThreads));
+    hipLaunchKernelGGL(hbm_fill, dim3(grid), dim3(kHbmThreads), 0, c.stream, static_cast<u32x4*>(c.peer_send), n16,
+                       seed_of(d), 0u);
+    PROBE_CHECK(hipGetLastError());
+    PROBE_CHECK(hipStreamSynchronize(c.stream));  // the fill is ~10 us; copies below must see it
+  }
+  // 2. all links at once, each timed on its source's stream. A source with two outgoing links
+  // (only with repeated devices) times them back to back on its one stream.
+  std::vector<hipEvent_t> t0(n, nullptr), t1(n, nullptr);
+  struct EvGuard {
+    std::vector<hipEvent_t>& a;
+    std::vector<hipEvent_t>& b;
+    ~EvGuard() {
+      for (auto* v : {&a, &b})
+        for (hipEvent_t e : *v)
+          if (e) (void)hipEventDestroy(e);
+    }
+  } guard{t0, t1};
+  for (size_t i = 0; i < n; ++i) {
+    if (!errs[i].empty()) continue;
+    const int src = devs[i], dst = devs[(i + 1) % n];
+    DeviceCtx& cs = g_ctx[static_cast<size_t>(src)];
+    DeviceCtx& cd = g_ctx[static_cast<size_t>(dst)];
+    PROBE_CHECK(hipSetDevice(src));
+    PROBE_CHECK(hipEventCreate(&t0[i]));
+    PROBE_CHECK(hipEventCreate(&t1[i]));
+    PROBE_CHECK(hipEventRecord(t0[i], cs.stream));
+    PROBE_CHECK(hipMemcpyPeerAsync(cd.peer_recv, dst, cs.peer_send, src, bytes, cs.stream));
+    PROBE_CHECK(hipEventRecord(t1[i], cs.stream));
+  }
+  for (int d : uniq) {
+    PROBE_CHECK(hipSetDevice(d));
+    PROBE_CHECK(hipStreamSynchronize(g_ctx[static_cast<size_t>(d)].stream));
+  }
+  // 3. every receiving link verifies what arrived (in link order: a receiver named twice verifies
+  // its window once per incoming link, each against that link's source pattern)
+  std::string out = "{\"bytes\":" + std::to_string(bytes) + ",\"links\":[";
+  bool all_ok = true;
+  for (size_t i = 0; i < n; ++i) {
+    const int src = devs[i], dst = devs[(i + 1) % n];
+    std::string link = "{\"src\":" + std::to_string(src) + ",\"dst\":" + std::to_string(dst);
+    if (!errs[i].empty()) {
+      link += ",\"canAccessPeer\":false,\"passed\":false,\"error\":" + jstr(errs[i]) + "}";
+      all_ok = false;
+    } else {
+      DeviceCtx& cd = g_ctx[static_cast<size_t>(dst)];
+      PROBE_CHECK(hipSetDevice(dst));
+      PROBE_CHECK(hipMemsetAsync(cd.peer_cnt, 0, sizeof(unsigned long long), cd.stream));
+      PROBE_CHECK(hipMemsetAsync(cd.peer_cnt + 1, 0xFF, sizeof(unsigned long long), cd.stream));
+      const int grid = std::min<int>(3 * cd.prop.multiProcessorCount, static_cast<int>((n16 + kHbmThreads - 1) / kHbmThreads));
+      hipLaunchKernelGGL(hbm_verify, dim3(grid), dim3(kHbmThreads), 0, cd.stream,
+                         static_cast<const u32x4*>(cd.peer_recv), n16, seed_of(src), 0u, cd.peer_cnt, cd.peer_cnt + 1);
+      PROBE_CHECK(hipGetLastError());
+      PROBE_CHECK(hipMemcpyAsync(cd.host_res, cd.peer_cnt, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 cd.stream));
+      PROBE_CHECK(hipStreamSynchronize(cd.stream));
+      const unsigned long long bad = cd.host_res[0];
+      float ms = 0;
+      PROBE_CHECK(hipSetDevice(src));
+      PROBE_CHECK(hipEventElapsedTime(&ms, t0[i], t1[i]));
+      const double gbps = ms > 0 ? static_cast<double>(bytes) / (ms * 1e-3) / 1e9 : 0.0;
+      all_ok = all_ok && bad == 0;
+      link += ",\"canAccessPeer\":true,\"passed\":" + std::string(bad == 0 ? "true" : "false") +
+              ",\"badBits\":" + std::to_string(bad) + ",\"bytes\":" + std::to_string(bytes) +
+              ",\"GBps\":" + jnum(gbps) + ",\"ms\":" + jnum(ms) + "}";
+    }
+    out += (i ? "," : "") + link;
+  }
+  return out + "],\"passed\":" + (all_ok ? "true" : "false") + "}";
+}
+
 // All free HBM minus ``reserve``, 2 MiB granular, as kSweepChunk pieces. Measured on MI355X
 // (profiles/r2h_sweep_claim_diag.txt): ~0.2 s to allocate ~282 GiB of fresh VRAM, ~6 s once the
 // driver must clear previously used VRAM; neither runs under the device lock a probe takes.
@@ -1212,6 +1352,25 @@ char* mi355x_probe_peer(int src, int dst, const char* opts_json) {
   }
 }
 
+char* mi355x_probe_peer_ring(const int* devs, int n, const char* opts_json) {
+  if (g_count < 0 || !devs || n < 2 || n > 64) return dup("{\"passed\":false,\"error\":\"bad ring\"}");
+  std::vector<int> ring(devs, devs + n);
+  for (int d : ring)
+    if (d < 0 || d >= g_count) return dup("{\"passed\":false,\"error\":\"bad device index\"}");
+  // every distinct device's probe lock, in index order (no deadlock against probes or pairs)
+  std::vector<int> uniq(ring);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (int d : uniq) locks.emplace_back(device_mutex(d));
+  try {
+    return dup(run_peer_ring(ring, opts_json));
+  } catch (const std::exception& e) {
+    (void)hipGetLastError();
+    return dup(std::string("{\"passed\":false,\"error\":") + jstr(e.what()) + "}");
+  }
+}
+
 // Frees the probe arenas idle for at least ``idle_ms`` (0: all, unconditionally); returns how many
 // were freed. With idle_ms > 0 an arena stays while its device holds an HBM sweep buffer or freed one
 // less than kSweepClearGrace ago.
@@ -1222,9 +1381,14 @@ int mi355x_probe_trim(int idle_ms) {
   for (int d = 0; d < g_count; ++d) {
     std::lock_guard<std::mutex> g(device_mutex(d));
     DeviceCtx& ctx = g_ctx[static_cast<size_t>(d)];
-    if (!ctx.arena || now - ctx.arena_used < std::chrono::milliseconds(idle_ms)) continue;
-    if (idle_ms > 0 && (!ctx.sweep.empty() || now - ctx.sweep_released < kSweepClearGrace)) continue;  // 0 = forced
+    const auto idle = std::chrono::milliseconds(idle_ms);
+    bool arena = ctx.arena && now - ctx.arena_used >= idle;
+    if (idle_ms > 0 && (!ctx.sweep.empty() || now - ctx.sweep_released < kSweepClearGrace)) arena = false;  // 0 = forced
+    const bool peer = ctx.peer_bytes && now - ctx.peer_used >= idle;  // the xGMI ring windows
+    if (!arena && !peer) continue;
     if (hipSetDevice(d) != hipSuccess) continue;
+    if (peer) free_peer_bufs(ctx);
+    if (!arena) continue;
     (void)hipFree(ctx.arena);
     ctx.arena = nullptr;
     ctx.arena_bytes = 0;

@@ -193,6 +193,28 @@ def test_peer_copy_path(hip):
         assert x["GBps"] > 10, x
 
 
+def test_peer_ring_in_one_call(hip):
+    """The concurrent ring entry point (all links at once, windows kept between calls). On a
+    1-GPU box rings of [0, 0] and [0, 0, 0] run every link as a local copy through the same code;
+    with more GPUs visible, the first four form a real xGMI ring."""
+    n = hip.init()
+    for ring in ([0, 0], [0, 0, 0]):
+        r = hip.peer_ring(ring, 32 << 20)
+        assert r["passed"] and len(r["links"]) == len(ring), r
+        for i, link in enumerate(r["links"]):
+            assert (link["src"], link["dst"]) == (ring[i], ring[(i + 1) % len(ring)])
+            assert link["passed"] and link["badBits"] == 0 and link["bytes"] == 32 << 20, link
+            assert link["GBps"] > 50, link
+    again = hip.peer_ring([0, 0], 32 << 20)  # windows reused
+    assert again["passed"], again
+    hip.trim(0)  # frees the ring windows with the arena; the next ring allocates them again
+    assert hip.peer_ring([0, 0], 16 << 20)["passed"]
+    if n > 1:
+        ring = list(range(min(n, 4)))
+        r = hip.peer_ring(ring, 64 << 20)
+        assert r["passed"] and all(x["GBps"] > 10 for x in r["links"]), r
+
+
 def test_probe_arena_reused_then_trimmed(hip):
     """The ~1.2 GiB probe arena is kept between back-to-back probes (no hipMalloc on the claim
     path) and handed back by trim(); a probe after a trim allocates again and still passes."""

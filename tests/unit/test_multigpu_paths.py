@@ -115,6 +115,56 @@ def test_peer_ring_maps_each_link_to_its_sender(devices):
         assert r["passed"] is (i != 3), (i, r)
 
 
+class RingStub(StubHip):
+    """A library with mi355x_probe_peer_ring: one call for the whole ring."""
+
+    def __init__(self, *a, broken: bool = False, **kw):
+        super().__init__(*a, **kw)
+        self.broken = broken
+
+    def peer_ring(self, ords: list[int], nbytes: int):
+        self.calls.append(("ring", len(ords), nbytes))
+        self.ring_ords = list(ords)
+        if self.broken:
+            return {"passed": False, "error": "hipMemcpyPeerAsync: invalid argument"}
+        links = []
+        for i, a in enumerate(ords):
+            b = ords[(i + 1) % len(ords)]
+            ok = (a, b) not in self.bad_links
+            links.append({"src": a, "dst": b, "passed": ok, "badBits": 0 if ok else 3,
+                          "GBps": 110.0, "ms": 0.6, "bytes": nbytes})
+        return {"bytes": nbytes, "links": links, "passed": all(x["passed"] for x in links)}
+
+
+def test_peer_ring_runs_as_one_concurrent_library_call(devices):
+    """With the ring entry point the prober issues ONE call (all links concurrently in the
+    library) and maps link i to its sender; pairwise calls are not made."""
+    stub = RingStub(ms=1, bad_links={(5, 6)})
+    p = inproc_prober(stub, devices)
+    try:
+        links = p.peer_ring(devices, {"xgmiBytes": 8 << 20})
+    finally:
+        p.close()
+    assert [c for c in stub.calls if c[0] == "ring"] == [("ring", 8, 8 << 20)]
+    assert not [c for c in stub.calls if c[0] == "peer"]
+    assert stub.ring_ords == [d["index"] for d in devices]
+    by_index = {d["uuid"]: d["index"] for d in devices}
+    for u, r in links.items():
+        i = by_index[u]
+        assert r["peer"] == devices[(i + 1) % 8]["uuid"] and r["passed"] is (i != 5), (i, r)
+
+
+def test_peer_ring_library_error_fails_every_link(devices):
+    stub = RingStub(ms=1, broken=True)
+    p = inproc_prober(stub, devices[:4])
+    try:
+        links = p.peer_ring(devices[:4], {})
+    finally:
+        p.close()
+    assert len(links) == 4
+    assert all(not r["passed"] and "invalid argument" in r["error"] for r in links.values())
+
+
 def test_peer_ring_failure_fails_the_right_gpus_probe(tmp_path, native_built):
     """Through the agent: an injected link failure on GPU 2's outgoing link (overlay
     xgmiPeerFail) fails GPU 2's claim-time probe with XGMIPeerCheckFailed, nothing else."""
