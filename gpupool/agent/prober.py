@@ -173,7 +173,8 @@ class Prober:
         n = len(devs)
         if n < 2 or self.mode not in ("inproc", "simulated"):
             return {}
-        nbytes = int(opts.get("xgmiBytes") or (64 << 20))
+        # 16 MiB per link: ~0.25 ms over one xGMI link, enough for a stable GB/s figure
+        nbytes = int(opts.get("xgmiBytes") or (16 << 20))
         if self.mode == "inproc":
             ring = self._ring_inproc(devs, nbytes)
             if ring is not None:
