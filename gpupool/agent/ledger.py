@@ -129,6 +129,9 @@ class Ledger:
 
     def flush(self, upto: int | None = None) -> None:
         """Make everything up to sequence ``upto`` (default: all) durable."""
+        with self._mu:  # already on disk: do not queue behind a writer busy with a newer state
+            if upto is not None and self._written >= upto:
+                return
         with self._wmu:
             with self._mu:
                 want = self._seq if upto is None else upto
