@@ -6,7 +6,7 @@ GPUCTL  := bin/gpuctl
 IMG     ?= gpupool:dev
 JOBS    ?= 8
 
-.PHONY: all manifests generate native build test test-gpu sanitize install run bench smoke \
+.PHONY: all manifests generate native build test test-gpu sanitize install run run-manager bench smoke \
         docker-build docker-push deploy undeploy fixtures clean
 
 all: manifests native
@@ -43,6 +43,14 @@ BACKEND ?= fake
 NODES   ?= 1
 run: native
 	$(PY) scripts/run_local.py --backend $(BACKEND) --nodes $(NODES)
+
+## run-manager: only the operator, against the cluster of the current kubeconfig / in-cluster
+## config (the reference's `make run`, README.md:259-263). CLOUD=fake|azure-arm selects the
+## AzureVmPool backend; KINDS the reconcilers.
+CLOUD ?= fake
+KINDS ?= mi355x,azure,job
+run-manager: native
+	build/native/gpupool-manager --cloud $(CLOUD) --kinds $(KINDS)
 
 ## bench: headline metric (p50 reconcile-to-Ready + readyReplicas accuracy)
 GPUS ?= 1
