@@ -154,6 +154,8 @@ def main() -> int:
                     help="agent full-telemetry sample period (s)")
     ap.add_argument("--scale-down-steps", type=int, default=3, help="config 4 repetitions (0 = skip)")
     ap.add_argument("--pool-steps", type=int, default=3, help="config 5 repetitions (0 = skip)")
+    ap.add_argument("--azure-steps", type=int, default=3,
+                    help="config 1 (AzureVmPool replicas=0 -> Ready) repetitions (0 = skip)")
     ap.add_argument("--health-steps", type=int, default=5,
                     help="fault->condition measurements (0 = skip)")
     ap.add_argument("--comm-check", default="auto", choices=["auto", "gloo", "off"],
@@ -229,6 +231,12 @@ def main() -> int:
                 "cross_pool_devices": sum(x["crossPoolDevices"] for x in tp)}
         elif args.pool_steps > 0:
             secondary["two_pools"] = {"skipped": "needs >= 2 GPUs (two pools of N//2)"}
+        if args.azure_steps > 0:
+            az = [run.azure_pool(i) for i in range(args.azure_steps)]
+            secondary["azure_config1"] = {
+                **summary([x["seconds"] for x in az], sum(x["ok"] for x in az)),
+                "delete_p50_s": round(statistics.median(x["deleteSeconds"] for x in az), 4),
+                "replicas": 0, "cloud": "in-process fake cloud"}
         health = run.health(pool, args.health_steps) if args.health_steps > 0 else {}
         try:
             agent_stats = run.agent_stats()
@@ -287,7 +295,8 @@ def main() -> int:
             "dtype": "bf16",
             "data": src + "; control plane against the in-repo apiserver-sim (no kube-apiserver/etcd)",
             "config": {
-                "model": "Mi355xPool scale 0->n, n in %s (BASELINE configs 2/3/4/5)" % sweep,
+                "model": "Mi355xPool scale 0->n, n in %s (BASELINE configs 2/3/4/5; config 1 in "
+                         "azure_config1)" % sweep,
                 "global_batch": n,
                 "seq_len": 0,
                 "parallelism": f"replicas{n}",

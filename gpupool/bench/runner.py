@@ -23,7 +23,7 @@ import statistics
 import time
 from dataclasses import dataclass, field
 
-from ..kube import MI355XPOOLS, PODS, KubeError
+from ..kube import AZUREVMPOOLS, MI355XPOOLS, PODS, SECRETS, KubeError
 from . import ground_truth as gt
 
 
@@ -237,6 +237,50 @@ class BenchRun:
         self.delete_pool(b["metadata"]["name"])
         return {"pools": [half, half], "seconds": dt, "ok": ok, "crossPoolDevices": len(ua & ub),
                 "truth": {"a": ta, "b": tb}}
+
+    # ------------------------------------------------------------ config 1
+    def azure_pool(self, step: int, replicas: int = 0) -> dict:
+        """BASELINE config 1: an AzureVmPool (the reference's own kind) created from scratch on the
+        same manager with the in-process cloud: create -> Ready (finalizer added, credentials
+        resolved, VMs listed by tag), then delete -> gone (finalizer-guarded cleanup)."""
+        import base64
+        if step == 0:
+            data = {k: base64.b64encode(v.encode()).decode() for k, v in {
+                "AZURE_CLIENT_ID": "00000000-0000-0000-0000-000000000001",
+                "AZURE_CLIENT_SECRET": "bench", "AZURE_TENANT_ID": "00000000-0000-0000-0000-000000000002",
+                "AZURE_SUBSCRIPTION_ID": "00000000-0000-0000-0000-000000000003"}.items()}
+            try:
+                self.c.create(SECRETS, {"apiVersion": "v1", "kind": "Secret",
+                                        "metadata": {"name": "azure-credentials"}, "data": data},
+                              self.ns)
+            except KubeError as e:
+                if e.code != 409:
+                    raise
+        name = f"az-bench-{step}"
+        body = {"apiVersion": "compute.my.domain/v1alpha1", "kind": "AzureVmPool",
+                "metadata": {"name": name},
+                "spec": {"replicas": replicas, "resourceGroupName": "bench-rg", "location": "eastus",
+                         "vmSize": "Standard_ND_MI300X_v5", "vnetName": "vnet", "subnetName": "default",
+                         "imageReference": {"publisher": "Canonical", "offer": "ubuntu-24_04-lts",
+                                            "sku": "server", "version": "latest"},
+                         "azureCredentialSecret": "azure-credentials"}}
+
+        def ready(o):
+            st = (o or {}).get("status") or {}
+            c = {x["type"]: x for x in st.get("conditions", [])}
+            return bool(o) and st.get("observedGeneration") == o["metadata"]["generation"] and \
+                st.get("readyReplicas", 0) == replicas and len(st.get("vms") or []) == replicas and \
+                c.get("Ready", {}).get("status") == "True"
+        t0 = time.perf_counter()
+        self.c.create(AZUREVMPOOLS, body, self.ns)
+        o = self.c.wait_for(AZUREVMPOOLS, name, self.ns, ready, timeout=self.timeout)
+        t_ready = time.perf_counter() - t0
+        fin = "compute.my.domain/device-release" in (o["metadata"].get("finalizers") or [])
+        t1 = time.perf_counter()
+        self.c.delete(AZUREVMPOOLS, name, self.ns)
+        self.c.wait_for(AZUREVMPOOLS, name, self.ns, lambda x: x is None, timeout=self.timeout)
+        return {"seconds": t_ready, "deleteSeconds": time.perf_counter() - t1,
+                "ok": fin and o["status"]["readyReplicas"] == replicas}
 
     def agent_stats(self) -> dict:
         """The agent's own counters (gpupool_agent_*): sample / health-poll cost, events."""
