@@ -59,6 +59,8 @@ def test_bench_gpus1_contract(native_built):
     assert cfg["scale_down"]["from"] == 1 and cfg["scale_down"]["to"] == 0
     assert cfg["scale_down"]["accuracy"] == 1.0
     assert "skipped" in cfg["two_pools"]
+    az = cfg["azure_config1"]  # BASELINE config 1 on the same manager
+    assert az["replicas"] == 0 and az["accuracy"] == 1.0 and az["p50_s"] < 30
 
 
 def test_bench_under_torchrun_two_ranks_with_comm_check(native_built):
