@@ -32,6 +32,14 @@ from ..ops import devlib
 from .ledger import Ledger
 from .prober import Prober, default_mode
 
+SLOT_SEP = "::"  # device-plugin ID of a time-sliced slot: "<uuid>::<slot>"
+
+
+def gpu_of(device_id: str) -> str:
+    """The GPU uuid behind a device-plugin ID (a plain uuid, or a shared GPU's slot)."""
+    return device_id.split(SLOT_SEP, 1)[0]
+
+
 log = logging.getLogger("gpupool.agent")
 
 
@@ -573,7 +581,9 @@ class Agent:
                 self._stop.wait(self.cfg.pod_watch_interval)
 
     def _refresh_pods(self) -> dict[str, list[dict]]:
-        pods = self._podres.list_pod_devices()
+        pods: dict[str, list[dict]] = {}
+        for did, ps in self._podres.list_pod_devices().items():
+            pods.setdefault(gpu_of(did), []).extend(ps)  # a shared GPU's slots -> the GPU
         with self.lock:
             old = self._pods_cache[1]
             self._pods_cache = (time.monotonic(), pods)
@@ -912,15 +922,31 @@ class Agent:
         return {"ok": True, "updated": len(changed)}
 
     # ================================================================ device plugin glue
+    @staticmethod
+    def _slots_of(rec: dict) -> int:
+        """spec.sharing.replicasPerGPU of the record's pool (time-sliced slots per GPU)."""
+        try:
+            return max(1, int(((rec.get("policy") or {}).get("sharing") or {})
+                              .get("replicasPerGPU") or 1))
+        except (TypeError, ValueError):
+            return 1
+
     def plugin_devices(self, resource: str) -> list[dict]:
+        """The device-plugin view of ``resource``: one entry per advertised device ID. A GPU of a
+        pool with ``sharing.replicasPerGPU`` = K is K IDs ``<uuid>::<slot>``, all with the GPU's
+        health (HAMi / time-slicing style: the kubelet places up to K pods on it)."""
         with self.lock:
             out = []
             for u, rec in sorted(self.records.items(),
                                  key=lambda kv: self.by_uuid.get(kv[0], {}).get("index", 99)):
                 if rec.get("resourceName", schema.DEFAULT_RESOURCE) != resource:
                     continue
-                out.append({"uuid": u, "advertisable": self._advertisable(u),
-                            "numa": self.by_uuid.get(u, {}).get("numa")})
+                k = self._slots_of(rec)
+                ok = self._advertisable(u)
+                numa = self.by_uuid.get(u, {}).get("numa")
+                for i in range(k):
+                    out.append({"id": u if k == 1 else f"{u}{SLOT_SEP}{i}", "uuid": u,
+                                "advertisable": ok, "numa": numa})
             return out
 
     def mark_advertised(self, resource: str, healthy: set[str] | None) -> None:
@@ -975,6 +1001,16 @@ class Agent:
             p.notify()
 
     def preferred(self, resource: str, available: list[str], must: list[str], size: int) -> list[str]:
+        if any(SLOT_SEP in i for i in available + must):
+            # shared GPUs: a pod's slots go to as few GPUs as possible, lowest index first
+            with self.lock:
+                idx = {u: self.by_uuid.get(u, {}).get("index", 99) for u in
+                       {gpu_of(i) for i in available + must}}
+            def key(i: str) -> tuple[int, int]:
+                u, _, slot = i.partition(SLOT_SEP)
+                return idx.get(u, 99), int(slot or 0)
+            rest = sorted((i for i in available if i not in must), key=key)
+            return list(must) + rest[:max(0, size - len(must))]
         with self.lock:
             idx = {u: self.by_uuid[u]["index"] for u in available + must if u in self.by_uuid}
             inv = {v: k for k, v in idx.items()}
@@ -990,6 +1026,8 @@ class Agent:
         return list(must) + [inv[i] for i in sel]
 
     def allocate_spec(self, resource: str, ids: list[str]) -> dict:
+        slots = list(ids)
+        ids = list(dict.fromkeys(gpu_of(i) for i in ids))  # slots of shared GPUs -> the GPUs
         for u in ids:  # a pod never starts while the HBM scrubber still frees its buffer
             if not self.scrubber.wait_released(u):
                 raise ValueError(f"device {u}: HBM scrub buffer still being released")
@@ -1017,6 +1055,8 @@ class Agent:
                     "GPUPOOL_NUM_GPUS": str(len(ids)),
                     "PET_NPROC_PER_NODE": str(len(ids)),
                     "GPUPOOL_NODE": self.cfg.node}
+            if slots != ids:  # time-sliced: the pod shares these GPUs with other pods
+                envs["GPUPOOL_GPU_SLOTS"] = ",".join(slots)
             return {"envs": envs, "devices": ["/dev/kfd"] + render,
                     "annotations": {schema.ANN_POD_DEVICES: ",".join(ids)}}
 

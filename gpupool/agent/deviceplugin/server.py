@@ -137,7 +137,7 @@ class DevicePluginServer:
         healthy = set()
         for d in self.agent.plugin_devices(self.resource):
             dev = resp.devices.add()
-            dev.ID = d["uuid"]
+            dev.ID = d.get("id") or d["uuid"]
             dev.health = "Healthy" if d["advertisable"] else "Unhealthy"
             if d.get("numa") is not None:
                 dev.topology.nodes.add().ID = int(d["numa"])

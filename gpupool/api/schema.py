@@ -213,6 +213,19 @@ MI355X_SPEC = {
                            "default": "Any"},
             },
         },
+        "sharing": {
+            "type": "object",
+            "default": {},
+            "description": "Time-sliced GPU sharing (the HAMi / NVIDIA time-slicing analogue of "
+                           "the reference platform, GPU调度平台搭建.md:289-298): every GPU of the "
+                           "pool is advertised as replicasPerGPU devices of resourceName, so that "
+                           "many pods share it. No memory or compute isolation between them (use "
+                           "CPX partitions for that); a GPU is drained and released only when "
+                           "every pod on any of its slots is gone.",
+            "properties": {
+                "replicasPerGPU": {**_I32, "minimum": 1, "maximum": 64, "default": 1},
+            },
+        },
         "health": {
             "type": "object",
             "default": {},
@@ -315,6 +328,8 @@ MI355X_STATUS = {
         "nodes": {"type": "array", "items": _S,
                   "description": "Every node holding GPUs of the pool (maxNodes > 1)."},
         "selector": _S,
+        "allocatable": {**_I32, "description": "Devices of resourceName the ready GPUs offer "
+                                                "(readyReplicas x sharing.replicasPerGPU)."},
         "devices": {"type": "array", "items": DEVICE_STATUS},
         "conditions": CONDITIONS_FIELD,
         "lastReconcileTime": _S,

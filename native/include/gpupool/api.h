@@ -69,6 +69,7 @@ struct Mi355xPoolSpec {
   Json probe_json() const;            // the probe options sent with claims and policy updates
   std::string replace_policy = "Replace";
   int32_t max_nodes = 1;  // nodes the pool may span
+  int32_t sharing_replicas = 1;  // time-sliced slots advertised per GPU (spec.sharing.replicasPerGPU)
   bool autoscale = false;  // demand-driven spec.replicas (Mi355xPoolAutoscaler)
   int32_t autoscale_min = 0, autoscale_max = 8;
   int64_t scale_down_delay_seconds = 300;

@@ -86,6 +86,7 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.probe_min_xgmi_gbps = pr["minXgmiGBps"].as_double(0);
   p.replace_policy = s["replacePolicy"].str_or("Replace");
   p.max_nodes = static_cast<int32_t>(s["maxNodes"].as_int(1));
+  p.sharing_replicas = static_cast<int32_t>(std::max<int64_t>(1, s.path("sharing.replicasPerGPU").as_int(1)));
   const Json& a = s["autoscale"];
   p.autoscale = a["enabled"].as_bool(false);
   p.autoscale_min = static_cast<int32_t>(a["minReplicas"].as_int(0));
@@ -113,6 +114,7 @@ Json Mi355xPoolSpec::policy_json() const {
   j["partition"]["compute"] = partition_compute;
   j["partition"]["memory"] = partition_memory;
   j["probe"] = probe_json();  // re-probe settings live with the claim (agent-side recheck)
+  if (sharing_replicas > 1) j["sharing"]["replicasPerGPU"] = sharing_replicas;  // device-plugin slots
   return j;
 }
 
@@ -246,6 +248,11 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
   if (s.contains("maxNodes")) {
     int64_t v = s["maxNodes"].as_int(0);
     if (!s["maxNodes"].is_int() || v < 1 || v > 64) errs.push_back("spec.maxNodes: must be within [1, 64]");
+  }
+  if (s.path("sharing").contains("replicasPerGPU")) {
+    const Json& r = s.path("sharing.replicasPerGPU");
+    if (!r.is_int() || r.as_int(0) < 1 || r.as_int(0) > 64)
+      errs.push_back("spec.sharing.replicasPerGPU: must be within [1, 64]");
   }
   const Json& h = s["health"];
   if (h.contains("thermal") && !in(h["thermal"].as_string(), {"belowCritical", "belowEmergency", "ignore"}))

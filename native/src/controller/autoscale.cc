@@ -106,11 +106,13 @@ int64_t Mi355xPoolAutoscaler::pool_demand(const std::vector<Json>& pods, const s
     if (!q.path("metadata.deletionTimestamp").as_string().empty()) continue;
     const std::string qns = q.path("metadata.namespace").as_string(), qname = q.path("metadata.name").as_string();
     const int64_t expl = explicit_of(qns, qname);
+    // capacities in devices of the resource: a shared GPU offers sharing.replicasPerGPU of them
+    const int64_t k = std::max<int64_t>(1, q.path("spec.sharing.replicasPerGPU").as_int(1));
     if (q.path("spec.autoscale.enabled").as_bool(false)) {
       const int64_t hi = std::max(q.path("spec.autoscale.minReplicas").as_int(0), q.path("spec.autoscale.maxReplicas").as_int(0));
-      autos.push_back({qns, qname, std::max<int64_t>(0, hi - expl), expl});
+      autos.push_back({qns, qname, std::max<int64_t>(0, hi * k - expl), expl});
     } else {
-      remaining -= std::max<int64_t>(0, q.path("spec.replicas").as_int(0) - expl);
+      remaining -= std::max<int64_t>(0, q.path("spec.replicas").as_int(0) * k - expl);
     }
   }
   remaining = std::max<int64_t>(0, remaining);
@@ -140,7 +142,9 @@ Outcome Mi355xPoolAutoscaler::reconcile(const std::string& ns, const std::string
   }
   const int64_t d = pool_demand(pods_.list(), jobs_.list(), pools_.list(), m.ns, m.name, spec.resource_name);
   const int64_t lo = spec.autoscale_min, hi = std::max(spec.autoscale_min, spec.autoscale_max);
-  const int64_t target = std::clamp(d, lo, hi);
+  // demand is in devices of the resource; a shared GPU (sharing.replicasPerGPU = K) serves K of them
+  const int64_t k = std::max<int32_t>(1, spec.sharing_replicas);
+  const int64_t target = std::clamp((d + k - 1) / k, lo, hi);
   demand_gauge().set({{"pool", m.key()}}, static_cast<double>(d));
   const auto now = std::chrono::steady_clock::now();
   ms wait{0};

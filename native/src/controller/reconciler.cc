@@ -489,6 +489,7 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
   }
   st["replicas"] = claimed;
   st["readyReplicas"] = ready;
+  st["allocatable"] = ready * static_cast<int64_t>(spec.sharing_replicas);  // slots of resourceName
   if (!o.node.empty()) st["nodeName"] = o.node;
   if (o.nodes.size() > 1 || spans_(spec)) {
     Json ns = Json::array();
@@ -890,8 +891,10 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
 
 // Per-namespace GPU quota (the reference's ResourceQuota practice,
 // GPU调度平台搭建.md:802): a ResourceQuota with spec.hard["<resourceName>"] or
-// spec.hard["requests.<resourceName>"] caps the GPUs all pools of that resource in the namespace
-// may claim. Usage = status.replicas of the other pools (informer cache) + our claimed + delta.
+// spec.hard["requests.<resourceName>"] caps the devices of that resource all pools in the namespace
+// may offer, in the resource's own units like the pods' requests it also bounds: a GPU counts once,
+// a shared GPU (spec.sharing.replicasPerGPU = K) K times. Usage = status.replicas x K of the pools
+// (informer cache, ours included) + delta x K.
 bool Mi355xPoolReconciler::quota_allows_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta,
                                          std::string* why) {
   trace::Span span("quota");
@@ -925,11 +928,12 @@ bool Mi355xPoolReconciler::quota_allows_(const ObjectMeta& m, const Mi355xPoolSp
   for (const auto& p : pools_.list()) {
     if (p.path("metadata.namespace").as_string() != m.ns) continue;
     if (p.path("spec.resourceName").str_or(gen::kDefaultResource) != spec.resource_name) continue;
-    used += p.path("status.replicas").as_int(0);
+    used += p.path("status.replicas").as_int(0) * std::max<int64_t>(1, p.path("spec.sharing.replicasPerGPU").as_int(1));
   }
-  if (used + delta <= hard) return true;
+  const int64_t more = static_cast<int64_t>(delta) * spec.sharing_replicas;
+  if (used + more <= hard) return true;
   *why = "ResourceQuota " + m.ns + "/" + qname + " allows " + std::to_string(hard) + " " + spec.resource_name +
-         "; " + std::to_string(used) + " in use, " + std::to_string(delta) + " more requested";
+         "; " + std::to_string(used) + " in use, " + std::to_string(more) + " more requested";
   return false;
 }
 

@@ -1,0 +1,104 @@
+"""Time-sliced GPU sharing (spec.sharing.replicasPerGPU): the HAMi / time-slicing analogue of the
+reference platform's GPU-sharing layer (GPU调度平台搭建.md:289-298). Each GPU of the pool is
+advertised as K device IDs, so K pods share it; drain and release still act per GPU."""
+from __future__ import annotations
+
+import pytest
+
+from gpupool.agent.agent import gpu_of
+from gpupool.kube import MI355XPOOLS, NODES, PODS
+
+from .helpers import mi_pool, pause_pod, wait_ready
+
+pytestmark = pytest.mark.slow
+
+
+def running(o):
+    return bool(o) and o["status"].get("phase") == "Running"
+
+
+def test_shared_gpus_hold_k_pods_each_and_drain_per_gpu(cluster_factory):
+    c = cluster_factory()
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("shared", 2, sharing={"replicasPerGPU": 4},
+                                  drain={"gracePeriodSeconds": 1}), "default")
+    o = wait_ready(k, "shared", 2)
+    assert o["status"]["allocatable"] == 8 and o["status"]["readyReplicas"] == 2
+    gpus = {d["uuid"]: d["index"] for d in o["status"]["devices"]}
+    k.wait_for(NODES, "mi355x-node-0", None, lambda n: (n["status"].get("allocatable") or {})
+               .get("amd.com/gpu") == "8", timeout=20)
+    for i in range(8):
+        k.create(PODS, pause_pod(f"s{i}"), "default")
+    for i in range(8):
+        k.wait_for(PODS, f"s{i}", "default", running, timeout=30)
+    # a ninth pod does not fit: 2 GPUs x 4 slots
+    k.create(PODS, pause_pod("s8"), "default")
+    p9 = k.wait_for(PODS, "s8", "default",
+                    lambda p: p and p["status"].get("phase") in ("Pending", "Failed"), timeout=10)
+    assert p9["status"].get("phase") != "Running"
+    k.delete(PODS, "s8", "default", grace=0)
+    by_gpu: dict[str, list[str]] = {}
+    for i in range(8):
+        slot = k.get(PODS, f"s{i}", "default")["metadata"]["annotations"]["gpupool.amd.com/devices"]
+        by_gpu.setdefault(gpu_of(slot), []).append(f"s{i}")
+    assert sorted(len(v) for v in by_gpu.values()) == [4, 4] and set(by_gpu) == set(gpus)
+    # the agent sees every slot's pod on its GPU
+    view = {d["uuid"]: d for d in c.agent_request("mi355x-node-0", "GET", "/v1/node")["devices"]}
+    assert all(len(view[u]["pods"]) == 4 for u in gpus)
+
+    # scale 2 -> 1: the victim (highest index) GPU's four pods are evicted, the other four stay
+    victim = max(gpus, key=gpus.get)
+    k.patch(MI355XPOOLS, "shared", {"spec": {"replicas": 1}}, "default")
+    o = wait_ready(k, "shared", 1, timeout=60)
+    assert [d["uuid"] for d in o["status"]["devices"]] == [u for u in gpus if u != victim]
+    assert o["status"]["allocatable"] == 4
+    left = {p["metadata"]["name"] for p in k.list(PODS, "default")["items"]
+            if not p["metadata"].get("deletionTimestamp")}
+    assert left == set(by_gpu[min(gpus, key=gpus.get)])
+    k.wait_for(NODES, "mi355x-node-0", None, lambda n: (n["status"].get("allocatable") or {})
+               .get("amd.com/gpu") == "4", timeout=20)
+
+
+def test_sharing_slots_in_allocate(tmp_path, native_built):
+    """Allocate of slots maps back to the GPUs: one ROCR_VISIBLE_DEVICES entry per GPU however
+    many of its slots a pod got; preferred allocation packs a pod's slots onto one GPU."""
+    from gpupool.agent.agent import Agent, AgentConfig
+    from gpupool.testing.cluster import FIXTURE
+    a = Agent(AgentConfig(node="n0", backend="fake", fixture=FIXTURE, state_dir=str(tmp_path / "s"),
+                          probe_mode="simulated", probe_sim_ms=1, fsync=False, scrub_interval_s=0))
+    try:
+        r = a.claim({"poolUID": "p", "pool": "default/p", "count": 2, "resourceName": "amd.com/gpu",
+                     "policy": {"sharing": {"replicasPerGPU": 3}}, "probe": {"enabled": True}})
+        assert r["ok"]
+        devs = a.plugin_devices("amd.com/gpu")
+        assert len(devs) == 6 and all("::" in d["id"] for d in devs)
+        u0, u1 = sorted({d["uuid"] for d in devs}, key=lambda u: a.by_uuid[u]["index"])
+        spec = a.allocate_spec("amd.com/gpu", [f"{u0}::0", f"{u0}::2"])
+        assert spec["envs"]["GPUPOOL_DEVICE_UUIDS"] == u0 and spec["envs"]["GPUPOOL_NUM_GPUS"] == "1"
+        assert spec["envs"]["ROCR_VISIBLE_DEVICES"].count(",") == 0
+        assert spec["envs"]["GPUPOOL_GPU_SLOTS"] == f"{u0}::0,{u0}::2"
+        avail = [d["id"] for d in devs]
+        assert a.preferred("amd.com/gpu", list(reversed(avail)), [], 2) == [f"{u0}::0", f"{u0}::1"]
+        # one ID per GPU without sharing
+        a.update_policy("p", {}, "amd.com/gpu")
+        assert [d["id"] for d in a.plugin_devices("amd.com/gpu")] == [u0, u1]
+    finally:
+        a.stop()
+
+
+def test_autoscaled_shared_pool_counts_slots(cluster_factory):
+    """Autoscaling a shared pool: demand is in devices of the resource (slots), so 6 pending pods
+    on a pool of 4 slots per GPU need ceil(6/4) = 2 GPUs, not 6."""
+    k = cluster_factory().client
+    res = "amd.com/gpu-shared"
+    k.create(MI355XPOOLS, mi_pool("sa", 0, resourceName=res, sharing={"replicasPerGPU": 4},
+                                  autoscale={"enabled": True, "minReplicas": 0, "maxReplicas": 8,
+                                             "scaleDownDelaySeconds": 60}), "default")
+    wait_ready(k, "sa", 0)
+    for i in range(6):
+        k.create(PODS, pause_pod(f"a{i}", resource=res), "default")
+    o = wait_ready(k, "sa", 2)
+    assert o["status"]["allocatable"] == 8
+    for i in range(6):
+        k.wait_for(PODS, f"a{i}", "default", running, timeout=30)
+    assert k.get(MI355XPOOLS, "sa", "default")["spec"]["replicas"] == 2

@@ -67,6 +67,9 @@ CASES = [
     {"kind": "Mi355xPool", "spec": {"replicas": 12, "maxNodes": 2}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "maxNodes": 0}},
     {"kind": "Mi355xPool", "spec": {"replicas": 1, "maxNodes": 65}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 2, "sharing": {"replicasPerGPU": 4}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 2, "sharing": {"replicasPerGPU": 0}}},
+    {"kind": "Mi355xPool", "spec": {"replicas": 2, "sharing": {"replicasPerGPU": 65}}},
     {"kind": "AzureVmPool", "spec": {"replicas": 0, "resourceGroupName": "rg", "location": "e",
                                      "vmSize": "s", "vnetName": "v", "subnetName": "s",
                                      "azureCredentialSecret": "c",
