@@ -303,3 +303,38 @@ def test_rccl_check_harness_on_real_gpu():
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     out = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
     assert out["exact"] and out["backend"] == "nccl" and out["world"] == 1
+
+
+def test_time_sliced_pods_share_the_real_gpu(cluster_factory):
+    """spec.sharing.replicasPerGPU on hardware: the one MI355X is advertised as 3 slots and three
+    pods compute on it at the same time (each a torch matmul loop through the ROCR_VISIBLE_DEVICES
+    the plugin handed it), all seeing the same GPU."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    k = c.client
+    k.create(MI355XPOOLS, pool("shared", 1, sharing={"replicasPerGPU": 3}), "default")
+    obj = k.wait_for(MI355XPOOLS, "shared", "default", ready_at(1), timeout=60)
+    assert obj["status"]["allocatable"] == 3
+    hip_uuid = obj["status"]["devices"][0]["hipUUID"]
+    code = ("import json, os, time, torch\n"
+            "x = torch.randn(2048, 2048, device='cuda', dtype=torch.bfloat16)\n"
+            "t0 = time.time(); n = 0\n"
+            "while time.time() - t0 < 3: x = (x @ x).clamp_(-1, 1); n += 1\n"
+            "torch.cuda.synchronize()\n"
+            "print(json.dumps({'rocr': os.environ.get('ROCR_VISIBLE_DEVICES'), 'iters': n,"
+            " 'slots': os.environ.get('GPUPOOL_GPU_SLOTS'),"
+            " 'arch': torch.cuda.get_device_properties(0).gcnArchName}))\n")
+    for i in range(3):
+        k.create(PODS, {"metadata": {"name": f"share{i}"}, "spec": {"restartPolicy": "Never",
+                        "containers": [{"name": "c", "command": ["python", "-c", code],
+                                        "resources": {"limits": {"amd.com/gpu": 1}}}]}}, "default")
+    outs = []
+    for i in range(3):
+        done = k.wait_for(PODS, f"share{i}", "default",
+                          lambda o: o and o.get("status", {}).get("phase") in ("Succeeded", "Failed"),
+                          timeout=240)
+        log = open(done["metadata"]["annotations"]["gpupool.amd.com/log-path"]).read()
+        assert done["status"]["phase"] == "Succeeded", log[-3000:]
+        outs.append(json.loads([x for x in log.splitlines() if x.startswith("{")][-1]))
+    assert all(o["rocr"] == hip_uuid and o["arch"].startswith("gfx950") and o["iters"] > 0
+               for o in outs), outs
+    assert len({o["slots"] for o in outs}) == 3  # three different slots of the one GPU
