@@ -106,6 +106,10 @@ BUILTINS = [
                  status_sub=True),
     ResourceType("networking.k8s.io", "v1", "networkpolicies", "NetworkPolicy", True,
                  "networkpolicy", ["netpol"]),
+    ResourceType("", "v1", "persistentvolumes", "PersistentVolume", False, "persistentvolume",
+                 ["pv"], status_sub=True),
+    ResourceType("", "v1", "persistentvolumeclaims", "PersistentVolumeClaim", True,
+                 "persistentvolumeclaim", ["pvc"], status_sub=True),
     ResourceType("rbac.authorization.k8s.io", "v1", "clusterroles", "ClusterRole", False,
                  "clusterrole"),
     ResourceType("rbac.authorization.k8s.io", "v1", "clusterrolebindings", "ClusterRoleBinding",

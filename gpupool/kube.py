@@ -77,6 +77,8 @@ BY_KIND = {
     "DaemonSet": Res("apps", "v1", "daemonsets"),
     "PodDisruptionBudget": Res("policy", "v1", "poddisruptionbudgets"),
     "NetworkPolicy": Res("networking.k8s.io", "v1", "networkpolicies"),
+    "PersistentVolume": Res("", "v1", "persistentvolumes", namespaced=False),
+    "PersistentVolumeClaim": Res("", "v1", "persistentvolumeclaims"),
 }
 
 

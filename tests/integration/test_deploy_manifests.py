@@ -132,3 +132,19 @@ def test_azure_overlay_flags_are_manager_flags(native_built):
     r = subprocess.run([native_bin("gpupool-manager"), *args, "--help"], capture_output=True,
                        text=True, timeout=30)
     assert r.returncode == 0, r.stderr
+
+
+def test_every_sample_applies(cluster_factory):
+    """Every manifest under config/samples passes admission (CRD schemas, built-in kinds incl. the
+    NFS workspace PersistentVolume/Claim) on the apiserver simulator."""
+    import glob
+    c = cluster_factory(nodes=[], manager=False)
+    files = sorted(glob.glob(os.path.join(ROOT, "config", "samples", "*.yaml")))
+    assert files
+    for f in files:
+        r = _gpuctl(c.url, "apply", "-f", f)
+        assert r.returncode == 0, (f, r.stdout, r.stderr)
+    pvc = c.client.get(BY_KIND["PersistentVolumeClaim"], "workspace", "default")
+    assert pvc["spec"]["volumeName"] == "gpupool-workspace"
+    job = c.client.get(BY_KIND["Mi355xJob"], "fmnist-ddp", "default")
+    assert job["spec"]["checkpointDir"].startswith("/workspace/")
