@@ -88,6 +88,7 @@ class FakeKubelet:
         # once must not land an older snapshot after a newer one
         self.status_lock = threading.Lock()
         self.stop_ev = threading.Event()
+        self._sched_kick = threading.Event()  # unscheduled pod seen or capacity changed
         self.threads: list[threading.Thread] = []
         self.reg_server: grpc.Server | None = None
         self.pr_server: grpc.Server | None = None
@@ -119,9 +120,11 @@ class FakeKubelet:
             t.start()
             self.threads.append(t)
         if self.schedule:
-            t = threading.Thread(target=self._scheduler_loop, daemon=True, name="scheduler")
-            t.start()
-            self.threads.append(t)
+            for fn, name in ((self._scheduler_loop, "scheduler"),
+                             (self._unscheduled_watch, "sched-watch")):
+                t = threading.Thread(target=fn, daemon=True, name=name)
+                t.start()
+                self.threads.append(t)
         log.info("fake kubelet %s up (plugins %s, podresources %s)", self.node, self.plugin_dir,
                  self.pr_socket)
 
@@ -169,6 +172,7 @@ class FakeKubelet:
                                      for d in resp.devices}
                         conn.updates += 1
                     self._update_node_status()
+                    self._sched_kick.set()  # new or healthier devices may fit a pending pod
                     backoff = 0.05
                     if self.stop_ev.is_set():
                         return
@@ -407,6 +411,7 @@ class FakeKubelet:
             for i in ids:
                 if self.assigned.get(i) == rp.uid:
                     del self.assigned[i]
+        self._sched_kick.set()  # freed devices may fit a pending pod
 
     def _forget(self, uid: str) -> None:
         with self.lock:
@@ -447,8 +452,37 @@ class FakeKubelet:
                 log.warning("pod status patch failed: %s", e)
 
     # ============================================================ scheduler
+    def _unscheduled_watch(self) -> None:
+        """Watch unscheduled pods (kube-scheduler's informer) and wake the scheduling pass, rather
+        than listing them every 50 ms: 20 LISTs/s per fake node loaded the apiserver-sim that the
+        timed reconciles share."""
+        rv = None
+        while not self.stop_ev.is_set():
+            try:
+                if rv is None:
+                    rv = self.client.list(PODS, field_selector="spec.nodeName=")["metadata"][
+                        "resourceVersion"]
+                    self._sched_kick.set()
+                for ev in self.client.watch(PODS, resource_version=rv, field_selector="spec.nodeName=",
+                                            stop=self.stop_ev, timeout_seconds=60):
+                    if ev["type"] == "ERROR":
+                        rv = None
+                        break
+                    rv = ev["object"]["metadata"].get("resourceVersion", rv)
+                    if ev["type"] in ("ADDED", "MODIFIED"):
+                        self._sched_kick.set()
+            except Exception as e:
+                if not self.stop_ev.is_set():
+                    log.warning("unscheduled-pod watch error: %s", e)
+                time.sleep(0.2)
+                rv = None
+
     def _scheduler_loop(self) -> None:
-        while not self.stop_ev.wait(0.05):
+        while not self.stop_ev.is_set():
+            self._sched_kick.wait(1.0)  # woken by the watch or a capacity change; 1 s resync
+            self._sched_kick.clear()
+            if self.stop_ev.is_set():
+                break
             try:
                 pending = self.client.list(PODS, field_selector="spec.nodeName=")["items"]
             except Exception:
