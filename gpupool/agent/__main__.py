@@ -26,6 +26,10 @@ def main() -> None:
     ap.add_argument("--socket", default="", help="unix socket for the manager RPC")
     ap.add_argument("--listen", default="", help="host:port for the manager RPC (TCP)")
     ap.add_argument("--endpoint", default="", help="endpoint written to the Node annotation")
+    ap.add_argument("--tls-cert", default=os.environ.get("GPUPOOL_AGENT_TLS_CERT", ""),
+                    help="PEM certificate: serve --listen over HTTPS (the manager verifies it "
+                         "with --agent-ca-file)")
+    ap.add_argument("--tls-key", default=os.environ.get("GPUPOOL_AGENT_TLS_KEY", ""))
     ap.add_argument("--apiserver", default=os.environ.get("GPUPOOL_APISERVER", ""))
     ap.add_argument("--token", default=os.environ.get("GPUPOOL_TOKEN", ""))
     ap.add_argument("--auth-token-file", default=os.environ.get("GPUPOOL_AGENT_TOKEN_FILE", ""),
@@ -70,7 +74,8 @@ def main() -> None:
             auth = f.read().strip()
     cfg = AgentConfig(node=a.node, auth_token=auth, backend=a.backend, fixture=a.fixture, faults=a.faults,
                       count=a.count, cli_dir=a.cli_dir, state_dir=a.state_dir, socket=a.socket,
-                      listen=a.listen, endpoint=a.endpoint, apiserver=a.apiserver, token=a.token,
+                      listen=a.listen, tls_cert=a.tls_cert, tls_key=a.tls_key,
+                      endpoint=a.endpoint, apiserver=a.apiserver, token=a.token,
                       plugin_dir=a.plugin_dir, pod_resources=a.pod_resources, probe_mode=a.probe,
                       probe_sim_ms=a.probe_sim_ms, probe_gemm_n=a.probe_gemm_n,
                       sample_interval=a.sample_interval, health_interval=a.health_interval,

@@ -58,6 +58,8 @@ class AgentConfig:
     state_dir: str = "/var/lib/gpupool"
     socket: str = ""                 # unix socket for the RPC server
     listen: str = ""                 # optional host:port
+    tls_cert: str = ""               # serve the TCP listener over HTTPS with this certificate
+    tls_key: str = ""
     endpoint: str = ""               # what the Node annotation advertises (default: socket)
     apiserver: str = ""              # empty: no Node registration
     token: str = ""
@@ -1131,7 +1133,7 @@ class Agent:
             return self.cfg.endpoint
         if self.cfg.socket:
             return "unix://" + os.path.abspath(self.cfg.socket)
-        return f"http://{self.cfg.listen}"
+        return f"{'https' if self.cfg.tls_cert else 'http'}://{self.cfg.listen}"
 
     # ================================================================ metrics
     def metrics_text(self) -> str:
@@ -1368,7 +1370,13 @@ async def serve(agent: Agent, ready_file: str | None = None) -> None:
         await web.UnixSite(runner, agent.cfg.socket).start()
     if agent.cfg.listen:
         host, port = agent.cfg.listen.rsplit(":", 1)
-        await web.TCPSite(runner, host or "0.0.0.0", int(port)).start()
+        ctx = None
+        if agent.cfg.tls_cert:  # across nodes the RPC (and its bearer token) travels encrypted
+            import ssl
+            ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+            ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+            ctx.load_cert_chain(agent.cfg.tls_cert, agent.cfg.tls_key or None)
+        await web.TCPSite(runner, host or "0.0.0.0", int(port), ssl_context=ctx).start()
     agent.start_background()
     if ready_file:
         with open(ready_file + ".tmp", "w") as f:

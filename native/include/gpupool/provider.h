@@ -157,9 +157,11 @@ class DeviceProvider {
 // Agents are discovered from Node objects annotated gpupool.amd.com/agent-endpoint.
 class RocmProvider : public DeviceProvider {
  public:
-  RocmProvider(Informer& nodes, int timeout_ms = 30000, std::string agent_token = "");
+  RocmProvider(Informer& nodes, int timeout_ms = 30000, std::string agent_token = "", TlsOptions agent_tls = {});
   // shared secret presented to the node agents (Authorization: Bearer)
   const std::string& agent_token() const { return agent_token_; }
+  // how https:// agent endpoints are verified (CA of the agents' serving certificates)
+  const TlsOptions& agent_tls() const { return agent_tls_; }
   std::vector<std::string> node_names() override;
   Json node_labels(const std::string& node) override;
   NodeView observe(const std::string& node) override;
@@ -193,6 +195,7 @@ class RocmProvider : public DeviceProvider {
   Informer& nodes_;
   int timeout_ms_;
   std::string agent_token_;
+  TlsOptions agent_tls_;
   std::mutex mu_;
   std::map<std::string, std::pair<std::string, std::shared_ptr<HttpClient>>> clients_;
   struct CachedView {

@@ -75,7 +75,7 @@ struct Flags {
   int slow_reconcile_ms = 1000;
   std::string validate;
   // TLS / auth for a real apiserver
-  std::string ca_file, client_cert, client_key, token_file, agent_token, agent_token_file;
+  std::string ca_file, client_cert, client_key, token_file, agent_token, agent_token_file, agent_ca_file;
   std::string kubeconfig, kube_context;
   bool insecure = false;
   bool apiserver_set = false;
@@ -107,6 +107,7 @@ controllers:
   --credentials-retry D (30s)  AzureVmPool retry after a credentials error
   --agent-timeout D (60s)      node-agent RPC timeout (covers on-claim GPU probes)
   --agent-token-file F         shared secret for the node-agent RPC   [$GPUPOOL_AGENT_TOKEN]
+  --agent-ca-file F            CA that signs https:// agent endpoints [$GPUPOOL_AGENT_CA_FILE]
   --orphan-sweep D (30s)       release claims whose pool no longer exists
 leader election:
   --leader-elect  --lease-namespace NS (gpupool-system)  --identity ID
@@ -138,6 +139,7 @@ Flags parse(int argc, char** argv) {
   env("GPUPOOL_TOKEN", f.token);
   env("GPUPOOL_NAMESPACE", f.ns);
   env("GPUPOOL_AGENT_TOKEN", f.agent_token);
+  env("GPUPOOL_AGENT_CA_FILE", f.agent_ca_file);
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&]() -> std::string {
@@ -158,6 +160,7 @@ Flags parse(int argc, char** argv) {
     else if (is("--client-key")) f.client_key = val();
     else if (is("--token-file")) f.token_file = val();
     else if (is("--agent-token-file")) f.agent_token_file = val();
+    else if (is("--agent-ca-file")) f.agent_ca_file = val();
     else if (is("--kubeconfig")) f.kubeconfig = val();
     else if (is("--context")) f.kube_context = val();
     else if (a == "--insecure-skip-tls-verify") f.insecure = true;
@@ -291,7 +294,7 @@ class AgentWatchers {
     while (!w->stop && !g_stop) {
       try {
         // the agent holds the answer up to timeoutSeconds: allow that plus slack before timing out
-        HttpClient c(Url::parse(w->endpoint), prov_.agent_token(), 10000);
+        HttpClient c(Url::parse(w->endpoint), prov_.agent_token(), 10000, prov_.agent_tls());
         std::string path = "/v1/events?timeoutSeconds=5&since=" + std::to_string(since);
         int status = c.stream_lines(
             path,
@@ -494,7 +497,9 @@ int main(int argc, char** argv) {
     Informer mipools(client, res::mi355xpools(), f.ns, std::chrono::milliseconds(f.resync_ms));
     Informer azpools(client, res::azurevmpools(), f.ns, std::chrono::milliseconds(f.resync_ms));
     Informer quotas(client, res::resourcequotas(), f.ns, std::chrono::milliseconds(f.resync_ms));
-    RocmProvider rocm(nodes, f.agent_timeout_ms, f.agent_token);
+    TlsOptions agent_tls;
+    agent_tls.ca_file = f.agent_ca_file;
+    RocmProvider rocm(nodes, f.agent_timeout_ms, f.agent_token, agent_tls);
     FakeCloudOptions fco;
     fco.provision = std::chrono::milliseconds(f.fakecloud_provision_ms);
     fco.deprovision = std::chrono::milliseconds(f.fakecloud_deprovision_ms);

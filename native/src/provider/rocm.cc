@@ -85,8 +85,8 @@ Json DeviceView::status_json() const {
   return s;
 }
 
-RocmProvider::RocmProvider(Informer& nodes, int timeout_ms, std::string agent_token)
-    : nodes_(nodes), timeout_ms_(timeout_ms), agent_token_(std::move(agent_token)) {}
+RocmProvider::RocmProvider(Informer& nodes, int timeout_ms, std::string agent_token, TlsOptions agent_tls)
+    : nodes_(nodes), timeout_ms_(timeout_ms), agent_token_(std::move(agent_token)), agent_tls_(std::move(agent_tls)) {}
 
 std::vector<std::string> RocmProvider::node_names() {
   std::vector<std::string> out;
@@ -114,7 +114,7 @@ std::shared_ptr<HttpClient> RocmProvider::client_for(const std::string& node) {
   auto& slot = clients_[node];
   if (!slot.second || slot.first != ep) {
     slot.first = ep;
-    slot.second = std::make_shared<HttpClient>(Url::parse(ep), agent_token_, timeout_ms_);
+    slot.second = std::make_shared<HttpClient>(Url::parse(ep), agent_token_, timeout_ms_, agent_tls_);
   }
   return slot.second;
 }
