@@ -82,6 +82,17 @@ class PoolReconcilerBase {
   std::map<std::string, int64_t> ready_gen_;
 };
 
+// The decision a Mi355xPool pass takes on its observed GPUs, before any RPC (pure; the C++
+// decision-table test drives it): which unhealthy GPUs to replace, which GPUs a scale-down drains
+// (in order), and how many to claim.
+struct PoolPlan {
+  std::vector<std::string> replace;  // claimed GPUs failing health or their probe (replacePolicy Replace)
+  std::vector<std::string> victims;  // scale-down: unhealthy first, then pod-free, smallest node, highest index
+  int64_t keep = 0;                  // GPUs active after this pass
+  int64_t need = 0;                  // GPUs to claim this pass (replicas - keep, never negative)
+};
+PoolPlan plan_pool(const Mi355xPoolSpec& spec, const std::vector<DeviceView>& mine);
+
 class Mi355xPoolReconciler : public PoolReconcilerBase {
  public:
   Mi355xPoolReconciler(KubeClient& client, Informer& pools, DeviceProvider& provider, EventRecorder* events,

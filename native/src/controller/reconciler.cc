@@ -603,6 +603,38 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
   return Outcome::done(ms(0));
 }
 
+PoolPlan plan_pool(const Mi355xPoolSpec& spec, const std::vector<DeviceView>& mine) {
+  PoolPlan plan;
+  std::vector<const DeviceView*> keep;
+  for (const auto& d : mine) {
+    if (d.state == "Draining") continue;  // already on its way out
+    const bool bad = d.state != "Probing" && (!d.healthy || !d.probe_passed);
+    if (bad && spec.replace_policy == "Replace") plan.replace.push_back(d.uuid);
+    else keep.push_back(&d);
+  }
+  auto n = static_cast<int64_t>(keep.size());
+  if (n > spec.replicas) {
+    // Deterministic victims (fixes README.md:214's arbitrary existingVMs[:n]): unhealthy first,
+    // then GPUs without pods, then the smallest node of a spanning pool, then the highest index.
+    std::map<std::string, int> on_node;
+    for (const DeviceView* d : keep) ++on_node[d->node];
+    std::sort(keep.begin(), keep.end(), [&on_node](const DeviceView* a, const DeviceView* b) {
+      bool ua = !a->healthy || !a->probe_passed, ub = !b->healthy || !b->probe_passed;
+      if (ua != ub) return ua;
+      bool pa = a->pods.size() > 0, pb = b->pods.size() > 0;
+      if (pa != pb) return !pa;
+      if (on_node[a->node] != on_node[b->node]) return on_node[a->node] < on_node[b->node];
+      if (a->node != b->node) return a->node > b->node;
+      return a->index > b->index;
+    });
+    for (int64_t i = 0; i < n - spec.replicas; ++i) plan.victims.push_back(keep[static_cast<size_t>(i)]->uuid);
+    n = spec.replicas;
+  }
+  plan.keep = n;
+  plan.need = std::max<int64_t>(0, spec.replicas - n);
+  return plan;
+}
+
 Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string& name) {
   auto cached = pools_.get(ns, name);
   if (!cached) return Outcome::done(ms(0));  // gone (finalizer already removed)
@@ -653,54 +685,26 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
   bool claimed_only = false;  // the only action was a successful claim
   std::vector<DeviceView> claimed;
   std::string claimed_node;
-  std::vector<const DeviceView*> active;
-  for (const auto& d : o.mine)
-    if (d.state != "Draining") active.push_back(&d);
-
-  std::vector<std::string> cordon;
-  std::vector<const DeviceView*> keep;
-  for (const DeviceView* d : active) {
-    bool bad = d->state != "Probing" && (!d->healthy || !d->probe_passed);
-    if (bad && spec.replace_policy == "Replace") {
-      cordon.push_back(d->uuid);
-      std::string why = join([&] {
-        std::vector<std::string> r;
-        for (const auto& x : d->verdict["reasons"].elements()) r.push_back(x.as_string());
-        if (!d->probe_passed) r.push_back("ProbeFailed: " + d->probe["error"].str_or("probe failed"));
-        return r;
-      }(), "; ");
-      event_(obj, "Warning", "HealthDegraded", short_id(*d) + " unhealthy (" + why + "): replacing");
-      progress_reason = "ReplacingUnhealthy";
-      progress_msg = "replacing " + short_id(*d);
-    } else {
-      keep.push_back(d);
-    }
+  const PoolPlan plan = plan_pool(spec, o.mine);
+  std::vector<std::string> cordon = plan.replace;
+  for (const auto& u : plan.replace) {
+    const DeviceView* d = nullptr;
+    for (const auto& x : o.mine)
+      if (x.uuid == u) d = &x;
+    std::vector<std::string> r;
+    for (const auto& x : d->verdict["reasons"].elements()) r.push_back(x.as_string());
+    if (!d->probe_passed) r.push_back("ProbeFailed: " + d->probe["error"].str_or("probe failed"));
+    event_(obj, "Warning", "HealthDegraded", short_id(*d) + " unhealthy (" + join(r, "; ") + "): replacing");
+    progress_reason = "ReplacingUnhealthy";
+    progress_msg = "replacing " + short_id(*d);
   }
-  int64_t n_active = static_cast<int64_t>(keep.size());
-  if (n_active > spec.replicas) {
-    // Deterministic victims (fixes README.md:214's arbitrary existingVMs[:n]): unhealthy first,
-    // then GPUs without pods, then the highest index.
-    std::vector<const DeviceView*> order = keep;
-    std::map<std::string, int> on_node;  // a spanning pool shrinks its smallest node first
-    for (const DeviceView* d : keep) ++on_node[d->node];
-    std::sort(order.begin(), order.end(), [&on_node](const DeviceView* a, const DeviceView* b) {
-      bool ua = !a->healthy || !a->probe_passed, ub = !b->healthy || !b->probe_passed;
-      if (ua != ub) return ua;
-      bool pa = a->pods.size() > 0, pb = b->pods.size() > 0;
-      if (pa != pb) return !pa;
-      if (on_node[a->node] != on_node[b->node]) return on_node[a->node] < on_node[b->node];
-      if (a->node != b->node) return a->node > b->node;
-      return a->index > b->index;
-    });
-    int64_t drop = n_active - spec.replicas;
-    std::vector<std::string> victims;
-    for (int64_t i = 0; i < drop; ++i) victims.push_back(order[static_cast<size_t>(i)]->uuid);
-    cordon.insert(cordon.end(), victims.begin(), victims.end());
+  if (!plan.victims.empty()) {
+    cordon.insert(cordon.end(), plan.victims.begin(), plan.victims.end());
     progress_reason = "ScalingDown";
-    progress_msg = "draining " + std::to_string(drop) + " GPU(s): " + join(victims, ",");
+    progress_msg = "draining " + std::to_string(plan.victims.size()) + " GPU(s): " + join(plan.victims, ",");
     event_(obj, "Normal", "DrainStarted", progress_msg);
-    n_active = spec.replicas;
   }
+  int64_t n_active = plan.keep;
   if (!cordon.empty()) {
     for (const auto& kv : by_node(o, cordon)) provider_.cordon(kv.first, m.uid, kv.second);
     acted = true;
