@@ -356,13 +356,31 @@ class Client:
              "fieldSelector": field_selector, "allowWatchBookmarks": "true" if bookmarks else None,
              "timeoutSeconds": timeout_seconds}
         path = res.path(ns) + "?" + urllib.parse.urlencode({k: v for k, v in q.items() if v})
-        conn = self._conn(timeout=1.0 if stop is not None else (timeout_seconds or 3600) + 5)
+        # Reads block (a quiet watch may see nothing for minutes). The socket timeout only catches
+        # a dead connection: after a timeout a response reader is unusable ("cannot read from
+        # timed out object"), so ``stop`` is honoured by shutting the socket down from a helper
+        # thread instead of polling with short timeouts — which broke every watch idle for 1 s,
+        # and a relist in that gap missed DELETED events.
+        conn = self._conn(timeout=(timeout_seconds or 3600) + 30)
         conn.request("GET", path, headers=self._headers())
         resp = conn.getresponse()
         if resp.status >= 400:
             raw = resp.read()
             conn.close()
             raise KubeError(resp.status, json.loads(raw) if raw else None)
+        done = threading.Event()
+        if stop is not None:
+            sock = conn.sock
+
+            def _stopper() -> None:
+                while not done.wait(0.2):
+                    if stop.is_set():
+                        try:
+                            sock.shutdown(socket.SHUT_RDWR)
+                        except OSError:
+                            pass
+                        return
+            threading.Thread(target=_stopper, daemon=True, name="watch-stop").start()
         buf = b""
         try:
             while True:
@@ -370,8 +388,10 @@ class Client:
                     return
                 try:
                     chunk = resp.read1(65536) if hasattr(resp, "read1") else resp.read(1)
-                except (socket.timeout, TimeoutError):
-                    continue
+                except (OSError, ValueError):
+                    if stop is not None and stop.is_set():
+                        return
+                    raise
                 if not chunk:
                     return
                 buf += chunk
@@ -380,6 +400,7 @@ class Client:
                     if line.strip():
                         yield json.loads(line)
         finally:
+            done.set()
             conn.close()
 
     def wait_for(self, res: Res, name: str, ns: str | None, pred, timeout: float = 30.0,

@@ -238,6 +238,12 @@ class FakeKubelet:
                     lst = self.client.list(PODS, field_selector=f"spec.nodeName={self.node}")
                     for p in lst["items"]:
                         self._handle_pod(p)
+                    # a relist is the truth: pods deleted while the watch was down are gone
+                    listed = {p["metadata"]["uid"] for p in lst["items"]}
+                    with self.lock:
+                        gone = [u for u in self.pods if u not in listed]
+                    for u in gone:
+                        self._forget(u)
                     rv = lst["metadata"]["resourceVersion"]
                 for ev in self.client.watch(PODS, resource_version=rv,
                                             field_selector=f"spec.nodeName={self.node}",

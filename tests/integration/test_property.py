@@ -154,3 +154,71 @@ def test_spanning_pools_converge(two_nodes, ops, final):
         k.delete(MI355XPOOLS, name, ns)
     for name in ("sa", "sb"):
         k.wait_for(MI355XPOOLS, name, ns, lambda o: o is None, timeout=30)
+
+
+chaos_op = st.one_of(
+    st.tuples(st.just("scale"), st.integers(0, 6)),
+    st.tuples(st.just("pod"), st.integers(0, 1000)),
+    st.tuples(st.just("restart-manager"), st.just(0)),
+    st.tuples(st.just("restart-agent"), st.just(0)),
+)
+
+
+@pytest.fixture(scope="module")
+def chaos(tmp_path_factory, native_built):
+    c = Cluster(str(tmp_path_factory.mktemp("chaos")), nodes=[NodeSpec("mi355x-node-0")],
+                sample_interval=0.2)
+    c.start()
+    yield c
+    c.stop()
+
+
+@settings(max_examples=5, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
+                                                                 HealthCheck.too_slow])
+@given(ops=st.lists(chaos_op, min_size=2, max_size=7), final=st.integers(0, 5))
+def test_restarts_and_pods_never_strand_a_pod(chaos, ops, final):
+    """Random replicas edits, GPU pods and restarts of the manager and of the node agent (the
+    SURVEY §4.2 property row). Once settled: readyReplicas == spec.replicas, the agent's claims
+    are exactly the pool's devices (restarts re-adopt from the ledger, nothing is double-claimed
+    or leaked), and every pod still running sits on a GPU the pool holds — no GPU was released
+    under a running pod."""
+    from gpupool.kube import PODS
+    from .helpers import pause_pod
+    c = chaos
+    k = c.client
+    node = c.nodes[0]
+    ns = f"c{int(time.time() * 1e6) % 10**9}"
+    res = "amd.com/gpu-chaos"
+    k.create(MI355XPOOLS, mi_pool("pc", 1, resourceName=res, drain={"gracePeriodSeconds": 1}), ns)
+    for kind, v in ops:
+        if kind == "scale":
+            k.patch(MI355XPOOLS, "pc", {"spec": {"replicas": v}}, ns)
+        elif kind == "pod":
+            k.create(PODS, pause_pod(f"w{v}-{len(ns)}-{time.time_ns() % 10**6}", resource=res), ns)
+        elif kind == "restart-manager":
+            c._kill("manager")
+            c.start_manager()
+        else:
+            c._kill(f"agent-{node.name}")
+            c.start_agent(node)
+        time.sleep(0.1)
+    k.patch(MI355XPOOLS, "pc", {"spec": {"replicas": final}}, ns)
+    o = k.wait_for(MI355XPOOLS, "pc", ns, ready_at(final), timeout=90)
+    held = {d["uuid"] for d in o["status"]["devices"]}
+    view = c.agent_request(node.name, "GET", "/v1/node")
+    assert {d["uuid"] for d in view["devices"] if d.get("poolUID") == o["metadata"]["uid"]} == held
+    deadline = time.time() + 15
+    while True:  # evictions of pods on released GPUs complete asynchronously (grace 1 s)
+        running = [p for p in k.list(PODS, ns)["items"]
+                   if p["status"].get("phase") == "Running" and not p["metadata"].get("deletionTimestamp")]
+        stray = [p["metadata"]["name"] for p in running
+                 if not set((p["metadata"].get("annotations") or {})
+                            .get("gpupool.amd.com/devices", "").split(",")) <= held]
+        if not stray or time.time() > deadline:
+            break
+        time.sleep(0.1)
+    assert not stray, (stray, held)
+    for p in k.list(PODS, ns)["items"]:
+        k.delete(PODS, p["metadata"]["name"], ns, grace=0)
+    k.delete(MI355XPOOLS, "pc", ns)
+    k.wait_for(MI355XPOOLS, "pc", ns, lambda x: x is None, timeout=60)
