@@ -116,6 +116,11 @@ class Agent:
         self.verdicts: dict[str, dict] = {}
         self.gen = 0
         self.changes: list[tuple[int, set[str]]] = []
+        # pools with a claim RPC in flight: their change events wait until the claim's reply is
+        # out (the reply carries the same state); answering the manager's event feed meanwhile
+        # only competed with the reply on the event loop
+        self._claiming: dict[str, int] = {}
+        self._deferred: set[str] = set()
         self.waiters: list[tuple[asyncio.AbstractEventLoop, asyncio.Future]] = []
         self.advertised: dict[str, set[str]] = {}
         self._adv_event = threading.Event()
@@ -509,6 +514,12 @@ class Agent:
     # ================================================================ events
     def _bump(self, pools: set[str]) -> None:
         with self.lock:
+            held = {p for p in pools if p in self._claiming}
+            if held:
+                self._deferred |= held
+                pools = set(pools) - held
+                if not pools:
+                    return
             self.gen += 1
             self.changes.append((self.gen, set(pools)))
             self.changes = self.changes[-256:]
@@ -685,14 +696,36 @@ class Agent:
                     "devices": devices, "topology": self.snap.get("topology", {})}
 
     # ================================================================ claims
-    def claim(self, req: dict) -> dict:
+    def claim(self, req: dict, hold_events: bool = False) -> dict:
         """Claim ``count`` GPUs for a pool, all or nothing: select (topology), commit to the
-        ledger, probe, commit, advertise through the device plugin, answer with device views."""
-        st = self._claim_start(req)
-        if not st.get("ok"):
-            return st
-        self._wait_advertised(st["_resource"], st["_uuids"])
-        return self._claim_finish(st)
+        ledger, probe, commit, advertise through the device plugin, answer with device views.
+        ``hold_events``: the pool's change events stay deferred after return until
+        ``release_events`` (the RPC handler calls it once the reply is written)."""
+        pool = req.get("poolUID", "")
+        with self.lock:
+            self._claiming[pool] = self._claiming.get(pool, 0) + 1
+        try:
+            st = self._claim_start(req)
+            if not st.get("ok"):
+                return st
+            self._wait_advertised(st["_resource"], st["_uuids"])
+            return self._claim_finish(st)
+        finally:
+            if not hold_events:
+                self.release_events(pool)
+
+    def release_events(self, pool: str) -> None:
+        """End a claim's event hold: one bump for whatever changed meanwhile."""
+        with self.lock:
+            n = self._claiming.get(pool, 0) - 1
+            if n > 0:
+                self._claiming[pool] = n
+                return
+            self._claiming.pop(pool, None)
+            flush = pool in self._deferred
+            self._deferred.discard(pool)
+        if flush:
+            self._bump({pool})
 
     def _claim_start(self, req: dict) -> dict:
         pool_uid, count = req["poolUID"], int(req["count"])
@@ -1272,12 +1305,18 @@ def build_app(agent: Agent) -> web.Application:
                                       "required"}, status=400)
         t_in = time.perf_counter()
         body["_t_in"] = t_in
-        out = await run_blocking(agent.claim, body)
-        t_back = time.perf_counter()
-        tm = out.get("timingsMs")
-        if tm is not None:  # the executor hop back to the event loop (GIL + loop wake-up)
-            tm["executorOut"] = round((t_back - out.pop("_t_done")) * 1e3, 3)
-        return web.Response(text=json.dumps(out), content_type="application/json")
+        try:
+            out = await run_blocking(agent.claim, body, True)
+            t_back = time.perf_counter()
+            tm = out.get("timingsMs")
+            if tm is not None:  # the executor hop back to the event loop (GIL + loop wake-up)
+                tm["executorOut"] = round((t_back - out.pop("_t_done")) * 1e3, 3)
+            resp = web.Response(text=json.dumps(out), content_type="application/json")
+            await resp.prepare(request)
+            await resp.write_eof()  # the reply is out: now the held change events may go
+            return resp
+        finally:
+            agent.release_events(body["poolUID"])
 
     async def cordon(request):
         b = await request.json()
