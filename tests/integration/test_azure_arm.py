@@ -245,3 +245,43 @@ def test_arm_bad_subnet_reference(arm, cluster_factory):
     assert "subnets/missing" in conds(o)["Degraded"]["message"]
     k.patch(AZUREVMPOOLS, "badnet", {"spec": {"subnetName": "default"}}, "default")
     k.wait_for(AZUREVMPOOLS, "badnet", "default", az_ready(1), timeout=30)
+
+
+@pytest.mark.parametrize("san", ["asan", "tsan"])
+def test_arm_provider_under_sanitizer(san, arm, cluster_factory):
+    """The ARM provider (token cache shared by worker threads, TLS client, paging, rollback) in the
+    ASan+UBSan and TSan builds of the manager, through scale up/down, throttling, a revoked token
+    and a delete with leftover NIC/disk."""
+    import subprocess
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "native"), f"SAN={san}", "host", "-j8"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    os.environ["TSAN_OPTIONS"] = "halt_on_error=0:report_signal_unsafe=0"
+    os.environ["ASAN_OPTIONS"] = "detect_leaks=0"
+    arm.page_size = 1
+    c = cluster_factory(nodes=[], kinds="azure",
+                        manager_bin=os.path.join(ROOT, "build", f"native-{san}", "gpupool-manager"),
+                        manager_args=["--cloud", "azure-arm", "--azure-arm-endpoint", arm.url,
+                                      "--azure-authority-host", arm.url, "--azure-ca-file", arm.ca,
+                                      "--credentials-retry", "300ms", "--workers", "4"])
+    k = c.client
+    k.create(SECRETS, secret(), "default")
+    for name in ("s1", "s2"):
+        k.create(AZUREVMPOOLS, sample(name, 2), "default")
+    for name in ("s1", "s2"):
+        k.wait_for(AZUREVMPOOLS, name, "default", az_ready(2), timeout=60)
+    arm.faults["throttle"] = 2
+    with arm.mu:
+        arm.tokens.clear()
+    k.patch(AZUREVMPOOLS, "s1", {"spec": {"replicas": 1}}, "default")
+    k.wait_for(AZUREVMPOOLS, "s1", "default", az_ready(1), timeout=60)
+    arm.add_orphans(SUB, RG, "default-s2", "s2-0abcd")
+    for name in ("s1", "s2"):
+        k.delete(AZUREVMPOOLS, name, "default")
+    for name in ("s1", "s2"):
+        k.wait_for(AZUREVMPOOLS, name, "default", lambda o: o is None, timeout=60)
+    st = arm.state()
+    assert st["vms"] == [] and st["nics"] == [] and st["disks"] == []
+    log = c.log("manager")
+    assert "WARNING: ThreadSanitizer" not in log, log[-6000:]
+    assert "ERROR: AddressSanitizer" not in log and "runtime error:" not in log, log[-6000:]
