@@ -148,3 +148,22 @@ def test_every_sample_applies(cluster_factory):
     assert pvc["spec"]["volumeName"] == "gpupool-workspace"
     job = c.client.get(BY_KIND["Mi355xJob"], "fmnist-ddp", "default")
     assert job["spec"]["checkpointDir"].startswith("/workspace/")
+
+
+def test_alert_rules_use_exported_metrics():
+    """Every metric an alert in config/prometheus/alerts.yaml queries is exported by the manager
+    (C++ sources) or the node agent, with the label values the rules select on."""
+    import yaml
+    doc = yaml.safe_load(open(os.path.join(ROOT, "config", "prometheus", "alerts.yaml")))
+    src = open(os.path.join(ROOT, "gpupool", "agent", "agent.py")).read()
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "native", "src")):
+        for f in files:
+            if f.endswith(".cc"):
+                src += open(os.path.join(dirpath, f)).read()
+    rules = [r for g in doc["spec"]["groups"] for r in g["rules"]]
+    assert len(rules) >= 8
+    for r in rules:
+        for m in re.findall(r"gpupool_[a-z_]+", r["expr"]):
+            assert m in src, (r["alert"], m)
+    for label in ('"uncorrectable"', '"hotspot"', '"error"', '"terminal"', 'state="{t}"'):
+        assert label in src, label
