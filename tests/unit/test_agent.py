@@ -224,3 +224,24 @@ def test_probe_performance_floors():
     # a failed probe keeps its own error
     bad = {"passed": False, "error": "HBM mismatch", "hbm": {"GBps": 1.0}}
     assert Prober.apply_floors(bad, {}, {"minHbmGBps": 4000})["error"] == "HBM mismatch"
+
+
+def test_claiming_pool_events_held_until_released(tmp_path, sockdir, native_built):
+    """A claim RPC holds its pool's change events (the reply carries that state) and emits one
+    bump when the handler releases them; other pools' events pass through meanwhile."""
+    a = make_agent(tmp_path, sockdir, plugin=False)
+    g0, _ = a.changed_since(-1)
+    r = a.claim({"poolUID": "held", "pool": "default/p", "count": 1, "resourceName": "amd.com/gpu",
+                 "policy": {}, "probe": {"enabled": True}}, hold_events=True)
+    assert r["ok"]
+    a._bump({"held", "other"})  # e.g. a health flip during the claim: "other" goes out now
+    g1, pools = a.changed_since(g0)
+    assert "other" in pools and "held" not in pools
+    a.release_events("held")
+    g2, pools = a.changed_since(g1)
+    assert g2 == g1 + 1 and pools == ["held"]
+    a.release_events("held")  # idempotent: nothing more
+    assert a.changed_since(g2)[0] == g2
+    # without the hold (direct callers) the claim releases its own hold when it returns
+    assert claim(a, uid="plain", count=1)["ok"]
+    assert not a._claiming and not a._deferred
