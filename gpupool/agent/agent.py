@@ -208,10 +208,29 @@ class Agent:
                     out[s_] = v
         return out
 
+    # spec.health defaults (the schema's): a pool asking for exactly these, with no partition
+    # requirement, is judged like a free GPU is after every poll
+    _DEFAULT_HEALTH = {k: v["default"] for k, v in
+                       schema.MI355X_SPEC["properties"]["health"]["properties"].items()
+                       if "default" in v}
+
+    @classmethod
+    def _is_default_policy(cls, policy: dict) -> bool:
+        h = policy.get("health") or {}
+        if set(h) - set(cls._DEFAULT_HEALTH) or any(h.get(k, v) != v
+                                                     for k, v in cls._DEFAULT_HEALTH.items()):
+            return False
+        p = policy.get("partition") or {}
+        return p.get("compute", "Any") == "Any" and p.get("memory", "Any") == "Any"
+
     def _claimable(self, devs: list[dict], policy: dict, policy_key: str) -> list[bool]:
-        """Healthy under the requesting pool's policy with baseline = now, for each device. Cached
-        per (device snapshot, policy) — a snapshot dict is replaced, never mutated, when the device
-        changes — and the misses evaluated in one native call."""
+        """Healthy under the requesting pool's policy with baseline = now, for each device.
+        Under the default policy that is the free GPU's current verdict (re-evaluated on every
+        health change, with the same baseline = now). Otherwise cached per (device snapshot,
+        policy) — a snapshot dict is replaced, never mutated, when the device changes, which on
+        hardware is every poll (temperatures move) — and the misses evaluated in one native call."""
+        if self._is_default_policy(policy):
+            return [bool(self.verdicts.get(d["uuid"], {}).get("healthy")) for d in devs]
         out: list[bool | None] = []
         miss = []
         for d in devs:
