@@ -55,6 +55,10 @@ class PoolReconcilerBase {
   virtual ~PoolReconcilerBase() = default;
   virtual Outcome reconcile(const std::string& ns, const std::string& name) = 0;
   const std::string& kind() const { return kind_; }
+  // True for the watch event of this reconciler's own status write (its resourceVersion is the
+  // one the write returned): nothing a pass acts on changed, so it needs no new pass (the
+  // GenerationChanged-style predicate controller-runtime operators use, exact to the write).
+  bool own_status_write(const Json& obj);
 
  protected:
   // Writes ``status`` (unless semantically unchanged) with a fresh-GET retry on 409.
@@ -80,6 +84,7 @@ class PoolReconcilerBase {
   // reconcile-to-Ready tracking: uid -> (generation, first time that generation was seen)
   std::map<std::string, std::pair<int64_t, std::chrono::steady_clock::time_point>> pending_;
   std::map<std::string, int64_t> ready_gen_;
+  std::map<std::string, std::string> own_rv_;  // uid -> resourceVersion of our last status write
 };
 
 // The decision a Mi355xPool pass takes on its observed GPUs, before any RPC (pure; the C++

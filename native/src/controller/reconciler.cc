@@ -115,7 +115,9 @@ void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
     Json upd = cur;
     upd["status"] = status;
     try {
-      client_.update(res_, ns, upd, "status");
+      Json out = client_.update(res_, ns, upd, "status");
+      std::lock_guard<std::mutex> g(mu_);
+      own_rv_[out.path("metadata.uid").as_string()] = out.path("metadata.resourceVersion").as_string();
       return;
     } catch (const KubeError& e) {
       if (!e.conflict()) throw;
@@ -124,6 +126,13 @@ void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
     }
   }
   throw KubeError(409, "Conflict", "status update kept conflicting for " + ns + "/" + name);
+}
+
+bool PoolReconcilerBase::own_status_write(const Json& obj) {
+  const std::string uid = obj.path("metadata.uid").as_string();
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = own_rv_.find(uid);
+  return it != own_rv_.end() && !it->second.empty() && it->second == obj.path("metadata.resourceVersion").as_string();
 }
 
 // Finalizer edits carry the object's resourceVersion (the list is replaced as a whole, so a
@@ -189,6 +198,7 @@ void PoolReconcilerBase::forget_(const std::string& uid) {
   std::lock_guard<std::mutex> g(mu_);
   pending_.erase(uid);
   ready_gen_.erase(uid);
+  own_rv_.erase(uid);
 }
 
 namespace {

@@ -535,15 +535,15 @@ int main(int argc, char** argv) {
     AzureVmPoolReconciler az(client, azpools, cloud, &events, ropts);
     AgentWatchers watchers(rocm, mipools, ctl);
 
-    auto pool_handler = [&ctl](const char* kind) {
-      return [&ctl, kind](const std::string& type, const Json& obj) {
-        (void)type;
+    auto pool_handler = [&ctl](const char* kind, PoolReconcilerBase* r = nullptr) {
+      return [&ctl, kind, r](const std::string& type, const Json& obj) {
+        if (r && type == "MODIFIED" && r->own_status_write(obj)) return;  // our own status write
         ctl.enqueue(kind, obj.path("metadata.namespace").as_string(), obj.path("metadata.name").as_string());
       };
     };
     if (want_mi) {
       ctl.add_reconciler(&mi);
-      mipools.add_handler(pool_handler("Mi355xPool"));
+      mipools.add_handler(pool_handler("Mi355xPool", &mi));
       nodes.add_handler([&](const std::string& type, const Json&) {
         if (type == "RESYNC") return;
         watchers.sync(rocm.node_names());
@@ -628,7 +628,7 @@ int main(int argc, char** argv) {
                Json::object().set("kinds", f.kinds).set("hint", "add 'job' to --kinds"));
     if (want_az) {
       ctl.add_reconciler(&az);
-      azpools.add_handler(pool_handler("AzureVmPool"));
+      azpools.add_handler(pool_handler("AzureVmPool", &az));
       azpools.start();
     }
     // Workers start only on synced caches (controller-runtime WaitForCacheSync); the wait is sliced
