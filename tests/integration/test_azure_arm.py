@@ -285,3 +285,18 @@ def test_arm_provider_under_sanitizer(san, arm, cluster_factory):
     log = c.log("manager")
     assert "WARNING: ThreadSanitizer" not in log, log[-6000:]
     assert "ERROR: AddressSanitizer" not in log and "runtime error:" not in log, log[-6000:]
+
+
+def test_arm_waits_for_nic_provisioning(arm, cluster_factory):
+    """ARM answers a NIC PUT with provisioningState Updating; the provider polls it to Succeeded
+    before the VM PUT references it (a VM PUT naming an unfinished NIC would be refused)."""
+    arm.nic_delay = 0.6
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(), "default")
+    k.create(AZUREVMPOOLS, sample("slow-nic", 1), "default")
+    k.wait_for(AZUREVMPOOLS, "slow-nic", "default", az_ready(1), timeout=30)
+    gets = [p for m, p, s in arm.calls if m == "GET" and "/networkInterfaces/" in p]
+    assert gets, "the provider never polled the NIC"
+    nic = arm.state()["nics"][0]
+    assert nic["properties"]["provisioningState"] == "Succeeded"

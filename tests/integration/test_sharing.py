@@ -102,3 +102,19 @@ def test_autoscaled_shared_pool_counts_slots(cluster_factory):
     for i in range(6):
         k.wait_for(PODS, f"a{i}", "default", running, timeout=30)
     assert k.get(MI355XPOOLS, "sa", "default")["spec"]["replicas"] == 2
+
+
+def test_sharing_cpx_partitions(cluster_factory):
+    """Sharing composes with CPX: each logical GPU (partition) of a pool is advertised as K
+    slots, so one MI355X in CPX mode with K=2 serves 16 pods."""
+    from gpupool.testing.cluster import ROOT, NodeSpec
+    import os
+    cpx = os.path.join(ROOT, "tests", "fixtures", "node_8x_mi355x_cpx.json")
+    c = cluster_factory(nodes=[NodeSpec("cpx-node", fixture=cpx)])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("cs", 8, partition={"compute": "CPX"},
+                                  sharing={"replicasPerGPU": 2}), "default")
+    o = wait_ready(k, "cs", 8, timeout=60)
+    assert o["status"]["allocatable"] == 16
+    k.wait_for(NODES, "cpx-node", None, lambda n: (n["status"].get("allocatable") or {})
+               .get("amd.com/gpu") == "16", timeout=20)
