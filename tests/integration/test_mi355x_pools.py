@@ -102,7 +102,7 @@ def test_drain_wakes_on_pod_exit_not_the_sample_period(cluster_factory):
     wait_ready(k, "p", 0, timeout=20)
     dt = time.perf_counter() - t0
     assert k.list(PODS, "default")["items"] == []
-    assert dt < 1.5, f"scale-down with drain took {dt:.2f} s"
+    assert dt < 2.5, f"scale-down with drain took {dt:.2f} s"  # vs >= 5 s without the pod watch
 
 
 def test_config5_two_pools_with_health_conditions(node8):
@@ -650,7 +650,7 @@ def test_lagging_watch_cache_does_not_fail_reconciles(cluster_factory):
     t0 = time.perf_counter()
     k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 3}}, "default")
     wait_ready(k, "p", 3, timeout=30)
-    assert time.perf_counter() - t0 < 3.0
+    assert time.perf_counter() - t0 < 5.0
     k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 0}}, "default")
     wait_ready(k, "p", 0, timeout=30)
     k.delete(MI355XPOOLS, "p", "default")

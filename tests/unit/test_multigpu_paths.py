@@ -82,7 +82,7 @@ def test_probe_many_runs_eight_gpus_concurrently(devices):
     assert [r["passed"] for r in res] == [True] * 8
     assert sorted(o for k, o, _ in stub.calls if k == "run") == list(range(8))
     assert stub.max_active == 8
-    assert wall < 0.6, wall  # ~T (0.2 s), far below 8T (1.6 s)
+    assert wall < 0.9, wall  # ~T (0.2 s), far below 8T (1.6 s)
 
 
 def test_same_device_probes_serialise_in_the_stub_like_the_library(devices):
