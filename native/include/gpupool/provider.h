@@ -143,6 +143,9 @@ class DeviceProvider {
   virtual ~DeviceProvider() = default;
   virtual std::vector<std::string> node_names() = 0;
   virtual Json node_labels(const std::string& node) = 0;
+  // false while the Node is cordoned (spec.unschedulable): no new GPUs are claimed there; pools
+  // already on it keep theirs (like pods on a cordoned node)
+  virtual bool node_schedulable(const std::string& /*node*/) { return true; }
   virtual NodeView observe(const std::string& node) = 0;
   // Only ``pool_uid``'s GPUs plus the node's free-healthy count (smaller, cheaper answer for the
   // reconcile path). Default: the full view.
@@ -164,6 +167,7 @@ class RocmProvider : public DeviceProvider {
   const TlsOptions& agent_tls() const { return agent_tls_; }
   std::vector<std::string> node_names() override;
   Json node_labels(const std::string& node) override;
+  bool node_schedulable(const std::string& node) override;
   NodeView observe(const std::string& node) override;
   NodeView observe_pool(const std::string& node, const std::string& pool_uid) override;
   ClaimResult claim(const std::string& node, const ClaimRequest& req) override;

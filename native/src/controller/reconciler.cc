@@ -271,6 +271,7 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
       else if (d.state == "Free" && d.healthy) ++free_healthy;
     }
     if (nv.free_healthy >= 0) free_healthy = nv.free_healthy;  // pool-scoped view
+    if (!provider_.node_schedulable(n)) free_healthy = 0;  // cordoned: no capacity for new claims
     o.free_by_node[n] = free_healthy;
     if (span_nodes) {
       for (auto& d : mine) o.mine.push_back(std::move(d));
@@ -304,7 +305,7 @@ std::vector<std::string> Mi355xPoolReconciler::choose_nodes_(const Mi355xPoolSpe
     bool match = true;
     for (const auto& kv : spec.node_selector)
       if (labels[kv.first].as_string() != kv.second) match = false;
-    if (!match) continue;
+    if (!match || !provider_.node_schedulable(n)) continue;  // cordoned nodes get no new claims
     NodeView nv = provider_.observe(n);
     if (!nv.reachable) continue;
     int64_t free = 0;
@@ -804,9 +805,12 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     int need = static_cast<int>(spec.replicas - n_active);
     // A pool lives on one node: extend where it already is, else try the fitting nodes in order.
     std::vector<std::string> candidates = o.mine.empty() ? choose_nodes_(spec, need) : std::vector<std::string>{o.node};
+    const bool cordoned = !o.mine.empty() && !provider_.node_schedulable(o.node);
+    if (cordoned) candidates.clear();  // a cordoned node keeps its GPUs but takes no new claims
     if (candidates.empty()) {
       blocked = "InsufficientDevices";
-      progress_msg = "no eligible node has " + std::to_string(need) + " free healthy GPU(s)";
+      progress_msg = cordoned ? "node " + o.node + " is cordoned (spec.unschedulable): no new GPUs claimed there"
+                              : "no eligible node has " + std::to_string(need) + " free healthy GPU(s)";
       event_(obj, "Warning", "InsufficientDevices", progress_msg);
     }
     for (size_t ci = 0; ci < candidates.size(); ++ci) {

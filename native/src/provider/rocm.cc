@@ -101,6 +101,11 @@ Json RocmProvider::node_labels(const std::string& node) {
   return n->path("metadata.labels");
 }
 
+bool RocmProvider::node_schedulable(const std::string& node) {
+  auto n = nodes_.get("", node);
+  return !n || !n->path("spec.unschedulable").as_bool(false);
+}
+
 std::string RocmProvider::endpoint_of(const std::string& node) {
   auto n = nodes_.get("", node);
   if (!n) return "";

@@ -222,7 +222,11 @@ def test_gpuctl_trainjob_verbs(node8, tmp_path):
     assert "created" in gpuctl("trainjob", "create", "-f", str(f))
     k.wait_for(MI355XJOBS, "cli-demo-1", "default", phase_is("Succeeded"), timeout=30)
     assert "cli-demo-1" in gpuctl("trainjob", "list") and "Succeeded" in gpuctl("trainjob", "list")
-    assert "hello-from-0" in gpuctl("trainjob", "logs", "cli-demo-1")
+    deadline = time.monotonic() + 15  # the kubelet annotates the log path asynchronously
+    while "hello-from-0" not in (out := gpuctl("trainjob", "logs", "cli-demo-1")) and \
+            time.monotonic() < deadline:
+        time.sleep(0.2)
+    assert "hello-from-0" in out
     exported = yaml.safe_load(gpuctl("trainjob", "template", "-s", "cli-demo-1"))
     assert exported["command"] == "echo hello-from-$RANK" and exported["title"] == "CLI Demo_1"
     bare = tmp_path / "job_full.yaml"

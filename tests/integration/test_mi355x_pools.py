@@ -657,3 +657,24 @@ def test_lagging_watch_cache_does_not_fail_reconciles(cluster_factory):
     k.wait_for(MI355XPOOLS, "p", "default", lambda o: o is None, timeout=30)
     failed = [ln for ln in c.log("manager").splitlines() if "reconcile failed" in ln]
     assert not failed, failed[:3]
+
+
+def test_cordoned_node_takes_no_new_claims(cluster_factory):
+    """A cordoned Node (spec.unschedulable, `kubectl cordon`) keeps the GPUs its pools hold but
+    takes no new claims: an unpinned pool is placed on another node, a pool pinned to the cordoned
+    node waits (InsufficientDevices, reason in the message) until the node is uncordoned."""
+    c = cluster_factory(nodes=[NodeSpec("node-a", count=4), NodeSpec("node-b", count=4)])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("held", 1, nodeName="node-a"), "default")
+    wait_ready(k, "held", 1)
+    k.patch(NODES, "node-a", {"spec": {"unschedulable": True}}, None)
+    k.create(MI355XPOOLS, mi_pool("free", 2), "default")
+    o = wait_ready(k, "free", 2)
+    assert o["status"]["nodeName"] == "node-b"
+    k.patch(MI355XPOOLS, "held", {"spec": {"replicas": 2}}, "default")
+    o = k.wait_for(MI355XPOOLS, "held", "default",
+                   cond_is("Progressing", "False", "InsufficientDevices"), timeout=20)
+    assert "cordoned" in conds(o)["Progressing"]["message"]
+    assert o["status"]["readyReplicas"] == 1  # its GPU stays
+    k.patch(NODES, "node-a", {"spec": {"unschedulable": False}}, None)
+    wait_ready(k, "held", 2, timeout=30)

@@ -132,6 +132,9 @@ def test_device_plugin_conformance(tmp_path, sockdir, native_built):
     a = make_agent(tmp_path, sockdir)
     try:
         r = claim(a, count=2)
+        deadline = time.time() + 5  # the plugin registers from its own thread
+        while not kubelet.registrations and time.time() < deadline:
+            time.sleep(0.02)
         assert kubelet.registrations == [("v1beta1", "gpupool-amd-com_gpu.sock", "amd.com/gpu", True)]
         ch = grpc.insecure_channel(unix_target(os.path.join(dp_dir, "gpupool-amd-com_gpu.sock")))
         stub = Stub(ch, "v1beta1.DevicePlugin")
