@@ -31,7 +31,13 @@ def main() -> None:
         import cProfile
         import signal
         prof = cProfile.Profile()
-        signal.signal(signal.SIGTERM, lambda *_: (_ for _ in ()).throw(KeyboardInterrupt()))
+        import os
+
+        def _dump_and_exit(*_):  # open watch streams would keep asyncio.run's shutdown waiting
+            prof.disable()
+            prof.dump_stats(a.profile)
+            os._exit(0)
+        signal.signal(signal.SIGTERM, _dump_and_exit)
         prof.enable()
     logging.basicConfig(level=logging.DEBUG if a.verbose else logging.WARNING,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")

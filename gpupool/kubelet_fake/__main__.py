@@ -19,6 +19,8 @@ def main() -> None:
     ap.add_argument("--root", required=True, help="kubelet root dir (device-plugins/, pod-resources/)")
     ap.add_argument("--workdir", default=os.getcwd(), help="cwd for pod processes")
     ap.add_argument("--no-schedule", action="store_true")
+    ap.add_argument("--node-status-delay", type=float, default=0.02,
+                    help="coalescing delay between a device-plugin update and the Node status PATCH (s)")
     ap.add_argument("--ready-file", default="")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
@@ -31,7 +33,7 @@ def main() -> None:
     k = FakeKubelet(a.node, a.apiserver, os.path.join(a.root, "device-plugins"),
                     os.path.join(a.root, "pod-resources", "kubelet.sock"), workdir=a.workdir,
                     log_dir=os.path.join(a.root, "pod-logs"), token=a.token,
-                    schedule=not a.no_schedule)
+                    schedule=not a.no_schedule, node_status_delay=a.node_status_delay)
     k.start()
     if a.ready_file:
         with open(a.ready_file, "w") as f:

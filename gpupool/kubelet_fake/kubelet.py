@@ -70,7 +70,8 @@ class RunningPod:
 class FakeKubelet:
     def __init__(self, node: str, apiserver: str, plugin_dir: str, pod_resources_socket: str,
                  workdir: str | None = None, log_dir: str | None = None, token: str | None = None,
-                 schedule: bool = True, extra_env: dict | None = None):
+                 schedule: bool = True, extra_env: dict | None = None,
+                 node_status_delay: float = 0.02):
         self.node = node
         self.client = Client(apiserver, token)
         self.apiserver = apiserver
@@ -89,6 +90,12 @@ class FakeKubelet:
         self.status_lock = threading.Lock()
         self.stop_ev = threading.Event()
         self._sched_kick = threading.Event()  # unscheduled pod seen or capacity changed
+        # Device-plugin updates reach Node status asynchronously and coalesced, as in a real
+        # kubelet (there: the periodic node-status sync, 10 s by default); a burst of
+        # ListAndWatch updates becomes one PATCH that does not queue in front of the control
+        # plane's own writes on the apiserver.
+        self.node_status_delay = node_status_delay
+        self._status_kick = threading.Event()
         self.threads: list[threading.Thread] = []
         self.reg_server: grpc.Server | None = None
         self.pr_server: grpc.Server | None = None
@@ -115,7 +122,8 @@ class FakeKubelet:
         self.pr_server.add_insecure_port(unix_target(self.pr_socket))
         self.pr_server.start()
         self._ensure_node()
-        for fn, name in ((self._pod_loop, "pods"), (self._reaper, "reaper")):
+        for fn, name in ((self._pod_loop, "pods"), (self._reaper, "reaper"),
+                         (self._node_status_loop, "node-status")):
             t = threading.Thread(target=fn, daemon=True, name=name)
             t.start()
             self.threads.append(t)
@@ -171,7 +179,7 @@ class FakeKubelet:
                         conn.numa = {d.ID: (d.topology.nodes[0].ID if d.topology.nodes else 0)
                                      for d in resp.devices}
                         conn.updates += 1
-                    self._update_node_status()
+                    self._status_kick.set()
                     self._sched_kick.set()  # new or healthier devices may fit a pending pod
                     backoff = 0.05
                     if self.stop_ev.is_set():
@@ -209,6 +217,14 @@ class FakeKubelet:
             if e.code != 409:
                 raise
         self._update_node_status()
+
+    def _node_status_loop(self) -> None:
+        while not self.stop_ev.is_set():
+            if not self._status_kick.wait(0.5):
+                continue
+            time.sleep(self.node_status_delay)  # coalesce a burst of plugin updates
+            self._status_kick.clear()
+            self._update_node_status()
 
     def _update_node_status(self) -> None:
         with self.status_lock:
