@@ -26,6 +26,8 @@ class EventRecorder {
               const std::string& message);
   void flush(std::chrono::milliseconds timeout);
   uint64_t posted() const { return posted_.load(); }
+  // How long a newly queued event waits before it is posted (0 = at once).
+  void set_delay(std::chrono::milliseconds d) { delay_ = d; }
 
  private:
   struct Pending {
@@ -42,6 +44,7 @@ class EventRecorder {
   std::deque<Pending> q_;
   bool stop_ = false;
   int inflight_ = 0;
+  std::chrono::milliseconds delay_{10};
   struct Agg {
     std::string name;
     int64_t count = 0;

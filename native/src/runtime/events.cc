@@ -59,6 +59,13 @@ void EventRecorder::loop_() {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
       if (q_.empty()) return;  // stop_ and drained
+      if (!stop_ && inflight_ == 0 && delay_.count() > 0) {
+        // Events are informational: let the pass that recorded this one finish its status write
+        // first instead of queueing in front of it on the apiserver (system_clock deadline: see
+        // RocmProvider::prefetch for why not wait_for).
+        auto until = std::chrono::system_clock::now() + delay_;
+        cv_.wait_until(lk, until, [this] { return stop_; });
+      }
       p = std::move(q_.front());
       q_.pop_front();
       inflight_++;

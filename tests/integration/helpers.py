@@ -1,7 +1,9 @@
 """Shared helpers for the integration suites (CPU, fake 8x MI355X backend)."""
 from __future__ import annotations
 
-from gpupool.kube import MI355XPOOLS
+import time
+
+from gpupool.kube import EVENTS, MI355XPOOLS
 
 
 def mi_pool(name: str, replicas: int, **spec) -> dict:
@@ -38,3 +40,17 @@ def pause_pod(name: str, resource: str = "amd.com/gpu", n: int = 1, grace: int =
             "spec": {"terminationGracePeriodSeconds": grace,
                      "containers": [{"name": "main", "command": ["sleep", "600"],
                                      "resources": {"limits": {resource: n}}}]}}
+
+
+def settled_events(client, ns: str = "default", quiet: float = 0.15, timeout: float = 5.0) -> list:
+    """The namespace's Events once the manager's recorder has gone quiet (it posts them
+    asynchronously, a few ms after the pass that recorded them)."""
+    deadline = time.monotonic() + timeout
+    last = None
+    while True:
+        items = client.list(EVENTS, ns)["items"]
+        sig = [(e["metadata"]["name"], e.get("count")) for e in items]
+        if sig == last or time.monotonic() > deadline:
+            return items
+        last = sig
+        time.sleep(quiet)

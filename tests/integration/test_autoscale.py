@@ -9,7 +9,7 @@ import pytest
 
 from gpupool.kube import EVENTS, MI355XJOBS, MI355XPOOLS, PODS
 
-from .helpers import mi_pool, pause_pod, wait_ready
+from .helpers import mi_pool, pause_pod, settled_events, wait_ready
 from .test_jobs import job, phase_is
 
 pytestmark = pytest.mark.slow
@@ -50,7 +50,7 @@ def test_pool_follows_pod_and_job_demand(cluster_factory):
     assert time.monotonic() - t0 >= 1.5
     still = {running(k, n)["metadata"]["annotations"]["gpupool.amd.com/devices"] for n in ("w0", "w1")}
     assert still == keep and keep <= {d["uuid"] for d in pool["status"]["devices"]}
-    reasons = [e["reason"] for e in k.list(EVENTS, "default")["items"]
+    reasons = [e["reason"] for e in settled_events(k)
                if e["involvedObject"]["name"] == "auto"]
     assert "AutoscaledUp" in reasons and "AutoscaledDown" in reasons
 

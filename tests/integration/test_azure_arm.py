@@ -20,7 +20,7 @@ from gpupool.kube import AZUREVMPOOLS, EVENTS, SECRETS
 from gpupool.testing.arm_sim import ArmSim
 from gpupool.testing.cluster import make_test_pki
 
-from .helpers import cond_is, conds
+from .helpers import cond_is, conds, settled_events
 
 pytestmark = pytest.mark.slow
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -82,7 +82,7 @@ def arm_cluster(cluster_factory, sim, extra=(), env=None):
 def wait_events(k, want: set, timeout=10.0) -> set:
     deadline = time.monotonic() + timeout
     while True:
-        reasons = {e["reason"] for e in k.list(EVENTS, "default")["items"]}
+        reasons = {e["reason"] for e in settled_events(k)}
         if want <= reasons or time.monotonic() > deadline:
             return reasons
         time.sleep(0.05)

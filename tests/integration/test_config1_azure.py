@@ -12,7 +12,7 @@ import yaml
 
 from gpupool.kube import AZUREVMPOOLS, EVENTS, SECRETS
 
-from .helpers import cond_is, conds
+from .helpers import cond_is, conds, settled_events
 
 pytestmark = pytest.mark.slow
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -82,7 +82,7 @@ def test_scale_up_down_and_cleanup(azure):
     # the event recorder posts asynchronously (aggregated, off the reconcile path): wait for it
     deadline = time.monotonic() + 10
     while True:
-        reasons = {e["reason"] for e in k.list(EVENTS, "default")["items"]}
+        reasons = {e["reason"] for e in settled_events(k)}
         if {"VMCreating", "VMDeleting", "Finalized"} <= reasons or time.monotonic() > deadline:
             break
         time.sleep(0.05)

@@ -12,7 +12,7 @@ import pytest
 from gpupool.kube import EVENTS, MI355XPOOLS
 from gpupool.testing.cluster import NodeSpec
 
-from .helpers import cond_is, mi_pool, wait_ready
+from .helpers import cond_is, mi_pool, settled_events, wait_ready
 
 pytestmark = pytest.mark.slow
 
@@ -61,7 +61,7 @@ def test_bad_hbm_window_quarantines_free_gpu(cluster_factory):
     assert "HBMSweepFailed" in d["quarantine"]["reason"]
     k = cl.client
     # the agent tells the cluster: a Warning Event on the Node
-    ev = wait(lambda: next((e for e in k.list(EVENTS, "default")["items"]
+    ev = wait(lambda: next((e for e in settled_events(k)
                             if e.get("reason") == "HBMSweepFailed"), None))
     assert ev["involvedObject"] == {"kind": "Node", "name": "mi355x-node-0", "apiVersion": "v1"}
     assert ev["type"] == "Warning" and victim in ev["message"]

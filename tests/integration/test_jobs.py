@@ -15,7 +15,7 @@ import yaml
 
 from gpupool.kube import EVENTS, MI355XJOBS, MI355XPOOLS, PODS, KubeError
 
-from .helpers import conds, mi_pool, wait_ready
+from .helpers import conds, mi_pool, settled_events, wait_ready
 
 pytestmark = pytest.mark.slow
 
@@ -79,7 +79,7 @@ def test_ddp_job_gang_runs_to_success(node8, tmp_path):
     assert '"world": 2' in log or "'world': 2" in log, log[-2000:]
     deadline = time.time() + 10  # the manager's event recorder is asynchronous
     while True:
-        reasons = [e["reason"] for e in k.list(EVENTS, "default")["items"]]
+        reasons = [e["reason"] for e in settled_events(k)]
         if "JobSucceeded" in reasons or time.time() > deadline:
             break
         time.sleep(0.05)
@@ -118,7 +118,7 @@ def test_gang_is_all_or_nothing_and_queue_is_ordered(node8):
     for n in ("hold", "high", "low"):
         k.wait_for(MI355XJOBS, n, "default", phase_is("Succeeded"), timeout=60)
     # placement order from the GangScheduled events (each written once: resourceVersion order)
-    evs = sorted(k.list(EVENTS, "default")["items"], key=lambda e: int(e["metadata"]["resourceVersion"]))
+    evs = sorted(settled_events(k), key=lambda e: int(e["metadata"]["resourceVersion"]))
     placed = [e["involvedObject"]["name"] for e in evs
               if e["reason"] == "GangScheduled" and e["involvedObject"]["name"] in ("high", "low")]
     assert placed.index("high") < placed.index("low"), placed
@@ -134,7 +134,7 @@ def test_gang_restart_then_backoff_limit(node8):
     k.create(MI355XJOBS, job("flaky", 2, flaky), "default")
     o = k.wait_for(MI355XJOBS, "flaky", "default", phase_is("Succeeded", "Failed"), timeout=60)
     assert o["status"]["phase"] == "Succeeded" and o["status"]["restarts"] == 1, o["status"]
-    reasons = [e["reason"] for e in k.list(EVENTS, "default")["items"]
+    reasons = [e["reason"] for e in settled_events(k)
                if e["involvedObject"]["name"] == "flaky"]
     assert "GangRestarting" in reasons
     # always failing with backoffLimit 1: two attempts, then Failed/BackoffLimitExceeded
@@ -264,7 +264,7 @@ def test_priority_preemption_picks_fewest_lowest_victims(node8):
     assert low["status"]["preemptions"] == 1 and low["status"]["restarts"] == 0
     mid = k.get(MI355XJOBS, "mid", "default")
     assert mid["status"]["phase"] == "Running" and not mid["status"].get("preemptions")
-    reasons = {(e["involvedObject"]["name"], e["reason"]) for e in k.list(EVENTS, "default")["items"]}
+    reasons = {(e["involvedObject"]["name"], e["reason"]) for e in settled_events(k)}
     assert ("urgent", "Preempting") in reasons and ("low", "Preempted") in reasons
     # the preemptor never overlapped a victim's pod on a GPU
     devs_u = {r.get("devices") for r in
@@ -448,7 +448,7 @@ def test_gpu_fault_under_running_gang_restarts_it_on_healthy_gpus(node8):
     assert o["status"]["restarts"] == 1
     assert conds(o)["Restarting"]["reason"] == "Restarted"
     assert any(e["reason"] == "GangRestarting" and e["involvedObject"]["name"] == "tr"
-               for e in k.list(EVENTS, "default")["items"])
+               for e in settled_events(k))
     devs = {r["devices"] for r in o["status"]["replicaStatuses"]}
     assert victim not in devs and len(devs) == 2
     node8.set_faults("mi355x-node-0", {})

@@ -9,7 +9,7 @@ import pytest
 from gpupool.kube import EVENTS, MI355XPOOLS, NODES, PODS, KubeError
 from gpupool.testing.cluster import NodeSpec
 
-from .helpers import cond_is, conds, mi_pool, pause_pod, ready_at, wait_ready
+from .helpers import cond_is, conds, mi_pool, pause_pod, ready_at, settled_events, wait_ready
 
 pytestmark = pytest.mark.slow
 
@@ -75,7 +75,7 @@ def test_config4_scale_down_8_to_4_with_drain(node8):
     for d in view["devices"]:
         if d["uuid"] not in kept:
             assert d["state"] == "Free" and not d["pods"]  # no pod left on a released GPU
-    reasons = {e["reason"] for e in k.list(EVENTS, "default")["items"]}
+    reasons = {e["reason"] for e in settled_events(k)}
     assert {"DrainStarted", "PodEvicted", "GPUReleased"} <= reasons
     # finalizer-guarded delete: pods evicted, GPUs released, then the CR disappears
     k.delete(MI355XPOOLS, "p", "default")
@@ -168,7 +168,7 @@ def test_probe_failure_replaced(cluster_factory):
     k.create(MI355XPOOLS, mi_pool("p", 2), "default")
     o = wait_ready(k, "p", 2, timeout=30)
     assert {d["index"] for d in o["status"]["devices"]}.isdisjoint({0, 1})
-    reasons = {e["reason"] for e in k.list(EVENTS, "default")["items"]}
+    reasons = {e["reason"] for e in settled_events(k)}
     assert "HealthDegraded" in reasons
 
 
@@ -183,7 +183,7 @@ def test_performance_floor_replaces_slow_gpu(cluster_factory):
     o = wait_ready(k, "p", 2, timeout=30)
     assert 0 not in {d["index"] for d in o["status"]["devices"]}
     assert all(d["probe"]["mfmaTflops"] >= 1000 for d in o["status"]["devices"])
-    msgs = " ".join(e.get("message", "") for e in k.list(EVENTS, "default")["items"])
+    msgs = " ".join(e.get("message", "") for e in settled_events(k))
     assert "PerformanceBelowFloor" in msgs and "MFMA 600 TFLOP/s < floor 1000" in msgs
 
 
@@ -422,11 +422,11 @@ def test_drain_respects_pod_disruption_budget(node8):
     k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 1}}, "default")
 
     def blocked(_o):
-        return any(e["reason"] == "EvictionBlocked" for e in k.list(EVENTS, "default")["items"])
+        return any(e["reason"] == "EvictionBlocked" for e in settled_events(k))
     try:
         k.wait_for(MI355XPOOLS, "p", "default", blocked, timeout=20)
     except TimeoutError:  # diagnostics for a rare flake seen once under full-suite load
-        ev = [(e["reason"], e.get("message", "")[:120]) for e in k.list(EVENTS, "default")["items"]]
+        ev = [(e["reason"], e.get("message", "")[:120]) for e in settled_events(k)]
         pods = [(p["metadata"]["name"], p["status"].get("phase"),
                  p["metadata"].get("annotations", {}).get("gpupool.amd.com/devices"))
                 for p in k.list(PODS, "default")["items"]]
@@ -478,7 +478,7 @@ def test_xgmi_peer_check(cluster_factory):
     devs = o["status"]["devices"]
     assert 1 not in {d["index"] for d in devs}
     assert all(d["probe"]["xgmiGBps"] > 10 for d in devs)
-    msgs = " ".join(e.get("message", "") for e in k.list(EVENTS, "default")["items"])
+    msgs = " ".join(e.get("message", "") for e in settled_events(k))
     assert "XGMIPeerCheckFailed" in msgs
 
 
@@ -634,7 +634,7 @@ def test_spanning_claim_is_all_or_nothing(cluster_factory):
     assert o["status"].get("replicas", 0) == 0
     for n in ("node-a", "node-b"):
         assert not any(d.get("pool") == "default/strict" for d in agent_view(c, n)["devices"])
-    msgs = " ".join(e.get("message", "") for e in k.list(EVENTS, "default")["items"])
+    msgs = " ".join(e.get("message", "") for e in settled_events(k))
     assert "other claims released" in msgs
 
 
