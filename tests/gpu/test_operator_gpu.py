@@ -55,7 +55,10 @@ def test_config2_pool_ready_on_real_gpu(cluster_factory):
     conds = {x["type"]: x["status"] for x in obj["status"]["conditions"]}
     assert conds["XGMILinksHealthy"] == "True" and conds["HBMECCHealthy"] == "True"
     assert conds["ThermalHealthy"] == "True" and conds["DeviceProbePassed"] == "True"
-    node = k.get(__import__("gpupool.kube", fromlist=["NODES"]).NODES, "gpu-node")
+    # the kubelet reports device-plugin capacity in Node status asynchronously (coalesced)
+    node = k.wait_for(__import__("gpupool.kube", fromlist=["NODES"]).NODES, "gpu-node", None,
+                      lambda n: (n["status"].get("allocatable") or {}).get("amd.com/gpu") == "1",
+                      timeout=10)
     assert node["status"]["allocatable"]["amd.com/gpu"] == "1"
 
 
