@@ -57,6 +57,7 @@ struct Flags {
   std::string health_addr;
   std::string port_file;
   int resync_ms = 10000;
+  int event_delay_ms = 10;
   int progress_ms = 250;
   int cred_retry_ms = 30000;
   int agent_timeout_ms = 60000;
@@ -103,6 +104,7 @@ in-cluster ServiceAccount, ~/.kube/config, http://127.0.0.1:6443:
 controllers:
   --kinds mi355x,azure,job     reconcilers to run            --namespace NS   watch one namespace
   --workers N (4)              reconcile worker threads      --resync D (10s) steady-state resync
+  --event-delay D (10ms)       Events post this long after the pass that records them
   --progress-poll D (250ms)    requeue while scaling/draining
   --credentials-retry D (30s)  AzureVmPool retry after a credentials error
   --agent-timeout D (60s)      node-agent RPC timeout (covers on-claim GPU probes)
@@ -175,6 +177,7 @@ Flags parse(int argc, char** argv) {
     else if (is("--health-addr")) f.health_addr = val();
     else if (is("--port-file")) f.port_file = val();
     else if (is("--resync")) f.resync_ms = parse_duration_ms(val());
+    else if (is("--event-delay")) f.event_delay_ms = parse_duration_ms(val());
     else if (is("--progress-poll")) f.progress_ms = parse_duration_ms(val());
     else if (is("--credentials-retry")) f.cred_retry_ms = parse_duration_ms(val());
     else if (is("--agent-timeout")) f.agent_timeout_ms = parse_duration_ms(val());
@@ -487,6 +490,7 @@ int main(int argc, char** argv) {
 
   auto run_controllers = [&]() {
     EventRecorder events(&client, "gpupool-manager");
+    events.set_delay(std::chrono::milliseconds(f.event_delay_ms));
     Controller ctl(f.workers);
     ReconcilerOptions ropts;
     ropts.resync = std::chrono::milliseconds(f.resync_ms);

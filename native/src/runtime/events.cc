@@ -54,29 +54,32 @@ void EventRecorder::flush(std::chrono::milliseconds timeout) {
 
 void EventRecorder::loop_() {
   for (;;) {
-    Pending p;
+    std::deque<Pending> batch;
     {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
       if (q_.empty()) return;  // stop_ and drained
-      if (!stop_ && inflight_ == 0 && delay_.count() > 0) {
-        // Events are informational: let the pass that recorded this one finish its status write
-        // first instead of queueing in front of it on the apiserver (system_clock deadline: see
-        // RocmProvider::prefetch for why not wait_for).
+      if (!stop_ && delay_.count() > 0) {
+        // Events are informational: let the pass that recorded the first of a burst finish its
+        // status write before they reach the apiserver; the whole burst then goes out back to back
+        // (one delay per burst, so a busy manager never falls behind). system_clock deadline: see
+        // RocmProvider::prefetch for why not wait_for.
         auto until = std::chrono::system_clock::now() + delay_;
         cv_.wait_until(lk, until, [this] { return stop_; });
       }
-      p = std::move(q_.front());
-      q_.pop_front();
-      inflight_++;
+      batch.swap(q_);
+      inflight_ += static_cast<int>(batch.size());
     }
-    try {
-      if (client_) post_(p);
-    } catch (const std::exception& e) {
-      Logger("events").warn("event post failed", Json::object().set("error", e.what()).set("reason", p.reason));
+    for (const Pending& p : batch) {
+      try {
+        if (client_) post_(p);
+      } catch (const std::exception& e) {
+        Logger("events").warn("event post failed", Json::object().set("error", e.what()).set("reason", p.reason));
+      }
+      std::lock_guard<std::mutex> g(mu_);
+      inflight_--;
     }
-    std::lock_guard<std::mutex> g(mu_);
-    inflight_--;
+    cv_.notify_all();
   }
 }
 
