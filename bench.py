@@ -139,7 +139,32 @@ def sweep_for(n: int) -> list[int]:
     return sorted({k for k in (1, 2, 4, 8) if k <= n} | {n})
 
 
+def _err(e: BaseException, phase: str, **kw) -> dict:
+    msg = f"{type(e).__name__}: {e}".strip()
+    return {"error": msg[:400], "phase": phase, **kw}
+
+
+def _span_p50(traces: list[dict]) -> dict:
+    """Median ms per span name (spans summed within a pass) over reconcile traces, + pass count."""
+    per_span: dict[str, list[float]] = {}
+    for t in traces:
+        per: dict[str, float] = {}
+        for sp in t["spans"]:
+            per[sp["name"]] = per.get(sp["name"], 0.0) + sp["ms"]
+        per["total"] = t["totalMs"]
+        for k, v in per.items():
+            per_span.setdefault(k, []).append(v)
+    out = {k: round(statistics.median(v), 3) for k, v in sorted(per_span.items())}
+    out["passes"] = len(traces)
+    return out
+
+
+def _window(traces: list[dict], t0: float, t1: float) -> list[dict]:
+    return [t for t in traces if t0 <= t["start"] <= t1]
+
+
 def main() -> int:
+    t_main = time.monotonic()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -150,6 +175,9 @@ def main() -> int:
     ap.add_argument("--workdir", default="")
     ap.add_argument("--keep", action="store_true", help="keep the workdir (logs)")
     ap.add_argument("--timeout", type=float, default=120.0, help="per-transition timeout (s)")
+    ap.add_argument("--budget-s", type=float, default=480.0,
+                    help="wall budget for the whole run (s): work not started by then is skipped "
+                         "and reported as such; the JSON line is always printed")
     ap.add_argument("--sample-interval", type=float, default=1.0,
                     help="agent full-telemetry sample period (s)")
     ap.add_argument("--scale-down-steps", type=int, default=3, help="config 4 repetitions (0 = skip)")
@@ -158,10 +186,20 @@ def main() -> int:
                     help="config 1 (AzureVmPool replicas=0 -> Ready) repetitions (0 = skip)")
     ap.add_argument("--health-steps", type=int, default=5,
                     help="fault->condition measurements (0 = skip)")
+    ap.add_argument("--fault-steps", type=int, default=20,
+                    help="readyReplicas-vs-ground-truth checks after random fault/clear steps "
+                         "(accuracy_under_faults; 0 = skip)")
     ap.add_argument("--comm-check", default="auto", choices=["auto", "gloo", "off"],
                     help="after the timed region with N>1 ranks: all-reduce across the ranks' "
                          "GPUs over RCCL (auto: when the GPUs are real) or gloo on CPU")
+    ap.add_argument("--inject-claim-hang", default="",
+                    help="fault injection: COUNT:SECONDS — the agent stalls every claim of >= "
+                         "COUNT GPUs (exercises the bench's failure isolation)")
     args = ap.parse_args()
+    deadline = t_main + args.budget_s
+
+    def budget_left() -> float:
+        return deadline - time.monotonic()
 
     rank, world = _dist_init()
     n = args.gpus
@@ -173,114 +211,225 @@ def main() -> int:
 
     cluster = run = pool = None
     cycles: list[dict] = []
+    errors: dict[str, list[dict]] = {}     # per N (str) and per scenario
+    skipped: dict[str, str] = {}
+    failed_at: int | None = None           # smallest N whose cycle failed: larger N are skipped
+    pool_ok = True                         # the bench pool is back at 0 after every failure
+    setup_error: dict | None = None
+    timed_steps = 0
     if rank == 0:
         from gpupool.bench.runner import BenchRun
         from gpupool.testing.cluster import Cluster, NodeSpec
         workdir = args.workdir or tempfile.mkdtemp(prefix="gpupool-bench-")
         # fake mode: simulated probe latency calibrated to the measured real 1 GiB probe
         # (profiles/r1z_bench_kernel_stats.csv: ~1.0 ms claim-time probe)
+        extra = [] if real else ["--probe-sim-ms", "1.0"]
+        if args.inject_claim_hang:
+            extra += ["--inject-claim-delay", args.inject_claim_hang]
         node = NodeSpec("mi355x-node-0", backend="amdsmi" if real else "fake",
                         probe="inproc" if real else "simulated",
-                        count=-1 if real else max(8, n),
-                        extra_args=[] if real else ["--probe-sim-ms", "1.0"])
+                        count=-1 if real else max(8, n), extra_args=extra)
         # production agent settings: ledger fsync on, 100 ms health poll, full sample every 1 s
         cluster = Cluster(workdir, nodes=[node], sample_interval=args.sample_interval, fsync=True)
-        cluster.start()  # all child processes exist before anything touches the GPU
-        run = BenchRun(cluster, node, real, hbm_bytes=args.hbm_bytes, timeout=args.timeout)
-        pool = run.make_pool("bench-pool", "amd.com/gpu", 0)
-        run.scale("bench-pool", 0)
-        run.refresh_health()  # also fixes the ECC baseline (CLI) for the whole run
-        for _ in range(args.warmup):
+        try:
+            cluster.start()  # all child processes exist before anything touches the GPU
+            run = BenchRun(cluster, node, real, hbm_bytes=args.hbm_bytes, timeout=args.timeout,
+                           deadline=deadline)
+            pool = run.make_pool("bench-pool", "amd.com/gpu", 0)
+            run.scale("bench-pool", 0)
+            run.refresh_health()  # also fixes the ECC baseline (CLI) for the whole run
+        except Exception as e:
+            setup_error = _err(e, "setup")
+            pool_ok = False
+
+        def failed(k: int, e: BaseException, step: int, stage: str) -> None:
+            nonlocal failed_at, pool_ok
+            errors.setdefault(str(k), []).append(_err(e, f"{stage}:{run.phase}", step=step))
+            failed_at = k if failed_at is None else min(failed_at, k)
+            pool_ok = run.recover("bench-pool", min(max(args.timeout, 30.0), budget_left()))
+            if not pool_ok:
+                errors.setdefault(str(k), []).append(
+                    {"error": "pool did not return to 0 replicas", "phase": "recover", "step": step})
+
+        for w in range(args.warmup if pool_ok else 0):
             for k in sweep:
-                run.cycle(pool, k)
-        run.gt_s = 0.0
+                if not pool_ok or (failed_at is not None and k >= failed_at) or budget_left() <= 0:
+                    continue
+                try:
+                    run.cycle(pool, k)
+                except Exception as e:
+                    failed(k, e, w, "warmup")
+        if run:
+            run.gt_s = 0.0
     _barrier(world)
     t_start = time.perf_counter()
-    if rank == 0:
-        for _ in range(args.steps):
-            run.refresh_health()
+    if rank == 0 and pool_ok:
+        for step in range(args.steps):
+            if budget_left() <= 0:
+                skipped["timed_steps"] = f"{args.steps - step} of {args.steps} not started: " \
+                                         f"wall budget ({args.budget_s:.0f} s) exhausted"
+                break
+            try:
+                run.refresh_health()
+            except Exception as e:
+                errors.setdefault("ground_truth", []).append(_err(e, "refresh_health", step=step))
             for k in sweep:
-                cycles.append(run.cycle(pool, k))
+                if failed_at is not None and k >= failed_at:
+                    continue
+                if budget_left() <= 0:
+                    break
+                try:
+                    cycles.append(run.cycle(pool, k))
+                except Exception as e:
+                    failed(k, e, step, "timed")
+                    if not pool_ok:
+                        break
+            timed_steps += 1
+            if not pool_ok:
+                skipped["timed_steps"] = f"{args.steps - step - 1} of {args.steps} not started: " \
+                                         "the bench pool could not be recovered"
+                break
     _barrier(world)
     elapsed = _gather_max(world, time.perf_counter() - t_start)
 
     if rank == 0:
         from gpupool.bench.runner import summary
-        gt_s = run.gt_s
-        try:  # the timed cycles' traces, before the secondary scenarios push them out of the ring
-            traces = cluster.manager_traces(key="Mi355xPool/default/bench-pool", n=1024)
-        except Exception:
-            traces = []
-        per_n = {}
+        gt_s = run.gt_s if run else 0.0
+
+        def traces_now() -> list:
+            try:
+                return cluster.manager_traces(n=2048)
+            except Exception:
+                return []
+        traces = [t for t in traces_now() if t.get("key") in (None, "Mi355xPool/default/bench-pool")]
+        per_n: dict[str, dict] = {}
         for k in sweep:
             cs = [cy for cy in cycles if cy["n"] == k]
             per_n[str(k)] = summary([cy["readySeconds"] for cy in cs], sum(cy["ok"] for cy in cs))
+            if str(k) in errors:
+                per_n[str(k)]["errors"] = errors[str(k)]
+                first = errors[str(k)][0]
+                per_n[str(k)].update({"error": first["error"], "phase": first["phase"]})
+            elif not cs:
+                per_n[str(k)]["skipped"] = (f"N={failed_at} failed earlier" if failed_at is not None
+                                            and k > failed_at else skipped.get("timed_steps")
+                                            or ("setup failed" if setup_error else "not run"))
         secondary: dict = {}
-        if args.scale_down_steps > 0:
-            sd = [run.scale_down(pool, n, i) for i in range(args.scale_down_steps)]
-            secondary["scale_down"] = {
-                **{k2: v for k2, v in summary([x["seconds"] for x in sd],
-                                              sum(x["ok"] for x in sd)).items()},
-                "from": n, "to": n // 2, "evicted_per_step": [x["evicted"] for x in sd],
-                "pods_left_on_released_gpus": sum(len(x["podsOnReleasedGPUs"]) for x in sd)}
+
+        def scenario(name: str, reps: int, fn, needs_pool: bool = True):
+            """Run ``fn(i)`` reps times, isolated: an exception is recorded with its phase and the
+            remaining reps are skipped; the bench pool is brought back to 0 before going on."""
+            nonlocal pool_ok
+            if reps <= 0:
+                return None
+            if setup_error is not None:
+                secondary[name] = {"skipped": "setup failed"}
+                return None
+            if needs_pool and not pool_ok:
+                secondary[name] = {"skipped": "the bench pool could not be recovered"}
+                return None
+            out, t0w = [], time.time()
+            for i in range(reps):
+                if budget_left() <= 0:
+                    secondary.setdefault(name, {})["skipped_steps"] = \
+                        f"{reps - i} of {reps}: wall budget exhausted"
+                    break
+                try:
+                    out.append(fn(i))
+                except Exception as e:
+                    secondary.setdefault(name, {})["error"] = _err(e, run.phase, step=i)
+                    pool_ok = run.cleanup(pool, name, i, min(max(args.timeout, 30.0), max(1.0, budget_left())))
+                    break
+            secondary.setdefault(name, {})["_window"] = (t0w, time.time())
+            return out
+
+        if pool_ok and n >= 1:
+            sd = scenario("scale_down", args.scale_down_steps, lambda i: run.scale_down(pool, n, i))
+            if sd:
+                secondary["scale_down"].update({
+                    **summary([x["seconds"] for x in sd], sum(x["ok"] for x in sd)),
+                    "from": n, "to": n // 2, "evicted_per_step": [x["evicted"] for x in sd],
+                    "pods_left_on_released_gpus": sum(len(x["podsOnReleasedGPUs"]) for x in sd)})
+        elif args.scale_down_steps > 0:
+            secondary["scale_down"] = {"skipped": "the bench pool could not be recovered"
+                                       if setup_error is None else "setup failed"}
         if args.pool_steps > 0 and n >= 2:
-            tp = [run.two_pools(n, i) for i in range(args.pool_steps)]
-            secondary["two_pools"] = {
-                **summary([x["seconds"] for x in tp], sum(x["ok"] for x in tp)),
-                "pools": [n // 2, n // 2],
-                "cross_pool_devices": sum(x["crossPoolDevices"] for x in tp)}
+            tp = scenario("two_pools", args.pool_steps, lambda i: run.two_pools(n, i),
+                          needs_pool=False)
+            if tp:
+                secondary["two_pools"].update({
+                    **summary([x["seconds"] for x in tp], sum(x["ok"] for x in tp)),
+                    "pools": [n // 2, n // 2],
+                    "cross_pool_devices": sum(x["crossPoolDevices"] for x in tp)})
         elif args.pool_steps > 0:
             secondary["two_pools"] = {"skipped": "needs >= 2 GPUs (two pools of N//2)"}
-        if args.azure_steps > 0:
-            az = [run.azure_pool(i) for i in range(args.azure_steps)]
-            secondary["azure_config1"] = {
+        az = scenario("azure_config1", args.azure_steps, lambda i: run.azure_pool(i),
+                      needs_pool=False)
+        if az:
+            secondary["azure_config1"].update({
                 **summary([x["seconds"] for x in az], sum(x["ok"] for x in az)),
                 "delete_p50_s": round(statistics.median(x["deleteSeconds"] for x in az), 4),
-                "replicas": 0, "cloud": "in-process fake cloud"}
-        health = run.health(pool, args.health_steps) if args.health_steps > 0 else {}
+                "replicas": 0, "cloud": "in-process fake cloud"})
+        health: dict = {}
+        if args.health_steps > 0:
+            hs = scenario("health", 1, lambda i: run.health(pool, args.health_steps))
+            got = secondary.pop("health", {})
+            health = hs[0] if hs else {k: v for k, v in got.items() if k != "_window"}
+        if args.fault_steps > 0:
+            fa = scenario("accuracy_under_faults", 1,
+                          lambda i: run.accuracy_under_faults(min(n, 8), args.fault_steps))
+            if fa:
+                secondary["accuracy_under_faults"].update(fa[0])
         try:
-            agent_stats = run.agent_stats()
+            agent_stats = run.agent_stats() if run else {}
         except Exception as e:
             agent_stats = {"error": repr(e)}
         try:
             metrics = cluster.manager_metrics()
         except Exception:
             metrics = ""
+        all_traces = traces_now()
+        # pass-span breakdown of each secondary scenario (scale-down passes, two-pool claims)
+        scen_traces = {}
+        for name, v in secondary.items():
+            w = v.pop("_window", None) if isinstance(v, dict) else None
+            if w:
+                tr = _window(all_traces, *w)
+                scen_traces[name] = tr
+                if tr:
+                    v["pass_span_p50_ms"] = _span_p50(tr)
         cluster.stop()
-        # latency breakdown of the scale-up passes (the reconcile that claims): median per span
+        # latency breakdown of the scale-up passes (the reconcile that claims): per timed cycle,
+        # the first claiming pass between its PATCH and its Ready
         claim_traces = [t for t in traces
-                        if any(s["name"] == "agent:POST /v1/claims" for s in t["spans"])]
-        span_ms: dict[str, list[float]] = {}
-        for t in claim_traces[:args.steps * len(sweep)]:
-            per: dict[str, float] = {}
-            for s in t["spans"]:
-                per[s["name"]] = per.get(s["name"], 0.0) + s["ms"]
-            per["total"] = t["totalMs"]
-            for k2, v in per.items():
-                span_ms.setdefault(k2, []).append(v)
-        span_p50 = {k2: round(statistics.median(v), 3) for k2, v in sorted(span_ms.items())}
-        # end-to-end accounting of each timed cycle (wall clocks of one host): PATCH -> the
-        # manager's claiming pass starts (apiserver write + watch + queue), the pass itself, and
-        # its status write -> the client's watch sees Ready
+                        if any(sp["name"] == "agent:POST /v1/claims" for sp in t["spans"])]
         e2e: dict[str, list[float]] = {"patch_to_pass_ms": [], "pass_ms": [],
                                        "status_to_client_ms": []}
+        by_n: dict[int, list[dict]] = {}
         for cy in cycles:
             hit = [t for t in claim_traces if cy["patchAt"] <= t["start"] <= cy["readyAtWall"]]
             if not hit:
                 continue
             t = min(hit, key=lambda x: x["start"])
+            by_n.setdefault(cy["n"], []).append(t)
             e2e["patch_to_pass_ms"].append((t["start"] - cy["patchAt"]) * 1e3)
             e2e["pass_ms"].append(t["totalMs"])
             e2e["status_to_client_ms"].append(
                 (cy["readyAtWall"] - t["start"]) * 1e3 - t["totalMs"])
+        span_per_n = {str(k): _span_p50(v) for k, v in sorted(by_n.items())}
         e2e_p50 = {k2: round(statistics.median(v), 3) for k2, v in e2e.items() if v}
         e2e_p50["cycles_matched"] = len(e2e["pass_ms"])
-        head = per_n[str(n)]
+        done = [k for k in sweep if per_n[str(k)]["p50_s"] is not None]
+        value_n = max(done) if done else None
+        head = per_n[str(value_n)] if value_n is not None else {"p50_s": None, "p90_s": None,
+                                                               "max_s": None}
         all_ok = sum(cy["ok"] for cy in cycles)
         src = ("real MI355X: amdsmi discovery + gfx950 HIP probe (HBM %d MiB + bf16 MFMA) + device "
                "plugin -> fake kubelet" % (args.hbm_bytes >> 20)) if real else \
               ("synthetic: 8x MI355X fake fixture (no GPU visible), simulated probe, device plugin "
                "-> fake kubelet")
+        status = "ok" if value_n == n and not errors and not skipped and setup_error is None \
+            else "partial" if value_n is not None else "failed"
         out = {
             "metric": METRIC,
             "value": head["p50_s"],
@@ -288,12 +437,15 @@ def main() -> int:
             "n_gpus": n,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed * 1e3 / max(1, args.steps), 2),
+            "ms_per_step": round(elapsed * 1e3 / max(1, timed_steps), 2),
             "higher_is_better": False,
             "scaling": "weak",
-            "vs_baseline": round(head["p50_s"] / BASELINE_TARGET_S, 5),
+            "vs_baseline": round(head["p50_s"] / BASELINE_TARGET_S, 5)
+            if head["p50_s"] is not None else None,
             "dtype": "bf16",
             "data": src + "; control plane against the in-repo apiserver-sim (no kube-apiserver/etcd)",
+            "status": status,
+            "value_n": value_n,
             "config": {
                 "model": "Mi355xPool scale 0->n, n in %s (BASELINE configs 2/3/4/5; config 1 in "
                          "azure_config1)" % sweep,
@@ -303,25 +455,38 @@ def main() -> int:
                 "backend": "amdsmi+hip" if real else "fake",
                 "dtype_note": "bf16 = the probe's MFMA GEMM check; the metric is a control-plane latency",
                 "baseline_target_s": BASELINE_TARGET_S,
+                "value_note": "p50 at replicas=%s (%s)" % (
+                    value_n, "the requested N" if value_n == n else
+                    "the largest N that completed; see per_n for the failure"),
                 "p90_s": head["p90_s"],
                 "max_s": head["max_s"],
                 "readyReplicas_accuracy": all_ok / len(cycles) if cycles else None,
                 "per_n": per_n,
-                "operator_ms_per_step": round((elapsed - gt_s) * 1e3 / max(1, args.steps), 2),
-                "ground_truth_ms_per_step": round(gt_s * 1e3 / max(1, args.steps), 2),
+                "timed_steps_completed": timed_steps,
+                "operator_ms_per_step": round((elapsed - gt_s) * 1e3 / max(1, timed_steps), 2),
+                "ground_truth_ms_per_step": round(gt_s * 1e3 / max(1, timed_steps), 2),
                 **secondary,
                 "health_condition_latency": health,
                 "sample_interval_s": args.sample_interval,
                 "health_poll_interval_s": 0.1,
                 "agent": agent_stats,
                 "world_size": world,
-                "claim_pass_span_p50_ms": span_p50,
+                "claim_pass_span_p50_ms": span_per_n.get(str(value_n), {}),
+                "claim_pass_span_p50_ms_per_n": span_per_n,
                 "e2e_breakdown_p50_ms": e2e_p50,
+                "budget": {"budget_s": args.budget_s,
+                           "used_s": round(time.monotonic() - t_main, 2),
+                           "skipped": skipped},
                 "steps_detail": [{k2: (round(v, 4) if isinstance(v, float) else v)
                                   for k2, v in cy.items() if k2 not in ("patchAt", "readyAtWall")}
                                  for cy in cycles[:len(sweep)]],
             },
         }
+        if setup_error is not None:
+            out["config"]["setup_error"] = setup_error
+        for k in ("ground_truth",):
+            if k in errors:
+                out["config"]["ground_truth_errors"] = errors[k]
     comm_backend = "gloo" if args.comm_check == "gloo" else "nccl" if real else ""
     if world > 1 and args.comm_check != "off" and comm_backend:
         comm = _comm_check(rank, world, comm_backend)
@@ -337,6 +502,9 @@ def main() -> int:
                 f.write(metrics)
             with open(os.path.join(cluster.workdir, "traces.json"), "w") as f:
                 json.dump(traces, f, indent=1)
+            for name, tr in scen_traces.items():
+                with open(os.path.join(cluster.workdir, f"traces_{name}.json"), "w") as f:
+                    json.dump(tr, f, indent=1)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -12,6 +12,13 @@ import sys
 from .agent import Agent, AgentConfig, serve
 
 
+def _count_seconds(v: str) -> tuple[int, float]:
+    if not v:
+        return (0, 0.0)
+    c, _, sec = v.partition(":")
+    return (int(c), float(sec or 0))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser(description="gpupool node agent (MI355X)")
     ap.add_argument("--node", default=os.environ.get("GPUPOOL_NODE", socket.gethostname()))
@@ -59,6 +66,9 @@ def main() -> None:
                     default=float(os.environ.get("GPUPOOL_GIL_SWITCH_INTERVAL", "0.0005")),
                     help="sys.setswitchinterval for the agent (s): how long a thread that wants "
                          "the GIL waits for the holder to yield (CPython default 0.005)")
+    ap.add_argument("--inject-claim-delay", default="",
+                    help="fault injection (tests/bench): COUNT:SECONDS — a claim of >= COUNT GPUs "
+                         "stalls SECONDS before selecting devices (a hung probe / driver call)")
     ap.add_argument("--ready-file", default="")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
@@ -83,7 +93,8 @@ def main() -> None:
                       fsync=not a.no_fsync, probe_arena_idle_s=a.probe_arena_idle,
                       scrub_interval_s=a.scrub_interval, scrub_window_bytes=a.scrub_window,
                       scrub_windows=a.scrub_windows, scrub_reserve_bytes=a.scrub_reserve,
-                      scrub_start_delay_s=a.scrub_start_delay)
+                      scrub_start_delay_s=a.scrub_start_delay,
+                      inject_claim_delay=_count_seconds(a.inject_claim_delay))
     agent = Agent(cfg)
     try:
         asyncio.run(serve(agent, a.ready_file or None))

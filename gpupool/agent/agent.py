@@ -81,6 +81,7 @@ class AgentConfig:
     scrub_windows: int = 8            # windows per device per pass
     scrub_reserve_bytes: int = 4 << 30
     scrub_start_delay_s: float = 30.0
+    inject_claim_delay: tuple = (0, 0.0)  # (min count, seconds): fault injection for tests/bench
 
 
 class Agent:
@@ -748,6 +749,10 @@ class Agent:
 
     def _claim_start(self, req: dict) -> dict:
         pool_uid, count = req["poolUID"], int(req["count"])
+        min_count, stall = self.cfg.inject_claim_delay
+        if min_count > 0 and count >= min_count and stall > 0:
+            log.warning("fault injection: claim of %d GPU(s) stalls %.1f s", count, stall)
+            time.sleep(stall)
         policy = req.get("policy") or {}
         resource = req.get("resourceName") or schema.DEFAULT_RESOURCE
         probe_opts = req.get("probe") or {}

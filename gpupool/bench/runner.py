@@ -19,6 +19,7 @@ independent ownership oracle (``ground_truth.pool_truth``).
 """
 from __future__ import annotations
 
+import os
 import statistics
 import time
 from dataclasses import dataclass, field
@@ -69,6 +70,25 @@ class BenchRun:
     baseline_cli: dict = field(default_factory=dict)
     healthy: set = field(default_factory=set)
     gt_s: float = 0.0             # time spent in ground-truth reads (reported separately)
+    deadline: float = 0.0         # time.monotonic() wall budget end (0 = none): caps every wait
+    phase: str = ""               # what the scenario is doing now (named in error records)
+
+    def _to(self) -> float:
+        """Per-wait timeout: the per-transition limit, cut to what the wall budget has left."""
+        if not self.deadline:
+            return self.timeout
+        return max(1.0, min(self.timeout, self.deadline - time.monotonic()))
+
+    def recover(self, name: str, timeout: float) -> bool:
+        """After a failed scenario step: scale ``name`` back to 0 and wait (bounded) for it, so
+        the next measurement starts from a clean pool. False if the pool did not get there."""
+        self.phase = "recover"
+        try:
+            self.c.patch(MI355XPOOLS, name, {"spec": {"replicas": 0}}, self.ns)
+            self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(0), timeout=max(1.0, timeout))
+            return True
+        except Exception:
+            return False
 
     @property
     def c(self):
@@ -138,7 +158,7 @@ class BenchRun:
     def scale(self, name: str, r: int, wait: bool = True) -> dict | None:
         self.c.patch(MI355XPOOLS, name, {"spec": {"replicas": r}}, self.ns)
         if wait:
-            return self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(r), timeout=self.timeout)
+            return self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(r), timeout=self._to())
         return None
 
     def delete_pool(self, name: str) -> None:
@@ -147,18 +167,21 @@ class BenchRun:
         except KubeError as e:
             if e.code != 404:
                 raise
-        self.c.wait_for(MI355XPOOLS, name, self.ns, lambda o: o is None, timeout=self.timeout)
+        self.c.wait_for(MI355XPOOLS, name, self.ns, lambda o: o is None, timeout=self._to())
 
     # ------------------------------------------------------------ config 2/3
     def cycle(self, pool: dict, n: int) -> dict:
         name = pool["metadata"]["name"]
         patch_at = time.time()  # wall clock, to place the manager's trace of this cycle
         t0 = time.perf_counter()
+        self.phase = "scale_up"
         obj = self.scale(name, n)
         t_ready = time.perf_counter() - t0
         ready_at_wall = patch_at + t_ready
+        self.phase = "ground_truth"
         truth = self.wait_truth(pool, n)
         ok = truth["ready"] == obj["status"]["readyReplicas"] == n and truth.get("ledgerAgrees", True)
+        self.phase = "release"
         self.scale(name, 0)
         return {"n": n, "readySeconds": t_ready, "ok": ok, "truth": truth,
                 "patchAt": patch_at, "readyAtWall": ready_at_wall,
@@ -179,7 +202,7 @@ class BenchRun:
         for nm in names:
             self.c.wait_for(PODS, nm, self.ns,
                             lambda o: bool(o) and o["status"].get("phase") == "Running",
-                            timeout=self.timeout)
+                            timeout=self._to())
         return names
 
     def _delete_pods(self, names: list[str]) -> None:
@@ -190,15 +213,18 @@ class BenchRun:
                 if e.code != 404:
                     raise
         for nm in names:
-            self.c.wait_for(PODS, nm, self.ns, lambda o: o is None, timeout=self.timeout)
+            self.c.wait_for(PODS, nm, self.ns, lambda o: o is None, timeout=self._to())
 
     def scale_down(self, pool: dict, n: int, step: int) -> dict:
         """n GPUs busy with one pod each -> replicas n//2: cordon, evict, wait, release."""
         name, res = pool["metadata"]["name"], pool["spec"]["resourceName"]
         keep = n // 2
+        self.phase = "scale_up"
         self.scale(name, n)
+        self.phase = "start_pods"
         pods = self._pods(f"sd{step}", n, res)
         t0 = time.perf_counter()
+        self.phase = "scale_down"
         obj = self.scale(name, keep)
         dt = time.perf_counter() - t0
         kept = {d["uuid"] for d in obj["status"]["devices"]}
@@ -210,6 +236,7 @@ class BenchRun:
                                   .get("gpupool.amd.com/devices", "").split(",")) <= kept]
         ok = truth["ready"] == obj["status"]["readyReplicas"] == keep and \
             truth.get("ledgerAgrees", True) and not on_released and len(left) == keep
+        self.phase = "cleanup"
         self._delete_pods([p["metadata"]["name"] for p in left])
         self.scale(name, 0)
         return {"from": n, "to": keep, "seconds": dt, "ok": ok, "evicted": n - len(left),
@@ -218,17 +245,20 @@ class BenchRun:
     # ------------------------------------------------------------ config 5
     def two_pools(self, n: int, step: int) -> dict:
         half = n // 2
+        self.phase = "create"
         a = self.make_pool(f"team-a-{step}", "amd.com/gpu-team-a", 0)
         b = self.make_pool(f"team-b-{step}", "amd.com/gpu-team-b", 0)
         t0 = time.perf_counter()
+        self.phase = "scale_up"
         self.scale(a["metadata"]["name"], half, wait=False)
         self.scale(b["metadata"]["name"], half, wait=False)
         oa = self.c.wait_for(MI355XPOOLS, a["metadata"]["name"], self.ns, ready_at(half),
-                             timeout=self.timeout)
+                             timeout=self._to())
         ob = self.c.wait_for(MI355XPOOLS, b["metadata"]["name"], self.ns, ready_at(half),
-                             timeout=self.timeout)
+                             timeout=self._to())
         dt = time.perf_counter() - t0
         ta, tb = self.wait_truth(a, half), self.wait_truth(b, half)
+        self.phase = "cleanup"
         ua = {d["uuid"] for d in oa["status"]["devices"]}
         ub = {d["uuid"] for d in ob["status"]["devices"]}
         ok = ta["ready"] == tb["ready"] == half and not (ua & ub) and \
@@ -237,6 +267,33 @@ class BenchRun:
         self.delete_pool(b["metadata"]["name"])
         return {"pools": [half, half], "seconds": dt, "ok": ok, "crossPoolDevices": len(ua & ub),
                 "truth": {"a": ta, "b": tb}}
+
+    def cleanup(self, pool: dict | None, scenario: str, step: int, timeout: float) -> bool:
+        """Best-effort undo of a failed secondary scenario (its pods, its extra pools), then the
+        main pool back to 0. False if the main pool could not be brought back."""
+        deadline = time.monotonic() + max(1.0, timeout)
+        try:
+            if scenario == "scale_down":
+                for p in self.c.list(PODS, self.ns)["items"]:
+                    if p["metadata"]["name"].startswith(f"sd{step}-"):
+                        try:
+                            self.c.delete(PODS, p["metadata"]["name"], self.ns, grace=0)
+                        except KubeError:
+                            pass
+            elif scenario == "two_pools":
+                for nm in (f"team-a-{step}", f"team-b-{step}"):
+                    try:
+                        self.c.delete(MI355XPOOLS, nm, self.ns)
+                    except KubeError:
+                        pass
+                for nm in (f"team-a-{step}", f"team-b-{step}"):
+                    self.c.wait_for(MI355XPOOLS, nm, self.ns, lambda o: o is None,
+                                    timeout=max(1.0, deadline - time.monotonic()))
+        except Exception:
+            pass
+        if pool is None:
+            return True
+        return self.recover(pool["metadata"]["name"], deadline - time.monotonic())
 
     # ------------------------------------------------------------ config 1
     def azure_pool(self, step: int, replicas: int = 0) -> dict:
@@ -273,14 +330,126 @@ class BenchRun:
                 c.get("Ready", {}).get("status") == "True"
         t0 = time.perf_counter()
         self.c.create(AZUREVMPOOLS, body, self.ns)
-        o = self.c.wait_for(AZUREVMPOOLS, name, self.ns, ready, timeout=self.timeout)
+        o = self.c.wait_for(AZUREVMPOOLS, name, self.ns, ready, timeout=self._to())
         t_ready = time.perf_counter() - t0
         fin = "compute.my.domain/device-release" in (o["metadata"].get("finalizers") or [])
         t1 = time.perf_counter()
         self.c.delete(AZUREVMPOOLS, name, self.ns)
-        self.c.wait_for(AZUREVMPOOLS, name, self.ns, lambda x: x is None, timeout=self.timeout)
+        self.c.wait_for(AZUREVMPOOLS, name, self.ns, lambda x: x is None, timeout=self._to())
         return {"seconds": t_ready, "deleteSeconds": time.perf_counter() - t1,
                 "ok": fin and o["status"]["readyReplicas"] == replicas}
+
+    # ------------------------------------------------------------ accuracy under faults
+    FAULT_KINDS = ("xgmi_down", "hotspot_critical", "hotspot_below", "vram_emergency",
+                   "ecc_uncorrectable", "ecc_correctable_at_limit", "ecc_correctable_over",
+                   "retired_at_limit", "retired_over", "pending", "missing")
+
+    def _fault(self, kind: str, dev: dict, health: dict) -> dict:
+        ecc = dev.get("ecc") or {}
+        temps = dev.get("temps") or {}
+        crit = lambda s, k="critical", d=100: (temps.get(s) or {}).get(k, d)  # noqa: E731
+        if kind == "xgmi_down":
+            links = list((dev.get("xgmi") or {}).get("links") or ["X"] + ["U"] * 7)
+            j = next((i for i, x in enumerate(links) if x != "X"), 0)
+            links[j] = "D"
+            return {"xgmi": {"links": links}}
+        if kind == "hotspot_critical":
+            return {"temps": {"hotspot": {"current": crit("hotspot")}}}
+        if kind == "hotspot_below":  # one degree under the limit: still healthy
+            return {"temps": {"hotspot": {"current": crit("hotspot") - 1}}}
+        if kind == "vram_emergency":
+            return {"temps": {"vram": {"current": crit("vram", "emergency", 125)}}}
+        if kind == "ecc_uncorrectable":
+            return {"ecc": {"uncorrectable": ecc.get("uncorrectable", 0) + 1}}
+        if kind == "ecc_correctable_at_limit":
+            return {"ecc": {"correctable": ecc.get("correctable", 0) + health["maxCorrectableECC"]}}
+        if kind == "ecc_correctable_over":
+            return {"ecc": {"correctable": ecc.get("correctable", 0) +
+                            health["maxCorrectableECC"] + 1}}
+        if kind == "retired_at_limit":
+            return {"ras": {"badPagesSupported": True, "retiredPages": health["maxRetiredPages"]}}
+        if kind == "retired_over":
+            return {"ras": {"badPagesSupported": True, "retiredPages": health["maxRetiredPages"] + 1}}
+        if kind == "pending":
+            return {"ras": {"badPagesSupported": True, "pendingPages": 1}}
+        if kind == "missing":
+            return {"present": False}
+        raise ValueError(kind)
+
+    def _state_now(self) -> dict[str, dict]:
+        """Device state from the independent source, before any fault overlay."""
+        return gt.cli_state() if self.real else gt.fixture_state(self.node.fixture, self.node.name)
+
+    def accuracy_under_faults(self, n: int, steps: int, seed: int = 0,
+                              truth_policy: dict | None = None, settle_s: float = 5.0) -> dict:
+        """readyReplicas vs ground truth after every step of a random fault / clear sequence on
+        the GPUs of a dedicated pool (replacePolicy Keep, so ownership is fixed and health is what
+        moves). The truth is ``ground_truth.device_healthy`` over the independent device state
+        (fixture or amd-smi CLI) + the injected overlay, under the pool's spec.health read back
+        from the API server (or ``truth_policy``, to prove a mismatching rule is caught). A step
+        counts as accurate when status.readyReplicas equals the truth — and the kubelet holds
+        exactly the truly healthy GPUs — within ``settle_s`` of the fault."""
+        import random
+        rng = random.Random(seed)
+        self.phase = "create"
+        pool = self.make_pool("acc-pool", "amd.com/gpu-acc", n, replacePolicy="Keep",
+                              health={"maxCorrectableECC": 10, "maxRetiredPages": 4,
+                                      "maxPendingPages": 0},
+                              probe={"enabled": True, "hbmBytes": min(self.hbm_bytes, 256 << 20),
+                                     "mfma": False, "xgmiPeerCheck": False})
+        name = pool["metadata"]["name"]
+        self.phase = "scale_up"
+        obj = self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(n), timeout=self._to())
+        policy = truth_policy if truth_policy is not None else obj["spec"]
+        health = {**gt.HEALTH_DEFAULTS, **(obj["spec"].get("health") or {})}
+        self.phase = "ground_truth"
+        base = self._state_now()                       # ECC baseline = state at claim
+        owned = gt.kubelet_allocatable(self.pr_socket).get("amd.com/gpu-acc", set())
+        ledger0 = gt.ledger_claims(self.state_dir, obj["metadata"]["uid"]) \
+            if os.path.exists(os.path.join(self.state_dir, "ledger.json")) else set()
+        samples: list[dict] = []
+        t_conv: list[float] = []
+        for i in range(steps):
+            self.phase = f"fault_step_{i}"
+            if i % 3 == 2 or not owned:
+                overlay, kinds = {}, {}
+            else:
+                victims = rng.sample(sorted(owned), k=min(len(owned), rng.choice((1, 1, 2))))
+                kinds = {u: rng.choice(self.FAULT_KINDS) for u in victims}
+                overlay = {"devices": {u: self._fault(k, base.get(u, {}), health)
+                                       for u, k in kinds.items()}}
+            t0 = time.perf_counter()
+            self.cluster.set_faults(self.node.name, overlay, sample=False, notify=True)
+            cur = gt.apply_overlay(base, overlay)
+            truth_ok = {u for u in owned if gt.device_healthy(cur.get(u, {"present": False}),
+                                                              base.get(u), policy)[0]}
+            deadline = time.monotonic() + settle_s
+            while True:
+                o = self.c.get(MI355XPOOLS, name, self.ns)
+                ready = (o.get("status") or {}).get("readyReplicas")
+                adv = gt.kubelet_allocatable(self.pr_socket).get("amd.com/gpu-acc", set())
+                agree = ready == len(truth_ok) and adv == truth_ok
+                if agree or time.monotonic() > deadline:
+                    break
+                time.sleep(0.01)
+            dt = time.perf_counter() - t0
+            if agree:
+                t_conv.append(dt)
+            samples.append({"step": i, "faults": {u[-8:]: k for u, k in kinds.items()},
+                            "truth": len(truth_ok), "readyReplicas": ready,
+                            "kubeletHealthy": len(adv), "ok": agree})
+        self.phase = "cleanup"
+        self.cluster.set_faults(self.node.name, {}, sample=True)
+        ledger1 = gt.ledger_claims(self.state_dir, obj["metadata"]["uid"]) \
+            if os.path.exists(os.path.join(self.state_dir, "ledger.json")) else set()
+        self.delete_pool(name)
+        ok = sum(x["ok"] for x in samples)
+        return {"accuracy": ok / len(samples) if samples else None, "samples": len(samples),
+                "pool_replicas": n, "ownership_stable": ledger1 == ledger0 or not ledger0,
+                "converge_p50_s": round(statistics.median(t_conv), 4) if t_conv else None,
+                "converge_max_s": round(max(t_conv), 4) if t_conv else None,
+                "fault_kinds": list(self.FAULT_KINDS),
+                "mismatches": [x for x in samples if not x["ok"]][:5]}
 
     def agent_stats(self) -> dict:
         """The agent's own counters (gpupool_agent_*): sample / health-poll cost, events."""
@@ -305,7 +474,7 @@ class BenchRun:
         GPU stays and the Conditions are what changes)."""
         name = pool["metadata"]["name"]
         self.c.patch(MI355XPOOLS, name, {"spec": {"replicas": 1, "replacePolicy": "Keep"}}, self.ns)
-        obj = self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(1), timeout=self.timeout)
+        obj = self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(1), timeout=self._to())
         victim = obj["status"]["devices"][0]["uuid"]
 
         def cond(o, t):
@@ -320,15 +489,15 @@ class BenchRun:
                 self.cluster.set_faults(self.node.name,
                                         {"devices": {victim: {"ecc": {"uncorrectable": 1 + i}}}},
                                         sample=forced, notify=notify)
-                self.c.wait_for(MI355XPOOLS, name, self.ns, faulted, timeout=self.timeout)
+                self.c.wait_for(MI355XPOOLS, name, self.ns, faulted, timeout=self._to())
                 out[key].append(time.perf_counter() - t0)
                 t0 = time.perf_counter()
                 self.cluster.set_faults(self.node.name, {}, sample=True)
-                self.c.wait_for(MI355XPOOLS, name, self.ns, cleared, timeout=self.timeout)
+                self.c.wait_for(MI355XPOOLS, name, self.ns, cleared, timeout=self._to())
                 out["recover"].append(time.perf_counter() - t0)
         self.c.patch(MI355XPOOLS, name, {"spec": {"replicas": 0, "replacePolicy": "Replace"}},
                      self.ns)
-        self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(0), timeout=self.timeout)
+        self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(0), timeout=self._to())
         return {
             # detection included, polled: the counter change is seen by the agent's health-only
             # poll (amdsmi signals no ECC event), nothing forces or announces it

@@ -16,7 +16,7 @@ namespace {
 
 thread_local Trace* tl_current = nullptr;
 
-constexpr size_t kRing = 256;
+constexpr size_t kRing = 4096;  // a bench run's timed passes + its secondary scenarios
 std::mutex g_mu;
 std::deque<Json> g_ring;  // newest at front
 std::atomic<int64_t> g_slow_ms{1000};

@@ -24,7 +24,7 @@ def run_bench(*args: str, timeout: float = 600) -> dict:
 
 def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
     out = run_bench("--gpus", "8", "--steps", "1", "--warmup", "0", "--scale-down-steps", "1",
-                    "--pool-steps", "1", "--health-steps", "1")
+                    "--pool-steps", "1", "--health-steps", "1", "--fault-steps", "20")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in out
@@ -49,6 +49,47 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
     for k in ("fault_to_condition_p50_s", "forced_sample_to_condition_p50_s",
               "fault_cleared_to_ready_p50_s"):
         assert h[k] is not None and h[k] < 30
+    # readyReplicas against the independent truth after every random fault / clear step
+    af = cfg["accuracy_under_faults"]
+    assert af["samples"] == 20 and af["accuracy"] == 1.0, af["mismatches"]
+    # per-N claim-pass breakdown, and the secondary scenarios' own pass traces
+    assert sorted(cfg["claim_pass_span_p50_ms_per_n"], key=int) == ["1", "2", "4", "8"]
+    assert cfg["claim_pass_span_p50_ms"] == cfg["claim_pass_span_p50_ms_per_n"]["8"]
+    assert "agent:POST /v1/claims" in cfg["claim_pass_span_p50_ms"]
+    assert cfg["scale_down"]["pass_span_p50_ms"]["passes"] >= 1
+    assert "agent:POST /v1/release" in cfg["scale_down"]["pass_span_p50_ms"]
+    assert out["status"] == "ok" and out["value_n"] == 8
+
+
+def test_bench_isolates_a_hung_n8_and_keeps_the_curve(native_built):
+    """A claim of 8 GPUs that hangs past the per-transition timeout costs only the N=8 point:
+    per_n 1/2/4 are measured, N=8 carries the error and its phase, ``value`` falls back to the
+    largest N that completed (and says so), the pool is recovered and the secondary scenarios
+    still run (scale-down, which needs 8 GPUs, records its own error)."""
+    out = run_bench("--gpus", "8", "--steps", "2", "--warmup", "0", "--timeout", "4",
+                    "--inject-claim-hang", "8:12", "--scale-down-steps", "1", "--pool-steps", "1",
+                    "--health-steps", "0", "--fault-steps", "0", "--azure-steps", "1",
+                    timeout=400)
+    cfg = out["config"]
+    for k in ("1", "2", "4"):
+        assert cfg["per_n"][k]["n"] == 2 and cfg["per_n"][k]["accuracy"] == 1.0, cfg["per_n"][k]
+    n8 = cfg["per_n"]["8"]
+    assert n8["n"] == 0 and n8["p50_s"] is None
+    assert "TimeoutError" in n8["error"] and n8["phase"] == "timed:scale_up", n8
+    assert out["status"] == "partial" and out["value_n"] == 4
+    assert out["value"] == cfg["per_n"]["4"]["p50_s"] and "largest N" in cfg["value_note"]
+    assert "phase" in cfg["scale_down"]["error"]
+    assert cfg["two_pools"]["accuracy"] == 1.0 and cfg["azure_config1"]["accuracy"] == 1.0
+
+
+def test_bench_wall_budget_always_prints_json(native_built):
+    out = run_bench("--gpus", "2", "--steps", "50", "--warmup", "0", "--budget-s", "1",
+                    "--scale-down-steps", "1", "--pool-steps", "1", "--health-steps", "1")
+    cfg = out["config"]
+    assert out["value"] is None and out["status"] == "failed"
+    assert "wall budget" in cfg["budget"]["skipped"]["timed_steps"]
+    assert all("skipped" in v for v in cfg["per_n"].values())
+    assert "wall budget" in cfg["scale_down"]["skipped_steps"]
 
 
 def test_bench_gpus1_contract(native_built):
