@@ -93,6 +93,7 @@ BUILTINS = [
     ResourceType("", "v1", "configmaps", "ConfigMap", True, "configmap", ["cm"]),
     ResourceType("", "v1", "resourcequotas", "ResourceQuota", True, "resourcequota", ["quota"],
                  status_sub=True),
+    ResourceType("", "v1", "limitranges", "LimitRange", True, "limitrange", ["limits"]),
     ResourceType("coordination.k8s.io", "v1", "leases", "Lease", True, "lease"),
     ResourceType("policy", "v1", "poddisruptionbudgets", "PodDisruptionBudget", True,
                  "poddisruptionbudget", ["pdb"], status_sub=True),
@@ -200,6 +201,50 @@ def parse_field_selector(sel: str | None) -> Callable[[dict], bool]:
             k, v = re.split(r"==?", p, maxsplit=1)
             reqs.append(lambda o, k=k.strip(), v=v.strip(): str(get_path(o, k) or "") == v)
     return lambda obj: all(r(obj) for r in reqs)
+
+
+# ------------------------------------------------------------------ quantities
+_QSUFFIX = {"m": 1e-3, "k": 1e3, "M": 1e6, "G": 1e9, "T": 1e12, "Ki": 1024, "Mi": 1024 ** 2,
+            "Gi": 1024 ** 3, "Ti": 1024 ** 4}
+
+
+def parse_quantity(v: Any) -> float:
+    """A Kubernetes resource.Quantity (``2``, ``"500m"``, ``"16Gi"``) as a number."""
+    if isinstance(v, (int, float)):
+        return float(v)
+    m = re.match(r"^\s*([0-9.]+)\s*([a-zA-Z]*)\s*$", str(v))
+    if not m or (m.group(2) and m.group(2) not in _QSUFFIX):
+        raise ApiError(422, "Invalid", f"quantities must match the regular expression: {v!r}")
+    return float(m.group(1)) * _QSUFFIX.get(m.group(2), 1.0)
+
+
+def _fmt_q(x: float) -> str:
+    return str(int(x)) if float(x).is_integer() else str(x)
+
+
+def _extended(name: str) -> bool:
+    """Extended resources (``amd.com/gpu``): requests must equal limits, default to them."""
+    return "/" in name and not name.startswith("kubernetes.io/")
+
+
+def pod_usage(pod: dict) -> dict[str, float]:
+    """ResourceQuota usage of one pod: ``pods`` and ``requests.<r>`` / ``limits.<r>`` per
+    resource (an extended resource's request is its limit), plus the bare ``<r>`` alias quota
+    accepts for extended resources."""
+    use: dict[str, float] = {"pods": 1.0}
+    for c in (pod.get("spec") or {}).get("containers") or []:
+        res = c.get("resources") or {}
+        lim, req = res.get("limits") or {}, dict(res.get("requests") or {})
+        for k, v in lim.items():
+            if _extended(k):
+                req.setdefault(k, v)
+        for k, v in req.items():
+            use[f"requests.{k}"] = use.get(f"requests.{k}", 0.0) + parse_quantity(v)
+            if _extended(k):
+                use[k] = use.get(k, 0.0) + parse_quantity(v)
+        for k, v in lim.items():
+            use[f"limits.{k}"] = use.get(f"limits.{k}", 0.0) + parse_quantity(v)
+    return use
 
 
 # ------------------------------------------------------------------ patches
@@ -333,6 +378,8 @@ class Store:
         self.log.append(ev)
         for fn in list(self.listeners):
             fn(ev)
+        if rt.kind == "Pod" or (rt.kind == "ResourceQuota" and etype != "DELETED"):
+            self._refresh_quota_status(obj["metadata"].get("namespace", ""))
 
     def _ensure_namespace(self, ns: str) -> None:
         nss = self.objects[("", "namespaces")]
@@ -379,6 +426,98 @@ class Store:
                            {"name": name, "kind": rt.plural,
                             "causes": [{"message": e} for e in errs]})
         return obj
+
+    # --------------------------------------------------------- pod admission
+    def _items(self, key: tuple[str, str], ns: str) -> list[dict]:
+        return [o for (ons, _), o in sorted(self.objects.get(key, {}).items()) if ons == ns]
+
+    def _admit_pod(self, ns: str, pod: dict) -> dict:
+        """The LimitRanger and ResourceQuota admission plugins for pods (reference practice
+        GPU调度平台搭建.md:802 "ResourceQuota + LimitRange"): LimitRange ``default`` /
+        ``defaultRequest`` fill containers that name no value, ``max`` / ``min`` bound each
+        container (type Container) or the pod's sum (type Pod); then every ResourceQuota of the
+        namespace must still fit with this pod's usage added (403 Forbidden otherwise)."""
+        name = pod["metadata"]["name"]
+        containers = (pod.get("spec") or {}).get("containers") or []
+
+        def forbid(msg: str) -> ApiError:
+            return ApiError(403, "Forbidden", f'pods "{name}" is forbidden: {msg}',
+                            {"name": name, "kind": "pods"})
+        for lr in self._items(("", "limitranges"), ns):
+            for lim in (lr.get("spec") or {}).get("limits") or []:
+                typ = lim.get("type", "Container")
+                if typ == "Container":
+                    for c in containers:
+                        res = c.setdefault("resources", {})
+                        limits = res.setdefault("limits", {})
+                        reqs = res.setdefault("requests", {})
+                        for k, v in (lim.get("default") or {}).items():
+                            limits.setdefault(k, v)
+                        for k, v in (lim.get("defaultRequest") or {}).items():
+                            reqs.setdefault(k, v)
+                        for k, v in limits.items():
+                            if _extended(k):
+                                reqs.setdefault(k, v)
+                        for k, v in (lim.get("max") or {}).items():
+                            got = limits.get(k, reqs.get(k))
+                            if got is not None and parse_quantity(got) > parse_quantity(v):
+                                raise forbid(f"maximum {k} usage per Container is {v}, but limit "
+                                             f"is {got}")
+                        for k, v in (lim.get("min") or {}).items():
+                            got = reqs.get(k, limits.get(k))
+                            if got is None or parse_quantity(got) < parse_quantity(v):
+                                raise forbid(f"minimum {k} usage per Container is {v}, but "
+                                             f"request is {got if got is not None else 0}")
+                elif typ == "Pod":
+                    use = pod_usage(pod)
+                    for k, v in (lim.get("max") or {}).items():
+                        got = use.get(f"limits.{k}", use.get(f"requests.{k}", 0.0))
+                        if got > parse_quantity(v):
+                            raise forbid(f"maximum {k} usage per Pod is {v}, but limit is "
+                                         f"{_fmt_q(got)}")
+                    for k, v in (lim.get("min") or {}).items():
+                        got = use.get(f"requests.{k}", 0.0)
+                        if got < parse_quantity(v):
+                            raise forbid(f"minimum {k} usage per Pod is {v}, but request is "
+                                         f"{_fmt_q(got)}")
+        new = pod_usage(pod)
+        for q in self._items(("", "resourcequotas"), ns):
+            hard = (q.get("spec") or {}).get("hard") or {}
+            used = self._quota_used(ns, hard)
+            over = [k for k in hard if new.get(k, 0.0) > 0 and
+                    used.get(k, 0.0) + new[k] > parse_quantity(hard[k])]
+            if over:
+                qn = q["metadata"]["name"]
+                raise forbid(f"exceeded quota: {qn}, requested: " +
+                             ",".join(f"{k}={_fmt_q(new[k])}" for k in over) + ", used: " +
+                             ",".join(f"{k}={_fmt_q(used.get(k, 0.0))}" for k in over) +
+                             ", limited: " + ",".join(f"{k}={hard[k]}" for k in over))
+        return pod
+
+    def _quota_used(self, ns: str, hard: dict) -> dict[str, float]:
+        used = {k: 0.0 for k in hard}
+        for p in self._items(("", "pods"), ns):
+            if (p.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+                continue  # terminal pods no longer count (quota controller semantics)
+            for k, v in pod_usage(p).items():
+                if k in used:
+                    used[k] += v
+        return used
+
+    def _refresh_quota_status(self, ns: str) -> None:
+        """ResourceQuota status.hard / status.used (the quota controller's job)."""
+        rt = self.types[("", "resourcequotas")]
+        for q in self._items(rt.key, ns):
+            hard = (q.get("spec") or {}).get("hard") or {}
+            try:
+                st = {"hard": dict(hard),
+                      "used": {k: _fmt_q(v) for k, v in self._quota_used(ns, hard).items()}}
+            except ApiError:
+                continue
+            if q.get("status") != st:
+                q["status"] = st
+                q["metadata"]["resourceVersion"] = str(self._next_rv())
+                self._emit(rt, "MODIFIED", q)
 
     def _check_ns(self, rt: ResourceType, ns: str | None) -> str:
         if rt.namespaced:
@@ -446,6 +585,7 @@ class Store:
         if rt.kind == "Pod":
             obj.setdefault("status", {}).setdefault("phase", "Pending")
             obj["spec"].setdefault("terminationGracePeriodSeconds", 30)
+            obj = self._admit_pod(ns, obj)
         if dry_run:
             return obj
         if rt.namespaced:

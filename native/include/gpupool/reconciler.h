@@ -125,7 +125,13 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
   // fewest new selector-matching nodes (most free first). Empty when it does not fit.
   std::vector<std::pair<std::string, int>> plan_span_(const Mi355xPoolSpec& spec, int need, const Observed& o);
   static bool spans_(const Mi355xPoolSpec& spec) { return spec.max_nodes > 1 && spec.node_name.empty(); }
-  bool quota_allows_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta, std::string* why);
+  // Quota admission: under quota_mu_, usage = per pool max(informer status.replicas,
+  // the replicas this manager last wrote) + reservations of claims in flight; a pass that fits
+  // reserves its delta before the claim RPC, so concurrent passes of different pools cannot both
+  // fit the same headroom. quota_settle_ (after the pass's status write) turns the reservation
+  // into the written count.
+  bool quota_reserve_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta, std::string* why);
+  void quota_settle_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int64_t replicas);
   Outcome finalize_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec);
   // Evicts pods on draining devices and releases drained ones. Returns #devices still draining.
   int drain_(const Json& obj, const std::string& node, const ObjectMeta& m, const Mi355xPoolSpec& spec,
@@ -139,6 +145,13 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
   std::map<std::string, std::set<std::string>> evicted_;  // pool uid -> pod keys already evicted
   std::map<std::string, std::set<std::string>> eviction_blocked_;  // pool uid -> pods refused by a PDB (evented)
   std::map<std::string, int64_t> policy_gen_;             // pool uid -> generation pushed to agents
+  struct QuotaHold {
+    std::string ns, resource;
+    int64_t written = 0;   // resource units (GPUs x replicasPerGPU) of our last status write
+    int64_t reserved = 0;  // units reserved by a pass whose claim is in flight
+  };
+  std::mutex quota_mu_;
+  std::map<std::string, QuotaHold> quota_holds_;  // pool uid -> hold
   // pool uid -> no spanning claim before this time: a rolled-back pass frees GPUs, whose capacity
   // event would otherwise wake the same pool into the same failing claim at once
   std::map<std::string, std::chrono::steady_clock::time_point> span_backoff_;

@@ -51,6 +51,12 @@ GaugeVec& ready_gauge() {
   static GaugeVec& g = Registry::global().gauge("gpupool_ready_replicas", "status.readyReplicas per pool.");
   return g;
 }
+GaugeVec& quota_gauge() {
+  static GaugeVec& g = Registry::global().gauge(
+      "gpupool_namespace_quota_units",
+      "Namespace ResourceQuota of a pool resource (type=hard) and the units pools use or reserve (type=used).");
+  return g;
+}
 GaugeVec& desired_gauge() {
   static GaugeVec& g = Registry::global().gauge("gpupool_desired_replicas", "spec.replicas per pool.");
   return g;
@@ -607,6 +613,10 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
     policy_gen_.erase(m.uid);
     span_backoff_.erase(m.uid);
   }
+  {
+    std::lock_guard<std::mutex> g(quota_mu_);
+    quota_holds_.erase(m.uid);
+  }
   forget_(m.uid);
   ready_gauge().erase({{"kind", kind_}, {"pool", m.key()}});
   desired_gauge().erase({{"kind", kind_}, {"pool", m.key()}});
@@ -722,7 +732,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
   }
   std::string quota_msg;
   bool over_quota = n_active < spec.replicas &&
-                    !quota_allows_(m, spec, static_cast<int>(spec.replicas - n_active), &quota_msg);
+                    !quota_reserve_(m, spec, static_cast<int>(spec.replicas - n_active), &quota_msg);
   if (over_quota) {
     blocked = "QuotaExceeded";
     progress_msg = quota_msg;
@@ -895,6 +905,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
   }
   Json status = build_status_(obj, m, spec, o, progress_reason, progress_msg, blocked, false);
   write_status_(obj, status);
+  quota_settle_(m, spec, static_cast<int64_t>(o.mine.size()));  // draining GPUs are still held
   int64_t ready = status["readyReplicas"].as_int(0);
   ready_gauge().set({{"kind", kind_}, {"pool", m.key()}}, static_cast<double>(ready));
   set_util_gauges({{"kind", kind_}, {"pool", m.key()}}, o.mine);
@@ -911,11 +922,19 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
 // GPU调度平台搭建.md:802): a ResourceQuota with spec.hard["<resourceName>"] or
 // spec.hard["requests.<resourceName>"] caps the devices of that resource all pools in the namespace
 // may offer, in the resource's own units like the pods' requests it also bounds: a GPU counts once,
-// a shared GPU (spec.sharing.replicasPerGPU = K) K times. Usage = status.replicas x K of the pools
-// (informer cache, ours included) + delta x K.
-bool Mi355xPoolReconciler::quota_allows_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta,
-                                         std::string* why) {
+// a shared GPU (spec.sharing.replicasPerGPU = K) K times.
+//
+// Admission is a reservation, not a read: the workers reconcile pools in parallel and the informer
+// copy of another pool's status lags its claim (and even our own last write lags the watch), so
+// "sum status.replicas from the cache, then claim" let three concurrent replicas=2 pools all pass a
+// quota of 3. Under quota_mu_ the usage of every pool of the namespace+resource is
+// max(informer status.replicas x K, units this manager last wrote for it) + units reserved by
+// passes whose claim is still in flight; a pass that fits reserves its delta before the claim RPC.
+// The lock is never held across an RPC (only across the quota LIST when no informer is synced).
+bool Mi355xPoolReconciler::quota_reserve_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta,
+                                          std::string* why) {
   trace::Span span("quota");
+  std::lock_guard<std::mutex> g(quota_mu_);
   std::vector<Json> items;
   if (quotas_ && quotas_->synced()) {
     for (auto& q : quotas_->list())
@@ -942,17 +961,46 @@ bool Mi355xPoolReconciler::quota_allows_(const ObjectMeta& m, const Mi355xPoolSp
     }
   }
   if (hard < 0) return true;
-  int64_t used = 0;
+  std::map<std::string, int64_t> per_pool;  // uid -> units
   for (const auto& p : pools_.list()) {
     if (p.path("metadata.namespace").as_string() != m.ns) continue;
     if (p.path("spec.resourceName").str_or(gen::kDefaultResource) != spec.resource_name) continue;
-    used += p.path("status.replicas").as_int(0) * std::max<int64_t>(1, p.path("spec.sharing.replicasPerGPU").as_int(1));
+    per_pool[p.path("metadata.uid").as_string()] =
+        p.path("status.replicas").as_int(0) * std::max<int64_t>(1, p.path("spec.sharing.replicasPerGPU").as_int(1));
   }
+  int64_t used = 0;
+  for (const auto& [uid, h] : quota_holds_) {
+    if (h.ns != m.ns || h.resource != spec.resource_name) continue;
+    int64_t& u = per_pool[uid];
+    u = std::max(u, h.written) + (uid == m.uid ? 0 : h.reserved);
+  }
+  for (const auto& kv : per_pool) used += kv.second;
   const int64_t more = static_cast<int64_t>(delta) * spec.sharing_replicas;
-  if (used + more <= hard) return true;
+  quota_gauge().set({{"namespace", m.ns}, {"resource", spec.resource_name}, {"quota", qname}, {"type", "hard"}},
+                    static_cast<double>(hard));
+  quota_gauge().set({{"namespace", m.ns}, {"resource", spec.resource_name}, {"quota", qname}, {"type", "used"}},
+                    static_cast<double>(used));
+  if (used + more <= hard) {
+    QuotaHold& h = quota_holds_[m.uid];
+    h.ns = m.ns;
+    h.resource = spec.resource_name;
+    h.reserved = more;
+    quota_gauge().set({{"namespace", m.ns}, {"resource", spec.resource_name}, {"quota", qname}, {"type", "used"}},
+                      static_cast<double>(used + more));
+    return true;
+  }
   *why = "ResourceQuota " + m.ns + "/" + qname + " allows " + std::to_string(hard) + " " + spec.resource_name +
-         "; " + std::to_string(used) + " in use, " + std::to_string(more) + " more requested";
+         "; " + std::to_string(used) + " in use or reserved, " + std::to_string(more) + " more requested";
   return false;
+}
+
+void Mi355xPoolReconciler::quota_settle_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int64_t replicas) {
+  std::lock_guard<std::mutex> g(quota_mu_);
+  QuotaHold& h = quota_holds_[m.uid];
+  h.ns = m.ns;
+  h.resource = spec.resource_name;
+  h.written = replicas * spec.sharing_replicas;
+  h.reserved = 0;
 }
 
 void Mi355xPoolReconciler::sweep_orphans() {

@@ -77,10 +77,30 @@ def test_manager_scenario_under_sanitizer(san, cluster_factory):
     k.delete(PODS, "aw", "default")
     wait_ready(k, "auto", 0, timeout=60)
     k.delete(MI355XPOOLS, "auto", "default")
+    # quota admission under concurrency: three pools created at once race for a quota of 3
+    # (reservations under the quota mutex, settled after each status write)
+    import threading
+    from gpupool.kube import Res
+    k.create(Res("", "v1", "resourcequotas"), {"metadata": {"name": "q"},
+                                               "spec": {"hard": {"amd.com/gpu-q": "3"}}}, "quota")
+    ts = [threading.Thread(target=k.create, args=(MI355XPOOLS, mi_pool(
+        n, 2, resourceName="amd.com/gpu-q"), "quota")) for n in ("qa", "qb", "qc")]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    from .helpers import cond_is, ready_at
+    objs = [k.wait_for(MI355XPOOLS, n, "quota", lambda o: ready_at(2)(o) or cond_is(
+        "Progressing", "False", "QuotaExceeded")(o), timeout=60) for n in ("qa", "qb", "qc")]
+    assert sum(1 for o in objs if ready_at(2)(o)) == 1
+    for n in ("qa", "qb", "qc"):
+        k.delete(MI355XPOOLS, n, "quota")
     for name in ("a", "b"):
         k.delete(MI355XPOOLS, name, "default")
     for name in ("a", "b"):
         k.wait_for(MI355XPOOLS, name, "default", lambda o: o is None, timeout=60)
+    for n in ("qa", "qb", "qc"):
+        k.wait_for(MI355XPOOLS, n, "quota", lambda o: o is None, timeout=60)
     c._kill("manager")
     log = c.log("manager")
     assert "WARNING: ThreadSanitizer" not in log, log[-8000:]

@@ -213,3 +213,58 @@ def test_crd_deletion_removes_instances(store):
     store.delete(crd_rt, None, "mi355xpools.compute.my.domain")
     with pytest.raises(ApiError):
         store.lookup("compute.my.domain", "mi355xpools")
+
+
+def _gpu_pod(name, n=None, phase=None):
+    c = {"name": "m", "image": "x"}
+    if n is not None:
+        c["resources"] = {"limits": {"amd.com/gpu": n}}
+    p = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name}, "spec": {"containers": [c]}}
+    if phase:
+        p["status"] = {"phase": phase}
+    return p
+
+
+def test_limitrange_defaults_and_bounds_gpu_per_container(store):
+    """LimitRange (GPU调度平台搭建.md:802): a container naming no GPU gets the default; one asking
+    above max (or a pod summing above the Pod max) is refused with 403 Forbidden."""
+    lr, pods = store.types[("", "limitranges")], store.types[("", "pods")]
+    store.create(lr, "team", {"metadata": {"name": "gpu-limits"}, "spec": {"limits": [
+        {"type": "Container", "default": {"amd.com/gpu": 1}, "max": {"amd.com/gpu": "4"}},
+        {"type": "Pod", "max": {"amd.com/gpu": 6}}]}})
+    p = store.create(pods, "team", _gpu_pod("d"))
+    res = p["spec"]["containers"][0]["resources"]
+    assert res["limits"]["amd.com/gpu"] == 1 and res["requests"]["amd.com/gpu"] == 1
+    with pytest.raises(ApiError) as e:
+        store.create(pods, "team", _gpu_pod("big", 8))
+    assert e.value.code == 403 and "maximum amd.com/gpu usage per Container is 4" in str(e.value)
+    two = _gpu_pod("two", 4)
+    two["spec"]["containers"].append({"name": "n", "image": "x",
+                                      "resources": {"limits": {"amd.com/gpu": 4}}})
+    with pytest.raises(ApiError) as e:
+        store.create(pods, "team", two)
+    assert e.value.code == 403 and "per Pod is 6" in str(e.value)
+    # other namespaces are unaffected
+    assert "resources" not in store.create(pods, "default", _gpu_pod("free"))["spec"]["containers"][0]
+
+
+def test_resourcequota_admission_and_status_used(store):
+    q, pods = store.types[("", "resourcequotas")], store.types[("", "pods")]
+    store.create(q, "team", {"metadata": {"name": "gpu-quota"},
+                             "spec": {"hard": {"requests.amd.com/gpu": "3", "pods": "5"}}})
+    store.create(pods, "team", _gpu_pod("a", 2))
+    got = store.get(q, "team", "gpu-quota")["status"]
+    assert got["used"] == {"requests.amd.com/gpu": "2", "pods": "1"}
+    with pytest.raises(ApiError) as e:
+        store.create(pods, "team", _gpu_pod("b", 2))
+    assert e.value.code == 403 and "exceeded quota: gpu-quota" in str(e.value) and \
+        "used: requests.amd.com/gpu=2" in str(e.value)
+    store.create(pods, "team", _gpu_pod("c", 1))
+    # a finished pod no longer counts; deleting one frees its share
+    done = store.get(pods, "team", "a")
+    done["status"] = {"phase": "Succeeded"}
+    store.update(pods, "team", "a", done, subresource="status")
+    assert store.get(q, "team", "gpu-quota")["status"]["used"]["requests.amd.com/gpu"] == "1"
+    store.create(pods, "team", _gpu_pod("b", 2))
+    store.delete(pods, "team", "b")
+    assert store.get(q, "team", "gpu-quota")["status"]["used"]["requests.amd.com/gpu"] == "1"
