@@ -66,6 +66,8 @@ def main() -> None:
                     default=float(os.environ.get("GPUPOOL_GIL_SWITCH_INTERVAL", "0.0005")),
                     help="sys.setswitchinterval for the agent (s): how long a thread that wants "
                          "the GIL waits for the holder to yield (CPython default 0.005)")
+    ap.add_argument("--xgmi-recheck", type=float, default=600.0,
+                    help="idle xGMI coverage ring period over pod-free GPUs, seconds (0 = off)")
     ap.add_argument("--inject-claim-delay", default="",
                     help="fault injection (tests/bench): COUNT:SECONDS — a claim of >= COUNT GPUs "
                          "stalls SECONDS before selecting devices (a hung probe / driver call)")
@@ -94,6 +96,7 @@ def main() -> None:
                       scrub_interval_s=a.scrub_interval, scrub_window_bytes=a.scrub_window,
                       scrub_windows=a.scrub_windows, scrub_reserve_bytes=a.scrub_reserve,
                       scrub_start_delay_s=a.scrub_start_delay,
+                      xgmi_recheck_s=a.xgmi_recheck,
                       inject_claim_delay=_count_seconds(a.inject_claim_delay))
     agent = Agent(cfg)
     try:

@@ -1,7 +1,7 @@
 """Claim ledger: the node agent's durable record of which GPU belongs to which pool.
 
 All claims live in one JSON document (``<state>/ledger.json``: ``{"version": 1, "claims": {uuid:
-record}, "hbmSweep": {uuid: scrubber cursor/coverage}}``) that is replaced atomically (write temp
+record}, "hbmSweep": {uuid: scrubber cursor/coverage}, "xgmiPairs": {"uA|uB": last peer check}}``) that is replaced atomically (write temp
 -> fsync -> rename -> fsync dir), so a claim of 8 GPUs costs one fsync, not eight, and a crash can
 never leave a half-written batch. Commits that must be durable before the agent acts on them
 (claim, release) are flushed synchronously — the claim's while its probe runs; transitions a crash
@@ -88,9 +88,12 @@ class Ledger:
         # agent lock), so a scrubber write never iterates a claim map another thread is editing
         self._claims_text = "{}"
         self._sweep: dict[str, dict] = {}
+        self._xgmi: dict[str, dict] = {}
         try:
             with open(self.path) as f:
-                self._sweep = dict((json.load(f) or {}).get("hbmSweep") or {})
+                doc = json.load(f) or {}
+            self._sweep = dict(doc.get("hbmSweep") or {})
+            self._xgmi = dict(doc.get("xgmiPairs") or {})
         except (OSError, ValueError):
             pass
 
@@ -138,8 +141,9 @@ class Ledger:
                 if self._written >= want:
                     return
                 seq = self._seq
-                text = '{"version": %d, "claims": %s, "hbmSweep": %s}' % (
-                    VERSION, self._claims_text, json.dumps(self._sweep, sort_keys=True))
+                text = '{"version": %d, "claims": %s, "hbmSweep": %s, "xgmiPairs": %s}' % (
+                    VERSION, self._claims_text, json.dumps(self._sweep, sort_keys=True),
+                    json.dumps(self._xgmi, sort_keys=True))
             _atomic_write_text(self.path, text, self.fsync)
             self.writes += 1
             with self._mu:
@@ -169,6 +173,22 @@ class Ledger:
             self._seq += 1
             seq = self._seq
         self.flush(seq)
+
+    def commit_xgmi(self, pairs: dict[str, dict], durable: bool = False) -> None:
+        """Persist the per-GPU-pair xGMI peer-check results (``"uuidA|uuidB"`` -> last result and
+        time), so link coverage survives agent restarts."""
+        with self._mu:
+            self._xgmi = {k: dict(r) for k, r in pairs.items()}
+            self._seq += 1
+            seq = self._seq
+        if durable:
+            self.flush(seq)
+        else:
+            self._kick_lazy()
+
+    def xgmi_state(self) -> dict[str, dict]:
+        with self._mu:
+            return {k: dict(r) for k, r in self._xgmi.items()}
 
     def sweep_state(self) -> dict[str, dict]:
         with self._mu:

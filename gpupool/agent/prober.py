@@ -183,11 +183,18 @@ class Prober:
         def one(i: int) -> tuple[str, dict]:
             src, dst = devs[i], devs[(i + 1) % n]
             faults = {**(src.get("faults") or {}), **src}
-            if self.mode == "simulated" or faults.get("xgmiPeerFail"):
-                ok = not faults.get("xgmiPeerFail")
-                r = {"passed": ok, "GBps": 64.0 * float(faults.get("probeScale") or 1.0),
-                     "badBits": 0 if ok else 1}
-                if not ok:
+            # fault overlay on the sending GPU: xgmiPeerFail (every outgoing copy corrupted),
+            # xgmiBadPeers [indices] (copies to those peers corrupted), xgmiPeerUnavailable (no
+            # peer access: an infrastructure problem, not corruption)
+            bad = bool(faults.get("xgmiPeerFail")) or \
+                dst.get("index") in (faults.get("xgmiBadPeers") or [])
+            if faults.get("xgmiPeerUnavailable"):
+                r = {"passed": False, "canAccessPeer": False, "error": "hipDeviceCanAccessPeer=0"}
+            elif self.mode == "simulated" or bad:
+                r = {"passed": not bad, "canAccessPeer": True,
+                     "GBps": 64.0 * float(faults.get("probeScale") or 1.0),
+                     "badBits": 0 if not bad else 1}
+                if bad:
                     r["error"] = "injected xGMI peer failure (fault overlay)"
             else:
                 a = self.ordinals.get(str(src.get("hipUUID", "")).lower())
@@ -216,7 +223,9 @@ class Prober:
         ords = []
         for d in devs:
             o = self.ordinals.get(str(d.get("hipUUID", "")).lower())
-            if o is None or {**(d.get("faults") or {}), **d}.get("xgmiPeerFail"):
+            f = {**(d.get("faults") or {}), **d}
+            if o is None or f.get("xgmiPeerFail") or f.get("xgmiBadPeers") or \
+                    f.get("xgmiPeerUnavailable"):
                 return None
             ords.append(o)
         r = self._hip.peer_ring(ords, nbytes)

@@ -170,6 +170,17 @@ DEVICE_STATUS = {
                 "message": _S,
             },
         },
+        "xgmi": {
+            "type": "object",
+            "description": "xGMI link coverage of this GPU: how many of its pairs with the node's "
+                           "other GPUs the agent's peer-copy rings (claim-time checks and idle "
+                           "rechecks, in an order rotating to unchecked pairs) have verified, "
+                           "which peers failed or could not be checked.",
+            "properties": {"pairsCovered": _I32, "pairsTotal": _I32,
+                           "failedPeers": {"type": "array", "items": _S},
+                           "unavailablePeers": {"type": "array", "items": _S},
+                           "lastCheckedAt": _S, "peerCheckUnavailable": _B},
+        },
         "hbmCoverage": {
             "type": "object",
             "description": "The agent's HBM scrubber on this GPU (rotating pattern-test windows "

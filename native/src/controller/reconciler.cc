@@ -471,7 +471,7 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
   Json st = Json::object();
   st["observedGeneration"] = m.generation;
   int64_t claimed = 0, ready = 0, probing = 0;
-  std::vector<std::string> xgmi_bad, ecc_bad, thermal_bad, probe_bad, unhealthy;
+  std::vector<std::string> xgmi_bad, xgmi_unknown, ecc_bad, thermal_bad, probe_bad, unhealthy;
   double min_gbps = 1e30, min_tf = 1e30, min_xgmi = 1e30;
   Json devices = Json::array();
   for (const auto& d : o.mine) {
@@ -492,6 +492,8 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
     if (!d.verdict["eccOk"].as_bool(true)) ecc_bad.push_back(reasons("HBM"));
     if (!d.verdict["thermalOk"].as_bool(true)) thermal_bad.push_back(reasons("Thermal"));
     if (d.probe.path("xgmi.GBps").is_number()) min_xgmi = std::min(min_xgmi, d.probe.path("xgmi.GBps").as_double(1e30));
+    if (d.probe.path("xgmi.unavailable").as_bool(false))
+      xgmi_unknown.push_back(short_id(d) + ": " + d.probe.path("xgmi.error").str_or("peer check could not run"));
     if (!d.probe_passed) {
       const std::string err = d.probe["error"].str_or(d.probe.is_object() ? "probe failed" : "not probed");
       probe_bad.push_back(short_id(d) + ": " + err);
@@ -528,7 +530,14 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
     std::snprintf(buf, sizeof buf, "; peer-copy ring min %.0f GB/s", min_xgmi);
     xgmi_ok_msg += buf;
   }
-  health_cond(gen::kCondXGMILinksHealthy, xgmi_bad, "XGMILinkDown", "AllLinksUp", xgmi_ok_msg.c_str());
+  if (xgmi_bad.empty() && !xgmi_unknown.empty()) {
+    // the peer-copy check could not run (no peer access / HIP error): the links are unverified,
+    // not faulty — Unknown, and no GPU is replaced for it
+    set_condition(conds, gen::kCondXGMILinksHealthy, "Unknown", "XGMIPeerCheckUnavailable", join(xgmi_unknown, " | "),
+                  gen, now);
+  } else {
+    health_cond(gen::kCondXGMILinksHealthy, xgmi_bad, "XGMILinkDown", "AllLinksUp", xgmi_ok_msg.c_str());
+  }
   health_cond(gen::kCondHBMECCHealthy, ecc_bad, "HBMECCErrors", "NoNewECCErrors", "no new HBM ECC errors since claim");
   health_cond(gen::kCondThermalHealthy, thermal_bad, "ThermalLimit", "WithinThermalLimits",
               "temperatures below device limits");

@@ -33,6 +33,7 @@ DeviceView DeviceView::from(const Json& j) {
   d.partition = j["partition"];
   d.drain_started_at = j["drainStartedAt"].as_string();
   d.hbm_sweep = j["hbmSweep"];
+  d.xgmi_pairs = j["xgmiPairs"];
   d.telemetry = j["telemetry"];
   return d;
 }
@@ -81,6 +82,15 @@ Json DeviceView::status_json() const {
     for (const char* k : {"passes", "fraction", "span", "cursor", "lastFullSweepAt", "lastBadBits"})
       if (!hbm_sweep[k].is_null()) c[k] = hbm_sweep[k];
     s["hbmCoverage"] = c;
+  }
+  if (xgmi_pairs.is_object() || probe.path("xgmi.unavailable").as_bool(false)) {
+    // xGMI link coverage of this GPU: pairs with the node's other GPUs the agent's peer-copy
+    // rings (claims + idle rechecks, rotating order) have checked, and which peers failed
+    Json x = Json::object();
+    for (const char* k : {"pairsCovered", "pairsTotal", "failedPeers", "unavailablePeers", "lastCheckedAt"})
+      if (!xgmi_pairs[k].is_null()) x[k] = xgmi_pairs[k];
+    if (probe.path("xgmi.unavailable").as_bool(false)) x["peerCheckUnavailable"] = true;
+    s["xgmi"] = x;
   }
   return s;
 }

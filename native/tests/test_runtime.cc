@@ -149,8 +149,8 @@ TEST(trace_spans_ring_and_scoping) {
   EXPECT_EQ(last["spans"].elements()[0]["name"].as_string(), std::string("observe"));
   EXPECT_EQ(last["spans"].elements()[1]["ms"].as_double(), 2.5);
   EXPECT_EQ(last.path("attrs.reason").as_string(), std::string("ScalingUp"));
-  for (int i = 0; i < 300; ++i) trace::Trace t("X/y/" + std::to_string(i));
-  EXPECT_EQ(trace::recent(1000).size(), static_cast<size_t>(256));
+  for (int i = 0; i < 4200; ++i) trace::Trace t("X/y/" + std::to_string(i));
+  EXPECT_EQ(trace::recent(5000).size(), static_cast<size_t>(4096));
   EXPECT_EQ(url_decode("Mi355xPool%2Fdefault%2Fa+b"), std::string("Mi355xPool/default/a b"));
   trace::reset();
 }
