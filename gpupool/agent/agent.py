@@ -35,6 +35,22 @@ from .prober import Prober, default_mode
 SLOT_SEP = "::"  # device-plugin ID of a time-sliced slot: "<uuid>::<slot>"
 
 
+def _ranges(bits: list[int]) -> str:
+    """[0, 1, 2, 5, 6] -> "0-2,5-6" (the CU-mask syntax libgpupool_share.so reads)."""
+    out, start, prev = [], None, None
+    for b in bits:
+        if start is None:
+            start = prev = b
+        elif b == prev + 1:
+            prev = b
+        else:
+            out.append(f"{start}-{prev}")
+            start = prev = b
+    if start is not None:
+        out.append(f"{start}-{prev}")
+    return ",".join(out)
+
+
 def gpu_of(device_id: str) -> str:
     """The GPU uuid behind a device-plugin ID (a plain uuid, or a shared GPU's slot)."""
     return device_id.split(SLOT_SEP, 1)[0]
@@ -1310,10 +1326,52 @@ class Agent:
                     "GPUPOOL_NUM_GPUS": str(len(ids)),
                     "PET_NPROC_PER_NODE": str(len(ids)),
                     "GPUPOOL_NODE": self.cfg.node}
+            mounts: list[dict] = []
             if slots != ids:  # time-sliced: the pod shares these GPUs with other pods
                 envs["GPUPOOL_GPU_SLOTS"] = ",".join(slots)
-            return {"envs": envs, "devices": ["/dev/kfd"] + render,
+                envs.update(self._isolation_env(slots, mounts))
+            return {"envs": envs, "devices": ["/dev/kfd"] + render, "mounts": mounts,
                     "annotations": {schema.ANN_POD_DEVICES: ",".join(ids)}}
+
+    SHARE_LIB_DIR = "/opt/gpupool/lib"  # where the pod sees libgpupool_share.so
+
+    def _isolation_env(self, slots: list[str], mounts: list[dict]) -> dict[str, str]:
+        """spec.sharing.hbmBytesPerSlot / cuPerSlot of the pool owning these slots: the ROCm
+        runtime loads libgpupool_share.so (HSA_TOOLS_LIB) into the pod, which caps its HBM per
+        GPU at (its slots on that GPU) x hbmBytesPerSlot and confines its queues to its slots'
+        CUs — slot i of a GPU owns CU-mask bits [i*cuPerSlot, (i+1)*cuPerSlot), disjoint from
+        the other slots (narrowed to the GPU's own CU count, e.g. a 32-CU CPX partition).
+        Called under self.lock."""
+        per_gpu: dict[str, list[int]] = {}
+        for sid in slots:
+            u, _, i = sid.partition(SLOT_SEP)
+            per_gpu.setdefault(u, []).append(int(i or 0))
+        hbm, cu_mask = 0, set()
+        for u, idx in per_gpu.items():
+            rec = self.records.get(u) or {}
+            share = (rec.get("policy") or {}).get("sharing") or {}
+            k = self._slots_of(rec)
+            per_slot_hbm = int(share.get("hbmBytesPerSlot") or 0)
+            cu = int(share.get("cuPerSlot") or 0)
+            if per_slot_hbm > 0:
+                hbm = max(hbm, per_slot_hbm * len(idx))
+            if cu > 0:
+                cus = int(((self.by_uuid.get(u) or {}).get("asic") or {}).get("computeUnits")
+                          or 256)
+                cu = max(1, min(cu, cus // k))
+                for i in idx:
+                    cu_mask.update(range(i * cu, (i + 1) * cu))
+        if not hbm and not cu_mask:
+            return {}
+        from ..ops import native_dir
+        mounts.append({"container_path": self.SHARE_LIB_DIR, "host_path": native_dir(),
+                       "read_only": True})
+        env = {"HSA_TOOLS_LIB": f"{self.SHARE_LIB_DIR}/libgpupool_share.so"}
+        if hbm:
+            env["GPUPOOL_HBM_LIMIT_BYTES"] = str(hbm)
+        if cu_mask:
+            env["GPUPOOL_CU_MASK"] = _ranges(sorted(cu_mask))
+        return env
 
     # ================================================================ node registration
     def register_node(self) -> None:

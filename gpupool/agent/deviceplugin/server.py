@@ -187,6 +187,9 @@ class DevicePluginServer:
                 c.annotations[k] = v
             for dspec in spec["devices"]:
                 c.devices.add(container_path=dspec, host_path=dspec, permissions="rw")
+            for m in spec.get("mounts") or []:  # e.g. libgpupool_share.so for isolated sharing
+                c.mounts.add(container_path=m["container_path"], host_path=m["host_path"],
+                             read_only=bool(m.get("read_only", True)))
         return out
 
     def PreStartContainer(self, request, context):

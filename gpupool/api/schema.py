@@ -227,14 +227,25 @@ MI355X_SPEC = {
         "sharing": {
             "type": "object",
             "default": {},
-            "description": "Time-sliced GPU sharing (the HAMi / NVIDIA time-slicing analogue of "
-                           "the reference platform, GPU调度平台搭建.md:289-298): every GPU of the "
-                           "pool is advertised as replicasPerGPU devices of resourceName, so that "
-                           "many pods share it. No memory or compute isolation between them (use "
-                           "CPX partitions for that); a GPU is drained and released only when "
-                           "every pod on any of its slots is gone.",
+            "description": "GPU sharing (the HAMi analogue of the reference platform, "
+                           "GPU调度平台搭建.md:289-298): every GPU of the pool is advertised as "
+                           "replicasPerGPU devices of resourceName, so that many pods share it. "
+                           "hbmBytesPerSlot / cuPerSlot isolate the sharers: the device plugin "
+                           "loads libgpupool_share.so into each pod (HSA_TOOLS_LIB), which caps "
+                           "the pod's HBM allocations per GPU at hbmBytesPerSlot (hipMalloc & co "
+                           "fail with hipErrorOutOfMemory past it, hipMemGetInfo reports the "
+                           "budget) and confines its waves to cuPerSlot CUs, disjoint from the "
+                           "other slots of the GPU. Without them the sharers are only "
+                           "time-sliced. A GPU is drained and released only when every pod on "
+                           "any of its slots is gone.",
             "properties": {
                 "replicasPerGPU": {**_I32, "minimum": 1, "maximum": 64, "default": 1},
+                "hbmBytesPerSlot": {**_I64, "minimum": 0, "default": 0,
+                                    "description": "HBM budget of one slot in bytes (0 = no "
+                                                   "budget)."},
+                "cuPerSlot": {**_I32, "minimum": 0, "maximum": 256, "default": 0,
+                              "description": "Compute units reserved for one slot (0 = all; "
+                                             "cuPerSlot x replicasPerGPU <= 256)."},
             },
         },
         "health": {

@@ -344,7 +344,15 @@ class FakeKubelet:
                     self._fail(pod, "UnexpectedAdmissionError", f"Allocate failed: {e.details()}")
                     return
                 cr = resp.container_responses[0]
-                envs.update(dict(cr.envs))
+                # the pod runs as a host process (no mount namespace): a device-plugin mount is
+                # realised by pointing its container paths at the host paths
+                rewrite = [(m.container_path, m.host_path) for m in cr.mounts
+                           if m.container_path != m.host_path]
+                for k, v in dict(cr.envs).items():
+                    for cp, hp in rewrite:
+                        if v.startswith(cp):
+                            v = hp + v[len(cp):]
+                    envs[k] = v
                 for i in ids:
                     self.assigned[i] = uid
                 devices[res] = ids

@@ -70,6 +70,8 @@ struct Mi355xPoolSpec {
   std::string replace_policy = "Replace";
   int32_t max_nodes = 1;  // nodes the pool may span
   int32_t sharing_replicas = 1;  // time-sliced slots advertised per GPU (spec.sharing.replicasPerGPU)
+  int64_t sharing_hbm_bytes = 0;  // per-slot HBM budget (spec.sharing.hbmBytesPerSlot; 0 = none)
+  int32_t sharing_cus = 0;        // per-slot CU share (spec.sharing.cuPerSlot; 0 = all CUs)
   bool autoscale = false;  // demand-driven spec.replicas (Mi355xPoolAutoscaler)
   int32_t autoscale_min = 0, autoscale_max = 8;
   int64_t scale_down_delay_seconds = 300;

@@ -87,6 +87,8 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.replace_policy = s["replacePolicy"].str_or("Replace");
   p.max_nodes = static_cast<int32_t>(s["maxNodes"].as_int(1));
   p.sharing_replicas = static_cast<int32_t>(std::max<int64_t>(1, s.path("sharing.replicasPerGPU").as_int(1)));
+  p.sharing_hbm_bytes = std::max<int64_t>(0, s.path("sharing.hbmBytesPerSlot").as_int(0));
+  p.sharing_cus = static_cast<int32_t>(std::max<int64_t>(0, s.path("sharing.cuPerSlot").as_int(0)));
   const Json& a = s["autoscale"];
   p.autoscale = a["enabled"].as_bool(false);
   p.autoscale_min = static_cast<int32_t>(a["minReplicas"].as_int(0));
@@ -115,6 +117,9 @@ Json Mi355xPoolSpec::policy_json() const {
   j["partition"]["memory"] = partition_memory;
   j["probe"] = probe_json();  // re-probe settings live with the claim (agent-side recheck)
   if (sharing_replicas > 1) j["sharing"]["replicasPerGPU"] = sharing_replicas;  // device-plugin slots
+  // isolation of the slots (the agent's Allocate loads libgpupool_share.so into the pod)
+  if (sharing_hbm_bytes > 0) j["sharing"]["hbmBytesPerSlot"] = sharing_hbm_bytes;
+  if (sharing_cus > 0) j["sharing"]["cuPerSlot"] = sharing_cus;
   return j;
 }
 
@@ -253,6 +258,15 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
     const Json& r = s.path("sharing.replicasPerGPU");
     if (!r.is_int() || r.as_int(0) < 1 || r.as_int(0) > 64)
       errs.push_back("spec.sharing.replicasPerGPU: must be within [1, 64]");
+  }
+  {
+    // disjoint CU shares: the slots of one GPU must fit its 256 CUs (MI355X, SPX)
+    const int64_t k = s.path("sharing.replicasPerGPU").as_int(1), cu = s.path("sharing.cuPerSlot").as_int(0);
+    if (cu < 0 || cu > 256) errs.push_back("spec.sharing.cuPerSlot: must be within [0, 256]");
+    else if (cu > 0 && cu * k > 256)
+      errs.push_back("spec.sharing.cuPerSlot: cuPerSlot x replicasPerGPU must not exceed the GPU's 256 CUs");
+    if (s.path("sharing.hbmBytesPerSlot").as_int(0) < 0)
+      errs.push_back("spec.sharing.hbmBytesPerSlot: should be greater than or equal to 0");
   }
   const Json& h = s["health"];
   if (h.contains("thermal") && !in(h["thermal"].as_string(), {"belowCritical", "belowEmergency", "ignore"}))

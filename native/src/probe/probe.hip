@@ -884,6 +884,8 @@ std::string run_probe(int dev, const char* opts) {
   double tflops = 0, gemm_ms = 0;
   const int reps = static_cast<int>(std::max(1LL, opt_int(opts, "gemmReps", 1)));
   const int census_fault_xcc = static_cast<int>(opt_int(opts, "injectCensusFaultXcc", -1));
+  const bool want_keys = opt_int(opts, "cuKeys", 0) != 0;
+  std::vector<int> cu_keys;
   if (do_mfma)
     launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, cnt, hres, ctx, s2);
 
@@ -926,6 +928,9 @@ std::string run_probe(int dev, const char* opts) {
     abft_bad = hres[kSlotAbft];
     census_bad = hres[kSlotCensusBad];
     census = count_cus(hres + kSlotCensusMap);
+    if (want_keys)  // the (xcc, se, sh, cu) key of every CU that proved its MFMA (isolation tests)
+      for (int k = 0; k < kCuKeys; ++k)
+        if (hres[kSlotCensusMap + k / 64] >> (k % 64) & 1ull) cu_keys.push_back(k);
     gemm_cus = count_cus(hres + kSlotGemmMap);
     // every CU the runtime reports must have proven its matrix cores (requireAllCUs, default on)
     const bool cus_ok = !require_all_cus || census.total >= cus;
@@ -975,7 +980,13 @@ std::string run_probe(int dev, const char* opts) {
     out += ",\"cus\":{\"expected\":" + std::to_string(cus) + ",\"mfmaVerified\":" + std::to_string(census.total) +
            ",\"perXcd\":" + per + "]" + ",\"gemmTiles\":" + std::to_string(gemm_cus.total) +
            ",\"badWaves\":" + std::to_string(census_bad) + ",\"ok\":" +
-           (census_bad == 0 && census.total >= cus ? "true" : "false") + "}";
+           (census_bad == 0 && census.total >= cus ? "true" : "false");
+    if (want_keys) {
+      out += ",\"cuKeys\":[";
+      for (size_t i = 0; i < cu_keys.size(); ++i) out += (i ? "," : "") + std::to_string(cu_keys[i]);
+      out += "]";
+    }
+    out += "}";
   }
   out += ",\"ms\":" + jnum(total_ms);
   out += ",\"phases\":{\"arenaReused\":" + std::string(reused ? "true" : "false") +

@@ -1,0 +1,172 @@
+// libgpupool_share.so on the CPU: OnLoad() against a fake HSA dispatch table (one GPU agent with a
+// VRAM pool, one CPU agent with a system pool), then the wrapped entry points: HBM budget per GPU,
+// frees returning budget, VMM handles counted, pool SIZE / MEMORY_AVAIL reporting the slot, CU
+// masks on new GPU queues and intersected with the application's own.
+#define AMD_INTERNAL_BUILD
+#include <dlfcn.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_api_trace.h>
+#include <hsa/hsa_ext_amd.h>
+#include <unistd.h>
+
+#include <climits>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "testing.h"
+
+namespace {
+
+constexpr uint64_t kGpu = 0x1000, kCpu = 0x2000, kGpuPool = 0x10, kCpuPool = 0x20;
+constexpr size_t kMi = 1024 * 1024;
+uint64_t g_next_ptr = 0x7000000;
+std::vector<uint32_t> g_last_mask;
+uint32_t g_last_bits = 0;
+int g_masks_set = 0;
+
+hsa_status_t f_iterate_agents(hsa_status_t (*cb)(hsa_agent_t, void*), void* data) {
+  cb(hsa_agent_t{kCpu}, data);
+  cb(hsa_agent_t{kGpu}, data);
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t f_agent_get_info(hsa_agent_t a, hsa_agent_info_t attr, void* v) {
+  if (attr == HSA_AGENT_INFO_DEVICE) {
+    *static_cast<hsa_device_type_t*>(v) = a.handle == kGpu ? HSA_DEVICE_TYPE_GPU : HSA_DEVICE_TYPE_CPU;
+    return HSA_STATUS_SUCCESS;
+  }
+  if (static_cast<int>(attr) == static_cast<int>(HSA_AMD_AGENT_INFO_MEMORY_AVAIL)) {
+    *static_cast<uint64_t*>(v) = 288ull << 30;
+    return HSA_STATUS_SUCCESS;
+  }
+  return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+}
+hsa_status_t f_iterate_pools(hsa_agent_t a, hsa_status_t (*cb)(hsa_amd_memory_pool_t, void*), void* data) {
+  cb(hsa_amd_memory_pool_t{a.handle == kGpu ? kGpuPool : kCpuPool}, data);
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t f_pool_get_info(hsa_amd_memory_pool_t p, hsa_amd_memory_pool_info_t attr, void* v) {
+  if (attr == HSA_AMD_MEMORY_POOL_INFO_LOCATION) {
+    *static_cast<hsa_amd_memory_pool_location_t*>(v) =
+        p.handle == kGpuPool ? HSA_AMD_MEMORY_POOL_LOCATION_GPU : HSA_AMD_MEMORY_POOL_LOCATION_CPU;
+    return HSA_STATUS_SUCCESS;
+  }
+  if (attr == HSA_AMD_MEMORY_POOL_INFO_SIZE) {
+    *static_cast<size_t*>(v) = 288ull << 30;
+    return HSA_STATUS_SUCCESS;
+  }
+  return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+}
+hsa_status_t f_allocate(hsa_amd_memory_pool_t, size_t, uint32_t, void** ptr) {
+  *ptr = reinterpret_cast<void*>(g_next_ptr);
+  g_next_ptr += 0x100000;
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t f_free(void*) { return HSA_STATUS_SUCCESS; }
+hsa_status_t f_vmem_create(hsa_amd_memory_pool_t, size_t, hsa_amd_memory_type_t, uint64_t,
+                           hsa_amd_vmem_alloc_handle_t* h) {
+  h->handle = g_next_ptr++;
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t f_vmem_release(hsa_amd_vmem_alloc_handle_t) { return HSA_STATUS_SUCCESS; }
+hsa_queue_t g_queue{};
+hsa_status_t f_queue_create(hsa_agent_t, uint32_t, hsa_queue_type32_t, void (*)(hsa_status_t, hsa_queue_t*, void*),
+                            void*, uint32_t, uint32_t, hsa_queue_t** q) {
+  *q = &g_queue;
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t f_cu_set_mask(const hsa_queue_t*, uint32_t bits, const uint32_t* mask) {
+  g_last_bits = bits;
+  g_last_mask.assign(mask, mask + bits / 32);
+  ++g_masks_set;
+  return HSA_STATUS_SUCCESS;
+}
+
+std::string share_lib() {
+  char buf[PATH_MAX];
+  ssize_t n = readlink("/proc/self/exe", buf, sizeof buf - 1);
+  std::string exe(buf, n > 0 ? static_cast<size_t>(n) : 0);
+  return exe.substr(0, exe.rfind('/')) + "/libgpupool_share.so";
+}
+
+}  // namespace
+
+TEST(share_lib_budget_and_cu_mask) {
+  setenv("GPUPOOL_HBM_LIMIT_BYTES", "1Gi", 1);
+  setenv("GPUPOOL_CU_MASK", "0-63,128-159", 1);
+  void* lib = dlopen(share_lib().c_str(), RTLD_NOW | RTLD_LOCAL);
+  EXPECT_TRUE(lib != nullptr);
+  auto on_load = reinterpret_cast<bool (*)(HsaApiTable*, uint64_t, uint64_t, const char* const*)>(dlsym(lib, "OnLoad"));
+  auto stats = reinterpret_cast<int (*)(char*, int)>(dlsym(lib, "gpupool_share_stats"));
+  EXPECT_TRUE(on_load && stats);
+
+  CoreApiTable core{};
+  AmdExtTable amd{};
+  core.hsa_iterate_agents_fn = f_iterate_agents;
+  core.hsa_agent_get_info_fn = f_agent_get_info;
+  core.hsa_queue_create_fn = f_queue_create;
+  amd.hsa_amd_agent_iterate_memory_pools_fn = f_iterate_pools;
+  amd.hsa_amd_memory_pool_get_info_fn = f_pool_get_info;
+  amd.hsa_amd_memory_pool_allocate_fn = f_allocate;
+  amd.hsa_amd_memory_pool_free_fn = f_free;
+  amd.hsa_amd_vmem_handle_create_fn = f_vmem_create;
+  amd.hsa_amd_vmem_handle_release_fn = f_vmem_release;
+  amd.hsa_amd_queue_cu_set_mask_fn = f_cu_set_mask;
+  HsaApiTable table{};
+  table.core_ = &core;
+  table.amd_ext_ = &amd;
+  EXPECT_TRUE(on_load(&table, 0, 0, nullptr));
+
+  const hsa_amd_memory_pool_t gpu{kGpuPool}, cpu{kCpuPool};
+  void *a = nullptr, *b = nullptr, *c = nullptr;
+  EXPECT_EQ(amd.hsa_amd_memory_pool_allocate_fn(gpu, 512 * kMi, 0, &a), HSA_STATUS_SUCCESS);
+  EXPECT_EQ(amd.hsa_amd_memory_pool_allocate_fn(gpu, 384 * kMi, 0, &b), HSA_STATUS_SUCCESS);
+  // 896 MiB live: 256 MiB more would pass 1 GiB
+  EXPECT_EQ(amd.hsa_amd_memory_pool_allocate_fn(gpu, 256 * kMi, 0, &c), HSA_STATUS_ERROR_OUT_OF_RESOURCES);
+  // system memory is not the slot's HBM
+  EXPECT_EQ(amd.hsa_amd_memory_pool_allocate_fn(cpu, 4096 * kMi, 0, &c), HSA_STATUS_SUCCESS);
+  uint64_t avail = 0;
+  EXPECT_EQ(core.hsa_agent_get_info_fn(hsa_agent_t{kGpu}, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_MEMORY_AVAIL),
+                                       &avail),
+            HSA_STATUS_SUCCESS);
+  EXPECT_EQ(avail, static_cast<uint64_t>(128 * kMi));
+  size_t size = 0;
+  EXPECT_EQ(amd.hsa_amd_memory_pool_get_info_fn(gpu, HSA_AMD_MEMORY_POOL_INFO_SIZE, &size), HSA_STATUS_SUCCESS);
+  EXPECT_EQ(size, static_cast<size_t>(1024 * kMi));
+  EXPECT_EQ(amd.hsa_amd_memory_pool_get_info_fn(cpu, HSA_AMD_MEMORY_POOL_INFO_SIZE, &size), HSA_STATUS_SUCCESS);
+  EXPECT_EQ(size, static_cast<size_t>(288ull << 30));
+  // a free returns its bytes; VMM physical handles count against the same budget
+  EXPECT_EQ(amd.hsa_amd_memory_pool_free_fn(a), HSA_STATUS_SUCCESS);
+  hsa_amd_vmem_alloc_handle_t h{};
+  EXPECT_EQ(amd.hsa_amd_vmem_handle_create_fn(gpu, 512 * kMi, MEMORY_TYPE_NONE, 0, &h), HSA_STATUS_SUCCESS);
+  hsa_amd_vmem_alloc_handle_t h2{};
+  EXPECT_EQ(amd.hsa_amd_vmem_handle_create_fn(gpu, 256 * kMi, MEMORY_TYPE_NONE, 0, &h2),
+            HSA_STATUS_ERROR_OUT_OF_RESOURCES);
+  EXPECT_EQ(amd.hsa_amd_vmem_handle_release_fn(h), HSA_STATUS_SUCCESS);
+  EXPECT_EQ(amd.hsa_amd_memory_pool_allocate_fn(gpu, 640 * kMi, 0, &c), HSA_STATUS_SUCCESS);
+
+  // every GPU queue gets the slot's CU mask (bits 0-63 and 128-159: 5 words)
+  hsa_queue_t* q = nullptr;
+  EXPECT_EQ(core.hsa_queue_create_fn(hsa_agent_t{kGpu}, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &q),
+            HSA_STATUS_SUCCESS);
+  EXPECT_EQ(g_masks_set, 1);
+  EXPECT_EQ(g_last_bits, 160u);
+  EXPECT_TRUE(g_last_mask == (std::vector<uint32_t>{~0u, ~0u, 0u, 0u, ~0u}));
+  core.hsa_queue_create_fn(hsa_agent_t{kCpu}, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &q);
+  EXPECT_EQ(g_masks_set, 1);  // not on CPU agents
+  // an application mask (hipExtStreamCreateWithCUMask) only narrows the slot's
+  const uint32_t app[2] = {0x0000FFFFu, 0xFFFFFFFFu};
+  amd.hsa_amd_queue_cu_set_mask_fn(&g_queue, 64, app);
+  EXPECT_TRUE(g_last_mask == (std::vector<uint32_t>{0x0000FFFFu, ~0u, 0u, 0u, 0u}));
+  const uint32_t outside[1] = {0};
+  amd.hsa_amd_queue_cu_set_mask_fn(&g_queue, 32, outside);  // nothing left: the slot's mask
+  EXPECT_TRUE(g_last_mask == (std::vector<uint32_t>{~0u, ~0u, 0u, 0u, ~0u}));
+
+  char buf[256];
+  stats(buf, sizeof buf);
+  std::string js(buf);
+  EXPECT_TRUE(js.find("\"denied\":2") != std::string::npos);
+  EXPECT_TRUE(js.find("\"maskBits\":160") != std::string::npos);
+  unsetenv("GPUPOOL_HBM_LIMIT_BYTES");
+  unsetenv("GPUPOOL_CU_MASK");
+}

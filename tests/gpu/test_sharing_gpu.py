@@ -1,0 +1,122 @@
+"""Isolated GPU sharing on a real MI355X (spec.sharing.hbmBytesPerSlot / cuPerSlot; the HAMi layer
+of the reference platform, GPU调度平台搭建.md:289-298): libgpupool_share.so, loaded by the ROCm
+runtime through HSA_TOOLS_LIB exactly as the device plugin's Allocate sets it up, caps a slot's HBM
+and confines its waves to the slot's CUs. Each case runs in child processes (the library is loaded
+at HSA init), with a time limit."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB = os.path.join(ROOT, "build", "native", "libgpupool_share.so")
+pytestmark = pytest.mark.gpu
+GiB = 1 << 30
+
+ALLOC = r"""
+import json, sys, time, torch
+hold = int(sys.argv[1]); extra = int(sys.argv[2]); wait = float(sys.argv[3])
+free, total = torch.cuda.mem_get_info(0)
+out = {"total": total, "free": free}
+a = torch.empty(hold, dtype=torch.uint8, device="cuda")
+a.fill_(1); torch.cuda.synchronize()
+out["held"] = hold
+try:
+    b = torch.empty(extra, dtype=torch.uint8, device="cuda"); b.fill_(2); torch.cuda.synchronize()
+    out["extra"] = "ok"
+except torch.OutOfMemoryError as e:
+    out["extra"] = "oom"
+print(json.dumps(out), flush=True)
+time.sleep(wait)
+"""
+
+CENSUS = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+from gpupool.ops import probe
+probe.init()
+r = probe.run(0, hbm_bytes=64 << 20, mfma=True, gemm_n=1024, cuKeys=1)
+print(json.dumps({"keys": r["cus"]["cuKeys"], "verified": r["cus"]["mfmaVerified"],
+                  "perXcd": r["cus"]["perXcd"], "mfmaOk": r["mfma"]["elementMismatches"] == 0}))
+"""
+
+
+def _env(**kw) -> dict:
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("HSA_TOOLS_LIB", "GPUPOOL_HBM_LIMIT_BYTES", "GPUPOOL_CU_MASK"):
+        env.pop(k, None)
+    env.update({k: str(v) for k, v in kw.items()})
+    return env
+
+
+def _json(p: subprocess.Popen, timeout: float = 90) -> dict:
+    deadline = time.monotonic() + timeout
+    line = ""
+    while time.monotonic() < deadline:
+        line = p.stdout.readline()
+        if line.startswith("{"):
+            return json.loads(line)
+        if not line and p.poll() is not None:
+            break
+    p.kill()
+    raise AssertionError(f"no result (rc={p.poll()}): {line} {p.stderr.read()[-2000:]}")
+
+
+def test_hbm_budget_per_slot_and_sibling_unaffected():
+    """Slot A (8 GiB budget) holds 6 GiB, then asks for 10 GiB more -> hipErrorOutOfMemory
+    (torch.OutOfMemoryError); torch.cuda.mem_get_info reports the 8 GiB budget. Its sibling slot,
+    running at the same time with its own 8 GiB, allocates its 6 GiB fine; an unshared process
+    allocates 16 GiB."""
+    assert os.path.exists(LIB), "build the native targets first"
+    slot = _env(HSA_TOOLS_LIB=LIB, GPUPOOL_HBM_LIMIT_BYTES=8 * GiB)
+    a = subprocess.Popen([sys.executable, "-c", ALLOC, str(6 * GiB), str(10 * GiB), "20"], env=slot,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        ra = _json(a)
+        b = subprocess.Popen([sys.executable, "-c", ALLOC, str(6 * GiB), str(1 * GiB), "0"],
+                             env=slot, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        rb = _json(b)
+        b.wait(timeout=60)
+    finally:
+        a.kill()
+        a.wait(timeout=30)
+    assert ra["total"] == 8 * GiB, ra
+    assert ra["held"] == 6 * GiB and ra["extra"] == "oom", ra
+    assert rb["held"] == 6 * GiB and rb["extra"] == "ok", rb
+    free = subprocess.run([sys.executable, "-c", ALLOC, str(16 * GiB), str(1 * GiB), "0"],
+                          env=_env(), capture_output=True, text=True, timeout=120)
+    rf = json.loads([x for x in free.stdout.splitlines() if x.startswith("{")][-1])
+    assert rf["total"] > 200 * GiB and rf["extra"] == "ok", rf
+
+
+def test_cu_share_confines_waves_to_the_slot():
+    """Four slots of 64 CUs: each slot's census (every CU that runs an MFMA wave marks its
+    XCC/SE/SH/CU hardware id) sees at most its own 64 CUs, the four slots' CU sets are disjoint,
+    and together they cover the GPU's 256; an unmasked process reaches all 256."""
+    assert os.path.exists(LIB), "build the native targets first"
+    full = subprocess.run([sys.executable, "-c", CENSUS, ROOT], env=_env(), capture_output=True,
+                          text=True, timeout=120)
+    assert full.returncode == 0, full.stderr[-2000:]
+    all_keys = set(json.loads(full.stdout.splitlines()[-1])["keys"])
+    assert len(all_keys) == 256, len(all_keys)
+    seen = []
+    for i in range(4):
+        r = subprocess.run([sys.executable, "-c", CENSUS, ROOT],
+                           env=_env(HSA_TOOLS_LIB=LIB, GPUPOOL_CU_MASK=f"{64 * i}-{64 * i + 63}"),
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = json.loads(r.stdout.splitlines()[-1])
+        assert out["mfmaOk"], out
+        keys = set(out["keys"])
+        print(f"slot {i}: {len(keys)} CUs, per XCD {out['perXcd']}")
+        assert 0 < len(keys) <= 64, (i, len(keys), out["perXcd"])
+        seen.append(keys)
+    for i in range(4):
+        for j in range(i + 1, 4):
+            assert not (seen[i] & seen[j]), (i, j, sorted(seen[i] & seen[j])[:8])
+    assert set().union(*seen) <= all_keys

@@ -118,3 +118,43 @@ def test_sharing_cpx_partitions(cluster_factory):
     assert o["status"]["allocatable"] == 16
     k.wait_for(NODES, "cpx-node", None, lambda n: (n["status"].get("allocatable") or {})
                .get("amd.com/gpu") == "16", timeout=20)
+
+
+def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_factory):
+    """spec.sharing.hbmBytesPerSlot / cuPerSlot (the HAMi layer): Allocate hands each pod the
+    ROCm tools library (HSA_TOOLS_LIB, mounted from the agent's build dir), its slot's HBM budget
+    and a CU range disjoint from the other slots of the same GPU."""
+    import os
+    import time
+    c = cluster_factory()
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("iso", 1, sharing={"replicasPerGPU": 4, "hbmBytesPerSlot": 8 << 30,
+                                                     "cuPerSlot": 64}), "default")
+    wait_ready(k, "iso", 1)
+    cmd = ["bash", "-c", "env | grep -E '^(HSA_TOOLS_LIB|GPUPOOL_CU_MASK|GPUPOOL_HBM_LIMIT_BYTES)=' "
+                         "| sort; sleep 600"]
+    for i in range(4):
+        pod = pause_pod(f"iso{i}")
+        pod["spec"]["containers"][0]["command"] = cmd
+        k.create(PODS, pod, "default")
+    envs = []
+    for i in range(4):
+        p = k.wait_for(PODS, f"iso{i}", "default", running, timeout=30)
+        path = p["metadata"]["annotations"]["gpupool.amd.com/log-path"]
+        deadline = time.monotonic() + 10
+        while time.monotonic() < deadline and open(path).read().count("\n") < 3:
+            time.sleep(0.05)
+        envs.append(dict(line.split("=", 1) for line in open(path).read().split()))
+    masks = sorted(e["GPUPOOL_CU_MASK"] for e in envs)
+    assert masks == ["0-63", "128-191", "192-255", "64-127"], masks
+    assert all(e["GPUPOOL_HBM_LIMIT_BYTES"] == str(8 << 30) for e in envs)
+    lib = envs[0]["HSA_TOOLS_LIB"]  # the container path, rewritten to the host path
+    assert lib.endswith("/libgpupool_share.so") and os.path.exists(lib)
+    # a pool whose slots overrun the GPU's CUs is rejected at admission of the manager
+    k.create(MI355XPOOLS, mi_pool("over", 1, sharing={"replicasPerGPU": 4, "cuPerSlot": 128}),
+             "default")
+    o = k.wait_for(MI355XPOOLS, "over", "default", lambda o: any(
+        x["reason"] == "InvalidSpec" for x in (o.get("status") or {}).get("conditions", [])),
+        timeout=20)
+    assert "256 CUs" in next(x["message"] for x in o["status"]["conditions"]
+                             if x["type"] == "Ready")
