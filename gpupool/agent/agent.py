@@ -156,6 +156,10 @@ class Agent:
             if q.get("maintenance")}
         self._rechecking: set[str] = set()
         self.xgmi_pairs: dict[str, dict] = self.ledger.xgmi_state()
+        self.pod_usage: dict[str, list[dict]] = {}        # uuid -> per-pod VRAM / gfx time
+        self._proc_prev: dict[tuple[str, int], list] = {}  # (uuid, pid) -> [(t, gfxNs)]
+        self._pid_pods: dict[int, dict] = {}
+        self._pods_by_uid: tuple[float, dict[str, dict]] = (0.0, {})
         self._xgmi_last = time.monotonic()
         self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0, "rechecks": 0,
                       "probe_ms_sum": 0.0, "samples": 0, "sample_ms_sum": 0.0,
@@ -325,6 +329,10 @@ class Agent:
         t0 = time.perf_counter()
         snap = self.dev.snapshot()
         dt = (time.perf_counter() - t0) * 1e3
+        try:
+            self._account(snap)
+        except Exception:  # accounting is telemetry: never fail a health sample for it
+            log.exception("per-pod GPU accounting failed")
         with self.lock:
             self.snap = snap
             self.by_uuid = {d["uuid"]: d for d in snap["devices"]}
@@ -585,6 +593,101 @@ class Agent:
             # waiting for devices; "*": resync everything
             return self.gen, sorted(pools)
 
+    # ================================================================ per-pod accounting
+    _POD_UID_RE = None
+
+    def _pod_of_pid(self, pid: int) -> dict:
+        """The pod a GPU process belongs to: from its cgroup (a kubelet's container cgroups carry
+        the pod UID: ``kubepods-…-pod<uid>.slice`` / ``kubepods/…/pod<uid>/``), resolved to
+        namespace/name through the API server; else from the pod identity in its environment
+        (POD_NAME / POD_NAMESPACE: the downward API on a real node, set by the fake kubelet). The
+        agent's own probe / scrubber buffers are reported as ``gpupool-agent``. {} if unknown."""
+        if pid == os.getpid():
+            return {"namespace": "", "pod": "gpupool-agent"}
+        hit = self._pid_pods.get(pid)
+        if hit is not None:
+            return hit
+        import re
+        pod: dict = {}
+        try:
+            with open(f"/proc/{pid}/cgroup") as f:
+                m = re.search(r"pod([0-9a-f]{8}[-_][0-9a-f]{4}[-_][0-9a-f]{4}[-_][0-9a-f]{4}"
+                              r"[-_][0-9a-f]{12})", f.read())
+            if m:
+                pod = self._pod_by_uid(m.group(1).replace("_", "-")) or {}
+        except OSError:
+            pass
+        if not pod:
+            try:
+                with open(f"/proc/{pid}/environ", "rb") as f:
+                    env = dict(x.split(b"=", 1) for x in f.read().split(b"\0") if b"=" in x)
+                if b"POD_NAME" in env:
+                    pod = {"namespace": env.get(b"POD_NAMESPACE", b"").decode(),
+                           "pod": env[b"POD_NAME"].decode()}
+            except OSError:
+                pass
+        if len(self._pid_pods) > 4096:
+            self._pid_pods.clear()
+        self._pid_pods[pid] = pod
+        return pod
+
+    def _pod_by_uid(self, uid: str) -> dict | None:
+        ts, by_uid = self._pods_by_uid
+        if uid not in by_uid and time.monotonic() - ts > 5.0 and self.cfg.apiserver:
+            from ..kube import PODS, Client
+            try:
+                c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
+                items = c.list(PODS, None, field_selector=f"spec.nodeName={self.cfg.node}")["items"]
+                by_uid = {p["metadata"]["uid"]: {"namespace": p["metadata"]["namespace"],
+                                                 "pod": p["metadata"]["name"]} for p in items}
+            except Exception as e:
+                log.debug("pod lookup for accounting failed: %s", e)
+            self._pods_by_uid = (time.monotonic(), by_uid)
+        return by_uid.get(uid)
+
+    def _account(self, snap: dict) -> None:
+        """Per-pod GPU accounting (reference ops practice "monitor GPU utilisation" and per-team
+        usage, GPU调度平台搭建.md:800-802): each GPU's processes (amdsmi_get_gpu_process_list) are
+        attributed to pods; per (GPU, pod) the VRAM they hold and their share of the GPU's time
+        (gfx-engine ns consumed between two samples / wall ns). On a time-shared GPU this is what
+        tells the sharers apart, and an idle pod on a claimed GPU shows up as a 0 share."""
+        now = time.monotonic()
+        window = max(0.2, 0.5 * self.cfg.sample_interval)
+        prev, new_prev = self._proc_prev, {}
+        usage: dict[str, list[dict]] = {}
+        for d in snap.get("devices") or []:
+            u = d.get("uuid")
+            per: dict[tuple[str, str], dict] = {}
+            for p in d.get("processes") or []:
+                pid = int(p.get("pid") or 0)
+                if pid <= 0:
+                    continue
+                who = self._pod_of_pid(pid)
+                gfx = int(p.get("gfxNs") or 0)
+                busy = None
+                # ratio over the newest earlier sample at least ``window`` old (event-triggered
+                # samples come ms apart: a ratio over a few ms is noise), else the oldest kept
+                hist = [h for h in prev.get((u, pid), []) if now - h[0] <= 20 * window and
+                        h[1] <= gfx]
+                ref = next((h for h in reversed(hist) if now - h[0] >= window),
+                           hist[0] if hist else None)
+                if ref and now > ref[0]:
+                    busy = (gfx - ref[1]) / ((now - ref[0]) * 1e9)
+                new_prev[(u, pid)] = (hist + [(now, gfx)])[-16:]
+                e = per.setdefault((who.get("namespace", ""), who.get("pod", "")), {
+                    "namespace": who.get("namespace", ""), "pod": who.get("pod", ""),
+                    "pids": [], "vramBytes": 0, "gfxBusy": None, "cuOccupancy": 0})
+                e["pids"].append(pid)
+                e["vramBytes"] += int(p.get("vramBytes") or p.get("memBytes") or 0)
+                e["cuOccupancy"] += int(p.get("cuOccupancy") or 0)
+                if busy is not None:
+                    e["gfxBusy"] = round((e["gfxBusy"] or 0.0) + busy, 4)
+            if per:
+                usage[u] = sorted(per.values(), key=lambda x: (x["namespace"], x["pod"]))
+        with self.lock:
+            self._proc_prev = new_prev
+            self.pod_usage = usage
+
     # ================================================================ views
     def _pods_by_device(self, fresh: bool = False) -> dict[str, list[dict]]:
         """device ID -> pods holding it, from the kubelet's PodResources API.
@@ -705,6 +808,8 @@ class Agent:
         xs = self._xgmi_summary(uuid)
         if xs:
             out["xgmiPairs"] = xs
+        if self.pod_usage.get(uuid):
+            out["usage"] = self.pod_usage[uuid]
         out["telemetry"] = self._telemetry(d)
         if not rec:
             q = self.ledger.quarantined().get(uuid) if self.ledger else None
@@ -1498,6 +1603,16 @@ class Agent:
                                  f"{float((pr.get('hbm') or {}).get('GBps') or 0):.1f}")
                     lines.append(f"gpupool_device_probe_mfma_tflops{{{lab}}} "
                                  f"{float((pr.get('mfma') or {}).get('tflops') or 0):.1f}")
+            lines.append("# TYPE gpupool_pod_vram_bytes gauge")
+            for u, pods in self.pod_usage.items():
+                d = self.by_uuid.get(u) or {}
+                pool = (self.records.get(u) or {}).get("pool", "")
+                for e in pods:
+                    lab = f'uuid="{u}",index="{d.get("index")}",node="{self.cfg.node}",' \
+                          f'pool="{pool}",namespace="{e["namespace"]}",pod="{e["pod"]}"'
+                    lines.append(f"gpupool_pod_vram_bytes{{{lab}}} {e['vramBytes']}")
+                    if e.get("gfxBusy") is not None:
+                        lines.append(f"gpupool_pod_gfx_busy_ratio{{{lab}}} {e['gfxBusy']}")
             for k, v in self.stats.items():
                 lines.append(f"gpupool_agent_{k} {v}")
             for src, ok in self.events_supported.items():

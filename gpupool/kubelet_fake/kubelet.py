@@ -389,6 +389,7 @@ class FakeKubelet:
         try:  # `gpuctl logs` finds the container log through this annotation
             self.client.patch(PODS, rp.name, {"metadata": {"annotations": {
                 "gpupool.amd.com/log-path": rp.log_path,
+                "gpupool.amd.com/pid": str(rp.proc.pid),
                 schema.ANN_POD_DEVICES: ",".join(i for ids in rp.devices.values() for i in ids)}}},
                 ns=rp.ns)
         except KubeError:

@@ -144,7 +144,9 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
   Informer* quotas_ = nullptr;
   std::map<std::string, std::set<std::string>> evicted_;  // pool uid -> pod keys already evicted
   std::map<std::string, std::set<std::string>> eviction_blocked_;  // pool uid -> pods refused by a PDB (evented)
-  std::map<std::string, int64_t> policy_gen_;             // pool uid -> generation pushed to agents
+  // pool uid -> the policy (+ resource name) the agents hold: pushed again only when it changes, so
+  // a replicas-only edit (new generation, same policy) costs no /v1/policy RPC
+  std::map<std::string, std::string> policy_sent_;
   struct QuotaHold {
     std::string ns, resource;
     int64_t written = 0;   // resource units (GPUs x replicasPerGPU) of our last status write

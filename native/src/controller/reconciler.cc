@@ -619,7 +619,7 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
     std::lock_guard<std::mutex> g(mu_);
     evicted_.erase(m.uid);
     eviction_blocked_.erase(m.uid);
-    policy_gen_.erase(m.uid);
+    policy_sent_.erase(m.uid);
     span_backoff_.erase(m.uid);
   }
   {
@@ -695,17 +695,19 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     ready_gauge().set({{"kind", kind_}, {"pool", m.key()}}, 0);
     return Outcome::transient("agent on " + o.node + " unreachable: " + o.error);
   }
-  // Push the (possibly edited) health policy to the agent owning our GPUs.
+  // Push the (possibly edited) health policy to the agent owning our GPUs — only when the policy
+  // itself changed (a replicas-only edit bumps the generation but not the policy).
+  const std::string policy_key = spec.policy_json().dump() + "|" + spec.resource_name;
   if (!o.mine.empty()) {
     bool push;
     {
       std::lock_guard<std::mutex> g(mu_);
-      push = policy_gen_[m.uid] != m.generation;
+      push = policy_sent_[m.uid] != policy_key;
     }
     if (push) {
       for (const auto& n : o.nodes) provider_.update_policy(n, m.uid, spec.policy_json(), spec.resource_name);
       std::lock_guard<std::mutex> g(mu_);
-      policy_gen_[m.uid] = m.generation;
+      policy_sent_[m.uid] = policy_key;
     }
   }
 
@@ -808,7 +810,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
         event_(obj, "Normal", "GPUClaimed", progress_msg);
         {
           std::lock_guard<std::mutex> g(mu_);
-          policy_gen_[m.uid] = m.generation;
+          policy_sent_[m.uid] = policy_key;
         }
         log.info("claimed", Json::object().set("nodes", static_cast<long long>(made.size())).set("count", need));
         {
@@ -862,7 +864,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
         event_(obj, "Normal", "GPUClaimed", progress_msg + ": " + join(ids, ", "));
         {
           std::lock_guard<std::mutex> g(mu_);
-          policy_gen_[m.uid] = m.generation;
+          policy_sent_[m.uid] = policy_key;
         }
         log.info("claimed", Json::object().set("node", node).set("count", need).set("claimMs", claim_ms));
         claimed_only = !acted;

@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 
 #include <cstdio>
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -47,6 +48,7 @@ struct Api {
   AMDSMI_FN(amdsmi_get_gpu_bad_page_info);
   AMDSMI_FN(amdsmi_get_gpu_ecc_count);
   AMDSMI_FN(amdsmi_get_gpu_memory_usage);
+  AMDSMI_FN(amdsmi_get_gpu_process_list);
   AMDSMI_FN(amdsmi_init_gpu_event_notification);
   AMDSMI_FN(amdsmi_set_gpu_event_notification_mask);
   AMDSMI_FN(amdsmi_get_gpu_event_notification);
@@ -118,6 +120,7 @@ class AmdSmiBackend : public Backend {
     bind_optional(api_.lib, api_.amdsmi_get_gpu_bad_page_info, "amdsmi_get_gpu_bad_page_info");
     bind_optional(api_.lib, api_.amdsmi_get_gpu_ecc_count, "amdsmi_get_gpu_ecc_count");
     bind_optional(api_.lib, api_.amdsmi_get_gpu_memory_usage, "amdsmi_get_gpu_memory_usage");
+    bind_optional(api_.lib, api_.amdsmi_get_gpu_process_list, "amdsmi_get_gpu_process_list");
     bind_optional(api_.lib, api_.amdsmi_init_gpu_event_notification, "amdsmi_init_gpu_event_notification");
     bind_optional(api_.lib, api_.amdsmi_set_gpu_event_notification_mask, "amdsmi_set_gpu_event_notification_mask");
     bind_optional(api_.lib, api_.amdsmi_get_gpu_event_notification, "amdsmi_get_gpu_event_notification");
@@ -199,6 +202,7 @@ class AmdSmiBackend : public Backend {
           api_.amdsmi_get_gpu_memory_usage(h, AMDSMI_MEM_TYPE_VRAM, &used) == AMDSMI_STATUS_SUCCESS)
         d["memUsedBytes"] = static_cast<long long>(used);
       d["ras"] = bad_pages_(h);
+      d["processes"] = processes_(h);
       char buf[64] = {0};
       if (api_.amdsmi_get_gpu_compute_partition(h, buf, sizeof buf) == AMDSMI_STATUS_SUCCESS) d["partition"]["compute"] = std::string(buf);
       char mbuf[64] = {0};
@@ -212,6 +216,29 @@ class AmdSmiBackend : public Backend {
   }
 
  private:
+  // Processes holding this GPU (amdsmi_get_gpu_process_list, KFD's per-process accounting):
+  // pid, VRAM, cumulative gfx-engine time, CUs occupied — what the agent attributes to pods.
+  Json processes_(amdsmi_processor_handle h) {
+    Json out = Json::array();
+    if (!api_.amdsmi_get_gpu_process_list) return out;
+    uint32_t n = 64;
+    std::vector<amdsmi_proc_info_t> list(n);
+    amdsmi_status_t st = api_.amdsmi_get_gpu_process_list(h, &n, list.data());
+    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return out;
+    for (uint32_t i = 0; i < std::min<uint32_t>(n, 64); ++i) {
+      const amdsmi_proc_info_t& p = list[i];
+      Json j = Json::object();
+      j["pid"] = static_cast<long long>(p.pid);
+      j["name"] = std::string(p.name, strnlen(p.name, sizeof p.name));
+      j["vramBytes"] = static_cast<long long>(p.memory_usage.vram_mem);
+      j["memBytes"] = static_cast<long long>(p.mem);
+      j["gfxNs"] = static_cast<long long>(p.engine_usage.gfx);
+      j["cuOccupancy"] = static_cast<long long>(p.cu_occupancy);
+      out.push_back(j);
+    }
+    return out;
+  }
+
   void read_static_() {
     size_t n = handles_.size();
     Json weights = Json::array(), types = Json::array();

@@ -341,3 +341,59 @@ def test_time_sliced_pods_share_the_real_gpu(cluster_factory):
     assert all(o["rocr"] == hip_uuid and o["arch"].startswith("gfx950") and o["iters"] > 0
                for o in outs), outs
     assert len({o["slots"] for o in outs}) == 3  # three different slots of the one GPU
+
+
+def test_isolated_slots_and_per_pod_accounting_on_the_real_gpu(cluster_factory):
+    """The HAMi layer end to end on hardware: a pool sharing the MI355X as 2 isolated slots
+    (8 GiB HBM and 128 CUs each). Pod "small" holds 2 GiB, pod "big" 6 GiB and is refused 4 GiB
+    more (its slot's budget), both see an 8 GiB GPU; meanwhile the agent's per-pod accounting
+    (amdsmi process list -> pod) shows both pods on the same uuid with their distinct VRAM."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    k = c.client
+    k.create(MI355XPOOLS, pool("iso", 1, sharing={"replicasPerGPU": 2, "hbmBytesPerSlot": 8 << 30,
+                                                  "cuPerSlot": 128}), "default")
+    obj = k.wait_for(MI355XPOOLS, "iso", "default", ready_at(1), timeout=60)
+    uuid = obj["status"]["devices"][0]["uuid"]
+    code = ("import json, os, sys, time, torch\n"
+            "hold, more = int(sys.argv[1]), int(sys.argv[2])\n"
+            "a = torch.ones(hold, dtype=torch.uint8, device='cuda'); torch.cuda.synchronize()\n"
+            "try:\n"
+            "    b = torch.ones(more, dtype=torch.uint8, device='cuda'); torch.cuda.synchronize(); r = 'ok'\n"
+            "except torch.OutOfMemoryError:\n"
+            "    r = 'oom'\n"
+            "print(json.dumps({'more': r, 'total': torch.cuda.mem_get_info(0)[1],"
+            " 'mask': os.environ.get('GPUPOOL_CU_MASK')}), flush=True)\n"
+            "time.sleep(20)\n")
+    for name, hold, more in (("small", 2 << 30, 1 << 30), ("big", 6 << 30, 4 << 30)):
+        k.create(PODS, {"metadata": {"name": name}, "spec": {"restartPolicy": "Never", "containers": [
+            {"name": "c", "command": ["python", "-c", code, str(hold), str(more)],
+             "resources": {"limits": {"amd.com/gpu": 1}}}]}}, "default")
+    outs = {}
+    for name in ("small", "big"):
+        p = k.wait_for(PODS, name, "default", lambda o: o and o["status"].get("phase") == "Running"
+                       and "gpupool.amd.com/log-path" in o["metadata"].get("annotations", {}),
+                       timeout=60)
+        path = p["metadata"]["annotations"]["gpupool.amd.com/log-path"]
+        deadline = time.monotonic() + 60
+        while time.monotonic() < deadline and "{" not in open(path).read():
+            time.sleep(0.2)
+        log = open(path).read()
+        outs[name] = json.loads([x for x in log.splitlines() if x.startswith("{")][-1])
+    assert outs["small"]["more"] == "ok" and outs["big"]["more"] == "oom", outs
+    assert outs["small"]["total"] == outs["big"]["total"] == 8 << 30, outs
+    assert {outs["small"]["mask"], outs["big"]["mask"]} == {"0-127", "128-255"}, outs
+    # per-pod accounting from the amdsmi process list, attributed through the pods' environment
+    deadline = time.monotonic() + 15
+    use = {}
+    while time.monotonic() < deadline:
+        c.agent_request("gpu-node", "POST", "/v1/sample", {})
+        view = c.agent_request("gpu-node", "GET", "/v1/node")
+        use = {e["pod"]: e for e in next(d for d in view["devices"] if d["uuid"] == uuid).get("usage", [])}
+        if {"small", "big"} <= set(use) and use["big"]["vramBytes"] >= 6 << 30:
+            break
+        time.sleep(0.5)
+    print({k2: (v["vramBytes"], v.get("gfxBusy")) for k2, v in use.items()})
+    assert 2 << 30 <= use["small"]["vramBytes"] < 6 << 30, use
+    assert 6 << 30 <= use["big"]["vramBytes"] <= 8 << 30, use
+    for name in ("small", "big"):
+        k.delete(PODS, name, "default", grace=0)

@@ -123,17 +123,6 @@ def test_probe_gemm_matches_torch_fp64_cpu(hip, mnk):
         hip.gemm_bf16(0, a.data_ptr(), bt.data_ptr(), c.data_ptr(), m + 1, n, k)
 
 
-def test_concurrent_probes_of_one_device_serialise(hip):
-    """Two probes of the same GPU from different threads (e.g. a claim racing a recheck) are
-    serialised by the per-device lock: both complete, both pass, neither corrupts the other."""
-    import concurrent.futures as cf
-    with cf.ThreadPoolExecutor(2) as ex:
-        futs = [ex.submit(hip.run, 0, 512 << 20) for _ in range(2)]
-        res = [f.result(timeout=60) for f in futs]
-    assert all(r["passed"] for r in res), res
-    assert all(r["hbm"]["badBits"] == 0 and r["mfma"]["abftMismatches"] == 0 for r in res)
-
-
 def test_hbm_sweep_windows_cover_free_hbm(hip):
     """The rotating sweep: windows of a buffer spanning (nearly) all free HBM are pattern-tested,
     an injected flip inside a window is found at the right offset, and the buffer is released."""

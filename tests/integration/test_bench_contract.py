@@ -58,6 +58,8 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
     assert "agent:POST /v1/claims" in cfg["claim_pass_span_p50_ms"]
     assert cfg["scale_down"]["pass_span_p50_ms"]["passes"] >= 1
     assert "agent:POST /v1/release" in cfg["scale_down"]["pass_span_p50_ms"]
+    # a replicas-only edit pushes no policy to the agent (only a changed policy is re-sent)
+    assert "agent:POST /v1/policy" not in cfg["scale_down"]["pass_span_p50_ms"]
     assert out["status"] == "ok" and out["value_n"] == 8
 
 

@@ -158,3 +158,43 @@ def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_
         timeout=20)
     assert "256 CUs" in next(x["message"] for x in o["status"]["conditions"]
                              if x["type"] == "Ready")
+
+
+def test_per_pod_accounting_on_a_time_shared_gpu(cluster_factory):
+    """Per-pod GPU accounting (GPU调度平台搭建.md:800-802): the GPU's process list (amdsmi; here
+    injected through the fault overlay for the fake backend) is attributed to the pods of a
+    time-shared GPU — distinct VRAM per pod on the same uuid, and each pod's share of the GPU's
+    time from the gfx-engine counter between two samples."""
+    import re
+    import time
+    c = cluster_factory()
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("acct", 1, sharing={"replicasPerGPU": 2}), "default")
+    o = wait_ready(k, "acct", 1)
+    gpu = o["status"]["devices"][0]
+    pids = {}
+    for name in ("small", "big"):
+        k.create(PODS, pause_pod(name), "default")
+        p = k.wait_for(PODS, name, "default", lambda p: running(p) and "gpupool.amd.com/pid" in
+                       p["metadata"].get("annotations", {}), timeout=30)
+        pids[name] = int(p["metadata"]["annotations"]["gpupool.amd.com/pid"])
+
+    def procs(gfx_small):
+        return {"devices": {str(gpu["index"]): {"processes": [
+            {"pid": pids["small"], "vramBytes": 2 << 30, "gfxNs": gfx_small},
+            {"pid": pids["big"], "vramBytes": 6 << 30, "gfxNs": 0}]}}}
+    c.set_faults("mi355x-node-0", procs(0), sample=True)
+    t0 = time.monotonic()
+    time.sleep(0.5)
+    c.set_faults("mi355x-node-0", procs(250_000_000), sample=True)  # 0.25 s of gfx time
+    dt = time.monotonic() - t0
+    view = c.agent_request("mi355x-node-0", "GET", "/v1/node")
+    use = {e["pod"]: e for e in next(d for d in view["devices"] if d["uuid"] == gpu["uuid"])["usage"]}
+    assert use["small"]["vramBytes"] == 2 << 30 and use["big"]["vramBytes"] == 6 << 30
+    assert use["small"]["namespace"] == "default" and use["small"]["pids"] == [pids["small"]]
+    assert 0.25 / (dt + 0.3) < use["small"]["gfxBusy"] < 0.25 / max(dt - 0.3, 0.05)
+    assert use["big"]["gfxBusy"] == 0
+    metrics = c.agent_request("mi355x-node-0", "GET", "/metrics")
+    got = dict(re.findall(r'gpupool_pod_vram_bytes\{[^}]*pod="(\w+)"\} (\d+)', str(metrics)))
+    assert got == {"small": str(2 << 30), "big": str(6 << 30)}
+    assert 'gpupool_pod_gfx_busy_ratio{' in str(metrics)
