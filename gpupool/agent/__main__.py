@@ -3,7 +3,6 @@
 from __future__ import annotations
 
 import argparse
-import asyncio
 import logging
 import os
 import socket
@@ -100,7 +99,7 @@ def main() -> None:
                       inject_claim_delay=_count_seconds(a.inject_claim_delay))
     agent = Agent(cfg)
     try:
-        asyncio.run(serve(agent, a.ready_file or None))
+        serve(agent, a.ready_file or None)
     except KeyboardInterrupt:
         pass
     finally:

@@ -14,7 +14,6 @@ node-local owner of physical devices.
 """
 from __future__ import annotations
 
-import asyncio
 import datetime as _dt
 import json
 import logging
@@ -24,8 +23,6 @@ import threading
 import time
 from dataclasses import dataclass, field
 from typing import Any
-
-from aiohttp import web
 
 from ..api import schema
 from ..ops import devlib
@@ -140,7 +137,7 @@ class Agent:
         # only competed with the reply on the event loop
         self._claiming: dict[str, int] = {}
         self._deferred: set[str] = set()
-        self.waiters: list[tuple[asyncio.AbstractEventLoop, asyncio.Future]] = []
+        self.gen_cv = threading.Condition()  # /v1/events long-polls wait here for a new gen
         self.advertised: dict[str, set[str]] = {}
         self._adv_event = threading.Event()
         self.plugins: dict = {}
@@ -287,18 +284,45 @@ class Agent:
                 bad.setdefault(self._asic_key(d), set()).add(u)
         return bad
 
+    def _evaluate_some(self, uuids: list[str]) -> set[str]:
+        """Re-evaluate only ``uuids`` (their record — baseline, policy — just changed: a claim or
+        a release), unless a package-level fault needs the ASIC fan-out: then everything.
+        Called under self.lock."""
+        uuids = [u for u in uuids if u in self.by_uuid]
+        if not uuids or self._asic_faulted():
+            return self._evaluate_all()
+        verdicts = devlib.evaluate_batch([
+            (self.by_uuid[u], (self.records.get(u) or {}).get("baseline") or self.by_uuid[u],
+             self._policy_for(u)) for u in uuids])
+        if any(v.get(f) is False for v in verdicts for f in self.ASIC_SCOPED):
+            return self._evaluate_all()
+        return self._apply_verdicts(dict(zip(uuids, verdicts)))
+
     def _evaluate_all(self) -> set[str]:
         """Re-evaluate every device; returns pool UIDs whose devices changed verdict."""
-        changed: set[str] = set()
         uuids = list(self.by_uuid)
         verdicts = devlib.evaluate_batch([
             (self.by_uuid[u], (self.records.get(u) or {}).get("baseline") or self.by_uuid[u],
              self._policy_for(u)) for u in uuids])
         raw: dict[str, dict] = dict(zip(uuids, verdicts))
-        raw = self._fan_out_asic(raw)
-        for uuid, d in self.by_uuid.items():
+        changed = self._apply_verdicts(self._fan_out_asic(raw))
+        # claimed devices that vanished from enumeration
+        for uuid, rec in self.records.items():
+            if uuid not in self.by_uuid:
+                v = {"healthy": False, "present": False, "xgmiOk": True, "eccOk": True,
+                     "thermalOk": True, "partitionOk": True,
+                     "reasons": ["DeviceMissing: device no longer enumerated"]}
+                if self.verdicts.get(uuid, {}).get("present", True):
+                    changed.add(rec["poolUID"])
+                self.verdicts[uuid] = v
+        return changed
+
+    def _apply_verdicts(self, raw: dict[str, dict]) -> set[str]:
+        """Store raw verdicts (reset / maintenance overrides applied); returns the pools (or
+        "*free*") whose devices changed verdict."""
+        changed: set[str] = set()
+        for uuid, v in raw.items():
             rec = self.records.get(uuid)
-            v = raw[uuid]
             if uuid in self.resetting:  # between amdsmi pre- and post-reset events
                 v = {**v, "healthy": False,
                      "reasons": list(v.get("reasons") or []) + ["GPUReset: the GPU is being reset"]}
@@ -314,15 +338,6 @@ class Agent:
                 else:
                     changed.add("*free*")
             self.verdicts[uuid] = v
-        # claimed devices that vanished from enumeration
-        for uuid, rec in self.records.items():
-            if uuid not in self.by_uuid:
-                v = {"healthy": False, "present": False, "xgmiOk": True, "eccOk": True,
-                     "thermalOk": True, "partitionOk": True,
-                     "reasons": ["DeviceMissing: device no longer enumerated"]}
-                if self.verdicts.get(uuid, {}).get("present", True):
-                    changed.add(rec["poolUID"])
-                self.verdicts[uuid] = v
         return changed
 
     def sample(self) -> set[str]:
@@ -575,9 +590,8 @@ class Agent:
             self.gen += 1
             self.changes.append((self.gen, set(pools)))
             self.changes = self.changes[-256:]
-            waiters, self.waiters = self.waiters, []
-        for loop, fut in waiters:
-            loop.call_soon_threadsafe(lambda f=fut: f.done() or f.set_result(None))
+        with self.gen_cv:
+            self.gen_cv.notify_all()
 
     def changed_since(self, since: int) -> tuple[int, list[str]]:
         with self.lock:
@@ -712,7 +726,8 @@ class Agent:
         return cache
 
     def _draining(self) -> bool:
-        return any(r.get("state") == "Draining" for r in self.records.values())
+        with self.lock:  # claims and releases edit the record map on other threads
+            return any(r.get("state") == "Draining" for r in self.records.values())
 
     def _watch_pods(self, seconds: float = 2.0) -> None:
         """Pod placement is about to change (a device-plugin Allocate): views refresh the pod map
@@ -920,8 +935,13 @@ class Agent:
             weights = topo.get("weights") or [[0 if i == j else 15 for j in range(n)]
                                               for i in range(n)]
             numa = [d.get("numa", 0) for d in sorted(self.snap["devices"], key=lambda x: x["index"])]
-            sel = devlib.select(count, free, owned, req.get("topologyPolicy", "xgmi-packed"),
-                                weights, numa)
+            if count == 1 and not owned:
+                # one GPU for an empty pool: every candidate scores the same on links and NUMA,
+                # so the selector's tie-break (lowest index) decides — no native call needed
+                sel = [min(free)] if free else []
+            else:
+                sel = devlib.select(count, free, owned, req.get("topologyPolicy", "xgmi-packed"),
+                                    weights, numa)
             if len(sel) < count:
                 return {"ok": False, "reason": "InsufficientDevices",
                         "message": f"need {count} free healthy GPU(s) on {self.cfg.node}, "
@@ -970,7 +990,7 @@ class Agent:
                     self.stats["probe_failures"] += 1
             # Probing -> Claimed may be lost by a crash (restart -> ProbeInterrupted -> replace)
             self.ledger.commit(self.records, durable=False)
-            self._evaluate_all()
+            self._evaluate_some([d["uuid"] for d in chosen])
         self.ledger.flush(claim_seq)
         lap("commit2")
         self._ensure_plugin(resource)
@@ -1227,6 +1247,7 @@ class Agent:
         return {"ok": True, "uuid": uuid, "maintenance": on, "claimedBy": pool}
 
     def cordon(self, pool_uid: str, uuids: list[str]) -> dict:
+        seq = 0
         with self.lock:
             n = 0
             for u in uuids:
@@ -1235,8 +1256,10 @@ class Agent:
                     rec["state"] = "Draining"
                     rec["drainStartedAt"] = now_rfc3339()
                     n += 1
-            if n:
-                self.ledger.commit(self.records)
+            if n:  # serialised under the lock, made durable (fsync) outside it
+                seq = self.ledger.commit(self.records, durable=False)
+        if seq:
+            self.ledger.flush(seq)
         if n:
             self._pods_kick.set()  # watch the evicted pods go
         self._notify_plugins()
@@ -1248,7 +1271,8 @@ class Agent:
         except Exception as e:
             return {"ok": False, "reason": "PodResourcesUnavailable", "released": [],
                     "message": f"cannot confirm the GPUs are pod-free: {e}"}
-        released, refused = [], []
+        released, refused, quarantined = [], [], []
+        seq = 0
         with self.lock:
             for u in uuids:
                 rec = self.records.get(u)
@@ -1264,13 +1288,19 @@ class Agent:
                 elif not probe_ok or not healthy:
                     why = "probe failed" if not probe_ok else "; ".join(
                         self.verdicts.get(u, {}).get("reasons", []))
-                    self.ledger.quarantine(u, self.cfg.quarantine_s, why)
+                    quarantined.append(self.ledger.quarantine(u, self.cfg.quarantine_s, why,
+                                                              write=False))
                 del self.records[u]
                 released.append(u)
             if released:
-                self.ledger.commit(self.records)
+                seq = self.ledger.commit(self.records, durable=False)
             self.stats["releases"] += len(released)
-            self._evaluate_all()
+            self._evaluate_some(released)
+        # durable before the reply, but no fsync under the lock (node views and claims wait on it)
+        for q in quarantined:
+            self.ledger.persist_quarantine(q)
+        if seq:
+            self.ledger.flush(seq)
         if released:
             self._bump({pool_uid, "*free*"})  # capacity freed: wake pools waiting for GPUs
         self._notify_plugins()
@@ -1281,6 +1311,7 @@ class Agent:
 
     def update_policy(self, pool_uid: str, policy: dict, resource: str | None) -> dict:
         changed = set()
+        seq = 0
         with self.lock:
             for u, rec in self.records.items():
                 if rec["poolUID"] != pool_uid:
@@ -1290,8 +1321,10 @@ class Agent:
                     rec["resourceName"] = resource
                 changed.add(u)
             if changed:
-                self.ledger.commit(self.records)
+                seq = self.ledger.commit(self.records, durable=False)
             self._evaluate_all()
+        if seq:
+            self.ledger.flush(seq)
         if resource:
             self._ensure_plugin(resource)
         self._notify_plugins()
@@ -1661,155 +1694,106 @@ class Agent:
 
 
 # ==================================================================== RPC server
-OPEN_PATHS = {"/healthz", "/metrics"}
+def build_routes(agent: Agent) -> dict:
+    """The manager-facing RPC surface (served by ``rpc.RpcServer``, one thread per connection;
+    every route but /healthz and /metrics requires the shared bearer token)."""
+    from .rpc import json_reply, text_reply
 
+    def body_json(body: bytes) -> dict:
+        return json.loads(body or b"{}")
 
-def auth_middleware(token: str):
-    """Every RPC except /healthz and /metrics needs ``Authorization: Bearer <token>`` (the shared
-    secret mounted into the agent and the manager): without it any pod could claim, cordon or
-    release GPUs or rewrite a pool's health policy. Constant-time comparison."""
-    import hmac
-    want = ("Bearer " + token).encode()
+    def node(q, body):
+        return json_reply(agent.node_view(q.get("pool", "")))
 
-    @web.middleware
-    async def mw(request, handler):
-        if request.path not in OPEN_PATHS:
-            got = request.headers.get("Authorization", "").encode()
-            if not hmac.compare_digest(got, want):
-                return web.json_response({"reason": "Unauthorized",
-                                          "message": "agent RPC requires the manager's token"},
-                                         status=401)
-        return await handler(request)
-    return mw
-
-
-def build_app(agent: Agent) -> web.Application:
-    app = web.Application(middlewares=[auth_middleware(agent.cfg.auth_token)]
-                          if agent.cfg.auth_token else [])
-    loop_holder: dict[str, Any] = {}
-
-    async def run_blocking(fn, *a):
-        return await asyncio.get_running_loop().run_in_executor(None, fn, *a)
-
-    async def node(request):
-        # served on the event loop: node_view never blocks on I/O (cached pod map), and skipping
-        # the executor hop saves a thread wake-up on every reconcile's observe
-        return web.json_response(agent.node_view(request.query.get("pool", "")))
-
-    async def claims(request):
-        body = await request.json()
-        if not body.get("poolUID") or int(body.get("count", 0)) <= 0:
-            return web.json_response({"reason": "BadRequest", "message": "poolUID and count>0 "
-                                      "required"}, status=400)
-        t_in = time.perf_counter()
-        body["_t_in"] = t_in
+    def claims(q, body):
+        req = body_json(body)
+        if not req.get("poolUID") or int(req.get("count", 0)) <= 0:
+            return json_reply({"reason": "BadRequest", "message": "poolUID and count>0 required"},
+                              400)
+        req["_t_in"] = time.perf_counter()
+        pool = req["poolUID"]
         try:
-            out = await run_blocking(agent.claim, body, True)
-            t_back = time.perf_counter()
-            tm = out.get("timingsMs")
-            if tm is not None:  # the executor hop back to the event loop (GIL + loop wake-up)
-                tm["executorOut"] = round((t_back - out.pop("_t_done")) * 1e3, 3)
-            resp = web.Response(text=json.dumps(out), content_type="application/json")
-            await resp.prepare(request)
-            await resp.write_eof()  # the reply is out: now the held change events may go
-            return resp
-        finally:
-            agent.release_events(body["poolUID"])
+            out = agent.claim(req, hold_events=True)
+        except BaseException:
+            agent.release_events(pool)
+            raise
+        tm = out.get("timingsMs")
+        if tm is not None:  # reply serialisation (the claim ran on this connection's thread)
+            tm["executorOut"] = round((time.perf_counter() - out.pop("_t_done")) * 1e3, 3)
+        # the reply goes out first; then the pool's held change events may go
+        return json_reply(out, after=lambda: agent.release_events(pool))
 
-    async def cordon(request):
-        b = await request.json()
-        return web.json_response(await run_blocking(agent.cordon, b["poolUID"], b.get("uuids", [])))
+    def cordon(q, body):
+        b = body_json(body)
+        return json_reply(agent.cordon(b["poolUID"], b.get("uuids", [])))
 
-    async def release(request):
-        b = await request.json()
-        out = await run_blocking(agent.release, b["poolUID"], b.get("uuids", []))
-        return web.json_response(out, status=200 if out.get("ok") else 409)
+    def release(q, body):
+        b = body_json(body)
+        out = agent.release(b["poolUID"], b.get("uuids", []))
+        return json_reply(out, 200 if out.get("ok") else 409)
 
-    async def maintenance(request):
-        b = await request.json()
-        out = await run_blocking(agent.set_maintenance, str(b.get("gpu", "")), bool(b.get("on", True)),
-                                 str(b.get("reason", "")))
-        return web.json_response(out, status=200 if out.get("ok") else 404)
+    def maintenance(q, body):
+        b = body_json(body)
+        out = agent.set_maintenance(str(b.get("gpu", "")), bool(b.get("on", True)),
+                                    str(b.get("reason", "")))
+        return json_reply(out, 200 if out.get("ok") else 404)
 
-    async def policy(request):
-        b = await request.json()
-        return web.json_response(await run_blocking(agent.update_policy, b["poolUID"],
-                                                    b.get("policy") or {}, b.get("resourceName")))
+    def policy(q, body):
+        b = body_json(body)
+        return json_reply(agent.update_policy(b["poolUID"], b.get("policy") or {},
+                                              b.get("resourceName")))
 
-    async def events(request):
-        since = int(request.query.get("since", "-1"))
-        timeout = float(request.query.get("timeoutSeconds", "30"))
+    def events(q, body):
+        since = int(q.get("since", "-1"))
+        timeout = min(float(q.get("timeoutSeconds", "30")), 300.0)
         gen, pools = agent.changed_since(since)
         if gen == since:
-            loop = asyncio.get_running_loop()
-            fut = loop.create_future()
-            with agent.lock:
-                if agent.gen == since:
-                    agent.waiters.append((loop, fut))
-                else:
-                    fut.set_result(None)
-            try:
-                await asyncio.wait_for(fut, timeout)
-            except asyncio.TimeoutError:
-                pass
+            with agent.gen_cv:
+                agent.gen_cv.wait_for(lambda: agent.gen != since, timeout)
             gen, pools = agent.changed_since(since)
-        return web.Response(text=json.dumps({"gen": gen, "pools": pools}) + "\n",
-                            content_type="application/json")
+        return 200, "application/json", (json.dumps({"gen": gen, "pools": pools}) + "\n").encode(), None
 
-    async def sample(request):
-        changed = await run_blocking(agent.sample)
-        return web.json_response({"changed": sorted(changed), "gen": agent.gen})
+    def sample(q, body):
+        changed = agent.sample()
+        return json_reply({"changed": sorted(changed), "gen": agent.gen})
 
-    async def scrub(request):
+    def scrub(q, body):
         """Synchronous HBM scrub of one free GPU (admin / tests): {"gpu": uuid|hipUUID|index,
         "windows": n}."""
-        b = await request.json()
+        b = body_json(body)
         ref = str(b.get("gpu", ""))
-        uuid = next((u for u, d in agent.by_uuid.items()
+        uuid = next((u for u, d in list(agent.by_uuid.items())
                      if ref in (u, d.get("hipUUID"), str(d.get("index")))), None)
         if uuid is None:
-            return web.json_response({"ok": False, "reason": "NotFound"}, status=404)
-        rec = await run_blocking(agent.scrubber.scrub_device, uuid, int(b.get("windows") or 1))
-        return web.json_response({"ok": True, "uuid": uuid, "coverage": agent.scrubber.coverage(uuid),
-                                  "record": rec})
+            return json_reply({"ok": False, "reason": "NotFound"}, 404)
+        rec = agent.scrubber.scrub_device(uuid, int(b.get("windows") or 1))
+        return json_reply({"ok": True, "uuid": uuid, "coverage": agent.scrubber.coverage(uuid),
+                           "record": rec})
 
-    async def xgmi_check(request):
+    def xgmi_check(q, body):
         """Run the idle xGMI coverage ring now (admin / tests)."""
-        return web.json_response(await run_blocking(agent.xgmi_recheck, True))
+        return json_reply(agent.xgmi_recheck(True))
 
-    async def healthz(request):
-        return web.Response(text="ok\n")
+    def healthz(q, body):
+        return text_reply("ok\n")
 
-    async def metrics(request):
-        return web.Response(text=await run_blocking(agent.metrics_text), content_type="text/plain")
+    def metrics(q, body):
+        return text_reply(agent.metrics_text())
 
-    app.router.add_get("/v1/node", node)
-    app.router.add_post("/v1/claims", claims)
-    app.router.add_post("/v1/cordon", cordon)
-    app.router.add_post("/v1/release", release)
-    app.router.add_post("/v1/policy", policy)
-    app.router.add_post("/v1/maintenance", maintenance)
-    app.router.add_get("/v1/events", events)
-    app.router.add_post("/v1/sample", sample)
-    app.router.add_post("/v1/scrub", scrub)
-    app.router.add_post("/v1/xgmi-check", xgmi_check)
-    app.router.add_get("/healthz", healthz)
-    app.router.add_get("/metrics", metrics)
-    app["loop_holder"] = loop_holder
-    return app
+    return {("GET", "/v1/node"): node, ("POST", "/v1/claims"): claims,
+            ("POST", "/v1/cordon"): cordon, ("POST", "/v1/release"): release,
+            ("POST", "/v1/policy"): policy, ("POST", "/v1/maintenance"): maintenance,
+            ("GET", "/v1/events"): events, ("POST", "/v1/sample"): sample,
+            ("POST", "/v1/scrub"): scrub, ("POST", "/v1/xgmi-check"): xgmi_check,
+            ("GET", "/healthz"): healthz, ("GET", "/metrics"): metrics}
 
 
-async def serve(agent: Agent, ready_file: str | None = None) -> None:
-    app = build_app(agent)
-    runner = web.AppRunner(app, access_log=None)
-    await runner.setup()
+def serve(agent: Agent, ready_file: str | None = None) -> None:
+    """Start the RPC listeners and the agent's background loops; block until interrupted."""
+    from .rpc import RpcServer
+    srv = RpcServer(build_routes(agent), agent.cfg.auth_token)
     if agent.cfg.socket:
-        try:
-            os.unlink(agent.cfg.socket)
-        except FileNotFoundError:
-            pass
-        os.makedirs(os.path.dirname(os.path.abspath(agent.cfg.socket)), exist_ok=True)
-        await web.UnixSite(runner, agent.cfg.socket).start()
+        srv.listen_unix(agent.cfg.socket)
     if agent.cfg.listen:
         host, port = agent.cfg.listen.rsplit(":", 1)
         ctx = None
@@ -1818,7 +1802,7 @@ async def serve(agent: Agent, ready_file: str | None = None) -> None:
             ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
             ctx.minimum_version = ssl.TLSVersion.TLSv1_2
             ctx.load_cert_chain(agent.cfg.tls_cert, agent.cfg.tls_key or None)
-        await web.TCPSite(runner, host or "0.0.0.0", int(port), ssl_context=ctx).start()
+        srv.listen_tcp(host, int(port), ctx)
     agent.start_background()
     if ready_file:
         with open(ready_file + ".tmp", "w") as f:
@@ -1826,5 +1810,8 @@ async def serve(agent: Agent, ready_file: str | None = None) -> None:
                        "devices": len(agent.by_uuid), "probe": agent.probe_mode}, f)
         os.replace(ready_file + ".tmp", ready_file)
     print(f"gpupool-agent {agent.cfg.node} serving on {agent.endpoint()}", flush=True)
-    while True:
-        await asyncio.sleep(3600)
+    try:
+        while True:
+            time.sleep(3600)
+    finally:
+        srv.close()

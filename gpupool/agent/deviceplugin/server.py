@@ -50,6 +50,9 @@ class DevicePluginServer:
         self.registered = False
         self._kubelet_ino = None
         self._mon: threading.Thread | None = None
+        self._pending: tuple | None = None  # (version, ListAndWatchResponse, healthy uuids)
+        self._mark_mu = threading.Lock()
+        self._marked = -1
 
     # ------------------------------------------------------------ lifecycle
     def start(self) -> None:
@@ -123,9 +126,22 @@ class DevicePluginServer:
         return (st.st_ino, st.st_ctime_ns)
 
     def notify(self) -> None:
+        """Publish the current device list: built on the caller's thread (a claim, a health
+        change) and queued for every ListAndWatch stream, whose generator then only sends it.
+        A device counts as advertised once its stream has sent the message — not before: a pod
+        placed on a GPU the kubelet has not heard of yet would fail admission."""
+        resp, healthy = self._devices_msg()
         with self.cv:
             self.version += 1
+            self._pending = (self.version, resp, healthy)
             self.cv.notify_all()
+
+    def _mark(self, version: int, healthy: set[str] | None) -> None:
+        with self._mark_mu:  # versions only move forward: a late stream send never undoes a newer one
+            if healthy is not None and version <= self._marked:
+                return
+            self._marked = max(self._marked, version)
+            self.agent.mark_advertised(self.resource, healthy)
 
     # ------------------------------------------------------------ API
     def GetDevicePluginOptions(self, request, context):
@@ -157,13 +173,19 @@ class DevicePluginServer:
                     if seen == self.version:
                         continue
                     seen = self.version
-                resp, healthy = self._devices_msg()
+                    pend = self._pending if self._pending and self._pending[0] == seen else None
+                if pend is None:  # first message of a new stream
+                    resp, healthy = self._devices_msg()
+                else:
+                    resp, healthy = pend[1], pend[2]
                 yield resp
-                self.agent.mark_advertised(self.resource, healthy)
+                # gRPC asks for the next message once this one is written: it is sent
+                # (a broken stream resets the bit in ``finally``)
+                self._mark(seen, healthy)
         finally:
             with self.cv:
                 self.streams -= 1
-            self.agent.mark_advertised(self.resource, None)
+            self._mark(self.version, None)
 
     def GetPreferredAllocation(self, request, context):
         out = DP.PreferredAllocationResponse()

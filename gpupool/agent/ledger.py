@@ -195,13 +195,21 @@ class Ledger:
             return {u: dict(r) for u, r in self._sweep.items()}
 
     # ---------------------------------------------------------------- quarantine
-    def quarantine(self, uuid: str, seconds: float, reason: str, maintenance: bool = False) -> None:
+    def quarantine(self, uuid: str, seconds: float, reason: str, maintenance: bool = False,
+                   write: bool = True) -> dict:
+        """Quarantine ``uuid`` (in memory at once). ``write=False`` leaves the durable file to
+        ``persist_quarantine`` — for callers holding a lock that fsyncs must not run under."""
         rec = {"uuid": uuid, "until": time.time() + seconds, "reason": reason,
                "maintenance": maintenance}
-        _atomic_write_text(os.path.join(self.quar_dir, _safe(uuid) + ".json"), json.dumps(rec),
-                           self.fsync)
         with self._mu:
             self._quar[uuid] = rec
+        if write:
+            self.persist_quarantine(rec)
+        return rec
+
+    def persist_quarantine(self, rec: dict) -> None:
+        _atomic_write_text(os.path.join(self.quar_dir, _safe(rec["uuid"]) + ".json"),
+                           json.dumps(rec), self.fsync)
 
     def quarantined(self) -> dict[str, dict]:
         now = time.time()

@@ -1,0 +1,168 @@
+"""The node agent's RPC server: HTTP/1.1 + JSON over a unix socket and/or TCP (optionally TLS),
+one thread per connection.
+
+The manager keeps a few persistent connections per agent (its workers' claim / observe / release
+calls and one long-poll on /v1/events). Serving each connection on its own thread lets a handler
+run where the request arrived: a claim runs on its connection's thread from request to reply — no
+event-loop hop into an executor and back, which on the claim path cost two GIL hand-offs and a
+loop wake-up (profiles/r2am claim spans: executorIn + executorOut + aiohttp framing ~ 1 ms) — and
+the event long-poll simply waits on a condition variable. Request framing is minimal on purpose:
+Content-Length bodies (no chunked requests), keep-alive by default, ``Connection: close`` honoured.
+"""
+from __future__ import annotations
+
+import hmac
+import json
+import logging
+import os
+import socket
+import ssl
+import threading
+import urllib.parse
+from typing import Callable
+
+log = logging.getLogger("gpupool.agent.rpc")
+
+# handler(query, body) -> (status, content_type, payload bytes, after_send or None)
+Handler = Callable[[dict, bytes], tuple]
+OPEN_PATHS = {"/healthz", "/metrics"}
+_REASONS = {200: "OK", 400: "Bad Request", 401: "Unauthorized", 404: "Not Found",
+            405: "Method Not Allowed", 409: "Conflict", 413: "Payload Too Large",
+            500: "Internal Server Error"}
+MAX_BODY = 16 << 20
+
+
+def json_reply(obj, status: int = 200, after: Callable[[], None] | None = None) -> tuple:
+    return status, "application/json", json.dumps(obj).encode(), after
+
+
+def text_reply(text: str, status: int = 200) -> tuple:
+    return status, "text/plain", text.encode(), None
+
+
+class RpcServer:
+    def __init__(self, routes: dict[tuple[str, str], Handler], token: str = ""):
+        self.routes = routes
+        self._auth = ("Bearer " + token).encode() if token else b""
+        self._listeners: list[socket.socket] = []
+        self._stop = threading.Event()
+        self.requests = 0
+
+    # ------------------------------------------------------------ listeners
+    def listen_unix(self, path: str) -> None:
+        try:
+            os.unlink(path)
+        except FileNotFoundError:
+            pass
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.bind(path)
+        s.listen(64)
+        self._start(s, None)
+
+    def listen_tcp(self, host: str, port: int, ssl_ctx: ssl.SSLContext | None = None) -> None:
+        s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        s.bind((host or "0.0.0.0", port))
+        s.listen(64)
+        self._start(s, ssl_ctx)
+
+    def _start(self, s: socket.socket, ssl_ctx) -> None:
+        self._listeners.append(s)
+        threading.Thread(target=self._accept, args=(s, ssl_ctx), daemon=True,
+                         name="rpc-accept").start()
+
+    def close(self) -> None:
+        self._stop.set()
+        for s in self._listeners:
+            try:
+                s.close()
+            except OSError:
+                pass
+
+    def _accept(self, s: socket.socket, ssl_ctx) -> None:
+        while not self._stop.is_set():
+            try:
+                conn, _ = s.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._serve_conn, args=(conn, ssl_ctx), daemon=True,
+                             name="rpc-conn").start()
+
+    # ------------------------------------------------------------ one connection
+    def _serve_conn(self, conn: socket.socket, ssl_ctx) -> None:
+        try:
+            if conn.family != socket.AF_UNIX:
+                conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            if ssl_ctx is not None:
+                conn = ssl_ctx.wrap_socket(conn, server_side=True)
+            rf = conn.makefile("rb", buffering=65536)
+            while not self._stop.is_set():
+                line = rf.readline(65537)
+                if not line:
+                    return
+                if line in (b"\r\n", b"\n"):
+                    continue
+                try:
+                    method, target, version = line.decode("latin-1").split(None, 2)
+                except ValueError:
+                    return
+                headers: dict[str, str] = {}
+                while True:
+                    h = rf.readline(65537)
+                    if h in (b"\r\n", b"\n", b""):
+                        break
+                    k, _, v = h.decode("latin-1").partition(":")
+                    headers[k.strip().lower()] = v.strip()
+                n = int(headers.get("content-length") or 0)
+                if n > MAX_BODY:
+                    self._send(conn, (413, "text/plain", b"body too large\n", None), False)
+                    return
+                body = rf.read(n) if n else b""
+                keep = headers.get("connection", "").lower() != "close" and \
+                    not version.strip().upper().endswith("1.0")
+                reply = self._dispatch(method.upper(), target, headers, body)
+                self._send(conn, reply, keep)
+                if reply[3] is not None:
+                    try:
+                        reply[3]()
+                    except Exception:
+                        log.exception("post-reply hook failed")
+                if not keep:
+                    return
+        except (OSError, ssl.SSLError, ValueError):
+            return
+        finally:
+            try:
+                conn.close()
+            except OSError:
+                pass
+
+    def _dispatch(self, method: str, target: str, headers: dict, body: bytes) -> tuple:
+        path, _, qs = target.partition("?")
+        self.requests += 1
+        if self._auth and path not in OPEN_PATHS and \
+                not hmac.compare_digest(headers.get("authorization", "").encode(), self._auth):
+            return json_reply({"reason": "Unauthorized",
+                               "message": "agent RPC requires the manager's token"}, 401)
+        h = self.routes.get((method, path))
+        if h is None:
+            known = any(p == path for _, p in self.routes)
+            return json_reply({"reason": "MethodNotAllowed" if known else "NotFound",
+                               "message": f"{method} {path}"}, 405 if known else 404)
+        query = {k: v[-1] for k, v in urllib.parse.parse_qs(qs).items()}
+        try:
+            return h(query, body)
+        except (ValueError, KeyError, TypeError) as e:
+            return json_reply({"reason": "BadRequest", "message": str(e)}, 400)
+        except Exception as e:  # a handler bug must not kill the connection thread silently
+            log.exception("RPC %s %s failed", method, path)
+            return json_reply({"reason": "InternalError", "message": repr(e)}, 500)
+
+    @staticmethod
+    def _send(conn: socket.socket, reply: tuple, keep: bool) -> None:
+        status, ctype, payload = reply[0], reply[1], reply[2]
+        head = (f"HTTP/1.1 {status} {_REASONS.get(status, 'OK')}\r\n"
+                f"Content-Type: {ctype}\r\nContent-Length: {len(payload)}\r\n"
+                f"Connection: {'keep-alive' if keep else 'close'}\r\n\r\n").encode()
+        conn.sendall(head + payload)

@@ -634,7 +634,8 @@ def agent_rbac() -> list[dict]:
     """ServiceAccount + ClusterRole + binding for the node agent DaemonSet: it registers its Node
     (labels, agent-endpoint annotation) and heartbeats the GPUPoolAgentReady/ROCmReady node
     conditions and posts Events on its Node (amdsmi hardware events, HBM sweep failures);
-    device/pod facts come from the kubelet's local sockets, not the API."""
+    device/pod facts come from the kubelet's local sockets; it lists pods only to resolve the pod
+    UID in a GPU process's cgroup to namespace/name for per-pod accounting."""
     sa = {"apiVersion": "v1", "kind": "ServiceAccount",
           "metadata": {"name": "gpupool-agent", "namespace": AGENT_NAMESPACE}}
     role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
@@ -642,7 +643,8 @@ def agent_rbac() -> list[dict]:
             "rules": [{"apiGroups": [""], "resources": ["nodes"],
                        "verbs": ["get", "create", "patch"]},
                       {"apiGroups": [""], "resources": ["nodes/status"], "verbs": ["patch"]},
-                      {"apiGroups": [""], "resources": ["events"], "verbs": ["create"]}]}
+                      {"apiGroups": [""], "resources": ["events"], "verbs": ["create"]},
+                      {"apiGroups": [""], "resources": ["pods"], "verbs": ["list"]}]}
     binding = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
                "metadata": {"name": "gpupool-agent-rolebinding"},
                "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",

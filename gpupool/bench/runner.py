@@ -381,14 +381,16 @@ class BenchRun:
         return gt.cli_state() if self.real else gt.fixture_state(self.node.fixture, self.node.name)
 
     def accuracy_under_faults(self, n: int, steps: int, seed: int = 0,
-                              truth_policy: dict | None = None, settle_s: float = 5.0) -> dict:
+                              truth_policy: dict | None = None, settle_s: float = 5.0,
+                              hold_s: float = 0.25) -> dict:
         """readyReplicas vs ground truth after every step of a random fault / clear sequence on
         the GPUs of a dedicated pool (replacePolicy Keep, so ownership is fixed and health is what
         moves). The truth is ``ground_truth.device_healthy`` over the independent device state
         (fixture or amd-smi CLI) + the injected overlay, under the pool's spec.health read back
         from the API server (or ``truth_policy``, to prove a mismatching rule is caught). A step
         counts as accurate when status.readyReplicas equals the truth — and the kubelet holds
-        exactly the truly healthy GPUs — within ``settle_s`` of the fault."""
+        exactly the truly healthy GPUs — within ``settle_s`` of the fault, and stays so for
+        ``hold_s``."""
         import random
         rng = random.Random(seed)
         self.phase = "create"
@@ -404,7 +406,12 @@ class BenchRun:
         health = {**gt.HEALTH_DEFAULTS, **(obj["spec"].get("health") or {})}
         self.phase = "ground_truth"
         base = self._state_now()                       # ECC baseline = state at claim
-        owned = gt.kubelet_allocatable(self.pr_socket).get("amd.com/gpu-acc", set())
+        deadline = time.monotonic() + 10  # the kubelet learns the devices asynchronously
+        while True:
+            owned = gt.kubelet_allocatable(self.pr_socket).get("amd.com/gpu-acc", set())
+            if len(owned) >= n or time.monotonic() > deadline:
+                break
+            time.sleep(0.01)
         ledger0 = gt.ledger_claims(self.state_dir, obj["metadata"]["uid"]) \
             if os.path.exists(os.path.join(self.state_dir, "ledger.json")) else set()
         samples: list[dict] = []
@@ -419,22 +426,34 @@ class BenchRun:
                 overlay = {"devices": {u: self._fault(k, base.get(u, {}), health)
                                        for u, k in kinds.items()}}
             t0 = time.perf_counter()
-            self.cluster.set_faults(self.node.name, overlay, sample=False, notify=True)
+            # delivered as an event (inotify) like a real amdsmi event; the forced sample makes
+            # the write a fence: when it returns the agent has applied the new state
+            self.cluster.set_faults(self.node.name, overlay, sample=True, notify=True)
             cur = gt.apply_overlay(base, overlay)
             truth_ok = {u for u in owned if gt.device_healthy(cur.get(u, {"present": False}),
                                                               base.get(u), policy)[0]}
-            deadline = time.monotonic() + settle_s
+            # agreement must hold for ``hold_s`` (a stale pre-fault status that happens to equal
+            # the new truth is not a correct answer: the operator would move off it)
+            deadline = time.monotonic() + settle_s + hold_s
+            first_agree = None
             while True:
                 o = self.c.get(MI355XPOOLS, name, self.ns)
                 ready = (o.get("status") or {}).get("readyReplicas")
                 adv = gt.kubelet_allocatable(self.pr_socket).get("amd.com/gpu-acc", set())
-                agree = ready == len(truth_ok) and adv == truth_ok
-                if agree or time.monotonic() > deadline:
+                now = time.monotonic()
+                if ready == len(truth_ok) and adv == truth_ok:
+                    if first_agree is None:
+                        first_agree = (now, time.perf_counter() - t0)
+                    elif now - first_agree[0] >= hold_s:
+                        break
+                else:
+                    first_agree = None
+                if now > deadline:
                     break
                 time.sleep(0.01)
-            dt = time.perf_counter() - t0
+            agree = first_agree is not None and time.monotonic() - first_agree[0] >= hold_s
             if agree:
-                t_conv.append(dt)
+                t_conv.append(first_agree[1])
             samples.append({"step": i, "faults": {u[-8:]: k for u, k in kinds.items()},
                             "truth": len(truth_ok), "readyReplicas": ready,
                             "kubeletHealthy": len(adv), "ok": agree})
