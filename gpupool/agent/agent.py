@@ -48,6 +48,32 @@ def _ranges(bits: list[int]) -> str:
     return ",".join(out)
 
 
+def _scan_pasids() -> dict[int, int]:
+    """PASID -> PID of every local process with an amdgpu render node open (the ``pasid:`` line
+    of its DRM fdinfo)."""
+    out: dict[int, int] = {}
+    for ent in os.listdir("/proc"):
+        if not ent.isdigit():
+            continue
+        fd_dir = f"/proc/{ent}/fd"
+        try:
+            fds = os.listdir(fd_dir)
+        except OSError:
+            continue
+        for fd in fds:
+            try:
+                if not os.readlink(f"{fd_dir}/{fd}").startswith("/dev/dri/renderD"):
+                    continue
+                with open(f"/proc/{ent}/fdinfo/{fd}") as f:
+                    for line in f:
+                        if line.startswith("pasid:"):
+                            out[int(line.split()[1])] = int(ent)
+                            break
+            except (OSError, ValueError, IndexError):
+                continue
+    return out
+
+
 def gpu_of(device_id: str) -> str:
     """The GPU uuid behind a device-plugin ID (a plain uuid, or a shared GPU's slot)."""
     return device_id.split(SLOT_SEP, 1)[0]
@@ -156,6 +182,9 @@ class Agent:
         self.pod_usage: dict[str, list[dict]] = {}        # uuid -> per-pod VRAM / gfx time
         self._proc_prev: dict[tuple[str, int], list] = {}  # (uuid, pid) -> [(t, gfxNs)]
         self._pid_pods: dict[int, dict] = {}
+        self._pid_miss: dict[int, float] = {}
+        self._pasids: dict[int, int] = {}    # KFD PASID -> PID in this namespace
+        self._pasid_scan = 0.0
         self._pods_by_uid: tuple[float, dict[str, dict]] = (0.0, {})
         self._xgmi_last = time.monotonic()
         self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0, "rechecks": 0,
@@ -616,11 +645,16 @@ class Agent:
         namespace/name through the API server; else from the pod identity in its environment
         (POD_NAME / POD_NAMESPACE: the downward API on a real node, set by the fake kubelet). The
         agent's own probe / scrubber buffers are reported as ``gpupool-agent``. {} if unknown."""
-        if pid == os.getpid():
-            return {"namespace": "", "pod": "gpupool-agent"}
         hit = self._pid_pods.get(pid)
         if hit is not None:
             return hit
+        if time.monotonic() - self._pid_miss.get(pid, -1e9) < 2.0:
+            return {}  # unresolved a moment ago: retry later, not on every sample
+        host_pid = pid
+        local = self._local_pid(pid)
+        if local == os.getpid():
+            return {"namespace": "", "pod": "gpupool-agent"}
+        pid = local
         import re
         pod: dict = {}
         try:
@@ -642,8 +676,30 @@ class Agent:
                 pass
         if len(self._pid_pods) > 4096:
             self._pid_pods.clear()
-        self._pid_pods[pid] = pod
+            self._pid_miss.clear()
+        if pod:
+            self._pid_pods[host_pid] = pod
+        else:
+            self._pid_miss[host_pid] = time.monotonic()
         return pod
+
+    def _local_pid(self, pid: int) -> int:
+        """amdsmi reports GPU processes by the kernel's (host) PID. An agent in its own PID
+        namespace (no hostPID) cannot open /proc/<host pid>; the KFD process's PASID bridges the
+        two: /sys/class/kfd/kfd/proc/<host pid>/pasid equals the ``pasid:`` of the process's
+        amdgpu render-node fd in /proc/<local pid>/fdinfo. Returns the PID as seen here (the
+        same number when the namespaces agree, or when no PASID is available)."""
+        try:
+            with open(f"/sys/class/kfd/kfd/proc/{pid}/pasid") as f:
+                pasid = int(f.read().strip() or 0)
+        except (OSError, ValueError):
+            return pid
+        m = self._pasids.get(pasid)
+        if m is None and time.monotonic() - self._pasid_scan > 1.0:
+            self._pasid_scan = time.monotonic()
+            self._pasids = _scan_pasids()
+            m = self._pasids.get(pasid)
+        return m if m is not None else pid
 
     def _pod_by_uid(self, uid: str) -> dict | None:
         ts, by_uid = self._pods_by_uid
