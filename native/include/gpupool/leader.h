@@ -37,6 +37,11 @@ class LeaderElector {
   LeaderConfig cfg_;
   Logger log_;
   std::atomic<bool> leader_{false};
+  // Expiry is timed from when *this* process saw the holder's record change (client-go's
+  // observedTime), never from the holder's renewTime against our wall clock: two replicas whose
+  // clocks disagree by more than leaseDurationSeconds must still not steal a live lease.
+  std::string observed_record_;
+  std::chrono::steady_clock::time_point observed_at_{};
 };
 
 }  // namespace gpupool

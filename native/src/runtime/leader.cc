@@ -8,7 +8,6 @@ LeaderElector::LeaderElector(KubeClient& client, LeaderConfig cfg)
     : client_(client), cfg_(std::move(cfg)), log_(Logger("leader").with("identity", cfg_.identity)) {}
 
 bool LeaderElector::try_acquire_or_renew() {
-  auto now_tp = std::chrono::system_clock::now();
   std::string now = microtime_now();
   int dur_s = static_cast<int>(std::chrono::duration_cast<std::chrono::seconds>(cfg_.lease_duration).count());
   Json lease;
@@ -38,14 +37,19 @@ bool LeaderElector::try_acquire_or_renew() {
   const Json& spec = lease["spec"];
   const std::string& holder = spec["holderIdentity"].as_string();
   bool mine = holder == cfg_.identity;
+  // the holder's record as we see it: any renewal (or hand-over) changes it
+  const std::string record = holder + "|" + spec["renewTime"].str_or("") + "|" +
+                             lease.path("metadata.resourceVersion").str_or("");
+  const auto steady_now = std::chrono::steady_clock::now();
+  if (record != observed_record_) {
+    observed_record_ = record;
+    observed_at_ = steady_now;
+  }
   if (!mine && !holder.empty()) {
-    std::chrono::system_clock::time_point renew;
-    if (parse_rfc3339(spec["renewTime"].as_string(), &renew)) {
-      auto expiry = renew + std::chrono::seconds(spec["leaseDurationSeconds"].as_int(dur_s));
-      if (expiry > now_tp) {
-        leader_ = false;
-        return false;  // held by a live leader
-      }
+    auto duration = std::chrono::seconds(spec["leaseDurationSeconds"].as_int(dur_s));
+    if (steady_now < observed_at_ + duration) {
+      leader_ = false;
+      return false;  // held by a live leader: its record changed less than a lease ago (our clock)
     }
   }
   Json upd = lease;

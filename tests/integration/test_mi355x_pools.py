@@ -678,3 +678,43 @@ def test_cordoned_node_takes_no_new_claims(cluster_factory):
     assert o["status"]["readyReplicas"] == 1  # its GPU stays
     k.patch(NODES, "node-a", {"spec": {"unschedulable": False}}, None)
     wait_ready(k, "held", 2, timeout=30)
+
+
+def test_leader_election_tolerates_clock_skew(cluster_factory):
+    """A live leader whose clock runs an hour behind renews with renewTimes far in the past: a
+    standby times the lease from when *it* saw the record change (client-go observedTime), so it
+    never takes over a lease that is still being renewed — and it does take over once the
+    renewals stop."""
+    import threading
+    from gpupool.kube import LEASES
+    c = cluster_factory(manager=False)
+    k = c.client
+    stale = "2001-01-01T00:00:%02d.000000Z"
+    k.create(LEASES, {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+                      "metadata": {"name": "gpupool-manager-leader"},
+                      "spec": {"holderIdentity": "skewed-leader", "leaseDurationSeconds": 2,
+                               "renewTime": stale % 0, "acquireTime": stale % 0}},
+             "gpupool-system")
+    stop = threading.Event()
+
+    def renew():
+        i = 0
+        while not stop.wait(0.4):
+            i += 1
+            o = k.get(LEASES, "gpupool-manager-leader", "gpupool-system")
+            if o["spec"]["holderIdentity"] != "skewed-leader":
+                return
+            o["spec"]["renewTime"] = stale % (i % 60)
+            k.update(LEASES, o, "gpupool-system")
+    t = threading.Thread(target=renew, daemon=True)
+    t.start()
+    c.manager_args = ["--leader-elect", "--lease-duration", "2s", "--renew-deadline", "1500ms",
+                      "--retry-period", "200ms", "--identity", "standby"]
+    c.start_manager()
+    time.sleep(4.0)  # two lease durations: the skewed holder keeps renewing
+    assert k.get(LEASES, "gpupool-manager-leader", "gpupool-system")["spec"]["holderIdentity"] == \
+        "skewed-leader"
+    stop.set()
+    t.join()
+    k.wait_for(LEASES, "gpupool-manager-leader", "gpupool-system",
+               lambda o: o and o["spec"]["holderIdentity"] == "standby", timeout=10, poll=0.1)
