@@ -17,6 +17,7 @@ provider depends on, with ARM's wire shapes:
 * Principals are scoped to subscriptions (403 AuthorizationFailed), resource groups must exist
   (404 ResourceGroupNotFound), VMs per resource group are capped (409 OperationNotAllowed).
 * ``POST /_sim/faults`` queues failures (``throttle``: n 429s, ``failVmPut``: n 500s,
+  ``lostVmPut``: n VM PUTs accepted but answered 504 and hidden from lists for 2 s,
   ``revokeTokens``), ``GET /_sim/state`` dumps everything (tests assert on it).
 
 Run in-process (``ArmSim(...).start()``, a daemon thread with its own event loop) or as
@@ -65,7 +66,7 @@ class ArmSim:
         self.vms: dict[str, dict] = {}    # lower-cased id -> resource
         self.nics: dict[str, dict] = {}
         self.disks: dict[str, dict] = {}
-        self.faults = {"throttle": 0, "failVmPut": 0}
+        self.faults = {"throttle": 0, "failVmPut": 0, "lostVmPut": 0}
         self.calls: list[tuple[str, str, int]] = []
         self.token_requests = 0
         self.mu = threading.Lock()
@@ -279,7 +280,9 @@ class ArmSim:
         return {k: v for k, v in res.items() if not k.startswith("_")}
 
     def _list(self, req: web.Request, table: dict, coll: str) -> web.Response:
-        items = sorted((v for k, v in table.items() if k.startswith(coll.lower() + "/")),
+        now = time.monotonic()
+        items = sorted((v for k, v in table.items() if k.startswith(coll.lower() + "/")
+                        and v.get("_listed_at", 0) <= now),  # ARM's eventually consistent lists
                        key=lambda v: v["name"])
         skip = int(req.query.get("$skiptoken", "0") or 0)
         page = items[skip:skip + self.page_size]
@@ -366,6 +369,12 @@ class ArmSim:
                              "storageProfile": {**(p.get("storageProfile") or {}), "osDisk": osd}},
               "_ready_at": time.monotonic() + self.vm_delay, "_rg": base}
         self.vms[key] = vm
+        if self.faults["lostVmPut"] > 0:
+            # accepted, but the reply is lost (gateway timeout) and lists will not show the VM
+            # for a while: a retry that picks a new name would create a second VM
+            self.faults["lostVmPut"] -= 1
+            vm["_listed_at"] = time.monotonic() + 2.0
+            return _err(504, "GatewayTimeout", "the request was accepted but the response timed out")
         return web.json_response(self._public(vm), status=201)
 
     def _delete(self, kind: tuple, key: str, name: str) -> web.Response:

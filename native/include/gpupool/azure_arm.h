@@ -35,7 +35,8 @@ class AzureArmProvider : public CloudProvider {
   VmRecord create(const Credentials& c, const AzureVmPoolSpec& spec, const std::string& owner,
                   const std::string& name) override;
   void destroy(const Credentials& c, const std::string& rg, const std::string& name) override;
-  std::vector<std::string> orphans(const Credentials& c, const std::string& rg, const std::string& owner) override;
+  std::vector<std::string> orphans(const Credentials& c, const std::string& rg, const std::string& owner,
+                                   const std::string& vm_prefix) override;
   uint64_t calls() const { return calls_.load(); }
 
  private:

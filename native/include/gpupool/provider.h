@@ -60,8 +60,11 @@ class CloudProvider {
   // Starts an asynchronous delete of VM + NIC + OS disk (README.md:216, :239). Idempotent.
   virtual void destroy(const Credentials& c, const std::string& rg, const std::string& name) = 0;
   // NICs / disks of ``owner`` that no longer belong to a VM, as "nic/<name>" / "disk/<name>"
-  // (must end up empty; destroy() accepts these ids).
-  virtual std::vector<std::string> orphans(const Credentials& c, const std::string& rg, const std::string& owner) = 0;
+  // (must end up empty; destroy() accepts these ids). NICs are matched by tag; OS disks (ARM
+  // gives implicitly created disks no tags) by the exact name "<vm_prefix><slot>-osdisk" of the
+  // pool's deterministic VM names.
+  virtual std::vector<std::string> orphans(const Credentials& c, const std::string& rg, const std::string& owner,
+                                           const std::string& vm_prefix) = 0;
 };
 
 struct FakeCloudOptions {
@@ -79,7 +82,8 @@ class FakeCloudProvider : public CloudProvider {
   VmRecord create(const Credentials& c, const AzureVmPoolSpec& spec, const std::string& owner,
                   const std::string& name) override;
   void destroy(const Credentials& c, const std::string& rg, const std::string& name) override;
-  std::vector<std::string> orphans(const Credentials& c, const std::string& rg, const std::string& owner) override;
+  std::vector<std::string> orphans(const Credentials& c, const std::string& rg, const std::string& owner,
+                                   const std::string& vm_prefix) override;
   Json dump();  // whole fake cloud (tests)
 
  private:

@@ -168,7 +168,6 @@ class AzureVmPoolReconciler : public PoolReconcilerBase {
  private:
   bool credentials_(const ObjectMeta& m, const AzureVmPoolSpec& spec, Credentials* out, std::string* why);
   CloudProvider& cloud_;
-  std::atomic<uint64_t> name_seq_{0};
 };
 
 // Mi355xJob: the GoHai platform's training-job path (reference GPU调度平台搭建.md:638-675 Volcano Job

@@ -1113,7 +1113,17 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
   }
   AzureVmPoolSpec spec = AzureVmPoolSpec::from(obj["spec"]);
   note_generation_(m);
-  const std::string owner = m.ns + "-" + m.name;  // README.md:238 owner tag
+  // README.md:238 tags every resource with its owner. "<ns>-<name>" (the reference's form) is
+  // ambiguous — pools a-b/c and a/b-c would share it and could list and delete each other's VMs
+  // — so the owner is "<ns>/<name>" ('/' occurs in neither part).
+  const std::string owner = m.ns + "/" + m.name;
+  // Deterministic VM names "<name>-<uid8>-<slot>": a create whose reply was lost is retried under
+  // the same name, so ARM's create-or-update PUT makes the retry idempotent (README.md:240) instead
+  // of creating a second VM; the uid part keeps a recreated pool of the same name distinct.
+  std::string uid8;
+  for (char ch : m.uid)
+    if (ch != '-' && uid8.size() < 8) uid8.push_back(ch);
+  const std::string vm_prefix = m.name + "-" + uid8 + "-";
   Credentials creds;
   std::string why;
   bool have_creds = credentials_(m, spec, &creds, &why);
@@ -1165,7 +1175,7 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
         if (vm.state != "Deleting") cloud_.destroy(creds, spec.resource_group, vm.name);
       vms = cloud_.list(creds, spec.resource_group, owner);
       // NICs / OS disks left by an interrupted create: removed once their VMs are gone
-      orphans = cloud_.orphans(creds, spec.resource_group, owner);
+      orphans = cloud_.orphans(creds, spec.resource_group, owner, vm_prefix);
       if (vms.empty())
         for (const auto& o : orphans) cloud_.destroy(creds, spec.resource_group, o);
     } catch (const ProviderError& e) {
@@ -1213,12 +1223,14 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
     }
     if (cur < desired) {
       progress_reason = "ScalingUp";
+      std::set<std::string> taken;  // every listed VM name, Deleting ones included
+      for (const auto& vm : vms) taken.insert(vm.name);
+      int64_t slot = 0;
       for (int64_t i = cur; i < desired; ++i) {
-        char suffix[16];
-        uint64_t seq = name_seq_++;
-        std::snprintf(suffix, sizeof suffix, "%05llx",
-                      static_cast<unsigned long long>((std::random_device{}() ^ (seq * 2654435761ULL)) & 0xFFFFF));
-        std::string vname = m.name + "-" + suffix;  // README.md:204-205 unique name
+        std::string vname;
+        do vname = vm_prefix + std::to_string(slot++);  // README.md:204-205 unique name
+        while (taken.count(vname));
+        taken.insert(vname);
         cloud_.create(creds, spec, owner, vname);
         event_(obj, "Normal", "VMCreating", "creating VM " + vname + " (" + spec.vm_size + ")");
       }

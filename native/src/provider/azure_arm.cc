@@ -6,7 +6,7 @@
 //           federated client assertion = Workload Identity, README.md:59-60/311), cached per client
 //           until 5 minutes before expiry, refreshed once on a 401
 //   list    GET  .../resourceGroups/{rg}/providers/Microsoft.Compute/virtualMachines (nextLink
-//           paging), filtered by the tags managed-by=azurevmpool-operator, owner=<ns>-<name>
+//           paging), filtered by the tags managed-by=azurevmpool-operator, owner=<ns>/<name>
 //   create  PUT  .../Microsoft.Network/networkInterfaces/{vm}-nic (subnet of spec.vnetName /
 //           spec.subnetName), waited for until Succeeded, then PUT .../virtualMachines/{vm} with
 //           spec.vmSize, spec.imageReference, an SSH-only Linux profile, and deleteOption=Delete on
@@ -14,7 +14,7 @@
 //           that fails removes the NIC it just made
 //   destroy DELETE .../virtualMachines/{vm} (async, 202); "nic/<name>" / "disk/<name>" delete a
 //           leftover NIC / OS disk
-//   orphans unattached NICs tagged for the owner and unattached "<pool>-*-osdisk" disks
+//   orphans unattached NICs tagged for the owner and unattached "<pool>-<uid8>-<slot>-osdisk" disks
 //
 // Every call is idempotent (PUT by name, DELETE 404 = done). Throttling (429) and 5xx are
 // transient ProviderErrors (the reconciler backs off); other 4xx carry ARM's error code.
@@ -299,7 +299,7 @@ void AzureArmProvider::destroy(const Credentials& c, const std::string& rg, cons
 }
 
 std::vector<std::string> AzureArmProvider::orphans(const Credentials& c, const std::string& rg,
-                                                   const std::string& owner) {
+                                                   const std::string& owner, const std::string& vm_prefix) {
   std::vector<std::string> out;
   const std::string rgp = rg_path_(c, rg);
   for (const auto& n : list_all_(c, rgp + "/providers/Microsoft.Network/networkInterfaces?api-version=" +
@@ -308,19 +308,16 @@ std::vector<std::string> AzureArmProvider::orphans(const Credentials& c, const s
         n.path("properties.provisioningState").as_string() != "Deleting")
       out.push_back("nic/" + n["name"].as_string());
   }
-  // OS disks carry no tags of their own: "<pool>-<suffix>-osdisk", unattached (owner = <ns>-<pool>)
-  std::set<std::string> pools;
-  for (size_t i = owner.find('-'); i != std::string::npos; i = owner.find('-', i + 1)) pools.insert(owner.substr(i + 1));
+  // OS disks carry no tags of their own: exactly "<vm_prefix><slot>-osdisk" (this pool's
+  // deterministic VM names; the prefix holds the pool UID, so no other pool's disk can match)
   for (const auto& d : list_all_(c, rgp + "/providers/Microsoft.Compute/disks?api-version=" + opts_.compute_api)) {
     const std::string dn = d["name"].as_string();
-    if (dn.size() < 8 || dn.compare(dn.size() - 7, 7, "-osdisk") != 0 || !d["managedBy"].as_string().empty()) continue;
-    bool mine = false;  // exactly "<pool>-<5 hex digits>-osdisk", the reconciler's VM naming
-    for (const auto& pool : pools) {
-      if (dn.size() != pool.size() + 1 + 5 + 7 || dn.rfind(pool + "-", 0) != 0) continue;
-      const std::string sfx = dn.substr(pool.size() + 1, 5);
-      mine = mine || sfx.find_first_not_of("0123456789abcdef") == std::string::npos;
-    }
-    if (mine) out.push_back("disk/" + dn);
+    if (vm_prefix.empty() || !d["managedBy"].as_string().empty()) continue;
+    if (dn.size() <= vm_prefix.size() + 7 || dn.rfind(vm_prefix, 0) != 0 ||
+        dn.compare(dn.size() - 7, 7, "-osdisk") != 0)
+      continue;
+    const std::string slot = dn.substr(vm_prefix.size(), dn.size() - vm_prefix.size() - 7);
+    if (slot.find_first_not_of("0123456789") == std::string::npos) out.push_back("disk/" + dn);
   }
   return out;
 }

@@ -146,7 +146,7 @@ void FakeCloudProvider::destroy(const Credentials& c, const std::string& rg, con
 }
 
 std::vector<std::string> FakeCloudProvider::orphans(const Credentials& c, const std::string& rg,
-                                                    const std::string& owner) {
+                                                    const std::string& owner, const std::string& /*vm_prefix*/) {
   check_creds_(c);
   std::lock_guard<std::mutex> g(mu_);
   advance_locked_();

@@ -237,7 +237,7 @@ TEST(fakecloud_lifecycle_and_cleanup) {
   EXPECT_EQ(cloud.list(c, "rg", "default-p")[0].state, std::string("Succeeded"));
   cloud.destroy(c, "rg", "p-1");
   EXPECT_EQ(cloud.list(c, "rg", "default-p").size(), 0u);
-  EXPECT_EQ(cloud.orphans(c, "rg", "default-p").size(), 0u);  // NIC + disk gone too
+  EXPECT_EQ(cloud.orphans(c, "rg", "default-p", "p-").size(), 0u);  // NIC + disk gone too
   Credentials bad;
   EXPECT_THROW(cloud.list(bad, "rg", "default-p"));
 }

@@ -99,7 +99,7 @@ def test_arm_scale_up_down_and_full_cleanup(arm, cluster_factory):
     assert sorted(o["status"]["vms"]) == sorted(v["name"] for v in st["vms"])
     for vm in st["vms"]:
         assert vm["tags"] == {"managed-by": "azurevmpool-operator",
-                              "owner": "default-gpu-pool-prod"}  # README.md:238
+                              "owner": "default/gpu-pool-prod"}  # README.md:238
         p = vm["properties"]
         assert p["provisioningState"] == "Succeeded"
         assert p["hardwareProfile"]["vmSize"] == "Standard_NC4as_T4_v3"
@@ -200,14 +200,39 @@ def test_arm_throttling_token_revocation_paging_and_orphans(arm, cluster_factory
     assert arm.state()["tokenRequests"] == before + 1
     assert conds(o)["CredentialsValid"]["status"] == "True"
     # a NIC + OS disk left behind by an interrupted create are removed with the pool
-    arm.add_orphans(SUB, RG, "default-busy", "busy-0abcd")
-    arm.add_orphans(SUB, RG, "default-other", "other-0abcd")  # not ours: must survive
+    uid8 = o["metadata"]["uid"].replace("-", "")[:8]
+    assert sorted(o["status"]["vms"]) == [f"busy-{uid8}-{i}" for i in range(4)]
+    arm.add_orphans(SUB, RG, "default/busy", f"busy-{uid8}-9")
+    arm.add_orphans(SUB, RG, "default/other", "other-0abcdef0-0")  # not ours: must survive
+    # another namespace's pool with a colliding "<ns>-<name>" ("default-busy") and a disk whose
+    # name merely starts like ours: neither is this pool's
+    arm.add_orphans(SUB, RG, "default-busy/x", f"busy-{uid8}x-0")
     k.delete(AZUREVMPOOLS, "busy", "default")
     k.wait_for(AZUREVMPOOLS, "busy", "default", lambda o: o is None, timeout=30)
     st = arm.state()
     assert st["vms"] == []
-    assert [n["name"] for n in st["nics"]] == ["other-0abcd-nic"]
-    assert [d["name"] for d in st["disks"]] == ["other-0abcd-osdisk"]
+    assert sorted(n["name"] for n in st["nics"]) == sorted(
+        ["other-0abcdef0-0-nic", f"busy-{uid8}x-0-nic"])
+    assert sorted(d["name"] for d in st["disks"]) == sorted(
+        ["other-0abcdef0-0-osdisk", f"busy-{uid8}x-0-osdisk"])
+
+
+def test_arm_lost_vm_put_is_retried_idempotently(arm, cluster_factory):
+    """A VM PUT that ARM accepted but whose reply was lost, with lists not yet showing the VM
+    (eventual consistency): the retry re-PUTs the same deterministic name, so the pool ends with
+    exactly its replicas — no duplicate VM created and trimmed later (README.md:240)."""
+    arm.faults["lostVmPut"] = 1
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(), "default")
+    k.create(AZUREVMPOOLS, sample("lost", 2), "default")
+    o = k.wait_for(AZUREVMPOOLS, "lost", "default", az_ready(2), timeout=30)
+    st = arm.state()
+    assert len(st["vms"]) == 2 and len(st["nics"]) == 2 and len(st["disks"]) == 2
+    uid8 = o["metadata"]["uid"].replace("-", "")[:8]
+    assert sorted(v["name"] for v in st["vms"]) == [f"lost-{uid8}-0", f"lost-{uid8}-1"]
+    reasons = [e["reason"] for e in settled_events(k)]
+    assert "GatewayTimeout" in reasons and "VMDeleting" not in reasons
 
 
 def test_arm_failed_vm_put_leaves_no_nic(arm, cluster_factory):
@@ -275,7 +300,8 @@ def test_arm_provider_under_sanitizer(san, arm, cluster_factory):
         arm.tokens.clear()
     k.patch(AZUREVMPOOLS, "s1", {"spec": {"replicas": 1}}, "default")
     k.wait_for(AZUREVMPOOLS, "s1", "default", az_ready(1), timeout=60)
-    arm.add_orphans(SUB, RG, "default-s2", "s2-0abcd")
+    uid8 = k.get(AZUREVMPOOLS, "s2", "default")["metadata"]["uid"].replace("-", "")[:8]
+    arm.add_orphans(SUB, RG, "default/s2", f"s2-{uid8}-7")
     for name in ("s1", "s2"):
         k.delete(AZUREVMPOOLS, name, "default")
     for name in ("s1", "s2"):

@@ -70,7 +70,7 @@ def test_scale_up_down_and_cleanup(azure):
     o = k.wait_for(AZUREVMPOOLS, "gpu-pool-prod", "default", az_ready(2), timeout=20)
     vms = cloud(azure)["vms"]
     assert len(vms) == 2
-    assert all(v["tags"] == {"managed-by": "azurevmpool-operator", "owner": "default-gpu-pool-prod"}
+    assert all(v["tags"] == {"managed-by": "azurevmpool-operator", "owner": "default/gpu-pool-prod"}
                for v in vms)  # README.md:238 tag contract
     assert sorted(o["status"]["vms"]) == sorted(v["name"] for v in vms)
     k.patch(AZUREVMPOOLS, "gpu-pool-prod", {"spec": {"replicas": 1}}, "default")
