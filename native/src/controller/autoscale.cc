@@ -1,5 +1,6 @@
 // Mi355xPoolAutoscaler — see the class comment in reconciler.h.
 #include <algorithm>
+#include <map>
 
 #include "gpupool/generated/schema_consts.h"
 #include "gpupool/reconciler.h"
@@ -92,7 +93,27 @@ int64_t Mi355xPoolAutoscaler::pool_demand(const std::vector<Json>& pods, const s
   std::vector<Json> unbound;
   for (const auto& j : jobs)
     if (j.path("spec.poolRef").as_string().empty()) unbound.push_back(j);
-  int64_t remaining = demand(pods, unbound, "", "", resource);
+  // A pod already running on a pool's GPUs (status.devices[].pods, from the agents' PodResources
+  // view) is that pool's demand: attributing it to whichever pool comes first in the split would
+  // grow an idle pool while the one it runs on looks over-provisioned and drains it.
+  std::map<std::string, std::string> pod_pool;  // "ns/pod" -> "ns/pool"
+  for (const auto& q : pools) {
+    if (q.path("spec.resourceName").str_or(gen::kDefaultResource) != resource) continue;
+    const std::string qkey = q.path("metadata.namespace").as_string() + "/" + q.path("metadata.name").as_string();
+    for (const auto& d : q.path("status.devices").elements())
+      for (const auto& pk : d["pods"].elements()) pod_pool[pk.as_string()] = qkey;
+  }
+  std::map<std::string, int64_t> bound;  // "ns/pool" -> GPUs its running pods use
+  std::vector<Json> pending;
+  for (const auto& p : pods) {
+    auto it = pod_pool.find(p.path("metadata.namespace").as_string() + "/" + p.path("metadata.name").as_string());
+    if (it == pod_pool.end()) {
+      pending.push_back(p);
+    } else if (!terminal(pod_phase(p)) && p.path("metadata.deletionTimestamp").as_string().empty()) {
+      bound[it->second] += pod_request(p, resource);
+    }
+  }
+  int64_t remaining = demand(pending, unbound, "", "", resource);
   // fixed-size pools of the same resource serve shared demand first (whatever their own gangs
   // leave free); what is left is split over the autoscaled pools in (namespace, name) order up to
   // each one's maxReplicas, so two autoscaled pools never both grow for the same pods
@@ -105,7 +126,7 @@ int64_t Mi355xPoolAutoscaler::pool_demand(const std::vector<Json>& pods, const s
     if (q.path("spec.resourceName").str_or(gen::kDefaultResource) != resource) continue;
     if (!q.path("metadata.deletionTimestamp").as_string().empty()) continue;
     const std::string qns = q.path("metadata.namespace").as_string(), qname = q.path("metadata.name").as_string();
-    const int64_t expl = explicit_of(qns, qname);
+    const int64_t expl = explicit_of(qns, qname) + bound[qns + "/" + qname];
     // capacities in devices of the resource: a shared GPU offers sharing.replicasPerGPU of them
     const int64_t k = std::max<int64_t>(1, q.path("spec.sharing.replicasPerGPU").as_int(1));
     if (q.path("spec.autoscale.enabled").as_bool(false)) {
@@ -126,7 +147,7 @@ int64_t Mi355xPoolAutoscaler::pool_demand(const std::vector<Json>& pods, const s
     remaining -= share;
     if (a.ns == ns && a.name == pool) return a.expl + share;
   }
-  return explicit_of(ns, pool);  // not (yet) in the pool list
+  return explicit_of(ns, pool) + bound[ns + "/" + pool];  // not (yet) in the pool list
 }
 
 Outcome Mi355xPoolAutoscaler::reconcile(const std::string& ns, const std::string& name) {

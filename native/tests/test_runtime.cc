@@ -518,6 +518,19 @@ TEST(autoscale_pool_demand_attribution) {
   // a single pool gets exactly demand()
   pools = {P("a", true, 0, 16)};
   EXPECT_EQ(A::pool_demand(pods, jobs, pools, "ns", "a", "r/g"), A::demand(pods, jobs, "ns", "a", "r/g"));
+  // two autoscaled pools, pods already running on the later one ("b"): their GPUs are b's
+  // demand, not the first pool's in the split (a would grow idle, b would drain them)
+  auto named = [&](const char* name, int n) {
+    return J((std::string(R"({"metadata":{"namespace":"ns","name":")") + name +
+              R"("},"status":{"phase":"Running"},"spec":{"containers":[{"resources":{"limits":{"r/g":)" +
+              std::to_string(n) + "}}}]}}").c_str());
+  };
+  gpupool::Json b = P("b", true, 2, 4);
+  b["status"] = J(R"({"devices":[{"uuid":"u1","pods":["ns/w1"]},{"uuid":"u2","pods":["ns/w2"]}]})");
+  pools = {P("a", true, 0, 4), b};
+  std::vector<gpupool::Json> running = {named("w1", 1), named("w2", 1), named("new", 1)};
+  EXPECT_EQ(A::pool_demand(running, {}, pools, "ns", "b", "r/g"), 2);  // its two running pods
+  EXPECT_EQ(A::pool_demand(running, {}, pools, "ns", "a", "r/g"), 1);  // only the pending one
 }
 
 TEST(job_validation) {

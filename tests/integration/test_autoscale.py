@@ -107,3 +107,29 @@ def test_two_pools_same_resource_do_not_double_count(cluster_factory):
         running(k, f"p{i}")
     time.sleep(1.0)
     assert k.get(MI355XPOOLS, "auto", "default")["spec"]["replicas"] == 2
+
+
+def test_two_autoscaled_pools_keep_their_running_pods(cluster_factory):
+    """Two autoscaled pools of one resource; pods already run on the later pool ("zb", grown for
+    them while it was the only one). Creating "za" (first in name order) must not hand it zb's
+    demand: za stays at 0 while zb keeps its GPUs and pods, even past scaleDownDelaySeconds."""
+    k = cluster_factory().client
+    auto = {"enabled": True, "minReplicas": 0, "maxReplicas": 4, "scaleDownDelaySeconds": 0}
+    k.create(MI355XPOOLS, mi_pool("zb", 0, resourceName=RES, autoscale=auto,
+                                  drain={"gracePeriodSeconds": 1}), "default")
+    for i in range(2):
+        k.create(PODS, pause_pod(f"w{i}", resource=RES), "default")
+    wait_ready(k, "zb", 2)
+    for i in range(2):
+        running(k, f"w{i}")
+    # zb's status lists its pods (the agents' PodResources view) before za appears
+    k.wait_for(MI355XPOOLS, "zb", "default", lambda o: sum(
+        len(d.get("pods") or []) for d in o["status"]["devices"]) == 2, timeout=20)
+    k.create(MI355XPOOLS, mi_pool("za", 0, resourceName=RES, autoscale=auto), "default")
+    wait_ready(k, "za", 0)
+    time.sleep(1.5)  # several autoscaler passes, scale-down delay 0
+    assert k.get(MI355XPOOLS, "za", "default")["spec"]["replicas"] == 0
+    zb = wait_ready(k, "zb", 2)
+    assert sum(len(d.get("pods") or []) for d in zb["status"]["devices"]) == 2
+    for i in range(2):
+        assert k.get(PODS, f"w{i}", "default")["status"]["phase"] == "Running"
