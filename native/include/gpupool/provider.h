@@ -190,10 +190,11 @@ class RocmProvider : public DeviceProvider {
   // of, younger than ``view_max_age`` (telemetry keeps moving without generation bumps) and no
   // mutating RPC to that node started since it was fetched; otherwise it is an RPC as before.
   void note_gen(const std::string& node, int64_t gen);
-  // Waits (up to ``max_wait_ms``) for the node's in-flight mutating RPCs to finish first: a
-  // claim bumps the agent's generation several times, and fetching the full view meanwhile only
-  // competes with the claim's reply on the agent's event loop for a view that is stale at once.
-  void prefetch(const std::string& node, int max_wait_ms = 30000);
+  // Skipped while a mutating RPC to the node is in flight (optionally after waiting up to
+  // ``max_wait_ms`` for it): a claim bumps the agent's generation several times and its reply
+  // invalidates the cache anyway, and the caller — the node's event-stream thread — must never
+  // stall behind RPC traffic (pod-exit and capacity events would queue up behind it).
+  void prefetch(const std::string& node, int max_wait_ms = 0);
   void set_view_max_age_ms(int ms) { view_max_age_ms_ = ms; }
   uint64_t view_cache_hits() const { return cache_hits_.load(); }
 

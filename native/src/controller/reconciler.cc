@@ -260,6 +260,7 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
     if (!spec.node_name.empty() && spec.node_name != hint) nodes.push_back(spec.node_name);
     if (nodes.empty()) nodes = provider_.node_names();
   }
+  std::vector<std::string> unreachable_hinted;
   for (const auto& n : nodes) {
     NodeView nv = provider_.observe_pool(n, m.uid);
     if (!nv.reachable) {
@@ -267,6 +268,7 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
         o.reachable = false;
         o.error = nv.error;
         o.node = n;
+        if (hinted.count(n)) unreachable_hinted.push_back(n);
       }
       continue;
     }
@@ -296,6 +298,12 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
     return a.node != b.node ? a.node < b.node : a.index < b.index;
   });
   index_nodes(o, span_nodes && o.reachable);
+  // A node that held GPUs of the pool and is unreachable now keeps its place in status.nodes: its
+  // GPUs (and their pods) are still held, so it must stay hinted — and block scale-up (the pass
+  // returns early while !reachable) — until it answers again.
+  for (const auto& n : unreachable_hinted)
+    if (std::find(o.nodes.begin(), o.nodes.end(), n) == o.nodes.end()) o.nodes.push_back(n);
+  std::sort(o.nodes.begin(), o.nodes.end());
   return o;
 }
 

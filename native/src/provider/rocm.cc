@@ -185,8 +185,12 @@ void RocmProvider::prefetch(const std::string& node, int max_wait_ms) {
     std::unique_lock<std::mutex> g(cache_mu_);
     // system_clock deadline: libstdc++ then waits with pthread_cond_timedwait, which TSan
     // intercepts (a steady_clock wait_for uses pthread_cond_clockwait, which GCC 11's TSan misses)
-    cache_cv_.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(max_wait_ms),
-                         [&] { return inflight_[node] == 0; });
+    if (max_wait_ms > 0)
+      cache_cv_.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(max_wait_ms),
+                           [&] { return inflight_[node] == 0; });
+    // a mutating RPC is in flight: its reply invalidates the cache anyway, and the caller (the
+    // node's event-stream thread) must not stall behind it — skip, the next observe asks the agent
+    if (inflight_[node] > 0) return;
     epoch = epoch_[node];
   }
   NodeView v = observe_pool(node, "");  // the full view (an RPC: the cache serves pools only)

@@ -718,3 +718,28 @@ def test_leader_election_tolerates_clock_skew(cluster_factory):
     t.join()
     k.wait_for(LEASES, "gpupool-manager-leader", "gpupool-system",
                lambda o: o and o["spec"]["holderIdentity"] == "standby", timeout=10, poll=0.1)
+
+
+def test_spanning_pool_keeps_unreachable_nodes(cluster_factory):
+    """A pool spanning three nodes loses two agents: status.nodes keeps listing them (their GPUs
+    and pods are still held), the pool reports AgentUnreachable and claims nothing elsewhere;
+    when the agents return it is Ready again on the same three nodes."""
+    nodes = [NodeSpec(f"sn-{i}", count=4) for i in range(3)]
+    c = cluster_factory(nodes=nodes)
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("wide", 12, maxNodes=3), "default")
+    o = wait_ready(k, "wide", 12, timeout=60)
+    assert sorted(o["status"]["nodes"]) == ["sn-0", "sn-1", "sn-2"]
+    before = {d["uuid"] for d in o["status"]["devices"]}
+    c._kill("agent-sn-1")
+    c._kill("agent-sn-2")
+    o = k.wait_for(MI355XPOOLS, "wide", "default", lambda o: conds(o).get("Ready", {}).get(
+        "reason") == "AgentUnreachable", timeout=60)
+    time.sleep(1.0)  # a few more passes with both nodes down
+    o = k.get(MI355XPOOLS, "wide", "default")
+    assert sorted(o["status"]["nodes"]) == ["sn-0", "sn-1", "sn-2"], o["status"].get("nodes")
+    for n in nodes[1:]:
+        c.start_agent(n)
+    o = wait_ready(k, "wide", 12, timeout=60)
+    assert sorted(o["status"]["nodes"]) == ["sn-0", "sn-1", "sn-2"]
+    assert {d["uuid"] for d in o["status"]["devices"]} == before
