@@ -1318,6 +1318,11 @@ class Agent:
             self.ledger.flush(seq)
         if n:
             self._pods_kick.set()  # watch the evicted pods go
+            if self._podres is not None:
+                try:  # the drain that follows must see every pod on these GPUs, not a cached map
+                    self._refresh_pods()
+                except Exception as e:
+                    log.debug("podresources refresh on cordon failed: %s", e)
         self._notify_plugins()
         return {"ok": True, "cordoned": n}
 

@@ -460,7 +460,16 @@ int Mi355xPoolReconciler::drain_(const Json& obj, const std::string& node, const
     }
   }
   for (const auto& kv : release) {
-    provider_.release(kv.first, m.uid, kv.second);
+    try {
+      provider_.release(kv.first, m.uid, kv.second);
+    } catch (const ProviderError& e) {
+      // The agent re-checks the kubelet before releasing: a pod our view did not show yet (it
+      // started after the view was taken) keeps its GPU. Not a failure: the release RPC
+      // invalidated the view cache, so the next pass observes the pod and evicts it.
+      if (e.code != "PodsRunning") throw;
+      still += static_cast<int>(kv.second.size());
+      continue;
+    }
     {
       std::lock_guard<std::mutex> g(mu_);
       evicted_[m.uid].clear();
