@@ -48,10 +48,11 @@ def _ranges(bits: list[int]) -> str:
     return ",".join(out)
 
 
-def _scan_pasids() -> dict[int, int]:
-    """PASID -> PID of every local process with an amdgpu render node open (the ``pasid:`` line
-    of its DRM fdinfo)."""
-    out: dict[int, int] = {}
+def _scan_drm_clients() -> dict[str, dict[int, dict]]:
+    """GPU memory and engine time per local process from the amdgpu DRM fdinfo of its
+    render-node fds (``drm-pdev``, ``drm-memory-vram``, ``drm-engine-*``): bdf -> pid -> usage.
+    Namespace-safe — it sees exactly the processes of this PID namespace, under their local PIDs."""
+    out: dict[str, dict[int, dict]] = {}
     for ent in os.listdir("/proc"):
         if not ent.isdigit():
             continue
@@ -60,17 +61,29 @@ def _scan_pasids() -> dict[int, int]:
             fds = os.listdir(fd_dir)
         except OSError:
             continue
+        seen: set[str] = set()
         for fd in fds:
             try:
                 if not os.readlink(f"{fd_dir}/{fd}").startswith("/dev/dri/renderD"):
                     continue
                 with open(f"/proc/{ent}/fdinfo/{fd}") as f:
-                    for line in f:
-                        if line.startswith("pasid:"):
-                            out[int(line.split()[1])] = int(ent)
-                            break
-            except (OSError, ValueError, IndexError):
+                    info = dict(line.split(":", 1) for line in f if ":" in line)
+            except (OSError, ValueError):
                 continue
+            client = info.get("drm-client-id", "").strip()
+            bdf = info.get("drm-pdev", "").strip().lower()
+            if not bdf or client in seen:
+                continue
+            seen.add(client)
+            vram = info.get("drm-memory-vram") or info.get("drm-total-vram") or "0"
+            parts = vram.split()
+            kib = {"KiB": 1 << 10, "MiB": 1 << 20, "GiB": 1 << 30}.get(parts[1], 1) \
+                if len(parts) > 1 else 1
+            eng = sum(int(v.split()[0]) for k, v in info.items()
+                      if k.startswith("drm-engine-") and v.split() and v.split()[0].isdigit())
+            u = out.setdefault(bdf, {}).setdefault(int(ent), {"vramBytes": 0, "engineNs": 0})
+            u["vramBytes"] += int(parts[0]) * kib if parts and parts[0].isdigit() else 0
+            u["engineNs"] += eng
     return out
 
 
@@ -183,8 +196,6 @@ class Agent:
         self._proc_prev: dict[tuple[str, int], list] = {}  # (uuid, pid) -> [(t, gfxNs)]
         self._pid_pods: dict[int, dict] = {}
         self._pid_miss: dict[int, float] = {}
-        self._pasids: dict[int, int] = {}    # KFD PASID -> PID in this namespace
-        self._pasid_scan = 0.0
         self._pods_by_uid: tuple[float, dict[str, dict]] = (0.0, {})
         self._xgmi_last = time.monotonic()
         self.stats = {"claims": 0, "releases": 0, "probes": 0, "probe_failures": 0, "rechecks": 0,
@@ -651,10 +662,8 @@ class Agent:
         if time.monotonic() - self._pid_miss.get(pid, -1e9) < 2.0:
             return {}  # unresolved a moment ago: retry later, not on every sample
         host_pid = pid
-        local = self._local_pid(pid)
-        if local == os.getpid():
+        if pid == os.getpid():
             return {"namespace": "", "pod": "gpupool-agent"}
-        pid = local
         import re
         pod: dict = {}
         try:
@@ -683,24 +692,6 @@ class Agent:
             self._pid_miss[host_pid] = time.monotonic()
         return pod
 
-    def _local_pid(self, pid: int) -> int:
-        """amdsmi reports GPU processes by the kernel's (host) PID. An agent in its own PID
-        namespace (no hostPID) cannot open /proc/<host pid>; the KFD process's PASID bridges the
-        two: /sys/class/kfd/kfd/proc/<host pid>/pasid equals the ``pasid:`` of the process's
-        amdgpu render-node fd in /proc/<local pid>/fdinfo. Returns the PID as seen here (the
-        same number when the namespaces agree, or when no PASID is available)."""
-        try:
-            with open(f"/sys/class/kfd/kfd/proc/{pid}/pasid") as f:
-                pasid = int(f.read().strip() or 0)
-        except (OSError, ValueError):
-            return pid
-        m = self._pasids.get(pasid)
-        if m is None and time.monotonic() - self._pasid_scan > 1.0:
-            self._pasid_scan = time.monotonic()
-            self._pasids = _scan_pasids()
-            m = self._pasids.get(pasid)
-        return m if m is not None else pid
-
     def _pod_by_uid(self, uid: str) -> dict | None:
         ts, by_uid = self._pods_by_uid
         if uid not in by_uid and time.monotonic() - ts > 5.0 and self.cfg.apiserver:
@@ -725,13 +716,23 @@ class Agent:
         window = max(0.2, 0.5 * self.cfg.sample_interval)
         prev, new_prev = self._proc_prev, {}
         usage: dict[str, list[dict]] = {}
+        drm: dict[str, dict[int, dict]] | None = None
         for d in snap.get("devices") or []:
             u = d.get("uuid")
             per: dict[tuple[str, str], dict] = {}
-            for p in d.get("processes") or []:
+            procs = [p for p in d.get("processes") or [] if int(p.get("pid") or 0) > 0]
+            # amdsmi names processes by the kernel's (host) PID. With the agent in the host PID
+            # namespace (hostPID, as deployed) they are all visible here; otherwise (a container
+            # with its own PID namespace) the GPU's processes are read from the DRM fdinfo of
+            # this namespace's processes instead — under local PIDs, VRAM per GPU by BDF.
+            if any(not os.path.exists(f"/proc/{int(p['pid'])}") for p in procs):
+                if drm is None:
+                    drm = _scan_drm_clients()
+                local = drm.get(str(d.get("bdf", "")).lower(), {})
+                procs = [{"pid": pid, "vramBytes": x["vramBytes"], "gfxNs": x["engineNs"],
+                          "source": "drm-fdinfo"} for pid, x in sorted(local.items())]
+            for p in procs:
                 pid = int(p.get("pid") or 0)
-                if pid <= 0:
-                    continue
                 who = self._pod_of_pid(pid)
                 gfx = int(p.get("gfxNs") or 0)
                 busy = None
