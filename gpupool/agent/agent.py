@@ -177,6 +177,7 @@ class Agent:
         self._claiming: dict[str, int] = {}
         self._deferred: set[str] = set()
         self.gen_cv = threading.Condition()  # /v1/events long-polls wait here for a new gen
+        self.rpc = None                      # the RPC server (its per-path timings in /metrics)
         self.advertised: dict[str, set[str]] = {}
         self._adv_event = threading.Event()
         self.plugins: dict = {}
@@ -1047,7 +1048,10 @@ class Agent:
                     self.stats["probe_failures"] += 1
             # Probing -> Claimed may be lost by a crash (restart -> ProbeInterrupted -> replace)
             self.ledger.commit(self.records, durable=False)
-            self._evaluate_some([d["uuid"] for d in chosen])
+            if not self._is_default_policy(policy):
+                # under the default policy the claimed GPU's verdict (baseline = the claim's
+                # snapshot = now) is the free GPU's current one: nothing to re-evaluate
+                self._evaluate_some([d["uuid"] for d in chosen])
         self.ledger.flush(claim_seq)
         lap("commit2")
         self._ensure_plugin(resource)
@@ -1840,7 +1844,8 @@ def build_routes(agent: Agent) -> dict:
         return text_reply("ok\n")
 
     def metrics(q, body):
-        return text_reply(agent.metrics_text())
+        extra = agent.rpc.metrics_lines() if agent.rpc is not None else []
+        return text_reply(agent.metrics_text() + "\n".join(extra) + ("\n" if extra else ""))
 
     return {("GET", "/v1/node"): node, ("POST", "/v1/claims"): claims,
             ("POST", "/v1/cordon"): cordon, ("POST", "/v1/release"): release,
@@ -1854,6 +1859,7 @@ def serve(agent: Agent, ready_file: str | None = None) -> None:
     """Start the RPC listeners and the agent's background loops; block until interrupted."""
     from .rpc import RpcServer
     srv = RpcServer(build_routes(agent), agent.cfg.auth_token)
+    agent.rpc = srv
     if agent.cfg.socket:
         srv.listen_unix(agent.cfg.socket)
     if agent.cfg.listen:

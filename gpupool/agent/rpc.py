@@ -18,6 +18,7 @@ import os
 import socket
 import ssl
 import threading
+import time
 import urllib.parse
 from typing import Callable
 
@@ -47,6 +48,8 @@ class RpcServer:
         self._listeners: list[socket.socket] = []
         self._stop = threading.Event()
         self.requests = 0
+        self.stats: dict[str, list] = {}  # path -> [count, seconds]
+        self._stats_mu = threading.Lock()
 
     # ------------------------------------------------------------ listeners
     def listen_unix(self, path: str) -> None:
@@ -121,8 +124,10 @@ class RpcServer:
                 body = rf.read(n) if n else b""
                 keep = headers.get("connection", "").lower() != "close" and \
                     not version.strip().upper().endswith("1.0")
+                t0 = time.perf_counter()
                 reply = self._dispatch(method.upper(), target, headers, body)
                 self._send(conn, reply, keep)
+                self._account(target.partition("?")[0], time.perf_counter() - t0)
                 if reply[3] is not None:
                     try:
                         reply[3]()
@@ -137,6 +142,23 @@ class RpcServer:
                 conn.close()
             except OSError:
                 pass
+
+    def _account(self, path: str, seconds: float) -> None:
+        with self._stats_mu:
+            st = self.stats.setdefault(path, [0, 0.0])
+            st[0] += 1
+            st[1] += seconds
+
+    def metrics_lines(self) -> list[str]:
+        """Server-side time per RPC path, request parsed -> reply written (``rpc_seconds``); the
+        manager's span for the same call minus this is transport + framing."""
+        with self._stats_mu:
+            items = sorted(self.stats.items())
+        out = []
+        for path, (n, sec) in items:
+            out.append(f'gpupool_agent_rpc_requests_total{{path="{path}"}} {n}')
+            out.append(f'gpupool_agent_rpc_seconds_sum{{path="{path}"}} {sec:.6f}')
+        return out
 
     def _dispatch(self, method: str, target: str, headers: dict, body: bytes) -> tuple:
         path, _, qs = target.partition("?")

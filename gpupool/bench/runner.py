@@ -486,6 +486,13 @@ class BenchRun:
             out["health_poll_ms_avg"] = round(st["health_poll_ms_sum"] / st["health_polls"], 3)
         if st.get("samples"):
             out["sample_ms_avg"] = round(st["sample_ms_sum"] / st["samples"], 3)
+        # the agent's own time per claim RPC (request parsed -> reply written): the manager's
+        # "agent:POST /v1/claims" span minus this is socket transport + the manager's side
+        import re
+        m = re.search(r'gpupool_agent_rpc_requests_total\{path="/v1/claims"\} (\d+)', str(text))
+        ms = re.search(r'gpupool_agent_rpc_seconds_sum\{path="/v1/claims"\} ([0-9.]+)', str(text))
+        if m and ms and int(m.group(1)):
+            out["claim_rpc_server_ms_avg"] = round(float(ms.group(1)) * 1e3 / int(m.group(1)), 3)
         return out
 
     def health(self, pool: dict, steps: int) -> dict:

@@ -42,8 +42,14 @@ def test_shared_gpus_hold_k_pods_each_and_drain_per_gpu(cluster_factory):
         slot = k.get(PODS, f"s{i}", "default")["metadata"]["annotations"]["gpupool.amd.com/devices"]
         by_gpu.setdefault(gpu_of(slot), []).append(f"s{i}")
     assert sorted(len(v) for v in by_gpu.values()) == [4, 4] and set(by_gpu) == set(gpus)
-    # the agent sees every slot's pod on its GPU
-    view = {d["uuid"]: d for d in c.agent_request("mi355x-node-0", "GET", "/v1/node")["devices"]}
+    # the agent sees every slot's pod on its GPU (its PodResources map refreshes asynchronously)
+    import time
+    deadline = time.monotonic() + 10
+    while True:
+        view = {d["uuid"]: d for d in c.agent_request("mi355x-node-0", "GET", "/v1/node")["devices"]}
+        if all(len(view[u]["pods"]) == 4 for u in gpus) or time.monotonic() > deadline:
+            break
+        time.sleep(0.05)
     assert all(len(view[u]["pods"]) == 4 for u in gpus)
 
     # scale 2 -> 1: the victim (highest index) GPU's four pods are evicted, the other four stay
