@@ -508,19 +508,28 @@ class BenchRun:
         faulted = (lambda o: cond(o, "HBMECCHealthy") == "False" and cond(o, "Degraded") == "True")
         cleared = (lambda o: cond(o, "HBMECCHealthy") == "True" and ready_at(1)(o))
         out: dict[str, list[float]] = {"detect": [], "event": [], "react": [], "recover": []}
+        checks = []  # readyReplicas vs the independent truth after every fault and every clear
+        base = self._state_now()
+
+        def check(overlay: dict, o: dict) -> None:
+            cur = gt.apply_overlay(base, overlay)
+            truth = int(gt.device_healthy(cur.get(victim, {"present": False}),
+                                          base.get(victim), o["spec"])[0])
+            checks.append(truth == (o.get("status") or {}).get("readyReplicas"))
         for i in range(steps):
             for key, forced, notify in (("detect", False, False), ("event", False, True),
                                         ("react", True, False)):
                 t0 = time.perf_counter()
-                self.cluster.set_faults(self.node.name,
-                                        {"devices": {victim: {"ecc": {"uncorrectable": 1 + i}}}},
-                                        sample=forced, notify=notify)
-                self.c.wait_for(MI355XPOOLS, name, self.ns, faulted, timeout=self._to())
+                fault = {"devices": {victim: {"ecc": {"uncorrectable": 1 + i}}}}
+                self.cluster.set_faults(self.node.name, fault, sample=forced, notify=notify)
+                o = self.c.wait_for(MI355XPOOLS, name, self.ns, faulted, timeout=self._to())
                 out[key].append(time.perf_counter() - t0)
+                check(fault, o)
                 t0 = time.perf_counter()
                 self.cluster.set_faults(self.node.name, {}, sample=True)
-                self.c.wait_for(MI355XPOOLS, name, self.ns, cleared, timeout=self._to())
+                o = self.c.wait_for(MI355XPOOLS, name, self.ns, cleared, timeout=self._to())
                 out["recover"].append(time.perf_counter() - t0)
+                check({}, o)
         self.c.patch(MI355XPOOLS, name, {"spec": {"replicas": 0, "replacePolicy": "Replace"}},
                      self.ns)
         self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(0), timeout=self._to())
@@ -536,5 +545,9 @@ class BenchRun:
             # reaction only: a forced agent sample, then long-poll -> reconcile -> status
             "forced_sample_to_condition_p50_s": summary(out["react"])["p50_s"],
             "fault_cleared_to_ready_p50_s": summary(out["recover"])["p50_s"],
+            # readyReplicas == independent truth (device state + injected overlay, pool policy)
+            # once the condition reported the fault / the clear
+            "readyReplicas_accuracy": sum(checks) / len(checks) if checks else None,
+            "accuracy_samples": len(checks),
             "steps": steps,
         }

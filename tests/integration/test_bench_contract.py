@@ -49,6 +49,7 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
     for k in ("fault_to_condition_p50_s", "forced_sample_to_condition_p50_s",
               "fault_cleared_to_ready_p50_s"):
         assert h[k] is not None and h[k] < 30
+    assert h["readyReplicas_accuracy"] == 1.0 and h["accuracy_samples"] == 6
     # readyReplicas against the independent truth after every random fault / clear step
     af = cfg["accuracy_under_faults"]
     assert af["samples"] == 20 and af["accuracy"] == 1.0, af["mismatches"]
