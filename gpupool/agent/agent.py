@@ -19,8 +19,10 @@ import json
 import logging
 import os
 import socket
+import struct
 import threading
 import time
+from uuid import uuid4
 from dataclasses import dataclass, field
 from typing import Any
 
@@ -1538,6 +1540,47 @@ class Agent:
                     "annotations": {schema.ANN_POD_DEVICES: ",".join(ids)}}
 
     SHARE_LIB_DIR = "/opt/gpupool/lib"  # where the pod sees libgpupool_share.so
+    SHARE_ACCOUNT_PATH = "/var/run/gpupool/share.acct"  # where it sees its pod's HBM account
+    # the account file libgpupool_share.so maps (native/src/share/share.cc, struct Account)
+    _ACCT_BYTES, _ACCT_IDS_AT = 16384, 8192
+
+    def _share_account(self, slots: list[str], limit: int, ngpus: int) -> str | None:
+        """One HBM account per allocation, shared by every process of the container: 16 KiB,
+        magic + per-GPU limit, zeroed counters, the slot ids as text at 8 KiB. A slot belongs to
+        one container at a time, so an earlier account naming any of these slots belongs to a
+        container that is gone: it is deleted here. Returns the host path (None if the state
+        directory is not writable: the budget is then per process)."""
+        d = os.path.join(self.cfg.state_dir, "share")
+        mine = set(slots)
+        try:
+            os.makedirs(d, exist_ok=True)
+            for name in os.listdir(d):
+                if not name.endswith(".acct"):
+                    continue
+                path = os.path.join(d, name)
+                try:
+                    with open(path, "rb") as f:
+                        f.seek(self._ACCT_IDS_AT)
+                        ids = f.read().split(b"\0", 1)[0].decode(errors="replace").split(",")
+                except OSError:
+                    continue
+                if mine & set(ids):
+                    os.unlink(path)
+            buf = bytearray(self._ACCT_BYTES)
+            buf[0:24] = b"GPSHARE1" + struct.pack("<QII", int(limit), 1, int(ngpus))
+            text = ",".join(slots).encode()[: self._ACCT_BYTES - self._ACCT_IDS_AT - 1]
+            buf[self._ACCT_IDS_AT:self._ACCT_IDS_AT + len(text)] = text
+            path = os.path.join(d, f"{uuid4().hex}.acct")
+            fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o666)
+            try:
+                os.write(fd, bytes(buf))
+                os.fchmod(fd, 0o666)  # pods may run as any user
+            finally:
+                os.close(fd)
+            return path
+        except OSError as e:
+            log.warning("HBM account for %s not created (%s): budget is per process", slots, e)
+            return None
 
     def _isolation_env(self, slots: list[str], mounts: list[dict]) -> dict[str, str]:
         """spec.sharing.hbmBytesPerSlot / cuPerSlot of the pool owning these slots: the ROCm
@@ -1573,6 +1616,11 @@ class Agent:
         env = {"HSA_TOOLS_LIB": f"{self.SHARE_LIB_DIR}/libgpupool_share.so"}
         if hbm:
             env["GPUPOOL_HBM_LIMIT_BYTES"] = str(hbm)
+            acct = self._share_account(slots, hbm, len(per_gpu))
+            if acct:
+                mounts.append({"container_path": self.SHARE_ACCOUNT_PATH, "host_path": acct,
+                               "read_only": False})
+                env["GPUPOOL_SHARE_ACCOUNT"] = self.SHARE_ACCOUNT_PATH
         if cu_mask:
             env["GPUPOOL_CU_MASK"] = _ranges(sorted(cu_mask))
         return env

@@ -9,7 +9,7 @@
 //
 //   * HBM budget (GPUPOOL_HBM_LIMIT_BYTES, per GPU): hsa_amd_memory_pool_allocate and
 //     hsa_amd_vmem_handle_create on a GPU-located pool fail with OUT_OF_RESOURCES once the
-//     process's live VRAM on that GPU would exceed the budget (HIP reports hipErrorOutOfMemory);
+//     pod's live VRAM on that GPU would exceed the budget (HIP reports hipErrorOutOfMemory);
 //     hsa_amd_memory_pool_free / hsa_amd_vmem_handle_release return the bytes. The pool SIZE and
 //     the agent's MEMORY_AVAIL report the budget, so hipMemGetInfo / torch.cuda.mem_get_info and
 //     the caching allocators that size themselves from it see the slot, not the whole GPU.
@@ -18,15 +18,26 @@
 //     hipExtStreamCreateWithCUMask mask is intersected with it — waves of this process can only
 //     be dispatched to the slot's CUs.
 //
-// Budgets are per process (a pod's rank on its slot); the agent gives sibling slots disjoint CU
-// ranges and budgets that sum to at most the GPU's HBM.
+// The budget covers every process of the container: the agent creates one account file per
+// allocation (GPUPOOL_SHARE_ACCOUNT, mounted into the container) and every process charges its
+// VRAM there with atomic compare-and-swap on the shared page, so a pod running 4 ranks or a
+// DataLoader's worker processes on its slot still gets (slots x hbmBytesPerSlot) in total, not
+// per process. Each process also records what it holds in its own entry (pid + start time), and
+// a process that finds the budget exhausted first returns the bytes of entries whose process is
+// gone (killed by OOM, SIGKILL — no free ever ran). Without the file the budget is per process.
+// The agent gives sibling slots disjoint CU ranges and budgets that sum to at most the GPU's HBM.
 #define AMD_INTERNAL_BUILD  // hsa_api_trace.h: include the sibling headers of /opt/rocm/include/hsa
+#include <fcntl.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_api_trace.h>
 #include <hsa/hsa_ext_amd.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -39,6 +50,31 @@
 
 namespace {
 
+// ---- the shared account file (written by the agent, gpupool/agent/agent.py _share_account) ----
+// [0,64) header, [64,128) live bytes per GPU ordinal, [128,8192) per-process entries,
+// [8192,16384) the allocation's slot ids as text (the agent's bookkeeping; ignored here).
+constexpr size_t kAcctBytes = 16384;
+constexpr int kAcctGpus = 8;
+constexpr int kAcctEntries = (8192 - 128) / 32;
+constexpr char kAcctMagic[8] = {'G', 'P', 'S', 'H', 'A', 'R', 'E', '1'};
+
+struct AcctEntry {
+  int32_t pid;     // 0 free, -1 being claimed or reclaimed, else the owning process
+  uint32_t gpu;    // GPU ordinal among the process's visible GPU agents
+  uint64_t start;  // the owner's start time (/proc/<pid>/stat field 22): pid reuse is not a match
+  uint64_t bytes;  // live bytes the owner holds on ``gpu``
+  uint64_t pad;
+};
+struct Account {
+  char magic[8];
+  uint64_t limit;  // bytes per GPU (the agent writes GPUPOOL_HBM_LIMIT_BYTES here too)
+  uint32_t version, ngpus;
+  uint64_t pad[5];
+  uint64_t used[kAcctGpus];
+  AcctEntry entries[kAcctEntries];
+};
+static_assert(sizeof(Account) == 8192, "account layout");
+
 struct State {
   std::mutex mu;
   CoreApiTable real_core{};
@@ -49,15 +85,134 @@ struct State {
   bool debug = false;
   bool pools_mapped = false;
   std::map<uint64_t, uint64_t> pool_agent;  // GPU-located pool handle -> agent handle
-  std::map<uint64_t, uint64_t> used;        // agent handle -> live bytes
+  std::map<uint64_t, uint64_t> used;        // agent handle -> live bytes (this process)
+  std::map<uint64_t, uint32_t> ordinal;     // agent handle -> GPU ordinal (account index)
   std::unordered_map<void*, std::pair<uint64_t, uint64_t>> ptrs;       // ptr -> (agent, bytes)
   std::unordered_map<uint64_t, std::pair<uint64_t, uint64_t>> vmem;    // handle -> (agent, bytes)
-  std::atomic<uint64_t> denied{0}, queues_masked{0}, peak{0};
+  std::atomic<uint64_t> denied{0}, queues_masked{0}, peak{0}, reclaimed{0};
+  Account* acct = nullptr;                  // shared account; null = per-process budget
+  int32_t me = 0;                           // pid the entries below belong to (fork changes it)
+  uint64_t me_start = 0;
+  AcctEntry* mine[kAcctGpus] = {};
 };
 
 State& st() {
   static State* s = new State();  // never destroyed: HSA may call in during process exit
   return *s;
+}
+
+// /proc/<pid>/stat field 22 (start time in clock ticks); 0 when unreadable.
+uint64_t proc_start(int32_t pid) {
+  char path[64];
+  std::snprintf(path, sizeof path, "/proc/%d/stat", pid);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return 0;
+  char buf[1024];
+  size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  const char* p = std::strrchr(buf, ')');  // comm may hold spaces: fields restart after ')'
+  if (!p) return 0;
+  int field = 2;
+  for (++p; *p && field < 22; ++p)
+    if (*p == ' ') ++field;
+  return std::strtoull(p, nullptr, 10);
+}
+
+bool proc_alive(int32_t pid, uint64_t start) {
+  if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+  uint64_t now = proc_start(pid);
+  return now == 0 || start == 0 || now == start;  // unreadable: assume alive (never over-return)
+}
+
+void sat_sub(uint64_t* v, uint64_t n) {
+  uint64_t cur = __atomic_load_n(v, __ATOMIC_ACQUIRE);
+  while (!__atomic_compare_exchange_n(v, &cur, cur > n ? cur - n : 0, true, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {}
+}
+
+// Return the bytes of entries whose process is gone. Returns the bytes reclaimed.
+uint64_t acct_reclaim(Account* a) {
+  uint64_t total = 0;
+  for (AcctEntry& e : a->entries) {
+    int32_t pid = __atomic_load_n(&e.pid, __ATOMIC_ACQUIRE);
+    if (pid <= 0 || proc_alive(pid, __atomic_load_n(&e.start, __ATOMIC_ACQUIRE))) continue;
+    if (!__atomic_compare_exchange_n(&e.pid, &pid, -1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
+      continue;  // another process is reclaiming it
+    uint64_t b = __atomic_exchange_n(&e.bytes, 0, __ATOMIC_ACQ_REL);
+    if (e.gpu < kAcctGpus) sat_sub(&a->used[e.gpu], b);
+    total += b;
+    __atomic_store_n(&e.pid, 0, __ATOMIC_RELEASE);
+  }
+  return total;
+}
+
+// This process's entry for GPU ordinal g (claimed on first use). Caller holds s.mu.
+AcctEntry* acct_entry(State& s, uint32_t g) {
+  int32_t pid = static_cast<int32_t>(getpid());
+  if (pid != s.me) {  // first call, or a forked child: it holds nothing of the parent's entries
+    s.me = pid;
+    s.me_start = proc_start(pid);
+    std::fill(std::begin(s.mine), std::end(s.mine), nullptr);
+  }
+  if (s.mine[g]) return s.mine[g];
+  for (int pass = 0; pass < 2; ++pass) {
+    for (AcctEntry& e : s.acct->entries) {
+      int32_t free_pid = 0;
+      if (!__atomic_compare_exchange_n(&e.pid, &free_pid, -1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
+        continue;
+      e.gpu = g;
+      __atomic_store_n(&e.start, s.me_start, __ATOMIC_RELEASE);
+      __atomic_store_n(&e.bytes, 0, __ATOMIC_RELEASE);
+      __atomic_store_n(&e.pid, pid, __ATOMIC_RELEASE);
+      return s.mine[g] = &e;
+    }
+    s.reclaimed.fetch_add(acct_reclaim(s.acct));  // table full: free the dead processes' entries
+  }
+  return nullptr;  // still full: charge the GPU total only
+}
+
+// Reserve ``size`` on GPU ordinal g in the shared account. Caller holds s.mu.
+bool acct_charge(State& s, uint32_t g, uint64_t size) {
+  uint64_t* used = &s.acct->used[g];
+  bool swept = false;
+  uint64_t cur = __atomic_load_n(used, __ATOMIC_ACQUIRE);
+  for (;;) {
+    if (cur + size > s.limit) {
+      if (swept) return false;
+      swept = true;  // over budget: first give back what dead processes of the pod still hold
+      s.reclaimed.fetch_add(acct_reclaim(s.acct));
+      cur = __atomic_load_n(used, __ATOMIC_ACQUIRE);
+      continue;
+    }
+    if (__atomic_compare_exchange_n(used, &cur, cur + size, true, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) break;
+  }
+  // total first, own entry second: a crash in between leaks ``size`` until the file is replaced
+  // but never lets a reclaim return bytes the total does not hold
+  if (AcctEntry* e = acct_entry(s, g)) __atomic_add_fetch(&e->bytes, size, __ATOMIC_ACQ_REL);
+  return true;
+}
+
+void acct_release(State& s, uint32_t g, uint64_t size) {
+  if (AcctEntry* e = acct_entry(s, g)) sat_sub(&e->bytes, size);
+  sat_sub(&s.acct->used[g], size);
+}
+
+Account* acct_open(const char* path, bool debug) {
+  if (!path || !*path) return nullptr;
+  int fd = open(path, O_RDWR | O_CLOEXEC);
+  if (fd < 0) {
+    if (debug) std::fprintf(stderr, "[gpupool-share] account %s: %s\n", path, std::strerror(errno));
+    return nullptr;
+  }
+  void* m = mmap(nullptr, kAcctBytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) return nullptr;
+  auto* a = static_cast<Account*>(m);
+  if (std::memcmp(a->magic, kAcctMagic, sizeof kAcctMagic) != 0) {
+    munmap(m, kAcctBytes);
+    return nullptr;
+  }
+  return a;
 }
 
 uint64_t parse_bytes(const char* v) {
@@ -118,6 +273,7 @@ hsa_status_t collect_agent(hsa_agent_t agent, void*) {
     return HSA_STATUS_SUCCESS;
   uint64_t h = agent.handle;
   s.used.emplace(h, 0);
+  s.ordinal.emplace(h, static_cast<uint32_t>(s.ordinal.size()));  // ROCr's enumeration order
   if (s.real_amd.hsa_amd_agent_iterate_memory_pools_fn)
     s.real_amd.hsa_amd_agent_iterate_memory_pools_fn(agent, collect_pool, &h);
   return HSA_STATUS_SUCCESS;
@@ -135,20 +291,47 @@ uint64_t agent_of(hsa_amd_memory_pool_t pool) {
 }
 
 // Reserve ``size`` bytes on the pool's GPU; false when over budget. Caller holds s.mu.
+// The account slot of ``agent``: its ordinal when the shared account covers it, else -1.
+int shared_index(State& s, uint64_t agent) {
+  if (!s.acct) return -1;
+  auto it = s.ordinal.find(agent);
+  return it != s.ordinal.end() && it->second < kAcctGpus ? static_cast<int>(it->second) : -1;
+}
+
+// Live bytes against the budget on ``agent``: the pod's total when shared. Caller holds s.mu.
+uint64_t budget_used(State& s, uint64_t agent) {
+  int g = shared_index(s, agent);
+  if (g >= 0) return __atomic_load_n(&s.acct->used[g], __ATOMIC_ACQUIRE);
+  auto it = s.used.find(agent);
+  return it == s.used.end() ? 0 : it->second;
+}
+
 bool charge(uint64_t agent, size_t size) {
   State& s = st();
   uint64_t& u = s.used[agent];
-  if (s.limit && u + size > s.limit) {
+  int g = shared_index(s, agent);
+  bool ok = g >= 0 ? acct_charge(s, static_cast<uint32_t>(g), size) : !(s.limit && u + size > s.limit);
+  if (!ok) {
     s.denied.fetch_add(1);
     if (s.debug)
-      std::fprintf(stderr, "[gpupool-share] deny %zu B: %llu in use of %llu\n", size,
-                   static_cast<unsigned long long>(u), static_cast<unsigned long long>(s.limit));
+      std::fprintf(stderr, "[gpupool-share] deny %zu B: %llu in use of %llu%s\n", size,
+                   static_cast<unsigned long long>(budget_used(s, agent)),
+                   static_cast<unsigned long long>(s.limit), g >= 0 ? " (pod total)" : "");
     return false;
   }
   u += size;
   uint64_t pk = s.peak.load();
   while (u > pk && !s.peak.compare_exchange_weak(pk, u)) {}
   return true;
+}
+
+// Return ``size`` bytes on ``agent``. Caller holds s.mu.
+void uncharge(uint64_t agent, uint64_t size) {
+  State& s = st();
+  uint64_t& u = s.used[agent];
+  u = u > size ? u - size : 0;
+  int g = shared_index(s, agent);
+  if (g >= 0) acct_release(s, static_cast<uint32_t>(g), size);
 }
 
 hsa_status_t w_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr) {
@@ -163,7 +346,7 @@ hsa_status_t w_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t f
   std::lock_guard<std::mutex> g(s.mu);
   if (!agent) return r;
   if (r == HSA_STATUS_SUCCESS && ptr && *ptr) s.ptrs[*ptr] = {agent, size};
-  else s.used[agent] -= size;
+  else uncharge(agent, size);
   return r;
 }
 
@@ -173,7 +356,7 @@ hsa_status_t w_pool_free(void* ptr) {
     std::lock_guard<std::mutex> g(s.mu);
     auto it = s.ptrs.find(ptr);
     if (it != s.ptrs.end()) {
-      s.used[it->second.first] -= it->second.second;
+      uncharge(it->second.first, it->second.second);
       s.ptrs.erase(it);
     }
   }
@@ -193,7 +376,7 @@ hsa_status_t w_vmem_create(hsa_amd_memory_pool_t pool, size_t size, hsa_amd_memo
   std::lock_guard<std::mutex> g(s.mu);
   if (!agent) return r;
   if (r == HSA_STATUS_SUCCESS && handle) s.vmem[handle->handle] = {agent, size};
-  else s.used[agent] -= size;
+  else uncharge(agent, size);
   return r;
 }
 
@@ -203,7 +386,7 @@ hsa_status_t w_vmem_release(hsa_amd_vmem_alloc_handle_t handle) {
     std::lock_guard<std::mutex> g(s.mu);
     auto it = s.vmem.find(handle.handle);
     if (it != s.vmem.end()) {
-      s.used[it->second.first] -= it->second.second;
+      uncharge(it->second.first, it->second.second);
       s.vmem.erase(it);
     }
   }
@@ -229,10 +412,10 @@ hsa_status_t w_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* va
       static_cast<int>(attr) != static_cast<int>(HSA_AMD_AGENT_INFO_MEMORY_AVAIL))
     return r;
   std::lock_guard<std::mutex> g(s.mu);
-  auto it = s.used.find(agent.handle);
-  if (it != s.used.end()) {
+  if (s.used.count(agent.handle)) {
     uint64_t* avail = static_cast<uint64_t*>(value);
-    uint64_t left = s.limit > it->second ? s.limit - it->second : 0;
+    uint64_t u = budget_used(s, agent.handle);  // with a shared account: what the whole pod holds
+    uint64_t left = s.limit > u ? s.limit - u : 0;
     *avail = std::min(*avail, left);
   }
   return r;
@@ -288,6 +471,8 @@ __attribute__((visibility("default"))) bool OnLoad(HsaApiTable* table, uint64_t 
   s.mask = parse_mask(std::getenv("GPUPOOL_CU_MASK"), &s.mask_bits);
   const char* dbg = std::getenv("GPUPOOL_SHARE_DEBUG");
   s.debug = dbg && *dbg && *dbg != '0';
+  s.acct = acct_open(std::getenv("GPUPOOL_SHARE_ACCOUNT"), s.debug);
+  if (s.acct && s.acct->limit) s.limit = s.acct->limit;  // the agent's number wins
   if (s.limit) {
     table->amd_ext_->hsa_amd_memory_pool_allocate_fn = w_pool_allocate;
     table->amd_ext_->hsa_amd_memory_pool_free_fn = w_pool_free;
@@ -301,8 +486,8 @@ __attribute__((visibility("default"))) bool OnLoad(HsaApiTable* table, uint64_t 
     table->amd_ext_->hsa_amd_queue_cu_set_mask_fn = w_queue_cu_set_mask;
   }
   if (s.debug)
-    std::fprintf(stderr, "[gpupool-share] loaded: HBM limit %llu B per GPU, CU mask %u bits\n",
-                 static_cast<unsigned long long>(s.limit), s.mask_bits);
+    std::fprintf(stderr, "[gpupool-share] loaded: HBM limit %llu B per GPU (%s), CU mask %u bits\n",
+                 static_cast<unsigned long long>(s.limit), s.acct ? "pod total" : "per process", s.mask_bits);
   return true;
 }
 
@@ -312,15 +497,19 @@ __attribute__((visibility("default"))) void OnUnload() {}
 __attribute__((visibility("default"))) int gpupool_share_stats(char* buf, int len) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
-  uint64_t used = 0;
-  for (const auto& kv : s.used) used = std::max(used, kv.second);
+  uint64_t used = 0, shared = 0;
+  for (const auto& kv : s.used) {
+    used = std::max(used, kv.second);
+    if (shared_index(s, kv.first) >= 0) shared = std::max(shared, budget_used(s, kv.first));
+  }
   return std::snprintf(buf, static_cast<size_t>(len),
                        "{\"limit\":%llu,\"used\":%llu,\"peak\":%llu,\"denied\":%llu,\"queuesMasked\":%llu,"
-                       "\"maskBits\":%u}",
+                       "\"maskBits\":%u,\"shared\":%d,\"podUsed\":%llu,\"reclaimed\":%llu}",
                        static_cast<unsigned long long>(s.limit), static_cast<unsigned long long>(used),
                        static_cast<unsigned long long>(s.peak.load()),
                        static_cast<unsigned long long>(s.denied.load()),
-                       static_cast<unsigned long long>(s.queues_masked.load()), s.mask_bits);
+                       static_cast<unsigned long long>(s.queues_masked.load()), s.mask_bits, s.acct ? 1 : 0,
+                       static_cast<unsigned long long>(shared), static_cast<unsigned long long>(s.reclaimed.load()));
 }
 
 }  // extern "C"

@@ -4,12 +4,15 @@
 // masks on new GPU queues and intersected with the application's own.
 #define AMD_INTERNAL_BUILD
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_api_trace.h>
 #include <hsa/hsa_ext_amd.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <climits>
+#include <cstring>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -87,6 +90,60 @@ std::string share_lib() {
   ssize_t n = readlink("/proc/self/exe", buf, sizeof buf - 1);
   std::string exe(buf, n > 0 ? static_cast<size_t>(n) : 0);
   return exe.substr(0, exe.rfind('/')) + "/libgpupool_share.so";
+}
+
+struct Fake {
+  CoreApiTable core{};
+  AmdExtTable amd{};
+  HsaApiTable table{};
+  Fake() {
+    core.hsa_iterate_agents_fn = f_iterate_agents;
+    core.hsa_agent_get_info_fn = f_agent_get_info;
+    core.hsa_queue_create_fn = f_queue_create;
+    amd.hsa_amd_agent_iterate_memory_pools_fn = f_iterate_pools;
+    amd.hsa_amd_memory_pool_get_info_fn = f_pool_get_info;
+    amd.hsa_amd_memory_pool_allocate_fn = f_allocate;
+    amd.hsa_amd_memory_pool_free_fn = f_free;
+    amd.hsa_amd_vmem_handle_create_fn = f_vmem_create;
+    amd.hsa_amd_vmem_handle_release_fn = f_vmem_release;
+    amd.hsa_amd_queue_cu_set_mask_fn = f_cu_set_mask;
+    table.core_ = &core;
+    table.amd_ext_ = &amd;
+  }
+};
+
+// A private copy of the library: dlopen of the same path would return the instance (and the
+// process-wide state) an earlier test already initialised.
+void* load_copy(const std::string& dst) {
+  std::string cmd = "cp '" + share_lib() + "' '" + dst + "'";
+  if (std::system(cmd.c_str()) != 0) return nullptr;
+  return dlopen(dst.c_str(), RTLD_NOW | RTLD_LOCAL);
+}
+
+// The account file the agent writes (gpupool/agent/agent.py _share_account): 16 KiB, magic,
+// limit per GPU; everything else zero.
+std::string make_account(uint64_t limit) {
+  std::string path = "/tmp/gpupool-share-test-" + std::to_string(getpid()) + ".acct";
+  std::vector<char> buf(16384, 0);
+  std::memcpy(buf.data(), "GPSHARE1", 8);
+  std::memcpy(buf.data() + 8, &limit, 8);
+  uint32_t ver = 1, ngpus = 1;
+  std::memcpy(buf.data() + 16, &ver, 4);
+  std::memcpy(buf.data() + 20, &ngpus, 4);
+  int fd = open(path.c_str(), O_CREAT | O_TRUNC | O_RDWR, 0600);
+  if (fd < 0 || write(fd, buf.data(), buf.size()) != static_cast<ssize_t>(buf.size())) path.clear();
+  if (fd >= 0) close(fd);
+  return path;
+}
+
+uint64_t account_used(const std::string& path) {
+  uint64_t v = 0;
+  int fd = open(path.c_str(), O_RDONLY);
+  if (fd >= 0) {
+    if (pread(fd, &v, 8, 64) != 8) v = ~0ull;
+    close(fd);
+  }
+  return v;
 }
 
 }  // namespace
@@ -169,4 +226,90 @@ TEST(share_lib_budget_and_cu_mask) {
   EXPECT_TRUE(js.find("\"maskBits\":160") != std::string::npos);
   unsetenv("GPUPOOL_HBM_LIMIT_BYTES");
   unsetenv("GPUPOOL_CU_MASK");
+}
+
+// GPUPOOL_SHARE_ACCOUNT: the budget is the pod's, over all its processes. A forked process charges
+// the same account; one that dies holding memory (no free ran) has its bytes returned by the next
+// process that finds the budget exhausted; a live process's bytes are never taken.
+TEST(share_lib_pod_account_across_processes) {
+  std::string acct = make_account(1024 * kMi);
+  EXPECT_TRUE(!acct.empty());
+  setenv("GPUPOOL_HBM_LIMIT_BYTES", "64Gi", 1);  // the account's limit wins
+  setenv("GPUPOOL_SHARE_ACCOUNT", acct.c_str(), 1);
+  std::string copy = "/tmp/libgpupool_share-test-" + std::to_string(getpid()) + ".so";
+  void* lib = load_copy(copy);
+  EXPECT_TRUE(lib != nullptr);
+  auto on_load = reinterpret_cast<bool (*)(HsaApiTable*, uint64_t, uint64_t, const char* const*)>(dlsym(lib, "OnLoad"));
+  auto stats = reinterpret_cast<int (*)(char*, int)>(dlsym(lib, "gpupool_share_stats"));
+  Fake f;
+  EXPECT_TRUE(on_load(&f.table, 0, 0, nullptr));
+  auto alloc = f.amd.hsa_amd_memory_pool_allocate_fn;
+  const hsa_amd_memory_pool_t gpu{kGpuPool};
+  void *a = nullptr, *b = nullptr;
+  EXPECT_EQ(alloc(gpu, 512 * kMi, 0, &a), HSA_STATUS_SUCCESS);
+  EXPECT_EQ(account_used(acct), static_cast<uint64_t>(512 * kMi));
+
+  // a second process of the pod: 384 MiB fits, 256 MiB more does not (pod total 1152 > 1024);
+  // it then dies without freeing
+  pid_t child = fork();
+  if (child == 0) {
+    void* p = nullptr;
+    int rc = alloc(gpu, 384 * kMi, 0, &p) == HSA_STATUS_SUCCESS ? 0 : 1;
+    if (alloc(gpu, 256 * kMi, 0, &p) != HSA_STATUS_ERROR_OUT_OF_RESOURCES) rc |= 2;
+    _exit(rc);
+  }
+  int status = 0;
+  waitpid(child, &status, 0);
+  EXPECT_EQ(WEXITSTATUS(status), 0);
+  EXPECT_EQ(account_used(acct), static_cast<uint64_t>(896 * kMi));
+  uint64_t avail = 0;
+  f.core.hsa_agent_get_info_fn(hsa_agent_t{kGpu}, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_MEMORY_AVAIL),
+                               &avail);
+  EXPECT_EQ(avail, static_cast<uint64_t>(128 * kMi));  // what the pod has left, not this process
+
+  // over budget -> the dead process's 384 MiB come back first
+  EXPECT_EQ(alloc(gpu, 256 * kMi, 0, &b), HSA_STATUS_SUCCESS);
+  EXPECT_EQ(account_used(acct), static_cast<uint64_t>(768 * kMi));
+
+  // a live sibling holding 200 MiB is not reclaimed
+  int go[2], done[2];
+  EXPECT_EQ(pipe(go), 0);
+  EXPECT_EQ(pipe(done), 0);
+  pid_t live = fork();
+  if (live == 0) {
+    close(go[0]);
+    close(done[1]);  // else the read below never sees EOF
+    alarm(20);       // never outlive a broken parent
+    void* p = nullptr;
+    char c = alloc(gpu, 200 * kMi, 0, &p) == HSA_STATUS_SUCCESS ? 'y' : 'n';
+    if (write(go[1], &c, 1) != 1) _exit(3);
+    if (read(done[0], &c, 1) < 0) _exit(4);  // hold until the parent says so (EOF)
+    _exit(0);
+  }
+  close(go[1]);
+  close(done[0]);
+  char c = 0;
+  EXPECT_EQ(read(go[0], &c, 1), 1);
+  EXPECT_EQ(c, 'y');
+  void* d = nullptr;
+  EXPECT_EQ(alloc(gpu, 100 * kMi, 0, &d), HSA_STATUS_ERROR_OUT_OF_RESOURCES);
+  close(done[1]);
+  waitpid(live, &status, 0);
+  EXPECT_EQ(alloc(gpu, 100 * kMi, 0, &d), HSA_STATUS_SUCCESS);  // its 200 MiB came back on exit
+  EXPECT_EQ(account_used(acct), static_cast<uint64_t>(868 * kMi));
+
+  // frees return bytes to the pod's account
+  EXPECT_EQ(f.amd.hsa_amd_memory_pool_free_fn(a), HSA_STATUS_SUCCESS);
+  EXPECT_EQ(account_used(acct), static_cast<uint64_t>(356 * kMi));
+  char buf[256];
+  stats(buf, sizeof buf);
+  std::string js(buf);
+  EXPECT_TRUE(js.find("\"shared\":1") != std::string::npos);
+  EXPECT_TRUE(js.find("\"limit\":1073741824") != std::string::npos);
+  EXPECT_TRUE(js.find("\"reclaimed\":" + std::to_string(584 * kMi)) != std::string::npos);
+  close(go[0]);
+  unlink(acct.c_str());
+  unlink(copy.c_str());
+  unsetenv("GPUPOOL_HBM_LIMIT_BYTES");
+  unsetenv("GPUPOOL_SHARE_ACCOUNT");
 }

@@ -46,9 +46,41 @@ print(json.dumps({"keys": r["cus"]["cuKeys"], "verified": r["cus"]["mfmaVerified
 """
 
 
+SECOND = r"""
+import json, sys, torch
+size = int(sys.argv[1])
+torch.zeros(1, device="cuda"); torch.cuda.synchronize()
+free, total = torch.cuda.mem_get_info(0)
+
+def attempt():
+    try:
+        b = torch.empty(size, dtype=torch.uint8, device="cuda"); b.fill_(3); torch.cuda.synchronize()
+        del b
+        torch.cuda.empty_cache()
+        return "ok"
+    except torch.OutOfMemoryError:
+        torch.cuda.empty_cache()
+        return "oom"
+
+print(json.dumps({"free": free, "total": total, "first": attempt()}), flush=True)
+sys.stdin.readline()
+print(json.dumps({"second": attempt()}), flush=True)
+"""
+
+
+def _account(path: str, limit: int) -> str:
+    """The agent's account file (gpupool/agent/agent.py _share_account)."""
+    buf = bytearray(16384)
+    buf[0:24] = b"GPSHARE1" + limit.to_bytes(8, "little") + (1).to_bytes(4, "little") + \
+        (1).to_bytes(4, "little")
+    with open(path, "wb") as f:
+        f.write(bytes(buf))
+    return path
+
+
 def _env(**kw) -> dict:
     env = dict(os.environ, PYTHONPATH=ROOT)
-    for k in ("HSA_TOOLS_LIB", "GPUPOOL_HBM_LIMIT_BYTES", "GPUPOOL_CU_MASK"):
+    for k in ("HSA_TOOLS_LIB", "GPUPOOL_HBM_LIMIT_BYTES", "GPUPOOL_CU_MASK", "GPUPOOL_SHARE_ACCOUNT"):
         env.pop(k, None)
     env.update({k: str(v) for k, v in kw.items()})
     return env
@@ -120,3 +152,40 @@ def test_cu_share_confines_waves_to_the_slot():
         for j in range(i + 1, 4):
             assert not (seen[i] & seen[j]), (i, j, sorted(seen[i] & seen[j])[:8])
     assert set().union(*seen) <= all_keys
+
+
+def test_hbm_budget_is_the_pods_across_its_processes(tmp_path):
+    """GPUPOOL_SHARE_ACCOUNT: two processes of one pod share its 8 GiB. Process A holds 6 GiB;
+    process B then sees at most 2 GiB free (mem_get_info) and a 4 GiB allocation fails. A is killed
+    with SIGKILL (no free runs); B's next 4 GiB allocation finds the budget exhausted, returns the
+    dead process's bytes to the account and succeeds."""
+    assert os.path.exists(LIB), "build the native targets first"
+    acct = _account(str(tmp_path / "pod.acct"), 8 * GiB)
+    env = _env(HSA_TOOLS_LIB=LIB, GPUPOOL_HBM_LIMIT_BYTES=8 * GiB, GPUPOOL_SHARE_ACCOUNT=acct)
+    a = subprocess.Popen([sys.executable, "-c", ALLOC, str(6 * GiB), str(1 << 20), "60"], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    b = None
+    try:
+        ra = _json(a)
+        assert ra["held"] == 6 * GiB and ra["extra"] == "ok", ra
+        used = int.from_bytes(open(acct, "rb").read()[64:72], "little")
+        assert 6 * GiB <= used < 7 * GiB, used
+        b = subprocess.Popen([sys.executable, "-c", SECOND, str(4 * GiB)], env=env, text=True,
+                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+        rb = _json(b)
+        print("pod account after A + B:", rb, "bytes", used)
+        # hipMemGetInfo in B reports what the pod has left, not what B holds
+        assert rb["total"] == 8 * GiB and rb["free"] <= 8 * GiB - used, (rb, used)
+        assert rb["first"] == "oom", rb
+        a.kill()
+        a.wait(timeout=30)
+        b.stdin.write("\n")
+        b.stdin.flush()
+        rb2 = _json(b)
+        assert rb2["second"] == "ok", rb2
+        b.wait(timeout=60)
+    finally:
+        for p in (a, b):
+            if p is not None and p.poll() is None:
+                p.kill()
+                p.wait(timeout=30)

@@ -137,25 +137,48 @@ def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_
     k.create(MI355XPOOLS, mi_pool("iso", 1, sharing={"replicasPerGPU": 4, "hbmBytesPerSlot": 8 << 30,
                                                      "cuPerSlot": 64}), "default")
     wait_ready(k, "iso", 1)
-    cmd = ["bash", "-c", "env | grep -E '^(HSA_TOOLS_LIB|GPUPOOL_CU_MASK|GPUPOOL_HBM_LIMIT_BYTES)=' "
-                         "| sort; sleep 600"]
-    for i in range(4):
-        pod = pause_pod(f"iso{i}")
+    cmd = ["bash", "-c", "env | grep -E '^(HSA_TOOLS_LIB|GPUPOOL_CU_MASK|GPUPOOL_HBM_LIMIT_BYTES|"
+                         "GPUPOOL_SHARE_ACCOUNT|GPUPOOL_GPU_SLOTS)=' | sort; sleep 600"]
+
+    def start(name: str) -> dict:
+        pod = pause_pod(name)
         pod["spec"]["containers"][0]["command"] = cmd
         k.create(PODS, pod, "default")
-    envs = []
-    for i in range(4):
-        p = k.wait_for(PODS, f"iso{i}", "default", running, timeout=30)
+
+    def env_of(name: str) -> dict:
+        p = k.wait_for(PODS, name, "default", running, timeout=30)
         path = p["metadata"]["annotations"]["gpupool.amd.com/log-path"]
         deadline = time.monotonic() + 10
-        while time.monotonic() < deadline and open(path).read().count("\n") < 3:
+        while time.monotonic() < deadline and open(path).read().count("\n") < 5:
             time.sleep(0.05)
-        envs.append(dict(line.split("=", 1) for line in open(path).read().split()))
+        return dict(line.split("=", 1) for line in open(path).read().split())
+
+    for i in range(4):
+        start(f"iso{i}")
+    envs = [env_of(f"iso{i}") for i in range(4)]
     masks = sorted(e["GPUPOOL_CU_MASK"] for e in envs)
     assert masks == ["0-63", "128-191", "192-255", "64-127"], masks
     assert all(e["GPUPOOL_HBM_LIMIT_BYTES"] == str(8 << 30) for e in envs)
     lib = envs[0]["HSA_TOOLS_LIB"]  # the container path, rewritten to the host path
     assert lib.endswith("/libgpupool_share.so") and os.path.exists(lib)
+    # one HBM account per container (shared by all its processes): the library's layout — magic,
+    # the per-GPU limit, zeroed counters, and the container's slot ids for the agent's cleanup
+    accts = [e["GPUPOOL_SHARE_ACCOUNT"] for e in envs]
+    assert len(set(accts)) == 4
+    for e, a in zip(envs, accts):
+        raw = open(a, "rb").read()
+        assert len(raw) == 16384 and raw[:8] == b"GPSHARE1", raw[:16]
+        assert int.from_bytes(raw[8:16], "little") == 8 << 30
+        assert not any(raw[64:8192])
+        assert raw[8192:].split(b"\0")[0].decode() == e["GPUPOOL_GPU_SLOTS"]
+    # the slot of a finished pod goes to a new pod: the old account is replaced, not reused
+    k.delete(PODS, "iso0", "default")
+    k.wait_for(PODS, "iso0", "default", lambda o: o is None, timeout=30)
+    start("iso4")
+    e4 = env_of("iso4")
+    assert e4["GPUPOOL_GPU_SLOTS"] == envs[0]["GPUPOOL_GPU_SLOTS"]
+    assert e4["GPUPOOL_SHARE_ACCOUNT"] != accts[0] and not os.path.exists(accts[0])
+    assert all(os.path.exists(a) for a in accts[1:] + [e4["GPUPOOL_SHARE_ACCOUNT"]])
     # a pool whose slots overrun the GPU's CUs is rejected at admission of the manager
     k.create(MI355XPOOLS, mi_pool("over", 1, sharing={"replicasPerGPU": 4, "cuPerSlot": 128}),
              "default")
