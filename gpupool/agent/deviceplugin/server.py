@@ -7,7 +7,11 @@ endpoint ``<plugin_dir>/gpupool-<resource>.sock`` registered with the kubelet:
 * ListAndWatch streams the pool-claimed GPUs for that resource: Healthy iff claimed, not draining,
   healthy under the owning pool's policy and probe-passed; a cordoned (draining) GPU turns
   Unhealthy so the kubelet places no new pods on it. Every send records which devices were
-  advertised Healthy — the agent's ``advertised`` bit that readyReplicas requires.
+  advertised Healthy — the agent's ``advertised`` bit that readyReplicas requires. The stream is
+  served in gRPC's non-blocking mode: the handler keeps the stream's send callback and returns,
+  and whoever changed the device list sends on it — a claim on its own thread (it writes the
+  update and sees it delivered without a hop through a stream thread), everything else through
+  the plugin's sender thread, so a sampler or health thread never blocks on the kubelet.
 * Allocate returns /dev/kfd + /dev/dri/renderD<N> DeviceSpecs and ``ROCR_VISIBLE_DEVICES`` set to
   the GPUs' ROCr UUIDs (``GPU-<serial>``), so a container sees exactly its GPUs.
 * GetPreferredAllocation picks xGMI/NUMA-close sets with libmi355x_dev's selector.
@@ -36,6 +40,16 @@ def socket_name(resource: str) -> str:
     return "gpupool-" + resource.replace("/", "_").replace(".", "-") + ".sock"
 
 
+class _Stream:
+    """One kubelet ListAndWatch stream: gRPC's send callback (blocks until the message is
+    written), the last version sent, and whether a thread is sending on it right now."""
+    __slots__ = ("send", "context", "sent", "busy", "alive")
+
+    def __init__(self, send, context):
+        self.send, self.context = send, context
+        self.sent, self.busy, self.alive = -1, False, True
+
+
 class DevicePluginServer:
     def __init__(self, agent: "Agent", resource: str, plugin_dir: str):
         self.agent = agent
@@ -50,6 +64,9 @@ class DevicePluginServer:
         self.registered = False
         self._kubelet_ino = None
         self._mon: threading.Thread | None = None
+        self._sender: threading.Thread | None = None
+        self._live: set[_Stream] = set()
+        self._wake = False  # the sender thread has work
         self._pending: tuple | None = None  # (version, ListAndWatchResponse, healthy uuids)
         self._mark_mu = threading.Lock()
         self._marked = -1
@@ -62,15 +79,22 @@ class DevicePluginServer:
             pass
         self.server = grpc.server(cf.ThreadPoolExecutor(max_workers=16,
                                                         thread_name_prefix=f"dp-{self.resource}"))
+
+        def list_and_watch(request, context, send):
+            return self.ListAndWatch(request, context, send)
+        list_and_watch.experimental_non_blocking = True  # handler gets gRPC's send callback
         self.server.add_generic_rpc_handlers((service_handler("v1beta1.DevicePlugin", {
             "GetDevicePluginOptions": self.GetDevicePluginOptions,
-            "ListAndWatch": self.ListAndWatch,
+            "ListAndWatch": list_and_watch,
             "GetPreferredAllocation": self.GetPreferredAllocation,
             "Allocate": self.Allocate,
             "PreStartContainer": self.PreStartContainer,
         }),))
         self.server.add_insecure_port(unix_target(self.sock))
         self.server.start()
+        self._sender = threading.Thread(target=self._send_loop, daemon=True,
+                                        name=f"dp-send-{self.resource}")
+        self._sender.start()
         self.register()  # synchronous first registration; the monitor handles kubelet restarts
         self._mon = threading.Thread(target=self._monitor_kubelet, daemon=True,
                                      name=f"dp-mon-{self.resource}")
@@ -79,7 +103,13 @@ class DevicePluginServer:
     def stop(self) -> None:
         self.stopped = True
         with self.cv:
+            live = list(self._live)
             self.cv.notify_all()
+        for st in live:  # end the streams with an OK status (the kubelet reconnects)
+            try:
+                st.send(None)
+            except Exception:
+                pass
         if self.server:
             self.server.stop(grace=0.5)
         try:
@@ -125,16 +155,68 @@ class DevicePluginServer:
             return None
         return (st.st_ino, st.st_ctime_ns)
 
-    def notify(self) -> None:
-        """Publish the current device list: built on the caller's thread (a claim, a health
-        change) and queued for every ListAndWatch stream, whose generator then only sends it.
-        A device counts as advertised once its stream has sent the message — not before: a pod
-        placed on a GPU the kubelet has not heard of yet would fail admission."""
+    def notify(self, sync: bool = False) -> None:
+        """Publish the current device list, built on the caller's thread. ``sync`` (the claim
+        path): send it on this thread to every stream no other thread is sending on, and return
+        once written — the caller then finds its GPUs advertised without waiting for another
+        thread. Otherwise the sender thread sends it. A device counts as advertised once a
+        stream has written the message — not before: a pod placed on a GPU the kubelet has not
+        heard of yet would fail admission."""
         resp, healthy = self._devices_msg()
         with self.cv:
             self.version += 1
             self._pending = (self.version, resp, healthy)
-            self.cv.notify_all()
+            live = list(self._live)
+            if not sync:
+                self._wake = True
+                self.cv.notify_all()
+        if sync:
+            for st in live:
+                self._drive(st)
+
+    def _drive(self, st: _Stream) -> None:
+        """Send the newest device list on ``st`` until it has sent the current version; returns
+        at once if another thread is sending on it (that thread re-checks the version before it
+        lets go, under the same lock notify() bumps it under, so no update is left unsent)."""
+        with self.cv:
+            if st.busy or not st.alive:
+                return
+            st.busy = True
+        try:
+            while True:
+                with self.cv:
+                    ver = self.version
+                    if st.sent >= ver or not st.alive or self.stopped:
+                        st.busy = False
+                        return
+                    pend = self._pending if self._pending and self._pending[0] == ver else None
+                if pend is None:  # first message of a new stream
+                    resp, healthy = self._devices_msg()
+                else:
+                    resp, healthy = pend[1], pend[2]
+                st.send(resp)  # returns once gRPC has written the message
+                st.sent = ver
+                if st.context.is_active():
+                    self._mark(ver, healthy)
+                else:
+                    st.alive = False
+        except BaseException:
+            with self.cv:
+                st.busy = False
+            raise
+
+    def _send_loop(self) -> None:
+        while not self.stopped:
+            with self.cv:
+                while not self._wake and not self.stopped:
+                    self.cv.wait(timeout=1.0)
+                self._wake = False
+                live = list(self._live)
+            for st in live:
+                try:
+                    self._drive(st)
+                except Exception:
+                    log.exception("ListAndWatch send failed")
 
     def _mark(self, version: int, healthy: set[str] | None) -> None:
         with self._mark_mu:  # versions only move forward: a late stream send never undoes a newer one
@@ -161,31 +243,25 @@ class DevicePluginServer:
                 healthy.add(d["uuid"])
         return resp, healthy
 
-    def ListAndWatch(self, request, context):
-        with self.cv:
-            self.streams += 1
-        try:
-            seen = -1
-            while not self.stopped and context.is_active():
-                with self.cv:
-                    if seen == self.version:
-                        self.cv.wait(timeout=1.0)
-                    if seen == self.version:
-                        continue
-                    seen = self.version
-                    pend = self._pending if self._pending and self._pending[0] == seen else None
-                if pend is None:  # first message of a new stream
-                    resp, healthy = self._devices_msg()
-                else:
-                    resp, healthy = pend[1], pend[2]
-                yield resp
-                # gRPC asks for the next message once this one is written: it is sent
-                # (a broken stream resets the bit in ``finally``)
-                self._mark(seen, healthy)
-        finally:
+    def ListAndWatch(self, request, context, send):
+        """Non-blocking handler: register the stream, send it the current list, return. The
+        stream stays open until the kubelet goes away or the plugin stops."""
+        st = _Stream(send, context)
+
+        def gone():
+            st.alive = False
             with self.cv:
-                self.streams -= 1
-            self._mark(self.version, None)
+                if st in self._live:
+                    self._live.discard(st)
+                    self.streams -= 1
+            self._mark(self.version, None)  # no stream left -> nothing counts as advertised
+        with self.cv:
+            self._live.add(st)
+            self.streams += 1
+        if not context.add_callback(gone):  # already terminated
+            gone()
+            return
+        self._drive(st)
 
     def GetPreferredAllocation(self, request, context):
         out = DP.PreferredAllocationResponse()

@@ -215,16 +215,19 @@ class Mi355xJobReconciler : public PoolReconcilerBase {
   // Tries to place the gang (under sched_mu_). Returns the placement, or empty with *why set. With
   // preemptionPolicy PreemptLowerPriority a placement may rely on GPUs of lower-priority running
   // jobs, returned in *victims (the smallest set found, lowest priority and newest first).
+  // ``pool_cap``: with a poolRef, the pool's ready device slots per node (status.devices Healthy
+  // and advertised x replicasPerGPU) — an upper bound on what the gang may take on each node, so a
+  // Node allocatable the kubelet has not lowered yet (the pool just shrank) is not trusted.
   std::vector<Slot> schedule_(const ObjectMeta& m, const Mi355xJobSpec& spec, const std::string& resource,
-                              const std::string& pool_node, std::string* reason, std::string* why,
-                              std::vector<Json>* victims);
+                              const std::string& pool_node, const std::map<std::string, int64_t>& pool_cap,
+                              std::string* reason, std::string* why, std::vector<Json>* victims);
   // True when every not-yet-created slot's node has that many GPUs free right now (pods of
   // preempted jobs may still be terminating on it).
   bool capacity_free_(const Mi355xJobSpec& spec, const std::string& resource, const Json& placement);
   Json build_pod_(const Json& job, const ObjectMeta& m, const Mi355xJobSpec& spec, const std::string& resource,
                   int attempt, int world, const Slot& slot, const std::string& master_addr);
   bool resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec& spec, std::string* resource, std::string* node,
-                     std::string* why);
+                     std::string* why, std::map<std::string, int64_t>* pool_cap = nullptr);
 
   Informer& nodes_;
   std::mutex sched_mu_;

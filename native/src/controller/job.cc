@@ -129,7 +129,8 @@ std::vector<Json> Mi355xJobReconciler::list_pods_(const ObjectMeta& m) {
 }
 
 bool Mi355xJobReconciler::resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec& spec, std::string* resource,
-                                        std::string* node, std::string* why) {
+                                        std::string* node, std::string* why,
+                                        std::map<std::string, int64_t>* pool_cap) {
   *resource = spec.resource_name.empty() ? gen::kDefaultResource : spec.resource_name;
   if (spec.pool_ref.empty()) return true;
   Json pool;
@@ -153,12 +154,20 @@ bool Mi355xJobReconciler::resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec
     *why = "Mi355xPool " + spec.pool_ref + " has no GPUs placed yet";
     return false;
   }
+  if (pool_cap) {
+    const int64_t slots = std::max<int64_t>(1, pool.path("spec.sharing.replicasPerGPU").as_int(1));
+    for (const auto& n : span.empty() ? std::vector<std::string>{*node} : span) (*pool_cap)[n] = 0;
+    for (const auto& d : pool.path("status.devices").elements())
+      if (d["health"].as_string() == "Healthy" && d["advertised"].as_bool(false))
+        (*pool_cap)[d["node"].as_string()] += slots;
+  }
   return true;
 }
 
 std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const ObjectMeta& m, const Mi355xJobSpec& spec,
                                                                       const std::string& resource,
                                                                       const std::string& pool_node,
+                                                                      const std::map<std::string, int64_t>& pool_cap,
                                                                       std::string* reason, std::string* why,
                                                                       std::vector<Json>* victims) {
   trace::Span span("schedule");
@@ -248,6 +257,10 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     if (!node_schedulable(n) || !selector_matches(spec.node_selector, n)) continue;
     if (!pool_node.empty() && ("," + pool_node + ",").find("," + name + ",") == std::string::npos) continue;
     free[name] = qty(n.path("status.allocatable")[resource]);
+    auto pc = pool_cap.find(name);
+    // the pool's own ready slots bound it: the kubelet lowers allocatable only after it heard
+    // of a drained GPU, the pool's status already says so
+    if (pc != pool_cap.end()) free[name] = std::min(free[name], pc->second);
     order.push_back(name);
   }
   if (spec.gpus_per_replica > 0) {
@@ -646,7 +659,8 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
       return Outcome::requeue(opts_.progress_poll, "waiting for previous pods to terminate");
     }
     std::string resource, pool_node, reason, why;
-    if (!resolve_pool_(m, spec, &resource, &pool_node, &why)) {
+    std::map<std::string, int64_t> pool_cap;
+    if (!resolve_pool_(m, spec, &resource, &pool_node, &why, &pool_cap)) {
       st["phase"] = phase == "Restarting" ? "Restarting" : "Pending";
       set_condition(conds, gen::kCondScheduled, "False", "PoolNotReady", why, m.generation, now);
       st["conditions"] = conds;
@@ -655,7 +669,7 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
     }
     std::lock_guard<std::mutex> g(sched_mu_);
     std::vector<Json> victims;
-    auto slots = schedule_(m, spec, resource, pool_node, &reason, &why, &victims);
+    auto slots = schedule_(m, spec, resource, pool_node, pool_cap, &reason, &why, &victims);
     if (slots.empty()) {
       st["phase"] = phase == "Restarting" ? "Restarting" : "Pending";
       const Json& prev = find_condition(conds, gen::kCondScheduled);
