@@ -1028,7 +1028,8 @@ class Agent:
             # The claim becomes durable while the probe runs (the ledger's writer fsyncs it
             # concurrently); the RPC answers only after it is on disk, so no crash can ever make
             # the manager believe it owns GPUs a restarted agent would hand out again.
-            claim_seq = self.ledger.commit(self.records, durable=False)
+            # encoded and fsynced by the ledger's writer while the probe runs
+            claim_seq = self.ledger.commit(self.records, durable=False, lock=self.lock)
             self.stats["claims"] += len(chosen)
         lap("commit")
         for d in chosen:  # an in-flight HBM scrub window finishes and hands its buffer back
@@ -1189,6 +1190,8 @@ class Agent:
             owned = [self.by_uuid[u] for u, r in self.records.items()
                      if r["poolUID"] == pool_uid and u in self.by_uuid and r.get("state") == "Claimed"]
         members = list({d["uuid"]: d for d in owned + chosen}.values())
+        if len(members) < 2:
+            return  # one GPU of the pool on this node: no link to ring
         ring = self._ring_order(members)
         links = self.prober.peer_ring(ring, opts)
         floor = float(opts.get("minXgmiGBps") or 0)

@@ -87,6 +87,8 @@ class Ledger:
         # serialised sections: each is rendered by its writer's thread (the claim map under the
         # agent lock), so a scrubber write never iterates a claim map another thread is editing
         self._claims_text = "{}"
+        self._claims_src: tuple | None = None  # (claims, lock) handed over by commit(lock=...)
+        self._src_seq = 0                      # the sequence number of that hand-over
         self._sweep: dict[str, dict] = {}
         self._xgmi: dict[str, dict] = {}
         try:
@@ -113,17 +115,24 @@ class Ledger:
                         continue
         return claims
 
-    def commit(self, claims: dict[str, dict], durable: bool = True) -> int:
+    def commit(self, claims: dict[str, dict], durable: bool = True,
+               lock: threading.RLock | None = None) -> int:
         """Record the full claim map; returns its sequence number. ``durable``: written and
         fsync'ed before returning (one write per agent operation, atomically replaced). Otherwise
         the write is left to a background writer (coalesced) — for transitions a crash may lose
         safely, e.g. Probing -> Claimed: a restarted agent turns a 'Probing' record into a failed
-        probe (ProbeInterrupted) and the pool replaces the GPU."""
-        text = json.dumps(claims, sort_keys=True)
+        probe (ProbeInterrupted) and the pool replaces the GPU — or made durable later by
+        ``flush(seq)``. With ``lock`` (the caller's lock guarding ``claims``; not durable) the map
+        is serialised by the writer too, under that lock: a claim hands its record over and probes
+        while the writer encodes and fsyncs it."""
+        text = None if lock is not None and not durable else json.dumps(claims, sort_keys=True)
         with self._mu:
-            self._claims_text = text
             self._seq += 1
             seq = self._seq
+            if text is None:
+                self._claims_src, self._src_seq = (claims, lock), seq
+            else:
+                self._claims_text, self._claims_src = text, None
         if durable:
             self.flush(seq)
         else:
@@ -131,23 +140,38 @@ class Ledger:
         return seq
 
     def flush(self, upto: int | None = None) -> None:
-        """Make everything up to sequence ``upto`` (default: all) durable."""
-        with self._mu:  # already on disk: do not queue behind a writer busy with a newer state
-            if upto is not None and self._written >= upto:
-                return
-        with self._wmu:
-            with self._mu:
-                want = self._seq if upto is None else upto
+        """Make everything up to sequence ``upto`` (default: all committed so far) durable."""
+        with self._mu:
+            want = self._seq if upto is None else upto
+        while True:
+            with self._mu:  # already on disk: do not queue behind a writer busy with a newer state
                 if self._written >= want:
                     return
-                seq = self._seq
-                text = '{"version": %d, "claims": %s, "hbmSweep": %s, "xgmiPairs": %s}' % (
-                    VERSION, self._claims_text, json.dumps(self._sweep, sort_keys=True),
-                    json.dumps(self._xgmi, sort_keys=True))
-            _atomic_write_text(self.path, text, self.fsync)
-            self.writes += 1
-            with self._mu:
-                self._written = max(self._written, seq)
+                src = self._claims_src
+            if src is not None:
+                # encode a handed-over claim map under its owner's lock — before taking _wmu:
+                # owners hold their lock while they flush (lock -> _wmu), never the reverse
+                claims, lock = src
+                with lock:
+                    text = json.dumps(claims, sort_keys=True)
+                with self._mu:
+                    if self._claims_src is src:  # a newer commit replaced it otherwise
+                        self._claims_text, self._claims_src = text, None
+            with self._wmu:
+                with self._mu:
+                    if self._written >= want:
+                        return
+                    seq = self._seq
+                    if self._claims_src is not None:  # handed over after the encode: next turn
+                        seq = self._src_seq - 1
+                    text = '{"version": %d, "claims": %s, "hbmSweep": %s, "xgmiPairs": %s}' % (
+                        VERSION, self._claims_text, json.dumps(self._sweep, sort_keys=True),
+                        json.dumps(self._xgmi, sort_keys=True))
+                if seq > self._written:
+                    _atomic_write_text(self.path, text, self.fsync)
+                    self.writes += 1
+                    with self._mu:
+                        self._written = max(self._written, seq)
 
     def _kick_lazy(self) -> None:
         if self._lazy_thread is None:
