@@ -133,7 +133,9 @@ class ApiServerSim:
         self.watch_delay = watch_delay
         self.token = token
         self.bookmark_interval = bookmark_interval
-        self.watchers: set[asyncio.Queue] = set()
+        # watch queues per resource type (a kube-apiserver's watch cache is per resource too): a
+        # write wakes only the watchers of its own type, not every informer of every kind
+        self.watchers: dict[tuple[str, str], set[asyncio.Queue]] = {}
         self.store.listeners.append(self._fanout)
         self.requests_total: dict[tuple[str, int], int] = {}
         self.started = time.time()
@@ -188,15 +190,17 @@ class ApiServerSim:
         for (m, c), n in sorted(self.requests_total.items()):
             lines.append(f'apiserver_request_total{{verb="{m}",code="{c}"}} {n}')
         lines.append("# TYPE apiserver_watchers gauge")
-        lines.append(f"apiserver_watchers {len(self.watchers)}")
+        lines.append(f"apiserver_watchers {sum(len(v) for v in self.watchers.values())}")
         lines.append("# TYPE etcd_resource_version gauge")
         lines.append(f"etcd_resource_version {self.store.rv}")
         return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
 
     def _fanout(self, ev: WatchEvent) -> None:
-        t = time.monotonic()
-        for q in list(self.watchers):
-            q.put_nowait((t, ev))
+        qs = self.watchers.get(ev.rtype)
+        if qs:
+            t = time.monotonic()
+            for q in list(qs):
+                q.put_nowait((t, ev))
 
     # -------------------------------------------------------------- discovery
     def _resources_for(self, group: str, version: str) -> list[dict]:
@@ -363,7 +367,7 @@ class ApiServerSim:
 
         queue: asyncio.Queue = asyncio.Queue()
         # Register before computing the backlog so nothing falls between the two.
-        self.watchers.add(queue)
+        self.watchers.setdefault(rt.key, set()).add(queue)
         try:
             initial: list[tuple[str, dict]] = []
             if rv_s in ("", "0"):
@@ -425,7 +429,7 @@ class ApiServerSim:
         except (ConnectionResetError, asyncio.CancelledError):
             raise
         finally:
-            self.watchers.discard(queue)
+            self.watchers.get(rt.key, set()).discard(queue)
 
 
 async def serve(host: str, port: int, sim: ApiServerSim, port_file: str | None = None,
