@@ -333,6 +333,7 @@ class Store:
         self.objects: dict[tuple[str, str], dict[tuple[str, str], dict]] = {}
         self.log: collections.deque[WatchEvent] = collections.deque(maxlen=window)
         self.listeners: list[Callable[[WatchEvent], None]] = []
+        self._vschema: dict[tuple[str, str], tuple[dict, dict]] = {}  # CRD -> (schema, w/o metadata)
         for rt in BUILTINS:
             self.register(rt)
         self._ensure_namespace("default")
@@ -414,10 +415,11 @@ class Store:
             return obj
         obj = openapi.prune(obj, rt.schema)
         obj = openapi.apply_defaults(obj, rt.schema)
-        errs = openapi.validate({k: v for k, v in obj.items() if k != "metadata"},
-                                {**rt.schema, "properties": {k: v for k, v in
-                                                             rt.schema.get("properties", {}).items()
-                                                             if k != "metadata"}})
+        vs = self._vschema.get(rt.key)
+        if vs is None or vs[0] is not rt.schema:  # the schema minus metadata, built once per CRD
+            vs = self._vschema[rt.key] = (rt.schema, {**rt.schema, "properties": {
+                k: v for k, v in rt.schema.get("properties", {}).items() if k != "metadata"}})
+        errs = openapi.validate({k: v for k, v in obj.items() if k != "metadata"}, vs[1])
         if errs:
             errs = [e.replace("<root>.", "") for e in errs]
             name = obj.get("metadata", {}).get("name", "")
