@@ -103,9 +103,13 @@ class DevicePluginServer:
     def stop(self) -> None:
         self.stopped = True
         with self.cv:
-            live = list(self._live)
+            # end idle streams with an OK status (the kubelet reconnects); a stream with a send
+            # in flight is left to server.stop, which cancels it
+            idle = [st for st in self._live if not st.busy and st.alive]
+            for st in idle:
+                st.busy = True  # no new send may start on it now
             self.cv.notify_all()
-        for st in live:  # end the streams with an OK status (the kubelet reconnects)
+        for st in idle:
             try:
                 st.send(None)
             except Exception:
