@@ -23,16 +23,21 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sizes", default="4096,8192")
+    ap.add_argument("--tiles", default="128,256",
+                    help="gemmTile kinds to compare: 128 (register-staged) and 256 (glds)")
+    ap.add_argument("--stress", type=int, default=0,
+                    help="extra exactness runs per tile at 512..4096 (race screen)")
     ap.add_argument("--device", type=int, default=0)
     a = ap.parse_args()
     n_dev = probe.init()
     assert n_dev >= 1, "no HIP device"
     sizes = [int(x) for x in a.sizes.split(",")]
+    tiles = [int(x) for x in a.tiles.split(",")]
     runs: dict[str, list[dict]] = {}
     failures = []
     for r in range(a.rounds):
         for n in sizes:
-            for tile in (128, 256):
+            for tile in tiles:
                 res = probe.run(a.device, hbm_bytes=1 << 28, gemm_n=n, gemm_tile=tile)
                 if not res.get("passed"):
                     failures.append(res)
@@ -41,7 +46,15 @@ def main() -> int:
         # overlapped on two streams) vs the same work serialised on one stream
         runs.setdefault("default_1GiB", []).append(probe.run(a.device))
         runs.setdefault("serial_1GiB", []).append(probe.run(a.device, overlap=0))
-    summary = {}
+    stress = {}
+    for i in range(a.stress):
+        for tile in tiles:
+            n = (512, 1024, 2048, 4096)[i % 4]
+            res = probe.run(a.device, hbm_bytes=1 << 24, gemm_n=n, gemm_tile=tile)
+            stress[tile] = stress.get(tile, 0) + 1
+            if not res.get("passed"):
+                failures.append(res)
+    summary = {"stress_runs": stress}
     for key, rs in runs.items():
         tf = [x["mfma"]["tflops"] for x in rs]
         summary[key] = {"tflops_median": round(statistics.median(tf), 1), "tflops_min": round(min(tf), 1),
