@@ -1555,8 +1555,15 @@ class Agent:
             if slots != ids:  # time-sliced: the pod shares these GPUs with other pods
                 envs["GPUPOOL_GPU_SLOTS"] = ",".join(slots)
                 envs.update(self._isolation_env(slots, mounts))
-            return {"envs": envs, "devices": ["/dev/kfd"] + render, "mounts": mounts,
-                    "annotations": {schema.ANN_POD_DEVICES: ",".join(ids)}}
+        if "GPUPOOL_HBM_LIMIT_BYTES" in envs:  # the pod-wide HBM account (file I/O: off the lock)
+            acct = self._share_account(slots, int(envs["GPUPOOL_HBM_LIMIT_BYTES"]),
+                                       len(ids))
+            if acct:
+                mounts.append({"container_path": self.SHARE_ACCOUNT_PATH, "host_path": acct,
+                               "read_only": False})
+                envs["GPUPOOL_SHARE_ACCOUNT"] = self.SHARE_ACCOUNT_PATH
+        return {"envs": envs, "devices": ["/dev/kfd"] + render, "mounts": mounts,
+                "annotations": {schema.ANN_POD_DEVICES: ",".join(ids)}}
 
     SHARE_LIB_DIR = "/opt/gpupool/lib"  # where the pod sees libgpupool_share.so
     SHARE_ACCOUNT_PATH = "/var/run/gpupool/share.acct"  # where it sees its pod's HBM account
@@ -1633,13 +1640,8 @@ class Agent:
         mounts.append({"container_path": self.SHARE_LIB_DIR, "host_path": native_dir(),
                        "read_only": True})
         env = {"HSA_TOOLS_LIB": f"{self.SHARE_LIB_DIR}/libgpupool_share.so"}
-        if hbm:
+        if hbm:  # allocate_spec adds the pod-wide account file (GPUPOOL_SHARE_ACCOUNT)
             env["GPUPOOL_HBM_LIMIT_BYTES"] = str(hbm)
-            acct = self._share_account(slots, hbm, len(per_gpu))
-            if acct:
-                mounts.append({"container_path": self.SHARE_ACCOUNT_PATH, "host_path": acct,
-                               "read_only": False})
-                env["GPUPOOL_SHARE_ACCOUNT"] = self.SHARE_ACCOUNT_PATH
         if cu_mask:
             env["GPUPOOL_CU_MASK"] = _ranges(sorted(cu_mask))
         return env
