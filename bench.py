@@ -403,7 +403,8 @@ def main() -> int:
         # the first claiming pass between its PATCH and its Ready
         claim_traces = [t for t in traces
                         if any(sp["name"] == "agent:POST /v1/claims" for sp in t["spans"])]
-        e2e: dict[str, list[float]] = {"patch_to_pass_ms": [], "pass_ms": [],
+        e2e: dict[str, list[float]] = {"patch_rtt_ms": [], "patch_to_pass_ms": [],
+                                       "queue_wait_ms": [], "pass_ms": [],
                                        "status_to_client_ms": []}
         by_n: dict[int, list[dict]] = {}
         for cy in cycles:
@@ -413,6 +414,11 @@ def main() -> int:
             t = min(hit, key=lambda x: x["start"])
             by_n.setdefault(cy["n"], []).append(t)
             e2e["patch_to_pass_ms"].append((t["start"] - cy["patchAt"]) * 1e3)
+            if cy.get("patchRttMs") is not None:  # the client's PATCH request -> response
+                e2e["patch_rtt_ms"].append(cy["patchRttMs"])
+            qw = (t.get("attrs") or {}).get("queueWaitMs")
+            if qw is not None:  # of which: ready in the manager's work queue, no worker yet
+                e2e["queue_wait_ms"].append(float(qw))
             e2e["pass_ms"].append(t["totalMs"])
             e2e["status_to_client_ms"].append(
                 (cy["readyAtWall"] - t["start"]) * 1e3 - t["totalMs"])

@@ -249,16 +249,25 @@ def pod_usage(pod: dict) -> dict[str, float]:
 
 # ------------------------------------------------------------------ patches
 def merge_patch(target: Any, patch: Any) -> Any:
-    """RFC 7386 JSON merge patch."""
+    """RFC 7386 JSON merge patch (the target is copied once, then patched in place)."""
     if not isinstance(patch, dict):
         return clone(patch)
     out = clone(target) if isinstance(target, dict) else {}
+    _merge_into(out, patch)
+    return out
+
+
+def _merge_into(out: dict, patch: dict) -> None:
     for k, v in patch.items():
         if v is None:
             out.pop(k, None)
+        elif isinstance(v, dict):
+            sub = out.get(k)
+            if not isinstance(sub, dict):
+                sub = out[k] = {}
+            _merge_into(sub, v)
         else:
-            out[k] = merge_patch(out.get(k), v)
-    return out
+            out[k] = clone(v)
 
 
 def _ptr_parts(path: str) -> list[str]:
@@ -403,8 +412,17 @@ class Store:
         for k in ("deletionTimestamp", "deletionGracePeriodSeconds"):
             md.pop(k, None)
 
-    def _admit_cr(self, rt: ResourceType, obj: dict) -> dict:
-        """Defaulting, pruning, validation for custom resources (+ secrets stringData)."""
+    def _admit_cr(self, rt: ResourceType, obj: dict, keep: str = "") -> dict:
+        """Defaulting, pruning, validation for custom resources (+ secrets stringData). ``keep``:
+        a top-level field taken unchanged from the stored object (status on a main-resource
+        write, spec on a status write), admitted when it was written: not walked again."""
+        if keep and keep in obj and rt.schema is not None and \
+                keep not in (rt.schema.get("required") or []) and \
+                "default" not in ((rt.schema.get("properties") or {}).get(keep) or {}):
+            held = obj.pop(keep)
+            obj = self._admit_cr(rt, obj)
+            obj[keep] = held
+            return obj
         if rt.kind == "Secret":
             sd = obj.pop("stringData", None) or {}
             data = obj.setdefault("data", {}) or {}
@@ -600,13 +618,13 @@ class Store:
         return clone(obj)
 
     def update(self, rt: ResourceType, ns: str | None, name: str, obj: dict,
-               subresource: str = "", dry_run: bool = False) -> dict:
+               subresource: str = "", dry_run: bool = False, owned: bool = False) -> dict:
         ns = self._check_ns(rt, ns) if rt.namespaced else ""
         cur = self.objects[rt.key].get((ns, name))
         if cur is None:
             raise ApiError(404, "NotFound", f'{rt.plural} "{name}" not found',
                            {"name": name, "kind": rt.plural})
-        new = clone(obj)
+        new = obj if owned else clone(obj)  # ``owned``: a private copy already (patch)
         nmd = new.setdefault("metadata", {})
         if nmd.get("name", name) != name:
             raise ApiError(400, "BadRequest", "the name of the object does not match the URL")
@@ -618,6 +636,7 @@ class Store:
                            "modified; please apply your changes to the latest version and try "
                            "again", {"name": name, "group": rt.group, "kind": rt.plural})
         cmd = cur["metadata"]
+        keep = ""
         if subresource == "status":
             merged = clone(cur)
             if "status" in new:
@@ -625,6 +644,7 @@ class Store:
             else:
                 merged.pop("status", None)
             new = merged
+            keep = "spec"
         else:
             # immutable / server-owned metadata
             for k in ("uid", "creationTimestamp", "deletionTimestamp",
@@ -637,6 +657,7 @@ class Store:
             if rt.status_sub:
                 if "status" in cur:
                     new["status"] = clone(cur["status"])
+                    keep = "status"
                 else:
                     new.pop("status", None)
             if cmd.get("deletionTimestamp"):
@@ -645,7 +666,7 @@ class Store:
                     raise ApiError(422, "Forbidden", f"no new finalizers can be added if the "
                                    f"object is being deleted, found new finalizers {sorted(added)}")
         new["apiVersion"], new["kind"] = rt.api_version, rt.kind
-        new = self._admit_cr(rt, new)
+        new = self._admit_cr(rt, new, keep)
         new["metadata"]["resourceVersion"] = cmd["resourceVersion"]
         if dry_run:
             return new
@@ -668,14 +689,18 @@ class Store:
 
     def patch(self, rt: ResourceType, ns: str | None, name: str, patch: Any, ptype: str,
               subresource: str = "", dry_run: bool = False) -> dict:
-        cur = self.get(rt, ns, name)
+        nsk = self._check_ns(rt, ns) if rt.namespaced else ""
+        cur = self.objects[rt.key].get((nsk, name))
+        if cur is None:
+            self.get(rt, ns, name)  # raises the NotFound
+        # both patch forms copy ``cur`` first: the stored object is never touched
         if ptype == "json":
             new = json_patch(cur, patch)
         else:  # merge / strategic (approximated as merge)
             new = merge_patch(cur, patch)
         if not (isinstance(patch, dict) and patch.get("metadata", {}).get("resourceVersion")):
             new.setdefault("metadata", {})["resourceVersion"] = cur["metadata"]["resourceVersion"]
-        return self.update(rt, ns, name, new, subresource, dry_run)
+        return self.update(rt, ns, name, new, subresource, dry_run, owned=True)
 
     def delete(self, rt: ResourceType, ns: str | None, name: str, grace: int | None = None,
                preconditions: dict | None = None, dry_run: bool = False) -> dict:

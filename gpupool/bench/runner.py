@@ -72,6 +72,7 @@ class BenchRun:
     gt_s: float = 0.0             # time spent in ground-truth reads (reported separately)
     deadline: float = 0.0         # time.monotonic() wall budget end (0 = none): caps every wait
     phase: str = ""               # what the scenario is doing now (named in error records)
+    last_patch_rtt: float = 0.0   # seconds, the last scale PATCH's request -> response
 
     def _to(self) -> float:
         """Per-wait timeout: the per-transition limit, cut to what the wall budget has left."""
@@ -156,7 +157,9 @@ class BenchRun:
             return self.c.get(MI355XPOOLS, name, self.ns)
 
     def scale(self, name: str, r: int, wait: bool = True) -> dict | None:
+        t0 = time.perf_counter()
         self.c.patch(MI355XPOOLS, name, {"spec": {"replicas": r}}, self.ns)
+        self.last_patch_rtt = time.perf_counter() - t0  # the apiserver's PATCH round trip
         if wait:
             return self.c.wait_for(MI355XPOOLS, name, self.ns, ready_at(r), timeout=self._to())
         return None
@@ -177,6 +180,7 @@ class BenchRun:
         self.phase = "scale_up"
         obj = self.scale(name, n)
         t_ready = time.perf_counter() - t0
+        patch_rtt = self.last_patch_rtt
         ready_at_wall = patch_at + t_ready
         self.phase = "ground_truth"
         truth = self.wait_truth(pool, n)
@@ -184,7 +188,7 @@ class BenchRun:
         self.phase = "release"
         self.scale(name, 0)
         return {"n": n, "readySeconds": t_ready, "ok": ok, "truth": truth,
-                "patchAt": patch_at, "readyAtWall": ready_at_wall,
+                "patchAt": patch_at, "readyAtWall": ready_at_wall, "patchRttMs": patch_rtt * 1e3,
                 "probeMs": [round(d.get("probe", {}).get("ms", 0.0), 3)
                             for d in obj["status"]["devices"]]}
 

@@ -31,10 +31,11 @@ class WorkQueue {
   int num_requeues(const std::string& key) const;
   Duration backoff_for(const std::string& key) const;  // next backoff (does not mutate)
 
-  // Blocks until a key is available or shutdown. Returns false on shutdown.
-  bool get(std::string* key);
+  // Blocks until a key is available or shutdown. Returns false on shutdown. ``waited_ms`` (if
+  // given): how long the key sat ready in the queue before this worker took it.
+  bool get(std::string* key, double* waited_ms = nullptr);
   // Like get() but gives up after ``timeout`` (returns false, key untouched).
-  bool get_for(std::string* key, Duration timeout);
+  bool get_for(std::string* key, Duration timeout, double* waited_ms = nullptr);
   void done(const std::string& key);
 
   void shutdown();
@@ -57,6 +58,7 @@ class WorkQueue {
   std::deque<std::string> queue_;
   std::set<std::string> dirty_;
   std::set<std::string> processing_;
+  std::map<std::string, Clock::time_point> ready_at_;  // key -> when it entered queue_
   std::priority_queue<Delayed, std::vector<Delayed>, std::greater<Delayed>> delayed_;
   std::map<std::string, Clock::time_point> delayed_at_;  // earliest pending time per key
   std::map<std::string, int> failures_;

@@ -1350,7 +1350,8 @@ void Controller::stop() {
 
 void Controller::worker_() {
   std::string key;
-  while (q_.get(&key)) {
+  double waited_ms = 0;
+  while (q_.get(&key, &waited_ms)) {
     auto s1 = key.find('/');
     auto s2 = key.find('/', s1 + 1);
     std::string kind = key.substr(0, s1), ns = key.substr(s1 + 1, s2 - s1 - 1), name = key.substr(s2 + 1);
@@ -1365,6 +1366,8 @@ void Controller::worker_() {
     static const char* names[] = {"done", "requeue", "error", "terminal"};
     {
       trace::Trace tr(key);
+      tr.attr("queueWaitMs", waited_ms);  // ready in the work queue -> this worker took it
+      waited_ms = 0;
       try {
         out = it->second->reconcile(ns, name);
       } catch (const std::exception& e) {

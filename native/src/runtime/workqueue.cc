@@ -12,6 +12,7 @@ void WorkQueue::add_locked_(const std::string& key) {
   dirty_.insert(key);
   if (processing_.count(key)) return;  // re-queued by done()
   queue_.push_back(key);
+  ready_at_[key] = Clock::now();
   cv_.notify_one();
 }
 
@@ -78,15 +79,15 @@ void WorkQueue::promote_due_locked_() {
   }
 }
 
-bool WorkQueue::get(std::string* key) {
+bool WorkQueue::get(std::string* key, double* waited_ms) {
   for (;;) {
-    if (get_for(key, Duration(3600 * 1000))) return true;
+    if (get_for(key, Duration(3600 * 1000), waited_ms)) return true;
     std::lock_guard<std::mutex> g(mu_);
     if (shutdown_) return false;
   }
 }
 
-bool WorkQueue::get_for(std::string* key, Duration timeout) {
+bool WorkQueue::get_for(std::string* key, Duration timeout, double* waited_ms) {
   std::unique_lock<std::mutex> lk(mu_);
   auto deadline = Clock::now() + timeout;
   for (;;) {
@@ -96,6 +97,11 @@ bool WorkQueue::get_for(std::string* key, Duration timeout) {
       queue_.pop_front();
       processing_.insert(*key);
       dirty_.erase(*key);
+      auto it = ready_at_.find(*key);
+      if (it != ready_at_.end()) {
+        if (waited_ms) *waited_ms = std::chrono::duration<double, std::milli>(Clock::now() - it->second).count();
+        ready_at_.erase(it);
+      }
       return true;
     }
     if (shutdown_) return false;
@@ -113,6 +119,7 @@ void WorkQueue::done(const std::string& key) {
   processing_.erase(key);
   if (dirty_.count(key)) {
     queue_.push_back(key);
+    ready_at_[key] = Clock::now();
     cv_.notify_one();
   }
 }

@@ -334,6 +334,19 @@ TEST(workqueue_dedup_and_processing) {
   EXPECT_EQ(q.len(), 1u);
   q.done("a");  // re-queued now
   EXPECT_EQ(q.len(), 2u);
+  // time spent ready in the queue (the reconcile trace's queueWaitMs)
+  double waited = -1;
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  EXPECT_TRUE(q.get_for(&k, std::chrono::milliseconds(10), &waited));
+  EXPECT_EQ(k, std::string("b"));
+  EXPECT_TRUE(waited >= 15.0 && waited < 5000.0);
+  q.done("b");
+  q.add("c");
+  EXPECT_TRUE(q.get_for(&k, std::chrono::milliseconds(10), &waited));  // "a", re-queued by done()
+  EXPECT_TRUE(waited >= 15.0);
+  EXPECT_TRUE(q.get_for(&k, std::chrono::milliseconds(10), &waited));
+  EXPECT_EQ(k, std::string("c"));
+  EXPECT_TRUE(waited >= 0.0 && waited < 15.0);
 }
 
 TEST(workqueue_delay_and_backoff) {
