@@ -656,7 +656,8 @@ class Store:
             nmd["name"] = name
             if rt.status_sub:
                 if "status" in cur:
-                    new["status"] = clone(cur["status"])
+                    if not (owned and new.get("status") == cur["status"]):  # a patch's own copy
+                        new["status"] = clone(cur["status"])
                     keep = "status"
                 else:
                     new.pop("status", None)
