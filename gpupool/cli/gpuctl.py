@@ -357,8 +357,10 @@ def cmd_devices(c: Client, ns: str, args) -> int:
 
 
 def cmd_top(c: Client, ns: str, args) -> int:
-    """gpuctl top [pools|gpus]: live GPU utilisation (kubectl top for the pools; the reference's
-    "Prometheus + Grafana, GPU utilisation", GPU调度平台搭建.md:800) read from every node agent."""
+    """gpuctl top [pools|gpus|pods]: live GPU utilisation (kubectl top for the pools; the
+    reference's "Prometheus + Grafana, GPU utilisation", GPU调度平台搭建.md:800) read from every
+    node agent; ``pods`` is the per-pod accounting of (time-shared) GPUs: VRAM and GPU-time share
+    per pod (GPU调度平台搭建.md:800-802)."""
     rows = []
     for n in c.list(NODES)["items"]:
         ep = (n["metadata"].get("annotations") or {}).get(schema.ANN_AGENT_ENDPOINT)
@@ -372,6 +374,18 @@ def cmd_top(c: Client, ns: str, args) -> int:
         for d in view["devices"]:
             rows.append((view["node"], d))
     num = lambda v: float(v) if isinstance(v, (int, float)) else 0.0  # noqa: E731
+    if args.what == "pods":  # per-pod accounting on (shared) GPUs: the agent's process -> pod map
+        print(f"{'NAMESPACE/POD':<36}{'NODE':<18}{'IDX':<5}{'POOL':<28}{'VRAM(GiB)':<11}{'GPU%':<6}"
+              "PIDS")
+        for node, d in sorted(rows, key=lambda r: (r[0], r[1].get("index", 0))):
+            for e in d.get("usage") or []:
+                busy = e.get("gfxBusy")
+                print(f"{e.get('namespace', '')}/{e.get('pod', ''):<{35 - len(e.get('namespace', ''))}}"
+                      f" {node:<18}{d.get('index', ''):<5}{d.get('pool', '') or '-':<28}"
+                      f"{num(e.get('vramBytes')) / 2**30:<11.2f}"
+                      f"{'-' if busy is None else f'{100 * busy:.0f}':<6}"
+                      f"{','.join(str(x) for x in e.get('pids') or [])}")
+        return 0
     if args.what == "gpus":
         print(f"{'NODE':<18}{'IDX':<5}{'POOL':<28}{'GFX%':<6}{'UMC%':<6}{'POWER(W)':<10}VRAM(GiB)")
         for node, d in sorted(rows, key=lambda r: (r[0], r[1].get("index", 0))):
@@ -719,7 +733,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("node")
     p.add_argument("-o", "--output", default="")
     p = sub.add_parser("top", help="GPU utilisation per pool (or per GPU) from the node agents")
-    p.add_argument("what", nargs="?", default="pools", choices=["pools", "gpus"])
+    p.add_argument("what", nargs="?", default="pools", choices=["pools", "gpus", "pods"])
     p = sub.add_parser("gpu", help="per-GPU maintenance: cordon | uncordon")
     p.add_argument("action", choices=["cordon", "uncordon"])
     p.add_argument("node")

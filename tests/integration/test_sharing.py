@@ -227,3 +227,14 @@ def test_per_pod_accounting_on_a_time_shared_gpu(cluster_factory):
     got = dict(re.findall(r'gpupool_pod_vram_bytes\{[^}]*pod="(\w+)"\} (\d+)', str(metrics)))
     assert got == {"small": str(2 << 30), "big": str(6 << 30)}
     assert 'gpupool_pod_gfx_busy_ratio{' in str(metrics)
+    # the same accounting from the CLI: gpuctl top pods
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([os.path.join(root, "bin", "gpuctl"), "--server", c.url, "top", "pods"],
+                       capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, GPUPOOL_AGENT_TOKEN=c.agent_token))
+    assert r.returncode == 0, r.stderr
+    rows = {ln.split()[0]: ln.split() for ln in r.stdout.splitlines()[1:]}
+    assert rows["default/small"][4] == "2.00" and rows["default/big"][4] == "6.00", r.stdout
+    assert rows["default/big"][5] == "0" and rows["default/small"][6] == str(pids["small"])
