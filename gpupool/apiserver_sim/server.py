@@ -102,6 +102,16 @@ def builtin_columns(rt: ResourceType) -> list[tuple[str, str, Any]]:
                     (o.get("involvedObject") or {}).get("kind", "").lower(),
                     (o.get("involvedObject") or {}).get("name", ""))),
                 ("Message", "string", lambda o: o.get("message", ""))]
+    if rt.kind == "ResourceQuota":  # kubectl's columns: "<resource>: used/hard" per kind
+        def usage(limits: bool):
+            def f(o):
+                hard = (o.get("status") or {}).get("hard") or (o.get("spec") or {}).get("hard") or {}
+                used = (o.get("status") or {}).get("used") or {}
+                return ", ".join(f"{k}: {used.get(k, '0')}/{v}" for k, v in sorted(hard.items())
+                                 if k.startswith("limits.") == limits)
+            return f
+        return [("Age", "date", lambda o: o["metadata"].get("creationTimestamp")),
+                ("Request", "string", usage(False)), ("Limit", "string", usage(True))]
     return [("Age", "date", lambda o: o["metadata"].get("creationTimestamp"))]
 
 

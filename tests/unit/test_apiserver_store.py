@@ -268,3 +268,21 @@ def test_resourcequota_admission_and_status_used(store):
     store.create(pods, "team", _gpu_pod("b", 2))
     store.delete(pods, "team", "b")
     assert store.get(q, "team", "gpu-quota")["status"]["used"]["requests.amd.com/gpu"] == "1"
+
+
+def test_resourcequota_table_shows_used_over_hard():
+    """`gpuctl get quota` (the Table the sim serves, kubectl's columns): per-resource used/hard,
+    requests and limits apart — the team's GPU budget at a glance (GPU调度平台搭建.md:802)."""
+    from gpupool.apiserver_sim.server import to_table
+    st = Store()
+    rt = st.types[("", "resourcequotas")]
+    q = {"metadata": {"name": "gpu-quota", "creationTimestamp": "2026-01-01T00:00:00Z"},
+         "spec": {"hard": {"requests.amd.com/gpu": "4", "limits.amd.com/gpu": "4", "pods": "10"}},
+         "status": {"hard": {"requests.amd.com/gpu": "4", "limits.amd.com/gpu": "4", "pods": "10"},
+                    "used": {"requests.amd.com/gpu": "3", "pods": "2"}}}
+    tbl = to_table(rt, [q], "1")
+    cols = [c["name"] for c in tbl["columnDefinitions"]]
+    assert cols == ["Name", "Age", "Request", "Limit"]
+    cells = tbl["rows"][0]["cells"]
+    assert cells[2] == "pods: 2/10, requests.amd.com/gpu: 3/4"
+    assert cells[3] == "limits.amd.com/gpu: 0/4"
