@@ -223,10 +223,15 @@ class DevicePluginServer:
                     log.exception("ListAndWatch send failed")
 
     def _mark(self, version: int, healthy: set[str] | None) -> None:
-        with self._mark_mu:  # versions only move forward: a late stream send never undoes a newer one
-            if healthy is not None and version <= self._marked:
-                return
-            self._marked = max(self._marked, version)
+        """A stream wrote device list ``version`` (``healthy`` = its Healthy GPUs), or ended
+        (``None``: with no stream left nothing counts as advertised). Versions only move forward —
+        a late send of an older list never undoes a newer one — but the same version may mark
+        again: a new stream (a restarted kubelet) starts by resending the current list."""
+        with self._mark_mu:
+            if healthy is not None:
+                if version < self._marked:
+                    return
+                self._marked = version
             self.agent.mark_advertised(self.resource, healthy)
 
     # ------------------------------------------------------------ API

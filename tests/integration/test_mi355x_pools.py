@@ -743,3 +743,20 @@ def test_spanning_pool_keeps_unreachable_nodes(cluster_factory):
     o = wait_ready(k, "wide", 12, timeout=60)
     assert sorted(o["status"]["nodes"]) == ["sn-0", "sn-1", "sn-2"]
     assert {d["uuid"] for d in o["status"]["devices"]} == before
+
+
+def test_kubelet_restart_readvertises_without_a_device_change(cluster_factory):
+    """The kubelet restarts (its ListAndWatch stream ends, the plugin re-registers, a new stream
+    opens): while it is gone the pool's GPUs are not advertised (readyReplicas 0); once the new
+    stream has resent the same device list the pool is Ready again — no device change needed."""
+    c = cluster_factory()
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("kr", 2), "default")
+    wait_ready(k, "kr", 2)
+    node = c.nodes[0]
+    c._kill(f"kubelet-{node.name}")
+    k.wait_for(MI355XPOOLS, "kr", "default",
+               lambda o: (o.get("status") or {}).get("readyReplicas") == 0, timeout=30)
+    c.start_kubelet(node)
+    o = wait_ready(k, "kr", 2, timeout=30)
+    assert all(d["advertised"] for d in o["status"]["devices"])

@@ -248,3 +248,43 @@ def test_claiming_pool_events_held_until_released(tmp_path, sockdir, native_buil
     # without the hold (direct callers) the claim releases its own hold when it returns
     assert claim(a, uid="plain", count=1)["ok"]
     assert not a._claiming and not a._deferred
+
+
+def test_new_listandwatch_stream_restores_advertised(tmp_path, sockdir, native_built):
+    """A kubelet restart drops its ListAndWatch stream (the advertised bits clear: nothing is
+    known to be advertised) and opens a new one: the new stream's first message — the same device
+    list version — must mark the GPUs advertised again, without waiting for a device change."""
+    dp_dir = os.path.join(sockdir, "dp")
+    kubelet = MiniKubelet(dp_dir)
+    a = make_agent(tmp_path, sockdir)
+    try:
+        r = claim(a, count=2)
+        mine = {d["uuid"] for d in r["devices"]}
+
+        def advertised() -> set:
+            return {d["uuid"] for d in a.node_view()["devices"] if d.get("advertised")}
+
+        def wait(pred, timeout=5.0):
+            deadline = time.time() + timeout
+            while time.time() < deadline and not pred():
+                time.sleep(0.02)
+            return pred()
+        sock = os.path.join(dp_dir, "gpupool-amd-com_gpu.sock")
+        assert wait(lambda: os.path.exists(sock))
+        ch = grpc.insecure_channel(unix_target(sock))
+        stream = Stub(ch, "v1beta1.DevicePlugin").ListAndWatch(DP.Empty())
+        next(stream)
+        assert wait(lambda: advertised() == mine)
+        stream.cancel()
+        ch.close()
+        assert wait(lambda: advertised() == set())  # no stream: nothing counts as advertised
+        ch2 = grpc.insecure_channel(unix_target(sock))
+        stream2 = Stub(ch2, "v1beta1.DevicePlugin").ListAndWatch(DP.Empty())
+        first = next(stream2)
+        assert {d.ID for d in first.devices if d.health == "Healthy"} == mine
+        assert wait(lambda: advertised() == mine), advertised()
+        stream2.cancel()
+        ch2.close()
+    finally:
+        a.stop()
+        kubelet.stop()
