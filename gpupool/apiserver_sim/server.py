@@ -474,6 +474,11 @@ async def serve(host: str, port: int, sim: ApiServerSim, port_file: str | None =
         os.replace(tmp, port_file)
     log.info("apiserver-sim listening on %s:%d", host, bound)
     print(f"apiserver-sim listening on {'https' if ssl_ctx else 'http'}://{host}:{bound}", flush=True)
+    # start-up state (aiohttp, the parsed CRDs and their compiled schemas) lives for the whole
+    # run: out of the collector's generations, so a full collection walks only request garbage
+    import gc
+    gc.collect()
+    gc.freeze()
     while True:
         await asyncio.sleep(3600)
 

@@ -286,3 +286,18 @@ def test_resourcequota_table_shows_used_over_hard():
     cells = tbl["rows"][0]["cells"]
     assert cells[2] == "pods: 2/10, requests.amd.com/gpu: 3/4"
     assert cells[3] == "limits.amd.com/gpu: 0/4"
+
+
+def test_old_watch_events_are_compacted_but_still_served():
+    """Events older than the newest LIVE_EVENTS keep only their encoded watch line (no object
+    tree for the garbage collector); a watch resuming from far back still gets them decoded."""
+    st = Store()
+    rt = st.types[("", "configmaps")]
+    n = Store.LIVE_EVENTS + 100
+    for i in range(n):
+        st.create(rt, "default", {"metadata": {"name": f"c{i}"}, "data": {"i": str(i)}})
+    evs = st.events_since(rt, 0)
+    assert len(evs) == n
+    assert evs[0]._obj is None and evs[-1]._obj is not None
+    assert [e.obj["data"]["i"] for e in evs] == [str(i) for i in range(n)]
+    assert sum(1 for e in st.log if e._obj is not None) == Store.LIVE_EVENTS
