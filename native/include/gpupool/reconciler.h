@@ -63,6 +63,10 @@ class PoolReconcilerBase {
  protected:
   // Writes ``status`` (unless semantically unchanged) with a fresh-GET retry on 409.
   void write_status_(const Json& obj, const Json& status);
+  // Throws a 409 when the pass read a stale copy whose status placement (nodeName/nodes) differs
+  // from the stored one, unless ``writing`` (an object carrying the status being written) already
+  // agrees with the stored placement.
+  static void stale_placement_check_(const Json& seen, const Json& fresh, const Json* writing = nullptr);
   // Adds/removes the finalizer with RV precondition; returns the updated object.
   Json edit_finalizers_(const Json& obj, bool add);
   Json ensure_finalizer_(const Json& obj);
@@ -117,6 +121,7 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
     std::vector<DeviceView> mine;
     int64_t free_healthy = 0;
     std::map<std::string, int64_t> free_by_node;   // free healthy GPUs per observed node
+    std::vector<std::string> unknown;              // unreachable nodes status did not name
   };
   Observed observe_(const ObjectMeta& m, const Mi355xPoolSpec& spec, const Json& status);
   // Nodes (reachable, selector-matching) with >= need free healthy GPUs, tightest fit first.

@@ -127,11 +127,35 @@ void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
       return;
     } catch (const KubeError& e) {
       if (!e.conflict()) throw;
-      cur = client_.get(res_, ns, name);  // fresh read, then re-apply our (re-derived) status
+      cur = client_.get(res_, ns, name);  // fresh read, then re-apply our status
       if (cur["status"] == status) return;
+      Json mine = Json::object();
+      mine["status"] = status;
+      stale_placement_check_(obj, cur, &mine);
     }
   }
   throw KubeError(409, "Conflict", "status update kept conflicting for " + ns + "/" + name);
+}
+
+// A pass observes where the pool's GPUs live from status.nodeName / status.nodes of the object it
+// read. When the informer served an object older than the stored one (it lags this reconciler's
+// own writes) and the stored placement differs, every conclusion of the pass may be wrong — e.g.
+// "no GPUs anywhere" when the named node's agent is down but the stale copy named no node. Such a
+// pass must not land its status or drop its finalizer: it fails with a conflict and re-runs on the
+// fresh object. Same placement — or a status write whose own placement matches the fresh one (the
+// pass found the GPUs where they are, the usual case right after this reconciler's own write) —
+// and the write is retried.
+void PoolReconcilerBase::stale_placement_check_(const Json& seen, const Json& fresh, const Json* writing) {
+  auto placement = [](const Json& o) {
+    std::vector<std::string> p{o.path("status.nodeName").as_string()};
+    for (const auto& n : o.path("status.nodes").elements()) p.push_back(n.as_string());
+    return p;
+  };
+  const auto now = placement(fresh);
+  if (placement(seen) != now && !(writing && placement(*writing) == now))
+    throw KubeError(409, "Conflict",
+                    "pass ran on a stale copy of " + fresh.path("metadata.namespace").as_string() + "/" +
+                        fresh.path("metadata.name").as_string() + " (status placement changed): re-running");
 }
 
 bool PoolReconcilerBase::own_status_write(const Json& obj) {
@@ -163,6 +187,7 @@ Json PoolReconcilerBase::edit_finalizers_(const Json& obj, bool add) {
     } catch (const KubeError& e) {
       if (!e.conflict() || attempt >= 3) throw;
       cur = client_.get(res_, m.ns, m.name);
+      if (!add) stale_placement_check_(obj, cur);  // removal was decided from obj's placement
     }
   }
 }
@@ -269,6 +294,8 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
         o.error = nv.error;
         o.node = n;
         if (hinted.count(n)) unreachable_hinted.push_back(n);
+      } else {
+        o.unknown.push_back(n);
       }
       continue;
     }
@@ -612,6 +639,16 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
   if (!o.reachable && !o.node.empty()) {
     write_status_(obj, build_status_(obj, m, spec, o, "Deleting", "agent unreachable", "", true));
     return Outcome::transient("agent unreachable during finalization: " + o.error);
+  }
+  // Status names no node (never placed, or a claim whose status write never landed) and some agent
+  // did not answer: it may hold GPUs of this pool, with pods on them. The finalizer stays until that
+  // agent answers or its node leaves the cluster — "all GPUs released" must be a fact, not a guess.
+  if (o.mine.empty() && o.nodes.empty() && !o.unknown.empty()) {
+    write_status_(obj, build_status_(obj, m, spec, o, "Deleting",
+                                     "waiting for unreachable agent(s) on " + join(o.unknown, ",") +
+                                         " to confirm no GPU of this pool is held",
+                                     "", true));
+    return Outcome::transient("agent(s) unreachable during finalization: " + join(o.unknown, ","));
   }
   std::vector<std::string> cordon;
   for (const auto& d : o.mine)

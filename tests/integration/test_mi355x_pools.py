@@ -236,6 +236,55 @@ def test_agent_crash_mid_probe_is_replaced(node8):
     assert d["state"] == "Quarantined" and "probe failed" in d["quarantine"]["reason"]
 
 
+def _deleting(k, name):
+    o = k.get(MI355XPOOLS, name, "default")
+    assert o["metadata"].get("deletionTimestamp") and o["metadata"].get("finalizers"), o["metadata"]
+    return o
+
+
+def test_delete_with_agent_down_waits_for_release(node8):
+    """Deleting a pool right after it turned ready, with its agent already dead: the finalizer
+    stays until the agent answers and the GPUs are really released. (A pass running on an
+    informer copy older than the pool's own status write saw no nodeName, skipped the dead
+    node as 'not ours' and removed the finalizer — GPUs still claimed on the agent.)"""
+    k = node8.client
+    o = k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    uid = o["metadata"]["uid"]
+    wait_ready(k, "p", 2)
+    node8._kill("agent-mi355x-node-0")
+    k.delete(MI355XPOOLS, "p", "default")
+    time.sleep(1.5)
+    st = _deleting(k, "p")["status"]
+    assert st.get("nodeName") == "mi355x-node-0", st
+    node8.start_agent(node8.nodes[0])
+    k.wait_for(MI355XPOOLS, "p", "default", lambda o: o is None, timeout=30)
+    assert not [d for d in agent_view(node8)["devices"] if d.get("poolUID") == uid]
+
+
+def test_delete_unplaced_pool_waits_for_unreachable_agent(node8):
+    """A pool whose status names no node (here: never placed) is deleted while an agent is down:
+    that agent could hold GPUs of the pool (a claim whose status write never landed), so the
+    finalizer stays — with a status saying which agent it waits for — until it answers."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("big", 9), "default")  # more than the node has
+    k.wait_for(MI355XPOOLS, "big", "default",
+               lambda o: conds(o).get("Ready", {}).get("reason") == "InsufficientDevices", timeout=30)
+    node8._kill("agent-mi355x-node-0")
+    # past the manager's agent-view cache age (5 s): the dead agent's last answer has expired, so
+    # the finalize pass must ask it — and gets no answer
+    time.sleep(5.5)
+    k.delete(MI355XPOOLS, "big", "default")
+
+    def waiting(o):
+        assert o is not None, "finalizer removed while the agent was unreachable"
+        return "unreachable agent(s) on mi355x-node-0" in conds(o).get("Progressing", {}).get("message", "")
+    k.wait_for(MI355XPOOLS, "big", "default", waiting, timeout=30)
+    time.sleep(0.5)
+    _deleting(k, "big")
+    node8.start_agent(node8.nodes[0])
+    k.wait_for(MI355XPOOLS, "big", "default", lambda o: o is None, timeout=30)
+
+
 def test_orphan_sweep_releases_claims_of_deleted_pool(cluster_factory):
     c = cluster_factory(manager_args=["--orphan-sweep", "500ms"])
     k = c.client
