@@ -75,6 +75,8 @@ class PoolReconcilerBase {
   void note_generation_(const ObjectMeta& m);  // starts the reconcile-to-Ready clock
   void observe_ready_(const ObjectMeta& m, bool ready, int64_t desired);
   void forget_(const std::string& uid);
+  // Placement (nodeName first, then nodes) of this manager's last status write for ``uid``.
+  std::vector<std::string> written_placement_(const std::string& uid);
 
   KubeClient& client_;
   Informer& pools_;
@@ -89,6 +91,9 @@ class PoolReconcilerBase {
   std::map<std::string, std::pair<int64_t, std::chrono::steady_clock::time_point>> pending_;
   std::map<std::string, int64_t> ready_gen_;
   std::map<std::string, std::string> own_rv_;  // uid -> resourceVersion of our last status write
+  // uid -> status.nodeName + status.nodes of our last status write: where this manager last put the
+  // pool, for passes that run on an informer copy from before that write (see observe_)
+  std::map<std::string, std::vector<std::string>> own_place_;
 };
 
 // The decision a Mi355xPool pass takes on its observed GPUs, before any RPC (pure; the C++

@@ -122,8 +122,12 @@ void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
     upd["status"] = status;
     try {
       Json out = client_.update(res_, ns, upd, "status");
+      std::vector<std::string> place{status["nodeName"].as_string()};
+      for (const auto& n : status["nodes"].elements()) place.push_back(n.as_string());
+      const std::string uid = out.path("metadata.uid").as_string();
       std::lock_guard<std::mutex> g(mu_);
-      own_rv_[out.path("metadata.uid").as_string()] = out.path("metadata.resourceVersion").as_string();
+      own_rv_[uid] = out.path("metadata.resourceVersion").as_string();
+      own_place_[uid] = std::move(place);
       return;
     } catch (const KubeError& e) {
       if (!e.conflict()) throw;
@@ -230,6 +234,13 @@ void PoolReconcilerBase::forget_(const std::string& uid) {
   pending_.erase(uid);
   ready_gen_.erase(uid);
   own_rv_.erase(uid);
+  own_place_.erase(uid);
+}
+
+std::vector<std::string> PoolReconcilerBase::written_placement_(const std::string& uid) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = own_place_.find(uid);
+  return it == own_place_.end() ? std::vector<std::string>{} : it->second;
 }
 
 namespace {
@@ -277,6 +288,14 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
   std::string hint = status["nodeName"].as_string();
   if (!hint.empty()) hinted.insert(hint);
   for (const auto& n : status["nodes"].elements()) hinted.insert(n.as_string());
+  // The informer may still hold a copy from before this manager's own last status write (a pass
+  // queued by that write's own watch event often runs first): where that write put the pool counts
+  // too. Without it a pass on the older copy (no nodeName yet) skips the pool's node when its agent
+  // is down — and concludes the pool holds nothing (scale-up elsewhere, or a finalizer removed).
+  const std::vector<std::string> wrote = written_placement_(m.uid);
+  if (hint.empty() && !wrote.empty()) hint = wrote[0];
+  for (const auto& n : wrote)
+    if (!n.empty()) hinted.insert(n);
   std::vector<std::string> nodes;
   if (span_nodes) {
     nodes = provider_.node_names();  // a spanning pool may hold GPUs on any agent: see them all

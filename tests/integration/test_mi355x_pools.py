@@ -261,6 +261,26 @@ def test_delete_with_agent_down_waits_for_release(node8):
     assert not [d for d in agent_view(node8)["devices"] if d.get("poolUID") == uid]
 
 
+def test_agent_down_right_after_ready_claims_nowhere_else(cluster_factory):
+    """Two nodes; the pool's agent dies just after the pool turned ready, and the pool is poked.
+    The passes that follow may run on an informer copy from before the manager's own status write
+    (no nodeName yet): they must still treat the pool's node as its home — blocked while that agent
+    is down — not see 'no GPUs anywhere' and claim a second set on the other node."""
+    c = cluster_factory(nodes=[NodeSpec("sn-a"), NodeSpec("sn-b")])
+    k = c.client
+    o = k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    uid = o["metadata"]["uid"]
+    home = wait_ready(k, "p", 2)["status"]["nodeName"]
+    other = "sn-b" if home == "sn-a" else "sn-a"
+    c._kill(f"agent-{home}")
+    for i in range(5):
+        k.patch(MI355XPOOLS, "p", {"metadata": {"labels": {"poke": str(i)}}}, "default")
+        time.sleep(0.05)
+    time.sleep(1.5)
+    assert not [d for d in agent_view(c, other)["devices"] if d.get("poolUID") == uid]
+    assert k.get(MI355XPOOLS, "p", "default")["status"].get("nodeName") == home
+
+
 def test_delete_unplaced_pool_waits_for_unreachable_agent(node8):
     """A pool whose status names no node (here: never placed) is deleted while an agent is down:
     that agent could hold GPUs of the pool (a claim whose status write never landed), so the
