@@ -167,6 +167,11 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
   // pool uid -> no spanning claim before this time: a rolled-back pass frees GPUs, whose capacity
   // event would otherwise wake the same pool into the same failing claim at once
   std::map<std::string, std::chrono::steady_clock::time_point> span_backoff_;
+  // uid -> nodes where a claim RPC failed in transport (reset, timeout): the agent may have
+  // committed it before the reply was lost. observe_ resolves them (adopt / release / forget).
+  std::map<std::string, std::set<std::string>> suspect_;
+  ClaimResult claim_(const std::string& node, const ClaimRequest& req);
+  void resolve_suspects_(const ObjectMeta& m, Observed& o);
 };
 
 class AzureVmPoolReconciler : public PoolReconcilerBase {

@@ -279,6 +279,66 @@ Mi355xPoolReconciler::Mi355xPoolReconciler(KubeClient& client, Informer& pools, 
                                            EventRecorder* events, ReconcilerOptions opts)
     : PoolReconcilerBase(client, pools, events, opts, "Mi355xPool", res::mi355xpools()), provider_(provider) {}
 
+ClaimResult Mi355xPoolReconciler::claim_(const std::string& node, const ClaimRequest& req) {
+  try {
+    return provider_.claim(node, req);
+  } catch (const ProviderError& e) {
+    if (e.code == "AgentUnreachable") {  // sent, but no reply: the agent may have committed it
+      std::lock_guard<std::mutex> g(mu_);
+      suspect_[req.pool_uid].insert(node);
+    }
+    throw;
+  }
+}
+
+// A claim whose reply was lost (the agent died or the connection reset after it committed) leaves
+// GPUs of a single-node pool on a node its status may never name: invisible to every later pass
+// and no orphan either (the pool lives). Each such node is asked once it answers: its GPUs become
+// the pool's when the pool holds none elsewhere, else they are released (never acknowledged, so
+// no pod can use them); a node without any is forgotten.
+void Mi355xPoolReconciler::resolve_suspects_(const ObjectMeta& m, Observed& o) {
+  std::set<std::string> sus;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = suspect_.find(m.uid);
+    if (it == suspect_.end()) return;
+    sus = it->second;
+  }
+  auto drop = [&](const std::string& n) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = suspect_.find(m.uid);
+    if (it == suspect_.end()) return;
+    it->second.erase(n);
+    if (it->second.empty()) suspect_.erase(it);
+  };
+  for (const auto& n : sus) {
+    if (!o.reachable) return;  // the pool's own node did not answer: nothing can be decided yet
+    if (n == o.node) {         // observed as the pool's node this pass: nothing hidden there
+      drop(n);
+      continue;
+    }
+    NodeView nv = provider_.observe_pool(n, m.uid);
+    if (!nv.reachable) continue;  // still unknown: ask again next pass
+    std::vector<DeviceView> got;
+    for (auto& d : nv.devices)
+      if (d.pool_uid == m.uid) got.push_back(std::move(d));
+    if (!got.empty() && o.mine.empty()) {
+      log_.warn("adopting GPUs of a claim whose reply was lost",
+                Json::object().set("pool", m.key()).set("node", n).set("count", static_cast<long long>(got.size())));
+      o.node = n;
+      o.mine = std::move(got);
+      o.free_healthy = nv.free_healthy >= 0 ? nv.free_healthy : 0;
+    } else if (!got.empty()) {
+      std::vector<std::string> uuids;
+      for (const auto& d : got) uuids.push_back(d.uuid);
+      log_.warn("releasing GPUs of a claim whose reply was lost",
+                Json::object().set("pool", m.key()).set("node", n).set("count", static_cast<long long>(uuids.size())));
+      provider_.release(n, m.uid, uuids);
+    }
+    drop(n);
+  }
+}
+
 Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& m, const Mi355xPoolSpec& spec,
                                                               const Json& status) {
   trace::Span span("observe");
@@ -340,6 +400,7 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
       if (!o.mine.empty()) break;
     }
   }
+  if (!span_nodes) resolve_suspects_(m, o);  // a spanning pool observes every node anyway
   std::sort(o.mine.begin(), o.mine.end(), [](const DeviceView& a, const DeviceView& b) {
     return a.node != b.node ? a.node < b.node : a.index < b.index;
   });
@@ -669,6 +730,17 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
                                      "", true));
     return Outcome::transient("agent(s) unreachable during finalization: " + join(o.unknown, ","));
   }
+  std::string lost;  // nodes of claims whose reply was lost and that have not answered since
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = suspect_.find(m.uid);
+    if (it != suspect_.end()) lost = join(std::vector<std::string>(it->second.begin(), it->second.end()), ",");
+  }
+  if (!lost.empty()) {
+    write_status_(obj, build_status_(obj, m, spec, o, "Deleting",
+                                     "waiting for agent(s) on " + lost + " (a claim reply was lost)", "", true));
+    return Outcome::transient("claim outcome unknown on " + lost);
+  }
   std::vector<std::string> cordon;
   for (const auto& d : o.mine)
     if (d.state != "Draining") cordon.push_back(d.uuid);
@@ -694,6 +766,7 @@ Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, co
     eviction_blocked_.erase(m.uid);
     policy_sent_.erase(m.uid);
     span_backoff_.erase(m.uid);
+    suspect_.erase(m.uid);
   }
   {
     std::lock_guard<std::mutex> g(quota_mu_);
@@ -852,7 +925,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
         req.resource_name = spec.resource_name;
         req.policy = spec.policy_json();
         req.probe = spec.probe_json();
-        ClaimResult cr = provider_.claim(step.first, req);
+        ClaimResult cr = claim_(step.first, req);
         if (!cr.ok) {
           fail_reason = cr.reason.empty() ? "InsufficientDevices" : cr.reason;
           fail_msg = step.first + ": " + cr.message;
@@ -918,7 +991,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
       req.policy = spec.policy_json();
       req.probe = spec.probe_json();
       auto t = clock_t_::now();
-      ClaimResult cr = provider_.claim(node, req);
+      ClaimResult cr = claim_(node, req);
       double claim_ms = std::chrono::duration<double, std::milli>(clock_t_::now() - t).count();
       if (!cr.ok) {
         const std::string reason = cr.reason.empty() ? "InsufficientDevices" : cr.reason;

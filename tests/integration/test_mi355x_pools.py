@@ -281,6 +281,36 @@ def test_agent_down_right_after_ready_claims_nowhere_else(cluster_factory):
     assert k.get(MI355XPOOLS, "p", "default")["status"].get("nodeName") == home
 
 
+def test_lost_claim_reply_neither_leaks_nor_double_claims(cluster_factory):
+    """Both agents die while claims are in flight (a pool scaled 1 -> 5 right after creation): a
+    claim the agent committed to its ledger before the connection reset survives the restart,
+    although the manager never got the reply. Such GPUs on a node the pool's status does not name
+    must be released (or adopted) — not stay claimed for a live pool that never sees them."""
+    c = cluster_factory(nodes=[NodeSpec("sn-a"), NodeSpec("sn-b")])
+    k = c.client
+    for it in range(3):
+        ns = f"lost{it}"
+        uid = k.create(MI355XPOOLS, mi_pool("p", 1), ns)["metadata"]["uid"]
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 5}}, ns)
+        for n in c.nodes:
+            c._kill(f"agent-{n.name}")
+        for n in c.nodes:
+            c.start_agent(n)
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 3}}, ns)
+        o = k.wait_for(MI355XPOOLS, "p", ns, ready_at(3), timeout=60)
+        held = {d["uuid"] for d in o["status"]["devices"]}
+        deadline = time.time() + 10
+        while True:
+            on_agents = {d["uuid"] for n in c.nodes for d in agent_view(c, n.name)["devices"]
+                         if d.get("poolUID") == uid}
+            if on_agents == held or time.time() > deadline:
+                break
+            time.sleep(0.1)
+        assert on_agents == held, (it, sorted(on_agents - held))
+        k.delete(MI355XPOOLS, "p", ns)
+        k.wait_for(MI355XPOOLS, "p", ns, lambda o: o is None, timeout=30)
+
+
 def test_delete_unplaced_pool_waits_for_unreachable_agent(node8):
     """A pool whose status names no node (here: never placed) is deleted while an agent is down:
     that agent could hold GPUs of the pool (a claim whose status write never landed), so the
