@@ -113,7 +113,8 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
                        ReconcilerOptions opts = {});
   Outcome reconcile(const std::string& ns, const std::string& name) override;
   // Releases claims whose pool no longer exists (manager restart / force-deleted CR).
-  void sweep_orphans();
+  // Returns (namespace, name) of pools to wake: GPUs of theirs sit on a node status does not name.
+  std::vector<std::pair<std::string, std::string>> sweep_orphans();
   // ResourceQuota cache; without one (or before it syncs) quota checks LIST from the API.
   void set_quota_informer(Informer* q) { quotas_ = q; }
 

@@ -1,6 +1,7 @@
 #include "gpupool/reconciler.h"
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -1160,15 +1161,41 @@ void Mi355xPoolReconciler::quota_settle_(const ObjectMeta& m, const Mi355xPoolSp
   h.reserved = 0;
 }
 
-void Mi355xPoolReconciler::sweep_orphans() {
+std::vector<std::pair<std::string, std::string>> Mi355xPoolReconciler::sweep_orphans() {
   std::set<std::string> live;
-  for (const auto& p : pools_.list()) live.insert(p.path("metadata.uid").as_string());
+  // single-node pools by uid -> (namespace, name, the node their status names)
+  std::map<std::string, std::array<std::string, 3>> single;
+  for (const auto& p : pools_.list()) {
+    const std::string uid = p.path("metadata.uid").as_string();
+    live.insert(uid);
+    const Mi355xPoolSpec spec = Mi355xPoolSpec::from(p["spec"]);
+    const std::string node = p.path("status.nodeName").as_string();
+    if (!spans_(spec) && !node.empty())
+      single[uid] = {p.path("metadata.namespace").as_string(), p.path("metadata.name").as_string(), node};
+  }
+  std::vector<std::pair<std::string, std::string>> wake;
   for (const auto& n : provider_.node_names()) {
     NodeView nv = provider_.observe(n);
     if (!nv.reachable) continue;
     std::map<std::string, std::vector<std::string>> orphans;
-    for (const auto& d : nv.devices)
+    std::set<std::string> misplaced;
+    for (const auto& d : nv.devices) {
       if (!d.pool_uid.empty() && !live.count(d.pool_uid) && d.pods.size() == 0) orphans[d.pool_uid].push_back(d.uuid);
+      auto it = single.find(d.pool_uid);
+      if (it != single.end() && it->second[2] != n) misplaced.insert(d.pool_uid);
+    }
+    // GPUs of a live single-node pool on a node its status does not name: a claim whose reply was
+    // lost before a manager restart (the in-memory record of it went with the old process). The
+    // pool's own pass decides — adopt or release — serialised with its other passes.
+    for (const auto& uid : misplaced) {
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        suspect_[uid].insert(n);
+      }
+      log_.warn("GPUs of a pool on a node its status does not name",
+                Json::object().set("node", n).set("poolUID", uid).set("pool", single[uid][0] + "/" + single[uid][1]));
+      wake.emplace_back(single[uid][0], single[uid][1]);
+    }
     for (const auto& kv : orphans) {
       log_.warn("releasing orphaned claims", Json::object().set("node", n).set("poolUID", kv.first).set("count", static_cast<long long>(kv.second.size())));
       try {
@@ -1178,6 +1205,7 @@ void Mi355xPoolReconciler::sweep_orphans() {
       }
     }
   }
+  return wake;
 }
 
 // ================================================================== AzureVmPool

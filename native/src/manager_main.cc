@@ -669,7 +669,7 @@ int main(int argc, char** argv) {
       if (want_mi && std::chrono::steady_clock::now() - last_sweep > std::chrono::milliseconds(f.orphan_sweep_ms)) {
         last_sweep = std::chrono::steady_clock::now();
         try {
-          mi.sweep_orphans();
+          for (const auto& key : mi.sweep_orphans()) ctl.enqueue("Mi355xPool", key.first, key.second);
         } catch (const std::exception& e) {
           log.warn("orphan sweep failed", Json::object().set("error", e.what()));
         }

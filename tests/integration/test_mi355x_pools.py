@@ -311,6 +311,30 @@ def test_lost_claim_reply_neither_leaks_nor_double_claims(cluster_factory):
         k.wait_for(MI355XPOOLS, "p", ns, lambda o: o is None, timeout=30)
 
 
+def test_sweep_finds_claims_on_a_node_status_does_not_name(cluster_factory):
+    """GPUs claimed for a live single-node pool on a node its status does not name — a lost claim
+    reply from before a manager restart, which no in-memory record remembers (simulated here by
+    claiming on the other agent directly). The sweep flags the node and wakes the pool, whose pass
+    releases them; the pool itself is untouched."""
+    c = cluster_factory(nodes=[NodeSpec("sn-a"), NodeSpec("sn-b")],
+                        manager_args=["--orphan-sweep", "300ms"])
+    k = c.client
+    uid = k.create(MI355XPOOLS, mi_pool("p", 2), "default")["metadata"]["uid"]
+    o = wait_ready(k, "p", 2)
+    home = o["status"]["nodeName"]
+    other = "sn-b" if home == "sn-a" else "sn-a"
+    r = c.agent_request(other, "POST", "/v1/claims", {"poolUID": uid, "pool": "default/p", "count": 3})
+    assert r["ok"] and len(r["devices"]) == 3
+    deadline = time.time() + 15
+    while [d for d in agent_view(c, other)["devices"] if d.get("poolUID") == uid]:
+        assert time.time() < deadline, "stray claims never released"
+        time.sleep(0.1)
+    o = k.get(MI355XPOOLS, "p", "default")
+    assert o["status"]["nodeName"] == home and o["status"]["readyReplicas"] == 2
+    assert {d["uuid"] for d in o["status"]["devices"]} == \
+        {d["uuid"] for d in agent_view(c, home)["devices"] if d.get("poolUID") == uid}
+
+
 def test_delete_unplaced_pool_waits_for_unreachable_agent(node8):
     """A pool whose status names no node (here: never placed) is deleted while an agent is down:
     that agent could hold GPUs of the pool (a claim whose status write never landed), so the
