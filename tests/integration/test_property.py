@@ -231,13 +231,16 @@ outage_op = st.one_of(
     st.tuples(st.just("delete"), st.just("")),
     st.tuples(st.just("create"), st.just("")),
     st.tuples(st.just("wait"), st.sampled_from([0.0, 0.02, 0.2])),
+    st.tuples(st.just("restart-manager"), st.just("")),
 )
 
 
 @pytest.fixture(scope="module")
 def outage(tmp_path_factory, native_built):
+    # the sweep runs every 2 s: a restarted manager forgets the claims whose reply it lost, and the
+    # sweep is what finds those again
     c = Cluster(str(tmp_path_factory.mktemp("outage")), nodes=[NodeSpec("on-a"), NodeSpec("on-b")],
-                sample_interval=0.2)
+                sample_interval=0.2, manager_args=["--orphan-sweep", "2s"])
     c.start()
     yield c
     c.stop()
@@ -247,11 +250,10 @@ def outage(tmp_path_factory, native_built):
                                                                  HealthCheck.too_slow])
 @given(ops=st.lists(outage_op, min_size=3, max_size=9), final=st.integers(1, 4))
 def test_agent_outages_never_leak_or_double_claim(outage, ops, final):
-    """Random replicas edits, pool deletes / re-creates and agent outages that last over several
-    operations, on two nodes (the default 30 s orphan sweep never runs within an example, so it
-    cannot hide a leak). Once every agent is back and the pool settles: the live pool's GPUs on
-    the agents are exactly its status.devices, all on one node; and no agent holds a GPU for a
-    pool that no longer exists (a finalizer removed while an agent was down would leave one)."""
+    """Random replicas edits, pool deletes / re-creates, manager restarts and agent outages that
+    last over several operations, on two nodes. Once every agent is back and the pool settles: the
+    live pool's GPUs on the agents are exactly its status.devices, all on one node; and no agent
+    holds a GPU for a pool that no longer exists."""
     c = outage
     k = c.client
     ns = f"o{int(time.time() * 1e6) % 10**9}"
@@ -287,6 +289,9 @@ def test_agent_outages_never_leak_or_double_claim(outage, ops, final):
             exists = True
         elif kind == "wait":
             time.sleep(v)
+        elif kind == "restart-manager":
+            c._kill("manager")
+            c.start_manager()
     for n in sorted(down):
         c.start_agent(by_name[n])
     if not exists:
@@ -295,15 +300,22 @@ def test_agent_outages_never_leak_or_double_claim(outage, ops, final):
     k.patch(MI355XPOOLS, "po", {"spec": {"replicas": final}}, ns)
     o = k.wait_for(MI355XPOOLS, "po", ns, ready_at(final), timeout=90)
     live = o["metadata"]["uid"]
-    held = {d["uuid"] for d in o["status"]["devices"]}
+    deadline = time.time() + 8  # a stray claim from before a manager restart waits for a sweep
+    while True:
+        o = k.get(MI355XPOOLS, "po", ns)
+        held = {d["uuid"] for d in o["status"]["devices"]}
+        mine, stale = set(), []
+        for n in c.nodes:
+            for d in c.agent_request(n.name, "GET", "/v1/node")["devices"]:
+                if d.get("poolUID") == live:
+                    mine.add(d["uuid"])
+                elif d.get("poolUID") in uids:
+                    stale.append((n.name, d["uuid"], d.get("state")))
+        if (mine == held and not stale) or time.time() > deadline:
+            break
+        time.sleep(0.2)
+    assert ready_at(final)(o)
     assert len({d["node"] for d in o["status"]["devices"]}) == 1, o["status"]["devices"]
-    mine, stale = set(), []
-    for n in c.nodes:
-        for d in c.agent_request(n.name, "GET", "/v1/node")["devices"]:
-            if d.get("poolUID") == live:
-                mine.add(d["uuid"])
-            elif d.get("poolUID") in uids:
-                stale.append((n.name, d["uuid"], d.get("state")))
     assert mine == held
     assert not stale, f"GPUs still held for deleted pools of this example: {stale}"
     k.delete(MI355XPOOLS, "po", ns)
