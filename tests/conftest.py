@@ -22,12 +22,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: multi-second integration test")
 
 
+def make_native(target: str, san: str = "", timeout: float | None = None):
+    """``make -C native`` under an exclusive file lock: pytest-xdist workers share one build tree,
+    and a worker relinking a binary another worker is executing fails that exec (ETXTBSY/EACCES)."""
+    import fcntl
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    argv = ["make", "-C", os.path.join(ROOT, "native")] + ([f"SAN={san}"] if san else []) + \
+        [target, "-j8"]
+    with open(os.path.join(ROOT, "build", ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        return subprocess.run(argv, capture_output=True, text=True, timeout=timeout)
+
+
 @pytest.fixture(scope="session")
 def native_built():
     """Build the native targets (host-only unless hipcc is present) once per session."""
     target = "all" if os.path.exists("/opt/rocm/bin/hipcc") else "host"
-    r = subprocess.run(["make", "-C", os.path.join(ROOT, "native"), target, "-j8"],
-                       capture_output=True, text=True)
+    r = make_native(target)
     if r.returncode != 0:
         pytest.fail("native build failed:\n" + r.stdout[-4000:] + r.stderr[-4000:])
     return os.path.join(ROOT, "build", "native")

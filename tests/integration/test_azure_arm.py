@@ -21,6 +21,7 @@ from gpupool.testing.arm_sim import ArmSim
 from gpupool.testing.cluster import make_test_pki
 
 from .helpers import cond_is, conds, settled_events
+from tests.conftest import make_native
 
 pytestmark = pytest.mark.slow
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -278,8 +279,7 @@ def test_arm_provider_under_sanitizer(san, arm, cluster_factory):
     ASan+UBSan and TSan builds of the manager, through scale up/down, throttling, a revoked token
     and a delete with leftover NIC/disk."""
     import subprocess
-    r = subprocess.run(["make", "-C", os.path.join(ROOT, "native"), f"SAN={san}", "host", "-j8"],
-                       capture_output=True, text=True, timeout=900)
+    r = make_native("host", san, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     os.environ["TSAN_OPTIONS"] = "halt_on_error=0:report_signal_unsafe=0"
     os.environ["ASAN_OPTIONS"] = "detect_leaks=0"

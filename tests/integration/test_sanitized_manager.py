@@ -11,6 +11,7 @@ import pytest
 from gpupool.kube import MI355XJOBS, MI355XPOOLS, PODS
 
 from .helpers import mi_pool, pause_pod, wait_ready
+from tests.conftest import make_native
 
 pytestmark = pytest.mark.slow
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -18,8 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 @pytest.mark.parametrize("san", ["tsan", "asan"])
 def test_manager_scenario_under_sanitizer(san, cluster_factory):
-    r = subprocess.run(["make", "-C", os.path.join(ROOT, "native"), f"SAN={san}", "host", "-j8"],
-                       capture_output=True, text=True, timeout=900)
+    r = make_native("host", san, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     os.environ["TSAN_OPTIONS"] = "halt_on_error=0:report_signal_unsafe=0"
     os.environ["ASAN_OPTIONS"] = "detect_leaks=0"

@@ -10,6 +10,7 @@ import sys
 import pytest
 
 from gpupool.apiserver_sim.store import ApiError, Store
+from tests.conftest import make_native
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -25,8 +26,7 @@ def test_cpp_unit_tests(native_built):
 @pytest.mark.parametrize("san", ["asan", "tsan"])
 def test_cpp_unit_tests_under_sanitizers(san):
     """SURVEY.md §5 race-detection row: host code under ASan+UBSan and TSan."""
-    r = subprocess.run(["make", "-C", os.path.join(ROOT, "native"), f"SAN={san}", "host", "-j8"],
-                       capture_output=True, text=True, timeout=900)
+    r = make_native("host", san, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
