@@ -159,6 +159,28 @@ def _span_p50(traces: list[dict]) -> dict:
     return out
 
 
+def _device_evidence(cs: list[dict]) -> dict:
+    """Per-N device-level numbers from the timed cycles' pool status: the claim-time probe per GPU
+    (the N probes of one claim run concurrently) and, for N >= 2, the xGMI peer ring of each claim
+    (every outgoing link's GB/s) and the pair coverage the rotating ring order reached."""
+    out: dict = {}
+    probe = [x for cy in cs for x in cy.get("probeMs") or [] if x]
+    if probe:
+        out["probe_ms_p50"] = round(statistics.median(probe), 3)
+        out["probe_ms_max"] = round(max(probe), 3)
+    links = [x for cy in cs for x in cy.get("xgmiGBps") or []]
+    if links:
+        out["xgmi_links_measured"] = len(links)
+        out["xgmi_link_GBps_min"] = round(min(links), 1)
+        out["xgmi_link_GBps_p50"] = round(statistics.median(links), 1)
+    pairs = [p for cy in cs for p in cy.get("xgmiPairs") or [] if p and p[1]]
+    if pairs and links:
+        last = cs[-1].get("xgmiPairs") or []
+        out["xgmi_pairs_covered_last"] = [p[0] for p in last]
+        out["xgmi_pairs_total"] = max(p[1] for p in pairs)
+    return out
+
+
 def _window(traces: list[dict], t0: float, t1: float) -> list[dict]:
     return [t for t in traces if t0 <= t["start"] <= t1]
 
@@ -306,6 +328,7 @@ def main() -> int:
         for k in sweep:
             cs = [cy for cy in cycles if cy["n"] == k]
             per_n[str(k)] = summary([cy["readySeconds"] for cy in cs], sum(cy["ok"] for cy in cs))
+            per_n[str(k)].update(_device_evidence(cs))
             if str(k) in errors:
                 per_n[str(k)]["errors"] = errors[str(k)]
                 first = errors[str(k)][0]

@@ -190,7 +190,15 @@ class BenchRun:
         return {"n": n, "readySeconds": t_ready, "ok": ok, "truth": truth,
                 "patchAt": patch_at, "readyAtWall": ready_at_wall, "patchRttMs": patch_rtt * 1e3,
                 "probeMs": [round(d.get("probe", {}).get("ms", 0.0), 3)
-                            for d in obj["status"]["devices"]]}
+                            for d in obj["status"]["devices"]],
+                # the xGMI peer ring of this claim (n >= 2): GB/s of each GPU's outgoing link as
+                # measured, and how many of the GPU's peer pairs have ever been checked
+                "xgmiGBps": [round(float((d.get("probe") or {})["xgmiGBps"]), 1)
+                             for d in obj["status"]["devices"]
+                             if isinstance((d.get("probe") or {}).get("xgmiGBps"), (int, float))],
+                "xgmiPairs": [[(d.get("xgmi") or {}).get("pairsCovered", 0),
+                               (d.get("xgmi") or {}).get("pairsTotal", 0)]
+                              for d in obj["status"]["devices"]]}
 
     # ------------------------------------------------------------ config 4
     def _pods(self, prefix: str, n: int, resource: str) -> list[str]:

@@ -36,6 +36,16 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
     for k, v in cfg["per_n"].items():
         assert v["accuracy"] == 1.0 and 0 < v["p50_s"] < 30, (k, v)
     assert out["value"] == cfg["per_n"]["8"]["p50_s"]
+    # device-level evidence per N: every claim's probe, and the xGMI ring of every multi-GPU
+    # claim (N links per claim of N GPUs), with the pair coverage the rotating order reached
+    for k, v in cfg["per_n"].items():
+        assert v["probe_ms_p50"] > 0, (k, v)
+        if int(k) >= 2:
+            assert v["xgmi_links_measured"] == int(k) * v["n"], (k, v)
+            assert v["xgmi_link_GBps_min"] > 0 and v["xgmi_pairs_total"] == 7, (k, v)
+            assert len(v["xgmi_pairs_covered_last"]) == int(k)
+        else:
+            assert "xgmi_links_measured" not in v
     assert cfg["readyReplicas_accuracy"] == 1.0
     # ground-truth time is reported apart from the operator's own time
     assert cfg["operator_ms_per_step"] + cfg["ground_truth_ms_per_step"] == \
