@@ -8,6 +8,12 @@ event-loop hop into an executor and back, which on the claim path cost two GIL h
 loop wake-up (profiles/r2am claim spans: executorIn + executorOut + aiohttp framing ~ 1 ms) — and
 the event long-poll simply waits on a condition variable. Request framing is minimal on purpose:
 Content-Length bodies (no chunked requests), keep-alive by default, ``Connection: close`` honoured.
+
+Exposure bounds (the TCP listener is reachable from the node network): at most ``max_conns``
+connections are served at once (more are closed on accept); a connection must finish its TLS
+handshake and its first request within ``first_request_timeout`` seconds, and stays bounded by it
+until a request is answered with something other than 401 — only then may it idle as a pooled
+keep-alive connection; a request refused for its token closes the connection.
 """
 from __future__ import annotations
 
@@ -42,8 +48,14 @@ def text_reply(text: str, status: int = 200) -> tuple:
 
 
 class RpcServer:
-    def __init__(self, routes: dict[tuple[str, str], Handler], token: str = ""):
+    def __init__(self, routes: dict[tuple[str, str], Handler], token: str = "",
+                 max_conns: int = 512, first_request_timeout: float = 10.0):
         self.routes = routes
+        self.max_conns = max_conns
+        self.first_request_timeout = first_request_timeout
+        self._conns = 0
+        self.refused_conns = 0
+        self._conns_mu = threading.Lock()
         self._auth = ("Bearer " + token).encode() if token else b""
         self._listeners: list[socket.socket] = []
         self._stop = threading.Event()
@@ -89,12 +101,31 @@ class RpcServer:
                 conn, _ = s.accept()
             except OSError:
                 return
+            with self._conns_mu:
+                full = self._conns >= self.max_conns
+                if full:
+                    self.refused_conns += 1
+                else:
+                    self._conns += 1
+            if full:
+                try:
+                    conn.close()
+                except OSError:
+                    pass
+                continue
             threading.Thread(target=self._serve_conn, args=(conn, ssl_ctx), daemon=True,
                              name="rpc-conn").start()
 
+    @property
+    def open_conns(self) -> int:
+        with self._conns_mu:
+            return self._conns
+
     # ------------------------------------------------------------ one connection
     def _serve_conn(self, conn: socket.socket, ssl_ctx) -> None:
+        trusted = False  # until a request is answered with something other than 401
         try:
+            conn.settimeout(self.first_request_timeout or None)  # handshake + first request
             if conn.family != socket.AF_UNIX:
                 conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             if ssl_ctx is not None:
@@ -126,6 +157,11 @@ class RpcServer:
                     not version.strip().upper().endswith("1.0")
                 t0 = time.perf_counter()
                 reply = self._dispatch(method.upper(), target, headers, body)
+                if reply[0] == 401:
+                    keep = False  # no second guess on this connection
+                elif not trusted:
+                    trusted = True
+                    conn.settimeout(None)  # a pooled keep-alive connection may idle from here
                 self._send(conn, reply, keep)
                 self._account(target.partition("?")[0], time.perf_counter() - t0)
                 if reply[3] is not None:
@@ -142,6 +178,8 @@ class RpcServer:
                 conn.close()
             except OSError:
                 pass
+            with self._conns_mu:
+                self._conns -= 1
 
     def _account(self, path: str, seconds: float) -> None:
         with self._stats_mu:
@@ -154,7 +192,8 @@ class RpcServer:
         manager's span for the same call minus this is transport + framing."""
         with self._stats_mu:
             items = sorted(self.stats.items())
-        out = []
+        out = [f"gpupool_agent_rpc_open_connections {self.open_conns}",
+               f"gpupool_agent_rpc_refused_connections_total {self.refused_conns}"]
         for path, (n, sec) in items:
             out.append(f'gpupool_agent_rpc_requests_total{{path="{path}"}} {n}')
             out.append(f'gpupool_agent_rpc_seconds_sum{{path="{path}"}} {sec:.6f}')
