@@ -656,7 +656,7 @@ class Store:
         cmd = cur["metadata"]
         keep = ""
         if subresource == "status":
-            merged = clone(cur)
+            merged = {k: clone(v) for k, v in cur.items() if k != "status"}  # status: replaced
             if "status" in new:
                 merged["status"] = new["status"]
             else:
