@@ -621,9 +621,6 @@ struct SweepBuf {
 struct DeviceCtx {
   hipStream_t stream = nullptr;   // HBM pattern test
   hipStream_t stream2 = nullptr;  // MFMA checks, overlapped with the bandwidth-bound HBM test
-  // the same pair with queue priorities (HBM test high, MFMA phase low): "streamPriority":1
-  hipStream_t stream_hi = nullptr;
-  hipStream_t stream2_lo = nullptr;
   hipEvent_t ev[1 + 2 * kMaxPatterns] = {};
   hipEvent_t gev[3] = {};         // GEMM timing + "counters zeroed" hand-off between the streams
   hipDeviceProp_t prop{};
@@ -839,10 +836,6 @@ std::string run_probe(int dev, const char* opts) {
   if (!ctx.ready) {
     PROBE_CHECK(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
     PROBE_CHECK(hipStreamCreateWithFlags(&ctx.stream2, hipStreamNonBlocking));
-    int least = 0, greatest = 0;
-    PROBE_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    PROBE_CHECK(hipStreamCreateWithPriority(&ctx.stream_hi, hipStreamNonBlocking, greatest));
-    PROBE_CHECK(hipStreamCreateWithPriority(&ctx.stream2_lo, hipStreamNonBlocking, least));
     for (auto& e : ctx.ev) PROBE_CHECK(hipEventCreate(&e));
     for (auto& e : ctx.gev) PROBE_CHECK(hipEventCreate(&e));
     PROBE_CHECK(hipGetDeviceProperties(&ctx.prop, dev));
@@ -850,8 +843,7 @@ std::string run_probe(int dev, const char* opts) {
     PROBE_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ctx.host_res), kResSlots * sizeof(unsigned long long)));
     ctx.ready = true;
   }
-  const bool prio = opt_int(opts, "streamPriority", 0) != 0;  // in-process A/B
-  hipStream_t s = prio ? ctx.stream_hi : ctx.stream;
+  hipStream_t s = ctx.stream;
   const hipDeviceProp_t& prop = ctx.prop;
   const int cus = prop.multiProcessorCount;
   auto ms_since = [](std::chrono::steady_clock::time_point a) {
@@ -900,7 +892,7 @@ std::string run_probe(int dev, const char* opts) {
   PROBE_CHECK(hipMemsetAsync(cnt, 0, kResSlots * sizeof(unsigned long long), s));
   for (int pi = 0; pi < patterns; ++pi)
     PROBE_CHECK(hipMemsetAsync(cnt + 2 * pi + 1, 0xFF, sizeof(unsigned long long), s));
-  hipStream_t s2 = overlap ? (prio ? ctx.stream2_lo : ctx.stream2) : s;
+  hipStream_t s2 = overlap ? ctx.stream2 : s;
   if (overlap) {
     PROBE_CHECK(hipEventRecord(ctx.gev[2], s));
     PROBE_CHECK(hipStreamWaitEvent(s2, ctx.gev[2], 0));
