@@ -285,6 +285,7 @@ def main() -> int:
             run.gt_s = 0.0
     _barrier(world)
     t_start = time.perf_counter()
+    last_progress = t_start
     if rank == 0 and pool_ok:
         for step in range(args.steps):
             if budget_left() <= 0:
@@ -307,6 +308,10 @@ def main() -> int:
                     if not pool_ok:
                         break
             timed_steps += 1
+            if time.perf_counter() - last_progress > 20.0:  # a long run shows it is alive
+                last_progress = time.perf_counter()
+                print(f"# timed step {step + 1}/{args.steps}, {len(cycles)} cycles, "
+                      f"{time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
             if not pool_ok:
                 skipped["timed_steps"] = f"{args.steps - step - 1} of {args.steps} not started: " \
                                          "the bench pool could not be recovered"
