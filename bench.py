@@ -284,6 +284,7 @@ def main() -> int:
         if run:
             run.gt_s = 0.0
     _barrier(world)
+    footprint_before = run.footprint() if rank == 0 and run else {}
     t_start = time.perf_counter()
     last_progress = t_start
     if rank == 0 and pool_ok:
@@ -318,6 +319,7 @@ def main() -> int:
                 break
     _barrier(world)
     elapsed = _gather_max(world, time.perf_counter() - t_start)
+    footprint_after = run.footprint() if rank == 0 and run else {}
 
     if rank == 0:
         from gpupool.bench.runner import summary
@@ -504,6 +506,8 @@ def main() -> int:
                 "sample_interval_s": args.sample_interval,
                 "health_poll_interval_s": 0.1,
                 "agent": agent_stats,
+                # agent + manager resident memory / threads / fds around the timed region
+                "footprint": {"before_timed": footprint_before, "after_timed": footprint_after},
                 "world_size": world,
                 "claim_pass_span_p50_ms": span_per_n.get(str(value_n), {}),
                 "claim_pass_span_p50_ms_per_n": span_per_n,

@@ -101,6 +101,24 @@ def now_rfc3339() -> str:
     return _dt.datetime.now(_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
 
 
+def process_metrics() -> list[str]:
+    """Prometheus' standard process metrics from /proc/self (resident memory, CPU time, threads,
+    open fds), as the client libraries' process collector exports them."""
+    out = []
+    try:
+        with open("/proc/self/statm") as f:
+            out.append(f"process_resident_memory_bytes {int(f.read().split()[1]) * os.sysconf('SC_PAGESIZE')}")
+        with open("/proc/self/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        out.append(f"process_cpu_seconds_total "
+                   f"{(int(fields[11]) + int(fields[12])) / os.sysconf('SC_CLK_TCK'):.3f}")
+        out.append(f"process_threads {int(fields[17])}")
+        out.append(f"process_open_fds {len(os.listdir('/proc/self/fd'))}")
+    except (OSError, IndexError, ValueError):
+        pass
+    return out
+
+
 @dataclass
 class AgentConfig:
     node: str = field(default_factory=socket.gethostname)
@@ -1788,6 +1806,7 @@ class Agent:
             for k, v in self.scrubber.stats.items():
                 lines.append(f"gpupool_agent_hbm_scrub_{k}_total {v}")
             lines.append(f"gpupool_agent_gen {self.gen}")
+        lines += process_metrics()
         return "\n".join(lines) + "\n"
 
     # ================================================================ lifecycle

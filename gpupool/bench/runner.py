@@ -482,6 +482,27 @@ class BenchRun:
                 "fault_kinds": list(self.FAULT_KINDS),
                 "mismatches": [x for x in samples if not x["ok"]][:5]}
 
+    def footprint(self) -> dict:
+        """Resident memory (MiB), threads and open fds of the node agent and the manager, from
+        their /metrics process_* lines: taken before and after the timed region, a leak or a
+        thread pile-up over many claim/release cycles shows as growth."""
+        out = {}
+        for who, get in (("agent", lambda: self.cluster.agent_request(self.node.name, "GET", "/metrics")),
+                         ("manager", self.cluster.manager_metrics)):
+            try:
+                vals = {}
+                for line in str(get()).splitlines():
+                    if line.startswith("process_"):
+                        k, _, v = line.partition(" ")
+                        vals[k] = float(v)
+                out[who] = {"rss_mib": round(vals.get("process_resident_memory_bytes", 0) / 2**20, 1),
+                            "threads": int(vals.get("process_threads", 0)),
+                            "open_fds": int(vals.get("process_open_fds", 0)),
+                            "cpu_s": round(vals.get("process_cpu_seconds_total", 0.0), 2)}
+            except Exception as e:  # never fail the bench over a diagnostic
+                out[who] = {"error": repr(e)[:200]}
+        return out
+
     def agent_stats(self) -> dict:
         """The agent's own counters (gpupool_agent_*): sample / health-poll cost, events."""
         text = self.cluster.agent_request(self.node.name, "GET", "/metrics")

@@ -1,8 +1,12 @@
 #include "gpupool/metrics.h"
 
+#include <dirent.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <stdexcept>
 
 namespace gpupool {
@@ -161,10 +165,55 @@ HistogramVec& Registry::histogram(const std::string& name, const std::string& he
   return static_cast<HistogramVec&>(*metrics_.back());
 }
 
+// Prometheus' standard process metrics (the client libraries' process collector) from /proc/self:
+// resident memory, CPU time, threads and open file descriptors — a leak or a thread pile-up in a
+// long-running manager shows on the dashboard before it shows as an outage.
+static void render_process(std::string& out) {
+  long pages = 0, resident = 0;
+  if (FILE* f = std::fopen("/proc/self/statm", "r")) {
+    if (std::fscanf(f, "%ld %ld", &pages, &resident) != 2) resident = 0;
+    std::fclose(f);
+  }
+  double cpu_s = 0;
+  long threads = 0;
+  if (FILE* f = std::fopen("/proc/self/stat", "r")) {
+    char buf[2048];
+    size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    if (const char* p = std::strrchr(buf, ')')) {  // fields restart after the command name
+      unsigned long utime = 0, stime = 0;
+      long nthreads = 0;
+      // state ppid pgrp session tty tpgid flags minflt cminflt majflt cmajflt utime stime cutime cstime
+      // priority nice num_threads
+      if (std::sscanf(p + 2, "%*c %*d %*d %*d %*d %*d %*u %*u %*u %*u %*u %lu %lu %*d %*d %*d %*d %ld",
+                      &utime, &stime, &nthreads) == 3) {
+        cpu_s = static_cast<double>(utime + stime) / static_cast<double>(sysconf(_SC_CLK_TCK));
+        threads = nthreads;
+      }
+    }
+  }
+  long fds = 0;
+  if (DIR* d = opendir("/proc/self/fd")) {
+    while (struct dirent* e = readdir(d))
+      if (e->d_name[0] != '.') ++fds;
+    closedir(d);
+  }
+  char line[512];
+  std::snprintf(line, sizeof line,
+                "# TYPE process_resident_memory_bytes gauge\nprocess_resident_memory_bytes %ld\n"
+                "# TYPE process_cpu_seconds_total counter\nprocess_cpu_seconds_total %.3f\n"
+                "# TYPE process_threads gauge\nprocess_threads %ld\n"
+                "# TYPE process_open_fds gauge\nprocess_open_fds %ld\n",
+                resident * sysconf(_SC_PAGESIZE), cpu_s, threads, fds);
+  out += line;
+}
+
 std::string Registry::render() const {
   std::lock_guard<std::mutex> g(mu_);
   std::string out;
   for (const auto& m : metrics_) m->render(out);
+  render_process(out);
   return out;
 }
 

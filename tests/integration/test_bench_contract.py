@@ -47,6 +47,11 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
         else:
             assert "xgmi_links_measured" not in v
     assert cfg["readyReplicas_accuracy"] == 1.0
+    # agent + manager footprint around the timed region (Prometheus process_* metrics)
+    for when in ("before_timed", "after_timed"):
+        for who in ("agent", "manager"):
+            fp = cfg["footprint"][when][who]
+            assert fp["rss_mib"] > 0 and fp["threads"] > 0 and fp["open_fds"] > 0, (when, who, fp)
     # ground-truth time is reported apart from the operator's own time
     assert cfg["operator_ms_per_step"] + cfg["ground_truth_ms_per_step"] == \
         pytest.approx(out["ms_per_step"], abs=0.05)
