@@ -163,7 +163,7 @@ def test_alert_rules_use_exported_metrics():
     rules = [r for g in doc["spec"]["groups"] for r in g["rules"]]
     assert len(rules) >= 8
     for r in rules:
-        for m in re.findall(r"gpupool_[a-z_]+", r["expr"]):
+        for m in re.findall(r"(?:gpupool|process)_[a-z_]+", r["expr"]):
             assert m in src, (r["alert"], m)
     for label in ('"uncorrectable"', '"hotspot"', '"error"', '"terminal"', 'state="{t}"'):
         assert label in src, label
