@@ -281,5 +281,6 @@ def test_utilisation_metrics_agent_and_pool(cluster_factory):
     exprs = " ".join(t["expr"] for p in dash["panels"] for t in p.get("targets", []))
     for name in ("gpupool_pool_gfx_activity_percent", "gpupool_device_vram_used_bytes",
                  "gpupool_ready_replicas", "gpupool_pod_vram_bytes", "gpupool_pod_gfx_busy_ratio",
-                 "gpupool_namespace_quota_units", "gpupool_device_xgmi_pairs_covered"):
+                 "gpupool_namespace_quota_units", "gpupool_device_xgmi_pairs_covered",
+                 "process_resident_memory_bytes", "process_threads"):
         assert name in exprs
