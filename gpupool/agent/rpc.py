@@ -113,8 +113,17 @@ class RpcServer:
                 except OSError:
                     pass
                 continue
-            threading.Thread(target=self._serve_conn, args=(conn, ssl_ctx), daemon=True,
-                             name="rpc-conn").start()
+            try:
+                threading.Thread(target=self._serve_conn, args=(conn, ssl_ctx), daemon=True,
+                                 name="rpc-conn").start()
+            except RuntimeError:  # no thread to be had: drop this connection, keep accepting
+                with self._conns_mu:
+                    self._conns -= 1
+                    self.refused_conns += 1
+                try:
+                    conn.close()
+                except OSError:
+                    pass
 
     @property
     def open_conns(self) -> int:
