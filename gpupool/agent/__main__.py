@@ -68,6 +68,13 @@ def main() -> None:
                          "returning from the HIP probe (GIL released) waits this long behind a "
                          "busy thread, e.g. the ledger writer encoding in the probe's shadow: "
                          "0.58 ms at 500 us, 0.08 ms at 50 us (profiles/r3o_probe_call_gil.json)")
+    ap.add_argument("--hbm-reserve", type=int, default=2 << 30,
+                    help="HBM bytes per GPU the agent keeps for itself (HIP context + probe "
+                         "arena): a shared pool whose replicasPerGPU x hbmBytesPerSlot does not "
+                         "fit beside it is refused (SharingOvercommitted)")
+    ap.add_argument("--share-acct-grace", type=float, default=10.0,
+                    help="an isolated slot's HBM account file younger than this (s) is kept even "
+                         "if the kubelet does not list its pod yet")
     ap.add_argument("--xgmi-recheck", type=float, default=600.0,
                     help="idle xGMI coverage ring period over pod-free GPUs, seconds (0 = off)")
     ap.add_argument("--inject-claim-delay", default="",
@@ -98,7 +105,8 @@ def main() -> None:
                       scrub_interval_s=a.scrub_interval, scrub_window_bytes=a.scrub_window,
                       scrub_windows=a.scrub_windows, scrub_reserve_bytes=a.scrub_reserve,
                       scrub_start_delay_s=a.scrub_start_delay,
-                      xgmi_recheck_s=a.xgmi_recheck,
+                      xgmi_recheck_s=a.xgmi_recheck, hbm_reserve_bytes=a.hbm_reserve,
+                      share_acct_grace_s=a.share_acct_grace,
                       inject_claim_delay=_count_seconds(a.inject_claim_delay))
     agent = Agent(cfg)
     try:

@@ -28,6 +28,7 @@ from typing import Any
 
 from ..api import schema
 from ..ops import devlib
+from . import slots as slotlib
 from .ledger import Ledger
 from .prober import Prober, default_mode
 
@@ -156,6 +157,10 @@ class AgentConfig:
     xgmi_recheck_s: float = 600.0     # idle xGMI coverage ring period (0 = off)
     xgmi_recheck_bytes: int = 16 << 20
     inject_claim_delay: tuple = (0, 0.0)  # (min count, seconds): fault injection for tests/bench
+    # HBM the agent keeps for itself on every GPU (HIP context ~668 MiB, profiles/
+    # r2q_agent_footprint_real.json, + the ~1.15 GiB probe arena): slot budgets must fit beside it
+    hbm_reserve_bytes: int = 2 << 30
+    share_acct_grace_s: float = 10.0  # an HBM account younger than this is never garbage-collected
 
 
 class Agent:
@@ -185,6 +190,8 @@ class Agent:
                                                  "the claim-time probe"}
         if interrupted:
             self.ledger.commit(self.records)
+        self.share_lib_dir = self._install_share_lib()
+        self._pod_ids: tuple[float, set[str]] | None = None  # (listed at, device IDs pods hold)
         self.snap = self.dev.snapshot()
         self.backend = self.snap.get("backend", cfg.backend)
         self.by_uuid = {d["uuid"]: d for d in self.snap["devices"]}
@@ -429,6 +436,7 @@ class Agent:
             if self._podres is not None:
                 try:
                     self._refresh_pods()
+                    self.gc_share_accounts()
                 except Exception as e:
                     log.debug("podresources list failed: %s", e)
             try:
@@ -835,7 +843,10 @@ class Agent:
 
     def _refresh_pods(self) -> dict[str, list[dict]]:
         pods: dict[str, list[dict]] = {}
-        for did, ps in self._podres.list_pod_devices().items():
+        listed_at = time.time()
+        listing = self._podres.list_pod_devices()
+        self._pod_ids = (listed_at, set(listing))  # slot-level: the HBM-account GC's input
+        for did, ps in listing.items():
             pods.setdefault(gpu_of(did), []).extend(ps)  # a shared GPU's slots -> the GPU
         with self.lock:
             old = self._pods_cache[1]
@@ -903,6 +914,13 @@ class Agent:
             out["xgmiPairs"] = xs
         if self.pod_usage.get(uuid):
             out["usage"] = self.pod_usage[uuid]
+        if rec and self._slots_of(rec) > 1:
+            lay = self._slot_layout(uuid, rec)
+            masks = lay.pop("masks", None)
+            if masks is not None:  # per slot: its CU-mask bits and the XCDs they land on
+                lay["slotCUMasks"] = [_ranges(m) for m in masks]
+                lay["slotXcds"] = [_ranges(slotlib.slot_xcds(m, lay["xcds"])) for m in masks]
+            out["sharing"] = lay
         out["telemetry"] = self._telemetry(d)
         if not rec:
             q = self.ledger.quarantined().get(uuid) if self.ledger else None
@@ -1010,8 +1028,14 @@ class Agent:
             # claimability under the requesting pool's policy (baseline = now: retired HBM pages
             # and absolute limits count, deltas start at the claim); no partition of the same ASIC
             # may carry a package-level fault (checked above)
+            sharing = policy.get("sharing") or {}
+            overcommitted = ""
             for d, ok in zip(cand, self._claimable(cand, policy, policy_key)):
-                if ok:
+                why = slotlib.overcommit(sharing, int(d.get("memTotalBytes") or 0),
+                                         self.cfg.hbm_reserve_bytes) if ok else ""
+                if why:
+                    overcommitted = why
+                elif ok:
                     free.append(d["index"])
             owned = [self.by_uuid[u]["index"] for u, r in self.records.items()
                      if r["poolUID"] == pool_uid and u in self.by_uuid]
@@ -1028,6 +1052,9 @@ class Agent:
                                                          key=lambda x: x["index"])]
                 sel = devlib.select(count, free, owned, req.get("topologyPolicy", "xgmi-packed"),
                                     weights, numa)
+            if len(sel) < count and overcommitted:
+                return {"ok": False, "reason": "SharingOvercommitted",
+                        "message": f"{overcommitted} on {self.cfg.node}", "devices": []}
             if len(sel) < count:
                 return {"ok": False, "reason": "InsufficientDevices",
                         "message": f"need {count} free healthy GPU(s) on {self.cfg.node}, "
@@ -1574,8 +1601,7 @@ class Agent:
                 envs["GPUPOOL_GPU_SLOTS"] = ",".join(slots)
                 envs.update(self._isolation_env(slots, mounts))
         if "GPUPOOL_HBM_LIMIT_BYTES" in envs:  # the pod-wide HBM account (file I/O: off the lock)
-            acct = self._share_account(slots, int(envs["GPUPOOL_HBM_LIMIT_BYTES"]),
-                                       len(ids))
+            acct = self._share_account(slots, int(envs["GPUPOOL_HBM_LIMIT_BYTES"]), ids)
             if acct:
                 mounts.append({"container_path": self.SHARE_ACCOUNT_PATH, "host_path": acct,
                                "read_only": False})
@@ -1585,15 +1611,58 @@ class Agent:
 
     SHARE_LIB_DIR = "/opt/gpupool/lib"  # where the pod sees libgpupool_share.so
     SHARE_ACCOUNT_PATH = "/var/run/gpupool/share.acct"  # where it sees its pod's HBM account
-    # the account file libgpupool_share.so maps (native/src/share/share.cc, struct Account)
-    _ACCT_BYTES, _ACCT_IDS_AT = 16384, 8192
+    SHARE_LIB = "libgpupool_share.so"
 
-    def _share_account(self, slots: list[str], limit: int, ngpus: int) -> str | None:
+    def _install_share_lib(self) -> str | None:
+        """Copy libgpupool_share.so from the agent's own tree (in the image) into
+        ``<state_dir>/lib``. The state dir is the DaemonSet's hostPath (/var/lib/gpupool), so the
+        copy exists on the HOST, where the container runtime resolves an Allocate mount's host
+        path — the image path it came from does not. Atomic (temp file + rename); a copy whose
+        bytes already match is kept, so pods that mapped it keep a stable inode. Returns the
+        host directory, or None (isolated slots then fail their Allocate, loudly)."""
+        from ..ops import native_dir
+        src = os.path.join(native_dir(), self.SHARE_LIB)
+        dst_dir = os.path.join(self.cfg.state_dir, "lib")
+        dst = os.path.join(dst_dir, self.SHARE_LIB)
+        try:
+            with open(src, "rb") as f:
+                data = f.read()
+        except OSError as e:
+            log.warning("isolated GPU sharing unavailable: %s not readable (%s)", src, e)
+            return None
+        try:
+            os.makedirs(dst_dir, exist_ok=True)
+            try:
+                with open(dst, "rb") as f:
+                    if f.read() == data:
+                        return dst_dir
+            except OSError:
+                pass
+            tmp = f"{dst}.{os.getpid()}.tmp"
+            with open(tmp, "wb") as f:
+                f.write(data)
+                f.flush()
+                os.fsync(f.fileno())
+            os.chmod(tmp, 0o755)
+            os.replace(tmp, dst)
+            return dst_dir
+        except OSError as e:
+            log.warning("isolated GPU sharing unavailable: cannot install %s (%s)", dst, e)
+            return None
+
+    def share_mounts(self) -> list[str]:
+        """Every host path an Allocate may mount (the deploy manifest must declare hostPath
+        volumes covering them; tests/unit/test_deploy_manifests.py checks it)."""
+        return [os.path.join(self.cfg.state_dir, "lib"), os.path.join(self.cfg.state_dir, "share")]
+
+    def _share_account(self, slots: list[str], limit: int, gpus: list[str]) -> str | None:
         """One HBM account per allocation, shared by every process of the container: 16 KiB,
-        magic + per-GPU limit, zeroed counters, the slot ids as text at 8 KiB. A slot belongs to
-        one container at a time, so an earlier account naming any of these slots belongs to a
-        container that is gone: it is deleted here. Returns the host path (None if the state
-        directory is not writable: the budget is then per process)."""
+        magic + per-GPU limit + the GPUs' HIP UUIDs (what the library matches each HSA agent
+        against, so ranks with different ROCR_VISIBLE_DEVICES charge the same counter for the same
+        GPU), zeroed counters, the slot ids as text. A slot belongs to one container at a time, so
+        an earlier account naming any of these slots belongs to a container that is gone: it is
+        deleted here (and by the sampler once the kubelet lists none of its slots). Returns the
+        host path (None if the state directory is not writable: the budget is then per process)."""
         d = os.path.join(self.cfg.state_dir, "share")
         mine = set(slots)
         try:
@@ -1602,22 +1671,14 @@ class Agent:
                 if not name.endswith(".acct"):
                     continue
                 path = os.path.join(d, name)
-                try:
-                    with open(path, "rb") as f:
-                        f.seek(self._ACCT_IDS_AT)
-                        ids = f.read().split(b"\0", 1)[0].decode(errors="replace").split(",")
-                except OSError:
-                    continue
-                if mine & set(ids):
+                if mine & set(slotlib.account_slots(path) or ()):
                     os.unlink(path)
-            buf = bytearray(self._ACCT_BYTES)
-            buf[0:24] = b"GPSHARE1" + struct.pack("<QII", int(limit), 1, int(ngpus))
-            text = ",".join(slots).encode()[: self._ACCT_BYTES - self._ACCT_IDS_AT - 1]
-            buf[self._ACCT_IDS_AT:self._ACCT_IDS_AT + len(text)] = text
+            with self.lock:
+                uuids = [(self.by_uuid.get(u) or {}).get("hipUUID") or "" for u in gpus]
             path = os.path.join(d, f"{uuid4().hex}.acct")
             fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o666)
             try:
-                os.write(fd, bytes(buf))
+                os.write(fd, slotlib.account_bytes(limit, slots, uuids))
                 os.fchmod(fd, 0o666)  # pods may run as any user
             finally:
                 os.close(fd)
@@ -1626,42 +1687,80 @@ class Agent:
             log.warning("HBM account for %s not created (%s): budget is per process", slots, e)
             return None
 
+    def gc_share_accounts(self, now: float | None = None) -> list[str]:
+        """Delete the HBM accounts of pods that are gone: no device ID the kubelet's last
+        PodResources listing shows is one of the account's slots. Runs every sample period."""
+        pod_ids = self._pod_ids
+        if pod_ids is None:
+            return []
+        listed_at, live = pod_ids
+        # an account made after that listing began may belong to a pod it could not show yet
+        cutoff = min(listed_at, (now or time.time()) - self.cfg.share_acct_grace_s)
+        gone = slotlib.gc_accounts(os.path.join(self.cfg.state_dir, "share"), live, cutoff)
+        if gone:
+            log.info("removed %d HBM account(s) of exited pods", len(gone))
+        return gone
+
+    def _slot_layout(self, uuid: str, rec: dict) -> dict:
+        """The isolation a GPU's slots get under its pool's spec.sharing: per-slot CU-mask bits and
+        layout (xcd | striped), the enforced per-slot HBM budget. Called under self.lock."""
+        share = (rec.get("policy") or {}).get("sharing") or {}
+        k = self._slots_of(rec)
+        d = self.by_uuid.get(uuid) or {}
+        out: dict = {"replicasPerGPU": k}
+        per_slot = int(share.get("hbmBytesPerSlot") or 0)
+        if per_slot > 0:
+            # never more than a fair share of what the agent leaves free, whatever the spec says
+            # (claims of an overcommitted pool are refused; this covers a later spec edit)
+            mem = int(d.get("memTotalBytes") or 0)
+            if mem > 0:
+                per_slot = min(per_slot, max(0, mem - self.cfg.hbm_reserve_bytes) // k)
+            out["hbmBytesPerSlot"] = per_slot
+        cu = int(share.get("cuPerSlot") or 0)
+        if cu > 0:
+            cus = int((d.get("asic") or {}).get("computeUnits") or 256)
+            xcds = slotlib.xcd_count(d)
+            masks, layout = [], "striped"
+            for i in range(k):
+                bits, layout = slotlib.slot_cus(i, k, cu, cus, xcds)
+                masks.append(bits)
+            out.update({"cuLayout": layout, "cuPerSlot": len(masks[0]), "xcds": xcds,
+                        "masks": masks})
+        return out
+
     def _isolation_env(self, slots: list[str], mounts: list[dict]) -> dict[str, str]:
         """spec.sharing.hbmBytesPerSlot / cuPerSlot of the pool owning these slots: the ROCm
         runtime loads libgpupool_share.so (HSA_TOOLS_LIB) into the pod, which caps its HBM per
         GPU at (its slots on that GPU) x hbmBytesPerSlot and confines its queues to its slots'
-        CUs — slot i of a GPU owns CU-mask bits [i*cuPerSlot, (i+1)*cuPerSlot), disjoint from
-        the other slots (narrowed to the GPU's own CU count, e.g. a 32-CU CPX partition).
-        Called under self.lock."""
+        CUs — whole XCDs per slot when they divide evenly (each slot then has its own L2s), else
+        contiguous mask bits; disjoint from the other slots either way (slots.py). The library
+        is mounted from its host copy under the state dir. Called under self.lock."""
         per_gpu: dict[str, list[int]] = {}
         for sid in slots:
             u, _, i = sid.partition(SLOT_SEP)
             per_gpu.setdefault(u, []).append(int(i or 0))
-        hbm, cu_mask = 0, set()
+        hbm, cu_mask, layouts = 0, set(), set()
         for u, idx in per_gpu.items():
-            rec = self.records.get(u) or {}
-            share = (rec.get("policy") or {}).get("sharing") or {}
-            k = self._slots_of(rec)
-            per_slot_hbm = int(share.get("hbmBytesPerSlot") or 0)
-            cu = int(share.get("cuPerSlot") or 0)
-            if per_slot_hbm > 0:
-                hbm = max(hbm, per_slot_hbm * len(idx))
-            if cu > 0:
-                cus = int(((self.by_uuid.get(u) or {}).get("asic") or {}).get("computeUnits")
-                          or 256)
-                cu = max(1, min(cu, cus // k))
+            lay = self._slot_layout(u, self.records.get(u) or {})
+            if lay.get("hbmBytesPerSlot"):
+                hbm = max(hbm, lay["hbmBytesPerSlot"] * len(idx))
+            if "masks" in lay:
+                layouts.add(lay["cuLayout"])
                 for i in idx:
-                    cu_mask.update(range(i * cu, (i + 1) * cu))
+                    cu_mask.update(lay["masks"][i % len(lay["masks"])])
         if not hbm and not cu_mask:
             return {}
-        from ..ops import native_dir
-        mounts.append({"container_path": self.SHARE_LIB_DIR, "host_path": native_dir(),
+        if not self.share_lib_dir:
+            raise ValueError("isolated GPU sharing requested but libgpupool_share.so is not "
+                             f"installed under {self.cfg.state_dir}/lib (see the agent log)")
+        mounts.append({"container_path": self.SHARE_LIB_DIR, "host_path": self.share_lib_dir,
                        "read_only": True})
-        env = {"HSA_TOOLS_LIB": f"{self.SHARE_LIB_DIR}/libgpupool_share.so"}
+        env = {"HSA_TOOLS_LIB": f"{self.SHARE_LIB_DIR}/{self.SHARE_LIB}"}
         if hbm:  # allocate_spec adds the pod-wide account file (GPUPOOL_SHARE_ACCOUNT)
             env["GPUPOOL_HBM_LIMIT_BYTES"] = str(hbm)
         if cu_mask:
             env["GPUPOOL_CU_MASK"] = _ranges(sorted(cu_mask))
+            env["GPUPOOL_CU_LAYOUT"] = "xcd" if layouts == {"xcd"} else "striped"
         return env
 
     # ================================================================ node registration

@@ -9,11 +9,19 @@ loop wake-up (profiles/r2am claim spans: executorIn + executorOut + aiohttp fram
 the event long-poll simply waits on a condition variable. Request framing is minimal on purpose:
 Content-Length bodies (no chunked requests), keep-alive by default, ``Connection: close`` honoured.
 
-Exposure bounds (the TCP listener is reachable from the node network): at most ``max_conns``
-connections are served at once (more are closed on accept); a connection must finish its TLS
-handshake and its first request within ``first_request_timeout`` seconds, and stays bounded by it
-until a request is answered with something other than 401 — only then may it idle as a pooled
-keep-alive connection; a request refused for its token closes the connection.
+Exposure bounds (the TCP listener is reachable from the node network):
+  * at most ``max_conns`` connections are served at once (more are closed on accept);
+  * an absolute deadline: a connection must finish its TLS handshake and its first request within
+    ``first_request_timeout`` seconds of its accept, however slowly its bytes trickle in — every
+    read waits only for what is left of it, and a reaper thread shuts down a connection still
+    untrusted at its deadline (which also bounds a stalled TLS handshake). Only a request answered
+    with something other than 401 makes the connection trusted: it may then idle as a pooled
+    keep-alive connection;
+  * the token is checked right after the headers, before any body byte is read; a request refused
+    for it closes the connection;
+  * at most ``MAX_HEADERS`` header lines of ``MAX_HEADER_BYTES`` in total; a body-carrying method
+    (POST/PUT/PATCH) needs a decimal Content-Length (missing, negative or non-numeric -> 400,
+    nothing read), at most ``MAX_BODY``.
 """
 from __future__ import annotations
 
@@ -35,8 +43,71 @@ Handler = Callable[[dict, bytes], tuple]
 OPEN_PATHS = {"/healthz", "/metrics"}
 _REASONS = {200: "OK", 400: "Bad Request", 401: "Unauthorized", 404: "Not Found",
             405: "Method Not Allowed", 409: "Conflict", 413: "Payload Too Large",
-            500: "Internal Server Error"}
+            431: "Request Header Fields Too Large", 500: "Internal Server Error"}
 MAX_BODY = 16 << 20
+MAX_HEADERS = 64
+MAX_HEADER_BYTES = 16 << 10
+MAX_LINE = 8 << 10
+BODY_METHODS = {"POST", "PUT", "PATCH"}
+
+
+class _Closed(Exception):
+    """The peer went away, or the connection's deadline passed."""
+
+
+class _Reader:
+    """Buffered reads from a socket under an optional absolute deadline (``time.monotonic``):
+    each recv waits only for the time left, so a peer dripping one byte at a time cannot stretch
+    the bound the way a per-recv socket timeout lets it."""
+
+    def __init__(self, conn):
+        self.conn = conn
+        self.buf = bytearray()
+        self.deadline: float | None = None
+        self._timed = False
+        self.total = 0  # bytes received on this connection
+
+    def _fill(self) -> None:
+        if self.deadline is not None:
+            left = self.deadline - time.monotonic()
+            if left <= 0:
+                raise _Closed("deadline")
+            self.conn.settimeout(left)
+            self._timed = True
+        elif self._timed:
+            self.conn.settimeout(None)
+            self._timed = False
+        try:
+            data = self.conn.recv(65536)
+        except socket.timeout:
+            raise _Closed("deadline") from None
+        if not data:
+            raise _Closed("eof")
+        self.total += len(data)
+        self.buf += data
+
+    def readline(self, limit: int) -> bytes:
+        """One line including its newline; ValueError past ``limit`` bytes without one."""
+        start = 0
+        while True:
+            i = self.buf.find(b"\n", start)
+            if i >= 0:
+                if i + 1 > limit:
+                    raise ValueError("line too long")
+                line = bytes(self.buf[:i + 1])
+                del self.buf[:i + 1]
+                return line
+            if len(self.buf) >= limit:
+                raise ValueError("line too long")
+            start = len(self.buf)
+            self._fill()
+
+    def read(self, n: int) -> bytes:
+        while len(self.buf) < n:
+            self._fill()
+        out = bytes(self.buf[:n])
+        del self.buf[:n]
+        return out
 
 
 def json_reply(obj, status: int = 200, after: Callable[[], None] | None = None) -> tuple:
@@ -62,6 +133,13 @@ class RpcServer:
         self.requests = 0
         self.stats: dict[str, list] = {}  # path -> [count, seconds]
         self._stats_mu = threading.Lock()
+        # untrusted connections -> their absolute deadline; the reaper shuts down the late ones
+        self._pending: dict[socket.socket, float] = {}
+        self._pending_cv = threading.Condition()
+        self.reaped = 0
+        self.rejected_requests = 0
+        self.bytes_read = 0  # over all finished connections (tests: what a rejected peer cost)
+        threading.Thread(target=self._reaper, daemon=True, name="rpc-reaper").start()
 
     # ------------------------------------------------------------ listeners
     def listen_unix(self, path: str) -> None:
@@ -89,6 +167,8 @@ class RpcServer:
 
     def close(self) -> None:
         self._stop.set()
+        with self._pending_cv:
+            self._pending_cv.notify()
         for s in self._listeners:
             try:
                 s.close()
@@ -130,19 +210,68 @@ class RpcServer:
         with self._conns_mu:
             return self._conns
 
+    # ------------------------------------------------------------ deadlines
+    def _reaper(self) -> None:
+        """Shuts down connections still untrusted at their deadline: a blocked recv (plain or in
+        a TLS handshake) then returns, and the connection's thread closes it."""
+        with self._pending_cv:
+            while not self._stop.is_set():
+                now = time.monotonic()
+                late = [c for c, d in self._pending.items() if d <= now]
+                for c in late:
+                    del self._pending[c]
+                    self.reaped += 1
+                    try:
+                        c.shutdown(socket.SHUT_RDWR)
+                    except OSError:
+                        pass
+                nxt = min(self._pending.values(), default=None)
+                self._pending_cv.wait(None if nxt is None else max(0.01, nxt - now))
+
+    def _watch(self, conn: socket.socket, deadline: float) -> None:
+        with self._pending_cv:
+            self._pending[conn] = deadline
+            self._pending_cv.notify()
+
+    def _unwatch(self, conn: socket.socket) -> None:
+        with self._pending_cv:
+            self._pending.pop(conn, None)
+
     # ------------------------------------------------------------ one connection
+    def _reject(self, conn, status: int, reason: str, message: str) -> None:
+        self.rejected_requests += 1
+        try:
+            self._send(conn, json_reply({"reason": reason, "message": message}, status), False)
+        except OSError:
+            pass
+
     def _serve_conn(self, conn: socket.socket, ssl_ctx) -> None:
         trusted = False  # until a request is answered with something other than 401
+        raw = conn
+        rf = None
+        deadline = time.monotonic() + self.first_request_timeout if self.first_request_timeout \
+            else None
+        if deadline is not None:
+            self._watch(raw, deadline)
         try:
-            conn.settimeout(self.first_request_timeout or None)  # handshake + first request
             if conn.family != socket.AF_UNIX:
                 conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             if ssl_ctx is not None:
-                conn = ssl_ctx.wrap_socket(conn, server_side=True)
-            rf = conn.makefile("rb", buffering=65536)
+                # the wrapper takes over the fd (the plain socket object is detached): watch the
+                # wrapper from here, then handshake — bounded by the reaper like any read
+                conn.settimeout(self.first_request_timeout or None)
+                conn = ssl_ctx.wrap_socket(conn, server_side=True, do_handshake_on_connect=False)
+                if deadline is not None:
+                    self._unwatch(raw)
+                    self._watch(conn, deadline)
+                raw = conn
+                conn.do_handshake()
+            rf = _Reader(conn)
+            rf.deadline = deadline
             while not self._stop.is_set():
-                line = rf.readline(65537)
-                if not line:
+                try:
+                    line = rf.readline(MAX_LINE)
+                except _Closed:
                     return
                 if line in (b"\r\n", b"\n"):
                     continue
@@ -150,45 +279,78 @@ class RpcServer:
                     method, target, version = line.decode("latin-1").split(None, 2)
                 except ValueError:
                     return
+                method = method.upper()
                 headers: dict[str, str] = {}
+                nbytes = 0
                 while True:
-                    h = rf.readline(65537)
-                    if h in (b"\r\n", b"\n", b""):
+                    h = rf.readline(MAX_LINE)
+                    if h in (b"\r\n", b"\n"):
                         break
+                    nbytes += len(h)
+                    if len(headers) >= MAX_HEADERS or nbytes > MAX_HEADER_BYTES:
+                        self._reject(conn, 431, "HeadersTooLarge",
+                                     f"at most {MAX_HEADERS} header lines / {MAX_HEADER_BYTES} bytes")
+                        return
                     k, _, v = h.decode("latin-1").partition(":")
                     headers[k.strip().lower()] = v.strip()
-                n = int(headers.get("content-length") or 0)
-                if n > MAX_BODY:
-                    self._send(conn, (413, "text/plain", b"body too large\n", None), False)
+                path = target.partition("?")[0]
+                # the token before the body: an unauthenticated peer never gets a byte buffered
+                if self._auth and path not in OPEN_PATHS and not hmac.compare_digest(
+                        headers.get("authorization", "").encode(), self._auth):
+                    self._reject(conn, 401, "Unauthorized", "agent RPC requires the manager's token")
                     return
-                body = rf.read(n) if n else b""
+                cl = headers.get("content-length")
+                if cl is None:
+                    if method in BODY_METHODS:
+                        self._reject(conn, 400, "BadRequest", "Content-Length required")
+                        return
+                    n = 0
+                elif not cl.isdigit() or not cl.isascii():  # no sign, no spaces, no hex
+                    self._reject(conn, 400, "BadRequest", f"bad Content-Length {cl[:32]!r}")
+                    return
+                else:
+                    n = int(cl)
+                if n > MAX_BODY:
+                    self._reject(conn, 413, "PayloadTooLarge", f"body over {MAX_BODY} bytes")
+                    return
+                try:
+                    body = rf.read(n) if n else b""
+                except _Closed:
+                    return
                 keep = headers.get("connection", "").lower() != "close" and \
                     not version.strip().upper().endswith("1.0")
                 t0 = time.perf_counter()
-                reply = self._dispatch(method.upper(), target, headers, body)
+                reply = self._dispatch(method, target, headers, body)
                 if reply[0] == 401:
                     keep = False  # no second guess on this connection
                 elif not trusted:
                     trusted = True
-                    conn.settimeout(None)  # a pooled keep-alive connection may idle from here
-                self._send(conn, reply, keep)
-                self._account(target.partition("?")[0], time.perf_counter() - t0)
-                if reply[3] is not None:
-                    try:
-                        reply[3]()
-                    except Exception:
-                        log.exception("post-reply hook failed")
+                    rf.deadline = None  # a pooled keep-alive connection may idle from here
+                    self._unwatch(raw)
+                try:
+                    self._send(conn, reply, keep)
+                    self._account(path, time.perf_counter() - t0)
+                finally:
+                    # the hook runs even when the peer is gone (e.g. a claim whose caller timed
+                    # out): it ends the claim's event hold, which must never stay raised
+                    if reply[3] is not None:
+                        try:
+                            reply[3]()
+                        except Exception:
+                            log.exception("post-reply hook failed")
                 if not keep:
                     return
-        except (OSError, ssl.SSLError, ValueError):
+        except (OSError, ssl.SSLError, ValueError, _Closed):
             return
         finally:
+            self._unwatch(raw)
             try:
                 conn.close()
             except OSError:
                 pass
             with self._conns_mu:
                 self._conns -= 1
+                self.bytes_read += rf.total if rf is not None else 0
 
     def _account(self, path: str, seconds: float) -> None:
         with self._stats_mu:
@@ -202,7 +364,9 @@ class RpcServer:
         with self._stats_mu:
             items = sorted(self.stats.items())
         out = [f"gpupool_agent_rpc_open_connections {self.open_conns}",
-               f"gpupool_agent_rpc_refused_connections_total {self.refused_conns}"]
+               f"gpupool_agent_rpc_refused_connections_total {self.refused_conns}",
+               f"gpupool_agent_rpc_deadline_closed_connections_total {self.reaped}",
+               f"gpupool_agent_rpc_rejected_requests_total {self.rejected_requests}"]
         for path, (n, sec) in items:
             out.append(f'gpupool_agent_rpc_requests_total{{path="{path}"}} {n}')
             out.append(f'gpupool_agent_rpc_seconds_sum{{path="{path}"}} {sec:.6f}')

@@ -1,0 +1,137 @@
+"""Slot isolation on a shared MI355X (spec.sharing; the HAMi layer of the reference platform,
+GPU调度平台搭建.md:289-298): which CUs a slot's queues may use, whether a pool's HBM budgets fit
+the GPU, and the pod-wide HBM account file libgpupool_share.so charges (native/src/share/share.cc).
+
+CU layout. ROCr's queue CU mask interleaves its bits over the XCDs: on an SPX MI355X (8 XCDs x 32
+CUs) bit b is a CU of XCD b mod 8 (measured with the probe's CU census, profiles/r3b_sharing_gpu.txt
+— a contiguous 64-bit range lands 8 CUs on every XCD). So a contiguous ("striped") slot spreads over
+every XCD and shares all eight 4 MB L2s with its siblings. When a slot is a whole number of XCDs and
+the slots fit (cuPerSlot a multiple of the XCD's CUs, replicasPerGPU x XCDs-per-slot <= XCDs), slot i
+is given whole XCDs instead — bits {b : b mod X in slot i's XCDs} — and so an L2 of its own
+("xcd" layout). Otherwise the striped layout is kept. A CPX partition is one XCD: always striped.
+"""
+from __future__ import annotations
+
+import os
+import struct
+import time
+
+# XCDs per logical GPU by compute partition (MI355X: 8 XCDs per package)
+XCDS_BY_PARTITION = {"SPX": 8, "DPX": 4, "QPX": 2, "CPX": 1}
+CUS_PER_XCD = 32  # MI355X: 256 CUs on 8 XCDs
+
+
+def xcd_count(dev: dict) -> int:
+    part = str(((dev or {}).get("partition") or {}).get("compute") or "").upper()
+    if part in XCDS_BY_PARTITION:
+        return XCDS_BY_PARTITION[part]
+    cus = int(((dev or {}).get("asic") or {}).get("computeUnits") or 256)
+    return max(1, cus // CUS_PER_XCD)
+
+
+def slot_cus(slot: int, slots: int, cu_per_slot: int, cus: int, xcds: int) -> tuple[list[int], str]:
+    """CU-mask bits of ``slot`` (of ``slots`` on the GPU) and the layout: ``"xcd"`` (whole XCDs) or
+    ``"striped"`` (a contiguous range, interleaved over every XCD). ``cu_per_slot`` is narrowed to
+    the GPU's own share (cus // slots), as the striped layout always did."""
+    cus, xcds, slots = max(1, cus), max(1, xcds), max(1, slots)
+    cu = max(1, min(cu_per_slot, cus // slots))
+    per_xcd = cus // xcds
+    if xcds > 1 and per_xcd > 0 and cus % xcds == 0 and cu % per_xcd == 0:
+        span = cu // per_xcd  # XCDs per slot
+        if slots * span <= xcds:
+            mine = set(range(slot * span, (slot + 1) * span))
+            return [b for b in range(cus) if b % xcds in mine], "xcd"
+    return list(range(slot * cu, (slot + 1) * cu)), "striped"
+
+
+def slot_xcds(bits: list[int], xcds: int) -> list[int]:
+    """The XCDs a mask's bits land on (the interleave above)."""
+    return sorted({b % max(1, xcds) for b in bits})
+
+
+def overcommit(sharing: dict, mem_total: int, reserve: int) -> str:
+    """Why a pool's slot budgets do not fit a GPU of ``mem_total`` bytes with ``reserve`` bytes kept
+    for the agent's own use of it (HIP context + probe arena), or "" when they fit."""
+    per_slot = int((sharing or {}).get("hbmBytesPerSlot") or 0)
+    k = max(1, int((sharing or {}).get("replicasPerGPU") or 1))
+    if per_slot <= 0 or mem_total <= 0:
+        return ""
+    usable = mem_total - max(0, reserve)
+    if k * per_slot <= usable:
+        return ""
+    return (f"replicasPerGPU {k} x hbmBytesPerSlot {per_slot} = {k * per_slot} B exceeds the GPU's "
+            f"{mem_total} B HBM minus the agent's {reserve} B reserve ({usable} B)")
+
+
+# ---- the pod-wide HBM account (layout: native/src/share/share.cc) ----
+ACCT_BYTES = 16384
+ACCT_UUIDS_AT = 8192   # version 2: 8 x 32-byte GPU identities (HSA agent UUID = amdsmi hip_uuid)
+ACCT_UUID_BYTES = 32
+ACCT_IDS_AT_V1 = 8192  # the slot ids as text (agent bookkeeping)
+ACCT_IDS_AT_V2 = ACCT_UUIDS_AT + 8 * ACCT_UUID_BYTES
+
+
+def account_bytes(limit: int, slots: list[str], gpu_uuids: list[str],
+                  created: float | None = None) -> bytes:
+    """A fresh version-2 account: magic, per-GPU limit, the GPUs' identities (account index g is
+    the g-th of ``gpu_uuids``), its creation time (header pad, ignored by the library: the file's
+    mtime moves with every charge), zeroed counters, the slot ids as text."""
+    buf = bytearray(ACCT_BYTES)
+    ids = list(gpu_uuids)[:8]
+    buf[0:32] = b"GPSHARE1" + struct.pack("<QIId", int(limit), 2, len(ids),
+                                          time.time() if created is None else created)
+    for g, u in enumerate(ids):
+        raw = u.encode()[:ACCT_UUID_BYTES - 1]
+        at = ACCT_UUIDS_AT + g * ACCT_UUID_BYTES
+        buf[at:at + len(raw)] = raw
+    text = ",".join(slots).encode()[: ACCT_BYTES - ACCT_IDS_AT_V2 - 1]
+    buf[ACCT_IDS_AT_V2:ACCT_IDS_AT_V2 + len(text)] = text
+    return bytes(buf)
+
+
+def read_account(path: str) -> dict | None:
+    """An account file's header and slot ids (None if unreadable / not an account)."""
+    try:
+        with open(path, "rb") as f:
+            head = f.read(32)
+            if len(head) < 32 or head[:8] != b"GPSHARE1":
+                return None
+            limit, version, ngpus, created = struct.unpack("<QIId", head[8:32])
+            f.seek(ACCT_IDS_AT_V2 if version >= 2 else ACCT_IDS_AT_V1)
+            text = f.read().split(b"\0", 1)[0].decode(errors="replace")
+    except OSError:
+        return None
+    if version < 2:
+        created = 0.0  # version 1 kept no creation time
+    return {"limit": limit, "version": version, "ngpus": ngpus, "created": created,
+            "slots": [s for s in text.split(",") if s]}
+
+
+def account_slots(path: str) -> list[str] | None:
+    """The slot ids an account file was made for (None if unreadable / not an account)."""
+    a = read_account(path)
+    return None if a is None else a["slots"]
+
+
+def gc_accounts(directory: str, live_ids: set[str], older_than: float) -> list[str]:
+    """Delete the account files none of whose slots a pod holds any more (``live_ids``: the device
+    IDs the kubelet's PodResources lists) and that were created before ``older_than`` (wall clock)
+    — an Allocate can precede the listing that shows its pod. Returns the deleted paths."""
+    gone = []
+    try:
+        names = os.listdir(directory)
+    except OSError:
+        return gone
+    for name in names:
+        if not name.endswith(".acct"):
+            continue
+        path = os.path.join(directory, name)
+        acct = read_account(path)
+        if acct is None or acct["created"] >= older_than or set(acct["slots"]) & live_ids:
+            continue
+        try:
+            os.unlink(path)
+            gone.append(path)
+        except OSError:
+            pass
+    return gone

@@ -181,6 +181,19 @@ DEVICE_STATUS = {
                            "unavailablePeers": {"type": "array", "items": _S},
                            "lastCheckedAt": _S, "peerCheckUnavailable": _B},
         },
+        "sharing": {
+            "type": "object",
+            "description": "Slot isolation of a shared GPU (spec.sharing): the enforced per-slot "
+                           "HBM budget (never above a fair share of the HBM the agent leaves "
+                           "free), and per slot its CU-mask bits and the XCDs they land on. "
+                           "cuLayout xcd: every slot owns whole XCDs, so an L2 of its own; "
+                           "striped: slots interleave over every XCD and share the L2s.",
+            "properties": {"replicasPerGPU": _I32, "hbmBytesPerSlot": _I64,
+                           "cuLayout": {"type": "string", "enum": ["xcd", "striped"]},
+                           "cuPerSlot": _I32, "xcds": _I32,
+                           "slotCUMasks": {"type": "array", "items": _S},
+                           "slotXcds": {"type": "array", "items": _S}},
+        },
         "hbmCoverage": {
             "type": "object",
             "description": "The agent's HBM scrubber on this GPU (rotating pattern-test windows "

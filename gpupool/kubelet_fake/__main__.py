@@ -21,6 +21,9 @@ def main() -> None:
     ap.add_argument("--no-schedule", action="store_true")
     ap.add_argument("--node-status-delay", type=float, default=0.02,
                     help="coalescing delay between a device-plugin update and the Node status PATCH (s)")
+    ap.add_argument("--host-path", action="append", default=None,
+                    help="strict mounts: a host path a device plugin may hand out (repeatable; "
+                         "an Allocate mount or device outside all of them fails the pod)")
     ap.add_argument("--ready-file", default="")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
@@ -33,7 +36,8 @@ def main() -> None:
     k = FakeKubelet(a.node, a.apiserver, os.path.join(a.root, "device-plugins"),
                     os.path.join(a.root, "pod-resources", "kubelet.sock"), workdir=a.workdir,
                     log_dir=os.path.join(a.root, "pod-logs"), token=a.token,
-                    schedule=not a.no_schedule, node_status_delay=a.node_status_delay)
+                    schedule=not a.no_schedule, node_status_delay=a.node_status_delay,
+                    host_paths=a.host_path)
     k.start()
     if a.ready_file:
         with open(a.ready_file, "w") as f:

@@ -71,7 +71,7 @@ class FakeKubelet:
     def __init__(self, node: str, apiserver: str, plugin_dir: str, pod_resources_socket: str,
                  workdir: str | None = None, log_dir: str | None = None, token: str | None = None,
                  schedule: bool = True, extra_env: dict | None = None,
-                 node_status_delay: float = 0.02):
+                 node_status_delay: float = 0.02, host_paths: list[str] | None = None):
         self.node = node
         self.client = Client(apiserver, token)
         self.apiserver = apiserver
@@ -81,6 +81,11 @@ class FakeKubelet:
         self.log_dir = log_dir or os.path.join(plugin_dir, "..", "pod-logs")
         self.schedule = schedule
         self.extra_env = extra_env or {}
+        # strict mounts: the host paths that exist on this "node" for a device plugin to hand out
+        # (the agent DaemonSet's same-path hostPath volumes). A container runtime resolves an
+        # Allocate's mount and device host paths on the HOST; one the agent only has inside its
+        # own container fails CreateContainer — so does it here. None: anything goes.
+        self.host_paths = [os.path.abspath(p) for p in host_paths] if host_paths else None
         self.plugins: dict[str, PluginConn] = {}
         self.pods: dict[str, RunningPod] = {}          # pod uid -> running pod
         self.assigned: dict[str, str] = {}             # device ID -> pod uid
@@ -344,6 +349,12 @@ class FakeKubelet:
                     self._fail(pod, "UnexpectedAdmissionError", f"Allocate failed: {e.details()}")
                     return
                 cr = resp.container_responses[0]
+                bad = self._off_node_paths(cr)
+                if bad:
+                    self._fail(pod, "CreateContainerError",
+                               f"host path(s) {', '.join(bad)} of the device plugin's Allocate do "
+                               f"not exist on node {self.node}")
+                    return
                 # the pod runs as a host process (no mount namespace): a device-plugin mount is
                 # realised by pointing its container paths at the host paths
                 rewrite = [(m.container_path, m.host_path) for m in cr.mounts
@@ -360,6 +371,17 @@ class FakeKubelet:
             rp = RunningPod(ns, name, uid, devices, container.get("name", "main"))
             self.pods[uid] = rp
         self._start_process(rp, pod, envs)
+
+    def _off_node_paths(self, cr) -> list[str]:
+        """Allocate host paths (mounts, device nodes) outside the node's declared host paths."""
+        if self.host_paths is None:
+            return []
+        paths = [m.host_path for m in cr.mounts] + [d.host_path for d in cr.devices]
+
+        def on_node(p: str) -> bool:
+            p = os.path.abspath(p)
+            return any(p == r or p.startswith(r.rstrip("/") + "/") for r in self.host_paths)
+        return [p for p in paths if not on_node(p)]
 
     def _start_process(self, rp: RunningPod, pod: dict, envs: dict[str, str]) -> None:
         container = (pod["spec"].get("containers") or [{}])[0]

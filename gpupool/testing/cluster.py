@@ -90,6 +90,10 @@ class NodeSpec:
     probe: str = ""               # "" -> agent default (simulated for fake, inproc for real)
     kubelet: bool = True
     extra_args: list[str] = field(default_factory=list)
+    # strict mounts (default): the fake kubelet fails a pod whose Allocate mounts or device
+    # nodes lie outside what the agent DaemonSet shares with the host — the agent's state dir
+    # (hostPath /var/lib/gpupool) and the GPU device nodes
+    strict_mounts: bool = True
 
 
 class Cluster:
@@ -189,14 +193,19 @@ class Cluster:
         rf = os.path.join(self.workdir, f"kubelet-{node.name}.ready")
         if os.path.exists(rf):
             os.remove(rf)
-        p = self._spawn(f"kubelet-{node.name}", [self.python, "-m", "gpupool.kubelet_fake",
-                                                 "--node", node.name, "--apiserver", self.url,
-                                                 "--root", root, "--workdir", ROOT,
-                                                 "--ready-file", rf])
+        argv = [self.python, "-m", "gpupool.kubelet_fake", "--node", node.name,
+                "--apiserver", self.url, "--root", root, "--workdir", ROOT, "--ready-file", rf]
+        if node.strict_mounts:
+            for hp in (self.state_dir(node.name), "/dev/kfd", "/dev/dri"):
+                argv += ["--host-path", hp]
+        p = self._spawn(f"kubelet-{node.name}", argv)
         _wait_file(rf, 60, p, os.path.join(self.workdir, f"kubelet-{node.name}.log"))
 
     def faults_path(self, node: str) -> str:
         return os.path.join(self.workdir, f"faults-{node}.json")
+
+    def state_dir(self, node: str) -> str:
+        return os.path.join(self.workdir, f"state-{node}")
 
     def agent_socket(self, node: str) -> str:
         return os.path.join(self.sockdir, f"a-{node}.sock")
@@ -206,7 +215,7 @@ class Cluster:
         if os.path.exists(rf):
             os.remove(rf)
         argv = [self.python, "-m", "gpupool.agent", "--node", node.name, "--backend", node.backend,
-                "--state-dir", os.path.join(self.workdir, f"state-{node.name}"),
+                "--state-dir", self.state_dir(node.name),
                 "--socket", self.agent_socket(node.name), "--apiserver", self.url,
                 "--faults", self.faults_path(node.name), "--ready-file", rf,
                 "--sample-interval", str(self.sample_interval),

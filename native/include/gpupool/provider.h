@@ -111,7 +111,7 @@ struct DeviceView {
   std::string state;  // Free | Claimed | Draining | Quarantined | Probing
   std::string pool_uid, pool;
   bool healthy = false, advertised = false, probe_passed = false;
-  Json verdict, probe, pods, partition, hbm_sweep, xgmi_pairs;
+  Json verdict, probe, pods, partition, hbm_sweep, xgmi_pairs, sharing;
   Json telemetry;     // agent-sampled utilisation: gfx/umc activity %, power W, VRAM used/total
   std::string claimed_at, drain_started_at;
   static DeviceView from(const Json& j);

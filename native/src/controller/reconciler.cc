@@ -366,8 +366,10 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
     if (nodes.empty()) nodes = provider_.node_names();
   }
   std::vector<std::string> unreachable_hinted;
+  std::set<std::string> answered;  // nodes observed this pass (a spanning pool's suspects among them are resolved)
   for (const auto& n : nodes) {
     NodeView nv = provider_.observe_pool(n, m.uid);
+    if (nv.reachable) answered.insert(n);
     if (!nv.reachable) {
       if (hinted.count(n) || n == spec.node_name) {
         o.reachable = false;
@@ -401,7 +403,19 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
       if (!o.mine.empty()) break;
     }
   }
-  if (!span_nodes) resolve_suspects_(m, o);  // a spanning pool observes every node anyway
+  if (!span_nodes) {
+    resolve_suspects_(m, o);
+  } else {
+    // A spanning pool observes every node: whatever a lost claim reply left on a node that answered
+    // this pass is in o.mine already (kept or released by this pass's plan), so that node is no
+    // longer a suspect. Without this a spanning pool could never be finalized after a lost reply.
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = suspect_.find(m.uid);
+    if (it != suspect_.end()) {
+      for (const auto& n : answered) it->second.erase(n);
+      if (it->second.empty()) suspect_.erase(it);
+    }
+  }
   std::sort(o.mine.begin(), o.mine.end(), [](const DeviceView& a, const DeviceView& b) {
     return a.node != b.node ? a.node < b.node : a.index < b.index;
   });
@@ -1120,14 +1134,23 @@ bool Mi355xPoolReconciler::quota_reserve_(const ObjectMeta& m, const Mi355xPoolS
   }
   if (hard < 0) return true;
   std::map<std::string, int64_t> per_pool;  // uid -> units
+  std::set<std::string> live{m.uid};
   for (const auto& p : pools_.list()) {
+    live.insert(p.path("metadata.uid").as_string());
     if (p.path("metadata.namespace").as_string() != m.ns) continue;
     if (p.path("spec.resourceName").str_or(gen::kDefaultResource) != spec.resource_name) continue;
     per_pool[p.path("metadata.uid").as_string()] =
         p.path("status.replicas").as_int(0) * std::max<int64_t>(1, p.path("spec.sharing.replicasPerGPU").as_int(1));
   }
   int64_t used = 0;
-  for (const auto& [uid, h] : quota_holds_) {
+  for (auto it = quota_holds_.begin(); it != quota_holds_.end();) {
+    // A pool that left the cache without a finalizer pass (finalizer force-removed) holds nothing:
+    // its hold goes with it, or its namespace's quota stays consumed until a manager restart.
+    if (!live.count(it->first)) {
+      it = quota_holds_.erase(it);
+      continue;
+    }
+    const auto& [uid, h] = *it++;
     if (h.ns != m.ns || h.resource != spec.resource_name) continue;
     int64_t& u = per_pool[uid];
     u = std::max(u, h.written) + (uid == m.uid ? 0 : h.reserved);

@@ -34,6 +34,7 @@ DeviceView DeviceView::from(const Json& j) {
   d.drain_started_at = j["drainStartedAt"].as_string();
   d.hbm_sweep = j["hbmSweep"];
   d.xgmi_pairs = j["xgmiPairs"];
+  d.sharing = j["sharing"];
   d.telemetry = j["telemetry"];
   return d;
 }
@@ -77,6 +78,7 @@ Json DeviceView::status_json() const {
     }
     s["probe"] = p;
   }
+  if (sharing.is_object() && sharing.size()) s["sharing"] = sharing;  // slot isolation (agent slots.py)
   if (hbm_sweep.is_object()) {  // HBM scrubber coverage of this GPU (agent's rotating sweep)
     Json c = Json::object();
     for (const char* k : {"passes", "fraction", "span", "cursor", "lastFullSweepAt", "lastBadBits"})

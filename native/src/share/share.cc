@@ -51,16 +51,20 @@
 namespace {
 
 // ---- the shared account file (written by the agent, gpupool/agent/agent.py _share_account) ----
-// [0,64) header, [64,128) live bytes per GPU ordinal, [128,8192) per-process entries,
-// [8192,16384) the allocation's slot ids as text (the agent's bookkeeping; ignored here).
+// [0,64) header, [64,128) live bytes per account GPU, [128,8192) per-process entries,
+// version 2: [8192,8448) the account GPUs' identities — 8 NUL-padded 32-byte strings, the
+// HSA_AMD_AGENT_INFO_UUID ("GPU-<hex>", amdsmi's hip_uuid) of account GPU g at 8192 + 32 g —
+// then the allocation's slot ids as text (the agent's bookkeeping; ignored here). Version 1 files
+// have no identities: account GPU g is the process's g-th GPU agent.
 constexpr size_t kAcctBytes = 16384;
 constexpr int kAcctGpus = 8;
 constexpr int kAcctEntries = (8192 - 128) / 32;
+constexpr size_t kAcctUuidsAt = 8192, kAcctUuidBytes = 32;
 constexpr char kAcctMagic[8] = {'G', 'P', 'S', 'H', 'A', 'R', 'E', '1'};
 
 struct AcctEntry {
   int32_t pid;     // 0 free, -1 being claimed or reclaimed, else the owning process
-  uint32_t gpu;    // GPU ordinal among the process's visible GPU agents
+  uint32_t gpu;    // account GPU index (see the layout above)
   uint64_t start;  // the owner's start time (/proc/<pid>/stat field 22): pid reuse is not a match
   uint64_t bytes;  // live bytes the owner holds on ``gpu``
   uint64_t pad;
@@ -86,7 +90,8 @@ struct State {
   bool pools_mapped = false;
   std::map<uint64_t, uint64_t> pool_agent;  // GPU-located pool handle -> agent handle
   std::map<uint64_t, uint64_t> used;        // agent handle -> live bytes (this process)
-  std::map<uint64_t, uint32_t> ordinal;     // agent handle -> GPU ordinal (account index)
+  std::map<uint64_t, uint32_t> ordinal;     // agent handle -> ROCr's enumeration order
+  std::map<uint64_t, int> acct_gpu;         // agent handle -> account GPU index (-1: not in the account)
   std::unordered_map<void*, std::pair<uint64_t, uint64_t>> ptrs;       // ptr -> (agent, bytes)
   std::unordered_map<uint64_t, std::pair<uint64_t, uint64_t>> vmem;    // handle -> (agent, bytes)
   std::atomic<uint64_t> denied{0}, queues_masked{0}, peak{0}, reclaimed{0};
@@ -255,6 +260,28 @@ std::vector<uint32_t> parse_mask(const char* v, uint32_t* bits) {
   return words;
 }
 
+// The account GPU of a GPU agent. Version 2 accounts name their GPUs, so every process of the pod
+// charges the same counter for the same physical GPU whatever subset of GPUs it sees (a launcher's
+// per-rank ROCR_VISIBLE_DEVICES reorders and narrows the enumeration); a GPU the account does not
+// name is not budgeted through it (-1). Version 1: the agent's ordinal. Caller holds s.mu.
+int acct_index(State& s, hsa_agent_t agent, uint32_t ordinal) {
+  if (s.acct->version < 2) return ordinal < static_cast<uint32_t>(kAcctGpus) ? static_cast<int>(ordinal) : -1;
+  char uuid[64] = {};
+  if (s.real_core.hsa_agent_get_info_fn(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_UUID), uuid) !=
+      HSA_STATUS_SUCCESS)
+    return -1;
+  uuid[sizeof uuid - 1] = 0;
+  const char* table = reinterpret_cast<const char*>(s.acct) + kAcctUuidsAt;
+  const uint32_t n = std::min<uint32_t>(s.acct->ngpus, kAcctGpus);
+  for (uint32_t g = 0; g < n; ++g) {
+    const char* id = table + g * kAcctUuidBytes;
+    if (id[0] && std::strncmp(id, uuid, kAcctUuidBytes) == 0 && std::strlen(uuid) < kAcctUuidBytes)
+      return static_cast<int>(g);
+  }
+  if (s.debug) std::fprintf(stderr, "[gpupool-share] GPU %s is not in the pod's account\n", uuid);
+  return -1;
+}
+
 hsa_status_t collect_pool(hsa_amd_memory_pool_t pool, void* agent_handle) {
   State& s = st();
   hsa_amd_memory_pool_location_t loc{};
@@ -273,7 +300,9 @@ hsa_status_t collect_agent(hsa_agent_t agent, void*) {
     return HSA_STATUS_SUCCESS;
   uint64_t h = agent.handle;
   s.used.emplace(h, 0);
-  s.ordinal.emplace(h, static_cast<uint32_t>(s.ordinal.size()));  // ROCr's enumeration order
+  const uint32_t ord = static_cast<uint32_t>(s.ordinal.size());  // ROCr's enumeration order
+  s.ordinal.emplace(h, ord);
+  if (s.acct) s.acct_gpu.emplace(h, acct_index(s, agent, ord));
   if (s.real_amd.hsa_amd_agent_iterate_memory_pools_fn)
     s.real_amd.hsa_amd_agent_iterate_memory_pools_fn(agent, collect_pool, &h);
   return HSA_STATUS_SUCCESS;
@@ -294,8 +323,8 @@ uint64_t agent_of(hsa_amd_memory_pool_t pool) {
 // The account slot of ``agent``: its ordinal when the shared account covers it, else -1.
 int shared_index(State& s, uint64_t agent) {
   if (!s.acct) return -1;
-  auto it = s.ordinal.find(agent);
-  return it != s.ordinal.end() && it->second < kAcctGpus ? static_cast<int>(it->second) : -1;
+  auto it = s.acct_gpu.find(agent);
+  return it != s.acct_gpu.end() ? it->second : -1;
 }
 
 // Live bytes against the budget on ``agent``: the pod's total when shared. Caller holds s.mu.

@@ -21,21 +21,28 @@
 
 namespace {
 
-constexpr uint64_t kGpu = 0x1000, kCpu = 0x2000, kGpuPool = 0x10, kCpuPool = 0x20;
+constexpr uint64_t kGpu = 0x1000, kCpu = 0x2000, kGpu2 = 0x3000, kGpuPool = 0x10, kCpuPool = 0x20, kGpuPool2 = 0x30;
 constexpr size_t kMi = 1024 * 1024;
 uint64_t g_next_ptr = 0x7000000;
 std::vector<uint32_t> g_last_mask;
 uint32_t g_last_bits = 0;
 int g_masks_set = 0;
+std::vector<uint64_t> g_gpus = {kGpu};  // the GPU agents this "process" sees, in ROCr's order
+
+const char* uuid_of(uint64_t agent) { return agent == kGpu ? "GPU-aaaa000000000001" : "GPU-bbbb000000000002"; }
 
 hsa_status_t f_iterate_agents(hsa_status_t (*cb)(hsa_agent_t, void*), void* data) {
   cb(hsa_agent_t{kCpu}, data);
-  cb(hsa_agent_t{kGpu}, data);
+  for (uint64_t g : g_gpus) cb(hsa_agent_t{g}, data);
   return HSA_STATUS_SUCCESS;
 }
 hsa_status_t f_agent_get_info(hsa_agent_t a, hsa_agent_info_t attr, void* v) {
   if (attr == HSA_AGENT_INFO_DEVICE) {
-    *static_cast<hsa_device_type_t*>(v) = a.handle == kGpu ? HSA_DEVICE_TYPE_GPU : HSA_DEVICE_TYPE_CPU;
+    *static_cast<hsa_device_type_t*>(v) = a.handle != kCpu ? HSA_DEVICE_TYPE_GPU : HSA_DEVICE_TYPE_CPU;
+    return HSA_STATUS_SUCCESS;
+  }
+  if (static_cast<int>(attr) == static_cast<int>(HSA_AMD_AGENT_INFO_UUID)) {
+    std::strcpy(static_cast<char*>(v), a.handle == kCpu ? "CPU-XX" : uuid_of(a.handle));
     return HSA_STATUS_SUCCESS;
   }
   if (static_cast<int>(attr) == static_cast<int>(HSA_AMD_AGENT_INFO_MEMORY_AVAIL)) {
@@ -45,13 +52,13 @@ hsa_status_t f_agent_get_info(hsa_agent_t a, hsa_agent_info_t attr, void* v) {
   return HSA_STATUS_ERROR_INVALID_ARGUMENT;
 }
 hsa_status_t f_iterate_pools(hsa_agent_t a, hsa_status_t (*cb)(hsa_amd_memory_pool_t, void*), void* data) {
-  cb(hsa_amd_memory_pool_t{a.handle == kGpu ? kGpuPool : kCpuPool}, data);
+  cb(hsa_amd_memory_pool_t{a.handle == kGpu ? kGpuPool : a.handle == kGpu2 ? kGpuPool2 : kCpuPool}, data);
   return HSA_STATUS_SUCCESS;
 }
 hsa_status_t f_pool_get_info(hsa_amd_memory_pool_t p, hsa_amd_memory_pool_info_t attr, void* v) {
   if (attr == HSA_AMD_MEMORY_POOL_INFO_LOCATION) {
     *static_cast<hsa_amd_memory_pool_location_t*>(v) =
-        p.handle == kGpuPool ? HSA_AMD_MEMORY_POOL_LOCATION_GPU : HSA_AMD_MEMORY_POOL_LOCATION_CPU;
+        p.handle != kCpuPool ? HSA_AMD_MEMORY_POOL_LOCATION_GPU : HSA_AMD_MEMORY_POOL_LOCATION_CPU;
     return HSA_STATUS_SUCCESS;
   }
   if (attr == HSA_AMD_MEMORY_POOL_INFO_SIZE) {
@@ -122,25 +129,27 @@ void* load_copy(const std::string& dst) {
 
 // The account file the agent writes (gpupool/agent/agent.py _share_account): 16 KiB, magic,
 // limit per GPU; everything else zero.
-std::string make_account(uint64_t limit) {
+// Version 2 (``uuids`` given): the account names its GPUs at 8192 + 32 g.
+std::string make_account(uint64_t limit, const std::vector<std::string>& uuids = {}) {
   std::string path = "/tmp/gpupool-share-test-" + std::to_string(getpid()) + ".acct";
   std::vector<char> buf(16384, 0);
   std::memcpy(buf.data(), "GPSHARE1", 8);
   std::memcpy(buf.data() + 8, &limit, 8);
-  uint32_t ver = 1, ngpus = 1;
+  uint32_t ver = uuids.empty() ? 1 : 2, ngpus = uuids.empty() ? 1 : static_cast<uint32_t>(uuids.size());
   std::memcpy(buf.data() + 16, &ver, 4);
   std::memcpy(buf.data() + 20, &ngpus, 4);
+  for (size_t g = 0; g < uuids.size(); ++g) std::memcpy(buf.data() + 8192 + 32 * g, uuids[g].c_str(), uuids[g].size());
   int fd = open(path.c_str(), O_CREAT | O_TRUNC | O_RDWR, 0600);
   if (fd < 0 || write(fd, buf.data(), buf.size()) != static_cast<ssize_t>(buf.size())) path.clear();
   if (fd >= 0) close(fd);
   return path;
 }
 
-uint64_t account_used(const std::string& path) {
+uint64_t account_used(const std::string& path, int gpu = 0) {
   uint64_t v = 0;
   int fd = open(path.c_str(), O_RDONLY);
   if (fd >= 0) {
-    if (pread(fd, &v, 8, 64) != 8) v = ~0ull;
+    if (pread(fd, &v, 8, 64 + 8 * gpu) != 8) v = ~0ull;
     close(fd);
   }
   return v;
@@ -310,6 +319,51 @@ TEST(share_lib_pod_account_across_processes) {
   close(go[0]);
   unlink(acct.c_str());
   unlink(copy.c_str());
+  unsetenv("GPUPOOL_HBM_LIMIT_BYTES");
+  unsetenv("GPUPOOL_SHARE_ACCOUNT");
+}
+
+// Version 2 accounts are keyed by GPU identity, not by each process's enumeration order: a rank that
+// sees only GPU B (ROCR_VISIBLE_DEVICES=<B>) and a rank that sees A and B both charge B's counter,
+// and a GPU the account does not name is never charged to another GPU's.
+TEST(share_lib_account_keyed_by_gpu_uuid) {
+  std::string acct = make_account(1024 * kMi, {uuid_of(kGpu), uuid_of(kGpu2)});
+  EXPECT_TRUE(!acct.empty());
+  setenv("GPUPOOL_HBM_LIMIT_BYTES", "1Gi", 1);
+  setenv("GPUPOOL_SHARE_ACCOUNT", acct.c_str(), 1);
+  const hsa_amd_memory_pool_t pool_b{kGpuPool2}, pool_a{kGpuPool};
+  void* p = nullptr;
+  {  // rank 0 sees [A, B]
+    g_gpus = {kGpu, kGpu2};
+    std::string copy = "/tmp/libgpupool_share-uuid0-" + std::to_string(getpid()) + ".so";
+    void* lib = load_copy(copy);
+    EXPECT_TRUE(lib != nullptr);
+    auto on_load = reinterpret_cast<bool (*)(HsaApiTable*, uint64_t, uint64_t, const char* const*)>(dlsym(lib, "OnLoad"));
+    Fake f;
+    EXPECT_TRUE(on_load(&f.table, 0, 0, nullptr));
+    EXPECT_EQ(f.amd.hsa_amd_memory_pool_allocate_fn(pool_b, 600 * kMi, 0, &p), HSA_STATUS_SUCCESS);
+    EXPECT_EQ(f.amd.hsa_amd_memory_pool_allocate_fn(pool_a, 100 * kMi, 0, &p), HSA_STATUS_SUCCESS);
+    unlink(copy.c_str());
+  }
+  EXPECT_EQ(account_used(acct, 0), static_cast<uint64_t>(100 * kMi));
+  EXPECT_EQ(account_used(acct, 1), static_cast<uint64_t>(600 * kMi));
+  {  // rank 1 sees only B, as its first (ordinal 0) GPU: it must charge B's counter, not A's
+    g_gpus = {kGpu2};
+    std::string copy = "/tmp/libgpupool_share-uuid1-" + std::to_string(getpid()) + ".so";
+    void* lib = load_copy(copy);
+    EXPECT_TRUE(lib != nullptr);
+    auto on_load = reinterpret_cast<bool (*)(HsaApiTable*, uint64_t, uint64_t, const char* const*)>(dlsym(lib, "OnLoad"));
+    Fake f;
+    EXPECT_TRUE(on_load(&f.table, 0, 0, nullptr));
+    // B holds 600 of its 1024 MiB pod-wide: 500 more is over, 400 fits
+    EXPECT_EQ(f.amd.hsa_amd_memory_pool_allocate_fn(pool_b, 500 * kMi, 0, &p), HSA_STATUS_ERROR_OUT_OF_RESOURCES);
+    EXPECT_EQ(f.amd.hsa_amd_memory_pool_allocate_fn(pool_b, 400 * kMi, 0, &p), HSA_STATUS_SUCCESS);
+    unlink(copy.c_str());
+  }
+  EXPECT_EQ(account_used(acct, 0), static_cast<uint64_t>(100 * kMi));
+  EXPECT_EQ(account_used(acct, 1), static_cast<uint64_t>(1000 * kMi));
+  g_gpus = {kGpu};
+  unlink(acct.c_str());
   unsetenv("GPUPOOL_HBM_LIMIT_BYTES");
   unsetenv("GPUPOOL_SHARE_ACCOUNT");
 }

@@ -189,3 +189,72 @@ def test_hbm_budget_is_the_pods_across_its_processes(tmp_path):
             if p is not None and p.poll() is None:
                 p.kill()
                 p.wait(timeout=30)
+
+
+def test_xcd_aligned_slots_own_whole_xcds():
+    """The agent's XCD layout (gpupool/agent/slots.py) for 4 slots x 64 CUs: each slot's census
+    shows exactly two XCDs with all 32 of their CUs and six XCDs with none, and no two slots share
+    an XCD — so each slot has L2s of its own (the striped layout puts 8 CUs on every XCD)."""
+    from gpupool.agent.agent import _ranges
+    from gpupool.agent.slots import slot_cus
+    assert os.path.exists(LIB), "build the native targets first"
+    owned = []
+    for i in range(4):
+        bits, layout = slot_cus(i, 4, 64, 256, 8)
+        assert layout == "xcd" and len(bits) == 64
+        r = subprocess.run([sys.executable, "-c", CENSUS, ROOT],
+                           env=_env(HSA_TOOLS_LIB=LIB, GPUPOOL_CU_MASK=_ranges(bits)),
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = json.loads(r.stdout.splitlines()[-1])
+        per = out["perXcd"]
+        print(f"xcd slot {i}: mask {_ranges(bits)[:40]}... per XCD {per}")
+        assert out["mfmaOk"], out
+        assert sorted(per) == [0] * 6 + [32, 32], (i, per)
+        owned.append({x for x in range(8) if per[x]})
+    for i in range(4):
+        for j in range(i + 1, 4):
+            assert not (owned[i] & owned[j]), (i, j, owned)
+
+
+ACCT_ALLOC = r"""
+import json, sys, torch
+torch.zeros(1, device="cuda"); torch.cuda.synchronize()
+a = torch.empty(int(sys.argv[1]), dtype=torch.uint8, device="cuda"); a.fill_(1)
+torch.cuda.synchronize()
+print(json.dumps({"held": int(sys.argv[1])}), flush=True)
+sys.stdin.readline()  # hold the memory until the parent has read the account
+"""
+
+
+def test_hbm_account_is_keyed_by_the_gpus_hip_uuid(tmp_path):
+    """A version-2 account names its GPUs: the real GPU's HIP UUID (HSA agent UUID) sits at
+    account index 1 behind a GPU this box does not have. A process that sees only that GPU (its
+    HIP ordinal 0) must charge index 1, not index 0 — so ranks with different
+    ROCR_VISIBLE_DEVICES charge one counter per physical GPU."""
+    from gpupool.agent.slots import account_bytes
+    info = subprocess.run([sys.executable, "-c",
+                           "import json,sys; sys.path.insert(0, sys.argv[1]);"
+                           "from gpupool.ops import probe; probe.init();"
+                           "print(json.dumps(probe.identify(0)))", ROOT],
+                          env=_env(), capture_output=True, text=True, timeout=120)
+    assert info.returncode == 0, info.stderr[-2000:]
+    uuid = json.loads(info.stdout.splitlines()[-1])["hipUUID"]
+    assert uuid.startswith("GPU-"), uuid
+    acct = tmp_path / "pod.acct"
+    acct.write_bytes(account_bytes(8 * GiB, ["x::0"], ["GPU-0000000000000000", uuid]))
+    p = subprocess.Popen([sys.executable, "-c", ACCT_ALLOC, str(1 * GiB)], text=True,
+                         env=_env(HSA_TOOLS_LIB=LIB, GPUPOOL_HBM_LIMIT_BYTES=8 * GiB,
+                                  GPUPOOL_SHARE_ACCOUNT=str(acct), ROCR_VISIBLE_DEVICES=uuid),
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    try:
+        assert _json(p)["held"] == 1 * GiB
+        raw = acct.read_bytes()
+    finally:
+        p.kill()
+        p.wait(timeout=30)
+    used0 = int.from_bytes(raw[64:72], "little")
+    used1 = int.from_bytes(raw[72:80], "little")
+    print(f"account: index0 {used0} B, index1 ({uuid}) {used1} B")
+    assert used0 == 0, used0
+    assert 1 * GiB <= used1 < 2 * GiB, used1

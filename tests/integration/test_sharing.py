@@ -137,7 +137,7 @@ def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_
     k.create(MI355XPOOLS, mi_pool("iso", 1, sharing={"replicasPerGPU": 4, "hbmBytesPerSlot": 8 << 30,
                                                      "cuPerSlot": 64}), "default")
     wait_ready(k, "iso", 1)
-    cmd = ["bash", "-c", "env | grep -E '^(HSA_TOOLS_LIB|GPUPOOL_CU_MASK|GPUPOOL_HBM_LIMIT_BYTES|"
+    cmd = ["bash", "-c", "env | grep -E '^(HSA_TOOLS_LIB|GPUPOOL_CU_MASK|GPUPOOL_CU_LAYOUT|GPUPOOL_HBM_LIMIT_BYTES|"
                          "GPUPOOL_SHARE_ACCOUNT|GPUPOOL_GPU_SLOTS)=' | sort; sleep 600"]
 
     def start(name: str) -> dict:
@@ -149,20 +149,39 @@ def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_
         p = k.wait_for(PODS, name, "default", running, timeout=30)
         path = p["metadata"]["annotations"]["gpupool.amd.com/log-path"]
         deadline = time.monotonic() + 10
-        while time.monotonic() < deadline and open(path).read().count("\n") < 5:
+        while time.monotonic() < deadline and open(path).read().count("\n") < 6:
             time.sleep(0.05)
         return dict(line.split("=", 1) for line in open(path).read().split())
 
     for i in range(4):
         start(f"iso{i}")
     envs = [env_of(f"iso{i}") for i in range(4)]
-    masks = sorted(e["GPUPOOL_CU_MASK"] for e in envs)
-    assert masks == ["0-63", "128-191", "192-255", "64-127"], masks
+    # 64-CU slots on an 8-XCD GPU: whole XCDs per slot (mask bit b is a CU of XCD b mod 8), so
+    # slot i owns XCDs {2i, 2i+1} and their L2s
+    from gpupool.agent.slots import slot_xcds
+    masks = {}
+    for e in envs:
+        bits = [b for r in e["GPUPOOL_CU_MASK"].split(",") for b in
+                range(int(r.split("-")[0]), int(r.split("-")[-1]) + 1)]
+        assert len(bits) == 64 and e["GPUPOOL_CU_LAYOUT"] == "xcd", e
+        masks[tuple(slot_xcds(bits, 8))] = bits
+    assert sorted(masks) == [(0, 1), (2, 3), (4, 5), (6, 7)], sorted(masks)
+    assert sorted(b for m in masks.values() for b in m) == list(range(256))
     assert all(e["GPUPOOL_HBM_LIMIT_BYTES"] == str(8 << 30) for e in envs)
     lib = envs[0]["HSA_TOOLS_LIB"]  # the container path, rewritten to the host path
     assert lib.endswith("/libgpupool_share.so") and os.path.exists(lib)
+    # mounted from the agent's copy under its state dir (the DaemonSet's hostPath), not from the
+    # agent's own tree (a path that exists only inside the agent image) — the fake kubelet runs
+    # with strict mounts and would have failed the pod otherwise
+    assert lib.startswith(c.state_dir("mi355x-node-0") + "/lib/"), lib
+    # status shows the layout per slot
+    gpu = k.get(MI355XPOOLS, "iso", "default")["status"]["devices"][0]
+    assert gpu["sharing"]["cuLayout"] == "xcd" and gpu["sharing"]["slotXcds"] == \
+        ["0-1", "2-3", "4-5", "6-7"], gpu.get("sharing")
     # one HBM account per container (shared by all its processes): the library's layout — magic,
-    # the per-GPU limit, zeroed counters, and the container's slot ids for the agent's cleanup
+    # the per-GPU limit, version 2 with the GPU's HIP UUID, zeroed counters, and the container's
+    # slot ids for the agent's cleanup
+    from gpupool.agent.slots import read_account
     accts = [e["GPUPOOL_SHARE_ACCOUNT"] for e in envs]
     assert len(set(accts)) == 4
     for e, a in zip(envs, accts):
@@ -170,7 +189,8 @@ def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_
         assert len(raw) == 16384 and raw[:8] == b"GPSHARE1", raw[:16]
         assert int.from_bytes(raw[8:16], "little") == 8 << 30
         assert not any(raw[64:8192])
-        assert raw[8192:].split(b"\0")[0].decode() == e["GPUPOOL_GPU_SLOTS"]
+        assert raw[8192:8224].split(b"\0")[0].decode() == gpu["hipUUID"]
+        assert read_account(a)["slots"] == e["GPUPOOL_GPU_SLOTS"].split(",")
     # the slot of a finished pod goes to a new pod: the old account is replaced, not reused
     k.delete(PODS, "iso0", "default")
     k.wait_for(PODS, "iso0", "default", lambda o: o is None, timeout=30)
@@ -238,3 +258,54 @@ def test_per_pod_accounting_on_a_time_shared_gpu(cluster_factory):
     rows = {ln.split()[0]: ln.split() for ln in r.stdout.splitlines()[1:]}
     assert rows["default/small"][4] == "2.00" and rows["default/big"][4] == "6.00", r.stdout
     assert rows["default/big"][5] == "0" and rows["default/small"][6] == str(pids["small"])
+
+
+def test_overcommitted_slot_budgets_are_refused(cluster_factory):
+    """replicasPerGPU x hbmBytesPerSlot must fit the GPU's HBM minus the agent's own reserve
+    (--hbm-reserve, default 2 GiB: HIP context + probe arena): 4 x 100 GiB on a 288 GiB MI355X is
+    refused with SharingOvercommitted on Ready/Progressing and no GPU is claimed; 4 x 64 GiB fits."""
+    c = cluster_factory()
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("big", 1, sharing={"replicasPerGPU": 4,
+                                                     "hbmBytesPerSlot": 100 << 30}), "default")
+    o = k.wait_for(MI355XPOOLS, "big", "default", lambda o: any(
+        x["reason"] == "SharingOvercommitted" for x in (o.get("status") or {}).get("conditions", [])),
+        timeout=30)
+    conds = {x["type"]: x for x in o["status"]["conditions"]}
+    assert conds["Ready"]["status"] == "False" and conds["Ready"]["reason"] == "SharingOvercommitted"
+    msg = conds["Progressing"]["message"]
+    assert "hbmBytesPerSlot" in msg and "reserve" in msg, msg
+    assert not o["status"].get("devices") and o["status"].get("readyReplicas", 0) == 0
+    k.create(MI355XPOOLS, mi_pool("fits", 1, sharing={"replicasPerGPU": 4,
+                                                      "hbmBytesPerSlot": 64 << 30}), "default")
+    o = wait_ready(k, "fits", 1)
+    assert o["status"]["devices"][0]["sharing"]["hbmBytesPerSlot"] == 64 << 30
+
+
+def test_hbm_account_of_an_exited_pod_is_removed(cluster_factory):
+    """The agent deletes an isolated slot's HBM account once the kubelet's PodResources lists none
+    of its slots: within one sample period of the pod's exit (after the creation grace)."""
+    import os
+    import time
+    from gpupool.testing.cluster import NodeSpec
+    c = cluster_factory(nodes=[NodeSpec("mi355x-node-0", extra_args=["--share-acct-grace", "0.2"])])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("gc", 1, sharing={"replicasPerGPU": 2,
+                                                    "hbmBytesPerSlot": 8 << 30}), "default")
+    wait_ready(k, "gc", 1)
+    share = os.path.join(c.state_dir("mi355x-node-0"), "share")
+    k.create(PODS, pause_pod("keep"), "default")
+    k.create(PODS, pause_pod("go"), "default")
+    for n in ("keep", "go"):
+        k.wait_for(PODS, n, "default", running, timeout=30)
+    assert len([f for f in os.listdir(share) if f.endswith(".acct")]) == 2
+    time.sleep(1.5)  # past the grace and several sample periods: both pods are listed, both kept
+    assert len([f for f in os.listdir(share) if f.endswith(".acct")]) == 2
+    k.delete(PODS, "go", "default", grace=0)
+    k.wait_for(PODS, "go", "default", lambda o: o is None, timeout=30)
+    t0 = time.monotonic()
+    while len([f for f in os.listdir(share) if f.endswith(".acct")]) > 1:
+        assert time.monotonic() - t0 < 3 * c.sample_interval + 1.0, os.listdir(share)
+        time.sleep(0.05)
+    print(f"account removed {time.monotonic() - t0:.2f} s after the pod was gone "
+          f"(sample period {c.sample_interval} s)")

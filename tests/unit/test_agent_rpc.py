@@ -115,3 +115,145 @@ def test_connection_cap_refuses_extra_connections():
 def test_defaults(max_conns):
     srv = RpcServer({})
     assert srv.max_conns == max_conns and srv.first_request_timeout == 10.0
+
+
+def _raw(port: int) -> socket.socket:
+    s = socket.create_connection(("127.0.0.1", port))
+    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    return s
+
+
+def _status(sock: socket.socket, timeout: float = 5.0) -> bytes:
+    sock.settimeout(timeout)
+    buf = b""
+    try:
+        while b"\r\n" not in buf:
+            chunk = sock.recv(4096)
+            if not chunk:
+                break
+            buf += chunk
+    except OSError:
+        pass
+    return buf.split(b"\r\n")[0]
+
+
+def test_negative_content_length_from_an_unauthenticated_peer_reads_nothing():
+    """Content-Length: -1 then 64 MiB from a client without the token: the server answers (401:
+    the token is checked before the body) having read no more than 64 KiB, and closes."""
+    import threading
+    srv, port = _server(token="secret")
+    try:
+        s = _raw(port)
+        s.sendall(b"POST /v1/claims HTTP/1.1\r\nHost: x\r\nContent-Length: -1\r\n\r\n")
+        sent = [0]
+
+        def flood():
+            chunk = b"x" * (1 << 20)
+            try:
+                for _ in range(64):
+                    s.sendall(chunk)
+                    sent[0] += len(chunk)
+            except OSError:
+                pass
+        t = threading.Thread(target=flood, daemon=True)
+        t.start()
+        assert _status(s).split(b" ")[1] in (b"400", b"401")
+        t.join(timeout=10)
+        assert _wait(lambda: srv.open_conns == 0)
+        assert srv.bytes_read <= 64 << 10, srv.bytes_read
+        s.close()
+    finally:
+        srv.close()
+
+
+@pytest.mark.parametrize("cl", ["-1", "abc", "+5", "0x10", " 12 3"])
+def test_bad_content_length_is_400_before_any_body(cl):
+    srv, port = _server(token="secret")
+    try:
+        s = _raw(port)
+        s.sendall(f"POST /v1/ping HTTP/1.1\r\nAuthorization: Bearer secret\r\n"
+                  f"Content-Length: {cl}\r\n\r\n".encode() + b"y" * 4096)
+        assert b"400" in _status(s)
+        assert _closed(s, 3.0)
+        s2 = _raw(port)  # a body-carrying method without Content-Length is refused too
+        s2.sendall(b"POST /v1/ping HTTP/1.1\r\nAuthorization: Bearer secret\r\n\r\n")
+        assert b"400" in _status(s2)
+        s.close()
+        s2.close()
+    finally:
+        srv.close()
+
+
+def test_header_drip_is_closed_at_the_absolute_deadline():
+    """One header byte every 1.5 s kept a per-recv timeout alive forever; the deadline is absolute:
+    the connection closes first_request_timeout (2.0 s) after accept, +-0.5 s, and its slot is
+    freed."""
+    import threading
+    srv, port = _server(first_request_timeout=2.0)
+    try:
+        s = _raw(port)
+        t0 = time.monotonic()
+        stop = threading.Event()
+
+        def drip():
+            for ch in b"GET /v1/ping HTTP/1.1\r\nX-Slow: " + b"a" * 64:
+                try:
+                    s.sendall(bytes([ch]))
+                except OSError:
+                    return
+                if stop.wait(1.5):
+                    return
+        threading.Thread(target=drip, daemon=True).start()
+        s.settimeout(6.0)
+        try:
+            got = s.recv(1)
+        except OSError:
+            got = b""
+        elapsed = time.monotonic() - t0
+        stop.set()
+        assert got == b"", got
+        assert 1.5 <= elapsed <= 2.5, elapsed
+        assert _wait(lambda: srv.open_conns == 0)
+        assert any(ln == "gpupool_agent_rpc_deadline_closed_connections_total 1" or
+                   ln.startswith("gpupool_agent_rpc_deadline_closed_connections_total")
+                   for ln in srv.metrics_lines())
+        s.close()
+    finally:
+        srv.close()
+
+
+def test_too_many_headers_are_refused():
+    srv, port = _server()
+    try:
+        s = _raw(port)
+        s.sendall(b"GET /v1/ping HTTP/1.1\r\n" + b"".join(f"X-{i}: v\r\n".encode() for i in range(200))
+                  + b"\r\n")
+        assert b"431" in _status(s)
+        assert _closed(s, 3.0)
+        s.close()
+    finally:
+        srv.close()
+
+
+def test_post_reply_hook_runs_when_the_peer_is_gone():
+    """A claim's reply hook ends its event hold (release_events): it must run even when writing the
+    reply fails because the manager gave up and reset the connection."""
+    import struct
+    import threading
+    ran = threading.Event()
+
+    def slow(q, b):
+        time.sleep(0.3)
+        return json_reply({"ok": True}, after=ran.set)
+    srv = RpcServer({("POST", "/v1/claims"): slow})
+    srv.listen_tcp("127.0.0.1", 0)
+    port = srv._listeners[-1].getsockname()[1]
+    try:
+        s = _raw(port)
+        s.sendall(b"POST /v1/claims HTTP/1.1\r\nContent-Length: 2\r\n\r\n{}")
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+        s.close()  # RST: the server's write of the reply fails
+        assert ran.wait(5.0)
+        assert _wait(lambda: srv.open_conns == 0)
+    finally:
+        srv.close()
