@@ -336,6 +336,15 @@ def main() -> int:
             cs = [cy for cy in cycles if cy["n"] == k]
             per_n[str(k)] = summary([cy["readySeconds"] for cy in cs], sum(cy["ok"] for cy in cs))
             per_n[str(k)].update(_device_evidence(cs))
+            # the agent at this N: its resident memory, the HIP contexts it holds, and the VRAM
+            # in use on the GPUs the last cycle of this N claimed (after the timed region)
+            fa = (footprint_after or {}).get("agent") or {}
+            if "rss_mib" in fa:
+                vram = fa.get("vram_used_mib") or {}
+                idx = cs[-1].get("indices") or [] if cs else []
+                per_n[str(k)]["agent"] = {
+                    "rss_mib": fa["rss_mib"], "hip_devices": fa.get("hip_devices"),
+                    "vram_used_mib_per_gpu": [vram.get(i) for i in idx]}
             if str(k) in errors:
                 per_n[str(k)]["errors"] = errors[str(k)]
                 first = errors[str(k)][0]

@@ -45,7 +45,10 @@ def main() -> None:
     ap.add_argument("--pod-resources", default="", help="kubelet PodResources socket")
     ap.add_argument("--probe", default="", choices=["", "inproc", "subprocess", "simulated", "off"])
     ap.add_argument("--probe-sim-ms", type=float, default=20.0)
-    ap.add_argument("--probe-gemm-n", type=int, default=4096)
+    ap.add_argument("--probe-gemm-n", type=int, default=4096,
+                    help="GEMM size of the serial probe (pools with performance floors)")
+    ap.add_argument("--probe-overlap-gemm-n", type=int, default=2048,
+                    help="GEMM size of the claim-time probe, which overlaps the HBM pattern test")
     ap.add_argument("--sample-interval", type=float, default=2.0,
                     help="full telemetry sample period (s): activity, power, VRAM, bad pages, pods")
     ap.add_argument("--health-interval", type=float, default=0.1,
@@ -99,6 +102,7 @@ def main() -> None:
                       endpoint=a.endpoint, apiserver=a.apiserver, token=a.token,
                       plugin_dir=a.plugin_dir, pod_resources=a.pod_resources, probe_mode=a.probe,
                       probe_sim_ms=a.probe_sim_ms, probe_gemm_n=a.probe_gemm_n,
+                      probe_overlap_gemm_n=a.probe_overlap_gemm_n,
                       sample_interval=a.sample_interval, health_interval=a.health_interval,
                       quarantine_s=a.quarantine,
                       fsync=not a.no_fsync, probe_arena_idle_s=a.probe_arena_idle,

@@ -141,7 +141,8 @@ class AgentConfig:
     pod_resources: str = ""          # kubelet PodResources socket
     probe_mode: str = ""             # inproc | subprocess | simulated | off (default by backend)
     probe_sim_ms: float = 20.0
-    probe_gemm_n: int = 4096
+    probe_gemm_n: int = 4096          # serial probe's GEMM (pools with performance floors)
+    probe_overlap_gemm_n: int = 2048  # claim-time probe's GEMM beside the HBM pattern test
     sample_interval: float = 2.0
     health_interval: float = 0.1     # fast poll of the health-only fields (0 = off)
     pod_watch_interval: float = 0.02  # PodResources poll while a GPU drains / after an Allocate
@@ -210,7 +211,8 @@ class Agent:
         self.plugins: dict = {}
         self.probe_mode = cfg.probe_mode or default_mode(self.backend)
         self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n,
-                             arena_idle_s=cfg.probe_arena_idle_s)
+                             arena_idle_s=cfg.probe_arena_idle_s,
+                             overlap_gemm_n=cfg.probe_overlap_gemm_n)
         self.last_probe: dict[str, dict] = {}
         self._probe_mono: dict[str, float] = {}  # uuid -> monotonic time of its last probe
         # admin maintenance (gpuctl gpu cordon): uuid -> reason; persisted as a quarantine entry
@@ -1031,8 +1033,9 @@ class Agent:
             sharing = policy.get("sharing") or {}
             overcommitted = ""
             for d, ok in zip(cand, self._claimable(cand, policy, policy_key)):
-                why = slotlib.overcommit(sharing, int(d.get("memTotalBytes") or 0),
-                                         self.cfg.hbm_reserve_bytes) if ok else ""
+                why = (slotlib.overcommit(sharing, int(d.get("memTotalBytes") or 0),
+                                          self.cfg.hbm_reserve_bytes)
+                       or slotlib.cu_floor(sharing, d)) if ok else ""
                 if why:
                     overcommitted = why
                 elif ok:
@@ -1053,7 +1056,8 @@ class Agent:
                 sel = devlib.select(count, free, owned, req.get("topologyPolicy", "xgmi-packed"),
                                     weights, numa)
             if len(sel) < count and overcommitted:
-                return {"ok": False, "reason": "SharingOvercommitted",
+                return {"ok": False, "reason": "SharingOvercommitted" if "hbmBytesPerSlot"
+                        in overcommitted else "SharingCUsBelowXCDs",
                         "message": f"{overcommitted} on {self.cfg.node}", "devices": []}
             if len(sel) < count:
                 return {"ok": False, "reason": "InsufficientDevices",
@@ -1732,20 +1736,19 @@ class Agent:
         """spec.sharing.hbmBytesPerSlot / cuPerSlot of the pool owning these slots: the ROCm
         runtime loads libgpupool_share.so (HSA_TOOLS_LIB) into the pod, which caps its HBM per
         GPU at (its slots on that GPU) x hbmBytesPerSlot and confines its queues to its slots'
-        CUs — whole XCDs per slot when they divide evenly (each slot then has its own L2s), else
-        contiguous mask bits; disjoint from the other slots either way (slots.py). The library
-        is mounted from its host copy under the state dir. Called under self.lock."""
+        CUs — contiguous mask bits, disjoint from the other slots, the same number of CUs on every
+        XCD (slots.py: why not whole XCDs). The library is mounted from its host copy under the
+        state dir. Called under self.lock."""
         per_gpu: dict[str, list[int]] = {}
         for sid in slots:
             u, _, i = sid.partition(SLOT_SEP)
             per_gpu.setdefault(u, []).append(int(i or 0))
-        hbm, cu_mask, layouts = 0, set(), set()
+        hbm, cu_mask = 0, set()
         for u, idx in per_gpu.items():
             lay = self._slot_layout(u, self.records.get(u) or {})
             if lay.get("hbmBytesPerSlot"):
                 hbm = max(hbm, lay["hbmBytesPerSlot"] * len(idx))
             if "masks" in lay:
-                layouts.add(lay["cuLayout"])
                 for i in idx:
                     cu_mask.update(lay["masks"][i % len(lay["masks"])])
         if not hbm and not cu_mask:
@@ -1760,7 +1763,7 @@ class Agent:
             env["GPUPOOL_HBM_LIMIT_BYTES"] = str(hbm)
         if cu_mask:
             env["GPUPOOL_CU_MASK"] = _ranges(sorted(cu_mask))
-            env["GPUPOOL_CU_LAYOUT"] = "xcd" if layouts == {"xcd"} else "striped"
+            env["GPUPOOL_CU_LAYOUT"] = "striped"
         return env
 
     # ================================================================ node registration
@@ -1905,6 +1908,9 @@ class Agent:
             for k, v in self.scrubber.stats.items():
                 lines.append(f"gpupool_agent_hbm_scrub_{k}_total {v}")
             lines.append(f"gpupool_agent_gen {self.gen}")
+            # devices the in-process HIP probe initialised (each holds a HIP context's VRAM)
+            lines.append(f"gpupool_agent_hip_devices {len(self.prober.ordinals)}")
+            lines.append(f"gpupool_agent_hip_init_ms {self.prober.init_ms:.1f}")
         lines += process_metrics()
         return "\n".join(lines) + "\n"
 

@@ -95,6 +95,8 @@ class DevicePluginServer:
         self._sender = threading.Thread(target=self._send_loop, daemon=True,
                                         name=f"dp-send-{self.resource}")
         self._sender.start()
+        self._streams_lost = False
+        self._kch = None
         self.register()  # synchronous first registration; the monitor handles kubelet restarts
         self._mon = threading.Thread(target=self._monitor_kubelet, daemon=True,
                                      name=f"dp-mon-{self.resource}")
@@ -114,6 +116,9 @@ class DevicePluginServer:
                 st.send(None)
             except Exception:
                 pass
+        kch = getattr(self, "_kch", None)
+        if kch is not None:
+            kch.close()
         if self.server:
             self.server.stop(grace=0.5)
         try:
@@ -134,11 +139,35 @@ class DevicePluginServer:
                                        resource_name=self.resource, options=opts), timeout=5)
             self.registered = True
             self._kubelet_ino = self._sock_identity(ksock)
+            self._watch_kubelet(ksock)
             log.info("registered %s with kubelet at %s", self.resource, ksock)
             return True
         except (grpc.RpcError, OSError) as e:
             log.warning("register %s failed: %s", self.resource, e)
             return False
+
+    def _watch_kubelet(self, ksock: str) -> None:
+        """A kubelet restart shows as a new socket identity — unless the new socket reuses the
+        inode within one ctime tick (tmpfs). So a channel to the kubelet is also kept connected:
+        when it drops out of READY the kubelet went away, and the monitor re-registers once a
+        kubelet answers again. No idle timeout: a quiet kubelet is not a restarted one."""
+        old = getattr(self, "_kch", None)
+        ch = grpc.insecure_channel(unix_target(ksock),
+                                   options=[("grpc.client_idle_timeout_ms", 2**31 - 1)])
+        was_ready = [False]
+
+        def on_state(state) -> None:
+            if self._kch is not ch or self.stopped:
+                return  # a replaced or closed watch channel says nothing about the kubelet
+            if state == grpc.ChannelConnectivity.READY:
+                was_ready[0] = True
+            elif was_ready[0]:
+                was_ready[0] = False
+                self._streams_lost = True
+        self._kch = ch
+        ch.subscribe(on_state, try_to_connect=True)
+        if old is not None:
+            old.close()
 
     def _monitor_kubelet(self) -> None:
         ksock = os.path.join(self.plugin_dir, KUBELET_SOCKET)
@@ -146,8 +175,9 @@ class DevicePluginServer:
             ident = self._sock_identity(ksock)
             if ident is None:
                 self.registered = False  # kubelet gone: register again when it comes back
-            elif ident != self._kubelet_ino:
-                self.register()
+            elif ident != self._kubelet_ino or (self._streams_lost and not self.stopped):
+                if self.register():  # a kubelet that is not answering yet keeps the signal
+                    self._streams_lost = False
             time.sleep(0.2)
 
     @staticmethod
@@ -263,7 +293,15 @@ class DevicePluginServer:
                 if st in self._live:
                     self._live.discard(st)
                     self.streams -= 1
-            self._mark(self.version, None)  # no stream left -> nothing counts as advertised
+                last = not self._live
+            # only when no stream is left does nothing count as advertised: a restarted kubelet's
+            # new stream may already have marked its list when the old stream's callback fires
+            if last:
+                self._mark(self.version, None)
+                # every stream ended: the kubelet went away (or restarted). Its new socket can
+                # carry the old (inode, ctime) on tmpfs when it comes back within one timestamp
+                # tick, so the monitor also re-registers on this signal
+                self._streams_lost = True
         with self.cv:
             self._live.add(st)
             self.streams += 1

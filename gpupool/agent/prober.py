@@ -27,10 +27,14 @@ log = logging.getLogger("gpupool.agent.prober")
 
 class Prober:
     def __init__(self, mode: str = "inproc", sim_ms: float = 20.0, gemm_n: int = 4096,
-                 max_workers: int = 16, arena_idle_s: float = 10.0):
+                 max_workers: int = 16, arena_idle_s: float = 10.0, overlap_gemm_n: int = 2048):
         self.mode = mode
         self.sim_ms = sim_ms
-        self.gemm_n = gemm_n
+        self.gemm_n = gemm_n                  # serial probe (pools with performance floors)
+        # the claim-time probe's GEMM when it overlaps the HBM pattern test: the element check,
+        # ABFT and the all-CU census run whatever its size, and a smaller GEMM takes less HBM
+        # bandwidth from the pattern test (profiles/r4_probe_gemm_overlap_ab.json)
+        self.overlap_gemm_n = overlap_gemm_n
         self.pool = cf.ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix="probe")
         self.ordinals: dict[str, int] = {}
         self.init_ms = 0.0
@@ -90,7 +94,8 @@ class Prober:
             # The HBM test and the MFMA phase normally overlap on two streams (~13 % shorter
             # probe). With performance floors the pool wants clean numbers: run them serially.
             floors = float(opts.get("minHbmGBps") or 0) > 0 or float(opts.get("minMfmaTflops") or 0) > 0
-            res = self._hip.run(ordinal, hbm_bytes=hbm, mfma=mfma, gemm_n=self.gemm_n,
+            res = self._hip.run(ordinal, hbm_bytes=hbm, mfma=mfma,
+                                gemm_n=self.gemm_n if floors else self.overlap_gemm_n,
                                 overlap=0 if floors else 1)
         else:
             cmd = [native_path("mi355x-probe"), "--device", str(ordinal), "--hbm-bytes", str(hbm),

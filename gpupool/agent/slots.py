@@ -3,12 +3,21 @@ GPU调度平台搭建.md:289-298): which CUs a slot's queues may use, whether a 
 the GPU, and the pod-wide HBM account file libgpupool_share.so charges (native/src/share/share.cc).
 
 CU layout. ROCr's queue CU mask interleaves its bits over the XCDs: on an SPX MI355X (8 XCDs x 32
-CUs) bit b is a CU of XCD b mod 8 (measured with the probe's CU census, profiles/r3b_sharing_gpu.txt
-— a contiguous 64-bit range lands 8 CUs on every XCD). So a contiguous ("striped") slot spreads over
-every XCD and shares all eight 4 MB L2s with its siblings. When a slot is a whole number of XCDs and
-the slots fit (cuPerSlot a multiple of the XCD's CUs, replicasPerGPU x XCDs-per-slot <= XCDs), slot i
-is given whole XCDs instead — bits {b : b mod X in slot i's XCDs} — and so an L2 of its own
-("xcd" layout). Otherwise the striped layout is kept. A CPX partition is one XCD: always striped.
+CUs) bit b is a CU of XCD b mod 8. And the dispatcher deals a kernel's workgroups round-robin over
+all 8 XCDs whatever the mask, so a queue needs CUs on every XCD. Measured on the MI355X
+(profiles/r4b_cu_mask_layouts.json, probe CU census per XCD):
+
+  * a mask that leaves any XCD empty is NOT applied — silently: ROCr reports success and the
+    queue runs on all 256 CUs (XCDs {0,1} only, XCDs {0..3}, every XCD but 7: all 256 CUs);
+  * with at least one CU on every XCD the mask holds (XCDs 0,1 whole + 1 CU on each other XCD:
+    exactly those 70 CUs) — but the round-robin then queues 6/8 of the workgroups on 6 single CUs.
+
+So an SPX slot cannot own whole XCDs (nor an L2 of its own: every slot runs on every XCD), and the
+balanced layout is the right one: slot i takes the contiguous bits [i*c, (i+1)*c), which land c/8
+CUs on each XCD ("striped"). A slot of fewer CUs than the partition has XCDs would leave XCDs empty
+and so run unconfined: such a pool is refused (``cu_floor``). L2 isolation between tenants comes
+from compute partitions instead (spec.partition.compute DPX/QPX/CPX: each logical GPU has XCDs and
+L2s of its own), with slots subdividing a partition.
 """
 from __future__ import annotations
 
@@ -30,23 +39,35 @@ def xcd_count(dev: dict) -> int:
 
 
 def slot_cus(slot: int, slots: int, cu_per_slot: int, cus: int, xcds: int) -> tuple[list[int], str]:
-    """CU-mask bits of ``slot`` (of ``slots`` on the GPU) and the layout: ``"xcd"`` (whole XCDs) or
-    ``"striped"`` (a contiguous range, interleaved over every XCD). ``cu_per_slot`` is narrowed to
-    the GPU's own share (cus // slots), as the striped layout always did."""
-    cus, xcds, slots = max(1, cus), max(1, xcds), max(1, slots)
+    """CU-mask bits of ``slot`` (of ``slots`` on the GPU) and the layout ("striped": contiguous
+    bits, cu/xcds CUs on every XCD). ``cu_per_slot`` is narrowed to the GPU's own share
+    (cus // slots)."""
+    cus, slots = max(1, cus), max(1, slots)
     cu = max(1, min(cu_per_slot, cus // slots))
-    per_xcd = cus // xcds
-    if xcds > 1 and per_xcd > 0 and cus % xcds == 0 and cu % per_xcd == 0:
-        span = cu // per_xcd  # XCDs per slot
-        if slots * span <= xcds:
-            mine = set(range(slot * span, (slot + 1) * span))
-            return [b for b in range(cus) if b % xcds in mine], "xcd"
     return list(range(slot * cu, (slot + 1) * cu)), "striped"
 
 
 def slot_xcds(bits: list[int], xcds: int) -> list[int]:
     """The XCDs a mask's bits land on (the interleave above)."""
     return sorted({b % max(1, xcds) for b in bits})
+
+
+def cu_floor(sharing: dict, dev: dict) -> str:
+    """Why a pool's cuPerSlot cannot be confined on this GPU (fewer CUs per slot than the
+    partition has XCDs: some XCD would get none, and the hardware would ignore the whole mask),
+    or "" when it can."""
+    cu = int((sharing or {}).get("cuPerSlot") or 0)
+    if cu <= 0:
+        return ""
+    k = max(1, int((sharing or {}).get("replicasPerGPU") or 1))
+    cus = int(((dev or {}).get("asic") or {}).get("computeUnits") or 256)
+    xcds = xcd_count(dev)
+    bits, _ = slot_cus(0, k, cu, cus, xcds)
+    if len(slot_xcds(bits, xcds)) >= xcds:
+        return ""
+    return (f"cuPerSlot {cu} (x replicasPerGPU {k} on {cus} CUs) leaves XCDs of this "
+            f"{xcds}-XCD GPU without CUs: the hardware would not apply the mask — use at least "
+            f"{xcds} CUs per slot")
 
 
 def overcommit(sharing: dict, mem_total: int, reserve: int) -> str:

@@ -185,11 +185,11 @@ DEVICE_STATUS = {
             "type": "object",
             "description": "Slot isolation of a shared GPU (spec.sharing): the enforced per-slot "
                            "HBM budget (never above a fair share of the HBM the agent leaves "
-                           "free), and per slot its CU-mask bits and the XCDs they land on. "
-                           "cuLayout xcd: every slot owns whole XCDs, so an L2 of its own; "
-                           "striped: slots interleave over every XCD and share the L2s.",
+                           "free), and per slot its CU-mask bits and the XCDs they land on "
+                           "(cuLayout striped: the same number of CUs on every XCD; slots share "
+                           "the XCDs' L2s — L2 isolation takes a compute partition).",
             "properties": {"replicasPerGPU": _I32, "hbmBytesPerSlot": _I64,
-                           "cuLayout": {"type": "string", "enum": ["xcd", "striped"]},
+                           "cuLayout": {"type": "string", "enum": ["striped"]},
                            "cuPerSlot": _I32, "xcds": _I32,
                            "slotCUMasks": {"type": "array", "items": _S},
                            "slotXcds": {"type": "array", "items": _S}},
@@ -248,7 +248,10 @@ MI355X_SPEC = {
                            "the pod's HBM allocations per GPU at hbmBytesPerSlot (hipMalloc & co "
                            "fail with hipErrorOutOfMemory past it, hipMemGetInfo reports the "
                            "budget) and confines its waves to cuPerSlot CUs, disjoint from the "
-                           "other slots of the GPU. Without them the sharers are only "
+                           "other slots of the GPU and spread evenly over its XCDs (a kernel's "
+                           "workgroups are dealt to every XCD, so a slot needs CUs on each: "
+                           "cuPerSlot must be at least the partition's XCD count, 8 on SPX). "
+                           "Without them the sharers are only "
                            "time-sliced. A GPU is drained and released only when every pod on "
                            "any of its slots is gone.",
             "properties": {

@@ -188,6 +188,7 @@ class BenchRun:
         self.phase = "release"
         self.scale(name, 0)
         return {"n": n, "readySeconds": t_ready, "ok": ok, "truth": truth,
+                "indices": [d.get("index") for d in obj["status"]["devices"]],
                 "patchAt": patch_at, "readyAtWall": ready_at_wall, "patchRttMs": patch_rtt * 1e3,
                 "probeMs": [round(d.get("probe", {}).get("ms", 0.0), 3)
                             for d in obj["status"]["devices"]],
@@ -499,6 +500,17 @@ class BenchRun:
                             "threads": int(vals.get("process_threads", 0)),
                             "open_fds": int(vals.get("process_open_fds", 0)),
                             "cpu_s": round(vals.get("process_cpu_seconds_total", 0.0), 2)}
+                if who == "agent":
+                    # HIP contexts the agent holds, and every GPU's VRAM in use (amdsmi): with N
+                    # devices initialised, what the agent costs each GPU and the node
+                    import re
+                    text = str(get())
+                    m = re.search(r"^gpupool_agent_hip_devices (\d+)", text, re.M)
+                    out[who]["hip_devices"] = int(m.group(1)) if m else None
+                    out[who]["vram_used_mib"] = {
+                        int(i): round(float(v) / 2**20, 1) for i, v in re.findall(
+                            r'^gpupool_device_vram_used_bytes\{[^}]*index="(\d+)"[^}]*\} ([0-9.e+]+)',
+                            text, re.M)}
             except Exception as e:  # never fail the bench over a diagnostic
                 out[who] = {"error": repr(e)[:200]}
         return out

@@ -129,8 +129,20 @@ def dump(obj: Any, fmt: str) -> None:
 
 # ------------------------------------------------------------------ commands
 def cmd_apply(c: Client, ns: str, args) -> int:
+    from .convert import ConvertError, convert, convertible
     rc = 0
     for doc in load_docs(args.filename):
+        if convertible(doc):  # the reference's Volcano Job / Kubeflow PyTorchJob: as a Mi355xJob
+            try:
+                doc, warns = convert(doc)
+            except ConvertError as e:
+                print(f"error: {e}", file=sys.stderr)
+                rc = 1
+                continue
+            print(f"converted {doc['metadata']['annotations']['gpupool.amd.com/converted-from']} "
+                  f"{doc['metadata']['name']} to Mi355xJob", file=sys.stderr)
+            for w in warns:
+                print(f"warning: {w}", file=sys.stderr)
         try:
             action, out = c.apply(doc, ns, dry_run=args.dry_run)
             suffix = " (dry run)" if args.dry_run else ""
@@ -611,6 +623,29 @@ def cmd_trainjob(c: Client, ns: str, args) -> int:
     return 2
 
 
+def cmd_convert(args) -> int:
+    """``gpuctl convert -f vcjob.yaml``: a Volcano Job or Kubeflow PyTorchJob as a Mi355xJob (no
+    server needed); warnings for what has no equivalent go to stderr."""
+    from .convert import ConvertError, convert
+    rc, out = 0, []
+    for doc in load_docs(args.filename):
+        try:
+            job, warns = convert(doc, pool=args.pool, resource=args.resource, image=args.image)
+        except ConvertError as e:
+            print(f"error: {e}", file=sys.stderr)
+            rc = 1
+            continue
+        for w in warns:
+            print(f"warning: {job['metadata']['name']}: {w}", file=sys.stderr)
+        out.append(job)
+    if args.output == "json":
+        print(json.dumps(out[0] if len(out) == 1 else {"apiVersion": "v1", "kind": "List",
+                                                         "items": out}, indent=2))
+    else:
+        print(yaml.safe_dump_all(out, sort_keys=False, allow_unicode=True).rstrip())
+    return rc
+
+
 def cmd_render(c, ns, args) -> int:
     for d in load_docs(args.filename):
         dump(render_job(d), args.output or "yaml")
@@ -760,6 +795,12 @@ def build_parser() -> argparse.ArgumentParser:
     for verb in ("suspend", "resume"):
         t = tsub.add_parser(verb, help=f"{verb} a job (spec.suspend): GPUs freed / re-queued")
         t.add_argument("job")
+    p = sub.add_parser("convert", help="Volcano Job / Kubeflow PyTorchJob -> Mi355xJob")
+    p.add_argument("-f", "--filename", required=True)
+    p.add_argument("--pool", default=None, help="spec.poolRef of the converted job")
+    p.add_argument("--resource", default=None, help="spec.resourceName (default: the pool's)")
+    p.add_argument("--image", default=None, help="replace the containers' image (e.g. a ROCm one)")
+    p.add_argument("-o", "--output", default="yaml", choices=["yaml", "json"])
     p = sub.add_parser("render")
     p.add_argument("what", choices=["job"])
     p.add_argument("-f", "--filename", required=True)
@@ -788,6 +829,8 @@ def main(argv: list[str] | None = None) -> int:
         return cmd_config(args)
     if args.cmd == "login":
         return cmd_login(args)
+    if args.cmd == "convert":
+        return cmd_convert(args)
     c, ns = connection(args)
     fn = {"apply": cmd_apply, "get": cmd_get, "describe": cmd_describe, "delete": cmd_delete,
           "scale": cmd_scale, "wait": cmd_wait, "logs": cmd_logs, "events": cmd_events,

@@ -2,10 +2,14 @@
 
 The operator's promise to a multi-GPU pod is that its GPUs talk to each other: `torch.distributed`
 over RCCL (backend "nccl" IS RCCL on ROCm) riding the xGMI mesh — the path DDP's gradient
-all-reduce takes (gpupool/parallel/ddp.py). One process per GPU all-reduces a bf16 buffer: the
-result is checked exactly (every element must equal the world size) and the achieved bandwidth is
-reported as algorithm and bus bandwidth (busbw = algbw * 2(n-1)/n, the ring all-reduce's per-link
-traffic — on an 8x MI355X node each of a GPU's 7 xGMI links carries one ring's share).
+all-reduce takes (gpupool/parallel/ddp.py). One process per GPU:
+
+  * exactness: rank r contributes a buffer of r + 1 (fp32, exact to 2^24), so the sum must be
+    world(world+1)/2 everywhere — a value only a real reduction over every rank's data produces.
+    A rank that skipped the collective, or a local copy (world = 1 aside), keeps r + 1 and fails;
+  * bandwidth: a bf16 buffer all-reduced ``--iters`` times, reported as algorithm and bus bandwidth
+    (busbw = algbw * 2(n-1)/n, the ring all-reduce's per-link traffic — on an 8x MI355X node each
+    of a GPU's 7 xGMI links carries one ring's share).
 
 bench.py launches it once per rank after its timed region when N > 1 GPUs are real (each in its own
 child process under a time limit, so a fabric problem cannot hang the bench) and reports it as
@@ -32,6 +36,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--inject", default="", choices=["", "skip-reduce"],
+                    help="test hook: skip the exactness reduction on this rank")
     a = ap.parse_args()
 
     import torch
@@ -50,11 +56,19 @@ def main() -> int:
     def sync():
         if a.device == "cuda":
             torch.cuda.synchronize(dev)
+    chk = torch.full((1 << 16,), float(a.rank + 1), dtype=torch.float32, device=dev)
+    if a.inject == "skip-reduce":
+        dist.all_reduce(chk.clone())  # joins the collective (peers do not hang), drops the result
+    else:
+        dist.all_reduce(chk)
+    want = a.world * (a.world + 1) // 2
+    sync()
+    got = chk.cpu()
+    ok = bool((got == want).all().item())
     for _ in range(a.warmup):
         x.fill_(1)
         dist.all_reduce(x)
     sync()
-    ok = bool((x == a.world).all().item())  # world <= 256 is exact in bf16
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.iters):
@@ -64,7 +78,8 @@ def main() -> int:
     algbw = a.bytes / dt / 1e9
     out = {"rank": a.rank, "world": a.world, "backend": a.backend, "bytes": a.bytes,
            "iters": a.iters, "ms": round(dt * 1e3, 3), "algbw_GBps": round(algbw, 1),
-           "busbw_GBps": round(algbw * 2 * (a.world - 1) / a.world, 1), "exact": ok}
+           "busbw_GBps": round(algbw * 2 * (a.world - 1) / a.world, 1), "exact": ok,
+           "expected": want, "got": [float(got.min()), float(got.max())]}
     if a.device == "cuda":
         out["device"] = torch.cuda.get_device_properties(dev).name
     print(json.dumps(out), flush=True)

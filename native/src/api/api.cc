@@ -265,6 +265,17 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
     if (cu < 0 || cu > 256) errs.push_back("spec.sharing.cuPerSlot: must be within [0, 256]");
     else if (cu > 0 && cu * k > 256)
       errs.push_back("spec.sharing.cuPerSlot: cuPerSlot x replicasPerGPU must not exceed the GPU's 256 CUs");
+    else if (cu > 0) {
+      // a queue's workgroups are dealt to every XCD of the (partition of the) GPU, and a CU mask
+      // that leaves an XCD empty is not applied at all (profiles/r4b_cu_mask_layouts.json): a
+      // slot needs at least one CU per XCD — 8 on SPX (the "Any" default may land there)
+      const std::string part = s.path("partition.compute").str_or("Any");
+      const int64_t xcds = part == "CPX" ? 1 : part == "QPX" ? 2 : part == "DPX" ? 4 : 8;
+      if (cu < xcds)
+        errs.push_back("spec.sharing.cuPerSlot: must be at least " + std::to_string(xcds) +
+                       " (one CU per XCD of a " + (part == "Any" ? std::string("SPX") : part) +
+                       " GPU), or 0");
+    }
     if (s.path("sharing.hbmBytesPerSlot").as_int(0) < 0)
       errs.push_back("spec.sharing.hbmBytesPerSlot: should be greater than or equal to 0");
   }

@@ -1,20 +1,22 @@
 #!/usr/bin/env python3
-"""Slot-interference A/B on one MI355X: striped vs XCD-aligned CU masks (gpupool/agent/slots.py).
+"""Slot-interference A/B on one MI355X: CU-masked slots vs plain time-slicing.
 
 Four 64-CU slots per GPU (spec.sharing replicasPerGPU=4, cuPerSlot=64). Slot A (slot 0) is the
-victim, slot B (slot 1) the aggressor; each is its own process with libgpupool_share.so loaded
-through HSA_TOOLS_LIB and GPUPOOL_CU_MASK, exactly as an isolated slot's Allocate sets it up.
+victim, slot B (slot 1) the aggressor; each is its own process, loading libgpupool_share.so through
+HSA_TOOLS_LIB with GPUPOOL_CU_MASK exactly as an isolated slot's Allocate sets it up.
 
-  striped: A = mask bits 0-63, B = 64-127   (every slot on all 8 XCDs: all L2s shared)
-  xcd:     A = bits b%8 in {0,1}, B = {2,3} (each slot owns 2 XCDs and their L2s)
+  striped:  A = mask bits 0-63, B = 64-127 (the agent's layout: 8 CUs of every XCD each; the
+            slots share the XCDs' L2s — whole-XCD masks are not applied by the hardware,
+            profiles/r4b_cu_mask_layouts.json)
+  unmasked: A and B both on all 256 CUs (replicasPerGPU without cuPerSlot: time-slicing only)
 
 Per layout and round (layouts interleaved round by round), the victim measures alone and then
 while the aggressor streams HBM (2 GiB copy, L2-thrashing):
-  * gemm   — torch bf16 4096^3 matmul TFLOP/s (hipBLASLt), median of 10 timed batches of 10;
-  * l2     — libmi355x_interfere.so L2-resident re-read of a 2 MB buffer, GB/s (median of 20);
-and a CU census of the victim's mask (probe cuKeys: CUs per XCD) proves the layout.
+  * gemm — torch bf16 4096^3 matmul TFLOP/s (hipBLASLt), median of 10 timed batches of 10;
+  * l2   — libmi355x_interfere.so L2-resident re-read of a 2 MB buffer, GB/s (median of 20);
+and a CU census of each mask proves what the slot really runs on.
 
-    python scripts/xcd_interference_ab.py --rounds 3 --out gpurun_out/xcd_ab.json
+    python scripts/slot_interference_ab.py --rounds 3 --out gpurun_out/slot_ab.json
 """
 from __future__ import annotations
 
@@ -85,10 +87,12 @@ print(json.dumps({"cus": len(r["cus"]["cuKeys"]), "perXcd": r["cus"]["perXcd"]})
 """
 
 
-def env_for(mask: list[int]) -> dict:
-    env = dict(os.environ, PYTHONPATH=ROOT, HSA_TOOLS_LIB=SHARE, GPUPOOL_CU_MASK=_ranges(mask))
-    for k in ("GPUPOOL_HBM_LIMIT_BYTES", "GPUPOOL_SHARE_ACCOUNT"):
+def env_for(mask: list[int] | None) -> dict:
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("HSA_TOOLS_LIB", "GPUPOOL_CU_MASK", "GPUPOOL_HBM_LIMIT_BYTES", "GPUPOOL_SHARE_ACCOUNT"):
         env.pop(k, None)
+    if mask is not None:
+        env.update(HSA_TOOLS_LIB=SHARE, GPUPOOL_CU_MASK=_ranges(mask))
     return env
 
 
@@ -101,7 +105,7 @@ def run_json(code: str, args: list[str], env: dict, timeout: float = 120) -> dic
     return json.loads(lines[-1])
 
 
-def victim(mask: list[int]) -> dict:
+def victim(mask: list[int] | None) -> dict:
     env = env_for(mask)
     out = {"gemm": run_json(GEMM, [], env)["tflops"]}
     l2 = run_json(L2, [INTERFERE], env)
@@ -111,7 +115,7 @@ def victim(mask: list[int]) -> dict:
     return out
 
 
-def contended(mask_a: list[int], mask_b: list[int], seconds: float) -> dict:
+def contended(mask_a: list[int] | None, mask_b: list[int] | None, seconds: float) -> dict:
     agg = subprocess.Popen([sys.executable, "-c", STREAM, INTERFERE, str(seconds)], env=env_for(mask_b),
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     try:
@@ -140,21 +144,18 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--seconds", type=float, default=20.0, help="aggressor duration per round")
-    ap.add_argument("--out", default="gpurun_out/xcd_ab.json")
+    ap.add_argument("--out", default="gpurun_out/slot_ab.json")
     a = ap.parse_args()
     for p in (SHARE, INTERFERE):
         if not os.path.exists(p):
             raise SystemExit(f"{p} missing: make -C native")
-    layouts = {}
-    for name, cu in (("striped", None), ("xcd", 64)):
-        ma, la = slot_cus(0, 4, 64, 256, 8 if cu else 1)  # xcds=1 forces the striped layout
-        mb, lb = slot_cus(1, 4, 64, 256, 8 if cu else 1)
-        assert la == lb == name, (la, lb, name)
-        layouts[name] = (ma, mb)
+    layouts = {"striped": (slot_cus(0, 4, 64, 256, 8)[0], slot_cus(1, 4, 64, 256, 8)[0]),
+               "unmasked": (None, None)}
     res: dict = {"config": {"slots": 4, "cuPerSlot": 64, "victim": "slot 0", "aggressor": "slot 1",
                             "gemm": "torch bf16 4096^3", "l2": "2 MB re-read x256 per launch",
                             "aggressorBuffer": "2 GiB copy"},
-                 "masks": {k: {"victim": _ranges(v[0]), "aggressor": _ranges(v[1])}
+                 "masks": {k: {"victim": _ranges(v[0]) if v[0] else "all",
+                               "aggressor": _ranges(v[1]) if v[1] else "all"}
                            for k, v in layouts.items()},
                  "census": {}, "rounds": []}
     for name, (ma, mb) in layouts.items():

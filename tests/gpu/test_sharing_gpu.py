@@ -191,30 +191,32 @@ def test_hbm_budget_is_the_pods_across_its_processes(tmp_path):
                 p.wait(timeout=30)
 
 
-def test_xcd_aligned_slots_own_whole_xcds():
-    """The agent's XCD layout (gpupool/agent/slots.py) for 4 slots x 64 CUs: each slot's census
-    shows exactly two XCDs with all 32 of their CUs and six XCDs with none, and no two slots share
-    an XCD — so each slot has L2s of its own (the striped layout puts 8 CUs on every XCD)."""
+def test_smallest_slot_spans_every_xcd():
+    """The smallest slot the agent builds on an SPX MI355X is 8 CUs (cuPerSlot below the XCD count
+    is refused: a mask that leaves an XCD empty is not applied by the hardware at all, see
+    gpupool/agent/slots.py and profiles/r4b_cu_mask_layouts.json). Four 8-CU slots: each one's
+    census shows exactly one CU on every XCD, and the slots' CUs are disjoint."""
     from gpupool.agent.agent import _ranges
-    from gpupool.agent.slots import slot_cus
+    from gpupool.agent.slots import cu_floor, slot_cus
     assert os.path.exists(LIB), "build the native targets first"
-    owned = []
+    spx = {"asic": {"computeUnits": 256}, "partition": {"compute": "SPX"}}
+    assert cu_floor({"replicasPerGPU": 4, "cuPerSlot": 4}, spx)
+    assert not cu_floor({"replicasPerGPU": 4, "cuPerSlot": 8}, spx)
+    seen = []
     for i in range(4):
-        bits, layout = slot_cus(i, 4, 64, 256, 8)
-        assert layout == "xcd" and len(bits) == 64
+        bits, layout = slot_cus(i, 32, 8, 256, 8)
         r = subprocess.run([sys.executable, "-c", CENSUS, ROOT],
                            env=_env(HSA_TOOLS_LIB=LIB, GPUPOOL_CU_MASK=_ranges(bits)),
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr[-2000:]
         out = json.loads(r.stdout.splitlines()[-1])
-        per = out["perXcd"]
-        print(f"xcd slot {i}: mask {_ranges(bits)[:40]}... per XCD {per}")
+        print(f"8-CU slot {i}: mask {_ranges(bits)} per XCD {out['perXcd']}")
         assert out["mfmaOk"], out
-        assert sorted(per) == [0] * 6 + [32, 32], (i, per)
-        owned.append({x for x in range(8) if per[x]})
+        assert out["perXcd"] == [1] * 8, (i, out["perXcd"])
+        seen.append(set(out["keys"]))
     for i in range(4):
         for j in range(i + 1, 4):
-            assert not (owned[i] & owned[j]), (i, j, owned)
+            assert not (seen[i] & seen[j]), (i, j)
 
 
 ACCT_ALLOC = r"""

@@ -46,6 +46,17 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
             assert len(v["xgmi_pairs_covered_last"]) == int(k)
         else:
             assert "xgmi_links_measured" not in v
+        # what the agent costs at this N: its RSS, the HIP contexts it holds (0: simulated probe
+        # on the fake backend), VRAM in use on each GPU the N-GPU claim got
+        ag = v["agent"]
+        assert ag["rss_mib"] > 0 and ag["hip_devices"] == 0, (k, ag)
+        assert len(ag["vram_used_mib_per_gpu"]) == int(k), (k, ag)
+        assert all(x is not None and x > 0 for x in ag["vram_used_mib_per_gpu"]), (k, ag)
+    # the N=8 point carries the fabric evidence the first real 8-GPU run must produce: 8 links
+    # measured by the claim's xGMI ring, pair coverage over the node's 7 peers per GPU
+    n8 = cfg["per_n"]["8"]
+    assert n8["xgmi_links_measured"] == 8 and n8["xgmi_pairs_total"] == 7
+    assert len(n8["xgmi_pairs_covered_last"]) == 8 and all(1 <= p <= 7 for p in n8["xgmi_pairs_covered_last"])
     assert cfg["readyReplicas_accuracy"] == 1.0
     # agent + manager footprint around the timed region (Prometheus process_* metrics)
     for when in ("before_timed", "after_timed"):

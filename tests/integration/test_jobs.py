@@ -512,3 +512,47 @@ def test_restarted_gang_resumes_from_checkpoint(node8, tmp_path):
     resume = next(e for e in events if e["event"] == "resume")
     done = next(e for e in events if e["event"] == "done")
     assert resume["step"] == 10 and done["steps"] == 20 and done["world"] == 2
+
+
+def test_reference_job_manifests_apply_unchanged(node8, tmp_path):
+    """A user of the reference platform keeps their manifests: `gpuctl apply -f` of a Volcano Job
+    (GPU调度平台搭建.md:643-672 shape) and of a Kubeflow PyTorchJob converts each to a Mi355xJob
+    gang on pool GPUs, which runs to success (the PyTorchJob as real 2-rank DDP; here gloo on
+    CPU). Only the command is swapped for a CPU-runnable one."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 2), "default")
+    wait_ready(k, "pool", 2)
+    train = [sys.executable, os.path.join(ROOT, "examples", "fmnist_train.py"), "--synthetic",
+             "--cpu", "--samples", "256", "--batch_size", "32", "--steps", "3", "--epochs", "1",
+             "--output", str(tmp_path / "out")]
+    vc = yaml.safe_load(open(os.path.join(ROOT, "config", "samples", "foreign",
+                                          "volcano_fashion_mnist_job.yaml")))
+    ct = vc["spec"]["tasks"][0]["template"]["spec"]["containers"][0]
+    ct["command"], ct["args"] = train, []
+    pt = yaml.safe_load(open(os.path.join(ROOT, "config", "samples", "foreign",
+                                          "kubeflow_pytorchjob.yaml")))
+    _port[0] += 1
+    for spec in pt["spec"]["pytorchReplicaSpecs"].values():
+        spec["template"]["spec"]["containers"][0]["command"] = train
+    files = []
+    for name, doc in (("vc.yaml", vc), ("ptj.yaml", pt)):
+        p = tmp_path / name
+        p.write_text(yaml.safe_dump(doc))
+        files.append(str(p))
+    env = dict(os.environ, PYTHONPATH=ROOT, GPUPOOL_APISERVER=node8.url)
+    for f in files:
+        r = subprocess.run([sys.executable, "-m", "gpupool.cli", "apply", "-f", f], cwd=ROOT,
+                           env=env, capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        assert "to Mi355xJob" in r.stderr and "mi355xjob" in r.stdout, (r.stdout, r.stderr)
+    o = k.wait_for(MI355XJOBS, "fashion-mnist-job", "default", phase_is("Succeeded", "Failed"),
+                   timeout=120)
+    assert o["status"]["phase"] == "Succeeded", o["status"]
+    assert o["metadata"]["annotations"]["gpupool.amd.com/converted-from"] == \
+        "batch.volcano.sh/v1alpha1/Job"
+    o = k.wait_for(MI355XJOBS, "fmnist-ddp", "default", phase_is("Succeeded", "Failed"),
+                   timeout=180)
+    assert o["status"]["phase"] == "Succeeded" and o["status"]["succeeded"] == 2, o["status"]
+    pods = {p["metadata"]["labels"]["gpupool.amd.com/replica-index"]: p
+            for p in job_pods(k, "fmnist-ddp")}
+    assert env_of(pods["1"])["WORLD_SIZE"] == "2" and env_of(pods["0"])["RANK"] == "0"

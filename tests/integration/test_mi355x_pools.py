@@ -883,3 +883,26 @@ def test_kubelet_restart_readvertises_without_a_device_change(cluster_factory):
     c.start_kubelet(node)
     o = wait_ready(k, "kr", 2, timeout=30)
     assert all(d["advertised"] for d in o["status"]["devices"])
+
+
+def test_spanning_pool_with_a_lost_claim_reply_can_be_deleted(cluster_factory):
+    """A spanning pool (maxNodes > 1) whose claim reply is lost (the agent stalls past the
+    manager's RPC timeout, then commits the claim) must still be deletable: the node it suspected
+    answers every later pass (a spanning pool observes every node), so the suspicion is resolved
+    and the finalizer comes off once its GPUs are released — not 'claim outcome unknown' forever."""
+    stall = ["--inject-claim-delay", "2:1.5"]  # claims of >= 2 GPUs stall 1.5 s
+    c = cluster_factory(nodes=[NodeSpec("sp-a", extra_args=stall), NodeSpec("sp-b", extra_args=stall)],
+                        manager_args=["--agent-timeout", "600ms", "--orphan-sweep", "1s"])
+    k = c.client
+    uid = k.create(MI355XPOOLS, mi_pool("span", 10, maxNodes=2), "default")["metadata"]["uid"]
+    deadline = time.time() + 20
+    while not [d for n in ("sp-a", "sp-b") for d in agent_view(c, n)["devices"]
+               if d.get("poolUID") == uid]:
+        assert time.time() < deadline, "no stalled claim ever landed"
+        time.sleep(0.1)
+    k.delete(MI355XPOOLS, "span", "default")
+    k.wait_for(MI355XPOOLS, "span", "default", lambda o: o is None, timeout=30)
+    deadline = time.time() + 15  # a claim still stalled at deletion lands as an orphan: swept
+    while [d for n in ("sp-a", "sp-b") for d in agent_view(c, n)["devices"] if d.get("poolUID") == uid]:
+        assert time.time() < deadline, "GPUs of the deleted pool still held"
+        time.sleep(0.2)

@@ -139,3 +139,29 @@ def test_random_concurrent_creates_and_edits_never_exceed_hard(cluster_factory, 
         for o in k.list(MI355XPOOLS, ns)["items"]:
             k.wait_for(MI355XPOOLS, o["metadata"]["name"], ns, lambda x: x is None, timeout=30)
     assert peak <= 4, peak
+
+
+def test_quota_hold_of_a_force_removed_pool_is_released(cluster_factory):
+    """A pool that leaves without a finalizer pass — deleted while its agent is down, then its
+    finalizer force-removed (merge-patch metadata.finalizers: []) — must not keep consuming its
+    namespace's quota in the manager: a new pool under the same quota is admitted right away
+    (the old pool's GPUs are orphans the sweep releases; the node has spare ones meanwhile)."""
+    c = cluster_factory()
+    k = c.client
+    ns = "leak"
+    k.create(QUOTAS, {"metadata": {"name": "gpu-quota"},
+                      "spec": {"hard": {"requests.amd.com/gpu": "2"}}}, ns)
+    k.create(MI355XPOOLS, mi_pool("old", 2), ns)
+    k.wait_for(MI355XPOOLS, "old", ns, ready_at(2), timeout=30)
+    c._kill("agent-mi355x-node-0")
+    k.delete(MI355XPOOLS, "old", ns)
+    time.sleep(0.5)  # the finalizer stays: the agent holding its GPUs does not answer
+    assert k.get(MI355XPOOLS, "old", ns)["metadata"].get("finalizers")
+    k.patch(MI355XPOOLS, "old", {"metadata": {"finalizers": []}}, ns)
+    k.wait_for(MI355XPOOLS, "old", ns, lambda o: o is None, timeout=10)
+    c.start_agent(c.nodes[0])
+    t0 = time.monotonic()
+    k.create(MI355XPOOLS, mi_pool("new", 2), ns)
+    o = k.wait_for(MI355XPOOLS, "new", ns, _settled, timeout=30)
+    assert ready_at(2)(o), o["status"]["conditions"]
+    print(f"new pool Ready {time.monotonic() - t0:.3f} s after create")

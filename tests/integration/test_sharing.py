@@ -156,17 +156,11 @@ def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_
     for i in range(4):
         start(f"iso{i}")
     envs = [env_of(f"iso{i}") for i in range(4)]
-    # 64-CU slots on an 8-XCD GPU: whole XCDs per slot (mask bit b is a CU of XCD b mod 8), so
-    # slot i owns XCDs {2i, 2i+1} and their L2s
-    from gpupool.agent.slots import slot_xcds
-    masks = {}
-    for e in envs:
-        bits = [b for r in e["GPUPOOL_CU_MASK"].split(",") for b in
-                range(int(r.split("-")[0]), int(r.split("-")[-1]) + 1)]
-        assert len(bits) == 64 and e["GPUPOOL_CU_LAYOUT"] == "xcd", e
-        masks[tuple(slot_xcds(bits, 8))] = bits
-    assert sorted(masks) == [(0, 1), (2, 3), (4, 5), (6, 7)], sorted(masks)
-    assert sorted(b for m in masks.values() for b in m) == list(range(256))
+    # contiguous, disjoint 64-bit masks: 8 CUs on each of the 8 XCDs per slot (a mask leaving an
+    # XCD empty is not applied by the hardware at all: gpupool/agent/slots.py)
+    masks = sorted(e["GPUPOOL_CU_MASK"] for e in envs)
+    assert masks == ["0-63", "128-191", "192-255", "64-127"], masks
+    assert all(e["GPUPOOL_CU_LAYOUT"] == "striped" for e in envs)
     assert all(e["GPUPOOL_HBM_LIMIT_BYTES"] == str(8 << 30) for e in envs)
     lib = envs[0]["HSA_TOOLS_LIB"]  # the container path, rewritten to the host path
     assert lib.endswith("/libgpupool_share.so") and os.path.exists(lib)
@@ -176,8 +170,9 @@ def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_
     assert lib.startswith(c.state_dir("mi355x-node-0") + "/lib/"), lib
     # status shows the layout per slot
     gpu = k.get(MI355XPOOLS, "iso", "default")["status"]["devices"][0]
-    assert gpu["sharing"]["cuLayout"] == "xcd" and gpu["sharing"]["slotXcds"] == \
-        ["0-1", "2-3", "4-5", "6-7"], gpu.get("sharing")
+    sh = gpu["sharing"]
+    assert sh["cuLayout"] == "striped" and sh["slotXcds"] == ["0-7"] * 4, sh
+    assert sh["slotCUMasks"] == ["0-63", "64-127", "128-191", "192-255"], sh
     # one HBM account per container (shared by all its processes): the library's layout — magic,
     # the per-GPU limit, version 2 with the GPU's HIP UUID, zeroed counters, and the container's
     # slot ids for the agent's cleanup
@@ -207,6 +202,15 @@ def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_
         timeout=20)
     assert "256 CUs" in next(x["message"] for x in o["status"]["conditions"]
                              if x["type"] == "Ready")
+    # fewer CUs per slot than the GPU has XCDs would leave XCDs empty: the hardware would ignore
+    # the mask, so such a pool is refused — on SPX (or Any) below 8, on CPX (1 XCD) any size goes
+    k.create(MI355XPOOLS, mi_pool("thin", 1, sharing={"replicasPerGPU": 4, "cuPerSlot": 4}),
+             "default")
+    o = k.wait_for(MI355XPOOLS, "thin", "default", lambda o: any(
+        x["reason"] == "InvalidSpec" for x in (o.get("status") or {}).get("conditions", [])),
+        timeout=20)
+    assert "at least 8" in next(x["message"] for x in o["status"]["conditions"]
+                                if x["type"] == "Ready")
 
 
 def test_per_pod_accounting_on_a_time_shared_gpu(cluster_factory):

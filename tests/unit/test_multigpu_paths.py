@@ -213,3 +213,41 @@ def test_select_eight_and_xgmi_packed_subsets(native_built):
     assert sel != [2, 3], sel
     # growing an owned set prefers its NUMA node
     assert devlib.select(2, [3, 4, 5, 6], [0, 1, 2], "xgmi-packed", amdsmi_weights(), numa)[0] == 3
+
+
+def _rccl_check_world2(extra_rank1: list[str]) -> list[tuple[int, dict]]:
+    """Two gloo ranks of gpupool.parallel.rccl_check on the CPU (the N>1 bench's comm check)."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [subprocess.Popen([sys.executable, "-m", "gpupool.parallel.rccl_check", "--rank", str(r),
+                               "--world", "2", "--master-port", str(port), "--backend", "gloo",
+                               "--device", "cpu", "--bytes", str(1 << 20), "--iters", "2",
+                               "--warmup", "1"] + (extra_rank1 if r == 1 else []),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=ROOT)
+             for r in range(2)]
+    out = []
+    for p in procs:
+        so, se = p.communicate(timeout=120)
+        lines = [x for x in so.splitlines() if x.startswith("{")]
+        out.append((p.returncode, json.loads(lines[-1]) if lines else {"stderr": se[-1500:]}))
+    return out
+
+
+def test_rccl_check_proves_data_moved_between_ranks():
+    """Rank r contributes r + 1: only a real reduction over both ranks yields 3 everywhere."""
+    res = _rccl_check_world2([])
+    for rc, o in res:
+        assert rc == 0 and o["exact"] and o["expected"] == 3 and o["got"] == [3.0, 3.0], o
+
+
+def test_rccl_check_fails_a_rank_that_skipped_the_reduction():
+    """A rank that joins the collective but drops its result keeps its own contribution (2): the
+    harness fails it (exit 2) — a local copy cannot pass as a collective."""
+    res = _rccl_check_world2(["--inject", "skip-reduce"])
+    rc1, o1 = res[1]
+    assert rc1 == 2 and o1["exact"] is False and o1["got"] == [2.0, 2.0], o1
