@@ -119,7 +119,9 @@ class MiniKubelet:
         return DP.Empty()
 
     def stop(self):
-        self.server.stop(0)
+        # wait for the teardown: gRPC removes its unix socket file when the listener is destroyed,
+        # which, done asynchronously, deleted a restarted kubelet's new socket (a test-only race)
+        self.server.stop(0).wait(5)
         try:
             os.unlink(os.path.join(self.dir, "kubelet.sock"))
         except FileNotFoundError:
