@@ -1676,7 +1676,10 @@ class Agent:
                     continue
                 path = os.path.join(d, name)
                 if mine & set(slotlib.account_slots(path) or ()):
-                    os.unlink(path)
+                    try:
+                        os.unlink(path)
+                    except FileNotFoundError:  # the sampler's GC got there first
+                        pass
             with self.lock:
                 uuids = [(self.by_uuid.get(u) or {}).get("hipUUID") or "" for u in gpus]
             path = os.path.join(d, f"{uuid4().hex}.acct")

@@ -71,6 +71,7 @@ def test_manager_rbac_covers_native_api_calls():
 
 def test_agent_rbac_covers_agent_api_calls():
     src = open(os.path.join(ROOT, "gpupool", "agent", "agent.py")).read()
+    src += open(os.path.join(ROOT, "gpupool", "agent", "rpc.py")).read()  # agent RPC counters
     used = set()
     for m in re.finditer(r"c\.(get|create|patch|update|delete|list)\((\w+)[^)]*?(sub=\"status\")?\)", src):
         res = {"NODES": "nodes", "PODS": "pods"}.get(m.group(2), m.group(2).lower())
@@ -156,6 +157,7 @@ def test_alert_rules_use_exported_metrics():
     import yaml
     doc = yaml.safe_load(open(os.path.join(ROOT, "config", "prometheus", "alerts.yaml")))
     src = open(os.path.join(ROOT, "gpupool", "agent", "agent.py")).read()
+    src += open(os.path.join(ROOT, "gpupool", "agent", "rpc.py")).read()  # agent RPC counters
     for dirpath, _, files in os.walk(os.path.join(ROOT, "native", "src")):
         for f in files:
             if f.endswith(".cc"):
