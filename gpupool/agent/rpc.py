@@ -102,6 +102,21 @@ class _Reader:
             start = len(self.buf)
             self._fill()
 
+    def read_head(self, limit: int) -> bytes | None:
+        """Everything up to and including the blank line that ends a request head; None past
+        ``limit`` bytes without one. One scan per received chunk, not one per header line."""
+        start = 0
+        while True:
+            i = self.buf.find(b"\r\n\r\n", start)
+            if i >= 0:
+                head = bytes(self.buf[:i + 4])
+                del self.buf[:i + 4]
+                return head
+            if len(self.buf) > limit:
+                return None
+            start = max(0, len(self.buf) - 3)
+            self._fill()
+
     def read(self, n: int) -> bytes:
         while len(self.buf) < n:
             self._fill()
@@ -270,27 +285,32 @@ class RpcServer:
             rf.deadline = deadline
             while not self._stop.is_set():
                 try:
-                    line = rf.readline(MAX_LINE)
+                    head = rf.read_head(MAX_LINE + MAX_HEADER_BYTES)
                 except _Closed:
                     return
-                if line in (b"\r\n", b"\n"):
+                if head is None:
+                    self._reject(conn, 431, "HeadersTooLarge",
+                                 f"request head over {MAX_LINE + MAX_HEADER_BYTES} bytes")
+                    return
+                lines = head.split(b"\r\n")
+                while lines and not lines[0]:  # blank lines before a request line are allowed
+                    lines.pop(0)
+                if not lines:
                     continue
+                if len(lines[0]) > MAX_LINE:
+                    return
                 try:
-                    method, target, version = line.decode("latin-1").split(None, 2)
+                    method, target, version = lines[0].decode("latin-1").split(None, 2)
                 except ValueError:
                     return
                 method = method.upper()
+                fields = [h for h in lines[1:] if h]
+                if len(fields) > MAX_HEADERS or len(head) - len(lines[0]) > MAX_HEADER_BYTES:
+                    self._reject(conn, 431, "HeadersTooLarge",
+                                 f"at most {MAX_HEADERS} header lines / {MAX_HEADER_BYTES} bytes")
+                    return
                 headers: dict[str, str] = {}
-                nbytes = 0
-                while True:
-                    h = rf.readline(MAX_LINE)
-                    if h in (b"\r\n", b"\n"):
-                        break
-                    nbytes += len(h)
-                    if len(headers) >= MAX_HEADERS or nbytes > MAX_HEADER_BYTES:
-                        self._reject(conn, 431, "HeadersTooLarge",
-                                     f"at most {MAX_HEADERS} header lines / {MAX_HEADER_BYTES} bytes")
-                        return
+                for h in fields:
                     k, _, v = h.decode("latin-1").partition(":")
                     headers[k.strip().lower()] = v.strip()
                 path = target.partition("?")[0]
@@ -374,11 +394,7 @@ class RpcServer:
 
     def _dispatch(self, method: str, target: str, headers: dict, body: bytes) -> tuple:
         path, _, qs = target.partition("?")
-        self.requests += 1
-        if self._auth and path not in OPEN_PATHS and \
-                not hmac.compare_digest(headers.get("authorization", "").encode(), self._auth):
-            return json_reply({"reason": "Unauthorized",
-                               "message": "agent RPC requires the manager's token"}, 401)
+        self.requests += 1  # the token was checked in _serve_conn, before the body was read
         h = self.routes.get((method, path))
         if h is None:
             known = any(p == path for _, p in self.routes)
