@@ -25,28 +25,29 @@
 // per process. Each process also records what it holds in its own entry (pid + start time), and
 // a process that finds the budget exhausted first returns the bytes of entries whose process is
 // gone (killed by OOM, SIGKILL — no free ever ran). Without the file the budget is per process.
-// The agent gives sibling slots disjoint CU ranges and budgets that sum to at most the GPU's HBM.
+// The agent gives sibling slots disjoint CU ranges and refuses pools whose budgets overcommit the
+// GPU (gpupool/agent/slots.py).
+//
+// The library is loaded into arbitrary pod images, and ROCr skips a tools library that fails to
+// load — silently dropping the slot's limits. So it depends on nothing but libc (GLIBC_2.14 at
+// most): no C++ standard library (fixed tables and an open-addressing hash of live allocations,
+// pthread mutexes, __atomic builtins), no exceptions, RTTI or guarded statics, and the global
+// state is constant-initialised (nothing runs at load or exit). Checked by
+// tests/unit/test_native.py::test_share_library_needs_only_old_glibc.
 #define AMD_INTERNAL_BUILD  // hsa_api_trace.h: include the sibling headers of /opt/rocm/include/hsa
+#include <errno.h>
 #include <fcntl.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_api_trace.h>
 #include <hsa/hsa_ext_amd.h>
+#include <pthread.h>
 #include <signal.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #include <sys/mman.h>
 #include <unistd.h>
-
-#include <algorithm>
-#include <atomic>
-#include <cerrno>
-#include <cstdint>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <map>
-#include <mutex>
-#include <string>
-#include <unordered_map>
-#include <vector>
 
 namespace {
 
@@ -79,49 +80,143 @@ struct Account {
 };
 static_assert(sizeof(Account) == 8192, "account layout");
 
-struct State {
-  std::mutex mu;
-  CoreApiTable real_core{};
-  AmdExtTable real_amd{};
-  uint64_t limit = 0;                       // bytes per GPU; 0 = no budget
-  std::vector<uint32_t> mask;               // CU mask words; empty = no mask
-  uint32_t mask_bits = 0;
-  bool debug = false;
-  bool pools_mapped = false;
-  std::map<uint64_t, uint64_t> pool_agent;  // GPU-located pool handle -> agent handle
-  std::map<uint64_t, uint64_t> used;        // agent handle -> live bytes (this process)
-  std::map<uint64_t, uint32_t> ordinal;     // agent handle -> ROCr's enumeration order
-  std::map<uint64_t, int> acct_gpu;         // agent handle -> account GPU index (-1: not in the account)
-  std::unordered_map<void*, std::pair<uint64_t, uint64_t>> ptrs;       // ptr -> (agent, bytes)
-  std::unordered_map<uint64_t, std::pair<uint64_t, uint64_t>> vmem;    // handle -> (agent, bytes)
-  std::atomic<uint64_t> denied{0}, queues_masked{0}, peak{0}, reclaimed{0};
-  Account* acct = nullptr;                  // shared account; null = per-process budget
-  int32_t me = 0;                           // pid the entries below belong to (fork changes it)
-  uint64_t me_start = 0;
-  AcctEntry* mine[kAcctGpus] = {};
+constexpr int kMaxAgents = 64;     // GPU agents one process sees (8 GPUs, or 64 CPX partitions)
+constexpr int kMaxPools = 512;     // GPU-located memory pools over all of them
+constexpr int kMaskWords = 128;    // CU-mask bits up to 4096
+
+struct AgentRec {
+  uint64_t handle;
+  uint64_t used;      // live bytes this process holds on it
+  uint32_t ordinal;   // ROCr's enumeration order
+  int acct_gpu;       // account GPU index, -1 when the shared account does not cover it
+};
+struct PoolRec {
+  uint64_t pool, agent;
 };
 
-State& st() {
-  static State* s = new State();  // never destroyed: HSA may call in during process exit
-  return *s;
+// Live allocations (pointer or VMM handle -> agent, bytes): open addressing, linear probing,
+// grown with calloc at 50 % occupancy (tombstones included). Key 0 = empty, ~0 = deleted.
+struct Alloc {
+  uint64_t key, agent, bytes;
+};
+struct AllocMap {
+  Alloc* slots;
+  size_t cap, live, used;  // capacity (power of two), live keys, live + tombstones
+};
+constexpr uint64_t kDeleted = ~0ull;
+
+// Keys are stored +1 so that a (theoretical) VMM handle 0 is not the empty marker.
+uint64_t enc(uint64_t key) { return key + 1; }
+
+size_t slot_of(uint64_t key, size_t cap) { return static_cast<size_t>((key * 0x9E3779B97F4A7C15ull) >> 17) & (cap - 1); }
+
+bool map_grow(AllocMap& m) {
+  size_t cap = m.cap ? m.cap * 2 : 1024;
+  while (m.live * 2 >= cap) cap *= 2;
+  Alloc* fresh = static_cast<Alloc*>(calloc(cap, sizeof(Alloc)));
+  if (!fresh) return false;
+  for (size_t i = 0; i < m.cap; ++i) {
+    const Alloc& a = m.slots[i];
+    if (a.key == 0 || a.key == kDeleted) continue;
+    size_t j = slot_of(a.key, cap);
+    while (fresh[j].key) j = (j + 1) & (cap - 1);
+    fresh[j] = a;
+  }
+  free(m.slots);
+  m.slots = fresh;
+  m.cap = cap;
+  m.used = m.live;
+  return true;
 }
+
+bool map_put(AllocMap& m, uint64_t raw, uint64_t agent, uint64_t bytes) {
+  const uint64_t key = enc(raw);
+  if (key == 0 || key == kDeleted) return false;
+  if ((m.used + 1) * 2 > m.cap && !map_grow(m)) return false;
+  size_t i = slot_of(key, m.cap), tomb = SIZE_MAX;
+  for (;; i = (i + 1) & (m.cap - 1)) {
+    if (m.slots[i].key == key) {
+      m.slots[i].agent = agent;
+      m.slots[i].bytes = bytes;
+      return true;
+    }
+    if (m.slots[i].key == kDeleted && tomb == SIZE_MAX) tomb = i;
+    if (m.slots[i].key == 0) break;
+  }
+  if (tomb != SIZE_MAX) i = tomb;
+  else ++m.used;
+  m.slots[i] = Alloc{key, agent, bytes};
+  ++m.live;
+  return true;
+}
+
+// Removes ``key``; true (and its record in *out) if it was there.
+bool map_take(AllocMap& m, uint64_t raw, Alloc* out) {
+  const uint64_t key = enc(raw);
+  if (!m.cap || key == 0 || key == kDeleted) return false;
+  for (size_t i = slot_of(key, m.cap);; i = (i + 1) & (m.cap - 1)) {
+    if (m.slots[i].key == 0) return false;
+    if (m.slots[i].key == key) {
+      *out = m.slots[i];
+      m.slots[i].key = kDeleted;
+      --m.live;
+      return true;
+    }
+  }
+}
+
+struct State {
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  CoreApiTable real_core;
+  AmdExtTable real_amd;
+  uint64_t limit;                   // bytes per GPU; 0 = no budget
+  uint32_t mask[kMaskWords];        // CU mask words
+  uint32_t mask_words;              // 0 = no mask
+  uint32_t mask_bits;
+  bool debug;
+  bool pools_mapped;
+  AgentRec agents[kMaxAgents];
+  int n_agents;
+  PoolRec pools[kMaxPools];
+  int n_pools;
+  AllocMap ptrs, vmem;
+  uint64_t denied, queues_masked, peak, reclaimed;  // __atomic counters
+  Account* acct;                    // shared account; null = per-process budget
+  int32_t me;                       // pid the entries below belong to (fork changes it)
+  uint64_t me_start;
+  AcctEntry* mine[kAcctGpus];
+};
+
+State g_state;  // constant-initialised: no constructor at load, no destructor at exit
+State& st() { return g_state; }
+
+struct Lock {  // the state's mutex for one scope
+  explicit Lock(State& s) : m(&s.mu) { pthread_mutex_lock(m); }
+  ~Lock() { pthread_mutex_unlock(m); }
+  Lock(const Lock&) = delete;
+  Lock& operator=(const Lock&) = delete;
+  pthread_mutex_t* m;
+};
+
+void count(uint64_t* c, uint64_t n = 1) { __atomic_add_fetch(c, n, __ATOMIC_RELAXED); }
+uint64_t load(const uint64_t* c) { return __atomic_load_n(c, __ATOMIC_RELAXED); }
 
 // /proc/<pid>/stat field 22 (start time in clock ticks); 0 when unreadable.
 uint64_t proc_start(int32_t pid) {
   char path[64];
-  std::snprintf(path, sizeof path, "/proc/%d/stat", pid);
-  FILE* f = std::fopen(path, "r");
+  snprintf(path, sizeof path, "/proc/%d/stat", pid);
+  FILE* f = fopen(path, "r");
   if (!f) return 0;
   char buf[1024];
-  size_t n = std::fread(buf, 1, sizeof buf - 1, f);
-  std::fclose(f);
+  size_t n = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
   buf[n] = 0;
-  const char* p = std::strrchr(buf, ')');  // comm may hold spaces: fields restart after ')'
+  const char* p = strrchr(buf, ')');  // comm may hold spaces: fields restart after ')'
   if (!p) return 0;
   int field = 2;
   for (++p; *p && field < 22; ++p)
     if (*p == ' ') ++field;
-  return std::strtoull(p, nullptr, 10);
+  return strtoull(p, nullptr, 10);
 }
 
 bool proc_alive(int32_t pid, uint64_t start) {
@@ -151,13 +246,13 @@ uint64_t acct_reclaim(Account* a) {
   return total;
 }
 
-// This process's entry for GPU ordinal g (claimed on first use). Caller holds s.mu.
+// This process's entry for account GPU g (claimed on first use). Caller holds s.mu.
 AcctEntry* acct_entry(State& s, uint32_t g) {
   int32_t pid = static_cast<int32_t>(getpid());
   if (pid != s.me) {  // first call, or a forked child: it holds nothing of the parent's entries
     s.me = pid;
     s.me_start = proc_start(pid);
-    std::fill(std::begin(s.mine), std::end(s.mine), nullptr);
+    for (AcctEntry*& e : s.mine) e = nullptr;
   }
   if (s.mine[g]) return s.mine[g];
   for (int pass = 0; pass < 2; ++pass) {
@@ -171,12 +266,12 @@ AcctEntry* acct_entry(State& s, uint32_t g) {
       __atomic_store_n(&e.pid, pid, __ATOMIC_RELEASE);
       return s.mine[g] = &e;
     }
-    s.reclaimed.fetch_add(acct_reclaim(s.acct));  // table full: free the dead processes' entries
+    count(&s.reclaimed, acct_reclaim(s.acct));  // table full: free the dead processes' entries
   }
   return nullptr;  // still full: charge the GPU total only
 }
 
-// Reserve ``size`` on GPU ordinal g in the shared account. Caller holds s.mu.
+// Reserve ``size`` on account GPU g. Caller holds s.mu.
 bool acct_charge(State& s, uint32_t g, uint64_t size) {
   uint64_t* used = &s.acct->used[g];
   bool swept = false;
@@ -185,7 +280,7 @@ bool acct_charge(State& s, uint32_t g, uint64_t size) {
     if (cur + size > s.limit) {
       if (swept) return false;
       swept = true;  // over budget: first give back what dead processes of the pod still hold
-      s.reclaimed.fetch_add(acct_reclaim(s.acct));
+      count(&s.reclaimed, acct_reclaim(s.acct));
       cur = __atomic_load_n(used, __ATOMIC_ACQUIRE);
       continue;
     }
@@ -206,14 +301,14 @@ Account* acct_open(const char* path, bool debug) {
   if (!path || !*path) return nullptr;
   int fd = open(path, O_RDWR | O_CLOEXEC);
   if (fd < 0) {
-    if (debug) std::fprintf(stderr, "[gpupool-share] account %s: %s\n", path, std::strerror(errno));
+    if (debug) fprintf(stderr, "[gpupool-share] account %s: %s\n", path, strerror(errno));
     return nullptr;
   }
   void* m = mmap(nullptr, kAcctBytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   if (m == MAP_FAILED) return nullptr;
   auto* a = static_cast<Account*>(m);
-  if (std::memcmp(a->magic, kAcctMagic, sizeof kAcctMagic) != 0) {
+  if (memcmp(a->magic, kAcctMagic, sizeof kAcctMagic) != 0) {
     munmap(m, kAcctBytes);
     return nullptr;
   }
@@ -223,41 +318,51 @@ Account* acct_open(const char* path, bool debug) {
 uint64_t parse_bytes(const char* v) {
   if (!v || !*v) return 0;
   char* end = nullptr;
-  double x = std::strtod(v, &end);
-  std::string suf = end ? end : "";
+  double x = strtod(v, &end);
+  const char* suf = end ? end : "";
   double mul = 1;
-  if (suf == "Ki" || suf == "K" || suf == "k") mul = 1024.0;
-  else if (suf == "Mi" || suf == "M") mul = 1024.0 * 1024;
-  else if (suf == "Gi" || suf == "G") mul = 1024.0 * 1024 * 1024;
-  else if (suf == "Ti" || suf == "T") mul = 1024.0 * 1024 * 1024 * 1024;
+  if (!strcmp(suf, "Ki") || !strcmp(suf, "K") || !strcmp(suf, "k")) mul = 1024.0;
+  else if (!strcmp(suf, "Mi") || !strcmp(suf, "M")) mul = 1024.0 * 1024;
+  else if (!strcmp(suf, "Gi") || !strcmp(suf, "G")) mul = 1024.0 * 1024 * 1024;
+  else if (!strcmp(suf, "Ti") || !strcmp(suf, "T")) mul = 1024.0 * 1024 * 1024 * 1024;
   return static_cast<uint64_t>(x * mul);
 }
 
-// "0-63,128-159" -> bit words (32 bits each); bits counted up to the highest set bit, rounded up to
-// a multiple of 32 as hsa_amd_queue_cu_set_mask requires.
-std::vector<uint32_t> parse_mask(const char* v, uint32_t* bits) {
-  std::vector<uint32_t> words;
-  *bits = 0;
-  if (!v || !*v) return words;
-  std::string s(v);
-  size_t pos = 0;
-  while (pos < s.size()) {
-    size_t comma = s.find(',', pos);
-    std::string part = s.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
-    pos = comma == std::string::npos ? s.size() : comma + 1;
-    if (part.empty()) continue;
-    size_t dash = part.find('-');
-    long lo = std::strtol(part.c_str(), nullptr, 10);
-    long hi = dash == std::string::npos ? lo : std::strtol(part.c_str() + dash + 1, nullptr, 10);
-    if (lo < 0 || hi < lo || hi > 4095) continue;
+// "0-63,128-159" -> bit words (32 bits each) in s.mask; bits counted up to the highest set bit,
+// rounded up to a multiple of 32 as hsa_amd_queue_cu_set_mask requires.
+void parse_mask(State& s, const char* v) {
+  s.mask_words = 0;
+  s.mask_bits = 0;
+  if (!v || !*v) return;
+  const char* p = v;
+  while (*p) {
+    char* end = nullptr;
+    long lo = strtol(p, &end, 10);
+    bool ok = end != p;
+    long hi = lo;
+    p = end;
+    if (ok && *p == '-') {
+      const char* q = p + 1;
+      hi = strtol(q, &end, 10);
+      ok = end != q;
+      p = end;
+    }
+    while (*p && *p != ',') ++p;  // skip to the next range (malformed tails are ignored)
+    if (*p == ',') ++p;
+    if (!ok || lo < 0 || hi < lo || hi >= kMaskWords * 32) continue;
     for (long b = lo; b <= hi; ++b) {
-      size_t w = static_cast<size_t>(b) / 32;
-      if (words.size() <= w) words.resize(w + 1, 0);
-      words[w] |= 1u << (b % 32);
+      const uint32_t w = static_cast<uint32_t>(b) / 32;
+      s.mask[w] |= 1u << (b % 32);
+      if (w + 1 > s.mask_words) s.mask_words = w + 1;
     }
   }
-  *bits = static_cast<uint32_t>(words.size() * 32);
-  return words;
+  s.mask_bits = s.mask_words * 32;
+}
+
+AgentRec* agent_rec(State& s, uint64_t handle) {
+  for (int i = 0; i < s.n_agents; ++i)
+    if (s.agents[i].handle == handle) return &s.agents[i];
+  return nullptr;
 }
 
 // The account GPU of a GPU agent. Version 2 accounts name their GPUs, so every process of the pod
@@ -272,13 +377,12 @@ int acct_index(State& s, hsa_agent_t agent, uint32_t ordinal) {
     return -1;
   uuid[sizeof uuid - 1] = 0;
   const char* table = reinterpret_cast<const char*>(s.acct) + kAcctUuidsAt;
-  const uint32_t n = std::min<uint32_t>(s.acct->ngpus, kAcctGpus);
+  const uint32_t n = s.acct->ngpus < static_cast<uint32_t>(kAcctGpus) ? s.acct->ngpus : kAcctGpus;
   for (uint32_t g = 0; g < n; ++g) {
     const char* id = table + g * kAcctUuidBytes;
-    if (id[0] && std::strncmp(id, uuid, kAcctUuidBytes) == 0 && std::strlen(uuid) < kAcctUuidBytes)
-      return static_cast<int>(g);
+    if (id[0] && strlen(uuid) < kAcctUuidBytes && strncmp(id, uuid, kAcctUuidBytes) == 0) return static_cast<int>(g);
   }
-  if (s.debug) std::fprintf(stderr, "[gpupool-share] GPU %s is not in the pod's account\n", uuid);
+  if (s.debug) fprintf(stderr, "[gpupool-share] GPU %s is not in the pod's account\n", uuid);
   return -1;
 }
 
@@ -287,8 +391,8 @@ hsa_status_t collect_pool(hsa_amd_memory_pool_t pool, void* agent_handle) {
   hsa_amd_memory_pool_location_t loc{};
   if (s.real_amd.hsa_amd_memory_pool_get_info_fn &&
       s.real_amd.hsa_amd_memory_pool_get_info_fn(pool, HSA_AMD_MEMORY_POOL_INFO_LOCATION, &loc) == HSA_STATUS_SUCCESS &&
-      loc == HSA_AMD_MEMORY_POOL_LOCATION_GPU)
-    s.pool_agent[pool.handle] = *static_cast<uint64_t*>(agent_handle);
+      loc == HSA_AMD_MEMORY_POOL_LOCATION_GPU && s.n_pools < kMaxPools)
+    s.pools[s.n_pools++] = PoolRec{pool.handle, *static_cast<uint64_t*>(agent_handle)};
   return HSA_STATUS_SUCCESS;
 }
 
@@ -296,98 +400,98 @@ hsa_status_t collect_agent(hsa_agent_t agent, void*) {
   State& s = st();
   hsa_device_type_t type{};
   if (s.real_core.hsa_agent_get_info_fn(agent, HSA_AGENT_INFO_DEVICE, &type) != HSA_STATUS_SUCCESS ||
-      type != HSA_DEVICE_TYPE_GPU)
+      type != HSA_DEVICE_TYPE_GPU || s.n_agents >= kMaxAgents)
     return HSA_STATUS_SUCCESS;
+  AgentRec& r = s.agents[s.n_agents];
+  r.handle = agent.handle;
+  r.used = 0;
+  r.ordinal = static_cast<uint32_t>(s.n_agents);  // ROCr's enumeration order
+  r.acct_gpu = s.acct ? acct_index(s, agent, r.ordinal) : -1;
+  ++s.n_agents;
   uint64_t h = agent.handle;
-  s.used.emplace(h, 0);
-  const uint32_t ord = static_cast<uint32_t>(s.ordinal.size());  // ROCr's enumeration order
-  s.ordinal.emplace(h, ord);
-  if (s.acct) s.acct_gpu.emplace(h, acct_index(s, agent, ord));
   if (s.real_amd.hsa_amd_agent_iterate_memory_pools_fn)
     s.real_amd.hsa_amd_agent_iterate_memory_pools_fn(agent, collect_pool, &h);
   return HSA_STATUS_SUCCESS;
 }
 
-// pool -> its GPU agent (0 if the pool is not GPU memory). Caller holds s.mu.
-uint64_t agent_of(hsa_amd_memory_pool_t pool) {
+void map_agents(State& s) {  // caller holds s.mu
+  if (s.pools_mapped) return;
+  s.pools_mapped = true;
+  if (s.real_core.hsa_iterate_agents_fn) s.real_core.hsa_iterate_agents_fn(collect_agent, nullptr);
+}
+
+// pool -> its GPU agent's record (null if the pool is not GPU memory). Caller holds s.mu.
+AgentRec* agent_of(hsa_amd_memory_pool_t pool) {
   State& s = st();
-  if (!s.pools_mapped) {
-    s.pools_mapped = true;
-    if (s.real_core.hsa_iterate_agents_fn) s.real_core.hsa_iterate_agents_fn(collect_agent, nullptr);
-  }
-  auto it = s.pool_agent.find(pool.handle);
-  return it == s.pool_agent.end() ? 0 : it->second;
+  map_agents(s);
+  for (int i = 0; i < s.n_pools; ++i)
+    if (s.pools[i].pool == pool.handle) return agent_rec(s, s.pools[i].agent);
+  return nullptr;
 }
 
-// Reserve ``size`` bytes on the pool's GPU; false when over budget. Caller holds s.mu.
-// The account slot of ``agent``: its ordinal when the shared account covers it, else -1.
-int shared_index(State& s, uint64_t agent) {
-  if (!s.acct) return -1;
-  auto it = s.acct_gpu.find(agent);
-  return it != s.acct_gpu.end() ? it->second : -1;
-}
+// The account slot of an agent: its account GPU when the shared account covers it, else -1.
+int shared_index(const State& s, const AgentRec* a) { return s.acct && a ? a->acct_gpu : -1; }
 
-// Live bytes against the budget on ``agent``: the pod's total when shared. Caller holds s.mu.
-uint64_t budget_used(State& s, uint64_t agent) {
-  int g = shared_index(s, agent);
+// Live bytes against the budget on ``a``: the pod's total when shared. Caller holds s.mu.
+uint64_t budget_used(State& s, const AgentRec* a) {
+  int g = shared_index(s, a);
   if (g >= 0) return __atomic_load_n(&s.acct->used[g], __ATOMIC_ACQUIRE);
-  auto it = s.used.find(agent);
-  return it == s.used.end() ? 0 : it->second;
+  return a ? a->used : 0;
 }
 
-bool charge(uint64_t agent, size_t size) {
+// Reserve ``size`` bytes on ``a``; false when over budget. Caller holds s.mu.
+bool charge(AgentRec* a, uint64_t size) {
   State& s = st();
-  uint64_t& u = s.used[agent];
-  int g = shared_index(s, agent);
-  bool ok = g >= 0 ? acct_charge(s, static_cast<uint32_t>(g), size) : !(s.limit && u + size > s.limit);
+  int g = shared_index(s, a);
+  bool ok = g >= 0 ? acct_charge(s, static_cast<uint32_t>(g), size) : !(s.limit && a->used + size > s.limit);
   if (!ok) {
-    s.denied.fetch_add(1);
+    count(&s.denied);
     if (s.debug)
-      std::fprintf(stderr, "[gpupool-share] deny %zu B: %llu in use of %llu%s\n", size,
-                   static_cast<unsigned long long>(budget_used(s, agent)),
-                   static_cast<unsigned long long>(s.limit), g >= 0 ? " (pod total)" : "");
+      fprintf(stderr, "[gpupool-share] deny %llu B: %llu in use of %llu%s\n", static_cast<unsigned long long>(size),
+              static_cast<unsigned long long>(budget_used(s, a)), static_cast<unsigned long long>(s.limit),
+              g >= 0 ? " (pod total)" : "");
     return false;
   }
-  u += size;
-  uint64_t pk = s.peak.load();
-  while (u > pk && !s.peak.compare_exchange_weak(pk, u)) {}
+  a->used += size;
+  uint64_t pk = __atomic_load_n(&s.peak, __ATOMIC_RELAXED);
+  while (a->used > pk && !__atomic_compare_exchange_n(&s.peak, &pk, a->used, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
   return true;
 }
 
-// Return ``size`` bytes on ``agent``. Caller holds s.mu.
-void uncharge(uint64_t agent, uint64_t size) {
+// Return ``size`` bytes on ``a``. Caller holds s.mu.
+void uncharge(AgentRec* a, uint64_t size) {
   State& s = st();
-  uint64_t& u = s.used[agent];
-  u = u > size ? u - size : 0;
-  int g = shared_index(s, agent);
+  if (!a) return;
+  a->used = a->used > size ? a->used - size : 0;
+  int g = shared_index(s, a);
   if (g >= 0) acct_release(s, static_cast<uint32_t>(g), size);
 }
 
 hsa_status_t w_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr) {
   State& s = st();
-  uint64_t agent = 0;
+  AgentRec* a = nullptr;
   {
-    std::lock_guard<std::mutex> g(s.mu);
-    agent = agent_of(pool);
-    if (agent && !charge(agent, size)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+    Lock g(s);
+    a = agent_of(pool);
+    if (a && !charge(a, size)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   }
   hsa_status_t r = s.real_amd.hsa_amd_memory_pool_allocate_fn(pool, size, flags, ptr);
-  std::lock_guard<std::mutex> g(s.mu);
-  if (!agent) return r;
-  if (r == HSA_STATUS_SUCCESS && ptr && *ptr) s.ptrs[*ptr] = {agent, size};
-  else uncharge(agent, size);
+  Lock g(s);
+  if (!a) return r;
+  if (r == HSA_STATUS_SUCCESS && ptr && *ptr) {
+    if (!map_put(s.ptrs, reinterpret_cast<uint64_t>(*ptr), a->handle, size)) uncharge(a, size);  // OOM: untracked
+  } else {
+    uncharge(a, size);
+  }
   return r;
 }
 
 hsa_status_t w_pool_free(void* ptr) {
   State& s = st();
   {
-    std::lock_guard<std::mutex> g(s.mu);
-    auto it = s.ptrs.find(ptr);
-    if (it != s.ptrs.end()) {
-      uncharge(it->second.first, it->second.second);
-      s.ptrs.erase(it);
-    }
+    Lock g(s);
+    Alloc rec;
+    if (map_take(s.ptrs, reinterpret_cast<uint64_t>(ptr), &rec)) uncharge(agent_rec(s, rec.agent), rec.bytes);
   }
   return s.real_amd.hsa_amd_memory_pool_free_fn(ptr);
 }
@@ -395,29 +499,29 @@ hsa_status_t w_pool_free(void* ptr) {
 hsa_status_t w_vmem_create(hsa_amd_memory_pool_t pool, size_t size, hsa_amd_memory_type_t type, uint64_t flags,
                            hsa_amd_vmem_alloc_handle_t* handle) {
   State& s = st();
-  uint64_t agent = 0;
+  AgentRec* a = nullptr;
   {
-    std::lock_guard<std::mutex> g(s.mu);
-    agent = agent_of(pool);
-    if (agent && !charge(agent, size)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+    Lock g(s);
+    a = agent_of(pool);
+    if (a && !charge(a, size)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   }
   hsa_status_t r = s.real_amd.hsa_amd_vmem_handle_create_fn(pool, size, type, flags, handle);
-  std::lock_guard<std::mutex> g(s.mu);
-  if (!agent) return r;
-  if (r == HSA_STATUS_SUCCESS && handle) s.vmem[handle->handle] = {agent, size};
-  else uncharge(agent, size);
+  Lock g(s);
+  if (!a) return r;
+  if (r == HSA_STATUS_SUCCESS && handle) {
+    if (!map_put(s.vmem, handle->handle, a->handle, size)) uncharge(a, size);
+  } else {
+    uncharge(a, size);
+  }
   return r;
 }
 
 hsa_status_t w_vmem_release(hsa_amd_vmem_alloc_handle_t handle) {
   State& s = st();
   {
-    std::lock_guard<std::mutex> g(s.mu);
-    auto it = s.vmem.find(handle.handle);
-    if (it != s.vmem.end()) {
-      uncharge(it->second.first, it->second.second);
-      s.vmem.erase(it);
-    }
+    Lock g(s);
+    Alloc rec;
+    if (map_take(s.vmem, handle.handle, &rec)) uncharge(agent_rec(s, rec.agent), rec.bytes);
   }
   return s.real_amd.hsa_amd_vmem_handle_release_fn(handle);
 }
@@ -426,10 +530,10 @@ hsa_status_t w_pool_get_info(hsa_amd_memory_pool_t pool, hsa_amd_memory_pool_inf
   State& s = st();
   hsa_status_t r = s.real_amd.hsa_amd_memory_pool_get_info_fn(pool, attr, value);
   if (r != HSA_STATUS_SUCCESS || attr != HSA_AMD_MEMORY_POOL_INFO_SIZE || !s.limit || !value) return r;
-  std::lock_guard<std::mutex> g(s.mu);
+  Lock g(s);
   if (agent_of(pool)) {
     size_t* sz = static_cast<size_t*>(value);
-    *sz = std::min<size_t>(*sz, static_cast<size_t>(s.limit));
+    if (*sz > s.limit) *sz = static_cast<size_t>(s.limit);
   }
   return r;
 }
@@ -440,12 +544,13 @@ hsa_status_t w_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void* va
   if (r != HSA_STATUS_SUCCESS || !s.limit || !value ||
       static_cast<int>(attr) != static_cast<int>(HSA_AMD_AGENT_INFO_MEMORY_AVAIL))
     return r;
-  std::lock_guard<std::mutex> g(s.mu);
-  if (s.used.count(agent.handle)) {
+  Lock g(s);
+  map_agents(s);
+  if (AgentRec* a = agent_rec(s, agent.handle)) {
     uint64_t* avail = static_cast<uint64_t*>(value);
-    uint64_t u = budget_used(s, agent.handle);  // with a shared account: what the whole pod holds
+    uint64_t u = budget_used(s, a);  // with a shared account: what the whole pod holds
     uint64_t left = s.limit > u ? s.limit - u : 0;
-    *avail = std::min(*avail, left);
+    if (*avail > left) *avail = left;
   }
   return r;
 }
@@ -462,12 +567,13 @@ hsa_status_t w_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t
   State& s = st();
   hsa_status_t r = s.real_core.hsa_queue_create_fn(agent, size, type, callback, data, private_segment_size,
                                                    group_segment_size, queue);
-  if (r == HSA_STATUS_SUCCESS && queue && *queue && !s.mask.empty() && is_gpu(agent)) {
-    hsa_status_t m = s.real_amd.hsa_amd_queue_cu_set_mask_fn(*queue, s.mask_bits, s.mask.data());
+  if (r == HSA_STATUS_SUCCESS && queue && *queue && s.mask_words && is_gpu(agent)) {
+    hsa_status_t m = s.real_amd.hsa_amd_queue_cu_set_mask_fn(*queue, s.mask_bits, s.mask);
     if (m == HSA_STATUS_SUCCESS || static_cast<int>(m) == static_cast<int>(HSA_STATUS_CU_MASK_REDUCED))
-      s.queues_masked.fetch_add(1);
-    if (s.debug) std::fprintf(stderr, "[gpupool-share] queue %p CU mask (%u bits): status %d\n",
-                              static_cast<void*>(*queue), s.mask_bits, static_cast<int>(m));
+      count(&s.queues_masked);
+    if (s.debug)
+      fprintf(stderr, "[gpupool-share] queue %p CU mask (%u bits): status %d\n", static_cast<void*>(*queue), s.mask_bits,
+              static_cast<int>(m));
   }
   return r;
 }
@@ -475,13 +581,17 @@ hsa_status_t w_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t
 hsa_status_t w_queue_cu_set_mask(const hsa_queue_t* queue, uint32_t bits, const uint32_t* mask) {
   // the application's own mask (hipExtStreamCreateWithCUMask) can only narrow the slot's
   State& s = st();
-  if (s.mask.empty()) return s.real_amd.hsa_amd_queue_cu_set_mask_fn(queue, bits, mask);
-  std::vector<uint32_t> m(s.mask);
-  if (bits > 0 && mask) {
-    for (size_t i = 0; i < m.size(); ++i) m[i] &= i < bits / 32 ? mask[i] : 0u;
-    if (std::all_of(m.begin(), m.end(), [](uint32_t w) { return w == 0; })) m = s.mask;
+  if (!s.mask_words) return s.real_amd.hsa_amd_queue_cu_set_mask_fn(queue, bits, mask);
+  uint32_t m[kMaskWords];
+  bool any = false;
+  for (uint32_t i = 0; i < s.mask_words; ++i) {
+    m[i] = s.mask[i];
+    if (bits > 0 && mask) m[i] &= i < bits / 32 ? mask[i] : 0u;
+    any = any || m[i];
   }
-  return s.real_amd.hsa_amd_queue_cu_set_mask_fn(queue, s.mask_bits, m.data());
+  if (bits > 0 && mask && !any)
+    for (uint32_t i = 0; i < s.mask_words; ++i) m[i] = s.mask[i];  // nothing left: the slot's mask
+  return s.real_amd.hsa_amd_queue_cu_set_mask_fn(queue, s.mask_bits, m);
 }
 
 }  // namespace
@@ -493,14 +603,14 @@ __attribute__((visibility("default"))) bool OnLoad(HsaApiTable* table, uint64_t 
                                                    uint64_t failed_tool_count, const char* const* failed_tool_names) {
   if (!table || !table->core_ || !table->amd_ext_) return false;
   State& s = st();
-  std::lock_guard<std::mutex> g(s.mu);
+  Lock g(s);
   s.real_core = *table->core_;
   s.real_amd = *table->amd_ext_;
-  s.limit = parse_bytes(std::getenv("GPUPOOL_HBM_LIMIT_BYTES"));
-  s.mask = parse_mask(std::getenv("GPUPOOL_CU_MASK"), &s.mask_bits);
-  const char* dbg = std::getenv("GPUPOOL_SHARE_DEBUG");
+  s.limit = parse_bytes(getenv("GPUPOOL_HBM_LIMIT_BYTES"));
+  parse_mask(s, getenv("GPUPOOL_CU_MASK"));
+  const char* dbg = getenv("GPUPOOL_SHARE_DEBUG");
   s.debug = dbg && *dbg && *dbg != '0';
-  s.acct = acct_open(std::getenv("GPUPOOL_SHARE_ACCOUNT"), s.debug);
+  s.acct = acct_open(getenv("GPUPOOL_SHARE_ACCOUNT"), s.debug);
   if (s.acct && s.acct->limit) s.limit = s.acct->limit;  // the agent's number wins
   if (s.limit) {
     table->amd_ext_->hsa_amd_memory_pool_allocate_fn = w_pool_allocate;
@@ -510,13 +620,13 @@ __attribute__((visibility("default"))) bool OnLoad(HsaApiTable* table, uint64_t 
     table->amd_ext_->hsa_amd_memory_pool_get_info_fn = w_pool_get_info;
     table->core_->hsa_agent_get_info_fn = w_agent_get_info;
   }
-  if (!s.mask.empty()) {
+  if (s.mask_words) {
     table->core_->hsa_queue_create_fn = w_queue_create;
     table->amd_ext_->hsa_amd_queue_cu_set_mask_fn = w_queue_cu_set_mask;
   }
   if (s.debug)
-    std::fprintf(stderr, "[gpupool-share] loaded: HBM limit %llu B per GPU (%s), CU mask %u bits\n",
-                 static_cast<unsigned long long>(s.limit), s.acct ? "pod total" : "per process", s.mask_bits);
+    fprintf(stderr, "[gpupool-share] loaded: HBM limit %llu B per GPU (%s), CU mask %u bits\n",
+            static_cast<unsigned long long>(s.limit), s.acct ? "pod total" : "per process", s.mask_bits);
   return true;
 }
 
@@ -525,20 +635,23 @@ __attribute__((visibility("default"))) void OnUnload() {}
 // Counters for tests and diagnostics: JSON into buf.
 __attribute__((visibility("default"))) int gpupool_share_stats(char* buf, int len) {
   State& s = st();
-  std::lock_guard<std::mutex> g(s.mu);
+  Lock g(s);
   uint64_t used = 0, shared = 0;
-  for (const auto& kv : s.used) {
-    used = std::max(used, kv.second);
-    if (shared_index(s, kv.first) >= 0) shared = std::max(shared, budget_used(s, kv.first));
+  for (int i = 0; i < s.n_agents; ++i) {
+    const AgentRec* a = &s.agents[i];
+    if (a->used > used) used = a->used;
+    if (shared_index(s, a) >= 0) {
+      uint64_t u = budget_used(s, a);
+      if (u > shared) shared = u;
+    }
   }
-  return std::snprintf(buf, static_cast<size_t>(len),
-                       "{\"limit\":%llu,\"used\":%llu,\"peak\":%llu,\"denied\":%llu,\"queuesMasked\":%llu,"
-                       "\"maskBits\":%u,\"shared\":%d,\"podUsed\":%llu,\"reclaimed\":%llu}",
-                       static_cast<unsigned long long>(s.limit), static_cast<unsigned long long>(used),
-                       static_cast<unsigned long long>(s.peak.load()),
-                       static_cast<unsigned long long>(s.denied.load()),
-                       static_cast<unsigned long long>(s.queues_masked.load()), s.mask_bits, s.acct ? 1 : 0,
-                       static_cast<unsigned long long>(shared), static_cast<unsigned long long>(s.reclaimed.load()));
+  return snprintf(buf, static_cast<size_t>(len),
+                  "{\"limit\":%llu,\"used\":%llu,\"peak\":%llu,\"denied\":%llu,\"queuesMasked\":%llu,"
+                  "\"maskBits\":%u,\"shared\":%d,\"podUsed\":%llu,\"reclaimed\":%llu}",
+                  static_cast<unsigned long long>(s.limit), static_cast<unsigned long long>(used),
+                  static_cast<unsigned long long>(load(&s.peak)), static_cast<unsigned long long>(load(&s.denied)),
+                  static_cast<unsigned long long>(load(&s.queues_masked)), s.mask_bits, s.acct ? 1 : 0,
+                  static_cast<unsigned long long>(shared), static_cast<unsigned long long>(load(&s.reclaimed)));
 }
 
 }  // extern "C"

@@ -143,3 +143,22 @@ def test_fake_fixture_is_fresh(tmp_path):
     subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "gen_fake_fixture.py")],
                    check=True, capture_output=True)
     assert [open(fx).read() for fx in fxs] == before
+
+
+def test_share_library_needs_only_old_glibc(native_built):
+    """libgpupool_share.so is loaded into arbitrary pod images through HSA_TOOLS_LIB, and ROCr
+    skips a tools library that fails to load (the slot's limits would silently vanish). So it may
+    need nothing but libc, at symbol versions every supported distro has (<= GLIBC_2.17), and may
+    export only its three entry points (no std:: instantiations to interpose on the pod's own)."""
+    import re
+    lib = os.path.join(native_built, "libgpupool_share.so")
+    dyn = subprocess.run(["objdump", "-p", lib], capture_output=True, text=True, check=True).stdout
+    needed = re.findall(r"NEEDED\s+(\S+)", dyn)
+    assert set(needed) <= {"libc.so.6"}, needed
+    syms = subprocess.run(["objdump", "-T", lib], capture_output=True, text=True, check=True).stdout
+    versions = set(re.findall(r"\((GLIBC[A-Z]*_[0-9.]+)\)", syms))
+    assert not any(v.startswith("GLIBCXX") or v.startswith("CXXABI") for v in versions), versions
+    newest = max(tuple(int(x) for x in v.split("_")[1].split(".")) for v in versions)
+    assert newest <= (2, 17), versions
+    exported = {ln.split()[-1] for ln in syms.splitlines() if " DF .text" in ln}
+    assert exported == {"OnLoad", "OnUnload", "gpupool_share_stats"}, exported
