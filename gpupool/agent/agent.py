@@ -193,6 +193,7 @@ class Agent:
             self.ledger.commit(self.records)
         self.share_lib_dir = self._install_share_lib()
         self._pod_ids: tuple[float, set[str]] | None = None  # (listed at, device IDs pods hold)
+        self._over_budget: set[tuple[str, str, str]] = set()  # (gpu, ns, pod) over their slot budget
         self.snap = self.dev.snapshot()
         self.backend = self.snap.get("backend", cfg.backend)
         self.by_uuid = {d["uuid"]: d for d in self.snap["devices"]}
@@ -786,9 +787,57 @@ class Agent:
                     e["gfxBusy"] = round((e["gfxBusy"] or 0.0) + busy, 4)
             if per:
                 usage[u] = sorted(per.values(), key=lambda x: (x["namespace"], x["pod"]))
+        over = self._check_slot_budgets(usage)
         with self.lock:
             self._proc_prev = new_prev
             self.pod_usage = usage
+        for msg in over:
+            self.node_event("SlotBudgetExceeded", msg)
+
+    # VRAM a pod may hold beyond its slots' budget: what ROCr allocates internally (queues, scratch,
+    # code objects), which the share library does not charge
+    SLOT_BUDGET_SLACK = (512 << 20, 0.05)
+
+    def _check_slot_budgets(self, usage: dict[str, list[dict]]) -> list[str]:
+        """Defence in depth for isolated slots: the HBM budget is enforced inside the pod by
+        libgpupool_share.so, and a pod in which it is not active (an image whose loader cannot
+        load it, a pod that unset HSA_TOOLS_LIB) would run unconfined without anyone noticing. The
+        agent sees each pod's VRAM per GPU (amdsmi / DRM fdinfo): a pod holding more than its
+        slots x hbmBytesPerSlot (+ ROCr's uncharged internals) is marked ``overBudget`` in the
+        usage view and metrics, and reported once per (pod, GPU) as a Node event. Returns the
+        messages of new violations."""
+        slots_of: dict[tuple[str, str, str], int] = {}
+        for gpu, pods in self._pods_cache[1].items():  # one entry per slot a pod holds
+            for pe in pods:
+                key = (gpu, pe.get("namespace", ""), pe.get("name", ""))
+                slots_of[key] = slots_of.get(key, 0) + 1
+        out, seen = [], set()
+        slack, frac = self.SLOT_BUDGET_SLACK
+        with self.lock:
+            for u, pods in usage.items():
+                rec = self.records.get(u)
+                if not rec or self._slots_of(rec) <= 1:
+                    continue
+                per_slot = self._slot_layout(u, rec).get("hbmBytesPerSlot") or 0
+                if not per_slot:
+                    continue
+                for e in pods:
+                    n = slots_of.get((u, e["namespace"], e["pod"]), 0)
+                    if not n:
+                        continue
+                    budget = n * per_slot
+                    e["slotBudgetBytes"] = budget
+                    if e["vramBytes"] > budget * (1 + frac) + slack:
+                        e["overBudget"] = True
+                        key = (u, e["namespace"], e["pod"])
+                        seen.add(key)
+                        if key not in self._over_budget:
+                            out.append(f"pod {e['namespace']}/{e['pod']} holds {e['vramBytes']} B of "
+                                       f"VRAM on GPU {u}, over its {n} slot(s) x {per_slot} B: "
+                                       f"its HBM limit is not in force (is libgpupool_share.so "
+                                       f"loaded in the pod?)")
+            self._over_budget = seen
+        return out
 
     # ================================================================ views
     def _pods_by_device(self, fresh: bool = False) -> dict[str, list[dict]]:
@@ -1902,6 +1951,10 @@ class Agent:
                     lab = f'uuid="{u}",index="{d.get("index")}",node="{self.cfg.node}",' \
                           f'pool="{pool}",namespace="{e["namespace"]}",pod="{e["pod"]}"'
                     lines.append(f"gpupool_pod_vram_bytes{{{lab}}} {e['vramBytes']}")
+                    if e.get("slotBudgetBytes"):
+                        lines.append(f"gpupool_pod_slot_budget_bytes{{{lab}}} {e['slotBudgetBytes']}")
+                        lines.append(f"gpupool_pod_over_slot_budget{{{lab}}} "
+                                     f"{1 if e.get('overBudget') else 0}")
                     if e.get("gfxBusy") is not None:
                         lines.append(f"gpupool_pod_gfx_busy_ratio{{{lab}}} {e['gfxBusy']}")
             for k, v in self.stats.items():

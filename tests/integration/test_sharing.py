@@ -313,3 +313,52 @@ def test_hbm_account_of_an_exited_pod_is_removed(cluster_factory):
         time.sleep(0.05)
     print(f"account removed {time.monotonic() - t0:.2f} s after the pod was gone "
           f"(sample period {c.sample_interval} s)")
+
+
+def test_pod_over_its_slot_budget_is_reported(cluster_factory):
+    """Defence in depth for the in-pod HBM limit: the agent compares each pod's VRAM on a shared
+    GPU (amdsmi process list; here injected through the fault overlay) with its slots x
+    hbmBytesPerSlot. A pod holding far more — its limit is not in force, e.g. the share library
+    did not load in its image — is flagged in the usage view and metrics and gets one Node event;
+    a pod within budget (+ ROCr's uncharged internals) is not."""
+    import time
+    from gpupool.kube import EVENTS
+    c = cluster_factory()
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("bud", 1, sharing={"replicasPerGPU": 2,
+                                                     "hbmBytesPerSlot": 8 << 30}), "default")
+    gpu = wait_ready(k, "bud", 1)["status"]["devices"][0]
+    pids = {}
+    for name in ("ok", "rogue"):
+        k.create(PODS, pause_pod(name), "default")
+        p = k.wait_for(PODS, name, "default", lambda p: running(p) and "gpupool.amd.com/pid" in
+                       p["metadata"].get("annotations", {}), timeout=30)
+        pids[name] = int(p["metadata"]["annotations"]["gpupool.amd.com/pid"])
+    deadline = time.monotonic() + 10  # the agent's PodResources view shows both slots' pods
+    while time.monotonic() < deadline:
+        view = c.agent_request("mi355x-node-0", "GET", "/v1/node")
+        if len(next(d for d in view["devices"] if d["uuid"] == gpu["uuid"])["pods"]) == 2:
+            break
+        time.sleep(0.1)
+    c.set_faults("mi355x-node-0", {"devices": {str(gpu["index"]): {"processes": [
+        {"pid": pids["ok"], "vramBytes": (8 << 30) + (200 << 20), "gfxNs": 0},
+        {"pid": pids["rogue"], "vramBytes": 20 << 30, "gfxNs": 0}]}}}, sample=True)
+    view = c.agent_request("mi355x-node-0", "GET", "/v1/node")
+    use = {e["pod"]: e for e in next(d for d in view["devices"] if d["uuid"] == gpu["uuid"])["usage"]}
+    assert use["rogue"]["overBudget"] and use["rogue"]["slotBudgetBytes"] == 8 << 30, use
+    assert not use["ok"].get("overBudget") and use["ok"]["slotBudgetBytes"] == 8 << 30, use
+    metrics = str(c.agent_request("mi355x-node-0", "GET", "/metrics"))
+    assert 'gpupool_pod_over_slot_budget{' in metrics and 'pod="rogue"} 1' in metrics
+    deadline = time.monotonic() + 10
+    evs = []
+    while time.monotonic() < deadline:
+        evs = [e for e in k.list(EVENTS, "default")["items"] if e["reason"] == "SlotBudgetExceeded"]
+        if evs:
+            break
+        time.sleep(0.1)
+    assert len(evs) == 1 and "default/rogue" in evs[0]["message"], evs
+    c.set_faults("mi355x-node-0", {"devices": {str(gpu["index"]): {"processes": [
+        {"pid": pids["rogue"], "vramBytes": 20 << 30, "gfxNs": 0}]}}}, sample=True)
+    time.sleep(0.5)  # still over: no second event for the same pod and GPU
+    assert len([e for e in k.list(EVENTS, "default")["items"]
+                if e["reason"] == "SlotBudgetExceeded"]) == 1
