@@ -260,3 +260,16 @@ def test_hbm_account_is_keyed_by_the_gpus_hip_uuid(tmp_path):
     print(f"account: index0 {used0} B, index1 ({uuid}) {used1} B")
     assert used0 == 0, used0
     assert 1 * GiB <= used1 < 2 * GiB, used1
+
+
+def test_share_library_loads_and_reports_in_this_process():
+    """The tools library as the test process itself maps it (the isolation tests above load it in
+    their child processes through HSA_TOOLS_LIB): it loads with nothing but libc and its
+    diagnostics entry point answers — not hooked here (ROCr never called OnLoad), so no limits."""
+    import ctypes
+    lib = ctypes.CDLL(LIB)
+    buf = ctypes.create_string_buffer(512)
+    n = lib.gpupool_share_stats(buf, len(buf))
+    st = json.loads(buf.value.decode())
+    assert n > 0 and st["limit"] == 0 and st["maskBits"] == 0 and st["shared"] == 0, st
+    assert hasattr(lib, "OnLoad") and hasattr(lib, "OnUnload")
