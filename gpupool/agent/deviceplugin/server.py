@@ -15,7 +15,9 @@ endpoint ``<plugin_dir>/gpupool-<resource>.sock`` registered with the kubelet:
 * Allocate returns /dev/kfd + /dev/dri/renderD<N> DeviceSpecs and ``ROCR_VISIBLE_DEVICES`` set to
   the GPUs' ROCr UUIDs (``GPU-<serial>``), so a container sees exactly its GPUs.
 * GetPreferredAllocation picks xGMI/NUMA-close sets with libmi355x_dev's selector.
-* The kubelet socket is watched; a kubelet restart (new socket inode) triggers re-registration.
+* The kubelet socket is watched; a kubelet restart (new socket, the watch channel to it dropping,
+  or — as a real kubelet does at start — our own endpoint socket removed, which restarts the
+  plugin's server) triggers re-registration.
 """
 from __future__ import annotations
 
@@ -72,26 +74,44 @@ class DevicePluginServer:
         self._marked = -1
 
     # ------------------------------------------------------------ lifecycle
-    def start(self) -> None:
+    def _serve(self) -> None:
+        """(Re)create the plugin's gRPC server on its socket."""
         try:
             os.unlink(self.sock)
         except FileNotFoundError:
             pass
-        self.server = grpc.server(cf.ThreadPoolExecutor(max_workers=16,
-                                                        thread_name_prefix=f"dp-{self.resource}"))
+        server = grpc.server(cf.ThreadPoolExecutor(max_workers=16,
+                                                   thread_name_prefix=f"dp-{self.resource}"))
 
         def list_and_watch(request, context, send):
             return self.ListAndWatch(request, context, send)
         list_and_watch.experimental_non_blocking = True  # handler gets gRPC's send callback
-        self.server.add_generic_rpc_handlers((service_handler("v1beta1.DevicePlugin", {
+        server.add_generic_rpc_handlers((service_handler("v1beta1.DevicePlugin", {
             "GetDevicePluginOptions": self.GetDevicePluginOptions,
             "ListAndWatch": list_and_watch,
             "GetPreferredAllocation": self.GetPreferredAllocation,
             "Allocate": self.Allocate,
             "PreStartContainer": self.PreStartContainer,
         }),))
-        self.server.add_insecure_port(unix_target(self.sock))
-        self.server.start()
+        server.add_insecure_port(unix_target(self.sock))
+        server.start()
+        self.server = server
+        self._sock_ino = self._sock_identity(self.sock)
+
+    def _reserve(self) -> None:
+        """A starting kubelet removes every socket in the device-plugin directory (its signal to
+        plugins to re-register): the endpoint it would dial for our registration is gone. Stop the
+        old server — and wait for it: gRPC unlinks its socket path when the listener is torn
+        down, which done late would delete the new socket — then serve again on a fresh socket."""
+        old = self.server
+        if old is not None:
+            old.stop(0).wait(5)
+        log.info("device-plugin socket %s was removed (kubelet restart): serving again", self.sock)
+        self._serve()
+
+    def start(self) -> None:
+        self._sock_ino = None
+        self._serve()
         self._sender = threading.Thread(target=self._send_loop, daemon=True,
                                         name=f"dp-send-{self.resource}")
         self._sender.start()
@@ -172,6 +192,13 @@ class DevicePluginServer:
     def _monitor_kubelet(self) -> None:
         ksock = os.path.join(self.plugin_dir, KUBELET_SOCKET)
         while not self.stopped:
+            own = self._sock_identity(self.sock)
+            if own is None or own != self._sock_ino:  # our endpoint was removed: serve it again
+                try:
+                    self._reserve()
+                    self._kubelet_ino = None  # and register with whichever kubelet is there
+                except Exception:
+                    log.exception("restarting the device-plugin server failed")
             ident = self._sock_identity(ksock)
             if ident is None:
                 self.registered = False  # kubelet gone: register again when it comes back

@@ -111,11 +111,19 @@ class FakeKubelet:
     # ============================================================ gRPC servers
     def start(self) -> None:
         ksock = os.path.join(self.plugin_dir, KUBELET_SOCKET)
-        for p in (ksock, self.pr_socket):
-            try:
-                os.unlink(p)
-            except FileNotFoundError:
-                pass
+        # like the kubelet's device manager at start: remove every socket in the plugin directory
+        # — stale plugin endpoints included; plugins take that as the signal to serve again and
+        # re-register
+        for name in os.listdir(self.plugin_dir):
+            if name.endswith(".sock"):
+                try:
+                    os.unlink(os.path.join(self.plugin_dir, name))
+                except FileNotFoundError:
+                    pass
+        try:
+            os.unlink(self.pr_socket)
+        except FileNotFoundError:
+            pass
         self.reg_server = grpc.server(cf.ThreadPoolExecutor(max_workers=8))
         self.reg_server.add_generic_rpc_handlers((service_handler("v1beta1.Registration",
                                                                   {"Register": self.Register}),))

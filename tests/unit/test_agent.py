@@ -101,11 +101,15 @@ def test_health_sampling_follows_fault_overlay(tmp_path, sockdir, native_built):
 class MiniKubelet:
     """Just the kubelet's Registration service + a ListAndWatch consumer."""
 
-    def __init__(self, plugin_dir):
+    def __init__(self, plugin_dir, wipe: bool = False):
         import concurrent.futures as cf
         from gpupool.agent.deviceplugin.proto import service_handler
         self.dir = plugin_dir
         self.registrations = []
+        if wipe:  # a real kubelet's device manager removes every socket in the directory at start
+            for name in os.listdir(plugin_dir) if os.path.isdir(plugin_dir) else []:
+                if name.endswith(".sock"):
+                    os.unlink(os.path.join(plugin_dir, name))
         self.server = grpc.server(cf.ThreadPoolExecutor(4))
         self.server.add_generic_rpc_handlers((service_handler("v1beta1.Registration",
                                                               {"Register": self.Register}),))
@@ -287,6 +291,37 @@ def test_new_listandwatch_stream_restores_advertised(tmp_path, sockdir, native_b
         assert wait(lambda: advertised() == mine), advertised()
         stream2.cancel()
         ch2.close()
+    finally:
+        a.stop()
+        kubelet.stop()
+
+
+def test_kubelet_restart_that_wipes_the_plugin_dir(tmp_path, sockdir, native_built):
+    """A starting kubelet removes every socket in the device-plugin directory, the plugin's own
+    endpoint included, and dials that endpoint when the plugin registers. So the plugin must notice
+    its socket is gone, serve again on a fresh one and re-register — after which the new kubelet
+    can open ListAndWatch on it."""
+    dp_dir = os.path.join(sockdir, "dp")
+    kubelet = MiniKubelet(dp_dir)
+    a = make_agent(tmp_path, sockdir)
+    sock = os.path.join(dp_dir, "gpupool-amd-com_gpu.sock")
+    try:
+        r = claim(a, count=1)
+        deadline = time.time() + 5
+        while not kubelet.registrations and time.time() < deadline:
+            time.sleep(0.02)
+        assert kubelet.registrations
+        kubelet.stop()
+        kubelet = MiniKubelet(dp_dir, wipe=True)
+        assert not os.path.exists(sock)
+        deadline = time.time() + 5
+        while time.time() < deadline and not (kubelet.registrations and os.path.exists(sock)):
+            time.sleep(0.05)
+        assert kubelet.registrations and os.path.exists(sock), (kubelet.registrations, os.listdir(dp_dir))
+        ch = grpc.insecure_channel(unix_target(sock))
+        first = next(Stub(ch, "v1beta1.DevicePlugin").ListAndWatch(DP.Empty()))
+        assert {d.ID for d in first.devices} == {r["devices"][0]["uuid"]}
+        ch.close()
     finally:
         a.stop()
         kubelet.stop()
