@@ -253,12 +253,37 @@ class RpcServer:
             self._pending.pop(conn, None)
 
     # ------------------------------------------------------------ one connection
-    def _reject(self, conn, status: int, reason: str, message: str) -> None:
+    LINGER_BYTES = 64 << 10  # at most this much of a refused request is ever read, in total
+    LINGER_S = 0.5
+
+    def _reject(self, conn, status: int, reason: str, message: str, rf: "_Reader | None" = None) -> None:
+        """Answer a refused request and close without reading its body — gracefully: the reply is
+        followed by a FIN, then whatever the client still sends is discarded for a moment
+        (bounded by LINGER_BYTES over the whole connection and LINGER_S), so the client reads the
+        status instead of a reset. Closing with unread bytes in the receive buffer makes TCP send
+        an RST, and the client's body write then fails with EPIPE before it sees the 401."""
         self.rejected_requests += 1
         try:
             self._send(conn, json_reply({"reason": reason, "message": message}, status), False)
+            conn.shutdown(socket.SHUT_WR)
         except OSError:
-            pass
+            return
+        budget = self.LINGER_BYTES - (rf.total if rf is not None else 0)
+        end = time.monotonic() + self.LINGER_S
+        while budget > 0:
+            left = end - time.monotonic()
+            if left <= 0:
+                break
+            try:
+                conn.settimeout(left)
+                data = conn.recv(min(65536, budget))
+            except (OSError, ValueError):
+                break
+            if not data:
+                break
+            budget -= len(data)
+            if rf is not None:
+                rf.total += len(data)
 
     def _serve_conn(self, conn: socket.socket, ssl_ctx) -> None:
         trusted = False  # until a request is answered with something other than 401
@@ -290,7 +315,7 @@ class RpcServer:
                     return
                 if head is None:
                     self._reject(conn, 431, "HeadersTooLarge",
-                                 f"request head over {MAX_LINE + MAX_HEADER_BYTES} bytes")
+                                 f"request head over {MAX_LINE + MAX_HEADER_BYTES} bytes", rf)
                     return
                 lines = head.split(b"\r\n")
                 while lines and not lines[0]:  # blank lines before a request line are allowed
@@ -307,7 +332,7 @@ class RpcServer:
                 fields = [h for h in lines[1:] if h]
                 if len(fields) > MAX_HEADERS or len(head) - len(lines[0]) > MAX_HEADER_BYTES:
                     self._reject(conn, 431, "HeadersTooLarge",
-                                 f"at most {MAX_HEADERS} header lines / {MAX_HEADER_BYTES} bytes")
+                                 f"at most {MAX_HEADERS} header lines / {MAX_HEADER_BYTES} bytes", rf)
                     return
                 headers: dict[str, str] = {}
                 for h in fields:
@@ -317,21 +342,21 @@ class RpcServer:
                 # the token before the body: an unauthenticated peer never gets a byte buffered
                 if self._auth and path not in OPEN_PATHS and not hmac.compare_digest(
                         headers.get("authorization", "").encode(), self._auth):
-                    self._reject(conn, 401, "Unauthorized", "agent RPC requires the manager's token")
+                    self._reject(conn, 401, "Unauthorized", "agent RPC requires the manager's token", rf)
                     return
                 cl = headers.get("content-length")
                 if cl is None:
                     if method in BODY_METHODS:
-                        self._reject(conn, 400, "BadRequest", "Content-Length required")
+                        self._reject(conn, 400, "BadRequest", "Content-Length required", rf)
                         return
                     n = 0
                 elif not cl.isdigit() or not cl.isascii():  # no sign, no spaces, no hex
-                    self._reject(conn, 400, "BadRequest", f"bad Content-Length {cl[:32]!r}")
+                    self._reject(conn, 400, "BadRequest", f"bad Content-Length {cl[:32]!r}", rf)
                     return
                 else:
                     n = int(cl)
                 if n > MAX_BODY:
-                    self._reject(conn, 413, "PayloadTooLarge", f"body over {MAX_BODY} bytes")
+                    self._reject(conn, 413, "PayloadTooLarge", f"body over {MAX_BODY} bytes", rf)
                     return
                 try:
                     body = rf.read(n) if n else b""
