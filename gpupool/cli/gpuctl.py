@@ -388,15 +388,19 @@ def cmd_top(c: Client, ns: str, args) -> int:
     num = lambda v: float(v) if isinstance(v, (int, float)) else 0.0  # noqa: E731
     if args.what == "pods":  # per-pod accounting on (shared) GPUs: the agent's process -> pod map
         print(f"{'NAMESPACE/POD':<36}{'NODE':<18}{'IDX':<5}{'POOL':<28}{'VRAM(GiB)':<11}{'GPU%':<6}"
-              "PIDS")
+              f"{'PIDS':<16}BUDGET(GiB)")
         for node, d in sorted(rows, key=lambda r: (r[0], r[1].get("index", 0))):
             for e in d.get("usage") or []:
                 busy = e.get("gfxBusy")
+                # isolated slots: the pod's HBM budget on this GPU, "!" when it holds more (its
+                # in-pod limit is not in force)
+                bud = e.get("slotBudgetBytes")
+                budget = "-" if not bud else f"{bud / 2**30:.2f}" + ("!" if e.get("overBudget") else "")
                 print(f"{e.get('namespace', '')}/{e.get('pod', ''):<{35 - len(e.get('namespace', ''))}}"
                       f" {node:<18}{d.get('index', ''):<5}{d.get('pool', '') or '-':<28}"
                       f"{num(e.get('vramBytes')) / 2**30:<11.2f}"
                       f"{'-' if busy is None else f'{100 * busy:.0f}':<6}"
-                      f"{','.join(str(x) for x in e.get('pids') or [])}")
+                      f"{','.join(str(x) for x in e.get('pids') or []):<16}{budget}")
         return 0
     if args.what == "gpus":
         print(f"{'NODE':<18}{'IDX':<5}{'POOL':<28}{'GFX%':<6}{'UMC%':<6}{'POWER(W)':<10}VRAM(GiB)")

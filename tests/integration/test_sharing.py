@@ -357,6 +357,14 @@ def test_pod_over_its_slot_budget_is_reported(cluster_factory):
             break
         time.sleep(0.1)
     assert len(evs) == 1 and "default/rogue" in evs[0]["message"], evs
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([os.path.join(root, "bin", "gpuctl"), "--server", c.url, "top", "pods"],
+                       capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, GPUPOOL_AGENT_TOKEN=c.agent_token))
+    rows = {ln.split()[0]: ln.split() for ln in r.stdout.splitlines()[1:]}
+    assert rows["default/rogue"][-1] == "8.00!" and rows["default/ok"][-1] == "8.00", r.stdout
     c.set_faults("mi355x-node-0", {"devices": {str(gpu["index"]): {"processes": [
         {"pid": pids["rogue"], "vramBytes": 20 << 30, "gfxNs": 0}]}}}, sample=True)
     time.sleep(0.5)  # still over: no second event for the same pod and GPU
