@@ -1162,7 +1162,7 @@ class Agent:
         self.ledger.flush(claim_seq)
         lap("commit2")
         self._ensure_plugin(resource)
-        self._notify_plugins(sync=True)  # written to the kubelet's stream on this thread
+        self._notify_plugins(sync=True)  # handed to the kubelet's stream before the reply
 
         def record_claimed() -> None:
             # Probing -> Claimed (with the probe result) goes to the ledger's background writer

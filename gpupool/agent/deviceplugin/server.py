@@ -216,21 +216,35 @@ class DevicePluginServer:
             return None
         return (st.st_ino, st.st_ctime_ns)
 
+    # ``notify(sync=True)`` (the claim path) marks the new list advertised as soon as it is handed
+    # to a live stream's sender instead of after gRPC reports the write complete. gRPC's Python
+    # server acknowledges a streamed write only after its completion-queue thread has run
+    # (0.29–0.35 ms per message here, profiles/r4g_advertise_ab.json), while the kubelet consumes
+    # the stream asynchronously anyway and publishes allocatable on its own node-status sync. A
+    # stream that turns out dead ends (``gone``), which clears the advertised bits again. False:
+    # the strict behaviour (mark only after the write completed, on the claim's thread).
+    ADVERTISE_ON_SUBMIT = os.environ.get("GPUPOOL_ADVERTISE_ON_WRITE", "") in ("", "0")
+
     def notify(self, sync: bool = False) -> None:
-        """Publish the current device list, built on the caller's thread. ``sync`` (the claim
-        path): send it on this thread to every stream no other thread is sending on, and return
-        once written — the caller then finds its GPUs advertised without waiting for another
-        thread. Otherwise the sender thread sends it. A device counts as advertised once a
-        stream has written the message — not before: a pod placed on a GPU the kubelet has not
-        heard of yet would fail admission."""
+        """Publish the current device list, built on the caller's thread, through the sender
+        thread. ``sync`` (the claim path): the caller then finds its GPUs advertised at once if
+        a live kubelet stream will carry the list (ADVERTISE_ON_SUBMIT), else it sends on this
+        thread and returns once written. Never before a stream exists: a pod placed on a GPU the
+        kubelet has not heard of would fail admission."""
         resp, healthy = self._devices_msg()
+        early = sync and self.ADVERTISE_ON_SUBMIT
         with self.cv:
             self.version += 1
-            self._pending = (self.version, resp, healthy)
-            live = list(self._live)
-            if not sync:
+            ver = self.version
+            self._pending = (ver, resp, healthy)
+            live = [st for st in self._live if st.alive]
+            if not sync or early:
                 self._wake = True
                 self.cv.notify_all()
+        if early:
+            if live:
+                self._mark(ver, healthy)
+            return
         if sync:
             for st in live:
                 self._drive(st)
