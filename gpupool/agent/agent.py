@@ -194,6 +194,7 @@ class Agent:
         self.share_lib_dir = self._install_share_lib()
         self._pod_ids: tuple[float, set[str]] | None = None  # (listed at, device IDs pods hold)
         self._over_budget: set[tuple[str, str, str]] = set()  # (gpu, ns, pod) over their slot budget
+        self._layouts: dict[tuple, dict] = {}  # memoised slot layouts (_slot_layout)
         self.snap = self.dev.snapshot()
         self.backend = self.snap.get("backend", cfg.backend)
         self.by_uuid = {d["uuid"]: d for d in self.snap["devices"]}
@@ -967,10 +968,7 @@ class Agent:
             out["usage"] = self.pod_usage[uuid]
         if rec and self._slots_of(rec) > 1:
             lay = self._slot_layout(uuid, rec)
-            masks = lay.pop("masks", None)
-            if masks is not None:  # per slot: its CU-mask bits and the XCDs they land on
-                lay["slotCUMasks"] = [_ranges(m) for m in masks]
-                lay["slotXcds"] = [_ranges(slotlib.slot_xcds(m, lay["xcds"])) for m in masks]
+            lay.pop("masks", None)
             out["sharing"] = lay
         out["telemetry"] = self._telemetry(d)
         if not rec:
@@ -1759,10 +1757,21 @@ class Agent:
 
     def _slot_layout(self, uuid: str, rec: dict) -> dict:
         """The isolation a GPU's slots get under its pool's spec.sharing: per-slot CU-mask bits and
-        layout (xcd | striped), the enforced per-slot HBM budget. Called under self.lock."""
+        layout, the enforced per-slot HBM budget. Memoised per (GPU, sharing policy, CU count,
+        partition, HBM size): node views ask for it on every observe. Called under self.lock."""
         share = (rec.get("policy") or {}).get("sharing") or {}
-        k = self._slots_of(rec)
         d = self.by_uuid.get(uuid) or {}
+        key = (uuid, json.dumps(share, sort_keys=True), (d.get("asic") or {}).get("computeUnits"),
+               json.dumps(d.get("partition") or {}, sort_keys=True), d.get("memTotalBytes"))
+        hit = self._layouts.get(key)
+        if hit is None:
+            if len(self._layouts) > 4096:
+                self._layouts.clear()
+            hit = self._layouts[key] = self._compute_slot_layout(rec, share, d)
+        return {k: (list(v) if isinstance(v, list) else v) for k, v in hit.items()}
+
+    def _compute_slot_layout(self, rec: dict, share: dict, d: dict) -> dict:
+        k = self._slots_of(rec)
         out: dict = {"replicasPerGPU": k}
         per_slot = int(share.get("hbmBytesPerSlot") or 0)
         if per_slot > 0:
@@ -1781,7 +1790,10 @@ class Agent:
                 bits, layout = slotlib.slot_cus(i, k, cu, cus, xcds)
                 masks.append(bits)
             out.update({"cuLayout": layout, "cuPerSlot": len(masks[0]), "xcds": xcds,
-                        "masks": masks})
+                        "masks": masks,
+                        # per slot: its CU-mask bits and the XCDs they land on (node views)
+                        "slotCUMasks": [_ranges(m) for m in masks],
+                        "slotXcds": [_ranges(slotlib.slot_xcds(m, xcds)) for m in masks]})
         return out
 
     def _isolation_env(self, slots: list[str], mounts: list[dict]) -> dict[str, str]:
