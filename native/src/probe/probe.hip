@@ -91,16 +91,37 @@ __device__ __forceinline__ u32x4 pattern16(uint64_t i16, uint32_t seed, uint32_t
 // MI355X, 9 interleaved rounds (profiles/r3h_probe_pattern_ab.json): 1 GiB test 6.16 -> 6.41 TB/s
 // (write 5.77 -> 6.06, read 6.64 -> 6.76), claim-time probe (beside the MFMA phase) 0.98 -> 0.91 ms.
 constexpr int kHbmPattern = 1;
+constexpr int kHbmLayout = 0;  // see hbm_fill; A/B in scripts/probe_hbm_layout_ab.py
 
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 constexpr int kHbmThreads = 256;
 constexpr int kHbmUnroll = 4;
 
-template <int kPat = kHbmPattern>
+// Layouts (probe option "hbmLayout", in-process A/B): 0 grid-stride — each unrolled access of a
+// thread is a whole grid (MiBs) apart; 1 tiled — a workgroup's kHbmUnroll accesses per iteration
+// cover one contiguous 16 KiB tile (more row-buffer locality per workgroup).
+constexpr uint64_t kHbmTile = static_cast<uint64_t>(kHbmThreads) * kHbmUnroll;  // 16-B vectors
+
+template <int kPat = kHbmPattern, int kLayout = 0>
 __global__ __launch_bounds__(kHbmThreads) void hbm_fill(u32x4* __restrict__ p, uint64_t n16,
                                                         uint32_t seed, uint32_t flip) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kHbmThreads;
+  if constexpr (kLayout == 1) {
+    const uint64_t tiles = n16 / kHbmTile;
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+      const uint64_t base = t * kHbmTile + threadIdx.x;
+#pragma unroll
+      for (int u = 0; u < kHbmUnroll; ++u) {
+        const uint64_t j = base + static_cast<uint64_t>(u) * kHbmThreads;
+        __builtin_nontemporal_store(pattern16<kPat>(j, seed, flip), &p[j]);
+      }
+    }
+    for (uint64_t i = tiles * kHbmTile + static_cast<uint64_t>(blockIdx.x) * kHbmThreads + threadIdx.x; i < n16;
+         i += stride)
+      __builtin_nontemporal_store(pattern16<kPat>(i, seed, flip), &p[i]);
+    return;
+  }
   uint64_t i = static_cast<uint64_t>(blockIdx.x) * kHbmThreads + threadIdx.x;
   for (; i + (kHbmUnroll - 1) * stride < n16; i += kHbmUnroll * stride) {
 #pragma unroll
@@ -118,34 +139,44 @@ __device__ __forceinline__ uint32_t mismatches16(u32x4 v, u32x4 e) {
 }
 
 // Counts flipped BITS; records the lowest faulting 16-byte index. One atomic per wave.
-template <int kPat = kHbmPattern>
+template <int kPat = kHbmPattern, int kLayout = 0>
 __global__ __launch_bounds__(kHbmThreads) void hbm_verify(const u32x4* __restrict__ p, uint64_t n16,
                                                           uint32_t seed, uint32_t flip,
                                                           unsigned long long* __restrict__ bad_bits,
                                                           unsigned long long* __restrict__ first_bad) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kHbmThreads;
-  uint64_t i = static_cast<uint64_t>(blockIdx.x) * kHbmThreads + threadIdx.x;
   uint32_t bad = 0;
   uint64_t first = ~0ull;
-  for (; i + (kHbmUnroll - 1) * stride < n16; i += kHbmUnroll * stride) {
-    u32x4 v[kHbmUnroll];
-#pragma unroll
-    for (int u = 0; u < kHbmUnroll; ++u) v[u] = __builtin_nontemporal_load(&p[i + u * stride]);
-#pragma unroll
-    for (int u = 0; u < kHbmUnroll; ++u) {
-      uint32_t m = mismatches16(v[u], pattern16<kPat>(i + u * stride, seed, flip));
-      if (m) {
-        bad += m;
-        first = umin64(first, i + u * stride);
-      }
-    }
-  }
-  for (; i < n16; i += stride) {
-    uint32_t m = mismatches16(__builtin_nontemporal_load(&p[i]), pattern16<kPat>(i, seed, flip));
+  auto check = [&](u32x4 v, uint64_t j) {
+    uint32_t m = mismatches16(v, pattern16<kPat>(j, seed, flip));
     if (m) {
       bad += m;
-      first = umin64(first, i);
+      first = umin64(first, j);
     }
+  };
+  if constexpr (kLayout == 1) {
+    const uint64_t tiles = n16 / kHbmTile;
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+      const uint64_t base = t * kHbmTile + threadIdx.x;
+      u32x4 v[kHbmUnroll];
+#pragma unroll
+      for (int u = 0; u < kHbmUnroll; ++u) v[u] = __builtin_nontemporal_load(&p[base + static_cast<uint64_t>(u) * kHbmThreads]);
+#pragma unroll
+      for (int u = 0; u < kHbmUnroll; ++u) check(v[u], base + static_cast<uint64_t>(u) * kHbmThreads);
+    }
+    for (uint64_t i = tiles * kHbmTile + static_cast<uint64_t>(blockIdx.x) * kHbmThreads + threadIdx.x; i < n16;
+         i += stride)
+      check(__builtin_nontemporal_load(&p[i]), i);
+  } else {
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * kHbmThreads + threadIdx.x;
+    for (; i + (kHbmUnroll - 1) * stride < n16; i += kHbmUnroll * stride) {
+      u32x4 v[kHbmUnroll];
+#pragma unroll
+      for (int u = 0; u < kHbmUnroll; ++u) v[u] = __builtin_nontemporal_load(&p[i + u * stride]);
+#pragma unroll
+      for (int u = 0; u < kHbmUnroll; ++u) check(v[u], i + u * stride);
+    }
+    for (; i < n16; i += stride) check(__builtin_nontemporal_load(&p[i]), i);
   }
   // wave64 reduction
 #pragma unroll
@@ -930,10 +961,13 @@ std::string run_probe(int dev, const char* opts) {
   const int verify_grid = hbm_grid_for("hbmVerifyBlocksPerCU", opt_int(opts, "hbmBlocksPerCU", 3));
   const uint32_t seed = 0xA5A50000u + static_cast<uint32_t>(dev);
   const bool cheap_pattern = opt_int(opts, "hbmPattern", kHbmPattern) == 1;  // in-process A/B
+  const bool tiled = cheap_pattern && opt_int(opts, "hbmLayout", kHbmLayout) == 1;
   PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
   for (int pi = 0; pi < patterns; ++pi) {
     const uint32_t flip = (pi & 1) ? 0xFFFFFFFFu : 0u;  // complementary polarity on odd passes
-    if (cheap_pattern)
+    if (tiled)
+      hipLaunchKernelGGL((hbm_fill<1, 1>), dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip);
+    else if (cheap_pattern)
       hipLaunchKernelGGL(hbm_fill<1>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip);
     else
       hipLaunchKernelGGL(hbm_fill<0>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip);
@@ -941,7 +975,10 @@ std::string run_probe(int dev, const char* opts) {
     if (pi == 0 && inject_flips > 0)
       hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(hbm), n16 * 4,
                          inject_flips);
-    if (cheap_pattern)
+    if (tiled)
+      hipLaunchKernelGGL((hbm_verify<1, 1>), dim3(verify_grid), dim3(kHbmThreads), 0, s, static_cast<const u32x4*>(hbm),
+                         n16, seed, flip, cnt + 2 * pi, cnt + 2 * pi + 1);
+    else if (cheap_pattern)
       hipLaunchKernelGGL(hbm_verify<1>, dim3(verify_grid), dim3(kHbmThreads), 0, s, static_cast<const u32x4*>(hbm), n16,
                          seed, flip, cnt + 2 * pi, cnt + 2 * pi + 1);
     else
