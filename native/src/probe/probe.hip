@@ -91,7 +91,9 @@ __device__ __forceinline__ u32x4 pattern16(uint64_t i16, uint32_t seed, uint32_t
 // MI355X, 9 interleaved rounds (profiles/r3h_probe_pattern_ab.json): 1 GiB test 6.16 -> 6.41 TB/s
 // (write 5.77 -> 6.06, read 6.64 -> 6.76), claim-time probe (beside the MFMA phase) 0.98 -> 0.91 ms.
 constexpr int kHbmPattern = 1;
-constexpr int kHbmLayout = 0;  // see hbm_fill; A/B in scripts/probe_hbm_layout_ab.py
+// Grid-stride (0) measured faster than tiled (1) for the fill (6.03 vs 5.51 TB/s) and within 4 % for
+// the verify: claim-time probe 0.757 vs 0.772 ms (profiles/r4h_probe_hbm_layout_ab_rejected.json).
+constexpr int kHbmLayout = 0;
 
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
