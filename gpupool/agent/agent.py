@@ -19,7 +19,6 @@ import json
 import logging
 import os
 import socket
-import struct
 import threading
 import time
 from uuid import uuid4
