@@ -105,9 +105,18 @@ constexpr int kHbmUnroll = 4;
 // cover one contiguous 16 KiB tile (more row-buffer locality per workgroup).
 constexpr uint64_t kHbmTile = static_cast<uint64_t>(kHbmThreads) * kHbmUnroll;  // 16-B vectors
 
+// Resets the first ``nreset`` result-counter pairs [bad bits = 0, first bad = all-ones] from block
+// 0 on its way (null/0: none), so the claim-time probe enqueues no memsets ahead of its first fill.
+__device__ __forceinline__ void reset_pairs(unsigned long long* __restrict__ cnt, int nreset) {
+  if (blockIdx.x == 0 && static_cast<int>(threadIdx.x) < 2 * nreset)
+    cnt[threadIdx.x] = (threadIdx.x & 1) ? ~0ull : 0ull;
+}
+
 template <int kPat = kHbmPattern, int kLayout = 0>
 __global__ __launch_bounds__(kHbmThreads) void hbm_fill(u32x4* __restrict__ p, uint64_t n16,
-                                                        uint32_t seed, uint32_t flip) {
+                                                        uint32_t seed, uint32_t flip,
+                                                        unsigned long long* __restrict__ reset, int nreset) {
+  reset_pairs(reset, nreset);
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kHbmThreads;
   if constexpr (kLayout == 1) {
     const uint64_t tiles = n16 / kHbmTile;
@@ -199,7 +208,11 @@ __device__ __forceinline__ short small_int_bf16(uint32_t h, int span) {
   return static_cast<short>(__float_as_uint(v) >> 16);
 }
 
-__global__ void gen_operand(short* __restrict__ out, uint64_t n, uint32_t seed, int span) {
+// ``zero``/``nzero``: block 0 also zeroes nzero (<= blockDim.x) counters (the MFMA phase's result
+// slots, so that phase's stream needs no memset and no hand-off from the HBM stream).
+__global__ void gen_operand(short* __restrict__ out, uint64_t n, uint32_t seed, int span,
+                            unsigned long long* __restrict__ zero, int nzero) {
+  if (blockIdx.x == 0 && static_cast<int>(threadIdx.x) < nzero) zero[threadIdx.x] = 0ull;
   uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   for (; i < n; i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
     out[i] = small_int_bf16(pattern_word(i, seed), span);
@@ -637,6 +650,8 @@ constexpr int kSlotSmall = 2 * kMaxPatterns, kSlotAbft = kSlotSmall + 1, kSlotCe
               kSlotCensusMap = kSlotCensusBad + 1, kSlotGemmMap = kSlotCensusMap + kCuMapWords,
               kResSlots = kSlotGemmMap + kCuMapWords;
 constexpr int kCensusIters = 128;
+static_assert(kResSlots - kSlotSmall <= 256, "gen_operand zeroes the MFMA slots from one 256-thread block");
+static_assert(2 * kMaxPatterns <= kHbmThreads, "hbm_fill resets the HBM pairs from one block");
 
 // The HBM sweep buffer is allocated as kSweepChunk pieces, not one ~282 GiB allocation: freeing
 // one huge mapping held the process's address-space lock for ~2.5 s, and every thread of the agent
@@ -756,9 +771,10 @@ std::string hip_uuid(int dev) {
 // Enqueues the whole MFMA phase on stream s (no host sync): (a) a 256^3 GEMM checked element by
 // element against the VALU reference with asymmetric operands, (b) the timed N^3 GEMM (events
 // ctx.gev[0..1]) with exact u32 (mod 2^32) ABFT row/column checksums, then copies the two mismatch
-// counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``.
+// counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``. zero_mfma: the first
+// kernel zeroes the phase's counters cnt[kSlotSmall..kResSlots) itself.
 void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inject_gemm, int census_fault_xcc,
-                       unsigned long long* cnt, unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
+                       bool zero_mfma, unsigned long long* cnt, unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
   const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
   auto align = [](size_t x) { return (x + 4095) & ~static_cast<size_t>(4095); };
   char* p = gbase;
@@ -784,8 +800,9 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inje
   };
   // (a) 256^3 full-element check vs the VALU reference; asymmetric operands
   const uint64_t e0 = static_cast<uint64_t>(n0) * n0;
-  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, a0, e0, 0x1234u, 3);
-  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, b0, e0, 0xBEEFu, 3);
+  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, a0, e0, 0x1234u, 3, zero_mfma ? cnt + kSlotSmall : nullptr,
+                     zero_mfma ? kResSlots - kSlotSmall : 0);
+  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, b0, e0, 0xBEEFu, 3, static_cast<unsigned long long*>(nullptr), 0);
   gemm(a0, b0, c0, static_cast<int>(n0), nullptr);
   hipLaunchKernelGGL(gemm_ref_valu, dim3(n0 / 256, n0), dim3(256), 0, s, a0, b0, r0, static_cast<int>(n0),
                      static_cast<int>(n0), static_cast<int>(n0));
@@ -795,8 +812,8 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inje
 
   // (b) N^3 timed GEMM + exact ABFT checksums
   const uint64_t e = static_cast<uint64_t>(n) * n;
-  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, a, e, 0x51u, 2);
-  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, b, e, 0x77u, 2);
+  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, a, e, 0x51u, 2, static_cast<unsigned long long*>(nullptr), 0);
+  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, b, e, 0x77u, 2, static_cast<unsigned long long*>(nullptr), 0);
   // the 256^3 check above already ran this kernel's code object: time the first launch
   PROBE_CHECK(hipEventRecord(ctx.gev[0], s));
   for (int rep = 0; rep < reps; ++rep) gemm(a, b, c, gemm_n, cnt + kSlotGemmMap);
@@ -921,14 +938,20 @@ std::string run_probe(int dev, const char* opts) {
   auto t_run = std::chrono::steady_clock::now();
 
   // counters: [2p] = flipped bits, [2p+1] = first bad 16-B index (init all-ones) of pattern p,
-  // then the two GEMM check counters. Zeroed on s; s2 waits for that before its first kernel.
-  PROBE_CHECK(hipMemsetAsync(cnt, 0, kResSlots * sizeof(unsigned long long), s));
-  for (int pi = 0; pi < patterns; ++pi)
-    PROBE_CHECK(hipMemsetAsync(cnt + 2 * pi + 1, 0xFF, sizeof(unsigned long long), s));
+  // then the MFMA phase's counters. zeroInKernel (default): the first fill resets the HBM pairs and
+  // the MFMA phase's first kernel its own slots, so neither stream starts behind memsets or waits
+  // on the other — after an idle gap each API call ahead of the first fill costs tens of us
+  // (profiles/r4i_probe_idle_gap_ab.json). 0: memsets on s, s2 waits for them (the older path).
+  const bool zero_in_kernel = opt_int(opts, "zeroInKernel", 1) != 0;
   hipStream_t s2 = overlap ? ctx.stream2 : s;
-  if (overlap) {
-    PROBE_CHECK(hipEventRecord(ctx.gev[2], s));
-    PROBE_CHECK(hipStreamWaitEvent(s2, ctx.gev[2], 0));
+  if (!zero_in_kernel) {
+    PROBE_CHECK(hipMemsetAsync(cnt, 0, kResSlots * sizeof(unsigned long long), s));
+    for (int pi = 0; pi < patterns; ++pi)
+      PROBE_CHECK(hipMemsetAsync(cnt + 2 * pi + 1, 0xFF, sizeof(unsigned long long), s));
+    if (overlap) {
+      PROBE_CHECK(hipEventRecord(ctx.gev[2], s));
+      PROBE_CHECK(hipStreamWaitEvent(s2, ctx.gev[2], 0));
+    }
   }
 
   // ---------------- MFMA phase (launched first so it starts beside the HBM fill)
@@ -945,9 +968,12 @@ std::string run_probe(int dev, const char* opts) {
   // patterns); the MFMA phase (~0.1 ms of GPU time beside it) costs ~20 API calls to enqueue. With
   // hbmFirst (default) the HBM kernels are enqueued first, so the fill starts ~20 launches earlier
   // and the MFMA phase is enqueued while it runs (profiles/r4e_probe_launch_order_ab.json).
-  const bool hbm_first = opt_int(opts, "hbmFirst", 1) != 0;
-  if (do_mfma && !hbm_first)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, cnt, hres, ctx, s2);
+  // hbmFirst=2: the MFMA phase is enqueued right after the first fill (in-process A/B), so it starts
+  // earlier on the GPU while the rest of the HBM test is still enqueued well ahead of need.
+  const int hbm_first = static_cast<int>(opt_int(opts, "hbmFirst", 1));
+  if (do_mfma && hbm_first == 0)
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
+                      ctx, s2);
 
   // ---------------- HBM: all patterns back to back, per-pattern counters
   auto* hbm = reinterpret_cast<u32x4*>(base);
@@ -967,13 +993,18 @@ std::string run_probe(int dev, const char* opts) {
   PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
   for (int pi = 0; pi < patterns; ++pi) {
     const uint32_t flip = (pi & 1) ? 0xFFFFFFFFu : 0u;  // complementary polarity on odd passes
+    unsigned long long* reset = zero_in_kernel && pi == 0 ? cnt : nullptr;
+    const int nreset = reset ? patterns : 0;
     if (tiled)
-      hipLaunchKernelGGL((hbm_fill<1, 1>), dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip);
+      hipLaunchKernelGGL((hbm_fill<1, 1>), dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip, reset, nreset);
     else if (cheap_pattern)
-      hipLaunchKernelGGL(hbm_fill<1>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip);
+      hipLaunchKernelGGL(hbm_fill<1>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip, reset, nreset);
     else
-      hipLaunchKernelGGL(hbm_fill<0>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip);
+      hipLaunchKernelGGL(hbm_fill<0>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip, reset, nreset);
     PROBE_CHECK(hipEventRecord(ctx.ev[1 + 2 * pi], s));
+    if (pi == 0 && do_mfma && hbm_first == 2)
+      launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
+                        ctx, s2);
     if (pi == 0 && inject_flips > 0)
       hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(hbm), n16 * 4,
                          inject_flips);
@@ -990,8 +1021,9 @@ std::string run_probe(int dev, const char* opts) {
   }
   PROBE_CHECK(hipGetLastError());
   PROBE_CHECK(hipMemcpyAsync(hres, cnt, 2 * patterns * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-  if (do_mfma && hbm_first)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, cnt, hres, ctx, s2);
+  if (do_mfma && hbm_first == 1)
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
+                      ctx, s2);
   const double launch_ms = ms_since(t_run);  // host time to enqueue the whole probe
   PROBE_CHECK(hipStreamSynchronize(s));
   const double hbm_wall_ms = ms_since(t_run);
@@ -1068,7 +1100,7 @@ std::string run_probe(int dev, const char* opts) {
   out += ",\"ms\":" + jnum(total_ms);
   out += ",\"phases\":{\"arenaReused\":" + std::string(reused ? "true" : "false") +
          ",\"setupMs\":" + jnum(setup_ms) + ",\"allocMs\":" + jnum(alloc_ms) + ",\"launchMs\":" + jnum(launch_ms) +
-         ",\"hbmFirst\":" + (hbm_first ? "true" : "false") +
+         ",\"hbmFirst\":" + std::to_string(hbm_first) +
          ",\"hbmWallMs\":" + jnum(hbm_wall_ms) + ",\"mfmaWallMs\":" + jnum(mfma_wall_ms) + ",\"freeMs\":" + jnum(free_ms) +
          "}";
   out += "}";
@@ -1108,7 +1140,8 @@ std::string run_peer(int src, int dst, const char* opts) {
   // src: write the pattern
   PROBE_CHECK(hipSetDevice(src));
   const int sgrid = std::min<int>(cs.prop.multiProcessorCount, static_cast<int>((n16 + kHbmThreads - 1) / kHbmThreads));
-  hipLaunchKernelGGL(hbm_fill<>, dim3(sgrid), dim3(kHbmThreads), 0, cs.stream, static_cast<u32x4*>(sbuf.p), n16, seed, 0u);
+  hipLaunchKernelGGL(hbm_fill<>, dim3(sgrid), dim3(kHbmThreads), 0, cs.stream, static_cast<u32x4*>(sbuf.p), n16, seed, 0u,
+                     static_cast<unsigned long long*>(nullptr), 0);
   PROBE_CHECK(hipGetLastError());
   // the copy over the peer link, timed on src's stream
   PROBE_CHECK(hipEventRecord(cs.gev[0], cs.stream));
@@ -1197,7 +1230,7 @@ std::string run_peer_ring(const std::vector<int>& devs, const char* opts) {
     PROBE_CHECK(hipSetDevice(d));
     const int grid = std::min<int>(c.prop.multiProcessorCount, static_cast<int>((n16 + kHbmThreads - 1) / kHbmThreads));
     hipLaunchKernelGGL(hbm_fill<>, dim3(grid), dim3(kHbmThreads), 0, c.stream, static_cast<u32x4*>(c.peer_send), n16,
-                       seed_of(d), 0u);
+                       seed_of(d), 0u, static_cast<unsigned long long*>(nullptr), 0);
     PROBE_CHECK(hipGetLastError());
     PROBE_CHECK(hipStreamSynchronize(c.stream));  // the fill is ~10 us; copies below must see it
   }
@@ -1342,7 +1375,8 @@ std::string run_sweep(int dev, const char* opts) {
     PROBE_CHECK(hipEventRecord(ctx.ev[0], s));
     for (int pi = 0; pi < 2; ++pi) {
       const uint32_t flip = pi ? 0xFFFFFFFFu : 0u;
-      hipLaunchKernelGGL(hbm_fill<>, dim3(fill_grid), dim3(kHbmThreads), 0, s, win, n16, seed, flip);
+      hipLaunchKernelGGL(hbm_fill<>, dim3(fill_grid), dim3(kHbmThreads), 0, s, win, n16, seed, flip,
+                         static_cast<unsigned long long*>(nullptr), 0);
       if (pi == 0 && inject_flips > 0 && pos == offset)
         hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(win), n16 * 4,
                            inject_flips);

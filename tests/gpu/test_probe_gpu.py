@@ -169,6 +169,23 @@ def test_overlapped_and_serial_probe_agree(hip):
         assert bad["hbm"]["badBits"] == 5 and bad["mfma"]["abftMismatches"] == 2
 
 
+@pytest.mark.parametrize("zero_in_kernel", [1, 0])
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_counters_reset_after_a_faulty_probe(hip, overlap, zero_in_kernel):
+    """The result counters live in the kept arena: a clean probe right after a faulty one must
+    start from zero (and the first-bad offset from all-ones) on both reset paths — in-kernel
+    (the first fill / operand kernel, default) and memsets."""
+    kw = dict(hbm_bytes=256 << 20, gemm_n=1024, overlap=overlap, zeroInKernel=zero_in_kernel)
+    bad = hip.run(0, injectBitFlips=7, injectGemmFault=1, injectCensusFaultXcc=3, **kw)
+    assert not bad["passed"] and bad["hbm"]["badBits"] == 7 and bad["mfma"]["abftMismatches"] == 2
+    assert bad["hbm"]["firstBadOffset"] is not None and bad["cus"]["badWaves"] > 0
+    clean = hip.run(0, **kw)
+    assert clean["passed"], clean
+    assert clean["hbm"]["badBits"] == 0 and clean["hbm"]["firstBadOffset"] is None
+    assert clean["mfma"]["abftMismatches"] == 0 and clean["mfma"]["elementMismatches"] == 0
+    assert clean["cus"]["badWaves"] == 0 and clean["cus"]["ok"]
+
+
 def test_peer_copy_path(hip):
     """The xGMI peer check's copy + bit-exact verify path. On a 1-GPU box src == dst exercises
     it as a local device copy; with more GPUs visible, 0 -> 1 goes over an xGMI link."""
