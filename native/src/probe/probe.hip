@@ -208,11 +208,13 @@ __device__ __forceinline__ short small_int_bf16(uint32_t h, int span) {
   return static_cast<short>(__float_as_uint(v) >> 16);
 }
 
-// ``zero``/``nzero``: block 0 also zeroes nzero (<= blockDim.x) counters (the MFMA phase's result
-// slots, so that phase's stream needs no memset and no hand-off from the HBM stream).
+// ``zero``/``nzero``: the grid also zeroes nzero words (the MFMA phase's result slots, its ABFT
+// accumulators), so that phase's stream needs no memsets and no hand-off from the HBM stream.
 __global__ void gen_operand(short* __restrict__ out, uint64_t n, uint32_t seed, int span,
-                            unsigned long long* __restrict__ zero, int nzero) {
-  if (blockIdx.x == 0 && static_cast<int>(threadIdx.x) < nzero) zero[threadIdx.x] = 0ull;
+                            uint32_t* __restrict__ zero, uint64_t nzero) {
+  for (uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; j < nzero;
+       j += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    zero[j] = 0u;
   uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   for (; i < n; i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
     out[i] = small_int_bf16(pattern_word(i, seed), span);
@@ -650,7 +652,6 @@ constexpr int kSlotSmall = 2 * kMaxPatterns, kSlotAbft = kSlotSmall + 1, kSlotCe
               kSlotCensusMap = kSlotCensusBad + 1, kSlotGemmMap = kSlotCensusMap + kCuMapWords,
               kResSlots = kSlotGemmMap + kCuMapWords;
 constexpr int kCensusIters = 128;
-static_assert(kResSlots - kSlotSmall <= 256, "gen_operand zeroes the MFMA slots from one 256-thread block");
 static_assert(2 * kMaxPatterns <= kHbmThreads, "hbm_fill resets the HBM pairs from one block");
 
 // The HBM sweep buffer is allocated as kSweepChunk pieces, not one ~282 GiB allocation: freeing
@@ -694,6 +695,7 @@ struct DeviceCtx {
   uint64_t peer_bytes = 0;
   unsigned long long* peer_cnt = nullptr;
   std::chrono::steady_clock::time_point peer_used{};
+  std::string uuid;  // hip_uuid(), cached: the runtime query is not free on a cold CPU
   bool ready = false;
 };
 
@@ -771,8 +773,8 @@ std::string hip_uuid(int dev) {
 // Enqueues the whole MFMA phase on stream s (no host sync): (a) a 256^3 GEMM checked element by
 // element against the VALU reference with asymmetric operands, (b) the timed N^3 GEMM (events
 // ctx.gev[0..1]) with exact u32 (mod 2^32) ABFT row/column checksums, then copies the two mismatch
-// counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``. zero_mfma: the first
-// kernel zeroes the phase's counters cnt[kSlotSmall..kResSlots) itself.
+// counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``. zero_mfma: the operand
+// kernels zero the phase's counters cnt[kSlotSmall..kResSlots) and ABFT accumulators themselves.
 void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inject_gemm, int census_fault_xcc,
                        bool zero_mfma, unsigned long long* cnt, unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
   const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
@@ -800,9 +802,10 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inje
   };
   // (a) 256^3 full-element check vs the VALU reference; asymmetric operands
   const uint64_t e0 = static_cast<uint64_t>(n0) * n0;
-  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, a0, e0, 0x1234u, 3, zero_mfma ? cnt + kSlotSmall : nullptr,
-                     zero_mfma ? kResSlots - kSlotSmall : 0);
-  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, b0, e0, 0xBEEFu, 3, static_cast<unsigned long long*>(nullptr), 0);
+  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, a0, e0, 0x1234u, 3,
+                     zero_mfma ? reinterpret_cast<uint32_t*>(cnt + kSlotSmall) : nullptr,
+                     zero_mfma ? static_cast<uint64_t>(kResSlots - kSlotSmall) * 2 : 0);
+  hipLaunchKernelGGL(gen_operand, dim3(256), dim3(256), 0, s, b0, e0, 0xBEEFu, 3, static_cast<uint32_t*>(nullptr), 0);
   gemm(a0, b0, c0, static_cast<int>(n0), nullptr);
   hipLaunchKernelGGL(gemm_ref_valu, dim3(n0 / 256, n0), dim3(256), 0, s, a0, b0, r0, static_cast<int>(n0),
                      static_cast<int>(n0), static_cast<int>(n0));
@@ -812,8 +815,12 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inje
 
   // (b) N^3 timed GEMM + exact ABFT checksums
   const uint64_t e = static_cast<uint64_t>(n) * n;
-  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, a, e, 0x51u, 2, static_cast<unsigned long long*>(nullptr), 0);
-  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, b, e, 0x77u, 2, static_cast<unsigned long long*>(nullptr), 0);
+  // ABFT checksums: 6 uint32 vectors [acol | bcol | colsumC | expCol | rowsumC | expRow]; the first
+  // three accumulate atomically and start from zero (zeroed by the operand kernel, or a memset)
+  uint32_t* v32 = reinterpret_cast<uint32_t*>(v);
+  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, a, e, 0x51u, 2, zero_mfma ? v32 : nullptr,
+                     zero_mfma ? 3 * n : 0);
+  hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, b, e, 0x77u, 2, static_cast<uint32_t*>(nullptr), 0);
   // the 256^3 check above already ran this kernel's code object: time the first launch
   PROBE_CHECK(hipEventRecord(ctx.gev[0], s));
   for (int rep = 0; rep < reps; ++rep) gemm(a, b, c, gemm_n, cnt + kSlotGemmMap);
@@ -822,11 +829,9 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inje
   if (inject_gemm)
     hipLaunchKernelGGL(inject_gemm_fault, dim3(1), dim3(1), 0, s, c, static_cast<int64_t>(gemm_n / 3) * gemm_n + gemm_n / 5,
                        inject_gemm);
-  // ABFT checksums: 6 uint32 vectors [acol | bcol | colsumC | expCol | rowsumC | expRow]
-  uint32_t* v32 = reinterpret_cast<uint32_t*>(v);
   uint32_t *vacol = v32, *vbcol = v32 + n, *vcolC = v32 + 2 * n, *vexpC = v32 + 3 * n, *vrowC = v32 + 4 * n,
            *vexpR = v32 + 5 * n;
-  PROBE_CHECK(hipMemsetAsync(v32, 0, 3 * n * sizeof(uint32_t), s));
+  if (!zero_mfma) PROBE_CHECK(hipMemsetAsync(v32, 0, 3 * n * sizeof(uint32_t), s));
   const int rows_y = (gemm_n + kColRows - 1) / kColRows;
   const dim3 cgrid_h((gemm_n + 511) / 512, rows_y), cgrid_f((gemm_n + 255) / 256, rows_y);
   const float bound = static_cast<float>(gemm_n) * 4.0f;  // |C| <= K * span^2, span 2
@@ -891,6 +896,7 @@ std::string run_probe(int dev, const char* opts) {
     PROBE_CHECK(hipGetDeviceProperties(&ctx.prop, dev));
     // pinned result slots: device->host copies of the counters are truly async (one sync per phase)
     PROBE_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ctx.host_res), kResSlots * sizeof(unsigned long long)));
+    ctx.uuid = hip_uuid(dev);
     ctx.ready = true;
   }
   hipStream_t s = ctx.stream;
@@ -1069,9 +1075,10 @@ std::string run_probe(int dev, const char* opts) {
   }
   const double free_ms = ms_since(t_free);
   double total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const auto t_report = std::chrono::steady_clock::now();
   std::string out = "{";
   out += "\"device\":" + std::to_string(dev);
-  out += ",\"hipUUID\":" + jstr(hip_uuid(dev));
+  out += ",\"hipUUID\":" + jstr(ctx.uuid);
   out += ",\"gcnArch\":" + jstr(prop.gcnArchName);
   out += ",\"passed\":" + std::string(hbm_ok && mfma_ok ? "true" : "false");
   out += ",\"hbm\":{\"ok\":" + std::string(hbm_ok ? "true" : "false") + ",\"bytes\":" + std::to_string(n16 * 16) +
@@ -1103,7 +1110,8 @@ std::string run_probe(int dev, const char* opts) {
          ",\"hbmFirst\":" + std::to_string(hbm_first) +
          ",\"hbmWallMs\":" + jnum(hbm_wall_ms) + ",\"mfmaWallMs\":" + jnum(mfma_wall_ms) + ",\"freeMs\":" + jnum(free_ms) +
          "}";
-  out += "}";
+  // host time spent building this report after the clock above stopped (timing of the binding)
+  out += ",\"reportMs\":" + jnum(ms_since(t_report)) + "}";
   return out;
 }
 

@@ -13,6 +13,7 @@ hbmFirst 1 (MFMA phase enqueued after the whole HBM test) vs 2 (after the first 
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import statistics
@@ -32,6 +33,23 @@ variants = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in v.split(","
             for v in (a.variant or ["zeroInKernel=1", "zeroInKernel=0"])]
 names = [",".join(f"{k}={v}" for k, v in o.items()) for o in variants]
 probe.init()
+
+
+def timed_run(dev: int, hbm_bytes: int, gemm_n: int, **o: int) -> dict:
+    """probe.run's steps (options JSON, the ctypes call, the reply JSON), each timed."""
+    t0 = time.perf_counter()
+    arg = json.dumps({"hbmBytes": hbm_bytes, "mfma": True, "gemmN": gemm_n, "patterns": 2,
+                      "gemmReps": 1, "gemmTile": 256, **o}).encode()
+    t1 = time.perf_counter()
+    p = probe.lib().mi355x_probe_run(dev, arg)
+    t2 = time.perf_counter()
+    r = json.loads(ctypes.string_at(p).decode())
+    probe.lib().mi355x_probe_free(p)
+    t3 = time.perf_counter()
+    r["py"] = {"argMs": (t1 - t0) * 1e3, "callMs": (t2 - t1) * 1e3, "replyMs": (t3 - t2) * 1e3,
+               "pyMs": (t3 - t0) * 1e3}
+    return r
+
 opts = dict(hbm_bytes=1 << 30, gemm_n=2048, overlap=1)
 for o in variants:
     assert probe.run(0, **opts, **o)["passed"]
@@ -39,13 +57,13 @@ res: dict[str, list[dict]] = {}
 for i in range(a.rounds):
     vi = (i + i // len(variants)) % len(variants)
     time.sleep(a.gap)
-    r = probe.run(0, **opts, **variants[vi])   # first probe after the idle gap
-    w = probe.run(0, **opts, **variants[vi])   # the next one, back to back
+    r = timed_run(0, 1 << 30, 2048, overlap=1, **variants[vi])   # first probe after the idle gap
+    w = timed_run(0, 1 << 30, 2048, overlap=1, **variants[vi])   # the next one, back to back
     for k, x in ((f"afterIdle {names[vi]}", r), (f"warm {names[vi]}", w)):
         assert x["passed"] and x["cus"]["ok"], x
         ph = x["phases"]
         res.setdefault(k, []).append({
-            "ms": x["ms"], "hbmKernelMs": x["hbm"]["ms"], "writeGBps": x["hbm"]["writeGBps"],
+            "ms": x["ms"], **x["py"], "reportMs": x.get("reportMs", 0.0), "hbmKernelMs": x["hbm"]["ms"], "writeGBps": x["hbm"]["writeGBps"],
             "readGBps": x["hbm"]["readGBps"], "launchMs": ph["launchMs"], "setupMs": ph["setupMs"],
             "allocMs": ph["allocMs"], "hbmWallMs": ph["hbmWallMs"], "mfmaWallMs": ph["mfmaWallMs"],
             "arenaReused": ph["arenaReused"]})
