@@ -179,17 +179,12 @@ class Agent:
         self.dev = devlib.DeviceLib(cfg.backend, **dev_cfg)
         self.ledger = Ledger(cfg.state_dir, fsync=cfg.fsync)
         self.records: dict[str, dict] = self.ledger.load()
-        # A claim commits 'Probing' before its probe runs; an agent that died mid-probe leaves such
-        # records behind. Nothing would ever finish them, so they become failed probes and take
-        # the normal replace path (drain -> release -> quarantine -> claim a healthy spare).
+        # A claim commits 'Probing' before its probe runs, and Probing -> Claimed reaches the disk
+        # through the ledger's background writer after the reply: an agent killed in between
+        # leaves such records behind. Nothing would ever finish them, so they are probed again
+        # once the prober is up (_reprobe_interrupted): a GPU that passes stays with its pool, one
+        # that fails takes the normal replace path (drain -> release -> quarantine -> spare).
         interrupted = [u for u, r in self.records.items() if r.get("state") == "Probing"]
-        for u in interrupted:
-            self.records[u]["state"] = "Claimed"
-            self.records[u]["probe"] = {"passed": False, "backend": "none", "ms": 0.0,
-                                        "error": "ProbeInterrupted: the agent restarted during "
-                                                 "the claim-time probe"}
-        if interrupted:
-            self.ledger.commit(self.records)
         self.share_lib_dir = self._install_share_lib()
         self._pod_ids: tuple[float, set[str]] | None = None  # (listed at, device IDs pods hold)
         self._over_budget: set[tuple[str, str, str]] = set()  # (gpu, ns, pod) over their slot budget
@@ -249,6 +244,7 @@ class Agent:
         self.scrubber = HbmScrubber(self, cfg.scrub_interval_s, cfg.scrub_window_bytes,
                                     cfg.scrub_windows, cfg.scrub_reserve_bytes,
                                     cfg.scrub_start_delay_s)
+        self._reprobe_interrupted(interrupted)
         self._evaluate_all()
         from .preflight import check as preflight_check
         self.preflight = preflight_check(self.snap, fake=self.backend == "fake")
@@ -258,6 +254,41 @@ class Agent:
         log.info("agent %s: backend=%s devices=%d probe=%s (init %.0f ms) ledger=%d claims",
                  cfg.node, self.backend, len(self.by_uuid), self.probe_mode, self.prober.init_ms,
                  len(self.records))
+
+    def _reprobe_interrupted(self, uuids: list[str]) -> None:
+        """Finish the claims a previous agent process left in 'Probing' (see __init__) by running
+        their claim-time probe again, before the RPC server starts. Failing them outright made a
+        kill in the few ms between the claim's reply and the background ledger write replace a
+        healthy GPU — and drain whatever its pool had started on it meanwhile. The probe is the
+        same ~1 ms test a claim runs; if a pod already holds most of the GPU's HBM the probe's
+        allocation fails and the GPU is replaced, as before."""
+        if not uuids:
+            return
+        for u in uuids:
+            rec = self.records[u]
+            d = self.by_uuid.get(u)
+            opts = (rec.get("policy") or {}).get("probe") or {}
+            if d is None:
+                res = {"passed": False, "backend": "none", "ms": 0.0,
+                       "error": "ProbeInterrupted: the agent restarted during the claim-time "
+                                "probe and the GPU is no longer visible"}
+            else:
+                res = self.prober.probe_many([d], {**opts, "enabled": opts.get("enabled", True)})[0]
+                res["rerunAtStart"] = True
+                if not res.get("passed"):
+                    res["error"] = "ProbeInterrupted, re-run at agent start: " + \
+                        str(res.get("error") or "probe failed")
+            rec["state"] = "Claimed"
+            rec["probe"] = res
+            self.last_probe[u] = res
+            self._probe_mono[u] = time.monotonic()
+            self.stats["probes"] += 1
+            self.stats["probe_ms_sum"] += float(res.get("ms", 0.0))
+            if not res.get("passed"):
+                self.stats["probe_failures"] += 1
+        self.ledger.commit(self.records)
+        log.warning("re-probed %d GPU(s) whose claim-time probe a restart interrupted: %s", len(uuids),
+                    {u: bool(self.records[u]["probe"].get("passed")) for u in uuids})
 
     # ================================================================ health
     def _policy_for(self, uuid: str) -> dict:
@@ -1163,8 +1194,8 @@ class Agent:
 
         def record_claimed() -> None:
             # Probing -> Claimed (with the probe result) goes to the ledger's background writer
-            # after the reply: a crash may lose it safely (restart -> ProbeInterrupted -> the
-            # pool replaces the GPU); the claim itself was made durable above
+            # after the reply: a crash may lose it safely (a restarted agent probes the GPU
+            # again, _reprobe_interrupted); the claim itself was made durable above
             with self.lock:
                 self.ledger.commit(self.records, durable=False)
         return {"ok": True, "probeWallMs": probe_wall, "timingsMs": timings, "_t_phase": t_phase,

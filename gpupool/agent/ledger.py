@@ -120,8 +120,8 @@ class Ledger:
         """Record the full claim map; returns its sequence number. ``durable``: written and
         fsync'ed before returning (one write per agent operation, atomically replaced). Otherwise
         the write is left to a background writer (coalesced) — for transitions a crash may lose
-        safely, e.g. Probing -> Claimed: a restarted agent turns a 'Probing' record into a failed
-        probe (ProbeInterrupted) and the pool replaces the GPU — or made durable later by
+        safely, e.g. Probing -> Claimed: a restarted agent probes a 'Probing' record's GPU again
+        (kept if it passes, replaced by its pool if not) — or made durable later by
         ``flush(seq)``. With ``lock`` (the caller's lock guarding ``claims``; not durable) the map
         is serialised by the writer too, under that lock: a claim hands its record over and probes
         while the writer encodes and fsyncs it."""

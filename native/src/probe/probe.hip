@@ -1076,8 +1076,9 @@ std::string run_probe(int dev, const char* opts) {
   const double free_ms = ms_since(t_free);
   double total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   const auto t_report = std::chrono::steady_clock::now();
-  std::string out = "{";
-  out += "\"device\":" + std::to_string(dev);
+  std::string out;
+  out.reserve(2048);  // one allocation for the whole report
+  out += "{\"device\":" + std::to_string(dev);
   out += ",\"hipUUID\":" + jstr(ctx.uuid);
   out += ",\"gcnArch\":" + jstr(prop.gcnArchName);
   out += ",\"passed\":" + std::string(hbm_ok && mfma_ok ? "true" : "false");

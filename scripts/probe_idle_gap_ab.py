@@ -38,8 +38,7 @@ probe.init()
 def timed_run(dev: int, hbm_bytes: int, gemm_n: int, **o: int) -> dict:
     """probe.run's steps (options JSON, the ctypes call, the reply JSON), each timed."""
     t0 = time.perf_counter()
-    arg = json.dumps({"hbmBytes": hbm_bytes, "mfma": True, "gemmN": gemm_n, "patterns": 2,
-                      "gemmReps": 1, "gemmTile": 256, **o}).encode()
+    arg = probe._run_opts(hbm_bytes, True, gemm_n, 2, 1, 256, tuple(sorted(o.items())))
     t1 = time.perf_counter()
     p = probe.lib().mi355x_probe_run(dev, arg)
     t2 = time.perf_counter()

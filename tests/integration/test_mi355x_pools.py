@@ -210,16 +210,11 @@ def test_agent_restart_keeps_ledger(node8):
         {d["uuid"] for d in before["status"]["devices"]}
 
 
-def test_agent_crash_mid_probe_is_replaced(node8):
-    """A claim is committed as 'Probing' before the probe runs; an agent killed between the two
-    ledger commits must not leave the pool stuck Progressing=Probing forever: on restart the record
-    becomes a failed probe (ProbeInterrupted) and the pool replaces that GPU."""
+def _interrupt_probe(node8, victim: str) -> None:
+    """Kill the agent and leave ``victim``'s record in 'Probing', as a kill between the claim's
+    reply and the ledger's background write of Probing -> Claimed does."""
     import json
     import os
-    k = node8.client
-    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
-    before = wait_ready(k, "p", 2)
-    victim = before["status"]["devices"][1]["uuid"]
     node8._kill("agent-mi355x-node-0")
     path = os.path.join(node8.workdir, "state-mi355x-node-0", "ledger.json")
     with open(path) as f:
@@ -227,13 +222,44 @@ def test_agent_crash_mid_probe_is_replaced(node8):
     doc["claims"][victim].update({"state": "Probing", "probe": None})
     with open(path, "w") as f:
         json.dump(doc, f)
+
+
+def test_agent_crash_mid_probe_reprobes_and_keeps_a_healthy_gpu(node8):
+    """A claim is committed as 'Probing' before the probe runs; an agent killed before the
+    Claimed state reached the disk must neither leave the pool stuck Progressing=Probing nor
+    replace a healthy GPU: the restarted agent runs the probe again and the GPU stays."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    before = wait_ready(k, "p", 2)
+    uuids = {d["uuid"] for d in before["status"]["devices"]}
+    victim = before["status"]["devices"][1]["uuid"]
+    _interrupt_probe(node8, victim)
+    node8.start_agent(node8.nodes[0])
+    d = next(x for x in agent_view(node8)["devices"] if x["uuid"] == victim)
+    assert d["state"] == "Claimed" and d["probe"]["passed"] and d["probe"]["rerunAtStart"], d
+    after = wait_ready(k, "p", 2, timeout=30)
+    assert {x["uuid"] for x in after["status"]["devices"]} == uuids
+
+
+def test_agent_crash_mid_probe_replaces_a_gpu_that_fails_the_rerun(node8):
+    """Same interrupted claim, but the GPU fails the probe the restarted agent runs: the record
+    becomes a failed probe (ProbeInterrupted) and the pool replaces that GPU."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    before = wait_ready(k, "p", 2)
+    victim = before["status"]["devices"][1]
+    _interrupt_probe(node8, victim["uuid"])
+    node8.set_faults("mi355x-node-0", {"devices": {str(victim["index"]): {"probeFail": True}}},
+                     sample=False)
     node8.start_agent(node8.nodes[0])
 
     def replaced(o):
-        return ready_at(2)(o) and victim not in {d["uuid"] for d in o["status"]["devices"]}
+        return ready_at(2)(o) and victim["uuid"] not in {d["uuid"] for d in o["status"]["devices"]}
     k.wait_for(MI355XPOOLS, "p", "default", replaced, timeout=30)
-    d = next(x for x in agent_view(node8)["devices"] if x["uuid"] == victim)
+    d = next(x for x in agent_view(node8)["devices"] if x["uuid"] == victim["uuid"])
     assert d["state"] == "Quarantined" and "probe failed" in d["quarantine"]["reason"]
+    msgs = " ".join(e.get("message", "") for e in settled_events(k))
+    assert "ProbeInterrupted, re-run at agent start" in msgs, msgs
 
 
 def _deleting(k, name):
