@@ -341,12 +341,14 @@ class ApiServerSim:
                 return web.json_response(to_table(rt, [obj], obj["metadata"]["resourceVersion"]))
             return web.json_response(obj)
         if m == "PUT":
-            return web.json_response(self.store.update(rt, ns, name, await request.json(), sub, dry))
+            # the decoded body is this request's own; the reply only serialises the result
+            return web.json_response(self.store.update(rt, ns, name, await request.json(), sub, dry,
+                                                       owned=True, copy_out=False))
         if m == "PATCH":
             ctype = request.headers.get("Content-Type", "")
             ptype = "json" if "json-patch" in ctype else "merge"
             return web.json_response(self.store.patch(rt, ns, name, await request.json(), ptype,
-                                                      sub, dry))
+                                                      sub, dry, copy_out=False))
         if m == "DELETE" and not sub:
             body = {}
             if request.can_read_body:

@@ -636,7 +636,12 @@ class Store:
         return clone(obj)
 
     def update(self, rt: ResourceType, ns: str | None, name: str, obj: dict,
-               subresource: str = "", dry_run: bool = False, owned: bool = False) -> dict:
+               subresource: str = "", dry_run: bool = False, owned: bool = False,
+               copy_out: bool = True) -> dict:
+        """``owned``: ``obj`` is the caller's private copy (a freshly decoded request body, a
+        patch result) and is stored as is. ``copy_out=False``: the stored object itself is
+        returned, for a caller that only serialises it before yielding (the HTTP front-end):
+        two full-object copies less per write, ~0.1 ms for an 8-GPU pool's status."""
         ns = self._check_ns(rt, ns) if rt.namespaced else ""
         cur = self.objects[rt.key].get((ns, name))
         if cur is None:
@@ -690,7 +695,7 @@ class Store:
         if dry_run:
             return new
         if new == cur:  # no-op update: no new resourceVersion, no event (apiserver behaviour)
-            return clone(cur)
+            return clone(cur) if copy_out else cur
         nmd = new["metadata"]
         if _spec_part(new) != _spec_part(cur):
             nmd["generation"] = int(cmd.get("generation", 1)) + 1
@@ -699,15 +704,15 @@ class Store:
         nmd["resourceVersion"] = str(self._next_rv())
         if nmd.get("deletionTimestamp") and not nmd.get("finalizers") and rt.kind != "Pod":
             self._remove(rt, ns, name, new)
-            return clone(new)
+            return clone(new) if copy_out else new
         self.objects[rt.key][(ns, name)] = new
         if rt.kind == "CustomResourceDefinition":
             self._register_crd(new)
         self._emit(rt, "MODIFIED", new)
-        return clone(new)
+        return clone(new) if copy_out else new
 
     def patch(self, rt: ResourceType, ns: str | None, name: str, patch: Any, ptype: str,
-              subresource: str = "", dry_run: bool = False) -> dict:
+              subresource: str = "", dry_run: bool = False, copy_out: bool = True) -> dict:
         nsk = self._check_ns(rt, ns) if rt.namespaced else ""
         cur = self.objects[rt.key].get((nsk, name))
         if cur is None:
@@ -719,7 +724,7 @@ class Store:
             new = merge_patch(cur, patch)
         if not (isinstance(patch, dict) and patch.get("metadata", {}).get("resourceVersion")):
             new.setdefault("metadata", {})["resourceVersion"] = cur["metadata"]["resourceVersion"]
-        return self.update(rt, ns, name, new, subresource, dry_run, owned=True)
+        return self.update(rt, ns, name, new, subresource, dry_run, owned=True, copy_out=copy_out)
 
     def delete(self, rt: ResourceType, ns: str | None, name: str, grace: int | None = None,
                preconditions: dict | None = None, dry_run: bool = False) -> dict:

@@ -301,3 +301,23 @@ def test_old_watch_events_are_compacted_but_still_served():
     assert evs[0]._obj is None and evs[-1]._obj is not None
     assert [e.obj["data"]["i"] for e in evs] == [str(i) for i in range(n)]
     assert sum(1 for e in st.log if e._obj is not None) == Store.LIVE_EVENTS
+
+
+def test_update_copy_semantics(store):
+    """The store never shares its objects with a caller unless asked: default writes copy the
+    body in and the result out; the HTTP front-end (owned body, copy_out=False) gets the stored
+    object for serialisation, and the watch event keeps its own copy either way."""
+    rt = mi(store)
+    store.create(rt, "default", pool("a"))
+    body = store.get(rt, "default", "a")
+    body["status"] = {"readyReplicas": 0}
+    out = store.update(rt, "default", "a", body, "status")
+    body["status"]["readyReplicas"] = 5
+    out["status"]["readyReplicas"] = 6
+    assert store.get(rt, "default", "a")["status"]["readyReplicas"] == 0
+    body = store.get(rt, "default", "a")
+    body["status"] = {"readyReplicas": 1}
+    out = store.update(rt, "default", "a", body, "status", owned=True, copy_out=False)
+    assert out is store.objects[rt.key][("default", "a")] and out["status"] is body["status"]
+    ev = store.log[-1]
+    assert ev.obj is not out and ev.obj == out
