@@ -1,0 +1,72 @@
+"""Agent crashes at random points of a pool's life (SIGKILL mid-claim, mid-release, idle) against
+the 8x MI355X fake node. After every step the pool must converge to its spec with no GPU lost,
+doubly owned or quarantined: nothing here is faulty, so a quarantine would mean a crash was taken
+for a hardware failure (the claim-time probe a kill interrupted is re-run, not failed)."""
+from __future__ import annotations
+
+import random
+import signal
+import time
+
+import pytest
+
+from gpupool.kube import MI355XPOOLS
+
+from .helpers import mi_pool, wait_ready
+
+pytestmark = pytest.mark.slow
+
+NODE = "mi355x-node-0"
+
+
+def _view(c):
+    return c.agent_request(NODE, "GET", "/v1/node")
+
+
+def _converged(c, uid: str, r: int, timeout: float = 30.0) -> dict:
+    """The pool Ready at r with exactly its r GPUs claimed on the agent (a lost claim reply may
+    leave extra claims for a pass or two: the manager adopts or releases them)."""
+    k = c.client
+    deadline = time.monotonic() + timeout
+    while True:
+        o = wait_ready(k, "p", r, timeout=max(1.0, deadline - time.monotonic()))
+        view = _view(c)
+        mine = [d for d in view["devices"] if d.get("poolUID") == uid]
+        status = {d["uuid"] for d in o["status"]["devices"]}
+        if len(mine) == r and {d["uuid"] for d in mine} == status:
+            return view
+        if time.monotonic() > deadline:
+            raise AssertionError(f"not converged at {r}: status {sorted(status)}, agent "
+                                 f"{sorted(d['uuid'] for d in mine)}")
+        time.sleep(0.1)
+
+
+def test_agent_kills_at_random_points_converge_without_quarantine(cluster_factory):
+    c = cluster_factory()
+    k = c.client
+    rng = random.Random(20261017)
+    o = k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    uid = o["metadata"]["uid"]
+    _converged(c, uid, 2)
+    kills = 0
+    for step in range(10):
+        r = rng.choice([1, 2, 3, 4, 5, 6])
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": r}}, "default")
+        if rng.random() < 0.7:
+            # land inside the claim / release (the fake probe takes ~20 ms) or just after it
+            time.sleep(rng.uniform(0.0, 0.06))
+            c._kill(f"agent-{NODE}", sig=signal.SIGKILL)
+            c.start_agent(c.nodes[0])
+            kills += 1
+        view = _converged(c, uid, r)
+        bad = [d for d in view["devices"] if d.get("state") in ("Quarantined", "Maintenance")]
+        assert not bad, f"step {step} (replicas {r}): {[(d['index'], d.get('quarantine')) for d in bad]}"
+        owners = [d.get("poolUID") for d in view["devices"] if d.get("poolUID")]
+        assert owners == [uid] * r, owners
+    assert kills >= 5
+    k.delete(MI355XPOOLS, "p", "default")
+    k.wait_for(MI355XPOOLS, "p", "default", lambda x: x is None, timeout=30)
+    view = _view(c)
+    assert not [d for d in view["devices"] if d.get("poolUID")]
+    assert all(d.get("state") == "Free" for d in view["devices"]), \
+        [(d["index"], d.get("state")) for d in view["devices"]]
