@@ -127,6 +127,20 @@ def unix_target(path: str) -> str:
     return "unix://" + os.path.abspath(path)
 
 
+# gRPC Python shares subchannels between channels to one target through a process-wide pool: a
+# new channel to a socket whose previous listener died inherits that subchannel's reconnect
+# backoff (1 s, growing towards 2 min while the peer stays away) and fails UNAVAILABLE until it
+# expires — a re-registration or a fresh ListAndWatch after a kubelet or agent restart then waits
+# out the old connection's backoff. Channels that mean "connect now" take a private pool, as
+# every new connection in Go's gRPC (the kubelet's) is.
+FRESH_CHANNEL = [("grpc.use_local_subchannel_pool", 1)]
+
+
+def fresh_channel(path: str, options: list | None = None):
+    import grpc
+    return grpc.insecure_channel(unix_target(path), options=FRESH_CHANNEL + list(options or []))
+
+
 def regenerate(check: bool = False) -> bool:
     """Recompile the descriptor sets with protoc (torch ships one). Returns True if up to date."""
     protoc = shutil.which("protoc")

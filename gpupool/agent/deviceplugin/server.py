@@ -30,7 +30,7 @@ from typing import TYPE_CHECKING
 
 import grpc
 
-from .proto import API_VERSION, DP, KUBELET_SOCKET, Stub, service_handler, unix_target
+from .proto import API_VERSION, DP, KUBELET_SOCKET, Stub, fresh_channel, service_handler, unix_target
 
 if TYPE_CHECKING:  # pragma: no cover
     from ..agent import Agent
@@ -151,7 +151,7 @@ class DevicePluginServer:
         if not os.path.exists(ksock):
             return False
         try:
-            with grpc.insecure_channel(unix_target(ksock)) as ch:
+            with fresh_channel(ksock) as ch:
                 opts = DP.DevicePluginOptions(pre_start_required=False,
                                               get_preferred_allocation_available=True)
                 Stub(ch, "v1beta1.Registration").Register(
@@ -172,8 +172,7 @@ class DevicePluginServer:
         when it drops out of READY the kubelet went away, and the monitor re-registers once a
         kubelet answers again. No idle timeout: a quiet kubelet is not a restarted one."""
         old = getattr(self, "_kch", None)
-        ch = grpc.insecure_channel(unix_target(ksock),
-                                   options=[("grpc.client_idle_timeout_ms", 2**31 - 1)])
+        ch = fresh_channel(ksock, [("grpc.client_idle_timeout_ms", 2**31 - 1)])
         was_ready = [False]
 
         def on_state(state) -> None:

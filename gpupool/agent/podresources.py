@@ -9,7 +9,7 @@ import threading
 
 import grpc
 
-from .deviceplugin.proto import PR, Stub, unix_target
+from .deviceplugin.proto import PR, Stub, fresh_channel
 
 
 class PodResourcesClient:
@@ -22,7 +22,7 @@ class PodResourcesClient:
     def _lister(self):
         with self._lock:
             if self._stub is None:
-                self._ch = grpc.insecure_channel(unix_target(self.socket_path))
+                self._ch = fresh_channel(self.socket_path)  # a reset must really reconnect
                 self._stub = Stub(self._ch, "v1.PodResourcesLister")
             return self._stub
 

@@ -31,7 +31,7 @@ from dataclasses import dataclass, field
 import grpc
 
 from ..agent.deviceplugin.proto import (API_VERSION, DP, KUBELET_SOCKET, PR, Stub,
-                                        service_handler, unix_target)
+                                        fresh_channel, service_handler, unix_target)
 from ..api import schema
 from ..kube import NODES, PODS, Client, KubeError
 
@@ -165,8 +165,9 @@ class FakeKubelet:
                           f"unsupported device plugin API version {request.version}")
         conn = PluginConn(resource=request.resource_name, endpoint=request.endpoint,
                           options=request.options)
-        conn.channel = grpc.insecure_channel(unix_target(os.path.join(self.plugin_dir,
-                                                                      request.endpoint)))
+        # a private subchannel pool: the plugin's previous process may have died on this very
+        # socket path, and a shared subchannel would make this connection wait out its backoff
+        conn.channel = fresh_channel(os.path.join(self.plugin_dir, request.endpoint))
         conn.stub = Stub(conn.channel, "v1beta1.DevicePlugin")
         with self.lock:
             old = self.plugins.get(request.resource_name)

@@ -4,6 +4,7 @@ doubly owned or quarantined: nothing here is faulty, so a quarantine would mean 
 for a hardware failure (the claim-time probe a kill interrupted is re-run, not failed)."""
 from __future__ import annotations
 
+import os
 import random
 import signal
 import time
@@ -17,6 +18,7 @@ from .helpers import mi_pool, wait_ready
 pytestmark = pytest.mark.slow
 
 NODE = "mi355x-node-0"
+# GPUPOOL_CHAOS_SEED=<n> replays another walk (the defaults are the committed ones)
 
 
 def _view(c):
@@ -44,7 +46,7 @@ def _converged(c, uid: str, r: int, timeout: float = 30.0) -> dict:
 def test_agent_kills_at_random_points_converge_without_quarantine(cluster_factory):
     c = cluster_factory()
     k = c.client
-    rng = random.Random(20261017)
+    rng = random.Random(int(os.environ.get("GPUPOOL_CHAOS_SEED", "20261017")))
     o = k.create(MI355XPOOLS, mi_pool("p", 2), "default")
     uid = o["metadata"]["uid"]
     _converged(c, uid, 2)
@@ -70,3 +72,35 @@ def test_agent_kills_at_random_points_converge_without_quarantine(cluster_factor
     assert not [d for d in view["devices"] if d.get("poolUID")]
     assert all(d.get("state") == "Free" for d in view["devices"]), \
         [(d["index"], d.get("state")) for d in view["devices"]]
+
+
+def test_manager_and_agent_kills_at_random_points_converge(cluster_factory):
+    """The same walk with the manager killed too (alone or together with the agent): a restarted
+    manager re-adopts what the ledger holds, resolves claims whose reply it never saw, and the
+    pool still converges with every GPU accounted for."""
+    c = cluster_factory()
+    k = c.client
+    rng = random.Random(int(os.environ.get("GPUPOOL_CHAOS_SEED", "4242")))
+    o = k.create(MI355XPOOLS, mi_pool("p", 3), "default")
+    uid = o["metadata"]["uid"]
+    _converged(c, uid, 3)
+    for step in range(10):
+        r = rng.choice([1, 2, 3, 4, 5, 6, 8])
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": r}}, "default")
+        what = rng.choice(["manager", "agent", "both", "none"])
+        time.sleep(rng.uniform(0.0, 0.06))
+        if what in ("manager", "both"):
+            c._kill("manager", sig=signal.SIGKILL)
+        if what in ("agent", "both"):
+            c._kill(f"agent-{NODE}", sig=signal.SIGKILL)
+            c.start_agent(c.nodes[0])
+        if what in ("manager", "both"):
+            c.start_manager()
+        t0 = time.monotonic()
+        view = _converged(c, uid, r)
+        print(f"step {step} {what} r={r} converged in {time.monotonic() - t0:.2f}s")
+        bad = [d for d in view["devices"] if d.get("state") in ("Quarantined", "Maintenance")]
+        assert not bad, f"step {step} ({what}, replicas {r}): {[(d['index'], d.get('quarantine')) for d in bad]}"
+    k.delete(MI355XPOOLS, "p", "default")
+    k.wait_for(MI355XPOOLS, "p", "default", lambda x: x is None, timeout=30)
+    assert not [d for d in _view(c)["devices"] if d.get("poolUID")]

@@ -325,3 +325,30 @@ def test_kubelet_restart_that_wipes_the_plugin_dir(tmp_path, sockdir, native_bui
     finally:
         a.stop()
         kubelet.stop()
+
+
+def test_plugin_reregisters_promptly_after_a_kubelet_outage(tmp_path, sockdir, native_built):
+    """While the kubelet is away, gRPC backs off reconnecting to its socket (1 s, growing). The
+    plugin's Register after the kubelet returns must not inherit that backoff from the channel it
+    keeps to watch the kubelet: it dials a fresh connection, so the new kubelet hears from the
+    plugin within the monitor's poll period, not a backoff later."""
+    dp_dir = os.path.join(sockdir, "dp")
+    kubelet = MiniKubelet(dp_dir)
+    a = make_agent(tmp_path, sockdir)
+    try:
+        claim(a, count=1)
+        deadline = time.time() + 5
+        while not kubelet.registrations and time.time() < deadline:
+            time.sleep(0.02)
+        assert kubelet.registrations
+        kubelet.stop()
+        time.sleep(1.5)  # long enough for a reconnect backoff to reach 1 s
+        kubelet = MiniKubelet(dp_dir)
+        t0 = time.monotonic()
+        while not kubelet.registrations and time.monotonic() - t0 < 10:
+            time.sleep(0.01)
+        took = time.monotonic() - t0
+        assert kubelet.registrations and took < 0.8, took
+    finally:
+        a.stop()
+        kubelet.stop()
