@@ -197,6 +197,9 @@ class RocmProvider : public DeviceProvider {
   void prefetch(const std::string& node, int max_wait_ms = 0);
   void set_view_max_age_ms(int ms) { view_max_age_ms_ = ms; }
   uint64_t view_cache_hits() const { return cache_hits_.load(); }
+  // RPCs the node's agent has answered so far: the event feed's reconnect loop backs off while
+  // the agent is away and retries at once when a reconcile's RPC shows it is back.
+  uint64_t answered(const std::string& node);
 
  private:
   Json post_(const std::string& node, const std::string& path, const Json& body);
@@ -218,6 +221,7 @@ class RocmProvider : public DeviceProvider {
   std::map<std::string, uint64_t> epoch_;      // bumped by every mutating RPC, per node
   std::map<std::string, int> inflight_;        // mutating RPCs in progress, per node
   std::condition_variable cache_cv_;           // signalled when a node's inflight_ drops to 0
+  std::map<std::string, uint64_t> answered_;   // RPCs answered (any status), per node
   int view_max_age_ms_ = 5000;
   std::atomic<uint64_t> cache_hits_{0};
 };

@@ -243,6 +243,7 @@ int run_validate(const std::string& path) {
 // then every pool with a claim on that node is enqueued.
 class AgentWatchers {
  public:
+  static constexpr int kMaxFeedBackoffMs = 1000;
   AgentWatchers(RocmProvider& prov, Informer& pools, Controller& ctl) : prov_(prov), pools_(pools), ctl_(ctl) {}
   ~AgentWatchers() { stop_all(); }
 
@@ -320,8 +321,13 @@ class AgentWatchers {
         backoff = 100;
       } catch (const std::exception& e) {
         log.debug("agent long-poll failed", Json::object().set("error", e.what()));
-        for (int i = 0; i < backoff / 50 && !w->stop; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(50));
-        backoff = std::min(backoff * 2, 5000);
+        // back off while the agent is away (a refused connect is cheap: at most one a second per
+        // node), and reconnect at once when a reconcile's RPC reaches it again: a restarted
+        // agent's events (re-advertised GPUs, faults) must not wait out a grown backoff
+        const uint64_t seen = prov_.answered(node);
+        for (int i = 0; i < backoff / 50 && !w->stop && prov_.answered(node) == seen; ++i)
+          std::this_thread::sleep_for(std::chrono::milliseconds(50));
+        backoff = prov_.answered(node) != seen ? 100 : std::min(backoff * 2, kMaxFeedBackoffMs);
       }
     }
   }

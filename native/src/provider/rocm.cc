@@ -158,6 +158,10 @@ Json RocmProvider::post_(const std::string& node, const std::string& path, const
   } catch (const std::exception& e) {
     throw ProviderError("AgentUnreachable", "agent on " + node + ": " + e.what());
   }
+  {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    ++answered_[node];
+  }
   auto j = Json::try_parse(r.body);
   if (r.status >= 400) {
     std::string msg = j ? (*j)["message"].str_or(r.body) : r.body;
@@ -169,6 +173,12 @@ Json RocmProvider::post_(const std::string& node, const std::string& path, const
 }
 
 NodeView RocmProvider::observe(const std::string& node) { return observe_pool(node, ""); }
+
+uint64_t RocmProvider::answered(const std::string& node) {
+  std::lock_guard<std::mutex> g(cache_mu_);
+  auto it = answered_.find(node);
+  return it == answered_.end() ? 0 : it->second;
+}
 
 void RocmProvider::note_gen(const std::string& node, int64_t gen) {
   std::lock_guard<std::mutex> g(cache_mu_);
@@ -241,6 +251,10 @@ NodeView RocmProvider::observe_pool(const std::string& node, const std::string& 
   try {
     std::shared_ptr<HttpClient> c = client_for(node);
     HttpResponse r = c->request("GET", pool_uid.empty() ? "/v1/node" : "/v1/node?pool=" + pool_uid);
+    {
+      std::lock_guard<std::mutex> g(cache_mu_);
+      ++answered_[node];
+    }
     if (r.status >= 400) throw ProviderError("AgentError", "GET /v1/node: HTTP " + std::to_string(r.status));
     Json j = Json::parse(r.body);
     nv.reachable = true;

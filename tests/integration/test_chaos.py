@@ -104,3 +104,25 @@ def test_manager_and_agent_kills_at_random_points_converge(cluster_factory):
     k.delete(MI355XPOOLS, "p", "default")
     k.wait_for(MI355XPOOLS, "p", "default", lambda x: x is None, timeout=30)
     assert not [d for d in _view(c)["devices"] if d.get("poolUID")]
+
+
+def test_fault_right_after_an_agent_outage_is_seen_promptly(cluster_factory):
+    """The manager follows each agent's event feed and backs off reconnecting while the agent is
+    down. After a multi-second outage a fault on a Ready pool's GPU must still reach the pool
+    within about a second of the agent's return (the feed's backoff is capped and resets as soon
+    as a reconcile reaches the agent), not after a backoff that grew during the outage."""
+    from .helpers import cond_is
+    c = cluster_factory()
+    k = c.client
+    o = k.create(MI355XPOOLS, mi_pool("p", 2, replacePolicy="Keep"), "default")
+    o = wait_ready(k, "p", 2)
+    victim = str(o["status"]["devices"][0]["index"])
+    c._kill(f"agent-{NODE}", sig=signal.SIGKILL)
+    time.sleep(3.0)
+    c.start_agent(c.nodes[0])
+    c.set_faults(NODE, {"devices": {victim: {"ecc": {"uncorrectable": 1}}}})
+    t0 = time.monotonic()
+    k.wait_for(MI355XPOOLS, "p", "default", cond_is("HBMECCHealthy", "False"), timeout=10)
+    took = time.monotonic() - t0
+    print(f"fault seen {took:.2f} s after the agent returned")
+    assert took < 1.5, took
