@@ -126,3 +126,63 @@ def test_fault_right_after_an_agent_outage_is_seen_promptly(cluster_factory):
     took = time.monotonic() - t0
     print(f"fault seen {took:.2f} s after the agent returned")
     assert took < 1.5, took
+
+
+def test_kills_during_drains_of_running_pods(cluster_factory):
+    """Scale-downs of a pool whose every GPU runs a pod, with the agent or the manager killed
+    while the drain evicts: the pool converges, exactly the pods on released GPUs are gone, every
+    surviving pod sits on a GPU the pool still owns, and no released GPU keeps a pod."""
+    from gpupool.kube import PODS
+
+    from .helpers import pause_pod
+    c = cluster_factory()
+    k = c.client
+    rng = random.Random(int(os.environ.get("GPUPOOL_CHAOS_SEED", "777")))
+    o = k.create(MI355XPOOLS, mi_pool("p", 6, drain={"gracePeriodSeconds": 1}), "default")
+    uid = o["metadata"]["uid"]
+    _converged(c, uid, 6)
+    seq = 0
+
+    def fill(n: int) -> None:
+        nonlocal seq
+        running = [p for p in k.list(PODS, "default")["items"]]
+        for _ in range(n - len(running)):
+            k.create(PODS, pause_pod(f"w{seq}"), "default")
+            seq += 1
+        deadline = time.monotonic() + 30
+        while time.monotonic() < deadline:
+            pods = k.list(PODS, "default")["items"]
+            if len(pods) == n and all(p["status"].get("phase") == "Running" for p in pods):
+                return
+            time.sleep(0.05)
+        raise AssertionError(f"pods not running: {[(p['metadata']['name'], p['status'].get('phase')) for p in pods]}")
+
+    r = 6
+    for step in range(5):
+        fill(r)
+        r = rng.choice([x for x in (1, 2, 3, 4, 5) if x < r] or [1]) if r > 1 else 6
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": r}}, "default")
+        what = rng.choice(["agent", "manager", "both"])
+        time.sleep(rng.uniform(0.0, 0.3))  # somewhere in the cordon -> evict -> wait -> release
+        if what in ("manager", "both"):
+            c._kill("manager", sig=signal.SIGKILL)
+        if what in ("agent", "both"):
+            c._kill(f"agent-{NODE}", sig=signal.SIGKILL)
+            c.start_agent(c.nodes[0])
+        if what in ("manager", "both"):
+            c.start_manager()
+        view = _converged(c, uid, r, timeout=60)
+        kept = {d["uuid"] for d in view["devices"] if d.get("poolUID") == uid}
+        deadline = time.monotonic() + 10
+        while True:  # evicted pods finish terminating (grace 1 s)
+            pods = k.list(PODS, "default")["items"]
+            if len(pods) <= r or time.monotonic() > deadline:
+                break
+            time.sleep(0.05)
+        assert len(pods) <= r, (step, what, r, [p["metadata"]["name"] for p in pods])
+        for p in pods:
+            assert p["metadata"]["annotations"]["gpupool.amd.com/devices"] in kept, (step, what)
+        for d in view["devices"]:
+            if d["uuid"] not in kept:
+                assert not d["pods"], (step, what, d["index"], d["pods"])
+            assert d.get("state") not in ("Quarantined", "Maintenance"), (step, what, d["index"])
