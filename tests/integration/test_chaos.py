@@ -186,3 +186,44 @@ def test_kills_during_drains_of_running_pods(cluster_factory):
             if d["uuid"] not in kept:
                 assert not d["pods"], (step, what, d["index"], d["pods"])
             assert d.get("state") not in ("Quarantined", "Maintenance"), (step, what, d["index"])
+
+
+def test_manager_kills_while_gangs_are_created(cluster_factory):
+    """Mi355xJob gangs created while the manager is killed at random points of pod creation:
+    every job ends up with exactly one pod per replica index (no duplicate from a pass that
+    re-ran after the crash), on distinct GPUs, and deleting the jobs leaves no pod behind."""
+    from gpupool.kube import MI355XJOBS, PODS
+    c = cluster_factory()
+    k = c.client
+    rng = random.Random(int(os.environ.get("GPUPOOL_CHAOS_SEED", "99")))
+    k.create(MI355XPOOLS, mi_pool("pool", 8), "default")
+    wait_ready(k, "pool", 8)
+    sizes = {}
+    for j in range(3):
+        n = rng.choice([1, 2, 3])
+        sizes[f"j{j}"] = n
+        k.create(MI355XJOBS, {
+            "apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xJob",
+            "metadata": {"name": f"j{j}"},
+            "spec": {"replicas": n, "gpusPerReplica": 1, "poolRef": "pool", "masterPort": 29950 + j,
+                     "template": {"spec": {"terminationGracePeriodSeconds": 1,
+                                           "containers": [{"name": "main", "command": ["sleep", "600"]}]}}}},
+            "default")
+        time.sleep(rng.uniform(0.0, 0.05))
+        c._kill("manager", sig=signal.SIGKILL)
+        c.start_manager()
+    for name, n in sizes.items():
+        k.wait_for(MI355XJOBS, name, "default",
+                   lambda o: bool(o) and (o.get("status") or {}).get("phase") == "Running", timeout=30)
+        pods = k.list(PODS, "default", label_selector=f"gpupool.amd.com/job-name={name}")["items"]
+        idx = sorted(p["metadata"]["labels"]["gpupool.amd.com/replica-index"] for p in pods)
+        assert idx == [str(i) for i in range(n)], (name, idx)
+    devs = [p["metadata"]["annotations"].get("gpupool.amd.com/devices")
+            for p in k.list(PODS, "default")["items"]]
+    assert len(devs) == len(set(devs)) == sum(sizes.values()), devs
+    for name in sizes:
+        k.delete(MI355XJOBS, name, "default")
+    deadline = time.monotonic() + 30
+    while k.list(PODS, "default")["items"] and time.monotonic() < deadline:
+        time.sleep(0.1)
+    assert k.list(PODS, "default")["items"] == []
