@@ -326,3 +326,39 @@ def test_arm_waits_for_nic_provisioning(arm, cluster_factory):
     assert gets, "the provider never polled the NIC"
     nic = arm.state()["nics"][0]
     assert nic["properties"]["provisioningState"] == "Succeeded"
+
+
+def test_arm_manager_kills_mid_create_and_delete_leave_nothing_behind(arm, cluster_factory):
+    """The manager killed at random points while VMs are being created (NIC, then VM with its OS
+    disk) and deleted: the pool converges to its spec with exactly that many VMs, each with its
+    own NIC and disk, and after the pool is deleted the resource group holds no VM, NIC or disk
+    of it — the deterministic per-slot names let a restarted manager find what its predecessor
+    started (README.md:238-240 isolation and cleanup contract)."""
+    import random
+    import signal
+    c = arm_cluster(cluster_factory, arm)
+    k = c.client
+    k.create(SECRETS, secret(), "default")
+    rng = random.Random(int(os.environ.get("GPUPOOL_CHAOS_SEED", "31")))
+    k.create(AZUREVMPOOLS, sample(replicas=1), "default")
+    k.wait_for(AZUREVMPOOLS, "gpu-pool-prod", "default", az_ready(1), timeout=30)
+    for step in range(4):
+        r = rng.choice([0, 1, 2, 3])
+        k.patch(AZUREVMPOOLS, "gpu-pool-prod", {"spec": {"replicas": r}}, "default")
+        time.sleep(rng.uniform(0.05, 0.4))  # inside the 0.3 s VM create / delete
+        c._kill("manager", sig=signal.SIGKILL)
+        c.start_manager()
+        o = k.wait_for(AZUREVMPOOLS, "gpu-pool-prod", "default", az_ready(r), timeout=60)
+        deadline = time.monotonic() + 15
+        while True:  # deletes of surplus VMs finish asynchronously after Ready
+            st = arm.state()
+            if len(st["vms"]) == len(st["nics"]) == len(st["disks"]) == r or \
+                    time.monotonic() > deadline:
+                break
+            time.sleep(0.1)
+        assert len(st["vms"]) == len(st["nics"]) == len(st["disks"]) == r, (step, r, st)
+        assert sorted(o["status"]["vms"]) == sorted(v["name"] for v in st["vms"]), step
+    k.delete(AZUREVMPOOLS, "gpu-pool-prod", "default")
+    k.wait_for(AZUREVMPOOLS, "gpu-pool-prod", "default", lambda o: o is None, timeout=60)
+    st = arm.state()
+    assert st["vms"] == [] and st["nics"] == [] and st["disks"] == []
