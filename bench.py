@@ -283,6 +283,12 @@ def main() -> int:
                     failed(k, e, w, "warmup")
         if run:
             run.gt_s = 0.0
+    # the latency clock runs in this process (PATCH sent -> Ready seen on the watch): take the
+    # set-up heap (torch, the cluster harness) out of the collector's generations, so a full
+    # collection that falls inside a timed cycle costs this process next to nothing
+    import gc
+    gc.collect()
+    gc.freeze()
     _barrier(world)
     footprint_before = run.footprint() if rank == 0 and run else {}
     t_start = time.perf_counter()
