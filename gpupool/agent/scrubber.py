@@ -112,12 +112,27 @@ class HbmScrubber:
         return {"passed": not bad, "offset": off, "bytes": n, "span": span, "badBits": bad,
                 "firstBadOffset": int(bad_at) if bad else None, "GBps": 6000.0, "ms": 0.0}
 
+    def _probes_quiet(self, timeout: float = 3.0) -> None:
+        """Wait (bounded) until no claim-time probe runs on this agent. Mapping or unmapping the
+        ~282 GiB sweep buffer while a probe runs stalls the probe: a claim that made the scrubbed
+        GPU ineligible used to start its probe exactly while the scrubber freed the buffer, and
+        that probe took 23.8 ms instead of 0.86 (profiles/r4o_bench_gpu1_real.json). The pod's
+        Allocate waits for the free anyway (``wait_released``), so the free can wait for the
+        probe."""
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline and not self._stop.is_set():
+            with self.agent.lock:
+                if not any(r.get("state") == "Probing" for r in self.agent.records.values()):
+                    return
+            time.sleep(0.002)
+
     def _hold(self, uuid: str) -> bool:
         """Allocate the sweep buffer (inproc: ~0.4 s for ~282 GiB) without any lock a claim takes."""
         with self._cv:
             self._held.add(uuid)
         t0 = time.perf_counter()
         if self.agent.prober.mode == "inproc":
+            self._probes_quiet()
             o = self._ordinal(uuid)
             # The claim-time probe arena comes first: a claim then never has to allocate while the
             # sweep buffer is held or while the driver clears it after the free (seconds).
@@ -198,6 +213,8 @@ class HbmScrubber:
                     self._fail(uuid, r)
                     break
         finally:
+            if self.agent.prober.mode == "inproc":
+                self._probes_quiet()
             self._release(uuid)
             with self._mu:
                 snap = {u: dict(r) for u, r in self.state.items()}

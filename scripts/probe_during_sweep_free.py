@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Does mapping / unmapping the scrubber's ~282 GiB sweep buffer stall a claim-time probe running
+at the same time on the same GPU? Claim-time probes (1 GiB, 2048^3 overlapped) back to back:
+alone, while another thread frees the sweep buffer (sweep_release: 4 GiB chunks), and while another
+thread allocates it (sweep_alloc). The scrubber now waits for running probes before either
+(gpupool/agent/scrubber.py _probes_quiet); this measures what that avoids.
+
+    python scripts/probe_during_sweep_free.py > gpurun_out/probe_during_sweep_free.json
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gpupool.ops import probe  # noqa: E402
+
+probe.init()
+opts = dict(hbm_bytes=1 << 30, gemm_n=2048, overlap=1)
+assert probe.run(0, **opts)["passed"]
+
+
+def probes_while(fn) -> tuple[list[float], float]:
+    out: list[float] = []
+    box = {}
+
+    def work():
+        t = time.perf_counter()
+        box["rc"] = fn()
+        box["ms"] = (time.perf_counter() - t) * 1e3
+    th = threading.Thread(target=work)
+    th.start()
+    while th.is_alive():
+        r = probe.run(0, **opts)
+        assert r["passed"], r
+        out.append(r["ms"])
+    th.join()
+    return out, box["ms"]
+
+
+def stats(xs: list[float]) -> dict:
+    return {"n": len(xs), "p50": round(statistics.median(xs), 3), "max": round(max(xs), 3),
+            "over2ms": sum(1 for x in xs if x > 2.0)} if xs else {"n": 0}
+
+
+alone = [probe.run(0, **opts)["ms"] for _ in range(200)]
+res = {"alone": stats(alone)}
+for rnd in range(2):
+    # fresh allocation, then probes during the free, then during a re-allocation (the driver
+    # clears the freed VRAM first: the slow case) and its free
+    assert probe.sweep_alloc(0, 4 << 30) >= 0
+    d, ms = probes_while(lambda: probe.sweep_release(0))
+    res[f"during_free_{rnd}"] = {**stats(d), "freeMs": round(ms, 1)}
+    d, ms = probes_while(lambda: probe.sweep_alloc(0, 4 << 30))
+    res[f"during_alloc_after_free_{rnd}"] = {**stats(d), "allocMs": round(ms, 1)}
+    d, ms = probes_while(lambda: probe.sweep_release(0))
+    res[f"during_free_b_{rnd}"] = {**stats(d), "freeMs": round(ms, 1)}
+    time.sleep(8)  # let the driver finish clearing before the next round
+    res[f"alone_after_{rnd}"] = stats([probe.run(0, **opts)["ms"] for _ in range(100)])
+probe.trim(0)
+print(json.dumps(res, indent=1))
