@@ -904,5 +904,15 @@ class Store:
         if rv < self.compacted_rv:
             raise ApiError(410, "Expired", f"too old resource version: {rv} "
                            f"({self.compacted_rv + 1})")
-        return [e for e in self.log if e.rtype == rt.key and e.rv > rv]
+        # the log is in resourceVersion order: walk back from the newest event only as far as rv
+        # (a resuming watch is usually a few events behind; scanning the whole 50 000-event window
+        # per watch (re)connect cost ~0.4 ms on the event loop)
+        out = []
+        for e in reversed(self.log):
+            if e.rv <= rv:
+                break
+            if e.rtype == rt.key:
+                out.append(e)
+        out.reverse()
+        return out
 
