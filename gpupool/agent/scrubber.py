@@ -35,6 +35,8 @@ log = logging.getLogger("gpupool.agent.scrubber")
 
 
 class HbmScrubber:
+    CLEAR_GRACE_S = 30.0  # no new sweep buffer on a GPU this soon after freeing its last one
+
     def __init__(self, agent, interval_s: float = 60.0, window_bytes: int = 4 << 30,
                  windows_per_pass: int = 8, reserve_bytes: int = 4 << 30,
                  start_delay_s: float = 30.0):
@@ -49,6 +51,10 @@ class HbmScrubber:
         self._mu = threading.Lock()
         self._cv = threading.Condition(self._mu)
         self._held: set[str] = set()  # GPUs whose sweep buffer is allocated
+        # GPU -> monotonic time its sweep buffer was freed: the driver clears freed VRAM (~6 s for
+        # ~282 GiB) and an allocation issued meanwhile waits for the clear — and stalls any probe
+        # of that GPU behind it (6.1 s, profiles/r4p_probe_during_sweep_free.json)
+        self._released_at: dict[str, float] = {}
         self._stop = threading.Event()
         self._kick = threading.Event()
         self._thread: threading.Thread | None = None
@@ -158,6 +164,7 @@ class HbmScrubber:
                      (time.perf_counter() - t0) * 1e3)
             with self._cv:
                 self._held.discard(uuid)
+                self._released_at[uuid] = time.monotonic()
                 self._cv.notify_all()
 
     def scrub_device(self, uuid: str, windows: int | None = None) -> dict:
@@ -169,6 +176,9 @@ class HbmScrubber:
         with self.agent.lock:
             if not self._eligible(uuid):
                 return rec
+        if self.agent.prober.mode == "inproc" and \
+                time.monotonic() - self._released_at.get(uuid, -1e9) < self.CLEAR_GRACE_S:
+            return rec  # the driver may still be clearing this GPU's previous buffer
         if not self._hold(uuid):
             log.warning("HBM sweep buffer allocation failed on %s", uuid)
             return rec

@@ -21,7 +21,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -1311,7 +1313,29 @@ std::string run_peer_ring(const std::vector<int>& devs, const char* opts) {
 // All free HBM minus ``reserve``, 2 MiB granular, as kSweepChunk pieces. Measured on MI355X
 // (profiles/r2h_sweep_claim_diag.txt): ~0.2 s to allocate ~282 GiB of fresh VRAM, ~6 s once the
 // driver must clear previously used VRAM; neither runs under the device lock a probe takes.
-SweepBuf sweep_alloc_raw(uint64_t reserve) {
+// Claim-time probes running per device (mi355x_probe_run). Mapping or unmapping the sweep buffer
+// stalls a probe that runs beside it — up to the whole 6 s allocation when the driver is still
+// clearing the previous buffer, 5-211 ms per chunk otherwise (profiles/r4p_probe_during_sweep_free.json)
+// — so the lock-free sweep alloc / free paths wait between 4 GiB chunks while a probe runs: a
+// probe then shares the device with at most one chunk operation.
+std::atomic<int> g_probes_active[64];
+
+struct ProbeActive {
+  int d;
+  explicit ProbeActive(int dev) : d(dev % 64) { g_probes_active[d].fetch_add(1); }
+  ~ProbeActive() { g_probes_active[d].fetch_sub(1); }
+};
+
+// Wait (bounded) until no probe runs on ``dev``; -1: never wait (callers holding the device lock).
+void yield_to_probes(int dev) {
+  static const bool off = std::getenv("GPUPOOL_SWEEP_NO_YIELD") != nullptr;  // in-process A/B only
+  if (dev < 0 || off) return;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+  while (g_probes_active[dev % 64].load() > 0 && std::chrono::steady_clock::now() < deadline)
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+}
+
+SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
   size_t free_b = 0, total_b = 0;
   PROBE_CHECK(hipMemGetInfo(&free_b, &total_b));
   const uint64_t gran = 2ull << 20;
@@ -1320,6 +1344,7 @@ SweepBuf sweep_alloc_raw(uint64_t reserve) {
   const uint64_t span = ((free_b - reserve) / gran) * gran;
   for (uint64_t at = 0; at < span; at += kSweepChunk) {
     void* p = nullptr;
+    yield_to_probes(yield_dev);
     hipError_t e = hipMalloc(&p, std::min<uint64_t>(kSweepChunk, span - at));
     if (e != hipSuccess) {
       for (void* q : b.chunks) (void)hipFree(q);
@@ -1332,8 +1357,11 @@ SweepBuf sweep_alloc_raw(uint64_t reserve) {
   return b;
 }
 
-void sweep_free(SweepBuf& b) {
-  for (void* p : b.chunks) (void)hipFree(p);  // one bounded unmap per chunk
+void sweep_free(SweepBuf& b, int yield_dev = -1) {
+  for (void* p : b.chunks) {  // one bounded unmap per chunk
+    yield_to_probes(yield_dev);
+    (void)hipFree(p);
+  }
   b.chunks.clear();
   b.span = 0;
 }
@@ -1458,6 +1486,7 @@ char* mi355x_probe_identify(int dev) {
 
 char* mi355x_probe_run(int dev, const char* opts_json) {
   if (g_count < 0 || dev < 0 || dev >= g_count) return dup("{\"passed\":false,\"error\":\"bad device index\"}");
+  ProbeActive active(dev);  // the sweep buffer's chunk (un)mapping waits while this runs
   // Per-device serialisation: concurrent probes of DIFFERENT devices run in parallel.
   std::lock_guard<std::mutex> g(device_mutex(dev));
   try {
@@ -1549,7 +1578,7 @@ int mi355x_probe_sweep_alloc(int dev, long long reserve) {
   SweepBuf b;
   try {
     if (hipSetDevice(dev) != hipSuccess) return -1;
-    b = sweep_alloc_raw(static_cast<uint64_t>(std::max(0LL, reserve)));
+    b = sweep_alloc_raw(static_cast<uint64_t>(std::max(0LL, reserve)), dev);
   } catch (const std::exception&) {
     (void)hipGetLastError();
     return -2;
@@ -1576,7 +1605,7 @@ int mi355x_probe_sweep_release(int dev) {
   }
   if (b.empty()) return 0;
   if (hipSetDevice(dev) != hipSuccess) return -1;
-  sweep_free(b);  // outside the device lock, chunk by chunk
+  sweep_free(b, dev);  // outside the device lock, chunk by chunk, between probes
   return 1;
 }
 

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Does mapping / unmapping the scrubber's ~282 GiB sweep buffer stall a claim-time probe running
-at the same time on the same GPU? Claim-time probes (1 GiB, 2048^3 overlapped) back to back:
-alone, while another thread frees the sweep buffer (sweep_release: 4 GiB chunks), and while another
-thread allocates it (sweep_alloc). The scrubber now waits for running probes before either
-(gpupool/agent/scrubber.py _probes_quiet); this measures what that avoids.
+at the same time on the same GPU? Claim-time probes (1 GiB, 2048^3 overlapped), one every ~10 ms
+(a burst of claims), alone, while another thread frees the sweep buffer (4 GiB chunks) and while it
+allocates it again right after the free (the driver is still clearing the freed VRAM: the slow
+case). ``GPUPOOL_SWEEP_NO_YIELD=1`` turns off the chunk loop's yielding to running probes (run the
+script once with, once without).
 
     python scripts/probe_during_sweep_free.py > gpurun_out/probe_during_sweep_free.json
 """
@@ -24,7 +25,7 @@ opts = dict(hbm_bytes=1 << 30, gemm_n=2048, overlap=1)
 assert probe.run(0, **opts)["passed"]
 
 
-def probes_while(fn) -> tuple[list[float], float]:
+def probes_while(fn, gap_s: float = 0.01) -> tuple[list[float], float]:
     out: list[float] = []
     box = {}
 
@@ -35,9 +36,11 @@ def probes_while(fn) -> tuple[list[float], float]:
     th = threading.Thread(target=work)
     th.start()
     while th.is_alive():
+        t = time.perf_counter()
         r = probe.run(0, **opts)
         assert r["passed"], r
-        out.append(r["ms"])
+        out.append((time.perf_counter() - t) * 1e3)  # wall, incl. any wait for the device
+        time.sleep(gap_s)
     th.join()
     return out, box["ms"]
 
@@ -47,19 +50,20 @@ def stats(xs: list[float]) -> dict:
             "over2ms": sum(1 for x in xs if x > 2.0)} if xs else {"n": 0}
 
 
-alone = [probe.run(0, **opts)["ms"] for _ in range(200)]
-res = {"alone": stats(alone)}
+res = {"yield": os.environ.get("GPUPOOL_SWEEP_NO_YIELD") is None,
+       "alone": stats([probe.run(0, **opts)["ms"] for _ in range(100)])}
 for rnd in range(2):
-    # fresh allocation, then probes during the free, then during a re-allocation (the driver
-    # clears the freed VRAM first: the slow case) and its free
     assert probe.sweep_alloc(0, 4 << 30) >= 0
     d, ms = probes_while(lambda: probe.sweep_release(0))
     res[f"during_free_{rnd}"] = {**stats(d), "freeMs": round(ms, 1)}
-    d, ms = probes_while(lambda: probe.sweep_alloc(0, 4 << 30))
+    d, ms = probes_while(lambda: probe.sweep_alloc(0, 4 << 30))  # right after the free: clearing
     res[f"during_alloc_after_free_{rnd}"] = {**stats(d), "allocMs": round(ms, 1)}
     d, ms = probes_while(lambda: probe.sweep_release(0))
     res[f"during_free_b_{rnd}"] = {**stats(d), "freeMs": round(ms, 1)}
-    time.sleep(8)  # let the driver finish clearing before the next round
-    res[f"alone_after_{rnd}"] = stats([probe.run(0, **opts)["ms"] for _ in range(100)])
+    time.sleep(8)  # the driver finishes clearing
+    d, ms = probes_while(lambda: probe.sweep_alloc(0, 4 << 30))  # after the clear: the scrubber's case
+    res[f"during_alloc_cleared_{rnd}"] = {**stats(d), "allocMs": round(ms, 1)}
+    assert probe.sweep_release(0) >= 0
+    time.sleep(8)
 probe.trim(0)
 print(json.dumps(res, indent=1))

@@ -92,3 +92,15 @@ def test_probe_wait_is_bounded():
     t0 = time.monotonic()
     s._probes_quiet(timeout=0.2)
     assert 0.18 < time.monotonic() - t0 < 1.0
+
+
+def test_no_new_sweep_buffer_while_the_driver_clears_the_last_one():
+    agent, hip = fake_agent()
+    s = HbmScrubber(agent, window_bytes=1 << 20, windows_per_pass=1)
+    s.scrub_device(UUID)
+    assert [k for k, _ in hip.calls] == ["alloc", "release"]
+    s.scrub_device(UUID)  # within CLEAR_GRACE_S of the free: skipped
+    assert [k for k, _ in hip.calls] == ["alloc", "release"]
+    s._released_at[UUID] -= s.CLEAR_GRACE_S
+    s.scrub_device(UUID)
+    assert [k for k, _ in hip.calls] == ["alloc", "release", "alloc", "release"]
