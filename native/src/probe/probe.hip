@@ -399,6 +399,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_mfma_nt(const short
 //     source address and the same involution on the read (rule 21);
 //   * one block per CU at N=4096 (256 tiles), XCD-aware bijective remap (T1).
 constexpr int G2_BM = 256, G2_BN = 256, G2_BK = 64;
+constexpr int kGemmGroupM = 0;  // tile order of gemm_bf16_mfma_256: 0 row-major, >1 grouped (A/B pending)
 constexpr int kGemm2Threads = 512;
 constexpr int G2_STAGE_SHORTS = (G2_BM + G2_BN) * G2_BK;  // one stage: A then B, 64 KiB
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -410,12 +411,26 @@ __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const sho
                                                                        const short* __restrict__ Bt,
                                                                        float* __restrict__ C, int M,
                                                                        int N, int K,
-                                                                       unsigned long long* __restrict__ cu_map) {
+                                                                       unsigned long long* __restrict__ cu_map,
+                                                                       int group_m) {
   __shared__ __attribute__((aligned(16))) short smem[2 * G2_STAGE_SHORTS];  // 128 KiB, the only LDS object
   if (cu_map && threadIdx.x == 0) mark_cu(cu_map);  // which CUs ran GEMM tiles (probe report)
-  const int tiles_n = N / G2_BN;
+  const int tiles_n = N / G2_BN, tiles_m = M / G2_BM;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile_m = wg / tiles_n, tile_n = wg % tiles_n;
+  // Tile order inside each XCD's contiguous range of wg (xcd_remap): row-major (group_m <= 1) walks
+  // whole tile rows, so the tiles an XCD runs at once share one or two A panels but need a B panel
+  // each; grouped (group_m rows at a time, column-major inside a group) makes them a group_m x k
+  // block that shares both, less operand traffic into the XCD's 4 MB L2 per K-step. Bijective.
+  int tile_m, tile_n;
+  if (group_m > 1) {
+    const int per_group = group_m * tiles_n, first_m = (wg / per_group) * group_m;
+    const int gm = min(tiles_m - first_m, group_m), r = wg % per_group;
+    tile_m = first_m + r % gm;
+    tile_n = r / gm;
+  } else {
+    tile_m = wg / tiles_n;
+    tile_n = wg % tiles_n;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
 
@@ -777,8 +792,9 @@ std::string hip_uuid(int dev) {
 // ctx.gev[0..1]) with exact u32 (mod 2^32) ABFT row/column checksums, then copies the two mismatch
 // counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``. zero_mfma: the operand
 // kernels zero the phase's counters cnt[kSlotSmall..kResSlots) and ABFT accumulators themselves.
-void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inject_gemm, int census_fault_xcc,
-                       bool zero_mfma, unsigned long long* cnt, unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
+void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int group_m, int reps, int inject_gemm,
+                       int census_fault_xcc, bool zero_mfma, unsigned long long* cnt, unsigned long long* hres,
+                       DeviceCtx& ctx, hipStream_t s) {
   const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
   auto align = [](size_t x) { return (x + 4095) & ~static_cast<size_t>(4095); };
   char* p = gbase;
@@ -798,7 +814,7 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int reps, int inje
   auto gemm = [&](const short* a_, const short* b_, float* c_, int nn, unsigned long long* cu_map) {
     if (tile256)
       hipLaunchKernelGGL(gemm_bf16_mfma_256, dim3((nn / G2_BM) * (nn / G2_BN)), dim3(kGemm2Threads), 0, s, a_, b_, c_, nn,
-                         nn, nn, cu_map);
+                         nn, nn, cu_map, group_m);
     else
       hipLaunchKernelGGL(gemm_bf16_mfma_nt, dim3((nn / BM) * (nn / BN)), dim3(kGemmThreads), 0, s, a_, b_, c_, nn, nn, nn);
   };
@@ -884,6 +900,7 @@ std::string run_probe(int dev, const char* opts) {
   const int inject_flips = static_cast<int>(std::min(4096LL, std::max(0LL, opt_int(opts, "injectBitFlips", 0))));
   const int inject_gemm = static_cast<int>(opt_int(opts, "injectGemmFault", 0));
   const bool tile256 = opt_int(opts, "gemmTile", 256) != 128;  // 128 = the older 128x128 kernel (A/B)
+  const int group_m = static_cast<int>(opt_int(opts, "gemmGroupM", kGemmGroupM));  // tile order (A/B)
   // The HBM test is bandwidth-bound with few waves per CU; the MFMA phase is compute-bound and
   // touches ~130 MiB: run them concurrently on two streams (overlap=0: one stream, serial).
   const bool overlap = opt_int(opts, "overlap", 1) != 0;
@@ -980,7 +997,7 @@ std::string run_probe(int dev, const char* opts) {
   // earlier on the GPU while the rest of the HBM test is still enqueued well ahead of need.
   const int hbm_first = static_cast<int>(opt_int(opts, "hbmFirst", 1));
   if (do_mfma && hbm_first == 0)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
                       ctx, s2);
 
   // ---------------- HBM: all patterns back to back, per-pattern counters
@@ -1011,7 +1028,7 @@ std::string run_probe(int dev, const char* opts) {
       hipLaunchKernelGGL(hbm_fill<0>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip, reset, nreset);
     PROBE_CHECK(hipEventRecord(ctx.ev[1 + 2 * pi], s));
     if (pi == 0 && do_mfma && hbm_first == 2)
-      launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
+      launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
                         ctx, s2);
     if (pi == 0 && inject_flips > 0)
       hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(hbm), n16 * 4,
@@ -1030,7 +1047,7 @@ std::string run_probe(int dev, const char* opts) {
   PROBE_CHECK(hipGetLastError());
   PROBE_CHECK(hipMemcpyAsync(hres, cnt, 2 * patterns * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   if (do_mfma && hbm_first == 1)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
                       ctx, s2);
   const double launch_ms = ms_since(t_run);  // host time to enqueue the whole probe
   PROBE_CHECK(hipStreamSynchronize(s));
@@ -1625,7 +1642,7 @@ int mi355x_probe_gemm_bf16(int dev, const void* A, const void* Bt, void* C, int 
     PROBE_CHECK(hipMemcpy(db.p, Bt, sb, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(gemm_bf16_mfma_256, dim3((m / G2_BM) * (n / G2_BN)), dim3(kGemm2Threads), 0, nullptr,
                        static_cast<const short*>(da.p), static_cast<const short*>(db.p), static_cast<float*>(dc.p), m, n,
-                       k, static_cast<unsigned long long*>(nullptr));
+                       k, static_cast<unsigned long long*>(nullptr), kGemmGroupM);
     PROBE_CHECK(hipGetLastError());
     PROBE_CHECK(hipMemcpy(C, dc.p, sc, hipMemcpyDeviceToHost));
     return 0;

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Tile order of the probe's 256x256 MFMA GEMM inside each XCD (probe option ``gemmGroupM``): 0 =
+row-major over the XCD's contiguous tile range, g > 1 = groups of g tile rows walked column-major
+(the tiles an XCD runs at once then share A and B panels in its L2). Interleaved rounds in one
+process, serial probe (no HBM test beside it), 10 GEMM reps per timing; every run's exact ABFT
+checksums and element check must pass.
+
+    python scripts/probe_gemm_group_ab.py [rounds] > gpurun_out/probe_gemm_group_ab.json
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gpupool.ops import probe  # noqa: E402
+
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 9
+groups = (0, 2, 4, 8, 16)
+probe.init()
+res: dict[str, list[float]] = {}
+for n in (4096, 8192):
+    for g in groups:  # warm every variant once
+        assert probe.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, overlap=0, gemmGroupM=g)["passed"]
+    for r in range(rounds):
+        order = groups if r % 2 == 0 else tuple(reversed(groups))
+        for g in order:
+            out = probe.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemm_reps=10, overlap=0,
+                            gemmGroupM=g)
+            assert out["passed"] and out["mfma"]["abftMismatches"] == 0, (n, g, out)
+            res.setdefault(f"{n}:g{g}", []).append(round(out["mfma"]["tflops"], 1))
+probe.trim(0)
+summary = {k: {"median": statistics.median(v), "min": min(v), "max": max(v)} for k, v in res.items()}
+print(json.dumps({"rounds": rounds, "summary": summary, "samples": res}, indent=1))

@@ -157,6 +157,17 @@ def test_gemm_kernels_exact_at_sizes(hip, n, tile):
     assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
 
 
+@pytest.mark.parametrize("n", [1280, 2048, 4096])
+@pytest.mark.parametrize("group_m", [2, 3, 4, 8])
+def test_grouped_tile_order_is_exact(hip, n, group_m):
+    """The grouped tile order (``gemmGroupM``) is a bijection over the tiles, also when the last
+    group is short (1280 = 5 tile rows with groups of 2, 3, 4): every C element is written once
+    and right (exact ABFT row/column checksums), and the census still sees every CU."""
+    r = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemmGroupM=group_m)
+    assert r["passed"], r
+    assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
+
+
 def test_overlapped_and_serial_probe_agree(hip):
     """The two-stream probe (HBM test beside the MFMA phase) finds the same injected faults as
     the serial one and both pass clean runs."""
