@@ -793,8 +793,8 @@ std::string hip_uuid(int dev) {
 // counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``. zero_mfma: the operand
 // kernels zero the phase's counters cnt[kSlotSmall..kResSlots) and ABFT accumulators themselves.
 void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int group_m, int reps, int inject_gemm,
-                       int census_fault_xcc, bool zero_mfma, unsigned long long* cnt, unsigned long long* hres,
-                       DeviceCtx& ctx, hipStream_t s) {
+                       int census_fault_xcc, bool zero_mfma, bool poison_c, unsigned long long* cnt,
+                       unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
   const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
   auto align = [](size_t x) { return (x + 4095) & ~static_cast<size_t>(4095); };
   char* p = gbase;
@@ -839,9 +839,12 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int group_m, int r
   hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, a, e, 0x51u, 2, zero_mfma ? v32 : nullptr,
                      zero_mfma ? 3 * n : 0);
   hipLaunchKernelGGL(gen_operand, dim3(2048), dim3(256), 0, s, b, e, 0x77u, 2, static_cast<uint32_t*>(nullptr), 0);
+  // test hook: C starts as all-ones words (NaN) so a tile the GEMM never writes fails the checks
+  // instead of passing on the previous run's identical result (the arena is reused)
+  if (poison_c) PROBE_CHECK(hipMemsetAsync(c, 0xFF, n * n * sizeof(float), s));
   // the 256^3 check above already ran this kernel's code object: time the first launch
   PROBE_CHECK(hipEventRecord(ctx.gev[0], s));
-  for (int rep = 0; rep < reps; ++rep) gemm(a, b, c, gemm_n, cnt + kSlotGemmMap);
+  for (int rep = 0; rep < reps; ++rep) gemm(a, b, c, gemm_n, cnt + kSlotGemmMap);  // reps 0: test hook
   PROBE_CHECK(hipEventRecord(ctx.gev[1], s));
   PROBE_CHECK(hipGetLastError());
   if (inject_gemm)
@@ -901,6 +904,7 @@ std::string run_probe(int dev, const char* opts) {
   const int inject_gemm = static_cast<int>(opt_int(opts, "injectGemmFault", 0));
   const bool tile256 = opt_int(opts, "gemmTile", 256) != 128;  // 128 = the older 128x128 kernel (A/B)
   const int group_m = static_cast<int>(opt_int(opts, "gemmGroupM", kGemmGroupM));  // tile order (A/B)
+  const bool poison_c = opt_int(opts, "poisonC", 0) != 0;                           // test hook
   // The HBM test is bandwidth-bound with few waves per CU; the MFMA phase is compute-bound and
   // touches ~130 MiB: run them concurrently on two streams (overlap=0: one stream, serial).
   const bool overlap = opt_int(opts, "overlap", 1) != 0;
@@ -985,7 +989,8 @@ std::string run_probe(int dev, const char* opts) {
   CuCount census, gemm_cus;
   const bool require_all_cus = opt_int(opts, "requireAllCUs", 1) != 0;
   double tflops = 0, gemm_ms = 0;
-  const int reps = static_cast<int>(std::max(1LL, opt_int(opts, "gemmReps", 1)));
+  // gemmSkip (test hook, with poisonC): no timed GEMM at all, so C keeps the poison
+  const int reps = opt_int(opts, "gemmSkip", 0) ? 0 : static_cast<int>(std::max(1LL, opt_int(opts, "gemmReps", 1)));
   const int census_fault_xcc = static_cast<int>(opt_int(opts, "injectCensusFaultXcc", -1));
   const bool want_keys = opt_int(opts, "cuKeys", 0) != 0;
   std::vector<int> cu_keys;
@@ -997,7 +1002,7 @@ std::string run_probe(int dev, const char* opts) {
   // earlier on the GPU while the rest of the HBM test is still enqueued well ahead of need.
   const int hbm_first = static_cast<int>(opt_int(opts, "hbmFirst", 1));
   if (do_mfma && hbm_first == 0)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                       ctx, s2);
 
   // ---------------- HBM: all patterns back to back, per-pattern counters
@@ -1028,7 +1033,7 @@ std::string run_probe(int dev, const char* opts) {
       hipLaunchKernelGGL(hbm_fill<0>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip, reset, nreset);
     PROBE_CHECK(hipEventRecord(ctx.ev[1 + 2 * pi], s));
     if (pi == 0 && do_mfma && hbm_first == 2)
-      launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
+      launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                         ctx, s2);
     if (pi == 0 && inject_flips > 0)
       hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(hbm), n16 * 4,
@@ -1047,7 +1052,7 @@ std::string run_probe(int dev, const char* opts) {
   PROBE_CHECK(hipGetLastError());
   PROBE_CHECK(hipMemcpyAsync(hres, cnt, 2 * patterns * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   if (do_mfma && hbm_first == 1)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                       ctx, s2);
   const double launch_ms = ms_since(t_run);  // host time to enqueue the whole probe
   PROBE_CHECK(hipStreamSynchronize(s));
@@ -1056,8 +1061,8 @@ std::string run_probe(int dev, const char* opts) {
     PROBE_CHECK(hipStreamSynchronize(s2));
     float ms;
     PROBE_CHECK(hipEventElapsedTime(&ms, ctx.gev[0], ctx.gev[1]));
-    gemm_ms = ms / reps;
-    tflops = 2.0 * gemm_n * static_cast<double>(gemm_n) * gemm_n / (gemm_ms * 1e-3) / 1e12;
+    gemm_ms = reps > 0 ? ms / reps : 0.0;
+    tflops = gemm_ms > 0 ? 2.0 * gemm_n * static_cast<double>(gemm_n) * gemm_n / (gemm_ms * 1e-3) / 1e12 : 0.0;
     small_bad = hres[kSlotSmall];
     abft_bad = hres[kSlotAbft];
     census_bad = hres[kSlotCensusBad];

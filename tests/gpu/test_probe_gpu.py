@@ -157,13 +157,25 @@ def test_gemm_kernels_exact_at_sizes(hip, n, tile):
     assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
 
 
+def test_poisoned_c_fails_when_the_gemm_does_not_run(hip):
+    """The poisonC hook is only meaningful if an unwritten C fails the checks even though the
+    reused arena still holds an identical earlier result: poison C, skip the GEMM (gemmSkip) and
+    the ABFT checks must fail — with the poison and a real GEMM the probe passes (below)."""
+    clean = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=1024)
+    assert clean["passed"], clean  # the arena now holds the right C for these operands
+    r = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=1024, poisonC=1, gemmSkip=1)
+    assert not r["passed"] and r["mfma"]["abftMismatches"] > 0, r
+    again = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=1024, poisonC=1)
+    assert again["passed"], again
+
+
 @pytest.mark.parametrize("n", [1280, 2048, 4096])
 @pytest.mark.parametrize("group_m", [2, 3, 4, 8])
 def test_grouped_tile_order_is_exact(hip, n, group_m):
     """The grouped tile order (``gemmGroupM``) is a bijection over the tiles, also when the last
     group is short (1280 = 5 tile rows with groups of 2, 3, 4): every C element is written once
     and right (exact ABFT row/column checksums), and the census still sees every CU."""
-    r = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemmGroupM=group_m)
+    r = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemmGroupM=group_m, poisonC=1)
     assert r["passed"], r
     assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
 
