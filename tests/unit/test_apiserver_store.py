@@ -321,3 +321,28 @@ def test_update_copy_semantics(store):
     assert out is store.objects[rt.key][("default", "a")] and out["status"] is body["status"]
     ev = store.log[-1]
     assert ev.obj is not out and ev.obj == out
+
+
+def test_events_since_filters_by_type_and_resource_version(store):
+    """A resuming watch gets exactly its own type's events newer than its resourceVersion, in
+    order, with other types' events interleaved in the log."""
+    mi_rt = mi(store)
+    cm_rt = store.lookup("", "configmaps") if ("", "configmaps") in store.types else None
+    other = cm_rt or store.types[("", "namespaces")]
+    a = store.create(mi_rt, "default", pool("a"))
+    rv_a = int(a["metadata"]["resourceVersion"])
+    for i in range(5):
+        store.patch(mi_rt, "default", "a", {"spec": {"replicas": i + 2}}, "merge")
+        if other.kind == "Namespace":
+            store.create(other, None, {"apiVersion": "v1", "kind": "Namespace",
+                                       "metadata": {"name": f"ns{i}"}})
+        else:
+            store.create(other, "default", {"apiVersion": "v1", "kind": "ConfigMap",
+                                            "metadata": {"name": f"c{i}"}})
+    evs = store.events_since(mi_rt, rv_a)
+    assert [e.rtype for e in evs] == [mi_rt.key] * 5
+    assert [e.obj["spec"]["replicas"] for e in evs] == [2, 3, 4, 5, 6]
+    assert all(e.rv > rv_a for e in evs) and [e.rv for e in evs] == sorted(e.rv for e in evs)
+    assert store.events_since(mi_rt, store.rv) == []
+    mid = evs[2].rv
+    assert [e.obj["spec"]["replicas"] for e in store.events_since(mi_rt, mid)] == [5, 6]
