@@ -452,11 +452,13 @@ def main() -> int:
                                        "queue_wait_ms": [], "pass_ms": [],
                                        "status_to_client_ms": []}
         by_n: dict[int, list[dict]] = {}
+        matched: dict[int, dict] = {}  # id(cycle) -> its claiming pass
         for cy in cycles:
             hit = [t for t in claim_traces if cy["patchAt"] <= t["start"] <= cy["readyAtWall"]]
             if not hit:
                 continue
             t = min(hit, key=lambda x: x["start"])
+            matched[id(cy)] = t
             by_n.setdefault(cy["n"], []).append(t)
             e2e["patch_to_pass_ms"].append((t["start"] - cy["patchAt"]) * 1e3)
             if cy.get("patchRttMs") is not None:  # the client's PATCH request -> response
@@ -468,6 +470,26 @@ def main() -> int:
             e2e["status_to_client_ms"].append(
                 (cy["readyAtWall"] - t["start"]) * 1e3 - t["totalMs"])
         span_per_n = {str(k): _span_p50(v) for k, v in sorted(by_n.items())}
+        # where the slowest timed cycle's time went (an outlier's cause is otherwise invisible in
+        # the medians): its client-side latency split and its claiming pass's spans
+        slowest = None
+        if cycles:
+            cy = max(cycles, key=lambda x: x["readySeconds"])
+            slowest = {"n": cy["n"], "ready_ms": round(cy["readySeconds"] * 1e3, 3),
+                       "patch_rtt_ms": round(cy.get("patchRttMs") or 0.0, 3),
+                       "probe_ms": cy.get("probeMs")}
+            t = matched.get(id(cy))
+            if t is not None:
+                per: dict[str, float] = {}
+                for sp in t["spans"]:
+                    per[sp["name"]] = round(per.get(sp["name"], 0.0) + sp["ms"], 3)
+                slowest.update({
+                    "patch_to_pass_ms": round((t["start"] - cy["patchAt"]) * 1e3, 3),
+                    "queue_wait_ms": (t.get("attrs") or {}).get("queueWaitMs"),
+                    "pass_ms": round(t["totalMs"], 3),
+                    "status_to_client_ms": round((cy["readyAtWall"] - t["start"]) * 1e3
+                                                 - t["totalMs"], 3),
+                    "pass_spans_ms": per})
         e2e_p50 = {k2: round(statistics.median(v), 3) for k2, v in e2e.items() if v}
         e2e_p50["cycles_matched"] = len(e2e["pass_ms"])
         done = [k for k in sweep if per_n[str(k)]["p50_s"] is not None]
@@ -527,6 +549,7 @@ def main() -> int:
                 "claim_pass_span_p50_ms": span_per_n.get(str(value_n), {}),
                 "claim_pass_span_p50_ms_per_n": span_per_n,
                 "e2e_breakdown_p50_ms": e2e_p50,
+                "slowest_cycle": slowest,
                 "budget": {"budget_s": args.budget_s,
                            "used_s": round(time.monotonic() - t_main, 2),
                            "skipped": skipped},

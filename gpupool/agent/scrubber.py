@@ -144,7 +144,10 @@ class HbmScrubber:
             # sweep buffer is held or while the driver clears it after the free (seconds).
             if o is not None:
                 self.agent.prober.warm_arena(o)
-            if o is None or self.agent.prober._hip.sweep_alloc(o, self.reserve_bytes) < 0:
+            rc = -1 if o is None else self.agent.prober._hip.sweep_alloc(o, self.reserve_bytes)
+            if rc < 0:
+                if rc == -3:  # freed VRAM still being cleared (by us or a pod): the grace restarts
+                    log.info("HBM sweep of %s deferred: the driver is still clearing freed VRAM", uuid)
                 self._release(uuid)
                 return False
             log.info("HBM sweep buffer of %s allocated in %.1f ms", uuid,
@@ -180,7 +183,6 @@ class HbmScrubber:
                 time.monotonic() - self._released_at.get(uuid, -1e9) < self.CLEAR_GRACE_S:
             return rec  # the driver may still be clearing this GPU's previous buffer
         if not self._hold(uuid):
-            log.warning("HBM sweep buffer allocation failed on %s", uuid)
             return rec
         try:
             for _ in range(windows or self.windows_per_pass):

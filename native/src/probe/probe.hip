@@ -399,7 +399,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_mfma_nt(const short
 //     source address and the same involution on the read (rule 21);
 //   * one block per CU at N=4096 (256 tiles), XCD-aware bijective remap (T1).
 constexpr int G2_BM = 256, G2_BN = 256, G2_BK = 64;
-constexpr int kGemmGroupM = 0;  // tile order of gemm_bf16_mfma_256: 0 row-major, >1 grouped (A/B pending)
+// Tile order of gemm_bf16_mfma_256: 0 row-major, > 1 grouped. Groups of 4 tile rows: 8192^3 1331 vs
+// 1118 TFLOP/s (+19 %), 4096^3 unchanged (1366 vs 1372) (profiles/r4q_probe_gemm_group_ab.json).
+constexpr int kGemmGroupM = 4;
 constexpr int kGemm2Threads = 512;
 constexpr int G2_STAGE_SHORTS = (G2_BM + G2_BN) * G2_BK;  // one stage: A then B, 64 KiB
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -1357,6 +1359,16 @@ void yield_to_probes(int dev) {
     std::this_thread::sleep_for(std::chrono::microseconds(200));
 }
 
+// A 4 GiB chunk maps in ~0.25 ms (the whole ~282 GiB buffer in 12-22 ms) unless the driver is still
+// clearing VRAM freed shortly before (by this process or another): then the allocation takes ~6 s
+// and stalls every probe of the device behind it (profiles/r4q_sweep_yield.json). A chunk slower
+// than this aborts the lock-free sweep allocation; the scrubber tries again later.
+constexpr double kSweepSlowChunkMs = 20.0;
+
+struct SweepBusy : ProbeError {
+  using ProbeError::ProbeError;
+};
+
 SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
   size_t free_b = 0, total_b = 0;
   PROBE_CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -1367,6 +1379,7 @@ SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
   for (uint64_t at = 0; at < span; at += kSweepChunk) {
     void* p = nullptr;
     yield_to_probes(yield_dev);
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipMalloc(&p, std::min<uint64_t>(kSweepChunk, span - at));
     if (e != hipSuccess) {
       for (void* q : b.chunks) (void)hipFree(q);
@@ -1374,6 +1387,12 @@ SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
       throw ProbeError(std::string("sweep chunk hipMalloc: ") + hipGetErrorString(e));
     }
     b.chunks.push_back(p);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    static const bool no_yield = std::getenv("GPUPOOL_SWEEP_NO_YIELD") != nullptr;  // in-process A/B only
+    if (yield_dev >= 0 && !no_yield && ms > kSweepSlowChunkMs) {  // the driver is clearing: retry later
+      for (void* q : b.chunks) (void)hipFree(q);
+      throw SweepBusy("sweep chunk took " + std::to_string(static_cast<int>(ms)) + " ms: VRAM still being cleared");
+    }
   }
   b.span = span;
   return b;
@@ -1601,6 +1620,9 @@ int mi355x_probe_sweep_alloc(int dev, long long reserve) {
   try {
     if (hipSetDevice(dev) != hipSuccess) return -1;
     b = sweep_alloc_raw(static_cast<uint64_t>(std::max(0LL, reserve)), dev);
+  } catch (const SweepBusy&) {
+    (void)hipGetLastError();
+    return -3;  // the driver is still clearing freed VRAM: nothing held, try again later
   } catch (const std::exception&) {
     (void)hipGetLastError();
     return -2;

@@ -3,8 +3,9 @@
 at the same time on the same GPU? Claim-time probes (1 GiB, 2048^3 overlapped), one every ~10 ms
 (a burst of claims), alone, while another thread frees the sweep buffer (4 GiB chunks) and while it
 allocates it again right after the free (the driver is still clearing the freed VRAM: the slow
-case). ``GPUPOOL_SWEEP_NO_YIELD=1`` turns off the chunk loop's yielding to running probes (run the
-script once with, once without).
+case; sweep_alloc now gives up with -3 when a chunk maps slower than 20 ms). ``GPUPOOL_SWEEP_NO_YIELD=1``
+turns off the chunk loop's yielding to running probes and that give-up (run the script once with,
+once without).
 
     python scripts/probe_during_sweep_free.py > gpurun_out/probe_during_sweep_free.json
 """
@@ -22,10 +23,12 @@ from gpupool.ops import probe  # noqa: E402
 
 probe.init()
 opts = dict(hbm_bytes=1 << 30, gemm_n=2048, overlap=1)
+last_rc = None
 assert probe.run(0, **opts)["passed"]
 
 
 def probes_while(fn, gap_s: float = 0.01) -> tuple[list[float], float]:
+    global last_rc
     out: list[float] = []
     box = {}
 
@@ -42,6 +45,7 @@ def probes_while(fn, gap_s: float = 0.01) -> tuple[list[float], float]:
         out.append((time.perf_counter() - t) * 1e3)  # wall, incl. any wait for the device
         time.sleep(gap_s)
     th.join()
+    last_rc = box["rc"]
     return out, box["ms"]
 
 
@@ -57,12 +61,12 @@ for rnd in range(2):
     d, ms = probes_while(lambda: probe.sweep_release(0))
     res[f"during_free_{rnd}"] = {**stats(d), "freeMs": round(ms, 1)}
     d, ms = probes_while(lambda: probe.sweep_alloc(0, 4 << 30))  # right after the free: clearing
-    res[f"during_alloc_after_free_{rnd}"] = {**stats(d), "allocMs": round(ms, 1)}
+    res[f"during_alloc_after_free_{rnd}"] = {**stats(d), "allocMs": round(ms, 1), "rc": last_rc}
     d, ms = probes_while(lambda: probe.sweep_release(0))
     res[f"during_free_b_{rnd}"] = {**stats(d), "freeMs": round(ms, 1)}
     time.sleep(8)  # the driver finishes clearing
     d, ms = probes_while(lambda: probe.sweep_alloc(0, 4 << 30))  # after the clear: the scrubber's case
-    res[f"during_alloc_cleared_{rnd}"] = {**stats(d), "allocMs": round(ms, 1)}
+    res[f"during_alloc_cleared_{rnd}"] = {**stats(d), "allocMs": round(ms, 1), "rc": last_rc}
     assert probe.sweep_release(0) >= 0
     time.sleep(8)
 probe.trim(0)

@@ -104,3 +104,15 @@ def test_no_new_sweep_buffer_while_the_driver_clears_the_last_one():
     s._released_at[UUID] -= s.CLEAR_GRACE_S
     s.scrub_device(UUID)
     assert [k for k, _ in hip.calls] == ["alloc", "release", "alloc", "release"]
+
+
+def test_sweep_deferred_while_the_driver_clears_freed_vram():
+    """sweep_alloc -3: a chunk mapped slowly because freed VRAM is still being cleared; nothing is
+    held, and the scrubber waits out the clear grace before trying this GPU again."""
+    agent, hip = fake_agent()
+    s = HbmScrubber(agent, window_bytes=1 << 20, windows_per_pass=1)
+    hip.sweep_alloc = lambda o, r: (hip.calls.append(("alloc", time.monotonic())), -3)[1]
+    s.scrub_device(UUID)
+    assert [k for k, _ in hip.calls] == ["alloc", "release"] and not s._held
+    s.scrub_device(UUID)  # within the grace: not even tried
+    assert [k for k, _ in hip.calls] == ["alloc", "release"]
