@@ -48,7 +48,7 @@ char* mi355x_probe_hbm_sweep(int device, const char* opts_json);
 /* Allocate / free the sweep buffer without holding the device's probe lock (allocating ~282 GiB
  * takes ~0.4 s and freeing it ~2.9 s on MI355X: a claim-time probe must never wait for either).
  * alloc: 1 = allocated, 0 = already held, -3 = the driver is still clearing recently freed VRAM
- * (a chunk took over 20 ms; nothing is held — try later), other <0 = error. Between chunks both
+ * (two chunks in a row took over 20 ms; nothing is held — try later), other <0 = error. Between chunks both
  * wait while a claim-time probe of the device runs. release: 1 = freed, 0 = none held. */
 int mi355x_probe_sweep_alloc(int device, long long reserve_bytes);
 int mi355x_probe_sweep_release(int device);

@@ -1361,8 +1361,8 @@ void yield_to_probes(int dev) {
 
 // A 4 GiB chunk maps in ~0.25 ms (the whole ~282 GiB buffer in 12-22 ms) unless the driver is still
 // clearing VRAM freed shortly before (by this process or another): then the allocation takes ~6 s
-// and stalls every probe of the device behind it (profiles/r4q_sweep_yield.json). A chunk slower
-// than this aborts the lock-free sweep allocation; the scrubber tries again later.
+// and stalls every probe of the device behind it (profiles/r4q_sweep_yield.json). Two chunks in a
+// row slower than this abort the lock-free sweep allocation; the scrubber tries again later.
 constexpr double kSweepSlowChunkMs = 20.0;
 
 struct SweepBusy : ProbeError {
@@ -1376,6 +1376,7 @@ SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
   if (free_b <= reserve + gran) throw ProbeError("not enough free HBM for a sweep window");
   SweepBuf b;
   const uint64_t span = ((free_b - reserve) / gran) * gran;
+  int slow = 0;
   for (uint64_t at = 0; at < span; at += kSweepChunk) {
     void* p = nullptr;
     yield_to_probes(yield_dev);
@@ -1389,9 +1390,13 @@ SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
     b.chunks.push_back(p);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     static const bool no_yield = std::getenv("GPUPOOL_SWEEP_NO_YIELD") != nullptr;  // in-process A/B only
-    if (yield_dev >= 0 && !no_yield && ms > kSweepSlowChunkMs) {  // the driver is clearing: retry later
+    static const bool trace = std::getenv("GPUPOOL_SWEEP_TRACE") != nullptr;        // chunk timings
+    if (trace) std::fprintf(stderr, "sweep chunk %zu: %.3f ms\n", b.chunks.size() - 1, ms);
+    // two slow chunks in a row: the driver is clearing (one slow chunk alone can be a first-use cost)
+    slow = ms > kSweepSlowChunkMs ? slow + 1 : 0;
+    if (yield_dev >= 0 && !no_yield && slow >= 2) {
       for (void* q : b.chunks) (void)hipFree(q);
-      throw SweepBusy("sweep chunk took " + std::to_string(static_cast<int>(ms)) + " ms: VRAM still being cleared");
+      throw SweepBusy("sweep chunks took " + std::to_string(static_cast<int>(ms)) + " ms: VRAM still being cleared");
     }
   }
   b.span = span;

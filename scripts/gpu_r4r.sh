@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r4r
 export PYTHONPATH=$GRAFT_REPO_ROOT
-timeout -k 10 300 python -u scripts/probe_during_sweep_free.py > gpurun_out/r4r/sweep_giveup.json 2> gpurun_out/r4r/sweep_giveup.err && \
+GPUPOOL_SWEEP_TRACE=1 timeout -k 10 300 python -u scripts/probe_during_sweep_free.py > gpurun_out/r4r/sweep_giveup.json 2> gpurun_out/r4r/sweep_giveup.err && \
 GPUPOOL_SWEEP_NO_YIELD=1 timeout -k 10 300 python -u scripts/probe_during_sweep_free.py > gpurun_out/r4r/sweep_nogiveup.json 2> gpurun_out/r4r/sweep_nogiveup.err && \
 timeout -k 10 900 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu tests > gpurun_out/r4r/pytest_gpu.txt 2>&1 && \
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4r/smoke.txt 2>&1 && \

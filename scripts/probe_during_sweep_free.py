@@ -57,7 +57,14 @@ def stats(xs: list[float]) -> dict:
 res = {"yield": os.environ.get("GPUPOOL_SWEEP_NO_YIELD") is None,
        "alone": stats([probe.run(0, **opts)["ms"] for _ in range(100)])}
 for rnd in range(2):
-    assert probe.sweep_alloc(0, 4 << 30) >= 0
+    t = time.perf_counter()
+    rc = probe.sweep_alloc(0, 4 << 30)
+    res[f"first_alloc_{rnd}"] = {"rc": rc, "ms": round((time.perf_counter() - t) * 1e3, 1)}
+    if rc < 0:  # the driver is still clearing what an earlier process freed: wait and retry once
+        time.sleep(10)
+        rc = probe.sweep_alloc(0, 4 << 30)
+        res[f"first_alloc_retry_{rnd}"] = {"rc": rc}
+    assert rc >= 0, res
     d, ms = probes_while(lambda: probe.sweep_release(0))
     res[f"during_free_{rnd}"] = {**stats(d), "freeMs": round(ms, 1)}
     d, ms = probes_while(lambda: probe.sweep_alloc(0, 4 << 30))  # right after the free: clearing
