@@ -210,6 +210,10 @@ class Agent:
                              arena_idle_s=cfg.probe_arena_idle_s,
                              overlap_gemm_n=cfg.probe_overlap_gemm_n)
         self.last_probe: dict[str, dict] = {}
+        # uuid -> monotonic time its VRAM was last freed wholesale (a release after its pods ended;
+        # agent start: the previous agent process's allocations): the driver clears freed VRAM for
+        # seconds, and the HBM scrubber must not map its sweep buffer into that (scrubber.py)
+        self.freed_at: dict[str, float] = {u: time.monotonic() for u in self.by_uuid}
         self._probe_mono: dict[str, float] = {}  # uuid -> monotonic time of its last probe
         # admin maintenance (gpuctl gpu cordon): uuid -> reason; persisted as a quarantine entry
         # without expiry so it survives agent restarts
@@ -1505,6 +1509,7 @@ class Agent:
                                                               write=False))
                 del self.records[u]
                 released.append(u)
+                self.freed_at[u] = time.monotonic()  # its pods' VRAM was just freed (scrubber)
             if released:
                 seq = self.ledger.commit(self.records, durable=False)
             self.stats["releases"] += len(released)
@@ -2130,7 +2135,7 @@ def build_routes(agent: Agent) -> dict:
                      if ref in (u, d.get("hipUUID"), str(d.get("index")))), None)
         if uuid is None:
             return json_reply({"ok": False, "reason": "NotFound"}, 404)
-        rec = agent.scrubber.scrub_device(uuid, int(b.get("windows") or 1))
+        rec = agent.scrubber.scrub_device(uuid, int(b.get("windows") or 1), grace=False)
         return json_reply({"ok": True, "uuid": uuid, "coverage": agent.scrubber.coverage(uuid),
                            "record": rec})
 

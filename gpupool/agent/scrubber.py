@@ -35,7 +35,11 @@ log = logging.getLogger("gpupool.agent.scrubber")
 
 
 class HbmScrubber:
-    CLEAR_GRACE_S = 30.0  # no new sweep buffer on a GPU this soon after freeing its last one
+    # No sweep buffer on a GPU this soon after VRAM was freed there (our last buffer, a released
+    # pool's pods, the previous agent process): the driver clears freed VRAM (~6 s for ~282 GiB)
+    # and an allocation issued meanwhile blocks, a probe of that GPU behind it (6.0 s measured,
+    # profiles/r4q_sweep_yield.json)
+    CLEAR_GRACE_S = 30.0
 
     def __init__(self, agent, interval_s: float = 60.0, window_bytes: int = 4 << 30,
                  windows_per_pass: int = 8, reserve_bytes: int = 4 << 30,
@@ -144,10 +148,8 @@ class HbmScrubber:
             # sweep buffer is held or while the driver clears it after the free (seconds).
             if o is not None:
                 self.agent.prober.warm_arena(o)
-            rc = -1 if o is None else self.agent.prober._hip.sweep_alloc(o, self.reserve_bytes)
-            if rc < 0:
-                if rc == -3:  # freed VRAM still being cleared (by us or a pod): the grace restarts
-                    log.info("HBM sweep of %s deferred: the driver is still clearing freed VRAM", uuid)
+            if o is None or self.agent.prober._hip.sweep_alloc(o, self.reserve_bytes) < 0:
+                log.warning("HBM sweep buffer allocation failed on %s", uuid)
                 self._release(uuid)
                 return False
             log.info("HBM sweep buffer of %s allocated in %.1f ms", uuid,
@@ -170,8 +172,9 @@ class HbmScrubber:
                 self._released_at[uuid] = time.monotonic()
                 self._cv.notify_all()
 
-    def scrub_device(self, uuid: str, windows: int | None = None) -> dict:
-        """One pass over ``windows`` windows of one GPU; returns its coverage record."""
+    def scrub_device(self, uuid: str, windows: int | None = None, grace: bool = True) -> dict:
+        """One pass over ``windows`` windows of one GPU; returns its coverage record. ``grace``
+        False (an operator's explicit scrub): do not wait out CLEAR_GRACE_S."""
         lock = self._lock_for(uuid)
         with self._mu:
             rec = dict(self.state.get(uuid) or {"cursor": 0, "span": 0, "coveredBytes": 0,
@@ -179,9 +182,11 @@ class HbmScrubber:
         with self.agent.lock:
             if not self._eligible(uuid):
                 return rec
-        if self.agent.prober.mode == "inproc" and \
-                time.monotonic() - self._released_at.get(uuid, -1e9) < self.CLEAR_GRACE_S:
-            return rec  # the driver may still be clearing this GPU's previous buffer
+        if grace and self.agent.prober.mode == "inproc":
+            freed = max(self._released_at.get(uuid, -1e9),
+                        getattr(self.agent, "freed_at", {}).get(uuid, -1e9))
+            if time.monotonic() - freed < self.CLEAR_GRACE_S:
+                return rec  # the driver may still be clearing VRAM freed there (ours or a pod's)
         if not self._hold(uuid):
             return rec
         try:

@@ -148,7 +148,7 @@ def hbm_sweep(dev: int, offset: int, nbytes: int = 16 << 30, reserve: int = 4 <<
 
 def sweep_alloc(dev: int, reserve: int = 4 << 30) -> int:
     """Allocate the sweep buffer (all free HBM minus ``reserve``) without blocking probes: 1
-    allocated, 0 already held, -3 the driver is still clearing freed VRAM (nothing held)."""
+    allocated, 0 already held, < 0 error."""
     return int(lib().mi355x_probe_sweep_alloc(dev, int(reserve)))
 
 

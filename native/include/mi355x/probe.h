@@ -47,9 +47,8 @@ char* mi355x_probe_peer_ring(const int* devs, int n, const char* opts_json);
 char* mi355x_probe_hbm_sweep(int device, const char* opts_json);
 /* Allocate / free the sweep buffer without holding the device's probe lock (allocating ~282 GiB
  * takes ~0.4 s and freeing it ~2.9 s on MI355X: a claim-time probe must never wait for either).
- * alloc: 1 = allocated, 0 = already held, -3 = the driver is still clearing recently freed VRAM
- * (two chunks in a row took over 20 ms; nothing is held — try later), other <0 = error. Between chunks both
- * wait while a claim-time probe of the device runs. release: 1 = freed, 0 = none held. */
+ * alloc: 1 = allocated, 0 = already held, <0 = error. Both work in 1 GiB chunks and wait between
+ * chunks while a claim-time probe of the device runs. release: 1 = freed, 0 = none held. */
 int mi355x_probe_sweep_alloc(int device, long long reserve_bytes);
 int mi355x_probe_sweep_release(int device);
 /* The probe's production GEMM (256x256x64 MFMA tile) on caller HOST buffers (copied in and out):

@@ -677,8 +677,10 @@ static_assert(2 * kMaxPatterns <= kHbmThreads, "hbm_fill resets the HBM pairs fr
 // one huge mapping held the process's address-space lock for ~2.5 s, and every thread of the agent
 // that mapped memory meanwhile (a thread start, a large malloc) stalled behind it — a claim issued
 // right after a scrub waited 2.46 s (profiles/r2o_scrub_claim_diag.txt). Per chunk the stall is
-// bounded by one 4 GiB unmap.
-constexpr uint64_t kSweepChunk = 4ull << 30;
+// bounded by one chunk's unmap. 1 GiB: VRAM that an earlier process used is cleared as it is mapped
+// again, at ~35 GB/s — 121 ms per 4 GiB chunk on a box whose last tenant left 90 GiB dirty
+// (profiles/r4r_sweep_chunks.txt) — and a claim-time probe that arrives mid-chunk waits for it.
+constexpr uint64_t kSweepChunk = 1ull << 30;
 
 struct SweepBuf {
   std::vector<void*> chunks;  // kSweepChunk bytes each, the last one possibly shorter
@@ -1340,8 +1342,8 @@ std::string run_peer_ring(const std::vector<int>& devs, const char* opts) {
 // Claim-time probes running per device (mi355x_probe_run). Mapping or unmapping the sweep buffer
 // stalls a probe that runs beside it — up to the whole 6 s allocation when the driver is still
 // clearing the previous buffer, 5-211 ms per chunk otherwise (profiles/r4p_probe_during_sweep_free.json)
-// — so the lock-free sweep alloc / free paths wait between 4 GiB chunks while a probe runs: a
-// probe then shares the device with at most one chunk operation.
+// — so the lock-free sweep alloc / free paths wait between chunks while a probe runs: a probe then
+// shares the device with at most one chunk operation (the scrubber avoids the pending clear).
 std::atomic<int> g_probes_active[64];
 
 struct ProbeActive {
@@ -1359,16 +1361,6 @@ void yield_to_probes(int dev) {
     std::this_thread::sleep_for(std::chrono::microseconds(200));
 }
 
-// A 4 GiB chunk maps in ~0.25 ms (the whole ~282 GiB buffer in 12-22 ms) unless the driver is still
-// clearing VRAM freed shortly before (by this process or another): then the allocation takes ~6 s
-// and stalls every probe of the device behind it (profiles/r4q_sweep_yield.json). Two chunks in a
-// row slower than this abort the lock-free sweep allocation; the scrubber tries again later.
-constexpr double kSweepSlowChunkMs = 20.0;
-
-struct SweepBusy : ProbeError {
-  using ProbeError::ProbeError;
-};
-
 SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
   size_t free_b = 0, total_b = 0;
   PROBE_CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -1376,7 +1368,6 @@ SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
   if (free_b <= reserve + gran) throw ProbeError("not enough free HBM for a sweep window");
   SweepBuf b;
   const uint64_t span = ((free_b - reserve) / gran) * gran;
-  int slow = 0;
   for (uint64_t at = 0; at < span; at += kSweepChunk) {
     void* p = nullptr;
     yield_to_probes(yield_dev);
@@ -1389,15 +1380,8 @@ SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
     }
     b.chunks.push_back(p);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    static const bool no_yield = std::getenv("GPUPOOL_SWEEP_NO_YIELD") != nullptr;  // in-process A/B only
     static const bool trace = std::getenv("GPUPOOL_SWEEP_TRACE") != nullptr;        // chunk timings
     if (trace) std::fprintf(stderr, "sweep chunk %zu: %.3f ms\n", b.chunks.size() - 1, ms);
-    // two slow chunks in a row: the driver is clearing (one slow chunk alone can be a first-use cost)
-    slow = ms > kSweepSlowChunkMs ? slow + 1 : 0;
-    if (yield_dev >= 0 && !no_yield && slow >= 2) {
-      for (void* q : b.chunks) (void)hipFree(q);
-      throw SweepBusy("sweep chunks took " + std::to_string(static_cast<int>(ms)) + " ms: VRAM still being cleared");
-    }
   }
   b.span = span;
   return b;
@@ -1625,9 +1609,6 @@ int mi355x_probe_sweep_alloc(int dev, long long reserve) {
   try {
     if (hipSetDevice(dev) != hipSuccess) return -1;
     b = sweep_alloc_raw(static_cast<uint64_t>(std::max(0LL, reserve)), dev);
-  } catch (const SweepBusy&) {
-    (void)hipGetLastError();
-    return -3;  // the driver is still clearing freed VRAM: nothing held, try again later
   } catch (const std::exception&) {
     (void)hipGetLastError();
     return -2;

@@ -106,13 +106,14 @@ def test_no_new_sweep_buffer_while_the_driver_clears_the_last_one():
     assert [k for k, _ in hip.calls] == ["alloc", "release", "alloc", "release"]
 
 
-def test_sweep_deferred_while_the_driver_clears_freed_vram():
-    """sweep_alloc -3: a chunk mapped slowly because freed VRAM is still being cleared; nothing is
-    held, and the scrubber waits out the clear grace before trying this GPU again."""
+def test_no_sweep_buffer_soon_after_a_release_freed_the_gpus_vram():
+    """A GPU released by its pool (its pods' VRAM just freed) or seen at agent start is not
+    scrubbed until the clear grace has passed since then."""
     agent, hip = fake_agent()
+    agent.freed_at = {UUID: time.monotonic()}
     s = HbmScrubber(agent, window_bytes=1 << 20, windows_per_pass=1)
-    hip.sweep_alloc = lambda o, r: (hip.calls.append(("alloc", time.monotonic())), -3)[1]
     s.scrub_device(UUID)
-    assert [k for k, _ in hip.calls] == ["alloc", "release"] and not s._held
-    s.scrub_device(UUID)  # within the grace: not even tried
+    assert hip.calls == []
+    agent.freed_at[UUID] -= s.CLEAR_GRACE_S
+    s.scrub_device(UUID)
     assert [k for k, _ in hip.calls] == ["alloc", "release"]
