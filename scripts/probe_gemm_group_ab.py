@@ -21,7 +21,8 @@ rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 9
 groups = (0, 2, 4, 8, 16)
 probe.init()
 res: dict[str, list[float]] = {}
-for n in (4096, 8192):
+sizes = tuple(int(x) for x in os.environ.get("GROUP_AB_SIZES", "4096,8192").split(","))
+for n in sizes:
     for g in groups:  # warm every variant once
         assert probe.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, overlap=0, gemmGroupM=g)["passed"]
     for r in range(rounds):
