@@ -409,6 +409,8 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // byte offset, inside a [rows][64] bf16 tile (128-B rows), of logical 16-B chunk c of row r
 __device__ __forceinline__ int g2_swz(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
+// kPrio: s_setprio(1) around each K-step's MFMA block (cdna_hip_programming.md T5; in-process A/B)
+template <bool kPrio = false>
 __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const short* __restrict__ A,
                                                                        const short* __restrict__ Bt,
                                                                        float* __restrict__ C, int M,
@@ -486,11 +488,13 @@ __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const sho
 #pragma unroll
       for (int m = 0; m < 8; ++m)
         af[m] = *reinterpret_cast<const bf16x8*>(as + g2_swz(wr * 128 + m * 16 + fr, c));
+      if constexpr (kPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int m = 0; m < 8; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+      if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt+1 has landed
     __syncthreads();                                   // ...and every other wave's; reads of kt done
@@ -796,7 +800,7 @@ std::string hip_uuid(int dev) {
 // ctx.gev[0..1]) with exact u32 (mod 2^32) ABFT row/column checksums, then copies the two mismatch
 // counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``. zero_mfma: the operand
 // kernels zero the phase's counters cnt[kSlotSmall..kResSlots) and ABFT accumulators themselves.
-void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int group_m, int reps, int inject_gemm,
+void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, bool prio, int group_m, int reps, int inject_gemm,
                        int census_fault_xcc, bool zero_mfma, bool poison_c, unsigned long long* cnt,
                        unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
   const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
@@ -816,9 +820,12 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int group_m, int r
   auto* c = reinterpret_cast<float*>(carve(n * n * 4));
   auto* v = reinterpret_cast<unsigned long long*>(carve(6 * n * 8));
   auto gemm = [&](const short* a_, const short* b_, float* c_, int nn, unsigned long long* cu_map) {
-    if (tile256)
-      hipLaunchKernelGGL(gemm_bf16_mfma_256, dim3((nn / G2_BM) * (nn / G2_BN)), dim3(kGemm2Threads), 0, s, a_, b_, c_, nn,
-                         nn, nn, cu_map, group_m);
+    if (tile256 && prio)
+      hipLaunchKernelGGL(gemm_bf16_mfma_256<true>, dim3((nn / G2_BM) * (nn / G2_BN)), dim3(kGemm2Threads), 0, s, a_, b_,
+                         c_, nn, nn, nn, cu_map, group_m);
+    else if (tile256)
+      hipLaunchKernelGGL(gemm_bf16_mfma_256<false>, dim3((nn / G2_BM) * (nn / G2_BN)), dim3(kGemm2Threads), 0, s, a_, b_,
+                         c_, nn, nn, nn, cu_map, group_m);
     else
       hipLaunchKernelGGL(gemm_bf16_mfma_nt, dim3((nn / BM) * (nn / BN)), dim3(kGemmThreads), 0, s, a_, b_, c_, nn, nn, nn);
   };
@@ -908,6 +915,7 @@ std::string run_probe(int dev, const char* opts) {
   const int inject_gemm = static_cast<int>(opt_int(opts, "injectGemmFault", 0));
   const bool tile256 = opt_int(opts, "gemmTile", 256) != 128;  // 128 = the older 128x128 kernel (A/B)
   const int group_m = static_cast<int>(opt_int(opts, "gemmGroupM", kGemmGroupM));  // tile order (A/B)
+  const bool gemm_prio = opt_int(opts, "gemmPrio", 0) != 0;                        // s_setprio (A/B)
   const bool poison_c = opt_int(opts, "poisonC", 0) != 0;                           // test hook
   // The HBM test is bandwidth-bound with few waves per CU; the MFMA phase is compute-bound and
   // touches ~130 MiB: run them concurrently on two streams (overlap=0: one stream, serial).
@@ -1006,7 +1014,7 @@ std::string run_probe(int dev, const char* opts) {
   // earlier on the GPU while the rest of the HBM test is still enqueued well ahead of need.
   const int hbm_first = static_cast<int>(opt_int(opts, "hbmFirst", 1));
   if (do_mfma && hbm_first == 0)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                       ctx, s2);
 
   // ---------------- HBM: all patterns back to back, per-pattern counters
@@ -1037,7 +1045,7 @@ std::string run_probe(int dev, const char* opts) {
       hipLaunchKernelGGL(hbm_fill<0>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip, reset, nreset);
     PROBE_CHECK(hipEventRecord(ctx.ev[1 + 2 * pi], s));
     if (pi == 0 && do_mfma && hbm_first == 2)
-      launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
+      launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                         ctx, s2);
     if (pi == 0 && inject_flips > 0)
       hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(hbm), n16 * 4,
@@ -1056,7 +1064,7 @@ std::string run_probe(int dev, const char* opts) {
   PROBE_CHECK(hipGetLastError());
   PROBE_CHECK(hipMemcpyAsync(hres, cnt, 2 * patterns * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   if (do_mfma && hbm_first == 1)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                       ctx, s2);
   const double launch_ms = ms_since(t_run);  // host time to enqueue the whole probe
   PROBE_CHECK(hipStreamSynchronize(s));
@@ -1653,7 +1661,7 @@ int mi355x_probe_gemm_bf16(int dev, const void* A, const void* Bt, void* C, int 
     PROBE_CHECK(hipMalloc(&dc.p, sc));
     PROBE_CHECK(hipMemcpy(da.p, A, sa, hipMemcpyHostToDevice));
     PROBE_CHECK(hipMemcpy(db.p, Bt, sb, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(gemm_bf16_mfma_256, dim3((m / G2_BM) * (n / G2_BN)), dim3(kGemm2Threads), 0, nullptr,
+    hipLaunchKernelGGL(gemm_bf16_mfma_256<false>, dim3((m / G2_BM) * (n / G2_BN)), dim3(kGemm2Threads), 0, nullptr,
                        static_cast<const short*>(da.p), static_cast<const short*>(db.p), static_cast<float*>(dc.p), m, n,
                        k, static_cast<unsigned long long*>(nullptr), kGemmGroupM);
     PROBE_CHECK(hipGetLastError());

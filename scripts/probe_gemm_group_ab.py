@@ -18,20 +18,25 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gpupool.ops import probe  # noqa: E402
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 9
-groups = (0, 2, 4, 8, 16)
+# variants: "gN" = gemmGroupM N; "pN" = gemmGroupM N with s_setprio around the MFMA block
+variants = tuple(os.environ.get("GROUP_AB_VARIANTS", "g0,g2,g4,g8,g16").split(","))
+
+
+def opts_of(v: str) -> dict:
+    return {"gemmGroupM": int(v[1:]), "gemmPrio": int(v[0] == "p")}
 probe.init()
 res: dict[str, list[float]] = {}
 sizes = tuple(int(x) for x in os.environ.get("GROUP_AB_SIZES", "4096,8192").split(","))
 for n in sizes:
-    for g in groups:  # warm every variant once
-        assert probe.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, overlap=0, gemmGroupM=g)["passed"]
+    for g in variants:  # warm every variant once
+        assert probe.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, overlap=0, **opts_of(g))["passed"]
     for r in range(rounds):
-        order = groups if r % 2 == 0 else tuple(reversed(groups))
+        order = variants if r % 2 == 0 else tuple(reversed(variants))
         for g in order:
             out = probe.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemm_reps=10, overlap=0,
-                            gemmGroupM=g)
+                            **opts_of(g))
             assert out["passed"] and out["mfma"]["abftMismatches"] == 0, (n, g, out)
-            res.setdefault(f"{n}:g{g}", []).append(round(out["mfma"]["tflops"], 1))
+            res.setdefault(f"{n}:{g}", []).append(round(out["mfma"]["tflops"], 1))
 probe.trim(0)
 summary = {k: {"median": statistics.median(v), "min": min(v), "max": max(v)} for k, v in res.items()}
 print(json.dumps({"rounds": rounds, "summary": summary, "samples": res}, indent=1))
