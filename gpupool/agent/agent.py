@@ -446,6 +446,8 @@ class Agent:
             self.verdicts[uuid] = v
         return changed
 
+    FREED_VRAM_BYTES = 1 << 30  # a drop in VRAM in use above this between samples counts as a free
+
     def sample(self) -> set[str]:
         t0 = time.perf_counter()
         snap = self.dev.snapshot()
@@ -455,6 +457,13 @@ class Agent:
         except Exception:  # accounting is telemetry: never fail a health sample for it
             log.exception("per-pod GPU accounting failed")
         with self.lock:
+            now = time.monotonic()
+            for d in snap["devices"]:  # VRAM freed wholesale by any process (pod or not): the
+                old = (self.by_uuid.get(d["uuid"]) or {}).get("memUsedBytes")  # driver clears it
+                new = d.get("memUsedBytes")                                     # for seconds
+                if isinstance(old, (int, float)) and isinstance(new, (int, float)) and \
+                        old - new > self.FREED_VRAM_BYTES:
+                    self.freed_at[d["uuid"]] = now
             self.snap = snap
             self.by_uuid = {d["uuid"]: d for d in snap["devices"]}
             changed = self._evaluate_all()

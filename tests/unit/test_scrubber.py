@@ -117,3 +117,26 @@ def test_no_sweep_buffer_soon_after_a_release_freed_the_gpus_vram():
     agent.freed_at[UUID] -= s.CLEAR_GRACE_S
     s.scrub_device(UUID)
     assert [k for k, _ in hip.calls] == ["alloc", "release"]
+
+
+def test_agent_notes_vram_freed_by_any_process(tmp_path):
+    """A drop of VRAM in use between two samples (a process outside any pool freed memory) marks
+    the GPU freed, so the scrubber waits out the driver's clear there too."""
+    import json
+    import os
+    from gpupool.agent.agent import Agent, AgentConfig
+    fixture = os.path.join(os.path.dirname(os.path.dirname(__file__)), "fixtures", "node_8x_mi355x.json")
+    faults = tmp_path / "faults.json"
+    faults.write_text("{}")
+    a = Agent(AgentConfig(node="n0", backend="fake", fixture=fixture, state_dir=str(tmp_path / "s"),
+                          probe_mode="simulated", probe_sim_ms=0.1, fsync=False, faults=str(faults),
+                          scrub_interval_s=0))
+    u = next(iter(a.by_uuid))
+    a.freed_at[u] = 0.0
+    idx = str(a.by_uuid[u]["index"])
+    faults.write_text(json.dumps({"devices": {idx: {"memUsedBytes": 200 << 30}}}))
+    a.sample()
+    assert a.freed_at[u] == 0.0 and a.by_uuid[u]["memUsedBytes"] == 200 << 30
+    faults.write_text(json.dumps({"devices": {idx: {"memUsedBytes": 1 << 30}}}))
+    a.sample()
+    assert a.freed_at[u] > 0.0
