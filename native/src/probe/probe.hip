@@ -409,7 +409,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // byte offset, inside a [rows][64] bf16 tile (128-B rows), of logical 16-B chunk c of row r
 __device__ __forceinline__ int g2_swz(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
-// kPrio: s_setprio(1) around each K-step's MFMA block (cdna_hip_programming.md T5; in-process A/B)
+// kPrio: s_setprio(1) around each K-step's MFMA block (cdna_hip_programming.md T5). Measured null on
+// this 2-phase loop (4096^3 1246 vs 1236, 8192^3 1315 vs 1312 TFLOP/s, profiles/
+// r4u_gemm_setprio_ab_rejected.json): off by default, selectable for A/B ("gemmPrio").
 template <bool kPrio = false>
 __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const short* __restrict__ A,
                                                                        const short* __restrict__ Bt,
