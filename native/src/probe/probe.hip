@@ -1354,20 +1354,23 @@ std::string run_peer_ring(const std::vector<int>& devs, const char* opts) {
 // clearing the previous buffer, 5-211 ms per chunk otherwise (profiles/r4p_probe_during_sweep_free.json)
 // — so the lock-free sweep alloc / free paths wait between chunks while a probe runs: a probe then
 // shares the device with at most one chunk operation (the scrubber avoids the pending clear).
-std::atomic<int> g_probes_active[64];
+// Counted over all devices: the HIP runtime serialises parts of an allocation process-wide, so a
+// chunk mapped on one GPU can hold up a probe launching on another (an 8-GPU node scrubs idle GPUs
+// while claims probe the others).
+std::atomic<int> g_probes_active{0};
 
 struct ProbeActive {
-  int d;
-  explicit ProbeActive(int dev) : d(dev % 64) { g_probes_active[d].fetch_add(1); }
-  ~ProbeActive() { g_probes_active[d].fetch_sub(1); }
+  ProbeActive() { g_probes_active.fetch_add(1); }
+  ~ProbeActive() { g_probes_active.fetch_sub(1); }
 };
 
-// Wait (bounded) until no probe runs on ``dev``; -1: never wait (callers holding the device lock).
+// Wait (bounded) until no claim-time probe runs in this process; dev -1: never wait (callers
+// holding a device lock).
 void yield_to_probes(int dev) {
   static const bool off = std::getenv("GPUPOOL_SWEEP_NO_YIELD") != nullptr;  // in-process A/B only
   if (dev < 0 || off) return;
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(2);
-  while (g_probes_active[dev % 64].load() > 0 && std::chrono::steady_clock::now() < deadline)
+  while (g_probes_active.load() > 0 && std::chrono::steady_clock::now() < deadline)
     std::this_thread::sleep_for(std::chrono::microseconds(200));
 }
 
@@ -1526,7 +1529,7 @@ char* mi355x_probe_identify(int dev) {
 
 char* mi355x_probe_run(int dev, const char* opts_json) {
   if (g_count < 0 || dev < 0 || dev >= g_count) return dup("{\"passed\":false,\"error\":\"bad device index\"}");
-  ProbeActive active(dev);  // the sweep buffer's chunk (un)mapping waits while this runs
+  ProbeActive active;  // the sweep buffer's chunk (un)mapping waits while this runs
   // Per-device serialisation: concurrent probes of DIFFERENT devices run in parallel.
   std::lock_guard<std::mutex> g(device_mutex(dev));
   try {
