@@ -412,7 +412,10 @@ __device__ __forceinline__ int g2_swz(int r, int c) { return r * 128 + ((c ^ ((r
 // kPrio: s_setprio(1) around each K-step's MFMA block (cdna_hip_programming.md T5). Measured null on
 // this 2-phase loop (4096^3 1246 vs 1236, 8192^3 1315 vs 1312 TFLOP/s, profiles/
 // r4u_gemm_setprio_ab_rejected.json): off by default, selectable for A/B ("gemmPrio").
-template <bool kPrio = false>
+// kVecC: the MFMA computes each 16x16 tile transposed (B fragment as the first operand), so a lane
+// holds 4 consecutive columns of one C row and the epilogue writes them as one 16-byte store
+// instead of four 4-byte ones (same MFMAs, same C; in-process A/B "gemmVecC").
+template <bool kPrio = false, bool kVecC = false>
 __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const short* __restrict__ A,
                                                                        const short* __restrict__ Bt,
                                                                        float* __restrict__ C, int M,
@@ -494,23 +497,39 @@ __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const sho
 #pragma unroll
       for (int m = 0; m < 8; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+        for (int n = 0; n < 4; ++n) {
+          if constexpr (kVecC)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[n], af[m], acc[m][n], 0, 0, 0);
+          else
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+        }
       if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt+1 has landed
     __syncthreads();                                   // ...and every other wave's; reads of kt done
   }
-  // C/D layout of 16x16x32: col = lane&15, row = 4*(lane>>4) + j
+  if constexpr (kVecC) {
+    // transposed tile: lane holds C[m*16 + (lane&15)][n*16 + 4*(lane>>4) + j], j = 0..3
 #pragma unroll
-  for (int m = 0; m < 8; ++m)
+    for (int m = 0; m < 8; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int col = tile_n * G2_BN + wc * 64 + n * 16 + fr;
-      const int row0 = tile_m * G2_BM + wr * 128 + m * 16 + 4 * fq;
+      for (int n = 0; n < 4; ++n) {
+        const int row = tile_m * G2_BM + wr * 128 + m * 16 + fr;
+        const int col0 = tile_n * G2_BN + wc * 64 + n * 16 + 4 * fq;
+        *reinterpret_cast<f32x4*>(C + static_cast<int64_t>(row) * N + col0) = acc[m][n];
+      }
+  } else {
+    // C/D layout of 16x16x32: col = lane&15, row = 4*(lane>>4) + j
 #pragma unroll
-      for (int j = 0; j < 4; ++j) C[static_cast<int64_t>(row0 + j) * N + col] = acc[m][n][j];
-    }
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int col = tile_n * G2_BN + wc * 64 + n * 16 + fr;
+        const int row0 = tile_m * G2_BM + wr * 128 + m * 16 + 4 * fq;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) C[static_cast<int64_t>(row0 + j) * N + col] = acc[m][n][j];
+      }
+  }
 }
 
 // Full VALU reference (independent of the matrix cores), fp32, k-ordered.
@@ -802,7 +821,7 @@ std::string hip_uuid(int dev) {
 // ctx.gev[0..1]) with exact u32 (mod 2^32) ABFT row/column checksums, then copies the two mismatch
 // counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``. zero_mfma: the operand
 // kernels zero the phase's counters cnt[kSlotSmall..kResSlots) and ABFT accumulators themselves.
-void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, bool prio, int group_m, int reps, int inject_gemm,
+void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, bool prio, bool vec_c, int group_m, int reps, int inject_gemm,
                        int census_fault_xcc, bool zero_mfma, bool poison_c, unsigned long long* cnt,
                        unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
   const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
@@ -822,12 +841,16 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, bool prio, int gro
   auto* c = reinterpret_cast<float*>(carve(n * n * 4));
   auto* v = reinterpret_cast<unsigned long long*>(carve(6 * n * 8));
   auto gemm = [&](const short* a_, const short* b_, float* c_, int nn, unsigned long long* cu_map) {
+    const dim3 grid((nn / G2_BM) * (nn / G2_BN));
     if (tile256 && prio)
-      hipLaunchKernelGGL(gemm_bf16_mfma_256<true>, dim3((nn / G2_BM) * (nn / G2_BN)), dim3(kGemm2Threads), 0, s, a_, b_,
-                         c_, nn, nn, nn, cu_map, group_m);
+      hipLaunchKernelGGL((gemm_bf16_mfma_256<true, false>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
+                         cu_map, group_m);
+    else if (tile256 && vec_c)
+      hipLaunchKernelGGL((gemm_bf16_mfma_256<false, true>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
+                         cu_map, group_m);
     else if (tile256)
-      hipLaunchKernelGGL(gemm_bf16_mfma_256<false>, dim3((nn / G2_BM) * (nn / G2_BN)), dim3(kGemm2Threads), 0, s, a_, b_,
-                         c_, nn, nn, nn, cu_map, group_m);
+      hipLaunchKernelGGL((gemm_bf16_mfma_256<false, false>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
+                         cu_map, group_m);
     else
       hipLaunchKernelGGL(gemm_bf16_mfma_nt, dim3((nn / BM) * (nn / BN)), dim3(kGemmThreads), 0, s, a_, b_, c_, nn, nn, nn);
   };
@@ -918,6 +941,7 @@ std::string run_probe(int dev, const char* opts) {
   const bool tile256 = opt_int(opts, "gemmTile", 256) != 128;  // 128 = the older 128x128 kernel (A/B)
   const int group_m = static_cast<int>(opt_int(opts, "gemmGroupM", kGemmGroupM));  // tile order (A/B)
   const bool gemm_prio = opt_int(opts, "gemmPrio", 0) != 0;                        // s_setprio (A/B)
+  const bool gemm_vec_c = opt_int(opts, "gemmVecC", 0) != 0;                       // 16-B C stores (A/B)
   const bool poison_c = opt_int(opts, "poisonC", 0) != 0;                           // test hook
   // The HBM test is bandwidth-bound with few waves per CU; the MFMA phase is compute-bound and
   // touches ~130 MiB: run them concurrently on two streams (overlap=0: one stream, serial).
@@ -1016,7 +1040,7 @@ std::string run_probe(int dev, const char* opts) {
   // earlier on the GPU while the rest of the HBM test is still enqueued well ahead of need.
   const int hbm_first = static_cast<int>(opt_int(opts, "hbmFirst", 1));
   if (do_mfma && hbm_first == 0)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, gemm_vec_c, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                       ctx, s2);
 
   // ---------------- HBM: all patterns back to back, per-pattern counters
@@ -1047,7 +1071,7 @@ std::string run_probe(int dev, const char* opts) {
       hipLaunchKernelGGL(hbm_fill<0>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip, reset, nreset);
     PROBE_CHECK(hipEventRecord(ctx.ev[1 + 2 * pi], s));
     if (pi == 0 && do_mfma && hbm_first == 2)
-      launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
+      launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, gemm_vec_c, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                         ctx, s2);
     if (pi == 0 && inject_flips > 0)
       hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(hbm), n16 * 4,
@@ -1066,7 +1090,7 @@ std::string run_probe(int dev, const char* opts) {
   PROBE_CHECK(hipGetLastError());
   PROBE_CHECK(hipMemcpyAsync(hres, cnt, 2 * patterns * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   if (do_mfma && hbm_first == 1)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, gemm_vec_c, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                       ctx, s2);
   const double launch_ms = ms_since(t_run);  // host time to enqueue the whole probe
   PROBE_CHECK(hipStreamSynchronize(s));
@@ -1666,7 +1690,7 @@ int mi355x_probe_gemm_bf16(int dev, const void* A, const void* Bt, void* C, int 
     PROBE_CHECK(hipMalloc(&dc.p, sc));
     PROBE_CHECK(hipMemcpy(da.p, A, sa, hipMemcpyHostToDevice));
     PROBE_CHECK(hipMemcpy(db.p, Bt, sb, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(gemm_bf16_mfma_256<false>, dim3((m / G2_BM) * (n / G2_BN)), dim3(kGemm2Threads), 0, nullptr,
+    hipLaunchKernelGGL((gemm_bf16_mfma_256<false, false>), dim3((m / G2_BM) * (n / G2_BN)), dim3(kGemm2Threads), 0, nullptr,
                        static_cast<const short*>(da.p), static_cast<const short*>(db.p), static_cast<float*>(dc.p), m, n,
                        k, static_cast<unsigned long long*>(nullptr), kGemmGroupM);
     PROBE_CHECK(hipGetLastError());

@@ -18,12 +18,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gpupool.ops import probe  # noqa: E402
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 9
-# variants: "gN" = gemmGroupM N; "pN" = gemmGroupM N with s_setprio around the MFMA block
+# variants: "gN" = gemmGroupM N; "pN" = that with s_setprio around the MFMA block; "vN" = that
+# with the transposed MFMA and 16-byte C stores
 variants = tuple(os.environ.get("GROUP_AB_VARIANTS", "g0,g2,g4,g8,g16").split(","))
 
 
 def opts_of(v: str) -> dict:
-    return {"gemmGroupM": int(v[1:]), "gemmPrio": int(v[0] == "p")}
+    return {"gemmGroupM": int(v[1:]), "gemmPrio": int(v[0] == "p"), "gemmVecC": int(v[0] == "v")}
 probe.init()
 res: dict[str, list[float]] = {}
 sizes = tuple(int(x) for x in os.environ.get("GROUP_AB_SIZES", "4096,8192").split(","))

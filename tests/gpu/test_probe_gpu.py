@@ -180,6 +180,16 @@ def test_grouped_tile_order_is_exact(hip, n, group_m):
     assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
 
 
+@pytest.mark.parametrize("n", [256, 1280, 4096])
+def test_vectorised_c_store_gemm_is_exact(hip, n):
+    """The transposed-MFMA variant with 16-byte C stores (``gemmVecC``) computes the same C: the
+    256^3 element-by-element check against the VALU reference and the exact ABFT checksums pass,
+    with C poisoned before the GEMM."""
+    r = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemmVecC=1, poisonC=1)
+    assert r["passed"], r
+    assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
+
+
 def test_overlapped_and_serial_probe_agree(hip):
     """The two-stream probe (HBM test beside the MFMA phase) finds the same injected faults as
     the serial one and both pass clean runs."""
