@@ -414,7 +414,8 @@ __device__ __forceinline__ int g2_swz(int r, int c) { return r * 128 + ((c ^ ((r
 // r4u_gemm_setprio_ab_rejected.json): off by default, selectable for A/B ("gemmPrio").
 // kVecC: the MFMA computes each 16x16 tile transposed (B fragment as the first operand), so a lane
 // holds 4 consecutive columns of one C row and the epilogue writes them as one 16-byte store
-// instead of four 4-byte ones (same MFMAs, same C; in-process A/B "gemmVecC").
+// instead of four 4-byte ones (same MFMAs, same C). Measured no faster (4096^3 1322 vs 1322, 2048^3
+// 315 vs 337 TFLOP/s, profiles/r4v_gemm_vecc_ab_rejected.json): off, selectable ("gemmVecC").
 template <bool kPrio = false, bool kVecC = false>
 __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const short* __restrict__ A,
                                                                        const short* __restrict__ Bt,
