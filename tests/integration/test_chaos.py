@@ -227,3 +227,26 @@ def test_manager_kills_while_gangs_are_created(cluster_factory):
     while k.list(PODS, "default")["items"] and time.monotonic() < deadline:
         time.sleep(0.1)
     assert k.list(PODS, "default")["items"] == []
+
+
+def test_agent_paused_mid_claim_converges(cluster_factory):
+    """A hung agent (SIGSTOP, then SIGCONT seconds later) while claims and releases are in flight:
+    the manager's RPCs time out or wait, the agent then finishes what it had started — the
+    manager must reconcile that (claims whose reply it never saw) to exactly the spec."""
+    c = cluster_factory()
+    k = c.client
+    rng = random.Random(int(os.environ.get("GPUPOOL_CHAOS_SEED", "5150")))
+    o = k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    uid = o["metadata"]["uid"]
+    _converged(c, uid, 2)
+    pid = c.procs[f"agent-{NODE}"].pid
+    for step in range(4):
+        r = rng.choice([1, 3, 4, 6])
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": r}}, "default")
+        time.sleep(rng.uniform(0.0, 0.04))
+        os.kill(pid, signal.SIGSTOP)
+        time.sleep(rng.uniform(1.0, 3.0))
+        os.kill(pid, signal.SIGCONT)
+        view = _converged(c, uid, r, timeout=60)
+        bad = [d for d in view["devices"] if d.get("state") in ("Quarantined", "Maintenance")]
+        assert not bad, (step, r, [(d["index"], d.get("quarantine")) for d in bad])
