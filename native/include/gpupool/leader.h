@@ -22,6 +22,14 @@ struct LeaderConfig {
   std::chrono::milliseconds retry_period{2000};
 };
 
+// Fencing for a paused leader (SIGSTOP, a VM pause, a long GC-less stall): with leader election on,
+// false once this process has gone longer than its renew deadline (steady clock, so time spent
+// stopped counts) without renewing its lease — another replica may be leading by then. The
+// controller checks it before every pass and the reconcilers before every mutating call (agent
+// claim / release RPCs, status writes); the elector itself renews through the plain client. Always
+// true without leader election.
+bool leader_fence_ok();
+
 class LeaderElector {
  public:
   LeaderElector(KubeClient& client, LeaderConfig cfg);

@@ -1,4 +1,5 @@
 #include "gpupool/reconciler.h"
+#include "gpupool/leader.h"
 
 #include <algorithm>
 #include <array>
@@ -114,6 +115,7 @@ PoolReconcilerBase::PoolReconcilerBase(KubeClient& client, Informer& pools, Even
 
 void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
   trace::Span span("status");
+  if (!leader_fence_ok()) throw std::runtime_error("not writing status: leadership not renewed in time");
   Json cur = obj;
   const std::string ns = obj.path("metadata.namespace").as_string();
   const std::string name = obj.path("metadata.name").as_string();
@@ -1538,6 +1540,12 @@ void Controller::worker_() {
     auto it = by_kind_.find(kind);
     if (it == by_kind_.end()) {
       q_.forget(key);
+      q_.done(key);
+      continue;
+    }
+    if (!leader_fence_ok()) {  // paused past the renew deadline: another replica may lead now
+      q_.forget(key);
+      q_.add_after(key, std::chrono::milliseconds(500));
       q_.done(key);
       continue;
     }

@@ -7,6 +7,7 @@
 #include "gpupool/informer.h"
 #include "gpupool/metrics.h"
 #include "gpupool/provider.h"
+#include "gpupool/leader.h"
 #include "gpupool/trace.h"
 
 namespace gpupool {
@@ -149,6 +150,8 @@ Json RocmProvider::post_(const std::string& node, const std::string& path, const
       if (--p->inflight_[node] == 0) p->cache_cv_.notify_all();
     }
   } done{this, node};
+  if (!leader_fence_ok())  // a paused leader must not claim or release after another took over
+    throw ProviderError("NotLeader", "agent on " + node + ": " + path + " not sent: leadership not renewed in time");
   invalidate_(node);  // every POST mutates the agent: the next observe must ask it
   trace::Span span("agent:POST " + path);
   std::shared_ptr<HttpClient> c = client_for(node);

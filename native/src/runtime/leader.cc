@@ -1,11 +1,27 @@
 #include "gpupool/leader.h"
 
+#include <atomic>
+#include <limits>
 #include <thread>
 
 namespace gpupool {
 
+namespace {
+using fence_clock = std::chrono::steady_clock;
+// steady-clock nanoseconds until which acting is allowed; max: no leader election in this process
+std::atomic<int64_t> g_fence_until_ns{std::numeric_limits<int64_t>::max()};
+
+int64_t fence_now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(fence_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+bool leader_fence_ok() { return fence_now_ns() < g_fence_until_ns.load(); }
+
 LeaderElector::LeaderElector(KubeClient& client, LeaderConfig cfg)
-    : client_(client), cfg_(std::move(cfg)), log_(Logger("leader").with("identity", cfg_.identity)) {}
+    : client_(client), cfg_(std::move(cfg)), log_(Logger("leader").with("identity", cfg_.identity)) {
+  g_fence_until_ns = 0;  // election on: nothing may act until the lease is ours
+}
 
 bool LeaderElector::try_acquire_or_renew() {
   std::string now = microtime_now();
@@ -87,26 +103,34 @@ void LeaderElector::run(const std::function<void()>& on_started,
     std::this_thread::sleep_for(cfg_.retry_period);
   }
   if (stop->load()) return;
+  auto fence_from = [this](clock::time_point renewed) {
+    g_fence_until_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           (renewed + cfg_.renew_deadline).time_since_epoch()).count();
+  };
+  auto last_renew = clock::now();
+  fence_from(last_renew);
   log_.info("became leader", Json::object().set("lease", cfg_.ns + "/" + cfg_.name));
   on_started();
-  auto last_renew = clock::now();
   while (!stop->load()) {
     std::this_thread::sleep_for(std::min(cfg_.retry_period, std::chrono::milliseconds(500)));
     if (clock::now() - last_renew < cfg_.retry_period) continue;
     bool ok = false;
+    const auto attempt = clock::now();  // the renewal holds from when it was sent, not answered
     try {
       ok = try_acquire_or_renew();
     } catch (const std::exception& e) {
       log_.warn("lease renew failed", Json::object().set("error", e.what()));
     }
     if (ok) {
-      last_renew = clock::now();
+      last_renew = attempt;
+      fence_from(attempt);
     } else if (clock::now() - last_renew > cfg_.renew_deadline) {
       log_.error("lost leadership", Json());
       leader_ = false;
       break;
     }
   }
+  g_fence_until_ns = 0;
   on_stopped();
 }
 

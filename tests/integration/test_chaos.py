@@ -250,3 +250,53 @@ def test_agent_paused_mid_claim_converges(cluster_factory):
         view = _converged(c, uid, r, timeout=60)
         bad = [d for d in view["devices"] if d.get("state") in ("Quarantined", "Maintenance")]
         assert not bad, (step, r, [(d["index"], d.get("quarantine")) for d in bad])
+
+
+def test_paused_leader_resumes_without_split_brain(cluster_factory):
+    """The leader manager is paused (SIGSTOP) past its lease while a scale-up is pending; the
+    standby takes the lease and converges the pool; the old leader, resumed, must notice it lost
+    the lease and stop before acting on its stale view: the pool still converges to its spec with
+    every GPU owned once."""
+    from gpupool.kube import LEASES
+    lease = ["--leader-elect", "--lease-duration", "2s", "--renew-deadline", "1500ms",
+             "--retry-period", "200ms"]
+    c = cluster_factory(manager_args=lease)
+    k = c.client
+    first = k.wait_for(LEASES, "gpupool-manager-leader", "gpupool-system",
+                       lambda o: bool(o) and bool(o["spec"].get("holderIdentity")), timeout=15,
+                       poll=0.05)["spec"]["holderIdentity"]
+    standby = c._spawn("manager2", [c.procs["manager"].args[0], "--apiserver", c.url,
+                                    "--identity", "standby", "--progress-poll", "100ms"] + lease)
+    o = k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    uid = o["metadata"]["uid"]
+    _converged(c, uid, 2)
+    leader = c.procs["manager"]
+    os.kill(leader.pid, signal.SIGSTOP)
+    try:
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 5}}, "default")
+        k.wait_for(LEASES, "gpupool-manager-leader", "gpupool-system",
+                   lambda x: x and x["spec"]["holderIdentity"] == "standby", timeout=15, poll=0.1)
+        _converged(c, uid, 5)
+    finally:
+        resumed_at = time.time()
+        os.kill(leader.pid, signal.SIGCONT)
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 3}}, "default")
+    view = _converged(c, uid, 3)
+    assert [d.get("poolUID") for d in view["devices"] if d.get("poolUID")] == [uid] * 3
+    deadline = time.monotonic() + 10
+    while leader.poll() is None and time.monotonic() < deadline:
+        time.sleep(0.1)
+    lease_now = k.get(LEASES, "gpupool-manager-leader", "gpupool-system")["spec"]["holderIdentity"]
+    assert lease_now == "standby" and first != "standby"
+    assert leader.poll() is not None, "the resumed old leader kept running after losing its lease"
+    assert standby.poll() is None
+    import json as _json
+    acted = []
+    for line in c.log("manager").splitlines():
+        try:
+            rec = _json.loads(line)
+        except ValueError:
+            continue
+        if rec.get("ts", 0) > resumed_at and rec.get("logger") == "reconciler":
+            acted.append(rec.get("msg"))
+    assert not acted, f"the old leader reconciled after it resumed: {acted}"
