@@ -300,3 +300,25 @@ def test_paused_leader_resumes_without_split_brain(cluster_factory):
         if rec.get("ts", 0) > resumed_at and rec.get("logger") == "reconciler":
             acted.append(rec.get("msg"))
     assert not acted, f"the old leader reconciled after it resumed: {acted}"
+
+
+def test_apiserver_paused_mid_scale_converges(cluster_factory):
+    """The apiserver hangs (SIGSTOP 1-3 s) right after a spec change: the manager's watch and
+    status writes stall or time out; once it answers again the informers catch up (or relist) and
+    the pool converges, every GPU owned once."""
+    c = cluster_factory()
+    k = c.client
+    rng = random.Random(int(os.environ.get("GPUPOOL_CHAOS_SEED", "1701")))
+    o = k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    uid = o["metadata"]["uid"]
+    _converged(c, uid, 2)
+    api = c.procs["apiserver"].pid
+    for step in range(3):
+        r = rng.choice([1, 3, 5, 6])
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": r}}, "default")
+        time.sleep(rng.uniform(0.0, 0.03))
+        os.kill(api, signal.SIGSTOP)
+        time.sleep(rng.uniform(1.0, 3.0))
+        os.kill(api, signal.SIGCONT)
+        view = _converged(c, uid, r, timeout=60)
+        assert [d.get("poolUID") for d in view["devices"] if d.get("poolUID")] == [uid] * r, step
