@@ -26,7 +26,8 @@ After the timed region (not part of ms_per_step):
     amdsmi event takes) — and reaction only (forced sample).
 
 ``value`` is the p50 reconcile-to-Ready latency at replicas = N (``--gpus``), the largest point of
-the sweep; ``per_n`` holds every point. With N GPUs visible (real MI355X) the agent uses the
+the sweep; ``per_n`` holds every point, ``e2e_breakdown_p50_ms`` / ``claim_pass_span_p50_ms`` the
+median split of a cycle and ``slowest_cycle`` the same split for the slowest timed cycle. With N GPUs visible (real MI355X) the agent uses the
 amdsmi backend and the in-process HIP probe; without GPUs it falls back to the 8-GPU fake fixture
 with a simulated probe, and says so in ``data``. The API server is always the in-repo apiserver
 simulator (no kube-apiserver/etcd in this environment).
