@@ -322,3 +322,45 @@ def test_apiserver_paused_mid_scale_converges(cluster_factory):
         os.kill(api, signal.SIGCONT)
         view = _converged(c, uid, r, timeout=60)
         assert [d.get("poolUID") for d in view["devices"] if d.get("poolUID")] == [uid] * r, step
+
+
+def test_kills_during_pool_deletion_leave_no_claim(cluster_factory):
+    """A pool whose GPUs run pods is deleted while the agent or the manager is killed somewhere
+    in the finalizer's drain -> release: the CR disappears only after every GPU is released and
+    every pod evicted — never earlier, never with a claim left behind."""
+    from gpupool.kube import PODS
+
+    from .helpers import pause_pod
+    c = cluster_factory()
+    k = c.client
+    rng = random.Random(int(os.environ.get("GPUPOOL_CHAOS_SEED", "808")))
+    for rnd in range(3):
+        name = f"p{rnd}"
+        o = k.create(MI355XPOOLS, mi_pool(name, 3, drain={"gracePeriodSeconds": 1}), "default")
+        uid = o["metadata"]["uid"]
+        wait_ready(k, name, 3)
+        for i in range(3):
+            k.create(PODS, pause_pod(f"{name}-w{i}"), "default")
+        deadline = time.monotonic() + 30
+        while time.monotonic() < deadline and not all(
+                p["status"].get("phase") == "Running" for p in k.list(PODS, "default")["items"]):
+            time.sleep(0.05)
+        k.delete(MI355XPOOLS, name, "default")
+        time.sleep(rng.uniform(0.0, 0.4))
+        what = rng.choice(["agent", "manager", "both"])
+        if what in ("manager", "both"):
+            c._kill("manager", sig=signal.SIGKILL)
+        if what in ("agent", "both"):
+            c._kill(f"agent-{NODE}", sig=signal.SIGKILL)
+            c.start_agent(c.nodes[0])
+        if what in ("manager", "both"):
+            c.start_manager()
+        k.wait_for(MI355XPOOLS, name, "default", lambda x: x is None, timeout=60)
+        view = _view(c)
+        assert not [d for d in view["devices"] if d.get("poolUID") == uid], (rnd, what)
+        deadline = time.monotonic() + 10
+        while k.list(PODS, "default")["items"] and time.monotonic() < deadline:
+            time.sleep(0.05)
+        assert k.list(PODS, "default")["items"] == [], (rnd, what)
+        assert all(d.get("state") == "Free" for d in view["devices"]), \
+            (rnd, what, [(d["index"], d.get("state")) for d in view["devices"]])
