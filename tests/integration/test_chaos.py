@@ -364,3 +364,28 @@ def test_kills_during_pool_deletion_leave_no_claim(cluster_factory):
         assert k.list(PODS, "default")["items"] == [], (rnd, what)
         assert all(d.get("state") == "Free" for d in view["devices"]), \
             (rnd, what, [(d["index"], d.get("state")) for d in view["devices"]])
+
+
+def test_agent_kills_with_an_isolated_sharing_pool(cluster_factory):
+    """The agent-kill walk on a pool that shares each GPU as isolated slots (HBM budget + CU
+    share per slot): it converges the same way and the restarted agent advertises every GPU's
+    slots again."""
+    c = cluster_factory()
+    k = c.client
+    rng = random.Random(int(os.environ.get("GPUPOOL_CHAOS_SEED", "4242")))
+    spec = dict(sharing={"replicasPerGPU": 2, "hbmBytesPerSlot": 64 << 30, "cuPerSlot": 64})
+    o = k.create(MI355XPOOLS, mi_pool("p", 2, **spec), "default")
+    uid = o["metadata"]["uid"]
+    _converged(c, uid, 2)
+    for step in range(5):
+        r = rng.choice([1, 2, 3, 4])
+        k.patch(MI355XPOOLS, "p", {"spec": {"replicas": r}}, "default")
+        time.sleep(rng.uniform(0.0, 0.06))
+        c._kill(f"agent-{NODE}", sig=signal.SIGKILL)
+        c.start_agent(c.nodes[0])
+        view = _converged(c, uid, r)
+        mine = [d for d in view["devices"] if d.get("poolUID") == uid]
+        assert all((d.get("sharing") or {}).get("replicasPerGPU") == 2 for d in mine), \
+            (step, [d.get("sharing") for d in mine])
+        bad = [d for d in view["devices"] if d.get("state") in ("Quarantined", "Maintenance")]
+        assert not bad, (step, r)
