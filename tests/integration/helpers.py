@@ -24,6 +24,38 @@ def ready_at(r: int):
     return pred
 
 
+def settled_pools(client, ns: str, finals: dict, agent_views, timeout: float = 30.0):
+    """One consistent snapshot of several pools once they have settled: every pool Ready at its
+    final size, no pool changed while the agents were read, and each agent claim sits with the
+    pool whose status lists it. Returns ``(pools, claims)`` — name -> object, and name -> the
+    uuids the agents hold for that pool — from the last snapshot taken (the caller asserts on it).
+
+    A pool's status is an observation written after the agent acted: a GPU released by pool A
+    and claimed by pool B can sit in both statuses for the moment between B's status write and
+    A's, and a fault event the agent sampled just before the faults cleared may still replace a
+    GPU after A reads Ready. Exclusivity itself is the agent's (one record per GPU); the statuses
+    agree with it once nothing moves any more, which is what this waits for."""
+    deadline = time.monotonic() + timeout
+    while True:
+        pools = {n: client.get(MI355XPOOLS, n, ns) for n in finals}
+        uid_to_name = {o["metadata"]["uid"]: n for n, o in pools.items()}
+        claims: dict = {n: set() for n in finals}
+        for view in agent_views():
+            for d in view["devices"]:
+                if d.get("poolUID") in uid_to_name:
+                    claims[uid_to_name[d["poolUID"]]].add(d["uuid"])
+        again = {n: client.get(MI355XPOOLS, n, ns) for n in finals}
+        stable = all(again[n]["metadata"]["resourceVersion"] == o["metadata"]["resourceVersion"]
+                     for n, o in pools.items())
+        if stable and all(ready_at(r)(pools[n]) for n, r in finals.items()) and \
+                all(claims[n] == {d["uuid"] for d in pools[n]["status"]["devices"]}
+                    for n in finals):
+            return pools, claims
+        if time.monotonic() > deadline:
+            return pools, claims
+        time.sleep(0.1)
+
+
 def cond_is(ctype: str, status: str, reason: str | None = None):
     def pred(o):
         c = conds(o).get(ctype, {})

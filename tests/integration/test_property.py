@@ -16,7 +16,7 @@ from hypothesis import strategies as st
 from gpupool.kube import MI355XPOOLS, NODES
 from gpupool.testing.cluster import Cluster, NodeSpec
 
-from .helpers import mi_pool, ready_at
+from .helpers import mi_pool, ready_at, settled_pools
 
 pytestmark = pytest.mark.slow
 
@@ -65,28 +65,32 @@ def test_random_edits_and_faults_converge(shared, ops, final):
         time.sleep(0.05)
     c.set_faults("mi355x-node-0", {})
     ra, rb = final
-    k.patch(MI355XPOOLS, "pa", {"spec": {"replicas": ra}}, ns)
-    k.patch(MI355XPOOLS, "pb", {"spec": {"replicas": rb}}, ns)
-    a = k.wait_for(MI355XPOOLS, "pa", ns, ready_at(ra), timeout=90)
-    b = k.wait_for(MI355XPOOLS, "pb", ns, ready_at(rb), timeout=90)
-    ua = {d["uuid"] for d in a["status"]["devices"]}
-    ub = {d["uuid"] for d in b["status"]["devices"]}
-    assert not ua & ub
-    view = c.agent_request("mi355x-node-0", "GET", "/v1/node")
-    claimed = {d["uuid"] for d in view["devices"] if d.get("poolUID") in
-               (a["metadata"]["uid"], b["metadata"]["uid"])}
-    assert claimed == ua | ub
-    deadline = time.time() + 10
-    while True:  # kubelet's view converges through ListAndWatch
-        alloc = k.get(NODES, "mi355x-node-0")["status"].get("allocatable", {})
-        if alloc.get("amd.com/gpu-a", "0") == str(ra) and alloc.get("amd.com/gpu-b", "0") == str(rb):
-            break
-        assert time.time() < deadline, alloc
-        time.sleep(0.05)
-    for name in ("pa", "pb"):
-        k.delete(MI355XPOOLS, name, ns)
-    for name in ("pa", "pb"):
-        k.wait_for(MI355XPOOLS, name, ns, lambda o: o is None, timeout=30)
+    try:
+        k.patch(MI355XPOOLS, "pa", {"spec": {"replicas": ra}}, ns)
+        k.patch(MI355XPOOLS, "pb", {"spec": {"replicas": rb}}, ns)
+        k.wait_for(MI355XPOOLS, "pa", ns, ready_at(ra), timeout=90)
+        k.wait_for(MI355XPOOLS, "pb", ns, ready_at(rb), timeout=90)
+        pools, claims = settled_pools(
+            k, ns, {"pa": ra, "pb": rb},
+            lambda: [c.agent_request("mi355x-node-0", "GET", "/v1/node")])
+        ua = {d["uuid"] for d in pools["pa"]["status"]["devices"]}
+        ub = {d["uuid"] for d in pools["pb"]["status"]["devices"]}
+        assert ready_at(ra)(pools["pa"]) and ready_at(rb)(pools["pb"])
+        assert not ua & ub
+        assert claims == {"pa": ua, "pb": ub}
+        deadline = time.time() + 10
+        while True:  # kubelet's view converges through ListAndWatch
+            alloc = k.get(NODES, "mi355x-node-0")["status"].get("allocatable", {})
+            if alloc.get("amd.com/gpu-a", "0") == str(ra) and \
+                    alloc.get("amd.com/gpu-b", "0") == str(rb):
+                break
+            assert time.time() < deadline, alloc
+            time.sleep(0.05)
+    finally:  # a failed example must not leave pools behind for the next one (same resources)
+        for name in ("pa", "pb"):
+            k.delete(MI355XPOOLS, name, ns)
+        for name in ("pa", "pb"):
+            k.wait_for(MI355XPOOLS, name, ns, lambda o: o is None, timeout=30)
 
 
 span_op = st.one_of(
@@ -135,25 +139,26 @@ def test_spanning_pools_converge(two_nodes, ops, final):
     for n in ("node-a", "node-b"):
         c.set_faults(n, {})
     ra, rb = final
-    k.patch(MI355XPOOLS, "sa", {"spec": {"replicas": ra}}, ns)
-    k.patch(MI355XPOOLS, "sb", {"spec": {"replicas": rb}}, ns)
-    a = k.wait_for(MI355XPOOLS, "sa", ns, ready_at(ra), timeout=90)
-    b = k.wait_for(MI355XPOOLS, "sb", ns, ready_at(rb), timeout=90)
-    ua = {d["uuid"] for d in a["status"]["devices"]}
-    ub = {d["uuid"] for d in b["status"]["devices"]}
-    assert not ua & ub
-    for o in (a, b):
-        assert len({d["node"] for d in o["status"]["devices"]}) <= 2
-    claimed = set()
-    for n in ("node-a", "node-b"):
-        view = c.agent_request(n, "GET", "/v1/node")
-        claimed |= {d["uuid"] for d in view["devices"] if d.get("poolUID") in
-                    (a["metadata"]["uid"], b["metadata"]["uid"])}
-    assert claimed == ua | ub
-    for name in ("sa", "sb"):
-        k.delete(MI355XPOOLS, name, ns)
-    for name in ("sa", "sb"):
-        k.wait_for(MI355XPOOLS, name, ns, lambda o: o is None, timeout=30)
+    try:
+        k.patch(MI355XPOOLS, "sa", {"spec": {"replicas": ra}}, ns)
+        k.patch(MI355XPOOLS, "sb", {"spec": {"replicas": rb}}, ns)
+        k.wait_for(MI355XPOOLS, "sa", ns, ready_at(ra), timeout=90)
+        k.wait_for(MI355XPOOLS, "sb", ns, ready_at(rb), timeout=90)
+        pools, claims = settled_pools(
+            k, ns, {"sa": ra, "sb": rb},
+            lambda: [c.agent_request(n, "GET", "/v1/node") for n in ("node-a", "node-b")])
+        ua = {d["uuid"] for d in pools["sa"]["status"]["devices"]}
+        ub = {d["uuid"] for d in pools["sb"]["status"]["devices"]}
+        assert ready_at(ra)(pools["sa"]) and ready_at(rb)(pools["sb"])
+        assert not ua & ub
+        for o in pools.values():
+            assert len({d["node"] for d in o["status"]["devices"]}) <= 2
+        assert claims == {"sa": ua, "sb": ub}
+    finally:
+        for name in ("sa", "sb"):
+            k.delete(MI355XPOOLS, name, ns)
+        for name in ("sa", "sb"):
+            k.wait_for(MI355XPOOLS, name, ns, lambda o: o is None, timeout=30)
 
 
 chaos_op = st.one_of(
