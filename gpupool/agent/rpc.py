@@ -14,7 +14,10 @@ Exposure bounds (the TCP listener is reachable from the node network):
   * an absolute deadline: a connection must finish its TLS handshake and its first request within
     ``first_request_timeout`` seconds of its accept, however slowly its bytes trickle in — every
     read waits only for what is left of it, and a reaper thread shuts down a connection still
-    untrusted at its deadline (which also bounds a stalled TLS handshake). Only a request answered
+    untrusted at its deadline (which also bounds a stalled TLS handshake). The deadline covers
+    receiving the request, not handling it: once an authorised request has been read whole it is
+    lifted, so a long handler (a scrub that maps the free HBM of a GPU whose VRAM the driver is
+    still clearing, a claim probing 8 GPUs) still gets its reply out. Only a request answered
     with something other than 401 makes the connection trusted: it may then idle as a pooled
     keep-alive connection;
   * the token is checked right after the headers, before any body byte is read; a request refused
@@ -364,6 +367,8 @@ class RpcServer:
                     return
                 keep = headers.get("connection", "").lower() != "close" and \
                     not version.strip().upper().endswith("1.0")
+                if not trusted:  # the request is in, authorised: its handling is not bounded
+                    self._unwatch(raw)
                 t0 = time.perf_counter()
                 reply = self._dispatch(method, target, headers, body)
                 if reply[0] == 401:
@@ -371,7 +376,6 @@ class RpcServer:
                 elif not trusted:
                     trusted = True
                     rf.deadline = None  # a pooled keep-alive connection may idle from here
-                    self._unwatch(raw)
                 try:
                     self._send(conn, reply, keep)
                     self._account(path, time.perf_counter() - t0)

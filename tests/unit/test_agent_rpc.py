@@ -75,6 +75,24 @@ def test_trusted_keep_alive_connection_may_idle():
         srv.close()
 
 
+def test_a_handler_slower_than_the_first_request_timeout_still_replies():
+    """The deadline bounds receiving the first request, not handling it: an explicit scrub that
+    maps a GPU's free HBM while the driver still clears its VRAM ran past 10 s on MI355X and the
+    reaper cut its reply off (RemoteDisconnected, profiles/r4y_pytest_gpu_scrub_rpc_cut.txt)."""
+    srv = RpcServer({("GET", "/v1/slow"): lambda q, b: (time.sleep(0.8), json_reply({"ok": True}))[1]},
+                    first_request_timeout=0.3)
+    srv.listen_tcp("127.0.0.1", 0)
+    port = srv._listeners[-1].getsockname()[1]
+    try:
+        s = socket.create_connection(("127.0.0.1", port))
+        s.settimeout(5.0)
+        assert b"200" in _get(s, "/v1/slow")  # 0.8 s of handling on a fresh connection
+        assert b"200" in _get(s, "/v1/slow")  # and the connection stays usable
+        s.close()
+    finally:
+        srv.close()
+
+
 def test_unauthorized_request_closes_the_connection():
     srv, port = _server(token="secret")
     try:
