@@ -17,9 +17,14 @@ Exposure bounds (the TCP listener is reachable from the node network):
     untrusted at its deadline (which also bounds a stalled TLS handshake). The deadline covers
     receiving the request, not handling it: once an authorised request has been read whole it is
     lifted, so a long handler (a scrub that maps the free HBM of a GPU whose VRAM the driver is
-    still clearing, a claim probing 8 GPUs) still gets its reply out. Only a request answered
-    with something other than 401 makes the connection trusted: it may then idle as a pooled
-    keep-alive connection;
+    still clearing, a claim probing 8 GPUs) still gets its reply out. Only a request that carried
+    the valid token makes the connection trusted (with no token configured: any request): it may
+    then idle as a pooled keep-alive connection. An unauthenticated request to an open path
+    (/healthz, /metrics) is answered with ``Connection: close`` — one keep-alive GET /healthz per
+    connection must not pin the ``max_conns`` slots the manager's claims need;
+  * a trusted connection may idle between requests, but once the first byte of a request head
+    arrives, the head and its body must be in within ``first_request_timeout``: a trusted peer
+    cannot drip a request either;
   * the token is checked right after the headers, before any body byte is read; a request refused
     for it closes the connection;
   * at most ``MAX_HEADERS`` header lines of ``MAX_HEADER_BYTES`` in total; a body-carrying method
@@ -156,6 +161,8 @@ class RpcServer:
         self._pending_cv = threading.Condition()
         self.reaped = 0
         self.rejected_requests = 0
+        self.open_path_closes = 0  # unauthenticated /healthz, /metrics answered and closed
+        self.request_deadline_closes = 0  # trusted connections cut mid-request at the deadline
         self.bytes_read = 0  # over all finished connections (tests: what a rejected peer cost)
         threading.Thread(target=self._reaper, daemon=True, name="rpc-reaper").start()
 
@@ -289,7 +296,7 @@ class RpcServer:
                 rf.total += len(data)
 
     def _serve_conn(self, conn: socket.socket, ssl_ctx) -> None:
-        trusted = False  # until a request is answered with something other than 401
+        trusted = False  # until a request carrying the token (or any, without one) is answered
         raw = conn
         rf = None
         deadline = time.monotonic() + self.first_request_timeout if self.first_request_timeout \
@@ -313,8 +320,17 @@ class RpcServer:
             rf.deadline = deadline
             while not self._stop.is_set():
                 try:
+                    if trusted and self.first_request_timeout:
+                        # idle keep-alive: no bound until the next request starts; from its first
+                        # byte, head and body share one absolute deadline
+                        rf.deadline = None
+                        if not rf.buf:
+                            rf._fill()
+                        rf.deadline = time.monotonic() + self.first_request_timeout
                     head = rf.read_head(MAX_LINE + MAX_HEADER_BYTES)
-                except _Closed:
+                except _Closed as e:
+                    if trusted and str(e) == "deadline":
+                        self.request_deadline_closes += 1
                     return
                 if head is None:
                     self._reject(conn, 431, "HeadersTooLarge",
@@ -343,8 +359,9 @@ class RpcServer:
                     headers[k.strip().lower()] = v.strip()
                 path = target.partition("?")[0]
                 # the token before the body: an unauthenticated peer never gets a byte buffered
-                if self._auth and path not in OPEN_PATHS and not hmac.compare_digest(
-                        headers.get("authorization", "").encode(), self._auth):
+                authed = not self._auth or hmac.compare_digest(
+                    headers.get("authorization", "").encode(), self._auth)
+                if not authed and path not in OPEN_PATHS:
                     self._reject(conn, 401, "Unauthorized", "agent RPC requires the manager's token", rf)
                     return
                 cl = headers.get("content-length")
@@ -363,19 +380,25 @@ class RpcServer:
                     return
                 try:
                     body = rf.read(n) if n else b""
-                except _Closed:
+                except _Closed as e:
+                    if trusted and str(e) == "deadline":
+                        self.request_deadline_closes += 1
                     return
+                rf.deadline = None  # the request is in: its handling is not bounded
                 keep = headers.get("connection", "").lower() != "close" and \
                     not version.strip().upper().endswith("1.0")
-                if not trusted:  # the request is in, authorised: its handling is not bounded
+                if not trusted:
                     self._unwatch(raw)
                 t0 = time.perf_counter()
                 reply = self._dispatch(method, target, headers, body)
                 if reply[0] == 401:
                     keep = False  # no second guess on this connection
+                elif not authed:
+                    # an open path answered without the token: it never earns a pooled slot
+                    keep = False
+                    self.open_path_closes += 1
                 elif not trusted:
-                    trusted = True
-                    rf.deadline = None  # a pooled keep-alive connection may idle from here
+                    trusted = True  # a pooled keep-alive connection may idle from here
                 try:
                     self._send(conn, reply, keep)
                     self._account(path, time.perf_counter() - t0)
@@ -415,7 +438,10 @@ class RpcServer:
         out = [f"gpupool_agent_rpc_open_connections {self.open_conns}",
                f"gpupool_agent_rpc_refused_connections_total {self.refused_conns}",
                f"gpupool_agent_rpc_deadline_closed_connections_total {self.reaped}",
-               f"gpupool_agent_rpc_rejected_requests_total {self.rejected_requests}"]
+               f"gpupool_agent_rpc_rejected_requests_total {self.rejected_requests}",
+               f"gpupool_agent_rpc_open_path_closed_connections_total {self.open_path_closes}",
+               f"gpupool_agent_rpc_request_deadline_closed_connections_total "
+               f"{self.request_deadline_closes}"]
         for path, (n, sec) in items:
             out.append(f'gpupool_agent_rpc_requests_total{{path="{path}"}} {n}')
             out.append(f'gpupool_agent_rpc_seconds_sum{{path="{path}"}} {sec:.6f}')

@@ -275,3 +275,106 @@ def test_post_reply_hook_runs_when_the_peer_is_gone():
         assert _wait(lambda: srv.open_conns == 0)
     finally:
         srv.close()
+
+
+def _open_path_server(**kw) -> tuple[RpcServer, int]:
+    from gpupool.agent.rpc import text_reply
+    srv = RpcServer({("GET", "/v1/ping"): lambda q, b: json_reply({"ok": True}),
+                     ("GET", "/healthz"): lambda q, b: text_reply("ok\n")}, **kw)
+    srv.listen_tcp("127.0.0.1", 0)
+    return srv, srv._listeners[-1].getsockname()[1]
+
+
+def test_unauthenticated_open_path_requests_cannot_pin_connection_slots():
+    """five unauthenticated clients each send a keep-alive GET /healthz and
+    idle. Before, the 200 made each connection trusted and lifted its deadline (open_conns stayed
+    5, reaped 0). Now an open path answered without the token closes its connection, so all are
+    gone well within first_request_timeout + 0.5 s."""
+    srv, port = _open_path_server(token="secret", first_request_timeout=1.0)
+    socks = []
+    try:
+        t0 = time.monotonic()
+        for _ in range(5):
+            s = _raw(port)
+            assert b"200" in _get(s, "/healthz")
+            socks.append(s)
+        assert all(_closed(s, 1.5) for s in socks)
+        assert _wait(lambda: srv.open_conns == 0, 1.5)
+        assert time.monotonic() - t0 <= 1.0 + 0.5 + 1.0  # 5 requests + the bound
+        assert srv.open_path_closes == 5
+        assert "gpupool_agent_rpc_open_path_closed_connections_total 5" in srv.metrics_lines()
+    finally:
+        for s in socks:
+            s.close()
+        srv.close()
+
+
+def test_a_head_dripped_after_an_open_path_request_is_cut():
+    """The second half of the repro: after GET /healthz the peer drips a second request head at
+    1 byte per 0.1 s. The connection is closed after the first reply, so nothing it drips is read
+    and its slot is free at once."""
+    import threading
+    srv, port = _open_path_server(token="secret", first_request_timeout=1.0)
+    try:
+        s = _raw(port)
+        assert b"200" in _get(s, "/healthz")
+        stop = threading.Event()
+
+        def drip():
+            for ch in b"GET /healthz HTTP/1.1\r\nX-Slow: " + b"a" * 200:
+                try:
+                    s.sendall(bytes([ch]))
+                except OSError:
+                    return
+                if stop.wait(0.1):
+                    return
+        threading.Thread(target=drip, daemon=True).start()
+        t0 = time.monotonic()
+        assert _closed(s, 2.0)
+        assert time.monotonic() - t0 <= 1.5
+        stop.set()
+        assert _wait(lambda: srv.open_conns == 0, 1.5)
+    finally:
+        srv.close()
+
+
+def test_a_trusted_connection_cannot_drip_a_later_request():
+    """After trust a connection may idle, but a request head that starts arriving must be in
+    within first_request_timeout: a bearer-authenticated peer dripping its second head is cut."""
+    import threading
+    srv, port = _open_path_server(token="secret", first_request_timeout=1.0)
+    try:
+        s = _raw(port)
+        assert b"200" in _get(s, "/v1/ping", token="secret")
+        time.sleep(1.3)  # idling past the bound is fine
+        stop = threading.Event()
+
+        def drip():
+            for ch in b"GET /v1/ping HTTP/1.1\r\nAuthorization: Bearer secret\r\nX-Slow: " + b"a" * 200:
+                try:
+                    s.sendall(bytes([ch]))
+                except OSError:
+                    return
+                if stop.wait(0.1):
+                    return
+        threading.Thread(target=drip, daemon=True).start()
+        t0 = time.monotonic()
+        assert _closed(s, 3.0)
+        assert 0.8 <= time.monotonic() - t0 <= 1.6
+        stop.set()
+        assert _wait(lambda: srv.open_conns == 0, 1.5)
+        assert srv.request_deadline_closes == 1
+    finally:
+        srv.close()
+
+
+def test_authenticated_open_path_request_keeps_the_connection():
+    srv, port = _open_path_server(token="secret", first_request_timeout=0.3)
+    try:
+        s = _raw(port)
+        assert b"200" in _get(s, "/healthz", token="secret")
+        time.sleep(0.6)
+        assert b"200" in _get(s, "/v1/ping", token="secret")
+        s.close()
+    finally:
+        srv.close()
