@@ -28,7 +28,7 @@ After the timed region (not part of ms_per_step):
 ``value`` is the p50 reconcile-to-Ready latency at replicas = N (``--gpus``), the largest point of
 the sweep; ``per_n`` holds every point, ``e2e_breakdown_p50_ms`` / ``claim_pass_span_p50_ms`` the
 median split of a cycle and ``slowest_cycle`` the same split for the slowest timed cycle. With N GPUs visible (real MI355X) the agent uses the
-amdsmi backend and the in-process HIP probe; without GPUs it falls back to the 8-GPU fake fixture
+amdsmi backend and the gfx950 HIP probe in per-GPU probe helpers; without GPUs it falls back to the 8-GPU fake fixture
 with a simulated probe, and says so in ``data``. The API server is always the in-repo apiserver
 simulator (no kube-apiserver/etcd in this environment).
 
@@ -215,6 +215,11 @@ def main() -> int:
     ap.add_argument("--comm-check", default="auto", choices=["auto", "gloo", "off"],
                     help="after the timed region with N>1 ranks: all-reduce across the ranks' "
                          "GPUs over RCCL (auto: when the GPUs are real) or gloo on CPU")
+    ap.add_argument("--probe-mode", default="",
+                    choices=["", "helper", "helper-sim", "inproc", "simulated"],
+                    help="where the agent runs the claim-time probe (default: helper on real GPUs "
+                         "— per-GPU child processes, the production setting — helper-sim on the "
+                         "fake backend; inproc only for an A/B of the helper's cost)")
     ap.add_argument("--inject-claim-hang", default="",
                     help="fault injection: COUNT:SECONDS — the agent stalls every claim of >= "
                          "COUNT GPUs (exercises the bench's failure isolation)")
@@ -250,7 +255,7 @@ def main() -> int:
         if args.inject_claim_hang:
             extra += ["--inject-claim-delay", args.inject_claim_hang]
         node = NodeSpec("mi355x-node-0", backend="amdsmi" if real else "fake",
-                        probe="inproc" if real else "simulated",
+                        probe=args.probe_mode or ("helper" if real else "helper-sim"),
                         count=-1 if real else max(8, n), extra_args=extra)
         # production agent settings: ledger fsync on, 100 ms health poll, full sample every 1 s
         cluster = Cluster(workdir, nodes=[node], sample_interval=args.sample_interval, fsync=True)
@@ -352,6 +357,9 @@ def main() -> int:
                 per_n[str(k)]["agent"] = {
                     "rss_mib": fa["rss_mib"], "hip_devices": fa.get("hip_devices"),
                     "vram_used_mib_per_gpu": [vram.get(i) for i in idx]}
+                if "helpers_rss_mib" in fa:  # the per-GPU probe helpers beside the agent
+                    per_n[str(k)]["agent"].update(probe_helpers=fa.get("helpers"),
+                                                  helpers_rss_mib=fa["helpers_rss_mib"])
             if str(k) in errors:
                 per_n[str(k)]["errors"] = errors[str(k)]
                 first = errors[str(k)][0]
@@ -498,10 +506,11 @@ def main() -> int:
         head = per_n[str(value_n)] if value_n is not None else {"p50_s": None, "p90_s": None,
                                                                "max_s": None}
         all_ok = sum(cy["ok"] for cy in cycles)
-        src = ("real MI355X: amdsmi discovery + gfx950 HIP probe (HBM %d MiB + bf16 MFMA) + device "
-               "plugin -> fake kubelet" % (args.hbm_bytes >> 20)) if real else \
-              ("synthetic: 8x MI355X fake fixture (no GPU visible), simulated probe, device plugin "
-               "-> fake kubelet")
+        pmode = args.probe_mode or ("helper" if real else "helper-sim")
+        src = ("real MI355X: amdsmi discovery + gfx950 HIP probe (HBM %d MiB + bf16 MFMA, probe "
+               "mode %s) + device plugin -> fake kubelet" % (args.hbm_bytes >> 20, pmode)) if real \
+            else ("synthetic: 8x MI355X fake fixture (no GPU visible), simulated probe (probe mode "
+                  "%s), device plugin -> fake kubelet" % pmode)
         status = "ok" if value_n == n and not errors and not skipped and setup_error is None \
             else "partial" if value_n is not None else "failed"
         out = {

@@ -8,7 +8,6 @@ import os
 import socket
 import sys
 
-from .agent import Agent, AgentConfig, serve
 
 
 def _count_seconds(v: str) -> tuple[int, float]:
@@ -19,6 +18,10 @@ def _count_seconds(v: str) -> tuple[int, float]:
 
 
 def main() -> None:
+    # Before anything touches a GPU (amdsmi in the device library, HIP anywhere): the forkserver the
+    # probe helpers are forked from, so no helper inherits GPU state (probehost.py).
+    from .probehost import start_spawner
+    start_spawner()
     ap = argparse.ArgumentParser(description="gpupool node agent (MI355X)")
     ap.add_argument("--node", default=os.environ.get("GPUPOOL_NODE", socket.gethostname()))
     ap.add_argument("--backend", default=os.environ.get("GPUPOOL_BACKEND", "auto"),
@@ -43,7 +46,12 @@ def main() -> None:
                          "$GPUPOOL_AGENT_TOKEN also works")
     ap.add_argument("--plugin-dir", default="", help="kubelet device-plugin directory")
     ap.add_argument("--pod-resources", default="", help="kubelet PodResources socket")
-    ap.add_argument("--probe", default="", choices=["", "inproc", "subprocess", "simulated", "off"])
+    ap.add_argument("--probe", default="",
+                    choices=["", "helper", "helper-sim", "inproc", "subprocess", "simulated", "off"],
+                    help="where the claim-time probe runs: helper (default with GPUs: per-GPU "
+                         "child processes, isolated, with a deadline), helper-sim (the same with "
+                         "simulated kernels), inproc (in the agent; A/B only), subprocess, "
+                         "simulated (default with the fake backend), off")
     ap.add_argument("--probe-sim-ms", type=float, default=20.0)
     ap.add_argument("--probe-gemm-n", type=int, default=4096,
                     help="GEMM size of the serial probe (pools with performance floors)")
@@ -86,6 +94,7 @@ def main() -> None:
     ap.add_argument("--ready-file", default="")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
+    from .agent import Agent, AgentConfig, serve
     if a.gil_switch_interval > 0:
         # The agent's threads (RPC loop, claim executor, sampler, device-plugin gRPC) hand the GIL
         # to each other on every claim; at the 5 ms default one hand-off can cost milliseconds.

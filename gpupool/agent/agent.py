@@ -29,7 +29,7 @@ from ..api import schema
 from ..ops import devlib
 from . import slots as slotlib
 from .ledger import Ledger
-from .prober import Prober, default_mode
+from .prober import DEFAULT_TIMEOUT_S, Prober, default_mode
 
 SLOT_SEP = "::"  # device-plugin ID of a time-sliced slot: "<uuid>::<slot>"
 
@@ -138,7 +138,7 @@ class AgentConfig:
     auth_token: str = ""             # shared secret the manager presents on the agent RPC
     plugin_dir: str = ""             # kubelet device-plugin dir; empty: device plugin disabled
     pod_resources: str = ""          # kubelet PodResources socket
-    probe_mode: str = ""             # inproc | subprocess | simulated | off (default by backend)
+    probe_mode: str = ""             # helper | helper-sim | inproc | subprocess | simulated | off
     probe_sim_ms: float = 20.0
     probe_gemm_n: int = 4096          # serial probe's GEMM (pools with performance floors)
     probe_overlap_gemm_n: int = 2048  # claim-time probe's GEMM beside the HBM pattern test
@@ -181,10 +181,13 @@ class Agent:
         self.records: dict[str, dict] = self.ledger.load()
         # A claim commits 'Probing' before its probe runs, and Probing -> Claimed reaches the disk
         # through the ledger's background writer after the reply: an agent killed in between
-        # leaves such records behind. Nothing would ever finish them, so they are probed again
-        # once the prober is up (_reprobe_interrupted): a GPU that passes stays with its pool, one
-        # that fails takes the normal replace path (drain -> release -> quarantine -> spare).
+        # leaves such records behind. Those whose probe-attempt marker is still there died WHILE
+        # the GPU was being probed; the rest only lost the state write. _reprobe_interrupted
+        # decides per record whether to probe again or fail it unprobed (ProbeInterrupted).
+        # Either way a failed GPU takes the normal replace path (drain -> release -> quarantine
+        # -> spare).
         interrupted = [u for u, r in self.records.items() if r.get("state") == "Probing"]
+        self._probing_since: dict[str, tuple[float, float]] = {}  # uuid -> (monotonic start, timeout)
         self.share_lib_dir = self._install_share_lib()
         self._pod_ids: tuple[float, set[str]] | None = None  # (listed at, device IDs pods hold)
         self._over_budget: set[tuple[str, str, str]] = set()  # (gpu, ns, pod) over their slot budget
@@ -208,7 +211,8 @@ class Agent:
         self.probe_mode = cfg.probe_mode or default_mode(self.backend)
         self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n,
                              arena_idle_s=cfg.probe_arena_idle_s,
-                             overlap_gemm_n=cfg.probe_overlap_gemm_n)
+                             overlap_gemm_n=cfg.probe_overlap_gemm_n,
+                             devices=[d for d in self.snap["devices"] if d.get("present", True)])
         self.last_probe: dict[str, dict] = {}
         # uuid -> monotonic time its VRAM was last freed wholesale (a release after its pods ended;
         # agent start: the previous agent process's allocations): the driver clears freed VRAM for
@@ -260,23 +264,47 @@ class Agent:
                  len(self.records))
 
     def _reprobe_interrupted(self, uuids: list[str]) -> None:
-        """Finish the claims a previous agent process left in 'Probing' (see __init__) by running
-        their claim-time probe again, before the RPC server starts. Failing them outright made a
-        kill in the few ms between the claim's reply and the background ledger write replace a
-        healthy GPU — and drain whatever its pool had started on it meanwhile. The probe is the
-        same ~1 ms test a claim runs; if a pod already holds most of the GPU's HBM the probe's
-        allocation fails and the GPU is replaced, as before."""
+        """Finish the claims a previous agent process left in 'Probing' (see __init__), before the
+        RPC server starts.
+
+        * Its probe-attempt marker (ledger.mark_probing) is there: the previous process died while
+          this GPU's probe was in flight. If that probe ran inside the dead process (inproc) or
+          this is the second death in a row during this GPU's probe, the GPU fails at once —
+          ProbeInterrupted, no new probe — so a GPU that takes down whatever probes it cannot
+          crash-loop the agent; its pool replaces it and the release quarantines it. Otherwise
+          (the probe ran in a helper, which a GPU fault cannot take the agent down with: the
+          death was something else — a rolling update, an OOM kill) it is probed again, once.
+        * No marker: the probe finished and only the Probing -> Claimed write was lost (a kill in
+          the few ms between the claim's reply and the background ledger write). Failing those
+          outright replaced healthy GPUs and drained what their pools had started on them, so
+          they are probed again; if a pod already holds most of the GPU's HBM the probe's
+          allocation fails and the GPU is replaced, as before.
+        Re-probes are marked like any probe, so a death during one counts as the second."""
+        markers = self.ledger.probing_markers()
         if not uuids:
+            self.ledger.clear_all_probing()
             return
+        failed_unprobed = []
         for u in uuids:
             rec = self.records[u]
             d = self.by_uuid.get(u)
             opts = (rec.get("policy") or {}).get("probe") or {}
-            if d is None:
+            m = markers.get(Ledger.safe_name(u))
+            if m is not None and (m.get("inAgent") or int(m.get("attempts") or 1) >= 2):
+                why = "its probe ran inside that process" if m.get("inAgent") else \
+                    f"{int(m.get('attempts') or 1)} agent processes in a row died during it"
+                res = {"passed": False, "backend": self.probe_mode, "ms": 0.0, "crashed": True,
+                       "error": f"ProbeInterrupted: the agent process died while this GPU's "
+                                f"claim-time probe was in flight ({why}); failed without probing "
+                                f"it again"}
+                failed_unprobed.append(u)
+            elif d is None:
                 res = {"passed": False, "backend": "none", "ms": 0.0,
                        "error": "ProbeInterrupted: the agent restarted during the claim-time "
                                 "probe and the GPU is no longer visible"}
             else:
+                self.ledger.mark_probing([u], in_agent=self.probe_mode == "inproc",
+                                         attempts=(int(m.get("attempts") or 1) + 1) if m else 1)
                 res = self.prober.probe_many([d], {**opts, "enabled": opts.get("enabled", True)})[0]
                 res["rerunAtStart"] = True
                 if not res.get("passed"):
@@ -291,7 +319,9 @@ class Agent:
             if not res.get("passed"):
                 self.stats["probe_failures"] += 1
         self.ledger.commit(self.records)
-        log.warning("re-probed %d GPU(s) whose claim-time probe a restart interrupted: %s", len(uuids),
+        self.ledger.clear_all_probing()
+        log.warning("finished %d claim(s) a restart interrupted (%d failed unprobed): %s",
+                    len(uuids), len(failed_unprobed),
                     {u: bool(self.records[u]["probe"].get("passed")) for u in uuids})
 
     # ================================================================ health
@@ -740,7 +770,7 @@ class Agent:
         if time.monotonic() - self._pid_miss.get(pid, -1e9) < 2.0:
             return {}  # unresolved a moment ago: retry later, not on every sample
         host_pid = pid
-        if pid == os.getpid():
+        if pid == os.getpid() or pid in self.prober.helper_pids():  # the agent / its probe helpers
             return {"namespace": "", "pod": "gpupool-agent"}
         import re
         pod: dict = {}
@@ -971,6 +1001,10 @@ class Agent:
         self._pods_kick = threading.Event()
         threading.Thread(target=run, daemon=True, name="podres-refresh").start()
 
+    # how long past spec.probe.timeoutSeconds a 'Probing' GPU is reported probeOverdue (the
+    # probe helper's own deadline answers well before: this covers a claim stuck elsewhere)
+    PROBE_GRACE_S = 5.0
+
     def _advertisable(self, uuid: str) -> bool:
         rec = self.records.get(uuid)
         if not rec or rec.get("state") != "Claimed":
@@ -993,6 +1027,13 @@ class Agent:
         }
         if rec:
             res = rec.get("resourceName", schema.DEFAULT_RESOURCE)
+            if rec.get("state") == "Probing":
+                ps = self._probing_since.get(uuid)
+                if ps is not None:
+                    el = time.monotonic() - ps[0]
+                    out["probingMs"] = round(el * 1e3, 1)
+                    if el > ps[1] + self.PROBE_GRACE_S:
+                        out["probeOverdue"] = True
             out.update({"state": rec.get("state", "Claimed"), "poolUID": rec["poolUID"],
                         "pool": rec.get("pool", ""), "resourceName": res,
                         "claimedAt": rec.get("claimedAt", ""),
@@ -1045,6 +1086,8 @@ class Agent:
                     self.verdicts.get(u, {}).get("healthy"))
                 uuids = [u for u in uuids if (self.records.get(u) or {}).get("poolUID") == pool_uid]
             devices = [self.device_view(u, pods) for u in uuids]
+            if self.prober.helpers is not None and not pool_uid:
+                extra["probeHelpers"] = self.prober.helpers.snapshot()
             return {"node": self.cfg.node, "backend": self.backend, "gen": self.gen, **extra,
                     "probeMode": self.probe_mode, "preflight": self.preflight,
                     "advertiseRequired": bool(self.cfg.plugin_dir),
@@ -1159,6 +1202,11 @@ class Agent:
             chosen = [by_index[i] for i in sel]
             lap("select")
             ts = now_rfc3339()
+            # a record still 'Probing' past its probe deadline (+ PROBE_GRACE_S) is reported
+            # probeOverdue: the manager replaces it instead of waiting on it forever
+            since = (time.monotonic(), float(probe_opts.get("timeoutSeconds") or DEFAULT_TIMEOUT_S))
+            for d in chosen:
+                self._probing_since[d["uuid"]] = since
             for d in chosen:
                 rec = {"uuid": d["uuid"], "poolUID": pool_uid, "pool": req.get("pool", ""),
                        "resourceName": resource, "policy": policy,
@@ -1176,10 +1224,20 @@ class Agent:
         for d in chosen:  # an in-flight HBM scrub window finishes and hands its buffer back
             self.scrubber.yield_device(d["uuid"])
         lap("scrubYield")
-        # probes run outside the lock, concurrently across GPUs
+        # probes run outside the lock, concurrently across GPUs, each in its GPU's probe helper;
+        # the probe-attempt markers tell a restarted agent which GPUs were mid-probe if this
+        # process dies now (_reprobe_interrupted)
+        uuids = [d["uuid"] for d in chosen]
+        probing = probe_opts.get("enabled", True) and self.probe_mode != "off"
         t0 = time.perf_counter()
-        results = self.prober.probe_many(chosen, {**probe_opts, "enabled":
-                                                  probe_opts.get("enabled", True)})
+        if probing:
+            self.ledger.mark_probing(uuids, in_agent=self.probe_mode == "inproc")
+        try:
+            results = self.prober.probe_many(chosen, {**probe_opts, "enabled":
+                                                      probe_opts.get("enabled", True)})
+        finally:
+            if probing:
+                self.ledger.clear_probing(uuids)
         probe_wall = (time.perf_counter() - t0) * 1e3
         lap("probe")
         if probe_opts.get("xgmiPeerCheck"):
@@ -1191,13 +1249,19 @@ class Agent:
                 if rec is None or rec["poolUID"] != pool_uid:
                     continue  # released concurrently
                 rec["probe"] = res
-                rec["state"] = "Claimed"
+                self._probing_since.pop(d["uuid"], None)
+                if rec.get("state") == "Probing":  # a pool may have cordoned it meanwhile
+                    rec["state"] = "Claimed"
                 self.last_probe[d["uuid"]] = res
                 self._probe_mono[d["uuid"]] = time.monotonic()
                 self.stats["probes"] += 1
                 self.stats["probe_ms_sum"] += float(res.get("ms", 0.0))
                 if not res.get("passed"):
                     self.stats["probe_failures"] += 1
+                    if res.get("timedOut"):
+                        self.stats["probe_timeouts"] = self.stats.get("probe_timeouts", 0) + 1
+                    elif res.get("crashed"):
+                        self.stats["probe_crashes"] = self.stats.get("probe_crashes", 0) + 1
             if not self._is_default_policy(policy):
                 # under the default policy the claimed GPU's verdict (baseline = the claim's
                 # snapshot = now) is the free GPU's current one: nothing to re-evaluate
@@ -1375,7 +1439,7 @@ class Agent:
         if not force and (every <= 0 or now - self._xgmi_last < every):
             return {}
         self._xgmi_last = now
-        if self.probe_mode not in ("inproc", "simulated"):
+        if self.probe_mode not in ("inproc", "simulated", "helper", "helper-sim"):
             return {}
         pods = self._pods_by_device()
         with self.lock:
@@ -1514,11 +1578,13 @@ class Agent:
                 if u in self.maintenance:
                     pass  # stays cordoned (its non-expiring maintenance entry is already there)
                 elif not probe_ok or not healthy:
-                    why = "probe failed" if not probe_ok else "; ".join(
+                    why = ("ProbeFailed: " + str((rec.get("probe") or {}).get("error") or
+                                                  "probe failed")) if not probe_ok else "; ".join(
                         self.verdicts.get(u, {}).get("reasons", []))
                     quarantined.append(self.ledger.quarantine(u, self.cfg.quarantine_s, why,
                                                               write=False))
                 del self.records[u]
+                self._probing_since.pop(u, None)
                 released.append(u)
                 self.freed_at[u] = time.monotonic()  # its pods' VRAM was just freed (scrubber)
             if released:
@@ -2022,9 +2088,18 @@ class Agent:
             for k, v in self.scrubber.stats.items():
                 lines.append(f"gpupool_agent_hbm_scrub_{k}_total {v}")
             lines.append(f"gpupool_agent_gen {self.gen}")
-            # devices the in-process HIP probe initialised (each holds a HIP context's VRAM)
-            lines.append(f"gpupool_agent_hip_devices {len(self.prober.ordinals)}")
+            # GPUs the agent's probe helpers (or, inproc, the agent) hold a HIP context on
+            lines.append(f"gpupool_agent_hip_devices {self.prober.hip_devices()}")
             lines.append(f"gpupool_agent_hip_init_ms {self.prober.init_ms:.1f}")
+            if self.prober.helpers is not None:
+                lines.append(f"gpupool_agent_probe_helpers_rss_bytes {self.prober.helpers_rss_bytes()}")
+                lines.append(f"gpupool_agent_probe_helpers {len(self.prober.helper_pids())}")
+                for k, v in self.prober.helpers.stats.items():
+                    lines.append(f"gpupool_agent_probe_{k}_total {v}")
+                for k, v in self.prober.helpers.snapshot().items():
+                    idx = self.by_uuid.get(k, {}).get("index", k)
+                    lines.append(f'gpupool_agent_probe_helper_up{{helper="{idx}",node="{self.cfg.node}"}} '
+                                 f"{1 if v.get('alive') else 0}")
         lines += process_metrics()
         return "\n".join(lines) + "\n"
 

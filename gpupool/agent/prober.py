@@ -1,14 +1,24 @@
 """Claim-time readiness probes (the MI355X replacement of `nvidia-smi` in a pod).
 
 Modes:
-  inproc     — libmi355x_probe.so loaded once in the agent; HIP contexts warmed at start so a
-               claim pays only the kernels (HBM pattern fill/verify + bf16 MFMA GEMM checks);
-               GPUs are probed concurrently (ctypes drops the GIL).
-  subprocess — `mi355x-probe --device N` per GPU: process isolation (a faulting probe cannot take
-               the agent down) at the cost of HIP initialisation per probe.
+  helper     — (default on real GPUs) the gfx950 probe runs in probe-helper child processes, one
+               per GPU, each with a HIP context on its GPU only (probehost.py): a probe that faults
+               kills its helper, not the agent; one that hangs is cut at spec.probe.timeoutSeconds.
+               Helpers are warm (started with the agent), so a claim pays the kernels plus one
+               pipe round trip. The xGMI peer ring runs in an on-demand fabric helper.
+  helper-sim — the same helpers running the simulated kernels (fake backend on CPU): the whole
+               isolation machinery — children, deadlines, crash replacement — without a GPU.
+  inproc     — libmi355x_probe.so loaded in the agent itself. Kept only for A/B measurements of
+               the helper's cost: a GPU fault in it takes the whole agent down.
+  subprocess — `mi355x-probe --device N` per GPU (cold HIP init per probe).
   simulated  — for the fake backend on CPU-only hosts: a fixed latency and a result that fails
                only when the fault overlay sets ``probeFail``. Never used with real GPUs.
   off        — no probe (result passes with backend "off").
+
+Probe failures the isolation produces (``error`` prefixes, surfaced on DeviceProbePassed):
+  ProbeCrashed — the helper died while probing this GPU (e.g. HIP aborted on a memory fault);
+  ProbeTimeout — the probe did not finish within spec.probe.timeoutSeconds; the helper was killed;
+  ProbeUnavailable — the GPU's helper is being replaced after a crash (backoff) or never came up.
 """
 from __future__ import annotations
 
@@ -21,13 +31,18 @@ import threading
 import time
 
 from ..ops import native_path
+from . import simprobe
 
 log = logging.getLogger("gpupool.agent.prober")
+
+HELPER_MODES = ("helper", "helper-sim")
+DEFAULT_TIMEOUT_S = 10.0  # spec.probe.timeoutSeconds default (schema.py)
 
 
 class Prober:
     def __init__(self, mode: str = "inproc", sim_ms: float = 20.0, gemm_n: int = 4096,
-                 max_workers: int = 16, arena_idle_s: float = 10.0, overlap_gemm_n: int = 2048):
+                 max_workers: int = 16, arena_idle_s: float = 10.0, overlap_gemm_n: int = 2048,
+                 devices: list[dict] | None = None, fabric_idle_s: float = 120.0):
         self.mode = mode
         self.sim_ms = sim_ms
         self.gemm_n = gemm_n                  # serial probe (pools with performance floors)
@@ -37,6 +52,7 @@ class Prober:
         self.overlap_gemm_n = overlap_gemm_n
         self.pool = cf.ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix="probe")
         self.ordinals: dict[str, int] = {}
+        self.helpers = None
         self.init_ms = 0.0
         t0 = time.perf_counter()
         if mode == "inproc":
@@ -44,12 +60,22 @@ class Prober:
             self._hip = hip_probe
             n = hip_probe.init()
             self.ordinals = hip_probe.hip_uuid_map()
-            log.info("HIP probe initialised: %d device(s) %s", n, sorted(self.ordinals))
+            log.warning("HIP probe initialised IN the agent (%d device(s)): a GPU fault during a "
+                        "probe takes the agent down; use --probe helper in production", n)
             # probe arenas stay allocated between back-to-back claims (scale-up bursts) and are
             # handed back to the GPU's workloads once idle for arena_idle_s
             self._trim_stop = threading.Event()
             self._trim_idle_ms = int(arena_idle_s * 1e3)
             threading.Thread(target=self._trim_loop, daemon=True, name="probe-trim").start()
+        elif mode in HELPER_MODES:
+            from .probehost import HelperPool
+            self.helpers = HelperPool("hip" if mode == "helper" else "sim", sim_ms=sim_ms,
+                                      arena_idle_s=arena_idle_s, fabric_idle_s=fabric_idle_s)
+            ready = self.helpers.start(list(devices or []))
+            up = sorted(u for u, r in ready.items() if r.get("ok"))
+            bad = {u: r.get("error") for u, r in ready.items() if not r.get("ok")}
+            log.info("probe helpers up for %d/%d GPU(s)%s", len(up), len(ready),
+                     f"; failed: {bad}" if bad else "")
         elif mode == "subprocess":
             out = subprocess.run([native_path("mi355x-probe"), "--list"], capture_output=True,
                                  text=True, timeout=120)
@@ -61,6 +87,62 @@ class Prober:
             raise ValueError(f"unknown probe mode {mode!r}")
         self.init_ms = (time.perf_counter() - t0) * 1e3
 
+    # ------------------------------------------------------------ visibility
+    def visible(self, dev: dict) -> bool:
+        """Can this prober run kernels on ``dev``?"""
+        if self.mode in HELPER_MODES:
+            return self.helpers.alive(dev["uuid"])
+        if self.mode in ("inproc", "subprocess"):
+            return str(dev.get("hipUUID", "")).lower() in self.ordinals
+        return True
+
+    def hip_devices(self) -> int:
+        """GPUs this agent holds a HIP context on (in itself or its helpers)."""
+        if self.mode == "helper":
+            return sum(1 for k, v in self.helpers.snapshot().items() if k != "fabric" and v.get("alive"))
+        return len(self.ordinals)  # helper-sim: no HIP anywhere (0)
+
+    def helpers_rss_bytes(self) -> int:
+        """Resident memory of the probe helpers together (the isolation's host-memory cost)."""
+        total = 0
+        for pid in self.helper_pids():
+            try:
+                with open(f"/proc/{pid}/statm") as f:
+                    total += int(f.read().split()[1]) * os.sysconf("SC_PAGESIZE")
+            except (OSError, ValueError, IndexError):
+                pass
+        return total
+
+    def helper_pids(self) -> set[int]:
+        return self.helpers.pids() if self.helpers is not None else set()
+
+    @staticmethod
+    def _hooks(dev: dict) -> dict:
+        """Fault-overlay hooks the helpers act out: probeCrash (the helper aborts, as HIP does on
+        a GPU memory fault) and probeHang (the probe never returns)."""
+        return {"crash": bool(simprobe.fault(dev, "probeCrash")),
+                "hang": bool(simprobe.fault(dev, "probeHang"))}
+
+    def _helper_call(self, dev: dict, op: str, args: dict, timeout: float) -> dict:
+        """A probe-like request to ``dev``'s helper; failures of the helper itself come back as a
+        failed result naming ProbeCrashed / ProbeTimeout / ProbeUnavailable."""
+        from .probehost import HelperError, HelperTimeout
+        idx = dev.get("index")
+        try:
+            h = self.helpers.get(dev["uuid"], dev)
+            return h.call(op, args, timeout)
+        except HelperTimeout:
+            self.helpers.kill(dev["uuid"], f"{op} of GPU {idx} missed its {timeout:g} s deadline")
+            return {"passed": False, "timedOut": True,
+                    "error": f"ProbeTimeout: the {op} of GPU {idx} did not finish within "
+                             f"{timeout:g} s (spec.probe.timeoutSeconds); its probe helper was "
+                             f"killed"}
+        except HelperError as e:
+            return {"passed": False, "crashed": e.kind == "ProbeCrashed",
+                    "error": f"{e.kind}: the probe helper of GPU {idx} {'died during the ' + op if e.kind == 'ProbeCrashed' else 'is unavailable'} ({e})"}
+        except RuntimeError as e:  # the request itself raised in the helper
+            return {"passed": False, "error": f"probe error: {e}"}
+
     def _one(self, dev: dict, opts: dict) -> dict:
         t0 = time.perf_counter()
         hbm = int(opts.get("hbmBytes", 1 << 30))
@@ -68,45 +150,38 @@ class Prober:
         if self.mode == "off" or not opts.get("enabled", True):
             return {"passed": True, "backend": "off", "ms": 0.0}
         if self.mode == "simulated":
-            time.sleep(self.sim_ms / 1e3)
-            fail = bool((dev.get("faults") or {}).get("probeFail")) or bool(dev.get("probeFail"))
-            # nominal numbers = the measured MI355X probe (profiles/r1c_probe_gemm_ab_real.json)
-            res = {"passed": not fail, "backend": "simulated",
-                   "hbm": {"ok": not fail, "GBps": 4900.0, "bytes": hbm},
-                   "mfma": {"ok": not fail, "tflops": 1200.0 if mfma else 0.0, "enabled": mfma}}
-            if mfma:  # the CU census: every CU of this (partition of the) GPU proves its MFMA pipes
-                cus = int((dev.get("asic") or {}).get("computeUnits") or 256)
-                dead = int(dev.get("cuFault") or 0)
-                res["cus"] = {"expected": cus, "mfmaVerified": cus - dead, "badWaves": dead * 8,
-                              "ok": dead == 0}
-                if dead and not fail:
-                    res["passed"] = False
-            if fail:
-                res["error"] = "injected probe failure (fault overlay)"
-            res["ms"] = (time.perf_counter() - t0) * 1e3
-            return res
-        ordinal = self.ordinals.get(str(dev.get("hipUUID", "")).lower())
-        if ordinal is None:
-            return {"passed": False, "backend": self.mode,
-                    "error": f"device {dev.get('hipUUID')} not visible to HIP in this process",
-                    "ms": 0.0}
-        if self.mode == "inproc":
-            # The HBM test and the MFMA phase normally overlap on two streams (~13 % shorter
-            # probe). With performance floors the pool wants clean numbers: run them serially.
-            floors = float(opts.get("minHbmGBps") or 0) > 0 or float(opts.get("minMfmaTflops") or 0) > 0
-            res = self._hip.run(ordinal, hbm_bytes=hbm, mfma=mfma,
-                                gemm_n=self.gemm_n if floors else self.overlap_gemm_n,
-                                overlap=0 if floors else 1)
+            return simprobe.probe(dev, opts, self.sim_ms)
+        # The HBM test and the MFMA phase normally overlap on two streams (~13 % shorter
+        # probe). With performance floors the pool wants clean numbers: run them serially.
+        floors = float(opts.get("minHbmGBps") or 0) > 0 or float(opts.get("minMfmaTflops") or 0) > 0
+        if self.mode in HELPER_MODES:
+            timeout = float(opts.get("timeoutSeconds") or DEFAULT_TIMEOUT_S)
+            args = {"hipUUID": dev.get("hipUUID", ""), "hbmBytes": hbm, "mfma": mfma,
+                    "gemmN": self.gemm_n if floors else self.overlap_gemm_n,
+                    "overlap": 0 if floors else 1, "hooks": self._hooks(dev)}
+            if self.mode == "helper-sim":
+                args.update(dev=dev, opts=opts)
+            res = self._helper_call(dev, "probe", args, timeout)
         else:
-            cmd = [native_path("mi355x-probe"), "--device", str(ordinal), "--hbm-bytes", str(hbm),
-                   "--gemm-n", str(self.gemm_n)] + ([] if mfma else ["--no-mfma"])
-            p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
-            try:
-                res = json.loads(p.stdout.strip().splitlines()[-1])
-            except (ValueError, IndexError):
-                res = {"passed": False, "error": f"probe exited {p.returncode}: {p.stderr[-300:]}"}
-        fault = (dev.get("faults") or {}).get("probeFail") or dev.get("probeFail")
-        if fault:  # fault overlay also applies on top of real hardware
+            ordinal = self.ordinals.get(str(dev.get("hipUUID", "")).lower())
+            if ordinal is None:
+                return {"passed": False, "backend": self.mode,
+                        "error": f"device {dev.get('hipUUID')} not visible to HIP in this process",
+                        "ms": 0.0}
+            if self.mode == "inproc":
+                res = self._hip.run(ordinal, hbm_bytes=hbm, mfma=mfma,
+                                    gemm_n=self.gemm_n if floors else self.overlap_gemm_n,
+                                    overlap=0 if floors else 1)
+            else:
+                cmd = [native_path("mi355x-probe"), "--device", str(ordinal), "--hbm-bytes",
+                       str(hbm), "--gemm-n", str(self.gemm_n)] + ([] if mfma else ["--no-mfma"])
+                p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+                try:
+                    res = json.loads(p.stdout.strip().splitlines()[-1])
+                except (ValueError, IndexError):
+                    res = {"passed": False, "error": f"probe exited {p.returncode}: {p.stderr[-300:]}"}
+        fault = simprobe.fault(dev, "probeFail")
+        if fault and res.get("passed"):  # fault overlay also applies on top of real hardware
             res["passed"] = False
             res["error"] = "injected probe failure (fault overlay)"
         res["backend"] = self.mode
@@ -176,12 +251,13 @@ class Prober:
         result {peer, GBps, passed[, error]}. Pairs run concurrently; the library serialises
         pairs that share a device. Empty when fewer than 2 GPUs or the mode cannot do it."""
         n = len(devs)
-        if n < 2 or self.mode not in ("inproc", "simulated"):
+        if n < 2 or self.mode not in ("inproc", "simulated") + HELPER_MODES:
             return {}
         # 16 MiB per link: ~0.25 ms over one xGMI link, enough for a stable GB/s figure
         nbytes = int(opts.get("xgmiBytes") or (16 << 20))
-        if self.mode == "inproc":
-            ring = self._ring_inproc(devs, nbytes)
+        timeout = float(opts.get("timeoutSeconds") or DEFAULT_TIMEOUT_S)
+        if self.mode in ("inproc",) + HELPER_MODES:
+            ring = self._ring_whole(devs, nbytes, timeout)
             if ring is not None:
                 return ring
 
@@ -193,14 +269,12 @@ class Prober:
             # peer access: an infrastructure problem, not corruption)
             bad = bool(faults.get("xgmiPeerFail")) or \
                 dst.get("index") in (faults.get("xgmiBadPeers") or [])
-            if faults.get("xgmiPeerUnavailable"):
-                r = {"passed": False, "canAccessPeer": False, "error": "hipDeviceCanAccessPeer=0"}
-            elif self.mode == "simulated" or bad:
-                r = {"passed": not bad, "canAccessPeer": True,
-                     "GBps": 64.0 * float(faults.get("probeScale") or 1.0),
-                     "badBits": 0 if not bad else 1}
-                if bad:
-                    r["error"] = "injected xGMI peer failure (fault overlay)"
+            if self.mode in ("simulated", "helper-sim") or bad or faults.get("xgmiPeerUnavailable"):
+                r = simprobe.link(src, dst)
+            elif self.mode == "helper":
+                r = self._fabric_call(devs, "peer", {"src": src.get("hipUUID", ""),
+                                                     "dst": dst.get("hipUUID", ""),
+                                                     "bytes": nbytes}, timeout)
             else:
                 a = self.ordinals.get(str(src.get("hipUUID", "")).lower())
                 b = self.ordinals.get(str(dst.get("hipUUID", "")).lower())
@@ -219,21 +293,44 @@ class Prober:
                 log.warning("xGMI peer check failed: %r", e)
         return out
 
-    def _ring_inproc(self, devs: list[dict], nbytes: int) -> dict[str, dict] | None:
+    def _fabric_call(self, devs: list[dict], op: str, args: dict, timeout: float) -> dict:
+        """A request to the fabric helper. Its failure says nothing about any one link, so it
+        comes back as a check that could not run (XGMIPeerCheckUnavailable, never a replace)."""
+        from .probehost import HelperError, HelperTimeout
+        try:
+            return self.helpers.fabric(devs).call(op, args, timeout)
+        except HelperTimeout:
+            self.helpers.kill("fabric", f"xGMI {op} missed its {timeout:g} s deadline")
+            return {"passed": False, "error": f"ProbeTimeout: xGMI {op} did not finish within "
+                                              f"{timeout:g} s; the fabric helper was killed"}
+        except HelperError as e:
+            return {"passed": False, "error": f"{e.kind}: fabric helper: {e}"}
+        except RuntimeError as e:
+            return {"passed": False, "error": f"xGMI {op} error: {e}"}
+
+    def _ring_whole(self, devs: list[dict], nbytes: int, timeout: float) -> dict[str, dict] | None:
         """All links of the ring in one library call, concurrently (each GPU pair of an MI355X node
         has its own xGMI link): one copy time instead of n. None when a device is not visible to HIP
         or an injected link fault must be honoured — the pairwise path handles those."""
-        if not hasattr(self._hip, "peer_ring"):
-            return None
-        ords = []
         for d in devs:
-            o = self.ordinals.get(str(d.get("hipUUID", "")).lower())
             f = {**(d.get("faults") or {}), **d}
-            if o is None or f.get("xgmiPeerFail") or f.get("xgmiBadPeers") or \
-                    f.get("xgmiPeerUnavailable"):
+            if f.get("xgmiPeerFail") or f.get("xgmiBadPeers") or f.get("xgmiPeerUnavailable"):
                 return None
-            ords.append(o)
-        r = self._hip.peer_ring(ords, nbytes)
+        if self.mode in HELPER_MODES:
+            args = {"hipUUIDs": [d.get("hipUUID", "") for d in devs], "bytes": nbytes}
+            if self.mode == "helper-sim":
+                args["devs"] = devs
+            r = self._fabric_call(devs, "peer_ring", args, timeout)
+        else:
+            if not hasattr(self._hip, "peer_ring"):
+                return None
+            ords = []
+            for d in devs:
+                o = self.ordinals.get(str(d.get("hipUUID", "")).lower())
+                if o is None:
+                    return None
+                ords.append(o)
+            r = self._hip.peer_ring(ords, nbytes)
         links = r.get("links")
         if not isinstance(links, list) or len(links) != len(devs):
             err = r.get("error") or "xGMI ring check returned no links"
@@ -246,11 +343,59 @@ class Prober:
             out[d["uuid"]] = link
         return out
 
-    def warm_arena(self, ordinal: int, hbm_bytes: int = 1 << 30) -> None:
+    # ------------------------------------------------------------ HBM scrubber kernels
+    SWEEP_TIMEOUT_S = 60.0      # one window: ~3 ms at 4 GiB; seconds behind a driver clear
+    SWEEP_MAP_TIMEOUT_S = 180.0  # mapping / freeing ~282 GiB: 0.2-6 s measured
+
+    def sweep_window(self, dev: dict, offset: int, nbytes: int, reserve: int) -> dict:
+        if self.mode == "simulated":
+            return simprobe.sweep_window(dev, offset, nbytes, reserve)
+        args = {"hipUUID": dev.get("hipUUID", ""), "offset": int(offset), "bytes": int(nbytes),
+                "reserve": int(reserve), "keep": True}
+        if self.mode in HELPER_MODES:
+            if self.mode == "helper-sim":
+                args["dev"] = dev
+            return self._helper_call(dev, "sweep", args, self.SWEEP_TIMEOUT_S)
+        o = self.ordinals.get(str(dev.get("hipUUID", "")).lower())
+        if o is None:
+            return {"passed": False, "error": "device not visible to HIP"}
+        return self._hip.hbm_sweep(o, offset, nbytes, reserve, keep=True)
+
+    def sweep_alloc(self, dev: dict, reserve: int) -> int:
+        """The scrubber's big buffer: 1 allocated, 0 already held, < 0 failed."""
+        if self.mode == "simulated":
+            return 1
+        if self.mode in HELPER_MODES:
+            r = self._helper_call(dev, "sweep_alloc", {"hipUUID": dev.get("hipUUID", ""),
+                                                       "reserve": int(reserve)},
+                                  self.SWEEP_MAP_TIMEOUT_S)
+            return r if isinstance(r, int) else -1
+        o = self.ordinals.get(str(dev.get("hipUUID", "")).lower())
+        return -1 if o is None else self._hip.sweep_alloc(o, reserve)
+
+    def sweep_release(self, dev: dict) -> None:
+        if self.mode == "simulated":
+            return
+        if self.mode in HELPER_MODES:
+            # a helper that died meanwhile took the buffer with it: nothing left to free
+            self._helper_call(dev, "sweep_release", {"hipUUID": dev.get("hipUUID", "")},
+                              self.SWEEP_MAP_TIMEOUT_S)
+            return
+        o = self.ordinals.get(str(dev.get("hipUUID", "")).lower())
+        if o is not None:
+            self._hip.sweep_release(o)
+
+    def warm_arena(self, dev: dict, hbm_bytes: int = 1 << 30) -> None:
         """Run one default-sized probe so the device's probe arena is allocated and kept (the
         library's trim skips it while an HBM sweep is held and for 30 s after its release)."""
         if self.mode == "inproc":
-            self._hip.run(ordinal, hbm_bytes=hbm_bytes, gemm_n=self.gemm_n)
+            o = self.ordinals.get(str(dev.get("hipUUID", "")).lower())
+            if o is not None:
+                self._hip.run(o, hbm_bytes=hbm_bytes, gemm_n=self.gemm_n)
+        elif self.mode in HELPER_MODES:
+            self._helper_call(dev, "warm", {"hipUUID": dev.get("hipUUID", ""),
+                                            "hbmBytes": hbm_bytes, "gemmN": self.gemm_n},
+                              self.SWEEP_TIMEOUT_S)
 
     def _trim_loop(self) -> None:
         period = max(0.05, min(1.0, self._trim_idle_ms / 4e3))
@@ -263,6 +408,8 @@ class Prober:
     def close(self) -> None:
         if self.mode == "inproc":
             self._trim_stop.set()
+        if self.helpers is not None:
+            self.helpers.stop()
         self.pool.shutdown(wait=False)
 
 
@@ -270,4 +417,4 @@ def default_mode(backend: str) -> str:
     env = os.environ.get("GPUPOOL_PROBE_MODE")
     if env:
         return env
-    return "simulated" if backend == "fake" else "inproc"
+    return "simulated" if backend == "fake" else "helper"

@@ -7,7 +7,8 @@ quarantined, no pod), every ``interval_s`` it tests ``windows_per_pass`` windows
 (``probe.hbm_sweep``, the same fill/verify kernels, both polarities), advancing a per-device
 cursor that is persisted with the claim ledger. One full sweep of 288 GB costs ~0.2 s of HBM time
 (4 passes over the data at ~6 TB/s), spread over passes so a claim never waits on more than one
-window (~3 ms at 4 GiB). Coverage is reported per device (``hbmSweep`` in the agent's device view
+window (~3 ms at 4 GiB). The kernels run in the GPU's probe helper (probehost.py), so a scrub that
+faults a GPU takes down that helper, never the agent. Coverage is reported per device (``hbmSweep`` in the agent's device view
 -> ``status.devices[].hbmCoverage``).
 
 Claims always win: the scrubber re-checks eligibility under a per-device lock before every window,
@@ -89,10 +90,6 @@ class HbmScrubber:
                 self._cv.wait(left)
         return True
 
-    def _ordinal(self, uuid: str) -> int | None:
-        d = self.agent.by_uuid.get(uuid) or {}
-        return self.agent.prober.ordinals.get(str(d.get("hipUUID", "")).lower())
-
     def _eligible(self, uuid: str) -> bool:
         a = self.agent
         if uuid in a.records or uuid in a.maintenance or uuid not in a.by_uuid:
@@ -105,22 +102,12 @@ class HbmScrubber:
 
     # ------------------------------------------------------------------ one window
     def _window(self, uuid: str, dev: dict, offset: int) -> dict:
+        """One window through the prober: in the GPU's probe helper (helper modes), the agent's
+        own HIP (inproc) or the simulated kernels (fake backend)."""
         p = self.agent.prober
-        if p.mode == "inproc":
-            ordinal = self._ordinal(uuid)
-            if ordinal is None:
-                return {"passed": False, "error": "device not visible to HIP"}
-            return p._hip.hbm_sweep(ordinal, offset, self.window_bytes, self.reserve_bytes,
-                                    keep=True)
-        # simulated: nominal window timing of the real kernels (~6 TB/s over 4 passes)
-        span = max(self.window_bytes, int(dev.get("memTotalBytes") or 288e9) - self.reserve_bytes)
-        off = offset % span
-        n = min(self.window_bytes, span - off)
-        time.sleep(min(0.05, 4 * n / 6e12))
-        bad_at = (dev.get("faults") or {}).get("hbmBadOffset", dev.get("hbmBadOffset"))
-        bad = 1 if bad_at is not None and off <= int(bad_at) < off + n else 0
-        return {"passed": not bad, "offset": off, "bytes": n, "span": span, "badBits": bad,
-                "firstBadOffset": int(bad_at) if bad else None, "GBps": 6000.0, "ms": 0.0}
+        if p.mode not in ("simulated", "helper-sim") and not p.visible(dev):
+            return {"passed": False, "error": "device not visible to HIP"}
+        return p.sweep_window(dev, offset, self.window_bytes, self.reserve_bytes)
 
     def _probes_quiet(self, timeout: float = 3.0) -> None:
         """Wait (bounded) until no claim-time probe runs on this agent. Mapping or unmapping the
@@ -141,14 +128,16 @@ class HbmScrubber:
         with self._cv:
             self._held.add(uuid)
         t0 = time.perf_counter()
-        if self.agent.prober.mode == "inproc":
+        p = self.agent.prober
+        if p.mode in ("inproc", "helper", "helper-sim"):
             self._probes_quiet()
-            o = self._ordinal(uuid)
+            dev = dict(self.agent.by_uuid.get(uuid) or {"uuid": uuid})
             # The claim-time probe arena comes first: a claim then never has to allocate while the
             # sweep buffer is held or while the driver clears it after the free (seconds).
-            if o is not None:
-                self.agent.prober.warm_arena(o)
-            if o is None or self.agent.prober._hip.sweep_alloc(o, self.reserve_bytes) < 0:
+            ok = p.visible(dev)
+            if ok:
+                p.warm_arena(dev)
+            if not ok or p.sweep_alloc(dev, self.reserve_bytes) < 0:
                 log.warning("HBM sweep buffer allocation failed on %s", uuid)
                 self._release(uuid)
                 return False
@@ -160,10 +149,10 @@ class HbmScrubber:
         """Free the sweep buffer (inproc: ~2.5 s for ~282 GiB, the driver clears released VRAM)."""
         t0 = time.perf_counter()
         try:
-            if self.agent.prober.mode == "inproc":
-                o = self._ordinal(uuid)
-                if o is not None:
-                    self.agent.prober._hip.sweep_release(o)
+            if self.agent.prober.mode in ("inproc", "helper", "helper-sim"):
+                self.agent.prober.sweep_release(dict(self.agent.by_uuid.get(uuid) or {"uuid": uuid}))
+        except Exception as e:  # a helper that died took the buffer with it
+            log.warning("HBM sweep buffer release on %s failed: %s", uuid, e)
         finally:
             log.info("HBM sweep buffer of %s released in %.1f ms", uuid,
                      (time.perf_counter() - t0) * 1e3)
@@ -182,7 +171,7 @@ class HbmScrubber:
         with self.agent.lock:
             if not self._eligible(uuid):
                 return rec
-        if grace and self.agent.prober.mode == "inproc":
+        if grace and self.agent.prober.mode in ("inproc", "helper"):
             freed = max(self._released_at.get(uuid, -1e9),
                         getattr(self.agent, "freed_at", {}).get(uuid, -1e9))
             if time.monotonic() - freed < self.CLEAR_GRACE_S:
@@ -230,7 +219,7 @@ class HbmScrubber:
                     self._fail(uuid, r)
                     break
         finally:
-            if self.agent.prober.mode == "inproc":
+            if self.agent.prober.mode in ("inproc", "helper", "helper-sim"):
                 self._probes_quiet()
             self._release(uuid)
             with self._mu:
@@ -291,7 +280,8 @@ class HbmScrubber:
             self._kick.clear()
 
     def start(self) -> None:
-        if self.interval_s <= 0 or self.agent.prober.mode not in ("inproc", "simulated"):
+        if self.interval_s <= 0 or self.agent.prober.mode not in ("inproc", "simulated", "helper",
+                                                                   "helper-sim"):
             return
         self._thread = threading.Thread(target=self._loop, daemon=True, name="hbm-scrub")
         self._thread.start()

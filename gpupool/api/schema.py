@@ -335,6 +335,16 @@ MI355X_SPEC = {
                                   "description": "Performance floor for the probe's 4096^3 bf16 "
                                                  "MFMA GEMM in TFLOP/s (0 = off; MI355X "
                                                  "measures ~1200)."},
+                "timeoutSeconds": {"type": "number", "minimum": 0.1, "maximum": 600,
+                                   "default": 10,
+                                   "description": "Deadline of one GPU's probe (and of the "
+                                                  "xGMI peer ring). The probe runs in a helper "
+                                                  "process per GPU: past the deadline the "
+                                                  "helper is killed and the GPU fails "
+                                                  "DeviceProbePassed (ProbeTimeout); a helper "
+                                                  "that dies mid-probe fails it as "
+                                                  "ProbeCrashed. A claim is answered within "
+                                                  "this deadline however the GPU behaves."},
             },
         },
         "replacePolicy": {"type": "string", "enum": ["Replace", "Keep"], "default": "Replace"},

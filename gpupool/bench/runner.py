@@ -507,6 +507,12 @@ class BenchRun:
                     text = str(get())
                     m = re.search(r"^gpupool_agent_hip_devices (\d+)", text, re.M)
                     out[who]["hip_devices"] = int(m.group(1)) if m else None
+                    # the per-GPU probe helpers (child processes: their RSS is not the agent's)
+                    m = re.search(r"^gpupool_agent_probe_helpers_rss_bytes (\d+)", text, re.M)
+                    if m:
+                        out[who]["helpers_rss_mib"] = round(int(m.group(1)) / 2**20, 1)
+                        m = re.search(r"^gpupool_agent_probe_helpers (\d+)", text, re.M)
+                        out[who]["helpers"] = int(m.group(1)) if m else None
                     out[who]["vram_used_mib"] = {
                         int(i): round(float(v) / 2**20, 1) for i, v in re.findall(
                             r'^gpupool_device_vram_used_bytes\{[^}]*index="(\d+)"[^}]*\} ([0-9.e+]+)',

@@ -66,6 +66,7 @@ struct Mi355xPoolSpec {
   int64_t probe_recheck_seconds = 0;  // periodic re-probe of idle claimed GPUs (0 = off)
   bool probe_xgmi_peer_check = false;   // ring peer-copy check across the pool's GPUs
   double probe_min_xgmi_gbps = 0;
+  double probe_timeout_seconds = 10;  // per-GPU probe deadline (agent's probe helper)
   Json probe_json() const;            // the probe options sent with claims and policy updates
   std::string replace_policy = "Replace";
   int32_t max_nodes = 1;  // nodes the pool may span

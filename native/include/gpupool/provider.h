@@ -111,6 +111,9 @@ struct DeviceView {
   std::string state;  // Free | Claimed | Draining | Quarantined | Probing
   std::string pool_uid, pool;
   bool healthy = false, advertised = false, probe_passed = false;
+  // 'Probing' past spec.probe.timeoutSeconds (+ the agent's grace): the claim that probes it is
+  // stuck outside its probe helper's deadline — replaced like a failed probe, never waited on
+  bool probe_overdue = false;
   Json verdict, probe, pods, partition, hbm_sweep, xgmi_pairs, sharing;
   Json telemetry;     // agent-sampled utilisation: gfx/umc activity %, power W, VRAM used/total
   std::string claimed_at, drain_started_at;

@@ -84,6 +84,7 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.probe_recheck_seconds = pr["recheckSeconds"].as_int(0);
   p.probe_xgmi_peer_check = pr["xgmiPeerCheck"].as_bool(false);
   p.probe_min_xgmi_gbps = pr["minXgmiGBps"].as_double(0);
+  p.probe_timeout_seconds = pr["timeoutSeconds"].as_double(10);
   p.replace_policy = s["replacePolicy"].str_or("Replace");
   p.max_nodes = static_cast<int32_t>(s["maxNodes"].as_int(1));
   p.sharing_replicas = static_cast<int32_t>(std::max<int64_t>(1, s.path("sharing.replicasPerGPU").as_int(1)));
@@ -107,6 +108,7 @@ Json Mi355xPoolSpec::probe_json() const {
   j["recheckSeconds"] = probe_recheck_seconds;
   j["xgmiPeerCheck"] = probe_xgmi_peer_check;
   j["minXgmiGBps"] = probe_min_xgmi_gbps;
+  j["timeoutSeconds"] = probe_timeout_seconds;
   return j;
 }
 
@@ -297,6 +299,10 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
     errs.push_back("spec.probe.recheckSeconds: should be greater than or equal to 0");
   if (pr.contains("xgmiPeerCheck") && !pr["xgmiPeerCheck"].is_bool())
     errs.push_back("spec.probe.xgmiPeerCheck: must be of type boolean");
+  if (pr.contains("timeoutSeconds") &&
+      (!pr["timeoutSeconds"].is_number() || pr["timeoutSeconds"].as_double(0) < 0.1 ||
+       pr["timeoutSeconds"].as_double(0) > 600))
+    errs.push_back("spec.probe.timeoutSeconds: must be within [0.1, 600]");
   for (const char* k : {"minHbmGBps", "minMfmaTflops", "minXgmiGBps"})
     if (pr.contains(k) && (!pr[k].is_number() || pr[k].as_double(0) < 0))
       errs.push_back(std::string("spec.probe.") + k + ": should be greater than or equal to 0");

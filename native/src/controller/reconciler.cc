@@ -619,8 +619,13 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
     devices.push_back(d.status_json());
     if (d.state == "Draining") continue;
     ++claimed;
-    if (d.state == "Probing") {
+    if (d.state == "Probing" && !d.probe_overdue) {
       ++probing;
+      continue;
+    }
+    if (d.probe_overdue) {
+      probe_bad.push_back(short_id(d) + ": ProbeTimeout: still Probing past spec.probe.timeoutSeconds");
+      unhealthy.push_back(short_id(d));
       continue;
     }
     auto reasons = [&](const char* prefix) {
@@ -685,7 +690,16 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
   if (probing) {
     set_condition(conds, gen::kCondDeviceProbePassed, "Unknown", "Probing", std::to_string(probing) + " GPU(s) probing", gen, now);
   } else if (!probe_bad.empty()) {
-    set_condition(conds, gen::kCondDeviceProbePassed, "False", "ProbeFailed", join(probe_bad, " | "), gen, now);
+    // the isolation outcomes name themselves (ProbeCrashed / ProbeTimeout / ProbeInterrupted /
+    // ProbeUnavailable: the probe helper died, missed its deadline, or a restarted agent found the
+    // GPU mid-probe); any other failure is ProbeFailed
+    std::string why = "ProbeFailed";
+    for (const char* k : {"ProbeCrashed", "ProbeTimeout", "ProbeInterrupted", "ProbeUnavailable"}) {
+      bool all = true;
+      for (const auto& b : probe_bad) all = all && b.find(std::string(": ") + k + ":") != std::string::npos;
+      if (all) why = k;
+    }
+    set_condition(conds, gen::kCondDeviceProbePassed, "False", why, join(probe_bad, " | "), gen, now);
   } else if (claimed) {
     char msg[200];
     std::snprintf(msg, sizeof msg, "%lld GPU(s) passed HBM+MFMA probe (min HBM %.0f GB/s, min MFMA %.0f TFLOP/s)",
@@ -801,7 +815,7 @@ PoolPlan plan_pool(const Mi355xPoolSpec& spec, const std::vector<DeviceView>& mi
   std::vector<const DeviceView*> keep;
   for (const auto& d : mine) {
     if (d.state == "Draining") continue;  // already on its way out
-    const bool bad = d.state != "Probing" && (!d.healthy || !d.probe_passed);
+    const bool bad = d.probe_overdue || (d.state != "Probing" && (!d.healthy || !d.probe_passed));
     if (bad && spec.replace_policy == "Replace") plan.replace.push_back(d.uuid);
     else keep.push_back(&d);
   }
@@ -888,7 +902,8 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
       if (x.uuid == u) d = &x;
     std::vector<std::string> r;
     for (const auto& x : d->verdict["reasons"].elements()) r.push_back(x.as_string());
-    if (!d->probe_passed) r.push_back("ProbeFailed: " + d->probe["error"].str_or("probe failed"));
+    if (d->probe_overdue) r.push_back("ProbeTimeout: still probing past spec.probe.timeoutSeconds");
+    else if (!d->probe_passed) r.push_back("ProbeFailed: " + d->probe["error"].str_or("probe failed"));
     event_(obj, "Warning", "HealthDegraded", short_id(*d) + " unhealthy (" + join(r, "; ") + "): replacing");
     progress_reason = "ReplacingUnhealthy";
     progress_msg = "replacing " + short_id(*d);

@@ -27,6 +27,7 @@ DeviceView DeviceView::from(const Json& j) {
   d.healthy = j["healthy"].as_bool(false);
   d.advertised = j["advertised"].as_bool(false);
   d.probe_passed = j.path("probe.passed").as_bool(false);
+  d.probe_overdue = d.state == "Probing" && j["probeOverdue"].as_bool(false);
   d.verdict = j["verdict"];
   d.probe = j["probe"];
   d.pods = j["pods"].is_array() ? j["pods"] : Json::array();
@@ -57,6 +58,7 @@ Json DeviceView::status_json() const {
     std::string msg = probe["error"].str_or(probe["message"].str_or("probe failed"));
     reasons.push_back("ProbeFailed: " + msg);
   }
+  if (probe_overdue) reasons.push_back("ProbeTimeout: still probing past spec.probe.timeoutSeconds");
   s["reasons"] = reasons;
   s["advertised"] = advertised;
   Json pods_out = Json::array();

@@ -69,6 +69,13 @@ TEST(plan_replaces_unhealthy_and_failed_probe) {
   p = plan_pool(spec(2), {gpu(0), gpu(1, true, false, 0, "Probing")});
   EXPECT_TRUE(p.replace.empty());
   EXPECT_EQ(p.need, 0);
+  // ...unless the agent reports it past its probe deadline: then it is replaced, not waited on
+  auto overdue = gpu(1, true, false, 0, "Probing");
+  overdue.probe_overdue = true;
+  p = plan_pool(spec(2), {gpu(0), overdue});
+  EXPECT_EQ(ids(p.replace), std::string("n0-gpu1"));
+  EXPECT_EQ(p.keep, 1);
+  EXPECT_EQ(p.need, 1);
 }
 
 TEST(plan_scale_down_victim_order) {

@@ -31,7 +31,7 @@ def main() -> int:
     a = ap.parse_args()
     wd = a.workdir or tempfile.mkdtemp(prefix="gpupool-run-")
     nodes = [NodeSpec(f"mi355x-node-{i}", backend=a.backend, kubelet=not a.no_kubelet,
-                      probe="" if a.backend == "fake" else "inproc") for i in range(a.nodes)]
+                      probe="" if a.backend == "fake" else "helper") for i in range(a.nodes)]
     c = Cluster(wd, nodes=nodes)
     c.start()
     cfg = load_config()

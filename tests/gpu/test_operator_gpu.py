@@ -42,7 +42,7 @@ def test_devlib_amdsmi_matches_cli(native_built):
 
 
 def test_config2_pool_ready_on_real_gpu(cluster_factory):
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
     k = c.client
     t0 = time.perf_counter()
     k.create(MI355XPOOLS, pool("p", 1), "default")
@@ -51,7 +51,7 @@ def test_config2_pool_ready_on_real_gpu(cluster_factory):
     assert dt < 30.0  # BASELINE target
     d = obj["status"]["devices"][0]
     assert d["health"] == "Healthy" and d["advertised"] and d["probe"]["passed"]
-    assert d["probe"]["backend"] == "inproc" and d["probe"]["hbmGBps"] > 1000
+    assert d["probe"]["backend"] == "helper" and d["probe"]["hbmGBps"] > 1000
     conds = {x["type"]: x["status"] for x in obj["status"]["conditions"]}
     assert conds["XGMILinksHealthy"] == "True" and conds["HBMECCHealthy"] == "True"
     assert conds["ThermalHealthy"] == "True" and conds["DeviceProbePassed"] == "True"
@@ -63,7 +63,7 @@ def test_config2_pool_ready_on_real_gpu(cluster_factory):
 
 
 def test_workload_pod_runs_on_allotted_gpu_then_drain(cluster_factory, tmp_path):
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
     k = c.client
     k.create(MI355XPOOLS, pool("p", 1), "default")
     obj = k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=60)
@@ -95,7 +95,7 @@ def test_workload_pod_runs_on_allotted_gpu_then_drain(cluster_factory, tmp_path)
 
 
 def test_fault_overlay_on_real_hardware(cluster_factory):
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
     k = c.client
     k.create(MI355XPOOLS, pool("p", 1, replacePolicy="Keep"), "default")
     obj = k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=60)
@@ -114,7 +114,7 @@ def test_fault_overlay_on_real_hardware(cluster_factory):
 def test_performance_floor_on_real_gpu(cluster_factory):
     """spec.probe.minMfmaTflops above what any MI355X reaches: the (correct) GPU fails
     DeviceProbePassed with PerformanceBelowFloor and the pool does not report Ready."""
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
     k = c.client
     k.create(MI355XPOOLS, pool("slow", 1, probe={"minMfmaTflops": 100000}, replacePolicy="Keep"),
              "default")
@@ -135,7 +135,7 @@ def test_mi355xjob_torchrun_worker_on_pool_gpu(cluster_factory, tmp_path):
     so world size is 1; multi-rank rendezvous is covered by the CPU job tests. Attempt 1 fails on
     purpose at step 25 and the restarted gang resumes from its checkpoint (spec.checkpointDir)."""
     from gpupool.kube import MI355XJOBS
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
     k = c.client
     k.create(MI355XPOOLS, pool("p", 1), "default")
     obj = k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=60)
@@ -177,7 +177,7 @@ def test_autoscaled_pool_grows_for_pending_gpu_pod(cluster_factory, tmp_path):
     """spec.autoscale on real hardware: an empty pool grows to 1 when a pod asks for its GPU,
     the GPU is probed and advertised, the pod runs on it, and the pool shrinks back once the pod
     has finished."""
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
     k = c.client
     k.create(MI355XPOOLS, pool("auto", 0, autoscale={"enabled": True, "maxReplicas": 1,
                                                      "scaleDownDelaySeconds": 0}), "default")
@@ -202,7 +202,7 @@ def test_hbm_scrub_on_real_gpu_and_claim_is_not_blocked(cluster_factory):
     pattern-tested through the RPC, coverage lands in the agent view; a claim issued right after
     (while the ~280 GB buffer is being freed, ~3 s) is Ready in well under a second, and the pod
     Allocate path waits for the free. status.devices[] carries the CU census and coverage."""
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc", extra_args=[
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper", extra_args=[
         "--scrub-interval", "0", "--scrub-window", str(16 << 30)])])
     r = c.agent_request("gpu-node", "POST", "/v1/scrub", {"gpu": "0", "windows": 2})
     assert r["ok"], r
@@ -269,7 +269,7 @@ def test_amdsmi_ras_event_source_and_utilisation_on_real_gpu(native_built):
 
 
 def test_agent_exports_events_and_utilisation_on_real_gpu(cluster_factory):
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
     k = c.client
     k.create(MI355XPOOLS, pool("u", 1), "default")
     k.wait_for(MI355XPOOLS, "u", "default", ready_at(1), timeout=60)
@@ -312,7 +312,7 @@ def test_time_sliced_pods_share_the_real_gpu(cluster_factory):
     """spec.sharing.replicasPerGPU on hardware: the one MI355X is advertised as 3 slots and three
     pods compute on it at the same time (each a torch matmul loop through the ROCR_VISIBLE_DEVICES
     the plugin handed it), all seeing the same GPU."""
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
     k = c.client
     k.create(MI355XPOOLS, pool("shared", 1, sharing={"replicasPerGPU": 3}), "default")
     obj = k.wait_for(MI355XPOOLS, "shared", "default", ready_at(1), timeout=60)
@@ -348,7 +348,7 @@ def test_isolated_slots_and_per_pod_accounting_on_the_real_gpu(cluster_factory):
     (8 GiB HBM and 128 CUs each). Pod "small" holds 2 GiB, pod "big" 6 GiB and is refused 4 GiB
     more (its slot's budget), both see an 8 GiB GPU; meanwhile the agent's per-pod accounting
     (amdsmi process list -> pod) shows both pods on the same uuid with their distinct VRAM."""
-    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="inproc")])
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
     k = c.client
     k.create(MI355XPOOLS, pool("iso", 1, sharing={"replicasPerGPU": 2, "hbmBytesPerSlot": 8 << 30,
                                                   "cuPerSlot": 128}), "default")
@@ -397,3 +397,87 @@ def test_isolated_slots_and_per_pod_accounting_on_the_real_gpu(cluster_factory):
     assert 6 << 30 <= use["big"]["vramBytes"] <= 8 << 30, use
     for name in ("small", "big"):
         k.delete(PODS, name, "default", grace=0)
+
+
+def _maps(pid: int) -> str:
+    with open(f"/proc/{pid}/maps") as f:
+        return f.read()
+
+
+def test_probe_runs_in_a_helper_never_in_the_agent(cluster_factory):
+    """The claim-time probe's HIP runs in the GPU's probe helper: the agent process (device plugin,
+    health, claims for every GPU of the node) never maps libmi355x_probe.so, the helper does."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
+    k = c.client
+    k.create(MI355XPOOLS, pool("p", 1), "default")
+    obj = k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=60)
+    assert obj["status"]["devices"][0]["probe"]["passed"]
+    agent_pid = c.procs["agent-gpu-node"].pid
+    assert "libmi355x_probe" not in _maps(agent_pid)
+    view = c.agent_request("gpu-node", "GET", "/v1/node")
+    helpers = {k2: v for k2, v in view["probeHelpers"].items() if k2 != "fabric"}
+    assert helpers and all(v["alive"] for v in helpers.values()), helpers
+    for v in helpers.values():
+        assert "libmi355x_probe" in _maps(v["pid"])
+    print("helpers", helpers)
+
+
+def _probe_cond(o):
+    return next((x for x in ((o or {}).get("status") or {}).get("conditions", [])
+                 if x["type"] == "DeviceProbePassed"), {})
+
+
+def test_probe_helper_crash_on_the_real_gpu_leaves_the_agent_serving(cluster_factory):
+    """A probe that aborts its process (what HIP does on a GPU memory fault; injected with the
+    overlay's probeCrash) on the MI355X: the pool's DeviceProbePassed turns False with reason
+    ProbeCrashed, the agent keeps answering, a fresh helper with a HIP context on the GPU replaces
+    the dead one, and once the fault is gone the GPU passes again."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper",
+                                        extra_args=["--quarantine", "1"])])
+    k = c.client
+    c.set_faults("gpu-node", {"devices": {"0": {"probeCrash": True}}})
+    k.create(MI355XPOOLS, pool("p", 1, replacePolicy="Keep"), "default")
+    o = k.wait_for(MI355XPOOLS, "p", "default",
+                   lambda o: _probe_cond(o).get("status") == "False", timeout=60)
+    cond = _probe_cond(o)
+    assert cond["reason"] == "ProbeCrashed" and "SIGABRT" in cond["message"], cond
+    view = c.agent_request("gpu-node", "GET", "/v1/node")  # the agent is alive and serving
+    uuid = o["status"]["devices"][0]["uuid"]
+    deadline = time.monotonic() + 60
+    while not (view["probeHelpers"].get(uuid) or {}).get("alive") and time.monotonic() < deadline:
+        time.sleep(0.2)
+        view = c.agent_request("gpu-node", "GET", "/v1/node")
+    assert view["probeHelpers"][uuid]["alive"], view["probeHelpers"]
+    assert "SIGABRT" in view["probeHelpers"][uuid]["lastExit"]
+    c.set_faults("gpu-node", {})
+    k.delete(MI355XPOOLS, "p", "default")
+    k.wait_for(MI355XPOOLS, "p", "default", lambda o: o is None, timeout=60)
+    time.sleep(1.5)  # the 1 s quarantine of the crashed GPU runs out
+    k.create(MI355XPOOLS, pool("q", 1), "default")
+    obj = k.wait_for(MI355XPOOLS, "q", "default", ready_at(1), timeout=60)
+    assert obj["status"]["devices"][0]["probe"]["passed"]
+
+
+def test_hung_probe_on_the_real_gpu_is_cut_at_its_deadline(cluster_factory):
+    """A probe that never returns (overlay probeHang) with spec.probe.timeoutSeconds 2: the claim
+    is answered within the deadline + 1 s, DeviceProbePassed says ProbeTimeout, the hung helper
+    is killed and replaced."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
+    k = c.client
+    c.set_faults("gpu-node", {"devices": {"0": {"probeHang": True}}})
+    t0 = time.monotonic()
+    k.create(MI355XPOOLS, pool("p", 1, replacePolicy="Keep", probe={"timeoutSeconds": 2}), "default")
+    o = k.wait_for(MI355XPOOLS, "p", "default",
+                   lambda o: _probe_cond(o).get("status") == "False", timeout=60)
+    dt = time.monotonic() - t0
+    cond = _probe_cond(o)
+    assert cond["reason"] == "ProbeTimeout", cond
+    assert dt < 2 + 1 + 1.0, dt  # deadline + 1 s (+ the manager's own round trips)
+    c.set_faults("gpu-node", {})
+    view = c.agent_request("gpu-node", "GET", "/v1/node")
+    uuid = o["status"]["devices"][0]["uuid"]
+    deadline = time.monotonic() + 60
+    while not (view["probeHelpers"].get(uuid) or {}).get("alive") and time.monotonic() < deadline:
+        time.sleep(0.2)
+        view = c.agent_request("gpu-node", "GET", "/v1/node")
+    assert view["probeHelpers"][uuid]["alive"], view["probeHelpers"]

@@ -257,7 +257,7 @@ def test_agent_crash_mid_probe_replaces_a_gpu_that_fails_the_rerun(node8):
         return ready_at(2)(o) and victim["uuid"] not in {d["uuid"] for d in o["status"]["devices"]}
     k.wait_for(MI355XPOOLS, "p", "default", replaced, timeout=30)
     d = next(x for x in agent_view(node8)["devices"] if x["uuid"] == victim["uuid"])
-    assert d["state"] == "Quarantined" and "probe failed" in d["quarantine"]["reason"]
+    assert d["state"] == "Quarantined" and "ProbeInterrupted" in d["quarantine"]["reason"]
     msgs = " ".join(e.get("message", "") for e in settled_events(k))
     assert "ProbeInterrupted, re-run at agent start" in msgs, msgs
 

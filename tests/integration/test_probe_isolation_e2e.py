@@ -1,0 +1,107 @@
+"""Probe isolation end to end (apiserver-sim + C++ manager + node agent with per-GPU probe helpers
+running the simulated kernels): a GPU whose claim-time probe aborts its process, or never returns,
+is failed (ProbeCrashed / ProbeTimeout on DeviceProbePassed), replaced by a spare and quarantined —
+and the agent keeps serving every other GPU. An agent killed while a probe hangs comes back and
+fails that GPU as ProbeInterrupted without probing it again (the
+reference's throwaway-pod GPU check, GPU调度平台搭建.md:134-138)."""
+from __future__ import annotations
+
+import signal
+import time
+
+import pytest
+
+from gpupool.kube import MI355XPOOLS
+from gpupool.testing.cluster import NodeSpec
+
+from .helpers import conds, mi_pool, ready_at, settled_events
+
+pytestmark = pytest.mark.slow
+NODE = "mi355x-node-0"
+
+
+def helper_node(**kw) -> NodeSpec:
+    return NodeSpec(NODE, probe="helper-sim", count=4,
+                    extra_args=["--probe-sim-ms", "2", "--scrub-interval", "0"], **kw)
+
+
+def view(c):
+    return c.agent_request(NODE, "GET", "/v1/node")
+
+
+def dev_by_index(c, i: int) -> dict:
+    return next(d for d in view(c)["devices"] if d["index"] == i)
+
+
+def test_probe_crash_is_replaced_and_quarantined_while_the_agent_serves(cluster_factory):
+    c = cluster_factory(nodes=[helper_node()])
+    k = c.client
+    agent_pid = c.procs[f"agent-{NODE}"].pid
+    c.set_faults(NODE, {"devices": {"0": {"probeCrash": True}}})
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    o = k.wait_for(MI355XPOOLS, "p", "default", ready_at(2), timeout=30)
+    assert 0 not in {d["index"] for d in o["status"]["devices"]}
+    events = settled_events(k)
+    assert any(e["reason"] == "HealthDegraded" and "ProbeCrashed" in e.get("message", "")
+               for e in events), [(e["reason"], e.get("message")) for e in events]
+    g0 = dev_by_index(c, 0)
+    assert g0["state"] == "Quarantined" and "ProbeCrashed" in g0["quarantine"]["reason"], g0
+    assert c.procs[f"agent-{NODE}"].poll() is None and c.procs[f"agent-{NODE}"].pid == agent_pid
+    metrics = c.agent_request(NODE, "GET", "/metrics")
+    assert "gpupool_agent_probe_helper_crashes_total 1" in metrics
+
+
+def test_crash_is_named_on_device_probe_passed(cluster_factory):
+    c = cluster_factory(nodes=[helper_node()])
+    k = c.client
+    c.set_faults(NODE, {"devices": {"0": {"probeCrash": True}}})
+    k.create(MI355XPOOLS, mi_pool("keep", 1, replacePolicy="Keep"), "default")
+    o = k.wait_for(MI355XPOOLS, "keep", "default",
+                   lambda o: conds(o).get("DeviceProbePassed", {}).get("status") == "False",
+                   timeout=30)
+    cond = conds(o)["DeviceProbePassed"]
+    assert cond["reason"] == "ProbeCrashed" and "SIGABRT" in cond["message"], cond
+    assert o["status"]["readyReplicas"] == 0
+
+
+def test_hung_probe_answers_at_its_deadline_and_the_pool_converges_on_a_spare(cluster_factory):
+    c = cluster_factory(nodes=[helper_node()])
+    k = c.client
+    c.set_faults(NODE, {"devices": {"0": {"probeHang": True}}})
+    t0 = time.monotonic()
+    k.create(MI355XPOOLS, mi_pool("p", 1, probe={"timeoutSeconds": 1}), "default")
+    o = k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=30)
+    dt = time.monotonic() - t0
+    assert o["status"]["devices"][0]["index"] == 1
+    assert dt < 1 + 1 + 3, dt  # the hung probe's deadline + 1 s, then the spare's claim
+    events = settled_events(k)
+    assert any("ProbeTimeout" in e.get("message", "") for e in events)
+    assert "ProbeTimeout" in dev_by_index(c, 0)["quarantine"]["reason"]
+
+
+def test_agent_killed_mid_probe_comes_back_and_converges(cluster_factory):
+    """The agent dies (SIGKILL, with its helpers) while GPU 0's probe hangs. The restarted agent
+    finds GPU 0 'Probing' with its probe-attempt marker: the probe ran in a helper, so the death
+    was not the GPU's doing and it is probed once more — in a helper, with its deadline — fails
+    (ProbeTimeout), and the pool converges on a spare. (A second death during that re-probe would
+    fail it unprobed: tests/unit/test_probe_isolation.py.)"""
+    node = helper_node()
+    c = cluster_factory(nodes=[node])
+    k = c.client
+    c.set_faults(NODE, {"devices": {"0": {"probeHang": True}}})
+    k.create(MI355XPOOLS, mi_pool("p", 1, probe={"timeoutSeconds": 2}), "default")
+    deadline = time.monotonic() + 20
+    while dev_by_index(c, 0).get("state") != "Probing":
+        assert time.monotonic() < deadline
+        time.sleep(0.05)
+    time.sleep(0.2)
+    c._kill(f"agent-{NODE}", signal.SIGKILL)
+    t0 = time.monotonic()
+    c.start_agent(node)
+    g0 = dev_by_index(c, 0)
+    assert g0["probe"]["error"].startswith("ProbeInterrupted, re-run at agent start: ProbeTimeout"), \
+        (g0["probe"], c.log(f"agent-{NODE}")[-3000:])
+    o = k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=30)
+    assert o["status"]["devices"][0]["index"] != 0
+    assert time.monotonic() - t0 < 20, c.log(f"agent-{NODE}")[-3000:]
+    assert "ProbeTimeout" in dev_by_index(c, 0)["quarantine"]["reason"]

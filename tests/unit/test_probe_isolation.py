@@ -1,0 +1,199 @@
+"""Probe isolation (gpupool/agent/probehost.py): the claim-time probe runs in per-GPU helper
+processes with a deadline, so a GPU whose probe aborts its process or never returns cannot take the
+node agent down or wedge its pool (the reference checks a GPU in a
+throwaway pod, GPU调度平台搭建.md:134-138).
+
+The helpers here run the simulated kernels (``helper-sim``): the same child processes, pipes,
+deadlines and crash replacement as on MI355X, with the fault overlay's ``probeCrash`` (the helper
+calls abort(), as HIP does on a GPU memory fault) and ``probeHang`` (the probe never returns)."""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+
+import pytest
+
+from gpupool.agent.agent import Agent, AgentConfig
+from gpupool.agent.ledger import Ledger
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+FIXTURE = os.path.join(ROOT, "tests", "fixtures", "node_8x_mi355x.json")
+
+
+def make_agent(tmp_path, faults: dict | None = None, count: int = 4) -> Agent:
+    fp = str(tmp_path / "faults.json")
+    json.dump(faults or {}, open(fp, "w"))
+    cfg = AgentConfig(node="n0", backend="fake", fixture=FIXTURE, count=count,
+                      state_dir=str(tmp_path / "state"), probe_mode="helper-sim", probe_sim_ms=2,
+                      fsync=False, faults=fp, scrub_interval_s=0)
+    return Agent(cfg)
+
+
+def claim(agent, uid="pool-1", count=1, **probe):
+    return agent.claim({"poolUID": uid, "pool": f"default/{uid}", "count": count,
+                        "resourceName": "amd.com/gpu", "policy": {},
+                        "topologyPolicy": "xgmi-packed", "probe": {"enabled": True, **probe}})
+
+
+def wait(pred, timeout=10.0):
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if pred():
+            return True
+        time.sleep(0.02)
+    return pred()
+
+
+@pytest.fixture
+def agents():
+    made = []
+    yield made
+    for a in made:
+        a.stop()
+
+
+def test_helpers_probe_and_the_agent_never_loads_the_probe_library(tmp_path, agents, native_built):
+    a = make_agent(tmp_path)
+    agents.append(a)
+    pids = a.prober.helper_pids()
+    assert len(pids) == 4 and os.getpid() not in pids
+    r = claim(a, count=2)
+    assert r["ok"] and all(d["probe"]["passed"] for d in r["devices"]), r
+    assert all(d["probe"]["backend"] == "helper-sim" for d in r["devices"])
+    # helpers' processes are the agent's own in per-pod accounting
+    assert a._pod_of_pid(next(iter(pids))) == {"namespace": "", "pod": "gpupool-agent"}
+    with open("/proc/self/maps") as f:
+        assert "libmi355x_probe" not in f.read()
+
+
+def test_probe_crash_fails_only_that_gpu_and_the_agent_survives(tmp_path, agents, native_built):
+    """(a) the agent survives a mid-probe abort, (b) a claim on another GPU concurrently succeeds,
+    (c) the aborted GPU's probe fails with ProbeCrashed and its release quarantines it."""
+    a = make_agent(tmp_path, {"devices": {"0": {"probeCrash": True}}})
+    agents.append(a)
+    out = {}
+
+    def other():  # a second pool claims concurrently; it gets a healthy GPU
+        out["r2"] = claim(a, uid="pool-2", count=1)
+    t = threading.Thread(target=other)
+    r = claim(a, count=1)  # lowest index first: GPU 0
+    t.start()
+    t.join(10)
+    d0 = r["devices"][0]
+    assert d0["index"] == 0 and not d0["probe"]["passed"]
+    assert d0["probe"]["error"].startswith("ProbeCrashed:"), d0["probe"]
+    assert "SIGABRT" in d0["probe"]["error"]
+    assert out["r2"]["ok"] and out["r2"]["devices"][0]["probe"]["passed"]
+    # the agent is fine: views, metrics, and the crashed GPU's helper is replaced by a fresh one
+    assert a.node_view()["devices"]
+    assert wait(lambda: a.prober.helpers.alive(d0["uuid"]))
+    assert a.prober.helpers.stats["helper_crashes"] == 1
+    assert a.stats["probe_crashes"] == 1
+    assert "gpupool_agent_probe_helper_crashes_total 1" in a.metrics_text()
+    # the pool replaces it: drain -> release -> quarantined with the crash as the reason
+    assert a.release("pool-1", [d0["uuid"]])["ok"]
+    v = {d["uuid"]: d for d in a.node_view()["devices"]}[d0["uuid"]]
+    assert v["state"] == "Quarantined" and "ProbeCrashed" in v["quarantine"]["reason"]
+
+
+def test_hung_probe_answers_within_its_deadline(tmp_path, agents, native_built):
+    """(e) a probe that never returns: the claim answers within timeoutSeconds + 1 s with
+    ProbeTimeout; the hung helper is killed and replaced; the next GPU probes normally."""
+    a = make_agent(tmp_path, {"devices": {"0": {"probeHang": True}}})
+    agents.append(a)
+    t0 = time.monotonic()
+    r = claim(a, count=1, timeoutSeconds=1)
+    dt = time.monotonic() - t0
+    d0 = r["devices"][0]
+    assert d0["index"] == 0 and dt < 1 + 1.0, dt
+    assert d0["probe"]["error"].startswith("ProbeTimeout:"), d0["probe"]
+    assert d0["state"] == "Claimed" and not d0["probe"]["passed"]
+    assert a.stats["probe_timeouts"] == 1
+    assert wait(lambda: a.prober.helpers.stats["helper_timeouts"] == 1)
+    assert wait(lambda: a.prober.helpers.alive(d0["uuid"]))
+    r2 = claim(a, uid="pool-2", count=1, timeoutSeconds=1)
+    assert r2["devices"][0]["index"] == 1 and r2["devices"][0]["probe"]["passed"]
+
+
+def _interrupted_state(tmp_path, marks: dict) -> tuple[str, str, str]:
+    """Claim GPUs 0-2, stop the agent, then rewrite the ledger as a process that died mid-claim
+    leaves it: the records 'Probing', probe-attempt markers as given (index -> kwargs)."""
+    a = make_agent(tmp_path)
+    r = claim(a, count=3)
+    uu = [d["uuid"] for d in sorted(r["devices"], key=lambda d: d["index"])]
+    a.stop()
+    led = Ledger(str(tmp_path / "state"), fsync=False)
+    claims = led.load()
+    for u in uu:
+        claims[u]["state"], claims[u]["probe"] = "Probing", None
+    led.commit(claims)
+    for i, kw in marks.items():
+        led.mark_probing([uu[i]], **kw)
+    return tuple(uu)
+
+
+def test_restart_after_dying_mid_probe_never_crash_loops(tmp_path, agents, native_built):
+    """(d) A restarted agent fails unprobed — ProbeInterrupted — a GPU whose probe was in flight
+    when the previous process died, if that probe ran inside the dead process (inproc) or if this
+    is the second death in a row during that GPU's probe: a GPU that takes down whatever probes
+    it cannot crash-loop the agent. One death during a helper's probe (not caused by the GPU: the
+    helper would have died, not the agent) gets one isolated re-probe; no marker at all (only the
+    state write was lost) is probed again as before."""
+    u0, u1, u2 = _interrupted_state(tmp_path, {0: {"in_agent": True}, 1: {"attempts": 2},
+                                               2: {"attempts": 1}})
+    # had GPU 0 or 1 been probed again, its helper would abort: the result would say ProbeCrashed
+    b = make_agent(tmp_path, {"devices": {"0": {"probeCrash": True}, "1": {"probeCrash": True}}})
+    agents.append(b)
+    for u in (u0, u1):
+        p = b.records[u]["probe"]
+        assert b.records[u]["state"] == "Claimed"
+        assert not p["passed"] and p["error"].startswith("ProbeInterrupted:"), p
+    assert "inside that process" in b.records[u0]["probe"]["error"]
+    assert "2 agent processes in a row" in b.records[u1]["probe"]["error"]
+    assert b.prober.helpers.stats["helper_crashes"] == 0  # neither was probed
+    p2 = b.records[u2]["probe"]
+    assert p2["passed"] and p2.get("rerunAtStart")  # one helper death: probed again, passes
+    assert not Ledger(str(tmp_path / "state")).probing_markers()  # consumed
+
+
+def test_a_death_during_the_restart_reprobe_counts_as_the_second(tmp_path, agents, native_built,
+                                                                  monkeypatch):
+    """The restart's re-probe is marked like any probe (attempts + 1): if the agent dies during
+    it, the next restart fails the GPU unprobed."""
+    u0, _, _ = _interrupted_state(tmp_path, {0: {"attempts": 1}})
+    seen = {}
+    orig = Ledger.mark_probing
+
+    def spy(self, uuids, in_agent=False, attempts=1):
+        seen.update({u: attempts for u in uuids})
+        return orig(self, uuids, in_agent, attempts)
+    monkeypatch.setattr(Ledger, "mark_probing", spy)
+    b = make_agent(tmp_path)
+    agents.append(b)
+    assert seen[u0] == 2 and b.records[u0]["probe"]["passed"]
+
+def test_probing_record_past_its_deadline_is_reported_overdue(tmp_path, agents, native_built,
+                                                              monkeypatch):
+    """Defence in depth for a claim stuck outside the probe: a GPU still 'Probing' past
+    timeoutSeconds + PROBE_GRACE_S is flagged probeOverdue in the node view, which the manager's
+    plan_pool replaces (native/src/controller/reconciler.cc)."""
+    a = make_agent(tmp_path)
+    agents.append(a)
+    monkeypatch.setattr(Agent, "PROBE_GRACE_S", 0.2)
+    gate = threading.Event()
+    orig = a.prober.probe_many
+    monkeypatch.setattr(a.prober, "probe_many", lambda devs, opts: (gate.wait(10), orig(devs, opts))[1])
+    t = threading.Thread(target=lambda: claim(a, count=1, timeoutSeconds=0.5))
+    t.start()
+    try:
+        assert wait(lambda: any(d.get("state") == "Probing" for d in a.node_view()["devices"]), 5)
+        view = lambda: [d for d in a.node_view()["devices"] if d.get("state") == "Probing"][0]  # noqa: E731
+        assert not view().get("probeOverdue")
+        assert wait(lambda: view().get("probeOverdue") is True, 3)
+        assert view()["probingMs"] >= 700
+    finally:
+        gate.set()
+        t.join(10)
+    assert not any(d.get("probeOverdue") for d in a.node_view()["devices"])

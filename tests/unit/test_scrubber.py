@@ -33,10 +33,13 @@ def fake_agent():
     hip = FakeHip()
     ledger = SimpleNamespace(sweep_state=lambda: {}, quarantined=lambda: {},
                              commit_sweep=lambda snap: None)
-    prober = SimpleNamespace(mode="inproc", ordinals={"gpu-hip-0": 0}, _hip=hip,
-                             warm_arena=lambda o: None)
+    from gpupool.agent.prober import Prober
+    prober = Prober("simulated")
+    prober.mode = "inproc"  # the real inproc code path, over the stub library
+    prober._hip, prober.ordinals = hip, {"gpu-hip-0": 0}
+    prober.warm_arena = lambda dev: None
     return SimpleNamespace(ledger=ledger, prober=prober, lock=threading.RLock(), records={},
-                           maintenance={}, by_uuid={UUID: {"hipUUID": "GPU-HIP-0"}},
+                           maintenance={}, by_uuid={UUID: {"uuid": UUID, "hipUUID": "GPU-HIP-0"}},
                            verdicts={UUID: {"healthy": True}}, _pods_by_device=lambda: {}), hip
 
 
