@@ -32,6 +32,8 @@ from .ledger import Ledger
 from .prober import DEFAULT_TIMEOUT_S, Prober, default_mode
 
 SLOT_SEP = "::"  # device-plugin ID of a time-sliced slot: "<uuid>::<slot>"
+# wake the chosen GPUs' probe helpers as soon as a claim has selected them (A/B switch)
+PREWAKE = os.environ.get("GPUPOOL_PROBE_PREWAKE", "1") != "0"
 
 
 def _ranges(bits: list[int]) -> str:
@@ -181,9 +183,8 @@ class Agent:
         self.records: dict[str, dict] = self.ledger.load()
         # A claim commits 'Probing' before its probe runs, and Probing -> Claimed reaches the disk
         # through the ledger's background writer after the reply: an agent killed in between
-        # leaves such records behind. Those whose probe-attempt marker is still there died WHILE
-        # the GPU was being probed; the rest only lost the state write. _reprobe_interrupted
-        # decides per record whether to probe again or fail it unprobed (ProbeInterrupted).
+        # leaves such records behind. _reprobe_interrupted probes them again once, or fails them
+        # unprobed (ProbeInterrupted) when their probe already outlived one agent process.
         # Either way a failed GPU takes the normal replace path (drain -> release -> quarantine
         # -> spare).
         interrupted = [u for u, r in self.records.items() if r.get("state") == "Probing"]
@@ -265,46 +266,47 @@ class Agent:
 
     def _reprobe_interrupted(self, uuids: list[str]) -> None:
         """Finish the claims a previous agent process left in 'Probing' (see __init__), before the
-        RPC server starts.
+        RPC server starts. The process died between the claim's commit and the lazy Probing ->
+        Claimed write: during the probe, or in the few ms after the reply. Each record counts its
+        probe attempts (``probeAttempts``, durable with the record before every probe):
 
-        * Its probe-attempt marker (ledger.mark_probing) is there: the previous process died while
-          this GPU's probe was in flight. If that probe ran inside the dead process (inproc) or
-          this is the second death in a row during this GPU's probe, the GPU fails at once —
-          ProbeInterrupted, no new probe — so a GPU that takes down whatever probes it cannot
-          crash-loop the agent; its pool replaces it and the release quarantines it. Otherwise
-          (the probe ran in a helper, which a GPU fault cannot take the agent down with: the
-          death was something else — a rolling update, an OOM kill) it is probed again, once.
-        * No marker: the probe finished and only the Probing -> Claimed write was lost (a kill in
-          the few ms between the claim's reply and the background ledger write). Failing those
-          outright replaced healthy GPUs and drained what their pools had started on them, so
-          they are probed again; if a pod already holds most of the GPU's HBM the probe's
-          allocation fails and the GPU is replaced, as before.
-        Re-probes are marked like any probe, so a death during one counts as the second."""
-        markers = self.ledger.probing_markers()
+        * first attempt: probed again (in the GPU's helper, with its deadline). Failing those
+          outright replaced healthy GPUs after an unrelated kill (a rolling update, an OOM kill)
+          and drained what their pools had started on them; a GPU that fails the re-probe takes
+          the normal replace path (drain -> release -> quarantine -> spare);
+        * the second death in a row during this GPU's probe: failed unprobed (ProbeInterrupted),
+          so a GPU that takes down whatever probes it can never crash-loop the agent — with the
+          probe in a helper the agent does not die of it in the first place; this bounds what is
+          left (a probe run in-process with ``--probe inproc``, a driver hang the agent's own
+          amdsmi calls run into)."""
         if not uuids:
-            self.ledger.clear_all_probing()
             return
-        failed_unprobed = []
+        failed_unprobed, again = [], []
         for u in uuids:
+            rec = self.records[u]
+            n = int(rec.get("probeAttempts") or 1)
+            if n >= 2:
+                rec["state"] = "Claimed"
+                rec["probe"] = {"passed": False, "backend": self.probe_mode, "ms": 0.0,
+                                "crashed": True,
+                                "error": f"ProbeInterrupted: {n} agent processes in a row died "
+                                         f"while this GPU's claim-time probe was in flight; "
+                                         f"failed without probing it again"}
+                failed_unprobed.append(u)
+            else:
+                rec["probeAttempts"] = n + 1
+                again.append(u)
+        if again:  # the attempt is on disk before the probe runs
+            self.ledger.commit(self.records)
+        for u in again:
             rec = self.records[u]
             d = self.by_uuid.get(u)
             opts = (rec.get("policy") or {}).get("probe") or {}
-            m = markers.get(Ledger.safe_name(u))
-            if m is not None and (m.get("inAgent") or int(m.get("attempts") or 1) >= 2):
-                why = "its probe ran inside that process" if m.get("inAgent") else \
-                    f"{int(m.get('attempts') or 1)} agent processes in a row died during it"
-                res = {"passed": False, "backend": self.probe_mode, "ms": 0.0, "crashed": True,
-                       "error": f"ProbeInterrupted: the agent process died while this GPU's "
-                                f"claim-time probe was in flight ({why}); failed without probing "
-                                f"it again"}
-                failed_unprobed.append(u)
-            elif d is None:
+            if d is None:
                 res = {"passed": False, "backend": "none", "ms": 0.0,
                        "error": "ProbeInterrupted: the agent restarted during the claim-time "
                                 "probe and the GPU is no longer visible"}
             else:
-                self.ledger.mark_probing([u], in_agent=self.probe_mode == "inproc",
-                                         attempts=(int(m.get("attempts") or 1) + 1) if m else 1)
                 res = self.prober.probe_many([d], {**opts, "enabled": opts.get("enabled", True)})[0]
                 res["rerunAtStart"] = True
                 if not res.get("passed"):
@@ -312,6 +314,8 @@ class Agent:
                         str(res.get("error") or "probe failed")
             rec["state"] = "Claimed"
             rec["probe"] = res
+        for u in uuids:
+            res = self.records[u]["probe"]
             self.last_probe[u] = res
             self._probe_mono[u] = time.monotonic()
             self.stats["probes"] += 1
@@ -319,7 +323,6 @@ class Agent:
             if not res.get("passed"):
                 self.stats["probe_failures"] += 1
         self.ledger.commit(self.records)
-        self.ledger.clear_all_probing()
         log.warning("finished %d claim(s) a restart interrupted (%d failed unprobed): %s",
                     len(uuids), len(failed_unprobed),
                     {u: bool(self.records[u]["probe"].get("passed")) for u in uuids})
@@ -1200,6 +1203,8 @@ class Agent:
                                    f"{len(free)} available (all-or-nothing)", "devices": []}
             by_index = {d["index"]: d for d in self.snap["devices"]}
             chosen = [by_index[i] for i in sel]
+            if probe_opts.get("enabled", True) and PREWAKE:
+                self.prober.prewake(chosen)
             lap("select")
             ts = now_rfc3339()
             # a record still 'Probing' past its probe deadline (+ PROBE_GRACE_S) is reported
@@ -1212,7 +1217,7 @@ class Agent:
                        "resourceName": resource, "policy": policy,
                        "baseline": {"ecc": dict(d.get("ecc") or {}),
                                     "eccUmc": dict(d.get("eccUmc") or {})}, "claimedAt": ts,
-                       "state": "Probing", "probe": None}
+                       "state": "Probing", "probe": None, "probeAttempts": 1}
                 self.records[d["uuid"]] = rec
             # The claim becomes durable while the probe runs (the ledger's writer fsyncs it
             # concurrently); the RPC answers only after it is on disk, so no crash can ever make
@@ -1224,20 +1229,10 @@ class Agent:
         for d in chosen:  # an in-flight HBM scrub window finishes and hands its buffer back
             self.scrubber.yield_device(d["uuid"])
         lap("scrubYield")
-        # probes run outside the lock, concurrently across GPUs, each in its GPU's probe helper;
-        # the probe-attempt markers tell a restarted agent which GPUs were mid-probe if this
-        # process dies now (_reprobe_interrupted)
-        uuids = [d["uuid"] for d in chosen]
-        probing = probe_opts.get("enabled", True) and self.probe_mode != "off"
+        # probes run outside the lock, concurrently across GPUs, each in its GPU's probe helper
         t0 = time.perf_counter()
-        if probing:
-            self.ledger.mark_probing(uuids, in_agent=self.probe_mode == "inproc")
-        try:
-            results = self.prober.probe_many(chosen, {**probe_opts, "enabled":
-                                                      probe_opts.get("enabled", True)})
-        finally:
-            if probing:
-                self.ledger.clear_probing(uuids)
+        results = self.prober.probe_many(chosen, {**probe_opts, "enabled":
+                                                  probe_opts.get("enabled", True)})
         probe_wall = (time.perf_counter() - t0) * 1e3
         lap("probe")
         if probe_opts.get("xgmiPeerCheck"):

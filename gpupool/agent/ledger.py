@@ -218,64 +218,6 @@ class Ledger:
         with self._mu:
             return {u: dict(r) for u, r in self._sweep.items()}
 
-    # ---------------------------------------------------------------- probe-attempt markers
-    # ``<state>/probing/<uuid>``: created right before a GPU's probe starts, removed once its result
-    # is in. A restarted agent that finds a 'Probing' record WITH its marker knows the previous
-    # process died while that GPU was being probed. Whether it may probe the GPU again depends on
-    # what the marker says (Agent._reprobe_interrupted): not if the probe ran inside the dead
-    # process (``inAgent``: the probe may be what killed it) or if this is already the second
-    # death in a row during this GPU's probe (``attempts`` >= 2) — so a GPU that takes down
-    # whatever probes it can never crash-loop the agent, while one unrelated kill (a rolling
-    # update, an OOM kill) landing on a claim does not throw a healthy GPU out. The marker is a
-    # plain create (no fsync, ~20 us): an agent process that dies leaves it in the page cache;
-    # only a host crash can lose it.
-    def _probing_dir(self) -> str:
-        return os.path.join(self.dir, "probing")
-
-    def mark_probing(self, uuids: list[str], in_agent: bool = False, attempts: int = 1) -> None:
-        d = self._probing_dir()
-        os.makedirs(d, exist_ok=True)
-        stamp = json.dumps({"pid": os.getpid(), "at": time.time(), "inAgent": bool(in_agent),
-                            "attempts": int(attempts)})
-        for u in uuids:
-            with open(os.path.join(d, _safe(u)), "w") as f:
-                f.write(stamp)
-
-    def clear_probing(self, uuids: list[str]) -> None:
-        d = self._probing_dir()
-        for u in uuids:
-            try:
-                os.remove(os.path.join(d, _safe(u)))
-            except FileNotFoundError:
-                pass
-
-    def probing_markers(self) -> dict[str, dict]:
-        """``_safe(uuid)`` -> marker ({pid, at, inAgent, attempts}) of every GPU whose probe was in
-        flight when a process died."""
-        out: dict[str, dict] = {}
-        try:
-            names = os.listdir(self._probing_dir())
-        except FileNotFoundError:
-            return out
-        for name in names:
-            try:
-                with open(os.path.join(self._probing_dir(), name)) as f:
-                    out[name] = json.loads(f.read() or "{}")
-            except (OSError, ValueError):
-                out[name] = {}
-        return out
-
-    def clear_all_probing(self) -> None:
-        for name in self.probing_markers():
-            try:
-                os.remove(os.path.join(self._probing_dir(), name))
-            except FileNotFoundError:
-                pass
-
-    @staticmethod
-    def safe_name(uuid: str) -> str:
-        return _safe(uuid)
-
     # ---------------------------------------------------------------- quarantine
     def quarantine(self, uuid: str, seconds: float, reason: str, maintenance: bool = False,
                    write: bool = True) -> dict:

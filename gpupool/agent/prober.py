@@ -113,6 +113,18 @@ class Prober:
                 pass
         return total
 
+    def prewake(self, devs: list[dict]) -> None:
+        """The claim has chosen these GPUs and probes them in ~0.1-0.2 ms (ledger commit first):
+        tell their helpers now, so each is running — not asleep in a blocking read — when its
+        probe request arrives (probehost.SPIN_S)."""
+        if self.helpers is None:
+            return
+        for d in devs:
+            try:
+                self.helpers.get(d["uuid"], d).notify("wake")
+            except Exception:  # a helper being replaced: the probe reports it
+                pass
+
     def helper_pids(self) -> set[int]:
         return self.helpers.pids() if self.helpers is not None else set()
 

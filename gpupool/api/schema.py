@@ -150,7 +150,9 @@ DEVICE_STATUS = {
         "node": _S,
         "renderNode": _S,
         "kfdNode": _I32,
-        "health": {"type": "string", "enum": ["Healthy", "Unhealthy", "Draining", "Probing"]},
+        # Unknown: the node's agent does not answer; the entry is its last observation
+        "health": {"type": "string", "enum": ["Healthy", "Unhealthy", "Draining", "Probing",
+                                              "Unknown"]},
         "reasons": {"type": "array", "items": _S},
         "advertised": _B,
         "pods": {"type": "array", "items": _S},

@@ -193,6 +193,8 @@ class RocmProvider : public DeviceProvider {
   // of, younger than ``view_max_age`` (telemetry keeps moving without generation bumps) and no
   // mutating RPC to that node started since it was fetched; otherwise it is an RPC as before.
   void note_gen(const std::string& node, int64_t gen);
+  // The node's event feed broke (agent gone): drop its cached view, so the next observe asks.
+  void forget_view(const std::string& node) { invalidate_(node); }
   // Skipped while a mutating RPC to the node is in flight (optionally after waiting up to
   // ``max_wait_ms`` for it): a claim bumps the agent's generation several times and its reply
   // invalidates the cache anyway, and the caller — the node's event-stream thread — must never

@@ -70,6 +70,7 @@ class PoolReconcilerBase {
   // Adds/removes the finalizer with RV precondition; returns the updated object.
   Json edit_finalizers_(const Json& obj, bool add);
   Json ensure_finalizer_(const Json& obj);
+  Json fresh_(const Json& obj);
   Json remove_finalizer_(const Json& obj);
   void event_(const Json& obj, const std::string& type, const std::string& reason, const std::string& msg);
   void note_generation_(const ObjectMeta& m);  // starts the reconcile-to-Ready clock
@@ -128,6 +129,7 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
     int64_t free_healthy = 0;
     std::map<std::string, int64_t> free_by_node;   // free healthy GPUs per observed node
     std::vector<std::string> unknown;              // unreachable nodes status did not name
+    std::vector<std::string> unreachable;          // nodes status names whose agent did not answer
   };
   Observed observe_(const ObjectMeta& m, const Mi355xPoolSpec& spec, const Json& status);
   // Nodes (reachable, selector-matching) with >= need free healthy GPUs, tightest fit first.

@@ -207,6 +207,18 @@ Json PoolReconcilerBase::ensure_finalizer_(const Json& obj) {
 
 Json PoolReconcilerBase::remove_finalizer_(const Json& obj) { return edit_finalizers_(obj, false); }
 
+// The stored object, read through the API server: a status written from what the pass could NOT
+// observe (an unreachable agent) is built on the newest status — the informer copy may predate this
+// reconciler's own last write and would carry no devices to keep. Falls back to ``obj``.
+Json PoolReconcilerBase::fresh_(const Json& obj) {
+  try {
+    Json cur = client_.get(res_, obj.path("metadata.namespace").as_string(), obj.path("metadata.name").as_string());
+    if (cur.path("metadata.uid") == obj.path("metadata.uid")) return cur;
+  } catch (const std::exception&) {
+  }
+  return obj;
+}
+
 void PoolReconcilerBase::event_(const Json& obj, const std::string& type, const std::string& reason,
                                 const std::string& msg) {
   if (events_ && opts_.emit_events) events_->record(obj, type, reason, msg);
@@ -428,6 +440,7 @@ Mi355xPoolReconciler::Observed Mi355xPoolReconciler::observe_(const ObjectMeta& 
   for (const auto& n : unreachable_hinted)
     if (std::find(o.nodes.begin(), o.nodes.end(), n) == o.nodes.end()) o.nodes.push_back(n);
   std::sort(o.nodes.begin(), o.nodes.end());
+  o.unreachable = unreachable_hinted;
   return o;
 }
 
@@ -652,7 +665,31 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
     if (!d.healthy || !d.probe_passed) unhealthy.push_back(short_id(d));
     if (d.state == "Claimed" && d.healthy && d.probe_passed && d.advertised) ++ready;
   }
-  st["replicas"] = claimed;
+  // An agent that does not answer (restarting, node network down) says nothing about its GPUs:
+  // they are still held, with whatever pods run on them. Its devices stay in status as last
+  // observed (health "Unknown") and count in replicas — never erased by a transient failure
+  // (the reference returns without touching status on a list error, README.md:189-193). They do
+  // not count as ready: with the agent its device plugin is gone too, so no new pod can be given
+  // them until it answers and they are verified again (Ready=Unknown, reason AgentUnreachable).
+  int64_t retained = 0;
+  if (!o.reachable) {
+    std::set<std::string> gone(o.unreachable.begin(), o.unreachable.end());
+    if (!o.node.empty()) {
+      bool seen = false;
+      for (const auto& d : o.mine) seen = seen || (d.node.empty() ? o.node : d.node) == o.node;
+      if (!seen) gone.insert(o.node);
+    }
+    for (const auto& d : obj.path("status.devices").elements()) {
+      if (!gone.count(d["node"].str_or(obj.path("status.nodeName").as_string()))) continue;
+      Json kept = d;
+      if (kept["health"].as_string() != "Draining") {
+        kept["health"] = "Unknown";
+        ++retained;
+      }
+      devices.push_back(kept);
+    }
+  }
+  st["replicas"] = claimed + retained;
   st["readyReplicas"] = ready;
   st["allocatable"] = ready * static_cast<int64_t>(spec.sharing_replicas);  // slots of resourceName
   if (!o.node.empty()) st["nodeName"] = o.node;
@@ -676,7 +713,9 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
     std::snprintf(buf, sizeof buf, "; peer-copy ring min %.0f GB/s", min_xgmi);
     xgmi_ok_msg += buf;
   }
-  if (xgmi_bad.empty() && !xgmi_unknown.empty()) {
+  if (!o.reachable && retained > 0) {
+    // the health of the unanswered node's GPUs is unknown: their conditions keep the last verdict
+  } else if (xgmi_bad.empty() && !xgmi_unknown.empty()) {
     // the peer-copy check could not run (no peer access / HIP error): the links are unverified,
     // not faulty — Unknown, and no GPU is replaced for it
     set_condition(conds, gen::kCondXGMILinksHealthy, "Unknown", "XGMIPeerCheckUnavailable", join(xgmi_unknown, " | "),
@@ -684,10 +723,14 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
   } else {
     health_cond(gen::kCondXGMILinksHealthy, xgmi_bad, "XGMILinkDown", "AllLinksUp", xgmi_ok_msg.c_str());
   }
-  health_cond(gen::kCondHBMECCHealthy, ecc_bad, "HBMECCErrors", "NoNewECCErrors", "no new HBM ECC errors since claim");
-  health_cond(gen::kCondThermalHealthy, thermal_bad, "ThermalLimit", "WithinThermalLimits",
-              "temperatures below device limits");
-  if (probing) {
+  if (o.reachable || retained == 0) {
+    health_cond(gen::kCondHBMECCHealthy, ecc_bad, "HBMECCErrors", "NoNewECCErrors", "no new HBM ECC errors since claim");
+    health_cond(gen::kCondThermalHealthy, thermal_bad, "ThermalLimit", "WithinThermalLimits",
+                "temperatures below device limits");
+  }
+  if (!o.reachable && retained > 0) {
+    // DeviceProbePassed keeps its last verdict too
+  } else if (probing) {
     set_condition(conds, gen::kCondDeviceProbePassed, "Unknown", "Probing", std::to_string(probing) + " GPU(s) probing", gen, now);
   } else if (!probe_bad.empty()) {
     // the isolation outcomes name themselves (ProbeCrashed / ProbeTimeout / ProbeInterrupted /
@@ -736,7 +779,7 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
                        : !progress_reason.empty() ? progress_reason
                        : !unhealthy.empty() ? "DeviceUnhealthy"
                        : "NotReady";
-  set_condition(conds, gen::kCondReady, is_ready ? "True" : "False", reason,
+  set_condition(conds, gen::kCondReady, is_ready ? "True" : (!o.reachable && !deleting) ? "Unknown" : "False", reason,
                 std::to_string(ready) + "/" + std::to_string(spec.replicas) + " GPUs ready" +
                     (o.nodes.size() > 1 ? " on " + std::to_string(o.nodes.size()) + " nodes"
                      : o.node.empty() ? "" : " on " + o.node),
@@ -748,7 +791,8 @@ Json Mi355xPoolReconciler::build_status_(const Json& obj, const ObjectMeta& m, c
 Outcome Mi355xPoolReconciler::finalize_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec) {
   Observed o = observe_(m, spec, obj["status"]);
   if (!o.reachable && !o.node.empty()) {
-    write_status_(obj, build_status_(obj, m, spec, o, "Deleting", "agent unreachable", "", true));
+    const Json cur = fresh_(obj);
+    write_status_(cur, build_status_(cur, m, spec, o, "Deleting", "agent unreachable", "", true));
     return Outcome::transient("agent unreachable during finalization: " + o.error);
   }
   // Status names no node (never placed, or a claim whose status write never landed) and some agent
@@ -868,7 +912,8 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
 
   Observed o = observe_(m, spec, obj["status"]);
   if (!o.reachable && !o.node.empty()) {
-    write_status_(obj, build_status_(obj, m, spec, o, "", "", "", false));
+    const Json cur = fresh_(obj);  // the devices it keeps come from the newest status, not a lagging copy
+    write_status_(cur, build_status_(cur, m, spec, o, "", "", "", false));
     ready_gauge().set({{"kind", kind_}, {"pool", m.key()}}, 0);
     return Outcome::transient("agent on " + o.node + " unreachable: " + o.error);
   }
@@ -1318,9 +1363,18 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
   Json conds = obj.path("status.conditions").is_array() ? obj.path("status.conditions") : Json::array();
   Json st = Json::object();
   st["observedGeneration"] = m.generation;
+  // What the last successful list observed. A pass that cannot observe (invalid spec, missing or
+  // refused credentials, an ARM 429/5xx) keeps it: the VMs still exist whether or not this pass
+  // could list them (the reference returns without touching status on a list error,
+  // README.md:189-193; replacing the whole status with only the error wiped readyReplicas and vms).
+  auto keep_observed = [&]() {
+    for (const char* k : {"readyReplicas", "replicas", "vms"})
+      if (!obj.path("status")[k].is_null()) st[k] = obj.path("status")[k];
+  };
   auto errs = validate_azure(obj);
   if (!errs.empty()) {
     set_condition(conds, gen::kCondReady, "False", "InvalidSpec", join(errs, "; "), m.generation, now);
+    keep_observed();
     st["conditions"] = conds;
     write_status_(obj, st);
     return Outcome::terminal("invalid spec");
@@ -1349,7 +1403,7 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
                   m.generation, now);
     st["readyReplicas"] = obj.path("status.readyReplicas").as_int(0);
     st["replicas"] = obj.path("status.replicas").as_int(0);
-    if (obj.path("status.vms").is_array()) st["vms"] = obj.path("status.vms");
+    keep_observed();
     st["conditions"] = conds;
     write_status_(obj, st);
     event_(obj, "Warning", "CredentialsMissing", why);
@@ -1373,6 +1427,7 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
       set_condition(conds, gen::kCondReady, "False", e.code, e.what(), m.generation, now);
     }
     set_condition(conds, gen::kCondDegraded, "True", e.code, e.what(), m.generation, now);
+    keep_observed();
     st["conditions"] = conds;
     write_status_(obj, st);
     if (refused) {
@@ -1394,6 +1449,7 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
         for (const auto& o : orphans) cloud_.destroy(creds, spec.resource_group, o);
     } catch (const ProviderError& e) {
       set_condition(conds, gen::kCondDegraded, "True", e.code, e.what(), m.generation, now);
+      keep_observed();
       st["conditions"] = conds;
       write_status_(obj, st);
       return Outcome::transient(e.what());
@@ -1473,7 +1529,15 @@ Outcome AzureVmPoolReconciler::reconcile(const std::string& ns, const std::strin
     event_(obj, "Warning", e.code, e.what());
   }
   // Re-observe after acting (fixes README.md:225 which reported the pre-action count).
-  vms = cloud_.list(creds, spec.resource_group, owner);
+  try {
+    vms = cloud_.list(creds, spec.resource_group, owner);
+  } catch (const ProviderError& e) {  // acted, but cannot see the result: keep the last observation
+    set_condition(conds, gen::kCondDegraded, "True", e.code, e.what(), m.generation, now);
+    keep_observed();
+    st["conditions"] = conds;
+    write_status_(obj, st);
+    return Outcome::transient(e.what());
+  }
   int64_t ready = 0, total = 0;
   bool inflight = false;
   Json names = Json::array();

@@ -295,6 +295,7 @@ class AgentWatchers {
     Logger log = Logger("agent-watch").with("node", node);
     int64_t since = -1;
     int backoff = 100;
+    bool connected = false;  // the feed answered since the last failure
     while (!w->stop && !g_stop) {
       try {
         // the agent holds the answer up to timeoutSeconds: allow that plus slack before timing out
@@ -305,6 +306,7 @@ class AgentWatchers {
             [&](std::string_view line) {
               auto j = Json::try_parse(line);
               if (!j) return true;
+              connected = true;
               int64_t gen = (*j)["gen"].as_int(since);
               prov_.note_gen(node, gen);
               const bool changed = gen != since;
@@ -321,6 +323,14 @@ class AgentWatchers {
         backoff = 100;
       } catch (const std::exception& e) {
         log.debug("agent long-poll failed", Json::object().set("error", e.what()));
+        if (connected) {
+          // the agent went away: its cached view no longer stands for anything, and the pools on
+          // the node must observe that now (Ready=Unknown, AgentUnreachable) — not after the
+          // view cache's age or the next resync
+          connected = false;
+          prov_.forget_view(node);
+          enqueue_pools(node, Json::array(), true);
+        }
         // back off while the agent is away (a refused connect is cheap: at most one a second per
         // node), and reconnect at once when a reconcile's RPC reaches it again: a restarted
         // agent's events (re-advertised GPUs, faults) must not wait out a grown backoff

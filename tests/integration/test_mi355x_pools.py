@@ -298,13 +298,33 @@ def test_agent_down_right_after_ready_claims_nowhere_else(cluster_factory):
     uid = o["metadata"]["uid"]
     home = wait_ready(k, "p", 2)["status"]["nodeName"]
     other = "sn-b" if home == "sn-a" else "sn-a"
+    before = k.get(MI355XPOOLS, "p", "default")["status"]
     c._kill(f"agent-{home}")
     for i in range(5):
         k.patch(MI355XPOOLS, "p", {"metadata": {"labels": {"poke": str(i)}}}, "default")
         time.sleep(0.05)
-    time.sleep(1.5)
+    # throughout the outage the pool keeps what it last observed: its GPUs
+    # (still held, pods and all), replicas and node; Ready is Unknown, readyReplicas 0 (the node's
+    # device plugin is down with the agent: nothing new can be scheduled on them until it answers)
+    saw_unknown = False
+    deadline = time.monotonic() + 1.5
+    while time.monotonic() < deadline:
+        st = k.get(MI355XPOOLS, "p", "default")["status"]
+        assert st.get("replicas") == 2, st
+        assert [d["uuid"] for d in st["devices"]] == [d["uuid"] for d in before["devices"]], st
+        assert st.get("nodeName") == home
+        ready = conds({"status": st})["Ready"]
+        if ready["status"] == "Unknown":
+            saw_unknown = True
+            assert ready["reason"] == "AgentUnreachable" and st["readyReplicas"] == 0, st
+            assert {d["health"] for d in st["devices"]} == {"Unknown"}, st["devices"]
+        time.sleep(0.01)
+    assert saw_unknown
     assert not [d for d in agent_view(c, other)["devices"] if d.get("poolUID") == uid]
     assert k.get(MI355XPOOLS, "p", "default")["status"].get("nodeName") == home
+    c.start_agent(next(n for n in c.nodes if n.name == home))  # back: verified and Ready again
+    o = wait_ready(k, "p", 2)
+    assert [d["uuid"] for d in o["status"]["devices"]] == [d["uuid"] for d in before["devices"]]
 
 
 def test_lost_claim_reply_neither_leaks_nor_double_claims(cluster_factory):

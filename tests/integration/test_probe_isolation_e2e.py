@@ -81,10 +81,9 @@ def test_hung_probe_answers_at_its_deadline_and_the_pool_converges_on_a_spare(cl
 
 def test_agent_killed_mid_probe_comes_back_and_converges(cluster_factory):
     """The agent dies (SIGKILL, with its helpers) while GPU 0's probe hangs. The restarted agent
-    finds GPU 0 'Probing' with its probe-attempt marker: the probe ran in a helper, so the death
-    was not the GPU's doing and it is probed once more — in a helper, with its deadline — fails
-    (ProbeTimeout), and the pool converges on a spare. (A second death during that re-probe would
-    fail it unprobed: tests/unit/test_probe_isolation.py.)"""
+    finds GPU 0 'Probing' at its first attempt: probed once more — in its helper, with its
+    deadline — it fails (ProbeTimeout), and the pool converges on a spare. (A second death during
+    that re-probe would fail it unprobed: tests/unit/test_probe_isolation.py.)"""
     node = helper_node()
     c = cluster_factory(nodes=[node])
     k = c.client

@@ -117,32 +117,32 @@ def test_hung_probe_answers_within_its_deadline(tmp_path, agents, native_built):
     assert r2["devices"][0]["index"] == 1 and r2["devices"][0]["probe"]["passed"]
 
 
-def _interrupted_state(tmp_path, marks: dict) -> tuple[str, str, str]:
+def _interrupted_state(tmp_path, attempts: dict) -> tuple[str, str, str]:
     """Claim GPUs 0-2, stop the agent, then rewrite the ledger as a process that died mid-claim
-    leaves it: the records 'Probing', probe-attempt markers as given (index -> kwargs)."""
+    leaves it: the records 'Probing', with the given probeAttempts (index -> n; absent: a record
+    of an older agent, which counts as 1)."""
     a = make_agent(tmp_path)
     r = claim(a, count=3)
     uu = [d["uuid"] for d in sorted(r["devices"], key=lambda d: d["index"])]
     a.stop()
     led = Ledger(str(tmp_path / "state"), fsync=False)
     claims = led.load()
-    for u in uu:
+    for i, u in enumerate(uu):
         claims[u]["state"], claims[u]["probe"] = "Probing", None
+        claims[u].pop("probeAttempts", None)
+        if i in attempts:
+            claims[u]["probeAttempts"] = attempts[i]
     led.commit(claims)
-    for i, kw in marks.items():
-        led.mark_probing([uu[i]], **kw)
     return tuple(uu)
 
 
 def test_restart_after_dying_mid_probe_never_crash_loops(tmp_path, agents, native_built):
-    """(d) A restarted agent fails unprobed — ProbeInterrupted — a GPU whose probe was in flight
-    when the previous process died, if that probe ran inside the dead process (inproc) or if this
-    is the second death in a row during that GPU's probe: a GPU that takes down whatever probes
-    it cannot crash-loop the agent. One death during a helper's probe (not caused by the GPU: the
-    helper would have died, not the agent) gets one isolated re-probe; no marker at all (only the
-    state write was lost) is probed again as before."""
-    u0, u1, u2 = _interrupted_state(tmp_path, {0: {"in_agent": True}, 1: {"attempts": 2},
-                                               2: {"attempts": 1}})
+    """(d) A restarted agent fails unprobed — ProbeInterrupted — a GPU whose probe already
+    outlived one agent process (probeAttempts >= 2): a GPU that takes down whatever probes it
+    cannot crash-loop the agent. A first interruption (the death was something else: the probe
+    runs in a helper, which a GPU fault cannot take the agent down with) gets one re-probe, in the
+    GPU's helper."""
+    u0, u1, u2 = _interrupted_state(tmp_path, {0: 2, 1: 3, 2: 1})
     # had GPU 0 or 1 been probed again, its helper would abort: the result would say ProbeCrashed
     b = make_agent(tmp_path, {"devices": {"0": {"probeCrash": True}, "1": {"probeCrash": True}}})
     agents.append(b)
@@ -150,29 +150,32 @@ def test_restart_after_dying_mid_probe_never_crash_loops(tmp_path, agents, nativ
         p = b.records[u]["probe"]
         assert b.records[u]["state"] == "Claimed"
         assert not p["passed"] and p["error"].startswith("ProbeInterrupted:"), p
-    assert "inside that process" in b.records[u0]["probe"]["error"]
-    assert "2 agent processes in a row" in b.records[u1]["probe"]["error"]
+        assert "in a row" in p["error"]
     assert b.prober.helpers.stats["helper_crashes"] == 0  # neither was probed
     p2 = b.records[u2]["probe"]
-    assert p2["passed"] and p2.get("rerunAtStart")  # one helper death: probed again, passes
-    assert not Ledger(str(tmp_path / "state")).probing_markers()  # consumed
+    assert p2["passed"] and p2.get("rerunAtStart")  # first interruption: probed again, passes
+    assert b.records[u2]["probeAttempts"] == 2
 
 
-def test_a_death_during_the_restart_reprobe_counts_as_the_second(tmp_path, agents, native_built,
-                                                                  monkeypatch):
-    """The restart's re-probe is marked like any probe (attempts + 1): if the agent dies during
-    it, the next restart fails the GPU unprobed."""
-    u0, _, _ = _interrupted_state(tmp_path, {0: {"attempts": 1}})
+def test_the_reprobe_attempt_is_durable_before_the_reprobe_runs(tmp_path, agents, native_built,
+                                                                 monkeypatch):
+    """The restart's re-probe is counted on disk first: if the agent dies during it, the next
+    restart finds probeAttempts 2 and fails the GPU unprobed. A record of an older agent (no
+    counter) counts as a first attempt."""
+    u0, _, _ = _interrupted_state(tmp_path, {})
     seen = {}
-    orig = Ledger.mark_probing
+    from gpupool.agent.prober import Prober
+    orig = Prober.probe_many
 
-    def spy(self, uuids, in_agent=False, attempts=1):
-        seen.update({u: attempts for u in uuids})
-        return orig(self, uuids, in_agent, attempts)
-    monkeypatch.setattr(Ledger, "mark_probing", spy)
+    def spy(self, devs, opts):
+        on_disk = Ledger(str(tmp_path / "state"), fsync=False).load()
+        seen.update({d["uuid"]: on_disk[d["uuid"]].get("probeAttempts") for d in devs})
+        return orig(self, devs, opts)
+    monkeypatch.setattr(Prober, "probe_many", spy)
     b = make_agent(tmp_path)
     agents.append(b)
     assert seen[u0] == 2 and b.records[u0]["probe"]["passed"]
+
 
 def test_probing_record_past_its_deadline_is_reported_overdue(tmp_path, agents, native_built,
                                                               monkeypatch):
