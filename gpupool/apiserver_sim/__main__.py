@@ -24,6 +24,9 @@ def main() -> None:
     ap.add_argument("--watch-delay", type=float, default=0.0,
                     help="deliver every watch event this many seconds late (stale informers)")
     ap.add_argument("--profile", default=None, help="write cProfile stats here on exit")
+    ap.add_argument("--fail-list", action="append", default=[],
+                    help="fault injection: LIST/WATCH of this resource plural answer 503 until "
+                         "cleared through POST /debug/faults (repeatable)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     prof = None
@@ -43,6 +46,7 @@ def main() -> None:
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     sim = ApiServerSim(token=a.token, bookmark_interval=a.bookmark_interval, window=a.window,
                        watch_delay=a.watch_delay)
+    sim.fail_list = {r: -1 for r in a.fail_list}
     try:
         asyncio.run(serve(a.host, a.port, sim, a.port_file, a.crd_dir, a.unix,
                           tls_cert=a.tls_cert, tls_key=a.tls_key, client_ca=a.client_ca))

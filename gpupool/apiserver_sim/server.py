@@ -148,6 +148,9 @@ class ApiServerSim:
         self.watchers: dict[tuple[str, str], set[asyncio.Queue]] = {}
         self.store.listeners.append(self._fanout)
         self.requests_total: dict[tuple[str, int], int] = {}
+        # fault injection (tests): resource plural -> LIST/WATCH requests still to fail with 503
+        # (-1: until cleared); set at start (--fail-list) or through POST /debug/faults
+        self.fail_list: dict[str, int] = {}
         self.started = time.time()
         self.app = web.Application(middlewares=[self._mw], client_max_size=64 << 20)
         r = self.app.router
@@ -156,6 +159,7 @@ class ApiServerSim:
         r.add_get("/livez", self._ok)
         r.add_get("/version", self._version)
         r.add_get("/metrics", self._metrics)
+        r.add_post("/debug/faults", self._set_faults)
         r.add_get("/api", self._api_versions)
         r.add_get("/apis", self._api_groups)
         r.add_get("/api/{version}", self._resource_list_core)
@@ -204,6 +208,21 @@ class ApiServerSim:
         lines.append("# TYPE etcd_resource_version gauge")
         lines.append(f"etcd_resource_version {self.store.rv}")
         return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
+
+    async def _set_faults(self, request):
+        """{"failList": {"resourcequotas": -1}}: LIST and WATCH of those resources answer 503
+        (the count: how many more; -1 until cleared). {} clears."""
+        body = await request.json()
+        self.fail_list = {str(k): int(v) for k, v in (body.get("failList") or {}).items()}
+        return web.json_response({"failList": self.fail_list})
+
+    def _inject_list_fault(self, rt) -> None:
+        n = self.fail_list.get(rt.plural)
+        if n is None or n == 0:
+            return
+        if n > 0:
+            self.fail_list[rt.plural] = n - 1
+        raise ApiError(503, "ServiceUnavailable", f"injected: {rt.plural} cannot be listed")
 
     def _fanout(self, ev: WatchEvent) -> None:
         qs = self.watchers.get(ev.rtype)
@@ -289,6 +308,7 @@ class ApiServerSim:
         m = request.method
         if name is None:
             if m == "GET":
+                self._inject_list_fault(rt)
                 if q.get("watch") in ("1", "true"):
                     return await self._watch(request, rt, ns)
                 lst = self.store.list(rt, ns, q.get("labelSelector"), q.get("fieldSelector"),

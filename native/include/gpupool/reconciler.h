@@ -45,6 +45,9 @@ struct ReconcilerOptions {
   std::chrono::milliseconds progress_poll{250};   // while scaling/draining
   std::chrono::milliseconds credentials_retry{30000};  // README.md:184's 30 s, now effective
   bool emit_events = true;
+  // ResourceQuotas unreadable (no synced informer, LIST failing): admit scale-ups anyway (clusters
+  // that use no quotas) instead of blocking them with QuotaUnknown until the quotas can be read
+  bool quota_fail_open = false;
 };
 
 // Shared base: status writes with conflict retry, finalizer management, metrics.
@@ -143,7 +146,9 @@ class Mi355xPoolReconciler : public PoolReconcilerBase {
   // reserves its delta before the claim RPC, so concurrent passes of different pools cannot both
   // fit the same headroom. quota_settle_ (after the pass's status write) turns the reservation
   // into the written count.
-  bool quota_reserve_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta, std::string* why);
+  // false: blocked, ``*reason`` QuotaExceeded (the quota is full) or QuotaUnknown (unreadable)
+  bool quota_reserve_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta, std::string* why,
+                      std::string* reason);
   void quota_settle_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int64_t replicas);
   Outcome finalize_(const Json& obj, const ObjectMeta& m, const Mi355xPoolSpec& spec);
   // Evicts pods on draining devices and releases drained ones. Returns #devices still draining.

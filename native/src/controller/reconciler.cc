@@ -964,13 +964,13 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
     for (const auto& kv : by_node(o, cordon)) provider_.cordon(kv.first, m.uid, kv.second);
     acted = true;
   }
-  std::string quota_msg;
+  std::string quota_msg, quota_reason;
   bool over_quota = n_active < spec.replicas &&
-                    !quota_reserve_(m, spec, static_cast<int>(spec.replicas - n_active), &quota_msg);
+                    !quota_reserve_(m, spec, static_cast<int>(spec.replicas - n_active), &quota_msg, &quota_reason);
   if (over_quota) {
-    blocked = "QuotaExceeded";
+    blocked = quota_reason;
     progress_msg = quota_msg;
-    event_(obj, "Warning", "QuotaExceeded", quota_msg);
+    event_(obj, "Warning", quota_reason, quota_msg);
   } else if (n_active < spec.replicas && spans_(spec)) {
     // spec.maxNodes > 1: the delta may be split over nodes; all-or-nothing per pass (a claim that
     // fails part-way hands back what this pass already claimed on the other nodes).
@@ -1166,7 +1166,7 @@ Outcome Mi355xPoolReconciler::reconcile(const std::string& ns, const std::string
 // passes whose claim is still in flight; a pass that fits reserves its delta before the claim RPC.
 // The lock is never held across an RPC (only across the quota LIST when no informer is synced).
 bool Mi355xPoolReconciler::quota_reserve_(const ObjectMeta& m, const Mi355xPoolSpec& spec, int delta,
-                                          std::string* why) {
+                                          std::string* why, std::string* reason) {
   trace::Span span("quota");
   std::lock_guard<std::mutex> g(quota_mu_);
   std::vector<Json> items;
@@ -1177,8 +1177,15 @@ bool Mi355xPoolReconciler::quota_reserve_(const ObjectMeta& m, const Mi355xPoolS
     try {
       Json quotas = client_.list(res::resourcequotas(), m.ns);
       items = quotas["items"].elements();
-    } catch (const std::exception&) {
-      return true;  // quota API unavailable: do not block claims on an optional policy
+    } catch (const std::exception& e) {
+      // Quotas unreadable: the namespace's limit is unknown, so a scale-up could exceed it. Fail
+      // closed (the tenancy promise of a quota, GPU调度平台搭建.md:802) and retry; clusters that use
+      // no quotas run with --quota-fail-open.
+      if (opts_.quota_fail_open) return true;
+      *reason = "QuotaUnknown";
+      *why = "ResourceQuotas of namespace " + m.ns + " cannot be read (" + e.what() +
+             "): scale-up blocked until they can (--quota-fail-open admits it)";
+      return false;
     }
   }
   int64_t hard = -1;
@@ -1232,6 +1239,7 @@ bool Mi355xPoolReconciler::quota_reserve_(const ObjectMeta& m, const Mi355xPoolS
                       static_cast<double>(used + more));
     return true;
   }
+  *reason = "QuotaExceeded";
   *why = "ResourceQuota " + m.ns + "/" + qname + " allows " + std::to_string(hard) + " " + spec.resource_name +
          "; " + std::to_string(used) + " in use or reserved, " + std::to_string(more) + " more requested";
   return false;

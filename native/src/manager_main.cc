@@ -51,6 +51,7 @@ struct Flags {
   int workers = 4;
   std::string kinds = "mi355x,azure,job";
   bool leader_elect = false;
+  bool quota_fail_open = false;
   std::string lease_ns = "gpupool-system";
   std::string identity;
   std::string metrics_addr = "127.0.0.1:0";
@@ -111,6 +112,8 @@ controllers:
   --agent-token-file F         shared secret for the node-agent RPC   [$GPUPOOL_AGENT_TOKEN]
   --agent-ca-file F            CA that signs https:// agent endpoints [$GPUPOOL_AGENT_CA_FILE]
   --orphan-sweep D (30s)       release claims whose pool no longer exists
+  --quota-fail-open            admit scale-ups when ResourceQuotas cannot be read (clusters without
+                               quotas); default: block them (Progressing=False, QuotaUnknown)
 leader election:
   --leader-elect  --lease-namespace NS (gpupool-system)  --identity ID
   --lease-duration D (15s)  --renew-deadline D (10s)  --retry-period D (2s)
@@ -171,6 +174,7 @@ Flags parse(int argc, char** argv) {
     else if (is("--workers")) f.workers = std::stoi(val());
     else if (is("--kinds")) f.kinds = val();
     else if (a == "--leader-elect") f.leader_elect = true;
+    else if (a == "--quota-fail-open") f.quota_fail_open = true;
     else if (is("--lease-namespace")) f.lease_ns = val();
     else if (is("--identity")) f.identity = val();
     else if (is("--metrics-addr")) f.metrics_addr = val();
@@ -512,6 +516,7 @@ int main(int argc, char** argv) {
     ropts.resync = std::chrono::milliseconds(f.resync_ms);
     ropts.progress_poll = std::chrono::milliseconds(f.progress_ms);
     ropts.credentials_retry = std::chrono::milliseconds(f.cred_retry_ms);
+    ropts.quota_fail_open = f.quota_fail_open;
 
     Informer nodes(client, res::nodes(), "", std::chrono::milliseconds(f.resync_ms));
     Informer mipools(client, res::mi355xpools(), f.ns, std::chrono::milliseconds(f.resync_ms));

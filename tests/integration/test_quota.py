@@ -165,3 +165,36 @@ def test_quota_hold_of_a_force_removed_pool_is_released(cluster_factory):
     o = k.wait_for(MI355XPOOLS, "new", ns, _settled, timeout=30)
     assert ready_at(2)(o), o["status"]["conditions"]
     print(f"new pool Ready {time.monotonic() - t0:.3f} s after create")
+
+
+def _set_apiserver_faults(c, faults: dict) -> None:
+    import json
+    import urllib.request
+    req = urllib.request.Request(c.url + "/debug/faults", data=json.dumps(faults).encode(),
+                                 method="POST", headers={"Content-Type": "application/json"})
+    urllib.request.urlopen(req, timeout=5).read()
+
+
+def test_unreadable_quotas_block_scale_up_as_quota_unknown(cluster_factory):
+    """the ResourceQuota LIST fails before the manager's quota informer has
+    synced. Admission fails closed — the pool reports Progressing=False, QuotaUnknown and claims
+    nothing — until the quotas can be read; then it scales up (no quota in the namespace)."""
+    c = cluster_factory(apiserver_args=["--fail-list", "resourcequotas"])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    o = k.wait_for(MI355XPOOLS, "p", "default", cond_is("Progressing", "False", "QuotaUnknown"),
+                   timeout=20)
+    assert o["status"].get("readyReplicas", 0) == 0
+    assert not read_claims(_state_dir(c))  # nothing claimed while the quota is unknown
+    msg = next(x["message"] for x in o["status"]["conditions"] if x["type"] == "Progressing")
+    assert "cannot be read" in msg and "--quota-fail-open" in msg
+    _set_apiserver_faults(c, {"failList": {}})
+    k.wait_for(MI355XPOOLS, "p", "default", ready_at(2), timeout=30)
+
+
+def test_quota_fail_open_flag_admits_when_quotas_are_unreadable(cluster_factory):
+    c = cluster_factory(apiserver_args=["--fail-list", "resourcequotas"],
+                        manager_args=["--quota-fail-open"])
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("p", 2), "default")
+    k.wait_for(MI355XPOOLS, "p", "default", ready_at(2), timeout=20)
