@@ -227,6 +227,9 @@ class Agent:
             if q.get("maintenance")}
         self._rechecking: set[str] = set()
         self.xgmi_pairs: dict[str, dict] = self.ledger.xgmi_state()
+        # the newest manager leader seen on a mutating RPC ({"holder", "epoch"}, ledger-persisted)
+        self.leader_fence: dict = self.ledger.leader_state()
+        self._fence_mu = threading.Lock()
         self.pod_usage: dict[str, list[dict]] = {}        # uuid -> per-pod VRAM / gfx time
         self._proc_prev: dict[tuple[str, int], list] = {}  # (uuid, pid) -> [(t, gfxNs)]
         self._pid_pods: dict[int, dict] = {}
@@ -1937,6 +1940,42 @@ class Agent:
             env["GPUPOOL_CU_LAYOUT"] = "striped"
         return env
 
+    # ================================================================ leader fencing
+    MUTATING = {"/v1/claims", "/v1/release", "/v1/cordon", "/v1/policy", "/v1/maintenance"}
+
+    def check_leader(self, method: str, path: str, headers: dict) -> tuple | None:
+        """Fencing tokens (the manager's Lease, README.md:162->242's missing manager step): every
+        mutating RPC of a leader-elected manager carries its identity and epoch (the Lease's
+        leaseTransitions). The newest epoch seen is persisted; an older one — a leader that was
+        paused between its own fence check and the send while a successor took over — is refused
+        with 409 StaleLeader before anything is touched. A request without a token (leader
+        election off, an admin's gpuctl) is not checked."""
+        if method != "POST" or path not in self.MUTATING:
+            return None
+        raw = headers.get("x-gpupool-leader-epoch")
+        if raw is None:
+            return None
+        from .rpc import json_reply
+        try:
+            epoch = int(raw)
+        except ValueError:
+            return json_reply({"reason": "BadRequest", "message": f"bad leader epoch {raw!r}"}, 400)
+        holder = headers.get("x-gpupool-leader", "")
+        with self._fence_mu:
+            cur_e = int(self.leader_fence.get("epoch", -1))
+            cur_h = str(self.leader_fence.get("holder", ""))
+            if epoch < cur_e or (epoch == cur_e and cur_h and holder != cur_h):
+                self.stats["stale_leader_refused"] = self.stats.get("stale_leader_refused", 0) + 1
+                log.warning("refused %s from stale leader %s (epoch %d; newest seen %s at %d)",
+                            path, holder, epoch, cur_h, cur_e)
+                return json_reply({"reason": "StaleLeader",
+                                   "message": f"leader {holder} epoch {epoch} is stale: {cur_h} holds "
+                                              f"epoch {cur_e}"}, 409)
+            if epoch > cur_e or not cur_h:
+                self.leader_fence = {"holder": holder, "epoch": epoch, "at": now_rfc3339()}
+                self.ledger.commit_leader(self.leader_fence)  # durable before acting on it
+        return None
+
     # ================================================================ node registration
     def register_node(self) -> None:
         if not self.cfg.apiserver:
@@ -2242,7 +2281,7 @@ def build_routes(agent: Agent) -> dict:
 def serve(agent: Agent, ready_file: str | None = None) -> None:
     """Start the RPC listeners and the agent's background loops; block until interrupted."""
     from .rpc import RpcServer
-    srv = RpcServer(build_routes(agent), agent.cfg.auth_token)
+    srv = RpcServer(build_routes(agent), agent.cfg.auth_token, guard=agent.check_leader)
     agent.rpc = srv
     # the start-up heap (modules, gRPC/protobuf descriptors, the device model) lives for the whole
     # run: out of the collector's generations, a full collection walks only what came after — one

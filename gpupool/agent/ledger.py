@@ -91,11 +91,13 @@ class Ledger:
         self._src_seq = 0                      # the sequence number of that hand-over
         self._sweep: dict[str, dict] = {}
         self._xgmi: dict[str, dict] = {}
+        self._leader: dict = {}
         try:
             with open(self.path) as f:
                 doc = json.load(f) or {}
             self._sweep = dict(doc.get("hbmSweep") or {})
             self._xgmi = dict(doc.get("xgmiPairs") or {})
+            self._leader = dict(doc.get("leaderFence") or {})
         except (OSError, ValueError):
             pass
 
@@ -164,9 +166,11 @@ class Ledger:
                     seq = self._seq
                     if self._claims_src is not None:  # handed over after the encode: next turn
                         seq = self._src_seq - 1
-                    text = '{"version": %d, "claims": %s, "hbmSweep": %s, "xgmiPairs": %s}' % (
-                        VERSION, self._claims_text, json.dumps(self._sweep, sort_keys=True),
-                        json.dumps(self._xgmi, sort_keys=True))
+                    text = '{"version": %d, "claims": %s, "hbmSweep": %s, "xgmiPairs": %s, ' \
+                        '"leaderFence": %s}' % (
+                            VERSION, self._claims_text, json.dumps(self._sweep, sort_keys=True),
+                            json.dumps(self._xgmi, sort_keys=True),
+                            json.dumps(self._leader, sort_keys=True))
                 if seq > self._written:
                     _atomic_write_text(self.path, text, self.fsync)
                     self.writes += 1
@@ -209,6 +213,19 @@ class Ledger:
             self.flush(seq)
         else:
             self._kick_lazy()
+
+    def commit_leader(self, fence: dict) -> None:
+        """Persist the highest leader fencing token seen (durable: a restarted agent must still
+        refuse an older leader)."""
+        with self._mu:
+            self._leader = dict(fence)
+            self._seq += 1
+            seq = self._seq
+        self.flush(seq)
+
+    def leader_state(self) -> dict:
+        with self._mu:
+            return dict(self._leader)
 
     def xgmi_state(self) -> dict[str, dict]:
         with self._mu:

@@ -143,8 +143,12 @@ def text_reply(text: str, status: int = 200) -> tuple:
 
 class RpcServer:
     def __init__(self, routes: dict[tuple[str, str], Handler], token: str = "",
-                 max_conns: int = 512, first_request_timeout: float = 10.0):
+                 max_conns: int = 512, first_request_timeout: float = 10.0,
+                 guard: Callable[[str, str, dict], tuple | None] | None = None):
         self.routes = routes
+        # guard(method, path, headers) -> a reply refusing the request, or None: runs after the
+        # token check and before the handler (the agent's leader fencing, StaleLeader)
+        self.guard = guard
         self.max_conns = max_conns
         self.first_request_timeout = first_request_timeout
         self._conns = 0
@@ -451,6 +455,10 @@ class RpcServer:
         path, _, qs = target.partition("?")
         self.requests += 1  # the token was checked in _serve_conn, before the body was read
         h = self.routes.get((method, path))
+        if h is not None and self.guard is not None:
+            refused = self.guard(method, path, headers)
+            if refused is not None:
+                return refused
         if h is None:
             known = any(p == path for _, p in self.routes)
             return json_reply({"reason": "MethodNotAllowed" if known else "NotFound",

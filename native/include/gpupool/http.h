@@ -70,10 +70,12 @@ class HttpClient {
   HttpClient(const HttpClient&) = delete;
   HttpClient& operator=(const HttpClient&) = delete;
 
+  // ``extra_headers``: preformatted "Name: value\r\n" lines (e.g. the leader's fencing token)
   HttpResponse request(const std::string& method, const std::string& path,
                        const std::string& body = "",
                        const std::string& content_type = "application/json",
-                       const std::string& accept = "application/json", int timeout_ms = -1);
+                       const std::string& accept = "application/json", int timeout_ms = -1,
+                       const std::string& extra_headers = "");
 
   // Streams a GET response line by line (k8s watch / agent long-poll). ``on_line`` returns false
   // to stop. Returns the HTTP status; for status >= 400 ``err_body`` receives the body. Stops
@@ -91,7 +93,7 @@ class HttpClient {
   void give_(std::unique_ptr<Conn> c);
   bool send_request_(Conn& c, const std::string& method, const std::string& path,
                      const std::string& body, const std::string& content_type,
-                     const std::string& accept);
+                     const std::string& accept, const std::string& extra_headers = "");
 
   Url url_;
   std::string token_;

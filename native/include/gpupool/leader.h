@@ -30,6 +30,17 @@ struct LeaderConfig {
 // true without leader election.
 bool leader_fence_ok();
 
+// The fencing token this process holds as leader: its identity and the Lease's leaseTransitions
+// when it last acquired or renewed (a takeover increments it, so a newer leader always carries a
+// larger epoch). epoch < 0 without leader election. Sent on every mutating node-agent RPC; the
+// agent remembers the highest epoch it has seen and refuses older ones (409 StaleLeader), so a
+// leader paused between its fence check and the send cannot act after a successor took over.
+struct LeaderToken {
+  std::string identity;
+  int64_t epoch = -1;
+};
+LeaderToken leader_token();
+
 class LeaderElector {
  public:
   LeaderElector(KubeClient& client, LeaderConfig cfg);

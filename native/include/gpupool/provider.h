@@ -208,6 +208,7 @@ class RocmProvider : public DeviceProvider {
 
  private:
   Json post_(const std::string& node, const std::string& path, const Json& body);
+  static void test_pause_after_fence_(const std::string& path);
   void invalidate_(const std::string& node);
   Informer& nodes_;
   int timeout_ms_;

@@ -10,6 +10,10 @@
 #include "gpupool/leader.h"
 #include "gpupool/trace.h"
 
+#include <cstdlib>
+#include <fstream>
+#include <thread>
+
 namespace gpupool {
 
 DeviceView DeviceView::from(const Json& j) {
@@ -154,12 +158,18 @@ Json RocmProvider::post_(const std::string& node, const std::string& path, const
   } done{this, node};
   if (!leader_fence_ok())  // a paused leader must not claim or release after another took over
     throw ProviderError("NotLeader", "agent on " + node + ": " + path + " not sent: leadership not renewed in time");
+  // The check above is local: a leader paused right after it would still send. The fencing token
+  // makes the agent the judge — it refuses an epoch older than one it has seen (StaleLeader).
+  std::string fence;
+  if (const LeaderToken tok = leader_token(); tok.epoch >= 0)
+    fence = "X-Gpupool-Leader: " + tok.identity + "\r\nX-Gpupool-Leader-Epoch: " + std::to_string(tok.epoch) + "\r\n";
+  test_pause_after_fence_(path);
   invalidate_(node);  // every POST mutates the agent: the next observe must ask it
   trace::Span span("agent:POST " + path);
   std::shared_ptr<HttpClient> c = client_for(node);
   HttpResponse r;
   try {
-    r = c->request("POST", path, body.dump());
+    r = c->request("POST", path, body.dump(), "application/json", "application/json", -1, fence);
   } catch (const std::exception& e) {
     throw ProviderError("AgentUnreachable", "agent on " + node + ": " + e.what());
   }
@@ -175,6 +185,31 @@ Json RocmProvider::post_(const std::string& node, const std::string& path, const
                         r.status >= 500);
   }
   return j ? *j : Json::object();
+}
+
+// Test hook (chaos tests only): with $GPUPOOL_TEST_FENCE_HOLD_DIR set, a mutating RPC whose path
+// has a file "<dir>/hold<path with / as _>" waits — after its fence check and token, before the
+// send — until that file is removed: the "leader paused between check and act" the fencing token
+// is for. Unset in production: one getenv per RPC.
+void RocmProvider::test_pause_after_fence_(const std::string& path) {
+  static const char* dir = std::getenv("GPUPOOL_TEST_FENCE_HOLD_DIR");
+  if (!dir || !*dir) return;
+  std::string tag;
+  for (char ch : path) tag.push_back(ch == '/' ? '_' : ch);
+  const std::string f = std::string(dir) + "/hold" + tag;
+  bool marked = false;
+  for (int i = 0; i < 6000; ++i) {  // at most 60 s
+    std::ifstream in(f);
+    if (!in.good()) return;
+    std::string who;  // the file names the identity to hold (empty: any)
+    std::getline(in, who);
+    if (!who.empty() && who != leader_token().identity) return;
+    if (!marked) {  // tell the test the send is being held
+      std::ofstream(std::string(dir) + "/held" + tag) << leader_token().epoch << "\n";
+      marked = true;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
 }
 
 NodeView RocmProvider::observe(const std::string& node) { return observe_pool(node, ""); }

@@ -452,7 +452,7 @@ void HttpClient::give_(std::unique_ptr<Conn> c) {
 
 bool HttpClient::send_request_(Conn& c, const std::string& method, const std::string& path,
                                const std::string& body, const std::string& content_type,
-                               const std::string& accept) {
+                               const std::string& accept, const std::string& extra_headers) {
   std::string req;
   req.reserve(256 + body.size());
   req += method + " " + path + " HTTP/1.1\r\n";
@@ -460,6 +460,7 @@ bool HttpClient::send_request_(Conn& c, const std::string& method, const std::st
   req += "User-Agent: gpupool-manager/0.1\r\n";
   req += "Accept: " + accept + "\r\n";
   if (!token_.empty()) req += "Authorization: Bearer " + token_ + "\r\n";
+  req += extra_headers;
   if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
     req += "Content-Type: " + content_type + "\r\n";
     req += "Content-Length: " + std::to_string(body.size()) + "\r\n";
@@ -541,13 +542,13 @@ bool read_head(ConnT& c, HttpResponse& r, int timeout_ms, std::string* err,
 
 HttpResponse HttpClient::request(const std::string& method, const std::string& path,
                                  const std::string& body, const std::string& content_type,
-                                 const std::string& accept, int timeout_ms) {
+                                 const std::string& accept, int timeout_ms, const std::string& extra_headers) {
   if (timeout_ms < 0) timeout_ms = timeout_ms_;
   for (int attempt = 0; attempt < 2; ++attempt) {
     std::unique_ptr<Conn> c = take_();
     bool reused = c != nullptr;
     if (!c) c = connect_(timeout_ms);
-    if (!send_request_(*c, method, path, body, content_type, accept)) {
+    if (!send_request_(*c, method, path, body, content_type, accept, extra_headers)) {
       if (reused) continue;
       throw HttpError("send failed: " + std::string(strerror(errno)));
     }

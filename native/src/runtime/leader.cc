@@ -2,6 +2,7 @@
 
 #include <atomic>
 #include <limits>
+#include <mutex>
 #include <thread>
 
 namespace gpupool {
@@ -17,6 +18,16 @@ int64_t fence_now_ns() {
 }  // namespace
 
 bool leader_fence_ok() { return fence_now_ns() < g_fence_until_ns.load(); }
+
+namespace {
+std::mutex g_token_mu;
+LeaderToken g_token;  // epoch -1: no election
+}  // namespace
+
+LeaderToken leader_token() {
+  std::lock_guard<std::mutex> g(g_token_mu);
+  return g_token;
+}
 
 LeaderElector::LeaderElector(KubeClient& client, LeaderConfig cfg)
     : client_(client), cfg_(std::move(cfg)), log_(Logger("leader").with("identity", cfg_.identity)) {
@@ -44,6 +55,8 @@ bool LeaderElector::try_acquire_or_renew() {
     try {
       client_.create(res::leases(), cfg_.ns, obj);
       leader_ = true;
+      std::lock_guard<std::mutex> g(g_token_mu);
+      g_token = {cfg_.identity, 0};
       return true;
     } catch (const KubeError& e2) {
       if (e2.code == 409) return false;  // someone else created it first
@@ -86,6 +99,10 @@ bool LeaderElector::try_acquire_or_renew() {
     throw;
   }
   leader_ = true;
+  {
+    std::lock_guard<std::mutex> g(g_token_mu);
+    g_token = {cfg_.identity, upd["spec"]["leaseTransitions"].as_int(0)};
+  }
   return true;
 }
 

@@ -1,0 +1,60 @@
+"""Agent-side leader fencing (gpupool/agent/agent.py ``check_leader``): the newest manager epoch
+seen on a mutating RPC is persisted in the ledger and older epochs are refused (409 StaleLeader)
+before the handler runs — also after an agent restart. Requests without a token (leader election
+off, gpuctl) pass unchecked."""
+from __future__ import annotations
+
+import json
+import os
+
+from gpupool.agent.agent import Agent, AgentConfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+FIXTURE = os.path.join(ROOT, "tests", "fixtures", "node_8x_mi355x.json")
+
+
+def make_agent(tmp_path) -> Agent:
+    return Agent(AgentConfig(node="n0", backend="fake", fixture=FIXTURE, count=2,
+                             state_dir=str(tmp_path / "state"), probe_mode="simulated",
+                             probe_sim_ms=0, fsync=False, scrub_interval_s=0))
+
+
+def tok(holder: str, epoch: int) -> dict:
+    return {"x-gpupool-leader": holder, "x-gpupool-leader-epoch": str(epoch)}
+
+
+def test_older_epochs_are_refused_and_the_newest_survives_a_restart(tmp_path, native_built):
+    a = make_agent(tmp_path)
+    assert a.check_leader("POST", "/v1/claims", tok("m-a", 3)) is None
+    assert a.check_leader("POST", "/v1/release", tok("m-a", 3)) is None  # same leader again
+    assert a.check_leader("POST", "/v1/claims", tok("m-b", 4)) is None   # a successor
+    r = a.check_leader("POST", "/v1/claims", tok("m-a", 3))              # the old one resumes
+    assert r[0] == 409 and json.loads(r[2])["reason"] == "StaleLeader"
+    r = a.check_leader("POST", "/v1/cordon", tok("m-c", 4))  # same epoch, another holder
+    assert r[0] == 409
+    assert a.stats["stale_leader_refused"] == 2
+    # not mutating / no token: never checked
+    assert a.check_leader("GET", "/v1/node", tok("m-a", 0)) is None
+    assert a.check_leader("POST", "/v1/claims", {}) is None
+    a.stop()
+    b = make_agent(tmp_path)  # restart: the fence is in the ledger
+    assert b.leader_fence["holder"] == "m-b" and b.leader_fence["epoch"] == 4
+    assert b.check_leader("POST", "/v1/release", tok("m-a", 3))[0] == 409
+    assert b.check_leader("POST", "/v1/release", tok("m-b", 4)) is None
+    b.stop()
+
+
+def test_a_refused_request_never_reaches_its_handler(tmp_path, native_built):
+    from gpupool.agent.agent import build_routes
+    from gpupool.agent.rpc import RpcServer
+    a = make_agent(tmp_path)
+    srv = RpcServer(build_routes(a), guard=a.check_leader)
+    a.check_leader("POST", "/v1/claims", tok("new", 7))
+    out = srv._dispatch("POST", "/v1/claims", tok("old", 6),
+                        json.dumps({"poolUID": "p", "count": 1}).encode())
+    assert out[0] == 409 and not a.records  # nothing claimed
+    out = srv._dispatch("POST", "/v1/claims", tok("new", 7),
+                        json.dumps({"poolUID": "p", "count": 1}).encode())
+    assert out[0] == 200 and len(a.records) == 1
+    srv.close()
+    a.stop()
