@@ -347,6 +347,12 @@ def main() -> int:
         for k in sweep:
             cs = [cy for cy in cycles if cy["n"] == k]
             per_n[str(k)] = summary([cy["readySeconds"] for cy in cs], sum(cy["ok"] for cy in cs))
+            if cs:  # ground truth read once at Ready (no grace): the fraction of cycles it agreed
+                per_n[str(k)]["truth_first_read_agrees"] = round(
+                    sum(1 for cy in cs if cy.get("truthFirstReadAgrees")) / len(cs), 4)
+                settle = [cy["truth"]["settleMs"] for cy in cs if "settleMs" in cy.get("truth", {})]
+                if settle:  # diagnostic: how long the kubelet side lagged when it did not
+                    per_n[str(k)]["truth_settle_ms_max"] = max(settle)
             per_n[str(k)].update(_device_evidence(cs))
             # the agent at this N: its resident memory, the HIP contexts it holds, and the VRAM
             # in use on the GPUs the last cycle of this N claimed (after the timed region)
@@ -544,6 +550,11 @@ def main() -> int:
                 "p90_s": head["p90_s"],
                 "max_s": head["max_s"],
                 "readyReplicas_accuracy": all_ok / len(cycles) if cycles else None,
+                # the truth behind that accuracy is read once, at the instant the pool reads Ready
+                "truth_first_read_agrees": (round(sum(1 for cy in cycles if cy.get(
+                    "truthFirstReadAgrees")) / len(cycles), 4) if cycles else None),
+                "readiness_mode": "advertise-on-submit" if os.environ.get(
+                    "GPUPOOL_ADVERTISE_ON_SUBMIT") == "1" else "strict (after the ListAndWatch write)",
                 "per_n": per_n,
                 "timed_steps_completed": timed_steps,
                 "operator_ms_per_step": round((elapsed - gt_s) * 1e3 / max(1, timed_steps), 2),

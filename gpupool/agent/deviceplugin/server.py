@@ -215,14 +215,14 @@ class DevicePluginServer:
             return None
         return (st.st_ino, st.st_ctime_ns)
 
-    # ``notify(sync=True)`` (the claim path) marks the new list advertised as soon as it is handed
-    # to a live stream's sender instead of after gRPC reports the write complete. gRPC's Python
-    # server acknowledges a streamed write only after its completion-queue thread has run
-    # (0.29–0.35 ms per message here, profiles/r4g_advertise_ab.json), while the kubelet consumes
-    # the stream asynchronously anyway and publishes allocatable on its own node-status sync. A
-    # stream that turns out dead ends (``gone``), which clears the advertised bits again. False:
-    # the strict behaviour (mark only after the write completed, on the claim's thread).
-    ADVERTISE_ON_SUBMIT = os.environ.get("GPUPOOL_ADVERTISE_ON_WRITE", "") in ("", "0")
+    # Strict by default: a GPU counts as advertised (and so towards readyReplicas) only once the
+    # ListAndWatch write carrying it has completed on a live kubelet stream — readyReplicas never
+    # runs ahead of what the kubelet was told. Opt-in fast mode (GPUPOOL_ADVERTISE_ON_SUBMIT=1):
+    # ``notify(sync=True)`` (the claim path) marks the list advertised as soon as it is handed to a
+    # live stream's sender, saving gRPC's write acknowledgement (0.24–0.35 ms per claim,
+    # profiles/r4g_advertise_ab.json) at the cost of that guarantee (a stream that turns out dead
+    # clears the bits again, but a reader may have seen them meanwhile).
+    ADVERTISE_ON_SUBMIT = os.environ.get("GPUPOOL_ADVERTISE_ON_SUBMIT", "0") == "1"
 
     def notify(self, sync: bool = False) -> None:
         """Publish the current device list, built on the caller's thread, through the sender

@@ -35,6 +35,8 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
     assert sorted(cfg["per_n"], key=int) == ["1", "2", "4", "8"]
     for k, v in cfg["per_n"].items():
         assert v["accuracy"] == 1.0 and 0 < v["p50_s"] < 30, (k, v)
+        # the truth is read once, at Ready, with no grace: readiness is strict by default
+        assert v["truth_first_read_agrees"] == 1.0, (k, v)
     assert out["value"] == cfg["per_n"]["8"]["p50_s"]
     # device-level evidence per N: every claim's probe, and the xGMI ring of every multi-GPU
     # claim (N links per claim of N GPUs), with the pair coverage the rotating order reached
@@ -58,6 +60,10 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
     assert n8["xgmi_links_measured"] == 8 and n8["xgmi_pairs_total"] == 7
     assert len(n8["xgmi_pairs_covered_last"]) == 8 and all(1 <= p <= 7 for p in n8["xgmi_pairs_covered_last"])
     assert cfg["readyReplicas_accuracy"] == 1.0
+    assert cfg["truth_first_read_agrees"] == 1.0
+    assert cfg["readiness_mode"].startswith("strict")
+    # the probe helpers beside the agent (helper-sim on the fake backend)
+    assert cfg["per_n"]["1"]["agent"]["probe_helpers"] >= 1
     # agent + manager footprint around the timed region (Prometheus process_* metrics)
     for when in ("before_timed", "after_timed"):
         for who in ("agent", "manager"):
