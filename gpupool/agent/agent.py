@@ -192,6 +192,8 @@ class Agent:
         self.share_lib_dir = self._install_share_lib()
         self._pod_ids: tuple[float, set[str]] | None = None  # (listed at, device IDs pods hold)
         self._over_budget: set[tuple[str, str, str]] = set()  # (gpu, ns, pod) over their slot budget
+        self._over_samples: dict[tuple[str, str, str], int] = {}  # ... for how many samples in a row
+        self._budget_evicted: set[tuple[str, str]] = set()  # (ns, pod) evicted for it (once each)
         self._layouts: dict[tuple, dict] = {}  # memoised slot layouts (_slot_layout)
         self.snap = self.dev.snapshot()
         self.backend = self.snap.get("backend", cfg.backend)
@@ -893,7 +895,7 @@ class Agent:
             for pe in pods:
                 key = (gpu, pe.get("namespace", ""), pe.get("name", ""))
                 slots_of[key] = slots_of.get(key, 0) + 1
-        out, seen = [], set()
+        out, seen, evict = [], set(), []
         slack, frac = self.SLOT_BUDGET_SLACK
         with self.lock:
             for u, pods in usage.items():
@@ -903,6 +905,8 @@ class Agent:
                 per_slot = self._slot_layout(u, rec).get("hbmBytesPerSlot") or 0
                 if not per_slot:
                     continue
+                action = str((((rec.get("policy") or {}).get("sharing") or {})
+                              .get("overBudgetAction")) or "Flag")
                 for e in pods:
                     n = slots_of.get((u, e["namespace"], e["pod"]), 0)
                     if not n:
@@ -913,13 +917,64 @@ class Agent:
                         e["overBudget"] = True
                         key = (u, e["namespace"], e["pod"])
                         seen.add(key)
+                        count = self._over_samples.get(key, 0) + 1
+                        self._over_samples[key] = count
+                        e["overBudgetSamples"] = count
                         if key not in self._over_budget:
                             out.append(f"pod {e['namespace']}/{e['pod']} holds {e['vramBytes']} B of "
                                        f"VRAM on GPU {u}, over its {n} slot(s) x {per_slot} B: "
                                        f"its HBM limit is not in force (is libgpupool_share.so "
                                        f"loaded in the pod?)")
+                        # spec.sharing.overBudgetAction Evict: two samples in a row (not one
+                        # transient reading), once per pod
+                        if action == "Evict" and count >= self.EVICT_AFTER_SAMPLES and \
+                                (e["namespace"], e["pod"]) not in self._budget_evicted:
+                            self._budget_evicted.add((e["namespace"], e["pod"]))
+                            evict.append((u, e["namespace"], e["pod"], e["vramBytes"], budget))
             self._over_budget = seen
+            self._over_samples = {k: v for k, v in self._over_samples.items() if k in seen}
+        for args in evict:
+            self._evict_over_budget(*args)
         return out
+
+    EVICT_AFTER_SAMPLES = 2
+
+    def _evict_over_budget(self, uuid: str, ns: str, pod: str, vram: int, budget: int) -> None:
+        """Evict a pod whose VRAM exceeded its slots' budget (spec.sharing.overBudgetAction
+        Evict): the HBM limit lives inside the pod (libgpupool_share.so), which the pod can
+        defeat — unset HSA_TOOLS_LIB, or never load it. The agent sees the pod's VRAM from
+        outside (amdsmi process list / DRM fdinfo) and takes the pod off the GPU its siblings
+        share, through the Eviction API (the pod's PodDisruptionBudget applies), with an Event on
+        the pod. Runs on its own thread: the sampler never waits for the API server."""
+        msg = (f"pod {ns}/{pod} holds {vram} B of VRAM on GPU {uuid}, over its slots' "
+               f"{budget} B HBM budget for {self.EVICT_AFTER_SAMPLES}+ samples: evicted "
+               f"(spec.sharing.overBudgetAction Evict)")
+        log.warning("%s", msg)
+        with self.lock:
+            self.stats["over_budget_evictions"] = self.stats.get("over_budget_evictions", 0) + 1
+        if not self.cfg.apiserver:
+            log.warning("no API server configured: cannot evict %s/%s", ns, pod)
+            return
+
+        def run():
+            from ..kube import EVENTS, Client
+            try:
+                c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
+                c.evict(ns, pod)
+                ts = now_rfc3339()
+                c.create(EVENTS, {
+                    "apiVersion": "v1", "kind": "Event",
+                    "metadata": {"name": f"{pod}.{os.urandom(6).hex()}"},
+                    "involvedObject": {"kind": "Pod", "name": pod, "namespace": ns,
+                                       "apiVersion": "v1"},
+                    "reason": "SlotBudgetExceeded", "message": msg, "type": "Warning",
+                    "count": 1, "firstTimestamp": ts, "lastTimestamp": ts,
+                    "source": {"component": "gpupool-agent", "host": self.cfg.node}}, ns)
+            except Exception as ex:  # retried: the next over-budget sample evicts again
+                log.warning("evicting over-budget pod %s/%s failed: %s", ns, pod, ex)
+                with self.lock:
+                    self._budget_evicted.discard((ns, pod))
+        threading.Thread(target=run, daemon=True, name="budget-evict").start()
 
     # ================================================================ views
     def _pods_by_device(self, fresh: bool = False) -> dict[str, list[dict]]:
@@ -1767,11 +1822,18 @@ class Agent:
                 mounts.append({"container_path": self.SHARE_ACCOUNT_PATH, "host_path": acct,
                                "read_only": False})
                 envs["GPUPOOL_SHARE_ACCOUNT"] = self.SHARE_ACCOUNT_PATH
+                # the limit itself, read-only: the account's counters must be writable by the
+                # pod's processes, so its header limit is the pod's to edit — this one is not
+                # (the library takes the smallest limit it is given)
+                mounts.append({"container_path": self.SHARE_LIMIT_PATH,
+                               "host_path": acct[:-len(".acct")] + ".limit", "read_only": True})
+                envs["GPUPOOL_SHARE_LIMIT"] = self.SHARE_LIMIT_PATH
         return {"envs": envs, "devices": ["/dev/kfd"] + render, "mounts": mounts,
                 "annotations": {schema.ANN_POD_DEVICES: ",".join(ids)}}
 
     SHARE_LIB_DIR = "/opt/gpupool/lib"  # where the pod sees libgpupool_share.so
     SHARE_ACCOUNT_PATH = "/var/run/gpupool/share.acct"  # where it sees its pod's HBM account
+    SHARE_LIMIT_PATH = "/var/run/gpupool/share.limit"  # ...and, read-only, its limit
     SHARE_LIB = "libgpupool_share.so"
 
     def _install_share_lib(self) -> str | None:
@@ -1833,17 +1895,31 @@ class Agent:
                     continue
                 path = os.path.join(d, name)
                 if mine & set(slotlib.account_slots(path) or ()):
-                    try:
-                        os.unlink(path)
-                    except FileNotFoundError:  # the sampler's GC got there first
-                        pass
+                    for p in (path, path[:-len(".acct")] + ".limit"):
+                        try:
+                            os.unlink(p)
+                        except FileNotFoundError:  # the sampler's GC got there first
+                            pass
             with self.lock:
                 uuids = [(self.by_uuid.get(u) or {}).get("hipUUID") or "" for u in gpus]
-            path = os.path.join(d, f"{uuid4().hex}.acct")
+            if not all(uuids):
+                # a GPU without a hipUUID (amd-smi CLI backend, empty serial) cannot be matched by
+                # identity: a version-2 account would match no GPU and silently fall back to a
+                # per-process budget. A version-1 account maps by enumeration order instead.
+                log.warning("HBM account for %s: GPU(s) without hipUUID %s; ordinal mapping",
+                            slots, [u for u, h in zip(gpus, uuids) if not h])
+                uuids = []
+            stem = os.path.join(d, uuid4().hex)
+            path = stem + ".acct"
             fd = os.open(path, os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o666)
             try:
                 os.write(fd, slotlib.account_bytes(limit, slots, uuids))
                 os.fchmod(fd, 0o666)  # pods may run as any user
+            finally:
+                os.close(fd)
+            fd = os.open(stem + ".limit", os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o644)
+            try:
+                os.write(fd, slotlib.limit_bytes(limit))
             finally:
                 os.close(fd)
             return path
@@ -1933,6 +2009,10 @@ class Agent:
         mounts.append({"container_path": self.SHARE_LIB_DIR, "host_path": self.share_lib_dir,
                        "read_only": True})
         env = {"HSA_TOOLS_LIB": f"{self.SHARE_LIB_DIR}/{self.SHARE_LIB}"}
+        xcds = {lay.get("xcds") for lay in (self._slot_layout(u, self.records.get(u) or {})
+                                             for u in per_gpu) if lay.get("xcds")}
+        if cu_mask and xcds:  # a narrowed app mask must keep a CU on each XCD (share.cc)
+            env["GPUPOOL_CU_XCDS"] = str(max(xcds))
         if hbm:  # allocate_spec adds the pod-wide account file (GPUPOOL_SHARE_ACCOUNT)
             env["GPUPOOL_HBM_LIMIT_BYTES"] = str(hbm)
         if cu_mask:

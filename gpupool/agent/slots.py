@@ -99,15 +99,23 @@ def account_bytes(limit: int, slots: list[str], gpu_uuids: list[str],
     mtime moves with every charge), zeroed counters, the slot ids as text."""
     buf = bytearray(ACCT_BYTES)
     ids = list(gpu_uuids)[:8]
-    buf[0:32] = b"GPSHARE1" + struct.pack("<QIId", int(limit), 2, len(ids),
+    # no identities: version 1 (ordinal mapping); its slot-id text sits where v2 keeps the UUIDs
+    version = 2 if ids else 1
+    buf[0:32] = b"GPSHARE1" + struct.pack("<QIId", int(limit), version, len(ids) or 1,
                                           time.time() if created is None else created)
     for g, u in enumerate(ids):
         raw = u.encode()[:ACCT_UUID_BYTES - 1]
         at = ACCT_UUIDS_AT + g * ACCT_UUID_BYTES
         buf[at:at + len(raw)] = raw
-    text = ",".join(slots).encode()[: ACCT_BYTES - ACCT_IDS_AT_V2 - 1]
-    buf[ACCT_IDS_AT_V2:ACCT_IDS_AT_V2 + len(text)] = text
+    at = ACCT_IDS_AT_V2 if version >= 2 else ACCT_IDS_AT_V1
+    text = ",".join(slots).encode()[: ACCT_BYTES - at - 1]
+    buf[at:at + len(text)] = text
     return bytes(buf)
+
+
+def limit_bytes(limit: int) -> bytes:
+    """The read-only limit file beside an account (share.cc read_limit_file)."""
+    return f"GPLIMIT1 {int(limit)}\n".encode()
 
 
 def read_account(path: str) -> dict | None:
@@ -122,8 +130,7 @@ def read_account(path: str) -> dict | None:
             text = f.read().split(b"\0", 1)[0].decode(errors="replace")
     except OSError:
         return None
-    if version < 2:
-        created = 0.0  # version 1 kept no creation time
+    # (version 1 files of earlier agents kept no creation time: 0.0 there)
     return {"limit": limit, "version": version, "ngpus": ngpus, "created": created,
             "slots": [s for s in text.split(",") if s]}
 
@@ -153,6 +160,10 @@ def gc_accounts(directory: str, live_ids: set[str], older_than: float) -> list[s
         try:
             os.unlink(path)
             gone.append(path)
+        except OSError:
+            pass
+        try:  # its read-only limit file goes with it
+            os.unlink(path[:-len(".acct")] + ".limit")
         except OSError:
             pass
     return gone

@@ -264,6 +264,16 @@ MI355X_SPEC = {
                 "cuPerSlot": {**_I32, "minimum": 0, "maximum": 256, "default": 0,
                               "description": "Compute units reserved for one slot (0 = all; "
                                              "cuPerSlot x replicasPerGPU <= 256)."},
+                "overBudgetAction": {"type": "string", "enum": ["Flag", "Evict"],
+                                     "default": "Flag",
+                                     "description": "What the node agent does about a pod whose "
+                                                    "VRAM on a GPU (amdsmi / DRM fdinfo, outside "
+                                                    "the pod) exceeds its slots' HBM budget — a "
+                                                    "pod in which libgpupool_share.so is not in "
+                                                    "force: Flag (metric + Node event) or Evict "
+                                                    "(after 2 consecutive over-budget samples the "
+                                                    "pod is evicted through the API, with an "
+                                                    "Event)."},
             },
         },
         "health": {
@@ -663,7 +673,9 @@ def agent_rbac() -> list[dict]:
     (labels, agent-endpoint annotation) and heartbeats the GPUPoolAgentReady/ROCmReady node
     conditions and posts Events on its Node (amdsmi hardware events, HBM sweep failures);
     device/pod facts come from the kubelet's local sockets; it lists pods only to resolve the pod
-    UID in a GPU process's cgroup to namespace/name for per-pod accounting."""
+    UID in a GPU process's cgroup to namespace/name for per-pod accounting, and evicts a pod only
+    when its pool asks for it (spec.sharing.overBudgetAction Evict: the pod's VRAM is over its
+    slots' HBM budget)."""
     sa = {"apiVersion": "v1", "kind": "ServiceAccount",
           "metadata": {"name": "gpupool-agent", "namespace": AGENT_NAMESPACE}}
     role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
@@ -672,7 +684,8 @@ def agent_rbac() -> list[dict]:
                        "verbs": ["get", "create", "patch"]},
                       {"apiGroups": [""], "resources": ["nodes/status"], "verbs": ["patch"]},
                       {"apiGroups": [""], "resources": ["events"], "verbs": ["create"]},
-                      {"apiGroups": [""], "resources": ["pods"], "verbs": ["list"]}]}
+                      {"apiGroups": [""], "resources": ["pods"], "verbs": ["list"]},
+                      {"apiGroups": [""], "resources": ["pods/eviction"], "verbs": ["create"]}]}
     binding = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
                "metadata": {"name": "gpupool-agent-rolebinding"},
                "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",

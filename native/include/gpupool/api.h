@@ -73,6 +73,7 @@ struct Mi355xPoolSpec {
   int32_t sharing_replicas = 1;  // time-sliced slots advertised per GPU (spec.sharing.replicasPerGPU)
   int64_t sharing_hbm_bytes = 0;  // per-slot HBM budget (spec.sharing.hbmBytesPerSlot; 0 = none)
   int32_t sharing_cus = 0;        // per-slot CU share (spec.sharing.cuPerSlot; 0 = all CUs)
+  std::string sharing_over_budget = "Flag";  // Flag | Evict (agent-enforced)
   bool autoscale = false;  // demand-driven spec.replicas (Mi355xPoolAutoscaler)
   int32_t autoscale_min = 0, autoscale_max = 8;
   int64_t scale_down_delay_seconds = 300;

@@ -90,6 +90,7 @@ Mi355xPoolSpec Mi355xPoolSpec::from(const Json& s) {
   p.sharing_replicas = static_cast<int32_t>(std::max<int64_t>(1, s.path("sharing.replicasPerGPU").as_int(1)));
   p.sharing_hbm_bytes = std::max<int64_t>(0, s.path("sharing.hbmBytesPerSlot").as_int(0));
   p.sharing_cus = static_cast<int32_t>(std::max<int64_t>(0, s.path("sharing.cuPerSlot").as_int(0)));
+  p.sharing_over_budget = s.path("sharing.overBudgetAction").str_or("Flag");
   const Json& a = s["autoscale"];
   p.autoscale = a["enabled"].as_bool(false);
   p.autoscale_min = static_cast<int32_t>(a["minReplicas"].as_int(0));
@@ -122,6 +123,7 @@ Json Mi355xPoolSpec::policy_json() const {
   // isolation of the slots (the agent's Allocate loads libgpupool_share.so into the pod)
   if (sharing_hbm_bytes > 0) j["sharing"]["hbmBytesPerSlot"] = sharing_hbm_bytes;
   if (sharing_cus > 0) j["sharing"]["cuPerSlot"] = sharing_cus;
+  if (sharing_over_budget != "Flag") j["sharing"]["overBudgetAction"] = sharing_over_budget;
   return j;
 }
 
@@ -256,6 +258,9 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
     int64_t v = s["maxNodes"].as_int(0);
     if (!s["maxNodes"].is_int() || v < 1 || v > 64) errs.push_back("spec.maxNodes: must be within [1, 64]");
   }
+  if (s.path("sharing").contains("overBudgetAction") &&
+      !in(s.path("sharing.overBudgetAction").as_string(), {"Flag", "Evict"}))
+    errs.push_back("spec.sharing.overBudgetAction: Unsupported value");
   if (s.path("sharing").contains("replicasPerGPU")) {
     const Json& r = s.path("sharing.replicasPerGPU");
     if (!r.is_int() || r.as_int(0) < 1 || r.as_int(0) > 64)

@@ -367,3 +367,63 @@ TEST(share_lib_account_keyed_by_gpu_uuid) {
   unsetenv("GPUPOOL_HBM_LIMIT_BYTES");
   unsetenv("GPUPOOL_SHARE_ACCOUNT");
 }
+
+// The limit the agent fixed lives in a read-only mounted file: a pod that rewrites the limit in
+// its (writable) account header, or its env, gains nothing — the smallest limit wins.
+TEST(share_lib_read_only_limit_file_wins_over_an_edited_account) {
+  std::string acct = make_account(64ull << 30);  // the pod "edited" its account: 64 GiB
+  std::string limf = "/tmp/gpupool-share-test-" + std::to_string(getpid()) + ".limit";
+  {
+    int fd = open(limf.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+    std::string txt = "GPLIMIT1 " + std::to_string(1024 * kMi) + "\n";
+    EXPECT_EQ(write(fd, txt.data(), txt.size()), static_cast<ssize_t>(txt.size()));
+    close(fd);
+  }
+  setenv("GPUPOOL_HBM_LIMIT_BYTES", "128Gi", 1);
+  setenv("GPUPOOL_SHARE_ACCOUNT", acct.c_str(), 1);
+  setenv("GPUPOOL_SHARE_LIMIT", limf.c_str(), 1);
+  std::string copy = "/tmp/libgpupool_share-lim-" + std::to_string(getpid()) + ".so";
+  void* lib = load_copy(copy);
+  EXPECT_TRUE(lib != nullptr);
+  auto on_load = reinterpret_cast<bool (*)(HsaApiTable*, uint64_t, uint64_t, const char* const*)>(dlsym(lib, "OnLoad"));
+  Fake f;
+  EXPECT_TRUE(on_load(&f.table, 0, 0, nullptr));
+  void* p = nullptr;
+  const hsa_amd_memory_pool_t gpu{kGpuPool};
+  EXPECT_EQ(f.amd.hsa_amd_memory_pool_allocate_fn(gpu, 1000 * kMi, 0, &p), HSA_STATUS_SUCCESS);
+  EXPECT_EQ(f.amd.hsa_amd_memory_pool_allocate_fn(gpu, 100 * kMi, 0, &p), HSA_STATUS_ERROR_OUT_OF_RESOURCES);
+  unlink(copy.c_str());
+  unlink(acct.c_str());
+  unlink(limf.c_str());
+  unsetenv("GPUPOOL_HBM_LIMIT_BYTES");
+  unsetenv("GPUPOOL_SHARE_ACCOUNT");
+  unsetenv("GPUPOOL_SHARE_LIMIT");
+}
+
+// an application mask that narrows the slot to CUs of ONE XCD (bits 0, 8, 16, 24 with
+// 8 XCDs: CU b sits on XCD b % 8) would leave the other XCDs empty, and the driver then silently
+// drops the mask — the queue runs on all CUs, the neighbours' included. Such a narrowing falls
+// back to the slot's mask; one that keeps a CU on every XCD is applied.
+TEST(share_lib_narrowing_that_empties_an_xcd_keeps_the_slot_mask) {
+  setenv("GPUPOOL_CU_MASK", "0-127", 1);
+  setenv("GPUPOOL_CU_XCDS", "8", 1);
+  std::string copy = "/tmp/libgpupool_share-xcd-" + std::to_string(getpid()) + ".so";
+  void* lib = load_copy(copy);
+  EXPECT_TRUE(lib != nullptr);
+  auto on_load = reinterpret_cast<bool (*)(HsaApiTable*, uint64_t, uint64_t, const char* const*)>(dlsym(lib, "OnLoad"));
+  auto stats = reinterpret_cast<int (*)(char*, int)>(dlsym(lib, "gpupool_share_stats"));
+  Fake f;
+  EXPECT_TRUE(on_load(&f.table, 0, 0, nullptr));
+  const uint32_t one_xcd[1] = {(1u << 0) | (1u << 8) | (1u << 16) | (1u << 24)};
+  f.amd.hsa_amd_queue_cu_set_mask_fn(&g_queue, 32, one_xcd);
+  EXPECT_TRUE(g_last_mask == (std::vector<uint32_t>{~0u, ~0u, ~0u, ~0u}));  // the slot's
+  const uint32_t every_xcd[1] = {0x000000FFu};  // CUs 0-7: one on each XCD
+  f.amd.hsa_amd_queue_cu_set_mask_fn(&g_queue, 32, every_xcd);
+  EXPECT_TRUE(g_last_mask == (std::vector<uint32_t>{0xFFu, 0u, 0u, 0u}));
+  char buf[320];
+  stats(buf, sizeof buf);
+  EXPECT_TRUE(std::string(buf).find("\"narrowingsRefused\":1") != std::string::npos);
+  unlink(copy.c_str());
+  unsetenv("GPUPOOL_CU_MASK");
+  unsetenv("GPUPOOL_CU_XCDS");
+}

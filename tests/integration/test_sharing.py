@@ -370,3 +370,75 @@ def test_pod_over_its_slot_budget_is_reported(cluster_factory):
     time.sleep(0.5)  # still over: no second event for the same pod and GPU
     assert len([e for e in k.list(EVENTS, "default")["items"]
                 if e["reason"] == "SlotBudgetExceeded"]) == 1
+
+
+def test_over_budget_pod_is_evicted_when_the_pool_says_so(cluster_factory):
+    """spec.sharing.overBudgetAction Evict (VERDICT r4 missing #4; HAMi enforces its limit per
+    container, GPU调度平台搭建.md:289-298): the pod holding 20 GiB against its 8 GiB slot — its
+    in-pod limit is not in force — is evicted through the API after two consecutive over-budget
+    samples, with a SlotBudgetExceeded event on the pod; its sibling within budget keeps
+    running."""
+    import time
+    from gpupool.kube import EVENTS
+    c = cluster_factory()
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("bud", 1, sharing={"replicasPerGPU": 2, "hbmBytesPerSlot": 8 << 30,
+                                                     "overBudgetAction": "Evict"}), "default")
+    gpu = wait_ready(k, "bud", 1)["status"]["devices"][0]
+    pids = {}
+    for name in ("ok", "rogue"):
+        k.create(PODS, pause_pod(name), "default")
+        p = k.wait_for(PODS, name, "default", lambda p: running(p) and "gpupool.amd.com/pid" in
+                       p["metadata"].get("annotations", {}), timeout=30)
+        pids[name] = int(p["metadata"]["annotations"]["gpupool.amd.com/pid"])
+    deadline = time.monotonic() + 10
+    while time.monotonic() < deadline:
+        view = c.agent_request("mi355x-node-0", "GET", "/v1/node")
+        if len(next(d for d in view["devices"] if d["uuid"] == gpu["uuid"])["pods"]) == 2:
+            break
+        time.sleep(0.1)
+    procs = {"devices": {str(gpu["index"]): {"processes": [
+        {"pid": pids["ok"], "vramBytes": 6 << 30, "gfxNs": 0},
+        {"pid": pids["rogue"], "vramBytes": 20 << 30, "gfxNs": 0}]}}}
+    c.set_faults("mi355x-node-0", procs, sample=True)  # the periodic samples follow (0.5 s)
+    k.wait_for(PODS, "rogue", "default", lambda o: o is None, timeout=30)
+    assert running(k.get(PODS, "ok", "default"))
+    deadline = time.monotonic() + 10
+    evs = []
+    while time.monotonic() < deadline and not evs:
+        evs = [e for e in k.list(EVENTS, "default")["items"]
+               if e["reason"] == "SlotBudgetExceeded" and e["involvedObject"]["kind"] == "Pod"]
+        time.sleep(0.1)
+    assert len(evs) == 1 and evs[0]["involvedObject"]["name"] == "rogue", evs
+    assert "evicted" in evs[0]["message"] and "overBudgetAction Evict" in evs[0]["message"]
+    assert "for 2+ samples" in evs[0]["message"]  # never on one reading
+    assert "gpupool_agent_over_budget_evictions 1" in str(c.agent_request("mi355x-node-0", "GET",
+                                                                            "/metrics"))
+
+
+def test_limit_file_is_mounted_read_only_beside_the_account(cluster_factory, tmp_path):
+    """The account a pod's processes charge is writable; the limit the agent fixed is a separate
+    read-only file (GPLIMIT1 <bytes>, mode 0644, mounted read_only) the share library takes the
+    smallest limit from: editing the account's header gains a pod nothing
+    (native/tests/test_share.cc has the library side)."""
+    import os
+    import time
+    c = cluster_factory()
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("lim", 1, sharing={"replicasPerGPU": 2,
+                                                     "hbmBytesPerSlot": 8 << 30}), "default")
+    wait_ready(k, "lim", 1)
+    pod = pause_pod("p0")
+    pod["spec"]["containers"][0]["command"] = [
+        "bash", "-c", "env | grep -E '^GPUPOOL_SHARE_(LIMIT|ACCOUNT)=' | sort; sleep 600"]
+    k.create(PODS, pod, "default")
+    p = k.wait_for(PODS, "p0", "default", running, timeout=30)
+    path = p["metadata"]["annotations"]["gpupool.amd.com/log-path"]
+    deadline = time.monotonic() + 10
+    while time.monotonic() < deadline and open(path).read().count("\n") < 2:
+        time.sleep(0.05)
+    env = dict(line.split("=", 1) for line in open(path).read().split())
+    lim, acct = env["GPUPOOL_SHARE_LIMIT"], env["GPUPOOL_SHARE_ACCOUNT"]
+    assert lim == acct[:-len(".acct")] + ".limit"
+    assert open(lim).read() == f"GPLIMIT1 {8 << 30}\n"
+    assert oct(os.stat(lim).st_mode & 0o777) == "0o644"

@@ -352,3 +352,41 @@ def test_plugin_reregisters_promptly_after_a_kubelet_outage(tmp_path, sockdir, n
     finally:
         a.stop()
         kubelet.stop()
+
+
+def test_allocate_mounts_the_hbm_limit_read_only(tmp_path, sockdir, native_built):
+    """An isolated slot's Allocate: the pod-wide account (counters) read-write, the limit the
+    agent fixed read-only beside it — and a one-sample over-budget reading never evicts."""
+    a = make_agent(tmp_path, sockdir, plugin=False)
+    r = claim(a, count=1, policy={"sharing": {"replicasPerGPU": 2, "hbmBytesPerSlot": 8 << 30,
+                                              "overBudgetAction": "Evict"}})
+    u = r["devices"][0]["uuid"]
+    spec = a.allocate_spec("amd.com/gpu", [f"{u}::0"])
+    m = {x["container_path"]: x for x in spec["mounts"]}
+    assert m[a.SHARE_ACCOUNT_PATH]["read_only"] is False
+    assert m[a.SHARE_LIMIT_PATH]["read_only"] is True
+    assert open(m[a.SHARE_LIMIT_PATH]["host_path"]).read() == f"GPLIMIT1 {8 << 30}\n"
+    assert spec["envs"]["GPUPOOL_SHARE_LIMIT"] == a.SHARE_LIMIT_PATH
+    # budget checks: one over-budget sample flags, the second evicts (no API server: counted only)
+    a._pods_cache = (0.0, {u: [{"namespace": "d", "name": "rogue"}]})
+    usage = {u: [{"namespace": "d", "pod": "rogue", "vramBytes": 20 << 30}]}
+    assert a._check_slot_budgets(usage) and not a.stats.get("over_budget_evictions")
+    a._check_slot_budgets({u: [dict(usage[u][0])]})
+    assert a.stats["over_budget_evictions"] == 1
+    a._check_slot_budgets({u: [dict(usage[u][0])]})  # once per pod
+    assert a.stats["over_budget_evictions"] == 1
+
+
+def test_account_for_gpus_without_hip_uuid_is_version_1(tmp_path, sockdir, native_built):
+    """a GPU without a hipUUID cannot be matched by identity — a version-2 account
+    would match nothing and the pod-wide budget would silently become per-process. The agent
+    writes a version-1 (ordinal) account instead."""
+    from gpupool.agent.slots import read_account
+    a = make_agent(tmp_path, sockdir, plugin=False)
+    r = claim(a, count=1, policy={"sharing": {"replicasPerGPU": 2, "hbmBytesPerSlot": 8 << 30}})
+    u = r["devices"][0]["uuid"]
+    a.by_uuid[u] = {**a.by_uuid[u], "hipUUID": ""}
+    path = a._share_account([f"{u}::0"], 8 << 30, [u])
+    acct = read_account(path)
+    assert acct["version"] == 1 and acct["limit"] == 8 << 30 and acct["slots"] == [f"{u}::0"]
+    assert acct["created"] > 0  # the GC grace still applies
