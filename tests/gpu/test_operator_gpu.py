@@ -481,3 +481,41 @@ def test_hung_probe_on_the_real_gpu_is_cut_at_its_deadline(cluster_factory):
         time.sleep(0.2)
         view = c.agent_request("gpu-node", "GET", "/v1/node")
     assert view["probeHelpers"][uuid]["alive"], view["probeHelpers"]
+
+
+def test_pod_that_escapes_its_hbm_limit_is_evicted_on_the_real_gpu(cluster_factory):
+    """spec.sharing.overBudgetAction Evict on hardware: a pod that drops the share library
+    (``env -u HSA_TOOLS_LIB``) and allocates 12 GiB against its 8 GiB slot is seen from outside
+    (amdsmi process list -> pod) and evicted within 3 samples; its sibling, within budget through
+    the library, keeps running."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
+    k = c.client
+    k.create(MI355XPOOLS, pool("iso", 1, sharing={"replicasPerGPU": 2, "hbmBytesPerSlot": 8 << 30,
+                                                  "overBudgetAction": "Evict"}), "default")
+    k.wait_for(MI355XPOOLS, "iso", "default", ready_at(1), timeout=60)
+    hold = ("import sys, time, torch\n"
+            "a = torch.ones(int(sys.argv[1]), dtype=torch.uint8, device='cuda')\n"
+            "torch.cuda.synchronize(); print('HOLDING', flush=True); time.sleep(120)\n")
+    specs = {"ok": ["python", "-c", hold, str(2 << 30)],
+             "rogue": ["env", "-u", "HSA_TOOLS_LIB", "python", "-c", hold, str(12 << 30)]}
+    for name, cmd in specs.items():
+        k.create(PODS, {"metadata": {"name": name}, "spec": {
+            "restartPolicy": "Never", "terminationGracePeriodSeconds": 2,
+            "containers": [{"name": "c", "command": cmd,
+                            "resources": {"limits": {"amd.com/gpu": 1}}}]}}, "default")
+    held = {}
+    deadline = time.monotonic() + 90
+    while len(held) < 2 and time.monotonic() < deadline:
+        for name in specs:
+            p = k.get(PODS, name, "default")
+            path = (p or {}).get("metadata", {}).get("annotations", {}).get("gpupool.amd.com/log-path")
+            if name not in held and path and os.path.exists(path) and "HOLDING" in open(path).read():
+                held[name] = time.monotonic()
+        time.sleep(0.1)
+    assert set(held) == {"ok", "rogue"}, held
+    k.wait_for(PODS, "rogue", "default", lambda o: o is None, timeout=60)
+    dt = time.monotonic() - held["rogue"]
+    print(f"rogue evicted {dt:.2f} s after it held 12 GiB (sample period {c.sample_interval} s)")
+    assert dt < 3 * c.sample_interval + 5.0, dt  # 3 samples + the pod's termination grace
+    assert k.get(PODS, "ok", "default")["status"]["phase"] == "Running"
+    k.delete(PODS, "ok", "default", grace=0)
