@@ -1994,13 +1994,18 @@ class Agent:
             u, _, i = sid.partition(SLOT_SEP)
             per_gpu.setdefault(u, []).append(int(i or 0))
         hbm, cu_mask = 0, set()
+        per_gpu_mask: dict[str, set[int]] = {}  # hipUUID -> the CUs of this pod's slots there
         for u, idx in per_gpu.items():
             lay = self._slot_layout(u, self.records.get(u) or {})
             if lay.get("hbmBytesPerSlot"):
                 hbm = max(hbm, lay["hbmBytesPerSlot"] * len(idx))
             if "masks" in lay:
+                hip = (self.by_uuid.get(u) or {}).get("hipUUID") or ""
                 for i in idx:
-                    cu_mask.update(lay["masks"][i % len(lay["masks"])])
+                    bits = lay["masks"][i % len(lay["masks"])]
+                    cu_mask.update(bits)
+                    if hip:
+                        per_gpu_mask.setdefault(hip, set()).update(bits)
         if not hbm and not cu_mask:
             return {}
         if not self.share_lib_dir:
@@ -2016,8 +2021,14 @@ class Agent:
         if hbm:  # allocate_spec adds the pod-wide account file (GPUPOOL_SHARE_ACCOUNT)
             env["GPUPOOL_HBM_LIMIT_BYTES"] = str(hbm)
         if cu_mask:
+            # each GPU's own slot CUs, keyed by the UUID the library reads from the queue's agent: a
+            # pod holding slot 0 of GPU A and slot 1 of GPU B must not get the union on both (it
+            # overlaps the sibling tenants); the union stays as the fallback for a GPU not named
             env["GPUPOOL_CU_MASK"] = _ranges(sorted(cu_mask))
             env["GPUPOOL_CU_LAYOUT"] = "striped"
+            if per_gpu_mask:
+                env["GPUPOOL_CU_MASKS"] = ";".join(f"{h}={_ranges(sorted(b))}"
+                                                   for h, b in sorted(per_gpu_mask.items()))
         return env
 
     # ================================================================ leader fencing

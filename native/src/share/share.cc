@@ -165,14 +165,34 @@ bool map_take(AllocMap& m, uint64_t raw, Alloc* out) {
   }
 }
 
+// A CU mask: bit words, the words in use (0 = no mask) and the bit count handed to ROCr.
+struct CuMask {
+  uint32_t w[kMaskWords];
+  uint32_t words, bits;
+};
+// Per-GPU masks (GPUPOOL_CU_MASKS): a pod holding slot 0 of GPU A and slot 1 of GPU B gets each
+// GPU's own slot CUs — the pod-wide union (GPUPOOL_CU_MASK) would overlap the sibling tenants'
+// slots on both. Matched by the queue's agent UUID.
+constexpr int kGpuMasks = 8;
+struct GpuMask {
+  char uuid[32];
+  CuMask m;
+};
+constexpr int kQueueMap = 256;  // queue -> the mask it got (for the application's narrowing)
+struct QueueMask {
+  const hsa_queue_t* q;
+  const CuMask* m;
+};
+
 struct State {
   pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
   CoreApiTable real_core;
   AmdExtTable real_amd;
   uint64_t limit;                   // bytes per GPU; 0 = no budget
-  uint32_t mask[kMaskWords];        // CU mask words
-  uint32_t mask_words;              // 0 = no mask
-  uint32_t mask_bits;
+  CuMask mask;                      // the pod-wide mask (GPUPOOL_CU_MASK): GPUs without their own
+  GpuMask gpu_masks[kGpuMasks];
+  int n_gpu_masks;
+  QueueMask qmap[kQueueMap];
   uint32_t xcds;  // XCDs of the GPU (GPUPOOL_CU_XCDS): a narrowed mask must keep a CU on each
   bool debug;
   bool pools_mapped;
@@ -352,14 +372,14 @@ uint64_t parse_bytes(const char* v) {
   return static_cast<uint64_t>(x * mul);
 }
 
-// "0-63,128-159" -> bit words (32 bits each) in s.mask; bits counted up to the highest set bit,
-// rounded up to a multiple of 32 as hsa_amd_queue_cu_set_mask requires.
-void parse_mask(State& s, const char* v) {
-  s.mask_words = 0;
-  s.mask_bits = 0;
-  if (!v || !*v) return;
+// "0-63,128-159" -> bit words (32 bits each); bits counted up to the highest set bit, rounded up
+// to a multiple of 32 as hsa_amd_queue_cu_set_mask requires. Parsing stops at ';' or the end.
+const char* parse_mask(CuMask& m, const char* v) {
+  m.words = 0;
+  m.bits = 0;
+  if (!v || !*v) return v;
   const char* p = v;
-  while (*p) {
+  while (*p && *p != ';') {
     char* end = nullptr;
     long lo = strtol(p, &end, 10);
     bool ok = end != p;
@@ -371,16 +391,49 @@ void parse_mask(State& s, const char* v) {
       ok = end != q;
       p = end;
     }
-    while (*p && *p != ',') ++p;  // skip to the next range (malformed tails are ignored)
+    while (*p && *p != ',' && *p != ';') ++p;  // skip to the next range (malformed tails are ignored)
     if (*p == ',') ++p;
     if (!ok || lo < 0 || hi < lo || hi >= kMaskWords * 32) continue;
     for (long b = lo; b <= hi; ++b) {
       const uint32_t w = static_cast<uint32_t>(b) / 32;
-      s.mask[w] |= 1u << (b % 32);
-      if (w + 1 > s.mask_words) s.mask_words = w + 1;
+      m.w[w] |= 1u << (b % 32);
+      if (w + 1 > m.words) m.words = w + 1;
     }
   }
-  s.mask_bits = s.mask_words * 32;
+  m.bits = m.words * 32;
+  return p;
+}
+
+// "GPU-aaaa=0-63,128-159;GPU-bbbb=64-127" -> s.gpu_masks
+void parse_gpu_masks(State& s, const char* v) {
+  s.n_gpu_masks = 0;
+  const char* p = v;
+  while (p && *p && s.n_gpu_masks < kGpuMasks) {
+    const char* eq = strchr(p, '=');
+    if (!eq) break;
+    GpuMask& g = s.gpu_masks[s.n_gpu_masks];
+    size_t n = static_cast<size_t>(eq - p);
+    if (n == 0 || n >= sizeof g.uuid) break;
+    memcpy(g.uuid, p, n);
+    g.uuid[n] = 0;
+    p = parse_mask(g.m, eq + 1);
+    if (g.m.words) ++s.n_gpu_masks;
+    if (p && *p == ';') ++p;
+  }
+}
+
+// The mask a queue on ``agent`` gets: its GPU's own (by UUID), else the pod-wide one, else none.
+const CuMask* mask_for(State& s, hsa_agent_t agent) {
+  if (s.n_gpu_masks) {
+    char uuid[64] = {};
+    if (s.real_core.hsa_agent_get_info_fn(agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_UUID), uuid) ==
+        HSA_STATUS_SUCCESS) {
+      uuid[sizeof uuid - 1] = 0;
+      for (int i = 0; i < s.n_gpu_masks; ++i)
+        if (strcmp(s.gpu_masks[i].uuid, uuid) == 0) return &s.gpu_masks[i].m;
+    }
+  }
+  return s.mask.words ? &s.mask : nullptr;
 }
 
 AgentRec* agent_rec(State& s, uint64_t handle) {
@@ -591,26 +644,46 @@ hsa_status_t w_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t
   State& s = st();
   hsa_status_t r = s.real_core.hsa_queue_create_fn(agent, size, type, callback, data, private_segment_size,
                                                    group_segment_size, queue);
-  if (r == HSA_STATUS_SUCCESS && queue && *queue && s.mask_words && is_gpu(agent)) {
-    hsa_status_t m = s.real_amd.hsa_amd_queue_cu_set_mask_fn(*queue, s.mask_bits, s.mask);
-    if (m == HSA_STATUS_SUCCESS || static_cast<int>(m) == static_cast<int>(HSA_STATUS_CU_MASK_REDUCED))
-      count(&s.queues_masked);
-    if (s.debug)
-      fprintf(stderr, "[gpupool-share] queue %p CU mask (%u bits): status %d\n", static_cast<void*>(*queue), s.mask_bits,
-              static_cast<int>(m));
+  if (r != HSA_STATUS_SUCCESS || !queue || !*queue || !is_gpu(agent)) return r;
+  const CuMask* cm = mask_for(s, agent);
+  if (!cm) return r;
+  {
+    Lock g(s);  // remember the queue's mask: the application may narrow it later
+    int free_at = -1;
+    for (int i = 0; i < kQueueMap; ++i) {
+      if (s.qmap[i].q == *queue) {
+        free_at = i;
+        break;
+      }
+      if (free_at < 0 && !s.qmap[i].q) free_at = i;
+    }
+    if (free_at >= 0) s.qmap[free_at] = QueueMask{*queue, cm};
   }
+  hsa_status_t m = s.real_amd.hsa_amd_queue_cu_set_mask_fn(*queue, cm->bits, cm->w);
+  if (m == HSA_STATUS_SUCCESS || static_cast<int>(m) == static_cast<int>(HSA_STATUS_CU_MASK_REDUCED))
+    count(&s.queues_masked);
+  if (s.debug)
+    fprintf(stderr, "[gpupool-share] queue %p CU mask (%u bits): status %d\n", static_cast<void*>(*queue), cm->bits,
+            static_cast<int>(m));
   return r;
+}
+
+const CuMask* queue_mask(State& s, const hsa_queue_t* q) {
+  Lock g(s);
+  for (int i = 0; i < kQueueMap; ++i)
+    if (s.qmap[i].q == q) return s.qmap[i].m;
+  return s.mask.words ? &s.mask : nullptr;
 }
 
 // Does ``m`` leave at least one CU on every XCD? CU-mask bit b lands on XCD b % xcds (ROCr
 // interleaves CUs over the XCDs), and a mask that leaves any XCD without CUs is silently NOT
 // applied by the driver (measured, profiles/r4b_cu_mask_layouts.txt): the queue would then run
 // on all 256 CUs, its slot neighbours' included.
-bool covers_every_xcd(const State& s, const uint32_t* m) {
+bool covers_every_xcd(const State& s, const uint32_t* m, uint32_t words) {
   if (s.xcds <= 1) return true;
   uint32_t seen = 0;  // one bit per XCD (at most 32)
   const uint32_t want = s.xcds >= 32 ? ~0u : (1u << s.xcds) - 1;
-  for (uint32_t w = 0; w < s.mask_words && seen != want; ++w)
+  for (uint32_t w = 0; w < words && seen != want; ++w)
     for (uint32_t b = 0; b < 32 && m[w] >> b; ++b)
       if (m[w] >> b & 1u) seen |= 1u << ((w * 32 + b) % s.xcds % 32);
   return (seen & want) == want;
@@ -619,21 +692,22 @@ bool covers_every_xcd(const State& s, const uint32_t* m) {
 hsa_status_t w_queue_cu_set_mask(const hsa_queue_t* queue, uint32_t bits, const uint32_t* mask) {
   // the application's own mask (hipExtStreamCreateWithCUMask) can only narrow the slot's
   State& s = st();
-  if (!s.mask_words) return s.real_amd.hsa_amd_queue_cu_set_mask_fn(queue, bits, mask);
+  const CuMask* cm = queue_mask(s, queue);
+  if (!cm) return s.real_amd.hsa_amd_queue_cu_set_mask_fn(queue, bits, mask);
   uint32_t m[kMaskWords];
   bool any = false;
-  for (uint32_t i = 0; i < s.mask_words; ++i) {
-    m[i] = s.mask[i];
+  for (uint32_t i = 0; i < cm->words; ++i) {
+    m[i] = cm->w[i];
     if (bits > 0 && mask) m[i] &= i < bits / 32 ? mask[i] : 0u;
     any = any || m[i];
   }
   // nothing left, or a narrowing that empties an XCD (the driver would then drop the mask and run
   // the queue on every CU): the slot's own mask
-  if (bits > 0 && mask && (!any || !covers_every_xcd(s, m))) {
-    for (uint32_t i = 0; i < s.mask_words; ++i) m[i] = s.mask[i];
+  if (bits > 0 && mask && (!any || !covers_every_xcd(s, m, cm->words))) {
+    for (uint32_t i = 0; i < cm->words; ++i) m[i] = cm->w[i];
     count(&s.narrowings_refused);
   }
-  return s.real_amd.hsa_amd_queue_cu_set_mask_fn(queue, s.mask_bits, m);
+  return s.real_amd.hsa_amd_queue_cu_set_mask_fn(queue, cm->bits, m);
 }
 
 }  // namespace
@@ -648,7 +722,8 @@ __attribute__((visibility("default"))) bool OnLoad(HsaApiTable* table, uint64_t 
   Lock g(s);
   s.real_core = *table->core_;
   s.real_amd = *table->amd_ext_;
-  parse_mask(s, getenv("GPUPOOL_CU_MASK"));
+  parse_mask(s.mask, getenv("GPUPOOL_CU_MASK"));
+  parse_gpu_masks(s, getenv("GPUPOOL_CU_MASKS"));
   const char* xcds = getenv("GPUPOOL_CU_XCDS");
   s.xcds = xcds && *xcds ? static_cast<uint32_t>(strtoul(xcds, nullptr, 10)) : 0;
   const char* dbg = getenv("GPUPOOL_SHARE_DEBUG");
@@ -668,13 +743,13 @@ __attribute__((visibility("default"))) bool OnLoad(HsaApiTable* table, uint64_t 
     table->amd_ext_->hsa_amd_memory_pool_get_info_fn = w_pool_get_info;
     table->core_->hsa_agent_get_info_fn = w_agent_get_info;
   }
-  if (s.mask_words) {
+  if (s.mask.words || s.n_gpu_masks) {
     table->core_->hsa_queue_create_fn = w_queue_create;
     table->amd_ext_->hsa_amd_queue_cu_set_mask_fn = w_queue_cu_set_mask;
   }
   if (s.debug)
     fprintf(stderr, "[gpupool-share] loaded: HBM limit %llu B per GPU (%s), CU mask %u bits\n",
-            static_cast<unsigned long long>(s.limit), s.acct ? "pod total" : "per process", s.mask_bits);
+            static_cast<unsigned long long>(s.limit), s.acct ? "pod total" : "per process", s.mask.bits);
   return true;
 }
 
@@ -699,7 +774,7 @@ __attribute__((visibility("default"))) int gpupool_share_stats(char* buf, int le
                   "\"narrowingsRefused\":%llu}",
                   static_cast<unsigned long long>(s.limit), static_cast<unsigned long long>(used),
                   static_cast<unsigned long long>(load(&s.peak)), static_cast<unsigned long long>(load(&s.denied)),
-                  static_cast<unsigned long long>(load(&s.queues_masked)), s.mask_bits, s.acct ? 1 : 0,
+                  static_cast<unsigned long long>(load(&s.queues_masked)), s.mask.bits, s.acct ? 1 : 0,
                   static_cast<unsigned long long>(shared), static_cast<unsigned long long>(load(&s.reclaimed)),
                   static_cast<unsigned long long>(load(&s.narrowings_refused)));
 }

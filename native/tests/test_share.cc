@@ -427,3 +427,44 @@ TEST(share_lib_narrowing_that_empties_an_xcd_keeps_the_slot_mask) {
   unsetenv("GPUPOOL_CU_MASK");
   unsetenv("GPUPOOL_CU_XCDS");
 }
+
+// a pod holding slot 0 on GPU A and slot 1 on GPU B must get slot 0's CUs on A and slot
+// 1's on B — not their union on both (which overlaps the sibling tenants). GPUPOOL_CU_MASKS keys
+// the masks by the GPU's UUID; a GPU it does not name falls back to GPUPOOL_CU_MASK.
+TEST(share_lib_cu_masks_per_gpu_by_uuid) {
+  setenv("GPUPOOL_CU_MASKS", "GPU-aaaa000000000001=0-63;GPU-bbbb000000000002=64-127", 1);
+  setenv("GPUPOOL_CU_XCDS", "8", 1);
+  g_gpus = {kGpu, kGpu2};
+  std::string copy = "/tmp/libgpupool_share-pergpu-" + std::to_string(getpid()) + ".so";
+  void* lib = load_copy(copy);
+  EXPECT_TRUE(lib != nullptr);
+  auto on_load = reinterpret_cast<bool (*)(HsaApiTable*, uint64_t, uint64_t, const char* const*)>(dlsym(lib, "OnLoad"));
+  Fake f;
+  EXPECT_TRUE(on_load(&f.table, 0, 0, nullptr));
+  hsa_queue_t* q = nullptr;
+  static hsa_queue_t q2;
+  EXPECT_EQ(f.core.hsa_queue_create_fn(hsa_agent_t{kGpu}, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &q),
+            HSA_STATUS_SUCCESS);
+  EXPECT_TRUE(g_last_mask == (std::vector<uint32_t>{~0u, ~0u}));  // A: 0-63
+  // the fake returns the same queue object for every create: give GPU B's queue its own address
+  auto make_b = [](hsa_agent_t, uint32_t, hsa_queue_type32_t, void (*)(hsa_status_t, hsa_queue_t*, void*), void*,
+                   uint32_t, uint32_t, hsa_queue_t** out) {
+    *out = &q2;
+    return HSA_STATUS_SUCCESS;
+  };
+  Fake f2;  // a fresh dispatch table (re-wrapping the wrapped one would recurse)
+  f2.core.hsa_queue_create_fn = make_b;
+  EXPECT_TRUE(on_load(&f2.table, 0, 0, nullptr));
+  EXPECT_EQ(f2.core.hsa_queue_create_fn(hsa_agent_t{kGpu2}, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &q),
+            HSA_STATUS_SUCCESS);
+  EXPECT_TRUE(q == &q2);
+  EXPECT_TRUE(g_last_mask == (std::vector<uint32_t>{0u, 0u, ~0u, ~0u}));  // B: 64-127
+  // an application narrowing on B's queue intersects with B's mask, not A's
+  const uint32_t app[4] = {~0u, ~0u, 0x000000FFu, 0u};
+  f2.amd.hsa_amd_queue_cu_set_mask_fn(&q2, 128, app);
+  EXPECT_TRUE(g_last_mask == (std::vector<uint32_t>{0u, 0u, 0xFFu, 0u}));
+  g_gpus = {kGpu};
+  unlink(copy.c_str());
+  unsetenv("GPUPOOL_CU_MASKS");
+  unsetenv("GPUPOOL_CU_XCDS");
+}

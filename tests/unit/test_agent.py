@@ -390,3 +390,17 @@ def test_account_for_gpus_without_hip_uuid_is_version_1(tmp_path, sockdir, nativ
     acct = read_account(path)
     assert acct["version"] == 1 and acct["limit"] == 8 << 30 and acct["slots"] == [f"{u}::0"]
     assert acct["created"] > 0  # the GC grace still applies
+
+
+def test_cu_masks_are_per_gpu_for_a_pod_spanning_slots_of_two_gpus(tmp_path, sockdir, native_built):
+    """a pod holding slot 0 of GPU A and slot 1 of GPU B gets slot 0's CUs on A and slot
+    1's on B (GPUPOOL_CU_MASKS by HIP UUID), not their union on both."""
+    a = make_agent(tmp_path, sockdir, plugin=False)
+    r = claim(a, count=2, policy={"sharing": {"replicasPerGPU": 2, "cuPerSlot": 128}})
+    ua, ub = (d["uuid"] for d in sorted(r["devices"], key=lambda d: d["index"]))
+    env = a.allocate_spec("amd.com/gpu", [f"{ua}::0", f"{ub}::1"])["envs"]
+    ha, hb = a.by_uuid[ua]["hipUUID"], a.by_uuid[ub]["hipUUID"]
+    masks = dict(x.split("=") for x in env["GPUPOOL_CU_MASKS"].split(";"))
+    assert masks == {ha: "0-127", hb: "128-255"}, masks
+    assert env["GPUPOOL_CU_MASK"] == "0-255"  # the union: fallback for a GPU the library cannot name
+    assert env["GPUPOOL_CU_XCDS"] == "8"
