@@ -186,11 +186,12 @@ def _apply_hooks(a: dict) -> None:
 
 # run on the helper's main thread: short, and what a claim waits for; everything else gets a thread
 _INLINE_OPS = ("probe", "ping")
-# After any message the helper polls its pipe without sleeping for this long: a claim sends "wake"
-# as soon as it has chosen its GPUs, so the probe request that follows ~0.1-0.2 ms later is picked
-# up by a running thread instead of one the kernel must first wake (tens to hundreds of us when
-# the core idles in a deep C-state). Bounded: an idle helper costs no CPU.
-SPIN_S = float(os.environ.get("GPUPOOL_HELPER_SPIN_MS", "3")) / 1e3
+# After a "wake" the helper polls its pipe without sleeping for at most this long: a claim sends
+# "wake" as soon as it has chosen its GPUs, so the probe request that follows ~0.1-0.2 ms later is
+# picked up by a running thread instead of one the kernel must first wake (tens to hundreds of us
+# when the core idles in a deep C-state). Only after a wake, and bounded: an idle helper costs no
+# CPU, and none spins once its probe is answered.
+SPIN_S = float(os.environ.get("GPUPOOL_HELPER_SPIN_MS", "1")) / 1e3
 
 
 def child_main(conn, spec: dict) -> None:
@@ -244,8 +245,8 @@ def child_main(conn, spec: dict) -> None:
             os._exit(0)  # the agent is gone
         if msg.get("op") == "exit":
             os._exit(0)
-        spin_until = time.perf_counter() + spin_s
         if msg.get("op") == "wake":  # a request is on its way: just be awake for it
+            spin_until = time.perf_counter() + spin_s
             continue
         if msg.get("op") in _INLINE_OPS:
             run(msg)  # the claim path: no thread start between the pipe and the kernels
