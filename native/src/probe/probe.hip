@@ -1389,15 +1389,25 @@ struct ProbeActive {
   ~ProbeActive() { g_probes_active.fetch_sub(1); }
 };
 
-// Wait (bounded) until no claim-time probe runs in this process; dev -1: never wait (callers
-// holding a device lock).
-void yield_to_probes(int dev) {
+// Wait until no claim-time probe runs in this process; dev -1: never wait (callers holding a
+// device lock). Bounded twice: at most 2 s before one chunk, and at most ``budget`` (what is left of
+// the whole alloc / free call's 3 s) over all its chunks — ~282 chunks under steady claim traffic
+// must not turn a free into minutes while the pod's Allocate waits for it. In the agent's probe
+// helpers a process holds one GPU, so only probes of that GPU are waited for. Returns the seconds
+// spent waiting (the sweep trace reports them).
+double yield_to_probes(int dev, double* budget) {
   static const bool off = std::getenv("GPUPOOL_SWEEP_NO_YIELD") != nullptr;  // in-process A/B only
-  if (dev < 0 || off) return;
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+  if (dev < 0 || off || !budget || *budget <= 0) return 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto deadline = t0 + std::chrono::duration<double>(std::min(2.0, *budget));
   while (g_probes_active.load() > 0 && std::chrono::steady_clock::now() < deadline)
     std::this_thread::sleep_for(std::chrono::microseconds(200));
+  const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  *budget -= waited;
+  return waited;
 }
+
+constexpr double kYieldBudgetS = 3.0;  // per sweep-buffer alloc / free call, over all its chunks
 
 SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
   size_t free_b = 0, total_b = 0;
@@ -1406,9 +1416,11 @@ SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
   if (free_b <= reserve + gran) throw ProbeError("not enough free HBM for a sweep window");
   SweepBuf b;
   const uint64_t span = ((free_b - reserve) / gran) * gran;
+  double budget = kYieldBudgetS, yielded = 0;
+  static const bool trace = std::getenv("GPUPOOL_SWEEP_TRACE") != nullptr;  // chunk timings
   for (uint64_t at = 0; at < span; at += kSweepChunk) {
     void* p = nullptr;
-    yield_to_probes(yield_dev);
+    yielded += yield_to_probes(yield_dev, &budget);
     const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipMalloc(&p, std::min<uint64_t>(kSweepChunk, span - at));
     if (e != hipSuccess) {
@@ -1418,18 +1430,21 @@ SweepBuf sweep_alloc_raw(uint64_t reserve, int yield_dev = -1) {
     }
     b.chunks.push_back(p);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    static const bool trace = std::getenv("GPUPOOL_SWEEP_TRACE") != nullptr;        // chunk timings
     if (trace) std::fprintf(stderr, "sweep chunk %zu: %.3f ms\n", b.chunks.size() - 1, ms);
   }
+  if (trace) std::fprintf(stderr, "sweep alloc: %zu chunks, %.1f ms yielded to probes\n", b.chunks.size(), yielded * 1e3);
   b.span = span;
   return b;
 }
 
 void sweep_free(SweepBuf& b, int yield_dev = -1) {
+  double budget = kYieldBudgetS, yielded = 0;
   for (void* p : b.chunks) {  // one bounded unmap per chunk
-    yield_to_probes(yield_dev);
+    yielded += yield_to_probes(yield_dev, &budget);
     (void)hipFree(p);
   }
+  static const bool trace = std::getenv("GPUPOOL_SWEEP_TRACE") != nullptr;
+  if (trace) std::fprintf(stderr, "sweep free: %zu chunks, %.1f ms yielded to probes\n", b.chunks.size(), yielded * 1e3);
   b.chunks.clear();
   b.span = 0;
 }
