@@ -65,6 +65,9 @@ def main() -> None:
     ap.add_argument("--no-fsync", action="store_true")
     ap.add_argument("--probe-arena-idle", type=float, default=10.0,
                     help="seconds before the kept probe arena (~1.2 GiB/GPU) is freed")
+    ap.add_argument("--probe-fabric-idle", type=float, default=0.0,
+                    help="seconds before an idle xGMI fabric helper exits (0 = resident and "
+                         "pre-warmed at start, so multi-GPU claims never pay its HIP init)")
     ap.add_argument("--scrub-interval", type=float, default=60.0,
                     help="HBM scrubber pass period over idle GPUs, seconds (0 = off)")
     ap.add_argument("--scrub-window", type=int, default=4 << 30, help="bytes per scrub window")
@@ -115,6 +118,7 @@ def main() -> None:
                       sample_interval=a.sample_interval, health_interval=a.health_interval,
                       quarantine_s=a.quarantine,
                       fsync=not a.no_fsync, probe_arena_idle_s=a.probe_arena_idle,
+                      probe_fabric_idle_s=a.probe_fabric_idle,
                       scrub_interval_s=a.scrub_interval, scrub_window_bytes=a.scrub_window,
                       scrub_windows=a.scrub_windows, scrub_reserve_bytes=a.scrub_reserve,
                       scrub_start_delay_s=a.scrub_start_delay,

@@ -151,6 +151,9 @@ class AgentConfig:
     advertise_wait_s: float = 2.0
     fsync: bool = True
     probe_arena_idle_s: float = 10.0  # free the kept ~1.2 GiB probe arena after this idle time
+    # the xGMI fabric helper (contexts on every GPU): 0 keeps it resident, pre-warmed at start, so
+    # a multi-GPU claim never pays its HIP init; > 0 lets it go after that many idle seconds
+    probe_fabric_idle_s: float = 0.0
     scrub_interval_s: float = 60.0    # HBM scrubber pass period over idle GPUs (0 = off)
     scrub_window_bytes: int = 4 << 30
     scrub_windows: int = 8            # windows per device per pass
@@ -215,7 +218,9 @@ class Agent:
         self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n,
                              arena_idle_s=cfg.probe_arena_idle_s,
                              overlap_gemm_n=cfg.probe_overlap_gemm_n,
-                             devices=[d for d in self.snap["devices"] if d.get("present", True)])
+                             devices=[d for d in self.snap["devices"] if d.get("present", True)],
+                             fabric_idle_s=cfg.probe_fabric_idle_s,
+                             fabric_prewarm=cfg.probe_fabric_idle_s <= 0)
         self.last_probe: dict[str, dict] = {}
         # uuid -> monotonic time its VRAM was last freed wholesale (a release after its pods ended;
         # agent start: the previous agent process's allocations): the driver clears freed VRAM for
@@ -2219,6 +2224,8 @@ class Agent:
             if self.prober.helpers is not None:
                 lines.append(f"gpupool_agent_probe_helpers_rss_bytes {self.prober.helpers_rss_bytes()}")
                 lines.append(f"gpupool_agent_probe_helpers {len(self.prober.helper_pids())}")
+                if self.prober.fabric_warm_ms is not None:
+                    lines.append(f"gpupool_agent_probe_fabric_warm_ms {self.prober.fabric_warm_ms:.1f}")
                 for k, v in self.prober.helpers.stats.items():
                     lines.append(f"gpupool_agent_probe_{k}_total {v}")
                 for k, v in self.prober.helpers.snapshot().items():

@@ -11,8 +11,10 @@ left its pool waiting on a ``Probing`` GPU forever. Here:
   * one helper per GPU, started with ``ROCR_VISIBLE_DEVICES=<that GPU's UUID>``: it holds a HIP
     context on its GPU only, and a fault takes down that helper only — probes of the other GPUs go
     on in theirs;
-  * a *fabric* helper that sees all of the node's GPUs runs the xGMI peer ring; it is started on
-    demand and exits after ``fabric_idle_s`` without work (its contexts cost VRAM on every GPU);
+  * a *fabric* helper that sees all of the node's GPUs runs the xGMI peer ring; the agent starts
+    and warms it (one 1 MiB ring) at start on a multi-GPU node and keeps it resident, so no
+    multi-GPU claim pays its HIP init; with ``fabric_idle_s`` > 0 it exits after that long idle
+    instead and is started again on demand (its contexts cost VRAM on every GPU);
   * every request has a deadline (``spec.probe.timeoutSeconds`` for probes and rings): past it the
     helper is SIGKILLed and the request fails (``ProbeTimeout``); a helper that dies mid-request
     fails what it had in flight (``ProbeCrashed``); a fresh child replaces it, with a backoff while
@@ -571,7 +573,7 @@ class HelperPool:
     ``max_backoff_s``), so a GPU that kills every helper does not spin the node's CPUs."""
 
     def __init__(self, kind: str, sim_ms: float = 20.0, arena_idle_s: float = 10.0,
-                 fabric_idle_s: float = 120.0, ready_timeout: float = 120.0,
+                 fabric_idle_s: float = 0.0, ready_timeout: float = 120.0,
                  max_backoff_s: float = 60.0, crash_window_s: float = 300.0):
         self.kind = kind
         self.sim_ms = sim_ms

@@ -42,7 +42,8 @@ DEFAULT_TIMEOUT_S = 10.0  # spec.probe.timeoutSeconds default (schema.py)
 class Prober:
     def __init__(self, mode: str = "inproc", sim_ms: float = 20.0, gemm_n: int = 4096,
                  max_workers: int = 16, arena_idle_s: float = 10.0, overlap_gemm_n: int = 2048,
-                 devices: list[dict] | None = None, fabric_idle_s: float = 120.0):
+                 devices: list[dict] | None = None, fabric_idle_s: float = 0.0,
+                 fabric_prewarm: bool = True):
         self.mode = mode
         self.sim_ms = sim_ms
         self.gemm_n = gemm_n                  # serial probe (pools with performance floors)
@@ -54,6 +55,7 @@ class Prober:
         self.ordinals: dict[str, int] = {}
         self.helpers = None
         self.init_ms = 0.0
+        self.fabric_warm_ms = None
         t0 = time.perf_counter()
         if mode == "inproc":
             from ..ops import probe as hip_probe
@@ -76,6 +78,12 @@ class Prober:
             bad = {u: r.get("error") for u, r in ready.items() if not r.get("ok")}
             log.info("probe helpers up for %d/%d GPU(s)%s", len(up), len(ready),
                      f"; failed: {bad}" if bad else "")
+            fabric = [d for d in (devices or []) if d["uuid"] in up]
+            if fabric_prewarm and len(fabric) >= 2:
+                # the fabric helper's HIP init on every GPU (seconds on 8) and the ring's first
+                # peer-access enable + buffer allocation happen now, not inside a multi-GPU
+                # claim's deadline; it then stays resident (fabric_idle_s 0)
+                self.pool.submit(self._warm_fabric, fabric)
         elif mode == "subprocess":
             out = subprocess.run([native_path("mi355x-probe"), "--list"], capture_output=True,
                                  text=True, timeout=120)
@@ -304,6 +312,15 @@ class Prober:
             except Exception as e:  # never take the agent down
                 log.warning("xGMI peer check failed: %r", e)
         return out
+
+    def _warm_fabric(self, devs: list[dict]) -> None:
+        devs = sorted(devs, key=lambda d: d.get("index", 0))
+        t0 = time.perf_counter()
+        ring = self._ring_whole(devs, 1 << 20, 120.0) or {}
+        self.fabric_warm_ms = (time.perf_counter() - t0) * 1e3
+        bad = {u: r.get("error") for u, r in ring.items() if not r.get("passed")}
+        log.info("fabric helper warm over %d GPU(s) in %.0f ms%s", len(devs), self.fabric_warm_ms,
+                 f"; links not passing: {bad}" if bad else "")
 
     def _fabric_call(self, devs: list[dict], op: str, args: dict, timeout: float) -> dict:
         """A request to the fabric helper. Its failure says nothing about any one link, so it

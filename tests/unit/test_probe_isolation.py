@@ -57,11 +57,17 @@ def agents():
 def test_helpers_probe_and_the_agent_never_loads_the_probe_library(tmp_path, agents, native_built):
     a = make_agent(tmp_path)
     agents.append(a)
+    # one helper per GPU, plus the fabric helper the agent starts and warms on a multi-GPU node
+    assert wait(lambda: a.prober.helpers.alive("fabric") and a.prober.fabric_warm_ms is not None)
     pids = a.prober.helper_pids()
-    assert len(pids) == 4 and os.getpid() not in pids
+    assert len(pids) == 5 and os.getpid() not in pids
+    assert a.prober.hip_devices() == 0  # helper-sim: no HIP anywhere
+    starts = a.prober.helpers.stats["helper_starts"]
     r = claim(a, count=2)
     assert r["ok"] and all(d["probe"]["passed"] for d in r["devices"]), r
     assert all(d["probe"]["backend"] == "helper-sim" for d in r["devices"])
+    # the claim's xGMI ring ran in the resident fabric helper: nothing was started for it
+    assert a.prober.helpers.stats["helper_starts"] == starts
     # helpers' processes are the agent's own in per-pod accounting
     assert a._pod_of_pid(next(iter(pids))) == {"namespace": "", "pod": "gpupool-agent"}
     with open("/proc/self/maps") as f:
