@@ -60,10 +60,13 @@ def scenarios(tag_dir: str) -> dict[str, list[tuple]]:
         "bench-ab": [(f"bench_{m}_{i}", _bench("--steps", "40", "--warmup", "3", "--probe-mode", m),
                       240, {}) for i in (1, 2) for m in ("helper", "inproc")],
         "helper-ab": [("helper_ab", [PY, "scripts/helper_overhead_ab.py"], 300, {})],
-        # kernel timing over the headline bench (probe kernels run in the agent's helpers)
+        # kernel timing over the headline bench. The probe runs in-process here: a helper forked
+        # from the agent's forkserver under rocprofv3's preloaded tool never came up (r5d: the
+        # bench sat silent until the box's 180 s hang guard), and the kernels are the same ones
+        # (helper vs inproc bench A/B: profiles/r5c_bench_helper_vs_inproc_ab.json)
         "prof": [("bench_prof", _prof(tag_dir, "bench_prof", PY, os.path.join(ROOT, "bench.py"),
                                       "--gpus", "1", "--steps", "10", "--warmup", "2",
-                                      "--health-steps", "0"), 500, {})],
+                                      "--health-steps", "0", "--probe-mode", "inproc"), 400, {})],
         # counters of the probe GEMM (one pass: 4 TCC counters at most per run)
         "pmc": [(f"gemm_l2_g{g}", _prof(tag_dir, f"gemm_l2_g{g}", PY,
                                           os.path.join(ROOT, "scripts", "gemm_l2_pmc.py"), "8192",
