@@ -519,3 +519,32 @@ def test_pod_that_escapes_its_hbm_limit_is_evicted_on_the_real_gpu(cluster_facto
     assert dt < 3 * c.sample_interval + 5.0, dt  # 3 samples + the pod's termination grace
     assert k.get(PODS, "ok", "default")["status"]["phase"] == "Running"
     k.delete(PODS, "ok", "default", grace=0)
+
+
+def test_fabric_helper_rings_on_the_real_gpu(native_built):
+    """The xGMI ring as the agent runs it: in the fabric helper (its own process, HIP on every
+    listed GPU), warmed once, then a claim-size ring answered by the same helper. On a 1-GPU box
+    the ring [gpu, gpu] runs its links as local copies through the same code and protocol."""
+    from gpupool.agent.prober import Prober
+    from gpupool.ops import devlib
+    devs = [d for d in devlib.DeviceLib("amdsmi", node="t").snapshot()["devices"]
+            if d.get("hipUUID")][:1]
+    assert devs, "no GPU with a hipUUID"
+    p = Prober("helper", devices=devs, fabric_prewarm=False)
+    try:
+        ring = [devs[0], devs[0]]
+        t0 = time.monotonic()
+        p._warm_fabric(ring)
+        assert p.fabric_warm_ms is not None and p.helpers.alive("fabric")
+        fabric_pid = p.helpers.snapshot()["fabric"]["pid"]
+        assert "libmi355x_probe" in _maps(fabric_pid)
+        starts = p.helpers.stats["helper_starts"]
+        links = p.peer_ring(ring, {"xgmiBytes": 16 << 20, "timeoutSeconds": 10})
+        link = links[devs[0]["uuid"]]
+        assert link["passed"] and link["badBits"] == 0 and link["GBps"] > 50, link
+        assert p.helpers.stats["helper_starts"] == starts  # the warmed helper answered
+        assert p.helpers.snapshot()["fabric"]["pid"] == fabric_pid
+        print(f"fabric warm {p.fabric_warm_ms:.0f} ms, ring {link['GBps']:.0f} GB/s, "
+              f"total {time.monotonic() - t0:.1f} s")
+    finally:
+        p.helpers.stop()
