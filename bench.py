@@ -353,6 +353,12 @@ def main() -> int:
                 settle = [cy["truth"]["settleMs"] for cy in cs if "settleMs" in cy.get("truth", {})]
                 if settle:  # diagnostic: how long the kubelet side lagged when it did not
                     per_n[str(k)]["truth_settle_ms_max"] = max(settle)
+                bad = next((cy for cy in cs if not cy.get("ok")), None)
+                if bad is not None:  # what the first disagreeing read saw (diagnostic)
+                    per_n[str(k)]["first_mismatch"] = {
+                        x: bad.get("truth", {}).get(x) for x in (
+                            "advertised", "healthyAdvertised", "ready", "ledgerClaimed",
+                            "ledgerProbing", "ledgerAgrees", "settleMs", "settled")}
             per_n[str(k)].update(_device_evidence(cs))
             # the agent at this N: its resident memory, the HIP contexts it holds, and the VRAM
             # in use on the GPUs the last cycle of this N claimed (after the timed region)
@@ -365,7 +371,8 @@ def main() -> int:
                     "vram_used_mib_per_gpu": [vram.get(i) for i in idx]}
                 if "helpers_rss_mib" in fa:  # the per-GPU probe helpers beside the agent
                     per_n[str(k)]["agent"].update(probe_helpers=fa.get("helpers"),
-                                                  helpers_rss_mib=fa["helpers_rss_mib"])
+                                                  helpers_rss_mib=fa["helpers_rss_mib"],
+                                                  helpers_pss_mib=fa.get("helpers_pss_mib"))
             if str(k) in errors:
                 per_n[str(k)]["errors"] = errors[str(k)]
                 first = errors[str(k)][0]

@@ -2222,7 +2222,9 @@ class Agent:
             lines.append(f"gpupool_agent_hip_devices {self.prober.hip_devices()}")
             lines.append(f"gpupool_agent_hip_init_ms {self.prober.init_ms:.1f}")
             if self.prober.helpers is not None:
-                lines.append(f"gpupool_agent_probe_helpers_rss_bytes {self.prober.helpers_rss_bytes()}")
+                rss, pss = self.prober.helpers_mem()
+                lines.append(f"gpupool_agent_probe_helpers_rss_bytes {rss}")
+                lines.append(f"gpupool_agent_probe_helpers_pss_bytes {pss}")
                 lines.append(f"gpupool_agent_probe_helpers {len(self.prober.helper_pids())}")
                 if self.prober.fabric_warm_ms is not None:
                     lines.append(f"gpupool_agent_probe_fabric_warm_ms {self.prober.fabric_warm_ms:.1f}")

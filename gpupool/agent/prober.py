@@ -110,16 +110,22 @@ class Prober:
             return sum(1 for k, v in self.helpers.snapshot().items() if k != "fabric" and v.get("alive"))
         return len(self.ordinals)  # helper-sim: no HIP anywhere (0)
 
-    def helpers_rss_bytes(self) -> int:
-        """Resident memory of the probe helpers together (the isolation's host-memory cost)."""
-        total = 0
+    def helpers_mem(self) -> tuple[int, int]:
+        """(RSS, PSS) of the probe helpers together, bytes: the isolation's host-memory cost. RSS
+        counts the HIP runtime's shared text once per helper; PSS splits shared pages between the
+        processes that map them (the fair share)."""
+        rss = pss = 0
         for pid in self.helper_pids():
             try:
-                with open(f"/proc/{pid}/statm") as f:
-                    total += int(f.read().split()[1]) * os.sysconf("SC_PAGESIZE")
+                with open(f"/proc/{pid}/smaps_rollup") as f:
+                    for line in f:
+                        if line.startswith("Rss:"):
+                            rss += int(line.split()[1]) << 10
+                        elif line.startswith("Pss:"):
+                            pss += int(line.split()[1]) << 10
             except (OSError, ValueError, IndexError):
                 pass
-        return total
+        return rss, pss
 
     def prewake(self, devs: list[dict]) -> None:
         """The claim has chosen these GPUs and probes them in ~0.1-0.2 ms (ledger commit first):

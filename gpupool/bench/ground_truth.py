@@ -281,13 +281,20 @@ def kubelet_allocatable(pod_resources_socket: str, timeout: float = 2.0) -> dict
     return out
 
 
-def ledger_claims(state_dir: str, pool_uid: str) -> set[str]:
-    """Claims of ``pool_uid`` read straight from the agent's ledger file on disk."""
+def ledger_claims(state_dir: str, pool_uid: str) -> tuple[set[str], set[str]]:
+    """Claims of ``pool_uid`` read straight from the agent's ledger file on disk: (probed and
+    passed — state Claimed, durable probe verdict; claimed with the verdict still on its way to the
+    disk — state Probing). A claim is made durable as 'Probing' before its probe runs and the
+    agent replies as soon as the probe passed; the Probing -> Claimed write follows through the
+    ledger's background writer (a crash in between re-probes the GPU), so right at Ready a loaded
+    host may still show 'Probing' on disk for a claim whose probe passed."""
     with open(os.path.join(state_dir, "ledger.json")) as f:
         claims = (json.load(f) or {}).get("claims") or {}
-    return {u for u, rec in claims.items()
-            if rec.get("poolUID") == pool_uid and rec.get("state") == "Claimed"
-            and (rec.get("probe") or {}).get("passed")}
+    mine = {u: rec for u, rec in claims.items() if rec.get("poolUID") == pool_uid}
+    passed = {u for u, rec in mine.items()
+              if rec.get("state") == "Claimed" and (rec.get("probe") or {}).get("passed")}
+    probing = {u for u, rec in mine.items() if rec.get("state") == "Probing"}
+    return passed, probing
 
 
 def pool_truth(pod_resources_socket: str, resource: str, healthy: set[str],
@@ -299,7 +306,8 @@ def pool_truth(pod_resources_socket: str, resource: str, healthy: set[str],
     good = adv & healthy
     out = {"advertised": len(adv), "healthyAdvertised": len(good), "ready": len(good)}
     if state_dir and pool_uid:
-        claimed = ledger_claims(state_dir, pool_uid)
-        out["ledgerClaimed"] = len(claimed)
-        out["ledgerAgrees"] = (claimed & healthy) == good
+        passed, probing = ledger_claims(state_dir, pool_uid)
+        out["ledgerClaimed"] = len(passed)
+        out["ledgerProbing"] = len(probing)  # durable claims whose verdict write is pending
+        out["ledgerAgrees"] = ((passed | probing) & healthy) == good
     return out

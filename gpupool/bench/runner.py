@@ -441,7 +441,7 @@ class BenchRun:
             if len(owned) >= n or time.monotonic() > deadline:
                 break
             time.sleep(0.01)
-        ledger0 = gt.ledger_claims(self.state_dir, obj["metadata"]["uid"]) \
+        ledger0 = set().union(*gt.ledger_claims(self.state_dir, obj["metadata"]["uid"])) \
             if os.path.exists(os.path.join(self.state_dir, "ledger.json")) else set()
         samples: list[dict] = []
         t_conv: list[float] = []
@@ -488,7 +488,7 @@ class BenchRun:
                             "kubeletHealthy": len(adv), "ok": agree})
         self.phase = "cleanup"
         self.cluster.set_faults(self.node.name, {}, sample=True)
-        ledger1 = gt.ledger_claims(self.state_dir, obj["metadata"]["uid"]) \
+        ledger1 = set().union(*gt.ledger_claims(self.state_dir, obj["metadata"]["uid"])) \
             if os.path.exists(os.path.join(self.state_dir, "ledger.json")) else set()
         self.delete_pool(name)
         ok = sum(x["ok"] for x in samples)
@@ -527,6 +527,9 @@ class BenchRun:
                     m = re.search(r"^gpupool_agent_probe_helpers_rss_bytes (\d+)", text, re.M)
                     if m:
                         out[who]["helpers_rss_mib"] = round(int(m.group(1)) / 2**20, 1)
+                        m = re.search(r"^gpupool_agent_probe_helpers_pss_bytes (\d+)", text, re.M)
+                        if m:
+                            out[who]["helpers_pss_mib"] = round(int(m.group(1)) / 2**20, 1)
                         m = re.search(r"^gpupool_agent_probe_helpers (\d+)", text, re.M)
                         out[who]["helpers"] = int(m.group(1)) if m else None
                     out[who]["vram_used_mib"] = {

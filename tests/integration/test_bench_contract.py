@@ -34,7 +34,7 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
     cfg = out["config"]
     assert sorted(cfg["per_n"], key=int) == ["1", "2", "4", "8"]
     for k, v in cfg["per_n"].items():
-        assert v["accuracy"] == 1.0 and 0 < v["p50_s"] < 30, (k, v)
+        assert v["accuracy"] == 1.0 and 0 < v["p50_s"] < 30, (k, json.dumps(v))
         # the truth is read once, at Ready, with no grace: readiness is strict by default
         assert v["truth_first_read_agrees"] == 1.0, (k, v)
     assert out["value"] == cfg["per_n"]["8"]["p50_s"]
