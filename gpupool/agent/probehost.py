@@ -11,10 +11,13 @@ left its pool waiting on a ``Probing`` GPU forever. Here:
   * one helper per GPU, started with ``ROCR_VISIBLE_DEVICES=<that GPU's UUID>``: it holds a HIP
     context on its GPU only, and a fault takes down that helper only — probes of the other GPUs go
     on in theirs;
-  * a *fabric* helper that sees all of the node's GPUs runs the xGMI peer ring; the agent starts
-    and warms it (one 1 MiB ring) at start on a multi-GPU node and keeps it resident, so no
+  * a *fabric* helper that sees all of the node's GPUs runs the xGMI peer ring. It runs one
+    1 MiB warm ring (peer access, ring windows) before it reports ready; on a multi-GPU node it
+    starts with the GPU helpers and is resident — replaced after an exit like them — so no
     multi-GPU claim pays its HIP init; with ``fabric_idle_s`` > 0 it exits after that long idle
     instead and is started again on demand (its contexts cost VRAM on every GPU);
+  * a helper whose HIP init does not finish within ``ready_timeout`` is killed and replaced as
+    after a crash, and a request waits for a starting helper no longer than its own deadline;
   * every request has a deadline (``spec.probe.timeoutSeconds`` for probes and rings): past it the
     helper is SIGKILLed and the request fails (``ProbeTimeout``); a helper that dies mid-request
     fails what it had in flight (``ProbeCrashed``); a fresh child replaces it, with a backoff while
@@ -105,6 +108,14 @@ class _HipKernel:
     def info(self) -> dict:
         return {"devices": self.n, "uuids": self.uuids}
 
+    def warm_ring(self) -> dict:
+        """One 1 MiB ring over every visible GPU: peer access enabled and the ring windows
+        allocated before the helper says it is ready, so a claim's first ring does neither."""
+        if self.n < 2:
+            return {}
+        r = self.hp.peer_ring(list(range(self.n)), 1 << 20)
+        return {"passed": bool(r.get("passed")), "links": len(r.get("links") or [])}
+
     def ordinal(self, hip_uuid: str) -> int:
         o = self.uuids.get(str(hip_uuid or "").lower())
         if o is None and self.single and self.n == 1:
@@ -144,9 +155,14 @@ class _SimKernel:
     def __init__(self, spec: dict):
         self.sim_ms = float(spec.get("simMs", 20.0))
         self.n = int(spec.get("devices") or 1)
+        if spec.get("initHang"):  # test hook: a HIP init that never returns
+            threading.Event().wait()
 
     def info(self) -> dict:
         return {"devices": self.n, "uuids": {}}
+
+    def warm_ring(self) -> dict:
+        return {"passed": True, "links": self.n} if self.n >= 2 else {}
 
     def call(self, op: str, a: dict) -> Any:
         from . import simprobe
@@ -219,8 +235,18 @@ def child_main(conn, spec: dict) -> None:
             send({"op": "ready", "ok": False, "error": repr(e)})
         finally:
             os._exit(3)
-    send({"op": "ready", "ok": True, "pid": os.getpid(),
-          "initMs": round((time.perf_counter() - t0) * 1e3, 1), **info})
+    info["initMs"] = round((time.perf_counter() - t0) * 1e3, 1)
+    if spec.get("warmRing"):
+        # the fabric helper: its first ring's peer-access enable and window allocation happen
+        # here, not inside a claim's deadline. A failure is reported, not fatal: the rings that
+        # follow report it per link (XGMIPeerCheckUnavailable)
+        t1 = time.perf_counter()
+        try:
+            info["warm"] = kernel.warm_ring()
+        except Exception as e:
+            info["warm"] = {"passed": False, "error": f"{type(e).__name__}: {e}"}
+        info["warmMs"] = round((time.perf_counter() - t1) * 1e3, 1)
+    send({"op": "ready", "ok": True, "pid": os.getpid(), **info})
 
     def run(msg: dict) -> None:
         try:
@@ -337,10 +363,11 @@ class Helper:
     # after the kernel has woken the blocked thread. Longer requests then block as usual.
     CALLER_SPIN_S = float(os.environ.get("GPUPOOL_CALLER_SPIN_MS", "0")) / 1e3
 
-    def __init__(self, key: str, spec: dict, on_exit=None):
+    def __init__(self, key: str, spec: dict, on_exit=None, ready_timeout: float = 120.0):
         self.key = key
         self.spec = spec
         self.on_exit = on_exit
+        self.ready_timeout = ready_timeout  # HIP init (+ the fabric's warm ring) must finish by then
         self.proc = None
         self.conn = None
         self.pid = 0
@@ -414,7 +441,12 @@ class Helper:
     def _watch(self) -> None:
         from multiprocessing.connection import wait
         try:  # the ready message (HIP init on the GPU: up to seconds)
+            give_up = self.started + self.ready_timeout
             while not self.ready.is_set():
+                if time.monotonic() > give_up:  # an init that hangs: replaced like a crash
+                    self.kill(f"probe helper {self.key} not ready within "
+                              f"{self.ready_timeout:g} s (HIP init hung)")
+                    break
                 if not self._read_one(1.0):
                     break
         finally:
@@ -476,12 +508,14 @@ class Helper:
     def wait_ready(self, timeout: float) -> bool:
         return self.ready.wait(timeout) and self.ready_ok and not self.dead
 
-    def call(self, op: str, args: dict, timeout: float, ready_timeout: float = 120.0) -> Any:
+    def call(self, op: str, args: dict, timeout: float) -> Any:
         """Run ``op`` in the helper. Raises HelperTimeout past ``timeout`` (the caller decides
         whether to kill), HelperDied if the helper is or goes away, HelperUnavailable if its HIP
-        never came up; RuntimeError for an error the request itself raised."""
-        if not self.ready.wait(ready_timeout):
-            raise HelperUnavailable(f"probe helper {self.key} not ready after {ready_timeout:.0f} s")
+        has not come up within the request's own deadline (a helper being replaced) or never
+        does; RuntimeError for an error the request itself raised."""
+        wait = min(timeout, self.ready_timeout)
+        if not self.ready.wait(wait):
+            raise HelperUnavailable(f"probe helper {self.key} still starting after {wait:g} s")
         if not self.ready_ok:
             raise HelperUnavailable(f"probe helper {self.key}: {self.ready_error or self.dead}")
         slot = _Slot()
@@ -574,8 +608,12 @@ class HelperPool:
 
     def __init__(self, kind: str, sim_ms: float = 20.0, arena_idle_s: float = 10.0,
                  fabric_idle_s: float = 0.0, ready_timeout: float = 120.0,
-                 max_backoff_s: float = 60.0, crash_window_s: float = 300.0):
+                 max_backoff_s: float = 60.0, crash_window_s: float = 300.0,
+                 resident_fabric: bool = False):
         self.kind = kind
+        # resident: the fabric helper is started with the GPU helpers (2+ GPUs) and replaced
+        # like them after an exit; otherwise it starts on a ring's demand
+        self.resident_fabric = resident_fabric
         self.sim_ms = sim_ms
         self.arena_idle_s = arena_idle_s
         self.fabric_idle_s = fabric_idle_s
@@ -604,7 +642,7 @@ class HelperPool:
 
     def _fabric_spec(self) -> dict:
         spec = {"kind": self.kind, "single": False, "simMs": self.sim_ms, "arenaIdleS": 0,
-                "devices": len(self._fabric_devs)}
+                "devices": len(self._fabric_devs), "warmRing": True}
         if self.kind == "hip":
             ids = [d.get("hipUUID") or str(d.get("index", 0)) for d in self._fabric_devs]
             spec["visible"] = ",".join(ids)
@@ -619,15 +657,20 @@ class HelperPool:
                 self._devs[d["uuid"]] = d
             self._fabric_devs = sorted(self._devs.values(), key=lambda d: d.get("index", 0))
             new = [self._spawn_locked(d["uuid"]) for d in devs if d["uuid"] not in self._helpers]
+            if self._fabric_wanted_locked() and "fabric" not in self._helpers:
+                self._spawn_locked("fabric")  # warms itself; nothing waits for it here
         if wait:
             deadline = time.monotonic() + self.ready_timeout
             for h in new:
                 h.ready.wait(max(0.0, deadline - time.monotonic()))
         return {u: dict(h.info) for u, h in self._helpers.items()}
 
+    def _fabric_wanted_locked(self) -> bool:
+        return self.resident_fabric and len(self._fabric_devs) >= 2 and not self._stopping
+
     def _spawn_locked(self, key: str) -> Helper:
         spec = self._fabric_spec() if key == "fabric" else self._gpu_spec(self._devs[key])
-        h = Helper(key, spec, on_exit=self._on_exit).start()
+        h = Helper(key, spec, on_exit=self._on_exit, ready_timeout=self.ready_timeout).start()
         self._helpers[key] = h
         self.stats["helper_starts"] += 1
         return h
@@ -651,14 +694,16 @@ class HelperPool:
             self._respawn_at[h.key] = now + delay
         log.warning("probe helper %s gone (%s); replacing it%s", h.key, why,
                     f" in {delay:.0f} s" if delay else "")
-        if h.key != "fabric":
+        if h.key != "fabric" or self.resident_fabric:
             t = threading.Timer(delay, self._respawn, args=(h.key,))
             t.daemon = True
             t.start()
 
     def _respawn(self, key: str) -> None:
         with self._mu:
-            if self._stopping or key in self._helpers or key not in self._devs:
+            if self._stopping or key in self._helpers:
+                return
+            if key not in self._devs and not (key == "fabric" and self._fabric_wanted_locked()):
                 return
             if time.monotonic() < self._respawn_at.get(key, 0.0):
                 return
@@ -730,6 +775,9 @@ class HelperPool:
             out = {}
             for k, h in self._helpers.items():
                 out[k] = {"pid": h.pid, "alive": h.alive, "initMs": h.info.get("initMs")}
+                if "warmMs" in h.info:
+                    out[k]["warmMs"] = h.info["warmMs"]
+                    out[k]["warm"] = h.info.get("warm")
             for k, why in self.last_exit.items():
                 out.setdefault(k, {"alive": False})["lastExit"] = why
             return out

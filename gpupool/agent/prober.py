@@ -55,7 +55,6 @@ class Prober:
         self.ordinals: dict[str, int] = {}
         self.helpers = None
         self.init_ms = 0.0
-        self.fabric_warm_ms = None
         t0 = time.perf_counter()
         if mode == "inproc":
             from ..ops import probe as hip_probe
@@ -71,19 +70,18 @@ class Prober:
             threading.Thread(target=self._trim_loop, daemon=True, name="probe-trim").start()
         elif mode in HELPER_MODES:
             from .probehost import HelperPool
+            # the xGMI fabric helper (2+ GPUs): resident (started with the GPU helpers, warmed
+            # with one 1 MiB ring before it reports ready, replaced after an exit) unless it is
+            # let go when idle (fabric_idle_s > 0) — then it starts on a ring's demand
             self.helpers = HelperPool("hip" if mode == "helper" else "sim", sim_ms=sim_ms,
-                                      arena_idle_s=arena_idle_s, fabric_idle_s=fabric_idle_s)
+                                      arena_idle_s=arena_idle_s, fabric_idle_s=fabric_idle_s,
+                                      resident_fabric=fabric_prewarm and fabric_idle_s <= 0)
             ready = self.helpers.start(list(devices or []))
+            ready.pop("fabric", None)  # not waited for: it warms in the background
             up = sorted(u for u, r in ready.items() if r.get("ok"))
             bad = {u: r.get("error") for u, r in ready.items() if not r.get("ok")}
             log.info("probe helpers up for %d/%d GPU(s)%s", len(up), len(ready),
                      f"; failed: {bad}" if bad else "")
-            fabric = [d for d in (devices or []) if d["uuid"] in up]
-            if fabric_prewarm and len(fabric) >= 2:
-                # the fabric helper's HIP init on every GPU (seconds on 8) and the ring's first
-                # peer-access enable + buffer allocation happen now, not inside a multi-GPU
-                # claim's deadline; it then stays resident (fabric_idle_s 0)
-                self.pool.submit(self._warm_fabric, fabric)
         elif mode == "subprocess":
             out = subprocess.run([native_path("mi355x-probe"), "--list"], capture_output=True,
                                  text=True, timeout=120)
@@ -109,6 +107,14 @@ class Prober:
         if self.mode == "helper":
             return sum(1 for k, v in self.helpers.snapshot().items() if k != "fabric" and v.get("alive"))
         return len(self.ordinals)  # helper-sim: no HIP anywhere (0)
+
+    @property
+    def fabric_warm_ms(self) -> float | None:
+        """How long the fabric helper's warm ring took before it reported ready (None: no
+        fabric helper up, or it did not warm)."""
+        if self.helpers is None:
+            return None
+        return (self.helpers.snapshot().get("fabric") or {}).get("warmMs")
 
     def helpers_mem(self) -> tuple[int, int]:
         """(RSS, PSS) of the probe helpers together, bytes: the isolation's host-memory cost. RSS
@@ -318,15 +324,6 @@ class Prober:
             except Exception as e:  # never take the agent down
                 log.warning("xGMI peer check failed: %r", e)
         return out
-
-    def _warm_fabric(self, devs: list[dict]) -> None:
-        devs = sorted(devs, key=lambda d: d.get("index", 0))
-        t0 = time.perf_counter()
-        ring = self._ring_whole(devs, 1 << 20, 120.0) or {}
-        self.fabric_warm_ms = (time.perf_counter() - t0) * 1e3
-        bad = {u: r.get("error") for u, r in ring.items() if not r.get("passed")}
-        log.info("fabric helper warm over %d GPU(s) in %.0f ms%s", len(devs), self.fabric_warm_ms,
-                 f"; links not passing: {bad}" if bad else "")
 
     def _fabric_call(self, devs: list[dict], op: str, args: dict, timeout: float) -> dict:
         """A request to the fabric helper. Its failure says nothing about any one link, so it

@@ -523,19 +523,21 @@ def test_pod_that_escapes_its_hbm_limit_is_evicted_on_the_real_gpu(cluster_facto
 
 def test_fabric_helper_rings_on_the_real_gpu(native_built):
     """The xGMI ring as the agent runs it: in the fabric helper (its own process, HIP on every
-    listed GPU), warmed once, then a claim-size ring answered by the same helper. On a 1-GPU box
-    the ring [gpu, gpu] runs its links as local copies through the same code and protocol."""
+    listed GPU; with 2+ GPUs it runs a warm ring before it reports ready), then a claim-size ring
+    answered by the same helper. On a 1-GPU box the ring [gpu, gpu] runs its links as local
+    copies through the same code and protocol."""
     from gpupool.agent.prober import Prober
     from gpupool.ops import devlib
     devs = [d for d in devlib.DeviceLib("amdsmi", node="t").snapshot()["devices"]
             if d.get("hipUUID")][:1]
     assert devs, "no GPU with a hipUUID"
-    p = Prober("helper", devices=devs, fabric_prewarm=False)
+    p = Prober("helper", devices=devs)
     try:
         ring = [devs[0], devs[0]]
         t0 = time.monotonic()
-        p._warm_fabric(ring)
-        assert p.fabric_warm_ms is not None and p.helpers.alive("fabric")
+        fab = p.helpers.fabric(ring)  # 1 GPU: not resident, started on demand, warmed before ready
+        assert fab.wait_ready(60), fab.ready_error
+        assert p.fabric_warm_ms is not None, p.helpers.snapshot()
         fabric_pid = p.helpers.snapshot()["fabric"]["pid"]
         assert "libmi355x_probe" in _maps(fabric_pid)
         starts = p.helpers.stats["helper_starts"]

@@ -206,3 +206,58 @@ def test_probing_record_past_its_deadline_is_reported_overdue(tmp_path, agents, 
         gate.set()
         t.join(10)
     assert not any(d.get("probeOverdue") for d in a.node_view()["devices"])
+
+
+def test_resident_fabric_helper_is_warm_before_ready_and_replaced_after_a_kill():
+    """On a multi-GPU node the fabric helper starts with the GPU helpers, runs its warm ring
+    before it reports ready, and — resident — is replaced (warm again) after it dies."""
+    from gpupool.agent.probehost import HelperPool
+    devs = [{"uuid": f"g{i}", "index": i} for i in range(3)]
+    pool = HelperPool("sim", sim_ms=1, resident_fabric=True)
+    try:
+        pool.start(devs)
+        assert wait(lambda: (pool.snapshot().get("fabric") or {}).get("warmMs") is not None)
+        first = pool.snapshot()["fabric"]
+        assert first["alive"] and first["warm"] == {"passed": True, "links": 3}, first
+        pool.kill("fabric", "test kill")
+        assert wait(lambda: (pool.snapshot().get("fabric") or {}).get("pid") not in (None, first["pid"])
+                    and pool.alive("fabric"))
+        assert pool.snapshot()["fabric"]["warmMs"] is not None
+        assert pool.stats["helper_timeouts"] == 1  # kill() = a missed deadline
+    finally:
+        pool.stop()
+
+
+def test_on_demand_fabric_helper_is_not_replaced():
+    from gpupool.agent.probehost import HelperPool
+    devs = [{"uuid": f"g{i}", "index": i} for i in range(2)]
+    pool = HelperPool("sim", sim_ms=1, resident_fabric=False)
+    try:
+        pool.start(devs)
+        assert "fabric" not in pool.snapshot()  # nothing until a ring asks
+        h = pool.fabric(devs)
+        assert h.wait_ready(10) and pool.alive("fabric")
+        pool.kill("fabric", "test kill")
+        assert wait(lambda: not pool.alive("fabric"))
+        time.sleep(0.3)
+        assert not pool.alive("fabric")
+    finally:
+        pool.stop()
+
+
+def test_a_helper_whose_init_hangs_is_killed_at_its_ready_timeout():
+    """A helper that never reports ready (a HIP init hung in the driver) is killed when its
+    ready timeout passes, like a request past its deadline, and callers are not held past their
+    own deadline meanwhile."""
+    from gpupool.agent.probehost import Helper, HelperUnavailable
+    exits = []
+    h = Helper("g0", {"kind": "sim", "initHang": True}, on_exit=lambda h_, why, cause:
+               exits.append((why, cause)), ready_timeout=1.5).start()
+    t0 = time.monotonic()
+    with pytest.raises(HelperUnavailable):
+        h.call("ping", {}, timeout=0.3)
+    assert time.monotonic() - t0 < 1.0
+    assert wait(lambda: exits, timeout=10)
+    why, cause = exits[0]
+    assert cause == "timeout" and "not ready within 1.5 s" in why, exits
+    assert h.dead and not h.ready_ok
