@@ -221,6 +221,8 @@ def child_main(conn, spec: dict) -> None:
         os.environ.pop(k, None)
     if spec.get("visible") is not None:
         os.environ["ROCR_VISIBLE_DEVICES"] = str(spec["visible"])
+    for k, v in (spec.get("env") or {}).items():  # read by the HIP runtime at its init, below
+        os.environ[str(k)] = str(v)
     send_mu = threading.Lock()
 
     def send(msg: dict) -> None:
@@ -599,6 +601,15 @@ class Helper:
             pass
 
 
+# Hardware queues per GPU in the fabric helper (0 = the runtime's default). Every HIP hardware
+# queue of an MI355X carries a context-save area for all 256 CUs' waves — 173 MiB of host memory
+# each (native/tests/queue_mem.hip, profiles/r5i_hip_host_memory.json) — and a context starts with
+# two. One queue per GPU saves 175 MiB of host memory per GPU in the fabric helper (1.4 GB on an
+# 8-GPU node) but measured +0.09 ms on a ring (profiles/r5j_helper_footprint.json): the default
+# keeps the runtime's queues, for the multi-GPU claim's latency; set 1 where host RAM is tight.
+FABRIC_HW_QUEUES = int(os.environ.get("GPUPOOL_FABRIC_HW_QUEUES", "0"))
+
+
 class HelperPool:
     """The agent's helpers: one per GPU (keyed by uuid), plus the on-demand fabric helper.
 
@@ -643,6 +654,8 @@ class HelperPool:
     def _fabric_spec(self) -> dict:
         spec = {"kind": self.kind, "single": False, "simMs": self.sim_ms, "arenaIdleS": 0,
                 "devices": len(self._fabric_devs), "warmRing": True}
+        if FABRIC_HW_QUEUES > 0:
+            spec["env"] = {"GPU_MAX_HW_QUEUES": str(FABRIC_HW_QUEUES)}
         if self.kind == "hip":
             ids = [d.get("hipUUID") or str(d.get("index", 0)) for d in self._fabric_devs]
             spec["visible"] = ",".join(ids)

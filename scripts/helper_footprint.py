@@ -84,6 +84,32 @@ def main() -> int:
         out["one_helper_top_mappings"] = top_mappings(pids[0])
     finally:
         pool.stop()
+    # the fabric helper (HIP on every GPU it rings; one here) with the runtime's default hardware
+    # queues per GPU and with the one it is started with (probehost.FABRIC_HW_QUEUES)
+    from gpupool.agent import probehost
+    out["fabric"] = {}
+    for cap in (0, 1):
+        probehost.FABRIC_HW_QUEUES = cap
+        fp = HelperPool("hip", arena_idle_s=0)
+        try:
+            h = fp.fabric([devs[0], devs[0]])
+            if not h.wait_ready(60):
+                out["fabric"][f"hwq{cap}"] = {"error": h.ready_error or "not ready"}
+                continue
+            ring = {"hipUUIDs": [dev.get("hipUUID", "")] * 2, "bytes": 16 << 20}
+            h.call("peer_ring", ring, 30)  # first ring allocates the windows
+            t = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                h.call("peer_ring", ring, 30)
+                t.append((time.perf_counter() - t0) * 1e3)
+            time.sleep(0.3)
+            m = mem(h.pid)
+            out["fabric"][f"hwq{cap}"] = {"RssMiB": round(m["Rss"] / 2**20, 1),
+                                          "PssMiB": round(m["Pss"] / 2**20, 1),
+                                          "ring_ms_p50": round(sorted(t)[2], 3)}
+        finally:
+            fp.stop()
     print(json.dumps(out, indent=1))
     return 0
 
