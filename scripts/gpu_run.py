@@ -76,6 +76,7 @@ def scenarios(tag_dir: str) -> dict[str, list[tuple]]:
         "probe": [("probe_report", [PY, "scripts/probe_report.py"], 200, {}),
                   ("probe_size_sweep", [PY, "scripts/probe_size_sweep.py"], 300, {})],
         "footprint": [("helper_footprint", [PY, "scripts/helper_footprint.py", "8"], 240, {}),
+                      ("hip_host_memory", [PY, "scripts/hip_host_memory.py"], 240, {}),
                       ("agent_footprint", [PY, "scripts/agent_footprint.py"], 300, {}),
                       ("amdsmi_call_costs", [PY, "scripts/amdsmi_call_costs.py"], 200, {})],
     }
@@ -163,7 +164,7 @@ def main() -> int:
     for n in names:
         for step, argv, timeout, env in table[n]:
             out = os.path.join(tag_dir, step + (".json" if "bench" in step or step in ("facts",
-                               "helper_ab", "helper_footprint") else ".txt"))
+                               "helper_ab", "helper_footprint", "hip_host_memory") else ".txt"))
             cmd = ["timeout", "-k", "10", str(timeout), *argv]
             print(f"[{n}] {step}: {' '.join(argv)} > {out}", flush=True)
             with open(out, "w") as fo, open(os.path.join(tag_dir, step + ".err"), "w") as fe:
