@@ -7,7 +7,7 @@ import time
 
 import pytest
 
-from gpupool.kube import EVENTS, MI355XJOBS, MI355XPOOLS, PODS
+from gpupool.kube import MI355XJOBS, MI355XPOOLS, PODS
 
 from .helpers import mi_pool, pause_pod, settled_events, wait_ready
 from .test_jobs import job, phase_is

@@ -16,7 +16,7 @@ import time
 import pytest
 import yaml
 
-from gpupool.kube import AZUREVMPOOLS, EVENTS, SECRETS
+from gpupool.kube import AZUREVMPOOLS, SECRETS
 from gpupool.testing.arm_sim import ArmSim
 from gpupool.testing.cluster import make_test_pki
 
@@ -278,7 +278,6 @@ def test_arm_provider_under_sanitizer(san, arm, cluster_factory):
     """The ARM provider (token cache shared by worker threads, TLS client, paging, rollback) in the
     ASan+UBSan and TSan builds of the manager, through scale up/down, throttling, a revoked token
     and a delete with leftover NIC/disk."""
-    import subprocess
     r = make_native("host", san, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     os.environ["TSAN_OPTIONS"] = "halt_on_error=0:report_signal_unsafe=0"

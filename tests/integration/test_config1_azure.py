@@ -10,7 +10,7 @@ import time
 import pytest
 import yaml
 
-from gpupool.kube import AZUREVMPOOLS, EVENTS, SECRETS
+from gpupool.kube import AZUREVMPOOLS, SECRETS
 
 from .helpers import cond_is, conds, settled_events
 

@@ -9,7 +9,7 @@ import time
 
 import pytest
 
-from gpupool.kube import EVENTS, MI355XPOOLS
+from gpupool.kube import MI355XPOOLS
 from gpupool.testing.cluster import NodeSpec
 
 from .helpers import cond_is, mi_pool, settled_events, wait_ready

@@ -13,7 +13,7 @@ import time
 import pytest
 import yaml
 
-from gpupool.kube import EVENTS, MI355XJOBS, MI355XPOOLS, PODS, KubeError
+from gpupool.kube import MI355XJOBS, MI355XPOOLS, PODS, KubeError
 
 from .helpers import conds, mi_pool, settled_events, wait_ready
 

@@ -6,7 +6,7 @@ import time
 
 import pytest
 
-from gpupool.kube import EVENTS, MI355XPOOLS, NODES, PODS, KubeError
+from gpupool.kube import MI355XPOOLS, NODES, PODS, KubeError
 from gpupool.testing.cluster import NodeSpec
 
 from .helpers import cond_is, conds, mi_pool, pause_pod, ready_at, settled_events, wait_ready

@@ -4,7 +4,6 @@ scenario ('TSan covers the informer/workqueue/worker threads').""
 from __future__ import annotations
 
 import os
-import subprocess
 
 import pytest
 
