@@ -2041,11 +2041,14 @@ class Agent:
 
     def check_leader(self, method: str, path: str, headers: dict) -> tuple | None:
         """Fencing tokens (the manager's Lease, README.md:162->242's missing manager step): every
-        mutating RPC of a leader-elected manager carries its identity and epoch (the Lease's
-        leaseTransitions). The newest epoch seen is persisted; an older one — a leader that was
-        paused between its own fence check and the send while a successor took over — is refused
-        with 409 StaleLeader before anything is touched. A request without a token (leader
-        election off, an admin's gpuctl) is not checked."""
+        mutating RPC of a leader-elected manager carries its identity, its epoch (the Lease's
+        leaseTransitions) and the Lease's generation (creationTimestamp + uid: leaseTransitions
+        starts again at 0 when the Lease is deleted and created anew). The newest token seen is
+        persisted; tokens are ordered by (generation, epoch): an older one — a leader that was
+        paused between its own fence check and the send while a successor took over, or a leader
+        of a Lease that has since been recreated — is refused with 409 StaleLeader before anything
+        is touched. A request without a token (leader election off, an admin's gpuctl) is not
+        checked."""
         if method != "POST" or path not in self.MUTATING:
             return None
         raw = headers.get("x-gpupool-leader-epoch")
@@ -2057,18 +2060,38 @@ class Agent:
         except ValueError:
             return json_reply({"reason": "BadRequest", "message": f"bad leader epoch {raw!r}"}, 400)
         holder = headers.get("x-gpupool-leader", "")
+        lease = headers.get("x-gpupool-leader-lease")  # "<creationTimestamp> <uid>"
+        created, _, uid = (lease or "").strip().partition(" ")
         with self._fence_mu:
-            cur_e = int(self.leader_fence.get("epoch", -1))
-            cur_h = str(self.leader_fence.get("holder", ""))
-            if epoch < cur_e or (epoch == cur_e and cur_h and holder != cur_h):
+            cur = self.leader_fence
+            cur_e, cur_h = int(cur.get("epoch", -1)), str(cur.get("holder", ""))
+            cur_c, cur_u = str(cur.get("leaseCreated", "")), str(cur.get("leaseUID", ""))
+            retired = list(cur.get("retiredLeaseUIDs") or [])
+            newer_lease = older_lease = False
+            if created and cur_c:
+                # RFC 3339 UTC timestamps of one apiserver compare as strings; a Lease recreated
+                # within the same second is told apart by its uid: one not seen before is the
+                # newer one, one this agent has already moved past is not
+                older_lease = created < cur_c or (uid != cur_u and uid in retired)
+                newer_lease = not older_lease and (
+                    created > cur_c or (created == cur_c and uid != cur_u))
+            stale = older_lease or (not newer_lease and (
+                epoch < cur_e or (epoch == cur_e and cur_h and holder != cur_h)))
+            if stale:
                 self.stats["stale_leader_refused"] = self.stats.get("stale_leader_refused", 0) + 1
-                log.warning("refused %s from stale leader %s (epoch %d; newest seen %s at %d)",
-                            path, holder, epoch, cur_h, cur_e)
+                log.warning("refused %s from stale leader %s (epoch %d, lease %s; newest seen %s "
+                            "at %d, lease %s)", path, holder, epoch, created or "?", cur_h, cur_e,
+                            cur_c or "?")
                 return json_reply({"reason": "StaleLeader",
                                    "message": f"leader {holder} epoch {epoch} is stale: {cur_h} holds "
-                                              f"epoch {cur_e}"}, 409)
-            if epoch > cur_e or not cur_h:
-                self.leader_fence = {"holder": holder, "epoch": epoch, "at": now_rfc3339()}
+                                              f"epoch {cur_e}"
+                                              + (" of a newer Lease" if older_lease else "")}, 409)
+            if newer_lease or epoch > cur_e or not cur_h or (created and not cur_c):
+                if newer_lease and cur_u:
+                    retired = (retired + [cur_u])[-8:]
+                self.leader_fence = {"holder": holder, "epoch": epoch, "at": now_rfc3339(),
+                                     **({"leaseCreated": created, "leaseUID": uid,
+                                         "retiredLeaseUIDs": retired} if created else {})}
                 self.ledger.commit_leader(self.leader_fence)  # durable before acting on it
         return None
 
@@ -2218,6 +2241,8 @@ class Agent:
             for k, v in self.scrubber.stats.items():
                 lines.append(f"gpupool_agent_hbm_scrub_{k}_total {v}")
             lines.append(f"gpupool_agent_gen {self.gen}")
+            # the newest manager fencing token seen (-1: none): a takeover raises it
+            lines.append(f"gpupool_agent_leader_epoch {int(self.leader_fence.get('epoch', -1))}")
             # GPUs the agent's probe helpers (or, inproc, the agent) hold a HIP context on
             lines.append(f"gpupool_agent_hip_devices {self.prober.hip_devices()}")
             lines.append(f"gpupool_agent_hip_init_ms {self.prober.init_ms:.1f}")

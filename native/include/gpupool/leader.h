@@ -35,9 +35,16 @@ bool leader_fence_ok();
 // larger epoch). epoch < 0 without leader election. Sent on every mutating node-agent RPC; the
 // agent remembers the highest epoch it has seen and refuses older ones (409 StaleLeader), so a
 // leader paused between its fence check and the send cannot act after a successor took over.
+//
+// leaseTransitions starts again at 0 when the Lease object is deleted and created anew, so the token
+// also names the Lease's generation — its creationTimestamp and uid: the agent orders tokens by
+// (creationTimestamp, epoch), so a recreated Lease's leader is accepted from epoch 0 while a leader
+// of the deleted Lease, however high its epoch, is refused.
 struct LeaderToken {
   std::string identity;
   int64_t epoch = -1;
+  std::string lease_created;  // metadata.creationTimestamp of the Lease
+  std::string lease_uid;      // metadata.uid of the Lease
 };
 LeaderToken leader_token();
 

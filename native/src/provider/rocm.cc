@@ -162,7 +162,8 @@ Json RocmProvider::post_(const std::string& node, const std::string& path, const
   // makes the agent the judge — it refuses an epoch older than one it has seen (StaleLeader).
   std::string fence;
   if (const LeaderToken tok = leader_token(); tok.epoch >= 0)
-    fence = "X-Gpupool-Leader: " + tok.identity + "\r\nX-Gpupool-Leader-Epoch: " + std::to_string(tok.epoch) + "\r\n";
+    fence = "X-Gpupool-Leader: " + tok.identity + "\r\nX-Gpupool-Leader-Epoch: " + std::to_string(tok.epoch) +
+            "\r\nX-Gpupool-Leader-Lease: " + tok.lease_created + " " + tok.lease_uid + "\r\n";
   test_pause_after_fence_(path);
   invalidate_(node);  // every POST mutates the agent: the next observe must ask it
   trace::Span span("agent:POST " + path);

@@ -53,10 +53,11 @@ bool LeaderElector::try_acquire_or_renew() {
     obj["spec"]["renewTime"] = now;
     obj["spec"]["leaseTransitions"] = 0;
     try {
-      client_.create(res::leases(), cfg_.ns, obj);
+      const Json made = client_.create(res::leases(), cfg_.ns, obj);
       leader_ = true;
       std::lock_guard<std::mutex> g(g_token_mu);
-      g_token = {cfg_.identity, 0};
+      g_token = {cfg_.identity, 0, made.path("metadata.creationTimestamp").str_or(""),
+                 made.path("metadata.uid").str_or("")};
       return true;
     } catch (const KubeError& e2) {
       if (e2.code == 409) return false;  // someone else created it first
@@ -89,8 +90,9 @@ bool LeaderElector::try_acquire_or_renew() {
     upd["spec"]["acquireTime"] = now;
     upd["spec"]["leaseTransitions"] = spec["leaseTransitions"].as_int(0) + 1;
   }
+  Json stored;
   try {
-    client_.update(res::leases(), cfg_.ns, upd);
+    stored = client_.update(res::leases(), cfg_.ns, upd);
   } catch (const KubeError& e) {
     if (e.conflict()) {
       leader_ = false;
@@ -101,7 +103,9 @@ bool LeaderElector::try_acquire_or_renew() {
   leader_ = true;
   {
     std::lock_guard<std::mutex> g(g_token_mu);
-    g_token = {cfg_.identity, upd["spec"]["leaseTransitions"].as_int(0)};
+    const Json& md = stored.is_object() ? stored["metadata"] : lease["metadata"];
+    g_token = {cfg_.identity, upd["spec"]["leaseTransitions"].as_int(0),
+               md["creationTimestamp"].str_or(""), md["uid"].str_or("")};
   }
   return true;
 }

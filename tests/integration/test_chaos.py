@@ -438,3 +438,44 @@ def test_leader_paused_between_fence_check_and_send_is_refused_by_the_agent(clus
     assert [d["uuid"] for d in view["devices"] if d.get("poolUID") == uid] == \
         [d["uuid"] for d in k.get(MI355XPOOLS, "p", "default")["status"]["devices"]]
     assert standby.poll() is None
+
+
+def test_deleting_the_lease_never_wedges_the_agents(cluster_factory):
+    """leaseTransitions restarts at 0 in a recreated Lease (an admin's `kubectl delete lease`, a
+    namespace rebuilt): the fencing token also names the Lease's generation, so the agents accept
+    the new leader from epoch 0 instead of refusing every claim as stale."""
+    from gpupool.kube import LEASES
+    lease = ["--leader-elect", "--lease-duration", "2s", "--renew-deadline", "1500ms",
+             "--retry-period", "200ms"]
+    c = cluster_factory(manager_args=lease)
+    k = c.client
+    k.wait_for(LEASES, "gpupool-manager-leader", "gpupool-system",
+               lambda o: bool(o) and bool(o["spec"].get("holderIdentity")), timeout=15, poll=0.05)
+    o = k.create(MI355XPOOLS, mi_pool("p", 1), "default")
+    uid = o["metadata"]["uid"]
+    _converged(c, uid, 1)
+    # bump the epoch so the old generation's is clearly above the new one's 0
+    from gpupool.kube import KubeError
+    bumped = 0
+    while bumped < 3:  # racing the leader's renewals: retry on a resourceVersion conflict
+        cur = k.get(LEASES, "gpupool-manager-leader", "gpupool-system")
+        cur["spec"]["leaseTransitions"] = int(cur["spec"].get("leaseTransitions") or 0) + 1
+        try:
+            k.update(LEASES, cur, "gpupool-system")
+            bumped += 1
+        except KubeError as e:
+            assert e.code == 409, e
+    time.sleep(0.6)  # the leader renews (every 200 ms) and carries the bumped epoch from then on
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 2}}, "default")
+    _converged(c, uid, 2)
+    assert "gpupool_agent_leader_epoch 3" in c.agent_request(NODE, "GET", "/metrics")
+    old_uid = k.get(LEASES, "gpupool-manager-leader", "gpupool-system")["metadata"]["uid"]
+    time.sleep(1.1)  # a later creationTimestamp (one-second resolution)
+    k.delete(LEASES, "gpupool-manager-leader", "gpupool-system")
+    new = k.wait_for(LEASES, "gpupool-manager-leader", "gpupool-system",
+                     lambda x: bool(x) and x["metadata"]["uid"] != old_uid, timeout=15, poll=0.05)
+    assert int(new["spec"].get("leaseTransitions") or 0) == 0
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 3}}, "default")
+    _converged(c, uid, 3)
+    metrics = c.agent_request(NODE, "GET", "/metrics")
+    assert "gpupool_agent_leader_epoch 0" in metrics, metrics[-1500:]  # the new generation's

@@ -19,8 +19,11 @@ def make_agent(tmp_path) -> Agent:
                              probe_sim_ms=0, fsync=False, scrub_interval_s=0))
 
 
-def tok(holder: str, epoch: int) -> dict:
-    return {"x-gpupool-leader": holder, "x-gpupool-leader-epoch": str(epoch)}
+def tok(holder: str, epoch: int, lease: str | None = None) -> dict:
+    h = {"x-gpupool-leader": holder, "x-gpupool-leader-epoch": str(epoch)}
+    if lease is not None:
+        h["x-gpupool-leader-lease"] = lease
+    return h
 
 
 def test_older_epochs_are_refused_and_the_newest_survives_a_restart(tmp_path, native_built):
@@ -58,3 +61,27 @@ def test_a_refused_request_never_reaches_its_handler(tmp_path, native_built):
     assert out[0] == 200 and len(a.records) == 1
     srv.close()
     a.stop()
+
+
+def test_a_recreated_lease_starts_a_new_generation(tmp_path, native_built):
+    """leaseTransitions restarts at 0 when the Lease is deleted and created again: its new leader
+    must be accepted (or no claim would ever pass again), and a leader of the deleted Lease —
+    whatever its epoch — refused."""
+    a = make_agent(tmp_path)
+    old = "2026-10-18T01:00:00Z uid-old"
+    new = "2026-10-18T02:00:00Z uid-new"
+    assert a.check_leader("POST", "/v1/claims", tok("m-a", 5, old)) is None
+    assert a.check_leader("POST", "/v1/claims", tok("m-b", 0, new)) is None  # recreated Lease
+    assert a.leader_fence["leaseUID"] == "uid-new" and a.leader_fence["epoch"] == 0
+    r = a.check_leader("POST", "/v1/release", tok("m-a", 5, old))  # the deleted Lease's leader
+    assert r[0] == 409 and "newer Lease" in json.loads(r[2])["message"]
+    assert a.check_leader("POST", "/v1/release", tok("m-b", 1, new)) is None
+    assert a.check_leader("POST", "/v1/release", tok("m-b", 0, new))[0] == 409  # older epoch
+    # recreated within the same second: told apart by its uid
+    same_sec = "2026-10-18T02:00:00Z uid-newer"
+    assert a.check_leader("POST", "/v1/claims", tok("m-c", 0, same_sec)) is None
+    a.stop()
+    b = make_agent(tmp_path)  # the generation is persisted with the epoch
+    assert b.leader_fence["leaseUID"] == "uid-newer"
+    assert b.check_leader("POST", "/v1/claims", tok("m-b", 1, new))[0] == 409
+    b.stop()
