@@ -299,7 +299,8 @@ def test_paused_leader_resumes_without_split_brain(cluster_factory):
             continue
         if rec.get("ts", 0) > resumed_at and rec.get("logger") == "reconciler":
             acted.append(rec.get("msg"))
-    assert not acted, f"the old leader reconciled after it resumed: {acted}"
+    assert not acted, (f"the old leader reconciled after it resumed: {acted}",
+                       c.log("manager")[-4000:], c.log(f"agent-{NODE}")[-3000:])
 
 
 def test_apiserver_paused_mid_scale_converges(cluster_factory):
