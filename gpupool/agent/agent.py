@@ -1228,6 +1228,12 @@ class Agent:
             cand = [d for uuid, d in self.by_uuid.items()
                     if uuid not in self.records and uuid not in quarantined and d.get("present", True)
                     and (not asic_bad or not asic_bad.get(self._asic_key(d), set()) - {uuid})]
+            no_helper = 0
+            if probe_opts.get("enabled", True) and self.prober.helpers is not None:
+                # a GPU whose probe helper is held back after an exit cannot be probed now:
+                # left out (another GPU, or InsufficientDevices and a retry), not failed
+                ok_cand = [d for d in cand if self.prober.can_probe(d)]
+                no_helper, cand = len(cand) - len(ok_cand), ok_cand
             # claimability under the requesting pool's policy (baseline = now: retired HBM pages
             # and absolute limits count, deltas start at the claim); no partition of the same ASIC
             # may carry a package-level fault (checked above)
@@ -1263,7 +1269,9 @@ class Agent:
             if len(sel) < count:
                 return {"ok": False, "reason": "InsufficientDevices",
                         "message": f"need {count} free healthy GPU(s) on {self.cfg.node}, "
-                                   f"{len(free)} available (all-or-nothing)", "devices": []}
+                                   f"{len(free)} available (all-or-nothing)"
+                                   + (f"; {no_helper} more wait for their probe helper to be "
+                                      f"replaced" if no_helper else ""), "devices": []}
             by_index = {d["index"]: d for d in self.snap["devices"]}
             chosen = [by_index[i] for i in sel]
             if probe_opts.get("enabled", True) and PREWAKE:

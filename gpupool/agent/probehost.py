@@ -773,6 +773,15 @@ class HelperPool:
         if h is not None:
             h.kill(why)
 
+    def available(self, key: str) -> bool:
+        """Can a request for ``key`` be served now or once its helper has started? False while
+        a helper that exited is held back by its respawn backoff."""
+        with self._mu:
+            h = self._helpers.get(key)
+            if h is not None and not h.dead:
+                return True
+            return time.monotonic() >= self._respawn_at.get(key, 0.0)
+
     def alive(self, key: str) -> bool:
         with self._mu:
             h = self._helpers.get(key)

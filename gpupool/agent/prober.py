@@ -102,6 +102,12 @@ class Prober:
             return str(dev.get("hipUUID", "")).lower() in self.ordinals
         return True
 
+    def can_probe(self, dev: dict) -> bool:
+        """False while ``dev``'s probe helper is held back after an exit (respawn backoff): a
+        claim then leaves the GPU out instead of failing it (and quarantining it) for a probe
+        that cannot run."""
+        return self.helpers is None or self.helpers.available(dev["uuid"])
+
     def hip_devices(self) -> int:
         """GPUs this agent holds a HIP context on (in itself or its helpers)."""
         if self.mode == "helper":

@@ -261,3 +261,28 @@ def test_a_helper_whose_init_hangs_is_killed_at_its_ready_timeout():
     why, cause = exits[0]
     assert cause == "timeout" and "not ready within 1.5 s" in why, exits
     assert h.dead and not h.ready_ok
+
+
+def test_a_gpu_whose_helper_is_held_back_is_left_out_not_failed(tmp_path, agents, native_built):
+    """A helper that exited twice in a row is replaced only after a backoff; meanwhile a claim
+    leaves its GPU out (InsufficientDevices naming the helper when nothing else fits) instead of
+    failing — and quarantining — a GPU whose probe could not run."""
+    a = make_agent(tmp_path, count=2)
+    agents.append(a)
+    u0 = next(d["uuid"] for d in a.snap["devices"] if d["index"] == 0)
+    pool = a.prober.helpers
+    pid0 = pool.snapshot()[u0]["pid"]
+    pool.kill(u0, "test kill 1")  # first exit: replaced at once
+    assert wait(lambda: pool.snapshot().get(u0, {}).get("pid") not in (None, pid0)
+                and pool.alive(u0))
+    pool.kill(u0, "test kill 2")  # second within the window: 1 s backoff
+    assert wait(lambda: not pool.available(u0), timeout=5)
+    r = claim(a, count=2)
+    assert not r["ok"] and r["reason"] == "InsufficientDevices", r
+    assert "1 more wait for their probe helper" in r["message"], r
+    r = claim(a, "pool-2", count=1)  # the other GPU is still claimable
+    assert r["ok"] and [d["index"] for d in r["devices"]] == [1], r
+    assert not a.ledger.quarantined()
+    assert wait(lambda: pool.alive(u0), timeout=10)  # replaced after the backoff
+    r = claim(a, "pool-3", count=1)
+    assert r["ok"] and [d["index"] for d in r["devices"]] == [0], r
