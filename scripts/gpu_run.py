@@ -73,6 +73,9 @@ def scenarios(tag_dir: str) -> dict[str, list[tuple]]:
                                           str(g), pmc=("TCC_HIT_sum", "TCC_MISS_sum")), 120, {})
                 for g in (0, 4)],
         "gemm": [("gemm_vs_hipblaslt", [PY, "scripts/gemm_vs_hipblaslt.py"], 300, {})],
+        # the probe's two-stream shape as one hipGraph vs eager launches (r5l: not adopted)
+        "graph": [("graph_events", [os.path.join(ROOT, "build", "native", "graph_events"), "1024",
+                                    "15"], 120, {})],
         "probe": [("probe_report", [PY, "scripts/probe_report.py"], 200, {}),
                   ("probe_size_sweep", [PY, "scripts/probe_size_sweep.py"], 300, {})],
         "footprint": [("helper_footprint", [PY, "scripts/helper_footprint.py", "8"], 240, {}),
