@@ -110,6 +110,8 @@ def facts() -> dict:
 
 def dry_check(argv: list[str]) -> str:
     """'' if the step's program is present and runnable here (without a GPU), else why not."""
+    if argv and argv[0].startswith(ROOT) and not os.access(argv[0], os.X_OK):
+        return f"{os.path.relpath(argv[0], ROOT)} missing (make -C native)"
     scripts = [a for a in argv if a.endswith(".py")]
     for s in scripts:
         path = s if os.path.isabs(s) else os.path.join(ROOT, s)
