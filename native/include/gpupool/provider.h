@@ -157,6 +157,17 @@ class DeviceProvider {
   // Only ``pool_uid``'s GPUs plus the node's free-healthy count (smaller, cheaper answer for the
   // reconcile path). Default: the full view.
   virtual NodeView observe_pool(const std::string& node, const std::string& /*pool_uid*/) { return observe(node); }
+  // Free healthy GPUs of ``node`` for placing a new claim (-1: unreachable). A ranking hint only —
+  // the claim itself is authoritative (InsufficientDevices makes the caller try the next node).
+  // Default: counted from a full observe.
+  virtual int64_t free_capacity(const std::string& node) {
+    NodeView nv = observe(node);
+    if (!nv.reachable) return -1;
+    int64_t free = 0;
+    for (const auto& d : nv.devices)
+      if (d.state == "Free" && d.healthy) ++free;
+    return free;
+  }
   virtual ClaimResult claim(const std::string& node, const ClaimRequest& req) = 0;
   virtual void cordon(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) = 0;
   virtual void release(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) = 0;
@@ -177,6 +188,11 @@ class RocmProvider : public DeviceProvider {
   bool node_schedulable(const std::string& node) override;
   NodeView observe(const std::string& node) override;
   NodeView observe_pool(const std::string& node, const std::string& pool_uid) override;
+  // From the node's last full view (younger than view_max_age) less the GPUs claimed there since
+  // and those claims in flight, so concurrent placements spread instead of all racing for the same
+  // tightest node; a full view (an RPC) only when there is none. Releases and a claim refused for
+  // capacity drop the estimate (the next call asks the agent).
+  int64_t free_capacity(const std::string& node) override;
   ClaimResult claim(const std::string& node, const ClaimRequest& req) override;
   void cordon(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) override;
   void release(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) override;
@@ -230,6 +246,15 @@ class RocmProvider : public DeviceProvider {
   std::map<std::string, uint64_t> answered_;   // RPCs answered (any status), per node
   int view_max_age_ms_ = 5000;
   std::atomic<uint64_t> cache_hits_{0};
+  struct Capacity {
+    bool valid = false;
+    std::chrono::steady_clock::time_point at;  // when the full view it counts was fetched
+    int64_t free = 0;                          // free healthy GPUs in that view
+    int64_t taken = 0;                         // GPUs claimed there since
+    int64_t pending = 0;                       // GPUs of claims in flight there
+  };
+  std::map<std::string, Capacity> cap_;  // under cache_mu_
+  void note_capacity_(const std::string& node, const NodeView& full);  // caller holds cache_mu_
 };
 
 }  // namespace gpupool

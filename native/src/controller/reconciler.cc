@@ -457,11 +457,10 @@ std::vector<std::string> Mi355xPoolReconciler::choose_nodes_(const Mi355xPoolSpe
     for (const auto& kv : spec.node_selector)
       if (labels[kv.first].as_string() != kv.second) match = false;
     if (!match || !provider_.node_schedulable(n)) continue;  // cordoned nodes get no new claims
-    NodeView nv = provider_.observe(n);
-    if (!nv.reachable) continue;
-    int64_t free = 0;
-    for (const auto& d : nv.devices)
-      if (d.state == "Free" && d.healthy) ++free;
+    // an estimate (the agents' last full views less claims made or in flight since): placing 256
+    // pools on 64 nodes at once asked every agent for its full view on every pass, and every
+    // worker raced for the same tightest node (scripts/scale_bench.py, profiles/r5n_*)
+    const int64_t free = provider_.free_capacity(n);
     if (free >= need) fit.push_back({n, free});
   }
   // Tightest fit first (bin-packing keeps whole nodes free for big pools); the caller falls

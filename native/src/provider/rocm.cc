@@ -213,7 +213,44 @@ void RocmProvider::test_pause_after_fence_(const std::string& path) {
   }
 }
 
-NodeView RocmProvider::observe(const std::string& node) { return observe_pool(node, ""); }
+NodeView RocmProvider::observe(const std::string& node) {
+  NodeView nv = observe_pool(node, "");
+  if (nv.reachable) {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    note_capacity_(node, nv);
+  }
+  return nv;
+}
+
+void RocmProvider::note_capacity_(const std::string& node, const NodeView& full) {
+  Capacity& c = cap_[node];
+  c.free = 0;
+  for (const auto& d : full.devices)
+    if (d.state == "Free" && d.healthy) ++c.free;
+  c.taken = 0;  // the view already shows what was claimed before it (pending claims still count)
+  c.at = std::chrono::steady_clock::now();
+  c.valid = true;
+}
+
+int64_t RocmProvider::free_capacity(const std::string& node) {
+  {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    auto it = cap_.find(node);
+    if (it != cap_.end() && it->second.valid &&
+        std::chrono::steady_clock::now() - it->second.at < std::chrono::milliseconds(view_max_age_ms_)) {
+      static CounterVec& hits = Registry::global().counter(
+          "gpupool_capacity_estimate_hits_total", "Placement capacity answered without an agent RPC.");
+      hits.inc({{"node", node}});
+      const Capacity& c = it->second;
+      return std::max<int64_t>(0, c.free - c.taken - c.pending);
+    }
+  }
+  NodeView nv = observe(node);  // refreshes cap_
+  if (!nv.reachable) return -1;
+  std::lock_guard<std::mutex> g(cache_mu_);
+  const Capacity& c = cap_[node];
+  return std::max<int64_t>(0, c.free - c.taken - c.pending);
+}
 
 uint64_t RocmProvider::answered(const std::string& node) {
   std::lock_guard<std::mutex> g(cache_mu_);
@@ -251,6 +288,7 @@ void RocmProvider::prefetch(const std::string& node, int max_wait_ms) {
   std::lock_guard<std::mutex> g(cache_mu_);
   auto lg = latest_gen_.find(node);
   if (epoch_[node] != epoch || (lg != latest_gen_.end() && v.gen < lg->second)) return;  // raced
+  note_capacity_(node, v);
   CachedView& c = cache_[node];
   c.valid = true;
   c.at = std::chrono::steady_clock::now();
@@ -324,9 +362,30 @@ ClaimResult RocmProvider::claim(const std::string& node, const ClaimRequest& req
   body["resourceName"] = req.resource_name;
   body["policy"] = req.policy;
   body["probe"] = req.probe;
+  {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    cap_[node].pending += req.count;
+  }
+  struct Unpend {
+    RocmProvider* p;
+    const std::string& node;
+    int64_t n;
+    ~Unpend() {
+      std::lock_guard<std::mutex> g(p->cache_mu_);
+      p->cap_[node].pending -= n;
+    }
+  } unpend{this, node, req.count};
   Json r = post_(node, "/v1/claims", body);
   ClaimResult out;
   out.ok = r["ok"].as_bool(false);
+  {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    Capacity& c = cap_[node];
+    if (out.ok)
+      c.taken += static_cast<int64_t>(r["devices"].elements().size());
+    else
+      c.valid = false;  // refused (capacity, sharing limits): ask the agent next time
+  }
   out.reason = r["reason"].as_string();
   out.message = r["message"].as_string();
   for (const auto& d : r["devices"].elements()) out.devices.push_back(DeviceView::from(d));
@@ -350,6 +409,8 @@ void RocmProvider::cordon(const std::string& node, const std::string& pool_uid, 
 
 void RocmProvider::release(const std::string& node, const std::string& pool_uid, const std::vector<std::string>& uuids) {
   post_(node, "/v1/release", uuid_body(pool_uid, uuids));
+  std::lock_guard<std::mutex> g(cache_mu_);
+  cap_[node].valid = false;  // GPUs came back (or went to quarantine): count them again
 }
 
 void RocmProvider::update_policy(const std::string& node, const std::string& pool_uid, const Json& policy,

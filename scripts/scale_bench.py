@@ -50,28 +50,39 @@ def proc_usage(pid: int) -> dict:
 
 
 def wait_all(k, names: list[str], pred, t0: float, timeout: float) -> dict[str, float]:
-    """Time at which each pool first satisfied ``pred``, from one watch stream (polling lists of
-    every pool would load the apiserver-sim more than the operator does)."""
+    """Time at which each pool first satisfied ``pred``, from a watch stream (polling lists of
+    every pool would load the apiserver-sim more than the operator does). A watch that ends early
+    (the server closes it, or its resourceVersion is too old) is resumed from a fresh list."""
     done: dict[str, float] = {}
-    lst = k.list(MI355XPOOLS, "default")
-    for o in lst["items"]:
-        if o["metadata"]["name"] in names and pred(o):
-            done[o["metadata"]["name"]] = time.perf_counter() - t0
-    stop = threading.Event()
-    timer = threading.Timer(timeout, stop.set)
-    timer.start()
-    try:
-        for ev in k.watch(MI355XPOOLS, "default", resource_version=lst["metadata"]["resourceVersion"],
-                          timeout_seconds=int(timeout) + 1, stop=stop):
-            o = ev.get("object") or {}
-            n = (o.get("metadata") or {}).get("name")
-            if ev.get("type") in ("ADDED", "MODIFIED") and n in names and n not in done and pred(o):
+    want = set(names)
+    deadline = time.monotonic() + timeout
+    while len(done) < len(want) and time.monotonic() < deadline:
+        lst = k.list(MI355XPOOLS, "default")
+        for o in lst["items"]:
+            n = o["metadata"]["name"]
+            if n in want and n not in done and pred(o):
                 done[n] = time.perf_counter() - t0
-            if len(done) == len(names):
-                break
-    finally:
-        stop.set()
-        timer.cancel()
+        if len(done) == len(want):
+            break
+        stop = threading.Event()
+        timer = threading.Timer(max(0.1, deadline - time.monotonic()), stop.set)
+        timer.start()
+        try:
+            for ev in k.watch(MI355XPOOLS, "default",
+                              resource_version=lst["metadata"]["resourceVersion"],
+                              timeout_seconds=int(deadline - time.monotonic()) + 1, stop=stop):
+                o = ev.get("object") or {}
+                n = (o.get("metadata") or {}).get("name")
+                if ev.get("type") in ("ADDED", "MODIFIED") and n in want and n not in done \
+                        and pred(o):
+                    done[n] = time.perf_counter() - t0
+                if len(done) == len(want):
+                    break
+        except Exception:  # a broken stream: list and watch again
+            time.sleep(0.05)
+        finally:
+            stop.set()
+            timer.cancel()
     return done
 
 

@@ -707,6 +707,18 @@ def test_many_pools_fill_every_gpu_across_nodes(cluster_factory):
     assert sum(1 for o in items if ready_at(1)(o)) == 32, time.monotonic() - t0
     uuids = [o["status"]["devices"][0]["uuid"] for o in items]
     assert len(set(uuids)) == 32
+    # placement spreads concurrent claims by the capacity the manager already committed (claims
+    # made or in flight since each agent's last full view), so few lose a race for a node
+    claims = full_views = 0
+    for i in range(4):
+        m = c.agent_request(f"n{i}", "GET", "/metrics")
+        for line in m.splitlines():
+            if line.startswith('gpupool_agent_rpc_requests_total{path="/v1/claims"}'):
+                claims += int(line.rsplit(" ", 1)[1])
+            if line.startswith('gpupool_agent_rpc_requests_total{path="/v1/node"}'):
+                full_views += int(line.rsplit(" ", 1)[1])
+    print("claim RPCs", claims, "node views", full_views)
+    assert claims <= 32 + 8, claims
     k.create(MI355XPOOLS, mi_pool("extra", 1), "default")
     k.wait_for(MI355XPOOLS, "extra", "default",
                cond_is("Progressing", "False", "InsufficientDevices"), timeout=15)
