@@ -18,6 +18,8 @@ def _count_seconds(v: str) -> tuple[int, float]:
 
 
 def main() -> None:
+    from ..utils import parent_watch
+    parent_watch.start()  # test harness only: exit when the test runner is gone
     # Before anything touches a GPU (amdsmi in the device library, HIP anywhere): the forkserver the
     # probe helpers are forked from, so no helper inherits GPU state (probehost.py).
     from .probehost import start_spawner

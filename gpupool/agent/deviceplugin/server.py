@@ -72,6 +72,11 @@ class DevicePluginServer:
         self._pending: tuple | None = None  # (version, ListAndWatchResponse, healthy uuids)
         self._mark_mu = threading.Lock()
         self._marked = -1
+        # a device list is built and numbered under one lock: two notifies built in one order and
+        # numbered in the other left the NEWEST version carrying the OLDER list — a claim whose
+        # GPUs the other claim's list lacked was never advertised (scripts/scale_bench.py, 128
+        # nodes: concurrent claims on one agent, pools stuck at 0/2 ready)
+        self._build_mu = threading.Lock()
 
     # ------------------------------------------------------------ lifecycle
     def _serve(self) -> None:
@@ -230,16 +235,17 @@ class DevicePluginServer:
         a live kubelet stream will carry the list (ADVERTISE_ON_SUBMIT), else it sends on this
         thread and returns once written. Never before a stream exists: a pod placed on a GPU the
         kubelet has not heard of would fail admission."""
-        resp, healthy = self._devices_msg()
         early = sync and self.ADVERTISE_ON_SUBMIT
-        with self.cv:
-            self.version += 1
-            ver = self.version
-            self._pending = (ver, resp, healthy)
-            live = [st for st in self._live if st.alive]
-            if not sync or early:
-                self._wake = True
-                self.cv.notify_all()
+        with self._build_mu:
+            resp, healthy = self._devices_msg()
+            with self.cv:
+                self.version += 1
+                ver = self.version
+                self._pending = (ver, resp, healthy)
+                live = [st for st in self._live if st.alive]
+                if not sync or early:
+                    self._wake = True
+                    self.cv.notify_all()
         if early:
             if live:
                 self._mark(ver, healthy)

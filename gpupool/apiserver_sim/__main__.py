@@ -9,6 +9,8 @@ from .server import ApiServerSim, serve
 
 
 def main() -> None:
+    from ..utils import parent_watch
+    parent_watch.start()  # test harness only: exit when the test runner is gone
     ap = argparse.ArgumentParser(description="gpupool kube-apiserver simulator")
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=6443)

@@ -12,6 +12,8 @@ from .kubelet import FakeKubelet
 
 
 def main() -> None:
+    from ..utils import parent_watch
+    parent_watch.start()  # test harness only: exit when the test runner is gone
     ap = argparse.ArgumentParser(description="fake kubelet (device plugins + pod runtime)")
     ap.add_argument("--node", required=True)
     ap.add_argument("--apiserver", required=True)

@@ -119,6 +119,9 @@ class Cluster:
         self.env.setdefault("PYTHONPATH", ROOT)
         self.env["PYTHONPATH"] = ROOT + os.pathsep + self.env.get("PYTHONPATH", "")
         self.env.update(env or {})
+        # every daemon started here exits once this process is gone (a runner killed at a
+        # timeout skips the teardown): gpupool/utils/parent_watch.py
+        self.env["GPUPOOL_EXIT_WITH_PARENT"] = str(os.getpid())
         self.sample_interval = sample_interval
         self.fsync = fsync  # agents' ledger fsync (the production default; tests skip it for speed)
         self.kinds = kinds

@@ -60,6 +60,7 @@ class Informer {
   std::vector<Handler> handlers_;
   std::string rv_;
   std::atomic<bool> stop_{false};
+  void backoff_(int ms);  // sleeps ``ms`` unless stop() is called meanwhile
   std::atomic<bool> synced_{false};
   std::atomic<uint64_t> relists_{0};
   std::condition_variable synced_cv_;

@@ -32,6 +32,14 @@ void Informer::stop() {
   if (th_.joinable()) th_.join();
 }
 
+// The retry backoff in slices, so stop() (a SIGTERM with the apiserver unreachable) returns within
+// ~50 ms instead of after a 5 s sleep per informer — the manager took 15 s to exit.
+void Informer::backoff_(int ms) {
+  const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
+  while (!stop_ && std::chrono::steady_clock::now() < until)
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+}
+
 bool Informer::wait_synced(std::chrono::milliseconds timeout) {
   std::unique_lock<std::mutex> lk(mu_);
   // system_clock deadline: see WorkQueue::get_for (TSan-visible pthread_cond_timedwait)
@@ -157,12 +165,12 @@ void Informer::run_() {
       }
       log_.warn("list/watch failed", Json::object().set("error", e.what()).set("backoffMs", backoff_ms));
       need_list = true;
-      std::this_thread::sleep_for(std::chrono::milliseconds(backoff_ms));
+      backoff_(backoff_ms);
       backoff_ms = std::min(backoff_ms * 2, 5000);
     } catch (const std::exception& e) {
       log_.warn("list/watch transport error", Json::object().set("error", e.what()).set("backoffMs", backoff_ms));
       need_list = true;
-      std::this_thread::sleep_for(std::chrono::milliseconds(backoff_ms));
+      backoff_(backoff_ms);
       backoff_ms = std::min(backoff_ms * 2, 5000);
     }
   }

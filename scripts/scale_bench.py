@@ -147,7 +147,29 @@ def main() -> int:
         up_t = wait_all(k, names, ready(a.replicas), t0, a.timeout)
         u1 = proc_usage(mgr)
         placed: dict[str, int] = {}
+        stuck = []
         for o in k.list(MI355XPOOLS, "default")["items"]:
+            if o["metadata"]["name"] not in up_t and len(stuck) < 5:  # diagnostics
+                st = o.get("status") or {}
+                entry = {"pool": o["metadata"]["name"],
+                         "conditions": {x["type"]: [x["status"], x.get("reason"),
+                                                    (x.get("message") or "")[:200]]
+                                        for x in st.get("conditions", [])},
+                         "status_devices": st.get("devices")}
+                node = st.get("nodeName")
+                if node:
+                    try:
+                        view = c.agent_request(node, "GET", "/v1/node")
+                        entry["agent_devices"] = [d for d in view.get("devices", [])
+                                                  if d.get("poolUID") == o["metadata"]["uid"]]
+                        entry["agent_gen"] = view.get("gen")
+                        m = c.agent_request(node, "GET", "/metrics")
+                        entry["agent_metrics"] = [ln for ln in m.splitlines()
+                                                  if "plugin" in ln or "stream" in ln
+                                                  or "advert" in ln][:20]
+                    except Exception as e:  # noqa: BLE001 - diagnostics only
+                        entry["agent_error"] = repr(e)
+                stuck.append(entry)
             for d in (o.get("status") or {}).get("devices", []):
                 placed[d["node"]] = placed.get(d["node"], 0) + 1
         t1 = time.perf_counter()
@@ -160,6 +182,10 @@ def main() -> int:
             if line.startswith("#") or " " not in line:
                 continue
             name = line.split("{", 1)[0].split(" ", 1)[0]
+            if name == "gpupool_reconcile_total":  # by result as well
+                res = line.split('result="', 1)[1].split('"', 1)[0] if 'result="' in line else "?"
+                metrics["reconcile_" + res] = metrics.get("reconcile_" + res, 0.0) + \
+                    float(line.rsplit(" ", 1)[1])
             if name in ("gpupool_reconcile_total", "gpupool_agent_view_cache_hits_total",
                         "gpupool_reconcile_duration_seconds_sum",
                         "gpupool_reconcile_duration_seconds_count"):
@@ -171,6 +197,7 @@ def main() -> int:
                          "last_s": round(max(up_t.values()), 4) if up_t else None},
                "scale_to_zero": {**pstats(list(down_t.values())), "all_done": len(down_t) == a.pools,
                                  "last_s": round(max(down_t.values()), 4) if down_t else None},
+               "not_ready": stuck,
                "gpus_per_node_used": {"min": min(placed.values()) if placed else 0,
                                       "max": max(placed.values()) if placed else 0,
                                       "nodes_used": len(placed)},
@@ -181,7 +208,9 @@ def main() -> int:
                            "reconcile_s_avg": round(metrics.get("gpupool_reconcile_duration_seconds_sum", 0)
                                                     / max(1, metrics.get(
                                                         "gpupool_reconcile_duration_seconds_count", 0)), 4),
-                           "view_cache_hits": int(metrics.get("gpupool_agent_view_cache_hits_total", 0))},
+                           "view_cache_hits": int(metrics.get("gpupool_agent_view_cache_hits_total", 0)),
+                           "reconciles_by_result": {k2[len("reconcile_"):]: int(v) for k2, v in
+                                                    metrics.items() if k2.startswith("reconcile_")}},
                "host_cpus": os.cpu_count()}
         print(json.dumps(out), flush=True)
         if a.out:

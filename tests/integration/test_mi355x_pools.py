@@ -498,9 +498,11 @@ def test_reconcile_traces(node8):
     assert traces and all(t["key"] == "Mi355xPool/default/tr" for t in traces)
     assert len(claim) == 1, traces
     names = [s["name"] for s in claim[0]["spans"]]
-    for want in ("observe", "agent:GET /v1/node", "agent.claim.select", "agent.claim.probe",
-                 "agent.claim.advertise", "status"):
+    for want in ("observe", "agent.claim.select", "agent.claim.probe", "agent.claim.advertise",
+                 "status"):
         assert want in names, names
+    # the pool's node view: an RPC, or the view cache the agent's event feed keeps fresh
+    assert "agent:GET /v1/node" in names or "agent:view-cache" in names, names
     assert claim[0]["totalMs"] >= max(s["ms"] for s in claim[0]["spans"]) - 1e-6
     assert len(claim[0]["reconcileID"]) == 16
     m = node8.manager_metrics()
