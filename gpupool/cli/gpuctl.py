@@ -349,6 +349,21 @@ def cmd_devices(c: Client, ns: str, args) -> int:
     src = view.get("eventSources") or {}
     print(f"node {view['node']}  backend {view['backend']}  probe {view.get('probeMode')}  "
           f"events {','.join(k for k, v in sorted(src.items()) if v) or '-'}")
+    helpers = view.get("probeHelpers") or {}
+    if helpers:  # the per-GPU probe processes (and the xGMI fabric helper)
+        by_uuid = {d["uuid"]: d.get("index") for d in view["devices"]}
+        up = sum(1 for v in helpers.values() if v.get("alive"))
+        fabric = helpers.get("fabric") or {}
+        line = f"probe helpers {up}/{len(helpers)} up"
+        if fabric:
+            line += (f"  fabric {'up' if fabric.get('alive') else 'DOWN'}"
+                     + (f" (warm {fabric['warmMs']:.0f} ms)" if fabric.get("warmMs") is not None else ""))
+        print(line)
+        for key, v in sorted(helpers.items(), key=lambda kv: str(by_uuid.get(kv[0], kv[0]))):
+            if not v.get("alive") or v.get("lastExit"):
+                who = "fabric" if key == "fabric" else f"gpu {by_uuid.get(key, key)}"
+                print(f"  helper {who}: {'up' if v.get('alive') else 'DOWN'}"
+                      + (f", last exit: {v['lastExit']}" if v.get("lastExit") else ""))
     print(f"{'IDX':<4}{'HIP UUID':<24}{'BDF':<15}{'PART':<5}{'STATE':<12}{'HEALTHY':<8}{'GFX%':<5}"
           f"{'VRAM(GiB)':<11}{'POWER':<7}{'POOL':<24}REASONS")
     for d in sorted(view["devices"], key=lambda x: x.get("index", 0)):
@@ -359,7 +374,8 @@ def cmd_devices(c: Client, ns: str, args) -> int:
         power = "-" if t.get("powerW") is None else f"{t['powerW']}W"
         print(f"{d.get('index', ''):<4}{d.get('hipUUID', ''):<24}{d.get('bdf', ''):<15}"
               f"{(d.get('partition') or {}).get('compute', '-'):<5}"
-              f"{d.get('state', ''):<12}{'yes' if d.get('healthy') else 'NO':<8}{gfx:<5}{vram:<11}"
+              f"{d.get('state', '') + ('!' if d.get('probeOverdue') else ''):<12}"
+              f"{'yes' if d.get('healthy') else 'NO':<8}{gfx:<5}{vram:<11}"
               f"{power:<7}{d.get('pool', '') or '-':<24}"
               f"{'; '.join((d.get('verdict') or {}).get('reasons', []))}")
     for e in view.get("recentEvents") or []:

@@ -49,6 +49,18 @@ def test_probe_crash_is_replaced_and_quarantined_while_the_agent_serves(cluster_
     assert c.procs[f"agent-{NODE}"].poll() is None and c.procs[f"agent-{NODE}"].pid == agent_pid
     metrics = c.agent_request(NODE, "GET", "/metrics")
     assert "gpupool_agent_probe_helper_crashes_total 1" in metrics
+    # an admin sees the helpers and the crashed one's last exit
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTHONPATH=c.env["PYTHONPATH"], GPUPOOL_APISERVER=c.url,
+               GPUPOOL_AGENT_TOKEN_FILE=c.agent_token_file)
+    r = subprocess.run([sys.executable, "-m", "gpupool.cli", "devices", NODE], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "probe helpers 4/5 up" in r.stdout or "probe helpers 5/5 up" in r.stdout, r.stdout
+    assert "fabric up" in r.stdout, r.stdout
+    assert "helper gpu 0" in r.stdout and "SIGABRT" in r.stdout, r.stdout
 
 
 def test_crash_is_named_on_device_probe_passed(cluster_factory):
