@@ -105,30 +105,51 @@ Json DeviceView::status_json() const {
 }
 
 RocmProvider::RocmProvider(Informer& nodes, int timeout_ms, std::string agent_token, TlsOptions agent_tls)
-    : nodes_(nodes), timeout_ms_(timeout_ms), agent_token_(std::move(agent_token)), agent_tls_(std::move(agent_tls)) {}
+    : nodes_(nodes), timeout_ms_(timeout_ms), agent_token_(std::move(agent_token)), agent_tls_(std::move(agent_tls)) {
+  // the handler first, then the informer's current contents: an update in between is applied by
+  // the handler and then again (same or newer state) by the seed
+  nodes_.add_handler([this](const std::string& type, const Json& obj) { note_node_(type, obj); });
+  for (const auto& n : nodes_.list()) note_node_("ADDED", n);
+}
+
+void RocmProvider::note_node_(const std::string& type, const Json& obj) {
+  const std::string name = obj.path("metadata.name").as_string();
+  if (name.empty()) return;
+  std::lock_guard<std::mutex> g(facts_mu_);
+  if (type == "DELETED") {
+    facts_.erase(name);
+    return;
+  }
+  NodeFacts& f = facts_[name];
+  f.labels = obj.path("metadata.labels").is_object() ? obj.path("metadata.labels") : Json::object();
+  f.schedulable = !obj.path("spec.unschedulable").as_bool(false);
+  f.endpoint = obj.path("metadata.annotations")[gen::kAnnAgentEndpoint].str_or("");
+}
 
 std::vector<std::string> RocmProvider::node_names() {
   std::vector<std::string> out;
-  for (const auto& n : nodes_.list())
-    if (n.path("metadata.annotations")[gen::kAnnAgentEndpoint].is_string()) out.push_back(n.path("metadata.name").as_string());
+  std::lock_guard<std::mutex> g(facts_mu_);
+  for (const auto& kv : facts_)
+    if (!kv.second.endpoint.empty()) out.push_back(kv.first);
   return out;
 }
 
 Json RocmProvider::node_labels(const std::string& node) {
-  auto n = nodes_.get("", node);
-  if (!n) return Json::object();
-  return n->path("metadata.labels");
+  std::lock_guard<std::mutex> g(facts_mu_);
+  auto it = facts_.find(node);
+  return it == facts_.end() ? Json::object() : it->second.labels;
 }
 
 bool RocmProvider::node_schedulable(const std::string& node) {
-  auto n = nodes_.get("", node);
-  return !n || !n->path("spec.unschedulable").as_bool(false);
+  std::lock_guard<std::mutex> g(facts_mu_);
+  auto it = facts_.find(node);
+  return it == facts_.end() || it->second.schedulable;
 }
 
 std::string RocmProvider::endpoint_of(const std::string& node) {
-  auto n = nodes_.get("", node);
-  if (!n) return "";
-  return n->path("metadata.annotations")[gen::kAnnAgentEndpoint].as_string();
+  std::lock_guard<std::mutex> g(facts_mu_);
+  auto it = facts_.find(node);
+  return it == facts_.end() ? "" : it->second.endpoint;
 }
 
 std::shared_ptr<HttpClient> RocmProvider::client_for(const std::string& node) {

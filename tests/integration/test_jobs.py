@@ -462,13 +462,15 @@ def test_gpuctl_get_watch_streams_rows(node8):
     wait_ready(k, "wp", 1)
     proc = subprocess.Popen([os.path.join(ROOT, "bin", "gpuctl"), "--server", node8.url, "get", "mxp",
                              "wp", "-w", "--watch-timeout", "4"], stdout=subprocess.PIPE, text=True)
-    time.sleep(1.0)
+    # the table is printed before the watch starts: change the pool only once it is out (a
+    # loaded host can take more than a second to start the CLI)
+    head = [proc.stdout.readline(), proc.stdout.readline()]
     k.patch(MI355XPOOLS, "wp", {"spec": {"replicas": 3}}, "default")
     wait_ready(k, "wp", 3)
     out, _ = proc.communicate(timeout=30)
-    lines = [x for x in out.splitlines() if x.strip()]
+    lines = [x for x in head + out.splitlines() if x.strip()]
     assert lines[0].startswith("NAME") and "wp" in lines[1]
-    assert any(x.split()[:3] == ["wp", "3", "3"] for x in lines[2:]), out
+    assert any(x.split()[:3] == ["wp", "3", "3"] for x in lines[2:]), "".join(head) + out
 
 
 def test_gpuctl_login_contexts_whoami(node8, tmp_path):
