@@ -56,6 +56,8 @@ def scenarios(tag_dir: str) -> dict[str, list[tuple]]:
         # the headline (BASELINE config 2) as the driver runs it
         "bench": [("bench", _bench("--steps", "20", "--warmup", "3"), 300, {})],
         "soak": [("bench_soak300", _bench("--steps", "300", "--warmup", "3"), 900, {})],
+        "soak600": [("bench_soak600", _bench("--steps", "600", "--warmup", "3", "--budget-s",
+                                             "1100"), 1150, {})],
         # the probe helper's cost: interleaved helper / in-process runs, and the call itself
         "bench-ab": [(f"bench_{m}_{i}", _bench("--steps", "40", "--warmup", "3", "--probe-mode", m),
                       240, {}) for i in (1, 2) for m in ("helper", "inproc")],
