@@ -5,7 +5,9 @@ older list predates would never count as advertised (found by scripts/scale_benc
 pools stuck at 0/2 ready with their GPUs claimed and healthy)."""
 from __future__ import annotations
 
+import random
 import threading
+import time
 
 from gpupool.agent.deviceplugin.server import DevicePluginServer
 
@@ -47,3 +49,38 @@ def test_the_newest_version_carries_the_newest_list(tmp_path):
     assert ver == 2
     assert healthy == {"g0", "g1"}, healthy
     assert sorted(d.ID for d in resp.devices) == ["g0", "g1"]
+
+
+def test_concurrent_notifies_end_on_the_final_state(tmp_path):
+    """Eight claims commit a GPU each and notify at once, with the device-list build descheduled
+    at random points: whatever the interleaving, the newest version lists every GPU."""
+    class Racy(StubAgent):
+        def __init__(self, rng):
+            super().__init__()
+            self.claimed = set()
+            self.rng = rng
+            self.mu = threading.Lock()
+
+        def plugin_devices(self, resource):
+            with self.mu:
+                snap = sorted(self.claimed)
+            time.sleep(self.rng.random() * 0.002)  # descheduled after reading the state
+            return [{"uuid": u, "advertisable": True} for u in snap]
+
+    for seed in range(20):
+        rng = random.Random(seed)
+        agent = Racy(rng)
+        dp = DevicePluginServer(agent, "amd.com/gpu", str(tmp_path))
+
+        def claim(i):
+            time.sleep(rng.random() * 0.001)
+            with agent.mu:
+                agent.claimed.add(f"g{i}")
+            dp.notify()
+        ts = [threading.Thread(target=claim, args=(i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(5)
+        ver, _, healthy = dp._pending
+        assert ver == 8 and healthy == {f"g{i}" for i in range(8)}, (seed, healthy)
