@@ -286,3 +286,22 @@ def test_a_gpu_whose_helper_is_held_back_is_left_out_not_failed(tmp_path, agents
     assert wait(lambda: pool.alive(u0), timeout=10)  # replaced after the backoff
     r = claim(a, "pool-3", count=1)
     assert r["ok"] and [d["index"] for d in r["devices"]] == [0], r
+
+
+def test_an_idle_on_demand_fabric_helper_exits_and_is_not_counted_as_a_crash():
+    """``--probe-fabric-idle S``: the fabric helper (contexts on every GPU) is let go after S idle
+    seconds and started again by the next ring."""
+    from gpupool.agent.probehost import HelperPool
+    devs = [{"uuid": f"g{i}", "index": i} for i in range(2)]
+    pool = HelperPool("sim", sim_ms=1, fabric_idle_s=0.5)
+    try:
+        pool.start(devs)
+        h = pool.fabric(devs)
+        assert h.wait_ready(10)
+        pid = h.pid
+        assert wait(lambda: not pool.alive("fabric"), timeout=10)
+        assert pool.stats["helper_crashes"] == 0 and pool.stats["helper_timeouts"] == 0
+        h2 = pool.fabric(devs)  # the next ring starts it again
+        assert h2.wait_ready(10) and h2.pid != pid
+    finally:
+        pool.stop()
