@@ -122,22 +122,38 @@ class Prober:
             return None
         return (self.helpers.snapshot().get("fabric") or {}).get("warmMs")
 
+    PSS_TTL_S = 60.0
+
     def helpers_mem(self) -> tuple[int, int]:
         """(RSS, PSS) of the probe helpers together, bytes: the isolation's host-memory cost. RSS
-        counts the HIP runtime's shared text once per helper; PSS splits shared pages between the
-        processes that map them (the fair share)."""
-        rss = pss = 0
-        for pid in self.helper_pids():
+        (``statm``: no page walk) is read on every call; PSS — shared pages split between the
+        processes that map them, the fair share — needs ``smaps_rollup``, which walks the helper's
+        page tables under its mmap lock (a probe allocating meanwhile would wait): at most once a
+        minute, so a metrics scrape never stalls a claim."""
+        page = os.sysconf("SC_PAGESIZE")
+        rss = 0
+        pids = self.helper_pids()
+        for pid in pids:
             try:
-                with open(f"/proc/{pid}/smaps_rollup") as f:
-                    for line in f:
-                        if line.startswith("Rss:"):
-                            rss += int(line.split()[1]) << 10
-                        elif line.startswith("Pss:"):
-                            pss += int(line.split()[1]) << 10
+                with open(f"/proc/{pid}/statm") as f:
+                    rss += int(f.read().split()[1]) * page
             except (OSError, ValueError, IndexError):
                 pass
-        return rss, pss
+        now = time.monotonic()
+        cached = getattr(self, "_pss", None)
+        if cached is None or now - cached[0] > self.PSS_TTL_S or cached[2] != pids:
+            pss = 0
+            for pid in pids:
+                try:
+                    with open(f"/proc/{pid}/smaps_rollup") as f:
+                        for line in f:
+                            if line.startswith("Pss:"):
+                                pss += int(line.split()[1]) << 10
+                                break
+                except (OSError, ValueError, IndexError):
+                    pass
+            self._pss = cached = (now, pss, pids)
+        return rss, cached[1]
 
     def prewake(self, devs: list[dict]) -> None:
         """The claim has chosen these GPUs and probes them in ~0.1-0.2 ms (ledger commit first):
