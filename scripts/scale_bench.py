@@ -182,6 +182,10 @@ def main() -> int:
             if line.startswith("#") or " " not in line:
                 continue
             name = line.split("{", 1)[0].split(" ", 1)[0]
+            if name in ("gpupool_reconcile_span_seconds_sum", "gpupool_reconcile_span_seconds_count"):
+                span = line.split('span="', 1)[1].split('"', 1)[0] if 'span="' in line else "?"
+                key = ("span_s_" if name.endswith("_sum") else "span_n_") + span
+                metrics[key] = metrics.get(key, 0.0) + float(line.rsplit(" ", 1)[1])
             if name == "gpupool_reconcile_total":  # by result as well
                 res = line.split('result="', 1)[1].split('"', 1)[0] if 'result="' in line else "?"
                 metrics["reconcile_" + res] = metrics.get("reconcile_" + res, 0.0) + \
@@ -210,7 +214,11 @@ def main() -> int:
                                                         "gpupool_reconcile_duration_seconds_count", 0)), 4),
                            "view_cache_hits": int(metrics.get("gpupool_agent_view_cache_hits_total", 0)),
                            "reconciles_by_result": {k2[len("reconcile_"):]: int(v) for k2, v in
-                                                    metrics.items() if k2.startswith("reconcile_")}},
+                                                    metrics.items() if k2.startswith("reconcile_")},
+                           # where the passes spent their time: span -> [count, total s]
+                           "spans": {k2[len("span_s_"):]: [int(metrics.get("span_n_" + k2[7:], 0)),
+                                                           round(v, 3)]
+                                     for k2, v in metrics.items() if k2.startswith("span_s_")}},
                "host_cpus": os.cpu_count()}
         print(json.dumps(out), flush=True)
         if a.out:
