@@ -765,6 +765,9 @@ class HelperPool:
                     continue
                 if time.monotonic() - h.last_used < self.fabric_idle_s:
                     continue
+                # out of the table first: a ring arriving now starts a fresh helper instead of
+                # being sent to this one while it stops
+                self._helpers.pop("fabric", None)
             h.stop("idle")
 
     def kill(self, key: str, why: str) -> None:
