@@ -11,8 +11,9 @@ left its pool waiting on a ``Probing`` GPU forever. Here:
   * one helper per GPU, started with ``ROCR_VISIBLE_DEVICES=<that GPU's UUID>``: it holds a HIP
     context on its GPU only, and a fault takes down that helper only — probes of the other GPUs go
     on in theirs;
-  * a *fabric* helper that sees all of the node's GPUs runs the xGMI peer ring. It runs one
-    1 MiB warm ring (peer access, ring windows) before it reports ready; on a multi-GPU node it
+  * a *fabric* helper that sees all of the node's GPUs runs the xGMI peer ring. Before it reports
+    ready it enables peer access for every directed GPU pair and allocates the ring windows at the
+    claim-time size (warm rings of every stride); on a multi-GPU node it
     starts with the GPU helpers and is resident — replaced after an exit like them — so no
     multi-GPU claim pays its HIP init; with ``fabric_idle_s`` > 0 it exits after that long idle
     instead and is started again on demand (its contexts cost VRAM on every GPU);
@@ -108,13 +109,33 @@ class _HipKernel:
     def info(self) -> dict:
         return {"devices": self.n, "uuids": self.uuids}
 
+    WARM_RING_BYTES = 16 << 20  # the claim-time ring's size (prober: xgmiBytes default)
+
     def warm_ring(self) -> dict:
-        """One 1 MiB ring over every visible GPU: peer access enabled and the ring windows
-        allocated before the helper says it is ready, so a claim's first ring does neither."""
+        """Before the helper says it is ready: every directed GPU pair's peer access enabled and
+        the ring windows allocated at the claim-time size, so no claim's ring does either. The
+        claims' rings rotate over the least recently checked pairs (agent._ring_order), so over a
+        node's first claims every pair would otherwise pay its first enable inside a claim. Rings
+        of stride s = 1 .. n-1 (each cycle of i -> i+s mod n) cover all n(n-1) directed pairs."""
         if self.n < 2:
             return {}
-        r = self.hp.peer_ring(list(range(self.n)), 1 << 20)
-        return {"passed": bool(r.get("passed")), "links": len(r.get("links") or [])}
+        n, links, ok = self.n, 0, True
+        for stride in range(1, n):
+            seen: set[int] = set()
+            for start in range(n):
+                if start in seen:
+                    continue
+                cycle, i = [], start
+                while i not in seen:
+                    seen.add(i)
+                    cycle.append(i)
+                    i = (i + stride) % n
+                if len(cycle) < 2:
+                    continue
+                r = self.hp.peer_ring(cycle, self.WARM_RING_BYTES)
+                links += len(r.get("links") or [])
+                ok = ok and bool(r.get("passed"))
+        return {"passed": ok, "links": links}
 
     def ordinal(self, hip_uuid: str) -> int:
         o = self.uuids.get(str(hip_uuid or "").lower())
@@ -162,7 +183,7 @@ class _SimKernel:
         return {"devices": self.n, "uuids": {}}
 
     def warm_ring(self) -> dict:
-        return {"passed": True, "links": self.n} if self.n >= 2 else {}
+        return {"passed": True, "links": self.n * (self.n - 1)} if self.n >= 2 else {}
 
     def call(self, op: str, a: dict) -> Any:
         from . import simprobe

@@ -218,7 +218,7 @@ def test_resident_fabric_helper_is_warm_before_ready_and_replaced_after_a_kill()
         pool.start(devs)
         assert wait(lambda: (pool.snapshot().get("fabric") or {}).get("warmMs") is not None)
         first = pool.snapshot()["fabric"]
-        assert first["alive"] and first["warm"] == {"passed": True, "links": 3}, first
+        assert first["alive"] and first["warm"] == {"passed": True, "links": 6}, first  # 3 x 2 pairs
         pool.kill("fabric", "test kill")
         assert wait(lambda: (pool.snapshot().get("fabric") or {}).get("pid") not in (None, first["pid"])
                     and pool.alive("fabric"))
