@@ -36,7 +36,9 @@ from . import simprobe
 log = logging.getLogger("gpupool.agent.prober")
 
 HELPER_MODES = ("helper", "helper-sim")
-DEFAULT_TIMEOUT_S = 10.0  # spec.probe.timeoutSeconds default (schema.py)
+DEFAULT_TIMEOUT_S = 10.0
+# deadline of one xGMI ring (all its links at once: ~1 ms at 16 MiB per link on MI355X)
+RING_TIMEOUT_S = float(os.environ.get("GPUPOOL_XGMI_RING_TIMEOUT_S", "3"))  # spec.probe.timeoutSeconds default (schema.py)
 
 
 class Prober:
@@ -309,7 +311,8 @@ class Prober:
             return {}
         # 16 MiB per link: ~0.25 ms over one xGMI link, enough for a stable GB/s figure
         nbytes = int(opts.get("xgmiBytes") or (16 << 20))
-        timeout = float(opts.get("timeoutSeconds") or DEFAULT_TIMEOUT_S)
+        # a ring of 16 MiB links takes ~1 ms: a hung one is cut long before the probe's deadline
+        timeout = min(float(opts.get("timeoutSeconds") or DEFAULT_TIMEOUT_S), RING_TIMEOUT_S)
         if self.mode in ("inproc",) + HELPER_MODES:
             ring = self._ring_whole(devs, nbytes, timeout)
             if ring is not None:
@@ -352,7 +355,13 @@ class Prober:
         comes back as a check that could not run (XGMIPeerCheckUnavailable, never a replace)."""
         from .probehost import HelperError, HelperTimeout
         try:
-            return self.helpers.fabric(devs).call(op, args, timeout)
+            h = self.helpers.fabric(devs)
+            if self.helpers.resident_fabric and not h.ready.is_set():
+                # the resident helper is (re)starting and warming its rings: this claim does not
+                # wait for it — the check could not run; the next claim or idle recheck rings
+                return {"passed": False, "error": "ProbeUnavailable: the xGMI fabric helper is "
+                                                  "still starting"}
+            return h.call(op, args, timeout)
         except HelperTimeout:
             self.helpers.kill("fabric", f"xGMI {op} missed its {timeout:g} s deadline")
             return {"passed": False, "error": f"ProbeTimeout: xGMI {op} did not finish within "

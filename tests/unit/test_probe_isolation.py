@@ -305,3 +305,26 @@ def test_an_idle_on_demand_fabric_helper_exits_and_is_not_counted_as_a_crash():
         assert h2.wait_ready(10) and h2.pid != pid
     finally:
         pool.stop()
+
+
+def test_a_claim_never_waits_for_a_warming_fabric_helper(monkeypatch):
+    """The resident fabric helper warms (every pair's peer access) before it reports ready; a
+    claim's ring arriving meanwhile reports the check unavailable at once instead of waiting —
+    here the helper's init never finishes at all."""
+    from gpupool.agent import probehost as ph
+    from gpupool.agent.prober import Prober
+    orig = ph.HelperPool._fabric_spec
+    monkeypatch.setattr(ph.HelperPool, "_fabric_spec", lambda self: {**orig(self), "initHang": True})
+    devs = [{"uuid": f"g{i}", "index": i, "hipUUID": f"GPU-{i}"} for i in range(2)]
+    p = Prober("helper-sim", sim_ms=1, devices=devs)
+    try:
+        t0 = time.monotonic()
+        links = p.peer_ring(devs, {"timeoutSeconds": 10})
+        assert time.monotonic() - t0 < 1.0
+        assert set(links) == {"g0", "g1"}
+        for link in links.values():
+            assert not link["passed"] and link["error"].startswith("ProbeUnavailable"), link
+        from gpupool.agent.agent import Agent
+        assert Agent._link_verdict(links["g0"], 0) == "unavailable"  # never a replace
+    finally:
+        p.helpers.stop()
