@@ -299,6 +299,13 @@ def test_paused_leader_resumes_without_split_brain(cluster_factory):
             continue
         if rec.get("ts", 0) > resumed_at and rec.get("logger") == "reconciler":
             acted.append(rec.get("msg"))
+    if acted:  # the whole story for the diagnosis
+        import tempfile
+        d = tempfile.gettempdir()
+        open(os.path.join(d, "paused_leader_manager.log"), "w").write(
+            f"resumed_at {resumed_at}\n" + c.log("manager"))
+        open(os.path.join(d, "paused_leader_standby.log"), "w").write(c.log("manager2"))
+        open(os.path.join(d, "paused_leader_agent.log"), "w").write(c.log(f"agent-{NODE}"))
     assert not acted, (f"the old leader reconciled after it resumed: {acted}",
                        c.log("manager")[-4000:], c.log(f"agent-{NODE}")[-3000:])
 
