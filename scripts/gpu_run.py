@@ -74,6 +74,11 @@ def scenarios(tag_dir: str) -> dict[str, list[tuple]]:
                                           os.path.join(ROOT, "scripts", "gemm_l2_pmc.py"), "8192",
                                           str(g), pmc=("TCC_HIT_sum", "TCC_MISS_sum")), 120, {})
                 for g in (0, 4)],
+        # HBM bytes per probe kernel as the memory system counts them (one TCC group per pass)
+        "probe-pmc": [(f"probe_{c.lower()}", _prof(tag_dir, f"probe_{c.lower()}", PY,
+                                                  os.path.join(ROOT, "scripts", "probe_hbm_pmc.py"),
+                                                  "5", pmc=(c,)), 120, {})
+                      for c in ("FETCH_SIZE", "WRITE_SIZE")],
         "gemm": [("gemm_vs_hipblaslt", [PY, "scripts/gemm_vs_hipblaslt.py"], 300, {})],
         # the probe's two-stream shape as one hipGraph vs eager launches (r5l: not adopted)
         "graph": [("graph_events", [os.path.join(ROOT, "build", "native", "graph_events"), "1024",
