@@ -127,8 +127,10 @@ class Ledger:
         ``flush(seq)``. With ``lock`` (the caller's lock guarding ``claims``; not durable) the map
         is serialised by the writer too, under that lock: a claim hands its record over and probes
         while the writer encodes and fsyncs it."""
-        text = None if lock is not None and not durable else json.dumps(claims, sort_keys=True)
         with self._mu:
+            # encoded and numbered together: two commits racing (callers normally serialise them
+            # under the agent's lock) can never number the older map after the newer one
+            text = None if lock is not None and not durable else json.dumps(claims, sort_keys=True)
             self._seq += 1
             seq = self._seq
             if text is None:
