@@ -373,6 +373,8 @@ def main() -> int:
                     per_n[str(k)]["agent"].update(probe_helpers=fa.get("helpers"),
                                                   helpers_rss_mib=fa["helpers_rss_mib"],
                                                   helpers_pss_mib=fa.get("helpers_pss_mib"))
+                if "fabric_warm" in fa:  # every GPU pair's peer access, before any claim
+                    per_n[str(k)]["agent"]["fabric_warm"] = fa["fabric_warm"]
             if str(k) in errors:
                 per_n[str(k)]["errors"] = errors[str(k)]
                 first = errors[str(k)][0]

@@ -2259,8 +2259,12 @@ class Agent:
                 lines.append(f"gpupool_agent_probe_helpers_rss_bytes {rss}")
                 lines.append(f"gpupool_agent_probe_helpers_pss_bytes {pss}")
                 lines.append(f"gpupool_agent_probe_helpers {len(self.prober.helper_pids())}")
-                if self.prober.fabric_warm_ms is not None:
-                    lines.append(f"gpupool_agent_probe_fabric_warm_ms {self.prober.fabric_warm_ms:.1f}")
+                fab = self.prober.helpers.snapshot().get("fabric") or {}
+                if fab.get("warmMs") is not None:  # the xGMI fabric helper's all-pairs warm-up
+                    warm = fab.get("warm") or {}
+                    lines.append(f"gpupool_agent_probe_fabric_warm_ms {fab['warmMs']:.1f}")
+                    lines.append(f"gpupool_agent_probe_fabric_warm_links {int(warm.get('links') or 0)}")
+                    lines.append(f"gpupool_agent_probe_fabric_warm_passed {int(bool(warm.get('passed')))}")
                 for k, v in self.prober.helpers.stats.items():
                     lines.append(f"gpupool_agent_probe_{k}_total {v}")
                 for k, v in self.prober.helpers.snapshot().items():

@@ -530,6 +530,14 @@ class BenchRun:
                         m = re.search(r"^gpupool_agent_probe_helpers_pss_bytes (\d+)", text, re.M)
                         if m:
                             out[who]["helpers_pss_mib"] = round(int(m.group(1)) / 2**20, 1)
+                        # the xGMI fabric helper's warm-up over every directed GPU pair (2+ GPUs)
+                        fw = {k: re.search(rf"^gpupool_agent_probe_fabric_warm_{k} ([0-9.]+)",
+                                           text, re.M) for k in ("ms", "links", "passed")}
+                        if fw["ms"]:
+                            out[who]["fabric_warm"] = {
+                                "ms": float(fw["ms"].group(1)),
+                                "links": int(float(fw["links"].group(1))) if fw["links"] else None,
+                                "passed": fw["passed"].group(1) == "1" if fw["passed"] else None}
                         m = re.search(r"^gpupool_agent_probe_helpers (\d+)", text, re.M)
                         out[who]["helpers"] = int(m.group(1)) if m else None
                     out[who]["vram_used_mib"] = {
