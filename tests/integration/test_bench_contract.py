@@ -43,8 +43,8 @@ def test_bench_gpus8_sweep_scale_down_two_pools(native_built):
         assert v["truth_first_read_agrees"] == 1.0, (k, v)
     assert out["value"] == cfg["per_n"]["8"]["p50_s"]
     # the xGMI fabric helper warmed every directed pair of the 8 GPUs before any claim
-    assert cfg["per_n"]["8"]["agent"]["fabric_warm"] == {"ms": 0.0, "links": 56, "passed": True} \
-        or cfg["per_n"]["8"]["agent"]["fabric_warm"]["links"] == 56
+    fw = cfg["per_n"]["8"]["agent"]["fabric_warm"]
+    assert fw["links"] == 8 * 7 and fw["passed"], fw
     # device-level evidence per N: every claim's probe, and the xGMI ring of every multi-GPU
     # claim (N links per claim of N GPUs), with the pair coverage the rotating order reached
     for k, v in cfg["per_n"].items():
