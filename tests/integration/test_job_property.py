@@ -9,6 +9,7 @@ scenario runs and after it settles:
 """
 from __future__ import annotations
 
+import os
 import time
 
 import pytest
@@ -21,6 +22,9 @@ from gpupool.testing.cluster import Cluster, NodeSpec
 from .helpers import mi_pool, wait_ready
 
 pytestmark = pytest.mark.slow
+
+# more examples for a deeper search: GPUPOOL_PROPERTY_SCALE=5 python -m pytest ...
+SCALE = max(1, int(os.environ.get("GPUPOOL_PROPERTY_SCALE", "1")))
 RES = "amd.com/gpu"
 CAP = 6
 
@@ -52,7 +56,7 @@ def check_capacity(k, seen_reasons: set) -> None:
     assert used <= alloc, (used, alloc)
 
 
-@settings(max_examples=12, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
+@settings(max_examples=12 * SCALE, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
                                                                  HealthCheck.too_slow])
 @given(ops=ops)
 def test_gang_scheduler_invariants(shared, ops):

@@ -7,6 +7,7 @@ faults on two pools sharing one 8-GPU node. After faults clear and the system se
 """
 from __future__ import annotations
 
+import os
 import time
 
 import pytest
@@ -19,6 +20,9 @@ from gpupool.testing.cluster import Cluster, NodeSpec
 from .helpers import mi_pool, ready_at, settled_pools
 
 pytestmark = pytest.mark.slow
+
+# more examples for a deeper search: GPUPOOL_PROPERTY_SCALE=5 python -m pytest ...
+SCALE = max(1, int(os.environ.get("GPUPOOL_PROPERTY_SCALE", "1")))
 
 op = st.one_of(
     st.tuples(st.just("scale"), st.sampled_from(["pa", "pb"]), st.integers(0, 6)),
@@ -42,7 +46,7 @@ FAULTS = {"ecc": {"ecc": {"uncorrectable": 1}},
           "thermal": {"temps": {"hotspot": {"current": 110}}}}
 
 
-@settings(max_examples=8, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
+@settings(max_examples=8 * SCALE, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
                                                                  HealthCheck.too_slow])
 @given(ops=st.lists(op, min_size=1, max_size=6), final=st.tuples(st.integers(0, 4),
                                                                   st.integers(0, 4)))
@@ -111,7 +115,7 @@ def two_nodes(tmp_path_factory, native_built):
     c.stop()
 
 
-@settings(max_examples=6, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
+@settings(max_examples=6 * SCALE, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
                                                                  HealthCheck.too_slow])
 @given(ops=st.lists(span_op, min_size=1, max_size=6),
        final=st.tuples(st.integers(0, 5), st.integers(0, 3)))
@@ -178,7 +182,7 @@ def chaos(tmp_path_factory, native_built):
     c.stop()
 
 
-@settings(max_examples=5, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
+@settings(max_examples=5 * SCALE, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
                                                                  HealthCheck.too_slow])
 @given(ops=st.lists(chaos_op, min_size=2, max_size=7), final=st.integers(0, 5))
 def test_restarts_and_pods_never_strand_a_pod(chaos, ops, final):
@@ -251,7 +255,7 @@ def outage(tmp_path_factory, native_built):
     c.stop()
 
 
-@settings(max_examples=6, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
+@settings(max_examples=6 * SCALE, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture,
                                                                  HealthCheck.too_slow])
 @given(ops=st.lists(outage_op, min_size=3, max_size=9), final=st.integers(1, 4))
 def test_agent_outages_never_leak_or_double_claim(outage, ops, final):
