@@ -291,17 +291,23 @@ def test_paused_leader_resumes_without_split_brain(cluster_factory):
     assert leader.poll() is not None, "the resumed old leader kept running after losing its lease"
     assert standby.poll() is None
     import json as _json
-    acted = []
+    # A pass that began before the pause may finish after it (a claim sent just before SIGSTOP
+    # took hold is answered while the process is stopped and logged on resume): that work was
+    # done as the leader. What must not happen is a pass that STARTS after the resume acting.
+    recs = []
     for line in c.log("manager").splitlines():
         try:
-            rec = _json.loads(line)
+            recs.append(_json.loads(line))
         except ValueError:
             continue
-        # "pool ready" is logged after the status PUT returns: a PUT the server committed before
-        # the pause (the test saw Ready and paused at once) is logged when the thread resumes
-        if rec.get("ts", 0) > resumed_at and rec.get("logger") == "reconciler" and \
-                rec.get("msg") != "pool ready":
-            acted.append(rec.get("msg"))
+    started = {r.get("reconcileID"): float(r.get("start", 0)) for r in recs
+               if r.get("msg") == "reconcile trace" and r.get("reconcileID")}
+    acted = [r.get("msg") for r in recs
+             if r.get("logger") == "reconciler" and r.get("ts", 0) > resumed_at
+             # "pool ready" is logged when a status PUT returns: one the server committed
+             # before the pause is logged on resume
+             and r.get("msg") != "pool ready"
+             and started.get(r.get("reconcileID"), r.get("ts", 0)) > resumed_at]
     if acted:  # the whole story for the diagnosis
         import tempfile
         d = tempfile.gettempdir()
