@@ -1297,14 +1297,17 @@ std::string run_peer_ring(const std::vector<int>& devs, const char* opts) {
     (void)hipGetLastError();  // clear a sticky "already enabled"
   }
   auto seed_of = [](int dev) { return 0x5EED0000u + static_cast<uint32_t>(dev) * 0x9E37u; };
-  for (int d : uniq) {  // 1. each source device writes its pattern once
+  for (int d : uniq) {  // 1. each source device writes its pattern once, all devices at once
     DeviceCtx& c = g_ctx[static_cast<size_t>(d)];
     PROBE_CHECK(hipSetDevice(d));
     const int grid = std::min<int>(c.prop.multiProcessorCount, static_cast<int>((n16 + kHbmThreads - 1) / kHbmThreads));
     hipLaunchKernelGGL(hbm_fill<>, dim3(grid), dim3(kHbmThreads), 0, c.stream, static_cast<u32x4*>(c.peer_send), n16,
                        seed_of(d), 0u, static_cast<unsigned long long*>(nullptr), 0);
     PROBE_CHECK(hipGetLastError());
-    PROBE_CHECK(hipStreamSynchronize(c.stream));  // the fill is ~10 us; copies below must see it
+  }
+  for (int d : uniq) {  // the copies below read other devices' windows: every fill must be done
+    PROBE_CHECK(hipSetDevice(d));
+    PROBE_CHECK(hipStreamSynchronize(g_ctx[static_cast<size_t>(d)].stream));
   }
   // 2. all links at once, each timed on its source's stream. A source with two outgoing links
   // (only with repeated devices) times them back to back on its one stream.
