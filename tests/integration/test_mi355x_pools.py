@@ -851,6 +851,9 @@ def test_cordoned_node_takes_no_new_claims(cluster_factory):
     k.create(MI355XPOOLS, mi_pool("held", 1, nodeName="node-a"), "default")
     wait_ready(k, "held", 1)
     k.patch(NODES, "node-a", {"spec": {"unschedulable": True}}, None)
+    # the manager learns of the cordon through its Node watch, asynchronously (as after a
+    # `kubectl cordon`): a pool created in the same instant may still be placed on the node
+    time.sleep(0.5)
     k.create(MI355XPOOLS, mi_pool("free", 2), "default")
     o = wait_ready(k, "free", 2)
     assert o["status"]["nodeName"] == "node-b"
