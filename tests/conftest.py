@@ -22,6 +22,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: multi-second integration test")
 
 
+@pytest.hookimpl(hookwrapper=True)
+def pytest_runtest_makereport(item, call):
+    outcome = yield
+    rep = outcome.get_result()
+    setattr(item, "rep_" + rep.when, rep)
+
+
 def make_native(target: str, san: str = "", timeout: float | None = None):
     """``make -C native`` under an exclusive file lock: pytest-xdist workers share one build tree,
     and a worker relinking a binary another worker is executing fails that exec (ETXTBSY/EACCES)."""
@@ -45,8 +52,10 @@ def native_built():
 
 
 @pytest.fixture
-def cluster_factory(tmp_path, native_built):
-    """Start local control planes; all are stopped at test teardown."""
+def cluster_factory(request, tmp_path, native_built):
+    """Start local control planes; all are stopped at test teardown. A failed test's cluster logs
+    are copied to ``$GPUPOOL_FAILED_LOGS`` (default /tmp/gpupool-failed/<test>): pytest rotates its
+    tmp dirs away after three sessions, and a rare flake is only diagnosable from its own logs."""
     from gpupool.testing.cluster import Cluster
     made = []
 
@@ -58,3 +67,15 @@ def cluster_factory(tmp_path, native_built):
     yield make
     for c in made:
         c.stop()
+    rep = getattr(request.node, "rep_call", None)
+    if made and rep is not None and rep.failed:
+        import re
+        import shutil
+        dest = os.path.join(os.environ.get("GPUPOOL_FAILED_LOGS", "/tmp/gpupool-failed"),
+                            re.sub(r"[^A-Za-z0-9_.-]+", "_", request.node.nodeid))
+        for i, c in enumerate(made):
+            shutil.copytree(c.workdir, os.path.join(dest, f"cluster{i}"), dirs_exist_ok=True,
+                            ignore=lambda d, names: [n for n in names
+                                                     if not n.endswith((".log", ".json"))
+                                                     and not os.path.isdir(os.path.join(d, n))])
+        sys.stderr.write(f"\ncluster logs of the failed test kept in {dest}\n")
