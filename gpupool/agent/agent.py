@@ -2083,6 +2083,11 @@ class Agent:
                 older_lease = created < cur_c or (uid != cur_u and uid in retired)
                 newer_lease = not older_lease and (
                     created > cur_c or (created == cur_c and uid != cur_u))
+            elif created and cur_e >= 0:
+                # a fence persisted before tokens carried the Lease generation: a Lease created
+                # after that fence was recorded is a newer one (else its epoch, restarted at 0,
+                # would be refused for good)
+                newer_lease = created > str(cur.get("at", ""))
             stale = older_lease or (not newer_lease and (
                 epoch < cur_e or (epoch == cur_e and cur_h and holder != cur_h)))
             if stale:

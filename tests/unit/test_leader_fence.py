@@ -85,3 +85,19 @@ def test_a_recreated_lease_starts_a_new_generation(tmp_path, native_built):
     assert b.leader_fence["leaseUID"] == "uid-newer"
     assert b.check_leader("POST", "/v1/claims", tok("m-b", 1, new))[0] == 409
     b.stop()
+
+
+def test_a_fence_from_before_lease_generations_accepts_a_later_lease(tmp_path, native_built):
+    """A fence persisted by an agent that predates the Lease-generation header has no generation
+    to compare: a token whose Lease was created after that fence was recorded is a recreated Lease
+    (its epoch restarted at 0) and is accepted; one created before it keeps the epoch order."""
+    a = make_agent(tmp_path)
+    assert a.check_leader("POST", "/v1/claims", tok("m-a", 5)) is None  # no generation
+    assert "leaseCreated" not in a.leader_fence
+    r = a.check_leader("POST", "/v1/claims", tok("m-x", 0, "2000-01-01T00:00:00Z uid-older"))
+    assert r[0] == 409
+    assert a.check_leader("POST", "/v1/claims", tok("m-b", 0, "2999-01-01T00:00:00Z uid-new")) is None
+    assert a.leader_fence["leaseUID"] == "uid-new" and a.leader_fence["epoch"] == 0
+    # the Lease before it, whatever its epoch, is now the older generation
+    assert a.check_leader("POST", "/v1/release", tok("m-a", 5, "2000-01-01T00:00:00Z uid-older"))[0] == 409
+    a.stop()
