@@ -201,7 +201,8 @@ def test_manager_kills_while_gangs_are_created(cluster_factory):
     wait_ready(k, "pool", 8)
     sizes = {}
     for j in range(3):
-        n = rng.choice([1, 2, 3])
+        # the three gangs must fit the pool's 8 GPUs together (3+3+3 would leave one unschedulable)
+        n = min(rng.choice([1, 2, 3]), 8 - sum(sizes.values()) - (2 - j))
         sizes[f"j{j}"] = n
         k.create(MI355XJOBS, {
             "apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xJob",
