@@ -65,6 +65,7 @@ class RunningPod:
     log_path: str = ""
     restarts: int = 0
     terminating: bool = False
+    running_written: bool = False  # its Running status is in the API: the exit may be reported
 
 
 class FakeKubelet:
@@ -88,6 +89,10 @@ class FakeKubelet:
         self.host_paths = [os.path.abspath(p) for p in host_paths] if host_paths else None
         self.plugins: dict[str, PluginConn] = {}
         self.pods: dict[str, RunningPod] = {}          # pod uid -> running pod
+        # pods whose containers already ran to completion: an event that still shows one of them
+        # Running (the watch delivers it between the exit and the Succeeded status write) must
+        # not admit it again — a pod's containers run once (restartPolicy Never / OnFailure)
+        self.finished: set[str] = set()
         self.assigned: dict[str, str] = {}             # device ID -> pod uid
         self.lock = threading.RLock()
         # serialises node-status snapshots with their PATCH: two ListAndWatch streams updating at
@@ -272,6 +277,7 @@ class FakeKubelet:
                     listed = {p["metadata"]["uid"] for p in lst["items"]}
                     with self.lock:
                         gone = [u for u in self.pods if u not in listed]
+                        self.finished &= listed
                     for u in gone:
                         self._forget(u)
                     rv = lst["metadata"]["resourceVersion"]
@@ -320,7 +326,7 @@ class FakeKubelet:
             return
         phase = pod.get("status", {}).get("phase", "Pending")
         with self.lock:
-            known = uid in self.pods
+            known = uid in self.pods or uid in self.finished
         if known or phase in ("Succeeded", "Failed"):
             return
         self._admit(pod)
@@ -425,15 +431,20 @@ class FakeKubelet:
                 ns=rp.ns)
         except KubeError:
             pass
-        self._set_status(rp.ns, rp.name, "Running", ready=True, extra={
-            "podIP": "127.0.0.1", "hostIP": "127.0.0.1", "startTime": now_rfc3339()})
+        try:
+            self._set_status(rp.ns, rp.name, "Running", ready=True, extra={
+                "podIP": "127.0.0.1", "hostIP": "127.0.0.1", "startTime": now_rfc3339()})
+        finally:
+            rp.running_written = True
 
     def _reaper(self) -> None:
         while not self.stop_ev.wait(0.1):
             with self.lock:
                 pods = list(self.pods.values())
             for rp in pods:
-                if rp.proc is None or rp.terminating:
+                # a container that exits before its Running status is written is reported after it,
+                # so the pod's phase never goes back from Succeeded/Failed to Running
+                if rp.proc is None or rp.terminating or not rp.running_written:
                     continue
                 rc = rp.proc.poll()
                 if rc is None:
@@ -442,6 +453,7 @@ class FakeKubelet:
                 with self.lock:
                     self._free(rp)
                     self.pods.pop(rp.uid, None)
+                    self.finished.add(rp.uid)
                 self._set_status(rp.ns, rp.name, phase, ready=False, exit_code=rc)
                 log.info("pod %s/%s exited %d", rp.ns, rp.name, rc)
 
@@ -477,6 +489,7 @@ class FakeKubelet:
 
     def _forget(self, uid: str) -> None:
         with self.lock:
+            self.finished.discard(uid)
             rp = self.pods.pop(uid, None)
             if rp:
                 self._kill(rp, 0)

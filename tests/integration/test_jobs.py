@@ -237,6 +237,28 @@ def test_gpuctl_trainjob_verbs(node8, tmp_path):
     k.wait_for(MI355XJOBS, "bare", "default", lambda o: o is None, timeout=30)
 
 
+def test_a_container_that_exits_at_once_runs_once_and_stays_succeeded(node8):
+    """A container that exits before its pod's Running status is written: the exit is reported
+    after it (the phase never goes back from Succeeded to Running, which made the job's cleanup
+    delete the finished pod), and the pod is not admitted again by a watch event that still shows
+    it Pending/Running (its log would then hold the output twice)."""
+    k = node8.client
+    k.create(MI355XPOOLS, mi_pool("pool", 8), "default")
+    wait_ready(k, "pool", 8)
+    names = [f"quick-{i}" for i in range(8)]
+    for n in names:
+        k.create(MI355XJOBS, job(n, 1, ["echo", f"ran-{n}"], poolRef="pool"), "default")
+    for n in names:
+        k.wait_for(MI355XJOBS, n, "default", phase_is("Succeeded"), timeout=30)
+    time.sleep(0.5)  # a late Running write or a second run would show by now
+    for n in names:
+        pods = job_pods(k, n)
+        assert len(pods) == 1 and pods[0]["status"]["phase"] == "Succeeded", (n, pods)
+        log_path = pods[0]["metadata"]["annotations"]["gpupool.amd.com/log-path"]
+        with open(log_path) as f:
+            assert f.read().split() == [f"ran-{n}"], n
+
+
 def test_priority_preemption_picks_fewest_lowest_victims(node8):
     """Volcano preempt / PriorityClass semantics: a PreemptLowerPriority gang that does not fit
     stops only the lowest-priority jobs it needs, holds its reservation until their pods are gone,
