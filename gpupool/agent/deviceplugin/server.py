@@ -121,7 +121,7 @@ class DevicePluginServer:
                                         name=f"dp-send-{self.resource}")
         self._sender.start()
         self._streams_lost = False
-        self._kch = None
+        self._kch, self._kcb = None, None
         self.register()  # synchronous first registration; the monitor handles kubelet restarts
         self._mon = threading.Thread(target=self._monitor_kubelet, daemon=True,
                                      name=f"dp-mon-{self.resource}")
@@ -143,7 +143,7 @@ class DevicePluginServer:
                 pass
         kch = getattr(self, "_kch", None)
         if kch is not None:
-            kch.close()
+            self._retire_channel(kch, self._kcb)
         if self.server:
             self.server.stop(grace=0.5)
         try:
@@ -176,7 +176,7 @@ class DevicePluginServer:
         inode within one ctime tick (tmpfs). So a channel to the kubelet is also kept connected:
         when it drops out of READY the kubelet went away, and the monitor re-registers once a
         kubelet answers again. No idle timeout: a quiet kubelet is not a restarted one."""
-        old = getattr(self, "_kch", None)
+        old, old_cb = getattr(self, "_kch", None), getattr(self, "_kcb", None)
         ch = fresh_channel(ksock, [("grpc.client_idle_timeout_ms", 2**31 - 1)])
         was_ready = [False]
 
@@ -188,10 +188,24 @@ class DevicePluginServer:
             elif was_ready[0]:
                 was_ready[0] = False
                 self._streams_lost = True
-        self._kch = ch
+        self._kch, self._kcb = ch, on_state
         ch.subscribe(on_state, try_to_connect=True)
         if old is not None:
-            old.close()
+            self._retire_channel(old, old_cb)
+
+    @staticmethod
+    def _retire_channel(ch, cb) -> None:
+        """Unsubscribe, then close once gRPC's connectivity-polling thread has seen that nothing is
+        subscribed (it re-checks every 0.2 s): closing a channel under that thread makes its next
+        poll raise 'Cannot monitor channel state: Channel closed!' and die with a traceback."""
+        if cb is not None:
+            try:
+                ch.unsubscribe(cb)
+            except Exception:
+                pass
+        t = threading.Timer(0.5, ch.close)
+        t.daemon = True
+        t.start()
 
     def _monitor_kubelet(self) -> None:
         ksock = os.path.join(self.plugin_dir, KUBELET_SOCKET)

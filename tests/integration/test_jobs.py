@@ -107,8 +107,12 @@ def test_gang_is_all_or_nothing_and_queue_is_ordered(node8):
     for n in ("a", "b", "c"):
         o = k.wait_for(MI355XJOBS, n, "default", phase_is("Succeeded", "Failed"), timeout=60)
         assert o["status"]["phase"] == "Succeeded", (n, o["status"])
-    start = {n: k.get(MI355XJOBS, n, "default")["status"]["startTime"] for n in ("a", "b", "c")}
-    assert start["a"] <= start["b"] <= start["c"]
+    # queue order is placement order (GangScheduled events, resourceVersion order): startTime is
+    # when every worker runs, and c's one pod can be Running before both of b's placed beside it
+    evs = sorted(settled_events(k), key=lambda e: int(e["metadata"]["resourceVersion"]))
+    placed = [e["involvedObject"]["name"] for e in evs
+              if e["reason"] == "GangScheduled" and e["involvedObject"]["name"] in ("a", "b", "c")]
+    assert placed.index("a") < placed.index("b") < placed.index("c"), placed
     # a higher priority jumps the queue
     k.create(MI355XJOBS, job("hold", 3, ["sleep", "2"]), "default")
     k.wait_for(MI355XJOBS, "hold", "default", phase_is("Running"), timeout=30)
