@@ -65,17 +65,33 @@ def cluster_factory(request, tmp_path, native_built):
         c.start()
         return c
     yield make
-    for c in made:
-        c.stop()
     rep = getattr(request.node, "rep_call", None)
     if made and rep is not None and rep.failed:
-        import re
-        import shutil
-        dest = os.path.join(os.environ.get("GPUPOOL_FAILED_LOGS", "/tmp/gpupool-failed"),
-                            re.sub(r"[^A-Za-z0-9_.-]+", "_", request.node.nodeid))
-        for i, c in enumerate(made):
+        _keep_cluster_logs(request.node.nodeid, made)
+    for c in made:
+        c.stop()
+
+
+def _keep_cluster_logs(nodeid: str, clusters: list) -> None:
+    """Copy the control planes' logs and the pods' logs (under the kubelets' socket dirs, which
+    ``Cluster.stop`` removes) before the clusters are stopped."""
+    import re
+    import shutil
+    dest = os.path.join(os.environ.get("GPUPOOL_FAILED_LOGS", "/tmp/gpupool-failed"),
+                        re.sub(r"[^A-Za-z0-9_.-]+", "_", nodeid))
+
+    def only_logs(d, names):
+        return [n for n in names if not n.endswith((".log", ".json"))
+                and not os.path.isdir(os.path.join(d, n))]
+    for i, c in enumerate(clusters):
+        try:
             shutil.copytree(c.workdir, os.path.join(dest, f"cluster{i}"), dirs_exist_ok=True,
-                            ignore=lambda d, names: [n for n in names
-                                                     if not n.endswith((".log", ".json"))
-                                                     and not os.path.isdir(os.path.join(d, n))])
-        sys.stderr.write(f"\ncluster logs of the failed test kept in {dest}\n")
+                            ignore=only_logs)
+            for node in c.nodes:
+                pods = os.path.join(c.kubelet_root(node), "pod-logs")
+                if os.path.isdir(pods):
+                    shutil.copytree(pods, os.path.join(dest, f"cluster{i}", f"pod-logs-{node.name}"),
+                                    dirs_exist_ok=True)
+        except OSError as e:
+            sys.stderr.write(f"\nkeeping cluster logs failed: {e}\n")
+    sys.stderr.write(f"\ncluster logs of the failed test kept in {dest}\n")
