@@ -20,16 +20,19 @@ from .helpers import conds, mi_pool, settled_events, wait_ready
 pytestmark = pytest.mark.slow
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-# per-process base: pytest-xdist workers each run their own copy of this module, so a fixed base
-# would hand two concurrently running DDP jobs the same rendezvous port
-_port = [29600 + 200 * (int(os.environ.get("PYTEST_XDIST_WORKER", "gw0")[2:] or 0) % 40)]
+def _free_port() -> int:
+    """A rendezvous port no other DDP job on this host holds: pods run as host processes, and
+    fixed per-worker bases collided between two test sessions running at once."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def job(name: str, replicas: int, command: list[str], gpus: int = 1, **spec) -> dict:
-    _port[0] += 1
     return {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xJob",
             "metadata": {"name": name},
-            "spec": {"replicas": replicas, "gpusPerReplica": gpus, "masterPort": _port[0],
+            "spec": {"replicas": replicas, "gpusPerReplica": gpus, "masterPort": _free_port(),
                      "template": {"spec": {"terminationGracePeriodSeconds": 1,
                                            "containers": [{"name": "main", "command": command}]}},
                      **spec}}
@@ -559,7 +562,6 @@ def test_reference_job_manifests_apply_unchanged(node8, tmp_path):
     ct["command"], ct["args"] = train, []
     pt = yaml.safe_load(open(os.path.join(ROOT, "config", "samples", "foreign",
                                           "kubeflow_pytorchjob.yaml")))
-    _port[0] += 1
     for spec in pt["spec"]["pytorchReplicaSpecs"].values():
         spec["template"]["spec"]["containers"][0]["command"] = train
     files = []
