@@ -212,7 +212,10 @@ class Agent:
         self.gen_cv = threading.Condition()  # /v1/events long-polls wait here for a new gen
         self.rpc = None                      # the RPC server (its per-path timings in /metrics)
         self.advertised: dict[str, set[str]] = {}
-        self._adv_event = threading.Event()
+        # advertised-set generation: a waiter reads it before checking and sleeps only until it
+        # moves (a shared Event cleared by one claim's waiter could hide a mark from another's)
+        self._adv_cv = threading.Condition()
+        self._adv_gen = 0
         self.plugins: dict = {}
         self.probe_mode = cfg.probe_mode or default_mode(self.backend)
         self.prober = Prober(self.probe_mode, sim_ms=cfg.probe_sim_ms, gemm_n=cfg.probe_gemm_n,
@@ -1730,7 +1733,9 @@ class Agent:
                 self.advertised[resource] = set(healthy)
             flipped = before ^ self.advertised.get(resource, set())
             pools = {self.records[u]["poolUID"] for u in flipped if u in self.records}
-        self._adv_event.set()
+        with self._adv_cv:
+            self._adv_gen += 1
+            self._adv_cv.notify_all()
         if pools:  # readiness depends on the advertised bit: tell the manager
             self._bump(pools)
 
@@ -1749,10 +1754,12 @@ class Agent:
             return
         deadline = time.monotonic() + self.cfg.advertise_wait_s
         while time.monotonic() < deadline:
+            with self._adv_cv:
+                gen = self._adv_gen
             if self._advertise_done(resource, uuids):
                 return
-            self._adv_event.wait(0.05)
-            self._adv_event.clear()
+            with self._adv_cv:
+                self._adv_cv.wait_for(lambda: self._adv_gen != gen, timeout=0.05)
 
 
     def _ensure_plugin(self, resource: str) -> None:
