@@ -478,7 +478,10 @@ def main() -> int:
         by_n: dict[int, list[dict]] = {}
         matched: dict[int, dict] = {}  # id(cycle) -> its claiming pass
         for cy in cycles:
-            hit = [t for t in claim_traces if cy["patchAt"] <= t["start"] <= cy["readyAtWall"]]
+            # the claiming pass may have started just before the PATCH landed (a pass already
+            # running reads the pool afresh and sees the new replicas): match by overlap
+            hit = [t for t in claim_traces if t["start"] <= cy["readyAtWall"]
+                   and t["start"] + t["totalMs"] / 1e3 >= cy["patchAt"]]
             if not hit:
                 continue
             t = min(hit, key=lambda x: x["start"])
