@@ -43,6 +43,11 @@ def main() -> None:
     ap.add_argument("--tls-key", default=os.environ.get("GPUPOOL_AGENT_TLS_KEY", ""))
     ap.add_argument("--apiserver", default=os.environ.get("GPUPOOL_APISERVER", ""))
     ap.add_argument("--token", default=os.environ.get("GPUPOOL_TOKEN", ""))
+    ap.add_argument("--token-file", default=os.environ.get("GPUPOOL_TOKEN_FILE", ""),
+                    help="apiserver bearer token file, re-read as it rotates (projected "
+                         "ServiceAccount token); in-cluster config does this by itself")
+    ap.add_argument("--heartbeat-interval", type=float, default=10.0,
+                    help="period of the agent's Node condition heartbeat (s)")
     ap.add_argument("--auth-token-file", default=os.environ.get("GPUPOOL_AGENT_TOKEN_FILE", ""),
                     help="shared secret required on the RPC (Authorization: Bearer); "
                          "$GPUPOOL_AGENT_TOKEN also works")
@@ -114,6 +119,7 @@ def main() -> None:
                       count=a.count, cli_dir=a.cli_dir, state_dir=a.state_dir, socket=a.socket,
                       listen=a.listen, tls_cert=a.tls_cert, tls_key=a.tls_key,
                       endpoint=a.endpoint, apiserver=a.apiserver, token=a.token,
+                      token_file=a.token_file, heartbeat_interval=a.heartbeat_interval,
                       plugin_dir=a.plugin_dir, pod_resources=a.pod_resources, probe_mode=a.probe,
                       probe_sim_ms=a.probe_sim_ms, probe_gemm_n=a.probe_gemm_n,
                       probe_overlap_gemm_n=a.probe_overlap_gemm_n,

@@ -166,6 +166,8 @@ class AgentConfig:
     # r2q_agent_footprint_real.json, + the ~1.15 GiB probe arena): slot budgets must fit beside it
     hbm_reserve_bytes: int = 2 << 30
     share_acct_grace_s: float = 10.0  # an HBM account younger than this is never garbage-collected
+    heartbeat_interval: float = 10.0  # Node condition heartbeat (nodereg.py)
+    token_file: str = ""              # apiserver bearer token file, re-read as it rotates
 
 
 class Agent:
@@ -262,6 +264,7 @@ class Agent:
         self._podres = PodResourcesClient(cfg.pod_resources) if cfg.pod_resources else None
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
+        self.registrar = None  # nodereg.NodeRegistrar once register_node ran
         from .scrubber import HbmScrubber
         self.scrubber = HbmScrubber(self, cfg.scrub_interval_s, cfg.scrub_window_bytes,
                                     cfg.scrub_windows, cfg.scrub_reserve_bytes,
@@ -2116,70 +2119,49 @@ class Agent:
         return None
 
     # ================================================================ node registration
-    def register_node(self) -> None:
-        if not self.cfg.apiserver:
-            return
-        from ..kube import NODES, Client, KubeError
-        c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
+    def _node_conditions(self) -> dict[str, tuple[str, str, str]]:
+        """The agent's own Node conditions (nodereg.OWN_CONDITIONS): type -> (status, reason,
+        message)."""
+        failed = {k: v["detail"] for k, v in self.preflight["checks"].items() if not v["ok"]}
+        return {
+            "GPUPoolAgentReady": ("True", "AgentRunning",
+                                  f"{len(self.by_uuid)} GPU(s) via {self.backend}; probe "
+                                  f"{self.probe_mode}"),
+            "ROCmReady": ("True" if self.preflight["ready"] else "False",
+                          "PreflightPassed" if self.preflight["ready"] else "PreflightFailed",
+                          "; ".join(f"{k}: {v}" for k, v in failed.items()) or
+                          "; ".join(v["detail"] for v in self.preflight["checks"].values()))}
+
+    def node_registrar(self, client=None):
+        """The Node registration / heartbeat writer (nodereg.py) for this agent."""
+        from ..kube import Client
+        from .nodereg import NodeRegistrar
         devs = self.snap["devices"]
         gfx = sorted({(d.get("asic") or {}).get("gfx", "") for d in devs} - {""})
         labels = {schema.LABEL_GFX: gfx[0] if gfx else "unknown",
                   "amd.com/gpu.count": str(len(devs)),
                   "amd.com/gpu.product": "MI355X",
-                  "gpupool.amd.com/backend": self.backend,
-                  "kubernetes.io/hostname": self.cfg.node}
+                  "gpupool.amd.com/backend": self.backend}
         parts = sorted({(d.get("partition") or {}).get("compute", "") for d in devs} - {""})
         if parts:
             labels["amd.com/compute-partition"] = parts[0]
-        ann = {schema.ANN_AGENT_ENDPOINT: self.endpoint()}
-        try:
-            c.create(NODES, {"apiVersion": "v1", "kind": "Node",
-                             "metadata": {"name": self.cfg.node, "labels": labels,
-                                          "annotations": ann}})
-        except KubeError as e:
-            if e.code != 409:
-                raise
-            c.patch(NODES, self.cfg.node, {"metadata": {"labels": labels, "annotations": ann}})
-        self._heartbeat(c)
+        c = client or Client.connect(self.cfg.apiserver, self.cfg.token or None,
+                                     token_file=self.cfg.token_file or None)
+        return NodeRegistrar(c, self.cfg.node, labels,
+                             {schema.ANN_AGENT_ENDPOINT: self.endpoint()}, self._node_conditions)
 
-    def _heartbeat(self, c) -> None:
-        from ..kube import NODES
-        ready = {"type": "GPUPoolAgentReady", "status": "True", "reason": "AgentRunning",
-                 "message": f"{len(self.by_uuid)} GPU(s) via {self.backend}; probe "
-                            f"{self.probe_mode}",
-                 "lastHeartbeatTime": now_rfc3339(), "lastTransitionTime": now_rfc3339()}
-        failed = {k: v["detail"] for k, v in self.preflight["checks"].items() if not v["ok"]}
-        rocm = {"type": "ROCmReady", "status": "True" if self.preflight["ready"] else "False",
-                "reason": "PreflightPassed" if self.preflight["ready"] else "PreflightFailed",
-                "message": "; ".join(f"{k}: {v}" for k, v in failed.items()) or
-                "; ".join(v["detail"] for v in self.preflight["checks"].values()),
-                "lastHeartbeatTime": now_rfc3339(), "lastTransitionTime": now_rfc3339()}
-        try:
-            node = c.get(NODES, self.cfg.node)
-            conds = [x for x in node.get("status", {}).get("conditions", [])
-                     if x.get("type") not in ("GPUPoolAgentReady", "ROCmReady")]
-            old = [x for x in node.get("status", {}).get("conditions", [])
-                   if x.get("type") == "GPUPoolAgentReady"]
-            if old and old[0].get("status") == "True":
-                ready["lastTransitionTime"] = old[0].get("lastTransitionTime", ready[
-                    "lastTransitionTime"])
-            st = node.get("status", {})
-            st["conditions"] = conds + [ready, rocm]
-            if not any(x.get("type") == "Ready" for x in conds):
-                st["conditions"].append({"type": "Ready", "status": "True",
-                                         "reason": "KubeletReady" if self.cfg.plugin_dir
-                                         else "AgentReady", "message": "",
-                                         "lastHeartbeatTime": now_rfc3339(),
-                                         "lastTransitionTime": now_rfc3339()})
-            c.patch(NODES, self.cfg.node, {"status": st}, sub="status")
-        except Exception as e:
-            log.warning("node heartbeat failed: %s", e)
+    def register_node(self) -> None:
+        if not self.cfg.apiserver:
+            return
+        self.registrar = self.node_registrar()
+        if not self.registrar.heartbeat():
+            log.info("node %s not registered by its kubelet yet: the heartbeat retries",
+                     self.cfg.node)
 
     def _heartbeater(self) -> None:
-        from ..kube import Client
-        c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
-        while not self._stop.wait(10.0):
-            self._heartbeat(c)
+        reg = self.registrar
+        while not self._stop.wait(self.cfg.heartbeat_interval if reg.registered else 1.0):
+            reg.heartbeat()
 
     def endpoint(self) -> str:
         if self.cfg.endpoint:
@@ -2256,6 +2238,9 @@ class Agent:
                         lines.append(f"gpupool_pod_gfx_busy_ratio{{{lab}}} {e['gfxBusy']}")
             for k, v in self.stats.items():
                 lines.append(f"gpupool_agent_{k} {v}")
+            if self.registrar is not None:  # Node registration / condition heartbeat (nodereg.py)
+                for k, v in self.registrar.stats.items():
+                    lines.append(f"gpupool_agent_node_{k} {v}")
             for src, ok in self.events_supported.items():
                 lines.append(f'gpupool_agent_event_source_supported{{source="{src}"}} {1 if ok else 0}')
             for k, v in self.scrubber.stats.items():

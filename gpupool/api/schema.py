@@ -680,8 +680,10 @@ def agent_rbac() -> list[dict]:
           "metadata": {"name": "gpupool-agent", "namespace": AGENT_NAMESPACE}}
     role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
             "metadata": {"name": "gpupool-agent-role"},
+            # no nodes:create — the kubelet registers the Node; patches are limited to the
+            # agent's own Node by the ValidatingAdmissionPolicy below
             "rules": [{"apiGroups": [""], "resources": ["nodes"],
-                       "verbs": ["get", "create", "patch"]},
+                       "verbs": ["get", "patch"]},
                       {"apiGroups": [""], "resources": ["nodes/status"], "verbs": ["patch"]},
                       {"apiGroups": [""], "resources": ["events"], "verbs": ["create"]},
                       {"apiGroups": [""], "resources": ["pods"], "verbs": ["list"]},
@@ -692,4 +694,74 @@ def agent_rbac() -> list[dict]:
                            "name": "gpupool-agent-role"},
                "subjects": [{"kind": "ServiceAccount", "name": "gpupool-agent",
                              "namespace": AGENT_NAMESPACE}]}
-    return [sa, role, binding]
+    return [sa, role, binding, *agent_node_policy()]
+
+
+AGENT_SA_USER = f"system:serviceaccount:{AGENT_NAMESPACE}:gpupool-agent"
+AGENT_OWN_CONDITIONS = ["GPUPoolAgentReady", "ROCmReady"]
+AGENT_LABEL_PREFIXES = ["amd.com/", "gpupool.amd.com/"]
+
+
+def agent_node_policy() -> list[dict]:
+    """RBAC cannot say "only your own Node": a ValidatingAdmissionPolicy can. A Node write by the
+    agent ServiceAccount is admitted only when (1) the bound token's node claim
+    (``authentication.kubernetes.io/node-name``, set on projected tokens of pods since k8s 1.30)
+    names that Node, (2) ``spec`` is untouched, (3) in ``status`` nothing but the agent's own
+    conditions changed (capacity, allocatable and the kubelet's conditions are the kubelet's), and
+    (4) only labels/annotations under the agent's prefixes changed. apiserver-sim enforces the same
+    rules natively (store.AgentNodePolicy) when this policy object is present."""
+    own = "[" + ", ".join(f"'{t}'" for t in AGENT_OWN_CONDITIONS) + "]"
+    pre = "[" + ", ".join(f"'{p}'" for p in AGENT_LABEL_PREFIXES) + "]"
+
+    def unchanged_outside_prefixes(field: str) -> str:
+        new, old = f"variables.{field}", f"variables.{field}Old"
+        return (f"{old}.all(k, {pre}.exists(p, k.startsWith(p)) || "
+                f"(k in {new} && {new}[k] == {old}[k])) && "
+                f"{new}.all(k, {pre}.exists(p, k.startsWith(p)) || k in {old})")
+    policy = {
+        "apiVersion": "admissionregistration.k8s.io/v1", "kind": "ValidatingAdmissionPolicy",
+        "metadata": {"name": "gpupool-agent-own-node"},
+        "spec": {
+            "failurePolicy": "Fail",
+            "matchConstraints": {"resourceRules": [{
+                "apiGroups": [""], "apiVersions": ["v1"], "operations": ["UPDATE"],
+                "resources": ["nodes", "nodes/status"]}]},
+            "matchConditions": [{"name": "gpupool-agent",
+                                 "expression": f"request.userInfo.username == '{AGENT_SA_USER}'"}],
+            "variables": [
+                {"name": "nodeClaim",
+                 "expression": "'authentication.kubernetes.io/node-name' in request.userInfo.extra"
+                               " ? request.userInfo.extra['authentication.kubernetes.io/node-name']"
+                               "[0] : ''"},
+                {"name": "others",
+                 "expression": f"has(object.status.conditions) ? object.status.conditions.filter("
+                               f"c, !(c.type in {own})) : []"},
+                {"name": "othersOld",
+                 "expression": f"has(oldObject.status.conditions) ? oldObject.status.conditions"
+                               f".filter(c, !(c.type in {own})) : []"},
+                *({"name": f"{f}{sfx}",
+                   "expression": f"has({o}.metadata.{f}) ? {o}.metadata.{f} : {{}}"}
+                  for f in ("labels", "annotations")
+                  for sfx, o in (("", "object"), ("Old", "oldObject")))],
+            "validations": [
+                {"expression": "variables.nodeClaim == object.metadata.name",
+                 "reason": "Forbidden",
+                 "message": "the gpupool agent may only write the Node it runs on"},
+                {"expression": "object.?spec == oldObject.?spec", "reason": "Forbidden",
+                 "message": "the gpupool agent may not change Node spec"},
+                {"expression": "object.status.?capacity == oldObject.status.?capacity && "
+                               "object.status.?allocatable == oldObject.status.?allocatable && "
+                               "variables.others == variables.othersOld",
+                 "reason": "Forbidden",
+                 "message": "the gpupool agent may only write its own Node conditions "
+                            f"({', '.join(AGENT_OWN_CONDITIONS)})"},
+                {"expression": unchanged_outside_prefixes("labels") + " && " +
+                               unchanged_outside_prefixes("annotations"),
+                 "reason": "Forbidden",
+                 "message": "the gpupool agent may only write labels/annotations under "
+                            f"{', '.join(AGENT_LABEL_PREFIXES)}"}]}}
+    binding = {"apiVersion": "admissionregistration.k8s.io/v1",
+               "kind": "ValidatingAdmissionPolicyBinding",
+               "metadata": {"name": "gpupool-agent-own-node"},
+               "spec": {"policyName": "gpupool-agent-own-node", "validationActions": ["Deny"]}}
+    return [policy, binding]

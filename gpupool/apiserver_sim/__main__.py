@@ -17,6 +17,9 @@ def main() -> None:
     ap.add_argument("--port-file", default=None, help="write the bound port here (for --port 0)")
     ap.add_argument("--crd-dir", default=None, help="pre-install every CRD YAML in this dir")
     ap.add_argument("--token", default=None, help="require 'Authorization: Bearer <token>'")
+    ap.add_argument("--users-file", default=None,
+                    help="JSON {token: {username, groups, extra, expiresAt}}: more identities "
+                         "beside --token (changeable at run time through POST /debug/tokens)")
     ap.add_argument("--bookmark-interval", type=float, default=5.0)
     ap.add_argument("--window", type=int, default=50000, help="watch event-log window")
     ap.add_argument("--unix", default=None, help="also listen on this unix socket")
@@ -49,6 +52,10 @@ def main() -> None:
     sim = ApiServerSim(token=a.token, bookmark_interval=a.bookmark_interval, window=a.window,
                        watch_delay=a.watch_delay)
     sim.fail_list = {r: -1 for r in a.fail_list}
+    if a.users_file:
+        import json
+        with open(a.users_file) as f:
+            sim.users = {str(k): dict(v) for k, v in json.load(f).items()}
     try:
         asyncio.run(serve(a.host, a.port, sim, a.port_file, a.crd_dir, a.unix,
                           tls_cert=a.tls_cert, tls_key=a.tls_key, client_ca=a.client_ca))

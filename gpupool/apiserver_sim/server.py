@@ -133,6 +133,33 @@ def to_table(rt: ResourceType, items: list[dict], rv: str) -> dict:
             "columnDefinitions": cols, "rows": rows}
 
 
+def agent_node_policy_violation(user: dict, old: dict, new: dict, own: list[str],
+                                prefixes: list[str]) -> str:
+    """The message of the first rule of schema.agent_node_policy that ``old -> new`` breaks, or
+    "" when the agent's Node write is admissible."""
+    claim = ((user.get("extra") or {}).get("authentication.kubernetes.io/node-name") or [""])[0]
+    if claim != new["metadata"]["name"]:
+        return "the gpupool agent may only write the Node it runs on"
+    if new.get("spec") != old.get("spec"):
+        return "the gpupool agent may not change Node spec"
+    ost, nst = old.get("status") or {}, new.get("status") or {}
+    others = [[c for c in (st.get("conditions") or []) if c.get("type") not in own]
+              for st in (ost, nst)]
+    if ost.get("capacity") != nst.get("capacity") or \
+            ost.get("allocatable") != nst.get("allocatable") or others[0] != others[1]:
+        return f"the gpupool agent may only write its own Node conditions ({', '.join(own)})"
+    for f in ("labels", "annotations"):
+        a, b = old["metadata"].get(f) or {}, new["metadata"].get(f) or {}
+        mine = lambda k: any(k.startswith(p) for p in prefixes)  # noqa: E731
+        if {k: v for k, v in a.items() if not mine(k)} != {k: v for k, v in b.items()
+                                                            if not mine(k)}:
+            return f"the gpupool agent may only write labels/annotations under {', '.join(prefixes)}"
+    return ""
+
+
+USER_KEY = web.RequestKey("user", dict) if hasattr(web, "RequestKey") else "user"
+
+
 # ------------------------------------------------------------------ server
 class ApiServerSim:
     def __init__(self, token: str | None = None, bookmark_interval: float = 5.0,
@@ -142,6 +169,11 @@ class ApiServerSim:
         # ``watch_delay`` seconds after the write, so informers see stale objects meanwhile
         self.watch_delay = watch_delay
         self.token = token
+        # bearer tokens beside the admin ``token``: token -> {"username", "groups", "extra",
+        # "expiresAt" (unix s, optional)}. An expired token answers 401, as a bound ServiceAccount
+        # token past its expiry does; POST /debug/tokens replaces the set (rotation tests)
+        self.users: dict[str, dict] = {}
+        self.auth_failures = 0
         self.bookmark_interval = bookmark_interval
         # watch queues per resource type (a kube-apiserver's watch cache is per resource too): a
         # write wakes only the watchers of its own type, not every informer of every kind
@@ -160,6 +192,7 @@ class ApiServerSim:
         r.add_get("/version", self._version)
         r.add_get("/metrics", self._metrics)
         r.add_post("/debug/faults", self._set_faults)
+        r.add_post("/debug/tokens", self._set_tokens)
         r.add_get("/api", self._api_versions)
         r.add_get("/apis", self._api_groups)
         r.add_get("/api/{version}", self._resource_list_core)
@@ -170,9 +203,12 @@ class ApiServerSim:
     # -------------------------------------------------------------- plumbing
     @web.middleware
     async def _mw(self, request: web.Request, handler):
-        if self.token and request.path not in ("/healthz", "/readyz", "/livez"):
-            if request.headers.get("Authorization") != f"Bearer {self.token}":
+        if (self.token or self.users) and request.path not in ("/healthz", "/readyz", "/livez"):
+            user = self.authenticate(request.headers.get("Authorization", ""))
+            if user is None:
+                self.auth_failures += 1
                 return self._err(ApiError(401, "Unauthorized", "Unauthorized"))
+            request[USER_KEY] = user
         try:
             resp = await handler(request)
         except ApiError as e:
@@ -208,6 +244,28 @@ class ApiServerSim:
         lines.append("# TYPE etcd_resource_version gauge")
         lines.append(f"etcd_resource_version {self.store.rv}")
         return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
+
+    ADMIN = {"username": "system:admin", "groups": ["system:masters"], "extra": {}}
+
+    def authenticate(self, header: str) -> dict | None:
+        if not header.startswith("Bearer "):
+            return None
+        tok = header[7:].strip()
+        if self.token and tok == self.token:
+            return self.ADMIN
+        u = self.users.get(tok)
+        if u is None or (u.get("expiresAt") and time.time() >= float(u["expiresAt"])):
+            return None
+        return u
+
+    async def _set_tokens(self, request):
+        """{"tokens": {token: {"username", "groups", "extra", "expiresAt"}}, "merge": bool}."""
+        if request.get(USER_KEY) not in (None, self.ADMIN):
+            raise ApiError(403, "Forbidden", "debug endpoints are admin-only")
+        body = await request.json()
+        toks = {str(k): dict(v or {}) for k, v in (body.get("tokens") or {}).items()}
+        self.users = {**self.users, **toks} if body.get("merge") else toks
+        return web.json_response({"tokens": len(self.users)})
 
     async def _set_faults(self, request):
         """{"failList": {"resourcequotas": -1}}: LIST and WATCH of those resources answer 503
@@ -353,6 +411,40 @@ class ApiServerSim:
             raise ApiError(404, "NotFound", f"unknown subresource {sub}")
         return await self._object(request, rt, ns, name, "", dry)
 
+    PATCH_TYPES = {"application/json-patch+json": "json",
+                   "application/merge-patch+json": "merge",
+                   "application/strategic-merge-patch+json": "strategic"}
+
+    @classmethod
+    def _patch_type(cls, ctype: str) -> str:
+        base = ctype.split(";", 1)[0].strip().lower()
+        if base in cls.PATCH_TYPES:
+            return cls.PATCH_TYPES[base]
+        raise ApiError(415, "UnsupportedMediaType",
+                       f"the body of the request was in an unknown format - accepted media types "
+                       f"include: {', '.join(cls.PATCH_TYPES)}")
+
+    def _admit_node_write(self, request, name: str, new: dict) -> None:
+        """The agent's ValidatingAdmissionPolicy (schema.agent_node_policy), evaluated natively
+        when that policy object is installed: no CEL engine here, the same four rules in Python.
+        ``new`` is the write's dry-run result; the decision happens before the real write, with
+        no await in between."""
+        from ..api import schema
+        user = request.get(USER_KEY)
+        if not user or user.get("username") != schema.AGENT_SA_USER:
+            return
+        vap = self.store.types.get(("admissionregistration.k8s.io",
+                                    "validatingadmissionpolicies"))
+        if vap is None or ("", "gpupool-agent-own-node") not in self.store.objects[vap.key]:
+            return
+        old = self.store.get(self.store.lookup("", "nodes"), None, name)
+        why = agent_node_policy_violation(user, old, new, schema.AGENT_OWN_CONDITIONS,
+                                          schema.AGENT_LABEL_PREFIXES)
+        if why:
+            raise ApiError(403, "Forbidden", f'nodes "{name}" is forbidden: '
+                           f"ValidatingAdmissionPolicy 'gpupool-agent-own-node' denied request: "
+                           f"{why}")
+
     async def _object(self, request, rt, ns, name, sub, dry):
         m = request.method
         if m == "GET":
@@ -361,13 +453,20 @@ class ApiServerSim:
                 return web.json_response(to_table(rt, [obj], obj["metadata"]["resourceVersion"]))
             return web.json_response(obj)
         if m == "PUT":
+            body = await request.json()
+            if rt.kind == "Node":
+                self._admit_node_write(request, name, self.store.update(
+                    rt, ns, name, body, sub, True))
             # the decoded body is this request's own; the reply only serialises the result
-            return web.json_response(self.store.update(rt, ns, name, await request.json(), sub, dry,
+            return web.json_response(self.store.update(rt, ns, name, body, sub, dry,
                                                        owned=True, copy_out=False))
         if m == "PATCH":
-            ctype = request.headers.get("Content-Type", "")
-            ptype = "json" if "json-patch" in ctype else "merge"
-            return web.json_response(self.store.patch(rt, ns, name, await request.json(), ptype,
+            ptype = self._patch_type(request.headers.get("Content-Type", ""))
+            body = await request.json()
+            if rt.kind == "Node":
+                self._admit_node_write(request, name, self.store.patch(
+                    rt, ns, name, body, ptype, sub, True))
+            return web.json_response(self.store.patch(rt, ns, name, body, ptype,
                                                       sub, dry, copy_out=False))
         if m == "DELETE" and not sub:
             body = {}

@@ -28,6 +28,7 @@ from dataclasses import dataclass, field
 from typing import Any, Callable
 
 from ..api import openapi
+from .smp import PatchError, strategic_merge
 
 
 def clone(o):
@@ -74,6 +75,7 @@ class ResourceType:
     status_sub: bool = False
     scale_sub: dict | None = None
     printer_columns: list = field(default_factory=list)
+    custom: bool = False                # served from a CRD (no strategic merge patch)
 
     @property
     def api_version(self) -> str:
@@ -115,6 +117,10 @@ BUILTINS = [
                  "clusterrole"),
     ResourceType("rbac.authorization.k8s.io", "v1", "clusterrolebindings", "ClusterRoleBinding",
                  False, "clusterrolebinding"),
+    ResourceType("admissionregistration.k8s.io", "v1", "validatingadmissionpolicies",
+                 "ValidatingAdmissionPolicy", False, "validatingadmissionpolicy", status_sub=True),
+    ResourceType("admissionregistration.k8s.io", "v1", "validatingadmissionpolicybindings",
+                 "ValidatingAdmissionPolicyBinding", False, "validatingadmissionpolicybinding"),
     ResourceType("apiextensions.k8s.io", "v1", "customresourcedefinitions",
                  "CustomResourceDefinition", False, "customresourcedefinition", ["crd", "crds"]),
 ]
@@ -720,7 +726,16 @@ class Store:
         # both patch forms copy ``cur`` first: the stored object is never touched
         if ptype == "json":
             new = json_patch(cur, patch)
-        else:  # merge / strategic (approximated as merge)
+        elif ptype == "strategic":
+            if rt.custom:  # apiserver: SMP needs Go struct tags, which a CRD does not have
+                raise ApiError(415, "UnsupportedMediaType",
+                               "strategic merge patch is not supported for custom resources; "
+                               "use a JSON merge patch or a JSON patch")
+            try:
+                new = strategic_merge(cur, patch, rt.kind)
+            except PatchError as e:
+                raise ApiError(422, "Invalid", str(e)) from e
+        else:
             new = merge_patch(cur, patch)
         if not (isinstance(patch, dict) and patch.get("metadata", {}).get("resourceVersion")):
             new.setdefault("metadata", {})["resourceVersion"] = cur["metadata"]["resourceVersion"]
@@ -892,7 +907,7 @@ class Store:
             short_names=list(names.get("shortNames") or []),
             schema=(ver.get("schema") or {}).get("openAPIV3Schema"),
             status_sub="status" in subs, scale_sub=subs.get("scale"),
-            printer_columns=list(ver.get("additionalPrinterColumns") or [])))
+            printer_columns=list(ver.get("additionalPrinterColumns") or []), custom=True))
         crd.setdefault("status", {})["conditions"] = [
             {"type": "Established", "status": "True", "reason": "InitialNamesAccepted",
              "message": "the initial names have been accepted",

@@ -79,6 +79,10 @@ BY_KIND = {
     "NetworkPolicy": Res("networking.k8s.io", "v1", "networkpolicies"),
     "PersistentVolume": Res("", "v1", "persistentvolumes", namespaced=False),
     "PersistentVolumeClaim": Res("", "v1", "persistentvolumeclaims"),
+    "ValidatingAdmissionPolicy": Res("admissionregistration.k8s.io", "v1",
+                                     "validatingadmissionpolicies", namespaced=False),
+    "ValidatingAdmissionPolicyBinding": Res("admissionregistration.k8s.io", "v1",
+                                            "validatingadmissionpolicybindings", namespaced=False),
 }
 
 
@@ -139,7 +143,8 @@ def load_kubeconfig(path: str | None = None, context: str | None = None) -> dict
 class Client:
     def __init__(self, server: str, token: str | None = None, timeout: float = 30.0,
                  ca_file: str | None = None, insecure: bool = False,
-                 client_cert: str | None = None, client_key: str | None = None):
+                 client_cert: str | None = None, client_key: str | None = None,
+                 token_file: str | None = None):
         u = urllib.parse.urlparse(server if "://" in server else "http://" + server)
         self.scheme = u.scheme
         self.host = u.hostname or "127.0.0.1"
@@ -147,6 +152,14 @@ class Client:
         self.unix = u.path if u.scheme == "unix" else None
         self.server = server
         self.token = token
+        # a rotating credential (projected ServiceAccount token, Workload Identity): re-read at
+        # most TOKEN_RELOAD_S after the last read and at once after a 401, as client-go does
+        self.token_file = token_file
+        self._token_read = -1e9
+        self._token_mu = threading.Lock()
+        self.token_reloads = 0
+        if token_file:
+            self._reload_token(force=True)
         self.timeout = timeout
         self.namespace: str | None = None  # kubeconfig context namespace, if any
         self._local = threading.local()
@@ -167,6 +180,27 @@ class Client:
             self._ssl = ctx
 
     SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+    TOKEN_RELOAD_S = 60.0
+
+    def _reload_token(self, force: bool = False) -> bool:
+        """Re-read ``token_file`` when due (or ``force``). True when the token changed."""
+        if not self.token_file:
+            return False
+        with self._token_mu:
+            now = time.monotonic()
+            if not force and now - self._token_read < self.TOKEN_RELOAD_S:
+                return False
+            self._token_read = now
+            try:
+                with open(self.token_file) as f:
+                    tok = f.read().strip()
+            except OSError:
+                return False  # mid-rotation (the kubelet swaps a symlink): keep the last one
+            if not tok or tok == self.token:
+                return False
+            self.token = tok
+            self.token_reloads += 1
+            return True
 
     @classmethod
     def from_env(cls) -> "Client":
@@ -190,10 +224,8 @@ class Client:
             return None
         if ":" in host:
             host = f"[{host}]"
-        with open(os.path.join(sa_dir, "token")) as f:
-            token = f.read().strip()
-        return cls(f"https://{host}:{os.environ.get('KUBERNETES_SERVICE_PORT', '443')}", token,
-                   ca_file=os.path.join(sa_dir, "ca.crt"))
+        return cls(f"https://{host}:{os.environ.get('KUBERNETES_SERVICE_PORT', '443')}", None,
+                   ca_file=os.path.join(sa_dir, "ca.crt"), token_file=os.path.join(sa_dir, "token"))
 
     @classmethod
     def from_kubeconfig(cls, path: str | None = None, context: str | None = None,
@@ -214,14 +246,16 @@ class Client:
         return c
 
     @classmethod
-    def connect(cls, server: str, token: str | None = None) -> "Client":
-        """``server == "in-cluster"`` selects the ServiceAccount config, anything else is a URL."""
+    def connect(cls, server: str, token: str | None = None,
+                token_file: str | None = None) -> "Client":
+        """``server == "in-cluster"`` selects the ServiceAccount config, anything else is a URL.
+        ``token_file`` (re-read as it rotates) wins over a fixed ``token``."""
         if server == "in-cluster":
             c = cls.in_cluster()
             if c is None:
                 raise RuntimeError("--apiserver in-cluster but no ServiceAccount / KUBERNETES_SERVICE_HOST")
             return c
-        return cls(server, token)
+        return cls(server, token, token_file=token_file)
 
     # ------------------------------------------------------------ transport
     def _conn(self, timeout: float | None = None) -> http.client.HTTPConnection:
@@ -233,6 +267,7 @@ class Client:
         return http.client.HTTPConnection(self.host, self.port, timeout=timeout or self.timeout)
 
     def _headers(self, ctype: str = "application/json", accept: str = "application/json") -> dict:
+        self._reload_token()
         h = {"Content-Type": ctype, "Accept": accept}
         if self.token:
             h["Authorization"] = f"Bearer {self.token}"
@@ -245,6 +280,18 @@ class Client:
             if q:
                 path += "?" + urllib.parse.urlencode(q)
         data = None if body is None else json.dumps(body).encode()
+        resp, raw = self._roundtrip(method, path, data, ctype, accept)
+        if resp.status == 401 and self._reload_token(force=True):  # rotated under us: once more
+            resp, raw = self._roundtrip(method, path, data, ctype, accept)
+        try:
+            out = json.loads(raw) if raw else None
+        except json.JSONDecodeError:
+            out = raw.decode(errors="replace")
+        if resp.status >= 400:
+            raise KubeError(resp.status, out)
+        return out
+
+    def _roundtrip(self, method: str, path: str, data: bytes | None, ctype: str, accept: str):
         for attempt in range(2):
             conn = getattr(self._local, "conn", None)
             fresh = conn is None
@@ -263,13 +310,7 @@ class Client:
                     pass
                 if fresh or attempt == 1:
                     raise
-        try:
-            out = json.loads(raw) if raw else None
-        except json.JSONDecodeError:
-            out = raw.decode(errors="replace")
-        if resp.status >= 400:
-            raise KubeError(resp.status, out)
-        return out
+        return resp, raw
 
     # ------------------------------------------------------------ verbs
     def get(self, res: Res, name: str, ns: str | None = None, sub: str | None = None) -> dict:
@@ -364,6 +405,12 @@ class Client:
         conn = self._conn(timeout=(timeout_seconds or 3600) + 30)
         conn.request("GET", path, headers=self._headers())
         resp = conn.getresponse()
+        if resp.status == 401 and self._reload_token(force=True):
+            resp.read()
+            conn.close()
+            conn = self._conn(timeout=(timeout_seconds or 3600) + 30)
+            conn.request("GET", path, headers=self._headers())
+            resp = conn.getresponse()
         if resp.status >= 400:
             raw = resp.read()
             conn.close()

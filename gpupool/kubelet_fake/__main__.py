@@ -23,6 +23,8 @@ def main() -> None:
     ap.add_argument("--no-schedule", action="store_true")
     ap.add_argument("--node-status-delay", type=float, default=0.02,
                     help="coalescing delay between a device-plugin update and the Node status PATCH (s)")
+    ap.add_argument("--status-interval", type=float, default=10.0,
+                    help="periodic node-status sync (Ready heartbeat, capacity/allocatable), s")
     ap.add_argument("--host-path", action="append", default=None,
                     help="strict mounts: a host path a device plugin may hand out (repeatable; "
                          "an Allocate mount or device outside all of them fails the pod)")
@@ -39,7 +41,7 @@ def main() -> None:
                     os.path.join(a.root, "pod-resources", "kubelet.sock"), workdir=a.workdir,
                     log_dir=os.path.join(a.root, "pod-logs"), token=a.token,
                     schedule=not a.no_schedule, node_status_delay=a.node_status_delay,
-                    host_paths=a.host_path)
+                    host_paths=a.host_path, status_interval=a.status_interval)
     k.start()
     if a.ready_file:
         with open(a.ready_file, "w") as f:

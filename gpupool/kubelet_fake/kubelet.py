@@ -72,7 +72,8 @@ class FakeKubelet:
     def __init__(self, node: str, apiserver: str, plugin_dir: str, pod_resources_socket: str,
                  workdir: str | None = None, log_dir: str | None = None, token: str | None = None,
                  schedule: bool = True, extra_env: dict | None = None,
-                 node_status_delay: float = 0.02, host_paths: list[str] | None = None):
+                 node_status_delay: float = 0.02, host_paths: list[str] | None = None,
+                 status_interval: float = 10.0):
         self.node = node
         self.client = Client(apiserver, token)
         self.apiserver = apiserver
@@ -105,6 +106,11 @@ class FakeKubelet:
         # ListAndWatch updates becomes one PATCH that does not queue in front of the control
         # plane's own writes on the apiserver.
         self.node_status_delay = node_status_delay
+        # the periodic node-status sync (kubelet --node-status-update-frequency, 10 s): the Ready
+        # condition's heartbeat plus capacity/allocatable, as a strategic merge patch
+        self.status_interval = status_interval
+        self._ready_since = ""
+        self.status_writes = 0
         self._status_kick = threading.Event()
         self.threads: list[threading.Thread] = []
         self.reg_server: grpc.Server | None = None
@@ -238,24 +244,43 @@ class FakeKubelet:
         self._update_node_status()
 
     def _node_status_loop(self) -> None:
+        next_sync = time.monotonic() + self.status_interval
         while not self.stop_ev.is_set():
-            if not self._status_kick.wait(0.5):
+            wait = max(0.0, min(0.5, next_sync - time.monotonic()))
+            if not self._status_kick.wait(wait):
+                if time.monotonic() >= next_sync:
+                    next_sync = time.monotonic() + self.status_interval
+                    self._update_node_status()
                 continue
             time.sleep(self.node_status_delay)  # coalesce a burst of plugin updates
             self._status_kick.clear()
             self._update_node_status()
 
     def _update_node_status(self) -> None:
+        """capacity/allocatable of every registered resource + the kubelet's own conditions
+        (Ready with its heartbeat), as one strategic merge patch of Node status — conditions merge
+        by type, so conditions other components own (the agent's) are left as they are."""
+        from ..apiserver_sim.store import now_rfc3339
         with self.status_lock:
             with self.lock:
                 cap = {r: str(len(c.devices)) for r, c in self.plugins.items()}
                 alloc = {r: str(sum(1 for h in c.devices.values() if h == "Healthy"))
                          for r, c in self.plugins.items()}
+            now = now_rfc3339()
+            self._ready_since = self._ready_since or now
+            conds = [{"type": t, "status": "False", "reason": f"KubeletHasNo{t}",
+                      "message": f"kubelet has no {t}", "lastHeartbeatTime": now,
+                      "lastTransitionTime": self._ready_since}
+                     for t in ("MemoryPressure", "DiskPressure", "PIDPressure")]
+            conds.append({"type": "Ready", "status": "True", "reason": "KubeletReady",
+                          "message": "kubelet is posting ready status", "lastHeartbeatTime": now,
+                          "lastTransitionTime": self._ready_since})
             try:
                 self.client.patch(NODES, self.node, {"status": {
                     "capacity": {"cpu": "64", "memory": "1Ti", "pods": "110", **cap},
-                    "allocatable": {"cpu": "64", "memory": "1Ti", "pods": "110", **alloc}}},
-                    sub="status")
+                    "allocatable": {"cpu": "64", "memory": "1Ti", "pods": "110", **alloc},
+                    "conditions": conds}}, sub="status", ptype="strategic")
+                self.status_writes += 1
             except KubeError as e:
                 log.warning("node status patch failed: %s", e)
 

@@ -90,6 +90,7 @@ class NodeSpec:
     probe: str = ""               # "" -> agent default (simulated for fake, inproc for real)
     kubelet: bool = True
     extra_args: list[str] = field(default_factory=list)
+    kubelet_args: list[str] = field(default_factory=list)
     # strict mounts (default): the fake kubelet fails a pod whose Allocate mounts or device
     # nodes lie outside what the agent DaemonSet shares with the host — the agent's state dir
     # (hostPath /var/lib/gpupool) and the GPU device nodes
@@ -201,6 +202,7 @@ class Cluster:
         if node.strict_mounts:
             for hp in (self.state_dir(node.name), "/dev/kfd", "/dev/dri"):
                 argv += ["--host-path", hp]
+        argv += node.kubelet_args
         p = self._spawn(f"kubelet-{node.name}", argv)
         _wait_file(rf, 60, p, os.path.join(self.workdir, f"kubelet-{node.name}.log"))
 
