@@ -70,10 +70,11 @@ def test_manager_rbac_covers_native_api_calls():
 
 
 def test_agent_rbac_covers_agent_api_calls():
-    src = open(os.path.join(ROOT, "gpupool", "agent", "agent.py")).read()
-    src += open(os.path.join(ROOT, "gpupool", "agent", "rpc.py")).read()  # agent RPC counters
+    import glob
+    src = "".join(open(p).read() for p in glob.glob(os.path.join(ROOT, "gpupool", "agent", "*.py")))
     used = set()
-    for m in re.finditer(r"c\.(get|create|patch|update|delete|list)\((\w+)[^)]*?(sub=\"status\")?\)", src):
+    for m in re.finditer(r"(?:\bc|self\.client)\.(get|create|patch|update|delete|list)\((\w+)"
+                         r"[^)]*?(sub=\"status\")?\)", src):
         res = {"NODES": "nodes", "PODS": "pods"}.get(m.group(2), m.group(2).lower())
         used.add((res + ("/status" if m.group(3) else ""), m.group(1)))
     granted = set()
@@ -82,6 +83,11 @@ def test_agent_rbac_covers_agent_api_calls():
             granted = _granted(o["rules"])
     missing = sorted(u for u in used if u not in granted)
     assert used and not missing, (used, missing)
+    # the kubelet registers Nodes: the agent can neither create one nor edit its spec/status
+    # beyond what the ValidatingAdmissionPolicy admits (schema.agent_node_policy)
+    assert ("nodes", "create") not in granted and ("nodes", "create") not in used
+    kinds = [o["kind"] for o in schema.agent_rbac()]
+    assert "ValidatingAdmissionPolicy" in kinds and "ValidatingAdmissionPolicyBinding" in kinds
 
 
 def test_kustomization_lists_every_deploy_manifest():

@@ -1,4 +1,4 @@
-"""Agent-side leader fencing (gpupool/agent/agent.py ``check_leader``): the newest manager epoch
+"""Agent-side leader fencing (gpupool/agent/fence.py, the agent's ``check_leader`` guard): the newest manager epoch
 seen on a mutating RPC is persisted in the ledger and older epochs are refused (409 StaleLeader)
 before the handler runs — also after an agent restart. Requests without a token (leader election
 off, gpuctl) pass unchecked."""
@@ -6,6 +6,8 @@ from __future__ import annotations
 
 import json
 import os
+
+import pytest
 
 from gpupool.agent.agent import Agent, AgentConfig
 
@@ -87,17 +89,45 @@ def test_a_recreated_lease_starts_a_new_generation(tmp_path, native_built):
     b.stop()
 
 
-def test_a_fence_from_before_lease_generations_accepts_a_later_lease(tmp_path, native_built):
+def test_a_fence_from_before_lease_generations_adopts_the_first_generation(tmp_path, native_built):
     """A fence persisted by an agent that predates the Lease-generation header has no generation
-    to compare: a token whose Lease was created after that fence was recorded is a recreated Lease
-    (its epoch restarted at 0) and is accepted; one created before it keeps the epoch order."""
+    to compare. The first token that carries one is adopted as the generation from then on —
+    comparing its creationTimestamp (apiserver clock) with the fence's "at" (the agent's clock)
+    refused a recreated Lease for good whenever the node clock ran ahead. From then on
+    generations order tokens as usual."""
     a = make_agent(tmp_path)
     assert a.check_leader("POST", "/v1/claims", tok("m-a", 5)) is None  # no generation
     assert "leaseCreated" not in a.leader_fence
-    r = a.check_leader("POST", "/v1/claims", tok("m-x", 0, "2000-01-01T00:00:00Z uid-older"))
-    assert r[0] == 409
+    # a Lease "created" before the fence's own timestamp (node clock ahead) is still adopted
+    assert a.check_leader("POST", "/v1/claims", tok("m-x", 0, "2000-01-01T00:00:00Z uid-older")) \
+        is None
+    assert a.leader_fence["leaseUID"] == "uid-older" and a.leader_fence["epoch"] == 0
     assert a.check_leader("POST", "/v1/claims", tok("m-b", 0, "2999-01-01T00:00:00Z uid-new")) is None
     assert a.leader_fence["leaseUID"] == "uid-new" and a.leader_fence["epoch"] == 0
     # the Lease before it, whatever its epoch, is now the older generation
     assert a.check_leader("POST", "/v1/release", tok("m-a", 5, "2000-01-01T00:00:00Z uid-older"))[0] == 409
     a.stop()
+
+
+def test_fence_unit_without_an_agent():
+    """fence.LeaderFence on its own (narrow interface: persisted state, a persist callback)."""
+    from gpupool.agent.fence import LeaderFence, StaleLeader
+    saved = []
+    f = LeaderFence({}, saved.append)
+    f.admit("POST", "/v1/claims", tok("m-a", 1))
+    assert saved[-1]["holder"] == "m-a" and f.epoch == 1
+    f.admit("GET", "/v1/node", tok("m-z", 0))  # reads are never fenced
+    f.admit("POST", "/v1/claims", {})          # no token: not checked
+    with pytest.raises(StaleLeader) as ei:
+        f.admit("POST", "/v1/release", tok("m-b", 0))
+    assert ei.value.status == 409 and f.stats["stale_leader_refused"] == 1
+    with pytest.raises(StaleLeader) as ei:
+        f.admit("POST", "/v1/release", {"x-gpupool-leader-epoch": "x"})
+    assert ei.value.status == 400
+
+    def boom(_):
+        raise OSError("disk full")
+    g = LeaderFence({"holder": "m-a", "epoch": 1}, boom)
+    with pytest.raises(OSError):
+        g.admit("POST", "/v1/claims", tok("m-b", 2))
+    assert g.epoch == 1  # not adopted unless durable
