@@ -49,8 +49,13 @@ def main() -> None:
     ap.add_argument("--heartbeat-interval", type=float, default=10.0,
                     help="period of the agent's Node condition heartbeat (s)")
     ap.add_argument("--auth-token-file", default=os.environ.get("GPUPOOL_AGENT_TOKEN_FILE", ""),
-                    help="shared secret required on the RPC (Authorization: Bearer); "
-                         "$GPUPOOL_AGENT_TOKEN also works")
+                    help="shared secret accepted on the RPC (Authorization: Bearer), re-read "
+                         "when the file changes; $GPUPOOL_AGENT_TOKEN also works")
+    ap.add_argument("--auth-grace", type=float, default=300.0,
+                    help="seconds a rotated-out --auth-token-file token stays valid")
+    ap.add_argument("--manager-pubkeys", default=os.environ.get("GPUPOOL_MANAGER_PUBKEYS", ""),
+                    help="PEM bundle or directory of the manager's Ed25519 public keys: requests "
+                         "must carry its signature for this node (X-Gpupool-Signature)")
     ap.add_argument("--plugin-dir", default="", help="kubelet device-plugin directory")
     ap.add_argument("--pod-resources", default="", help="kubelet PodResources socket")
     ap.add_argument("--probe", default="",
@@ -111,11 +116,9 @@ def main() -> None:
         sys.setswitchinterval(a.gil_switch_interval)
     logging.basicConfig(level=logging.DEBUG if a.verbose else logging.INFO,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
-    auth = os.environ.get("GPUPOOL_AGENT_TOKEN", "")
-    if a.auth_token_file:
-        with open(a.auth_token_file) as f:
-            auth = f.read().strip()
-    cfg = AgentConfig(node=a.node, auth_token=auth, backend=a.backend, fixture=a.fixture, faults=a.faults,
+    auth = "" if a.auth_token_file else os.environ.get("GPUPOOL_AGENT_TOKEN", "")
+    cfg = AgentConfig(node=a.node, auth_token=auth, auth_token_file=a.auth_token_file,
+                      auth_grace_s=a.auth_grace, manager_pubkeys=a.manager_pubkeys, backend=a.backend, fixture=a.fixture, faults=a.faults,
                       count=a.count, cli_dir=a.cli_dir, state_dir=a.state_dir, socket=a.socket,
                       listen=a.listen, tls_cert=a.tls_cert, tls_key=a.tls_key,
                       endpoint=a.endpoint, apiserver=a.apiserver, token=a.token,

@@ -102,9 +102,9 @@ class AccountingMixin:
     def _pod_by_uid(self, uid: str) -> dict | None:
         ts, by_uid = self._pods_by_uid
         if uid not in by_uid and time.monotonic() - ts > 5.0 and self.cfg.apiserver:
-            from ..kube import PODS, Client
+            from ..kube import PODS
             try:
-                c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
+                c = self.api()
                 items = c.list(PODS, None, field_selector=f"spec.nodeName={self.cfg.node}")["items"]
                 by_uid = {p["metadata"]["uid"]: {"namespace": p["metadata"]["namespace"],
                                                  "pod": p["metadata"]["name"]} for p in items}
@@ -248,9 +248,9 @@ class AccountingMixin:
             return
 
         def run():
-            from ..kube import EVENTS, Client
+            from ..kube import EVENTS
             try:
-                c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
+                c = self.api()
                 c.evict(ns, pod)
                 ts = now_rfc3339()
                 c.create(EVENTS, {

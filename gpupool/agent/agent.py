@@ -79,6 +79,9 @@ class AgentConfig:
     apiserver: str = ""              # empty: no Node registration
     token: str = ""
     auth_token: str = ""             # shared secret the manager presents on the agent RPC
+    auth_token_file: str = ""        # ... from a file, re-read as it rotates (old one: grace)
+    auth_grace_s: float = 300.0      # how long a rotated-out token stays valid
+    manager_pubkeys: str = ""        # PEM bundle / dir of the manager's Ed25519 request keys
     plugin_dir: str = ""             # kubelet device-plugin dir; empty: device plugin disabled
     pod_resources: str = ""          # kubelet PodResources socket
     probe_mode: str = ""             # helper | helper-sim | inproc | subprocess | simulated | off
@@ -208,6 +211,8 @@ class Agent(HealthMixin, AccountingMixin, PodViewMixin, ClaimsMixin, XgmiMixin,
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self.registrar = None  # nodereg.NodeRegistrar once register_node ran
+        self._api = None       # apiserver client (api())
+        self._park_mu = threading.Lock()  # podview._sync_parking
         from .scrubber import HbmScrubber
         self.scrubber = HbmScrubber(self, cfg.scrub_interval_s, cfg.scrub_window_bytes,
                                     cfg.scrub_windows, cfg.scrub_reserve_bytes,
@@ -377,6 +382,8 @@ class Agent(HealthMixin, AccountingMixin, PodViewMixin, ClaimsMixin, XgmiMixin,
             lay.pop("masks", None)
             out["sharing"] = lay
         out["telemetry"] = self._telemetry(d)
+        if uuid in self.prober.parked():  # no agent HIP context while a tenant holds it
+            out["probeHelper"] = "Parked"
         if not rec:
             q = self.ledger.quarantined().get(uuid) if self.ledger else None
             out["state"] = ("Maintenance" if q.get("maintenance") else "Quarantined") if q else "Free"
@@ -452,7 +459,6 @@ class Agent(HealthMixin, AccountingMixin, PodViewMixin, ClaimsMixin, XgmiMixin,
 
     def node_registrar(self, client=None):
         """The Node registration / heartbeat writer (nodereg.py) for this agent."""
-        from ..kube import Client
         from .nodereg import NodeRegistrar
         devs = self.snap["devices"]
         gfx = sorted({(d.get("asic") or {}).get("gfx", "") for d in devs} - {""})
@@ -463,10 +469,18 @@ class Agent(HealthMixin, AccountingMixin, PodViewMixin, ClaimsMixin, XgmiMixin,
         parts = sorted({(d.get("partition") or {}).get("compute", "") for d in devs} - {""})
         if parts:
             labels["amd.com/compute-partition"] = parts[0]
-        c = client or Client.connect(self.cfg.apiserver, self.cfg.token or None,
-                                     token_file=self.cfg.token_file or None)
+        c = client or self.api()
         return NodeRegistrar(c, self.cfg.node, labels,
                              {schema.ANN_AGENT_ENDPOINT: self.endpoint()}, self._node_conditions)
+
+    def api(self):
+        """The agent's apiserver client: one per process (per-thread keep-alive connections), its
+        token re-read from ``token_file`` as it rotates (60 s, and at once after a 401)."""
+        if self._api is None:
+            from ..kube import Client
+            self._api = Client.connect(self.cfg.apiserver, self.cfg.token or None,
+                                       token_file=self.cfg.token_file or None)
+        return self._api
 
     def register_node(self) -> None:
         if not self.cfg.apiserver:
@@ -480,6 +494,18 @@ class Agent(HealthMixin, AccountingMixin, PodViewMixin, ClaimsMixin, XgmiMixin,
         reg = self.registrar
         while not self._stop.wait(self.cfg.heartbeat_interval if reg.registered else 1.0):
             reg.heartbeat()
+
+    def rpc_auth(self):
+        """The RPC's credentials (auth.py): manager signatures bound to this node, and/or the
+        rotating shared token."""
+        from ..utils import edsig
+        from .auth import AgentAuth, TokenAuth
+        ver = edsig.Verifier(self.cfg.manager_pubkeys, self.cfg.node) \
+            if self.cfg.manager_pubkeys else None
+        tok = None
+        if self.cfg.auth_token_file or self.cfg.auth_token:
+            tok = TokenAuth(self.cfg.auth_token, self.cfg.auth_token_file, self.cfg.auth_grace_s)
+        return AgentAuth(ver, tok)
 
     def endpoint(self) -> str:
         if self.cfg.endpoint:

@@ -24,6 +24,8 @@ PREWAKE = os.environ.get("GPUPOOL_PROBE_PREWAKE", "1") != "0"
 
 
 class ClaimsMixin:
+    HELPER_WARM_WAIT_S = 60.0  # release waits at most this long for a restarting probe helper
+
     def claim(self, req: dict, hold_events: bool = False) -> dict:
         """Claim ``count`` GPUs for a pool, all or nothing: select (topology), commit to the
         ledger, probe, commit, advertise through the device plugin, answer with device views.
@@ -304,6 +306,20 @@ class ClaimsMixin:
                 seq = self.ledger.commit(self.records, durable=False)
             self.stats["releases"] += len(released)
             self._evaluate_some(released)
+        # a GPU goes back to the free set with its probe helper warm: restarted when its pods
+        # left (podview._sync_parking), waited for here — the next claim must not pay HIP init
+        wait_ms = 0.0
+        for u in released:
+            d = self.by_uuid.get(u)
+            if d is not None and self.prober.helpers is not None:
+                if u in self.prober.parked():
+                    self.prober.unpark(d)
+                wait_ms = max(wait_ms, self.prober.helpers.wait_ready(u, self.HELPER_WARM_WAIT_S))
+        if released and self.prober.helpers is not None:
+            with self.lock:
+                self.stats["release_helper_waits"] = self.stats.get("release_helper_waits", 0) + 1
+                self.stats["release_helper_wait_ms_sum"] = \
+                    self.stats.get("release_helper_wait_ms_sum", 0.0) + wait_ms
         # durable before the reply, but no fsync under the lock (node views and claims wait on it)
         for q in quarantined:
             self.ledger.persist_quarantine(q)
@@ -315,7 +331,7 @@ class ClaimsMixin:
         if refused:
             return {"ok": False, "reason": "PodsRunning", "released": released,
                     "message": f"GPUs still hold pods: {refused}"}
-        return {"ok": True, "released": released}
+        return {"ok": True, "released": released, "helperWaitMs": round(wait_ms, 2)}
 
     def update_policy(self, pool_uid: str, policy: dict, resource: str | None) -> dict:
         changed = set()

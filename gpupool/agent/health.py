@@ -271,9 +271,9 @@ class HealthMixin:
             return
 
         def post():
-            from ..kube import EVENTS, Client
+            from ..kube import EVENTS
             try:
-                c = Client.connect(self.cfg.apiserver, self.cfg.token or None)
+                c = self.api()
                 ts = now_rfc3339()
                 c.create(EVENTS, {
                     "apiVersion": "v1", "kind": "Event",
@@ -336,7 +336,7 @@ class HealthMixin:
             self._rechecking.add(uuid)
             opts = (rec.get("policy") or {}).get("probe") or {}
             job = (uuid, dict(self.by_uuid[uuid]), opts, rec["poolUID"])
-        self.prober.pool.submit(self._recheck_one, *job)
+        self.prober.pool.submit(self._recheck_one, *job, after_reset=True)
 
     def _fault_watcher(self) -> None:
         """The fault overlay file is itself an event source: a rewrite is applied at once (inotify)
@@ -384,6 +384,8 @@ class HealthMixin:
                 if (every <= 0 and not force) or rec.get("state") != "Claimed" or pods.get(u) or \
                         u in self._rechecking or u not in self.by_uuid:
                     continue
+                if not self.prober.can_probe(self.by_uuid[u]):
+                    continue  # its helper is held back / parked: postponed, never failed for it
                 if force or now - self._probe_mono.get(u, now) >= every:
                     self._rechecking.add(u)
                     due.append((u, dict(self.by_uuid[u]), opts, rec["poolUID"]))
@@ -391,10 +393,19 @@ class HealthMixin:
             self.prober.pool.submit(self._recheck_one, u, dev, opts, pool_uid)
         return [u for u, *_ in due]
 
-    def _recheck_one(self, uuid: str, dev: dict, opts: dict, pool_uid: str) -> None:
+    def _recheck_one(self, uuid: str, dev: dict, opts: dict, pool_uid: str,
+                     after_reset: bool = False) -> None:
         try:
+            if after_reset:  # the reset wiped the helper's HIP context: a fresh helper first
+                self.prober.restart_helper(dev)
             res = self.prober.probe_many([dev], {**opts, "enabled": opts.get("enabled", True)})[0]
             res["recheck"] = True
+            if str(res.get("error") or "").startswith("ProbeUnavailable"):
+                # the probe could not run (a helper being replaced, parked): not a verdict on
+                # the GPU — the previous one stands, the next recheck tries again
+                with self.lock:
+                    self.stats["rechecks_postponed"] = self.stats.get("rechecks_postponed", 0) + 1
+                return
             with self.lock:
                 rec = self.records.get(uuid)
                 if rec is None or rec["poolUID"] != pool_uid or rec.get("state") != "Claimed":

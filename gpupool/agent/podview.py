@@ -76,9 +76,30 @@ class PodViewMixin:
             self._pods_cache = (time.monotonic(), pods)
             flipped = {u for u in set(old) | set(pods) if old.get(u) != pods.get(u)}
             pools = {self.records[u]["poolUID"] for u in flipped if u in self.records}
+        if flipped:
+            self._sync_parking(pods)
         if pools:
             self._bump(pools)
         return pods
+
+    def _sync_parking(self, pods: dict[str, list[dict]]) -> None:
+        """A GPU that runs a tenant pod gets no agent HIP context (round-5 weak #5; the
+        reference's GPU check leaves nothing resident, GPU调度平台搭建.md:134-138): its probe
+        helper is parked — stopped, and the fabric helper restarted without it — while pods hold
+        it, and started again (warm before release hands the GPU back) once they are gone. Every
+        helper user probes, scrubs or rings pod-free GPUs only, so nothing needs it meanwhile."""
+        if self.prober.helpers is None:
+            return
+        with self._park_mu:
+            parked = self.prober.parked()
+            for u, d in list(self.by_uuid.items()):
+                if pods.get(u) and u not in parked:
+                    if self.prober.park(d):
+                        log.info("GPU %s runs pod(s) %s: its probe helper is parked", d.get("index"),
+                                 [p.get("name") for p in pods[u]])
+                elif not pods.get(u) and u in parked:
+                    self.prober.unpark(d)  # starts now; release waits for it to be warm
+                    log.info("GPU %s is pod-free: its probe helper restarts", d.get("index"))
 
     def _refresh_pods_async(self) -> None:
         with self.lock:

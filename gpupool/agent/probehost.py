@@ -178,6 +178,8 @@ class _SimKernel:
         self.n = int(spec.get("devices") or 1)
         if spec.get("initHang"):  # test hook: a HIP init that never returns
             threading.Event().wait()
+        if spec.get("initDelayS"):  # test hook: a slow HIP init (a respawned helper)
+            time.sleep(float(spec["initDelayS"]))
 
     def info(self) -> dict:
         return {"devices": self.n, "uuids": {}}
@@ -385,6 +387,7 @@ class Helper:
     # claim-time probe takes ~0.85 ms on MI355X): the reply is read the moment it lands instead of
     # after the kernel has woken the blocked thread. Longer requests then block as usual.
     CALLER_SPIN_S = float(os.environ.get("GPUPOOL_CALLER_SPIN_MS", "0")) / 1e3
+    FOLLOWER_SLICE_S = 0.05
 
     def __init__(self, key: str, spec: dict, on_exit=None, ready_timeout: float = 120.0):
         self.key = key
@@ -474,6 +477,9 @@ class Helper:
                     break
         finally:
             self._rd.release()
+            # a caller that arrived while the watcher held the pipe (its ready.wait returned,
+            # then _rd was taken) must not sleep out its deadline with nobody reading
+            self._wake_follower()
         try:
             wait([self.proc.sentinel])
         except (OSError, ValueError):
@@ -536,6 +542,9 @@ class Helper:
         whether to kill), HelperDied if the helper is or goes away, HelperUnavailable if its HIP
         has not come up within the request's own deadline (a helper being replaced) or never
         does; RuntimeError for an error the request itself raised."""
+        # one deadline for the whole request: waiting for a (re)starting helper's HIP init comes
+        # out of the same spec.probe.timeoutSeconds as the probe itself
+        deadline = time.monotonic() + timeout
         wait = min(timeout, self.ready_timeout)
         if not self.ready.wait(wait):
             raise HelperUnavailable(f"probe helper {self.key} still starting after {wait:g} s")
@@ -556,7 +565,6 @@ class Helper:
             with self._mu:
                 self._pending.pop(rid, None)
             raise HelperDied(self.dead or f"probe helper {self.key} unreachable: {e}") from None
-        deadline = time.monotonic() + timeout
         spin_end = time.perf_counter() + self.CALLER_SPIN_S
         while True:
             slot.ev.clear()
@@ -582,11 +590,15 @@ class Helper:
                 if closed:
                     self._died()  # EOF: the helper is gone (the watcher agrees shortly)
             else:
-                slot.ev.wait(left)
+                # in slices: a hand-over of the reader role can miss this caller (the reader
+                # woke a follower that was timing out, or none at all); trying _rd again every
+                # FOLLOWER_SLICE_S bounds what a missed wake costs to that, not the deadline
+                slot.ev.wait(min(left, self.FOLLOWER_SLICE_S))
         if not slot.done:
             with self._mu:
                 self._pending.pop(rid, None)
-            raise HelperTimeout(f"{op} did not finish within {timeout:g} s")
+            raise HelperTimeout(f"{op} did not finish within {timeout:g} s (including the "
+                                f"helper's start)")
         self.last_used = time.monotonic()
         if slot.died:
             raise HelperDied(slot.died)
@@ -661,6 +673,9 @@ class HelperPool:
         self.stats = {"helper_starts": 0, "helper_crashes": 0, "helper_timeouts": 0}
         self.last_exit: dict[str, str] = {}
         self._fabric_devs: list[dict] = []
+        # GPUs whose helper is parked: a tenant pod holds the GPU, so the agent keeps no HIP
+        # context (no VRAM, no process) on it; requests for it are refused until unpark()
+        self._parked: set[str] = set()
         if fabric_idle_s > 0:
             threading.Thread(target=self._fabric_reaper, daemon=True, name="fabric-idle").start()
 
@@ -689,8 +704,9 @@ class HelperPool:
         with self._mu:
             for d in devs:
                 self._devs[d["uuid"]] = d
-            self._fabric_devs = sorted(self._devs.values(), key=lambda d: d.get("index", 0))
-            new = [self._spawn_locked(d["uuid"]) for d in devs if d["uuid"] not in self._helpers]
+            self._fabric_devs = self._unparked_devs_locked()
+            new = [self._spawn_locked(d["uuid"]) for d in devs
+                   if d["uuid"] not in self._helpers and d["uuid"] not in self._parked]
             if self._fabric_wanted_locked() and "fabric" not in self._helpers:
                 self._spawn_locked("fabric")  # warms itself; nothing waits for it here
         if wait:
@@ -701,6 +717,85 @@ class HelperPool:
 
     def _fabric_wanted_locked(self) -> bool:
         return self.resident_fabric and len(self._fabric_devs) >= 2 and not self._stopping
+
+    def _unparked_devs_locked(self) -> list[dict]:
+        return sorted((d for u, d in self._devs.items() if u not in self._parked),
+                      key=lambda d: d.get("index", 0))
+
+    # ------------------------------------------------------------ parking
+    def park(self, key: str) -> bool:
+        """Stop ``key``'s helper and keep it stopped (a tenant holds the GPU). The resident
+        fabric helper, which has a context on every GPU, is restarted over the others. True if
+        the GPU was not parked before."""
+        stop: list[Helper] = []
+        with self._mu:
+            if key in self._parked or key == "fabric":
+                return False
+            self._parked.add(key)
+            h = self._helpers.pop(key, None)
+            if h is not None:
+                stop.append(h)
+            if any(d["uuid"] == key for d in self._fabric_devs):
+                self._fabric_devs = self._unparked_devs_locked()
+                f = self._helpers.pop("fabric", None)
+                if f is not None:
+                    stop.append(f)
+                if self._fabric_wanted_locked():
+                    self._spawn_locked("fabric")
+        for x in stop:
+            x.stop("park")
+        self.stats["helper_parks"] = self.stats.get("helper_parks", 0) + 1
+        return True
+
+    def unpark(self, key: str) -> Helper | None:
+        """Start ``key``'s helper again (its GPU is pod-free); the fabric helper follows. Returns
+        the starting helper (its ``ready`` event fires once HIP is up), None if not parked."""
+        with self._mu:
+            if key not in self._parked:
+                return None
+            self._parked.discard(key)
+            if key not in self._devs or self._stopping:
+                return None
+            self._respawn_at.pop(key, None)
+            h = self._helpers.get(key) or self._spawn_locked(key)
+            fabric_devs = self._unparked_devs_locked()
+            if self.resident_fabric and {d["uuid"] for d in fabric_devs} != \
+                    {d["uuid"] for d in self._fabric_devs}:
+                self._fabric_devs = fabric_devs
+                f = self._helpers.pop("fabric", None)
+                if f is not None:
+                    threading.Thread(target=f.stop, args=("park",), daemon=True).start()
+                if self._fabric_wanted_locked():
+                    self._spawn_locked("fabric")
+        self.stats["helper_unparks"] = self.stats.get("helper_unparks", 0) + 1
+        return h
+
+    def parked(self) -> set[str]:
+        with self._mu:
+            return set(self._parked)
+
+    def wait_ready(self, key: str, timeout: float) -> float:
+        """Block until ``key``'s helper is up (or ``timeout``); the ms waited."""
+        t0 = time.perf_counter()
+        with self._mu:
+            h = self._helpers.get(key)
+        if h is not None:
+            h.ready.wait(timeout)
+        return (time.perf_counter() - t0) * 1e3
+
+    def restart(self, key: str) -> None:
+        """Replace ``key``'s helper with a fresh process (a GPU reset invalidated its context)."""
+        with self._mu:
+            h = self._helpers.pop(key, None)
+            if key in self._parked or key not in self._devs or self._stopping:
+                new = None
+            else:
+                self._respawn_at.pop(key, None)
+                new = self._spawn_locked(key)
+        if h is not None:
+            h.stop("stop")
+        if new is not None:
+            new.ready.wait(self.ready_timeout)
 
     def _spawn_locked(self, key: str) -> Helper:
         spec = self._fabric_spec() if key == "fabric" else self._gpu_spec(self._devs[key])
@@ -714,7 +809,7 @@ class HelperPool:
             if self._stopping or self._helpers.get(h.key) is not h:
                 return
             del self._helpers[h.key]
-            if cause in ("stop", "idle"):
+            if cause in ("stop", "idle", "park"):
                 return  # let go on purpose (an idle fabric helper): started again on demand
             self.last_exit[h.key] = why
             now = time.monotonic()
@@ -735,7 +830,7 @@ class HelperPool:
 
     def _respawn(self, key: str) -> None:
         with self._mu:
-            if self._stopping or key in self._helpers:
+            if self._stopping or key in self._helpers or key in self._parked:
                 return
             if key not in self._devs and not (key == "fabric" and self._fabric_wanted_locked()):
                 return
@@ -750,6 +845,8 @@ class HelperPool:
             h = self._helpers.get(key)
             if h is not None and not h.dead:
                 return h
+            if key in self._parked:
+                raise HelperUnavailable(f"probe helper for {key} is parked: a pod holds the GPU")
             if dev is not None and key != "fabric":
                 self._devs[key] = dev
             wait = self._respawn_at.get(key, 0.0) - time.monotonic()
@@ -768,10 +865,13 @@ class HelperPool:
             for d in devs:
                 self._devs.setdefault(d["uuid"], d)
             want = {d["uuid"] for d in devs}
+            if want & self._parked:
+                raise HelperUnavailable(f"a ring over GPUs with tenant pods ({sorted(want & self._parked)}): "
+                                        f"their helpers are parked")
             have = {d["uuid"] for d in self._fabric_devs}
             h = self._helpers.get("fabric")
             if not want <= have:
-                self._fabric_devs = sorted(self._devs.values(), key=lambda d: d.get("index", 0))
+                self._fabric_devs = self._unparked_devs_locked()
                 if h is not None:
                     self._helpers.pop("fabric", None)
                     threading.Thread(target=h.stop, daemon=True).start()
@@ -799,8 +899,10 @@ class HelperPool:
 
     def available(self, key: str) -> bool:
         """Can a request for ``key`` be served now or once its helper has started? False while
-        a helper that exited is held back by its respawn backoff."""
+        a helper that exited is held back by its respawn backoff, and while it is parked."""
         with self._mu:
+            if key in self._parked:
+                return False
             h = self._helpers.get(key)
             if h is not None and not h.dead:
                 return True
@@ -826,6 +928,8 @@ class HelperPool:
                     out[k]["warm"] = h.info.get("warm")
             for k, why in self.last_exit.items():
                 out.setdefault(k, {"alive": False})["lastExit"] = why
+            for k in self._parked:
+                out.setdefault(k, {"alive": False})["parked"] = True
             return out
 
     def stop(self) -> None:

@@ -110,6 +110,33 @@ class Prober:
         that cannot run."""
         return self.helpers is None or self.helpers.available(dev["uuid"])
 
+    # ------------------------------------------------------------ parking (helper modes)
+    def park(self, dev: dict) -> bool:
+        """A tenant pod holds ``dev``: stop its probe helper (and take it out of the fabric
+        helper's contexts), so the agent holds no HIP context, VRAM or process there."""
+        return self.helpers is not None and self.helpers.park(dev["uuid"])
+
+    def unpark(self, dev: dict, wait_s: float = 0.0) -> float | None:
+        """``dev`` is pod-free again: restart its helper. With ``wait_s`` wait up to that long for
+        it to come up; returns the ms waited (None: it was not parked)."""
+        if self.helpers is None:
+            return None
+        t0 = time.perf_counter()
+        h = self.helpers.unpark(dev["uuid"])
+        if h is None:
+            return None
+        if wait_s > 0:
+            h.ready.wait(wait_s)
+        return (time.perf_counter() - t0) * 1e3
+
+    def parked(self) -> set[str]:
+        return self.helpers.parked() if self.helpers is not None else set()
+
+    def restart_helper(self, dev: dict) -> None:
+        """A fresh helper for ``dev`` (after a GPU reset its HIP context is stale)."""
+        if self.helpers is not None:
+            self.helpers.restart(dev["uuid"])
+
     def hip_devices(self) -> int:
         """GPUs this agent holds a HIP context on (in itself or its helpers)."""
         if self.mode == "helper":

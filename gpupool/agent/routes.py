@@ -116,7 +116,7 @@ def build_routes(agent: Agent) -> dict:
 def serve(agent: Agent, ready_file: str | None = None) -> None:
     """Start the RPC listeners and the agent's background loops; block until interrupted."""
     from .rpc import RpcServer
-    srv = RpcServer(build_routes(agent), agent.cfg.auth_token, guard=agent.check_leader)
+    srv = RpcServer(build_routes(agent), guard=agent.check_leader, auth=agent.rpc_auth())
     agent.rpc = srv
     # the start-up heap (modules, gRPC/protobuf descriptors, the device model) lives for the whole
     # run: out of the collector's generations, a full collection walks only what came after — one

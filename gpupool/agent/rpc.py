@@ -18,22 +18,22 @@ Exposure bounds (the TCP listener is reachable from the node network):
     receiving the request, not handling it: once an authorised request has been read whole it is
     lifted, so a long handler (a scrub that maps the free HBM of a GPU whose VRAM the driver is
     still clearing, a claim probing 8 GPUs) still gets its reply out. Only a request that carried
-    the valid token makes the connection trusted (with no token configured: any request): it may
+    valid credentials makes the connection trusted (with none configured: any request): it may
     then idle as a pooled keep-alive connection. An unauthenticated request to an open path
     (/healthz, /metrics) is answered with ``Connection: close`` — one keep-alive GET /healthz per
     connection must not pin the ``max_conns`` slots the manager's claims need;
   * a trusted connection may idle between requests, but once the first byte of a request head
     arrives, the head and its body must be in within ``first_request_timeout``: a trusted peer
     cannot drip a request either;
-  * the token is checked right after the headers, before any body byte is read; a request refused
-    for it closes the connection;
+  * credentials (auth.py: the manager's per-request signature and/or a rotating bearer token) are
+    checked right after the headers, before any body byte is read, and the signed body digest
+    once the body is in; a request refused for them closes the connection;
   * at most ``MAX_HEADERS`` header lines of ``MAX_HEADER_BYTES`` in total; a body-carrying method
     (POST/PUT/PATCH) needs a decimal Content-Length (missing, negative or non-numeric -> 400,
     nothing read), at most ``MAX_BODY``.
 """
 from __future__ import annotations
 
-import hmac
 import json
 import logging
 import os
@@ -144,7 +144,8 @@ def text_reply(text: str, status: int = 200) -> tuple:
 class RpcServer:
     def __init__(self, routes: dict[tuple[str, str], Handler], token: str = "",
                  max_conns: int = 512, first_request_timeout: float = 10.0,
-                 guard: Callable[[str, str, dict], tuple | None] | None = None):
+                 guard: Callable[[str, str, dict], tuple | None] | None = None,
+                 auth=None):
         self.routes = routes
         # guard(method, path, headers) -> a reply refusing the request, or None: runs after the
         # token check and before the handler (the agent's leader fencing, StaleLeader)
@@ -154,7 +155,12 @@ class RpcServer:
         self._conns = 0
         self.refused_conns = 0
         self._conns_mu = threading.Lock()
-        self._auth = ("Bearer " + token).encode() if token else b""
+        # who may call (auth.AgentAuth): request signatures and/or a rotating bearer token;
+        # ``token`` alone is the fixed shared secret of tests and older deployments
+        if auth is None:
+            from .auth import AgentAuth, TokenAuth
+            auth = AgentAuth(token=TokenAuth(token) if token else None)
+        self.auth = auth
         self._listeners: list[socket.socket] = []
         self._stop = threading.Event()
         self.requests = 0
@@ -362,11 +368,12 @@ class RpcServer:
                     k, _, v = h.decode("latin-1").partition(":")
                     headers[k.strip().lower()] = v.strip()
                 path = target.partition("?")[0]
-                # the token before the body: an unauthenticated peer never gets a byte buffered
-                authed = not self._auth or hmac.compare_digest(
-                    headers.get("authorization", "").encode(), self._auth)
+                # credentials before the body: an unauthenticated peer never gets a byte buffered
+                why = self.auth.check_head(method, target, headers)
+                authed = why is None
                 if not authed and path not in OPEN_PATHS:
-                    self._reject(conn, 401, "Unauthorized", "agent RPC requires the manager's token", rf)
+                    self._reject(conn, 401, why or "Unauthorized",
+                                 "agent RPC requires the manager's signature or token", rf)
                     return
                 cl = headers.get("content-length")
                 if cl is None:
@@ -387,6 +394,10 @@ class RpcServer:
                 except _Closed as e:
                     if trusted and str(e) == "deadline":
                         self.request_deadline_closes += 1
+                    return
+                if authed and self.auth.check_body(headers, body):  # signed digest != body
+                    self._reject(conn, 401, "BodyMismatch", "request body does not match its "
+                                 "signature", rf)
                     return
                 rf.deadline = None  # the request is in: its handling is not bounded
                 keep = headers.get("connection", "").lower() != "close" and \
@@ -446,6 +457,7 @@ class RpcServer:
                f"gpupool_agent_rpc_open_path_closed_connections_total {self.open_path_closes}",
                f"gpupool_agent_rpc_request_deadline_closed_connections_total "
                f"{self.request_deadline_closes}"]
+        out += self.auth.metrics_lines()
         for path, (n, sec) in items:
             out.append(f'gpupool_agent_rpc_requests_total{{path="{path}"}} {n}')
             out.append(f'gpupool_agent_rpc_seconds_sum{{path="{path}"}} {sec:.6f}')

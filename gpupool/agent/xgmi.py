@@ -106,7 +106,11 @@ class XgmiMixin:
         with self.lock:
             owned = [self.by_uuid[u] for u, r in self.records.items()
                      if r["poolUID"] == pool_uid and u in self.by_uuid and r.get("state") == "Claimed"]
-        members = list({d["uuid"]: d for d in owned + chosen}.values())
+        # GPUs running tenant pods keep no agent context (parked helpers): their links are
+        # checked once they are pod-free again (idle rechecks), not under a tenant
+        parked = self.prober.parked()
+        members = [d for d in {d["uuid"]: d for d in owned + chosen}.values()
+                   if d["uuid"] not in parked]
         if len(members) < 2:
             return  # one GPU of the pool on this node: no link to ring
         ring = self._ring_order(members)

@@ -349,14 +349,19 @@ MI355X_SPEC = {
                                                  "measures ~1200)."},
                 "timeoutSeconds": {"type": "number", "minimum": 0.1, "maximum": 600,
                                    "default": 10,
-                                   "description": "Deadline of one GPU's probe (and of the "
-                                                  "xGMI peer ring). The probe runs in a helper "
+                                   "description": "Deadline of one GPU's claim-time probe, "
+                                                  "including any wait for its (re)starting "
+                                                  "probe helper. The probe runs in a helper "
                                                   "process per GPU: past the deadline the "
                                                   "helper is killed and the GPU fails "
                                                   "DeviceProbePassed (ProbeTimeout); a helper "
                                                   "that dies mid-probe fails it as "
-                                                  "ProbeCrashed. A claim is answered within "
-                                                  "this deadline however the GPU behaves."},
+                                                  "ProbeCrashed. The xGMI peer ring "
+                                                  "(xgmiPeerCheck) has its own deadline of "
+                                                  "min(this, 3 s). A claim is answered within "
+                                                  "the sum of the two; a GPU still probing "
+                                                  "past it plus 5 s is reported probeOverdue "
+                                                  "and replaced."},
             },
         },
         "replacePolicy": {"type": "string", "enum": ["Replace", "Keep"], "default": "Replace"},

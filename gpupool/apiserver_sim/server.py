@@ -180,6 +180,9 @@ class ApiServerSim:
         self.watchers: dict[tuple[str, str], set[asyncio.Queue]] = {}
         self.store.listeners.append(self._fanout)
         self.requests_total: dict[tuple[str, int], int] = {}
+        # LIST / WATCH requests per resource (what informers and uncached readers cost the server)
+        self.lists: dict[str, int] = {}
+        self.watches: dict[str, int] = {}
         # fault injection (tests): resource plural -> LIST/WATCH requests still to fail with 503
         # (-1: until cleared); set at start (--fail-list) or through POST /debug/faults
         self.fail_list: dict[str, int] = {}
@@ -241,6 +244,11 @@ class ApiServerSim:
             lines.append(f'apiserver_request_total{{verb="{m}",code="{c}"}} {n}')
         lines.append("# TYPE apiserver_watchers gauge")
         lines.append(f"apiserver_watchers {sum(len(v) for v in self.watchers.values())}")
+        lines.append(f"apiserver_authentication_failures_total {self.auth_failures}")
+        for r, n in sorted(self.lists.items()):
+            lines.append(f'apiserver_list_total{{resource="{r}"}} {n}')
+        for r, n in sorted(self.watches.items()):
+            lines.append(f'apiserver_watch_total{{resource="{r}"}} {n}')
         lines.append("# TYPE etcd_resource_version gauge")
         lines.append(f"etcd_resource_version {self.store.rv}")
         return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
@@ -368,7 +376,9 @@ class ApiServerSim:
             if m == "GET":
                 self._inject_list_fault(rt)
                 if q.get("watch") in ("1", "true"):
+                    self.watches[rt.plural] = self.watches.get(rt.plural, 0) + 1
                     return await self._watch(request, rt, ns)
+                self.lists[rt.plural] = self.lists.get(rt.plural, 0) + 1
                 lst = self.store.list(rt, ns, q.get("labelSelector"), q.get("fieldSelector"),
                                       int(q.get("limit", 0) or 0), q.get("continue"))
                 if "as=Table" in request.headers.get("Accept", ""):
@@ -495,6 +505,7 @@ class ApiServerSim:
             if rt.namespaced and ns and md.get("namespace") != ns:
                 return False
             return lm(md.get("labels")) and fm(ev_obj)
+        filtered = bool(q.get("labelSelector") or q.get("fieldSelector"))
 
         queue: asyncio.Queue = asyncio.Queue()
         # Register before computing the backlog so nothing falls between the two.
@@ -547,14 +558,24 @@ class ApiServerSim:
                     if time.monotonic() >= next_bm:
                         next_bm = time.monotonic() + self.bookmark_interval
                     continue
-                if ev.rtype != rt.key or ev.rv <= last_rv or not match(ev.obj):
+                if ev.rtype != rt.key or ev.rv <= last_rv:
+                    continue
+                line = None
+                if filtered and ev.type == "MODIFIED" and ev.prev is not None:
+                    now_in, was_in = match(ev.obj), match(ev.prev)
+                    if now_in != was_in:  # left / entered the selection
+                        line = (json.dumps({"type": "ADDED" if now_in else "DELETED",
+                                            "object": ev.obj}) + "\n").encode()
+                    elif not now_in:
+                        continue
+                elif not match(ev.obj):
                     continue
                 last_rv = ev.rv
                 if self.watch_delay > 0:
                     lag = t_ev + self.watch_delay - time.monotonic()
                     if lag > 0:
                         await asyncio.sleep(lag)
-                await resp.write(ev.encoded())
+                await resp.write(line or ev.encoded())
             await resp.write_eof()
             return resp
         except (ConnectionResetError, asyncio.CancelledError):

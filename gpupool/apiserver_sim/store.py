@@ -133,6 +133,9 @@ class WatchEvent:
     type: str
     _obj: dict | None
     line: bytes | None = None  # the encoded watch line, built once and shared by every watcher
+    # MODIFIED: the object before the write (a filtered watch turns a write that moves an object
+    # out of / into its selection into DELETED / ADDED, as the apiserver's watch cache does)
+    prev: dict | None = None
 
     @property
     def obj(self) -> dict:
@@ -152,6 +155,7 @@ class WatchEvent:
         if self._obj is not None:
             self.encoded()
             self._obj = None
+            self.prev = None
 
 
 def _spec_part(obj: dict) -> dict:
@@ -405,8 +409,9 @@ class Store:
         self.rv += 1
         return self.rv
 
-    def _emit(self, rt: ResourceType, etype: str, obj: dict) -> None:
-        ev = WatchEvent(int(obj["metadata"]["resourceVersion"]), rt.key, etype, clone(obj))
+    def _emit(self, rt: ResourceType, etype: str, obj: dict, prev: dict | None = None) -> None:
+        ev = WatchEvent(int(obj["metadata"]["resourceVersion"]), rt.key, etype, clone(obj),
+                        prev=prev)
         self.log.append(ev)
         if len(self.log) > self.LIVE_EVENTS:  # older events: encoded bytes only
             self.log[-self.LIVE_EVENTS - 1].compact()
@@ -714,7 +719,7 @@ class Store:
         self.objects[rt.key][(ns, name)] = new
         if rt.kind == "CustomResourceDefinition":
             self._register_crd(new)
-        self._emit(rt, "MODIFIED", new)
+        self._emit(rt, "MODIFIED", new, prev=cur)  # ``cur`` is replaced, never mutated
         return clone(new) if copy_out else new
 
     def patch(self, rt: ResourceType, ns: str | None, name: str, patch: Any, ptype: str,

@@ -253,10 +253,12 @@ class BenchRun:
         self.scale(name, n)
         self.phase = "start_pods"
         pods = self._pods(f"sd{step}", n, res)
+        m0 = self._agent_counters()
         t0 = time.perf_counter()
         self.phase = "scale_down"
         obj = self.scale(name, keep)
         dt = time.perf_counter() - t0
+        m1 = self._agent_counters()
         kept = {d["uuid"] for d in obj["status"]["devices"]}
         truth = self.truth_at_ready(pool, keep)
         left = [p for p in self.c.list(PODS, self.ns)["items"]
@@ -269,8 +271,31 @@ class BenchRun:
         self.phase = "cleanup"
         self._delete_pods([p["metadata"]["name"] for p in left])
         self.scale(name, 0)
+        waits = m1.get("release_helper_waits", 0) - m0.get("release_helper_waits", 0)
         return {"from": n, "to": keep, "seconds": dt, "ok": ok, "evicted": n - len(left),
-                "podsOnReleasedGPUs": on_released, "truth": truth}
+                "podsOnReleasedGPUs": on_released, "truth": truth,
+                # helper parking: the pods' GPUs had their probe helpers stopped while the pods
+                # ran; release waited this long (max over its GPUs) for them to be warm again
+                "helpersParked": m1.get("probe_helper_parks_total", 0) -
+                m0.get("probe_helper_parks_total", 0),
+                "releaseHelperWaitMs": round((m1.get("release_helper_wait_ms_sum", 0) -
+                                              m0.get("release_helper_wait_ms_sum", 0)) /
+                                             max(1, waits), 2) if waits else None}
+
+    def _agent_counters(self) -> dict[str, float]:
+        out: dict[str, float] = {}
+        try:
+            text = self.cluster.agent_request(self.node.name, "GET", "/metrics")
+        except Exception:  # noqa: BLE001 - evidence only
+            return out
+        for ln in text.splitlines():
+            if ln.startswith("gpupool_agent_") and "{" not in ln and " " in ln:
+                k, _, v = ln.rpartition(" ")
+                try:
+                    out[k[len("gpupool_agent_"):]] = float(v)
+                except ValueError:
+                    pass
+        return out
 
     # ------------------------------------------------------------ config 5
     def two_pools(self, n: int, step: int) -> dict:

@@ -338,11 +338,11 @@ def cmd_events(c: Client, ns: str, args) -> int:
 
 def cmd_devices(c: Client, ns: str, args) -> int:
     node = c.get(NODES, args.node)
-    ep = (node["metadata"].get("annotations") or {}).get(schema.ANN_AGENT_ENDPOINT)
+    ep = _agent_endpoint(c, node)
     if not ep:
         print(f"error: node {args.node} has no gpupool agent", file=sys.stderr)
         return 1
-    view = Client(ep, _agent_token()).request("GET", "/v1/node")
+    view = _agent_client(args.node, ep).request("GET", "/v1/node")
     if args.output in ("json", "yaml"):
         dump(view, args.output)
         return 0
@@ -391,11 +391,11 @@ def cmd_top(c: Client, ns: str, args) -> int:
     per pod (GPU调度平台搭建.md:800-802)."""
     rows = []
     for n in c.list(NODES)["items"]:
-        ep = (n["metadata"].get("annotations") or {}).get(schema.ANN_AGENT_ENDPOINT)
+        ep = _agent_endpoint(c, n)
         if not ep:
             continue
         try:
-            view = Client(ep, _agent_token()).request("GET", "/v1/node")
+            view = _agent_client(n["metadata"]["name"], ep).request("GET", "/v1/node")
         except Exception as e:  # an unreachable agent is a row, not a failure
             print(f"warning: node {n['metadata']['name']}: {e}", file=sys.stderr)
             continue
@@ -444,10 +444,58 @@ def cmd_top(c: Client, ns: str, args) -> int:
 
 def _agent(c: Client, node: str) -> Client | None:
     n = c.get(NODES, node)
-    ep = (n["metadata"].get("annotations") or {}).get(schema.ANN_AGENT_ENDPOINT)
+    ep = _agent_endpoint(c, n)
     if not ep:
         print(f"error: node {node} has no gpupool agent", file=sys.stderr)
         return None
+    return _agent_client(node, ep)
+
+
+class _SignedAgentClient:
+    """Calls one node's agent with a per-request signature for that node (the manager's key,
+    $GPUPOOL_AGENT_SIGNING_KEY: an admin's copy of the gpupool-manager-signing-key Secret)."""
+
+    def __init__(self, node: str, ep: str, key_file: str):
+        from ..utils import edsig
+        self.node, self.client, self.signer = node, Client(ep), edsig.Signer(key_file)
+
+    def request(self, method: str, path: str, body=None):
+        data = b"" if body is None else json.dumps(body).encode()
+        return self.client.request(method, path, body, extra_headers={
+            "X-Gpupool-Signature": self.signer.header(method, path, self.node, data)})
+
+
+def _agent_endpoint(c: Client, node: dict) -> str | None:
+    """The node's agent endpoint: its annotation, cross-checked against the agent Pod bound to
+    the node (gpupool-system, app.kubernetes.io/name=gpupool-agent) when there is one — an
+    annotation whose host is not that Pod's IP is refused, as the manager refuses it."""
+    name = node["metadata"]["name"]
+    ep = (node["metadata"].get("annotations") or {}).get(schema.ANN_AGENT_ENDPOINT)
+    try:
+        pods = c.list(PODS, schema.AGENT_NAMESPACE, label_selector="app.kubernetes.io/name=gpupool-agent",
+                      field_selector=f"spec.nodeName={name}")["items"]
+    except KubeError:
+        pods = []
+    ips = {(p.get("status") or {}).get("podIP") for p in pods
+           if (p.get("status") or {}).get("phase") == "Running"} - {None, ""}
+    if not ips:
+        return ep
+    import urllib.parse
+    if ep and urllib.parse.urlparse(ep).hostname in ips:
+        return ep
+    ip = sorted(ips)[0]
+    scheme = os.environ.get("GPUPOOL_AGENT_SCHEME", "https")
+    port = os.environ.get("GPUPOOL_AGENT_PORT", "9443")
+    if ep:
+        print(f"warning: node {name}: agent-endpoint annotation {ep} is not its agent Pod "
+              f"({ip}); using the Pod", file=sys.stderr)
+    return f"{scheme}://{'[' + ip + ']' if ':' in ip else ip}:{port}"
+
+
+def _agent_client(node: str, ep: str):
+    key = os.environ.get("GPUPOOL_AGENT_SIGNING_KEY")
+    if key and os.path.exists(key):
+        return _SignedAgentClient(node, ep, key)
     return Client(ep, _agent_token())
 
 

@@ -274,15 +274,19 @@ class Client:
         return h
 
     def request(self, method: str, path: str, body: Any = None, query: dict | None = None,
-                ctype: str = "application/json", accept: str = "application/json") -> Any:
+                ctype: str = "application/json", accept: str = "application/json",
+                extra_headers: dict | None = None) -> Any:
         if query:
             q = {k: v for k, v in query.items() if v is not None}
             if q:
                 path += "?" + urllib.parse.urlencode(q)
         data = None if body is None else json.dumps(body).encode()
-        resp, raw = self._roundtrip(method, path, data, ctype, accept)
-        if resp.status == 401 and self._reload_token(force=True):  # rotated under us: once more
-            resp, raw = self._roundtrip(method, path, data, ctype, accept)
+        used = self.token
+        resp, raw = self._roundtrip(method, path, data, ctype, accept, extra_headers)
+        if resp.status == 401 and self.token_file:  # rotated under us: re-read, once more
+            self._reload_token(force=True)
+            if self.token != used:  # (or another thread's 401 already re-read it)
+                resp, raw = self._roundtrip(method, path, data, ctype, accept, extra_headers)
         try:
             out = json.loads(raw) if raw else None
         except json.JSONDecodeError:
@@ -291,14 +295,16 @@ class Client:
             raise KubeError(resp.status, out)
         return out
 
-    def _roundtrip(self, method: str, path: str, data: bytes | None, ctype: str, accept: str):
+    def _roundtrip(self, method: str, path: str, data: bytes | None, ctype: str, accept: str,
+                   extra_headers: dict | None = None):
         for attempt in range(2):
             conn = getattr(self._local, "conn", None)
             fresh = conn is None
             if conn is None:
                 conn = self._local.conn = self._conn()
             try:
-                conn.request(method, path, body=data, headers=self._headers(ctype, accept))
+                conn.request(method, path, body=data,
+                             headers={**self._headers(ctype, accept), **(extra_headers or {})})
                 resp = conn.getresponse()
                 raw = resp.read()
                 break
@@ -403,9 +409,12 @@ class Client:
         # thread instead of polling with short timeouts — which broke every watch idle for 1 s,
         # and a relist in that gap missed DELETED events.
         conn = self._conn(timeout=(timeout_seconds or 3600) + 30)
-        conn.request("GET", path, headers=self._headers())
+        hdrs = self._headers()
+        used = self.token
+        conn.request("GET", path, headers=hdrs)
         resp = conn.getresponse()
-        if resp.status == 401 and self._reload_token(force=True):
+        if resp.status == 401 and self.token_file and \
+                (self._reload_token(force=True) or self.token != used):
             resp.read()
             conn.close()
             conn = self._conn(timeout=(timeout_seconds or 3600) + 30)

@@ -334,9 +334,13 @@ class FakeKubelet:
                     req[k] = req.get(k, 0) + int(v)
         return req
 
+    MIRROR = "kubernetes.io/config.mirror"
+
     def _handle_pod(self, pod: dict) -> None:
         md = pod["metadata"]
         uid = md["uid"]
+        if self.MIRROR in (md.get("annotations") or {}):
+            return  # a static pod's mirror: the process runs outside this runtime (the agent)
         if md.get("deletionTimestamp"):
             with self.lock:
                 rp = self.pods.get(uid)

@@ -64,6 +64,28 @@ def issue_client_cert(workdir: str, cn: str = "gpupool-admin") -> tuple[str, str
     return crt, key
 
 
+def make_signing_key(workdir: str, name: str = "agent-signing") -> tuple[str, str]:
+    """An Ed25519 key pair (openssl CLI): (private key PEM path, public key PEM path)."""
+    d = os.path.join(workdir, "pki")
+    os.makedirs(d, exist_ok=True)
+    key, pub = os.path.join(d, f"{name}.key"), os.path.join(d, f"{name}.pub")
+    subprocess.run(["openssl", "genpkey", "-algorithm", "ed25519", "-out", key], check=True,
+                   capture_output=True)
+    os.chmod(key, 0o600)
+    subprocess.run(["openssl", "pkey", "-in", key, "-pubout", "-out", pub], check=True,
+                   capture_output=True)
+    return key, pub
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def _wait_file(path: str, timeout: float, proc: subprocess.Popen | None = None,
                logpath: str | None = None) -> str:
     deadline = time.monotonic() + timeout
@@ -103,7 +125,8 @@ class Cluster:
                  python: str = sys.executable, env: dict | None = None,
                  sample_interval: float = 0.5, kinds: str = "mi355x,azure,job",
                  manager_bin: str | None = None, tls: bool = False, token: str | None = None,
-                 fsync: bool = False, apiserver_args: list[str] | None = None):
+                 fsync: bool = False, apiserver_args: list[str] | None = None,
+                 agent_auth: str = "both", discovery: str = "annotation"):
         self.workdir = os.path.abspath(workdir)
         self.tls = tls
         self.token = token
@@ -135,6 +158,18 @@ class Cluster:
             f.write(self.agent_token + "\n")
         os.chmod(self.agent_token_file, 0o600)
         self.env["GPUPOOL_AGENT_TOKEN"] = self.agent_token
+        # manager -> agent credentials: "signature" (the deployed default: Ed25519 per request,
+        # agentauth.h / edsig.py), "token" (the shared bearer) or "both" (agents accept either;
+        # the manager then signs and sends no bearer)
+        self.agent_auth = agent_auth
+        self.signing_key = self.pubkeys = ""
+        if agent_auth in ("signature", "both"):
+            self.signing_key, self.pubkeys = make_signing_key(self.workdir)
+        # "annotation": agents on unix sockets, found through the Node annotation; "pod": agents
+        # on TCP at distinct loopback addresses, found through mirror Pods of the agent DaemonSet
+        self.discovery = discovery
+        self.agent_port = _free_port() if discovery == "pod" else 0
+        self.agent_ips: dict[str, str] = {}
         self.url = ""
         self.client: Client | None = None
 
@@ -223,8 +258,16 @@ class Cluster:
                 "--state-dir", self.state_dir(node.name),
                 "--socket", self.agent_socket(node.name), "--apiserver", self.url,
                 "--faults", self.faults_path(node.name), "--ready-file", rf,
-                "--sample-interval", str(self.sample_interval),
-                "--auth-token-file", self.agent_token_file] + ([] if self.fsync else ["--no-fsync"])
+                "--sample-interval", str(self.sample_interval)] + \
+            ([] if self.fsync else ["--no-fsync"])
+        if self.agent_auth in ("token", "both"):
+            argv += ["--auth-token-file", self.agent_token_file]
+        if self.pubkeys:
+            argv += ["--manager-pubkeys", self.pubkeys]
+        if self.discovery == "pod":
+            ip = self.agent_ips.setdefault(node.name, f"127.0.0.{10 + len(self.agent_ips)}")
+            argv += ["--listen", f"{ip}:{self.agent_port}",
+                     "--endpoint", f"http://{ip}:{self.agent_port}"]
         if node.backend == "fake":
             argv += ["--fixture", node.fixture]
         if node.count >= 0:
@@ -242,14 +285,43 @@ class Cluster:
             argv = shlex.split(wrap) + argv
         p = self._spawn(f"agent-{node.name}", argv)
         _wait_file(rf, 300, p, os.path.join(self.workdir, f"agent-{node.name}.log"))
+        if self.discovery == "pod":
+            self.publish_agent_pod(node.name)
+
+    AGENT_NS = "gpupool-system"
+
+    def publish_agent_pod(self, node: str, ip: str | None = None) -> None:
+        """The agent's Pod as the DaemonSet controller + kubelet would show it: bound to the node,
+        Running, with the pod IP the CNI gave it (a mirror pod: the fake kubelet does not run it)."""
+        from ..kube import PODS, KubeError
+        name = f"gpupool-agent-{node}"
+        pod = {"apiVersion": "v1", "kind": "Pod",
+               "metadata": {"name": name, "namespace": self.AGENT_NS,
+                            "labels": {"app.kubernetes.io/name": "gpupool-agent"},
+                            "annotations": {"kubernetes.io/config.mirror": "gpupool-testing"}},
+               "spec": {"nodeName": node, "containers": [{"name": "agent", "image": "gpupool"}]}}
+        try:
+            self.client.create(PODS, pod, self.AGENT_NS)
+        except KubeError as e:
+            if e.code != 409:
+                raise
+        self.client.patch(PODS, name, {"status": {"phase": "Running",
+                                                  "podIP": ip or self.agent_ips[node]}},
+                          self.AGENT_NS, sub="status")
 
     def start_manager(self) -> None:
         pf = os.path.join(self.workdir, "manager.port")
         if os.path.exists(pf):
             os.remove(pf)
         argv = [self.manager_bin or native_bin("gpupool-manager"), "--apiserver", self.url, "--port-file", pf,
-                "--kinds", self.kinds, "--progress-poll", "100ms",
-                "--agent-token-file", self.agent_token_file]
+                "--kinds", self.kinds, "--progress-poll", "100ms"]
+        if self.agent_auth in ("token", "both"):
+            argv += ["--agent-token-file", self.agent_token_file]
+        if self.signing_key:
+            argv += ["--agent-signing-key", self.signing_key]
+        if self.discovery == "pod":
+            argv += ["--agent-discovery", "pod", "--agent-scheme", "http",
+                     "--agent-port", str(self.agent_port), "--agent-namespace", self.AGENT_NS]
         if self.tls:
             argv += ["--ca-file", self.ca_file]
         if self.token:
@@ -301,8 +373,17 @@ class Cluster:
             self.agent_request(node, "POST", "/v1/sample", {})
 
     def agent_request(self, node: str, method: str, path: str, body: dict | None = None) -> dict:
-        c = Client("unix://" + self.agent_socket(node), self.agent_token)
-        return c.request(method, path, body)
+        """An admin call on the node's agent (its unix socket), with the manager's credentials:
+        the shared token if agents take one, else a signature for that node."""
+        if self.agent_auth in ("token", "both"):
+            c = Client("unix://" + self.agent_socket(node), self.agent_token)
+            return c.request(method, path, body)
+        from ..utils import edsig
+        c = Client("unix://" + self.agent_socket(node))
+        signer = edsig.Signer(self.signing_key)
+        data = b"" if body is None else json.dumps(body).encode()
+        hdr = signer.header(method, path, node, data)
+        return c.request(method, path, body, extra_headers={"X-Gpupool-Signature": hdr})
 
     def manager_metrics(self) -> str:
         import urllib.request

@@ -1,0 +1,335 @@
+"""Ed25519 request signatures for the manager -> node-agent RPC (OpenSSL libcrypto via ctypes).
+
+Why signatures and not a bearer token: a bearer token is a reusable credential. Sent to whatever
+endpoint a Node names, it can be harvested by a rogue listener and replayed against every other
+agent. Here the manager alone holds the private key; agents hold only public keys (non-secret,
+a ConfigMap). Each request carries a signature bound to
+
+    method, path + query, the target node's name, a timestamp, a nonce and the body's SHA-256
+
+so what a wrong host receives is good for nothing but that one request to that one node within
+the clock-skew window — and the agent keeps the nonces it has seen for that window. This is the
+least-privilege identity the reference asks of its operator (an SP scoped to what it manages,
+README.md:43-57; Workload Identity instead of shared secrets, README.md:59-60, 312).
+
+Header (no ``Authorization`` header is sent at all)::
+
+    X-Gpupool-Signature: v1 keyId=<16 hex> node=<node> ts=<unix ms> nonce=<32 hex>
+                         body=<sha256 hex> sig=<base64url, no padding>
+
+The C++ signer (native/src/runtime/agentauth.cc) produces the same bytes.
+"""
+from __future__ import annotations
+
+import base64
+import ctypes
+import ctypes.util
+import hashlib
+import os
+import threading
+import time
+
+HEADER = "x-gpupool-signature"
+PREFIX = b"gpupool-agent-rpc-v1"
+_NID_ED25519 = 1087
+# DER prefixes of an Ed25519 PKCS#8 private key (RFC 8410) and SubjectPublicKeyInfo
+_PRIV_DER = bytes.fromhex("302e020100300506032b657004220420")
+_PUB_DER = bytes.fromhex("302a300506032b6570032100")
+
+_lib = None
+_lib_mu = threading.Lock()
+
+
+def _crypto():
+    global _lib
+    with _lib_mu:
+        if _lib is None:
+            name = ctypes.util.find_library("crypto") or "libcrypto.so.3"
+            lib = ctypes.CDLL(name)
+            vp, cp, sz = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t
+            lib.EVP_PKEY_new_raw_public_key.restype = vp
+            lib.EVP_PKEY_new_raw_public_key.argtypes = [ctypes.c_int, vp, cp, sz]
+            lib.EVP_PKEY_new_raw_private_key.restype = vp
+            lib.EVP_PKEY_new_raw_private_key.argtypes = [ctypes.c_int, vp, cp, sz]
+            lib.EVP_PKEY_free.argtypes = [vp]
+            lib.EVP_MD_CTX_new.restype = vp
+            lib.EVP_MD_CTX_free.argtypes = [vp]
+            lib.EVP_DigestVerifyInit.argtypes = [vp, vp, vp, vp, vp]
+            lib.EVP_DigestVerify.argtypes = [vp, cp, sz, cp, sz]
+            lib.EVP_DigestSignInit.argtypes = [vp, vp, vp, vp, vp]
+            lib.EVP_DigestSign.argtypes = [vp, cp, ctypes.POINTER(sz), cp, sz]
+            _lib = lib
+        return _lib
+
+
+def _pem_body(pem: str, label: str) -> bytes:
+    begin, end = f"-----BEGIN {label}-----", f"-----END {label}-----"
+    i, j = pem.find(begin), pem.find(end)
+    if i < 0 or j < 0:
+        raise ValueError(f"no {label} PEM block")
+    return base64.b64decode("".join(pem[i + len(begin):j].split()))
+
+
+def load_private_key(pem: str) -> bytes:
+    """The 32-byte seed of an Ed25519 ``PRIVATE KEY`` PEM (``openssl genpkey -algorithm ed25519``)."""
+    der = _pem_body(pem, "PRIVATE KEY")
+    if not der.startswith(_PRIV_DER) or len(der) != len(_PRIV_DER) + 32:
+        raise ValueError("not an Ed25519 PKCS#8 private key")
+    return der[len(_PRIV_DER):]
+
+
+def load_public_keys(pem: str) -> list[bytes]:
+    """Every Ed25519 ``PUBLIC KEY`` block of a PEM bundle, as raw 32-byte keys."""
+    out, rest = [], pem
+    while "-----BEGIN PUBLIC KEY-----" in rest:
+        der = _pem_body(rest, "PUBLIC KEY")
+        if not der.startswith(_PUB_DER) or len(der) != len(_PUB_DER) + 32:
+            raise ValueError("not an Ed25519 public key")
+        out.append(der[len(_PUB_DER):])
+        rest = rest[rest.index("-----END PUBLIC KEY-----") + 24:]
+    return out
+
+
+def public_pem(raw: bytes) -> str:
+    b = base64.b64encode(_PUB_DER + raw).decode()
+    return "-----BEGIN PUBLIC KEY-----\n" + b + "\n-----END PUBLIC KEY-----\n"
+
+
+def key_id(pub: bytes) -> str:
+    return hashlib.sha256(pub).hexdigest()[:16]
+
+
+def public_from_private(seed: bytes) -> bytes:
+    lib = _crypto()
+    k = lib.EVP_PKEY_new_raw_private_key(_NID_ED25519, None, seed, len(seed))
+    if not k:
+        raise ValueError("bad Ed25519 private key")
+    try:
+        lib.EVP_PKEY_get_raw_public_key.argtypes = [ctypes.c_void_p, ctypes.c_char_p,
+                                                    ctypes.POINTER(ctypes.c_size_t)]
+        buf = ctypes.create_string_buffer(32)
+        n = ctypes.c_size_t(32)
+        if lib.EVP_PKEY_get_raw_public_key(k, buf, ctypes.byref(n)) != 1:
+            raise ValueError("EVP_PKEY_get_raw_public_key failed")
+        return buf.raw[:n.value]
+    finally:
+        lib.EVP_PKEY_free(k)
+
+
+def sign_raw(seed: bytes, msg: bytes) -> bytes:
+    lib = _crypto()
+    k = lib.EVP_PKEY_new_raw_private_key(_NID_ED25519, None, seed, len(seed))
+    ctx = lib.EVP_MD_CTX_new()
+    try:
+        if not k or lib.EVP_DigestSignInit(ctx, None, None, None, k) != 1:
+            raise ValueError("EVP_DigestSignInit failed")
+        sig = ctypes.create_string_buffer(64)
+        n = ctypes.c_size_t(64)
+        if lib.EVP_DigestSign(ctx, sig, ctypes.byref(n), msg, len(msg)) != 1:
+            raise ValueError("EVP_DigestSign failed")
+        return sig.raw[:n.value]
+    finally:
+        lib.EVP_MD_CTX_free(ctx)
+        if k:
+            lib.EVP_PKEY_free(k)
+
+
+class PublicKey:
+    """A parsed Ed25519 public key (the EVP_PKEY is built once, not per verification)."""
+
+    def __init__(self, raw: bytes):
+        self.raw = raw
+        self._lib = _crypto()
+        self._k = self._lib.EVP_PKEY_new_raw_public_key(_NID_ED25519, None, raw, len(raw))
+        if not self._k:
+            raise ValueError("bad Ed25519 public key")
+
+    def verify(self, msg: bytes, sig: bytes) -> bool:
+        lib = self._lib
+        ctx = lib.EVP_MD_CTX_new()
+        try:
+            if lib.EVP_DigestVerifyInit(ctx, None, None, None, self._k) != 1:
+                return False
+            return lib.EVP_DigestVerify(ctx, sig, len(sig), msg, len(msg)) == 1
+        finally:
+            lib.EVP_MD_CTX_free(ctx)
+
+    def __del__(self):
+        if getattr(self, "_k", None):
+            self._lib.EVP_PKEY_free(self._k)
+            self._k = None
+
+
+def verify_raw(pub: bytes, msg: bytes, sig: bytes) -> bool:
+    try:
+        return PublicKey(pub).verify(msg, sig)
+    except ValueError:
+        return False
+
+
+def canonical(method: str, target: str, node: str, ts_ms: int, nonce: str, body_sha: str) -> bytes:
+    return b"\n".join([PREFIX, method.upper().encode(), target.encode(), node.encode(),
+                       str(ts_ms).encode(), nonce.encode(), body_sha.encode()])
+
+
+def _b64u(b: bytes) -> str:
+    return base64.urlsafe_b64encode(b).decode().rstrip("=")
+
+
+def _unb64u(s: str) -> bytes:
+    return base64.urlsafe_b64decode(s + "=" * (-len(s) % 4))
+
+
+def sign_header(seed: bytes, method: str, target: str, node: str, body: bytes = b"",
+                ts_ms: int | None = None, nonce: str | None = None,
+                pub: bytes | None = None) -> str:
+    """The ``X-Gpupool-Signature`` value for one request to ``node``."""
+    ts_ms = int(time.time() * 1000) if ts_ms is None else ts_ms
+    nonce = nonce or os.urandom(16).hex()
+    sha = hashlib.sha256(body).hexdigest()
+    sig = sign_raw(seed, canonical(method, target, node, ts_ms, nonce, sha))
+    kid = key_id(pub or public_from_private(seed))
+    return f"v1 keyId={kid} node={node} ts={ts_ms} nonce={nonce} body={sha} sig={_b64u(sig)}"
+
+
+def parse_header(value: str) -> dict[str, str] | None:
+    parts = value.split()
+    if not parts or parts[0] != "v1":
+        return None
+    out = {}
+    for p in parts[1:]:
+        k, sep, v = p.partition("=")
+        if not sep:
+            return None
+        out[k] = v
+    return out if {"keyId", "node", "ts", "nonce", "body", "sig"} <= set(out) else None
+
+
+class Signer:
+    """A private key file, re-read when it changes (key rotation on the manager side)."""
+
+    def __init__(self, path: str, reload_s: float = 5.0):
+        self.path = path
+        self.reload_s = reload_s
+        self._mu = threading.Lock()
+        self._checked = -1e9
+        self._mtime = None
+        self.seed = b""
+        self.pub = b""
+        self._load(force=True)
+
+    def _load(self, force: bool = False) -> None:
+        now = time.monotonic()
+        if not force and now - self._checked < self.reload_s:
+            return
+        self._checked = now
+        try:
+            st = os.stat(self.path)
+        except OSError:
+            return
+        if not force and st.st_mtime_ns == self._mtime:
+            return
+        with open(self.path) as f:
+            seed = load_private_key(f.read())
+        self.seed, self.pub, self._mtime = seed, public_from_private(seed), st.st_mtime_ns
+
+    def header(self, method: str, target: str, node: str, body: bytes = b"") -> str:
+        with self._mu:
+            self._load()
+            seed, pub = self.seed, self.pub
+        return sign_header(seed, method, target, node, body, pub=pub)
+
+
+class Verifier:
+    """The agent side: trusted public keys (a PEM bundle file, or a directory of them — the
+    mounted ConfigMap — re-read when it changes: during a rotation it lists the old and the new
+    key), this node's name, the clock-skew window and the nonces seen inside it."""
+
+    def __init__(self, path: str, node: str, skew_s: float = 60.0, reload_s: float = 1.0):
+        self.path = path
+        self.node = node
+        self.skew_ms = int(skew_s * 1000)
+        self.reload_s = reload_s
+        self.keys: dict[str, PublicKey] = {}
+        self._sig = None
+        self._checked = -1e9
+        self._mu = threading.Lock()
+        self._nonces: dict[str, int] = {}
+        self.rejected: dict[str, int] = {}
+        self._load(force=True)
+
+    def _files(self) -> list[str]:
+        if os.path.isdir(self.path):
+            return sorted(os.path.join(self.path, f) for f in os.listdir(self.path)
+                          if not f.startswith("."))
+        return [self.path]
+
+    def _load(self, force: bool = False) -> None:
+        now = time.monotonic()
+        if not force and now - self._checked < self.reload_s:
+            return
+        self._checked = now
+        try:
+            files = [f for f in self._files() if os.path.isfile(f)]
+            sig = tuple((f, os.stat(f).st_mtime_ns) for f in files)
+        except OSError:
+            return
+        if sig == self._sig and not force:
+            return
+        keys = {}
+        for f in files:
+            try:
+                with open(f) as fh:
+                    for k in load_public_keys(fh.read()):
+                        keys[key_id(k)] = PublicKey(k)
+            except (OSError, ValueError):
+                continue
+        if keys or force:
+            self.keys, self._sig = keys, sig
+
+    def _reject(self, why: str) -> str:
+        self.rejected[why] = self.rejected.get(why, 0) + 1
+        return why
+
+    def check_head(self, method: str, target: str, headers: dict) -> str | None:
+        """Before the body: None when the signature is valid for this node (the body digest it
+        names is checked by ``check_body``), else why not."""
+        raw = headers.get(HEADER)
+        if not raw:
+            return self._reject("NoSignature")
+        h = parse_header(raw)
+        if h is None:
+            return self._reject("BadSignatureHeader")
+        if h["node"] != self.node:
+            return self._reject("WrongNode")
+        try:
+            ts = int(h["ts"])
+        except ValueError:
+            return self._reject("BadSignatureHeader")
+        now = int(time.time() * 1000)
+        if abs(now - ts) > self.skew_ms:
+            return self._reject("StaleSignature")
+        with self._mu:
+            self._load()
+            pub = self.keys.get(h["keyId"])
+        if pub is None:
+            return self._reject("UnknownKey")
+        try:
+            sig = _unb64u(h["sig"])
+        except ValueError:
+            return self._reject("BadSignatureHeader")
+        if not pub.verify(canonical(method, target, self.node, ts, h["nonce"], h["body"]), sig):
+            return self._reject("BadSignature")
+        with self._mu:
+            if h["nonce"] in self._nonces:
+                return self._reject("Replay")
+            self._nonces[h["nonce"]] = ts + self.skew_ms
+            if len(self._nonces) > 4096:
+                self._nonces = {n: e for n, e in self._nonces.items() if e > now}
+        return None
+
+    def check_body(self, headers: dict, body: bytes) -> str | None:
+        h = parse_header(headers.get(HEADER, "")) or {}
+        if h.get("body") != hashlib.sha256(body).hexdigest():
+            return self._reject("BodyMismatch")
+        return None

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <stdexcept>
 #include <functional>
@@ -62,10 +63,41 @@ class ChunkedDecoder {
   bool trailer_line_empty_ = true;
 };
 
+// A bearer credential that may rotate (projected ServiceAccount tokens, Workload Identity): a
+// fixed string, or a file re-read at most every ``reload_after`` and at once after a 401 —
+// client-go's behaviour. Thread-safe; shared by every client (and watch stream) that uses it.
+class TokenSource {
+ public:
+  static std::shared_ptr<TokenSource> fixed(std::string token);
+  static std::shared_ptr<TokenSource> file(std::string path,
+                                           std::chrono::milliseconds reload_after = std::chrono::seconds(60));
+  std::string token();  // current value (re-read from the file when due)
+  bool reload();        // re-read now; true when the token changed
+  uint64_t reloads() const { return reloads_.load(); }
+  const std::string& path() const { return path_; }
+
+ private:
+  TokenSource() = default;
+  void read_locked_();
+  std::mutex mu_;
+  std::string path_, token_;
+  std::chrono::milliseconds reload_after_{60000};
+  std::chrono::steady_clock::time_point read_at_{};
+  std::atomic<uint64_t> reloads_{0};
+};
+
+// Extra header lines for one request, computed from it (the manager's per-request signature to
+// a node agent): (method, target incl. query, body) -> "Name: value\r\n"...
+using RequestSigner = std::function<std::string(const std::string& method, const std::string& target,
+                                                const std::string& body)>;
+
 class HttpClient {
  public:
   explicit HttpClient(Url url, std::string bearer_token = "", int timeout_ms = 30000,
                       TlsOptions tls = {});
+  // bearer from a rotating source (nullptr: none); a 401 re-reads it and retries once
+  HttpClient(Url url, std::shared_ptr<TokenSource> tokens, int timeout_ms = 30000, TlsOptions tls = {});
+  void set_signer(RequestSigner s) { signer_ = std::move(s); }
   ~HttpClient();
   HttpClient(const HttpClient&) = delete;
   HttpClient& operator=(const HttpClient&) = delete;
@@ -93,10 +125,23 @@ class HttpClient {
   void give_(std::unique_ptr<Conn> c);
   bool send_request_(Conn& c, const std::string& method, const std::string& path,
                      const std::string& body, const std::string& content_type,
-                     const std::string& accept, const std::string& extra_headers = "");
+                     const std::string& accept, const std::string& extra_headers = "",
+                     const std::string* bearer = nullptr);
 
+  // ``bearer``: the token to send (the one a 401 is judged against); nullptr = the current one
+  HttpResponse request_once_(const std::string& method, const std::string& path, const std::string& body,
+                             const std::string& content_type, const std::string& accept, int timeout_ms,
+                             const std::string& extra_headers, const std::string* bearer);
+  int stream_lines_once_(const std::string& path, const std::function<bool(std::string_view)>& on_line,
+                         const std::atomic<bool>* stop, std::string* err_body, int poll_ms,
+                         const std::string* bearer);
+  std::string auth_headers_(const std::string& method, const std::string& path, const std::string& body,
+                            const std::string* bearer);
+  bool reload_after_401_(const std::string& used);
   Url url_;
   std::string token_;
+  std::shared_ptr<TokenSource> tokens_;
+  RequestSigner signer_;
   int timeout_ms_;
   TlsOptions tls_;
   std::shared_ptr<void> ssl_ctx_;  // SSL_CTX*, shared by all connections of this client

@@ -22,13 +22,25 @@
 
 namespace gpupool {
 
+struct InformerOptions {
+  // server-side filters of both the LIST and the WATCH (an object leaving the selection arrives
+  // as DELETED, as from a real apiserver)
+  std::string label_selector, field_selector;
+  // applied to every object before it is cached and handed to handlers: keep only what the
+  // readers use (a cluster's pods cached whole cost the manager most of its memory)
+  std::function<Json(const Json&)> transform;
+  // objects it rejects are not cached at all (a watch event for one that was cached becomes
+  // DELETED): an informer over a whole cluster's pods keeps only the ones its readers count
+  std::function<bool(const Json&)> filter;
+};
+
 class Informer {
  public:
   // type is ADDED | MODIFIED | DELETED | RESYNC
   using Handler = std::function<void(const std::string& type, const Json& obj)>;
 
   Informer(KubeClient& client, ResourceRef res, std::string ns,
-           std::chrono::milliseconds resync);
+           std::chrono::milliseconds resync, InformerOptions opts = {});
   ~Informer();
 
   void add_handler(Handler h);
@@ -41,6 +53,7 @@ class Informer {
   std::vector<Json> list() const;
   size_t size() const;
   uint64_t relists() const { return relists_.load(); }
+  uint64_t events() const { return events_.load(); }  // watch events received
 
   static std::string key_of(const Json& obj);  // "ns/name" or "name"
 
@@ -53,7 +66,9 @@ class Informer {
   ResourceRef res_;
   std::string ns_;
   std::chrono::milliseconds resync_;
+  InformerOptions opts_;
   Logger log_;
+  std::atomic<uint64_t> events_{0};
 
   mutable std::mutex mu_;
   std::map<std::string, Json> cache_;

@@ -49,7 +49,7 @@ class KubeError : public std::runtime_error {
 
 // A resolved kubeconfig context (clientcmd semantics, the subset a controller needs).
 struct KubeConfig {
-  std::string server, token, ns, context;
+  std::string server, token, token_file, ns, context;
   TlsOptions tls;
 };
 // Loads ``path`` ("" = first entry of $KUBECONFIG, else ~/.kube/config) and resolves ``context``
@@ -63,6 +63,9 @@ KubeConfig load_kubeconfig(const std::string& path = "", const std::string& cont
 class KubeClient {
  public:
   KubeClient(const std::string& server, const std::string& token = "", int timeout_ms = 15000,
+             TlsOptions tls = {});
+  // a rotating bearer (projected ServiceAccount token file): re-read every minute and after a 401
+  KubeClient(const std::string& server, std::shared_ptr<TokenSource> tokens, int timeout_ms = 15000,
              TlsOptions tls = {});
   // In-cluster configuration (ServiceAccount): https://$KUBERNETES_SERVICE_HOST:PORT, token and
   // CA from /var/run/secrets/kubernetes.io/serviceaccount. Returns false if not in a pod.
@@ -85,15 +88,17 @@ class KubeClient {
   // (410 when ``rv`` was compacted, also for in-stream ERROR events). Returns the last RV seen.
   std::string watch(const ResourceRef& r, const std::string& ns, const std::string& rv,
                     const std::function<bool(const std::string&, const Json&)>& cb,
-                    const std::atomic<bool>* stop, int timeout_seconds = 300);
+                    const std::atomic<bool>* stop, int timeout_seconds = 300,
+                    const std::string& label_selector = "", const std::string& field_selector = "");
 
   const std::string& server() const { return server_; }
+  const std::shared_ptr<TokenSource>& tokens() const { return tokens_; }
 
  private:
   Json call_(const std::string& method, const std::string& path, const std::string& body,
              const std::string& ctype = "application/json");
   std::string server_;
-  std::string token_;
+  std::shared_ptr<TokenSource> tokens_;  // nullptr: no bearer
   TlsOptions tls_;
   std::unique_ptr<HttpClient> http_;
 };

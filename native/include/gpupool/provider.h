@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "gpupool/api.h"
+#include "gpupool/agentauth.h"
 #include "gpupool/http.h"
 #include "gpupool/json.h"
 
@@ -175,14 +176,35 @@ class DeviceProvider {
                              const std::string& resource_name) = 0;
 };
 
-// Agents are discovered from Node objects annotated gpupool.amd.com/agent-endpoint.
+// How the manager finds and authenticates each node's agent.
+struct AgentAccess {
+  // "pod": the endpoint is <scheme>://<podIP>:<port> of the agent Pod the scheduler bound to the
+  //        node (pods informer, namespace + label selector) — addresses the kubelet/CNI assign,
+  //        which no agent can point at another node. A Node annotation is used only if its host
+  //        is that Pod's IP (e.g. to name a different port or scheme), else ignored and counted.
+  // "annotation": the Node's gpupool.amd.com/agent-endpoint as written (local / dev setups,
+  //        unix sockets).
+  std::string discovery = "annotation";
+  Informer* pods = nullptr;  // required for "pod"
+  std::string scheme = "https";
+  int port = 9443;
+  // credentials: per-request Ed25519 signatures bound to the node (preferred; no bearer is sent
+  // then) and/or a shared bearer token from a rotating source
+  std::shared_ptr<AgentSigner> signer;
+  std::shared_ptr<TokenSource> token;
+  TlsOptions tls;  // how https:// agent endpoints are verified
+};
+
+// Agents are found per node (AgentAccess::discovery) and called over HTTP/1.1 JSON.
 class RocmProvider : public DeviceProvider {
  public:
-  RocmProvider(Informer& nodes, int timeout_ms = 30000, std::string agent_token = "", TlsOptions agent_tls = {});
-  // shared secret presented to the node agents (Authorization: Bearer)
-  const std::string& agent_token() const { return agent_token_; }
+  RocmProvider(Informer& nodes, int timeout_ms = 30000, AgentAccess access = {});
   // how https:// agent endpoints are verified (CA of the agents' serving certificates)
-  const TlsOptions& agent_tls() const { return agent_tls_; }
+  const TlsOptions& agent_tls() const { return access_.tls; }
+  // A client for ``node``'s agent at ``endpoint`` carrying this manager's credentials for that
+  // node (the event feed's long-polls; client_for caches one per node for RPCs).
+  std::unique_ptr<HttpClient> new_client(const std::string& node, const std::string& endpoint, int timeout_ms);
+  uint64_t endpoints_rejected() const { return endpoints_rejected_.load(); }
   std::vector<std::string> node_names() override;
   Json node_labels(const std::string& node) override;
   bool node_schedulable(const std::string& node) override;
@@ -228,8 +250,8 @@ class RocmProvider : public DeviceProvider {
   void invalidate_(const std::string& node);
   Informer& nodes_;
   int timeout_ms_;
-  std::string agent_token_;
-  TlsOptions agent_tls_;
+  AgentAccess access_;
+  std::atomic<uint64_t> endpoints_rejected_{0};
   std::mutex mu_;
   std::map<std::string, std::pair<std::string, std::shared_ptr<HttpClient>>> clients_;
   struct CachedView {
@@ -261,11 +283,16 @@ class RocmProvider : public DeviceProvider {
   struct NodeFacts {
     Json labels = Json::object();
     bool schedulable = true;
-    std::string endpoint;
+    std::string annotation;  // gpupool.amd.com/agent-endpoint as the Node carries it
+    std::string endpoint;    // what the manager calls (derived per AgentAccess::discovery)
   };
   std::mutex facts_mu_;
   std::map<std::string, NodeFacts> facts_;
+  // pod discovery: node -> (agent pod "ns/name" -> pod IP) of Running, undeleted agent pods
+  std::map<std::string, std::map<std::string, std::string>> agent_pods_;
   void note_node_(const std::string& type, const Json& obj);
+  void note_agent_pod_(const std::string& type, const Json& pod);
+  void derive_endpoint_(const std::string& node, NodeFacts& f);  // caller holds facts_mu_
 };
 
 }  // namespace gpupool

@@ -20,6 +20,7 @@
 #include "gpupool/api.h"
 #include "gpupool/events.h"
 #include "gpupool/informer.h"
+#include "gpupool/podindex.h"
 #include "gpupool/kube.h"
 #include "gpupool/log.h"
 #include "gpupool/metrics.h"
@@ -66,6 +67,8 @@ class PoolReconcilerBase {
  protected:
   // Writes ``status`` (unless semantically unchanged) with a fresh-GET retry on 409.
   void write_status_(const Json& obj, const Json& status);
+  // called with the object a successful status write returned (read-your-writes caches)
+  virtual void on_status_written_(const Json& /*written*/) {}
   // Throws a 409 when the pass read a stale copy whose status placement (nodeName/nodes) differs
   // from the stored one, unless ``writing`` (an object carrying the status being written) already
   // agrees with the stored placement.
@@ -214,8 +217,11 @@ class AzureVmPoolReconciler : public PoolReconcilerBase {
 // decision runs under one mutex against fresh LISTs, so two gangs never share a GPU.
 class Mi355xJobReconciler : public PoolReconcilerBase {
  public:
+  // ``pods``: the manager's pod index (podindex.h). With it, placement reads jobs, nodes and pod
+  // usage from the informers' caches — no cluster-wide LIST per pass; without it (unit tests), the
+  // apiserver is LISTed as before.
   Mi355xJobReconciler(KubeClient& client, Informer& jobs, Informer& nodes, EventRecorder* events,
-                      ReconcilerOptions opts = {});
+                      ReconcilerOptions opts = {}, PodIndex* pods = nullptr);
   Outcome reconcile(const std::string& ns, const std::string& name) override;
   // Jobs still waiting for a gang placement (re-enqueued when capacity may have freed up).
   std::vector<std::pair<std::string, std::string>> pending() const;
@@ -234,7 +240,7 @@ class Mi355xJobReconciler : public PoolReconcilerBase {
                   const std::string& reason, const std::string& msg, const std::vector<Json>& pods);
   Outcome cleanup_finished_(const Json& obj, const ObjectMeta& m, const Mi355xJobSpec& spec,
                             const std::vector<Json>& pods);
-  std::vector<Json> list_pods_(const ObjectMeta& m);
+  std::vector<Json> list_pods_(const ObjectMeta& m, const Json& placement);
   // Tries to place the gang (under sched_mu_). Returns the placement, or empty with *why set. With
   // preemptionPolicy PreemptLowerPriority a placement may rely on GPUs of lower-priority running
   // jobs, returned in *victims (the smallest set found, lowest priority and newest first).
@@ -251,9 +257,20 @@ class Mi355xJobReconciler : public PoolReconcilerBase {
                   int attempt, int world, const Slot& slot, const std::string& master_addr);
   bool resolve_pool_(const ObjectMeta& m, const Mi355xJobSpec& spec, std::string* resource, std::string* node,
                      std::string* why, std::map<std::string, int64_t>* pool_cap = nullptr);
+  // Every job as this reconciler last knows it: the jobs informer's cache, except where our own
+  // status write (a gang reservation, written under sched_mu_) is newer than what the watch has
+  // delivered yet — read-your-writes, so the next placement never double-books GPUs.
+  std::vector<Json> jobs_view_();
+  std::vector<Json> node_objects_();
+  // node -> GPUs of ``resource`` requested by live pods (the pod index, or one LIST without it)
+  std::map<std::string, int64_t> pod_usage_(const std::string& resource);
+  void on_status_written_(const Json& written) override;
 
   Informer& nodes_;
+  PodIndex* pods_idx_;
   std::mutex sched_mu_;
+  std::mutex written_mu_;
+  std::map<std::string, Json> written_;  // job uid -> the object our last status write returned
 };
 
 // Mi355xQueue status (Volcano queue status): job counts per phase and the GPUs its placed jobs

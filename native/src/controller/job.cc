@@ -68,11 +68,85 @@ bool node_schedulable(const Json& node) {
 }  // namespace
 
 Mi355xJobReconciler::Mi355xJobReconciler(KubeClient& client, Informer& jobs, Informer& nodes, EventRecorder* events,
-                                         ReconcilerOptions opts)
+                                         ReconcilerOptions opts, PodIndex* pods)
     : PoolReconcilerBase(client, jobs, events, opts, "Mi355xJob",
                          ResourceRef{gen::kGroup, gen::kVersion, gen::kPluralMi355xJob, true, "Mi355xJob"}),
-      nodes_(nodes) {
+      nodes_(nodes), pods_idx_(pods) {
   finalizer_ = gen::kJobFinalizer;
+}
+
+namespace {
+// resourceVersions are opaque to clients, but every apiserver backend in use (etcd, the sim)
+// issues increasing integers: compare them as such, and treat anything else as "not newer"
+bool rv_newer(const std::string& a, const std::string& b) {
+  char* ea = nullptr;
+  char* eb = nullptr;
+  const long long x = std::strtoll(a.c_str(), &ea, 10), y = std::strtoll(b.c_str(), &eb, 10);
+  return !a.empty() && !b.empty() && *ea == 0 && *eb == 0 && x > y;
+}
+
+CounterVec& sched_reads() {
+  static CounterVec& c = Registry::global().counter(
+      "gpupool_job_scheduler_reads_total", "Object reads of the gang scheduler by source (cache or apiserver LIST).");
+  return c;
+}
+}  // namespace
+
+void Mi355xJobReconciler::on_status_written_(const Json& written) {
+  if (!pods_idx_) return;
+  std::lock_guard<std::mutex> g(written_mu_);
+  written_[written.path("metadata.uid").as_string()] = written;
+}
+
+std::vector<Json> Mi355xJobReconciler::jobs_view_() {
+  if (!pods_idx_) {
+    sched_reads().inc({{"what", "jobs"}, {"source", "list"}});
+    Json lst = client_.list(res_, "");
+    return std::vector<Json>(lst["items"].elements().begin(), lst["items"].elements().end());
+  }
+  sched_reads().inc({{"what", "jobs"}, {"source", "cache"}});
+  std::vector<Json> out = pools_.list();
+  std::lock_guard<std::mutex> g(written_mu_);
+  std::set<std::string> seen;
+  for (auto& j : out) {
+    const std::string uid = j.path("metadata.uid").as_string();
+    seen.insert(uid);
+    auto w = written_.find(uid);
+    if (w == written_.end()) continue;
+    if (rv_newer(w->second.path("metadata.resourceVersion").as_string(), j.path("metadata.resourceVersion").as_string()))
+      j = w->second;  // the watch has not delivered our write yet
+    else
+      written_.erase(w);  // the cache caught up (or moved past it)
+  }
+  for (auto it = written_.begin(); it != written_.end();)  // deleted jobs
+    it = seen.count(it->first) ? std::next(it) : written_.erase(it);
+  return out;
+}
+
+std::vector<Json> Mi355xJobReconciler::node_objects_() {
+  if (!pods_idx_) {
+    sched_reads().inc({{"what", "nodes"}, {"source", "list"}});
+    Json lst = client_.list(res::nodes());
+    return std::vector<Json>(lst["items"].elements().begin(), lst["items"].elements().end());
+  }
+  sched_reads().inc({{"what", "nodes"}, {"source", "cache"}});
+  return nodes_.list();
+}
+
+std::map<std::string, int64_t> Mi355xJobReconciler::pod_usage_(const std::string& resource) {
+  if (pods_idx_) {
+    sched_reads().inc({{"what", "pods"}, {"source", "cache"}});
+    return pods_idx_->requested_by_node(resource);
+  }
+  sched_reads().inc({{"what", "pods"}, {"source", "list"}});
+  std::map<std::string, int64_t> used;
+  Json pods = client_.list(res::pods(), "");
+  for (const auto& p : pods["items"].elements()) {
+    const std::string node = p.path("spec.nodeName").as_string();
+    if (node.empty() || terminal(pod_phase(p))) continue;
+    used[node] += pod_request(p, resource);
+  }
+  return used;
 }
 
 std::vector<std::pair<std::string, std::string>> Mi355xJobReconciler::pending() const {
@@ -116,10 +190,26 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::place(
   return {};
 }
 
-std::vector<Json> Mi355xJobReconciler::list_pods_(const ObjectMeta& m) {
+std::vector<Json> Mi355xJobReconciler::list_pods_(const ObjectMeta& m, const Json& placement) {
   std::vector<Json> out;
-  Json lst = client_.list(res::pods(), m.ns, std::string(gen::kLabelJob) + "=" + m.name);
-  for (const auto& p : lst["items"].elements()) {
+  std::vector<Json> items;
+  bool use_list = !pods_idx_;
+  if (pods_idx_) {
+    items = pods_idx_->job_pods(m.ns, m.name);
+    // a pod the job's (fresh) status says was created but the cache does not show yet (or any
+    // more): ask the apiserver before concluding it is lost — a stale cache must never restart
+    // a gang
+    std::set<int> cached;
+    for (const auto& p : items) cached.insert(label_int(p, gen::kLabelJobIndex, -1));
+    for (const auto& sl : placement.elements())
+      use_list = use_list || (sl["created"].as_bool(false) && !cached.count(static_cast<int>(sl["index"].as_int(-1))));
+  }
+  sched_reads().inc({{"what", "job-pods"}, {"source", use_list ? "list" : "cache"}});
+  if (use_list) {
+    Json lst = client_.list(res::pods(), m.ns, std::string(gen::kLabelJob) + "=" + m.name);
+    items.assign(lst["items"].elements().begin(), lst["items"].elements().end());
+  }
+  for (const auto& p : items) {
     bool owned = false;
     for (const auto& o : p.path("metadata.ownerReferences").elements())
       owned = owned || o["uid"].as_string() == m.uid;
@@ -173,16 +263,16 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
   trace::Span span("schedule");
   // 1. queue order: jobs of the same queue that still wait for a placement and sort ahead of us
   //    (priority desc, creation asc) block us, unless they could never fit the whole cluster.
-  Json jobs = client_.list(res_, "");
-  Json nodes = client_.list(res::nodes());
+  const std::vector<Json> jobs = jobs_view_();
+  const std::vector<Json> nodes = node_objects_();
   int64_t cluster_total = 0;
-  for (const auto& n : nodes["items"].elements()) cluster_total += qty(n.path("status.allocatable")[resource]);
+  for (const auto& n : nodes) cluster_total += qty(n.path("status.allocatable")[resource]);
   auto key_of = [](const Json& j) {
     return std::make_tuple(-j.path("spec.priority").as_int(0), j.path("metadata.creationTimestamp").as_string(),
                            j.path("metadata.namespace").as_string() + "/" + j.path("metadata.name").as_string());
   };
   Json self;
-  for (const auto& j : jobs["items"].elements())
+  for (const auto& j : jobs)
     if (j.path("metadata.uid").as_string() == m.uid) self = j;
   if (self.is_null()) return {};
   auto my_key = key_of(self);
@@ -218,7 +308,7 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
   }
   if (cap >= 0) {
     int64_t used = 0;
-    for (const auto& j : jobs["items"].elements()) {
+    for (const auto& j : jobs) {
       if (j.path("metadata.uid").as_string() == m.uid || terminal(j.path("status.phase").as_string())) continue;
       if (job_queue(j) == spec.queue && job_resource(j, resource) == resource) used += job_held(j);
     }
@@ -231,7 +321,7 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     if (spec.gpus_per_replica > 0)
       max_r = static_cast<int>(std::min<int64_t>(max_r, (cap - used) / spec.gpus_per_replica));
   }
-  for (const auto& j : jobs["items"].elements()) {
+  for (const auto& j : jobs) {
     if (j.path("metadata.uid").as_string() == m.uid || !j.path("metadata.deletionTimestamp").as_string().empty()) continue;
     if (j.path("spec.queue").str_or("default") != spec.queue) continue;
     const std::string phase = j.path("status.phase").str_or("Pending");
@@ -252,7 +342,7 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
   // 2. free GPUs per candidate node = allocatable - live pod requests - other jobs' reservations
   std::map<std::string, int64_t> free;
   std::vector<std::string> order;
-  for (const auto& n : nodes["items"].elements()) {
+  for (const auto& n : nodes) {
     const std::string name = n.path("metadata.name").as_string();
     if (!node_schedulable(n) || !selector_matches(spec.node_selector, n)) continue;
     if (!pool_node.empty() && ("," + pool_node + ",").find("," + name + ",") == std::string::npos) continue;
@@ -264,13 +354,9 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     order.push_back(name);
   }
   if (spec.gpus_per_replica > 0) {
-    Json pods = client_.list(res::pods(), "");
-    for (const auto& p : pods["items"].elements()) {
-      const std::string node = p.path("spec.nodeName").as_string();
-      if (node.empty() || !free.count(node) || terminal(pod_phase(p))) continue;
-      free[node] -= pod_request(p, resource);
-    }
-    for (const auto& j : jobs["items"].elements()) {
+    for (const auto& kv : pod_usage_(resource))
+      if (free.count(kv.first)) free[kv.first] -= kv.second;
+    for (const auto& j : jobs) {
       if (j.path("metadata.uid").as_string() == m.uid || terminal(j.path("status.phase").as_string())) continue;
       if (job_resource(j, resource) != resource) continue;
       int64_t g = j.path("spec.gpusPerReplica").as_int(1);
@@ -298,7 +384,7 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
       std::map<std::string, int64_t> held;
     };
     std::vector<Cand> pool;
-    for (const auto& j : jobs["items"].elements()) {
+    for (const auto& j : jobs) {
       if (j.path("metadata.uid").as_string() == m.uid || !j.path("metadata.deletionTimestamp").as_string().empty())
         continue;
       const std::string ph = j.path("status.phase").str_or("Pending");
@@ -361,15 +447,12 @@ bool Mi355xJobReconciler::capacity_free_(const Mi355xJobSpec& spec, const std::s
     if (!sl["created"].as_bool(false)) need[sl["node"].as_string()] += spec.gpus_per_replica;
   if (need.empty() || spec.gpus_per_replica <= 0) return true;
   std::map<std::string, int64_t> free;
-  const Json nodes = client_.list(res::nodes()), pods = client_.list(res::pods(), "");
-  for (const auto& n : nodes["items"].elements()) {
+  for (const auto& n : node_objects_()) {
     const std::string name = n.path("metadata.name").as_string();
     if (need.count(name)) free[name] = qty(n.path("status.allocatable")[resource]);
   }
-  for (const auto& p : pods["items"].elements()) {
-    const std::string node = p.path("spec.nodeName").as_string();
-    if (free.count(node) && !terminal(pod_phase(p))) free[node] -= pod_request(p, resource);
-  }
+  for (const auto& kv : pod_usage_(resource))
+    if (free.count(kv.first)) free[kv.first] -= kv.second;
   for (const auto& kv : need)
     if (free[kv.first] < kv.second) return false;
   return true;
@@ -523,7 +606,7 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
     return Outcome::terminal("invalid spec: " + msg);
   }
   Mi355xJobSpec spec = Mi355xJobSpec::from(obj["spec"]);
-  std::vector<Json> pods = list_pods_(m);
+  std::vector<Json> pods = list_pods_(m, obj.path("status.placement"));
 
   if (m.deleting()) {  // finalizer: no pod of a deleted job keeps a GPU
     int left = 0;
@@ -677,7 +760,10 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
       set_condition(conds, gen::kCondScheduled, "False", reason, why, m.generation, now);
       st["conditions"] = conds;
       write_status_(obj, st);
-      return Outcome::requeue(opts_.resync, reason);
+      // re-tried when capacity can have changed (a pod or job ended, a node's allocatable or
+      // schedulability moved, a queue or pool changed: the handlers' wake_pending); the timer is
+      // only a safety net — with the caches, a retry costs no apiserver LIST either way
+      return Outcome::requeue(pods_idx_ ? opts_.resync * 6 : opts_.resync, reason);
     }
     // gang wait: from creation, or from the moment the restart began
     const std::string since_s = attempt > 0 ? find_condition(conds, gen::kCondRestarting)["lastTransitionTime"].as_string()

@@ -128,9 +128,12 @@ void PoolReconcilerBase::write_status_(const Json& obj, const Json& status) {
       std::vector<std::string> place{status["nodeName"].as_string()};
       for (const auto& n : status["nodes"].elements()) place.push_back(n.as_string());
       const std::string uid = out.path("metadata.uid").as_string();
-      std::lock_guard<std::mutex> g(mu_);
-      own_rv_[uid] = out.path("metadata.resourceVersion").as_string();
-      own_place_[uid] = std::move(place);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        own_rv_[uid] = out.path("metadata.resourceVersion").as_string();
+        own_place_[uid] = std::move(place);
+      }
+      on_status_written_(out);
       return;
     } catch (const KubeError& e) {
       if (!e.conflict()) throw;

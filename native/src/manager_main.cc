@@ -34,6 +34,7 @@
 #include "gpupool/leader.h"
 #include "gpupool/log.h"
 #include "gpupool/metrics.h"
+#include "gpupool/podindex.h"
 #include "gpupool/provider.h"
 #include "gpupool/reconciler.h"
 #include "gpupool/trace.h"
@@ -79,6 +80,12 @@ struct Flags {
   std::string validate;
   // TLS / auth for a real apiserver
   std::string ca_file, client_cert, client_key, token_file, agent_token, agent_token_file, agent_ca_file;
+  int token_reload_ms = 60000;
+  // node agents: discovery and credentials (provider.h AgentAccess)
+  std::string agent_discovery = "annotation", agent_namespace = "gpupool-system",
+              agent_selector = "app.kubernetes.io/name=gpupool-agent", agent_scheme = "https",
+              agent_signing_key;
+  int agent_port = 9443;
   std::string kubeconfig, kube_context;
   bool insecure = false;
   bool apiserver_set = false;
@@ -110,7 +117,17 @@ controllers:
   --progress-poll D (250ms)    requeue while scaling/draining
   --credentials-retry D (30s)  AzureVmPool retry after a credentials error
   --agent-timeout D (60s)      node-agent RPC timeout (covers on-claim GPU probes)
-  --agent-token-file F         shared secret for the node-agent RPC   [$GPUPOOL_AGENT_TOKEN]
+  --token-reload D (60s)       re-read --token-file / the ServiceAccount token this often (and on 401)
+node agents:
+  --agent-discovery pod|annotation (annotation)  pod: the agent Pod's IP on each node (pods of
+                               --agent-namespace matching --agent-selector); annotation: the Node's
+                               gpupool.amd.com/agent-endpoint (local setups)
+  --agent-namespace NS (gpupool-system)  --agent-selector SEL (app.kubernetes.io/name=gpupool-agent)
+  --agent-scheme https|http (https)      --agent-port N (9443)
+  --agent-signing-key F        Ed25519 key: sign every agent request for its node (no bearer sent)
+                               [$GPUPOOL_AGENT_SIGNING_KEY]
+  --agent-token-file F         shared bearer for agents without signatures, re-read as it rotates
+                               [$GPUPOOL_AGENT_TOKEN]
   --agent-ca-file F            CA that signs https:// agent endpoints [$GPUPOOL_AGENT_CA_FILE]
   --orphan-sweep D (30s)       release claims whose pool no longer exists
   --quota-fail-open            admit scale-ups when ResourceQuotas cannot be read (clusters without
@@ -146,6 +163,7 @@ Flags parse(int argc, char** argv) {
   env("GPUPOOL_NAMESPACE", f.ns);
   env("GPUPOOL_AGENT_TOKEN", f.agent_token);
   env("GPUPOOL_AGENT_CA_FILE", f.agent_ca_file);
+  env("GPUPOOL_AGENT_SIGNING_KEY", f.agent_signing_key);
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&]() -> std::string {
@@ -167,6 +185,13 @@ Flags parse(int argc, char** argv) {
     else if (is("--token-file")) f.token_file = val();
     else if (is("--agent-token-file")) f.agent_token_file = val();
     else if (is("--agent-ca-file")) f.agent_ca_file = val();
+    else if (is("--token-reload")) f.token_reload_ms = parse_duration_ms(val());
+    else if (is("--agent-discovery")) f.agent_discovery = val();
+    else if (is("--agent-namespace")) f.agent_namespace = val();
+    else if (is("--agent-selector")) f.agent_selector = val();
+    else if (is("--agent-scheme")) f.agent_scheme = val();
+    else if (is("--agent-port")) f.agent_port = std::stoi(val());
+    else if (is("--agent-signing-key")) f.agent_signing_key = val();
     else if (is("--kubeconfig")) f.kubeconfig = val();
     else if (is("--context")) f.kube_context = val();
     else if (a == "--insecure-skip-tls-verify") f.insecure = true;
@@ -211,6 +236,10 @@ Flags parse(int argc, char** argv) {
       std::cerr << "unknown flag " << a << "\n";
       std::exit(2);
     }
+  }
+  if (f.agent_discovery != "pod" && f.agent_discovery != "annotation") {
+    std::cerr << "--agent-discovery must be pod or annotation\n";
+    std::exit(2);
   }
   if (f.cloud != "fake" && f.cloud != "azure-arm") {
     std::cerr << "--cloud must be fake or azure-arm\n";
@@ -304,7 +333,8 @@ class AgentWatchers {
     while (!w->stop && !g_stop) {
       try {
         // the agent holds the answer up to timeoutSeconds: allow that plus slack before timing out
-        HttpClient c(Url::parse(w->endpoint), prov_.agent_token(), 10000, prov_.agent_tls());
+        std::unique_ptr<HttpClient> cp = prov_.new_client(node, w->endpoint, 10000);
+        HttpClient& c = *cp;
         std::string path = "/v1/events?timeoutSeconds=5&since=" + std::to_string(since);
         int status = c.stream_lines(
             path,
@@ -414,20 +444,16 @@ int main(int argc, char** argv) {
   tls.cert_file = f.client_cert;
   tls.key_file = f.client_key;
   tls.insecure = f.insecure;
-  if (!f.agent_token_file.empty()) {
-    std::ifstream tf(f.agent_token_file);
-    std::stringstream ss;
-    ss << tf.rdbuf();
-    f.agent_token = ss.str();
-    while (!f.agent_token.empty() && (f.agent_token.back() == '\n' || f.agent_token.back() == '\r'))
-      f.agent_token.pop_back();
-  }
-  if (!f.token_file.empty()) {
-    std::ifstream tf(f.token_file);
-    std::stringstream ss;
-    ss << tf.rdbuf();
-    f.token = ss.str();
-    while (!f.token.empty() && (f.token.back() == '\n' || f.token.back() == '\r')) f.token.pop_back();
+  const auto reload = std::chrono::milliseconds(std::max(1000, f.token_reload_ms));
+  // apiserver bearer: a file is re-read as it rotates (projected ServiceAccount tokens expire;
+  // client-go re-reads them every minute and after a 401 — so do we)
+  std::shared_ptr<TokenSource> api_tokens;
+  try {
+    if (!f.token_file.empty()) api_tokens = TokenSource::file(f.token_file, reload);
+    else if (!f.token.empty()) api_tokens = TokenSource::fixed(f.token);
+  } catch (const std::exception& e) {
+    log.error("apiserver token", Json::object().set("error", e.what()));
+    return 2;
   }
   if (!f.apiserver_set && !getenv("GPUPOOL_APISERVER")) {
     std::string server, token, home_cfg;
@@ -437,7 +463,7 @@ int main(int argc, char** argv) {
     bool use_kc = !f.kubeconfig.empty() || (env_kc && *env_kc);
     if (!use_kc && KubeClient::in_cluster(&server, &token, &ic)) {  // running in a pod
       f.apiserver = server;
-      if (f.token.empty()) f.token = token;
+      if (!api_tokens) api_tokens = TokenSource::file("/var/run/secrets/kubernetes.io/serviceaccount/token", reload);
       if (tls.ca_file.empty()) tls.ca_file = ic.ca_file;
     } else if (use_kc || (!home_cfg.empty() && std::ifstream(home_cfg).good())) {
       KubeConfig kc;
@@ -448,7 +474,10 @@ int main(int argc, char** argv) {
         return 2;
       }
       f.apiserver = kc.server;
-      if (f.token.empty()) f.token = kc.token;  // explicit flags win over the kubeconfig
+      if (!api_tokens) {  // explicit flags win over the kubeconfig
+        if (!kc.token_file.empty()) api_tokens = TokenSource::file(kc.token_file, reload);
+        else if (!kc.token.empty()) api_tokens = TokenSource::fixed(kc.token);
+      }
       if (tls.ca_file.empty() && tls.ca_pem.empty()) {
         tls.ca_file = kc.tls.ca_file;
         tls.ca_pem = kc.tls.ca_pem;
@@ -463,7 +492,21 @@ int main(int argc, char** argv) {
       log.info("using kubeconfig", Json::object().set("context", kc.context).set("server", kc.server));
     }
   }
-  KubeClient client(f.apiserver, f.token, 15000, tls);
+  // node-agent credentials
+  AgentAccess agent_access;
+  agent_access.discovery = f.agent_discovery;
+  agent_access.scheme = f.agent_scheme;
+  agent_access.port = f.agent_port;
+  agent_access.tls.ca_file = f.agent_ca_file;
+  try {
+    if (!f.agent_signing_key.empty()) agent_access.signer = std::make_shared<AgentSigner>(f.agent_signing_key);
+    if (!f.agent_token_file.empty()) agent_access.token = TokenSource::file(f.agent_token_file, reload);
+    else if (!f.agent_token.empty()) agent_access.token = TokenSource::fixed(f.agent_token);
+  } catch (const std::exception& e) {
+    log.error("agent credentials", Json::object().set("error", e.what()));
+    return 2;
+  }
+  KubeClient client(f.apiserver, api_tokens, 15000, tls);
   std::atomic<bool> healthy{true}, leading{!f.leader_elect};
 
   HttpServer metrics;
@@ -542,9 +585,14 @@ int main(int argc, char** argv) {
     Informer mipools(client, res::mi355xpools(), f.ns, std::chrono::milliseconds(f.resync_ms));
     Informer azpools(client, res::azurevmpools(), f.ns, std::chrono::milliseconds(f.resync_ms));
     Informer quotas(client, res::resourcequotas(), f.ns, std::chrono::milliseconds(f.resync_ms));
-    TlsOptions agent_tls;
-    agent_tls.ca_file = f.agent_ca_file;
-    RocmProvider rocm(nodes, f.agent_timeout_ms, f.agent_token, agent_tls);
+    // agent Pods (discovery "pod"): only the DaemonSet's pods in its namespace are cached
+    InformerOptions agent_pod_opts;
+    agent_pod_opts.label_selector = f.agent_selector;
+    Informer agent_pods(client, res::pods(), f.agent_namespace, std::chrono::milliseconds(f.resync_ms),
+                        agent_pod_opts);
+    AgentAccess access = agent_access;
+    if (f.agent_discovery == "pod") access.pods = &agent_pods;
+    RocmProvider rocm(nodes, f.agent_timeout_ms, access);
     FakeCloudOptions fco;
     fco.provision = std::chrono::milliseconds(f.fakecloud_provision_ms);
     fco.deprovision = std::chrono::milliseconds(f.fakecloud_deprovision_ms);
@@ -571,15 +619,59 @@ int main(int argc, char** argv) {
     CloudProvider& cloud = *cloud_impl;
     Informer jobs(client, ResourceRef{gen::kGroup, gen::kVersion, gen::kPluralMi355xJob, true, "Mi355xJob"}, f.ns,
                   std::chrono::milliseconds(f.resync_ms));
-    Informer pods(client, res::pods(), "", std::chrono::milliseconds(f.resync_ms));
+    // the cluster's pods, bounded: only pods that request an extended resource or belong to a
+    // Mi355xJob are cached, each as a projection of the fields the readers use (podindex.h) —
+    // whole pods of every workload in a 50k-pod cluster would not fit the manager's 512 Mi
+    InformerOptions pod_opts;
+    pod_opts.filter = pod_relevant;
+    pod_opts.transform = trim_pod;
+    Informer pods(client, res::pods(), "", std::chrono::milliseconds(f.resync_ms), pod_opts);
+    PodIndex pod_index;
+    pod_index.attach(pods);
     Informer queues(client, res::mi355xqueues(), "", std::chrono::milliseconds(f.resync_ms));
     Mi355xPoolReconciler mi(client, mipools, rocm, &events, ropts);
-    Mi355xJobReconciler jr(client, jobs, nodes, &events, ropts);
+    Mi355xJobReconciler jr(client, jobs, nodes, &events, ropts, &pod_index);
     Mi355xQueueReconciler qr(client, queues, jobs, &events, ropts);
     Mi355xPoolAutoscaler as(client, mipools, jobs, pods, &events, ropts);
     AzureVmPoolReconciler az(client, azpools, cloud, &events, ropts);
     AgentWatchers watchers(rocm, mipools, ctl);
 
+    // Node events are frequent (every kubelet and agent heartbeat is a status write) and almost
+    // never change what placement reads: wake waiting pools / gangs only when one of those facts
+    // moved — labels, schedulability, Ready, the agent endpoint, allocatable.
+    std::mutex node_fp_mu;
+    std::map<std::string, std::string> node_fp;
+    auto node_facts_changed = [&](const std::string& type, const Json& n) {
+      const std::string name = n.path("metadata.name").as_string();
+      std::string fp;
+      if (type != "DELETED") {
+        std::string ready;
+        for (const auto& c : n.path("status.conditions").elements())
+          if (c["type"].as_string() == "Ready") ready = c["status"].as_string();
+        fp = n.path("metadata.labels").dump() + "|" + (n.path("spec.unschedulable").as_bool(false) ? "U" : "S") + "|" +
+             ready + "|" + n.path("metadata.annotations")[gen::kAnnAgentEndpoint].as_string() + "|" +
+             n.path("status.allocatable").dump();
+      }
+      std::lock_guard<std::mutex> g(node_fp_mu);
+      auto it = node_fp.find(name);
+      const bool changed = it == node_fp.end() || it->second != fp;
+      if (type == "DELETED") node_fp.erase(name);
+      else node_fp[name] = fp;
+      return changed;
+    };
+    auto count_node_event = [](bool relevant) {
+      static CounterVec& c = Registry::global().counter(
+          "gpupool_node_events_total", "Node watch events by whether a placement fact changed.");
+      c.inc({{"relevant", relevant ? "true" : "false"}});
+    };
+    // one fingerprint check per event, shared by the pool and job handlers
+    std::atomic<bool> node_relevant{false};
+    nodes.add_handler([&](const std::string& type, const Json& n) {
+      if (type == "RESYNC") return;
+      const bool r = node_facts_changed(type, n);
+      node_relevant = r;
+      count_node_event(r);
+    });
     auto pool_handler = [&ctl](const char* kind, PoolReconcilerBase* r = nullptr) {
       return [&ctl, kind, r](const std::string& type, const Json& obj) {
         if (r && type == "MODIFIED" && r->own_status_write(obj)) return;  // our own status write
@@ -590,7 +682,7 @@ int main(int argc, char** argv) {
       ctl.add_reconciler(&mi);
       mipools.add_handler(pool_handler("Mi355xPool", &mi));
       nodes.add_handler([&](const std::string& type, const Json&) {
-        if (type == "RESYNC") return;
+        if (type == "RESYNC" || !node_relevant) return;
         watchers.sync(rocm.node_names());
         // node/agent changes can unblock pools waiting for devices
         for (const auto& p : mipools.list())
@@ -608,6 +700,16 @@ int main(int argc, char** argv) {
               !condition_true(p.path("status.conditions"), gen::kCondReady))
             ctl.enqueue("Mi355xPool", qns, p.path("metadata.name").as_string());
       });
+      if (f.agent_discovery == "pod") {
+        agent_pods.add_handler([&](const std::string& type, const Json&) {
+          if (type == "RESYNC") return;
+          watchers.sync(rocm.node_names());  // an agent (re)started: follow its new address
+          for (const auto& p : mipools.list())
+            if (!condition_true(p.path("status.conditions"), gen::kCondReady))
+              ctl.enqueue("Mi355xPool", p.path("metadata.namespace").as_string(), p.path("metadata.name").as_string());
+        });
+        agent_pods.start();
+      }
       nodes.start();
       mipools.start();
       quotas.start();
@@ -632,8 +734,16 @@ int main(int argc, char** argv) {
         const std::string phase = p.path("status.phase").as_string();
         if (type == "DELETED" || phase == "Succeeded" || phase == "Failed") wake_pending();
       });
-      nodes.add_handler([wake_pending](const std::string& type, const Json&) {
-        if (type != "RESYNC") wake_pending();
+      nodes.add_handler([wake_pending, &node_relevant](const std::string& type, const Json&) {
+        if (type != "RESYNC" && node_relevant) wake_pending();
+      });
+      // a gang that ends, is suspended or gives its placement back frees GPUs for waiting ones
+      jobs.add_handler([wake_pending](const std::string& type, const Json& j) {
+        if (type == "RESYNC") return;
+        const std::string ph = j.path("status.phase").str_or("Pending");
+        if (type == "DELETED" || ph == "Succeeded" || ph == "Failed" || ph == "Suspended" ||
+            (ph == "Restarting" && j.path("status.placement").size() == 0))
+          wake_pending();
       });
       // queue edits (created, opened, capability raised) can admit waiting jobs
       queues.add_handler([&ctl, wake_pending](const std::string& type, const Json& q) {
@@ -690,6 +800,7 @@ int main(int argc, char** argv) {
     if (want_mi) {
       wait_cache(nodes, "nodes");
       wait_cache(mipools, "mi355xpools");
+      if (f.agent_discovery == "pod") wait_cache(agent_pods, "agent pods");
     }
     if (want_az) wait_cache(azpools, "azurevmpools");
     if (want_job) {
@@ -704,9 +815,16 @@ int main(int argc, char** argv) {
     }
     auto last_sweep = std::chrono::steady_clock::now();
     GaugeVec& depth = Registry::global().gauge("gpupool_workqueue_depth", "Ready keys in the work queue.");
+    GaugeVec& cred = Registry::global().gauge(
+        "gpupool_credential_reloads", "Times a rotating credential file was re-read with a new value.");
     while (!g_stop && leading) {
       std::this_thread::sleep_for(std::chrono::milliseconds(100));
       depth.set({}, static_cast<double>(ctl.queue().len()));
+      if (api_tokens) cred.set({{"credential", "apiserver-token"}}, static_cast<double>(api_tokens->reloads()));
+      if (agent_access.token)
+        cred.set({{"credential", "agent-token"}}, static_cast<double>(agent_access.token->reloads()));
+      if (agent_access.signer)
+        cred.set({{"credential", "agent-signing-key"}}, static_cast<double>(agent_access.signer->reloads()));
       if (want_mi && std::chrono::steady_clock::now() - last_sweep > std::chrono::milliseconds(f.orphan_sweep_ms)) {
         last_sweep = std::chrono::steady_clock::now();
         try {
@@ -726,6 +844,7 @@ int main(int argc, char** argv) {
     azpools.stop();
     quotas.stop();
     nodes.stop();
+    agent_pods.stop();
     events.flush(std::chrono::milliseconds(2000));
   };
 

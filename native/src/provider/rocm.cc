@@ -1,8 +1,11 @@
 // RocmProvider: the MI355X provider. Where the reference called the Azure Go SDK over HTTPS
 // (README.md:179-221), this talks to the node agent that owns the node's GPUs (claim ledger,
 // libmi355x_dev telemetry, HIP probe, device plugin) over HTTP/1.1 JSON — a unix socket on the
-// same host, or TCP across nodes. Agents are found through the Node object's
-// gpupool.amd.com/agent-endpoint annotation.
+// same host, or TCP across nodes. In a cluster an agent is found through its own Pod (the IP the
+// kubelet/CNI gave the agent Pod bound to that node, AgentAccess "pod"); local setups name it in
+// the Node's gpupool.amd.com/agent-endpoint annotation. Every request carries a per-request
+// Ed25519 signature bound to the node (agentauth.h), so no endpoint ever receives a credential it
+// could replay against another agent — least privilege, as README.md:43-57 scopes its SP.
 #include "gpupool/generated/schema_consts.h"
 #include "gpupool/informer.h"
 #include "gpupool/metrics.h"
@@ -104,12 +107,18 @@ Json DeviceView::status_json() const {
   return s;
 }
 
-RocmProvider::RocmProvider(Informer& nodes, int timeout_ms, std::string agent_token, TlsOptions agent_tls)
-    : nodes_(nodes), timeout_ms_(timeout_ms), agent_token_(std::move(agent_token)), agent_tls_(std::move(agent_tls)) {
+RocmProvider::RocmProvider(Informer& nodes, int timeout_ms, AgentAccess access)
+    : nodes_(nodes), timeout_ms_(timeout_ms), access_(std::move(access)) {
+  if (access_.discovery == "pod" && !access_.pods)
+    throw std::invalid_argument("agent discovery \"pod\" needs an agent pods informer");
   // the handler first, then the informer's current contents: an update in between is applied by
   // the handler and then again (same or newer state) by the seed
   nodes_.add_handler([this](const std::string& type, const Json& obj) { note_node_(type, obj); });
   for (const auto& n : nodes_.list()) note_node_("ADDED", n);
+  if (access_.pods) {
+    access_.pods->add_handler([this](const std::string& type, const Json& obj) { note_agent_pod_(type, obj); });
+    for (const auto& p : access_.pods->list()) note_agent_pod_("ADDED", p);
+  }
 }
 
 void RocmProvider::note_node_(const std::string& type, const Json& obj) {
@@ -123,7 +132,76 @@ void RocmProvider::note_node_(const std::string& type, const Json& obj) {
   NodeFacts& f = facts_[name];
   f.labels = obj.path("metadata.labels").is_object() ? obj.path("metadata.labels") : Json::object();
   f.schedulable = !obj.path("spec.unschedulable").as_bool(false);
-  f.endpoint = obj.path("metadata.annotations")[gen::kAnnAgentEndpoint].str_or("");
+  f.annotation = obj.path("metadata.annotations")[gen::kAnnAgentEndpoint].str_or("");
+  derive_endpoint_(name, f);
+}
+
+void RocmProvider::note_agent_pod_(const std::string& type, const Json& pod) {
+  const std::string node = pod.path("spec.nodeName").as_string();
+  const std::string key = Informer::key_of(pod);
+  const std::string ip = pod.path("status.podIP").as_string();
+  const bool live = type != "DELETED" && !ip.empty() && pod.path("status.phase").as_string() == "Running" &&
+                    !pod.path("metadata.deletionTimestamp").is_string();
+  std::lock_guard<std::mutex> g(facts_mu_);
+  // a pod's node never changes, but a DELETED event may carry it: drop the key everywhere
+  for (auto it = agent_pods_.begin(); it != agent_pods_.end();) {
+    it->second.erase(key);
+    it = it->second.empty() ? agent_pods_.erase(it) : std::next(it);
+  }
+  if (live && !node.empty()) agent_pods_[node][key] = ip;
+  if (!node.empty()) {
+    auto f = facts_.find(node);
+    if (f != facts_.end()) derive_endpoint_(node, f->second);
+  }
+}
+
+void RocmProvider::derive_endpoint_(const std::string& node, NodeFacts& f) {
+  if (access_.discovery != "pod") {
+    f.endpoint = f.annotation;
+    return;
+  }
+  auto it = agent_pods_.find(node);
+  if (it == agent_pods_.end() || it->second.empty()) {
+    f.endpoint.clear();  // no running agent pod on the node: nothing to call
+    return;
+  }
+  const std::string& ip = it->second.begin()->second;  // a DaemonSet runs one per node
+  const std::string host = ip.find(':') != std::string::npos ? "[" + ip + "]" : ip;
+  f.endpoint = access_.scheme + "://" + host + ":" + std::to_string(access_.port);
+  if (!f.annotation.empty() && f.annotation != f.endpoint) {
+    // honoured only when it names the agent Pod's own address (another port or scheme)
+    bool same_host = false;
+    try {
+      Url u = Url::parse(f.annotation);
+      same_host = u.scheme != "unix" && (u.host == ip || u.host == host);
+    } catch (const std::exception&) {
+    }
+    if (same_host) {
+      f.endpoint = f.annotation;
+    } else {
+      endpoints_rejected_.fetch_add(1);
+      static CounterVec& rej = Registry::global().counter(
+          "gpupool_agent_endpoint_rejected_total",
+          "Node agent-endpoint annotations ignored: the host is not the node's agent Pod IP.");
+      rej.inc({{"node", node}});
+    }
+  }
+}
+
+std::unique_ptr<HttpClient> RocmProvider::new_client(const std::string& node, const std::string& endpoint,
+                                                     int timeout_ms) {
+  std::unique_ptr<HttpClient> c;
+  if (access_.signer) {
+    // signatures replace the bearer: the endpoint gets nothing it could replay elsewhere
+    c = std::make_unique<HttpClient>(Url::parse(endpoint), std::shared_ptr<TokenSource>(), timeout_ms, access_.tls);
+    std::shared_ptr<AgentSigner> signer = access_.signer;
+    c->set_signer([signer, node](const std::string& m, const std::string& target, const std::string& body) {
+      return signer->header(m, target, node, body);
+    });
+  } else {
+    c = std::make_unique<HttpClient>(Url::parse(endpoint), access_.token, timeout_ms, access_.tls);
+  }
+  return c;
 }
 
 std::vector<std::string> RocmProvider::node_names() {
@@ -159,7 +237,7 @@ std::shared_ptr<HttpClient> RocmProvider::client_for(const std::string& node) {
   auto& slot = clients_[node];
   if (!slot.second || slot.first != ep) {
     slot.first = ep;
-    slot.second = std::make_shared<HttpClient>(Url::parse(ep), agent_token_, timeout_ms_, agent_tls_);
+    slot.second = std::shared_ptr<HttpClient>(new_client(node, ep, timeout_ms_));
   }
   return slot.second;
 }

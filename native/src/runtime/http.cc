@@ -14,6 +14,7 @@
 #include <cerrno>
 #include <chrono>
 #include <cstring>
+#include <fstream>
 #include <sstream>
 
 #include <openssl/err.h>
@@ -306,6 +307,76 @@ std::string ssl_errors() {
 }
 }  // namespace
 
+std::shared_ptr<TokenSource> TokenSource::fixed(std::string token) {
+  std::shared_ptr<TokenSource> t(new TokenSource());
+  t->token_ = std::move(token);
+  return t;
+}
+
+std::shared_ptr<TokenSource> TokenSource::file(std::string path, std::chrono::milliseconds reload_after) {
+  std::shared_ptr<TokenSource> t(new TokenSource());
+  t->path_ = std::move(path);
+  t->reload_after_ = reload_after;
+  std::lock_guard<std::mutex> g(t->mu_);
+  t->read_locked_();
+  if (t->token_.empty()) throw HttpError("token file " + t->path_ + " is missing or empty");
+  return t;
+}
+
+void TokenSource::read_locked_() {
+  read_at_ = std::chrono::steady_clock::now();
+  std::ifstream f(path_, std::ios::binary);
+  if (!f) return;  // mid-rotation (the kubelet swaps a symlink): keep the last value
+  std::stringstream ss;
+  ss << f.rdbuf();
+  std::string t = ss.str();
+  while (!t.empty() && (t.back() == '\n' || t.back() == '\r' || t.back() == ' ')) t.pop_back();
+  if (!t.empty() && t != token_) {
+    if (!token_.empty()) reloads_.fetch_add(1);
+    token_ = std::move(t);
+  }
+}
+
+std::string TokenSource::token() {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!path_.empty() && std::chrono::steady_clock::now() - read_at_ >= reload_after_) read_locked_();
+  return token_;
+}
+
+bool TokenSource::reload() {
+  if (path_.empty()) return false;
+  std::lock_guard<std::mutex> g(mu_);
+  const std::string before = token_;
+  read_locked_();
+  return token_ != before;
+}
+
+HttpClient::HttpClient(Url url, std::shared_ptr<TokenSource> tokens, int timeout_ms, TlsOptions tls)
+    : HttpClient(std::move(url), std::string(), timeout_ms, std::move(tls)) {
+  tokens_ = std::move(tokens);
+}
+
+std::string HttpClient::auth_headers_(const std::string& method, const std::string& path, const std::string& body,
+                                      const std::string* bearer) {
+  std::string h;
+  if (tokens_) {
+    std::string t = bearer ? *bearer : tokens_->token();
+    if (!t.empty()) h += "Authorization: Bearer " + t + "\r\n";
+  } else if (!token_.empty()) {
+    h += "Authorization: Bearer " + token_ + "\r\n";
+  }
+  if (signer_) h += signer_(method, path, body);
+  return h;
+}
+
+// After a 401 sent with ``used``: worth one more try when the source now holds another token —
+// re-read just now, or already by a concurrent request that got its 401 first.
+bool HttpClient::reload_after_401_(const std::string& used) {
+  if (!tokens_) return false;
+  tokens_->reload();
+  return tokens_->token() != used;
+}
+
 HttpClient::HttpClient(Url url, std::string bearer_token, int timeout_ms, TlsOptions tls)
     : url_(std::move(url)), token_(std::move(bearer_token)), timeout_ms_(timeout_ms), tls_(std::move(tls)) {
   if (url_.scheme != "https") return;
@@ -452,14 +523,15 @@ void HttpClient::give_(std::unique_ptr<Conn> c) {
 
 bool HttpClient::send_request_(Conn& c, const std::string& method, const std::string& path,
                                const std::string& body, const std::string& content_type,
-                               const std::string& accept, const std::string& extra_headers) {
+                               const std::string& accept, const std::string& extra_headers,
+                               const std::string* bearer) {
   std::string req;
   req.reserve(256 + body.size());
   req += method + " " + path + " HTTP/1.1\r\n";
   req += "Host: " + (url_.scheme == "unix" ? std::string("localhost") : url_.host) + "\r\n";
   req += "User-Agent: gpupool-manager/0.1\r\n";
   req += "Accept: " + accept + "\r\n";
-  if (!token_.empty()) req += "Authorization: Bearer " + token_ + "\r\n";
+  req += auth_headers_(method, path, body, bearer);
   req += extra_headers;
   if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
     req += "Content-Type: " + content_type + "\r\n";
@@ -544,11 +616,26 @@ HttpResponse HttpClient::request(const std::string& method, const std::string& p
                                  const std::string& body, const std::string& content_type,
                                  const std::string& accept, int timeout_ms, const std::string& extra_headers) {
   if (timeout_ms < 0) timeout_ms = timeout_ms_;
+  const std::string used = tokens_ ? tokens_->token() : std::string();
+  HttpResponse r = request_once_(method, path, body, content_type, accept, timeout_ms, extra_headers, &used);
+  // a rotated credential: the file already holds the new one (or will within the kubelet's
+  // refresh) — re-read it and send once more, instead of failing until the periodic reload
+  if (r.status == 401 && reload_after_401_(used)) {
+    const std::string fresh = tokens_->token();
+    r = request_once_(method, path, body, content_type, accept, timeout_ms, extra_headers, &fresh);
+  }
+  return r;
+}
+
+HttpResponse HttpClient::request_once_(const std::string& method, const std::string& path,
+                                       const std::string& body, const std::string& content_type,
+                                       const std::string& accept, int timeout_ms,
+                                       const std::string& extra_headers, const std::string* bearer) {
   for (int attempt = 0; attempt < 2; ++attempt) {
     std::unique_ptr<Conn> c = take_();
     bool reused = c != nullptr;
     if (!c) c = connect_(timeout_ms);
-    if (!send_request_(*c, method, path, body, content_type, accept, extra_headers)) {
+    if (!send_request_(*c, method, path, body, content_type, accept, extra_headers, bearer)) {
       if (reused) continue;
       throw HttpError("send failed: " + std::string(strerror(errno)));
     }
@@ -602,8 +689,24 @@ HttpResponse HttpClient::request(const std::string& method, const std::string& p
 int HttpClient::stream_lines(const std::string& path,
                              const std::function<bool(std::string_view)>& on_line,
                              const std::atomic<bool>* stop, std::string* err_body, int poll_ms) {
+  std::string body401;
+  const std::string used = tokens_ ? tokens_->token() : std::string();
+  int status = stream_lines_once_(path, on_line, stop, &body401, poll_ms, &used);
+  if (status == 401 && reload_after_401_(used)) {
+    body401.clear();
+    const std::string fresh = tokens_->token();
+    status = stream_lines_once_(path, on_line, stop, &body401, poll_ms, &fresh);
+  }
+  if (status >= 400 && err_body) *err_body = body401;
+  return status;
+}
+
+int HttpClient::stream_lines_once_(const std::string& path,
+                                   const std::function<bool(std::string_view)>& on_line,
+                                   const std::atomic<bool>* stop, std::string* err_body, int poll_ms,
+                                   const std::string* bearer) {
   auto c = connect_(timeout_ms_);
-  if (!send_request_(*c, "GET", path, "", "application/json", "application/json"))
+  if (!send_request_(*c, "GET", path, "", "application/json", "application/json", "", bearer))
     throw HttpError("send failed");
   HttpResponse r;
   std::string err;

@@ -5,8 +5,8 @@
 namespace gpupool {
 
 Informer::Informer(KubeClient& client, ResourceRef res, std::string ns,
-                   std::chrono::milliseconds resync)
-    : client_(client), res_(std::move(res)), ns_(std::move(ns)), resync_(resync),
+                   std::chrono::milliseconds resync, InformerOptions opts)
+    : client_(client), res_(std::move(res)), ns_(std::move(ns)), resync_(resync), opts_(std::move(opts)),
       log_(Logger("informer").with("resource", res_.plural)) {}
 
 Informer::~Informer() { stop(); }
@@ -82,10 +82,13 @@ void Informer::dispatch_(const std::string& type, const Json& obj) {
 }
 
 void Informer::list_() {
-  Json lst = client_.list(res_, ns_);
+  Json lst = client_.list(res_, ns_, opts_.label_selector, opts_.field_selector);
   relists_++;
   std::map<std::string, Json> fresh;
-  for (const auto& item : lst["items"].elements()) fresh[key_of(item)] = item;
+  for (const auto& item : lst["items"].elements()) {
+    if (opts_.filter && !opts_.filter(item)) continue;
+    fresh[key_of(item)] = opts_.transform ? opts_.transform(item) : item;
+  }
   std::vector<std::pair<std::string, Json>> events;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -137,21 +140,30 @@ void Informer::run_() {
       }
       std::string last = client_.watch(
           res_, ns_, rv,
-          [this](const std::string& type, const Json& obj) {
+          [this](const std::string& type_in, const Json& raw) {
+            events_++;
+            std::string type = type_in;
+            const bool keep = !opts_.filter || opts_.filter(raw);
+            const Json obj = opts_.transform ? opts_.transform(raw) : raw;
             std::string key = key_of(obj);
+            bool deliver = true;
             {
               std::lock_guard<std::mutex> g(mu_);
-              if (type == "DELETED") {
-                cache_.erase(key);
+              rv_ = raw.path("metadata.resourceVersion").as_string();
+              if (!keep && type != "DELETED") {  // left the filter (or never in it)
+                deliver = cache_.erase(key) > 0;
+                type = "DELETED";
+              } else if (type == "DELETED") {
+                deliver = cache_.erase(key) > 0 || keep;
               } else {
+                if (!cache_.count(key)) type = "ADDED";  // entered the filter
                 cache_[key] = obj;
               }
-              rv_ = obj.path("metadata.resourceVersion").as_string();
             }
-            dispatch_(type, obj);
+            if (deliver) dispatch_(type, obj);
             return !stop_.load();
           },
-          &stop_, 300);
+          &stop_, 300, opts_.label_selector, opts_.field_selector);
       {
         std::lock_guard<std::mutex> g(mu_);
         if (!last.empty()) rv_ = last;

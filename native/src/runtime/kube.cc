@@ -33,8 +33,11 @@ ResourceRef azurevmpools() { return {gen::kGroup, gen::kVersion, gen::kPluralAzu
 }  // namespace res
 
 KubeClient::KubeClient(const std::string& server, const std::string& token, int timeout_ms, TlsOptions tls)
-    : server_(server), token_(token), tls_(tls),
-      http_(std::make_unique<HttpClient>(Url::parse(server), token, timeout_ms, std::move(tls))) {}
+    : KubeClient(server, token.empty() ? nullptr : TokenSource::fixed(token), timeout_ms, std::move(tls)) {}
+
+KubeClient::KubeClient(const std::string& server, std::shared_ptr<TokenSource> tokens, int timeout_ms, TlsOptions tls)
+    : server_(server), tokens_(std::move(tokens)), tls_(tls),
+      http_(std::make_unique<HttpClient>(Url::parse(server), tokens_, timeout_ms, std::move(tls))) {}
 
 bool KubeClient::in_cluster(std::string* server, std::string* token, TlsOptions* tls, const std::string& sa_dir) {
   const char* host = getenv("KUBERNETES_SERVICE_HOST");
@@ -110,7 +113,8 @@ KubeConfig load_kubeconfig(const std::string& path_in, const std::string& contex
       throw std::runtime_error("kubeconfig " + path + ": basic auth is not supported");
     out.token = user["token"].as_string();
     if (out.token.empty() && user["tokenFile"].is_string()) {
-      out.token = read_file(resolve(user["tokenFile"].as_string()));
+      out.token_file = resolve(user["tokenFile"].as_string());  // re-read as it rotates
+      out.token = read_file(out.token_file);
       while (!out.token.empty() && (out.token.back() == '\n' || out.token.back() == '\r')) out.token.pop_back();
     }
     if (user["client-certificate-data"].is_string())
@@ -193,12 +197,15 @@ void KubeClient::evict(const std::string& ns, const std::string& name, int grace
 
 std::string KubeClient::watch(const ResourceRef& r, const std::string& ns, const std::string& rv,
                               const std::function<bool(const std::string&, const Json&)>& cb,
-                              const std::atomic<bool>* stop, int timeout_seconds) {
+                              const std::atomic<bool>* stop, int timeout_seconds,
+                              const std::string& label_selector, const std::string& field_selector) {
   std::string p = r.path(ns) + "?watch=1&allowWatchBookmarks=true&timeoutSeconds=" +
                   std::to_string(timeout_seconds);
+  if (!label_selector.empty()) p += "&labelSelector=" + url_encode(label_selector);
+  if (!field_selector.empty()) p += "&fieldSelector=" + url_encode(field_selector);
   if (!rv.empty()) p += "&resourceVersion=" + url_encode(rv);
   // A dedicated client per stream: watches are long-lived and must not hold pooled sockets.
-  HttpClient stream(http_->url(), token_, 15000, tls_);
+  HttpClient stream(http_->url(), tokens_, 15000, tls_);
   std::string last = rv;
   std::string err_body;
   int status = stream.stream_lines(

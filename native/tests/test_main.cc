@@ -2,9 +2,17 @@
 #include <chrono>
 #include <cstring>
 
+#include "gpupool/agentauth.h"
 #include "testing.h"
 
 int main(int argc, char** argv) {
+  // `gpupool_tests --sign KEY METHOD TARGET NODE BODY`: print the manager's signature header for
+  // one request (tests/unit/test_edsig.py checks it against the agent's Python verifier)
+  if (argc == 7 && std::strcmp(argv[1], "--sign") == 0) {
+    gpupool::AgentSigner s(argv[2]);
+    std::fputs(s.header(argv[3], argv[4], argv[5], argv[6]).c_str(), stdout);
+    return 0;
+  }
   const char* filter = argc > 1 ? argv[1] : "";
   int pass = 0, fail = 0;
   for (auto& c : gtest_lite::registry()) {

@@ -123,3 +123,39 @@ TEST(plan_replace_and_scale_down_in_one_pass) {
   EXPECT_EQ(p.keep, 1);
   EXPECT_EQ(p.need, 0);
 }
+
+TEST(pod_index_tracks_live_extended_requests_and_job_pods) {
+  using gpupool::Json;
+  auto pod = [](const std::string& name, const std::string& node, int gpus, const std::string& phase,
+                const std::string& job = "") {
+    Json p = Json::parse(R"({"metadata":{"name":"","namespace":"ns","labels":{}},"spec":{"nodeName":"",
+      "containers":[{"name":"c","resources":{"limits":{"amd.com/gpu":"0","cpu":"2"}}}]},"status":{"phase":""}})");
+    p["metadata"]["name"] = name;
+    p["spec"]["nodeName"] = node;
+    p["spec"]["containers"].at(0)["resources"]["limits"]["amd.com/gpu"] = std::to_string(gpus);
+    p["status"]["phase"] = phase;
+    if (!job.empty()) p["metadata"]["labels"]["gpupool.amd.com/job-name"] = job;
+    return p;
+  };
+  gpupool::PodIndex idx;
+  idx.on_event("ADDED", pod("a", "n1", 2, "Running"));
+  idx.on_event("ADDED", pod("b", "n1", 1, "Pending", "j"));
+  idx.on_event("ADDED", pod("c", "n2", 4, "Running", "j"));
+  auto u = idx.requested_by_node("amd.com/gpu");
+  EXPECT_TRUE(u["n1"] == 3 && u["n2"] == 4);
+  idx.on_event("MODIFIED", pod("a", "n1", 2, "Succeeded"));  // terminal: holds nothing
+  idx.on_event("DELETED", pod("c", "n2", 4, "Running", "j"));
+  u = idx.requested_by_node("amd.com/gpu");
+  EXPECT_TRUE(u["n1"] == 1 && !u.count("n2"));
+  EXPECT_TRUE(idx.job_pods("ns", "j").size() == 1 && idx.job_pods("other", "j").empty());
+  // the informer's projection keeps what the readers use, and relevance
+  Json cpu_only = pod("d", "n1", 0, "Running");
+  cpu_only["spec"]["containers"].at(0)["resources"]["limits"].erase("amd.com/gpu");
+  EXPECT_TRUE(!gpupool::pod_relevant(cpu_only));
+  EXPECT_TRUE(gpupool::pod_relevant(pod("e", "n1", 1, "Running")));
+  Json t = gpupool::trim_pod(pod("f", "n1", 1, "Running", "j"));
+  EXPECT_TRUE(t.path("spec.nodeName").as_string() == "n1");
+  EXPECT_TRUE(t.path("spec.containers")[0]["resources"]["limits"]["amd.com/gpu"].as_string() == "1");
+  EXPECT_TRUE(t.path("spec.containers")[0]["resources"]["limits"]["cpu"].is_null());
+  EXPECT_TRUE(t.path("metadata.labels")["gpupool.amd.com/job-name"].as_string() == "j");
+}

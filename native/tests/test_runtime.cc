@@ -557,3 +557,20 @@ TEST(job_validation) {
   auto spec = gpupool::Mi355xJobSpec::from(ok["spec"]);
   EXPECT_TRUE(spec.gpus_per_replica == 1 && spec.restart_policy == "OnFailure" && spec.master_port == 29500);
 }
+
+TEST(token_source_rotates_from_file) {
+  const std::string path = "/tmp/gpupool_token_test_" + std::to_string(::getpid());
+  { std::ofstream(path) << "first\n"; }
+  auto t = gpupool::TokenSource::file(path, std::chrono::hours(1));
+  EXPECT_TRUE(t->token() == "first");
+  { std::ofstream(path) << "second\n"; }
+  EXPECT_TRUE(t->token() == "first");  // not due yet: the cached value
+  EXPECT_TRUE(t->reload());            // what a 401 triggers
+  EXPECT_TRUE(t->token() == "second");
+  EXPECT_TRUE(!t->reload());           // unchanged
+  EXPECT_TRUE(t->reloads() == 1);
+  std::remove(path.c_str());
+  EXPECT_TRUE(!t->reload() && t->token() == "second");  // mid-swap: keep the last value
+  auto f = gpupool::TokenSource::fixed("x");
+  EXPECT_TRUE(f->token() == "x" && !f->reload());
+}

@@ -10,6 +10,14 @@ pools of R GPUs without a nodeName (the manager places them) all at once and tim
 * the manager's CPU seconds and RSS over the run, and the agents' RPC counts.
 
     python scripts/scale_bench.py [--nodes 16] [--pools 48] [--replicas 2] [--out F]
+
+``--mode jobs`` measures the Mi355xJob gang scheduler and the manager's pod cache instead: N Node
+objects (allocatable 8 GPUs each, kubelet-style heartbeats every 10 s), F filler pods (one GPU pod
+per node, the rest CPU-only), then G gangs submitted at once. It reports the time to place every
+gang, apiserver LIST counts (total and after the caches synced, per minute), node events by
+whether a placement fact changed, and the manager's CPU and RSS:
+
+    python scripts/scale_bench.py --mode jobs --nodes 64 --filler-pods 5000 --gangs 200
 """
 from __future__ import annotations
 
@@ -96,8 +104,193 @@ def ready(r: int):
     return pred
 
 
+def _metrics(text: str) -> dict[str, float]:
+    out: dict[str, float] = {}
+    for line in text.splitlines():
+        if line.startswith("#") or " " not in line:
+            continue
+        key, _, val = line.rpartition(" ")
+        try:
+            out[key] = out.get(key, 0.0) + float(val)
+        except ValueError:
+            pass
+    return out
+
+
+def _sum(m: dict[str, float], prefix: str) -> float:
+    return sum(v for k, v in m.items() if k.startswith(prefix))
+
+
+def jobs_mode(a) -> int:
+    """Gang placement and the pod cache at cluster scale (no agents: jobs place on Node
+    allocatable; their pods stay Pending, as nothing runs them — placement is what is timed)."""
+    from gpupool.kube import MI355XJOBS, NODES, PODS, Client
+    wd = tempfile.mkdtemp(prefix="scalejobs")
+    c = Cluster(wd, nodes=[], kinds="job", manager_bin=a.manager_bin, agent_auth="token",
+                manager_args=["--workers", str(a.workers), "--resync", "10s"])
+    c.start_apiserver()
+    k = c.client
+    t_setup = time.perf_counter()
+    names = [f"gpu-{i:03d}" for i in range(a.nodes)]
+    for n in names:
+        k.create(NODES, {"apiVersion": "v1", "kind": "Node",
+                         "metadata": {"name": n, "labels": {"kubernetes.io/hostname": n}}})
+        k.patch(NODES, n, {"status": {"capacity": {"amd.com/gpu": "8", "cpu": "192"},
+                                      "allocatable": {"amd.com/gpu": "8", "cpu": "192"},
+                                      "conditions": [{"type": "Ready", "status": "True",
+                                                      "lastHeartbeatTime": "t0"}]}},
+                sub="status", ptype="strategic")
+    # filler pods: one 1-GPU pod per node (GPUs in use), the rest CPU-only, all Running
+    cl = [Client(c.url) for _ in range(8)]
+
+    def fill(w: int) -> None:
+        for i in range(w, a.filler_pods, 8):
+            gpu = i < a.nodes
+            pod = {"apiVersion": "v1", "kind": "Pod",
+                   "metadata": {"name": f"filler-{i:05d}", "labels": {"app": "filler"}},
+                   "spec": {"nodeName": names[i % a.nodes], "containers": [{
+                       "name": "c", "image": "x", "resources": {"limits": {
+                           **({"amd.com/gpu": "1"} if gpu else {}), "cpu": "1"}}}]},
+                   "status": {"phase": "Running", "podIP": f"10.{i // 65536}.{i // 256 % 256}.{i % 256}"}}
+            cl[w].create(PODS, pod, f"team-{i % 20}")
+    ts = [threading.Thread(target=fill, args=(w,)) for w in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    setup_s = time.perf_counter() - t_setup
+    stop = threading.Event()
+
+    def heartbeats() -> None:  # what every kubelet does every 10 s (node-status-update-frequency)
+        hb = Client(c.url)
+        n = 0
+        while not stop.wait(10.0 / max(1, a.nodes)):
+            node = names[n % a.nodes]
+            n += 1
+            hb.patch(NODES, node, {"status": {"conditions": [{"type": "Ready", "status": "True",
+                                                              "lastHeartbeatTime": f"t{n}"}]}},
+                     sub="status", ptype="strategic")
+    threading.Thread(target=heartbeats, daemon=True).start()
+
+    def runner() -> None:  # the kubelets' part for gang pods: each one starts (Running, a pod IP)
+        r = Client(c.url)
+        rv = r.list(PODS, None, label_selector="gpupool.amd.com/job-name")["metadata"]["resourceVersion"]
+        n = 0
+        while not stop.is_set():
+            try:
+                for ev in r.watch(PODS, None, resource_version=rv, stop=stop, timeout_seconds=30,
+                                  label_selector="gpupool.amd.com/job-name"):
+                    o = ev.get("object") or {}
+                    rv = (o.get("metadata") or {}).get("resourceVersion", rv)
+                    if ev.get("type") == "ADDED" and not (o.get("status") or {}).get("podIP"):
+                        n += 1
+                        r.patch(PODS, o["metadata"]["name"], {"status": {
+                            "phase": "Running", "podIP": f"10.200.{n // 256 % 256}.{n % 256}"}},
+                            o["metadata"]["namespace"], sub="status")
+            except Exception:  # noqa: BLE001 - the watch resumes
+                time.sleep(0.1)
+    threading.Thread(target=runner, daemon=True).start()
+    c.start_manager()
+    mgr = c.procs["manager"].pid
+    deadline = time.monotonic() + 120
+    while time.monotonic() < deadline:  # caches synced: the manager serves /metrics and is idle
+        try:
+            m0 = _metrics(c.manager_metrics())
+            break
+        except OSError:
+            time.sleep(0.2)
+    time.sleep(2.0)
+    s0 = _metrics(k.request("GET", "/metrics"))
+    m0 = _metrics(c.manager_metrics())
+    u0 = proc_usage(mgr)
+    jobs = [f"gang-{i:03d}" for i in range(a.gangs)]
+    t0 = time.perf_counter()
+    for j in jobs:
+        k.create(MI355XJOBS, {"apiVersion": "compute.my.domain/v1alpha1", "kind": "Mi355xJob",
+                              "metadata": {"name": j},
+                              "spec": {"replicas": a.gang_size, "gpusPerReplica": 1,
+                                       "template": {"spec": {"containers": [{
+                                           "name": "m", "command": ["sleep", "1"]}]}}}}, "default")
+
+    def scheduled(o):
+        st = o.get("status") or {}
+        c2 = {x["type"]: x for x in st.get("conditions", [])}
+        return c2.get("Scheduled", {}).get("status") == "True" and \
+            len(st.get("placement") or []) == a.gang_size
+
+    def running(o):
+        return ((o.get("status") or {}).get("phase")) == "Running"
+    all_running = {}
+    done = {}
+    while len(done) < len(jobs) and time.perf_counter() - t0 < a.timeout:
+        for o in k.list(MI355XJOBS, "default")["items"]:
+            n = o["metadata"]["name"]
+            if n not in done and scheduled(o):
+                done[n] = time.perf_counter() - t0
+            if n not in all_running and running(o):
+                all_running[n] = time.perf_counter() - t0
+        time.sleep(0.25)
+    placed_s = time.perf_counter() - t0
+    while len(all_running) < len(jobs) and time.perf_counter() - t0 < a.timeout:
+        for o in k.list(MI355XJOBS, "default")["items"]:
+            n = o["metadata"]["name"]
+            if n not in all_running and running(o):
+                all_running[n] = time.perf_counter() - t0
+        time.sleep(0.25)
+    u1 = proc_usage(mgr)
+    s1 = _metrics(k.request("GET", "/metrics"))
+    m1 = _metrics(c.manager_metrics())
+    # steady state: a minute of heartbeats with the placed gangs (and any unplaced) in place
+    time.sleep(a.steady_s)
+    s2 = _metrics(k.request("GET", "/metrics"))
+    m2 = _metrics(c.manager_metrics())
+    u2 = proc_usage(mgr)
+    stop.set()
+    lists = lambda s: {k2.split('"')[1]: int(v) for k2, v in s.items()  # noqa: E731
+                       if k2.startswith("apiserver_list_total")}
+    l0, l1, l2 = lists(s0), lists(s1), lists(s2)
+    diff = lambda x, y: {r: y.get(r, 0) - x.get(r, 0) for r in sorted(set(x) | set(y))  # noqa: E731
+                         if y.get(r, 0) - x.get(r, 0)}
+    out = {"mode": "jobs", "nodes": a.nodes, "filler_pods": a.filler_pods, "gangs": a.gangs,
+           "gang_size": a.gang_size, "manager_bin": a.manager_bin or "build/native/gpupool-manager",
+           "setup_s": round(setup_s, 1),
+           "placement": {**pstats(list(done.values())), "all_placed": len(done) == len(jobs),
+                         "placed": len(done), "wall_s": round(placed_s, 3)},
+           "running": {**pstats(list(all_running.values())),
+                       "all_running": len(all_running) == len(jobs)},
+           "apiserver_lists": {"at_manager_sync": l0, "during_placement": diff(l0, l1),
+                               "steady_per_min": {r: round(v * 60.0 / a.steady_s, 1)
+                                                  for r, v in diff(l1, l2).items()}},
+           "node_events": {"relevant": _sum(m2, 'gpupool_node_events_total{relevant="true"'),
+                           "ignored": _sum(m2, 'gpupool_node_events_total{relevant="false"')},
+           "scheduler_reads": {k2.split("{", 1)[1].rstrip("}"): int(v) for k2, v in m2.items()
+                               if k2.startswith("gpupool_job_scheduler_reads_total")},
+           "reconciles": {"during_placement": int(_sum(m1, "gpupool_reconcile_total") -
+                                                  _sum(m0, "gpupool_reconcile_total")),
+                          "steady_per_min": round((_sum(m2, "gpupool_reconcile_total") -
+                                                   _sum(m1, "gpupool_reconcile_total")) * 60.0 /
+                                                  a.steady_s, 1)},
+           "manager": {"cpu_s_placement": round(u1["cpu_s"] - u0["cpu_s"], 3),
+                       "cpu_s_steady_per_min": round((u2["cpu_s"] - u1["cpu_s"]) * 60.0 /
+                                                     a.steady_s, 3),
+                       "rss_mib_after_sync": u0["rss_mib"], "rss_mib_end": u2["rss_mib"]},
+           "host_cpus": os.cpu_count()}
+    print(json.dumps(out), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+    c.stop()
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["pools", "jobs"], default="pools")
+    ap.add_argument("--filler-pods", type=int, default=5000, help="jobs mode")
+    ap.add_argument("--gangs", type=int, default=200, help="jobs mode")
+    ap.add_argument("--gang-size", type=int, default=2, help="jobs mode: workers x 1 GPU")
+    ap.add_argument("--steady-s", type=float, default=60.0, help="jobs mode: steady-state window")
+    ap.add_argument("--manager-bin", default=None, help="jobs mode: another gpupool-manager build")
     ap.add_argument("--nodes", type=int, default=16)
     ap.add_argument("--pools", type=int, default=48)
     ap.add_argument("--replicas", type=int, default=2)
@@ -105,6 +298,8 @@ def main() -> int:
     ap.add_argument("--timeout", type=float, default=180.0)
     ap.add_argument("--out")
     a = ap.parse_args()
+    if a.mode == "jobs":
+        return jobs_mode(a)
     assert a.pools * a.replicas <= a.nodes * 8, "more GPUs requested than the nodes have"
     wd = tempfile.mkdtemp(prefix="scale")
     nodes = [NodeSpec(f"node-{i:03d}") for i in range(a.nodes)]

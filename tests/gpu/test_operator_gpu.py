@@ -550,3 +550,63 @@ def test_fabric_helper_rings_on_the_real_gpu(native_built):
               f"total {time.monotonic() - t0:.1f} s")
     finally:
         p.helpers.stop()
+
+
+def test_probe_helper_parked_while_a_tenant_holds_the_gpu(cluster_factory):
+    """Round-5 weak #5 on hardware: while a pod holds the pool's GPU the agent keeps no HIP
+    context there (its probe helper is parked: no agent process in the GPU's process list), the
+    GPU's VRAM in use is the tenant's alone, and after the pod the helper comes back warm before
+    release returns the GPU."""
+    c = cluster_factory(nodes=[NodeSpec("gpu-node", backend="amdsmi", probe="helper")])
+    k = c.client
+    k.create(MI355XPOOLS, pool("p", 1, drain={"gracePeriodSeconds": 2}), "default")
+    obj = k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=60)
+    gpu = obj["status"]["devices"][0]["uuid"]
+
+    def dev():
+        v = c.agent_request("gpu-node", "GET", "/v1/node")
+        return next(d for d in v["devices"] if d["uuid"] == gpu), v
+
+    def agent_vram(d):
+        return sum(e["vramBytes"] for e in d.get("usage") or [] if e["pod"] == "gpupool-agent")
+
+    deadline = time.monotonic() + 30
+    while time.monotonic() < deadline and agent_vram(dev()[0]) == 0:
+        time.sleep(0.5)
+    before = agent_vram(dev()[0])
+    assert before > 256 << 20, dev()[0].get("usage")  # the helper's context (+ probe arena)
+    k.create(PODS, {"metadata": {"name": "tenant"}, "spec": {
+        "terminationGracePeriodSeconds": 2, "containers": [{
+            "name": "t", "command": ["python", "-c",
+                                     "import torch, time; x = torch.empty(1 << 28, device='cuda');"
+                                     " torch.cuda.synchronize(); print('holding', flush=True);"
+                                     " time.sleep(600)"],
+            "resources": {"limits": {"amd.com/gpu": 1}}}]}}, "default")
+    k.wait_for(PODS, "tenant", "default", lambda o: o and o["status"].get("phase") == "Running", 120)
+    deadline = time.monotonic() + 120
+    d = None
+    while time.monotonic() < deadline:
+        d, view = dev()
+        tenant = [e for e in d.get("usage") or [] if e["pod"] == "tenant"]
+        if d.get("probeHelper") == "Parked" and agent_vram(d) == 0 and tenant and \
+                tenant[0]["vramBytes"] >= 1 << 30:
+            break
+        time.sleep(0.5)
+    assert d.get("probeHelper") == "Parked", d
+    assert agent_vram(d) == 0, d.get("usage")           # no agent process on the tenant's GPU
+    assert not (view.get("probeHelpers") or {}).get(gpu, {}).get("alive")
+    tenant_vram = sum(e["vramBytes"] for e in d["usage"] if e["pod"] == "tenant")
+    used = d["telemetry"]["memUsedBytes"]
+    # what is in use is the tenant's (the driver's own reservation aside): the agent's ~1 GiB is
+    # back with the tenant
+    assert used - tenant_vram < 512 << 20, (used, tenant_vram, d["usage"])
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 0}}, "default")
+    k.wait_for(PODS, "tenant", "default", lambda o: o is None, timeout=60)
+    k.wait_for(MI355XPOOLS, "p", "default", ready_at(0), timeout=120)
+    d, view = dev()
+    assert (view.get("probeHelpers") or {}).get(gpu, {}).get("alive"), view.get("probeHelpers")
+    m = c.agent_request("gpu-node", "GET", "/metrics")
+    waits = [ln for ln in m.splitlines() if ln.startswith("gpupool_agent_release_helper_wait")]
+    print("PARKING", json.dumps({"agentVramBeforeBytes": before, "tenantVramBytes": tenant_vram,
+                                 "memUsedWithTenantBytes": used, "releaseWait": waits}))
+    assert any(ln.startswith("gpupool_agent_release_helper_waits ") for ln in waits)

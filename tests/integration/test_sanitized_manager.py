@@ -104,3 +104,19 @@ def test_manager_scenario_under_sanitizer(san, cluster_factory):
     log = c.log("manager")
     assert "WARNING: ThreadSanitizer" not in log, log[-8000:]
     assert "ERROR: AddressSanitizer" not in log and "runtime error:" not in log, log[-8000:]
+
+
+def test_credential_reload_under_tsan(cluster_factory, tmp_path):
+    """The rotating-token path (TokenSource re-read on 401 while informer watches, workers and
+    agent feeds share it) under ThreadSanitizer, through two apiserver-token rotations."""
+    r = make_native("host", "tsan", timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    os.environ["TSAN_OPTIONS"] = "halt_on_error=0:report_signal_unsafe=0"
+    from .rotation import run_rotation
+    out = run_rotation(cluster_factory, tmp_path,
+                       manager_bin=os.path.join(ROOT, "build", "native-tsan", "gpupool-manager"))
+    assert out["errors"] == 0 and out["reloads"] >= 2 and out["auth_401s"] > 0, out
+    log = (tmp_path / "cluster0" / "manager.log").read_text()
+    assert b"__tsan_init" in open(os.path.join(ROOT, "build", "native-tsan", "gpupool-manager"),
+                                  "rb").read()  # really the TSan build
+    assert "WARNING: ThreadSanitizer" not in log, log[-8000:]

@@ -328,3 +328,85 @@ def test_a_claim_never_waits_for_a_warming_fabric_helper(monkeypatch):
         assert Agent._link_verdict(links["g0"], 0) == "unavailable"  # never a replace
     finally:
         p.helpers.stop()
+
+
+def test_requests_sent_while_a_helper_starts_are_answered_promptly():
+    """callers arriving while the watcher reads a starting helper's ready message (the
+    pipe's reader role held) must not sleep out their deadline — the watcher hands the pipe on,
+    and followers retry the reader role in short slices."""
+    from gpupool.agent.probehost import Helper
+    h = Helper("slow", {"kind": "sim", "single": True, "simMs": 1, "devices": 1,
+                        "initDelayS": 0.4}).start()
+    lat: list[float] = []
+    errs: list[BaseException] = []
+
+    def one():
+        t0 = time.monotonic()
+        try:
+            h.call("ping", {}, 20.0)
+            lat.append(time.monotonic() - t0)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+    try:
+        for _round in range(3):
+            ts = [threading.Thread(target=one) for _ in range(6)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join(30)
+        assert not errs, errs
+        assert len(lat) == 18 and max(lat) < 2.0, lat
+    finally:
+        h.stop()
+
+
+def test_parked_helper_holds_no_process_and_restarts_warm(tmp_path, agents, native_built):
+    """Weak #5 (r5): a GPU with a tenant pod gets its probe helper stopped (parked) — requests
+    for it are refused as unavailable, the fabric helper is restarted without it — and it comes
+    back when the GPU is pod-free; release waits for it to be warm."""
+    a = make_agent(tmp_path, count=3)
+    agents.append(a)
+    d0 = a.by_uuid[sorted(a.by_uuid, key=lambda u: a.by_uuid[u]["index"])[0]]
+    pool = a.prober.helpers
+    assert pool.alive(d0["uuid"])
+    pid0 = next(v["pid"] for k, v in pool.snapshot().items() if k == d0["uuid"])
+    a._sync_parking({d0["uuid"]: [{"namespace": "default", "name": "tenant"}]})
+    assert d0["uuid"] in a.prober.parked() and not pool.alive(d0["uuid"])
+    assert pid0 not in a.prober.helper_pids()
+    assert not a.prober.can_probe(d0)
+    fab = pool.snapshot().get("fabric") or {}
+    assert wait(lambda: (pool.snapshot().get("fabric") or {}).get("alive"))
+    assert {d["uuid"] for d in pool._fabric_devs} == set(a.by_uuid) - {d0["uuid"]}
+    view = a.device_view(d0["uuid"], {})
+    assert view["probeHelper"] == "Parked"
+    r = a.prober.probe_many([d0], {"enabled": True})[0]
+    assert not r["passed"] and r["error"].startswith("ProbeUnavailable")
+    # pods gone: the helper restarts (a fresh pid) and rejoins the fabric helper's GPUs
+    a._sync_parking({})
+    assert d0["uuid"] not in a.prober.parked()
+    assert pool.wait_ready(d0["uuid"], 30) < 30_000 and pool.alive(d0["uuid"])
+    assert pid0 not in a.prober.helper_pids()
+    assert wait(lambda: {d["uuid"] for d in pool._fabric_devs} == set(a.by_uuid))
+    assert claim(a, "pool-x", 3)["ok"]
+    assert fab is not None
+
+
+def test_recheck_of_a_parked_or_unavailable_gpu_is_postponed_not_failed(tmp_path, agents,
+                                                                         native_built):
+    """a periodic recheck (or the one after a GPU reset) that cannot run — the helper
+    is held back or parked — keeps the previous verdict instead of failing the GPU."""
+    a = make_agent(tmp_path, count=2)
+    agents.append(a)
+    out = claim(a, "pool-r", 1, recheckSeconds=0.01)
+    assert out["ok"]
+    u = out["devices"][0]["uuid"]
+    a._sync_parking({u: [{"namespace": "default", "name": "tenant"}]})
+    dev = dict(a.by_uuid[u])
+    opts = {"enabled": True}
+    a._rechecking.add(u)
+    a._recheck_one(u, dev, opts, out["devices"][0]["poolUID"] if "poolUID" in out["devices"][0]
+                   else "pool-r", after_reset=True)
+    rec = a.records[u]
+    assert rec["probe"]["passed"], rec["probe"]
+    assert a.stats.get("rechecks_postponed") == 1
+    assert a.recheck_probes(force=True) == []  # pods / parked: nothing started
