@@ -225,6 +225,10 @@ class Mi355xJobReconciler : public PoolReconcilerBase {
   Outcome reconcile(const std::string& ns, const std::string& name) override;
   // Jobs still waiting for a gang placement (re-enqueued when capacity may have freed up).
   std::vector<std::pair<std::string, std::string>> pending() const;
+  // How to enqueue a job: a gang queued behind another is woken when that one is placed (or
+  // ends: wake_blocked_by), not on every queue or job event.
+  void set_waker(std::function<void(const std::string& ns, const std::string& name)> w) { waker_ = std::move(w); }
+  void wake_blocked_by(const std::string& ns, const std::string& name) { wake_blocked_by_(ns + "/" + name); }
 
   struct Slot {
     int index = 0;
@@ -266,6 +270,10 @@ class Mi355xJobReconciler : public PoolReconcilerBase {
   std::map<std::string, int64_t> pod_usage_(const std::string& resource);
   void on_status_written_(const Json& written) override;
 
+  void wake_blocked_by_(const std::string& key);
+  std::function<void(const std::string&, const std::string&)> waker_;
+  std::mutex blocked_mu_;
+  std::map<std::string, std::string> blocked_by_;  // "ns/job" queued behind -> "ns/job" ahead
   Informer& nodes_;
   PodIndex* pods_idx_;
   std::mutex sched_mu_;

@@ -92,6 +92,26 @@ CounterVec& sched_reads() {
 }
 }  // namespace
 
+void Mi355xJobReconciler::wake_blocked_by_(const std::string& key) {
+  std::vector<std::string> wake;
+  {
+    std::lock_guard<std::mutex> g(blocked_mu_);
+    for (auto it = blocked_by_.begin(); it != blocked_by_.end();) {
+      if (it->second == key) {
+        wake.push_back(it->first);
+        it = blocked_by_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  if (!waker_) return;
+  for (const auto& w : wake) {
+    const auto slash = w.find('/');
+    waker_(w.substr(0, slash), w.substr(slash + 1));
+  }
+}
+
 void Mi355xJobReconciler::on_status_written_(const Json& written) {
   if (!pods_idx_) return;
   std::lock_guard<std::mutex> g(written_mu_);
@@ -321,6 +341,7 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     if (spec.gpus_per_replica > 0)
       max_r = static_cast<int>(std::min<int64_t>(max_r, (cap - used) / spec.gpus_per_replica));
   }
+  Json blocker;
   for (const auto& j : jobs) {
     if (j.path("metadata.uid").as_string() == m.uid || !j.path("metadata.deletionTimestamp").as_string().empty()) continue;
     if (j.path("spec.queue").str_or("default") != spec.queue) continue;
@@ -332,12 +353,17 @@ std::vector<Mi355xJobReconciler::Slot> Mi355xJobReconciler::schedule_(const Obje
     int64_t jneed = std::min(jrep, std::max<int64_t>(1, jmin)) * j.path("spec.gpusPerReplica").as_int(1);
     // can never run (bigger than the cluster or than the queue's capability): must not block it
     if (jres == resource && (jneed > cluster_total || (cap >= 0 && jneed > cap))) continue;
-    if (key_of(j) < my_key) {
-      *reason = "QueuedBehind";
-      *why = "queue " + spec.queue + ": waiting behind " + j.path("metadata.namespace").as_string() + "/" +
-             j.path("metadata.name").as_string();
-      return {};
-    }
+    // the nearest job ahead in queue order is the one to wait for: once it is placed, nothing
+    // further ahead is still waiting (it could only be placed after them)
+    if (key_of(j) < my_key && (blocker.is_null() || key_of(blocker) < key_of(j))) blocker = j;
+  }
+  if (!blocker.is_null()) {
+    const std::string bkey = blocker.path("metadata.namespace").as_string() + "/" + blocker.path("metadata.name").as_string();
+    *reason = "QueuedBehind";
+    *why = "queue " + spec.queue + ": waiting behind " + bkey;
+    std::lock_guard<std::mutex> g(blocked_mu_);
+    blocked_by_[m.ns + "/" + m.name] = bkey;
+    return {};
   }
   // 2. free GPUs per candidate node = allocatable - live pod requests - other jobs' reservations
   std::map<std::string, int64_t> free;
@@ -812,6 +838,7 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
     // The reservation (status.placement) is written before any pod exists and while sched_mu_ is
     // held, so the next placement decision sees it.
     write_status_(obj, st);
+    wake_blocked_by_(m.ns + "/" + m.name);
     obj = client_.get(res_, m.ns, m.name);
     std::chrono::system_clock::time_point since;
     if (parse_rfc3339(since_s, &since))

@@ -738,18 +738,35 @@ int main(int argc, char** argv) {
         if (type != "RESYNC" && node_relevant) wake_pending();
       });
       // a gang that ends, is suspended or gives its placement back frees GPUs for waiting ones
-      jobs.add_handler([wake_pending](const std::string& type, const Json& j) {
+      jobs.add_handler([wake_pending, &jr](const std::string& type, const Json& j) {
         if (type == "RESYNC") return;
         const std::string ph = j.path("status.phase").str_or("Pending");
         if (type == "DELETED" || ph == "Succeeded" || ph == "Failed" || ph == "Suspended" ||
             (ph == "Restarting" && j.path("status.placement").size() == 0))
           wake_pending();
+        else if (j.path("status.placement").size() > 0)  // placed: those queued behind it go next
+          jr.wake_blocked_by(j.path("metadata.namespace").as_string(), j.path("metadata.name").as_string());
       });
-      // queue edits (created, opened, capability raised) can admit waiting jobs
-      queues.add_handler([&ctl, wake_pending](const std::string& type, const Json& q) {
-        ctl.enqueue("Mi355xQueue", "", q.path("metadata.name").as_string());
-        if (type != "RESYNC") wake_pending();
+      // queue edits (created, opened, capability raised) can admit waiting jobs — spec edits
+      // only: the queue's status is rewritten on every job change and admits nothing
+      auto queue_gen = std::make_shared<std::map<std::string, int64_t>>();
+      auto queue_gen_mu = std::make_shared<std::mutex>();
+      queues.add_handler([&ctl, wake_pending, queue_gen, queue_gen_mu](const std::string& type, const Json& q) {
+        const std::string name = q.path("metadata.name").as_string();
+        ctl.enqueue("Mi355xQueue", "", name);
+        if (type == "RESYNC") return;
+        const int64_t gen = q.path("metadata.generation").as_int(0);
+        bool changed;
+        {
+          std::lock_guard<std::mutex> g(*queue_gen_mu);
+          auto it = queue_gen->find(name);
+          changed = type != "MODIFIED" || it == queue_gen->end() || it->second != gen;
+          if (type == "DELETED") queue_gen->erase(name);
+          else (*queue_gen)[name] = gen;
+        }
+        if (changed) wake_pending();
       });
+      jr.set_waker([&ctl](const std::string& ns, const std::string& name) { ctl.enqueue("Mi355xJob", ns, name); });
       // pool changes (GPUs advertised or released) change capacity too
       mipools.add_handler([wake_pending](const std::string& type, const Json&) {
         if (type != "RESYNC") wake_pending();

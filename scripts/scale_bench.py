@@ -57,7 +57,7 @@ def proc_usage(pid: int) -> dict:
     return {"cpu_s": round(cpu, 3), "rss_mib": round(rss / 2**20, 1)}
 
 
-def wait_all(k, names: list[str], pred, t0: float, timeout: float) -> dict[str, float]:
+def wait_all(k, names: list[str], pred, t0: float, timeout: float, res=MI355XPOOLS) -> dict[str, float]:
     """Time at which each pool first satisfied ``pred``, from a watch stream (polling lists of
     every pool would load the apiserver-sim more than the operator does). A watch that ends early
     (the server closes it, or its resourceVersion is too old) is resumed from a fresh list."""
@@ -65,7 +65,7 @@ def wait_all(k, names: list[str], pred, t0: float, timeout: float) -> dict[str, 
     want = set(names)
     deadline = time.monotonic() + timeout
     while len(done) < len(want) and time.monotonic() < deadline:
-        lst = k.list(MI355XPOOLS, "default")
+        lst = k.list(res, "default")
         for o in lst["items"]:
             n = o["metadata"]["name"]
             if n in want and n not in done and pred(o):
@@ -76,7 +76,7 @@ def wait_all(k, names: list[str], pred, t0: float, timeout: float) -> dict[str, 
         timer = threading.Timer(max(0.1, deadline - time.monotonic()), stop.set)
         timer.start()
         try:
-            for ev in k.watch(MI355XPOOLS, "default",
+            for ev in k.watch(res, "default",
                               resource_version=lst["metadata"]["resourceVersion"],
                               timeout_seconds=int(deadline - time.monotonic()) + 1, stop=stop):
                 o = ev.get("object") or {}
@@ -221,22 +221,20 @@ def jobs_mode(a) -> int:
     def running(o):
         return ((o.get("status") or {}).get("phase")) == "Running"
     all_running = {}
-    done = {}
-    while len(done) < len(jobs) and time.perf_counter() - t0 < a.timeout:
-        for o in k.list(MI355XJOBS, "default")["items"]:
-            n = o["metadata"]["name"]
-            if n not in done and scheduled(o):
-                done[n] = time.perf_counter() - t0
-            if n not in all_running and running(o):
-                all_running[n] = time.perf_counter() - t0
-        time.sleep(0.25)
-    placed_s = time.perf_counter() - t0
-    while len(all_running) < len(jobs) and time.perf_counter() - t0 < a.timeout:
-        for o in k.list(MI355XJOBS, "default")["items"]:
-            n = o["metadata"]["name"]
-            if n not in all_running and running(o):
-                all_running[n] = time.perf_counter() - t0
-        time.sleep(0.25)
+    # followed through one watch (a LIST per poll would load the apiserver like the operator)
+    got: dict[str, dict[str, float]] = {"placed": {}, "running": {}}
+
+    def both(o):
+        n = o["metadata"]["name"]
+        now = time.perf_counter() - t0
+        if scheduled(o):
+            got["placed"].setdefault(n, now)
+        if running(o):
+            got["running"].setdefault(n, now)
+        return n in got["running"]
+    wait_all(k, jobs, both, t0, a.timeout, res=MI355XJOBS)
+    done, all_running = got["placed"], got["running"]
+    placed_s = max(done.values()) if done else a.timeout
     u1 = proc_usage(mgr)
     s1 = _metrics(k.request("GET", "/metrics"))
     m1 = _metrics(c.manager_metrics())
