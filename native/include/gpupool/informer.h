@@ -56,6 +56,7 @@ class Informer {
   uint64_t events() const { return events_.load(); }  // watch events received
 
   static std::string key_of(const Json& obj);  // "ns/name" or "name"
+  static constexpr int64_t kListPage = 500;
 
  private:
   void run_();

@@ -75,7 +75,7 @@ class KubeClient {
   Json get(const ResourceRef& r, const std::string& ns, const std::string& name,
            const std::string& sub = "");
   Json list(const ResourceRef& r, const std::string& ns = "", const std::string& label_selector = "",
-            const std::string& field_selector = "");
+            const std::string& field_selector = "", int64_t limit = 0, const std::string& cont = "");
   Json create(const ResourceRef& r, const std::string& ns, const Json& obj);
   Json update(const ResourceRef& r, const std::string& ns, const Json& obj,
               const std::string& sub = "");

@@ -82,13 +82,20 @@ void Informer::dispatch_(const std::string& type, const Json& obj) {
 }
 
 void Informer::list_() {
-  Json lst = client_.list(res_, ns_, opts_.label_selector, opts_.field_selector);
+  // in pages (client-go's 500): a cluster's worth of pods is never one response held whole in
+  // memory — each page is filtered and projected, then dropped
   relists_++;
   std::map<std::string, Json> fresh;
-  for (const auto& item : lst["items"].elements()) {
-    if (opts_.filter && !opts_.filter(item)) continue;
-    fresh[key_of(item)] = opts_.transform ? opts_.transform(item) : item;
-  }
+  std::string cont, list_rv;
+  do {
+    Json lst = client_.list(res_, ns_, opts_.label_selector, opts_.field_selector, kListPage, cont);
+    if (list_rv.empty()) list_rv = lst.path("metadata.resourceVersion").as_string();
+    for (const auto& item : lst["items"].elements()) {
+      if (opts_.filter && !opts_.filter(item)) continue;
+      fresh[key_of(item)] = opts_.transform ? opts_.transform(item) : item;
+    }
+    cont = lst.path("metadata.continue").as_string();
+  } while (!cont.empty() && !stop_);
   std::vector<std::pair<std::string, Json>> events;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -103,7 +110,7 @@ void Informer::list_() {
       }
     }
     cache_ = std::move(fresh);
-    rv_ = lst.path("metadata.resourceVersion").as_string();
+    rv_ = list_rv;
   }
   for (auto& e : events) dispatch_(e.first, e.second);
   if (!synced_.exchange(true)) {

@@ -154,11 +154,13 @@ Json KubeClient::get(const ResourceRef& r, const std::string& ns, const std::str
 }
 
 Json KubeClient::list(const ResourceRef& r, const std::string& ns, const std::string& ls,
-                      const std::string& fs) {
+                      const std::string& fs, int64_t limit, const std::string& cont) {
   std::string p = r.path(ns);
   std::string q;
   if (!ls.empty()) q += "labelSelector=" + url_encode(ls);
   if (!fs.empty()) q += (q.empty() ? "" : "&") + std::string("fieldSelector=") + url_encode(fs);
+  if (limit > 0) q += (q.empty() ? "" : "&") + std::string("limit=") + std::to_string(limit);
+  if (!cont.empty()) q += (q.empty() ? "" : "&") + std::string("continue=") + url_encode(cont);
   if (!q.empty()) p += "?" + q;
   return call_("GET", p, "");
 }

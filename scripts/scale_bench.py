@@ -192,13 +192,9 @@ def jobs_mode(a) -> int:
     threading.Thread(target=runner, daemon=True).start()
     c.start_manager()
     mgr = c.procs["manager"].pid
-    deadline = time.monotonic() + 120
-    while time.monotonic() < deadline:  # caches synced: the manager serves /metrics and is idle
-        try:
-            m0 = _metrics(c.manager_metrics())
-            break
-        except OSError:
-            time.sleep(0.2)
+    deadline = time.monotonic() + 300
+    while time.monotonic() < deadline and "controllers running" not in c.log("manager"):
+        time.sleep(0.2)  # every informer cache synced (the manager starts its workers then)
     time.sleep(2.0)
     s0 = _metrics(k.request("GET", "/metrics"))
     m0 = _metrics(c.manager_metrics())

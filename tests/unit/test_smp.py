@@ -3,6 +3,9 @@ patchMergeKey for the built-in kinds, the patch directives, and the apiserver's 
 (strategic merge patch on a custom resource, unknown patch media types)."""
 from __future__ import annotations
 
+import threading
+import time
+
 import pytest
 
 from gpupool.apiserver_sim.smp import PatchError, strategic_merge, two_way
@@ -128,3 +131,51 @@ def test_store_and_http_media_types():
     with pytest.raises(KubeError) as ei:
         c.request("PATCH", PODS.path("default", "x"), {}, ctype="application/yaml")
     assert ei.value.code == 415
+
+
+def test_paged_list_and_filtered_watch_semantics():
+    """LIST pages (continue tokens carry the first page's resourceVersion and the last key) and
+    a label-selected watch turning a write that leaves / enters the selection into DELETED /
+    ADDED, as the apiserver's watch cache does (the manager's filtered informers rely on both)."""
+    sim = SimThread()
+    c = Client(sim.url)
+    for i in range(7):
+        c.create(PODS, {"apiVersion": "v1", "kind": "Pod",
+                        "metadata": {"name": f"p{i}", "labels": {"gpu": "yes" if i % 2 else "no"}},
+                        "spec": {"containers": [{"name": "c"}]}}, "pg")
+    seen, cont, rvs = [], None, set()
+    while True:
+        q = {"limit": 3, **({"continue": cont} if cont else {})}
+        page = c.request("GET", PODS.path("pg"), query=q)
+        seen += [o["metadata"]["name"] for o in page["items"]]
+        rvs.add(page["metadata"]["resourceVersion"])
+        c.create(PODS, {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"late{len(seen)}"},
+                        "spec": {"containers": [{"name": "c"}]}}, "other")  # writes between pages
+        cont = page["metadata"].get("continue")
+        if not cont:
+            break
+    assert seen == sorted(f"p{i}" for i in range(7)) and len(rvs) == 1
+    rv = c.list(PODS, "pg")["metadata"]["resourceVersion"]
+    stop, evs = threading.Event(), []
+
+    def watch():
+        try:
+            for ev in Client(sim.url).watch(PODS, "pg", resource_version=rv,
+                                            label_selector="gpu=yes", stop=stop,
+                                            timeout_seconds=10):
+                if ev["type"] != "BOOKMARK":
+                    evs.append((ev["type"], ev["object"]["metadata"]["name"]))
+        except Exception:  # noqa: BLE001 — the stop shut the socket down mid-read
+            pass
+    t = threading.Thread(target=watch, daemon=True)
+    t.start()
+    time.sleep(0.3)
+    c.patch(PODS, "p1", {"metadata": {"labels": {"gpu": "no"}}}, "pg")    # leaves
+    c.patch(PODS, "p2", {"metadata": {"labels": {"gpu": "yes"}}}, "pg")   # enters
+    c.patch(PODS, "p3", {"metadata": {"labels": {"x": "1"}}}, "pg")       # stays in
+    c.patch(PODS, "p4", {"metadata": {"labels": {"x": "1"}}}, "pg")       # stays out
+    deadline = time.monotonic() + 5
+    while len(evs) < 3 and time.monotonic() < deadline:
+        time.sleep(0.05)
+    stop.set()
+    assert evs == [("DELETED", "p1"), ("ADDED", "p2"), ("MODIFIED", "p3")], evs
