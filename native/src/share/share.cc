@@ -668,11 +668,32 @@ hsa_status_t w_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t
   return r;
 }
 
-const CuMask* queue_mask(State& s, const hsa_queue_t* q) {
+// The mask a queue got at creation. A queue the map does not hold (created before the library
+// was loaded, or beyond kQueueMap live queues): with per-GPU masks the union is NOT a safe stand-in
+// — it overlaps the sibling tenants' slots on every GPU — so *unknown is set and the caller keeps
+// whatever the queue has; with one pod-wide mask that mask is the queue's.
+const CuMask* queue_mask(State& s, const hsa_queue_t* q, bool* unknown) {
   Lock g(s);
+  *unknown = false;
   for (int i = 0; i < kQueueMap; ++i)
     if (s.qmap[i].q == q) return s.qmap[i].m;
+  if (s.n_gpu_masks) {
+    *unknown = true;
+    return nullptr;
+  }
   return s.mask.words ? &s.mask : nullptr;
+}
+
+// Queues go away: their map entries are freed, so a process that creates and destroys queues all
+// its life (a stream per request) never runs out of entries.
+hsa_status_t w_queue_destroy(hsa_queue_t* queue) {
+  State& s = st();
+  {
+    Lock g(s);
+    for (int i = 0; i < kQueueMap; ++i)
+      if (s.qmap[i].q == queue) s.qmap[i] = QueueMask{};
+  }
+  return s.real_core.hsa_queue_destroy_fn(queue);
 }
 
 // Does ``m`` leave at least one CU on every XCD? CU-mask bit b lands on XCD b % xcds (ROCr
@@ -692,7 +713,12 @@ bool covers_every_xcd(const State& s, const uint32_t* m, uint32_t words) {
 hsa_status_t w_queue_cu_set_mask(const hsa_queue_t* queue, uint32_t bits, const uint32_t* mask) {
   // the application's own mask (hipExtStreamCreateWithCUMask) can only narrow the slot's
   State& s = st();
-  const CuMask* cm = queue_mask(s, queue);
+  bool unknown = false;
+  const CuMask* cm = queue_mask(s, queue, &unknown);
+  if (unknown) {  // not ours to widen or narrow blind: the queue keeps its creation mask
+    count(&s.narrowings_refused);
+    return HSA_STATUS_SUCCESS;
+  }
   if (!cm) return s.real_amd.hsa_amd_queue_cu_set_mask_fn(queue, bits, mask);
   uint32_t m[kMaskWords];
   bool any = false;
@@ -745,6 +771,7 @@ __attribute__((visibility("default"))) bool OnLoad(HsaApiTable* table, uint64_t 
   }
   if (s.mask.words || s.n_gpu_masks) {
     table->core_->hsa_queue_create_fn = w_queue_create;
+    table->core_->hsa_queue_destroy_fn = w_queue_destroy;
     table->amd_ext_->hsa_amd_queue_cu_set_mask_fn = w_queue_cu_set_mask;
   }
   if (s.debug)

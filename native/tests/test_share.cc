@@ -85,6 +85,11 @@ hsa_status_t f_queue_create(hsa_agent_t, uint32_t, hsa_queue_type32_t, void (*)(
   *q = &g_queue;
   return HSA_STATUS_SUCCESS;
 }
+int g_destroyed = 0;
+hsa_status_t f_queue_destroy(hsa_queue_t*) {
+  ++g_destroyed;
+  return HSA_STATUS_SUCCESS;
+}
 hsa_status_t f_cu_set_mask(const hsa_queue_t*, uint32_t bits, const uint32_t* mask) {
   g_last_bits = bits;
   g_last_mask.assign(mask, mask + bits / 32);
@@ -107,6 +112,7 @@ struct Fake {
     core.hsa_iterate_agents_fn = f_iterate_agents;
     core.hsa_agent_get_info_fn = f_agent_get_info;
     core.hsa_queue_create_fn = f_queue_create;
+    core.hsa_queue_destroy_fn = f_queue_destroy;
     amd.hsa_amd_agent_iterate_memory_pools_fn = f_iterate_pools;
     amd.hsa_amd_memory_pool_get_info_fn = f_pool_get_info;
     amd.hsa_amd_memory_pool_allocate_fn = f_allocate;
@@ -466,5 +472,51 @@ TEST(share_lib_cu_masks_per_gpu_by_uuid) {
   g_gpus = {kGpu};
   unlink(copy.c_str());
   unsetenv("GPUPOOL_CU_MASKS");
+  unsetenv("GPUPOOL_CU_XCDS");
+}
+
+// queue-map entries are freed on hsa_queue_destroy (a process creating and destroying
+// queues for its whole life keeps its per-queue masks), and a queue the map does not know never
+// gets the pod-wide union under per-GPU masks (it would overlap sibling tenants).
+TEST(share_lib_queue_map_recycles_and_never_widens_unknown_queues) {
+  setenv("GPUPOOL_CU_MASKS", "GPU-aaaa000000000001=0-63", 1);
+  setenv("GPUPOOL_CU_MASK", "0-127", 1);
+  setenv("GPUPOOL_CU_XCDS", "8", 1);
+  std::string copy = "/tmp/libgpupool_share-qmap-" + std::to_string(getpid()) + ".so";
+  void* lib = load_copy(copy);
+  EXPECT_TRUE(lib != nullptr);
+  auto on_load = reinterpret_cast<bool (*)(HsaApiTable*, uint64_t, uint64_t, const char* const*)>(dlsym(lib, "OnLoad"));
+  static hsa_queue_t pool_q[600];
+  static int next_q = 0;
+  auto make = [](hsa_agent_t, uint32_t, hsa_queue_type32_t, void (*)(hsa_status_t, hsa_queue_t*, void*), void*,
+                 uint32_t, uint32_t, hsa_queue_t** out) {
+    *out = &pool_q[next_q++ % 600];
+    return HSA_STATUS_SUCCESS;
+  };
+  Fake f;
+  f.core.hsa_queue_create_fn = make;
+  EXPECT_TRUE(on_load(&f.table, 0, 0, nullptr));
+  const uint32_t app[4] = {0x0000FFFFu, 0u, 0u, 0u};  // narrows to CUs 0-15 (2 per XCD)
+  // 600 create/destroy cycles, far past the 256-entry map: every queue still narrows within its
+  // own slot's mask (0-63)
+  for (int i = 0; i < 600; ++i) {
+    hsa_queue_t* q = nullptr;
+    EXPECT_EQ(f.core.hsa_queue_create_fn(hsa_agent_t{kGpu}, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &q),
+              HSA_STATUS_SUCCESS);
+    g_last_mask.clear();
+    f.amd.hsa_amd_queue_cu_set_mask_fn(q, 128, app);
+    EXPECT_TRUE(g_last_mask == (std::vector<uint32_t>{0x0000FFFFu, 0u}));
+    const int before = g_destroyed;
+    f.core.hsa_queue_destroy_fn(q);
+    EXPECT_EQ(g_destroyed, before + 1);
+  }
+  // a queue created outside the library's view: the narrowing is refused, nothing is widened
+  static hsa_queue_t stranger;
+  const int sets = g_masks_set;
+  EXPECT_EQ(f.amd.hsa_amd_queue_cu_set_mask_fn(&stranger, 128, app), HSA_STATUS_SUCCESS);
+  EXPECT_EQ(g_masks_set, sets);
+  unlink(copy.c_str());
+  unsetenv("GPUPOOL_CU_MASKS");
+  unsetenv("GPUPOOL_CU_MASK");
   unsetenv("GPUPOOL_CU_XCDS");
 }
