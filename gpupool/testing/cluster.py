@@ -290,11 +290,12 @@ class Cluster:
 
     AGENT_NS = "gpupool-system"
 
-    def publish_agent_pod(self, node: str, ip: str | None = None) -> None:
+    def publish_agent_pod(self, node: str, ip: str | None = None, ready: bool = True,
+                          name: str | None = None) -> None:
         """The agent's Pod as the DaemonSet controller + kubelet would show it: bound to the node,
         Running, with the pod IP the CNI gave it (a mirror pod: the fake kubelet does not run it)."""
         from ..kube import PODS, KubeError
-        name = f"gpupool-agent-{node}"
+        name = name or f"gpupool-agent-{node}"
         pod = {"apiVersion": "v1", "kind": "Pod",
                "metadata": {"name": name, "namespace": self.AGENT_NS,
                             "labels": {"app.kubernetes.io/name": "gpupool-agent"},
@@ -305,9 +306,10 @@ class Cluster:
         except KubeError as e:
             if e.code != 409:
                 raise
-        self.client.patch(PODS, name, {"status": {"phase": "Running",
-                                                  "podIP": ip or self.agent_ips[node]}},
-                          self.AGENT_NS, sub="status")
+        self.client.patch(PODS, name, {"status": {
+            "phase": "Running", "podIP": ip or self.agent_ips[node],
+            "conditions": [{"type": "Ready", "status": "True" if ready else "False"}]}},
+            self.AGENT_NS, sub="status")
 
     def start_manager(self) -> None:
         pf = os.path.join(self.workdir, "manager.port")

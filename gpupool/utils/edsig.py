@@ -325,7 +325,8 @@ class Verifier:
                 return self._reject("Replay")
             self._nonces[h["nonce"]] = ts + self.skew_ms
             if len(self._nonces) > 4096:
-                self._nonces = {n: e for n, e in self._nonces.items() if e > now}
+                # keep a nonce while its timestamp still passes the skew check (now <= ts+skew)
+                self._nonces = {n: e for n, e in self._nonces.items() if e >= now}
         return None
 
     def check_body(self, headers: dict, body: bytes) -> str | None:

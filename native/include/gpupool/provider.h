@@ -288,8 +288,13 @@ class RocmProvider : public DeviceProvider {
   };
   std::mutex facts_mu_;
   std::map<std::string, NodeFacts> facts_;
-  // pod discovery: node -> (agent pod "ns/name" -> pod IP) of Running, undeleted agent pods
-  std::map<std::string, std::map<std::string, std::string>> agent_pods_;
+  // pod discovery: node -> (agent pod "ns/name" -> its address) of Running, undeleted agent pods
+  struct AgentPod {
+    std::string ip;
+    bool ready = false;
+    std::string created;  // RFC 3339: orders as a string
+  };
+  std::map<std::string, std::map<std::string, AgentPod>> agent_pods_;
   void note_node_(const std::string& type, const Json& obj);
   void note_agent_pod_(const std::string& type, const Json& pod);
   void derive_endpoint_(const std::string& node, NodeFacts& f);  // caller holds facts_mu_

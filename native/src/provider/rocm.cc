@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <fstream>
 #include <thread>
+#include <tuple>
 
 namespace gpupool {
 
@@ -148,7 +149,12 @@ void RocmProvider::note_agent_pod_(const std::string& type, const Json& pod) {
     it->second.erase(key);
     it = it->second.empty() ? agent_pods_.erase(it) : std::next(it);
   }
-  if (live && !node.empty()) agent_pods_[node][key] = ip;
+  if (live && !node.empty()) {
+    bool ready = false;
+    for (const auto& c : pod.path("status.conditions").elements())
+      if (c["type"].str_or("") == "Ready") ready = c["status"].str_or("") == "True";
+    agent_pods_[node][key] = AgentPod{ip, ready, pod.path("metadata.creationTimestamp").str_or("")};
+  }
   if (!node.empty()) {
     auto f = facts_.find(node);
     if (f != facts_.end()) derive_endpoint_(node, f->second);
@@ -165,7 +171,13 @@ void RocmProvider::derive_endpoint_(const std::string& node, NodeFacts& f) {
     f.endpoint.clear();  // no running agent pod on the node: nothing to call
     return;
   }
-  const std::string& ip = it->second.begin()->second;  // a DaemonSet runs one per node
+  // a DaemonSet runs one per node, but a surge rollout briefly runs two: the Ready one, then the
+  // newer one (the old pod is about to go)
+  const AgentPod* best = nullptr;
+  for (const auto& kv : it->second)
+    if (!best || std::tie(kv.second.ready, kv.second.created) > std::tie(best->ready, best->created))
+      best = &kv.second;
+  const std::string& ip = best->ip;
   const std::string host = ip.find(':') != std::string::npos ? "[" + ip + "]" : ip;
   f.endpoint = access_.scheme + "://" + host + ":" + std::to_string(access_.port);
   if (!f.annotation.empty() && f.annotation != f.endpoint) {

@@ -82,6 +82,9 @@ def test_pod_discovery_ignores_a_redirected_annotation(cluster_factory):
     try:
         k.patch(NODES, "node-b", {"metadata": {"annotations": {
             "gpupool.amd.com/agent-endpoint": rogue.url}}})
+        # a surge rollout's second agent pod on node B, newer but not Ready yet, at another
+        # address: the manager stays with the Ready one (else B's claims would fail to connect)
+        c.publish_agent_pod("node-b", ip="127.0.0.99", ready=False, name="gpupool-agent-4x7kq")  # sorts first
         # make the manager talk to node B's agent: scale up and down, then a resync
         k.patch(MI355XPOOLS, "pb", {"spec": {"replicas": 3}}, "default")
         wait_ready(k, "pb", 3, timeout=60)
