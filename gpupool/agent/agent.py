@@ -480,6 +480,7 @@ class Agent(HealthMixin, AccountingMixin, PodViewMixin, ClaimsMixin, XgmiMixin,
             from ..kube import Client
             self._api = Client.connect(self.cfg.apiserver, self.cfg.token or None,
                                        token_file=self.cfg.token_file or None)
+            self._api.user_agent = "gpupool-agent/0.1"
         return self._api
 
     def register_node(self) -> None:

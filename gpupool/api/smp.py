@@ -210,3 +210,58 @@ def _diff(a: dict, b: dict, keys: dict, path: tuple) -> dict:
         else:
             out[k] = v
     return out
+
+
+def three_way(original: dict | None, modified: dict, current: dict, kind: str | None) -> dict:
+    """``kubectl apply``'s client-side patch: what changed from ``current`` to ``modified``
+    (additions and changes), plus deletions of what the last apply set (``original``, the
+    last-applied-configuration) and this one no longer does. Fields neither apply set — written by
+    controllers, other users, defaulting — are left alone. ``kind=None``: a JSON merge patch (a
+    custom resource: lists are atomic); else a strategic merge patch with ``kind``'s list keys."""
+    keys = {} if kind is None else MERGE_KEYS.get(kind, _META)
+    return _three(original or {}, modified, current or {}, keys, (), kind is not None)
+
+
+def _three(orig: dict, mod: dict, cur: dict, keys: dict, path: tuple, strategic: bool) -> dict:
+    out: dict = {}
+    for k in orig:
+        if k not in mod and k in cur:
+            out[k] = None
+    for k, v in mod.items():
+        sub = path + (k,)
+        c, o = cur.get(k), orig.get(k)
+        if isinstance(v, dict) and isinstance(c, dict):
+            d = _three(o if isinstance(o, dict) else {}, v, c, keys, sub, strategic)
+            if d:
+                out[k] = d
+        elif strategic and isinstance(v, list) and isinstance(c, list) and sub in keys:
+            mk = keys[sub]
+            if mk == "":  # a set: add what is missing, delete what the last apply had
+                add = [x for x in v if x not in c]
+                gone = [x for x in (o if isinstance(o, list) else []) if x not in v and x in c]
+                if add:
+                    out[k] = add
+                if gone:
+                    out[f"$deleteFromPrimitiveList/{k}"] = gone
+                continue
+            curs = {x.get(mk): x for x in c if isinstance(x, dict)}
+            origs = {x.get(mk): x for x in (o if isinstance(o, list) else []) if isinstance(x, dict)}
+            items, ids = [], set()
+            for x in v:
+                if not isinstance(x, dict):
+                    continue
+                ident = x.get(mk)
+                ids.add(ident)
+                if ident not in curs:
+                    items.append(x)
+                else:
+                    d = _three(origs.get(ident) or {}, x, curs[ident], keys, sub, strategic)
+                    if d:
+                        items.append({mk: ident, **d})
+            items += [{mk: i, "$patch": "delete"} for i in origs if i not in ids and i in curs]
+            if items:
+                out[k] = items
+                out[f"$setElementOrder/{k}"] = [{mk: x.get(mk)} for x in v if isinstance(x, dict)]
+        elif c != v:
+            out[k] = v
+    return out

@@ -21,6 +21,7 @@ import re
 import time
 from typing import Any
 
+import yaml
 from aiohttp import web
 
 from .store import ApiError, ResourceType, Store, WatchEvent, get_path, parse_field_selector, \
@@ -404,13 +405,15 @@ class ApiServerSim:
             if m == "GET":
                 return web.json_response(self.store.get_scale(rt, ns, name))
             if m == "PUT":
-                return web.json_response(self.store.update_scale(rt, ns, name, await request.json()))
+                return web.json_response(self.store.update_scale(rt, ns, name, await request.json(),
+                                                                 self._manager(request)))
             if m == "PATCH":
                 body = await request.json()
                 cur = self.store.get_scale(rt, ns, name)
                 cur["spec"]["replicas"] = body.get("spec", {}).get("replicas", cur["spec"]["replicas"])
                 cur["metadata"].pop("resourceVersion", None)
-                return web.json_response(self.store.update_scale(rt, ns, name, cur))
+                return web.json_response(self.store.update_scale(rt, ns, name, cur,
+                                                                 self._manager(request)))
             raise ApiError(405, "MethodNotAllowed", f"{m} not allowed on scale")
         if sub == "eviction":
             if rt.kind != "Pod" or m != "POST":
@@ -423,7 +426,17 @@ class ApiServerSim:
 
     PATCH_TYPES = {"application/json-patch+json": "json",
                    "application/merge-patch+json": "merge",
-                   "application/strategic-merge-patch+json": "strategic"}
+                   "application/strategic-merge-patch+json": "strategic",
+                   "application/apply-patch+yaml": "apply"}
+
+    @staticmethod
+    def _manager(request) -> str:
+        """The field manager of a write: ``fieldManager``, else the User-Agent's product."""
+        m = request.query.get("fieldManager")
+        if m:
+            return m
+        ua = request.headers.get("User-Agent", "").split("/", 1)[0].strip()
+        return ua or "unknown"
 
     @classmethod
     def _patch_type(cls, ctype: str) -> str:
@@ -464,20 +477,33 @@ class ApiServerSim:
             return web.json_response(obj)
         if m == "PUT":
             body = await request.json()
+            mgr = self._manager(request)
             if rt.kind == "Node":
                 self._admit_node_write(request, name, self.store.update(
-                    rt, ns, name, body, sub, True))
+                    rt, ns, name, body, sub, True, manager=mgr))
             # the decoded body is this request's own; the reply only serialises the result
             return web.json_response(self.store.update(rt, ns, name, body, sub, dry,
-                                                       owned=True, copy_out=False))
+                                                       owned=True, copy_out=False, manager=mgr))
         if m == "PATCH":
             ptype = self._patch_type(request.headers.get("Content-Type", ""))
-            body = await request.json()
+            if ptype == "apply":  # YAML (JSON is YAML too)
+                try:
+                    body = yaml.safe_load(await request.text())
+                except yaml.YAMLError as e:
+                    raise ApiError(400, "BadRequest", f"invalid apply patch: {e}") from e
+                mgr = request.query.get("fieldManager", "")
+            else:
+                body = await request.json()
+                mgr = self._manager(request)
+            force = request.query.get("force") in ("true", "1")
             if rt.kind == "Node":
                 self._admit_node_write(request, name, self.store.patch(
-                    rt, ns, name, body, ptype, sub, True))
-            return web.json_response(self.store.patch(rt, ns, name, body, ptype,
-                                                      sub, dry, copy_out=False))
+                    rt, ns, name, body, ptype, sub, True, manager=mgr, force=force))
+            created = ptype == "apply" and \
+                ((ns or "") if rt.namespaced else "", name) not in self.store.objects[rt.key]
+            out = self.store.patch(rt, ns, name, body, ptype, sub, dry, copy_out=False,
+                                   manager=mgr, force=force)
+            return web.json_response(out, status=201 if created else 200)
         if m == "DELETE" and not sub:
             body = {}
             if request.can_read_body:

@@ -28,7 +28,8 @@ from dataclasses import dataclass, field
 from typing import Any, Callable
 
 from ..api import openapi
-from .smp import PatchError, strategic_merge
+from . import ssa
+from ..api.smp import PatchError, strategic_merge
 
 
 def clone(o):
@@ -369,6 +370,7 @@ class Store:
         self.log: collections.deque[WatchEvent] = collections.deque(maxlen=window)
         self.listeners: list[Callable[[WatchEvent], None]] = []
         self._vschema: dict[tuple[str, str], tuple[dict, dict]] = {}  # CRD -> (schema, w/o metadata)
+        self._list_keys: dict[tuple[str, str], tuple[Any, dict]] = {}  # type -> (schema, keys)
         for rt in BUILTINS:
             self.register(rt)
         self._ensure_namespace("default")
@@ -619,7 +621,8 @@ class Store:
                 "items": items}
 
     # --------------------------------------------------------- writes
-    def create(self, rt: ResourceType, ns: str | None, obj: dict, dry_run: bool = False) -> dict:
+    def create(self, rt: ResourceType, ns: str | None, obj: dict, dry_run: bool = False,
+               managed: bool = False) -> dict:
         obj = clone(obj)
         ns = self._check_ns(rt, ns or obj.get("metadata", {}).get("namespace"))
         md = obj.setdefault("metadata", {})
@@ -644,6 +647,8 @@ class Store:
             raise ApiError(409, "AlreadyExists", f'{rt.plural}{"." + rt.group if rt.group else ""}'
                            f' "{name}" already exists',
                            {"name": name, "group": rt.group, "kind": rt.plural})
+        if not managed:
+            md.pop("managedFields", None)  # only server-side apply records ownership (ssa.py)
         if rt.status_sub and rt.schema is not None:
             obj.pop("status", None)  # CR status is not settable on create
         obj = self._admit_cr(rt, obj)
@@ -664,7 +669,7 @@ class Store:
 
     def update(self, rt: ResourceType, ns: str | None, name: str, obj: dict,
                subresource: str = "", dry_run: bool = False, owned: bool = False,
-               copy_out: bool = True) -> dict:
+               copy_out: bool = True, manager: str = "unknown", applied: bool = False) -> dict:
         """``owned``: ``obj`` is the caller's private copy (a freshly decoded request body, a
         patch result) and is stored as is. ``copy_out=False``: the stored object itself is
         returned, for a caller that only serialises it before yielding (the HTTP front-end):
@@ -693,6 +698,8 @@ class Store:
                 merged["status"] = new["status"]
             else:
                 merged.pop("status", None)
+            if applied:  # the apply's own ownership record
+                merged["metadata"]["managedFields"] = nmd.get("managedFields") or []
             new = merged
             keep = "spec"
         else:
@@ -719,6 +726,12 @@ class Store:
         new["apiVersion"], new["kind"] = rt.api_version, rt.kind
         new = self._admit_cr(rt, new, keep)
         new["metadata"]["resourceVersion"] = cmd["resourceVersion"]
+        if not applied:  # field ownership of a non-apply write (objects someone applied)
+            if cmd.get("managedFields"):
+                ssa.record_update(cur, new, manager, self.list_keys(rt), rt.status_sub,
+                                  subresource, rt.api_version, now_rfc3339())
+            else:
+                new["metadata"].pop("managedFields", None)
         if dry_run:
             return new
         if new == cur:  # no-op update: no new resourceVersion, no event (apiserver behaviour)
@@ -738,8 +751,54 @@ class Store:
         self._emit(rt, "MODIFIED", new, prev=cur)  # ``cur`` is replaced, never mutated
         return clone(new) if copy_out else new
 
+    def list_keys(self, rt: ResourceType) -> dict:
+        """List strategies for field ownership (ssa.list_keys), once per type and schema."""
+        got = self._list_keys.get(rt.key)
+        if got is None or got[0] is not rt.schema:
+            got = self._list_keys[rt.key] = (rt.schema, ssa.list_keys(rt.kind, rt.schema))
+        return got[1]
+
+    def apply(self, rt: ResourceType, ns: str | None, name: str, cfg: Any, manager: str,
+              force: bool = False, subresource: str = "", dry_run: bool = False) -> dict:
+        """Server-side apply (ssa.py): creates the object when it does not exist."""
+        if not manager:
+            raise ApiError(400, "BadRequest", "PATCH requests with an apply patch require a "
+                           "fieldManager query parameter")
+        if not isinstance(cfg, dict):
+            raise ApiError(400, "BadRequest", "an apply patch must be an object")
+        if cfg.get("kind") and cfg["kind"] != rt.kind or \
+                cfg.get("apiVersion") and cfg["apiVersion"] != rt.api_version:
+            raise ApiError(400, "BadRequest", f"the apply patch is a {cfg.get('apiVersion')} "
+                           f"{cfg.get('kind')}, the request is for {rt.api_version} {rt.kind}")
+        md = cfg.get("metadata") or {}
+        if md.get("name", name) != name:
+            raise ApiError(400, "BadRequest", "the name of the object does not match the URL")
+        nsk = self._check_ns(rt, ns) if rt.namespaced else ""
+        cur = self.objects[rt.key].get((nsk, name))
+        cfg = {**cfg, "metadata": {**md, "name": name}}
+        try:
+            new = ssa.apply(cur, cfg, manager, force, self.list_keys(rt), rt.status_sub,
+                            subresource, rt.api_version, now_rfc3339())
+        except ssa.Conflict as e:
+            n = len(e.conflicts)
+            raise ApiError(409, "Conflict", f"Apply failed with {n} conflict{'s' * (n > 1)}: " +
+                           "; ".join(f'conflict with "{m}": .{f}' for m, f in e.conflicts),
+                           {"name": name, "group": rt.group, "kind": rt.plural, "causes": [
+                               {"reason": "FieldManagerConflict",
+                                "message": f'conflict with "{m}"', "field": "." + f}
+                               for m, f in e.conflicts]}) from e
+        if cur is None:
+            if subresource:
+                self.get(rt, ns, name)  # raises the NotFound
+            return self.create(rt, ns, new, dry_run, managed=True)
+        new["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
+        return self.update(rt, ns, name, new, subresource, dry_run, owned=True, applied=True)
+
     def patch(self, rt: ResourceType, ns: str | None, name: str, patch: Any, ptype: str,
-              subresource: str = "", dry_run: bool = False, copy_out: bool = True) -> dict:
+              subresource: str = "", dry_run: bool = False, copy_out: bool = True,
+              manager: str = "unknown", force: bool = False) -> dict:
+        if ptype == "apply":
+            return self.apply(rt, ns, name, patch, manager, force, subresource, dry_run)
         nsk = self._check_ns(rt, ns) if rt.namespaced else ""
         cur = self.objects[rt.key].get((nsk, name))
         if cur is None:
@@ -760,7 +819,8 @@ class Store:
             new = merge_patch(cur, patch)
         if not (isinstance(patch, dict) and patch.get("metadata", {}).get("resourceVersion")):
             new.setdefault("metadata", {})["resourceVersion"] = cur["metadata"]["resourceVersion"]
-        return self.update(rt, ns, name, new, subresource, dry_run, owned=True, copy_out=copy_out)
+        return self.update(rt, ns, name, new, subresource, dry_run, owned=True, copy_out=copy_out,
+                           manager=manager)
 
     def delete(self, rt: ResourceType, ns: str | None, name: str, grace: int | None = None,
                preconditions: dict | None = None, dry_run: bool = False) -> dict:
@@ -901,7 +961,8 @@ class Store:
                 "spec": {"replicas": get_path(obj, spec_path) or 0},
                 "status": {"replicas": get_path(obj, st_path) or 0}}
 
-    def update_scale(self, rt: ResourceType, ns: str, name: str, scale: dict) -> dict:
+    def update_scale(self, rt: ResourceType, ns: str, name: str, scale: dict,
+                     manager: str = "unknown") -> dict:
         obj = self.get(rt, ns, name)
         rv = scale.get("metadata", {}).get("resourceVersion")
         if rv and rv != obj["metadata"]["resourceVersion"]:
@@ -912,7 +973,7 @@ class Store:
         for p in path[:-1]:
             cur = cur.setdefault(p, {})
         cur[path[-1]] = int(scale.get("spec", {}).get("replicas", 0))
-        self.update(rt, ns, name, obj)
+        self.update(rt, ns, name, obj, manager=manager)
         return self.get_scale(rt, ns, name)
 
     # --------------------------------------------------------- CRDs

@@ -1,6 +1,8 @@
 """gpuctl — the kubectl stand-in for the gpupool operator.
 
-  gpuctl apply -f FILE [--dry-run]        create-or-update every document (kubectl apply, README.md:288-290)
+  gpuctl apply -f FILE [--dry-run] [--server-side [--force-conflicts] [--field-manager M]]
+                                          kubectl apply (README.md:288-290): three-way merge with
+                                          the last applied configuration, or server-side apply
   gpuctl get KIND [NAME] [-o wide|yaml|json] [-l SEL] [-A]   server-side printing (printer columns)
   gpuctl describe KIND NAME               spec/status, conditions table, devices, events
   gpuctl delete KIND NAME | -f FILE [--wait]
@@ -52,6 +54,9 @@ def save_config(cfg: dict) -> None:
         yaml.safe_dump(cfg, f, sort_keys=False)
 
 
+USER_AGENT = "gpuctl/0.1"  # the field manager the apiserver records for gpuctl's plain writes
+
+
 def connection(args) -> tuple[Client, str]:
     """First match wins: --server / $GPUPOOL_APISERVER, --kubeconfig / $KUBECONFIG, the current
     gpuctl context, ~/.kube/config, http://127.0.0.1:6443."""
@@ -66,11 +71,14 @@ def connection(args) -> tuple[Client, str]:
         c = Client.from_kubeconfig(kubeconfig, getattr(args, "context", None))
         if args.token:
             c.token = args.token
+        c.user_agent = USER_AGENT
         return c, args.namespace or c.namespace or "default"
     server = server or ctx.get("server") or "http://127.0.0.1:6443"
     token = args.token or os.environ.get("GPUPOOL_TOKEN") or ctx.get("token")
     ns = args.namespace or ctx.get("namespace") or "default"
-    return Client(server, token), ns
+    c = Client(server, token)
+    c.user_agent = USER_AGENT
+    return c, ns
 
 
 # ------------------------------------------------------------------ discovery
@@ -144,7 +152,8 @@ def cmd_apply(c: Client, ns: str, args) -> int:
             for w in warns:
                 print(f"warning: {w}", file=sys.stderr)
         try:
-            action, out = c.apply(doc, ns, dry_run=args.dry_run)
+            action, out = c.apply(doc, ns, dry_run=args.dry_run, server_side=args.server_side,
+                                  field_manager=args.field_manager, force=args.force_conflicts)
             suffix = " (dry run)" if args.dry_run else ""
             print(f"{doc['kind'].lower()}.{res_for(doc).group or 'core'}/{doc['metadata']['name']} "
                   f"{action}{suffix}")
@@ -802,6 +811,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-f", "--filename", required=True)
     p.add_argument("--dry-run", action="store_true")
     p.add_argument("-o", "--output", default=None)
+    p.add_argument("--server-side", action="store_true",
+                   help="server-side apply (field ownership in managedFields)")
+    p.add_argument("--field-manager", default="gpuctl")
+    p.add_argument("--force-conflicts", action="store_true",
+                   help="server-side apply: take fields other managers own")
     p = sub.add_parser("get")
     p.add_argument("kind")
     p.add_argument("name", nargs="?")

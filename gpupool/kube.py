@@ -161,6 +161,8 @@ class Client:
         if token_file:
             self._reload_token(force=True)
         self.timeout = timeout
+        # "<product>/<version>": the apiserver names a writer's field manager after it
+        self.user_agent = "gpupool-client/0.1"
         self.namespace: str | None = None  # kubeconfig context namespace, if any
         self._local = threading.local()
         self._ssl = None
@@ -268,7 +270,7 @@ class Client:
 
     def _headers(self, ctype: str = "application/json", accept: str = "application/json") -> dict:
         self._reload_token()
-        h = {"Content-Type": ctype, "Accept": accept}
+        h = {"Content-Type": ctype, "Accept": accept, "User-Agent": self.user_agent}
         if self.token:
             h["Authorization"] = f"Bearer {self.token}"
         return h
@@ -363,35 +365,70 @@ class Client:
             body["deleteOptions"] = {"gracePeriodSeconds": grace}
         return self.request("POST", PODS.path(ns, name, "eviction"), body)
 
-    def apply(self, obj: dict, ns: str | None = None, dry_run: bool = False) -> tuple[str, dict]:
-        """kubectl-apply-like create-or-update (replace semantics; retries 409 on update)."""
+    LAST_APPLIED = "kubectl.kubernetes.io/last-applied-configuration"
+
+    def apply(self, obj: dict, ns: str | None = None, dry_run: bool = False,
+              server_side: bool = False, field_manager: str = "gpuctl",
+              force: bool = False) -> tuple[str, dict]:
+        """``kubectl apply``. Client-side (the default): create, or patch with the three-way
+        diff of the last applied configuration (kept in the ``last-applied-configuration``
+        annotation), this manifest and the live object — fields others set (a ``scale``, a
+        controller, a label someone added) survive, fields dropped from the manifest go; a
+        strategic merge patch for built-in kinds, a JSON merge patch for custom resources.
+        ``server_side``: server-side apply as ``field_manager`` (conflicts are the server's
+        409 unless ``force``)."""
+        from .api.smp import three_way
         res = res_for(obj)
         ns = (obj.get("metadata", {}).get("namespace") or ns or "default") if res.namespaced else None
         name = obj["metadata"]["name"]
-        for _ in range(10):
+        if server_side:
+            existed = True
             try:
-                cur = self.get(res, name, ns)
+                self.get(res, name, ns)
             except KubeError as e:
                 if e.code != 404:
                     raise
-                return "created", self.create(res, obj, ns, dry_run)
-            new = json.loads(json.dumps(obj))
-            md = new.setdefault("metadata", {})
-            md["resourceVersion"] = cur["metadata"]["resourceVersion"]
-            for k in ("finalizers", "labels", "annotations", "ownerReferences"):
-                if k not in md and k in cur["metadata"]:
-                    md[k] = cur["metadata"][k]
-            if "status" in cur:
-                new["status"] = cur["status"]
+                existed = False
+            out = self.request("PATCH", res.path(ns, name), obj, ctype="application/apply-patch+yaml",
+                               query={"fieldManager": field_manager, "force": "true" if force else None,
+                                      "dryRun": "All" if dry_run else None})
+            return ("serverside-applied" if existed else "created"), out
+        cfg = json.loads(json.dumps(obj))
+        ann = cfg.setdefault("metadata", {}).get("annotations") or {}
+        ann.pop(self.LAST_APPLIED, None)
+        if not ann:
+            cfg["metadata"].pop("annotations", None)
+        modified = json.loads(json.dumps(cfg))
+        modified["metadata"].setdefault("annotations", {})[self.LAST_APPLIED] = \
+            json.dumps(cfg, sort_keys=True, separators=(",", ":"))
+        try:
+            cur = self.get(res, name, ns)
+        except KubeError as e:
+            if e.code != 404:
+                raise
+            return "created", self.create(res, modified, ns, dry_run)
+        try:
+            original = json.loads((cur["metadata"].get("annotations") or {})
+                                  .get(self.LAST_APPLIED) or "null")
+        except json.JSONDecodeError:
+            original = None
+        builtin = res.group in ("", "apps", "batch", "policy", "autoscaling") or \
+            res.group.endswith(".k8s.io")
+        for kind in ((obj.get("kind"), None) if builtin else (None,)):
+            patch = three_way(original, modified, cur, kind)
+            patch.pop("status", None)  # apply never writes status through the main resource
+            if not patch:
+                return "unchanged", cur
             try:
-                out = self.update(res, new, ns, dry_run=dry_run)
+                out = self.patch(res, name, patch, ns, ptype="strategic" if kind else "merge",
+                                 dry_run=dry_run)
             except KubeError as e:
-                if e.code == 409:
+                if e.code == 415 and kind:  # no strategic merge for this type: merge patch
                     continue
                 raise
             changed = out["metadata"]["resourceVersion"] != cur["metadata"]["resourceVersion"]
             return ("configured" if changed else "unchanged"), out
-        raise KubeError(409, {"message": "apply: too many conflicts"})
+        raise KubeError(415, {"message": "apply: no patch type accepted"})
 
     # ------------------------------------------------------------ watch
     def watch(self, res: Res, ns: str | None = None, resource_version: str | None = None,

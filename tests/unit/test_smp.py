@@ -1,4 +1,4 @@
-"""Strategic merge patch in apiserver-sim (gpupool/apiserver_sim/smp.py): list merge by
+"""Strategic merge patch in apiserver-sim (gpupool/api/smp.py): list merge by
 patchMergeKey for the built-in kinds, the patch directives, and the apiserver's 415 answers
 (strategic merge patch on a custom resource, unknown patch media types)."""
 from __future__ import annotations
@@ -8,7 +8,7 @@ import time
 
 import pytest
 
-from gpupool.apiserver_sim.smp import PatchError, strategic_merge, two_way
+from gpupool.api.smp import PatchError, strategic_merge, two_way
 from gpupool.apiserver_sim.store import ApiError, Store
 from gpupool.kube import MI355XPOOLS, NODES, PODS, Client, KubeError
 from tests.unit.test_apiserver_http import SimThread
