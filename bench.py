@@ -419,7 +419,10 @@ def main() -> int:
                     **summary([x["seconds"] for x in sd], sum(x["ok"] for x in sd)),
                     "from": n, "to": n // 2, "evicted_per_step": [x["evicted"] for x in sd],
                     "helpers_parked_per_step": [x.get("helpersParked") for x in sd],
-                    "release_helper_wait_ms": [x.get("releaseHelperWaitMs") for x in sd],
+                    "helpers_restarting_at_release": [x.get("helpersRestartingAtRelease")
+                                                      for x in sd],
+                    "claim_helper_waits": [x.get("claimHelperWaits") for x in sd],
+                    "claim_helper_wait_ms": [x.get("claimHelperWaitMs") for x in sd],
                     "pods_left_on_released_gpus": sum(len(x["podsOnReleasedGPUs"]) for x in sd)})
         elif args.scale_down_steps > 0:
             secondary["scale_down"] = {"skipped": "the bench pool could not be recovered"

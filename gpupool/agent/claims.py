@@ -24,7 +24,6 @@ PREWAKE = os.environ.get("GPUPOOL_PROBE_PREWAKE", "1") != "0"
 
 
 class ClaimsMixin:
-    HELPER_WARM_WAIT_S = 60.0  # release waits at most this long for a restarting probe helper
 
     def claim(self, req: dict, hold_events: bool = False) -> dict:
         """Claim ``count`` GPUs for a pool, all or nothing: select (topology), commit to the
@@ -111,6 +110,14 @@ class ClaimsMixin:
                     overcommitted = why
                 elif ok:
                     free.append(d["index"])
+            if self.prober.helpers is not None and probe_opts.get("enabled", True):
+                # a GPU released a moment ago may still be starting its probe helper (it was
+                # parked under a tenant): claims take warm GPUs first and a cold one only when
+                # the warm ones do not suffice (the probe then waits for its helper)
+                warm_idx = {d["index"] for d in cand if self.prober.warm(d)}
+                warm = [i for i in free if i in warm_idx]
+                if len(warm) >= count:
+                    free = warm
             owned = [self.by_uuid[u]["index"] for u, r in self.records.items()
                      if r["poolUID"] == pool_uid and u in self.by_uuid]
             if count == 1 and not owned:
@@ -164,6 +171,19 @@ class ClaimsMixin:
         for d in chosen:  # an in-flight HBM scrub window finishes and hands its buffer back
             self.scrubber.yield_device(d["uuid"])
         lap("scrubYield")
+        cold = [d for d in chosen if self.prober.helpers is not None and
+                probe_opts.get("enabled", True) and not self.prober.warm(d)]
+        if cold:
+            # a helper still starting: the wait comes out of the probe's own deadline (one
+            # deadline per claim, as inside Helper.call; probeOverdue is measured against it)
+            budget = float(probe_opts.get("timeoutSeconds") or DEFAULT_TIMEOUT_S)
+            waited = max(self.prober.helpers.wait_ready(d["uuid"], budget) for d in cold)
+            probe_opts = {**probe_opts, "timeoutSeconds": max(0.5, budget - waited / 1e3)}
+            with self.lock:
+                self.stats["claim_helper_waits"] = self.stats.get("claim_helper_waits", 0) + 1
+                self.stats["claim_helper_wait_ms_sum"] = \
+                    self.stats.get("claim_helper_wait_ms_sum", 0.0) + waited
+            lap("helperWait")
         # probes run outside the lock, concurrently across GPUs, each in its GPU's probe helper
         t0 = time.perf_counter()
         results = self.prober.probe_many(chosen, {**probe_opts, "enabled":
@@ -306,20 +326,20 @@ class ClaimsMixin:
                 seq = self.ledger.commit(self.records, durable=False)
             self.stats["releases"] += len(released)
             self._evaluate_some(released)
-        # a GPU goes back to the free set with its probe helper warm: restarted when its pods
-        # left (podview._sync_parking), waited for here — the next claim must not pay HIP init
-        wait_ms = 0.0
+        # a parked helper restarts now (if the pod view has not restarted it already): the GPU
+        # is free at once, and claims take it only when no warm GPU suffices (_claim_start), so
+        # neither this release nor the next claim normally waits for its HIP init
+        restarting = 0
         for u in released:
             d = self.by_uuid.get(u)
             if d is not None and self.prober.helpers is not None:
                 if u in self.prober.parked():
                     self.prober.unpark(d)
-                wait_ms = max(wait_ms, self.prober.helpers.wait_ready(u, self.HELPER_WARM_WAIT_S))
-        if released and self.prober.helpers is not None:
+                restarting += not self.prober.warm(d)
+        if restarting:
             with self.lock:
-                self.stats["release_helper_waits"] = self.stats.get("release_helper_waits", 0) + 1
-                self.stats["release_helper_wait_ms_sum"] = \
-                    self.stats.get("release_helper_wait_ms_sum", 0.0) + wait_ms
+                self.stats["release_helpers_restarting"] = \
+                    self.stats.get("release_helpers_restarting", 0) + restarting
         # durable before the reply, but no fsync under the lock (node views and claims wait on it)
         for q in quarantined:
             self.ledger.persist_quarantine(q)
@@ -331,7 +351,7 @@ class ClaimsMixin:
         if refused:
             return {"ok": False, "reason": "PodsRunning", "released": released,
                     "message": f"GPUs still hold pods: {refused}"}
-        return {"ok": True, "released": released, "helperWaitMs": round(wait_ms, 2)}
+        return {"ok": True, "released": released, "helpersRestarting": restarting}
 
     def update_policy(self, pool_uid: str, policy: dict, resource: str | None) -> dict:
         changed = set()

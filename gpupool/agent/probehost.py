@@ -685,6 +685,8 @@ class HelperPool:
                 "arenaIdleS": self.arena_idle_s, "devices": 1}
         if self.kind == "hip":
             spec["visible"] = dev.get("hipUUID") or str(dev.get("index", 0))
+        elif os.environ.get("GPUPOOL_HELPER_SIM_INIT_S"):  # test hook: a HIP init's duration
+            spec["initDelayS"] = float(os.environ["GPUPOOL_HELPER_SIM_INIT_S"])
         return spec
 
     def _fabric_spec(self) -> dict:
@@ -742,8 +744,9 @@ class HelperPool:
                     stop.append(f)
                 if self._fabric_wanted_locked():
                     self._spawn_locked("fabric")
-        for x in stop:
-            x.stop("park")
+        for x in stop:  # off the caller's path (a cordon, a pod-view refresh): ~60 ms a stop
+            threading.Thread(target=x.stop, args=("park",), daemon=True,
+                             name=f"park-{x.key[:8]}").start()
         self.stats["helper_parks"] = self.stats.get("helper_parks", 0) + 1
         return True
 

@@ -110,6 +110,10 @@ class Prober:
         that cannot run."""
         return self.helpers is None or self.helpers.available(dev["uuid"])
 
+    def warm(self, dev: dict) -> bool:
+        """Would a probe of ``dev`` start at once (its helper is up), not after a HIP init?"""
+        return self.helpers is None or self.helpers.alive(dev["uuid"])
+
     # ------------------------------------------------------------ parking (helper modes)
     def park(self, dev: dict) -> bool:
         """A tenant pod holds ``dev``: stop its probe helper (and take it out of the fabric

@@ -271,16 +271,21 @@ class BenchRun:
         self.phase = "cleanup"
         self._delete_pods([p["metadata"]["name"] for p in left])
         self.scale(name, 0)
-        waits = m1.get("release_helper_waits", 0) - m0.get("release_helper_waits", 0)
+        m2 = self._agent_counters()  # after the cleanup scale to 0 (and any claim after it)
+        waits = m2.get("claim_helper_waits", 0) - m0.get("claim_helper_waits", 0)
         return {"from": n, "to": keep, "seconds": dt, "ok": ok, "evicted": n - len(left),
                 "podsOnReleasedGPUs": on_released, "truth": truth,
                 # helper parking: the pods' GPUs had their probe helpers stopped while the pods
-                # ran; release waited this long (max over its GPUs) for them to be warm again
+                # ran; release hands them back at once while the helpers restart, and a claim
+                # that had to take one still starting waited this long for it
                 "helpersParked": m1.get("probe_helper_parks_total", 0) -
                 m0.get("probe_helper_parks_total", 0),
-                "releaseHelperWaitMs": round((m1.get("release_helper_wait_ms_sum", 0) -
-                                              m0.get("release_helper_wait_ms_sum", 0)) /
-                                             max(1, waits), 2) if waits else None}
+                "helpersRestartingAtRelease": m1.get("release_helpers_restarting", 0) -
+                m0.get("release_helpers_restarting", 0),
+                "claimHelperWaits": waits,
+                "claimHelperWaitMs": round((m2.get("claim_helper_wait_ms_sum", 0) -
+                                            m0.get("claim_helper_wait_ms_sum", 0)) / waits, 2)
+                if waits else None}
 
     def _agent_counters(self) -> dict[str, float]:
         out: dict[str, float] = {}

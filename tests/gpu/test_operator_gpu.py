@@ -603,10 +603,20 @@ def test_probe_helper_parked_while_a_tenant_holds_the_gpu(cluster_factory):
     k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 0}}, "default")
     k.wait_for(PODS, "tenant", "default", lambda o: o is None, timeout=60)
     k.wait_for(MI355XPOOLS, "p", "default", ready_at(0), timeout=120)
-    d, view = dev()
+    deadline = time.monotonic() + 60  # the release hands the GPU back while the helper restarts
+    while time.monotonic() < deadline:
+        d, view = dev()
+        if (view.get("probeHelpers") or {}).get(gpu, {}).get("alive"):
+            break
+        time.sleep(0.2)
     assert (view.get("probeHelpers") or {}).get(gpu, {}).get("alive"), view.get("probeHelpers")
+    # claimable again: the claim's probe runs in the restarted helper
+    k.patch(MI355XPOOLS, "p", {"spec": {"replicas": 1}}, "default")
+    k.wait_for(MI355XPOOLS, "p", "default", ready_at(1), timeout=60)
     m = c.agent_request("gpu-node", "GET", "/metrics")
-    waits = [ln for ln in m.splitlines() if ln.startswith("gpupool_agent_release_helper_wait")]
+    lines = [ln for ln in m.splitlines() if ln.startswith(("gpupool_agent_release_helpers",
+                                                           "gpupool_agent_claim_helper",
+                                                           "gpupool_agent_probe_helper_"))]
     print("PARKING", json.dumps({"agentVramBeforeBytes": before, "tenantVramBytes": tenant_vram,
-                                 "memUsedWithTenantBytes": used, "releaseWait": waits}))
-    assert any(ln.startswith("gpupool_agent_release_helper_waits ") for ln in waits)
+                                 "memUsedWithTenantBytes": used, "helperCounters": lines}))
+    assert any(ln.startswith("gpupool_agent_probe_helper_unparks_total 1") for ln in lines)

@@ -1,6 +1,6 @@
 """Probe helpers leave tenant GPUs alone (round-5 weak #5): with a pod on a pool's GPU the agent
-parks that GPU's helper (no process, no context), and restarts it — warm before release hands
-the GPU back — once the pod is gone (CPU: helper-sim kernels; the GPU tier checks the HIP
+parks that GPU's helper (no process, no context), and restarts it once the pod is gone; claims
+take warm GPUs before one whose helper is still starting (CPU: helper-sim kernels; the GPU tier checks the HIP
 context and VRAM on a real MI355X)."""
 from __future__ import annotations
 
@@ -55,17 +55,48 @@ def test_helper_parked_while_a_pod_holds_the_gpu(cluster_factory):
     assert dev.get("probeHelper") == "Parked"
     assert _wait(lambda: _counter(c.agent_request("park-node", "GET", "/metrics"),
                                   "gpupool_agent_probe_helper_parks_total") == 1)
-    # pod gone and the pool scaled to 0: the release waits for the restarted helper
+    # pod gone and the pool scaled to 0: the helper restarts (release does not wait for it)
     k.delete(PODS, "tenant", "default")
     k.wait_for(PODS, "tenant", "default", lambda p: p is None, 30)
     k.patch(MI355XPOOLS, "pp", {"spec": {"replicas": 0}}, "default")
     wait_ready(k, "pp", 0, timeout=60)
-    view = c.agent_request("park-node", "GET", "/v1/node")
-    assert helper(view).get("alive") and not helper(view).get("parked")
+    view = _wait(lambda: (lambda v: v if helper(v).get("alive") else None)(
+        c.agent_request("park-node", "GET", "/v1/node")))
+    assert view and not helper(view).get("parked")
     assert helper(view).get("pid") != pid  # a fresh process
     m = c.agent_request("park-node", "GET", "/metrics")
     assert _counter(m, "gpupool_agent_probe_helper_unparks_total") == 1
-    assert _counter(m, "gpupool_agent_release_helper_waits") >= 1
-    # and the GPU is claimable again with a warm helper
+    # and the GPU is claimable again
     k.patch(MI355XPOOLS, "pp", {"spec": {"replicas": 2}}, "default")
     wait_ready(k, "pp", 2, timeout=60)
+
+
+def test_claims_take_warm_gpus_before_one_whose_helper_restarts(cluster_factory):
+    """Release hands a GPU back while its parked helper restarts (2 s of simulated HIP init
+    here); a claim arriving meanwhile takes the other, warm GPU instead of waiting for it."""
+    c = cluster_factory(nodes=[NodeSpec("warm-node", count=2, probe="helper-sim")],
+                        env={"GPUPOOL_HELPER_SIM_INIT_S": "2.0"})
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("pw", 1, drain={"gracePeriodSeconds": 1}), "default")
+    first = wait_ready(k, "pw", 1, timeout=60)["status"]["devices"][0]["uuid"]
+    k.create(PODS, pause_pod("tenant"), "default")
+    k.wait_for(PODS, "tenant", "default", lambda p: p and p["status"].get("phase") == "Running",
+               30)
+    assert _wait(lambda: first in {u for u, h in (c.agent_request("warm-node", "GET", "/v1/node")
+                                                  .get("probeHelpers") or {}).items()
+                                   if h.get("parked")})
+    k.delete(PODS, "tenant", "default", grace=0)
+    k.wait_for(PODS, "tenant", "default", lambda p: p is None, 30)
+    t0 = time.monotonic()
+    k.patch(MI355XPOOLS, "pw", {"spec": {"replicas": 0}}, "default")
+    wait_ready(k, "pw", 0, timeout=60)
+    k.patch(MI355XPOOLS, "pw", {"spec": {"replicas": 1}}, "default")
+    o = wait_ready(k, "pw", 1, timeout=60)
+    took = time.monotonic() - t0
+    assert o["status"]["devices"][0]["uuid"] != first  # the warm GPU
+    m = c.agent_request("warm-node", "GET", "/metrics")
+    assert _counter(m, "gpupool_agent_claim_helper_waits") == 0
+    assert took < 1.5, took  # neither the release nor the claim waited out the 2 s init
+    # both GPUs: the second one's probe waits for its helper (out of the probe deadline)
+    k.patch(MI355XPOOLS, "pw", {"spec": {"replicas": 2}}, "default")
+    wait_ready(k, "pw", 2, timeout=60)
