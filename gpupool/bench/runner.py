@@ -250,7 +250,9 @@ class BenchRun:
         name, res = pool["metadata"]["name"], pool["spec"]["resourceName"]
         keep = n // 2
         self.phase = "scale_up"
-        self.scale(name, n)
+        m_up = self._agent_counters()
+        self.scale(name, n)  # right after the previous step's release (its helpers restarting)
+        m_up1 = self._agent_counters()
         self.phase = "start_pods"
         pods = self._pods(f"sd{step}", n, res)
         m0 = self._agent_counters()
@@ -271,20 +273,20 @@ class BenchRun:
         self.phase = "cleanup"
         self._delete_pods([p["metadata"]["name"] for p in left])
         self.scale(name, 0)
-        m2 = self._agent_counters()  # after the cleanup scale to 0 (and any claim after it)
-        waits = m2.get("claim_helper_waits", 0) - m0.get("claim_helper_waits", 0)
+        waits = m_up1.get("claim_helper_waits", 0) - m_up.get("claim_helper_waits", 0)
         return {"from": n, "to": keep, "seconds": dt, "ok": ok, "evicted": n - len(left),
                 "podsOnReleasedGPUs": on_released, "truth": truth,
                 # helper parking: the pods' GPUs had their probe helpers stopped while the pods
-                # ran; release hands them back at once while the helpers restart, and a claim
-                # that had to take one still starting waited this long for it
+                # ran; release hands them back at once while the helpers restart, and the claim
+                # that opened this step (right after the previous step's release) waited this
+                # long when it had to take a GPU whose helper was still starting
                 "helpersParked": m1.get("probe_helper_parks_total", 0) -
                 m0.get("probe_helper_parks_total", 0),
                 "helpersRestartingAtRelease": m1.get("release_helpers_restarting", 0) -
                 m0.get("release_helpers_restarting", 0),
                 "claimHelperWaits": waits,
-                "claimHelperWaitMs": round((m2.get("claim_helper_wait_ms_sum", 0) -
-                                            m0.get("claim_helper_wait_ms_sum", 0)) / waits, 2)
+                "claimHelperWaitMs": round((m_up1.get("claim_helper_wait_ms_sum", 0) -
+                                            m_up.get("claim_helper_wait_ms_sum", 0)) / waits, 2)
                 if waits else None}
 
     def _agent_counters(self) -> dict[str, float]:
