@@ -40,7 +40,6 @@ class PodIndex {
   struct Entry {
     std::string node, job_key;
     std::map<std::string, int64_t> req;  // extended resource -> count (live pods only)
-    Json pod;
   };
   void remove_locked_(const std::string& key);
   mutable std::mutex mu_;

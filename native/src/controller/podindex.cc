@@ -4,6 +4,8 @@
 #include "gpupool/informer.h"
 #include "job_util.h"
 
+#include <algorithm>
+
 namespace gpupool {
 
 using namespace detail;
@@ -12,19 +14,45 @@ namespace {
 
 bool extended(const std::string& name) { return name.find('/') != std::string::npos && name.rfind("kubernetes.io/", 0) != 0; }
 
-// extended resource -> count asked for by the pod's containers (limits, else requests)
+std::map<std::string, int64_t> container_requests(const Json& c) {
+  const Json& r = c["resources"];
+  std::map<std::string, int64_t> mine;
+  for (const auto& kv : r["requests"].members())
+    if (extended(kv.first)) mine[kv.first] = qty(kv.second);
+  for (const auto& kv : r["limits"].members())  // an extended resource's request is its limit
+    if (extended(kv.first) && qty(kv.second)) mine[kv.first] = qty(kv.second);
+  return mine;
+}
+
+// extended resource -> what the pod holds, as the scheduler counts it: the sum over its
+// containers, or the largest init container's request if that is more (init containers run one
+// at a time, before the others)
 std::map<std::string, int64_t> extended_requests(const Json& pod) {
   std::map<std::string, int64_t> out;
-  for (const auto& c : pod.path("spec.containers").elements()) {
-    const Json& r = c["resources"];
-    std::map<std::string, int64_t> mine;
-    for (const auto& kv : r["requests"].members())
-      if (extended(kv.first)) mine[kv.first] = qty(kv.second);
-    for (const auto& kv : r["limits"].members())  // an extended resource's request is its limit
-      if (extended(kv.first) && qty(kv.second)) mine[kv.first] = qty(kv.second);
-    for (const auto& kv : mine) out[kv.first] += kv.second;
-  }
+  for (const auto& c : pod.path("spec.containers").elements())
+    for (const auto& kv : container_requests(c)) out[kv.first] += kv.second;
+  for (const auto& c : pod.path("spec.initContainers").elements())
+    for (const auto& kv : container_requests(c)) out[kv.first] = std::max(out[kv.first], kv.second);
+  for (auto it = out.begin(); it != out.end();) it = it->second > 0 ? std::next(it) : out.erase(it);
   return out;
+}
+
+Json trim_containers(const Json& list) {
+  Json containers = Json::array();
+  for (const auto& c : list.elements()) {
+    Json res = Json::object();
+    for (const char* part : {"limits", "requests"}) {
+      Json q = Json::object();
+      for (const auto& kv : c["resources"][part].members())
+        if (extended(kv.first)) q[kv.first] = kv.second;
+      if (q.size()) res[part] = q;
+    }
+    Json cc = Json::object();
+    cc["name"] = c["name"];
+    if (res.size()) cc["resources"] = res;
+    containers.push_back(cc);
+  }
+  return containers;
 }
 
 }  // namespace
@@ -60,21 +88,8 @@ Json trim_pod(const Json& pod) {
   out["metadata"] = m;
   Json spec = Json::object();
   if (pod.path("spec.nodeName").is_string()) spec["nodeName"] = pod.path("spec.nodeName");
-  Json containers = Json::array();
-  for (const auto& c : pod.path("spec.containers").elements()) {
-    Json res = Json::object();
-    for (const char* part : {"limits", "requests"}) {
-      Json q = Json::object();
-      for (const auto& kv : c["resources"][part].members())
-        if (extended(kv.first)) q[kv.first] = kv.second;
-      if (q.size()) res[part] = q;
-    }
-    Json cc = Json::object();
-    cc["name"] = c["name"];
-    if (res.size()) cc["resources"] = res;
-    containers.push_back(cc);
-  }
-  spec["containers"] = containers;
+  spec["containers"] = trim_containers(pod.path("spec.containers"));
+  if (pod.path("spec.initContainers").size()) spec["initContainers"] = trim_containers(pod.path("spec.initContainers"));
   out["spec"] = spec;
   const Json& st = pod["status"];
   Json s = Json::object();
@@ -129,8 +144,7 @@ void PodIndex::on_event(const std::string& type, const Json& pod) {
   // still be running out their grace period)
   if (!e.node.empty() && !terminal(pod_phase(pod))) e.req = extended_requests(pod);
   for (const auto& kv : e.req) by_res_node_[kv.first][e.node] += kv.second;
-  if (!e.job_key.empty()) by_job_[e.job_key][key] = pod;
-  e.pod = pod;
+  if (!e.job_key.empty()) by_job_[e.job_key][key] = pod;  // the only copy kept: job pods
   pods_[key] = std::move(e);
 }
 

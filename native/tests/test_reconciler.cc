@@ -158,4 +158,16 @@ TEST(pod_index_tracks_live_extended_requests_and_job_pods) {
   EXPECT_TRUE(t.path("spec.containers")[0]["resources"]["limits"]["amd.com/gpu"].as_string() == "1");
   EXPECT_TRUE(t.path("spec.containers")[0]["resources"]["limits"]["cpu"].is_null());
   EXPECT_TRUE(t.path("metadata.labels")["gpupool.amd.com/job-name"].as_string() == "j");
+  // init containers: the pod holds max(sum of containers, largest init container), as the
+  // scheduler counts it; a pod asking only in an init container is relevant and kept so
+  Json init = pod("g", "n3", 1, "Running");
+  init["spec"]["initContainers"] = Json::parse(
+      R"([{"name":"i1","resources":{"limits":{"amd.com/gpu":"3"}}},{"name":"i2","resources":{"limits":{"amd.com/gpu":"2"}}}])");
+  idx.on_event("ADDED", init);
+  EXPECT_TRUE(idx.requested_by_node("amd.com/gpu")["n3"] == 3);
+  Json only_init = cpu_only;
+  only_init["spec"]["initContainers"] = Json::parse(R"([{"name":"i","resources":{"limits":{"amd.com/gpu":"1"}}}])");
+  EXPECT_TRUE(gpupool::pod_relevant(only_init));
+  EXPECT_TRUE(gpupool::trim_pod(only_init).path("spec.initContainers")[0]["resources"]["limits"]["amd.com/gpu"]
+                  .as_string() == "1");
 }
