@@ -3,6 +3,7 @@
   gpuctl apply -f FILE [--dry-run] [--server-side [--force-conflicts] [--field-manager M]]
                                           kubectl apply (README.md:288-290): three-way merge with
                                           the last applied configuration, or server-side apply
+  gpuctl diff -f FILE [--server-side]     what apply would change (server dry run), exit 1 if any
   gpuctl get KIND [NAME] [-o wide|yaml|json] [-l SEL] [-A]   server-side printing (printer columns)
   gpuctl describe KIND NAME               spec/status, conditions table, devices, events
   gpuctl delete KIND NAME | -f FILE [--wait]
@@ -163,6 +164,62 @@ def cmd_apply(c: Client, ns: str, args) -> int:
             print(f"error: {e}", file=sys.stderr)
             rc = 1
     return rc
+
+
+_DIFF_SKIP_META = ("resourceVersion", "generation", "managedFields", "uid", "creationTimestamp")
+
+
+def _diff_view(obj: dict | None) -> str:
+    """An object as ``kubectl diff`` compares it: server bookkeeping and apply's own annotation
+    left out, YAML with stable key order."""
+    if obj is None:
+        return ""
+    o = json.loads(json.dumps(obj))
+    md = o.get("metadata") or {}
+    for k in _DIFF_SKIP_META:
+        md.pop(k, None)
+    ann = md.get("annotations") or {}
+    ann.pop(Client.LAST_APPLIED, None)
+    if not ann:
+        md.pop("annotations", None)
+    return yaml.safe_dump(o, sort_keys=True)
+
+
+def cmd_diff(c: Client, ns: str, args) -> int:
+    """``kubectl diff``: what ``apply`` would change, from a server-side dry run of that apply
+    (defaulting, admission and the merge as the server does them). Exit 1 when anything would
+    change, 0 when nothing would, >1 on errors."""
+    import difflib
+    changed = False
+    from .convert import convert, convertible
+    for doc in load_docs(args.filename):
+        if convertible(doc):
+            doc, _ = convert(doc)
+        res = res_for(doc)
+        name = doc["metadata"]["name"]
+        dns = (doc["metadata"].get("namespace") or ns) if res.namespaced else None
+        try:
+            cur = c.get(res, name, dns)
+        except KubeError as e:
+            if e.code != 404:
+                print(f"error: {e}", file=sys.stderr)
+                return 2
+            cur = None
+        try:
+            _, out = c.apply(doc, dns, dry_run=True, server_side=args.server_side,
+                             field_manager=args.field_manager, force=args.force_conflicts)
+        except KubeError as e:
+            print(f"error: {e}", file=sys.stderr)
+            return 2
+        a, b = _diff_view(cur), _diff_view(out)
+        if a == b:
+            continue
+        changed = True
+        label = f"{res.group or 'v1'}.{doc['kind']}.{dns + '.' if dns else ''}{name}"
+        sys.stdout.writelines(difflib.unified_diff(
+            a.splitlines(keepends=True), b.splitlines(keepends=True),
+            fromfile=f"live/{label}", tofile=f"merged/{label}"))
+    return 1 if changed else 0
 
 
 def cmd_get(c: Client, ns: str, args) -> int:
@@ -816,6 +873,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--field-manager", default="gpuctl")
     p.add_argument("--force-conflicts", action="store_true",
                    help="server-side apply: take fields other managers own")
+    p = sub.add_parser("diff")
+    p.add_argument("-f", "--filename", required=True)
+    p.add_argument("--server-side", action="store_true")
+    p.add_argument("--field-manager", default="gpuctl")
+    p.add_argument("--force-conflicts", action="store_true")
     p = sub.add_parser("get")
     p.add_argument("kind")
     p.add_argument("name", nargs="?")
@@ -914,7 +976,8 @@ def main(argv: list[str] | None = None) -> int:
     if args.cmd == "convert":
         return cmd_convert(args)
     c, ns = connection(args)
-    fn = {"apply": cmd_apply, "get": cmd_get, "describe": cmd_describe, "delete": cmd_delete,
+    fn = {"apply": cmd_apply, "diff": cmd_diff, "get": cmd_get, "describe": cmd_describe,
+          "delete": cmd_delete,
           "scale": cmd_scale, "wait": cmd_wait, "logs": cmd_logs, "events": cmd_events,
           "devices": cmd_devices, "install": cmd_install, "render": cmd_render,
           "gpu": cmd_gpu, "trainjob": cmd_trainjob, "whoami": cmd_whoami, "top": cmd_top}[args.cmd]

@@ -199,3 +199,30 @@ def test_ssa_over_http_with_gpuctl(tmp_path, capsys):
     c.create(NODES, {"apiVersion": "v1", "kind": "Node", "metadata": {"name": "plain"}})
     c.patch(NODES, "plain", {"metadata": {"labels": {"a": "b"}}})
     assert "managedFields" not in c.get(NODES, "plain")["metadata"]
+
+
+def test_gpuctl_diff_shows_what_apply_would_change(tmp_path, capsys):
+    """``kubectl diff``: a server-side dry run of the apply, compared with the live object."""
+    sim = SimThread()
+    c = Client(sim.url)
+    f = tmp_path / "p.yaml"
+    f.write_text(json.dumps(_pool(1)))
+    base = ["--server", sim.url, "-n", "default"]
+    assert gpuctl.main(base + ["diff", "-f", str(f)]) == 1  # not there yet: all of it is new
+    out = capsys.readouterr().out
+    assert "+  replicas: 1" in out and "+  resourceName: amd.com/gpu" in out  # defaulted
+    assert gpuctl.main(base + ["apply", "-f", str(f)]) == 0
+    capsys.readouterr()
+    assert gpuctl.main(base + ["diff", "-f", str(f)]) == 0
+    assert capsys.readouterr().out == ""
+    f.write_text(json.dumps(_pool(3)))
+    assert gpuctl.main(base + ["diff", "-f", str(f)]) == 1
+    out = capsys.readouterr().out
+    assert "-  replicas: 1" in out and "+  replicas: 3" in out
+    assert c.get(MI355XPOOLS, "p", "default")["spec"]["replicas"] == 1  # a dry run only
+    # server-side: the fields the client-side apply set have an owner (before-first-apply),
+    # so changing one conflicts, as it would on a cluster, unless forced
+    assert gpuctl.main(base + ["diff", "--server-side", "-f", str(f)]) == 2
+    assert 'conflict with "before-first-apply": .spec.replicas' in capsys.readouterr().err
+    assert gpuctl.main(base + ["diff", "--server-side", "--force-conflicts", "-f", str(f)]) == 1
+    assert "+  replicas: 3" in capsys.readouterr().out
