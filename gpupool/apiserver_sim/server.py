@@ -17,6 +17,7 @@ import asyncio
 import datetime as _dt
 import json
 import logging
+import os
 import re
 import time
 from typing import Any
@@ -415,6 +416,10 @@ class ApiServerSim:
                 return web.json_response(self.store.update_scale(rt, ns, name, cur,
                                                                  self._manager(request)))
             raise ApiError(405, "MethodNotAllowed", f"{m} not allowed on scale")
+        if sub == "log":
+            if rt.kind != "Pod" or m != "GET":
+                raise ApiError(405, "MethodNotAllowed", "log is GET on pods only")
+            return await self._pod_log(request, ns, name)
         if sub == "eviction":
             if rt.kind != "Pod" or m != "POST":
                 raise ApiError(405, "MethodNotAllowed", "eviction is POST on pods only")
@@ -423,6 +428,54 @@ class ApiServerSim:
         if sub:
             raise ApiError(404, "NotFound", f"unknown subresource {sub}")
         return await self._object(request, rt, ns, name, "", dry)
+
+    async def _pod_log(self, request, ns: str, name: str):
+        """``pods/{name}/log``: what the kubelet proxies on a cluster; here the test kubelet's log
+        file (the pod's ``gpupool.amd.com/log-path`` annotation). ``tailLines``, ``limitBytes``
+        and ``follow`` (streams until the pod ends or the client goes)."""
+        q = request.query
+        pods = self.store.lookup("", "pods")
+        pod = self.store.get(pods, ns, name)
+        path = (pod["metadata"].get("annotations") or {}).get("gpupool.amd.com/log-path")
+        if not path or not os.path.exists(path):
+            if pod.get("status", {}).get("phase") == "Pending":
+                raise ApiError(400, "BadRequest", f'container in pod "{name}" is waiting to start')
+            return web.Response(text="", content_type="text/plain")
+
+        def read(off: int) -> bytes:
+            with open(path, "rb") as f:
+                f.seek(off)
+                return f.read()
+        data = read(0)
+        if q.get("tailLines"):
+            n = int(q["tailLines"])
+            lines = data.splitlines(keepends=True)
+            data = b"".join(lines[-n:]) if n > 0 else b""
+        if q.get("limitBytes"):
+            data = data[:int(q["limitBytes"])]
+        if q.get("follow") not in ("true", "1"):
+            return web.Response(body=data, content_type="text/plain")
+        resp = web.StreamResponse(headers={"Content-Type": "text/plain"})
+        await resp.prepare(request)
+        await resp.write(data)
+        off = os.path.getsize(path)
+        while True:
+            await asyncio.sleep(0.1)
+            try:
+                more = read(off)
+            except OSError:
+                break
+            if more:
+                off += len(more)
+                await resp.write(more)
+            cur = self.store.objects[pods.key].get((ns, name))
+            if cur is None or cur.get("status", {}).get("phase") in ("Succeeded", "Failed"):
+                tail = read(off)
+                if tail:
+                    await resp.write(tail)
+                break
+        await resp.write_eof()
+        return resp
 
     PATCH_TYPES = {"application/json-patch+json": "json",
                    "application/merge-patch+json": "merge",

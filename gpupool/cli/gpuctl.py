@@ -9,7 +9,9 @@
   gpuctl delete KIND NAME | -f FILE [--wait]
   gpuctl scale KIND NAME --replicas N     via the scale subresource
   gpuctl wait KIND NAME --for condition=Ready|delete|jsonpath=.status.readyReplicas=N [--timeout 60]
-  gpuctl logs POD                         fake-kubelet container log
+  gpuctl logs POD [-f] [--tail N]         the pod's log (pods/log)
+  gpuctl create namespace NAME | secret generic NAME --from-literal k=v | configmap NAME ...
+  gpuctl run NAME --image IMG [--gpus N] [--rm] -- CMD...   one pod; --rm: wait, log, delete
   gpuctl events [-n NS]
   gpuctl devices NODE                     the node agent's live device view
   gpuctl gpu cordon|uncordon NODE GPU     per-GPU maintenance (replace it in its pool, never claim)
@@ -387,14 +389,122 @@ def cmd_wait(c: Client, ns: str, args) -> int:
     return 0
 
 
-def cmd_logs(c: Client, ns: str, args) -> int:
-    pod = c.get(PODS, args.pod, ns)
-    path = (pod["metadata"].get("annotations") or {}).get("gpupool.amd.com/log-path")
-    if not path or not os.path.exists(path):
-        print("error: no log available for this pod (fake kubelet log path unknown)", file=sys.stderr)
+def pod_log(c: Client, ns: str, name: str, tail: int | None = None, follow: bool = False,
+            out=None) -> int:
+    """``pods/{name}/log`` (the kubelet's log through the apiserver, as ``kubectl logs``)."""
+    out = out or sys.stdout
+    q = {"tailLines": tail, "follow": "true" if follow else None}
+    path = PODS.path(ns, name, "log")
+    if not follow:
+        try:
+            text = c.request("GET", path, query=q, accept="text/plain")
+        except KubeError as e:
+            print(f"error: {e}", file=sys.stderr)
+            return 1
+        out.write(text if isinstance(text, str) else json.dumps(text) + "\n")
+        return 0
+    conn = c._conn(timeout=None)
+    conn.request("GET", path + "?" + "&".join(f"{k}={v}" for k, v in q.items() if v is not None),
+                 headers=c._headers("application/json", "text/plain"))
+    resp = conn.getresponse()
+    if resp.status >= 400:
+        print(f"error: HTTP {resp.status}: {resp.read().decode(errors='replace')}", file=sys.stderr)
         return 1
-    sys.stdout.write(open(path).read())
+    while True:
+        chunk = resp.read1(65536) if hasattr(resp, "read1") else resp.read(4096)
+        if not chunk:
+            break
+        out.write(chunk.decode(errors="replace"))
+        out.flush()
+    conn.close()
     return 0
+
+
+def cmd_logs(c: Client, ns: str, args) -> int:
+    return pod_log(c, ns, args.pod, args.tail, args.follow)
+
+
+def cmd_create(c: Client, ns: str, args) -> int:
+    """``kubectl create namespace|secret generic|configmap`` (README.md:244-252 creates the
+    Azure credentials Secret this way)."""
+    import base64
+    from ..kube import CONFIGMAPS, NAMESPACES, SECRETS
+    names = list(args.name)
+    if args.what == "secret" and names[0] == "generic":
+        names = names[1:]
+    if len(names) != 1:
+        print(f"error: create {args.what} takes one name", file=sys.stderr)
+        return 1
+    name = names[0]
+    if args.what == "namespace":
+        c.create(NAMESPACES, {"apiVersion": "v1", "kind": "Namespace",
+                              "metadata": {"name": name}})
+        print(f"namespace/{name} created")
+        return 0
+    data: dict[str, str] = {}
+    for lit in args.from_literal or []:
+        k, sep, v = lit.partition("=")
+        if not sep:
+            print(f"error: --from-literal {lit!r} is not key=value", file=sys.stderr)
+            return 1
+        data[k] = v
+    for spec in args.from_file or []:
+        k, sep, f = spec.partition("=")
+        if not sep:
+            k, f = os.path.basename(spec), spec
+        with open(f, "rb") as fh:
+            raw = fh.read()
+        data[k] = raw.decode() if args.what == "configmap" else raw  # type: ignore[assignment]
+    if args.what == "configmap":
+        c.create(CONFIGMAPS, {"apiVersion": "v1", "kind": "ConfigMap",
+                              "metadata": {"name": name}, "data": data}, ns)
+        print(f"configmap/{name} created")
+        return 0
+    enc = {k: base64.b64encode(v if isinstance(v, bytes) else v.encode()).decode()
+           for k, v in data.items()}
+    c.create(SECRETS, {"apiVersion": "v1", "kind": "Secret", "type": "Opaque",
+                       "metadata": {"name": name}, "data": enc}, ns)
+    print(f"secret/{name} created")
+    return 0
+
+
+def cmd_run(c: Client, ns: str, args) -> int:
+    """``kubectl run NAME --image IMG [--gpus N] [--rm] -- CMD...``: one pod (restartPolicy
+    Never) asking for N GPUs of ``--resource``; with ``--rm`` wait for it, print its log, delete
+    it, and exit with its exit code — the reference's GPU smoke test
+    (``kubectl run --rm -it --gpus=1 gpu-test ... nvidia-smi``, GPU调度平台搭建.md:134-138) is
+    ``gpuctl run --rm --gpus 1 gpu-test --image rocm/dev-ubuntu-22.04 -- amd-smi static``."""
+    cmd = list(args.command or [])
+    ctr: dict[str, Any] = {"name": args.name, "image": args.image}
+    if cmd:
+        ctr["command"] = cmd
+    if args.gpus:
+        ctr["resources"] = {"limits": {args.resource: args.gpus}}
+    pod = {"apiVersion": "v1", "kind": "Pod",
+           "metadata": {"name": args.name, "labels": {"run": args.name}},
+           "spec": {"restartPolicy": "Never", "containers": [ctr]}}
+    c.create(PODS, pod, ns)
+    if not args.rm:
+        print(f"pod/{args.name} created")
+        return 0
+    try:
+        o = c.wait_for(PODS, args.name, ns, lambda o: not o or o.get("status", {}).get("phase")
+                       in ("Succeeded", "Failed"), timeout=args.timeout)
+        pod_log(c, ns, args.name)
+        code = 1
+        if o:
+            cs = (o.get("status") or {}).get("containerStatuses") or []
+            term = ((cs[0].get("state") or {}).get("terminated") or {}) if cs else {}
+            code = int(term.get("exitCode", 0 if o["status"].get("phase") == "Succeeded" else 1))
+    except TimeoutError:
+        print(f"error: pod/{args.name} did not finish within {args.timeout:g} s", file=sys.stderr)
+        code = 1
+    try:
+        c.delete(PODS, args.name, ns, grace=0)
+    except KubeError:
+        pass
+    print(f'pod "{args.name}" deleted', file=sys.stderr)
+    return code
 
 
 def cmd_events(c: Client, ns: str, args) -> int:
@@ -748,11 +858,9 @@ def cmd_trainjob(c: Client, ns: str, args) -> int:
             print(f"error: no pods for trainjob {args.job}", file=sys.stderr)
             return 1
         for p in pods:
-            path = (p["metadata"].get("annotations") or {}).get("gpupool.amd.com/log-path")
             if len(pods) > 1:
                 print(f"==> {p['metadata']['name']} <==")
-            if path and os.path.exists(path):
-                sys.stdout.write(open(path).read())
+            pod_log(c, ns, p["metadata"]["name"])
         return 0
     return 2
 
@@ -906,6 +1014,23 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--timeout", type=float, default=60)
     p = sub.add_parser("logs")
     p.add_argument("pod")
+    p.add_argument("-f", "--follow", action="store_true")
+    p.add_argument("--tail", type=int, default=None)
+    p = sub.add_parser("create")
+    p.add_argument("what", choices=["namespace", "secret", "configmap"])
+    p.add_argument("name", nargs="+", help="NAME, or 'generic NAME' for a secret")
+    p.add_argument("--from-literal", action="append")
+    p.add_argument("--from-file", action="append")
+    p = sub.add_parser("run")
+    p.add_argument("name")
+    p.add_argument("--image", required=True)
+    p.add_argument("--gpus", type=int, default=0)
+    p.add_argument("--resource", default=schema.DEFAULT_RESOURCE)
+    p.add_argument("--rm", action="store_true", help="wait, print the log, delete the pod")
+    p.add_argument("-i", "--stdin", action="store_true", help="accepted for kubectl parity")
+    p.add_argument("-t", "--tty", action="store_true", help="accepted for kubectl parity")
+    p.add_argument("--timeout", type=float, default=300.0)
+    p.add_argument("command", nargs="*", help="after --: the container's command")
     p = sub.add_parser("events")
     p.add_argument("-A", "--all-namespaces", action="store_true")
     p = sub.add_parser("devices")
@@ -968,7 +1093,14 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def main(argv: list[str] | None = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    command: list[str] = []
+    if "run" in argv and "--" in argv[argv.index("run"):]:  # `run NAME ... -- CMD ARGS...`
+        i = argv.index("--", argv.index("run"))
+        argv, command = argv[:i], argv[i + 1:]
     args = build_parser().parse_args(argv)
+    if args.cmd == "run":
+        args.command = command + list(args.command or [])
     if args.cmd == "config":
         return cmd_config(args)
     if args.cmd == "login":
@@ -979,6 +1111,7 @@ def main(argv: list[str] | None = None) -> int:
     fn = {"apply": cmd_apply, "diff": cmd_diff, "get": cmd_get, "describe": cmd_describe,
           "delete": cmd_delete,
           "scale": cmd_scale, "wait": cmd_wait, "logs": cmd_logs, "events": cmd_events,
+          "create": cmd_create, "run": cmd_run,
           "devices": cmd_devices, "install": cmd_install, "render": cmd_render,
           "gpu": cmd_gpu, "trainjob": cmd_trainjob, "whoami": cmd_whoami, "top": cmd_top}[args.cmd]
     try:
