@@ -587,6 +587,7 @@ class ApiServerSim:
         filtered = bool(q.get("labelSelector") or q.get("fieldSelector"))
 
         queue: asyncio.Queue = asyncio.Queue()
+        resp: web.StreamResponse | None = None
         # Register before computing the backlog so nothing falls between the two.
         self.watchers.setdefault(rt.key, set()).add(queue)
         try:
@@ -657,8 +658,10 @@ class ApiServerSim:
                 await resp.write(line or ev.encoded())
             await resp.write_eof()
             return resp
-        except (ConnectionResetError, asyncio.CancelledError):
-            raise
+        except ConnectionResetError:
+            # the client went away mid-stream (a watch it stopped, a process that exited): the
+            # stream just ends, as the apiserver's does
+            return resp if resp is not None else web.Response(status=499)
         finally:
             self.watchers.get(rt.key, set()).discard(queue)
 
