@@ -676,6 +676,7 @@ class HelperPool:
         # GPUs whose helper is parked: a tenant pod holds the GPU, so the agent keeps no HIP
         # context (no VRAM, no process) on it; requests for it are refused until unpark()
         self._parked: set[str] = set()
+        self._fabric_timer_armed = False
         if fabric_idle_s > 0:
             threading.Thread(target=self._fabric_reaper, daemon=True, name="fabric-idle").start()
 
@@ -741,9 +742,8 @@ class HelperPool:
                 self._fabric_devs = self._unparked_devs_locked()
                 f = self._helpers.pop("fabric", None)
                 if f is not None:
-                    stop.append(f)
-                if self._fabric_wanted_locked():
-                    self._spawn_locked("fabric")
+                    stop.append(f)  # it has a context on this GPU: it goes now
+                self._respawn_fabric_later_locked()
         for x in stop:  # off the caller's path (a cordon, a pod-view refresh): ~60 ms a stop
             threading.Thread(target=x.stop, args=("park",), daemon=True,
                              name=f"park-{x.key[:8]}").start()
@@ -768,10 +768,30 @@ class HelperPool:
                 f = self._helpers.pop("fabric", None)
                 if f is not None:
                     threading.Thread(target=f.stop, args=("park",), daemon=True).start()
-                if self._fabric_wanted_locked():
-                    self._spawn_locked("fabric")
+                self._respawn_fabric_later_locked()
         self.stats["helper_unparks"] = self.stats.get("helper_unparks", 0) + 1
         return h
+
+    # a burst of parks / unparks (a drain of several GPUs, a gang's pods starting) restarts the
+    # resident fabric helper once, over the GPUs pod-free at the end of the burst, not once per GPU
+    # (each start is a HIP init on every GPU plus the all-pairs warm-up)
+    FABRIC_RESPAWN_DEBOUNCE_S = 0.25
+
+    def _respawn_fabric_later_locked(self) -> None:
+        if not self.resident_fabric or self._fabric_timer_armed:
+            return
+        self._fabric_timer_armed = True
+
+        def fire() -> None:
+            with self._mu:
+                self._fabric_timer_armed = False
+                self._fabric_devs = self._unparked_devs_locked()
+                if self._fabric_wanted_locked() and "fabric" not in self._helpers:
+                    self._spawn_locked("fabric")
+                    self.stats["fabric_respawns"] = self.stats.get("fabric_respawns", 0) + 1
+        t = threading.Timer(self.FABRIC_RESPAWN_DEBOUNCE_S, fire)
+        t.daemon = True
+        t.start()
 
     def parked(self) -> set[str]:
         with self._mu:

@@ -228,6 +228,38 @@ def test_resident_fabric_helper_is_warm_before_ready_and_replaced_after_a_kill()
         pool.stop()
 
 
+def test_a_burst_of_parks_restarts_the_fabric_helper_once():
+    """Parking several GPUs at once (a drain, a gang's pods starting) stops the resident fabric
+    helper at once — it has a context on each of them — and starts it again once, over the GPUs
+    still pod-free at the end of the burst; unparking them brings them back the same way."""
+    from gpupool.agent.probehost import HelperPool
+    devs = [{"uuid": f"g{i}", "index": i} for i in range(4)]
+    pool = HelperPool("sim", sim_ms=1, resident_fabric=True)
+    try:
+        pool.start(devs)
+        assert wait(lambda: pool.alive("fabric"))
+        first = pool.snapshot()["fabric"]["pid"]
+        starts = pool.stats["helper_starts"]
+        for u in ("g0", "g1"):
+            assert pool.park(u)
+        assert not pool.alive("fabric")  # gone at once: it had a context on g0 and g1
+        assert wait(lambda: pool.alive("fabric"))
+        time.sleep(2 * pool.FABRIC_RESPAWN_DEBOUNCE_S)
+        assert pool.snapshot()["fabric"]["pid"] != first
+        assert pool.stats["helper_starts"] == starts + 1  # one start for the two parks
+        assert pool.stats["fabric_respawns"] == 1
+        assert wait(lambda: (pool.snapshot()["fabric"].get("warm") or {}).get("links") == 2)
+        for u in ("g0", "g1"):
+            pool.unpark(u)
+        assert wait(lambda: pool.alive("fabric") and
+                    (pool.snapshot()["fabric"].get("warm") or {}).get("links") == 12)
+        time.sleep(2 * pool.FABRIC_RESPAWN_DEBOUNCE_S)
+        assert pool.stats["fabric_respawns"] == 2
+        assert wait(lambda: all(pool.alive(f"g{i}") for i in range(4)))
+    finally:
+        pool.stop()
+
+
 def test_on_demand_fabric_helper_is_not_replaced():
     from gpupool.agent.probehost import HelperPool
     devs = [{"uuid": f"g{i}", "index": i} for i in range(2)]
