@@ -83,6 +83,11 @@ class AgentAuth:
     def required(self) -> bool:
         return self.verifier is not None or self.token is not None
 
+    @staticmethod
+    def presented(headers: dict) -> bool:
+        """Does the request carry any credential at all?"""
+        return edsig.HEADER in headers or "authorization" in headers
+
     def check_head(self, method: str, target: str, headers: dict) -> str | None:
         if not self.required:
             return None
@@ -117,5 +122,10 @@ class AgentAuth:
         self.stats[k] = self.stats.get(k, 0) + 1
 
     def metrics_lines(self) -> list[str]:
-        return [f'gpupool_agent_rpc_auth_total{{result="{k}"}} {v}'
-                for k, v in sorted(self.stats.items())]
+        out = [f'gpupool_agent_rpc_auth_total{{result="{k}"}} {v}'
+               for k, v in sorted(self.stats.items())]
+        if self.verifier is not None:  # key rotation: what this agent trusts and sees in use
+            out += [f'gpupool_agent_trusted_key{{keyId="{k}"}} 1' for k in self.verifier.trusted()]
+            out += [f'gpupool_agent_rpc_signatures_total{{keyId="{k}"}} {v}'
+                    for k, v in sorted(self.verifier.accepted.items())]
+        return out

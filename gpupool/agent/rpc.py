@@ -368,8 +368,13 @@ class RpcServer:
                     k, _, v = h.decode("latin-1").partition(":")
                     headers[k.strip().lower()] = v.strip()
                 path = target.partition("?")[0]
-                # credentials before the body: an unauthenticated peer never gets a byte buffered
-                why = self.auth.check_head(method, target, headers)
+                # credentials before the body: an unauthenticated peer never gets a byte buffered.
+                # An open path asked without credentials (a Prometheus scrape, a probe) is served
+                # untrusted and not counted as a refused credential
+                if path in OPEN_PATHS and not self.auth.presented(headers):
+                    why = "NoCredentials" if self.auth.required else None
+                else:
+                    why = self.auth.check_head(method, target, headers)
                 authed = why is None
                 if not authed and path not in OPEN_PATHS:
                     self._reject(conn, 401, why or "Unauthorized",

@@ -12,6 +12,7 @@
   gpuctl logs POD [-f] [--tail N]         the pod's log (pods/log)
   gpuctl create namespace NAME | secret generic NAME --from-literal k=v | configmap NAME ...
   gpuctl run NAME --image IMG [--gpus N] [--rm] -- CMD...   one pod; --rm: wait, log, delete
+  gpuctl keys [status|init|rotate|prune]  the manager's agent-RPC signing key, rotated in steps
   gpuctl events [-n NS]
   gpuctl devices NODE                     the node agent's live device view
   gpuctl gpu cordon|uncordon NODE GPU     per-GPU maintenance (replace it in its pool, never claim)
@@ -466,6 +467,11 @@ def cmd_create(c: Client, ns: str, args) -> int:
                        "metadata": {"name": name}, "data": enc}, ns)
     print(f"secret/{name} created")
     return 0
+
+
+def cmd_keys(c: Client, ns: str, args) -> int:
+    from . import keys
+    return keys.main(c, args)
 
 
 def cmd_run(c: Client, ns: str, args) -> int:
@@ -1016,6 +1022,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("pod")
     p.add_argument("-f", "--follow", action="store_true")
     p.add_argument("--tail", type=int, default=None)
+    p = sub.add_parser("keys", help="the manager's agent-RPC signing key (gpupool/cli/keys.py)")
+    p.add_argument("keys_cmd", choices=["status", "init", "rotate", "prune"], nargs="?",
+                   default="status")
+    p.add_argument("--force", action="store_true", help="skip the check on the agents")
+    p.add_argument("--key-namespace", default=None, help="default: gpupool-system")
     p = sub.add_parser("create")
     p.add_argument("what", choices=["namespace", "secret", "configmap"])
     p.add_argument("name", nargs="+", help="NAME, or 'generic NAME' for a secret")
@@ -1111,7 +1122,7 @@ def main(argv: list[str] | None = None) -> int:
     fn = {"apply": cmd_apply, "diff": cmd_diff, "get": cmd_get, "describe": cmd_describe,
           "delete": cmd_delete,
           "scale": cmd_scale, "wait": cmd_wait, "logs": cmd_logs, "events": cmd_events,
-          "create": cmd_create, "run": cmd_run,
+          "create": cmd_create, "run": cmd_run, "keys": cmd_keys,
           "devices": cmd_devices, "install": cmd_install, "render": cmd_render,
           "gpu": cmd_gpu, "trainjob": cmd_trainjob, "whoami": cmd_whoami, "top": cmd_top}[args.cmd]
     try:

@@ -90,6 +90,15 @@ def load_public_keys(pem: str) -> list[bytes]:
     return out
 
 
+def private_pem(seed: bytes) -> str:
+    """A 32-byte seed as an Ed25519 PKCS#8 ``PRIVATE KEY`` PEM (what ``openssl genpkey`` writes);
+    a fresh key is ``private_pem(os.urandom(32))`` — any 32 bytes are an Ed25519 seed."""
+    if len(seed) != 32:
+        raise ValueError("an Ed25519 seed is 32 bytes")
+    b = base64.b64encode(_PRIV_DER + seed).decode()
+    return "-----BEGIN PRIVATE KEY-----\n" + b + "\n-----END PRIVATE KEY-----\n"
+
+
 def public_pem(raw: bytes) -> str:
     b = base64.b64encode(_PUB_DER + raw).decode()
     return "-----BEGIN PUBLIC KEY-----\n" + b + "\n-----END PUBLIC KEY-----\n"
@@ -256,6 +265,7 @@ class Verifier:
         self._mu = threading.Lock()
         self._nonces: dict[str, int] = {}
         self.rejected: dict[str, int] = {}
+        self.accepted: dict[str, int] = {}  # key id -> requests it signed (rotation progress)
         self._load(force=True)
 
     def _files(self) -> list[str]:
@@ -286,6 +296,12 @@ class Verifier:
                 continue
         if keys or force:
             self.keys, self._sig = keys, sig
+
+    def trusted(self) -> list[str]:
+        """Ids of the public keys currently trusted (re-read from the bundle first)."""
+        with self._mu:
+            self._load()
+            return sorted(self.keys)
 
     def _reject(self, why: str) -> str:
         self.rejected[why] = self.rejected.get(why, 0) + 1
@@ -324,6 +340,7 @@ class Verifier:
             if h["nonce"] in self._nonces:
                 return self._reject("Replay")
             self._nonces[h["nonce"]] = ts + self.skew_ms
+            self.accepted[h["keyId"]] = self.accepted.get(h["keyId"], 0) + 1
             if len(self._nonces) > 4096:
                 # keep a nonce while its timestamp still passes the skew check (now <= ts+skew)
                 self._nonces = {n: e for n, e in self._nonces.items() if e >= now}
