@@ -745,12 +745,20 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
   }
 
   // ---- deadline
+  // a running gang is re-checked on its pods' events (the pod index wakes it); the resync is a
+  // safety net, never later than the job's deadline
+  auto running_resync = pods_idx_ ? opts_.resync * 6 : opts_.resync;
   if (spec.active_deadline_seconds > 0) {
     std::chrono::system_clock::time_point started;
-    if (parse_rfc3339(cst["startTime"].as_string(), &started) &&
-        now_tp - started > std::chrono::seconds(spec.active_deadline_seconds))
-      return finish_(obj, m, spec, st, "Failed", "DeadlineExceeded",
-                     "ran longer than activeDeadlineSeconds=" + std::to_string(spec.active_deadline_seconds), pods);
+    if (parse_rfc3339(cst["startTime"].as_string(), &started)) {
+      const auto end = started + std::chrono::seconds(spec.active_deadline_seconds);
+      if (now_tp > end)
+        return finish_(obj, m, spec, st, "Failed", "DeadlineExceeded",
+                       "ran longer than activeDeadlineSeconds=" + std::to_string(spec.active_deadline_seconds),
+                       pods);
+      const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(end - now_tp) + ms(50);
+      if (left < running_resync) running_resync = left;
+    }
   }
 
   int attempt = static_cast<int>(cst["attempt"].as_int(0));
@@ -978,7 +986,7 @@ Outcome Mi355xJobReconciler::reconcile(const std::string& ns, const std::string&
                   now);
     st["conditions"] = conds;
     write_status_(obj, st);
-    return Outcome::done(opts_.resync);
+    return Outcome::done(running_resync);
   }
   st["phase"] = phase == "Running" ? "Running" : "Pending";
   st["conditions"] = conds;
