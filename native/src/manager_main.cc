@@ -617,8 +617,10 @@ int main(int argc, char** argv) {
       cloud_impl = std::make_unique<FakeCloudProvider>(fco);
     }
     CloudProvider& cloud = *cloud_impl;
+    // jobs are driven by their own events, their pods' (the pod index below) and their
+    // reconciler's requeues: the informer's RESYNC re-delivery is only a drift net, once a minute
     Informer jobs(client, ResourceRef{gen::kGroup, gen::kVersion, gen::kPluralMi355xJob, true, "Mi355xJob"}, f.ns,
-                  std::chrono::milliseconds(f.resync_ms));
+                  std::chrono::milliseconds(f.resync_ms) * 6);
     // the cluster's pods, bounded: only pods that request an extended resource or belong to a
     // Mi355xJob are cached, each as a projection of the fields the readers use (podindex.h) —
     // whole pods of every workload in a 50k-pod cluster would not fit the manager's 512 Mi

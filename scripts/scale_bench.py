@@ -263,7 +263,12 @@ def jobs_mode(a) -> int:
                                                   _sum(m0, "gpupool_reconcile_total")),
                           "steady_per_min": round((_sum(m2, "gpupool_reconcile_total") -
                                                    _sum(m1, "gpupool_reconcile_total")) * 60.0 /
-                                                  a.steady_s, 1)},
+                                                  a.steady_s, 1),
+                          "steady_per_min_by_label": {
+                              k2.split("{", 1)[1].rstrip("}"): round((v - m1.get(k2, 0)) * 60.0 /
+                                                                     a.steady_s, 1)
+                              for k2, v in m2.items() if k2.startswith("gpupool_reconcile_total{")
+                              and v - m1.get(k2, 0) > 0}},
            "manager": {"cpu_s_placement": round(u1["cpu_s"] - u0["cpu_s"], 3),
                        "cpu_s_steady_per_min": round((u2["cpu_s"] - u1["cpu_s"]) * 60.0 /
                                                      a.steady_s, 3),
