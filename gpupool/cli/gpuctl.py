@@ -4,7 +4,7 @@
                                           kubectl apply (README.md:288-290): three-way merge with
                                           the last applied configuration, or server-side apply
   gpuctl diff -f FILE [--server-side]     what apply would change (server dry run), exit 1 if any
-  gpuctl get KIND [NAME] [-o wide|yaml|json] [-l SEL] [-A]   server-side printing (printer columns)
+  gpuctl get KIND [NAME] [-o wide|yaml|json|name|jsonpath=TPL] [-l SEL] [-A]   server-side printing
   gpuctl describe KIND NAME               spec/status, conditions table, devices, events
   gpuctl delete KIND NAME | -f FILE [--wait]
   gpuctl scale KIND NAME --replicas N     via the scale subresource
@@ -228,9 +228,23 @@ def cmd_diff(c: Client, ns: str, args) -> int:
 def cmd_get(c: Client, ns: str, args) -> int:
     res = resolve(c, args.kind)
     target_ns = None if (args.all_namespaces or not res.namespaced) else ns
-    if args.output in ("yaml", "json"):
+    if args.output in ("yaml", "json") or args.output.startswith("jsonpath=") or \
+            args.output == "name":
         out = c.get(res, args.name, target_ns) if args.name else \
             c.list(res, target_ns, label_selector=args.selector)
+        if args.output == "name":  # kubectl get -o name: kind.group/name per object
+            for o in ([out] if args.name else out["items"]):
+                kind = (o.get("kind") or res.plural.rstrip("s")).lower()
+                print(f"{kind}{'.' + res.group if res.group else ''}/{o['metadata']['name']}")
+            return 0
+        if args.output.startswith("jsonpath="):
+            from .jsonpath import JsonPathError, render
+            try:
+                sys.stdout.write(render(out, args.output.split("=", 1)[1]))
+            except JsonPathError as e:
+                print(f"error: {e}", file=sys.stderr)
+                return 1
+            return 0
         dump(out, args.output)
         return 0
     tbl = c.table(res, target_ns, args.name, label_selector=args.selector)
@@ -365,13 +379,16 @@ def parse_for(cond: str):
             o["metadata"].get("generation")
             for x in (o.get("status") or {}).get("conditions", []))
     if cond.startswith("jsonpath="):
-        path, _, want = cond.split("=", 1)[1].partition("=")
+        from .jsonpath import _str, evaluate
+        spec = cond.split("=", 1)[1]
+        if spec.startswith("{"):  # kubectl form: jsonpath='{.status.readyReplicas}'=2
+            j = spec.index("}")
+            path, want = spec[1:j], spec[j + 1:].lstrip("=")
+        else:
+            path, _, want = spec.partition("=")
 
         def pred(o):
-            cur: Any = o
-            for p in path.strip(".").split("."):
-                cur = cur.get(p) if isinstance(cur, dict) else None
-            return o is not None and str(cur) == want
+            return o is not None and any(_str(v) == want for v in evaluate(o, path))
         return pred
     raise SystemExit(f"error: unsupported --for {cond}")
 

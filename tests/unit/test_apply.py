@@ -226,3 +226,31 @@ def test_gpuctl_diff_shows_what_apply_would_change(tmp_path, capsys):
     assert 'conflict with "before-first-apply": .spec.replicas' in capsys.readouterr().err
     assert gpuctl.main(base + ["diff", "--server-side", "--force-conflicts", "-f", str(f)]) == 1
     assert "+  replicas: 3" in capsys.readouterr().out
+
+
+def test_jsonpath_output_and_wait(capsys):
+    """``kubectl get -o jsonpath=`` / ``-o name`` and ``wait --for=jsonpath=`` (the reference's
+    scripts read readyReplicas this way)."""
+    from gpupool.cli.jsonpath import JsonPathError, render
+    o = {"items": [{"metadata": {"name": "a", "annotations": {"gpupool.amd.com/x": "1"}},
+                    "status": {"readyReplicas": 2, "conditions": [
+                        {"type": "Ready", "status": "True"}, {"type": "X", "status": "False"}]}},
+                   {"metadata": {"name": "b"}, "status": {"readyReplicas": 0}}]}
+    assert render(o, '{range .items[*]}{.metadata.name}{"\\t"}{.status.readyReplicas}{"\\n"}{end}') \
+        == "a\t2\nb\t0\n"
+    assert render(o, "{.items[*].metadata.name}") == "a b"
+    assert render(o, '{.items[0].status.conditions[?(@.type=="Ready")].status}') == "True"
+    assert render(o, "{.items[0].metadata.annotations['gpupool.amd.com/x']}") == "1"
+    assert render(o, "{.items[-1].metadata}") == '{"name":"b"}'
+    with pytest.raises(JsonPathError):
+        render(o, "{range .items[*]}{.x}")
+    sim = SimThread()
+    c = Client(sim.url)
+    c.create(CONFIGMAPS, _cm({"a": "1"}, "one"), "default")
+    base = ["--server", sim.url, "-n", "default"]
+    assert gpuctl.main(base + ["get", "configmaps", "-o", "name"]) == 0
+    assert "configmap/one" in capsys.readouterr().out.split()
+    assert gpuctl.main(base + ["get", "configmaps", "one", "-o", "jsonpath={.data.a}"]) == 0
+    assert capsys.readouterr().out == "1"
+    assert gpuctl.main(base + ["wait", "configmaps", "one", "--for",
+                               "jsonpath={.data.a}=1", "--timeout", "5"]) == 0
