@@ -6,7 +6,6 @@ import json
 import os
 import sys
 
-
 from ..api import schema
 from ..kube import NODES, PODS, Client, KubeError
 from .common import dump

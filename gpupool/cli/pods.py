@@ -7,7 +7,6 @@ import os
 import sys
 from typing import Any
 
-
 from ..kube import EVENTS, PODS, Client, KubeError
 from .common import print_table
 
