@@ -212,6 +212,7 @@ class Agent(HealthMixin, AccountingMixin, PodViewMixin, ClaimsMixin, XgmiMixin,
         self._threads: list[threading.Thread] = []
         self.registrar = None  # nodereg.NodeRegistrar once register_node ran
         self._api = None       # apiserver client (api())
+        self._kx = None        # X25519 key of the per-node RPC MAC (kx)
         self._park_mu = threading.Lock()  # podview._sync_parking
         from .scrubber import HbmScrubber
         self.scrubber = HbmScrubber(self, cfg.scrub_interval_s, cfg.scrub_window_bytes,
@@ -470,8 +471,10 @@ class Agent(HealthMixin, AccountingMixin, PodViewMixin, ClaimsMixin, XgmiMixin,
         if parts:
             labels["amd.com/compute-partition"] = parts[0]
         c = client or self.api()
-        return NodeRegistrar(c, self.cfg.node, labels,
-                             {schema.ANN_AGENT_ENDPOINT: self.endpoint()}, self._node_conditions)
+        ann = {schema.ANN_AGENT_ENDPOINT: self.endpoint()}
+        if self.kx is not None:  # the per-node MAC key's public half (edsig v2)
+            ann[schema.ANN_AGENT_KX] = self.kx.annotation()
+        return NodeRegistrar(c, self.cfg.node, labels, ann, self._node_conditions)
 
     def api(self):
         """The agent's apiserver client: one per process (per-thread keep-alive connections), its
@@ -501,12 +504,21 @@ class Agent(HealthMixin, AccountingMixin, PodViewMixin, ClaimsMixin, XgmiMixin,
         rotating shared token."""
         from ..utils import edsig
         from .auth import AgentAuth, TokenAuth
-        ver = edsig.Verifier(self.cfg.manager_pubkeys, self.cfg.node) \
+        ver = edsig.Verifier(self.cfg.manager_pubkeys, self.cfg.node, kx=self.kx) \
             if self.cfg.manager_pubkeys else None
         tok = None
         if self.cfg.auth_token_file or self.cfg.auth_token:
             tok = TokenAuth(self.cfg.auth_token, self.cfg.auth_token_file, self.cfg.auth_grace_s)
         return AgentAuth(ver, tok)
+
+    @property
+    def kx(self):
+        """This agent's X25519 key (state dir; None without manager public keys)."""
+        if self._kx is None and self.cfg.manager_pubkeys:
+            from ..utils import edsig
+            os.makedirs(self.cfg.state_dir, exist_ok=True)
+            self._kx = edsig.AgentKx(os.path.join(self.cfg.state_dir, "agent-kx.key"))
+        return self._kx
 
     def endpoint(self) -> str:
         if self.cfg.endpoint:

@@ -128,4 +128,7 @@ class AgentAuth:
             out += [f'gpupool_agent_trusted_key{{keyId="{k}"}} 1' for k in self.verifier.trusted()]
             out += [f'gpupool_agent_rpc_signatures_total{{keyId="{k}"}} {v}'
                     for k, v in sorted(self.verifier.accepted.items())]
+            # v1: Ed25519 signature; v2: the per-node MAC (edsig.py)
+            out += [f'gpupool_agent_rpc_signature_versions_total{{version="{k}"}} {v}'
+                    for k, v in sorted(self.verifier.by_version.items())]
         return out

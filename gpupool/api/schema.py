@@ -30,6 +30,9 @@ FINALIZER = "compute.my.domain/device-release"
 
 # Well-known annotation/label keys shared by agent, manager and kubelet-fake.
 ANN_AGENT_ENDPOINT = "gpupool.amd.com/agent-endpoint"
+# the agent's X25519 key-exchange public key (base64url): the manager derives the per-node MAC
+# key of its RPCs from it (gpupool/utils/edsig.py, v2)
+ANN_AGENT_KX = "gpupool.amd.com/agent-kx"
 ANN_POD_DEVICES = "gpupool.amd.com/devices"
 LABEL_GFX = "amd.com/gpu.family"
 LABEL_POOL = "gpupool.amd.com/pool"

@@ -481,8 +481,8 @@ class Client:
                     return
                 try:
                     chunk = resp.read1(65536) if hasattr(resp, "read1") else resp.read(1)
-                except (OSError, ValueError):
-                    if stop is not None and stop.is_set():
+                except (OSError, ValueError, http.client.HTTPException):
+                    if stop is not None and stop.is_set():  # our own shutdown of the socket
                         return
                     raise
                 if not chunk:

@@ -285,7 +285,9 @@ class RocmProvider : public DeviceProvider {
     bool schedulable = true;
     std::string annotation;  // gpupool.amd.com/agent-endpoint as the Node carries it
     std::string endpoint;    // what the manager calls (derived per AgentAccess::discovery)
+    std::string kx;          // gpupool.amd.com/agent-kx: the agent's X25519 key (v2 MAC)
   };
+  std::string agent_kx_(const std::string& node);
   std::mutex facts_mu_;
   std::map<std::string, NodeFacts> facts_;
   // pod discovery: node -> (agent pod "ns/name" -> its address) of Running, undeleted agent pods

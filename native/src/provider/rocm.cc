@@ -134,6 +134,7 @@ void RocmProvider::note_node_(const std::string& type, const Json& obj) {
   f.labels = obj.path("metadata.labels").is_object() ? obj.path("metadata.labels") : Json::object();
   f.schedulable = !obj.path("spec.unschedulable").as_bool(false);
   f.annotation = obj.path("metadata.annotations")[gen::kAnnAgentEndpoint].str_or("");
+  f.kx = obj.path("metadata.annotations")[gen::kAnnAgentKx].str_or("");
   derive_endpoint_(name, f);
 }
 
@@ -207,13 +208,20 @@ std::unique_ptr<HttpClient> RocmProvider::new_client(const std::string& node, co
     // signatures replace the bearer: the endpoint gets nothing it could replay elsewhere
     c = std::make_unique<HttpClient>(Url::parse(endpoint), std::shared_ptr<TokenSource>(), timeout_ms, access_.tls);
     std::shared_ptr<AgentSigner> signer = access_.signer;
-    c->set_signer([signer, node](const std::string& m, const std::string& target, const std::string& body) {
-      return signer->header(m, target, node, body);
+    // v2 (a MAC keyed per node) once the agent has published its key-exchange key, else v1
+    c->set_signer([this, signer, node](const std::string& m, const std::string& target, const std::string& body) {
+      return signer->header(m, target, node, body, agent_kx_(node));
     });
   } else {
     c = std::make_unique<HttpClient>(Url::parse(endpoint), access_.token, timeout_ms, access_.tls);
   }
   return c;
+}
+
+std::string RocmProvider::agent_kx_(const std::string& node) {
+  std::lock_guard<std::mutex> g(facts_mu_);
+  auto it = facts_.find(node);
+  return it == facts_.end() ? std::string() : it->second.kx;
 }
 
 std::vector<std::string> RocmProvider::node_names() {

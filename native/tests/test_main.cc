@@ -8,9 +8,10 @@
 int main(int argc, char** argv) {
   // `gpupool_tests --sign KEY METHOD TARGET NODE BODY`: print the manager's signature header for
   // one request (tests/unit/test_edsig.py checks it against the agent's Python verifier)
-  if (argc == 7 && std::strcmp(argv[1], "--sign") == 0) {
+  // (with an 8th argument, the agent's base64url X25519 key: the v2 per-node MAC header)
+  if ((argc == 7 || argc == 8) && std::strcmp(argv[1], "--sign") == 0) {
     gpupool::AgentSigner s(argv[2]);
-    std::fputs(s.header(argv[3], argv[4], argv[5], argv[6]).c_str(), stdout);
+    std::fputs(s.header(argv[3], argv[4], argv[5], argv[6], argc == 8 ? argv[7] : "").c_str(), stdout);
     return 0;
   }
   const char* filter = argc > 1 ? argv[1] : "";

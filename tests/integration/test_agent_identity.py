@@ -104,6 +104,8 @@ def test_pod_discovery_ignores_a_redirected_annotation(cluster_factory):
         # the agents saw only signed requests for themselves
         am = c.agent_request("node-b", "GET", "/metrics")
         assert 'gpupool_agent_rpc_auth_total{result="signature"}' in am
+        # once the agent's key-exchange key is on its Node, the manager MACs per node (v2)
+        assert 'gpupool_agent_rpc_signature_versions_total{version="v2"}' in am
     finally:
         rogue.close()
 

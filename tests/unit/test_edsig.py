@@ -88,6 +88,38 @@ def test_cpp_signer_matches_python_verifier(keys, native_built):
     assert v.check_body(h, b'{"a":1}') is None
 
 
+def test_cpp_mac_matches_python_verifier(keys, native_built, tmp_path):
+    """v2: the C++ signer derives the same per-node MAC key from the agent's X25519 key as the
+    agent does from the manager's Ed25519 public key (one point on two curves); a MAC for
+    another node, another agent key or a tampered request is refused."""
+    exe = os.path.join(native_built, "gpupool_tests")
+    kx = edsig.AgentKx(str(tmp_path / "agent-kx.key"))
+    out = subprocess.run([exe, "--sign", keys["k1"], "POST", "/v1/claims?x=1", "node-b",
+                          '{"a":1}', kx.annotation()], capture_output=True, text=True, timeout=30)
+    assert out.returncode == 0, out.stderr
+    line = out.stdout.strip()
+    assert line.startswith("X-Gpupool-Signature: v2 ") and f"kx={kx.id}" in line
+    h = {edsig.HEADER: line.split(": ", 1)[1]}
+    v = edsig.Verifier(keys["p1"], "node-b", kx=kx)
+    assert v.check_head("POST", "/v1/claims?x=1", dict(h)) is None
+    assert v.check_body(h, b'{"a":1}') is None
+    assert v.by_version == {"v2": 1}
+    assert v.check_head("POST", "/v1/claims?x=1", dict(h)) == "Replay"
+    assert edsig.Verifier(keys["p1"], "node-b", kx=edsig.AgentKx(str(tmp_path / "o.key"))) \
+        .check_head("POST", "/v1/claims?x=1", dict(h)) == "StaleAgentKey"
+    assert edsig.Verifier(keys["p1"], "node-b").check_head("POST", "/v1/claims?x=1", dict(h)) \
+        == "NoAgentKey"
+    out = subprocess.run([exe, "--sign", keys["k1"], "POST", "/v1/release", "node-b", "{}",
+                          kx.annotation()], capture_output=True, text=True, timeout=30)
+    h2 = {edsig.HEADER: out.stdout.strip().split(": ", 1)[1]}
+    assert v.check_head("POST", "/v1/claims", dict(h2)) == "BadSignature"  # another target
+    # the Ed25519 -> X25519 map: the manager's X25519 public key from its seed and the agent's
+    # from the Ed25519 public key it trusts are the same bytes
+    seed = edsig.load_private_key(open(keys["k1"]).read())
+    assert edsig.x25519_public(edsig.x25519_private_from_ed25519_seed(seed)) == \
+        edsig.x25519_from_ed25519_public(edsig.public_from_private(seed))
+
+
 def _server(auth):
     routes = {("POST", "/v1/claims"): lambda q, b: json_reply({"ok": True, "n": len(b)}),
               ("GET", "/v1/node"): lambda q, b: json_reply({"node": "node-b"})}
