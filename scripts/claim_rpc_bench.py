@@ -70,8 +70,32 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--count", type=int, default=1)
     ap.add_argument("--gap", type=float, default=0.05, help="idle seconds between cycles")
+    ap.add_argument("--auth", choices=["none", "v1", "v2"], default="none",
+                    help="sign the calls as the manager does: v1 Ed25519, v2 the per-node MAC")
     args = ap.parse_args()
     d = tempfile.mkdtemp(prefix="claimbench", dir="/tmp")
+    auth_args: list[str] = []
+    signer = None
+    if args.auth != "none":
+        from gpupool.utils import edsig
+        seed = os.urandom(32)
+        pub = edsig.public_from_private(seed)
+        with open(os.path.join(d, "manager.pem"), "w") as f:
+            f.write(edsig.public_pem(pub))
+        auth_args = ["--manager-pubkeys", os.path.join(d, "manager.pem")]
+
+        def signer(method: str, path: str, body: bytes) -> dict:
+            if args.auth == "v1":
+                return {"X-Gpupool-Signature": edsig.sign_header(seed, method, path, "n0", body,
+                                                                 pub=pub)}
+            kx = edsig.AgentKx(os.path.join(d, "state", "agent-kx.key"))  # the agent's, read once
+            if not hasattr(signer, "key"):
+                xm_priv = edsig.x25519_private_from_ed25519_seed(seed)
+                xm = edsig.x25519_public(xm_priv)
+                signer.key = edsig.mac_key(edsig.x25519(xm_priv, kx.public), "n0", xm, kx.public)
+                signer.kx = kx.public
+            return {"X-Gpupool-Signature": edsig.mac_header(signer.key, edsig.key_id(pub),
+                                                            signer.kx, method, path, "n0", body)}
     # the kubelet is its own process (as on a node): its stream reader must not share this
     # client's GIL
     kubelet = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--kubelet",
@@ -87,7 +111,7 @@ def main() -> int:
          "--fixture", os.path.join(ROOT, "tests", "fixtures", "node_8x_mi355x.json"),
          "--state-dir", os.path.join(d, "state"), "--socket", sock,
          "--plugin-dir", os.path.join(d, "dp"), "--probe", "simulated", "--probe-sim-ms", "1",
-         "--scrub-interval", "0", "--ready-file", ready],
+         "--scrub-interval", "0", "--ready-file", ready, *auth_args],
         cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT), stderr=open("/tmp/agent_claimbench.err", "w"))
     try:
         deadline = time.monotonic() + 60
@@ -95,9 +119,12 @@ def main() -> int:
             time.sleep(0.05)
         conn = UnixHTTP(sock)
 
+        def hdrs(path: str, b: bytes) -> dict:
+            return {"Content-Type": "application/json", **(signer("POST", path, b) if signer else {})}
+
         def call(path: str, body: dict) -> dict:
             b = json.dumps(body).encode()
-            conn.request("POST", path, b, {"Content-Type": "application/json"})
+            conn.request("POST", path, b, hdrs(path, b))
             r = conn.getresponse()
             return json.loads(r.read())
 
@@ -106,9 +133,10 @@ def main() -> int:
                "probe": {"enabled": True}}
         rows = []
         for i in range(args.warmup + args.iters):
+            b = json.dumps(req).encode()
+            h = hdrs("/v1/claims", b)  # signed outside the timed window (the manager's C++ cost)
             t0 = time.perf_counter()
-            conn.request("POST", "/v1/claims", json.dumps(req).encode(),
-                         {"Content-Type": "application/json"})
+            conn.request("POST", "/v1/claims", b, h)
             raw = conn.getresponse().read()
             rt = (time.perf_counter() - t0) * 1e3
             out = json.loads(raw)
