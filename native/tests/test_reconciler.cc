@@ -4,6 +4,10 @@
 #include "gpupool/reconciler.h"
 #include "testing.h"
 
+#include <algorithm>
+#include <map>
+#include <random>
+
 using gpupool::DeviceView;
 using gpupool::Json;
 using gpupool::Mi355xPoolSpec;
@@ -170,4 +174,74 @@ TEST(pod_index_tracks_live_extended_requests_and_job_pods) {
   EXPECT_TRUE(gpupool::pod_relevant(only_init));
   EXPECT_TRUE(gpupool::trim_pod(only_init).path("spec.initContainers")[0]["resources"]["limits"]["amd.com/gpu"]
                   .as_string() == "1");
+}
+
+// Randomised: after every ADDED / MODIFIED / DELETED event the incremental per-node usage equals a
+// recount of the live pods from scratch (phases, node moves of unscheduled pods, init containers,
+// requests without limits, pods that ask for nothing), and job membership follows the label.
+TEST(pod_index_matches_a_recount_under_random_events) {
+  using gpupool::Json;
+  std::mt19937 rng(12345);
+  auto pick = [&](int n) { return static_cast<int>(rng() % static_cast<unsigned>(n)); };
+  const char* phases[] = {"Pending", "Running", "Succeeded", "Failed"};
+  const char* nodes[] = {"", "n1", "n2", "n3"};
+  std::map<std::string, Json> live;
+  gpupool::PodIndex idx;
+  for (int step = 0; step < 3000; ++step) {
+    const std::string name = "p" + std::to_string(pick(40));
+    if (live.count(name) && pick(5) == 0) {
+      idx.on_event("DELETED", live[name]);
+      live.erase(name);
+    } else {
+      Json p = Json::parse(R"({"metadata":{"name":"","namespace":"ns","labels":{}},"spec":{"containers":[]},"status":{}})");
+      p["metadata"]["name"] = name;
+      if (pick(3) == 0) p["metadata"]["labels"]["gpupool.amd.com/job-name"] = pick(2) ? "j1" : "j2";
+      const std::string node = nodes[pick(4)];
+      if (!node.empty()) p["spec"]["nodeName"] = node;
+      p["status"]["phase"] = phases[pick(4)];
+      for (int c = 0, n = pick(3); c < n; ++c) {
+        Json ctr = Json::object();
+        ctr["name"] = "c" + std::to_string(c);
+        const std::string part = pick(2) ? "limits" : "requests";
+        if (pick(4)) ctr["resources"][part]["amd.com/gpu"] = std::to_string(pick(4));
+        p["spec"]["containers"].push_back(ctr);
+      }
+      if (pick(4) == 0) {
+        Json init = Json::object();
+        init["name"] = "init";
+        init["resources"]["limits"]["amd.com/gpu"] = std::to_string(pick(6));
+        p["spec"]["initContainers"] = Json::array();
+        p["spec"]["initContainers"].push_back(init);
+      }
+      idx.on_event(live.count(name) ? "MODIFIED" : "ADDED", p);
+      live[name] = p;
+    }
+    // the recount
+    std::map<std::string, int64_t> want;
+    for (const auto& kv : live) {
+      const Json& p = kv.second;
+      const std::string node = p.path("spec.nodeName").as_string();
+      const std::string phase = p.path("status.phase").as_string();
+      if (node.empty() || phase == "Succeeded" || phase == "Failed") continue;
+      int64_t sum = 0, init = 0;
+      for (const auto& c : p.path("spec.containers").elements()) {
+        const Json& r = c["resources"];
+        const std::string v = r["limits"]["amd.com/gpu"].is_string() ? r["limits"]["amd.com/gpu"].as_string()
+                              : r["requests"]["amd.com/gpu"].as_string();
+        sum += v.empty() ? 0 : std::stoll(v);
+      }
+      for (const auto& c : p.path("spec.initContainers").elements())
+        init = std::max<int64_t>(init, std::stoll(c["resources"]["limits"]["amd.com/gpu"].as_string()));
+      const int64_t n = std::max(sum, init);
+      if (n > 0) want[node] += n;
+    }
+    auto got = idx.requested_by_node("amd.com/gpu");
+    EXPECT_TRUE(got == want);
+    if (got != want) return;
+    size_t members = 0;
+    for (const auto& kv : live)
+      members += kv.second.path("metadata.labels")["gpupool.amd.com/job-name"].as_string() == "j1";
+    EXPECT_TRUE(idx.job_pods("ns", "j1").size() == members);
+  }
+  EXPECT_TRUE(idx.size() == live.size());
 }
