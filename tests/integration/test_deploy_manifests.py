@@ -4,6 +4,7 @@ to the apiserver simulator through gpuctl; and the RBAC grants cover every API c
 and agent make (audited against their sources)."""
 from __future__ import annotations
 
+import glob
 import os
 import re
 import subprocess
@@ -162,8 +163,7 @@ def test_alert_rules_use_exported_metrics():
     (C++ sources) or the node agent, with the label values the rules select on."""
     import yaml
     doc = yaml.safe_load(open(os.path.join(ROOT, "config", "prometheus", "alerts.yaml")))
-    src = open(os.path.join(ROOT, "gpupool", "agent", "agent.py")).read()
-    src += open(os.path.join(ROOT, "gpupool", "agent", "rpc.py")).read()  # agent RPC counters
+    src = "".join(open(f).read() for f in glob.glob(os.path.join(ROOT, "gpupool", "agent", "*.py")))
     for dirpath, _, files in os.walk(os.path.join(ROOT, "native", "src")):
         for f in files:
             if f.endswith(".cc"):
