@@ -288,6 +288,11 @@ class RocmProvider : public DeviceProvider {
     std::string kx;          // gpupool.amd.com/agent-kx: the agent's X25519 key (v2 MAC)
   };
   std::string agent_kx_(const std::string& node);
+  // a 401 StaleAgentKey / NoAgentKey: the agent has another key-exchange key than its Node says
+  // (a wiped state dir, a restart racing its re-registration) — stop MACing with that key until
+  // the Node shows a different one (Ed25519 meanwhile); true when the request should be re-sent
+  bool stale_kx_(const std::string& node, const HttpResponse& r);
+  std::map<std::string, std::string> bad_kx_;  // node -> kx the agent refused (under facts_mu_)
   std::mutex facts_mu_;
   std::map<std::string, NodeFacts> facts_;
   // pod discovery: node -> (agent pod "ns/name" -> its address) of Running, undeleted agent pods

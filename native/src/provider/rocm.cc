@@ -221,7 +221,24 @@ std::unique_ptr<HttpClient> RocmProvider::new_client(const std::string& node, co
 std::string RocmProvider::agent_kx_(const std::string& node) {
   std::lock_guard<std::mutex> g(facts_mu_);
   auto it = facts_.find(node);
-  return it == facts_.end() ? std::string() : it->second.kx;
+  if (it == facts_.end()) return "";
+  auto bad = bad_kx_.find(node);
+  return bad != bad_kx_.end() && bad->second == it->second.kx ? std::string() : it->second.kx;
+}
+
+bool RocmProvider::stale_kx_(const std::string& node, const HttpResponse& r) {
+  if (r.status != 401) return false;
+  auto j = Json::try_parse(r.body);
+  const std::string why = j ? (*j)["reason"].str_or("") : "";
+  if (why != "StaleAgentKey" && why != "NoAgentKey") return false;
+  std::lock_guard<std::mutex> g(facts_mu_);
+  auto it = facts_.find(node);
+  if (it == facts_.end() || it->second.kx.empty() || bad_kx_[node] == it->second.kx) return false;
+  bad_kx_[node] = it->second.kx;
+  static CounterVec& c = Registry::global().counter(
+      "gpupool_agent_kx_refused_total", "Agent RPCs refused for a stale key-exchange key (re-sent with Ed25519).");
+  c.inc({{"node", node}});
+  return true;
 }
 
 std::vector<std::string> RocmProvider::node_names() {
@@ -290,6 +307,8 @@ Json RocmProvider::post_(const std::string& node, const std::string& path, const
   HttpResponse r;
   try {
     r = c->request("POST", path, body.dump(), "application/json", "application/json", -1, fence);
+    // refused before its body was read (nothing executed): once more, signed with Ed25519
+    if (stale_kx_(node, r)) r = c->request("POST", path, body.dump(), "application/json", "application/json", -1, fence);
   } catch (const std::exception& e) {
     throw ProviderError("AgentUnreachable", "agent on " + node + ": " + e.what());
   }
@@ -448,7 +467,9 @@ NodeView RocmProvider::observe_pool(const std::string& node, const std::string& 
   trace::Span span("agent:GET /v1/node");
   try {
     std::shared_ptr<HttpClient> c = client_for(node);
-    HttpResponse r = c->request("GET", pool_uid.empty() ? "/v1/node" : "/v1/node?pool=" + pool_uid);
+    const std::string target = pool_uid.empty() ? "/v1/node" : "/v1/node?pool=" + pool_uid;
+    HttpResponse r = c->request("GET", target);
+    if (stale_kx_(node, r)) r = c->request("GET", target);
     {
       std::lock_guard<std::mutex> g(cache_mu_);
       ++answered_[node];

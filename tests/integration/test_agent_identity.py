@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import http.server
 import json
+import os
 import socketserver
 import threading
 import time
@@ -140,3 +141,29 @@ def test_annotation_mode_rogue_gets_no_reusable_credential(cluster_factory):
         assert ei.value.code == 401 and ei.value.reason == "WrongNode"
     finally:
         rogue.close()
+
+
+def test_a_stale_key_exchange_key_falls_back_to_signatures(cluster_factory):
+    """The Node names another X25519 key than the agent holds (its state dir was wiped, or an
+    admin edit): the agent refuses the MAC before reading the body (StaleAgentKey), the manager
+    re-sends that request signed with Ed25519 and keeps doing so for that key — no reconcile
+    fails."""
+    from gpupool.utils import edsig
+    c = cluster_factory(nodes=[NodeSpec("node-k", count=4)], agent_auth="signature")
+    k = c.client
+    k.create(MI355XPOOLS, mi_pool("pk", 1), "default")
+    wait_ready(k, "pk", 1, timeout=60)
+    other = edsig.x25519_public(os.urandom(32))
+    k.patch(NODES, "node-k", {"metadata": {"annotations": {
+        "gpupool.amd.com/agent-kx": edsig._b64u(other)}}})
+    time.sleep(0.5)
+    for n in (3, 1, 2):
+        k.patch(MI355XPOOLS, "pk", {"spec": {"replicas": n}}, "default")
+        wait_ready(k, "pk", n, timeout=60)
+    am = c.agent_request("node-k", "GET", "/metrics")
+    assert 'gpupool_agent_rpc_auth_total{result="rejected_StaleAgentKey"} 1' in am, \
+        [ln for ln in am.splitlines() if "rpc_auth" in ln]
+    assert 'gpupool_agent_rpc_signature_versions_total{version="v1"}' in am
+    mm = c.manager_metrics()
+    assert 'gpupool_agent_kx_refused_total{node="node-k"} 1' in mm
+    assert 'gpupool_reconcile_total{kind="Mi355xPool",result="error"}' not in mm
