@@ -288,6 +288,13 @@ class RocmProvider : public DeviceProvider {
     std::string kx;          // gpupool.amd.com/agent-kx: the agent's X25519 key (v2 MAC)
   };
   std::string agent_kx_(const std::string& node);
+
+ public:
+  // the node's agent refused a request whose reason the caller could not read (a watch stream's
+  // 401): stop MACing with the key its Node names until that changes (Ed25519 always works)
+  void distrust_kx(const std::string& node);
+
+ private:
   // a 401 StaleAgentKey / NoAgentKey: the agent has another key-exchange key than its Node says
   // (a wiped state dir, a restart racing its re-registration) — stop MACing with that key until
   // the Node shows a different one (Ed25519 meanwhile); true when the request should be re-sent

@@ -354,6 +354,7 @@ class AgentWatchers {
               return true;
             },
             &w->stop);
+        if (status == 401) prov_.distrust_kx(node);  // the next attempt is Ed25519-signed
         if (status >= 400) throw std::runtime_error("HTTP " + std::to_string(status));
         backoff = 100;
       } catch (const std::exception& e) {

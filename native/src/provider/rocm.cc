@@ -226,6 +226,12 @@ std::string RocmProvider::agent_kx_(const std::string& node) {
   return bad != bad_kx_.end() && bad->second == it->second.kx ? std::string() : it->second.kx;
 }
 
+void RocmProvider::distrust_kx(const std::string& node) {
+  std::lock_guard<std::mutex> g(facts_mu_);
+  auto it = facts_.find(node);
+  if (it != facts_.end() && !it->second.kx.empty()) bad_kx_[node] = it->second.kx;
+}
+
 bool RocmProvider::stale_kx_(const std::string& node, const HttpResponse& r) {
   if (r.status != 401) return false;
   auto j = Json::try_parse(r.body);
