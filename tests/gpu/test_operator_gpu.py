@@ -620,3 +620,5 @@ def test_probe_helper_parked_while_a_tenant_holds_the_gpu(cluster_factory):
     print("PARKING", json.dumps({"agentVramBeforeBytes": before, "tenantVramBytes": tenant_vram,
                                  "memUsedWithTenantBytes": used, "helperCounters": lines}))
     assert any(ln.startswith("gpupool_agent_probe_helper_unparks_total 1") for ln in lines)
+    # the manager's RPCs to this agent were authenticated with the per-node MAC (edsig v2)
+    assert 'gpupool_agent_rpc_signature_versions_total{version="v2"}' in m
