@@ -6,7 +6,8 @@ reference's ``+kubebuilder:validation:Minimum=0`` marker would (README.md:94-95)
 
 Supported keywords: type, properties, required, additionalProperties (schema form), items,
 enum, minimum, maximum, minLength, maxLength, pattern, minItems, maxItems, default, nullable,
-x-kubernetes-preserve-unknown-fields, x-kubernetes-list-type=map + list-map-keys (uniqueness).
+x-kubernetes-preserve-unknown-fields, x-kubernetes-list-type=map + list-map-keys (uniqueness),
+x-kubernetes-validations (CEL rules, the subset gpupool/api/cel.py interprets).
 
 A schema is compiled once into nested checker closures (cached per schema object), so a write
 pays only the checks its schema has — no keyword lookups per node — and a field path is rendered
@@ -294,6 +295,25 @@ def _build(s: dict) -> Check:
                                         f"{dict(zip(keys, key))}")
                         seen.add(hk)
             checks.append(c_listmap)
+
+    if s.get("x-kubernetes-validations"):
+        # CEL rules (apiserver-side cross-field validation), run once the node's own schema
+        # checks passed, with ``self`` bound to the node (gpupool/api/cel.py)
+        from . import cel
+        rules = [(r["rule"], cel.compile_rule(r["rule"]), r.get("message") or
+                  f"failed rule: {r['rule']}") for r in s["x-kubernetes-validations"]]
+
+        def c_cel(v, trail, errs):
+            for src, ast, msg in rules:
+                try:
+                    ok = cel.evaluate(ast, v)
+                except cel.CelError as e:
+                    errs.append(f"{_render(trail)}: Invalid value: \"object\": {msg} "
+                                f"(rule evaluation error: {e})")
+                    continue
+                if ok is not True:
+                    errs.append(f"{_render(trail)}: Invalid value: \"object\": {msg}")
+        checks.append(c_cel)
 
     def check(v, trail, errs):
         if v is None:

@@ -216,6 +216,25 @@ MI355X_SPEC = {
     "description": "Desired state of a pool of MI355X (gfx950) GPUs on one node (or up to "
                    "spec.maxNodes nodes).",
     "required": ["replicas"],
+    # cross-field rules the apiserver enforces at admission (CEL); the manager checks the same
+    # in native/src/api/api.cc and reports InvalidSpec for objects written before a rule existed
+    "x-kubernetes-validations": [
+        {"rule": "!has(self.sharing) || !has(self.sharing.cuPerSlot) || "
+                 "self.sharing.cuPerSlot == 0 || self.sharing.cuPerSlot * "
+                 "(has(self.sharing.replicasPerGPU) ? self.sharing.replicasPerGPU : 1) <= 256",
+         "message": "sharing.cuPerSlot x sharing.replicasPerGPU must not exceed the GPU's 256 CUs"},
+        {"rule": "!has(self.sharing) || !has(self.sharing.cuPerSlot) || "
+                 "self.sharing.cuPerSlot == 0 || self.sharing.cuPerSlot >= "
+                 "(has(self.partition) && has(self.partition.compute) ? "
+                 "(self.partition.compute == 'CPX' ? 1 : self.partition.compute == 'QPX' ? 2 : "
+                 "self.partition.compute == 'DPX' ? 4 : 8) : 8)",
+         "message": "sharing.cuPerSlot must be 0 or at least one CU per XCD of the partition "
+                    "(8 on SPX): a CU mask that leaves an XCD empty is not applied"},
+        {"rule": "!has(self.autoscale) || !has(self.autoscale.minReplicas) || "
+                 "!has(self.autoscale.maxReplicas) || "
+                 "self.autoscale.minReplicas <= self.autoscale.maxReplicas",
+         "message": "autoscale.minReplicas must not exceed autoscale.maxReplicas"},
+    ],
     "properties": {
         "replicas": {**_I32, "minimum": 0, "maximum": 1024,
                      "description": "Number of healthy GPUs to claim, probe and advertise."},
@@ -413,6 +432,10 @@ MI355X_JOB_SPEC = {
     "type": "object",
     "description": "A gang-scheduled distributed training job on pool-advertised MI355X GPUs.",
     "required": ["replicas", "template"],
+    "x-kubernetes-validations": [
+        {"rule": "!has(self.minAvailable) || self.minAvailable <= self.replicas",
+         "message": "minAvailable must not exceed replicas"},
+    ],
     "properties": {
         "replicas": {**_I32, "minimum": 1, "maximum": 1024,
                      "description": "Worker pods (torchrun nnodes); placed all-or-nothing."},

@@ -216,6 +216,9 @@ std::vector<std::string> validate_job(const Json& obj) {
   int_range("activeDeadlineSeconds", 0, INT64_MAX, false);
   int_range("ttlSecondsAfterFinished", -1, INT64_MAX, false);
   int_range("masterPort", 1, 65535, false);
+  if (s["minAvailable"].is_int() && s["replicas"].is_int() &&
+      s["minAvailable"].as_int() > s["replicas"].as_int())
+    errs.push_back("spec: minAvailable must not exceed replicas");
   if (s.contains("resourceName")) {
     static const std::regex re("^[a-z0-9.-]+/[a-z0-9.-]+$");
     if (!s["resourceName"].is_string() || !std::regex_match(s["resourceName"].as_string(), re))
@@ -324,6 +327,10 @@ std::vector<std::string> validate_mi355x(const Json& obj) {
   if (as.contains("scaleDownDelaySeconds") &&
       (!as["scaleDownDelaySeconds"].is_int() || as["scaleDownDelaySeconds"].as_int(0) < 0))
     errs.push_back("spec.autoscale.scaleDownDelaySeconds: should be greater than or equal to 0");
+  // the CRD's x-kubernetes-validations rules, for objects written before the rules existed
+  if (as["minReplicas"].is_int() && as["maxReplicas"].is_int() &&
+      as["minReplicas"].as_int() > as["maxReplicas"].as_int())
+    errs.push_back("spec.autoscale: minReplicas must not exceed maxReplicas");
   return errs;
 }
 

@@ -437,6 +437,20 @@ TEST(validation_matches_crd) {
   EXPECT_EQ(validate_mi355x(neg).size(), 1u);
   Json badres = Json::parse(R"({"kind":"Mi355xPool","spec":{"replicas":1,"resourceName":"BAD"}})");
   EXPECT_EQ(validate_mi355x(badres).size(), 1u);
+  // the cross-field rules the CRD states in CEL (x-kubernetes-validations), checked again here
+  for (const char* bad : {R"({"replicas":1,"sharing":{"replicasPerGPU":4,"cuPerSlot":128}})",
+                          R"({"replicas":1,"sharing":{"replicasPerGPU":4,"cuPerSlot":4}})",
+                          R"({"replicas":1,"partition":{"compute":"DPX"},"sharing":{"cuPerSlot":2}})",
+                          R"({"replicas":1,"autoscale":{"minReplicas":5,"maxReplicas":2}})"}) {
+    Json o = Json::parse(std::string(R"({"kind":"Mi355xPool","spec":)") + bad + "}");
+    EXPECT_EQ(validate_mi355x(o).size(), 1u);
+  }
+  for (const char* good : {R"({"replicas":1,"sharing":{"replicasPerGPU":4,"cuPerSlot":64}})",
+                           R"({"replicas":1,"partition":{"compute":"CPX"},"sharing":{"cuPerSlot":1}})",
+                           R"({"replicas":1,"autoscale":{"minReplicas":2,"maxReplicas":2}})"}) {
+    Json o = Json::parse(std::string(R"({"kind":"Mi355xPool","spec":)") + good + "}");
+    EXPECT_TRUE(validate_mi355x(o).empty());
+  }
   Json az = Json::parse(R"({"kind":"AzureVmPool","spec":{"replicas":0,"resourceGroupName":"rg","location":"eastus",
     "vmSize":"s","vnetName":"v","subnetName":"s","azureCredentialSecret":"c",
     "imageReference":{"publisher":"p","offer":"o","sku":"s","version":"v"}}})");
@@ -554,6 +568,11 @@ TEST(job_validation) {
       R"({"spec":{"replicas":0,"gpusPerReplica":-1,"restartPolicy":"Always","masterPort":70000}})");
   auto errs = gpupool::validate_job(bad);
   EXPECT_EQ(errs.size(), 5u);  // replicas, gpusPerReplica, masterPort, restartPolicy, template
+  // minAvailable <= replicas (the CRD's CEL rule)
+  EXPECT_EQ(gpupool::validate_job(Json::parse(
+      R"({"spec":{"replicas":2,"minAvailable":3,"template":{}}})")).size(), 1u);
+  EXPECT_TRUE(gpupool::validate_job(Json::parse(
+      R"({"spec":{"replicas":2,"minAvailable":2,"template":{}}})")).empty());
   auto spec = gpupool::Mi355xJobSpec::from(ok["spec"]);
   EXPECT_TRUE(spec.gpus_per_replica == 1 && spec.restart_policy == "OnFailure" && spec.master_port == 29500);
 }

@@ -88,7 +88,8 @@ def scenarios(tag_dir: str) -> dict[str, list[tuple]]:
         "footprint": [("helper_footprint", [PY, "scripts/helper_footprint.py", "8"], 240, {}),
                       ("hip_host_memory", [PY, "scripts/hip_host_memory.py"], 240, {}),
                       ("agent_footprint", [PY, "scripts/agent_footprint.py"], 300, {}),
-                      ("amdsmi_call_costs", [PY, "scripts/amdsmi_call_costs.py"], 200, {})],
+                      ("amdsmi_call_costs", [PY, "scripts/amdsmi_call_costs.py"], 200, {}),
+                      ("helper_init_breakdown", [PY, "scripts/helper_init_breakdown.py"], 400, {})],
     }
 
 

@@ -6,7 +6,7 @@ from __future__ import annotations
 import pytest
 
 from gpupool.agent.agent import gpu_of
-from gpupool.kube import MI355XPOOLS, NODES, PODS
+from gpupool.kube import MI355XPOOLS, NODES, PODS, KubeError
 
 from .helpers import mi_pool, pause_pod, wait_ready
 
@@ -194,23 +194,18 @@ def test_isolated_slots_get_the_share_library_disjoint_cus_and_a_budget(cluster_
     assert e4["GPUPOOL_GPU_SLOTS"] == envs[0]["GPUPOOL_GPU_SLOTS"]
     assert e4["GPUPOOL_SHARE_ACCOUNT"] != accts[0] and not os.path.exists(accts[0])
     assert all(os.path.exists(a) for a in accts[1:] + [e4["GPUPOOL_SHARE_ACCOUNT"]])
-    # a pool whose slots overrun the GPU's CUs is rejected at admission of the manager
-    k.create(MI355XPOOLS, mi_pool("over", 1, sharing={"replicasPerGPU": 4, "cuPerSlot": 128}),
-             "default")
-    o = k.wait_for(MI355XPOOLS, "over", "default", lambda o: any(
-        x["reason"] == "InvalidSpec" for x in (o.get("status") or {}).get("conditions", [])),
-        timeout=20)
-    assert "256 CUs" in next(x["message"] for x in o["status"]["conditions"]
-                             if x["type"] == "Ready")
+    # a pool whose slots overrun the GPU's CUs is refused at admission by the CRD's CEL rule
+    # (the manager checks the same, InvalidSpec, for objects written before the rule existed)
+    with pytest.raises(KubeError) as ei:
+        k.create(MI355XPOOLS, mi_pool("over", 1, sharing={"replicasPerGPU": 4, "cuPerSlot": 128}),
+                 "default")
+    assert ei.value.code == 422 and "256 CUs" in str(ei.value)
     # fewer CUs per slot than the GPU has XCDs would leave XCDs empty: the hardware would ignore
     # the mask, so such a pool is refused — on SPX (or Any) below 8, on CPX (1 XCD) any size goes
-    k.create(MI355XPOOLS, mi_pool("thin", 1, sharing={"replicasPerGPU": 4, "cuPerSlot": 4}),
-             "default")
-    o = k.wait_for(MI355XPOOLS, "thin", "default", lambda o: any(
-        x["reason"] == "InvalidSpec" for x in (o.get("status") or {}).get("conditions", [])),
-        timeout=20)
-    assert "at least 8" in next(x["message"] for x in o["status"]["conditions"]
-                                if x["type"] == "Ready")
+    with pytest.raises(KubeError) as ei:
+        k.create(MI355XPOOLS, mi_pool("thin", 1, sharing={"replicasPerGPU": 4, "cuPerSlot": 4}),
+                 "default")
+    assert ei.value.code == 422 and "one CU per XCD" in str(ei.value)
 
 
 def test_per_pod_accounting_on_a_time_shared_gpu(cluster_factory):

@@ -12,7 +12,7 @@ import yaml
 from hypothesis import given, settings
 from hypothesis import strategies as st
 
-from gpupool.api import openapi
+from gpupool.api import cel, openapi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 _TYPES = {
@@ -68,6 +68,15 @@ def oracle(v, s, path, errs):
                 oracle(sub, props[k], f"{path}.{k}", errs)
             elif isinstance(ap, dict):
                 oracle(sub, ap, f"{path}.{k}", errs)
+        for r in s.get("x-kubernetes-validations", []):  # CEL (the interpreter: test_cel.py)
+            msg = r.get("message") or f"failed rule: {r['rule']}"
+            try:
+                ok = cel.evaluate(r["rule"], v)
+            except cel.CelError as e:
+                errs.append(f'{path}: Invalid value: "object": {msg} (rule evaluation error: {e})')
+                continue
+            if ok is not True:
+                errs.append(f'{path}: Invalid value: "object": {msg}')
     elif t == "array":
         if "minItems" in s and len(v) < s["minItems"]:
             errs.append(f"{path}: Invalid value: should have at least {s['minItems']} items")
