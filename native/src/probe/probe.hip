@@ -12,9 +12,11 @@
 //
 // Design for CDNA4: 64-wide waves; 16-byte vector loads/stores everywhere (Guideline 13);
 // HBM kernels grid-stride with ~8 workgroups per CU and 4 independent 16-B accesses in flight per
-// lane; the GEMM (gemm_bf16_mfma_256) uses a 256x256x64 tile, 8 waves each owning 128x64, operands
-// DMA'd HBM->LDS with global_load_lds (two stages, XOR-swizzled) and an XCD-aware bijective
-// workgroup remap (T1) so neighbouring tiles share an XCD's L2. The older 128x128 register-staged
+// lane; the GEMM (gemm_bf16_mfma_256p) uses a 256x256x64 tile, 8 waves each owning a 64x32 block of
+// every 128x128 quadrant, operands DMA'd HBM->LDS with global_load_lds (two stages, XOR-swizzled) in
+// half-tiles that stay in flight across barriers (counted vmcnt), the two wave groups one barrier
+// apart, and an XCD-aware bijective workgroup remap (T1) so neighbouring tiles share an XCD's L2.
+// The 2-phase loop (gemm_bf16_mfma_256) stays selectable ("gemmPipe":0). The older 128x128 register-staged
 // kernel stays selectable ("gemmTile":128) for in-process A/B comparisons. Host side: one arena
 // allocation per probe (the HBM pattern region is reused for the GEMM operands), pinned result
 // slots and one stream sync per phase.
@@ -24,6 +26,7 @@
 #include <atomic>
 #include <chrono>
 #include <thread>
+#include <type_traits>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -402,6 +405,11 @@ constexpr int G2_BM = 256, G2_BN = 256, G2_BK = 64;
 // Tile order of gemm_bf16_mfma_256: 0 row-major, > 1 grouped. Groups of 4 tile rows: 8192^3 1331 vs
 // 1118 TFLOP/s (+19 %), 4096^3 unchanged (1366 vs 1372) (profiles/r4q_probe_gemm_group_ab.json).
 constexpr int kGemmGroupM = 4;
+// K-loop of the 256x256 GEMM ("gemmPipe" selects per probe): 0 the 2-phase loop, 1 the half-tile
+// pipeline, 2 the half-tile pipeline with staggered wave groups (default: 4096^3 1322 / 1392 / 1284
+// vs 1251 / 1292 / 1226 TFLOP/s for 0 on three boxes, 8192^3 +6 %; profiles/r6q_gemm_vs_hipblaslt.json,
+// r6s_gemm_kloop_ab.json), 3 the 32x32x16 fragment-ring variant (measured slower, r6t: A/B only).
+constexpr int kGemmPipe = 2;
 constexpr int kGemm2Threads = 512;
 constexpr int G2_STAGE_SHORTS = (G2_BM + G2_BN) * G2_BK;  // one stage: A then B, 64 KiB
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -531,6 +539,371 @@ __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const sho
         for (int j = 0; j < 4; ++j) C[static_cast<int64_t>(row0 + j) * N + col] = acc[m][n][j];
       }
   }
+}
+
+// ------------------------------------------------------------------ MFMA GEMM, 256x256, half-tile pipeline
+// Same tile, LDS image, swizzle and tile order as gemm_bf16_mfma_256, but the K-loop no longer
+// drains its DMA at every K-step (cdna_hip_programming.md §5 "Pipelining across barriers", T3+T4):
+//   * a K-tile is four half-tiles (A rows 0-127 "A0", B rows 0-127 "B0", "B1", "A1"), each 16 KiB,
+//     two global_load_lds per thread; K-tile t+1's half h is issued in phase h of K-tile t;
+//   * each wave owns a 64x32 sub-block in each of the block tile's four 128x128 quadrants, so
+//     phase 0 needs only A0+B0, phase 1 B1, phase 2 A1 (phase 3 computes from registers): the
+//     wait before a phase retires just the halves it reads — counted vmcnt(4), i.e. two halves
+//     stay in flight across every barrier — and a raw s_barrier (no __syncthreads: its fence
+//     would drain the DMA) publishes them to every wave;
+//   * WAR: half h of K-tile t+1 lands in K-tile t-1's buffer, whose half h was last read in a
+//     phase <= h of K-tile t-1, at least one barrier earlier;
+//   * s_setprio(1) around each 16-MFMA quadrant keeps hipcc from moving the cluster across the
+//     barriers (T5).
+// All LDS is the one __shared__ array (a second LDS object makes hipcc wait vmcnt(0) before ds_reads).
+// kStagger: waves 4-7 run one phase (one barrier) behind waves 0-3, so on each SIMD one wave reads
+// LDS while the other runs its MFMAs. Every wave then retires a half one phase BEFORE the phase that
+// reads it (a reader one barrier behind the writer needs one barrier more: §5 "Read a staged buffer
+// one phase AFTER the wait that retires it"), every phase has a barrier, and both groups execute
+// the same number of barriers (group 1 one extra before the loop, group 0 one extra after it).
+// kAblate (timing experiments only, wrong C): 1 = no DMA inside the K-loop, 2 = no MFMAs.
+template <bool kStagger, int kAblate = 0>
+__global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256p(const short* __restrict__ A,
+                                                                        const short* __restrict__ Bt,
+                                                                        float* __restrict__ C, int M,
+                                                                        int N, int K,
+                                                                        unsigned long long* __restrict__ cu_map,
+                                                                        int group_m) {
+  __shared__ __attribute__((aligned(16))) short smem[2 * G2_STAGE_SHORTS];  // 128 KiB
+  if (cu_map && threadIdx.x == 0) mark_cu(cu_map);
+  const int tiles_n = N / G2_BN, tiles_m = M / G2_BM;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int tile_m, tile_n;
+  if (group_m > 1) {
+    const int per_group = group_m * tiles_n, first_m = (wg / per_group) * group_m;
+    const int gm = min(tiles_m - first_m, group_m), r = wg % per_group;
+    tile_m = first_m + r % gm;
+    tile_n = r / gm;
+  } else {
+    tile_m = wg / tiles_n;
+    tile_n = wg % tiles_n;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // half-tile h (0 A0, 1 B0, 2 B1, 3 A1): operand and row half
+  // chunk q = i*512 + tid (i = 0, 1) of a 128x8-chunk half lands at byte q*16 of the half's LDS
+  // image: row q>>3, slot q&7 holding logical chunk slot ^ ((row>>1)&7) (the full-tile row has
+  // the same bits 1..3, so the swizzle matches g2_swz on the 256-row image)
+  const short* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const bool is_a = (h == 0 || h == 3);
+    const int half = (h == 0 || h == 1) ? 0 : 1;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = i * kGemm2Threads + tid, row = q >> 3, slot = q & 7;
+      const int chunk = slot ^ ((row >> 1) & 7);
+      const int grow = (is_a ? tile_m * G2_BM : tile_n * G2_BN) + half * 128 + row;
+      src[h][i] = (is_a ? A : Bt) + static_cast<int64_t>(grow) * K + chunk * 8;
+    }
+  }
+  auto stage_half = [&](int buf, int h, int k0) {
+    if (kAblate == 1 && k0 > 0) return;
+    const bool is_a = (h == 0 || h == 3);
+    const int half = (h == 0 || h == 1) ? 0 : 1;
+    char* base = reinterpret_cast<char*>(smem) + buf * G2_STAGE_SHORTS * 2 + (is_a ? 0 : G2_BM * 128) +
+                 half * 128 * 128;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(src[h][i] + k0, (lds_void_t*)(base + (i * kGemm2Threads + wave * 64) * 16),
+                                       16, 0, 0);
+  };
+
+  f32x4 acc[4][4][2];  // [quadrant i*2+j][m][n]
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) acc[q][m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ksteps = K / G2_BK;
+  bf16x8 af[2][4], b0f[2][2], b1f[2][2];  // [k-sub][m|n]
+  auto read_a = [&](const char* as, int half) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        af[ks][m] = *reinterpret_cast<const bf16x8*>(as + g2_swz(half * 128 + wr * 64 + m * 16 + fr, ks * 4 + fq));
+  };
+  auto read_b = [&](const char* bs, int half, bf16x8 (&bf)[2][2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        bf[ks][n] = *reinterpret_cast<const bf16x8*>(bs + g2_swz(half * 128 + wc * 32 + n * 16 + fr, ks * 4 + fq));
+  };
+  auto quadrant = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2]) {
+    if constexpr (kAblate == 2) {  // keep the fragment reads alive without the matrix work
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) asm volatile("" ::"v"(af[ks][m]));
+#pragma unroll
+        for (int n = 0; n < 2; ++n) asm volatile("" ::"v"(bf[ks][n]));
+      }
+      return;
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          c[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][m], bf[ks][n], c[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // no LDS read moves above the barrier
+  };
+
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage_half(0, h, 0);
+  // group 1 = waves 4-7; readfirstlane makes the branch scalar (a divergent-looking `if` would
+  // run the s_barrier for every wave: balanced, but no stagger)
+  const bool group1 = __builtin_amdgcn_readfirstlane(wave) >= 4;
+  if constexpr (kStagger) {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A0, B0 of tile 0
+    sync();
+    if (group1) sync();
+  }
+  // one K-tile: kLast drops the prefetch and retires the tail with smaller counts
+  auto ktile = [&](int t, auto last_tag) {
+    constexpr bool kLast = decltype(last_tag)::value;
+    const int cur = t & 1, k1 = (t + 1) * G2_BK;
+    const char* as = reinterpret_cast<const char*>(smem) + cur * G2_STAGE_SHORTS * 2;
+    const char* bs = as + G2_BM * 128;
+    if constexpr (kStagger) {
+      // waits retire what the NEXT phase reads: outstanding before phase 0 = B1, A1 of this tile
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // B1 (read in phase 1)
+      sync();
+      if constexpr (!kLast) stage_half(cur ^ 1, 0, k1);
+      read_a(as, 0);
+      read_b(bs, 0, b0f);
+      quadrant(acc[0], b0f);
+      if constexpr (kLast) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A1 (read in phase 2); A0' in flight
+      sync();
+      if constexpr (!kLast) stage_half(cur ^ 1, 1, k1);
+      read_b(bs, 1, b1f);
+      quadrant(acc[1], b1f);
+      sync();
+      if constexpr (!kLast) stage_half(cur ^ 1, 2, k1);
+      read_a(as, 1);
+      quadrant(acc[3], b1f);
+      if constexpr (!kLast) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A0', B0' (next tile's phase 0)
+      sync();
+      if constexpr (!kLast) stage_half(cur ^ 1, 3, k1);
+      quadrant(acc[2], b0f);
+    } else {
+      // phase 0: A0 + B0 of this tile (A1, B1 may still be in flight)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      sync();
+      if constexpr (!kLast) stage_half(cur ^ 1, 0, k1);
+      read_a(as, 0);
+      read_b(bs, 0, b0f);
+      quadrant(acc[0], b0f);
+      // phase 1: B1
+      if constexpr (kLast) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      sync();
+      if constexpr (!kLast) stage_half(cur ^ 1, 1, k1);
+      read_b(bs, 1, b1f);
+      quadrant(acc[1], b1f);
+      // phase 2: A1
+      if constexpr (kLast) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      sync();
+      if constexpr (!kLast) stage_half(cur ^ 1, 2, k1);
+      read_a(as, 1);
+      quadrant(acc[3], b1f);
+      // phase 3: registers only (A1 x B0); A1 of the next tile goes out
+      if constexpr (!kLast) stage_half(cur ^ 1, 3, k1);
+      quadrant(acc[2], b0f);
+    }
+  };
+  for (int t = 0; t + 1 < ksteps; ++t) ktile(t, std::false_type{});
+  ktile(ksteps - 1, std::true_type{});
+  if constexpr (kStagger) {
+    if (!group1) sync();  // balance group 1's extra barrier: every wave ran 4*ksteps + 2
+  }
+
+  // C/D layout of 16x16x32: col = lane&15, row = 4*(lane>>4) + j; quadrant q = i*2 + j
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int col = tile_n * G2_BN + (q & 1) * 128 + wc * 32 + n * 16 + fr;
+        const int row0 = tile_m * G2_BM + (q >> 1) * 128 + wr * 64 + m * 16 + 4 * fq;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) C[static_cast<int64_t>(row0 + j) * N + col] = acc[q][m][n][j];
+      }
+}
+
+// ------------------------------------------------------------------ MFMA GEMM, 256x256, 32x32x16 + fragment ring
+// The same tile, LDS image and DMA as gemm_bf16_mfma_256 (one 64 KiB K-tile per stage, two stages,
+// one barrier per K-tile), with the fragment reads pipelined instead of issued in a burst:
+//   * v_mfma_f32_32x32x16_bf16: a wave's 128x64 is 4x2 tiles of 32x32, a K-tile 4 k-steps of 16,
+//     8 MFMAs (256 matrix cycles) per k-step;
+//   * two fragment register sets (A 4 x 16 B, B 2 x 16 B each): while k-step s runs its MFMAs from
+//     one set, the 6 ds_read_b128 of k-step s+1 fill the other — the reads sit in the MFMA gaps
+//     (2 per 32-cycle gap cost ~nothing, MI355X_MICROARCH.md §LDS) instead of in front of them;
+//   * k-step 0 of the next K-tile is read during k-step 3 of this one, so the K-tile's barrier sits
+//     between k-steps 2 and 3: vmcnt(0) (this wave's DMA of the next tile, issued a K-tile ago) +
+//     lgkmcnt(0) (its reads of this tile's last k-step, so the stage can be overwritten) + barrier,
+//     then the DMA of the tile after next goes into this tile's stage.
+// 32x32x16 operand map: lane l holds A[row l&31][k 8*(l>>5) + j], B likewise; C: col = l&31,
+// row = (reg&3) + 8*(reg>>2) + 4*(l>>5).
+__global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256x(const short* __restrict__ A,
+                                                                        const short* __restrict__ Bt,
+                                                                        float* __restrict__ C, int M,
+                                                                        int N, int K,
+                                                                        unsigned long long* __restrict__ cu_map,
+                                                                        int group_m) {
+  __shared__ __attribute__((aligned(16))) short smem[2 * G2_STAGE_SHORTS];  // 128 KiB
+  if (cu_map && threadIdx.x == 0) mark_cu(cu_map);
+  const int tiles_n = N / G2_BN, tiles_m = M / G2_BM;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int tile_m, tile_n;
+  if (group_m > 1) {
+    const int per_group = group_m * tiles_n, first_m = (wg / per_group) * group_m;
+    const int gm = min(tiles_m - first_m, group_m), r = wg % per_group;
+    tile_m = first_m + r % gm;
+    tile_n = r / gm;
+  } else {
+    tile_m = wg / tiles_n;
+    tile_n = wg % tiles_n;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const short* a_src[4];
+  const short* b_src[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = i * kGemm2Threads + tid, row = q >> 3, slot = q & 7;
+    const int chunk = slot ^ ((row >> 1) & 7);
+    a_src[i] = A + static_cast<int64_t>(tile_m * G2_BM + row) * K + chunk * 8;
+    b_src[i] = Bt + static_cast<int64_t>(tile_n * G2_BN + row) * K + chunk * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+    char* base = reinterpret_cast<char*>(smem) + buf * G2_STAGE_SHORTS * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int off = (i * kGemm2Threads + wave * 64) * 16;
+      __builtin_amdgcn_global_load_lds(a_src[i] + k0, (lds_void_t*)(base + off), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(b_src[i] + k0, (lds_void_t*)(base + G2_BM * 128 + off), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[m][n][j] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  bf16x8 ra0[4], rb0[2], ra1[4], rb1[2];  // the two fragment sets
+  // Fragment reads are inline-asm ds_read_b128 with hand-counted lgkmcnt: hipcc waits lgkmcnt(0)
+  // for its own reads before every MFMA group here, which serialises the ring. hipcc neither
+  // tracks nor waits for these, so every use sits behind an explicit wait + sched_barrier
+  // (cdna_hip_programming.md §5.4 rule 18).
+  typedef __attribute__((address_space(3))) char lds_char_t;
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_char_t*)smem));
+  // per-lane byte offset of k-step s inside a stage, A rows (wr*128 + fr) and B rows (wc*64 + fr);
+  // the m / n tiles add 32 rows = 4096 B (the swizzle depends on row bits 1..3 only)
+  uint32_t a_off[4], b_off[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    a_off[st] = lds0 + g2_swz(wr * 128 + fr, 2 * st + fh);
+    b_off[st] = lds0 + G2_BM * 128 + g2_swz(wc * 64 + fr, 2 * st + fh);
+  }
+  auto ds16 = [](uint32_t addr) {
+    bf16x8 r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+    return r;
+  };
+  auto read = [&](int buf, int st, bf16x8 (&ra)[4], bf16x8 (&rb)[2]) {
+    const uint32_t bo = static_cast<uint32_t>(buf) * (G2_STAGE_SHORTS * 2);
+#pragma unroll
+    for (int n = 0; n < 2; ++n) rb[n] = ds16(b_off[st] + bo + n * 4096);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) ra[m] = ds16(a_off[st] + bo + m * 4096);
+  };
+  auto wait_lgkm6 = [] {
+    asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto wait_lgkm0 = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mfma = [&](const bf16x8 (&ra)[4], const bf16x8 (&rb)[2]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[m], rb[n], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int ksteps = K / G2_BK;
+  stage(0, 0);
+  if (ksteps > 1) stage(1, G2_BK);
+  if (ksteps > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage 0 (stage 1 in flight)
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  read(0, 0, ra0, rb0);
+  for (int t = 0; t < ksteps; ++t) {
+    const int cur = t & 1;
+    read(cur, 1, ra1, rb1);
+    wait_lgkm6();  // k-step 0's six reads are in, k-step 1's six may be in flight
+    mfma(ra0, rb0);
+    read(cur, 2, ra0, rb0);
+    wait_lgkm6();
+    mfma(ra1, rb1);
+    read(cur, 3, ra1, rb1);
+    wait_lgkm6();
+    mfma(ra0, rb0);
+    if (t + 1 < ksteps) {
+      // the next tile's stage has landed (this wave's part; the barrier makes it everyone's) and
+      // this wave's reads of this stage are done, so the tile after next may overwrite it
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 2 < ksteps) stage(cur, (t + 2) * G2_BK);
+      __builtin_amdgcn_sched_barrier(0);
+      read(cur ^ 1, 0, ra0, rb0);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      wait_lgkm0();
+    }
+    mfma(ra1, rb1);
+  }
+
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int col = tile_n * G2_BN + wc * 64 + n * 32 + fr;
+      const int rbase = tile_m * G2_BM + wr * 128 + m * 32 + 4 * fh;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        C[static_cast<int64_t>(rbase + (j & 3) + 8 * (j >> 2)) * N + col] = acc[m][n][j];
+    }
 }
 
 // Full VALU reference (independent of the matrix cores), fp32, k-ordered.
@@ -822,7 +1195,7 @@ std::string hip_uuid(int dev) {
 // ctx.gev[0..1]) with exact u32 (mod 2^32) ABFT row/column checksums, then copies the two mismatch
 // counters to hres[kSlotSmall..kSlotAbft]. Operands are carved from ``gbase``. zero_mfma: the operand
 // kernels zero the phase's counters cnt[kSlotSmall..kResSlots) and ABFT accumulators themselves.
-void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, bool prio, bool vec_c, int group_m, int reps, int inject_gemm,
+void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int pipe, bool prio, bool vec_c, int group_m, int reps, int inject_gemm,
                        int census_fault_xcc, bool zero_mfma, bool poison_c, unsigned long long* cnt,
                        unsigned long long* hres, DeviceCtx& ctx, hipStream_t s) {
   const size_t n = static_cast<size_t>(gemm_n), n0 = 256;
@@ -843,7 +1216,21 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, bool prio, bool ve
   auto* v = reinterpret_cast<unsigned long long*>(carve(6 * n * 8));
   auto gemm = [&](const short* a_, const short* b_, float* c_, int nn, unsigned long long* cu_map) {
     const dim3 grid((nn / G2_BM) * (nn / G2_BN));
-    if (tile256 && prio)
+    if (tile256 && pipe == 1)
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<false>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn, cu_map,
+                         group_m);
+    else if (tile256 && pipe == 2)
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn, cu_map,
+                         group_m);
+    else if (tile256 && pipe == 3)
+      hipLaunchKernelGGL(gemm_bf16_mfma_256x, grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn, cu_map, group_m);
+    else if (tile256 && pipe == 11)  // ablations (timing only; the checks fail)
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 1>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
+                         cu_map, group_m);
+    else if (tile256 && pipe == 12)
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 2>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
+                         cu_map, group_m);
+    else if (tile256 && prio)
       hipLaunchKernelGGL((gemm_bf16_mfma_256<true, false>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
                          cu_map, group_m);
     else if (tile256 && vec_c)
@@ -941,6 +1328,7 @@ std::string run_probe(int dev, const char* opts) {
   const int inject_gemm = static_cast<int>(opt_int(opts, "injectGemmFault", 0));
   const bool tile256 = opt_int(opts, "gemmTile", 256) != 128;  // 128 = the older 128x128 kernel (A/B)
   const int group_m = static_cast<int>(opt_int(opts, "gemmGroupM", kGemmGroupM));  // tile order (A/B)
+  const int gemm_pipe = static_cast<int>(opt_int(opts, "gemmPipe", kGemmPipe));      // 1, 2: half-tile pipeline
   const bool gemm_prio = opt_int(opts, "gemmPrio", 0) != 0;                        // s_setprio (A/B)
   const bool gemm_vec_c = opt_int(opts, "gemmVecC", 0) != 0;                       // 16-B C stores (A/B)
   const bool poison_c = opt_int(opts, "poisonC", 0) != 0;                           // test hook
@@ -1041,7 +1429,7 @@ std::string run_probe(int dev, const char* opts) {
   // earlier on the GPU while the rest of the HBM test is still enqueued well ahead of need.
   const int hbm_first = static_cast<int>(opt_int(opts, "hbmFirst", 1));
   if (do_mfma && hbm_first == 0)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, gemm_vec_c, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_pipe, gemm_prio, gemm_vec_c, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                       ctx, s2);
 
   // ---------------- HBM: all patterns back to back, per-pattern counters
@@ -1072,7 +1460,7 @@ std::string run_probe(int dev, const char* opts) {
       hipLaunchKernelGGL(hbm_fill<0>, dim3(fill_grid), dim3(kHbmThreads), 0, s, hbm, n16, seed, flip, reset, nreset);
     PROBE_CHECK(hipEventRecord(ctx.ev[1 + 2 * pi], s));
     if (pi == 0 && do_mfma && hbm_first == 2)
-      launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, gemm_vec_c, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
+      launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_pipe, gemm_prio, gemm_vec_c, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                         ctx, s2);
     if (pi == 0 && inject_flips > 0)
       hipLaunchKernelGGL(inject_bit_flips, dim3(1), dim3(256), 0, s, reinterpret_cast<unsigned int*>(hbm), n16 * 4,
@@ -1091,7 +1479,7 @@ std::string run_probe(int dev, const char* opts) {
   PROBE_CHECK(hipGetLastError());
   PROBE_CHECK(hipMemcpyAsync(hres, cnt, 2 * patterns * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   if (do_mfma && hbm_first == 1)
-    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_prio, gemm_vec_c, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
+    launch_mfma_phase(base + hbm_region, gemm_n, tile256, gemm_pipe, gemm_prio, gemm_vec_c, group_m, reps, inject_gemm, census_fault_xcc, zero_in_kernel, poison_c, cnt, hres,
                       ctx, s2);
   const double launch_ms = ms_since(t_run);  // host time to enqueue the whole probe
   PROBE_CHECK(hipStreamSynchronize(s));
@@ -1151,7 +1539,7 @@ std::string run_probe(int dev, const char* opts) {
          ",\"writeGBps\":" + jnum(write_gbps) + ",\"readGBps\":" + jnum(read_gbps) + ",\"GBps\":" + jnum(hbm_gbps) +
          ",\"ms\":" + jnum(write_ms + read_ms) + "}";
   out += ",\"mfma\":{\"ok\":" + std::string(mfma_ok ? "true" : "false") + ",\"enabled\":" + (do_mfma ? "true" : "false") +
-         ",\"n\":" + std::to_string(gemm_n) + ",\"tile\":" + (tile256 ? "256" : "128") +
+         ",\"n\":" + std::to_string(gemm_n) + ",\"tile\":" + (tile256 ? "256" : "128") + ",\"pipe\":" + std::to_string(tile256 ? gemm_pipe : 0) +
          ",\"elementMismatches\":" + std::to_string(small_bad) + ",\"abftMismatches\":" + std::to_string(abft_bad) +
          ",\"tflops\":" + jnum(tflops) + ",\"ms\":" + jnum(gemm_ms) + "}";
   if (do_mfma) {
@@ -1735,9 +2123,19 @@ int mi355x_probe_gemm_bf16(int dev, const void* A, const void* Bt, void* C, int 
     PROBE_CHECK(hipMalloc(&dc.p, sc));
     PROBE_CHECK(hipMemcpy(da.p, A, sa, hipMemcpyHostToDevice));
     PROBE_CHECK(hipMemcpy(db.p, Bt, sb, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL((gemm_bf16_mfma_256<false, false>), dim3((m / G2_BM) * (n / G2_BN)), dim3(kGemm2Threads), 0, nullptr,
-                       static_cast<const short*>(da.p), static_cast<const short*>(db.p), static_cast<float*>(dc.p), m, n,
-                       k, static_cast<unsigned long long*>(nullptr), kGemmGroupM);
+    const dim3 grid((m / G2_BM) * (n / G2_BN));
+    if (kGemmPipe == 2)
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true>), grid, dim3(kGemm2Threads), 0, nullptr,
+                         static_cast<const short*>(da.p), static_cast<const short*>(db.p), static_cast<float*>(dc.p), m,
+                         n, k, static_cast<unsigned long long*>(nullptr), kGemmGroupM);
+    else if (kGemmPipe == 1)
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<false>), grid, dim3(kGemm2Threads), 0, nullptr, static_cast<const short*>(da.p),
+                         static_cast<const short*>(db.p), static_cast<float*>(dc.p), m, n, k,
+                         static_cast<unsigned long long*>(nullptr), kGemmGroupM);
+    else
+      hipLaunchKernelGGL((gemm_bf16_mfma_256<false, false>), grid, dim3(kGemm2Threads), 0, nullptr,
+                         static_cast<const short*>(da.p), static_cast<const short*>(db.p), static_cast<float*>(dc.p), m,
+                         n, k, static_cast<unsigned long long*>(nullptr), kGemmGroupM);
     PROBE_CHECK(hipGetLastError());
     PROBE_CHECK(hipMemcpy(C, dc.p, sc, hipMemcpyDeviceToHost));
     return 0;

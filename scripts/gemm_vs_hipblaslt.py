@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""The probe's hand-written MFMA GEMM (gemm_bf16_mfma_256, 256x256x64 glds tile) against the vendor
+"""The probe's hand-written MFMA GEMMs (gemm_bf16_mfma_256, 256x256x64 glds tile, 2-phase loop;
+gemm_bf16_mfma_256p, the same tile with the half-tile pipeline, "probe_pipe"; "probe_pipe2" with
+the two wave groups one barrier apart) against the vendor
 library on the same box: torch.matmul (hipBLASLt) on bf16 A[N,K] @ B[N,K]^T with fp32 accumulate,
 interleaved rounds in one process. The probe's operands are small integers in [-2, 2] (exact
 checks need them); data changes the clock the chip holds (cdna_hip_programming.md §5.4 rule 25),
@@ -41,10 +43,11 @@ for n in (2048, 4096, 8192):
         return flop * reps / (ev0.elapsed_time(ev1) * 1e-3) / 1e12
 
     for r in range(rounds):
-        order = ("probe", "lib_small", "lib_random") if r % 2 == 0 else ("lib_random", "lib_small", "probe")
-        for what in order:
-            if what == "probe":
-                out = probe.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemm_reps=10, overlap=0)
+        order = ("probe", "probe_pipe", "probe_pipe2", "lib_small", "lib_random")
+        for what in (order if r % 2 == 0 else order[::-1]):
+            if what.startswith("probe"):
+                out = probe.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemm_reps=10, overlap=0,
+                                gemmPipe={"probe": 0, "probe_pipe": 1}.get(what, 2))
                 assert out["passed"], out
                 tf = out["mfma"]["tflops"]
             elif what == "lib_small":
@@ -57,8 +60,9 @@ for n in (2048, 4096, 8192):
 probe.trim(0)
 summary = {k: {"median_tflops": statistics.median(v), "max_tflops": max(v)} for k, v in res.items()}
 for n in (2048, 4096, 8192):
-    p, ls = summary[f"{n}:probe"]["median_tflops"], summary[f"{n}:lib_small"]["median_tflops"]
-    summary[f"{n}:probe_vs_lib_same_data"] = round(p / ls, 3)
+    ls = summary[f"{n}:lib_small"]["median_tflops"]
+    for what in ("probe", "probe_pipe", "probe_pipe2"):
+        summary[f"{n}:{what}_vs_lib_same_data"] = round(summary[f"{n}:{what}"]["median_tflops"] / ls, 3)
 print(json.dumps({"rounds": rounds, "note": "torch.matmul bf16 (hipBLASLt) vs the probe's MFMA GEMM; "
                   "fp32 accumulate; peak bf16 dense ~2500 TFLOP/s", "summary": summary,
                   "samples": res}, indent=1))

@@ -40,6 +40,11 @@ def _prof(tag_dir: str, name: str, *cmd: str, pmc: tuple[str, ...] = ()) -> list
                    *cmd]
 
 
+GEMM_SQ_PASSES = (("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                   "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
+                   "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE"),)
+
+
 # scenario -> steps: (name, argv or callable(tag_dir) -> argv, timeout s, env overrides)
 def scenarios(tag_dir: str) -> dict[str, list[tuple]]:
     pytest = [PY, "-u", "-m", "pytest", "-x", "-v", "--timeout", "200", "--timeout-method",
@@ -74,12 +79,18 @@ def scenarios(tag_dir: str) -> dict[str, list[tuple]]:
                                           os.path.join(ROOT, "scripts", "gemm_l2_pmc.py"), "8192",
                                           str(g), pmc=("TCC_HIT_sum", "TCC_MISS_sum")), 120, {})
                 for g in (0, 4)],
+        # SQ counters of the GEMM K-loops (2-phase, half-tile pipeline, staggered), 8 SQ per pass
+        "gemm-sq": [(f"gemm_sq{i}_p{p}", _prof(tag_dir, f"gemm_sq{i}_p{p}", PY,
+                                              os.path.join(ROOT, "scripts", "gemm_l2_pmc.py"),
+                                              "4096", "4", str(p), pmc=c), 120, {})
+                    for i, c in enumerate(GEMM_SQ_PASSES) for p in (0, 1, 2)],
         # HBM bytes per probe kernel as the memory system counts them (one TCC group per pass)
         "probe-pmc": [(f"probe_{c.lower()}", _prof(tag_dir, f"probe_{c.lower()}", PY,
                                                   os.path.join(ROOT, "scripts", "probe_hbm_pmc.py"),
                                                   "5", pmc=(c,)), 120, {})
                       for c in ("FETCH_SIZE", "WRITE_SIZE")],
         "gemm": [("gemm_vs_hipblaslt", [PY, "scripts/gemm_vs_hipblaslt.py"], 300, {})],
+        "gemm-ab": [("gemm_kloop_ab", [PY, "scripts/gemm_kloop_ab.py"], 300, {})],
         # the probe's two-stream shape as one hipGraph vs eager launches (r5l: not adopted)
         "graph": [("graph_events", [os.path.join(ROOT, "build", "native", "graph_events"), "1024",
                                     "15"], 120, {})],

@@ -190,6 +190,21 @@ def test_vectorised_c_store_gemm_is_exact(hip, n):
     assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
 
 
+@pytest.mark.parametrize("pipe", [0, 1, 2, 3])
+@pytest.mark.parametrize("n", [256, 512, 1280, 2048, 4096])
+def test_half_tile_pipelined_gemm_is_exact_run_after_run(hip, n, pipe):
+    """The K-loops of the 256x256 kernel — the 2-phase loop and the half-tile pipeline whose DMA
+    stays in flight across barriers (``gemmPipe`` 1; 2 with the wave groups one barrier apart) —
+    against the exact checks, with C poisoned
+    before each run, several runs per size: a read placed before its DMA has landed would show as
+    a wrong tile in some runs and not others (cdna_hip_programming.md §5 "Read a staged buffer
+    one phase AFTER the wait that retires it"). 256 is one K-tile (prologue + last tile only)."""
+    for _ in range(8):
+        r = hip.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemmPipe=pipe, poisonC=1)
+        assert r["passed"], r
+        assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
+
+
 def test_overlapped_and_serial_probe_agree(hip):
     """The two-stream probe (HBM test beside the MFMA phase) finds the same injected faults as
     the serial one and both pass clean runs."""
