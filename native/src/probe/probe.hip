@@ -406,9 +406,10 @@ constexpr int G2_BM = 256, G2_BN = 256, G2_BK = 64;
 // 1118 TFLOP/s (+19 %), 4096^3 unchanged (1366 vs 1372) (profiles/r4q_probe_gemm_group_ab.json).
 constexpr int kGemmGroupM = 4;
 // K-loop of the 256x256 GEMM ("gemmPipe" selects per probe): 0 the 2-phase loop, 1 the half-tile
-// pipeline, 2 the half-tile pipeline with staggered wave groups (default: 4096^3 1322 / 1392 / 1284
-// vs 1251 / 1292 / 1226 TFLOP/s for 0 on three boxes, 8192^3 +6 %; profiles/r6q_gemm_vs_hipblaslt.json,
-// r6s_gemm_kloop_ab.json), 3 the 32x32x16 fragment-ring variant (measured slower, r6t: A/B only).
+// pipeline, 2 the half-tile pipeline with staggered wave groups and a static s_setprio(1) for waves
+// 4-7 (default: 4096^3 1411 vs 1276 TFLOP/s for 0, 8192^3 1459 vs 1339, profiles/r6v_gemm_prio_ab.json),
+// 21 the same with s_setprio flips around every MFMA cluster instead (1358 / 1430; r6q, r6s), 22 with
+// no s_setprio, 3 the 32x32x16 fragment-ring variant (measured slower, r6t: A/B only).
 constexpr int kGemmPipe = 2;
 constexpr int kGemm2Threads = 512;
 constexpr int G2_STAGE_SHORTS = (G2_BM + G2_BN) * G2_BK;  // one stage: A then B, 64 KiB
@@ -562,7 +563,9 @@ __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256(const sho
 // one phase AFTER the wait that retires it"), every phase has a barrier, and both groups execute
 // the same number of barriers (group 1 one extra before the loop, group 0 one extra after it).
 // kAblate (timing experiments only, wrong C): 1 = no DMA inside the K-loop, 2 = no MFMAs.
-template <bool kStagger, int kAblate = 0>
+// kPrio: 0 s_setprio(1) around every quadrant's MFMAs, 1 one static s_setprio(1) for waves 4-7 and
+// no flips (MI355X_MICROARCH.md §Two waves per SIMD item 4), 2 none.
+template <bool kStagger, int kAblate = 0, int kPrio = 0>
 __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256p(const short* __restrict__ A,
                                                                         const short* __restrict__ Bt,
                                                                         float* __restrict__ C, int M,
@@ -651,7 +654,7 @@ __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256p(const sh
       }
       return;
     }
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (kPrio == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -659,7 +662,7 @@ __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256p(const sh
 #pragma unroll
         for (int n = 0; n < 2; ++n)
           c[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][m], bf[ks][n], c[m][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (kPrio == 0) __builtin_amdgcn_s_setprio(0);
   };
   auto sync = [&]() {
     __builtin_amdgcn_s_barrier();
@@ -671,6 +674,9 @@ __global__ __launch_bounds__(kGemm2Threads, 1) void gemm_bf16_mfma_256p(const sh
   // group 1 = waves 4-7; readfirstlane makes the branch scalar (a divergent-looking `if` would
   // run the s_barrier for every wave: balanced, but no stagger)
   const bool group1 = __builtin_amdgcn_readfirstlane(wave) >= 4;
+  if constexpr (kPrio == 1) {
+    if (group1) __builtin_amdgcn_s_setprio(1);
+  }
   if constexpr (kStagger) {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A0, B0 of tile 0
     sync();
@@ -1220,15 +1226,21 @@ void launch_mfma_phase(char* gbase, int gemm_n, bool tile256, int pipe, bool pri
       hipLaunchKernelGGL((gemm_bf16_mfma_256p<false>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn, cu_map,
                          group_m);
     else if (tile256 && pipe == 2)
-      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn, cu_map,
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 0, 1>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn, cu_map,
                          group_m);
     else if (tile256 && pipe == 3)
       hipLaunchKernelGGL(gemm_bf16_mfma_256x, grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn, cu_map, group_m);
+    else if (tile256 && pipe == 21)
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 0, 0>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
+                         cu_map, group_m);
+    else if (tile256 && pipe == 22)
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 0, 2>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
+                         cu_map, group_m);
     else if (tile256 && pipe == 11)  // ablations (timing only; the checks fail)
-      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 1>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 1, 1>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
                          cu_map, group_m);
     else if (tile256 && pipe == 12)
-      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 2>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 2, 1>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
                          cu_map, group_m);
     else if (tile256 && prio)
       hipLaunchKernelGGL((gemm_bf16_mfma_256<true, false>), grid, dim3(kGemm2Threads), 0, s, a_, b_, c_, nn, nn, nn,
@@ -2125,7 +2137,7 @@ int mi355x_probe_gemm_bf16(int dev, const void* A, const void* Bt, void* C, int 
     PROBE_CHECK(hipMemcpy(db.p, Bt, sb, hipMemcpyHostToDevice));
     const dim3 grid((m / G2_BM) * (n / G2_BN));
     if (kGemmPipe == 2)
-      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true>), grid, dim3(kGemm2Threads), 0, nullptr,
+      hipLaunchKernelGGL((gemm_bf16_mfma_256p<true, 0, 1>), grid, dim3(kGemm2Threads), 0, nullptr,
                          static_cast<const short*>(da.p), static_cast<const short*>(db.p), static_cast<float*>(dc.p), m,
                          n, k, static_cast<unsigned long long*>(nullptr), kGemmGroupM);
     else if (kGemmPipe == 1)

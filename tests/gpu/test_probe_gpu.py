@@ -190,7 +190,7 @@ def test_vectorised_c_store_gemm_is_exact(hip, n):
     assert r["mfma"]["abftMismatches"] == 0 and r["mfma"]["elementMismatches"] == 0
 
 
-@pytest.mark.parametrize("pipe", [0, 1, 2, 3])
+@pytest.mark.parametrize("pipe", [0, 1, 2, 3, 21])
 @pytest.mark.parametrize("n", [256, 512, 1280, 2048, 4096])
 def test_half_tile_pipelined_gemm_is_exact_run_after_run(hip, n, pipe):
     """The K-loops of the 256x256 kernel — the 2-phase loop and the half-tile pipeline whose DMA
