@@ -409,7 +409,11 @@ constexpr int kGemmGroupM = 4;
 // pipeline, 2 the half-tile pipeline with staggered wave groups and a static s_setprio(1) for waves
 // 4-7 (default: 4096^3 1411 vs 1276 TFLOP/s for 0, 8192^3 1459 vs 1339, profiles/r6v_gemm_prio_ab.json),
 // 21 the same with s_setprio flips around every MFMA cluster instead (1358 / 1430; r6q, r6s), 22 with
-// no s_setprio, 3 the 32x32x16 fragment-ring variant (measured slower, r6t: A/B only).
+// no s_setprio, 3 the 32x32x16 fragment-ring variant (measured slower, r6t: A/B only). Also measured
+// and dropped: the phase reads as inline-asm ds_read_b128 in k-sub order with counted lgkmcnt, so a
+// quadrant's first MFMAs start on half its fragments (4096^3 1354 vs 1411, 8192^3 1420 vs 1456,
+// profiles/r6za_gemm_counted_reads_ab_rejected.json), and tile-row groups of 2/8/16 instead of 4
+// (r6z_gemm_group_ab.json).
 constexpr int kGemmPipe = 2;
 constexpr int kGemm2Threads = 512;
 constexpr int G2_STAGE_SHORTS = (G2_BM + G2_BN) * G2_BK;  // one stage: A then B, 64 KiB

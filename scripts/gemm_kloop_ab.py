@@ -10,7 +10,7 @@ timing-only ablations that bound where the time goes:
 
 The ablations compute a wrong C (the probe reports failed); only their time is used.
 
-    python scripts/gemm_kloop_ab.py [rounds] > gpurun_out/gemm_kloop_ab.json
+    python scripts/gemm_kloop_ab.py [rounds] [variants, e.g. 0,2,2g8] [sizes] > gpurun_out/gemm_kloop_ab.json
 """
 from __future__ import annotations
 
@@ -23,17 +23,20 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gpupool.ops import probe  # noqa: E402
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-variants = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "2", "3", "11", "12"])]
+# a variant is "<pipe>" or "<pipe>g<group_m>" (tile-row group size of the tile order, default 4)
+variants = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "2", "3", "11", "12"]
+sizes = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [2048, 4096, 8192]
 probe.init()
 res: dict[str, list[float]] = {}
-for n in (2048, 4096, 8192):
+for n in sizes:
     for r in range(rounds):
-        for pipe in (variants if r % 2 == 0 else variants[::-1]):
+        for v in (variants if r % 2 == 0 else variants[::-1]):
+            pipe, _, group = v.partition("g")
             out = probe.run(0, hbm_bytes=1 << 20, patterns=1, gemm_n=n, gemm_reps=10, overlap=0,
-                            gemmPipe=pipe)
-            if pipe < 10:
+                            gemmPipe=int(pipe), gemmGroupM=int(group or 4))
+            if int(pipe) < 10:
                 assert out["passed"], out
-            res.setdefault(f"{n}:pipe{pipe}", []).append(round(out["mfma"]["tflops"], 1))
+            res.setdefault(f"{n}:pipe{v}", []).append(round(out["mfma"]["tflops"], 1))
 probe.trim(0)
 print(json.dumps({"rounds": rounds, "summary": {k: statistics.median(v) for k, v in res.items()},
                   "samples": res}, indent=1))
