@@ -78,3 +78,64 @@ def test_crd_rules_reject_at_admission():
                                     "spec": {"replicas": 2, "minAvailable": 3, "template": {
                                         "spec": {"containers": [{"name": "c"}]}}}})
     assert "minAvailable must not exceed replicas" in str(ei.value)
+
+
+# ---- precedence and associativity: a random expression printed with the fewest parentheses CEL's
+# precedence allows must evaluate like the same tree printed fully parenthesised
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+_PREC = {"||": 1, "&&": 2, "==": 3, "!=": 3, "<": 3, "<=": 3, ">": 3, ">=": 3,
+         "+": 4, "-": 4, "*": 5, "/": 5, "%": 5}
+
+
+@st.composite
+def _int_expr(draw, depth=0):
+    if depth > 3 or draw(st.integers(0, 3)) == 0:
+        return ("lit", draw(st.integers(-20, 20)))
+    op = draw(st.sampled_from(["+", "-", "*", "/", "%"]))
+    return ("bin", op, draw(_int_expr(depth + 1)), draw(_int_expr(depth + 1)))
+
+
+@st.composite
+def _bool_expr(draw, depth=0):
+    kind = draw(st.integers(0, 3 if depth < 2 else 1))
+    if kind <= 1:
+        return ("bin", draw(st.sampled_from(["==", "!=", "<", "<=", ">", ">="])),
+                draw(_int_expr(2)), draw(_int_expr(2)))
+    if kind == 2:
+        return ("not", draw(_bool_expr(depth + 1)))
+    return ("bin", draw(st.sampled_from(["&&", "||"])), draw(_bool_expr(depth + 1)),
+            draw(_bool_expr(depth + 1)))
+
+
+def _full(e) -> str:
+    if e[0] == "lit":
+        return f"({e[1]})" if e[1] < 0 else str(e[1])
+    if e[0] == "not":
+        return f"(!{_full(e[1])})"
+    return f"({_full(e[2])} {e[1]} {_full(e[3])})"
+
+
+def _minimal(e, parent: int = 0, right: bool = False) -> str:
+    if e[0] == "lit":
+        return f"({e[1]})" if e[1] < 0 else str(e[1])
+    if e[0] == "not":
+        return "!" + _minimal(e[1], 9)
+    p = _PREC[e[1]]
+    s = f"{_minimal(e[2], p)} {e[1]} {_minimal(e[3], p, True)}"
+    # left-associative: a right operand of equal precedence keeps its parentheses; so does any
+    # comparison operand of a comparison (CEL relations do not chain)
+    need = p < parent or (p == parent and right) or (p == parent == 3)
+    return f"({s})" if need else s
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.one_of(_int_expr(), _bool_expr()))
+def test_precedence_matches_full_parenthesisation(e):
+    def run(src):
+        try:
+            return ("ok", cel.evaluate(src, {}))
+        except cel.CelError as err:
+            return ("err", type(err).__name__)
+    assert run(_minimal(e)) == run(_full(e)), (_minimal(e), _full(e))
