@@ -92,6 +92,7 @@ def scenarios(tag_dir: str) -> dict[str, list[tuple]]:
         "gemm": [("gemm_vs_hipblaslt", [PY, "scripts/gemm_vs_hipblaslt.py"], 300, {})],
         "gemm-ab": [("gemm_kloop_ab", [PY, "scripts/gemm_kloop_ab.py"], 300, {})],
         "hbm-cache": [("hbm_cache_residency", [PY, "scripts/hbm_cache_residency.py"], 300, {})],
+        "claim-gemm-ab": [("claim_probe_gemm_ab", [PY, "scripts/claim_probe_gemm_ab.py"], 300, {})],
         # the probe's two-stream shape as one hipGraph vs eager launches (r5l: not adopted)
         "graph": [("graph_events", [os.path.join(ROOT, "build", "native", "graph_events"), "1024",
                                     "15"], 120, {})],
