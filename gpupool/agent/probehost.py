@@ -744,10 +744,10 @@ class HelperPool:
                 if f is not None:
                     stop.append(f)  # it has a context on this GPU: it goes now
                 self._respawn_fabric_later_locked()
+            self.stats["helper_parks"] = self.stats.get("helper_parks", 0) + 1
         for x in stop:  # off the caller's path (a cordon, a pod-view refresh): ~60 ms a stop
             threading.Thread(target=x.stop, args=("park",), daemon=True,
                              name=f"park-{x.key[:8]}").start()
-        self.stats["helper_parks"] = self.stats.get("helper_parks", 0) + 1
         return True
 
     def unpark(self, key: str) -> Helper | None:
@@ -769,7 +769,7 @@ class HelperPool:
                 if f is not None:
                     threading.Thread(target=f.stop, args=("park",), daemon=True).start()
                 self._respawn_fabric_later_locked()
-        self.stats["helper_unparks"] = self.stats.get("helper_unparks", 0) + 1
+            self.stats["helper_unparks"] = self.stats.get("helper_unparks", 0) + 1
         return h
 
     # a burst of parks / unparks (a drain of several GPUs, a gang's pods starting) restarts the

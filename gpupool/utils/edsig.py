@@ -389,6 +389,7 @@ class Verifier:
         self._checked = -1e9
         self._mu = threading.Lock()
         self._nonces: dict[str, int] = {}
+        self._nonce_prune_at = 4096
         self.rejected: dict[str, int] = {}
         self.accepted: dict[str, int] = {}  # key id -> requests it signed (rotation progress)
         self.kx = kx  # v2: this agent's X25519 key; per manager key id the MAC key, derived once
@@ -481,9 +482,12 @@ class Verifier:
                 return self._reject("Replay")
             self._nonces[h["nonce"]] = ts + self.skew_ms
             self.accepted[h["keyId"]] = self.accepted.get(h["keyId"], 0) + 1
-            if len(self._nonces) > 4096:
-                # keep a nonce while its timestamp still passes the skew check (now <= ts+skew)
+            if len(self._nonces) > self._nonce_prune_at:
+                # keep a nonce while its timestamp still passes the skew check (now <= ts+skew);
+                # a burst that keeps more than that alive moves the next prune out (amortised
+                # O(1) per request instead of a full sweep on every one)
                 self._nonces = {n: e for n, e in self._nonces.items() if e >= now}
+                self._nonce_prune_at = max(4096, 2 * len(self._nonces))
         return None
 
     def _mac_key(self, kid: str, pub: PublicKey) -> bytes:

@@ -43,7 +43,8 @@ class AgentSigner {
   std::shared_ptr<void> xkey_;  // EVP_PKEY* (X25519: the same secret scalar)
   std::string xpub_;            // its public key (32 bytes)
   std::string kid_;
-  std::map<std::string, std::string> mac_keys_;  // node \n agent key -> K (cleared on reload)
+  static constexpr size_t kMaxMacKeys = 4096;    // ~2 keys per node on a large cluster
+  std::map<std::string, std::string> mac_keys_;  // node \n agent key -> K (cleared on reload / when full)
   std::atomic<uint64_t> reloads_{0};
 };
 

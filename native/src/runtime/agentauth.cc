@@ -183,6 +183,8 @@ std::string AgentSigner::header(const std::string& method, const std::string& ta
         auto it = mac_keys_.find(ck);
         if (it == mac_keys_.end()) {
           const std::string shared = x25519(static_cast<EVP_PKEY*>(xkey_.get()), agent_x);
+          // agents rotate their keys: stale node/key pairs would pile up for the manager's lifetime
+          if (mac_keys_.size() >= kMaxMacKeys) mac_keys_.clear();
           if (!shared.empty())
             it = mac_keys_.emplace(ck, hmac_sha256(shared, "gpupool-agent-rpc-v2\n" + node + "\n" + xpub_ + agent_x))
                      .first;

@@ -48,6 +48,20 @@ def test_signature_is_bound_to_request_node_and_time(keys):
     assert v_b.check_head("GET", "/v1/node", {}) == "NoSignature"
 
 
+def test_nonce_cache_under_a_burst_inside_the_skew_window(keys):
+    """More live nonces than the prune threshold: every fresh request passes, every replay of
+    one still inside the window is refused, and the sweep is not repeated on each request."""
+    s = edsig.Signer(keys["k1"])
+    v = edsig.Verifier(keys["p1"], "node-b")
+    v._nonce_prune_at = 64  # the production threshold (4096) scaled down for the test's speed
+    sent = [hdr(s, "GET", f"/v1/node?i={i}", "node-b") for i in range(300)]
+    assert all(v.check_head("GET", f"/v1/node?i={i}", dict(h)) is None for i, h in enumerate(sent))
+    assert v._nonce_prune_at >= 2 * 64  # all 300 alive: the threshold moved out
+    assert len(v._nonces) == 300
+    assert all(v.check_head("GET", f"/v1/node?i={i}", dict(sent[i])) == "Replay"
+               for i in (0, 63, 64, 299))
+
+
 def test_key_rotation_through_the_bundle(keys):
     bundle = keys["dir"] / "bundle"
     bundle.mkdir()
