@@ -299,6 +299,7 @@ class RocmProvider : public DeviceProvider {
   // (a wiped state dir, a restart racing its re-registration) — stop MACing with that key until
   // the Node shows a different one (Ed25519 meanwhile); true when the request should be re-sent
   bool stale_kx_(const std::string& node, const HttpResponse& r);
+  bool mark_kx_bad_locked_(const std::string& node);  // true when newly marked (counted)
   std::map<std::string, std::string> bad_kx_;  // node -> kx the agent refused (under facts_mu_)
   std::mutex facts_mu_;
   std::map<std::string, NodeFacts> facts_;

@@ -228,8 +228,18 @@ std::string RocmProvider::agent_kx_(const std::string& node) {
 
 void RocmProvider::distrust_kx(const std::string& node) {
   std::lock_guard<std::mutex> g(facts_mu_);
+  mark_kx_bad_locked_(node);
+}
+
+// one count per (node, key) refused, whichever path saw the 401 first (an RPC or the long-poll feed)
+bool RocmProvider::mark_kx_bad_locked_(const std::string& node) {
   auto it = facts_.find(node);
-  if (it != facts_.end() && !it->second.kx.empty()) bad_kx_[node] = it->second.kx;
+  if (it == facts_.end() || it->second.kx.empty() || bad_kx_[node] == it->second.kx) return false;
+  bad_kx_[node] = it->second.kx;
+  static CounterVec& c = Registry::global().counter(
+      "gpupool_agent_kx_refused_total", "Agent RPCs refused for a stale key-exchange key (re-sent with Ed25519).");
+  c.inc({{"node", node}});
+  return true;
 }
 
 bool RocmProvider::stale_kx_(const std::string& node, const HttpResponse& r) {
@@ -238,13 +248,11 @@ bool RocmProvider::stale_kx_(const std::string& node, const HttpResponse& r) {
   const std::string why = j ? (*j)["reason"].str_or("") : "";
   if (why != "StaleAgentKey" && why != "NoAgentKey") return false;
   std::lock_guard<std::mutex> g(facts_mu_);
+  if (mark_kx_bad_locked_(node)) return true;
+  // another path (the feed) marked this key first: the request went out MACed before that, so
+  // re-send it signed — it was refused before its body was read
   auto it = facts_.find(node);
-  if (it == facts_.end() || it->second.kx.empty() || bad_kx_[node] == it->second.kx) return false;
-  bad_kx_[node] = it->second.kx;
-  static CounterVec& c = Registry::global().counter(
-      "gpupool_agent_kx_refused_total", "Agent RPCs refused for a stale key-exchange key (re-sent with Ed25519).");
-  c.inc({{"node", node}});
-  return true;
+  return it != facts_.end() && !it->second.kx.empty();
 }
 
 std::vector<std::string> RocmProvider::node_names() {
