@@ -374,7 +374,11 @@ class RpcServer:
                 if path in OPEN_PATHS and not self.auth.presented(headers):
                     why = "NoCredentials" if self.auth.required else None
                 else:
-                    why = self.auth.check_head(method, target, headers)
+                    try:
+                        why = self.auth.check_head(method, target, headers)
+                    except Exception:  # a broken key file or verifier: refuse, never drop the thread
+                        log.exception("agent RPC credential check failed")
+                        why = "AuthError"
                 authed = why is None
                 if not authed and path not in OPEN_PATHS:
                     self._reject(conn, 401, why or "Unauthorized",
@@ -400,7 +404,12 @@ class RpcServer:
                     if trusted and str(e) == "deadline":
                         self.request_deadline_closes += 1
                     return
-                if authed and self.auth.check_body(headers, body):  # signed digest != body
+                try:
+                    bad_body = authed and self.auth.check_body(headers, body)
+                except Exception:
+                    log.exception("agent RPC body check failed")
+                    bad_body = "AuthError"
+                if bad_body:  # signed digest != body
                     self._reject(conn, 401, "BodyMismatch", "request body does not match its "
                                  "signature", rf)
                     return

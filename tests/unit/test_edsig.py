@@ -179,3 +179,20 @@ def test_rpc_server_with_signatures_and_rotating_token(keys):
         assert 'result="signature"' in m and 'result="rejected_WrongNode"' in m
     finally:
         srv.close()
+
+
+def test_a_credential_check_that_raises_is_a_refusal_not_a_dropped_connection(keys):
+    """A verifier that throws (a corrupt key bundle, a bug) answers 401 AuthError: the caller
+    learns why, and the connection thread does not die with the exception."""
+    class Broken(AgentAuth):
+        def check_head(self, method, target, headers):
+            raise AttributeError("verifier state")
+
+    srv, url = _server(Broken(edsig.Verifier(keys["p1"], "node-b")))
+    try:
+        with pytest.raises(KubeError) as ei:
+            Client(url).request("POST", "/v1/claims", {"count": 1}, extra_headers={
+                "X-Gpupool-Signature": "v1 keyId=x node=node-b ts=1 nonce=n body=b sig=s"})
+        assert ei.value.code == 401 and ei.value.reason == "AuthError"
+    finally:
+        srv.close()
